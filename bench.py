@@ -1,0 +1,169 @@
+#!/usr/bin/env python3
+"""Headline benchmark: avg sec/step of BERT-base phase-1 pre-training.
+
+Config (BASELINE.json): BERT-base (110,106,428 params, random init),
+seq_len 128, 32 sequences per GPU per step (update-freq 1), synthetic
+NVIDIA-format HDF5 shards read through the native loader, fused Adam,
+--fast-stat-sync (as in every documented reference run), weak scaling.
+
+    python bench.py --gpus N --steps K --warmup W [--dtype fp32|bf16]
+
+For N > 1 launch with torch.distributed.run (one rank per GPU, RCCL).
+Timed region: K full training steps (data -> H2D -> fwd -> bwd -> bucketed
+all-reduce -> stats all-reduce -> clip -> Adam), bracketed by a barrier and
+device synchronisation on both sides; the reported time is the MAX over
+ranks.  Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+BASELINE_SEC_PER_STEP = 2.60  # README.md:65, 1 node x 4 GPUs, 32 seq/GPU/step
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
+    p.add_argument("--seq-len", type=int, default=128)
+    p.add_argument("--batch", type=int, default=32)
+    p.add_argument("--max-pred", type=int, default=20)
+    p.add_argument("--update-freq", type=int, default=1)
+    p.add_argument("--layers", type=int, default=12)
+    p.add_argument("--bucket-cap-mb", type=int, default=25)
+    p.add_argument("--no-fused", action="store_true")
+    p.add_argument("--gemm", default=None, choices=[None, "hip", "blas", "auto"])
+    p.add_argument("--profile-phases", action="store_true")
+    return p.parse_args()
+
+
+def main():
+    b = parse()
+    if b.gemm:
+        os.environ["HETSEQ_GEMM"] = b.gemm
+    import torch
+    import torch.distributed as dist
+
+    from hetseq_amd import options
+    from hetseq_amd.controller import Controller
+    from hetseq_amd.data.synthetic import write_bert_config, write_bert_shards, write_vocab
+    from hetseq_amd.ops import gemm as G
+    from hetseq_amd.parallel import distributed_utils
+    from hetseq_amd.tasks import LanguageModelingTask
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", init_method="env://", world_size=world, rank=rank,
+                                device_id=torch.device("cuda", local_rank))
+        dist.all_reduce(torch.zeros(1, device="cuda"))
+    work = tempfile.mkdtemp(prefix="hetseq_bench_r%d_" % rank)
+    data_dir = os.path.join(work, "data")
+    # every rank writes the SAME shards (same seed) and takes its strided share of the
+    # globally shuffled batch list, exactly like training (index randomisation + assignment)
+    per_shard = max(256, b.batch * b.update_freq * (b.steps + b.warmup + 2) * world // 2 + 1)
+    write_bert_shards(data_dir, num_shards=2, per_shard=per_shard, seq_len=b.seq_len, max_pred=b.max_pred,
+                      vocab_size=30522, seed=17, split="train", full_length=False)
+    write_vocab(os.path.join(work, "vocab.txt"))
+    cfg = write_bert_config(os.path.join(work, "bert_base.json"), num_hidden_layers=b.layers)
+    argv = ["--task", "bert", "--data", data_dir, "--dict", os.path.join(work, "vocab.txt"), "--config_file", cfg,
+            "--max-sentences", str(b.batch), "--lr", "1e-4", "--warmup-updates", "100", "--weight-decay", "0.01",
+            "--fast-stat-sync", "--clip-norm", "25", "--dtype", b.dtype, "--bucket-cap-mb", str(b.bucket_cap_mb),
+            "--distributed-world-size", str(world), "--num-workers", "2", "--log-format", "none",
+            "--update-freq", str(b.update_freq)]
+    if b.no_fused:
+        argv.append("--no-fused")
+    args = options.parse_cli(argv)
+    args.distributed_rank = rank
+    args.device_id = local_rank
+    torch.manual_seed(args.seed)
+    task = LanguageModelingTask.setup_task(args)
+    model = task.build_model(args)
+    nparams = sum(p.numel() for p in model.parameters())
+    ctl = Controller(args, task, model)
+    task.load_dataset("train")
+    task.prepare_model_for_data(ctl.get_model(), "train")
+    epoch_itr = task.get_batch_iterator(task.dataset("train"), max_sentences=b.batch, seed=args.seed, num_shards=world,
+                                        shard_id=rank, num_workers=2, epoch=0, device=ctl.device)
+
+    def batches():
+        while True:
+            itr = epoch_itr.next_epoch_itr(shuffle=True)
+            group = []
+            for s in itr:
+                if s is None or s[0].shape[0] != b.batch:
+                    continue
+                group.append(s)
+                if len(group) == b.update_freq:
+                    yield group
+                    group = []
+
+    gen = batches()
+    ctl.optimizer  # build optimizer/scheduler (and the DP engine) before timing
+    for _ in range(b.warmup):
+        ctl.train_step(next(gen))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(b.steps):
+        ctl.train_step(next(gen))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    loss = float(ctl.get_meter("train_loss").avg)
+    from hetseq_amd.ops import bert_ops
+
+    bert_ops.check_device_errors()
+    sec = elapsed / b.steps
+    seqs = b.batch * b.update_freq * world
+    if rank == 0:
+        out = {
+            "metric": "avg sec/step, BERT-base seq128 bs=32/GPU",
+            "value": round(sec, 6),
+            "unit": "s/step",
+            "n_gpus": world,
+            "steps": b.steps,
+            "warmup": b.warmup,
+            "ms_per_step": round(sec * 1000, 3),
+            "higher_is_better": False,
+            "scaling": "weak",
+            "vs_baseline": round(sec / BASELINE_SEC_PER_STEP, 6),
+            "speedup_vs_baseline": round(BASELINE_SEC_PER_STEP / sec, 2),
+            "seq_per_s": round(seqs / sec, 1),
+            "tokens_per_s": round(seqs * b.seq_len / sec, 1),
+            "dtype": b.dtype,
+            "data": "synthetic NVIDIA-format HDF5 shards (random tokens), random-init weights",
+            "config": {"model": "bert-base-uncased (L12 H768 A12, %d params)" % nparams,
+                       "global_batch": seqs, "seq_len": b.seq_len, "per_gpu_batch": b.batch,
+                       "update_freq": b.update_freq, "parallelism": "dp%d" % world,
+                       "fused_kernels": not b.no_fused, "bucket_cap_mb": b.bucket_cap_mb},
+            "final_train_loss_logged": round(loss, 5),
+            "gemm_choices": {str(k): v for k, v in list(G.GEMM_CHOICES.items())[:32]},
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

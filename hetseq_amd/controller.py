@@ -1,0 +1,369 @@
+"""Controller: the synchronous data-parallel training engine.
+
+API parity with the reference ``Controller`` (reference: controller.py:21-438):
+``model``/``optimizer``/``lr_scheduler`` properties, ``train_step(samples)``,
+``get_train_iterator``, ``save_checkpoint``/``load_checkpoint``,
+``lr_step``/``lr_step_update``/``get_lr``, meters, ``get/set_num_updates``.
+Reference semantics kept on purpose: per-update reseeding
+with ``seed + num_updates`` (Q14), ``sample_size = len(sample[0][0])`` grad
+normalisation (Q03), fast-stat loss units ``sum loss / (sum sample_size *
+ln 2)`` (Q02), dummy batch with ``loss * 0`` for padded shards (C26), grad
+clipping at ``--clip-norm``.
+
+MI355X-first engine underneath:
+* parameters/gradients live in a flat store; DP uses ``FlatDDP`` (in-place
+  bucketed all-reduce on RCCL, overlapped with backward) instead of DDP;
+* the whole update (grad scale, clip, Adam) is one reduction + one fused
+  kernel reading the scale from device memory -- the stats all-reduce
+  result never round-trips to the host inside ``train_step``;
+* meters take device tensors lazily, so with logging off a training step
+  issues no host synchronisation at all (the reference syncs 3-4 times per
+  update);
+* ``--dtype bf16`` keeps fp32 master weights and a bf16 shadow copy.
+"""
+from __future__ import annotations
+
+import contextlib
+import math
+import os
+from collections import OrderedDict
+from itertools import chain
+
+import torch
+import torch.distributed as dist
+
+from hetseq_amd import checkpoint_utils, utils
+from hetseq_amd.meters import AverageMeter, StopwatchMeter, TimeMeter
+from hetseq_amd.optim import build_lr_scheduler, build_optimizer
+from hetseq_amd.parallel import distributed_utils
+from hetseq_amd.parallel.ddp import BMUF, FlatDDP
+from hetseq_amd.runtime import profiling, rng
+from hetseq_amd.runtime.flat import FlatParamStore
+
+LN2 = math.log(2)
+
+
+class Controller(object):
+    def __init__(self, args, task, model, criterion=None, dummy_batch=None, oom_batch=None):
+        self.args = args
+        self.task = task
+        self.cuda = torch.cuda.is_available() and not args.cpu
+        self.device = torch.device("cuda", torch.cuda.current_device()) if self.cuda else torch.device("cpu")
+        self._model = model.to(self.device)
+        if not getattr(args, "fused", True):
+            os.environ["HETSEQ_DISABLE_FUSED"] = "1"
+        self.compute_dtype = torch.bfloat16 if getattr(args, "dtype", "fp32") == "bf16" else torch.float32
+        shadow = torch.bfloat16 if self.compute_dtype == torch.bfloat16 else None
+        self.store = FlatParamStore(self._model, device=self.device, shadow_dtype=shadow)
+        if hasattr(self._model, "attach_store"):
+            self._model.attach_store(self.store, self.compute_dtype)
+        elif self.compute_dtype != torch.float32:
+            raise ValueError("--dtype bf16 is only implemented for the BERT models")
+        self._dummy_batch = dummy_batch
+        self._oom_batch = oom_batch or dummy_batch
+        self._lr_scheduler = None
+        self._num_updates = 0
+        self._optim_history = None
+        self._optimizer = None
+        self._prev_grad_norm = None
+        self._wrapped_model = None
+        self._bmuf = None
+        self._all_reduce_list = [0.0] * 6
+        self.fast_stat_sync = args.fast_stat_sync
+        self.phase_timer = profiling.PhaseTimer()
+        self.init_meters(args)
+
+    def init_meters(self, args):
+        self.meters = OrderedDict()
+        self.meters["train_loss"] = AverageMeter()
+        self.meters["train_nll_loss"] = AverageMeter()
+        self.meters["valid_loss"] = AverageMeter()
+        self.meters["valid_nll_loss"] = AverageMeter()
+        self.meters["wps"] = TimeMeter()
+        self.meters["ups"] = TimeMeter()
+        self.meters["wpb"] = AverageMeter()
+        self.meters["bsz"] = AverageMeter()
+        self.meters["gnorm"] = AverageMeter()
+        self.meters["clip"] = AverageMeter()
+        self.meters["wall"] = TimeMeter()
+        self.meters["train_wall"] = StopwatchMeter()
+
+    # ------------------------------------------------------------------ properties
+    @property
+    def model(self):
+        if self._wrapped_model is None:
+            if self.args.distributed_world_size > 1 and dist.is_initialized() and not self.args.use_bmuf:
+                self._wrapped_model = FlatDDP(self._model, self.store, bucket_cap_mb=self.args.bucket_cap_mb,
+                                              find_unused_parameters=self.args.find_unused_parameters)
+            else:
+                self._wrapped_model = self._model
+                if self.args.distributed_world_size > 1 and dist.is_initialized() and self.args.use_bmuf:
+                    self._bmuf = BMUF(self.store, block_momentum=self.args.bmuf_block_momentum,
+                                      sync_interval=self.args.bmuf_sync_interval)
+        return self._wrapped_model
+
+    @property
+    def optimizer(self):
+        if self._optimizer is None:
+            self._build_optimizer()
+        return self._optimizer
+
+    @property
+    def lr_scheduler(self):
+        if self._lr_scheduler is None:
+            self._build_optimizer()
+        return self._lr_scheduler
+
+    def _build_optimizer(self):
+        params = list(filter(lambda p: p.requires_grad, chain(self.model.parameters())))
+        self._optimizer = build_optimizer(self.args, params, self.store)
+        self._lr_scheduler = build_lr_scheduler(self.args, self._optimizer)
+        self._lr_scheduler.step_update(0)
+
+    # ------------------------------------------------------------------ checkpoints
+    def save_checkpoint(self, filename, extra_state):
+        if distributed_utils.is_master(self.args):
+            extra_state["train_meters"] = self.meters
+            checkpoint_utils.save_state(filename, self.args, self.get_model().state_dict(), None, self.optimizer,
+                                        self.lr_scheduler, self.get_num_updates(), self._optim_history, extra_state)
+
+    def load_checkpoint(self, filename, reset_optimizer=False, reset_lr_scheduler=False, optimizer_overrides=None,
+                        reset_meters=False):
+        extra_state, self._optim_history, last_optim_state = None, [], None
+        if os.path.exists(filename):
+            state = checkpoint_utils.load_checkpoint_to_cpu(filename)
+            try:
+                self.get_model().load_state_dict(state["model"], strict=True)
+            except Exception:
+                raise Exception("Cannot load model parameters from checkpoint {}; please ensure that the "
+                                "architectures match.".format(filename))
+            self.store.sync_shadow()
+            extra_state = state["extra_state"]
+            self._optim_history = state["optimizer_history"]
+            last_optim_state = state.get("last_optimizer_state", None)
+        if last_optim_state is not None and not reset_optimizer:
+            self._build_optimizer()
+            last_optim = self._optim_history[-1]
+            assert last_optim["optimizer_name"] == self.optimizer.__class__.__name__, \
+                "Optimizer does not match; please reset the optimizer (--reset-optimizer)."
+            if not reset_lr_scheduler:
+                self.lr_scheduler.load_state_dict(last_optim["lr_scheduler_state"])
+            self.optimizer.load_state_dict(last_optim_state, optimizer_overrides)
+            self.set_num_updates(last_optim["num_updates"])
+        if extra_state is not None:
+            itr = extra_state.get("train_iterator", {"epoch": 0})
+            epoch = itr["epoch"]
+            print("| loaded checkpoint {} (epoch {} @ {} updates)".format(filename, epoch, self.get_num_updates()))
+            self.lr_step(epoch)
+            if "train_meters" in extra_state and not reset_meters:
+                checkpoint_utils.restore_meters(self.meters, extra_state["train_meters"])
+                del extra_state["train_meters"]
+                for meter in self.meters.values():
+                    if isinstance(meter, TimeMeter):
+                        meter.reset()
+        else:
+            print("| no existing checkpoint found {}".format(filename))
+        return extra_state
+
+    def get_train_iterator(self, epoch, combine=True, load_dataset=True):
+        if load_dataset:
+            print("| loading train data for epoch {}".format(epoch))
+            self.task.load_dataset(self.args.train_subset)
+        return self.task.get_batch_iterator(
+            dataset=self.task.dataset(self.args.train_subset), max_tokens=self.args.max_tokens,
+            max_sentences=self.args.max_sentences, max_positions=None, ignore_invalid_inputs=True,
+            required_batch_size_multiple=self.args.required_batch_size_multiple, seed=self.args.seed,
+            num_shards=self.args.distributed_world_size, shard_id=self.args.distributed_rank,
+            num_workers=self.args.num_workers, epoch=epoch, device=self.device if self.cuda else None)
+
+    # ------------------------------------------------------------------ training
+    def train_step(self, samples, dummy_batch=False, raise_oom=False):
+        """Forward, backward and parameter update for one group of micro-batches."""
+        if self._dummy_batch is None:
+            self._dummy_batch = next((s for s in samples if s is not None and len(s) > 0), None)
+        self._set_seed()
+        self.model.train()
+        self.zero_grad()
+        if not dummy_batch:
+            self.meters["train_wall"].start()
+        logging_outputs, sample_sizes, ooms = [], [], 0
+        stats = torch.zeros(6, dtype=torch.float64, device=self.device) if self.fast_stat_sync else None
+        sample_size = 0
+        logging_output = {}
+        for i, sample in enumerate(samples):
+            sample = self._prepare_sample(sample)
+            if sample is None:
+                sample = self._prepare_sample(self._dummy_batch)
+                ignore_grad = True
+            else:
+                ignore_grad = False
+
+            def maybe_no_sync():
+                if self.args.distributed_world_size > 1 and hasattr(self.model, "no_sync") and i < len(samples) - 1:
+                    return self.model.no_sync()
+                return contextlib.ExitStack()
+
+            try:
+                with maybe_no_sync():
+                    tok = self.phase_timer.start("fwd_bwd")
+                    loss, sample_size, logging_output = self.task.train_step(sample, self.model, self.optimizer,
+                                                                             ignore_grad)
+                    self.phase_timer.stop(tok)
+                if not ignore_grad:
+                    logging_outputs.append(logging_output)
+                    sample_sizes.append(sample_size)
+                    if self.fast_stat_sync:
+                        stats[0] += sample_size
+                        stats[1] += logging_output.get("nsentences", 0.0)
+                        stats[2] += _as_f64(logging_output.get("loss", 0.0), self.device)
+                        stats[3] += _as_f64(logging_output.get("nll_loss", 0.0), self.device)
+                        stats[4] += logging_output.get("ntokens", 0.0)
+            except RuntimeError as e:
+                if "out of memory" in str(e):
+                    raise RuntimeError("ran out of memory with exception") from e
+                raise e
+        if dummy_batch:
+            return None
+
+        scale = None  # grad multiplier: W/sample_size of the reference, divided by W (we sum, not average)
+        if self.fast_stat_sync:
+            if self._sync_stats():
+                dist.all_reduce(stats)
+            stats[2:4].div_(stats[0:1] * LN2)
+            sample_size_t = stats[0]
+            logging_output = {"nsentences": stats[1], "loss": stats[2], "nll_loss": stats[3], "ntokens": stats[4]}
+            ooms = stats[5]
+            w = 1.0 if isinstance(self.model, FlatDDP) else float(self.args.distributed_world_size)
+            scale = torch.where(sample_size_t > 0, w / sample_size_t.clamp(min=1e-30),
+                                torch.ones_like(sample_size_t)).float()
+            sample_size_for_meter = sample_size_t
+        else:
+            if self._sync_stats():
+                gathered = distributed_utils.all_gather_list(
+                    [_to_host(logging_outputs), sample_sizes, ooms, _host(self._prev_grad_norm)])
+                logging_outputs_all, sample_sizes_all, ooms_all, prev_norms = zip(*gathered)
+                ooms = sum(ooms_all)
+                if not self.args.use_bmuf:
+                    assert (all(n == prev_norms[0] for n in prev_norms)
+                            or all(n is None or math.isnan(n) or math.isinf(n) for n in prev_norms)), \
+                        "Fatal error: gradients are inconsistent between workers"
+            if sample_size > 0:
+                # reference: W/sample_size applied to DDP-averaged grads == 1/sample_size on summed grads
+                scale = 1.0 / float(sample_size)
+                if not (self.args.distributed_world_size > 1 and dist.is_initialized() and not self.args.use_bmuf):
+                    scale = float(self.args.distributed_world_size) / float(sample_size)
+            sample_size_for_meter = sample_size
+        if not all(k in logging_output for k in ["ntokens", "nsentences"]):
+            raise Exception("Please update the {}.aggregate_logging_outputs() method to return ntokens and "
+                            "nsentences".format(self.task.__class__.__name__))
+        try:
+            tok = self.phase_timer.start("optimizer")
+            profiling.range_push("optimizer")
+            if scale is not None:
+                self.optimizer.multiply_grads(scale)
+            grad_norm = self.optimizer.clip_grad_norm(self.args.clip_norm)
+            self._prev_grad_norm = grad_norm
+            self.optimizer.step()
+            if self._bmuf is not None:
+                self._bmuf.after_step()
+            profiling.range_pop()
+            self.phase_timer.stop(tok)
+            self.set_num_updates(self.get_num_updates() + 1)
+            self.task.update_step(self._num_updates)
+            ntokens = logging_output.get("ntokens", 0)
+            nsentences = logging_output.get("nsentences", 0)
+            self.meters["wps"].update(ntokens)
+            self.meters["ups"].update(1.0)
+            self.meters["wpb"].update(ntokens)
+            self.meters["bsz"].update(nsentences)
+            self.meters["gnorm"].update(grad_norm)
+            if self.args.clip_norm > 0:
+                self.meters["clip"].update((grad_norm > self.args.clip_norm).float() if torch.is_tensor(grad_norm)
+                                           else float(grad_norm > self.args.clip_norm))
+            else:
+                self.meters["clip"].update(0.0)
+            self.meters["train_loss"].update(logging_output.get("loss", 0), sample_size_for_meter)
+            if self.args.check_consistency and self._num_updates % self.args.check_consistency == 0:
+                self.check_consistency()
+        except OverflowError as e:
+            print("| WARNING: overflow detected, " + str(e))
+            self.zero_grad()
+            logging_output = None
+        self.clear_buffered_stats()
+        self.meters["train_wall"].stop()
+        return logging_output
+
+    def check_consistency(self):
+        """All-reduce the parameter checksum and fail if ranks diverged."""
+        if not (dist.is_initialized() and self.args.distributed_world_size > 1) or self.args.use_bmuf:
+            return
+        cs = self.store.checksum().reshape(1)
+        lo, hi = cs.clone(), cs.clone()
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        if float(hi - lo) > 1e-6 * max(1.0, abs(float(cs))):
+            raise RuntimeError("parameter checksum diverged across ranks: min {} max {}".format(float(lo), float(hi)))
+
+    def zero_grad(self):
+        self.optimizer.zero_grad()
+
+    def clear_buffered_stats(self):
+        self._all_reduce_list = [0.0] * 6
+
+    def lr_step(self, epoch, val_loss=None):
+        self.lr_scheduler.step(epoch, val_loss)
+        return self.lr_step_update()
+
+    def lr_step_update(self):
+        return self.lr_scheduler.step_update(self.get_num_updates())
+
+    def get_lr(self):
+        return self.optimizer.get_lr()
+
+    def get_model(self):
+        return self._model
+
+    def get_meter(self, name):
+        return self.meters.get(name)
+
+    def get_num_updates(self):
+        return self._num_updates
+
+    def set_num_updates(self, num_updates):
+        self._num_updates = num_updates
+        self.lr_step_update()
+
+    def _prepare_sample(self, sample):
+        if sample is None or len(sample) == 0:
+            return None
+        if self.cuda:
+            sample = utils.move_to_cuda(sample, self.device)
+        return sample
+
+    def _set_seed(self):
+        seed = self.args.seed + self.get_num_updates()
+        if getattr(self.args, "per_rank_seed", False):
+            seed += 1000003 * int(self.args.distributed_rank or 0)
+        torch.manual_seed(seed)
+        if self.cuda:
+            torch.cuda.manual_seed(seed)
+        rng.set_seed(seed)
+
+    def _sync_stats(self):
+        return self.args.distributed_world_size > 1 and dist.is_initialized()
+
+
+def _as_f64(v, device):
+    if torch.is_tensor(v):
+        return v.detach().to(device=device, dtype=torch.float64)
+    return float(v)
+
+
+def _host(v):
+    if torch.is_tensor(v):
+        return float(v.item())
+    return v
+
+
+def _to_host(logging_outputs):
+    return [{k: _host(v) for k, v in lo.items()} for lo in logging_outputs]

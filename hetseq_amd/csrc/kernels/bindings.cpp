@@ -1,0 +1,207 @@
+// pybind11 entry points for the gfx950 kernel library.
+//
+// Every entry takes raw device addresses (Python passes tensor.data_ptr())
+// and the HIP stream handle (torch.cuda.current_stream().cuda_stream).  Shape
+// and dtype validation happens in Python (hetseq_amd/ops/_C.py) BEFORE the
+// launch, so a kernel never sees a shape its grid does not assume.
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+
+namespace py = pybind11;
+using u64 = uint64_t;
+using i64 = int64_t;
+
+#define P(T, x) reinterpret_cast<T>(static_cast<uintptr_t>(x))
+#define ST(x) reinterpret_cast<hipStream_t>(static_cast<uintptr_t>(x))
+
+// optim.hip
+void launch_grad_norm(const float*, int64_t, double*, const float*, float, float*, hipStream_t);
+void launch_adam_flat(float*, const float*, float*, float*, void*, int64_t, const float*, float, float, float, float,
+                      float, float, hipStream_t);
+void launch_adadelta_flat(float*, const float*, float*, float*, void*, int64_t, const float*, float, float, float,
+                          float, hipStream_t);
+void launch_lamb_flat(float*, const float*, float*, float*, float*, void*, const int64_t*, int, float*, const float*,
+                      float, float, float, float, float, float, float, hipStream_t);
+void launch_cast_f32_bf16(const float*, void*, int64_t, hipStream_t);
+// layernorm.hip
+int ln_bwd_num_blocks();
+int launch_ln_fwd(int, const void*, const float*, const void*, const float*, const float*, void*, float*, float*,
+                  float*, int, int, float, float, u64, u64, int, hipStream_t);
+int launch_ln_bwd(int, const void*, const float*, const float*, const float*, const float*, void*, void*, float*,
+                  float*, float*, int, int, float, u64, u64, int, hipStream_t);
+int launch_emb_fwd(int, const int64_t*, const int64_t*, const float*, const float*, const float*, const float*,
+                   const float*, void*, float*, float*, float*, int, int, int, int, int, float, float, u64, u64, int*,
+                   hipStream_t);
+int launch_emb_bwd(int, const void*, const int64_t*, const int64_t*, const float*, const float*, const float*,
+                   const float*, float*, float*, float*, float*, float*, int, int, int, int, int, float, u64, u64,
+                   hipStream_t);
+void launch_colpart_finalize(const float* const*, float* const*, int, int, int, int, hipStream_t);
+// elementwise.hip
+void launch_bias_gelu_fwd(int, const void*, const float*, void*, int64_t, int, hipStream_t);
+void launch_bias_tanh_fwd(int, const void*, const float*, void*, int64_t, int, hipStream_t);
+int colsum_row_chunks(int64_t);
+void launch_colsum(int, const void*, const void*, const float*, void*, float*, float*, int64_t, int, int, hipStream_t);
+void launch_mlm_compact(const int64_t*, int, int, int, int32_t*, int64_t*, int32_t*, int*, hipStream_t);
+void launch_gather_rows(int, const void*, const int32_t*, void*, int, int, hipStream_t);
+void launch_scatter_add_rows(int, const void*, const int32_t*, void*, int, int, hipStream_t);
+// attention.hip
+int launch_attn_fwd(int, const void*, const int64_t*, void*, float*, int, int, int, int, float, u64, u64, hipStream_t);
+int launch_attn_bwd(int, const void*, const int64_t*, const void*, const void*, const float*, float*, void*, int, int,
+                    int, int, float, u64, u64, hipStream_t);
+// xent.hip
+void launch_xent_fwd(int, const void*, const int64_t*, int, int, int64_t, int, float*, float*, float*, hipStream_t);
+void launch_xent_bwd(int, void*, const int64_t*, const float*, int, int, int64_t, int, const float*, const float*,
+                     hipStream_t);
+// gemm.hip
+int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, int64_t lda, const void* B,
+                int64_t ldb, void* C, int64_t ldc, const float* bias, int epi, float beta, hipStream_t st);
+
+static void check(int rc, const char* what) {
+  if (rc != 0) throw std::invalid_argument(std::string(what) + ": unsupported shape for the HIP kernel");
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+static void check_launch(const char* what) { check(0, what); }
+
+PYBIND11_MODULE(_hip, m) {
+  m.doc() = "hetseq_amd CDNA4 (gfx950) kernels";
+  m.attr("arch") = "gfx950";
+
+  m.def("grad_norm", [](i64 g, i64 n, i64 partial, i64 scale, float max_norm, i64 out, i64 st) {
+    launch_grad_norm(P(const float*, g), n, P(double*, partial), P(const float*, scale), max_norm, P(float*, out), ST(st));
+    check_launch("grad_norm");
+  });
+  m.def("adam_flat", [](i64 p, i64 g, i64 mm, i64 v, i64 shadow, i64 n, i64 gmul, float lr, float b1, float b2,
+                        float eps, float wd, float step_size, i64 st) {
+    launch_adam_flat(P(float*, p), P(const float*, g), P(float*, mm), P(float*, v), P(void*, shadow), n,
+                     P(const float*, gmul), lr, b1, b2, eps, wd, step_size, ST(st));
+    check_launch("adam_flat");
+  });
+  m.def("adadelta_flat", [](i64 p, i64 g, i64 sq, i64 acc, i64 shadow, i64 n, i64 gmul, float lr, float rho, float eps,
+                            float wd, i64 st) {
+    launch_adadelta_flat(P(float*, p), P(const float*, g), P(float*, sq), P(float*, acc), P(void*, shadow), n,
+                         P(const float*, gmul), lr, rho, eps, wd, ST(st));
+    check_launch("adadelta_flat");
+  });
+  m.def("lamb_flat", [](i64 p, i64 g, i64 mm, i64 v, i64 upd, i64 shadow, i64 seg_off, int nseg, i64 seg_norms, i64 gmul,
+                        float lr, float b1, float b2, float eps, float wd, float bc1, float bc2, i64 st) {
+    launch_lamb_flat(P(float*, p), P(const float*, g), P(float*, mm), P(float*, v), P(float*, upd), P(void*, shadow),
+                     P(const int64_t*, seg_off), nseg, P(float*, seg_norms), P(const float*, gmul), lr, b1, b2, eps, wd,
+                     bc1, bc2, ST(st));
+    check_launch("lamb_flat");
+  });
+  m.def("cast_f32_bf16", [](i64 x, i64 y, i64 n, i64 st) {
+    launch_cast_f32_bf16(P(const float*, x), P(void*, y), n, ST(st));
+    check_launch("cast_f32_bf16");
+  });
+
+  m.def("ln_bwd_num_blocks", &ln_bwd_num_blocks);
+  m.def("ln_fwd", [](int dt, i64 a, i64 bias, i64 resid, i64 gamma, i64 beta, i64 y, i64 zsave, i64 mean, i64 rstd,
+                     int rows, int H, float eps, float p, u64 seed, u64 off, int mode, i64 st) {
+    check(launch_ln_fwd(dt, P(const void*, a), P(const float*, bias), P(const void*, resid), P(const float*, gamma),
+                        P(const float*, beta), P(void*, y), P(float*, zsave), P(float*, mean), P(float*, rstd), rows, H,
+                        eps, p, seed, off, mode, ST(st)),
+          "ln_fwd");
+  });
+  m.def("ln_bwd", [](int dt, i64 dy, i64 zsave, i64 mean, i64 rstd, i64 gamma, i64 dz, i64 da, i64 pg, i64 pb, i64 pbias,
+                     int rows, int H, float p, u64 seed, u64 off, int mode, i64 st) {
+    check(launch_ln_bwd(dt, P(const void*, dy), P(const float*, zsave), P(const float*, mean), P(const float*, rstd),
+                        P(const float*, gamma), P(void*, dz), P(void*, da), P(float*, pg), P(float*, pb),
+                        P(float*, pbias), rows, H, p, seed, off, mode, ST(st)),
+          "ln_bwd");
+  });
+  m.def("emb_fwd", [](int dt, i64 ids, i64 tt, i64 w, i64 pe, i64 te, i64 gamma, i64 beta, i64 y, i64 zsave, i64 mean,
+                      i64 rstd, int rows, int S, int H, int V, int TV, float eps, float p, u64 seed, u64 off, i64 err,
+                      i64 st) {
+    check(launch_emb_fwd(dt, P(const int64_t*, ids), P(const int64_t*, tt), P(const float*, w), P(const float*, pe),
+                         P(const float*, te), P(const float*, gamma), P(const float*, beta), P(void*, y),
+                         P(float*, zsave), P(float*, mean), P(float*, rstd), rows, S, H, V, TV, eps, p, seed, off,
+                         P(int*, err), ST(st)),
+          "emb_fwd");
+  });
+  m.def("emb_bwd", [](int dt, i64 dy, i64 ids, i64 tt, i64 zsave, i64 mean, i64 rstd, i64 gamma, i64 dw, i64 dp, i64 dtp,
+                      i64 pg, i64 pb, int rows, int S, int H, int V, int TV, float p, u64 seed, u64 off, i64 st) {
+    check(launch_emb_bwd(dt, P(const void*, dy), P(const int64_t*, ids), P(const int64_t*, tt), P(const float*, zsave),
+                         P(const float*, mean), P(const float*, rstd), P(const float*, gamma), P(float*, dw),
+                         P(float*, dp), P(float*, dtp), P(float*, pg), P(float*, pb), rows, S, H, V, TV, p, seed, off,
+                         ST(st)),
+          "emb_bwd");
+  });
+  m.def("colpart_finalize", [](py::list parts, py::list outs, int nparts, int H, int accumulate, i64 st) {
+    const int n = static_cast<int>(parts.size());
+    if (n < 1 || n > 3 || outs.size() != parts.size()) throw std::invalid_argument("colpart_finalize: 1..3 pairs");
+    const float* pp[3];
+    float* oo[3];
+    for (int i = 0; i < n; ++i) {
+      pp[i] = P(const float*, parts[i].cast<i64>());
+      oo[i] = P(float*, outs[i].cast<i64>());
+    }
+    launch_colpart_finalize(pp, oo, n, nparts, H, accumulate, ST(st));
+    check_launch("colpart_finalize");
+  });
+
+  m.def("bias_gelu_fwd", [](int dt, i64 x, i64 b, i64 y, i64 rows, int N, i64 st) {
+    launch_bias_gelu_fwd(dt, P(const void*, x), P(const float*, b), P(void*, y), rows, N, ST(st));
+    check_launch("bias_gelu_fwd");
+  });
+  m.def("bias_tanh_fwd", [](int dt, i64 x, i64 b, i64 y, i64 rows, int N, i64 st) {
+    launch_bias_tanh_fwd(dt, P(const void*, x), P(const float*, b), P(void*, y), rows, N, ST(st));
+    check_launch("bias_tanh_fwd");
+  });
+  m.def("colsum_row_chunks", &colsum_row_chunks);
+  m.def("colsum", [](int dt, i64 dy, i64 x, i64 b, i64 dx, i64 part, i64 out, i64 rows, int N, int accumulate, i64 st) {
+    launch_colsum(dt, P(const void*, dy), P(const void*, x), P(const float*, b), P(void*, dx), P(float*, part),
+                  P(float*, out), rows, N, accumulate, ST(st));
+    check_launch("colsum");
+  });
+  m.def("mlm_compact", [](i64 labels, int rows, int ignore, int cap, i64 idx, i64 lab_out, i64 count, i64 err, i64 st) {
+    launch_mlm_compact(P(const int64_t*, labels), rows, ignore, cap, P(int32_t*, idx), P(int64_t*, lab_out),
+                       P(int32_t*, count), P(int*, err), ST(st));
+    check_launch("mlm_compact");
+  });
+  m.def("gather_rows", [](int dt, i64 src, i64 idx, i64 out, int n, int H, i64 st) {
+    launch_gather_rows(dt, P(const void*, src), P(const int32_t*, idx), P(void*, out), n, H, ST(st));
+    check_launch("gather_rows");
+  });
+  m.def("scatter_add_rows", [](int dt, i64 src, i64 idx, i64 dst, int n, int H, i64 st) {
+    launch_scatter_add_rows(dt, P(const void*, src), P(const int32_t*, idx), P(void*, dst), n, H, ST(st));
+    check_launch("scatter_add_rows");
+  });
+
+  m.def("attn_fwd", [](int dt, i64 qkv, i64 mask, i64 ctx, i64 lse, int B, int S, int NH, int D, float p, u64 seed,
+                       u64 off, i64 st) {
+    check(launch_attn_fwd(dt, P(const void*, qkv), P(const int64_t*, mask), P(void*, ctx), P(float*, lse), B, S, NH, D,
+                          p, seed, off, ST(st)),
+          "attn_fwd");
+  });
+  m.def("attn_bwd", [](int dt, i64 qkv, i64 mask, i64 ctx, i64 dctx, i64 lse, i64 dbuf, i64 dqkv, int B, int S, int NH,
+                       int D, float p, u64 seed, u64 off, i64 st) {
+    check(launch_attn_bwd(dt, P(const void*, qkv), P(const int64_t*, mask), P(const void*, ctx), P(const void*, dctx),
+                          P(const float*, lse), P(float*, dbuf), P(void*, dqkv), B, S, NH, D, p, seed, off, ST(st)),
+          "attn_bwd");
+  });
+
+  m.def("xent_fwd", [](int dt, i64 logits, i64 labels, int rows, int V, i64 ldv, int ignore, i64 row_loss, i64 lse,
+                       i64 out, i64 st) {
+    launch_xent_fwd(dt, P(const void*, logits), P(const int64_t*, labels), rows, V, ldv, ignore, P(float*, row_loss),
+                    P(float*, lse), P(float*, out), ST(st));
+    check_launch("xent_fwd");
+  });
+  m.def("xent_bwd", [](int dt, i64 logits, i64 labels, i64 lse, int rows, int V, i64 ldv, int ignore, i64 dloss,
+                       i64 stats, i64 st) {
+    launch_xent_bwd(dt, P(void*, logits), P(const int64_t*, labels), P(const float*, lse), rows, V, ldv, ignore,
+                    P(const float*, dloss), P(const float*, stats), ST(st));
+    check_launch("xent_bwd");
+  });
+
+  m.def("gemm", [](int dt, int ta, int tb, int M, int N, int K, i64 A, i64 lda, i64 B, i64 ldb, i64 C, i64 ldc, i64 bias,
+                   int epi, float beta, i64 st) {
+    check(launch_gemm(dt, ta, tb, M, N, K, P(const void*, A), lda, P(const void*, B), ldb, P(void*, C), ldc,
+                      P(const float*, bias), epi, beta, ST(st)),
+          "gemm");
+  });
+}

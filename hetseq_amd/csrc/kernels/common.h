@@ -1,0 +1,134 @@
+// Shared device helpers for the gfx950 (CDNA4) kernel library.
+//
+// Conventions used by every kernel in this directory:
+//  * wave64 everywhere: lane = threadIdx.x & 63, reductions use __shfl_xor over
+//    64 lanes; blocks are multiples of 64 threads.
+//  * storage types are `float` and `bf16_t` (raw uint16 bits); all math is
+//    fp32.  bf16 conversion is round-to-nearest-even with NaN kept NaN.
+//  * randomness is counter-based Philox4x32-10 keyed by (seed, offset), so a
+//    dropout mask is regenerated bit-identically in the backward kernel and no
+//    mask tensor is ever stored.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define HS_DEVICE __device__ __forceinline__
+
+namespace hs {
+
+struct bf16_t {
+  uint16_t x;
+};
+
+HS_DEVICE float to_f(float v) { return v; }
+HS_DEVICE float to_f(bf16_t v) { return __uint_as_float(static_cast<uint32_t>(v.x) << 16); }
+
+template <typename T>
+HS_DEVICE T from_f(float v);
+template <>
+HS_DEVICE float from_f<float>(float v) { return v; }
+template <>
+HS_DEVICE bf16_t from_f<bf16_t>(float v) {
+  uint32_t u = __float_as_uint(v);
+  bf16_t r;
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) {
+    r.x = static_cast<uint16_t>((u >> 16) | 0x40);  // quiet NaN stays NaN
+  } else {
+    u += 0x7fffu + ((u >> 16) & 1u);
+    r.x = static_cast<uint16_t>(u >> 16);
+  }
+  return r;
+}
+
+// ---------------------------------------------------------------- reductions
+HS_DEVICE float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+HS_DEVICE float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+HS_DEVICE double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// ---------------------------------------------------------------- Philox
+struct Philox {
+  // Philox4x32-10 (Salmon et al., SC'11).  One call yields 4 uint32.
+  HS_DEVICE static uint4 gen(uint64_t seed, uint64_t counter_hi, uint32_t counter_lo) {
+    uint32_t k0 = static_cast<uint32_t>(seed), k1 = static_cast<uint32_t>(seed >> 32);
+    uint32_t c0 = counter_lo, c1 = 0u, c2 = static_cast<uint32_t>(counter_hi),
+             c3 = static_cast<uint32_t>(counter_hi >> 32);
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+      const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+      const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+      c0 = hi1 ^ c1 ^ k0;
+      c1 = lo1;
+      c2 = hi0 ^ c3 ^ k1;
+      c3 = lo0;
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    return make_uint4(c0, c1, c2, c3);
+  }
+};
+
+// Keep-decision for element `idx` of a dropout site: uniform in [0,1) from 24
+// random bits, keep if u >= p.  4 consecutive elements share one Philox call.
+HS_DEVICE float u01(uint32_t r) { return static_cast<float>(r >> 8) * (1.0f / 16777216.0f); }
+
+HS_DEVICE uint4 philox_at(uint64_t seed, uint64_t offset, uint64_t q) {
+  // counter = (offset + high bits of q, low 32 bits of q)
+  return Philox::gen(seed, offset + (q >> 32), static_cast<uint32_t>(q));
+}
+
+HS_DEVICE void keep4(uint64_t seed, uint64_t offset, uint64_t q, float p, float scale, float m[4]) {
+  const uint4 r = philox_at(seed, offset, q);
+  m[0] = u01(r.x) >= p ? scale : 0.f;
+  m[1] = u01(r.y) >= p ? scale : 0.f;
+  m[2] = u01(r.z) >= p ? scale : 0.f;
+  m[3] = u01(r.w) >= p ? scale : 0.f;
+}
+
+// vector load/store helpers for 4 consecutive elements
+HS_DEVICE void load4(const float* p, float v[4]) {
+  const float4 t = *reinterpret_cast<const float4*>(p);
+  v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+}
+HS_DEVICE void load4(const bf16_t* p, float v[4]) {
+  const uint2 t = *reinterpret_cast<const uint2*>(p);
+  v[0] = __uint_as_float(t.x << 16);
+  v[1] = __uint_as_float(t.x & 0xffff0000u);
+  v[2] = __uint_as_float(t.y << 16);
+  v[3] = __uint_as_float(t.y & 0xffff0000u);
+}
+HS_DEVICE void store4(float* p, const float v[4]) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+}
+HS_DEVICE void store4(bf16_t* p, const float v[4]) {
+  const bf16_t a = from_f<bf16_t>(v[0]), b = from_f<bf16_t>(v[1]), c = from_f<bf16_t>(v[2]),
+               d = from_f<bf16_t>(v[3]);
+  uint2 t;
+  t.x = static_cast<uint32_t>(a.x) | (static_cast<uint32_t>(b.x) << 16);
+  t.y = static_cast<uint32_t>(c.x) | (static_cast<uint32_t>(d.x) << 16);
+  *reinterpret_cast<uint2*>(p) = t;
+}
+
+// erf-GELU with the reference's 1.41421 constant (reference: bert_modeling.py:104-111)
+HS_DEVICE float gelu_f(float x) { return x * 0.5f * (1.0f + erff(x / 1.41421f)); }
+HS_DEVICE float gelu_grad_f(float x) {
+  // d/dx [x/2 (1+erf(x/c))] = 1/2 (1+erf(x/c)) + x/(c*sqrt(pi)) exp(-(x/c)^2)
+  const float c = 1.41421f;
+  const float xc = x / c;
+  return 0.5f * (1.0f + erff(xc)) + x * (0.5641895835477563f / c) * __expf(-xc * xc);
+}
+
+inline int ceil_div(int64_t a, int64_t b) { return static_cast<int>((a + b - 1) / b); }
+
+}  // namespace hs

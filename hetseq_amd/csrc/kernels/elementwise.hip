@@ -1,0 +1,270 @@
+// Elementwise / reduction kernels for the BERT hot path.
+//
+//  * bias_gelu_fwd: y = gelu(x + b) with the reference's erf(x/1.41421) GELU
+//    (reference: bert_modeling.py:108-111, LinearActivation :166-172)  [K04]
+//  * gelu_bwd_colsum: dx = dy * gelu'(x + b) fused with the column sum of dx
+//    (the bias gradient) as per-block partials                         [K04]
+//  * colsum_partial: column partial sums of a [rows, N] matrix (bias grads)
+//  * mlm_compact: device-side compaction of the masked-LM rows (label != -1)
+//    into a fixed-capacity index list -- the decoder then runs on only those
+//    rows, exactly (rows with label -1 contribute neither loss nor gradient;
+//    reference runs the decoder on every token, bert_modeling.py:547) [K07]
+//  * gather_rows / scatter_rows: move hidden rows in and out of that list.
+//
+// Rows are processed as tiles: a block of 256 threads covers 1024 columns
+// (4 per thread, 16-byte vectors) and a chunk of rows, keeping per-column
+// partial sums in registers -> one partial row per block, no atomics.
+#include "common.h"
+
+namespace hs {
+
+template <typename T>
+__global__ void __launch_bounds__(256) bias_gelu_fwd_kernel(const T* __restrict__ x, const float* __restrict__ b,
+                                                            T* __restrict__ y, int64_t rows, int N) {
+  const int64_t total4 = rows * N / 4;
+  const int n4 = N / 4;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total4; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % n4) * 4;
+    float v[4], bb[4];
+    load4(x + 4 * i, v);
+    load4(b + c, bb);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = gelu_f(v[j] + bb[j]);
+    store4(y + 4 * i, v);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) bias_tanh_fwd_kernel(const T* __restrict__ x, const float* __restrict__ b,
+                                                            T* __restrict__ y, int64_t rows, int N) {
+  const int64_t total = rows * N;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % N);
+    y[i] = from_f<T>(tanhf(to_f(x[i]) + b[c]));
+  }
+}
+
+// grid = (ceil(N/1024), row_chunks); part is [row_chunks, N]
+template <typename T, bool kGelu>
+__global__ void __launch_bounds__(256) colsum_tile_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                          const float* __restrict__ b, T* __restrict__ dx,
+                                                          float* __restrict__ part, int64_t rows, int N,
+                                                          int rows_per_chunk) {
+  const int c = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (c >= N) return;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_chunk;
+  int64_t r1 = r0 + rows_per_chunk;
+  if (r1 > rows) r1 = rows;
+  float bb[4] = {0.f, 0.f, 0.f, 0.f};
+  if (kGelu) load4(b + c, bb);
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int64_t r = r0; r < r1; ++r) {
+    const int64_t o = r * N + c;
+    float d[4];
+    load4(dy + o, d);
+    if (kGelu) {
+      float v[4];
+      load4(x + o, v);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) d[j] *= gelu_grad_f(v[j] + bb[j]);
+      store4(dx + o, d);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] += d[j];
+  }
+  store4(part + (int64_t)blockIdx.y * N + c, acc);
+}
+
+// column partial sums for N not a multiple of 4 (e.g. the 30522-wide vocab)
+template <typename T>
+__global__ void __launch_bounds__(256) colsum_scalar_kernel(const T* __restrict__ x, float* __restrict__ part,
+                                                            int64_t rows, int N, int rows_per_chunk) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= N) return;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_chunk;
+  int64_t r1 = r0 + rows_per_chunk;
+  if (r1 > rows) r1 = rows;
+  float acc = 0.f;
+  for (int64_t r = r0; r < r1; ++r) acc += to_f(x[r * N + c]);
+  part[(int64_t)blockIdx.y * N + c] = acc;
+}
+
+__global__ void partial_rows_sum_kernel(const float* __restrict__ part, int nparts, int N, float* __restrict__ out,
+                                        int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= N) return;
+  float s = 0.f;
+  for (int r = 0; r < nparts; ++r) s += part[(int64_t)r * N + c];
+  out[c] = accumulate ? out[c] + s : s;
+}
+
+// Single-block exclusive scan over `rows` labels; writes idx[cap] (padded
+// with -1), count[0] = number of valid rows, overflow flag if count > cap.
+__global__ void __launch_bounds__(1024) mlm_compact_kernel(const int64_t* __restrict__ labels, int rows,
+                                                           int ignore_index, int cap, int32_t* __restrict__ idx,
+                                                           int64_t* __restrict__ lab_out, int32_t* __restrict__ count,
+                                                           int* __restrict__ err) {
+  __shared__ int wsum[16];
+  __shared__ int carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int base = 0; base < rows; base += 1024) {
+    const int r = base + threadIdx.x;
+    const int64_t lab = r < rows ? labels[r] : ignore_index;
+    const int flag = lab != ignore_index ? 1 : 0;
+    // wave inclusive scan via ballot popcount
+    const unsigned long long bal = __ballot(flag);
+    const unsigned long long below = lane == 0 ? 0ull : (bal & ((~0ull) >> (64 - lane)));
+    const int wpre = __popcll(below);
+    if (lane == 63) wsum[w] = wpre + flag;
+    __syncthreads();
+    int off = carry;
+    for (int i = 0; i < w; ++i) off += wsum[i];
+    const int pos = off + wpre;
+    if (flag && pos < cap) {
+      idx[pos] = r;
+      lab_out[pos] = lab;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int t = 0;
+      for (int i = 0; i < 16; ++i) t += wsum[i];
+      carry += t;
+    }
+    __syncthreads();
+  }
+  const int total = carry;
+  for (int i = threadIdx.x; i < cap; i += 1024)
+    if (i >= total) {
+      idx[i] = -1;
+      lab_out[i] = ignore_index;
+    }
+  if (threadIdx.x == 0) {
+    count[0] = total < cap ? total : cap;
+    if (total > cap) atomicOr(err, 2);
+  }
+}
+
+// out[i] = src[idx[i]] (zero row for idx < 0); H multiple of 4
+template <typename T>
+__global__ void gather_rows_kernel(const T* __restrict__ src, const int32_t* __restrict__ idx, T* __restrict__ out,
+                                   int n, int H) {
+  const int i = blockIdx.x;
+  const int r = idx[i];
+  for (int c = threadIdx.x * 4; c < H; c += blockDim.x * 4) {
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    if (r >= 0) load4(src + (int64_t)r * H + c, v);
+    store4(out + (int64_t)i * H + c, v);
+  }
+}
+
+// dst[idx[i]] += src[i] (rows unique by construction, so no atomics needed)
+template <typename T>
+__global__ void scatter_add_rows_kernel(const T* __restrict__ src, const int32_t* __restrict__ idx,
+                                        T* __restrict__ dst, int n, int H) {
+  const int i = blockIdx.x;
+  const int r = idx[i];
+  if (r < 0) return;
+  for (int c = threadIdx.x * 4; c < H; c += blockDim.x * 4) {
+    float a[4], b[4];
+    load4(src + (int64_t)i * H + c, a);
+    load4(dst + (int64_t)r * H + c, b);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[j] += a[j];
+    store4(dst + (int64_t)r * H + c, b);
+  }
+}
+
+static int ew_grid(int64_t n) {
+  int64_t g = (n + 255) / 256;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace hs
+
+using namespace hs;
+
+void launch_bias_gelu_fwd(int dtype, const void* x, const float* b, void* y, int64_t rows, int N, hipStream_t st) {
+  const int g = ew_grid(rows * N / 4);
+  if (dtype == 0)
+    hipLaunchKernelGGL(bias_gelu_fwd_kernel<float>, dim3(g), dim3(256), 0, st, (const float*)x, b, (float*)y, rows, N);
+  else
+    hipLaunchKernelGGL(bias_gelu_fwd_kernel<bf16_t>, dim3(g), dim3(256), 0, st, (const bf16_t*)x, b, (bf16_t*)y, rows,
+                       N);
+}
+
+void launch_bias_tanh_fwd(int dtype, const void* x, const float* b, void* y, int64_t rows, int N, hipStream_t st) {
+  const int g = ew_grid(rows * N);
+  if (dtype == 0)
+    hipLaunchKernelGGL(bias_tanh_fwd_kernel<float>, dim3(g), dim3(256), 0, st, (const float*)x, b, (float*)y, rows, N);
+  else
+    hipLaunchKernelGGL(bias_tanh_fwd_kernel<bf16_t>, dim3(g), dim3(256), 0, st, (const bf16_t*)x, b, (bf16_t*)y, rows,
+                       N);
+}
+
+int colsum_row_chunks(int64_t rows) {
+  int chunks = (int)((rows + 31) / 32);
+  if (chunks > 256) chunks = 256;
+  if (chunks < 1) chunks = 1;
+  return chunks;
+}
+
+// gelu backward fused with bias-grad partials; if x == nullptr plain column sum of dy.
+void launch_colsum(int dtype, const void* dy, const void* x, const float* b, void* dx, float* part, float* out,
+                   int64_t rows, int N, int accumulate, hipStream_t st) {
+  const int chunks = colsum_row_chunks(rows);
+  const int rpc = (int)((rows + chunks - 1) / chunks);
+  dim3 grid((N / 4 + 255) / 256, chunks);
+  if (N % 4 != 0) {  // plain column sum only (callers guarantee x == nullptr)
+    dim3 g2((N + 255) / 256, chunks);
+    if (dtype == 0)
+      hipLaunchKernelGGL(colsum_scalar_kernel<float>, g2, dim3(256), 0, st, (const float*)dy, part, rows, N, rpc);
+    else
+      hipLaunchKernelGGL(colsum_scalar_kernel<bf16_t>, g2, dim3(256), 0, st, (const bf16_t*)dy, part, rows, N, rpc);
+  } else if (dtype == 0) {
+    if (x)
+      hipLaunchKernelGGL((colsum_tile_kernel<float, true>), grid, dim3(256), 0, st, (const float*)dy, (const float*)x,
+                         b, (float*)dx, part, rows, N, rpc);
+    else
+      hipLaunchKernelGGL((colsum_tile_kernel<float, false>), grid, dim3(256), 0, st, (const float*)dy, nullptr, b,
+                         nullptr, part, rows, N, rpc);
+  } else {
+    if (x)
+      hipLaunchKernelGGL((colsum_tile_kernel<bf16_t, true>), grid, dim3(256), 0, st, (const bf16_t*)dy,
+                         (const bf16_t*)x, b, (bf16_t*)dx, part, rows, N, rpc);
+    else
+      hipLaunchKernelGGL((colsum_tile_kernel<bf16_t, false>), grid, dim3(256), 0, st, (const bf16_t*)dy, nullptr, b,
+                         nullptr, part, rows, N, rpc);
+  }
+  hipLaunchKernelGGL(partial_rows_sum_kernel, dim3((N + 255) / 256), dim3(256), 0, st, part, chunks, N, out,
+                     accumulate);
+}
+
+void launch_mlm_compact(const int64_t* labels, int rows, int ignore_index, int cap, int32_t* idx, int64_t* lab_out,
+                        int32_t* count, int* err, hipStream_t st) {
+  hipLaunchKernelGGL(mlm_compact_kernel, dim3(1), dim3(1024), 0, st, labels, rows, ignore_index, cap, idx, lab_out,
+                     count, err);
+}
+
+void launch_gather_rows(int dtype, const void* src, const int32_t* idx, void* out, int n, int H, hipStream_t st) {
+  if (n <= 0) return;
+  if (dtype == 0)
+    hipLaunchKernelGGL(gather_rows_kernel<float>, dim3(n), dim3(64), 0, st, (const float*)src, idx, (float*)out, n, H);
+  else
+    hipLaunchKernelGGL(gather_rows_kernel<bf16_t>, dim3(n), dim3(64), 0, st, (const bf16_t*)src, idx, (bf16_t*)out, n,
+                       H);
+}
+
+void launch_scatter_add_rows(int dtype, const void* src, const int32_t* idx, void* dst, int n, int H,
+                             hipStream_t st) {
+  if (n <= 0) return;
+  if (dtype == 0)
+    hipLaunchKernelGGL(scatter_add_rows_kernel<float>, dim3(n), dim3(64), 0, st, (const float*)src, idx, (float*)dst,
+                       n, H);
+  else
+    hipLaunchKernelGGL(scatter_add_rows_kernel<bf16_t>, dim3(n), dim3(64), 0, st, (const bf16_t*)src, idx,
+                       (bf16_t*)dst, n, H);
+}

@@ -1,0 +1,455 @@
+// Row LayerNorm family for BERT (K03, K05, K06, K10 of SURVEY §2.4).
+//
+// Reference math (bert_modeling.py:285-289): u = mean(x); s = mean((x-u)^2);
+// y = w * (x-u)/sqrt(s+eps) + b with eps = 1e-12 and a BIASED variance.
+// Reference call sites fused here:
+//   * BertSelfOutput/BertOutput (bert_modeling.py:387-391, 423-427):
+//       y = LN(dropout(dense_out + bias) + residual)        -> mode kBDR
+//   * BertEmbeddings (bert_modeling.py:306-320):
+//       y = dropout(LN(word[id] + pos[s] + type[tt]))         -> emb kernels
+//   * BertPredictionHeadTransform LN (bert_modeling.py:525-528) -> mode kPlain
+//
+// Layout: one wave per row, lane l owns columns (k*64+l)*4 .. +3 for k < NV,
+// so every global access is a coalesced 16-byte-per-lane vector (H = NV*256).
+// Statistics are two-pass in registers (exactly the reference's formula).
+// Backward kernels produce the row gradient and per-block column partials of
+// dgamma/dbeta/dbias; `colpart_finalize` reduces the partials (no atomics,
+// deterministic).  Dropout masks are regenerated from Philox (seed, offset).
+#include "common.h"
+
+namespace hs {
+
+enum LnMode : int { kPlain = 0, kBDR = 1 };
+
+template <int NV>
+HS_DEVICE void row_stats(const float (&x)[NV][4], int H, float& mean, float& rstd, float eps) {
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) s += (x[k][0] + x[k][1]) + (x[k][2] + x[k][3]);
+  mean = wave_sum(s) / H;
+  float v = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float d = x[k][j] - mean;
+      v = fmaf(d, d, v);
+    }
+  v = wave_sum(v) / H;
+  rstd = 1.0f / sqrtf(v + eps);
+}
+
+template <int NV, typename T>
+__global__ void __launch_bounds__(256) ln_fwd_kernel(const T* __restrict__ a, const float* __restrict__ bias,
+                                                     const T* __restrict__ resid, const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta, T* __restrict__ y,
+                                                     float* __restrict__ zsave, float* __restrict__ mean_out,
+                                                     float* __restrict__ rstd_out, int rows, float eps, float p,
+                                                     uint64_t seed, uint64_t off, int mode) {
+  constexpr int H = NV * 256;
+  const int lane = threadIdx.x & 63;
+  const float scale = p < 1.f ? 1.0f / (1.0f - p) : 0.f;
+  for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += gridDim.x * 4) {
+    const int64_t base = (int64_t)row * H;
+    float x[NV][4];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = (k * 64 + lane) * 4;
+      load4(a + base + c, x[k]);
+      if (bias) {
+        float b[4];
+        load4(bias + c, b);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) x[k][j] += b[j];
+      }
+      if (mode == kBDR && p > 0.f) {
+        float m[4];
+        keep4(seed, off, (uint64_t)(base + c) >> 2, p, scale, m);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) x[k][j] *= m[j];
+      }
+      if (resid) {
+        float r[4];
+        load4(resid + base + c, r);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) x[k][j] += r[j];
+      }
+      if (zsave) store4(zsave + base + c, x[k]);
+    }
+    float mean, rstd;
+    row_stats<NV>(x, H, mean, rstd, eps);
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = (k * 64 + lane) * 4;
+      float gw[4], gb[4], o[4];
+      load4(gamma + c, gw);
+      load4(beta + c, gb);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = gw[j] * ((x[k][j] - mean) * rstd) + gb[j];
+      store4(y + base + c, o);
+    }
+    if (lane == 0) {
+      mean_out[row] = mean;
+      rstd_out[row] = rstd;
+    }
+  }
+}
+
+// Column partials are written as part[blockIdx.x][H] (one row per block).
+template <int NV>
+HS_DEVICE void block_colpart_store(float (&acc)[NV][4], float* __restrict__ part, float* lds) {
+  constexpr int H = NV * 256;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // lds: [4][H]
+#pragma unroll
+  for (int k = 0; k < NV; ++k) store4(lds + w * H + (k * 64 + lane) * 4, acc[k]);
+  __syncthreads();
+  for (int c = threadIdx.x; c < H; c += blockDim.x)
+    part[(int64_t)blockIdx.x * H + c] = (lds[c] + lds[H + c]) + (lds[2 * H + c] + lds[3 * H + c]);
+  __syncthreads();
+}
+
+template <int NV, typename T>
+__global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, const float* __restrict__ zsave,
+                                                     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+                                                     const float* __restrict__ gamma, T* __restrict__ dz_out,
+                                                     T* __restrict__ da_out, float* __restrict__ part_gamma,
+                                                     float* __restrict__ part_beta, float* __restrict__ part_bias,
+                                                     int rows, float p, uint64_t seed, uint64_t off, int mode) {
+  constexpr int H = NV * 256;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int lane = threadIdx.x & 63;
+  const float scale = p < 1.f ? 1.0f / (1.0f - p) : 0.f;
+  float ag[NV][4], ab[NV][4], abias[NV][4];
+#pragma unroll
+  for (int k = 0; k < NV; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ag[k][j] = ab[k][j] = abias[k][j] = 0.f;
+  for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += gridDim.x * 4) {
+    const int64_t base = (int64_t)row * H;
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float xh[NV][4], g[NV][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = (k * 64 + lane) * 4;
+      float d[4], z[4], gw[4];
+      load4(dy + base + c, d);
+      load4(zsave + base + c, z);
+      load4(gamma + c, gw);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        xh[k][j] = (z[j] - mean) * rstd;
+        g[k][j] = d[j] * gw[j];
+        ag[k][j] = fmaf(d[j], xh[k][j], ag[k][j]);
+        ab[k][j] += d[j];
+        s1 += g[k][j];
+        s2 = fmaf(g[k][j], xh[k][j], s2);
+      }
+    }
+    s1 = wave_sum(s1) / H;
+    s2 = wave_sum(s2) / H;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = (k * 64 + lane) * 4;
+      float dz[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dz[j] = rstd * (g[k][j] - s1 - xh[k][j] * s2);
+      if (dz_out) store4(dz_out + base + c, dz);
+      if (mode == kBDR) {
+        float m[4] = {1.f, 1.f, 1.f, 1.f};
+        if (p > 0.f) keep4(seed, off, (uint64_t)(base + c) >> 2, p, scale, m);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          dz[j] *= m[j];
+          abias[k][j] += dz[j];
+        }
+        if (da_out) store4(da_out + base + c, dz);
+      }
+    }
+  }
+  block_colpart_store<NV>(ag, part_gamma, lds);
+  block_colpart_store<NV>(ab, part_beta, lds);
+  if (mode == kBDR && part_bias) block_colpart_store<NV>(abias, part_bias, lds);
+}
+
+// ------------------------------------------------------------ embeddings
+template <int NV, typename T>
+__global__ void __launch_bounds__(256) emb_fwd_kernel(const int64_t* __restrict__ ids, const int64_t* __restrict__ tt,
+                                                      const float* __restrict__ wemb, const float* __restrict__ pemb,
+                                                      const float* __restrict__ temb, const float* __restrict__ gamma,
+                                                      const float* __restrict__ beta, T* __restrict__ y,
+                                                      float* __restrict__ zsave, float* __restrict__ mean_out,
+                                                      float* __restrict__ rstd_out, int rows, int S, int V, int TV,
+                                                      float eps, float p, uint64_t seed, uint64_t off,
+                                                      int* __restrict__ err) {
+  constexpr int H = NV * 256;
+  const int lane = threadIdx.x & 63;
+  const float scale = p < 1.f ? 1.0f / (1.0f - p) : 0.f;
+  for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += gridDim.x * 4) {
+    const int64_t base = (int64_t)row * H;
+    int64_t id = ids[row];
+    int64_t t = tt ? tt[row] : 0;
+    if (id < 0 || id >= V || t < 0 || t >= TV) {  // never read out of bounds; flag it
+      if (lane == 0) atomicOr(err, 1);
+      id = id < 0 ? 0 : (id >= V ? V - 1 : id);
+      t = t < 0 ? 0 : (t >= TV ? TV - 1 : t);
+    }
+    const int s = row % S;
+    float x[NV][4];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = (k * 64 + lane) * 4;
+      float w[4], q[4], r[4];
+      load4(wemb + id * H + c, w);
+      load4(pemb + (int64_t)s * H + c, q);
+      load4(temb + t * H + c, r);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) x[k][j] = (w[j] + q[j]) + r[j];
+      store4(zsave + base + c, x[k]);
+    }
+    float mean, rstd;
+    row_stats<NV>(x, H, mean, rstd, eps);
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = (k * 64 + lane) * 4;
+      float gw[4], gb[4], o[4], m[4] = {1.f, 1.f, 1.f, 1.f};
+      load4(gamma + c, gw);
+      load4(beta + c, gb);
+      if (p > 0.f) keep4(seed, off, (uint64_t)(base + c) >> 2, p, scale, m);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = (gw[j] * ((x[k][j] - mean) * rstd) + gb[j]) * m[j];
+      store4(y + base + c, o);
+    }
+    if (lane == 0) {
+      mean_out[row] = mean;
+      rstd_out[row] = rstd;
+    }
+  }
+}
+
+// dword/dpos are accumulated with float atomics (full 256-B wave rows, the
+// fast atomic shape); the token-type gradient (2 rows in BERT) is pre-reduced
+// in registers and LDS first -- 4096 rows into 2 would otherwise serialise.
+template <int NV, typename T>
+__global__ void __launch_bounds__(256) emb_bwd_kernel(const T* __restrict__ dy, const int64_t* __restrict__ ids,
+                                                      const int64_t* __restrict__ tt, const float* __restrict__ zsave,
+                                                      const float* __restrict__ mean_in,
+                                                      const float* __restrict__ rstd_in,
+                                                      const float* __restrict__ gamma, float* __restrict__ dword,
+                                                      float* __restrict__ dpos, float* __restrict__ dtype,
+                                                      float* __restrict__ part_gamma, float* __restrict__ part_beta,
+                                                      int rows, int S, int V, int TV, float p, uint64_t seed,
+                                                      uint64_t off) {
+  constexpr int H = NV * 256;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int lane = threadIdx.x & 63;
+  const float scale = p < 1.f ? 1.0f / (1.0f - p) : 0.f;
+  float ag[NV][4], ab[NV][4], at0[NV][4], at1[NV][4];
+#pragma unroll
+  for (int k = 0; k < NV; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ag[k][j] = ab[k][j] = at0[k][j] = at1[k][j] = 0.f;
+  for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += gridDim.x * 4) {
+    const int64_t base = (int64_t)row * H;
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    int64_t id = ids[row];
+    int64_t t = tt ? tt[row] : 0;
+    id = id < 0 ? 0 : (id >= V ? V - 1 : id);
+    t = t < 0 ? 0 : (t >= TV ? TV - 1 : t);
+    const int s = row % S;
+    float xh[NV][4], g[NV][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = (k * 64 + lane) * 4;
+      float d[4], z[4], gw[4], m[4] = {1.f, 1.f, 1.f, 1.f};
+      load4(dy + base + c, d);
+      load4(zsave + base + c, z);
+      load4(gamma + c, gw);
+      if (p > 0.f) keep4(seed, off, (uint64_t)(base + c) >> 2, p, scale, m);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        d[j] *= m[j];
+        xh[k][j] = (z[j] - mean) * rstd;
+        g[k][j] = d[j] * gw[j];
+        ag[k][j] = fmaf(d[j], xh[k][j], ag[k][j]);
+        ab[k][j] += d[j];
+        s1 += g[k][j];
+        s2 = fmaf(g[k][j], xh[k][j], s2);
+      }
+    }
+    s1 = wave_sum(s1) / H;
+    s2 = wave_sum(s2) / H;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = (k * 64 + lane) * 4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float dz = rstd * (g[k][j] - s1 - xh[k][j] * s2);
+        atomicAdd(dword + id * H + c + j, dz);
+        atomicAdd(dpos + (int64_t)s * H + c + j, dz);
+        if (TV <= 2) {
+          if (t == 0) at0[k][j] += dz; else at1[k][j] += dz;
+        } else {
+          atomicAdd(dtype + t * H + c + j, dz);
+        }
+      }
+    }
+  }
+  block_colpart_store<NV>(ag, part_gamma, lds);
+  block_colpart_store<NV>(ab, part_beta, lds);
+  if (TV <= 2) {
+    const int w = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) store4(lds + w * H + (k * 64 + lane) * 4, at0[k]);
+    __syncthreads();
+    for (int c = threadIdx.x; c < H; c += blockDim.x)
+      atomicAdd(dtype + c, (lds[c] + lds[H + c]) + (lds[2 * H + c] + lds[3 * H + c]));
+    __syncthreads();
+    if (TV == 2) {
+#pragma unroll
+      for (int k = 0; k < NV; ++k) store4(lds + w * H + (k * 64 + lane) * 4, at1[k]);
+      __syncthreads();
+      for (int c = threadIdx.x; c < H; c += blockDim.x)
+        atomicAdd(dtype + H + c, (lds[c] + lds[H + c]) + (lds[2 * H + c] + lds[3 * H + c]));
+    }
+  }
+}
+
+// out[c] (+)= sum_r part[r][c]; grid.y selects one of up to 3 (part, out) pairs.
+struct ColPartArgs {
+  const float* part[3];
+  float* out[3];
+};
+__global__ void colpart_finalize_kernel(ColPartArgs args, int nparts, int H, int accumulate) {
+  const float* part = args.part[blockIdx.y];
+  float* out = args.out[blockIdx.y];
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= H) return;
+  float s = 0.f;
+  for (int r = 0; r < nparts; ++r) s += part[(int64_t)r * H + c];
+  out[c] = accumulate ? out[c] + s : s;
+}
+
+constexpr int kLnBwdBlocks = 256;
+
+template <int NV, typename T>
+void ln_fwd_launch(const void* a, const float* bias, const void* resid, const float* gamma, const float* beta, void* y,
+                   float* zsave, float* mean, float* rstd, int rows, float eps, float p, uint64_t seed, uint64_t off,
+                   int mode, hipStream_t st) {
+  int grid = (rows + 3) / 4;
+  if (grid > 4096) grid = 4096;
+  hipLaunchKernelGGL((ln_fwd_kernel<NV, T>), dim3(grid), dim3(256), 0, st, (const T*)a, bias, (const T*)resid, gamma,
+                     beta, (T*)y, zsave, mean, rstd, rows, eps, p, seed, off, mode);
+}
+
+template <int NV, typename T>
+void ln_bwd_launch(const void* dy, const float* zsave, const float* mean, const float* rstd, const float* gamma,
+                   void* dz, void* da, float* pg, float* pb, float* pbias, int rows, float p, uint64_t seed,
+                   uint64_t off, int mode, hipStream_t st) {
+  constexpr int H = NV * 256;
+  hipLaunchKernelGGL((ln_bwd_kernel<NV, T>), dim3(kLnBwdBlocks), dim3(256), 4 * H * sizeof(float), st, (const T*)dy,
+                     zsave, mean, rstd, gamma, (T*)dz, (T*)da, pg, pb, pbias, rows, p, seed, off, mode);
+}
+
+template <int NV, typename T>
+void emb_fwd_launch(const int64_t* ids, const int64_t* tt, const float* w, const float* pe, const float* te,
+                    const float* gamma, const float* beta, void* y, float* zsave, float* mean, float* rstd, int rows,
+                    int S, int V, int TV, float eps, float p, uint64_t seed, uint64_t off, int* err, hipStream_t st) {
+  int grid = (rows + 3) / 4;
+  if (grid > 4096) grid = 4096;
+  hipLaunchKernelGGL((emb_fwd_kernel<NV, T>), dim3(grid), dim3(256), 0, st, ids, tt, w, pe, te, gamma, beta, (T*)y,
+                     zsave, mean, rstd, rows, S, V, TV, eps, p, seed, off, err);
+}
+
+template <int NV, typename T>
+void emb_bwd_launch(const void* dy, const int64_t* ids, const int64_t* tt, const float* zsave, const float* mean,
+                    const float* rstd, const float* gamma, float* dw, float* dp, float* dt, float* pg, float* pb,
+                    int rows, int S, int V, int TV, float p, uint64_t seed, uint64_t off, hipStream_t st) {
+  constexpr int H = NV * 256;
+  hipLaunchKernelGGL((emb_bwd_kernel<NV, T>), dim3(kLnBwdBlocks), dim3(256), 4 * H * sizeof(float), st,
+                     (const T*)dy, ids, tt, zsave, mean, rstd, gamma, dw, dp, dt, pg, pb, rows, S, V, TV, p, seed,
+                     off);
+}
+
+}  // namespace hs
+
+using namespace hs;
+
+#define HS_DISPATCH_H(H, ...)                              \
+  switch (H) {                                             \
+    case 256: { constexpr int NV = 1; __VA_ARGS__; break; } \
+    case 512: { constexpr int NV = 2; __VA_ARGS__; break; } \
+    case 768: { constexpr int NV = 3; __VA_ARGS__; break; } \
+    case 1024: { constexpr int NV = 4; __VA_ARGS__; break; } \
+    case 1536: { constexpr int NV = 6; __VA_ARGS__; break; } \
+    case 2048: { constexpr int NV = 8; __VA_ARGS__; break; } \
+    default: return -1;                                    \
+  }
+
+int ln_bwd_num_blocks() { return kLnBwdBlocks; }
+
+int launch_ln_fwd(int dtype, const void* a, const float* bias, const void* resid, const float* gamma,
+                  const float* beta, void* y, float* zsave, float* mean, float* rstd, int rows, int H, float eps,
+                  float p, uint64_t seed, uint64_t off, int mode, hipStream_t st) {
+  if (dtype == 0) {
+    HS_DISPATCH_H(H, (ln_fwd_launch<NV, float>(a, bias, resid, gamma, beta, y, zsave, mean, rstd, rows, eps, p, seed,
+                                               off, mode, st)));
+  } else {
+    HS_DISPATCH_H(H, (ln_fwd_launch<NV, bf16_t>(a, bias, resid, gamma, beta, y, zsave, mean, rstd, rows, eps, p, seed,
+                                                off, mode, st)));
+  }
+  return 0;
+}
+
+int launch_ln_bwd(int dtype, const void* dy, const float* zsave, const float* mean, const float* rstd,
+                  const float* gamma, void* dz, void* da, float* pg, float* pb, float* pbias, int rows, int H, float p,
+                  uint64_t seed, uint64_t off, int mode, hipStream_t st) {
+  if (dtype == 0) {
+    HS_DISPATCH_H(H, (ln_bwd_launch<NV, float>(dy, zsave, mean, rstd, gamma, dz, da, pg, pb, pbias, rows, p, seed, off,
+                                               mode, st)));
+  } else {
+    HS_DISPATCH_H(H, (ln_bwd_launch<NV, bf16_t>(dy, zsave, mean, rstd, gamma, dz, da, pg, pb, pbias, rows, p, seed,
+                                                off, mode, st)));
+  }
+  return 0;
+}
+
+int launch_emb_fwd(int dtype, const int64_t* ids, const int64_t* tt, const float* w, const float* pe, const float* te,
+                   const float* gamma, const float* beta, void* y, float* zsave, float* mean, float* rstd, int rows,
+                   int S, int H, int V, int TV, float eps, float p, uint64_t seed, uint64_t off, int* err,
+                   hipStream_t st) {
+  if (dtype == 0) {
+    HS_DISPATCH_H(H, (emb_fwd_launch<NV, float>(ids, tt, w, pe, te, gamma, beta, y, zsave, mean, rstd, rows, S, V, TV,
+                                                eps, p, seed, off, err, st)));
+  } else {
+    HS_DISPATCH_H(H, (emb_fwd_launch<NV, bf16_t>(ids, tt, w, pe, te, gamma, beta, y, zsave, mean, rstd, rows, S, V,
+                                                 TV, eps, p, seed, off, err, st)));
+  }
+  return 0;
+}
+
+int launch_emb_bwd(int dtype, const void* dy, const int64_t* ids, const int64_t* tt, const float* zsave,
+                   const float* mean, const float* rstd, const float* gamma, float* dw, float* dp, float* dt, float* pg,
+                   float* pb, int rows, int S, int H, int V, int TV, float p, uint64_t seed, uint64_t off,
+                   hipStream_t st) {
+  if (dtype == 0) {
+    HS_DISPATCH_H(H, (emb_bwd_launch<NV, float>(dy, ids, tt, zsave, mean, rstd, gamma, dw, dp, dt, pg, pb, rows, S, V,
+                                                TV, p, seed, off, st)));
+  } else {
+    HS_DISPATCH_H(H, (emb_bwd_launch<NV, bf16_t>(dy, ids, tt, zsave, mean, rstd, gamma, dw, dp, dt, pg, pb, rows, S,
+                                                 V, TV, p, seed, off, st)));
+  }
+  return 0;
+}
+
+void launch_colpart_finalize(const float* const* parts, float* const* outs, int n, int nparts, int H, int accumulate,
+                             hipStream_t st) {
+  ColPartArgs a{};
+  for (int i = 0; i < n; ++i) {
+    a.part[i] = parts[i];
+    a.out[i] = outs[i];
+  }
+  hipLaunchKernelGGL(colpart_finalize_kernel, dim3((H + 255) / 256, n), dim3(256), 0, st, a, nparts, H, accumulate);
+}

@@ -1,0 +1,258 @@
+// Fused flat-buffer optimizer kernels (K11-K14 of SURVEY §2.4).
+//
+// The reference runs a Python loop over 206 parameters with ~8-10 ATen
+// kernels each (reference: optim.py:162-231 Adam, :263-304 Adadelta) plus a
+// per-parameter multiply_grads (optim.py:59-63) and clip_grad_norm
+// (optim.py:65-70).  Here every parameter lives in ONE contiguous fp32 buffer
+// (hetseq_amd/runtime/flat.py), so the whole update is:
+//   1. sumsq_partial  -- grid-stride sum of g^2 into per-block partials
+//   2. norm_finalize  -- total norm, clip coefficient and the combined grad
+//                        multiplier (grad-scale x clip) written to device memory
+//   3. adam_flat / adadelta_flat -- one vectorised pass reading the multiplier
+//                        from device memory (no host sync anywhere)
+// Adam math follows the reference exactly (Q20): decoupled weight decay
+// applied to every element before the update, denom = sqrt(v) + eps, step
+// size lr*sqrt(1-b2^t)/(1-b1^t).
+#include "common.h"
+
+namespace hs {
+
+constexpr int kRedBlocks = 1024;
+constexpr int kRedThreads = 256;
+
+__global__ void __launch_bounds__(kRedThreads) sumsq_partial_kernel(const float* __restrict__ g, int64_t n,
+                                                                    double* __restrict__ partial) {
+  const int64_t n4 = n >> 2;
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  float acc = 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const float4 v = g4[i];
+    acc = fmaf(v.x, v.x, acc);
+    acc = fmaf(v.y, v.y, acc);
+    acc = fmaf(v.z, v.z, acc);
+    acc = fmaf(v.w, v.w, acc);
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+    const float v = g[(n4 << 2) + threadIdx.x];
+    acc = fmaf(v, v, acc);
+  }
+  double d = wave_sum_d(static_cast<double>(acc));
+  __shared__ double red[kRedThreads / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) red[w] = d;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0;
+    for (int i = 0; i < kRedThreads / 64; ++i) s += red[i];
+    partial[blockIdx.x] = s;
+  }
+}
+
+// out[0] = total norm of (scale*g); out[1] = combined multiplier for g;
+// out[2] = clip coefficient actually applied (1 when not clipping).
+// `scale` is read from device memory (may be nullptr -> 1).
+__global__ void norm_finalize_kernel(const double* __restrict__ partial, int nparts, const float* __restrict__ scale,
+                                     float max_norm, float* __restrict__ out) {
+  double s = 0;
+  for (int i = threadIdx.x; i < nparts; i += blockDim.x) s += partial[i];
+  s = wave_sum_d(s);
+  __shared__ double red[16];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) red[w] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double tot = 0;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) tot += red[i];
+    const float c = scale ? scale[0] : 1.0f;
+    const float norm = fabsf(c) * static_cast<float>(sqrt(tot));
+    float clip = 1.0f;
+    if (max_norm > 0.f) {
+      // torch.nn.utils.clip_grad_norm_: coef = max_norm / (norm + 1e-6), clamped to 1
+      const float coef = max_norm / (norm + 1e-6f);
+      clip = coef < 1.0f ? coef : 1.0f;
+    }
+    out[0] = norm;
+    out[1] = c * clip;
+    out[2] = clip;
+  }
+}
+
+template <bool kShadow>
+__global__ void __launch_bounds__(256) adam_flat_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                        float* __restrict__ m, float* __restrict__ v,
+                                                        bf16_t* __restrict__ shadow, int64_t n,
+                                                        const float* __restrict__ gmul, float lr, float b1,
+                                                        float b2, float eps, float wd, float step_size) {
+  const float mul = gmul ? gmul[0] : 1.0f;
+  const float omb1 = 1.0f - b1, omb2 = 1.0f - b2, decay = -wd * lr;
+  const int64_t n4 = n >> 2;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    float pp[4], gg[4], mm[4], vv[4];
+    load4(p + 4 * i, pp);
+    load4(g + 4 * i, gg);
+    load4(m + 4 * i, mm);
+    load4(v + 4 * i, vv);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float gk = gg[k] * mul;
+      mm[k] = mm[k] * b1 + omb1 * gk;
+      vv[k] = vv[k] * b2 + omb2 * gk * gk;
+      const float denom = sqrtf(vv[k]) + eps;
+      if (wd != 0.f) pp[k] = pp[k] + decay * pp[k];
+      pp[k] = pp[k] - step_size * (mm[k] / denom);
+    }
+    store4(p + 4 * i, pp);
+    store4(m + 4 * i, mm);
+    store4(v + 4 * i, vv);
+    if (kShadow) store4(shadow + 4 * i, pp);
+  }
+  // scalar tail
+  const int64_t tail = n - (n4 << 2);
+  if (blockIdx.x == 0 && threadIdx.x < tail) {
+    const int64_t i = (n4 << 2) + threadIdx.x;
+    const float gk = g[i] * mul;
+    float mk = m[i] * b1 + omb1 * gk;
+    float vk = v[i] * b2 + omb2 * gk * gk;
+    float pk = p[i];
+    if (wd != 0.f) pk = pk + decay * pk;
+    pk = pk - step_size * (mk / (sqrtf(vk) + eps));
+    p[i] = pk;
+    m[i] = mk;
+    v[i] = vk;
+    if (kShadow) shadow[i] = from_f<bf16_t>(pk);
+  }
+}
+
+template <bool kShadow>
+__global__ void __launch_bounds__(256) adadelta_flat_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                            float* __restrict__ sq, float* __restrict__ acc,
+                                                            bf16_t* __restrict__ shadow, int64_t n,
+                                                            const float* __restrict__ gmul, float lr, float rho,
+                                                            float eps, float wd) {
+  const float mul = gmul ? gmul[0] : 1.0f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float gk = g[i] * mul;
+    float pk = p[i];
+    if (wd != 0.f) gk = gk + wd * pk;
+    const float s = sq[i] * rho + (1.f - rho) * gk * gk;
+    const float stdv = sqrtf(s + eps);
+    const float delta = sqrtf(acc[i] + eps) / stdv * gk;
+    pk = pk - lr * delta;
+    acc[i] = acc[i] * rho + (1.f - rho) * delta * delta;
+    sq[i] = s;
+    p[i] = pk;
+    if (kShadow) shadow[i] = from_f<bf16_t>(pk);
+  }
+}
+
+// LAMB (extension beyond the reference; BASELINE north star names it).
+// Stage 1: per-segment update direction u = m_hat/(sqrt(v_hat)+eps) + wd*p is
+// written into `upd`, and per-segment ||p||^2, ||u||^2 partials accumulate via
+// one atomic per block per segment.  Stage 2 applies p -= lr * trust * u.
+__global__ void __launch_bounds__(256) lamb_stage1_kernel(const float* __restrict__ p, const float* __restrict__ g,
+                                                          float* __restrict__ m, float* __restrict__ v,
+                                                          float* __restrict__ upd, const int64_t* __restrict__ seg_off,
+                                                          int nseg, float* __restrict__ seg_norms,
+                                                          const float* __restrict__ gmul, float b1, float b2,
+                                                          float eps, float wd, float bc1, float bc2) {
+  const int s = blockIdx.y;
+  const int64_t beg = seg_off[s], end = seg_off[s + 1];
+  const float mul = gmul ? gmul[0] : 1.0f;
+  float pn = 0.f, un = 0.f;
+  for (int64_t i = beg + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < end; i += (int64_t)gridDim.x * blockDim.x) {
+    const float gk = g[i] * mul;
+    const float mk = m[i] * b1 + (1.f - b1) * gk;
+    const float vk = v[i] * b2 + (1.f - b2) * gk * gk;
+    m[i] = mk;
+    v[i] = vk;
+    const float u = (mk / bc1) / (sqrtf(vk / bc2) + eps) + wd * p[i];
+    upd[i] = u;
+    pn = fmaf(p[i], p[i], pn);
+    un = fmaf(u, u, un);
+  }
+  pn = wave_sum(pn);
+  un = wave_sum(un);
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(&seg_norms[2 * s], pn);
+    atomicAdd(&seg_norms[2 * s + 1], un);
+  }
+}
+
+template <bool kShadow>
+__global__ void __launch_bounds__(256) lamb_stage2_kernel(float* __restrict__ p, const float* __restrict__ upd,
+                                                          bf16_t* __restrict__ shadow,
+                                                          const int64_t* __restrict__ seg_off,
+                                                          const float* __restrict__ seg_norms, float lr) {
+  const int s = blockIdx.y;
+  const int64_t beg = seg_off[s], end = seg_off[s + 1];
+  const float pn = sqrtf(seg_norms[2 * s]), un = sqrtf(seg_norms[2 * s + 1]);
+  const float trust = (pn > 0.f && un > 0.f) ? pn / un : 1.0f;
+  for (int64_t i = beg + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < end; i += (int64_t)gridDim.x * blockDim.x) {
+    const float pk = p[i] - lr * trust * upd[i];
+    p[i] = pk;
+    if (kShadow) shadow[i] = from_f<bf16_t>(pk);
+  }
+}
+
+__global__ void cast_f32_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    y[i] = from_f<bf16_t>(x[i]);
+}
+
+static int grid_for(int64_t n_items, int threads, int cap = 4096) {
+  int64_t g = (n_items + threads - 1) / threads;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return static_cast<int>(g);
+}
+
+}  // namespace hs
+
+using namespace hs;
+
+void launch_grad_norm(const float* g, int64_t n, double* partial, const float* scale, float max_norm, float* out,
+                      hipStream_t st) {
+  hipLaunchKernelGGL(sumsq_partial_kernel, dim3(kRedBlocks), dim3(kRedThreads), 0, st, g, n, partial);
+  hipLaunchKernelGGL(norm_finalize_kernel, dim3(1), dim3(1024), 0, st, partial, kRedBlocks, scale, max_norm, out);
+}
+
+void launch_adam_flat(float* p, const float* g, float* m, float* v, void* shadow, int64_t n, const float* gmul,
+                      float lr, float b1, float b2, float eps, float wd, float step_size, hipStream_t st) {
+  const int grid = grid_for(n / 4 + 1, 256, 8192);
+  if (shadow)
+    hipLaunchKernelGGL(adam_flat_kernel<true>, dim3(grid), dim3(256), 0, st, p, g, m, v,
+                       reinterpret_cast<bf16_t*>(shadow), n, gmul, lr, b1, b2, eps, wd, step_size);
+  else
+    hipLaunchKernelGGL(adam_flat_kernel<false>, dim3(grid), dim3(256), 0, st, p, g, m, v, nullptr, n, gmul, lr, b1,
+                       b2, eps, wd, step_size);
+}
+
+void launch_adadelta_flat(float* p, const float* g, float* sq, float* acc, void* shadow, int64_t n,
+                          const float* gmul, float lr, float rho, float eps, float wd, hipStream_t st) {
+  const int grid = grid_for(n, 256, 8192);
+  if (shadow)
+    hipLaunchKernelGGL(adadelta_flat_kernel<true>, dim3(grid), dim3(256), 0, st, p, g, sq, acc,
+                       reinterpret_cast<bf16_t*>(shadow), n, gmul, lr, rho, eps, wd);
+  else
+    hipLaunchKernelGGL(adadelta_flat_kernel<false>, dim3(grid), dim3(256), 0, st, p, g, sq, acc, nullptr, n, gmul,
+                       lr, rho, eps, wd);
+}
+
+void launch_lamb_flat(float* p, const float* g, float* m, float* v, float* upd, void* shadow, const int64_t* seg_off,
+                      int nseg, float* seg_norms, const float* gmul, float lr, float b1, float b2, float eps, float wd,
+                      float bc1, float bc2, hipStream_t st) {
+  hipMemsetAsync(seg_norms, 0, sizeof(float) * 2 * nseg, st);
+  hipLaunchKernelGGL(lamb_stage1_kernel, dim3(32, nseg), dim3(256), 0, st, p, g, m, v, upd, seg_off, nseg, seg_norms,
+                     gmul, b1, b2, eps, wd, bc1, bc2);
+  if (shadow)
+    hipLaunchKernelGGL(lamb_stage2_kernel<true>, dim3(32, nseg), dim3(256), 0, st, p, upd,
+                       reinterpret_cast<bf16_t*>(shadow), seg_off, seg_norms, lr);
+  else
+    hipLaunchKernelGGL(lamb_stage2_kernel<false>, dim3(32, nseg), dim3(256), 0, st, p, upd, nullptr, seg_off,
+                       seg_norms, lr);
+}
+
+void launch_cast_f32_bf16(const float* x, void* y, int64_t n, hipStream_t st) {
+  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0, st, x,
+                     reinterpret_cast<bf16_t*>(y), n);
+}

@@ -1,0 +1,229 @@
+"""BERT pre-training shards over the native HDF5 reader.
+
+Capability parity with ``BertH5pyData`` / ``ConBertH5pyData`` (reference:
+data/h5pyDataset.py:13-134): per-shard datasets, concatenation with global
+index -> (shard, row) bisect, ``ordered_indices = arange``, constant
+``num_tokens = size = max_pred_length`` (Q11), a ``default_collate``-style
+collater returning ``[input_ids, segment_ids, input_mask, masked_lm_labels,
+next_sentence_labels]`` (int64) and ``None`` for an empty batch.
+
+The MI355X data path (``make_batch_stream``) replaces per-sample
+``h5py.File`` opens (the reference opens the file for every sample) with:
+C++ reader threads -> pinned staging ring -> non_blocking H2D on a side HIP
+stream, event-fenced to the compute stream.
+"""
+from __future__ import annotations
+
+import bisect
+
+import numpy as np
+import torch
+import torch.utils.data
+
+from hetseq_amd.ops._C import h5 as _h5
+
+
+class BertH5Dataset(torch.utils.data.Dataset):
+    """One HDF5 shard (file opened once, kept open)."""
+
+    def __init__(self, path, max_pred_length=512):
+        super().__init__()
+        self.path = path
+        self.max_pred_length = max_pred_length
+        self.shard = _h5().H5Shard(path, max_pred_length)
+        self._len = len(self.shard)
+        self.seq_len = self.shard.seq_len
+        self.num_pred = self.shard.num_pred
+
+    def __len__(self):
+        return self._len
+
+    def __getitem__(self, index):
+        if index < 0 or index >= self._len:
+            raise IndexError("index out of range")
+        S = self.seq_len
+        ids, seg, mask, lab = (np.empty((1, S), np.int64) for _ in range(4))
+        nsp = np.empty((1,), np.int64)
+        self.shard.read_rows(int(index), 1, ids.ctypes.data, seg.ctypes.data, mask.ctypes.data, lab.ctypes.data,
+                             nsp.ctypes.data, 0)
+        return [torch.from_numpy(ids[0]), torch.from_numpy(seg[0]), torch.from_numpy(mask[0]),
+                torch.from_numpy(lab[0]), torch.from_numpy(nsp)[0]]
+
+    def size(self, idx):
+        return self.max_pred_length
+
+    def set_epoch(self, epoch):
+        pass
+
+
+def _collate(samples):
+    if len(samples) == 0:
+        return None
+    return [torch.stack([s[k] for s in samples]) for k in range(5)]
+
+
+class ConBertH5Dataset(torch.utils.data.Dataset):
+    """Concatenation of shards (reference: ConBertH5pyData)."""
+
+    @staticmethod
+    def cumsum(sequence, sample_ratios):
+        r, s = [], 0
+        for e, ratio in zip(sequence, sample_ratios):
+            curr_len = int(ratio * len(e))
+            r.append(curr_len + s)
+            s += curr_len
+        return r
+
+    def __init__(self, datasets, sample_ratios=1):
+        super().__init__()
+        assert len(datasets) > 0, "datasets should not be an empty iterable"
+        self.datasets = list(datasets)
+        if isinstance(sample_ratios, int):
+            sample_ratios = [sample_ratios] * len(self.datasets)
+        self.sample_ratios = sample_ratios
+        self.cumulative_sizes = self.cumsum(self.datasets, sample_ratios)
+        self.real_sizes = [len(d) for d in self.datasets]
+        self.seq_len = self.datasets[0].seq_len
+        self.num_pred = max(d.num_pred for d in self.datasets)
+        self.max_pred_length = self.datasets[0].max_pred_length
+        self._set = None
+        if all(r == 1 for r in sample_ratios):
+            self._set = _h5().ShardSet([d.shard for d in self.datasets])
+
+    # ---- reference protocol
+    def __len__(self):
+        return self.cumulative_sizes[-1]
+
+    def __getitem__(self, idx):
+        dataset_idx, sample_idx = self._get_dataset_and_sample_index(idx)
+        return self.datasets[dataset_idx][sample_idx]
+
+    def _get_dataset_and_sample_index(self, idx):
+        dataset_idx = bisect.bisect_right(self.cumulative_sizes, idx)
+        sample_idx = idx if dataset_idx == 0 else idx - self.cumulative_sizes[dataset_idx - 1]
+        sample_idx = sample_idx % self.real_sizes[dataset_idx]
+        return dataset_idx, sample_idx
+
+    def collater(self, samples):
+        return _collate(samples)
+
+    def ordered_indices(self):
+        return np.arange(len(self))
+
+    @property
+    def constant_num_tokens(self):
+        return self.max_pred_length
+
+    def num_tokens(self, index):
+        return self.max_pred_length
+
+    def size(self, idx):
+        return self.max_pred_length
+
+    def set_epoch(self, epoch):
+        pass
+
+    # ---- native data path
+    def read_batch(self, indices):
+        """Collate ``indices`` into freshly allocated CPU int64 tensors."""
+        idx = np.ascontiguousarray(np.asarray(indices, dtype=np.int64))
+        n, S = len(idx), self.seq_len
+        out = [torch.empty((n, S), dtype=torch.int64) for _ in range(4)] + [torch.empty((n,), dtype=torch.int64)]
+        if n:
+            self._set.gather(idx, *[t.data_ptr() for t in out])
+        return out
+
+    def make_batch_stream(self, batches, num_threads=1, device=None):
+        if self._set is None:
+            return None
+        return NativeBatchStream(self, batches, num_threads=num_threads, device=device)
+
+
+class NativeBatchStream(object):
+    """Iterator over collated batches read by C++ threads into pinned slots."""
+
+    DEPTH = 4
+
+    def __init__(self, dataset, batches, num_threads=1, device=None):
+        self.dataset = dataset
+        self.batches = [np.ascontiguousarray(np.asarray(b, dtype=np.int64)) for b in batches]
+        self.device = torch.device(device) if device is not None else None
+        self.num_threads = num_threads
+        self._pf = None
+
+    def __len__(self):
+        return len(self.batches)
+
+    def _start(self):
+        S = self.dataset.seq_len
+        max_bsz = max([len(b) for b in self.batches] + [1])
+        pin = self.device is not None and self.device.type == "cuda"
+        depth = min(self.DEPTH, max(1, len(self.batches)))
+        self._slots = []
+        for _ in range(depth):
+            bufs = [torch.empty((max_bsz, S), dtype=torch.int64, pin_memory=pin) for _ in range(4)]
+            bufs.append(torch.empty((max_bsz,), dtype=torch.int64, pin_memory=pin))
+            self._slots.append(bufs)
+        ptrs = [[t.data_ptr() for t in s] for s in self._slots]
+        self._pf = _h5().Prefetcher(self.dataset._set, self.batches, ptrs, max_bsz, self.num_threads)
+        if pin:
+            self._copy_stream = torch.cuda.Stream(device=self.device)
+        self._inflight = []  # (slot, event)
+
+    def __iter__(self):
+        if self._pf is None:
+            self._start()
+        try:
+            while True:
+                slot, bsz = self._pf.next()
+                if slot < 0:
+                    return
+                if bsz == 0:
+                    self._pf.release(slot)
+                    yield None
+                    continue
+                yield self._deliver(slot, bsz)
+        finally:
+            self.close()
+
+    def _deliver(self, slot, bsz):
+        bufs = self._slots[slot]
+        if self.device is None or self.device.type != "cuda":
+            out = [bufs[k][:bsz].clone() for k in range(5)]
+            self._pf.release(slot)
+            return out
+        # retire slots whose copies have completed
+        keep = []
+        for s, ev in self._inflight:
+            if ev.query():
+                self._pf.release(s)
+            else:
+                keep.append((s, ev))
+        self._inflight = keep
+        compute = torch.cuda.current_stream(self.device)
+        with torch.cuda.stream(self._copy_stream):
+            out = [bufs[k][:bsz].to(self.device, non_blocking=True) for k in range(5)]
+            ev = torch.cuda.Event()
+            ev.record(self._copy_stream)
+        compute.wait_event(ev)
+        for t in out:
+            t.record_stream(compute)
+        self._inflight.append((slot, ev))
+        if len(self._inflight) >= len(self._slots):
+            s, e = self._inflight.pop(0)
+            e.synchronize()
+            self._pf.release(s)
+        return out
+
+    def close(self):
+        if self._pf is not None:
+            for s, ev in getattr(self, "_inflight", []):
+                ev.synchronize()
+            self._pf.stop()
+            self._pf = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

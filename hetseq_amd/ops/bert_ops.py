@@ -1,0 +1,433 @@
+"""Fused BERT operators (autograd Functions over the gfx950 kernels).
+
+Each Function owns a whole sub-graph of the reference model so the
+intermediate tensors, kernel fusion and gradient accumulation are under our
+control:
+
+* ``FusedEmbedding``   word+pos+type gather -> LN -> dropout   (bert_modeling.py:306-320)
+* ``FusedBertLayer``   QKV GEMM -> flash attention -> out-proj -> bias/dropout/residual/LN
+                       -> FFN1 -> bias+GELU -> FFN2 -> bias/dropout/residual/LN
+                       (bert_modeling.py:323-441), with in-Function activation
+                       recomputation for ``--checkpoint-activations``
+* ``FusedMLMLoss``     masked-row compaction -> transform(GEMM+GELU+LN) -> tied decoder
+                       GEMM on masked rows only -> fused cross-entropy
+                       (bert_modeling.py:519-549, 880-882)
+Standalone ops used by tests and other models: ``attention``, ``layer_norm``,
+``bias_dropout_residual_ln``, ``bias_gelu``.
+
+All shapes are checked on the host before any launch.  Gradients of
+parameters are produced in fp32 (master precision) in both --dtype modes.
+"""
+from __future__ import annotations
+
+import torch
+
+from hetseq_amd.ops import gemm as G
+from hetseq_amd.ops._C import dtype_code, hip, stream_handle
+from hetseq_amd.runtime import rng
+
+LN_WIDTHS = (256, 512, 768, 1024, 1536, 2048)
+
+
+def _err_flag(device):
+    """Device-side error word (bit0: embedding id out of range, bit1: MLM overflow)."""
+    key = ("err", device.index)
+    buf = _BUFS.get(key)
+    if buf is None:
+        buf = torch.zeros(1, dtype=torch.int32, device=device)
+        _BUFS[key] = buf
+    return buf
+
+
+_BUFS: dict = {}
+
+
+def check_device_errors(device=None):
+    for k, v in list(_BUFS.items()):
+        if k[0] == "err" and (device is None or v.device == device):
+            e = int(v.item())
+            if e & 1:
+                raise RuntimeError("embedding lookup got an id outside the vocabulary / type range")
+            if e & 2:
+                raise RuntimeError("masked-LM rows exceeded the configured capacity (max_predictions_per_seq)")
+
+
+def _colpart_buf(nparts, H, device, n=3):
+    return torch.empty((n, nparts, H), dtype=torch.float32, device=device)
+
+
+# --------------------------------------------------------------------- basic ops
+def ln_fwd(a, gamma, beta, eps=1e-12, bias=None, resid=None, p=0.0, mode=0, seed=0, off=0, save_z=True):
+    rows, H = a.shape
+    assert H in LN_WIDTHS and a.is_contiguous() and (resid is None or resid.shape == a.shape)
+    y = torch.empty_like(a)
+    z = torch.empty((rows, H), dtype=torch.float32, device=a.device) if save_z else None
+    mean = torch.empty(rows, dtype=torch.float32, device=a.device)
+    rstd = torch.empty_like(mean)
+    hip().ln_fwd(dtype_code(a), a.data_ptr(), bias.data_ptr() if bias is not None else 0,
+                 resid.data_ptr() if resid is not None else 0, gamma.data_ptr(), beta.data_ptr(), y.data_ptr(),
+                 z.data_ptr() if z is not None else 0, mean.data_ptr(), rstd.data_ptr(), rows, H, float(eps), float(p),
+                 seed, off, mode, stream_handle())
+    return y, z, mean, rstd
+
+
+def ln_bwd(dy, z, mean, rstd, gamma, p=0.0, mode=0, seed=0, off=0, want_dz=True, want_da=False, dz_out=None):
+    rows, H = dy.shape
+    nb = hip().ln_bwd_num_blocks()
+    part = _colpart_buf(nb, H, dy.device)
+    dz = (dz_out if dz_out is not None else torch.empty_like(dy)) if want_dz else None
+    da = torch.empty_like(dy) if want_da else None
+    hip().ln_bwd(dtype_code(dy), dy.data_ptr(), z.data_ptr(), mean.data_ptr(), rstd.data_ptr(), gamma.data_ptr(),
+                 dz.data_ptr() if dz is not None else 0, da.data_ptr() if da is not None else 0, part[0].data_ptr(),
+                 part[1].data_ptr(), part[2].data_ptr(), rows, H, float(p), seed, off, mode, stream_handle())
+    n = 3 if mode == 1 else 2
+    outs = torch.empty((n, H), dtype=torch.float32, device=dy.device)
+    hip().colpart_finalize([part[i].data_ptr() for i in range(n)], [outs[i].data_ptr() for i in range(n)], nb, H, 0,
+                           stream_handle())
+    dgamma, dbeta = outs[0], outs[1]
+    dbias = outs[2] if mode == 1 else None
+    return dz, da, dgamma, dbeta, dbias
+
+
+def bias_gelu_fwd(x, b):
+    y = torch.empty_like(x)
+    rows, N = x.shape
+    assert N % 4 == 0 and x.is_contiguous()
+    hip().bias_gelu_fwd(dtype_code(x), x.data_ptr(), b.data_ptr(), y.data_ptr(), rows, N, stream_handle())
+    return y
+
+
+def gelu_bwd_colsum(dy, x, b):
+    """dx = dy * gelu'(x+b) and db = sum_rows(dx)."""
+    rows, N = dy.shape
+    assert N % 4 == 0 and dy.is_contiguous() and x.is_contiguous()
+    chunks = hip().colsum_row_chunks(rows)
+    part = torch.empty((chunks, N), dtype=torch.float32, device=dy.device)
+    db = torch.empty(N, dtype=torch.float32, device=dy.device)
+    dx = torch.empty_like(dy)
+    hip().colsum(dtype_code(dy), dy.data_ptr(), x.data_ptr(), b.data_ptr(), dx.data_ptr(), part.data_ptr(),
+                 db.data_ptr(), rows, N, 0, stream_handle())
+    return dx, db
+
+
+def colsum(x):
+    rows, N = x.shape
+    assert x.is_contiguous()
+    chunks = hip().colsum_row_chunks(rows)
+    part = torch.empty((chunks, N), dtype=torch.float32, device=x.device)
+    out = torch.empty(N, dtype=torch.float32, device=x.device)
+    hip().colsum(dtype_code(x), x.data_ptr(), 0, 0, 0, part.data_ptr(), out.data_ptr(), rows, N, 0, stream_handle())
+    return out
+
+
+def attn_fwd(qkv, mask, B, S, NH, p, seed, off):
+    T, H3 = qkv.shape
+    H = H3 // 3
+    assert T == B * S and H == NH * 64 and S % 32 == 0 and qkv.is_contiguous()
+    assert mask.dtype == torch.int64 and mask.shape == (B, S) and mask.is_contiguous()
+    ctx = torch.empty((T, H), dtype=qkv.dtype, device=qkv.device)
+    lse = torch.empty((B * NH * S,), dtype=torch.float32, device=qkv.device)
+    hip().attn_fwd(dtype_code(qkv), qkv.data_ptr(), mask.data_ptr(), ctx.data_ptr(), lse.data_ptr(), B, S, NH, 64,
+                   float(p), seed, off, stream_handle())
+    return ctx, lse
+
+
+def attn_bwd(qkv, mask, ctx, dctx, lse, B, S, NH, p, seed, off):
+    assert dctx.is_contiguous() and dctx.shape == ctx.shape
+    dqkv = torch.empty_like(qkv)
+    dbuf = torch.empty_like(lse)
+    hip().attn_bwd(dtype_code(qkv), qkv.data_ptr(), mask.data_ptr(), ctx.data_ptr(), dctx.data_ptr(), lse.data_ptr(),
+                   dbuf.data_ptr(), dqkv.data_ptr(), B, S, NH, 64, float(p), seed, off, stream_handle())
+    return dqkv
+
+
+# --------------------------------------------------------------------- standalone autograd ops
+class _Attention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, mask, B, S, NH, p):
+        seed, off = rng.fork() if p > 0 else (0, 0)
+        out, lse = attn_fwd(qkv.contiguous(), mask, B, S, NH, p, seed, off)
+        ctx.save_for_backward(qkv, mask, out, lse)
+        ctx.cfg = (B, S, NH, p, seed, off)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, mask, out, lse = ctx.saved_tensors
+        B, S, NH, p, seed, off = ctx.cfg
+        return attn_bwd(qkv, mask, out, dout.contiguous(), lse, B, S, NH, p, seed, off), None, None, None, None, None
+
+
+def attention(qkv, mask, B, S, NH, p=0.0):
+    """Fused BERT attention: qkv [B*S, 3H] -> context [B*S, H]."""
+    return _Attention.apply(qkv, mask, B, S, NH, p)
+
+
+class _LayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, eps, bias, resid, p, mode):
+        seed, off = rng.fork() if p > 0 else (0, 0)
+        y, z, mean, rstd = ln_fwd(x.contiguous(), gamma, beta, eps, bias, resid, p, mode, seed, off)
+        ctx.save_for_backward(z, mean, rstd, gamma)
+        ctx.cfg = (p, mode, seed, off, bias is not None, resid is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        z, mean, rstd, gamma = ctx.saved_tensors
+        p, mode, seed, off, has_bias, has_res = ctx.cfg
+        dz, da, dg, db, dbias = ln_bwd(dy.contiguous(), z, mean, rstd, gamma, p, mode, seed, off, True, mode == 1)
+        dx = da if mode == 1 else dz
+        if mode == 0 and has_bias:
+            dbias = dx.float().sum(0)
+        return dx, dg, db, None, dbias if has_bias else None, dz if has_res else None, None, None
+
+
+def layer_norm(x, gamma, beta, eps=1e-12):
+    return _LayerNorm.apply(x, gamma, beta, eps, None, None, 0.0, 0)
+
+
+def bias_dropout_residual_ln(a, bias, resid, gamma, beta, p=0.0, eps=1e-12):
+    """LN(dropout(a + bias) + resid) (reference: BertSelfOutput / BertOutput)."""
+    return _LayerNorm.apply(a, gamma, beta, eps, bias, resid, p, 1)
+
+
+class _BiasGelu(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, b):
+        x = x.contiguous()
+        ctx.save_for_backward(x, b)
+        return bias_gelu_fwd(x, b)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, b = ctx.saved_tensors
+        dx, db = gelu_bwd_colsum(dy.contiguous(), x, b)
+        return dx, db
+
+
+def bias_gelu(x, b):
+    return _BiasGelu.apply(x, b)
+
+
+# --------------------------------------------------------------------- embeddings
+class FusedEmbedding(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, tt, wword, wpos, wtype, gamma, beta, p, eps, out_dtype):
+        B, S = ids.shape
+        V, H = wword.shape
+        TV = wtype.shape[0]
+        assert H in LN_WIDTHS and S <= wpos.shape[0] and ids.dtype == torch.int64
+        ids = ids.contiguous()
+        tt = tt.contiguous() if tt is not None else None
+        rows = B * S
+        y = torch.empty((rows, H), dtype=out_dtype, device=ids.device)
+        z = torch.empty((rows, H), dtype=torch.float32, device=ids.device)
+        mean = torch.empty(rows, dtype=torch.float32, device=ids.device)
+        rstd = torch.empty_like(mean)
+        seed, off = rng.fork() if p > 0 else (0, 0)
+        err = _err_flag(ids.device)
+        hip().emb_fwd(dtype_code(y), ids.data_ptr(), tt.data_ptr() if tt is not None else 0, wword.data_ptr(),
+                      wpos.data_ptr(), wtype.data_ptr(), gamma.data_ptr(), beta.data_ptr(), y.data_ptr(), z.data_ptr(),
+                      mean.data_ptr(), rstd.data_ptr(), rows, S, H, V, TV, float(eps), float(p), seed, off,
+                      err.data_ptr(), stream_handle())
+        ctx.save_for_backward(ids, tt if tt is not None else ids.new_zeros(0), z, mean, rstd, gamma)
+        ctx.cfg = (B, S, V, H, TV, wpos.shape[0], p, seed, off, tt is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        ids, tt, z, mean, rstd, gamma = ctx.saved_tensors
+        B, S, V, H, TV, P, p, seed, off, has_tt = ctx.cfg
+        dy = dy.contiguous()
+        dev = dy.device
+        dword = torch.zeros((V, H), dtype=torch.float32, device=dev)
+        dpos = torch.zeros((P, H), dtype=torch.float32, device=dev)
+        dtype_ = torch.zeros((TV, H), dtype=torch.float32, device=dev)
+        nb = hip().ln_bwd_num_blocks()
+        part = _colpart_buf(nb, H, dev, 2)
+        hip().emb_bwd(dtype_code(dy), dy.data_ptr(), ids.data_ptr(), tt.data_ptr() if has_tt else 0, z.data_ptr(),
+                      mean.data_ptr(), rstd.data_ptr(), gamma.data_ptr(), dword.data_ptr(), dpos.data_ptr(),
+                      dtype_.data_ptr(), part[0].data_ptr(), part[1].data_ptr(), B * S, S, H, V, TV, float(p), seed,
+                      off, stream_handle())
+        outs = torch.empty((2, H), dtype=torch.float32, device=dev)
+        hip().colpart_finalize([part[0].data_ptr(), part[1].data_ptr()], [outs[0].data_ptr(), outs[1].data_ptr()], nb,
+                               H, 0, stream_handle())
+        return None, None, dword, dpos, dtype_, outs[0], outs[1], None, None, None
+
+
+# --------------------------------------------------------------------- encoder layer
+class LayerWeights(object):
+    """Compute views of one encoder layer's weights (fp32 master or bf16 shadow)."""
+
+    __slots__ = ("wqkv", "bqkv", "wo", "bo", "g1", "b1", "w1", "bi", "w2", "b2", "g2", "bb2")
+
+
+def _layer_forward(x, mask, W, cfg, save):
+    B, S, NH, p_h, p_a, eps, seeds = cfg
+    (s_a, o_a), (s_1, o_1), (s_2, o_2) = seeds
+    qkv = G.linear_fwd(x, W.wqkv, W.bqkv.to(x.dtype) if x.dtype != torch.float32 else W.bqkv)
+    ctx_, lse = attn_fwd(qkv, mask, B, S, NH, p_a, s_a, o_a)
+    a = G.linear_fwd(ctx_, W.wo)
+    h1, z1, m1, r1 = ln_fwd(a, W.g1, W.b1, eps, bias=W.bo, resid=x, p=p_h, mode=1, seed=s_1, off=o_1)
+    f1pre = G.linear_fwd(h1, W.w1)
+    f1 = bias_gelu_fwd(f1pre, W.bi)
+    o = G.linear_fwd(f1, W.w2)
+    h2, z2, m2, r2 = ln_fwd(o, W.g2, W.bb2, eps, bias=W.b2, resid=h1, p=p_h, mode=1, seed=s_2, off=o_2)
+    if save:
+        return h2, (qkv, ctx_, lse, z1, m1, r1, h1, f1pre, f1, z2, m2, r2)
+    return h2, None
+
+
+class FusedBertLayer(torch.autograd.Function):
+    """One post-LN BERT encoder layer.  Inputs after ``x, mask, meta`` are the
+    16 parameters in reference order (q.w, q.b, k.w, k.b, v.w, v.b, o.w, o.b,
+    ln1.w, ln1.b, i.w, i.b, out.w, out.b, ln2.w, ln2.b)."""
+
+    @staticmethod
+    def forward(ctx, x, mask, meta, *params):
+        W, cfg, recompute = meta["weights"](), meta["cfg"], meta["recompute"]
+        h2, saved = _layer_forward(x, mask, W, cfg, save=not recompute)
+        ctx.meta = meta
+        ctx.cfg = cfg
+        if recompute:
+            ctx.save_for_backward(x, mask)
+        else:
+            ctx.save_for_backward(x, mask, *saved)
+        return h2
+
+    @staticmethod
+    def backward(ctx, dh2):
+        meta, cfg = ctx.meta, ctx.cfg
+        W = meta["weights"]()
+        if meta["recompute"]:
+            x, mask = ctx.saved_tensors
+            with torch.no_grad():
+                _, saved = _layer_forward(x, mask, W, cfg, save=True)
+        else:
+            x, mask = ctx.saved_tensors[:2]
+            saved = ctx.saved_tensors[2:]
+        qkv, ctx_, lse, z1, m1, r1, h1, f1pre, f1, z2, m2, r2 = saved
+        B, S, NH, p_h, p_a, eps, seeds = cfg
+        (s_a, o_a), (s_1, o_1), (s_2, o_2) = seeds
+        dh2 = dh2.contiguous()
+        # LN2 (bias-dropout-residual) backward
+        dz2, do_, dg2, dbb2, db2 = ln_bwd(dh2, z2, m2, r2, W.g2, p_h, 1, s_2, o_2, True, True)
+        dW2 = G.linear_wgrad(do_, f1)
+        df1 = G.linear_dgrad(do_, W.w2)
+        df1pre, dbi = gelu_bwd_colsum(df1, f1pre, W.bi)
+        dW1 = G.linear_wgrad(df1pre, h1)
+        dh1 = G.linear_dgrad(df1pre, W.w1, out=dz2, accumulate=True)  # dz2 + df1pre @ W1
+        dz1, da1, dg1, db1, dbo = ln_bwd(dh1, z1, m1, r1, W.g1, p_h, 1, s_1, o_1, True, True)
+        dWo = G.linear_wgrad(da1, ctx_)
+        dctx = G.linear_dgrad(da1, W.wo)
+        dqkv = attn_bwd(qkv, mask, ctx_, dctx, lse, B, S, NH, p_a, s_a, o_a)
+        dWqkv = G.linear_wgrad(dqkv, x)
+        dbqkv = colsum(dqkv)
+        dx = G.linear_dgrad(dqkv, W.wqkv, out=dz1, accumulate=True)  # dz1 + dqkv @ Wqkv
+        H = x.shape[1]
+        return (dx, None, None,
+                dWqkv[:H], dbqkv[:H], dWqkv[H:2 * H], dbqkv[H:2 * H], dWqkv[2 * H:], dbqkv[2 * H:],
+                dWo, dbo, dg1, db1, dW1, dbi, dW2, db2, dg2, dbb2)
+
+
+# --------------------------------------------------------------------- MLM head + loss
+def mlm_compact(labels_flat, cap, ignore_index=-1):
+    rows = labels_flat.numel()
+    dev = labels_flat.device
+    idx = torch.empty(cap, dtype=torch.int32, device=dev)
+    lab = torch.empty(cap, dtype=torch.int64, device=dev)
+    cnt = torch.empty(1, dtype=torch.int32, device=dev)
+    hip().mlm_compact(labels_flat.data_ptr(), rows, ignore_index, cap, idx.data_ptr(), lab.data_ptr(), cnt.data_ptr(),
+                      _err_flag(dev).data_ptr(), stream_handle())
+    return idx, lab, cnt
+
+
+def gather_rows(src, idx):
+    n = idx.numel()
+    H = src.shape[1]
+    out = torch.empty((n, H), dtype=src.dtype, device=src.device)
+    hip().gather_rows(dtype_code(src), src.data_ptr(), idx.data_ptr(), out.data_ptr(), n, H, stream_handle())
+    return out
+
+
+def xent_fwd(logits, labels, ignore_index=-1):
+    rows, V = logits.shape
+    dev = logits.device
+    row_loss = torch.empty(rows, dtype=torch.float32, device=dev)
+    lse = torch.empty(rows, dtype=torch.float32, device=dev)
+    out = torch.empty(2, dtype=torch.float32, device=dev)
+    hip().xent_fwd(dtype_code(logits), logits.data_ptr(), labels.data_ptr(), rows, V, logits.stride(0), ignore_index,
+                   row_loss.data_ptr(), lse.data_ptr(), out.data_ptr(), stream_handle())
+    return out, lse
+
+
+def xent_bwd_(logits, labels, lse, dloss, stats, ignore_index=-1):
+    rows, V = logits.shape
+    hip().xent_bwd(dtype_code(logits), logits.data_ptr(), labels.data_ptr(), lse.data_ptr(), rows, V,
+                   logits.stride(0), ignore_index, dloss.data_ptr(), stats.data_ptr(), stream_handle())
+    return logits
+
+
+class FusedCrossEntropy(torch.autograd.Function):
+    """mean CE over rows whose label != ignore_index (reference CrossEntropyLoss(ignore_index=-1))."""
+
+    @staticmethod
+    def forward(ctx, logits, labels, ignore_index):
+        logits = logits.contiguous()
+        out, lse = xent_fwd(logits, labels, ignore_index)
+        ctx.save_for_backward(logits, labels, lse, out)
+        ctx.ignore = ignore_index
+        return out[0]
+
+    @staticmethod
+    def backward(ctx, dloss):
+        logits, labels, lse, out = ctx.saved_tensors
+        d = logits.clone()
+        xent_bwd_(d, labels, lse, dloss.reshape(1).float().contiguous(), out, ctx.ignore)
+        return d, None, None
+
+
+def cross_entropy(logits, labels, ignore_index=-1):
+    return FusedCrossEntropy.apply(logits, labels, ignore_index)
+
+
+class FusedMLMLoss(torch.autograd.Function):
+    """Sparse masked-LM head + loss.  Exact w.r.t. the dense reference: rows with
+    label -1 contribute neither loss nor gradient, so only the (at most ``cap``)
+    labelled rows go through the transform, the tied decoder GEMM and the CE."""
+
+    @staticmethod
+    def forward(ctx, seq, labels, meta, wt, bt, g, b, wdec, bdec):
+        T, H = seq.shape
+        cap, eps = meta["cap"], meta["eps"]
+        Wt, Wd = meta["weights"]()
+        idx, lab, cnt = mlm_compact(labels.reshape(-1), cap)
+        hsel = gather_rows(seq, idx)
+        t1pre = G.linear_fwd(hsel, Wt)
+        t1 = bias_gelu_fwd(t1pre, bt)
+        t2, z, mean, rstd = ln_fwd(t1, g, b, eps)
+        logits = G.gemm(t2, Wd, ta=False, tb=True, bias=bdec, epi=1, out_dtype=torch.float32) \
+            if t2.dtype == torch.float32 else G.gemm(t2, Wd, tb=True, bias=bdec, epi=1, out_dtype=torch.float32)
+        out, lse = xent_fwd(logits, lab)
+        ctx.save_for_backward(idx, lab, hsel, t1pre, t1, z, mean, rstd, t2, logits, lse, out, g, bt)
+        ctx.meta = meta
+        ctx.T = T
+        return out[0]
+
+    @staticmethod
+    def backward(ctx, dloss):
+        idx, lab, hsel, t1pre, t1, z, mean, rstd, t2, logits, lse, out, g, bt = ctx.saved_tensors
+        Wt, Wd = ctx.meta["weights"]()
+        dlogits = xent_bwd_(logits, lab, lse, dloss.reshape(1).float().contiguous(), out)  # in place, fp32
+        dWdec = G.linear_wgrad(dlogits, t2.float() if t2.dtype != torch.float32 else t2)
+        dbdec = colsum(dlogits)
+        dt2 = G.gemm(dlogits.to(t2.dtype) if t2.dtype != torch.float32 else dlogits, Wd)
+        dt1, _, dg, db, _ = ln_bwd(dt2, z, mean, rstd, g, 0.0, 0)
+        dt1pre, dbt = gelu_bwd_colsum(dt1, t1pre, bt)
+        dWt = G.linear_wgrad(dt1pre, hsel)
+        dhsel = G.linear_dgrad(dt1pre, Wt)
+        dseq = torch.zeros((ctx.T, hsel.shape[1]), dtype=hsel.dtype, device=hsel.device)
+        hip().scatter_add_rows(dtype_code(dseq), dhsel.data_ptr(), idx.data_ptr(), dseq.data_ptr(), idx.numel(),
+                               hsel.shape[1], stream_handle())
+        return dseq, None, None, dWt, dbt, dg, db, dWdec, dbdec

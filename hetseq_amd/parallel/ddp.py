@@ -1,0 +1,189 @@
+"""Flat-bucket data-parallel engine.
+
+Replaces ``torch.nn.parallel.DistributedDataParallel`` (reference:
+controller.py:74-89) with an engine built on the flat gradient buffer
+(hetseq_amd/runtime/flat.py):
+
+* buckets are CONTIGUOUS slices of ``store.grad`` formed in reverse
+  parameter order (the order gradients become ready in backward) up to
+  ``--bucket-cap-mb`` -- the all-reduce runs in place on the slice, no
+  gather/scatter copies;
+* each parameter's post-accumulate-grad hook counts down its bucket; ready
+  buckets are launched strictly in bucket order (same collective order on
+  every rank) as async ``all_reduce`` on the process group -- RCCL runs them on
+  its own stream, overlapping with the rest of backward; a callback queued on
+  the autograd engine waits for them at the end of backward (stream-level
+  wait, no host sync on GPU);
+* gradients are SUMMED, not averaged: the controller's grad-scale factor
+  (reference: W / sample_size after DDP's 1/W) is folded into the fused
+  optimizer as 1 / sample_size, saving a full pass over the gradients;
+* ``no_sync()`` skips communication for the first update_freq-1 micro
+  batches (reference: controller.py:245-258);
+* the constructor broadcasts rank 0's parameters (one collective on the flat
+  buffer, X3).
+
+Bucket sizing for MI355X: with 7 xGMI links per GPU a ring all-reduce is
+per-link bound; the default 25 MB (reference default) yields one bucket per
+BERT layer (7.1 M params = 28 MB) so communication of layer i overlaps the
+backward of layer i-1.
+"""
+from __future__ import annotations
+
+import contextlib
+
+import torch
+import torch.distributed as dist
+
+from hetseq_amd.runtime import profiling
+
+
+class FlatDDP(torch.nn.Module):
+    def __init__(self, module, store, process_group=None, bucket_cap_mb=25, find_unused_parameters=False,
+                 broadcast=True):
+        super().__init__()
+        self.module = module
+        self.store = store
+        self.process_group = process_group or dist.group.WORLD
+        self.world_size = dist.get_world_size(self.process_group)
+        self.find_unused_parameters = find_unused_parameters
+        self.require_sync = True
+        cap = max(1, int(bucket_cap_mb * 1024 * 1024 / 4))
+        params = list(store.params)
+        order = sorted(params, key=lambda p: store.offset(p), reverse=True)
+        self.buckets = []  # (lo, hi, [params])
+        cur, size = [], 0
+        for p in order:
+            cur.append(p)
+            size += p.numel()
+            if size >= cap:
+                self.buckets.append(cur)
+                cur, size = [], 0
+        if cur:
+            self.buckets.append(cur)
+        self.ranges = []
+        self.bucket_of = {}
+        for bi, ps in enumerate(self.buckets):
+            lo = min(store.offset(p) for p in ps)
+            hi = max(store.offset(p) + p.numel() for p in ps)
+            self.ranges.append((lo, hi))
+            for p in ps:
+                self.bucket_of[id(p)] = bi
+        # extend ranges to cover alignment gaps so the buckets tile the buffer
+        self._reset_state()
+        self._hooks = [p.register_post_accumulate_grad_hook(self._grad_ready) for p in params]
+        if broadcast and self.world_size > 1:
+            with torch.no_grad():
+                dist.broadcast(store.param, src=0, group=self.process_group)
+            store.sync_shadow()
+
+    def _reset_state(self):
+        self.pending = [len(ps) for ps in self.buckets]
+        self.ready = [False] * len(self.buckets)
+        self.next_launch = 0
+        self.works = []
+        self.callback_queued = False
+
+    # ------------------------------------------------------------- forward
+    def forward(self, *inputs, **kwargs):
+        if self.require_sync:
+            self._reset_state()
+        return self.module(*inputs, **kwargs)
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        old = self.require_sync
+        self.require_sync = False
+        try:
+            yield
+        finally:
+            self.require_sync = old
+
+    # ------------------------------------------------------------- hooks
+    def _grad_ready(self, p):
+        if not self.require_sync:
+            return
+        if not self.callback_queued:
+            self.callback_queued = True
+            torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
+        b = self.bucket_of[id(p)]
+        self.pending[b] -= 1
+        if self.pending[b] == 0:
+            self.ready[b] = True
+            self._launch_ready()
+
+    def _launch_ready(self):
+        while self.next_launch < len(self.buckets) and self.ready[self.next_launch]:
+            self._launch(self.next_launch)
+            self.next_launch += 1
+
+    def _launch(self, b):
+        lo, hi = self.ranges[b]
+        profiling.range_push("allreduce_bucket%d" % b)
+        work = dist.all_reduce(self.store.grad[lo:hi], group=self.process_group, async_op=True)
+        profiling.range_pop()
+        self.works.append(work)
+
+    def _finalize(self):
+        if self.next_launch < len(self.buckets):
+            missing = [i for i in range(len(self.buckets)) if not self.ready[i]]
+            if missing and not self.find_unused_parameters:
+                raise RuntimeError(
+                    "Expected to have finished reduction in the prior iteration; buckets {} never became ready. "
+                    "Pass --find-unused-parameters if some parameters legitimately receive no gradient.".format(
+                        missing))
+            for i in missing:
+                self.ready[i] = True
+            self._launch_ready()
+        for w in self.works:
+            w.wait()
+        self.works = []
+
+    def parameters(self, recurse=True):
+        return self.module.parameters(recurse)
+
+    def named_parameters(self, *a, **k):
+        return self.module.named_parameters(*a, **k)
+
+    def state_dict(self, *a, **k):
+        return self.module.state_dict(*a, **k)
+
+    def load_state_dict(self, *a, **k):
+        return self.module.load_state_dict(*a, **k)
+
+
+class BMUF(object):
+    """Blockwise Model-Update Filtering (Chen & Huo 2016) for ``--use-bmuf``.
+
+    Each rank runs its own optimizer; every ``sync_interval`` updates the
+    flat parameters are averaged (one all-reduce) and a block-momentum
+    filtered global step is applied.  The reference only exposes the flag
+    and silently trains ranks independently (Q08).
+    """
+
+    def __init__(self, store, process_group=None, block_momentum=0.875, block_lr=1.0, sync_interval=1):
+        self.store = store
+        self.group = process_group or dist.group.WORLD
+        self.world_size = dist.get_world_size(self.group)
+        self.bm = block_momentum
+        self.blr = block_lr
+        self.interval = max(1, sync_interval)
+        with torch.no_grad():
+            dist.broadcast(store.param, src=0, group=self.group)
+        self.global_params = store.param.detach().clone()
+        self.smoothed = torch.zeros_like(self.global_params)
+        self.count = 0
+
+    @torch.no_grad()
+    def after_step(self):
+        self.count += 1
+        if self.count % self.interval:
+            return
+        p = self.store.param
+        dist.all_reduce(p, group=self.group)
+        p.div_(self.world_size)
+        delta = self.global_params - p
+        self.smoothed.mul_(self.bm).add_(delta, alpha=self.blr)
+        self.global_params.sub_(self.smoothed)
+        # Nesterov-style look-ahead for the next block
+        p.copy_(self.global_params).sub_(self.smoothed, alpha=self.bm)
+        self.store.sync_shadow()

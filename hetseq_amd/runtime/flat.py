@@ -1,0 +1,139 @@
+"""Flat parameter / gradient storage.
+
+Every trainable parameter of a model is re-homed into ONE contiguous fp32
+buffer (``store.param``) and its ``.grad`` into one contiguous fp32 buffer
+(``store.grad``); ``p.data`` and ``p.grad`` become views.  This is the
+memory layout everything else is designed around:
+
+* the optimizer is one vectorised kernel over the whole buffer (no per-tensor
+  Python loop, reference optim.py:172-229);
+* the gradient-norm / clip is one reduction over one buffer;
+* data-parallel buckets are contiguous slices of ``store.grad`` -- all-reduce
+  runs in place, zero-copy (hetseq_amd/parallel/ddp.py);
+* zero_grad is one memset;
+* an optional bf16 ``shadow`` buffer (same offsets) holds the compute copy
+  of the weights for ``--dtype bf16``; the optimizer kernel refreshes it.
+
+Modules may declare contiguity groups (``_flat_groups``: lists of parameters
+that must be adjacent, e.g. the Q/K/V projection weights) so a fused kernel
+can address them as one tensor (``store.combined``).  Group starts and
+standalone tensors are aligned to 64 elements (256 B).
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+
+import torch
+
+ALIGN = 64
+
+
+def _align(n, a=ALIGN):
+    return (n + a - 1) // a * a
+
+
+class FlatParamStore(object):
+    def __init__(self, module, device=None, shadow_dtype=None):
+        named = OrderedDict()
+        seen = set()
+        for name, p in module.named_parameters():
+            if id(p) in seen or not p.requires_grad:
+                continue
+            seen.add(id(p))
+            named[name] = p
+        groups = {}
+        for m in module.modules():
+            for g in getattr(m, "_flat_groups", ()):
+                for p in g:
+                    groups[id(p)] = g
+        order, placed = [], set()
+        for name, p in named.items():
+            if id(p) in placed:
+                continue
+            g = groups.get(id(p))
+            members = list(g) if g is not None else [p]
+            order.append(members)
+            placed.update(id(q) for q in members)
+        dev = torch.device(device) if device is not None else next(iter(named.values())).device
+        offsets, cur = OrderedDict(), 0
+        for members in order:
+            cur = _align(cur)
+            for q in members:
+                offsets[id(q)] = cur
+                cur += q.numel()
+        total = _align(cur)
+        self.numel = total
+        self.device = dev
+        self.param = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.params = []
+        self.names = []
+        self.offsets = offsets
+        name_of = {id(p): n for n, p in named.items()}
+        with torch.no_grad():
+            for members in order:
+                for q in members:
+                    off, n = offsets[id(q)], q.numel()
+                    self.param[off : off + n].copy_(q.detach().reshape(-1).to(dev, torch.float32))
+                    q.data = self.param[off : off + n].view(q.shape)
+                    q.grad = self.grad[off : off + n].view(q.shape)
+                    self.params.append(q)
+                    self.names.append(name_of[id(q)])
+        self.shadow = None
+        if shadow_dtype is not None:
+            self.shadow = torch.empty(total, dtype=shadow_dtype, device=dev)
+            self.sync_shadow()
+
+    # ------------------------------------------------------------ views
+    def offset(self, p):
+        return self.offsets[id(p)]
+
+    def shadow_view(self, p):
+        if self.shadow is None:
+            return p.detach()
+        off = self.offsets[id(p)]
+        return self.shadow[off : off + p.numel()].view(p.shape)
+
+    def combined(self, params, shape, shadow=False):
+        """A single view over adjacent parameters (None if not adjacent)."""
+        off = self.offsets.get(id(params[0]))
+        if off is None:
+            return None
+        cur = off
+        for p in params:
+            if self.offsets.get(id(p)) != cur:
+                return None
+            cur += p.numel()
+        buf = self.shadow if (shadow and self.shadow is not None) else self.param
+        return buf[off:cur].view(shape)
+
+    def grad_slice(self, p):
+        off = self.offsets[id(p)]
+        return self.grad[off : off + p.numel()]
+
+    # ------------------------------------------------------------ ops
+    def zero_grad(self):
+        self.grad.zero_()
+        # re-attach views in case something replaced p.grad
+        for p in self.params:
+            if p.grad is None or p.grad.data_ptr() != self.grad.data_ptr() + 4 * self.offsets[id(p)]:
+                off = self.offsets[id(p)]
+                p.grad = self.grad[off : off + p.numel()].view(p.shape)
+
+    def sync_shadow(self):
+        if self.shadow is None:
+            return
+        with torch.no_grad():
+            if self.param.is_cuda and self.shadow.dtype == torch.bfloat16:
+                from hetseq_amd.ops._C import hip, stream_handle
+
+                hip().cast_f32_bf16(self.param.data_ptr(), self.shadow.data_ptr(), self.numel, stream_handle())
+            else:
+                self.shadow.copy_(self.param)
+
+    def checksum(self):
+        return self.param.double().sum()
+
+    def segments(self):
+        """[(offset, numel)] per parameter, in buffer order."""
+        return [(self.offsets[id(p)], p.numel()) for p in self.params]

@@ -1,0 +1,347 @@
+"""Numerics of every gfx950 HIP kernel against a plain PyTorch fp32 oracle."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref_ln(x, g, b, eps=1e-12):
+    u = x.mean(-1, keepdim=True)
+    s = (x - u).pow(2).mean(-1, keepdim=True)
+    return g * (x - u) / torch.sqrt(s + eps) + b
+
+
+def _close(a, b, rtol=1e-4, atol=1e-5, msg=""):
+    a, b = a.float(), b.float()
+    err = (a - b).abs().max().item()
+    tol = atol + rtol * b.abs().max().item()
+    assert err <= tol, "%s max err %.3e > %.3e" % (msg, err, tol)
+
+
+@pytest.mark.parametrize("H", [256, 768, 1024])
+def test_layernorm_fwd_bwd(cuda, H):
+    from hetseq_amd.ops.bert_ops import layer_norm
+
+    torch.manual_seed(0)
+    x = torch.randn(300, H, device=cuda, requires_grad=True)
+    g = torch.randn(H, device=cuda, requires_grad=True)
+    b = torch.randn(H, device=cuda, requires_grad=True)
+    y = layer_norm(x, g, b)
+    x2, g2, b2 = (t.detach().clone().requires_grad_() for t in (x, g, b))
+    y2 = _ref_ln(x2, g2, b2)
+    _close(y, y2, msg="ln fwd")
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    y2.backward(dy)
+    _close(x.grad, x2.grad, 1e-4, 1e-4, "ln dx")
+    _close(g.grad, g2.grad, 1e-4, 1e-3, "ln dgamma")
+    _close(b.grad, b2.grad, 1e-4, 1e-3, "ln dbeta")
+
+
+def test_bias_dropout_residual_ln_nodrop(cuda):
+    from hetseq_amd.ops.bert_ops import bias_dropout_residual_ln
+
+    torch.manual_seed(1)
+    T, H = 512, 768
+    a = torch.randn(T, H, device=cuda, requires_grad=True)
+    bias = torch.randn(H, device=cuda, requires_grad=True)
+    r = torch.randn(T, H, device=cuda, requires_grad=True)
+    g = torch.rand(H, device=cuda, requires_grad=True)
+    be = torch.randn(H, device=cuda, requires_grad=True)
+    y = bias_dropout_residual_ln(a, bias, r, g, be, p=0.0)
+    leaves = [t.detach().clone().requires_grad_() for t in (a, bias, r, g, be)]
+    y2 = _ref_ln(leaves[0] + leaves[1] + leaves[2], leaves[3], leaves[4])
+    _close(y, y2, msg="bdrln fwd")
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    y2.backward(dy)
+    for t1, t2, n in zip((a, bias, r, g, be), leaves, "a bias r g b".split()):
+        _close(t1.grad, t2.grad, 1e-4, 1e-3, "bdrln d" + n)
+
+
+def test_bias_dropout_residual_ln_dropout_consistent(cuda):
+    """With dropout, the backward must use exactly the forward's mask."""
+    from hetseq_amd.ops.bert_ops import bias_dropout_residual_ln
+    from hetseq_amd.runtime import rng
+
+    torch.manual_seed(2)
+    T, H, p = 256, 768, 0.1
+    a = torch.randn(T, H, device=cuda, requires_grad=True)
+    bias = torch.zeros(H, device=cuda)
+    r = torch.zeros(T, H, device=cuda)
+    g = torch.ones(H, device=cuda)
+    be = torch.zeros(H, device=cuda)
+    rng.set_seed(1234)
+    y = bias_dropout_residual_ln(a, bias, r, g, be, p=p)
+    # recover the mask through the gradient of sum(y * w) with LN folded out: use identity check instead
+    rng.set_seed(1234)
+    y_again = bias_dropout_residual_ln(a.detach(), bias, r, g, be, p=p)
+    assert torch.equal(y.detach(), y_again), "Philox mask not reproducible for a fixed (seed, offset)"
+    # kept fraction ~ 1-p: a zero row element of dropout output shows up as pre-LN zero; check via z
+    from hetseq_amd.ops import bert_ops
+
+    rng.set_seed(99)
+    _, z, _, _ = bert_ops.ln_fwd(torch.ones(T, H, device=cuda), g, be, bias=bias, resid=r, p=p, mode=1,
+                                 seed=99, off=0)
+    kept = (z != 0).float().mean().item()
+    assert abs(kept - (1 - p)) < 0.01, kept
+    assert torch.allclose(z[z != 0], torch.full_like(z[z != 0], 1 / (1 - p)))
+    # gradient check against an explicit-mask reference at the same (seed=99, off=0) site
+    mask = (z != 0).float() / (1 - p)
+    a2 = a.detach().clone().requires_grad_()
+    y2 = _ref_ln(a2 * mask, g, be)
+    y_f, z_f, m_f, rs_f = bert_ops.ln_fwd(a2.detach(), g, be, bias=bias, resid=r, p=p, mode=1, seed=99, off=0)
+    _close(y_f, y2.detach(), msg="masked fwd")
+    dy = torch.randn_like(y_f)
+    y2.backward(dy)
+    dz, da, dg, db, dbias = bert_ops.ln_bwd(dy, z_f, m_f, rs_f, g, p, 1, 99, 0, True, True)
+    _close(da, a2.grad, 1e-4, 1e-4, "dropout-masked grad")
+
+
+def test_bias_gelu(cuda):
+    from hetseq_amd.models.bert import bias_gelu as ref
+    from hetseq_amd.ops.bert_ops import bias_gelu
+
+    torch.manual_seed(3)
+    x = torch.randn(1000, 3072, device=cuda, requires_grad=True)
+    b = torch.randn(3072, device=cuda, requires_grad=True)
+    y = bias_gelu(x, b)
+    x2, b2 = x.detach().clone().requires_grad_(), b.detach().clone().requires_grad_()
+    y2 = ref(b2, x2)
+    _close(y, y2, 1e-5, 1e-5, "gelu fwd")
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    y2.backward(dy)
+    _close(x.grad, x2.grad, 1e-4, 1e-5, "gelu dx")
+    _close(b.grad, b2.grad, 1e-4, 1e-3, "gelu db")
+
+
+def _ref_attention(qkv, mask, B, S, NH):
+    H = qkv.shape[1] // 3
+    q, k, v = qkv.view(B, S, 3, NH, 64).permute(2, 0, 3, 1, 4)
+    scores = torch.matmul(q, k.transpose(-1, -2)) / 8.0
+    scores = scores + ((1.0 - mask.float()) * -10000.0)[:, None, None, :]
+    p = torch.softmax(scores, -1)
+    return torch.matmul(p, v).permute(0, 2, 1, 3).reshape(B * S, H)
+
+
+@pytest.mark.parametrize("B,S,NH", [(2, 128, 12), (3, 64, 4), (1, 512, 2), (2, 96, 2)])
+def test_attention_fwd_bwd(cuda, B, S, NH):
+    from hetseq_amd.ops.bert_ops import attention
+
+    torch.manual_seed(4)
+    H = NH * 64
+    qkv = torch.randn(B * S, 3 * H, device=cuda, requires_grad=True)
+    mask = torch.ones(B, S, dtype=torch.int64, device=cuda)
+    mask[0, S - 17:] = 0
+    if B > 1:
+        mask[1, 5:9] = 0
+    out = attention(qkv, mask, B, S, NH, 0.0)
+    qkv2 = qkv.detach().clone().requires_grad_()
+    out2 = _ref_attention(qkv2, mask, B, S, NH)
+    _close(out, out2, 1e-4, 1e-5, "attn fwd")
+    dout = torch.randn_like(out)
+    out.backward(dout)
+    out2.backward(dout)
+    _close(qkv.grad, qkv2.grad, 1e-4, 1e-5, "attn dqkv")
+
+
+def test_attention_fully_masked_row(cuda):
+    """-10000 additive mask (not -inf): a fully masked sequence still attends (Q27)."""
+    from hetseq_amd.ops.bert_ops import attention
+
+    torch.manual_seed(5)
+    B, S, NH = 1, 64, 2
+    qkv = torch.randn(B * S, 3 * NH * 64, device=cuda)
+    mask = torch.zeros(B, S, dtype=torch.int64, device=cuda)
+    out = attention(qkv, mask, B, S, NH, 0.0)
+    _close(out, _ref_attention(qkv, mask, B, S, NH), 1e-4, 1e-5, "masked fwd")
+    assert torch.isfinite(out).all()
+
+
+def test_attention_dropout(cuda):
+    """Dropout: deterministic for a fixed seed, unbiased, and backward consistent with forward."""
+    from hetseq_amd.ops import bert_ops
+
+    torch.manual_seed(6)
+    B, S, NH, p = 2, 128, 4, 0.1
+    H = NH * 64
+    qkv = torch.randn(B * S, 3 * H, device=cuda)
+    mask = torch.ones(B, S, dtype=torch.int64, device=cuda)
+    o1, l1 = bert_ops.attn_fwd(qkv, mask, B, S, NH, p, 7, 0)
+    o2, l2 = bert_ops.attn_fwd(qkv, mask, B, S, NH, p, 7, 0)
+    assert torch.equal(o1, o2)
+    o3, _ = bert_ops.attn_fwd(qkv, mask, B, S, NH, p, 8, 0)
+    assert not torch.equal(o1, o3)
+    # expectation over many seeds approaches the no-dropout output
+    acc = torch.zeros_like(o1)
+    n = 64
+    for s in range(n):
+        acc += bert_ops.attn_fwd(qkv, mask, B, S, NH, p, 1000 + s, 0)[0]
+    ref, _ = bert_ops.attn_fwd(qkv, mask, B, S, NH, 0.0, 0, 0)
+    assert (acc / n - ref).abs().mean().item() < 0.05 * ref.abs().mean().item() + 1e-3
+    # gradient consistency: finite-difference of sum(out * w) along a random direction
+    qkv64 = qkv.double()
+    w = torch.randn_like(o1)
+    dqkv = bert_ops.attn_bwd(qkv, mask, o1, w, l1, B, S, NH, p, 7, 0)
+    d = torch.randn_like(qkv) * 1e-2
+    fp = (bert_ops.attn_fwd(qkv + d, mask, B, S, NH, p, 7, 0)[0] * w).sum().item()
+    fm = (bert_ops.attn_fwd(qkv - d, mask, B, S, NH, p, 7, 0)[0] * w).sum().item()
+    fd = (fp - fm) / 2
+    an = (dqkv * d).sum().item()
+    assert abs(fd - an) <= 2e-2 * abs(an) + 1e-3, (fd, an)
+
+
+def test_embedding_fwd_bwd(cuda):
+    from hetseq_amd.ops.bert_ops import FusedEmbedding
+
+    torch.manual_seed(7)
+    B, S, V, H, P, TV = 4, 128, 1000, 768, 512, 2
+    ids = torch.randint(0, V, (B, S), device=cuda)
+    tt = torch.randint(0, TV, (B, S), device=cuda)
+    ww = torch.randn(V, H, device=cuda, requires_grad=True)
+    wp = torch.randn(P, H, device=cuda, requires_grad=True)
+    wt = torch.randn(TV, H, device=cuda, requires_grad=True)
+    g = torch.rand(H, device=cuda, requires_grad=True)
+    b = torch.randn(H, device=cuda, requires_grad=True)
+    y = FusedEmbedding.apply(ids, tt, ww, wp, wt, g, b, 0.0, 1e-12, torch.float32)
+    leaves = [t.detach().clone().requires_grad_() for t in (ww, wp, wt, g, b)]
+    pos = torch.arange(S, device=cuda).expand(B, S)
+    e = F.embedding(ids, leaves[0]) + F.embedding(pos, leaves[1]) + F.embedding(tt, leaves[2])
+    y2 = _ref_ln(e, leaves[3], leaves[4]).view(B * S, H)
+    _close(y, y2, 1e-4, 1e-5, "emb fwd")
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    y2.backward(dy)
+    for t1, t2, n in zip((ww, wp, wt, g, b), leaves, ["word", "pos", "type", "gamma", "beta"]):
+        _close(t1.grad, t2.grad, 1e-4, 1e-3, "emb d" + n)
+
+
+def test_cross_entropy(cuda):
+    from hetseq_amd.ops.bert_ops import cross_entropy
+
+    torch.manual_seed(8)
+    for V in (2, 30522):
+        x = torch.randn(200, V, device=cuda, requires_grad=True)
+        lab = torch.randint(0, V, (200,), device=cuda)
+        lab[::3] = -1
+        l1 = cross_entropy(x, lab)
+        x2 = x.detach().clone().requires_grad_()
+        l2 = F.cross_entropy(x2, lab, ignore_index=-1)
+        _close(l1, l2, 1e-5, 1e-6, "xent fwd")
+        l1.backward()
+        l2.backward()
+        _close(x.grad, x2.grad, 1e-4, 1e-8, "xent bwd")
+
+
+@pytest.mark.parametrize("ta,tb", [(0, 1), (0, 0), (1, 0)])
+@pytest.mark.parametrize("M,N,K", [(256, 384, 128), (300, 130, 72), (4096, 768, 768), (640, 30522, 64)])
+def test_gemm_hip(cuda, ta, tb, M, N, K):
+    from hetseq_amd.ops import gemm as G
+
+    torch.manual_seed(9)
+    a = torch.randn((K, M) if ta else (M, K), device=cuda)
+    b = torch.randn((N, K) if tb else (K, N), device=cuda)
+    bias = torch.randn(N, device=cuda)
+    ref = (a.t() if ta else a).double() @ (b.t() if tb else b).double()
+    out = torch.empty(M, N, device=cuda)
+    G._hip_gemm(a, b, ta, tb, out)
+    _close(out, ref, 1e-5, 1e-4, "gemm")
+    G._hip_gemm(a, b, ta, tb, out, bias=bias, epi=1)
+    _close(out, ref + bias.double(), 1e-5, 1e-4, "gemm+bias")
+    c0 = torch.randn(M, N, device=cuda)
+    out.copy_(c0)
+    G._hip_gemm(a, b, ta, tb, out, beta=1.0)
+    _close(out, ref + c0.double(), 1e-5, 1e-4, "gemm beta")
+    G._hip_gemm(a, b, ta, tb, out, bias=bias, epi=2)
+    from hetseq_amd.models.bert import f_gelu
+
+    _close(out, f_gelu(ref + bias.double()), 1e-5, 1e-4, "gemm gelu")
+
+
+def test_adam_flat_matches_reference(cuda):
+    from argparse import Namespace
+
+    from hetseq_amd.optim.optimizers import AdamReference, _Adam
+    from hetseq_amd.runtime.flat import FlatParamStore
+
+    torch.manual_seed(10)
+    m = torch.nn.Sequential(torch.nn.Linear(64, 33), torch.nn.Linear(33, 7)).to(cuda)
+    m_ref = torch.nn.Sequential(torch.nn.Linear(64, 33), torch.nn.Linear(33, 7)).to(cuda)
+    m_ref.load_state_dict(m.state_dict())
+    store = FlatParamStore(m)
+    args = Namespace(lr=[1e-2], adam_betas="(0.9, 0.98)", adam_eps=1e-6, weight_decay=0.01)
+    opt = _Adam(args, list(m.parameters()), store)
+    ref = AdamReference(m_ref.parameters(), lr=1e-2, betas=(0.9, 0.98), eps=1e-6, weight_decay=0.01)
+    for step in range(5):
+        x = torch.randn(16, 64, device=cuda)
+        opt.zero_grad()
+        ref.zero_grad()
+        m(x).pow(2).sum().backward()
+        m_ref(x).pow(2).sum().backward()
+        opt.multiply_grads(0.5)
+        for p in m_ref.parameters():
+            p.grad.mul_(0.5)
+        n1 = opt.clip_grad_norm(1.0)
+        n2 = torch.nn.utils.clip_grad_norm_(list(m_ref.parameters()), 1.0)
+        _close(n1, n2, 1e-5, 1e-6, "grad norm")
+        opt.step()
+        ref.step()
+    for p1, p2 in zip(m.parameters(), m_ref.parameters()):
+        _close(p1, p2, 1e-5, 1e-6, "adam params")
+
+
+def test_adadelta_flat_matches_torch(cuda):
+    from argparse import Namespace
+
+    from hetseq_amd.optim.optimizers import _Adadelta
+    from hetseq_amd.runtime.flat import FlatParamStore
+
+    torch.manual_seed(11)
+    m = torch.nn.Linear(50, 20).to(cuda)
+    m_ref = torch.nn.Linear(50, 20).to(cuda)
+    m_ref.load_state_dict(m.state_dict())
+    store = FlatParamStore(m)
+    args = Namespace(lr=[1.0], adadelta_rho=0.9, adadelta_eps=1e-6, dadelta_weight_decay=0.001)
+    opt = _Adadelta(args, list(m.parameters()), store)
+    ref = torch.optim.Adadelta(m_ref.parameters(), lr=1.0, rho=0.9, eps=1e-6, weight_decay=0.001)
+    for _ in range(4):
+        x = torch.randn(8, 50, device=cuda)
+        opt.zero_grad()
+        ref.zero_grad()
+        m(x).sum().backward()
+        m_ref(x).sum().backward()
+        opt.step()
+        ref.step()
+    for p1, p2 in zip(m.parameters(), m_ref.parameters()):
+        _close(p1, p2, 1e-5, 1e-6, "adadelta")
+
+
+def test_mlm_compact_and_gather(cuda):
+    from hetseq_amd.ops import bert_ops
+
+    torch.manual_seed(12)
+    T = 5000
+    labels = torch.full((T,), -1, dtype=torch.int64, device=cuda)
+    sel = torch.randperm(T, device=cuda)[:700].sort().values
+    labels[sel] = torch.randint(0, 100, (700,), device=cuda)
+    idx, lab, cnt = bert_ops.mlm_compact(labels, 800)
+    assert int(cnt.item()) == 700
+    assert torch.equal(idx[:700].long(), sel)
+    assert torch.equal(lab[:700], labels[sel])
+    assert (idx[700:] == -1).all() and (lab[700:] == -1).all()
+    src = torch.randn(T, 256, device=cuda)
+    g = bert_ops.gather_rows(src, idx)
+    assert torch.equal(g[:700], src[sel]) and (g[700:] == 0).all()
+
+
+@pytest.mark.parametrize("N", [3072, 30522, 2])
+def test_colsum(cuda, N):
+    from hetseq_amd.ops.bert_ops import colsum
+
+    torch.manual_seed(13)
+    x = torch.randn(700, N, device=cuda)
+    _close(colsum(x), x.double().sum(0), 1e-5, 1e-4, "colsum")
