@@ -15,6 +15,7 @@
 // (4 per thread, 16-byte vectors) and a chunk of rows, keeping per-column
 // partial sums in registers -> one partial row per block, no atomics.
 #include "common.h"
+#include "reduce.h"
 
 namespace hs {
 
@@ -87,15 +88,6 @@ __global__ void __launch_bounds__(256) colsum_scalar_kernel(const T* __restrict_
   float acc = 0.f;
   for (int64_t r = r0; r < r1; ++r) acc += to_f(x[r * N + c]);
   part[(int64_t)blockIdx.y * N + c] = acc;
-}
-
-__global__ void partial_rows_sum_kernel(const float* __restrict__ part, int nparts, int N, float* __restrict__ out,
-                                        int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= N) return;
-  float s = 0.f;
-  for (int r = 0; r < nparts; ++r) s += part[(int64_t)r * N + c];
-  out[c] = accumulate ? out[c] + s : s;
 }
 
 // Single-block exclusive scan over `rows` labels; writes idx[cap] (padded
@@ -239,8 +231,9 @@ void launch_colsum(int dtype, const void* dy, const void* x, const float* b, voi
       hipLaunchKernelGGL((colsum_tile_kernel<bf16_t, false>), grid, dim3(256), 0, st, (const bf16_t*)dy, nullptr, b,
                          nullptr, part, rows, N, rpc);
   }
-  hipLaunchKernelGGL(partial_rows_sum_kernel, dim3((N + 255) / 256), dim3(256), 0, st, part, chunks, N, out,
-                     accumulate);
+  const float* pp[1] = {part};
+  float* oo[1] = {out};
+  launch_reduce_rows(pp, oo, 1, chunks, N, accumulate, st);
 }
 
 void launch_mlm_compact(const int64_t* labels, int rows, int ignore_index, int cap, int32_t* idx, int64_t* lab_out,

@@ -16,6 +16,7 @@
 // dgamma/dbeta/dbias; `colpart_finalize` reduces the partials (no atomics,
 // deterministic).  Dropout masks are regenerated from Philox (seed, offset).
 #include "common.h"
+#include "reduce.h"
 
 namespace hs {
 
@@ -317,21 +318,6 @@ __global__ void __launch_bounds__(256) emb_bwd_kernel(const T* __restrict__ dy, 
   }
 }
 
-// out[c] (+)= sum_r part[r][c]; grid.y selects one of up to 3 (part, out) pairs.
-struct ColPartArgs {
-  const float* part[3];
-  float* out[3];
-};
-__global__ void colpart_finalize_kernel(ColPartArgs args, int nparts, int H, int accumulate) {
-  const float* part = args.part[blockIdx.y];
-  float* out = args.out[blockIdx.y];
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= H) return;
-  float s = 0.f;
-  for (int r = 0; r < nparts; ++r) s += part[(int64_t)r * H + c];
-  out[c] = accumulate ? out[c] + s : s;
-}
-
 constexpr int kLnBwdBlocks = 256;
 
 template <int NV, typename T>
@@ -446,10 +432,5 @@ int launch_emb_bwd(int dtype, const void* dy, const int64_t* ids, const int64_t*
 
 void launch_colpart_finalize(const float* const* parts, float* const* outs, int n, int nparts, int H, int accumulate,
                              hipStream_t st) {
-  ColPartArgs a{};
-  for (int i = 0; i < n; ++i) {
-    a.part[i] = parts[i];
-    a.out[i] = outs[i];
-  }
-  hipLaunchKernelGGL(colpart_finalize_kernel, dim3((H + 255) / 256, n), dim3(256), 0, st, a, nparts, H, accumulate);
+  launch_reduce_rows(parts, outs, n, nparts, H, accumulate, st);
 }

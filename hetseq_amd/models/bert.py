@@ -230,10 +230,15 @@ class BertEmbeddings(nn.Module):
         from hetseq_amd.ops.bert_ops import FusedEmbedding
 
         p = self.dropout.p if self.training else 0.0
-        return FusedEmbedding.apply(input_ids, token_type_ids, self.word_embeddings.weight,
-                                    self.position_embeddings.weight, self.token_type_embeddings.weight,
-                                    self.LayerNorm.weight, self.LayerNorm.bias, p, self.LayerNorm.variance_epsilon,
-                                    out_dtype)
+        params = [self.word_embeddings.weight, self.position_embeddings.weight, self.token_type_embeddings.weight,
+                  self.LayerNorm.weight, self.LayerNorm.bias]
+        store = getattr(self, "_hs_store", None)
+        sink = None
+        if store is not None:
+            sink = {"views": lambda: [store.grad_view(q) for q in params],
+                    "notify": lambda: store.notify_ready(params)}
+        return FusedEmbedding.apply(input_ids, token_type_ids, *params, p, self.LayerNorm.variance_epsilon,
+                                    out_dtype, sink)
 
 
 class BertSelfAttention(nn.Module):
@@ -383,7 +388,31 @@ class BertLayer(nn.Module):
         seeds = tuple(rng.fork() if p > 0 else (0, 0) for p in (p_a, p_h, p_h))
         cfg = (B, S, self.attention.self.num_attention_heads, p_h, p_a, self.output.LayerNorm.variance_epsilon, seeds)
         meta = {"weights": self._weights, "cfg": cfg, "recompute": recompute}
+        store = getattr(self, "_hs_store", None)
+        if store is not None:
+            params = self.fused_params()
+            meta["grad_sink"] = self._grad_views
+            meta["notify"] = lambda: store.notify_ready(params)
         return FusedBertLayer.apply(x2d, mask_i64, meta, *self.fused_params())
+
+    def _grad_views(self):
+        """fp32 views of this layer's gradients inside the flat store (accumulated in place)."""
+        from hetseq_amd.ops.bert_ops import LayerWeights
+
+        store = self._hs_store
+        sa, ao, o = self.attention.self, self.attention.output, self.output
+        H = sa.query.weight.shape[1]
+        g = LayerWeights()
+        g.wqkv = store.combined_grad([sa.query.weight, sa.key.weight, sa.value.weight], (3 * sa.all_head_size, H))
+        g.bqkv = store.combined_grad([sa.query.bias, sa.key.bias, sa.value.bias], (3 * sa.all_head_size,))
+        assert g.wqkv is not None and g.bqkv is not None, "Q/K/V parameters are not adjacent in the flat store"
+        gv = store.grad_view
+        g.wo, g.bo = gv(ao.dense.weight), gv(ao.dense.bias)
+        g.g1, g.b1 = gv(ao.LayerNorm.weight), gv(ao.LayerNorm.bias)
+        g.w1, g.bi = gv(self.intermediate.dense_act.weight), gv(self.intermediate.dense_act.bias)
+        g.w2, g.b2 = gv(o.dense.weight), gv(o.dense.bias)
+        g.g2, g.bb2 = gv(o.LayerNorm.weight), gv(o.LayerNorm.bias)
+        return g
 
 
 class BertEncoder(nn.Module):
@@ -688,6 +717,13 @@ class BertForPreTraining(BertPreTrainedModel):
         cap = B * S if self.max_predictions_per_seq is None else min(B * S, B * int(self.max_predictions_per_seq))
         t = self.cls.predictions.transform
         meta = {"cap": cap, "eps": t.LayerNorm.variance_epsilon, "weights": self._mlm_weights}
+        store = getattr(self, "_hs_store", None)
+        if store is not None:
+            cls_params = [t.dense_act.weight, t.dense_act.bias, t.LayerNorm.weight, t.LayerNorm.bias,
+                          self.cls.predictions.decoder.weight, self.cls.predictions.bias]
+            meta["grad_sink"] = lambda: [store.grad_view(q) for q in cls_params]
+            # decoder.weight is the (tied) word embedding: announced by the embedding backward
+            meta["notify"] = lambda: store.notify_ready(cls_params[:4] + cls_params[5:])
         mlm_loss = FusedMLMLoss.apply(seq2d, labels.reshape(-1).contiguous(), meta, t.dense_act.weight,
                                       t.dense_act.bias, t.LayerNorm.weight, t.LayerNorm.bias,
                                       self.cls.predictions.decoder.weight, self.cls.predictions.bias)

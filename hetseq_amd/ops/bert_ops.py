@@ -71,7 +71,10 @@ def ln_fwd(a, gamma, beta, eps=1e-12, bias=None, resid=None, p=0.0, mode=0, seed
     return y, z, mean, rstd
 
 
-def ln_bwd(dy, z, mean, rstd, gamma, p=0.0, mode=0, seed=0, off=0, want_dz=True, want_da=False, dz_out=None):
+def ln_bwd(dy, z, mean, rstd, gamma, p=0.0, mode=0, seed=0, off=0, want_dz=True, want_da=False, dz_out=None,
+           acc=None):
+    """LN backward.  ``acc`` = (dgamma, dbeta[, dbias]) fp32 tensors to ACCUMULATE into
+    (flat-store gradient views); otherwise fresh tensors are returned."""
     rows, H = dy.shape
     nb = hip().ln_bwd_num_blocks()
     part = _colpart_buf(nb, H, dy.device)
@@ -81,9 +84,15 @@ def ln_bwd(dy, z, mean, rstd, gamma, p=0.0, mode=0, seed=0, off=0, want_dz=True,
                  dz.data_ptr() if dz is not None else 0, da.data_ptr() if da is not None else 0, part[0].data_ptr(),
                  part[1].data_ptr(), part[2].data_ptr(), rows, H, float(p), seed, off, mode, stream_handle())
     n = 3 if mode == 1 else 2
-    outs = torch.empty((n, H), dtype=torch.float32, device=dy.device)
-    hip().colpart_finalize([part[i].data_ptr() for i in range(n)], [outs[i].data_ptr() for i in range(n)], nb, H, 0,
-                           stream_handle())
+    if acc is not None:
+        outs = list(acc[:n])
+        assert all(o.is_contiguous() and o.dtype == torch.float32 for o in outs)
+        hip().colpart_finalize([part[i].data_ptr() for i in range(n)], [o.data_ptr() for o in outs], nb, H, 1,
+                               stream_handle())
+    else:
+        outs = torch.empty((n, H), dtype=torch.float32, device=dy.device)
+        hip().colpart_finalize([part[i].data_ptr() for i in range(n)], [outs[i].data_ptr() for i in range(n)], nb, H,
+                               0, stream_handle())
     dgamma, dbeta = outs[0], outs[1]
     dbias = outs[2] if mode == 1 else None
     return dz, da, dgamma, dbeta, dbias
@@ -97,26 +106,28 @@ def bias_gelu_fwd(x, b):
     return y
 
 
-def gelu_bwd_colsum(dy, x, b):
-    """dx = dy * gelu'(x+b) and db = sum_rows(dx)."""
+def gelu_bwd_colsum(dy, x, b, db_acc=None):
+    """dx = dy * gelu'(x+b) and db = sum_rows(dx) (accumulated into ``db_acc`` if given)."""
     rows, N = dy.shape
     assert N % 4 == 0 and dy.is_contiguous() and x.is_contiguous()
     chunks = hip().colsum_row_chunks(rows)
     part = torch.empty((chunks, N), dtype=torch.float32, device=dy.device)
-    db = torch.empty(N, dtype=torch.float32, device=dy.device)
+    db = db_acc if db_acc is not None else torch.empty(N, dtype=torch.float32, device=dy.device)
     dx = torch.empty_like(dy)
     hip().colsum(dtype_code(dy), dy.data_ptr(), x.data_ptr(), b.data_ptr(), dx.data_ptr(), part.data_ptr(),
-                 db.data_ptr(), rows, N, 0, stream_handle())
+                 db.data_ptr(), rows, N, 1 if db_acc is not None else 0, stream_handle())
     return dx, db
 
 
-def colsum(x):
+def colsum(x, acc=None):
+    """Column sums of x (fp32), accumulated into ``acc`` if given."""
     rows, N = x.shape
     assert x.is_contiguous()
     chunks = hip().colsum_row_chunks(rows)
     part = torch.empty((chunks, N), dtype=torch.float32, device=x.device)
-    out = torch.empty(N, dtype=torch.float32, device=x.device)
-    hip().colsum(dtype_code(x), x.data_ptr(), 0, 0, 0, part.data_ptr(), out.data_ptr(), rows, N, 0, stream_handle())
+    out = acc if acc is not None else torch.empty(N, dtype=torch.float32, device=x.device)
+    hip().colsum(dtype_code(x), x.data_ptr(), 0, 0, 0, part.data_ptr(), out.data_ptr(), rows, N,
+                 1 if acc is not None else 0, stream_handle())
     return out
 
 
@@ -213,7 +224,7 @@ def bias_gelu(x, b):
 # --------------------------------------------------------------------- embeddings
 class FusedEmbedding(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, ids, tt, wword, wpos, wtype, gamma, beta, p, eps, out_dtype):
+    def forward(ctx, ids, tt, wword, wpos, wtype, gamma, beta, p, eps, out_dtype, sink=None):
         B, S = ids.shape
         V, H = wword.shape
         TV = wtype.shape[0]
@@ -233,6 +244,7 @@ class FusedEmbedding(torch.autograd.Function):
                       err.data_ptr(), stream_handle())
         ctx.save_for_backward(ids, tt if tt is not None else ids.new_zeros(0), z, mean, rstd, gamma)
         ctx.cfg = (B, S, V, H, TV, wpos.shape[0], p, seed, off, tt is not None)
+        ctx.sink = sink
         return y
 
     @staticmethod
@@ -241,19 +253,27 @@ class FusedEmbedding(torch.autograd.Function):
         B, S, V, H, TV, P, p, seed, off, has_tt = ctx.cfg
         dy = dy.contiguous()
         dev = dy.device
-        dword = torch.zeros((V, H), dtype=torch.float32, device=dev)
-        dpos = torch.zeros((P, H), dtype=torch.float32, device=dev)
-        dtype_ = torch.zeros((TV, H), dtype=torch.float32, device=dev)
+        sink = ctx.sink
+        if sink is not None:  # accumulate straight into the flat gradient buffer
+            dword, dpos, dtype_, dg, db = sink["views"]()
+        else:
+            dword = torch.zeros((V, H), dtype=torch.float32, device=dev)
+            dpos = torch.zeros((P, H), dtype=torch.float32, device=dev)
+            dtype_ = torch.zeros((TV, H), dtype=torch.float32, device=dev)
+            outs = torch.empty((2, H), dtype=torch.float32, device=dev)
+            dg, db = outs[0], outs[1]
         nb = hip().ln_bwd_num_blocks()
         part = _colpart_buf(nb, H, dev, 2)
         hip().emb_bwd(dtype_code(dy), dy.data_ptr(), ids.data_ptr(), tt.data_ptr() if has_tt else 0, z.data_ptr(),
                       mean.data_ptr(), rstd.data_ptr(), gamma.data_ptr(), dword.data_ptr(), dpos.data_ptr(),
                       dtype_.data_ptr(), part[0].data_ptr(), part[1].data_ptr(), B * S, S, H, V, TV, float(p), seed,
                       off, stream_handle())
-        outs = torch.empty((2, H), dtype=torch.float32, device=dev)
-        hip().colpart_finalize([part[0].data_ptr(), part[1].data_ptr()], [outs[0].data_ptr(), outs[1].data_ptr()], nb,
-                               H, 0, stream_handle())
-        return None, None, dword, dpos, dtype_, outs[0], outs[1], None, None, None
+        hip().colpart_finalize([part[0].data_ptr(), part[1].data_ptr()], [dg.data_ptr(), db.data_ptr()], nb, H,
+                               1 if sink is not None else 0, stream_handle())
+        if sink is not None:
+            sink["notify"]()
+            return (None,) * 11
+        return None, None, dword, dpos, dtype_, dg, db, None, None, None, None
 
 
 # --------------------------------------------------------------------- encoder layer
@@ -311,21 +331,29 @@ class FusedBertLayer(torch.autograd.Function):
         B, S, NH, p_h, p_a, eps, seeds = cfg
         (s_a, o_a), (s_1, o_1), (s_2, o_2) = seeds
         dh2 = dh2.contiguous()
+        H = x.shape[1]
+        sink = meta.get("grad_sink")
+        Gv = sink() if sink is not None else None  # flat-store gradient views (accumulate in place)
+        acc = Gv is not None
         # LN2 (bias-dropout-residual) backward
-        dz2, do_, dg2, dbb2, db2 = ln_bwd(dh2, z2, m2, r2, W.g2, p_h, 1, s_2, o_2, True, True)
-        dW2 = G.linear_wgrad(do_, f1)
+        dz2, do_, dg2, dbb2, db2 = ln_bwd(dh2, z2, m2, r2, W.g2, p_h, 1, s_2, o_2, True, True,
+                                          acc=(Gv.g2, Gv.bb2, Gv.b2) if acc else None)
+        dW2 = G.linear_wgrad(do_, f1, out=Gv.w2 if acc else None, accumulate=acc)
         df1 = G.linear_dgrad(do_, W.w2)
-        df1pre, dbi = gelu_bwd_colsum(df1, f1pre, W.bi)
-        dW1 = G.linear_wgrad(df1pre, h1)
+        df1pre, dbi = gelu_bwd_colsum(df1, f1pre, W.bi, db_acc=Gv.bi if acc else None)
+        dW1 = G.linear_wgrad(df1pre, h1, out=Gv.w1 if acc else None, accumulate=acc)
         dh1 = G.linear_dgrad(df1pre, W.w1, out=dz2, accumulate=True)  # dz2 + df1pre @ W1
-        dz1, da1, dg1, db1, dbo = ln_bwd(dh1, z1, m1, r1, W.g1, p_h, 1, s_1, o_1, True, True)
-        dWo = G.linear_wgrad(da1, ctx_)
+        dz1, da1, dg1, db1, dbo = ln_bwd(dh1, z1, m1, r1, W.g1, p_h, 1, s_1, o_1, True, True,
+                                         acc=(Gv.g1, Gv.b1, Gv.bo) if acc else None)
+        dWo = G.linear_wgrad(da1, ctx_, out=Gv.wo if acc else None, accumulate=acc)
         dctx = G.linear_dgrad(da1, W.wo)
         dqkv = attn_bwd(qkv, mask, ctx_, dctx, lse, B, S, NH, p_a, s_a, o_a)
-        dWqkv = G.linear_wgrad(dqkv, x)
-        dbqkv = colsum(dqkv)
+        dWqkv = G.linear_wgrad(dqkv, x, out=Gv.wqkv if acc else None, accumulate=acc)
+        dbqkv = colsum(dqkv, acc=Gv.bqkv if acc else None)
         dx = G.linear_dgrad(dqkv, W.wqkv, out=dz1, accumulate=True)  # dz1 + dqkv @ Wqkv
-        H = x.shape[1]
+        if acc:
+            meta["notify"]()
+            return (dx, None, None) + (None,) * 16
         return (dx, None, None,
                 dWqkv[:H], dbqkv[:H], dWqkv[H:2 * H], dbqkv[H:2 * H], dWqkv[2 * H:], dbqkv[2 * H:],
                 dWo, dbo, dg1, db1, dW1, dbi, dW2, db2, dg2, dbb2)
@@ -419,15 +447,23 @@ class FusedMLMLoss(torch.autograd.Function):
     def backward(ctx, dloss):
         idx, lab, hsel, t1pre, t1, z, mean, rstd, t2, logits, lse, out, g, bt = ctx.saved_tensors
         Wt, Wd = ctx.meta["weights"]()
+        sink = ctx.meta.get("grad_sink")
+        Gv = sink() if sink is not None else None  # (wt, bt, g, b, wdec, bdec) flat-store views
+        acc = Gv is not None
         dlogits = xent_bwd_(logits, lab, lse, dloss.reshape(1).float().contiguous(), out)  # in place, fp32
-        dWdec = G.linear_wgrad(dlogits, t2.float() if t2.dtype != torch.float32 else t2)
-        dbdec = colsum(dlogits)
+        # tied decoder weight: accumulates into the word-embedding gradient
+        dWdec = G.linear_wgrad(dlogits, t2.float() if t2.dtype != torch.float32 else t2,
+                               out=Gv[4] if acc else None, accumulate=acc)
+        dbdec = colsum(dlogits, acc=Gv[5] if acc else None)
         dt2 = G.gemm(dlogits.to(t2.dtype) if t2.dtype != torch.float32 else dlogits, Wd)
-        dt1, _, dg, db, _ = ln_bwd(dt2, z, mean, rstd, g, 0.0, 0)
-        dt1pre, dbt = gelu_bwd_colsum(dt1, t1pre, bt)
-        dWt = G.linear_wgrad(dt1pre, hsel)
+        dt1, _, dg, db, _ = ln_bwd(dt2, z, mean, rstd, g, 0.0, 0, acc=(Gv[2], Gv[3]) if acc else None)
+        dt1pre, dbt = gelu_bwd_colsum(dt1, t1pre, bt, db_acc=Gv[1] if acc else None)
+        dWt = G.linear_wgrad(dt1pre, hsel, out=Gv[0] if acc else None, accumulate=acc)
         dhsel = G.linear_dgrad(dt1pre, Wt)
         dseq = torch.zeros((ctx.T, hsel.shape[1]), dtype=hsel.dtype, device=hsel.device)
         hip().scatter_add_rows(dtype_code(dseq), dhsel.data_ptr(), idx.data_ptr(), dseq.data_ptr(), idx.numel(),
                                hsel.shape[1], stream_handle())
+        if acc:
+            ctx.meta["notify"]()  # the tied decoder weight is announced by the embedding backward
+            return dseq, None, None, None, None, None, None, None, None
         return dseq, None, None, dWt, dbt, dg, db, dWdec, dbdec

@@ -122,6 +122,6 @@ def linear_dgrad(dy, w, out=None, accumulate=False):
     return gemm(dy, w, ta=False, tb=False, out=out, beta=1.0 if accumulate else 0.0)
 
 
-def linear_wgrad(dy, x, out=None):
-    """dy[T,N]^T @ x[T,K] -> [N,K] in fp32."""
-    return gemm(dy, x, ta=True, tb=False, out=out, out_dtype=torch.float32)
+def linear_wgrad(dy, x, out=None, accumulate=False):
+    """dy[T,N]^T @ x[T,K] -> [N,K] in fp32; accumulate=True adds into ``out`` (flat grad view)."""
+    return gemm(dy, x, ta=True, tb=False, out=out, out_dtype=torch.float32, beta=1.0 if accumulate else 0.0)

@@ -71,6 +71,7 @@ class FlatDDP(torch.nn.Module):
         # extend ranges to cover alignment gaps so the buckets tile the buffer
         self._reset_state()
         self._hooks = [p.register_post_accumulate_grad_hook(self._grad_ready) for p in params]
+        store.add_ready_callback(self._grad_ready)  # fused kernels that write grads directly
         if broadcast and self.world_size > 1:
             with torch.no_grad():
                 dist.broadcast(store.param, src=0, group=self.process_group)

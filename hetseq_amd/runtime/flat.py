@@ -111,6 +111,35 @@ class FlatParamStore(object):
         off = self.offsets[id(p)]
         return self.grad[off : off + p.numel()]
 
+    def grad_view(self, p):
+        off = self.offsets[id(p)]
+        return self.grad[off : off + p.numel()].view(p.shape)
+
+    def combined_grad(self, params, shape):
+        off = self.offsets.get(id(params[0]))
+        cur = off
+        for p in params:
+            if self.offsets.get(id(p)) != cur:
+                return None
+            cur += p.numel()
+        return self.grad[off:cur].view(shape)
+
+    # ------------------------------------------------------------ direct gradients
+    # Fused backward kernels accumulate parameter gradients straight into
+    # ``self.grad`` (GEMM beta=1, kernel-side accumulate flags, atomics) and
+    # return None to autograd, so no per-parameter ``grad += new`` pass runs.
+    # They then call ``notify_ready`` -- the data-parallel engine subscribes
+    # to it exactly like to post-accumulate-grad hooks.
+    def add_ready_callback(self, fn):
+        if not hasattr(self, "_ready_cbs"):
+            self._ready_cbs = []
+        self._ready_cbs.append(fn)
+
+    def notify_ready(self, params):
+        for fn in getattr(self, "_ready_cbs", ()):
+            for p in params:
+                fn(p)
+
     # ------------------------------------------------------------ ops
     def zero_grad(self):
         self.grad.zero_()
