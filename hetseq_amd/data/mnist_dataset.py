@@ -52,9 +52,25 @@ def find_split_file(path, split):
                 "MNIST not found under {} (no network: place processed/{{training,test}}.pt or raw IDX files there, "
                 "or generate synthetic ones with tools/make_synthetic_mnist.py)".format(path))
     files = [os.path.join(path, f) for f in os.listdir(path)] if os.path.isdir(path) else [path]
-    files = sorted([f for f in files if split in os.path.basename(f) or split in f])
+    files = select_split_files(files, split)
     assert len(files) == 1, "no suitable file in split ***{}***".format(split)
     return files[0]
+
+
+def select_split_files(files, split):
+    """Files of a split: the reference matches ``split in path`` on the FULL path
+    (reference: tasks.py:240-241, Q10), so a directory named e.g. ``test_128``
+    selects everything.  Match on the file name first and fall back to the
+    reference's full-path rule only when no file name matches."""
+    by_name = sorted(f for f in files if split in os.path.basename(f))
+    if by_name:
+        return by_name
+    by_path = sorted(f for f in files if split in f)
+    if by_path:
+        import warnings
+
+        warnings.warn("split '{}' matched only through directory names (reference full-path rule)".format(split))
+    return by_path
 
 
 def _idx_pair(raw, split):

@@ -793,9 +793,9 @@ class BertForMultipleChoice(BertPreTrainedModel):
         self.apply(self.init_bert_weights)
 
     def forward(self, input_ids, token_type_ids=None, attention_mask=None, labels=None, checkpoint_activations=False):
-        flat_input_ids = input_ids.view(-1, input_ids.size(-1))
-        flat_token_type_ids = token_type_ids.view(-1, token_type_ids.size(-1))
-        flat_attention_mask = attention_mask.view(-1, attention_mask.size(-1))
+        flat_input_ids = input_ids.reshape(-1, input_ids.size(-1))
+        flat_token_type_ids = token_type_ids.reshape(-1, token_type_ids.size(-1))
+        flat_attention_mask = attention_mask.reshape(-1, attention_mask.size(-1))
         _, pooled_output = self.bert(flat_input_ids, flat_token_type_ids, flat_attention_mask,
                                      output_all_encoded_layers=False)
         logits = self.classifier(self.dropout(pooled_output))

@@ -39,7 +39,7 @@ def distributed_init(args):
         warnings.warn("Distributed is already initialized, cannot initialize twice!")
     else:
         backend = args.distributed_backend
-        if backend == "nccl" and not torch.cuda.is_available():
+        if backend == "nccl" and (not torch.cuda.is_available() or getattr(args, "cpu", False)):
             backend = "gloo"  # CPU runs: RCCL needs a GPU
             args.distributed_backend = backend
         print("| distributed init (rank {}): {}".format(args.distributed_rank, args.distributed_init_method), flush=True)

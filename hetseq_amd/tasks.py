@@ -20,7 +20,7 @@ import numpy as np
 import torch
 
 from hetseq_amd.data import data_utils, iterators
-from hetseq_amd.data.mnist_dataset import MNISTDataset, find_split_file
+from hetseq_amd.data.mnist_dataset import MNISTDataset, find_split_file, select_split_files
 
 
 class Task(object):
@@ -119,7 +119,7 @@ class LanguageModelingTask(Task):
         if not os.path.exists(path):
             raise FileNotFoundError("Dataset not found: ({})".format(path))
         files = [os.path.join(path, f) for f in os.listdir(path)] if os.path.isdir(path) else [path]
-        files = sorted([f for f in files if split in f])
+        files = select_split_files(files, split)
         if self.args.num_file > 0:
             files = files[0:self.args.num_file]
         assert len(files) > 0, "no suitable file in split ***{}***".format(split)
