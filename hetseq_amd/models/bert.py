@@ -235,8 +235,7 @@ class BertEmbeddings(nn.Module):
         store = getattr(self, "_hs_store", None)
         sink = None
         if store is not None:
-            sink = {"views": lambda: [store.grad_view(q) for q in params],
-                    "notify": lambda: store.notify_ready(params)}
+            sink = {"views": lambda: [store.grad_view(q) for q in params]}
         return FusedEmbedding.apply(input_ids, token_type_ids, *params, p, self.LayerNorm.variance_epsilon,
                                     out_dtype, sink)
 
@@ -390,9 +389,7 @@ class BertLayer(nn.Module):
         meta = {"weights": self._weights, "cfg": cfg, "recompute": recompute}
         store = getattr(self, "_hs_store", None)
         if store is not None:
-            params = self.fused_params()
             meta["grad_sink"] = self._grad_views
-            meta["notify"] = lambda: store.notify_ready(params)
         return FusedBertLayer.apply(x2d, mask_i64, meta, *self.fused_params())
 
     def _grad_views(self):
@@ -722,8 +719,6 @@ class BertForPreTraining(BertPreTrainedModel):
             cls_params = [t.dense_act.weight, t.dense_act.bias, t.LayerNorm.weight, t.LayerNorm.bias,
                           self.cls.predictions.decoder.weight, self.cls.predictions.bias]
             meta["grad_sink"] = lambda: [store.grad_view(q) for q in cls_params]
-            # decoder.weight is the (tied) word embedding: announced by the embedding backward
-            meta["notify"] = lambda: store.notify_ready(cls_params[:4] + cls_params[5:])
         mlm_loss = FusedMLMLoss.apply(seq2d, labels.reshape(-1).contiguous(), meta, t.dense_act.weight,
                                       t.dense_act.bias, t.LayerNorm.weight, t.LayerNorm.bias,
                                       self.cls.predictions.decoder.weight, self.cls.predictions.bias)

@@ -271,7 +271,6 @@ class FusedEmbedding(torch.autograd.Function):
         hip().colpart_finalize([part[0].data_ptr(), part[1].data_ptr()], [dg.data_ptr(), db.data_ptr()], nb, H,
                                1 if sink is not None else 0, stream_handle())
         if sink is not None:
-            sink["notify"]()
             return (None,) * 11
         return None, None, dword, dpos, dtype_, dg, db, None, None, None, None
 
@@ -352,7 +351,6 @@ class FusedBertLayer(torch.autograd.Function):
         dbqkv = colsum(dqkv, acc=Gv.bqkv if acc else None)
         dx = G.linear_dgrad(dqkv, W.wqkv, out=dz1, accumulate=True)  # dz1 + dqkv @ Wqkv
         if acc:
-            meta["notify"]()
             return (dx, None, None) + (None,) * 16
         return (dx, None, None,
                 dWqkv[:H], dbqkv[:H], dWqkv[H:2 * H], dbqkv[H:2 * H], dWqkv[2 * H:], dbqkv[2 * H:],
@@ -464,6 +462,5 @@ class FusedMLMLoss(torch.autograd.Function):
         hip().scatter_add_rows(dtype_code(dseq), dhsel.data_ptr(), idx.data_ptr(), dseq.data_ptr(), idx.numel(),
                                hsel.shape[1], stream_handle())
         if acc:
-            ctx.meta["notify"]()  # the tied decoder weight is announced by the embedding backward
             return dseq, None, None, None, None, None, None, None, None
         return dseq, None, None, dWt, dbt, dg, db, dWdec, dbdec

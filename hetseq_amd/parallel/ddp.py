@@ -70,8 +70,11 @@ class FlatDDP(torch.nn.Module):
                 self.bucket_of[id(p)] = bi
         # extend ranges to cover alignment gaps so the buckets tile the buffer
         self._reset_state()
+        # Readiness = post-accumulate-grad hooks.  They also fire when a fused
+        # Function returned None for a parameter whose gradient it accumulated
+        # directly into the flat buffer (the AccumulateGrad node still runs, after
+        # that Function's kernels were enqueued), so one signal covers both paths.
         self._hooks = [p.register_post_accumulate_grad_hook(self._grad_ready) for p in params]
-        store.add_ready_callback(self._grad_ready)  # fused kernels that write grads directly
         if broadcast and self.world_size > 1:
             with torch.no_grad():
                 dist.broadcast(store.param, src=0, group=self.process_group)

@@ -124,21 +124,11 @@ class FlatParamStore(object):
             cur += p.numel()
         return self.grad[off:cur].view(shape)
 
-    # ------------------------------------------------------------ direct gradients
-    # Fused backward kernels accumulate parameter gradients straight into
-    # ``self.grad`` (GEMM beta=1, kernel-side accumulate flags, atomics) and
-    # return None to autograd, so no per-parameter ``grad += new`` pass runs.
-    # They then call ``notify_ready`` -- the data-parallel engine subscribes
-    # to it exactly like to post-accumulate-grad hooks.
-    def add_ready_callback(self, fn):
-        if not hasattr(self, "_ready_cbs"):
-            self._ready_cbs = []
-        self._ready_cbs.append(fn)
-
-    def notify_ready(self, params):
-        for fn in getattr(self, "_ready_cbs", ()):
-            for p in params:
-                fn(p)
+    # Direct gradients: fused backward kernels accumulate parameter gradients
+    # straight into ``self.grad`` (GEMM beta=1, kernel-side accumulate flags,
+    # atomics) and return None to autograd, so no per-parameter ``grad += new``
+    # pass runs.  Autograd still runs the (empty) AccumulateGrad node, whose
+    # post-accumulate-grad hook is the data-parallel readiness signal.
 
     # ------------------------------------------------------------ ops
     def zero_grad(self):
