@@ -132,6 +132,10 @@ def main():
     from hetseq_amd.ops import bert_ops
 
     bert_ops.check_device_errors()
+    if os.environ.get("HETSEQ_TUNABLEOP_OUT"):
+        from hetseq_amd.runtime import gemm_tuning
+
+        gemm_tuning.flush()
     sec = elapsed / b.steps
     seqs = b.batch * b.update_freq * world
     if rank == 0:

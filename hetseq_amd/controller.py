@@ -53,6 +53,10 @@ class Controller(object):
         if not getattr(args, "fused", True):
             os.environ["HETSEQ_DISABLE_FUSED"] = "1"
         self.compute_dtype = torch.bfloat16 if getattr(args, "dtype", "fp32") == "bf16" else torch.float32
+        if self.cuda and getattr(args, "gemm_tuning", True):
+            from hetseq_amd.runtime import gemm_tuning
+
+            gemm_tuning.enable(getattr(args, "dtype", "fp32"))
         shadow = torch.bfloat16 if self.compute_dtype == torch.bfloat16 else None
         self.store = FlatParamStore(self._model, device=self.device, shadow_dtype=shadow)
         if hasattr(self._model, "attach_store"):

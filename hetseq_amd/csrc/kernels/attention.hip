@@ -7,9 +7,11 @@
 //
 // Here the kernels read Q, K, V straight out of the fused QKV projection
 // output [B*S, 3H] (no permute/contiguous copies), never materialise the
-// [B,nh,S,S] probability tensor (online softmax, flash style), regenerate the
-// dropout mask from Philox in the backward pass, and write the context in the
-// [B*S, H] layout the output projection consumes.
+// [B,nh,S,S] probability tensor (online softmax, flash style), keep only a
+// 1-bit-per-probability dropout mask (Philox keep decisions packed into one
+// 32-bit word per query x 32 keys, 786 KB per BERT-base layer) for the
+// backward pass, and write the context in the [B*S, H] layout the output
+// projection consumes.  The QKV bias is added on load (no biased copy).
 //
 // MFMA mapping (v_mfma_f32_32x32x2_f32, exact fp32 -- the reference is fp32):
 //  * a wave owns 32 rows (queries in fwd/dQ, keys in dK/dV); lane l holds row
@@ -38,40 +40,45 @@ HS_DEVICE f32x16 mfma32(float a, float b, f32x16 c) { return __builtin_amdgcn_mf
 // key/query offset (within a 32-tile) held in accumulator register r by lane half hf
 HS_DEVICE int crow(int r, int hf) { return (r & 3) + 8 * (r >> 2) + 4 * hf; }
 
+// out[kk] = (src[kk] + bias[kk]) * scale for a 32-wide half row (bias may be null).
+// The QKV projection bias is folded in here, so the projection GEMM runs
+// without a bias epilogue and no biased copy of Q/K/V is ever written.
 template <typename T>
-HS_DEVICE void load_row_half(const T* src, float scale, float (&out)[32]) {
+HS_DEVICE void load_row_half(const T* src, const float* bias, float scale, float (&out)[32]) {
 #pragma unroll
   for (int kk = 0; kk < 32; kk += 4) {
-    float v[4];
+    float v[4], b[4] = {0.f, 0.f, 0.f, 0.f};
     load4(src + kk, v);
-    out[kk] = v[0] * scale;
-    out[kk + 1] = v[1] * scale;
-    out[kk + 2] = v[2] * scale;
-    out[kk + 3] = v[3] * scale;
+    if (bias) load4(bias + kk, b);
+    out[kk] = (v[0] + b[0]) * scale;
+    out[kk + 1] = (v[1] + b[1]) * scale;
+    out[kk + 2] = (v[2] + b[2]) * scale;
+    out[kk + 3] = (v[3] + b[3]) * scale;
   }
 }
 
-// Stage rows [r0, r0+n) of a head slice (column offset col) into LDS (fp32).
+// Stage rows [r0, r0+n) of a head slice (column offset col) into LDS (fp32),
+// adding the (nullable) per-column bias `bias` (already offset to `col`).
 template <typename T>
-HS_DEVICE void stage_rows(float* lds, const T* base, int64_t ld, int r0, int n, int col, float scale) {
+HS_DEVICE void stage_rows(float* lds, const T* base, int64_t ld, int r0, int n, int col, const float* bias,
+                          float scale) {
   for (int i = threadIdx.x; i < n * 16; i += blockDim.x) {
     const int r = i >> 4, c4 = (i & 15) * 4;
-    float v[4];
+    float v[4], b[4] = {0.f, 0.f, 0.f, 0.f};
     load4(base + (int64_t)(r0 + r) * ld + col + c4, v);
-    *reinterpret_cast<float4*>(lds + r * kLD + c4) = make_float4(v[0] * scale, v[1] * scale, v[2] * scale, v[3] * scale);
+    if (bias) load4(bias + c4, b);
+    *reinterpret_cast<float4*>(lds + r * kLD + c4) =
+        make_float4((v[0] + b[0]) * scale, (v[1] + b[1]) * scale, (v[2] + b[2]) * scale, (v[3] + b[3]) * scale);
   }
 }
 
-HS_DEVICE float keep_one(uint64_t seed, uint64_t off, uint64_t e, float p, float scale) {
-  const uint4 r = philox_at(seed, off, e >> 2);
-  const uint32_t x = (e & 3) == 0 ? r.x : ((e & 3) == 1 ? r.y : ((e & 3) == 2 ? r.z : r.w));
-  return u01(x) >= p ? scale : 0.f;
-}
+HS_DEVICE const float* boff(const float* b, int off) { return b ? b + off : nullptr; }
 
 template <typename T>
 __global__ void __launch_bounds__(256, 2)
-    attn_fwd_kernel(const T* __restrict__ qkv, const int64_t* __restrict__ mask, T* __restrict__ ctx,
-                    float* __restrict__ lse, int S, int NH, float p, uint64_t seed, uint64_t off) {
+    attn_fwd_kernel(const T* __restrict__ qkv, const int64_t* __restrict__ mask, const float* __restrict__ bqkv,
+                    T* __restrict__ ctx, float* __restrict__ lse, uint32_t* __restrict__ dmask, int S, int NH, float p,
+                    uint64_t seed, uint64_t off) {
   __shared__ __attribute__((aligned(16))) float Ks[kCH * kLD];
   __shared__ __attribute__((aligned(16))) float Vs[kCH * kLD];
   __shared__ float Ms[kCH];
@@ -85,7 +92,7 @@ __global__ void __launch_bounds__(256, 2)
   const float dscale = p < 1.f ? 1.f / (1.f - p) : 0.f;
 
   float qr[32];
-  if (active) load_row_half(rows + (int64_t)(q0 + li) * ld + h * kD + hf * 32, 0.125f, qr);
+  if (active) load_row_half(rows + (int64_t)(q0 + li) * ld + h * kD + hf * 32, boff(bqkv, h * kD + hf * 32), 0.125f, qr);
   f32x16 o0 = {}, o1 = {};
   float m = -1e30f, l = 0.f;
   const uint64_t erow = ((uint64_t)bh * S + (q0 + li)) * (uint64_t)S;
@@ -93,8 +100,8 @@ __global__ void __launch_bounds__(256, 2)
   for (int c0 = 0; c0 < S; c0 += kCH) {
     const int clen = min(kCH, S - c0);
     __syncthreads();
-    stage_rows(Ks, rows, ld, c0, clen, H + h * kD, 1.f);
-    stage_rows(Vs, rows, ld, c0, clen, 2 * H + h * kD, 1.f);
+    stage_rows(Ks, rows, ld, c0, clen, H + h * kD, boff(bqkv, H + h * kD), 1.f);
+    stage_rows(Vs, rows, ld, c0, clen, 2 * H + h * kD, boff(bqkv, 2 * H + h * kD), 1.f);
     for (int i = threadIdx.x; i < clen; i += blockDim.x)
       Ms[i] = (1.f - (float)mask[(int64_t)b * S + c0 + i]) * -10000.f;
     __syncthreads();
@@ -132,13 +139,20 @@ __global__ void __launch_bounds__(256, 2)
       o0 *= alpha;
       o1 *= alpha;
       if (p > 0.f) {
+        uint32_t bits = 0u;  // keep-bit of key (c0+t+k) at bit k, this lane's half
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           float mk[4];
           keep4(seed, off, (erow + c0 + t + 8 * g + 4 * hf) >> 2, p, dscale, mk);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) pr[4 * g + j] *= mk[j];
+          for (int j = 0; j < 4; ++j) {
+            pr[4 * g + j] *= mk[j];
+            bits |= (mk[j] != 0.f ? 1u : 0u) << (8 * g + 4 * hf + j);
+          }
         }
+        // one 32-bit word per (query, 32-key tile) for the backward kernels
+        bits |= static_cast<uint32_t>(__shfl_xor(static_cast<int>(bits), 32, 64));
+        if (dmask && hf == 0) dmask[((uint64_t)bh * S + q0 + li) * (uint64_t)(S >> 5) + ((c0 + t) >> 5)] = bits;
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -164,9 +178,10 @@ __global__ void __launch_bounds__(256, 2)
 
 template <typename T>
 __global__ void __launch_bounds__(256, 2)
-    attn_bwd_dq_kernel(const T* __restrict__ qkv, const int64_t* __restrict__ mask, const T* __restrict__ ctx,
+    attn_bwd_dq_kernel(const T* __restrict__ qkv, const int64_t* __restrict__ mask, const float* __restrict__ bqkv,
+                       const T* __restrict__ ctx,
                        const T* __restrict__ dctx, const float* __restrict__ lse, float* __restrict__ Dout,
-                       T* __restrict__ dqkv, int S, int NH, float p, uint64_t seed, uint64_t off) {
+                       T* __restrict__ dqkv, int S, int NH, float p, const uint32_t* __restrict__ dmask) {
   __shared__ __attribute__((aligned(16))) float Ks[kCH * kLD];
   __shared__ __attribute__((aligned(16))) float Vs[kCH * kLD];
   __shared__ float Ms[kCH];
@@ -183,10 +198,10 @@ __global__ void __launch_bounds__(256, 2)
   float dsum = 0.f, lq = 0.f;
   if (active) {
     const int64_t tok = (int64_t)b * S + q0 + li;
-    load_row_half(rows + (int64_t)(q0 + li) * ld + h * kD + hf * 32, 0.125f, qr);
-    load_row_half(dctx + tok * H + h * kD + hf * 32, 1.f, dor);
+    load_row_half(rows + (int64_t)(q0 + li) * ld + h * kD + hf * 32, boff(bqkv, h * kD + hf * 32), 0.125f, qr);
+    load_row_half(dctx + tok * H + h * kD + hf * 32, nullptr, 1.f, dor);
     float orow[32];
-    load_row_half(ctx + tok * H + h * kD + hf * 32, 1.f, orow);
+    load_row_half(ctx + tok * H + h * kD + hf * 32, nullptr, 1.f, orow);
 #pragma unroll
     for (int kk = 0; kk < 32; ++kk) dsum = fmaf(dor[kk], orow[kk], dsum);
     dsum += __shfl_xor(dsum, 32, 64);
@@ -194,13 +209,12 @@ __global__ void __launch_bounds__(256, 2)
     lq = lse[(int64_t)bh * S + q0 + li];
   }
   f32x16 dq0 = {}, dq1 = {};
-  const uint64_t erow = ((uint64_t)bh * S + (q0 + li)) * (uint64_t)S;
 
   for (int c0 = 0; c0 < S; c0 += kCH) {
     const int clen = min(kCH, S - c0);
     __syncthreads();
-    stage_rows(Ks, rows, ld, c0, clen, H + h * kD, 1.f);
-    stage_rows(Vs, rows, ld, c0, clen, 2 * H + h * kD, 1.f);
+    stage_rows(Ks, rows, ld, c0, clen, H + h * kD, boff(bqkv, H + h * kD), 1.f);
+    stage_rows(Vs, rows, ld, c0, clen, 2 * H + h * kD, boff(bqkv, 2 * H + h * kD), 1.f);
     for (int i = threadIdx.x; i < clen; i += blockDim.x)
       Ms[i] = (1.f - (float)mask[(int64_t)b * S + c0 + i]) * -10000.f;
     __syncthreads();
@@ -224,16 +238,12 @@ __global__ void __launch_bounds__(256, 2)
       }
       float ds[16];
       if (p > 0.f) {
+        const uint32_t word = dmask[((uint64_t)bh * S + q0 + li) * (uint64_t)(S >> 5) + ((c0 + t) >> 5)];
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          float mk[4];
-          keep4(seed, off, (erow + c0 + t + 8 * g + 4 * hf) >> 2, p, dscale, mk);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int r = 4 * g + j;
-            const float pv = __expf(s[r] + Ms[t + crow(r, hf)] - lq);
-            ds[r] = pv * (dp[r] * mk[j] - dsum);
-          }
+        for (int r = 0; r < 16; ++r) {
+          const float mk = ((word >> crow(r, hf)) & 1u) ? dscale : 0.f;
+          const float pv = __expf(s[r] + Ms[t + crow(r, hf)] - lq);
+          ds[r] = pv * (dp[r] * mk - dsum);
         }
       } else {
 #pragma unroll
@@ -264,9 +274,10 @@ __global__ void __launch_bounds__(256, 2)
 
 template <typename T>
 __global__ void __launch_bounds__(256, 2)
-    attn_bwd_dkv_kernel(const T* __restrict__ qkv, const int64_t* __restrict__ mask, const T* __restrict__ dctx,
+    attn_bwd_dkv_kernel(const T* __restrict__ qkv, const int64_t* __restrict__ mask, const float* __restrict__ bqkv,
+                        const T* __restrict__ dctx,
                         const float* __restrict__ lse, const float* __restrict__ Dd, T* __restrict__ dqkv, int S,
-                        int NH, float p, uint64_t seed, uint64_t off) {
+                        int NH, float p, const uint32_t* __restrict__ dmask) {
   __shared__ __attribute__((aligned(16))) float Qs[kCH * kLD];
   __shared__ __attribute__((aligned(16))) float Os[kCH * kLD];
   __shared__ float Ls[kCH];
@@ -285,18 +296,18 @@ __global__ void __launch_bounds__(256, 2)
   float kr[32], vr[32];
   float madd = 0.f;
   if (active) {
-    load_row_half(rows + (int64_t)key * ld + H + h * kD + hf * 32, 1.f, kr);
-    load_row_half(rows + (int64_t)key * ld + 2 * H + h * kD + hf * 32, 1.f, vr);
+    load_row_half(rows + (int64_t)key * ld + H + h * kD + hf * 32, boff(bqkv, H + h * kD + hf * 32), 1.f, kr);
+    load_row_half(rows + (int64_t)key * ld + 2 * H + h * kD + hf * 32, boff(bqkv, 2 * H + h * kD + hf * 32), 1.f,
+                  vr);
     madd = (1.f - (float)mask[(int64_t)b * S + key]) * -10000.f;
   }
   f32x16 dk0 = {}, dk1 = {}, dv0 = {}, dv1 = {};
-  const uint64_t ebase = (uint64_t)bh * S * (uint64_t)S + key;
 
   for (int c0 = 0; c0 < S; c0 += kCH) {
     const int clen = min(kCH, S - c0);
     __syncthreads();
-    stage_rows(Qs, rows, ld, c0, clen, h * kD, 0.125f);
-    stage_rows(Os, drows, H, c0, clen, h * kD, 1.f);
+    stage_rows(Qs, rows, ld, c0, clen, h * kD, boff(bqkv, h * kD), 0.125f);
+    stage_rows(Os, drows, H, c0, clen, h * kD, nullptr, 1.f);
     for (int i = threadIdx.x; i < clen; i += blockDim.x) {
       Ls[i] = lse[(int64_t)bh * S + c0 + i];
       Ds[i] = Dd[(int64_t)bh * S + c0 + i];
@@ -325,7 +336,9 @@ __global__ void __launch_bounds__(256, 2)
       for (int r = 0; r < 16; ++r) {
         const int qi = t + crow(r, hf);
         const float pv = __expf(s[r] + madd - Ls[qi]);
-        const float mk = p > 0.f ? keep_one(seed, off, ebase + (uint64_t)(c0 + qi) * S, p, dscale) : 1.f;
+        const float mk = p > 0.f ? (((dmask[((uint64_t)bh * S + c0 + qi) * (uint64_t)(S >> 5) + (key >> 5)] >>
+                                       (key & 31)) & 1u) ? dscale : 0.f)
+                                 : 1.f;
         pd[r] = pv * mk;
         ds[r] = pv * (dp[r] * mk - Ds[qi]);
       }
@@ -362,34 +375,37 @@ __global__ void __launch_bounds__(256, 2)
 
 using namespace hs;
 
-int launch_attn_fwd(int dtype, const void* qkv, const int64_t* mask, void* ctx, float* lse, int B, int S, int NH,
-                    int D, float p, uint64_t seed, uint64_t off, hipStream_t st) {
+// dmask: uint32 keep-bits [B*NH*S*(S/32)] written by the forward when p > 0
+// and read by both backward kernels (required when p > 0).
+int launch_attn_fwd(int dtype, const void* qkv, const int64_t* mask, const float* bqkv, void* ctx, float* lse,
+                    uint32_t* dmask, int B, int S, int NH, int D, float p, uint64_t seed, uint64_t off,
+                    hipStream_t st) {
   if (D != kD || S % 32 != 0 || S <= 0) return -1;
   dim3 grid((S + 127) / 128, B * NH);
   if (dtype == 0)
-    hipLaunchKernelGGL(attn_fwd_kernel<float>, grid, dim3(256), 0, st, (const float*)qkv, mask, (float*)ctx, lse, S,
-                       NH, p, seed, off);
+    hipLaunchKernelGGL(attn_fwd_kernel<float>, grid, dim3(256), 0, st, (const float*)qkv, mask, bqkv, (float*)ctx,
+                       lse, dmask, S, NH, p, seed, off);
   else
-    hipLaunchKernelGGL(attn_fwd_kernel<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)qkv, mask, (bf16_t*)ctx, lse,
-                       S, NH, p, seed, off);
+    hipLaunchKernelGGL(attn_fwd_kernel<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)qkv, mask, bqkv,
+                       (bf16_t*)ctx, lse, dmask, S, NH, p, seed, off);
   return 0;
 }
 
-int launch_attn_bwd(int dtype, const void* qkv, const int64_t* mask, const void* ctx, const void* dctx,
-                    const float* lse, float* Dbuf, void* dqkv, int B, int S, int NH, int D, float p, uint64_t seed,
-                    uint64_t off, hipStream_t st) {
-  if (D != kD || S % 32 != 0 || S <= 0) return -1;
+int launch_attn_bwd(int dtype, const void* qkv, const int64_t* mask, const float* bqkv, const void* ctx,
+                    const void* dctx, const float* lse, float* Dbuf, void* dqkv, const uint32_t* dmask, int B, int S,
+                    int NH, int D, float p, hipStream_t st) {
+  if (D != kD || S % 32 != 0 || S <= 0 || (p > 0.f && dmask == nullptr)) return -1;
   dim3 grid((S + 127) / 128, B * NH);
   if (dtype == 0) {
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<float>, grid, dim3(256), 0, st, (const float*)qkv, mask, (const float*)ctx,
-                       (const float*)dctx, lse, Dbuf, (float*)dqkv, S, NH, p, seed, off);
-    hipLaunchKernelGGL(attn_bwd_dkv_kernel<float>, grid, dim3(256), 0, st, (const float*)qkv, mask,
-                       (const float*)dctx, lse, Dbuf, (float*)dqkv, S, NH, p, seed, off);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<float>, grid, dim3(256), 0, st, (const float*)qkv, mask, bqkv,
+                       (const float*)ctx, (const float*)dctx, lse, Dbuf, (float*)dqkv, S, NH, p, dmask);
+    hipLaunchKernelGGL(attn_bwd_dkv_kernel<float>, grid, dim3(256), 0, st, (const float*)qkv, mask, bqkv,
+                       (const float*)dctx, lse, Dbuf, (float*)dqkv, S, NH, p, dmask);
   } else {
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)qkv, mask,
-                       (const bf16_t*)ctx, (const bf16_t*)dctx, lse, Dbuf, (bf16_t*)dqkv, S, NH, p, seed, off);
-    hipLaunchKernelGGL(attn_bwd_dkv_kernel<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)qkv, mask,
-                       (const bf16_t*)dctx, lse, Dbuf, (bf16_t*)dqkv, S, NH, p, seed, off);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)qkv, mask, bqkv,
+                       (const bf16_t*)ctx, (const bf16_t*)dctx, lse, Dbuf, (bf16_t*)dqkv, S, NH, p, dmask);
+    hipLaunchKernelGGL(attn_bwd_dkv_kernel<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)qkv, mask, bqkv,
+                       (const bf16_t*)dctx, lse, Dbuf, (bf16_t*)dqkv, S, NH, p, dmask);
   }
   return 0;
 }

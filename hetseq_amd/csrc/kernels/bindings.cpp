@@ -49,9 +49,10 @@ void launch_mlm_compact(const int64_t*, int, int, int, int32_t*, int64_t*, int32
 void launch_gather_rows(int, const void*, const int32_t*, void*, int, int, hipStream_t);
 void launch_scatter_add_rows(int, const void*, const int32_t*, void*, int, int, hipStream_t);
 // attention.hip
-int launch_attn_fwd(int, const void*, const int64_t*, void*, float*, int, int, int, int, float, u64, u64, hipStream_t);
-int launch_attn_bwd(int, const void*, const int64_t*, const void*, const void*, const float*, float*, void*, int, int,
-                    int, int, float, u64, u64, hipStream_t);
+int launch_attn_fwd(int, const void*, const int64_t*, const float*, void*, float*, uint32_t*, int, int, int, int, float,
+                    u64, u64, hipStream_t);
+int launch_attn_bwd(int, const void*, const int64_t*, const float*, const void*, const void*, const float*, float*,
+                    void*, const uint32_t*, int, int, int, int, float, hipStream_t);
 // xent.hip
 void launch_xent_fwd(int, const void*, const int64_t*, int, int, int64_t, int, float*, float*, float*, hipStream_t);
 void launch_xent_bwd(int, void*, const int64_t*, const float*, int, int, int64_t, int, const float*, const float*,
@@ -172,16 +173,17 @@ PYBIND11_MODULE(_hip, m) {
     check_launch("scatter_add_rows");
   });
 
-  m.def("attn_fwd", [](int dt, i64 qkv, i64 mask, i64 ctx, i64 lse, int B, int S, int NH, int D, float p, u64 seed,
-                       u64 off, i64 st) {
-    check(launch_attn_fwd(dt, P(const void*, qkv), P(const int64_t*, mask), P(void*, ctx), P(float*, lse), B, S, NH, D,
-                          p, seed, off, ST(st)),
+  m.def("attn_fwd", [](int dt, i64 qkv, i64 mask, i64 bqkv, i64 ctx, i64 lse, i64 dmask, int B, int S, int NH, int D,
+                       float p, u64 seed, u64 off, i64 st) {
+    check(launch_attn_fwd(dt, P(const void*, qkv), P(const int64_t*, mask), P(const float*, bqkv), P(void*, ctx),
+                          P(float*, lse), P(uint32_t*, dmask), B, S, NH, D, p, seed, off, ST(st)),
           "attn_fwd");
   });
-  m.def("attn_bwd", [](int dt, i64 qkv, i64 mask, i64 ctx, i64 dctx, i64 lse, i64 dbuf, i64 dqkv, int B, int S, int NH,
-                       int D, float p, u64 seed, u64 off, i64 st) {
-    check(launch_attn_bwd(dt, P(const void*, qkv), P(const int64_t*, mask), P(const void*, ctx), P(const void*, dctx),
-                          P(const float*, lse), P(float*, dbuf), P(void*, dqkv), B, S, NH, D, p, seed, off, ST(st)),
+  m.def("attn_bwd", [](int dt, i64 qkv, i64 mask, i64 bqkv, i64 ctx, i64 dctx, i64 lse, i64 dbuf, i64 dqkv, i64 dmask,
+                       int B, int S, int NH, int D, float p, i64 st) {
+    check(launch_attn_bwd(dt, P(const void*, qkv), P(const int64_t*, mask), P(const float*, bqkv),
+                          P(const void*, ctx), P(const void*, dctx), P(const float*, lse), P(float*, dbuf),
+                          P(void*, dqkv), P(const uint32_t*, dmask), B, S, NH, D, p, ST(st)),
           "attn_bwd");
   });
 

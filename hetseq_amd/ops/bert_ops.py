@@ -131,24 +131,33 @@ def colsum(x, acc=None):
     return out
 
 
-def attn_fwd(qkv, mask, B, S, NH, p, seed, off):
+def attn_fwd(qkv, mask, B, S, NH, p, seed, off, bias=None):
+    """qkv [B*S, 3H] (un-biased projection output if ``bias`` [3H] fp32 is given)."""
     T, H3 = qkv.shape
     H = H3 // 3
     assert T == B * S and H == NH * 64 and S % 32 == 0 and qkv.is_contiguous()
     assert mask.dtype == torch.int64 and mask.shape == (B, S) and mask.is_contiguous()
+    assert bias is None or (bias.shape == (H3,) and bias.dtype == torch.float32 and bias.is_contiguous())
     ctx = torch.empty((T, H), dtype=qkv.dtype, device=qkv.device)
     lse = torch.empty((B * NH * S,), dtype=torch.float32, device=qkv.device)
-    hip().attn_fwd(dtype_code(qkv), qkv.data_ptr(), mask.data_ptr(), ctx.data_ptr(), lse.data_ptr(), B, S, NH, 64,
+    # 1 keep-bit per attention probability, packed 32 keys per word, for the backward
+    dmask = torch.empty((B * NH * S * (S // 32),), dtype=torch.int32, device=qkv.device) if p > 0 else None
+    hip().attn_fwd(dtype_code(qkv), qkv.data_ptr(), mask.data_ptr(), bias.data_ptr() if bias is not None else 0,
+                   ctx.data_ptr(), lse.data_ptr(), dmask.data_ptr() if dmask is not None else 0, B, S, NH, 64,
                    float(p), seed, off, stream_handle())
-    return ctx, lse
+    return ctx, (lse, dmask)
 
 
-def attn_bwd(qkv, mask, ctx, dctx, lse, B, S, NH, p, seed, off):
+def attn_bwd(qkv, mask, ctx, dctx, lse, B, S, NH, p, seed=0, off=0, bias=None):
+    """``lse`` is the (lse, dropout-bitmask) pair returned by :func:`attn_fwd`."""
+    lse, dmask = lse
     assert dctx.is_contiguous() and dctx.shape == ctx.shape
+    assert p == 0 or dmask is not None
     dqkv = torch.empty_like(qkv)
     dbuf = torch.empty_like(lse)
-    hip().attn_bwd(dtype_code(qkv), qkv.data_ptr(), mask.data_ptr(), ctx.data_ptr(), dctx.data_ptr(), lse.data_ptr(),
-                   dbuf.data_ptr(), dqkv.data_ptr(), B, S, NH, 64, float(p), seed, off, stream_handle())
+    hip().attn_bwd(dtype_code(qkv), qkv.data_ptr(), mask.data_ptr(), bias.data_ptr() if bias is not None else 0,
+                   ctx.data_ptr(), dctx.data_ptr(), lse.data_ptr(), dbuf.data_ptr(), dqkv.data_ptr(),
+                   dmask.data_ptr() if dmask is not None else 0, B, S, NH, 64, float(p), stream_handle())
     return dqkv
 
 
@@ -157,16 +166,16 @@ class _Attention(torch.autograd.Function):
     @staticmethod
     def forward(ctx, qkv, mask, B, S, NH, p):
         seed, off = rng.fork() if p > 0 else (0, 0)
-        out, lse = attn_fwd(qkv.contiguous(), mask, B, S, NH, p, seed, off)
-        ctx.save_for_backward(qkv, mask, out, lse)
+        out, (lse, dmask) = attn_fwd(qkv.contiguous(), mask, B, S, NH, p, seed, off)
+        ctx.save_for_backward(qkv, mask, out, lse, dmask)
         ctx.cfg = (B, S, NH, p, seed, off)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        qkv, mask, out, lse = ctx.saved_tensors
+        qkv, mask, out, lse, dmask = ctx.saved_tensors
         B, S, NH, p, seed, off = ctx.cfg
-        return attn_bwd(qkv, mask, out, dout.contiguous(), lse, B, S, NH, p, seed, off), None, None, None, None, None
+        return attn_bwd(qkv, mask, out, dout.contiguous(), (lse, dmask), B, S, NH, p), None, None, None, None, None
 
 
 def attention(qkv, mask, B, S, NH, p=0.0):
@@ -285,8 +294,8 @@ class LayerWeights(object):
 def _layer_forward(x, mask, W, cfg, save):
     B, S, NH, p_h, p_a, eps, seeds = cfg
     (s_a, o_a), (s_1, o_1), (s_2, o_2) = seeds
-    qkv = G.linear_fwd(x, W.wqkv, W.bqkv.to(x.dtype) if x.dtype != torch.float32 else W.bqkv)
-    ctx_, lse = attn_fwd(qkv, mask, B, S, NH, p_a, s_a, o_a)
+    qkv = G.linear_fwd(x, W.wqkv)  # bias folded into the attention kernels' Q/K/V loads
+    ctx_, (lse, dmask) = attn_fwd(qkv, mask, B, S, NH, p_a, s_a, o_a, bias=W.bqkv)
     a = G.linear_fwd(ctx_, W.wo)
     h1, z1, m1, r1 = ln_fwd(a, W.g1, W.b1, eps, bias=W.bo, resid=x, p=p_h, mode=1, seed=s_1, off=o_1)
     f1pre = G.linear_fwd(h1, W.w1)
@@ -294,7 +303,7 @@ def _layer_forward(x, mask, W, cfg, save):
     o = G.linear_fwd(f1, W.w2)
     h2, z2, m2, r2 = ln_fwd(o, W.g2, W.bb2, eps, bias=W.b2, resid=h1, p=p_h, mode=1, seed=s_2, off=o_2)
     if save:
-        return h2, (qkv, ctx_, lse, z1, m1, r1, h1, f1pre, f1, z2, m2, r2)
+        return h2, (qkv, ctx_, lse, dmask, z1, m1, r1, h1, f1pre, f1, z2, m2, r2)
     return h2, None
 
 
@@ -326,7 +335,7 @@ class FusedBertLayer(torch.autograd.Function):
         else:
             x, mask = ctx.saved_tensors[:2]
             saved = ctx.saved_tensors[2:]
-        qkv, ctx_, lse, z1, m1, r1, h1, f1pre, f1, z2, m2, r2 = saved
+        qkv, ctx_, lse, dmask, z1, m1, r1, h1, f1pre, f1, z2, m2, r2 = saved
         B, S, NH, p_h, p_a, eps, seeds = cfg
         (s_a, o_a), (s_1, o_1), (s_2, o_2) = seeds
         dh2 = dh2.contiguous()
@@ -346,7 +355,7 @@ class FusedBertLayer(torch.autograd.Function):
                                          acc=(Gv.g1, Gv.b1, Gv.bo) if acc else None)
         dWo = G.linear_wgrad(da1, ctx_, out=Gv.wo if acc else None, accumulate=acc)
         dctx = G.linear_dgrad(da1, W.wo)
-        dqkv = attn_bwd(qkv, mask, ctx_, dctx, lse, B, S, NH, p_a, s_a, o_a)
+        dqkv = attn_bwd(qkv, mask, ctx_, dctx, (lse, dmask), B, S, NH, p_a, bias=W.bqkv)
         dWqkv = G.linear_wgrad(dqkv, x, out=Gv.wqkv if acc else None, accumulate=acc)
         dbqkv = colsum(dqkv, acc=Gv.bqkv if acc else None)
         dx = G.linear_dgrad(dqkv, W.wqkv, out=dz1, accumulate=True)  # dz1 + dqkv @ Wqkv

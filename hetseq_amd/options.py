@@ -19,6 +19,7 @@ change a reference default):
   --checkpoint-activations  recompute encoder layers in backward
   --json-log PATH           append one JSON object per logged update
   --profile                 roctx ranges + per-phase hipEvent timing
+  --no-gemm-tuning          skip the measured GEMM selection table
 """
 from __future__ import annotations
 
@@ -210,6 +211,8 @@ def add_mi355x_args(parser):
     group.add_argument("--json-log", type=str, default=None, metavar="PATH",
                        help="append one JSON object per logged update")
     group.add_argument("--profile", action="store_true", help="roctx ranges and per-phase hipEvent timing")
+    group.add_argument("--no-gemm-tuning", dest="gemm_tuning", action="store_false",
+                       help="do not load the measured hipBLASLt/rocBLAS GEMM table (configs/tunableop)")
     group.add_argument("--bmuf-block-momentum", type=float, default=0.875,
                        help="block momentum for --use-bmuf")
     group.add_argument("--bmuf-sync-interval", type=int, default=1,

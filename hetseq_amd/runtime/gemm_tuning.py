@@ -1,0 +1,57 @@
+"""Measured library-GEMM selection (hipBLASLt / rocBLAS) via PyTorch TunableOp.
+
+hipBLASLt's heuristic picks a poor tile for several BERT shapes (e.g. the
+[4096 x 768] x [768 x 2304] QKV projection ran at 91 TF/s on MT96x32x128).
+TunableOp times every hipBLASLt and rocBLAS solution for each GEMM shape once
+and keeps the fastest.  Tables measured on MI355X (gfx950, ROCm 7 /
+hipBLASLt of this image) are committed under ``configs/tunableop/`` and
+loaded at start-up; shapes missing from the table are tuned on first use
+(during warm-up) unless ``HETSEQ_GEMM_TUNING=0``.  Rows carry validators
+(PyTorch / HIP / hipBLASLt / rocBLAS versions, GPU arch), so a table from a
+different software stack is ignored rather than misapplied.
+"""
+from __future__ import annotations
+
+import os
+import tempfile
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+TABLE_DIR = os.path.join(ROOT, "configs", "tunableop")
+_done = False
+
+
+def enable(dtype_tag="fp32", tune_missing=None):
+    """Turn on TunableOp for this process and load the committed table for ``dtype_tag``."""
+    global _done
+    if _done or not torch.cuda.is_available() or os.environ.get("HETSEQ_GEMM_TUNING", "1") == "0":
+        return False
+    import torch.cuda.tunable as tn
+
+    if tune_missing is None:
+        tune_missing = os.environ.get("HETSEQ_GEMM_TUNE_MISSING", "1") == "1"
+    tn.enable(True)
+    tn.tuning_enable(bool(tune_missing))
+    if "PYTORCH_TUNABLEOP_MAX_TUNING_DURATION_MS" not in os.environ:
+        tn.set_max_tuning_duration(100)
+    # results of new tunings go to a private file (never into the repository) unless
+    # HETSEQ_TUNABLEOP_OUT names one (tools/gpu_tune.sh uses that to refresh the tables)
+    out = os.environ.get("HETSEQ_TUNABLEOP_OUT")
+    if not out:
+        out = os.path.join(tempfile.mkdtemp(prefix="hetseq_tunableop_"), "tunableop_%s.csv" % dtype_tag)
+    tn.set_filename(out, insert_device_ordinal=True)
+    for tag in ("fp32", "bf16") if dtype_tag == "bf16" else ("fp32",):
+        path = os.path.join(TABLE_DIR, "gfx950_%s.csv" % tag)
+        if os.path.exists(path):
+            tn.read_file(path)
+    _done = True
+    return True
+
+
+def flush():
+    """Write every tuned result (loaded + newly measured) to the output file now."""
+    if _done:
+        import torch.cuda.tunable as tn
+
+        tn.write_file()
