@@ -16,6 +16,15 @@ def _f(v):
     return v
 
 
+class _Folded(object):
+    """A compacted run of lazy updates: sum of val*n and sum of n (device tensors or numbers)."""
+
+    __slots__ = ("total", "count")
+
+    def __init__(self, total, count):
+        self.total, self.count = total, count
+
+
 class AverageMeter(object):
     """Computes and stores the average and current value"""
 
@@ -31,9 +40,22 @@ class AverageMeter(object):
     def update(self, val, n=1):
         if torch.is_tensor(val) or torch.is_tensor(n):
             self._pending.append((val, n))
+            if len(self._pending) >= 64:
+                self._compact()
         else:
             self._fold(val, n)
         self._last = (val, n)
+
+    def _compact(self):
+        """Fold the pending device values into one (sum, count) pair on the device (no host sync)."""
+        last = self._pending[-1]
+        tot, cnt = 0, 0
+        for v, n in self._pending[:-1]:
+            if isinstance(v, _Folded):
+                tot, cnt = tot + v.total, cnt + v.count
+            else:
+                tot, cnt = tot + v * n, cnt + n
+        self._pending = [(_Folded(tot, cnt), 1), last]
 
     def _fold(self, val, n):
         self._val = val
@@ -44,7 +66,11 @@ class AverageMeter(object):
         if self._pending:
             pend, self._pending = self._pending, []
             for v, n in pend:
-                self._fold(_f(v), _f(n))
+                if isinstance(v, _Folded):
+                    self._sum += _f(v.total)
+                    self.count += _f(v.count)
+                else:
+                    self._fold(_f(v), _f(n))
 
     @property
     def val(self):
@@ -85,10 +111,25 @@ class TimeMeter(object):
     def reset(self, init=0):
         self.init = init
         self.start = time.time()
-        self.n = 0
+        self._n = 0
+        self._dn = None  # lazily accumulated device count (no per-update host sync)
 
     def update(self, val=1):
-        self.n += _f(val)
+        if torch.is_tensor(val):
+            self._dn = val.detach().clone() if self._dn is None else self._dn.add_(val)
+        else:
+            self._n += val
+
+    @property
+    def n(self):
+        if self._dn is not None:
+            self._n += _f(self._dn)
+            self._dn = None
+        return self._n
+
+    @n.setter
+    def n(self, v):
+        self._n, self._dn = v, None
 
     @property
     def avg(self):

@@ -98,8 +98,8 @@ def ln_bwd(dy, z, mean, rstd, gamma, p=0.0, mode=0, seed=0, off=0, want_dz=True,
     return dz, da, dgamma, dbeta, dbias
 
 
-def bias_gelu_fwd(x, b):
-    y = torch.empty_like(x)
+def bias_gelu_fwd(x, b, out=None):
+    y = torch.empty_like(x) if out is None else out
     rows, N = x.shape
     assert N % 4 == 0 and x.is_contiguous()
     hip().bias_gelu_fwd(dtype_code(x), x.data_ptr(), b.data_ptr(), y.data_ptr(), rows, N, stream_handle())
@@ -298,8 +298,7 @@ def _layer_forward(x, mask, W, cfg, save):
     ctx_, (lse, dmask) = attn_fwd(qkv, mask, B, S, NH, p_a, s_a, o_a, bias=W.bqkv)
     a = G.linear_fwd(ctx_, W.wo)
     h1, z1, m1, r1 = ln_fwd(a, W.g1, W.b1, eps, bias=W.bo, resid=x, p=p_h, mode=1, seed=s_1, off=o_1)
-    f1pre = G.linear_fwd(h1, W.w1)
-    f1 = bias_gelu_fwd(f1pre, W.bi)
+    f1, f1pre = G.linear_gelu_fwd(h1, W.w1, W.bi)  # f1pre: un-biased pre-activation (for the backward)
     o = G.linear_fwd(f1, W.w2)
     h2, z2, m2, r2 = ln_fwd(o, W.g2, W.bb2, eps, bias=W.b2, resid=h1, p=p_h, mode=1, seed=s_2, off=o_2)
     if save:
@@ -347,8 +346,7 @@ class FusedBertLayer(torch.autograd.Function):
         dz2, do_, dg2, dbb2, db2 = ln_bwd(dh2, z2, m2, r2, W.g2, p_h, 1, s_2, o_2, True, True,
                                           acc=(Gv.g2, Gv.bb2, Gv.b2) if acc else None)
         dW2 = G.linear_wgrad(do_, f1, out=Gv.w2 if acc else None, accumulate=acc)
-        df1 = G.linear_dgrad(do_, W.w2)
-        df1pre, dbi = gelu_bwd_colsum(df1, f1pre, W.bi, db_acc=Gv.bi if acc else None)
+        df1pre, dbi = G.linear_dgrad_dgelu(do_, W.w2, f1pre, W.bi, db_acc=Gv.bi if acc else None)
         dW1 = G.linear_wgrad(df1pre, h1, out=Gv.w1 if acc else None, accumulate=acc)
         dh1 = G.linear_dgrad(df1pre, W.w1, out=dz2, accumulate=True)  # dz2 + df1pre @ W1
         dz1, da1, dg1, db1, dbo = ln_bwd(dh1, z1, m1, r1, W.g1, p_h, 1, s_1, o_1, True, True,

@@ -1,17 +1,23 @@
 """GEMM dispatch for the BERT hot path.
 
 ``linear_fwd`` / ``linear_dgrad`` / ``linear_wgrad`` are the three products
-of a Linear layer.  Two engines:
+of a Linear layer; ``linear_gelu_fwd`` and ``linear_dgrad_dgelu`` are the FFN
+products with the GELU (and its backward + bias gradient) fused into the GEMM
+epilogue.  Two engines:
 
 * ``hip``  -- the hand-written gfx950 MFMA kernel (csrc/kernels/gemm.hip) with
-             fused epilogues (bias, bias+GELU, beta-accumulate); fp32 today.
-* ``blas`` -- hipBLASLt through ``torch.addmm`` (plain library GEMM).
+             fused epilogues (bias, bias+GELU, dGELU+bias-grad, beta-accumulate);
+             fp32 shapes that tile exactly.
+* ``blas`` -- hipBLASLt / rocBLAS through ``torch.mm`` (plain library GEMM; the
+             per-shape solution comes from the measured TunableOp table, see
+             runtime/gemm_tuning.py), followed by the separate HIP epilogue kernels.
 
-``HETSEQ_GEMM=hip|blas|auto`` selects; ``auto`` (default) times both engines
-once per (shape, transpose, dtype) on the GPU and keeps the faster one --
-the choice is recorded in ``GEMM_CHOICES`` and logged by the benchmark.
-In bf16 mode the weight-gradient GEMM writes fp32 directly (``out_dtype``),
-so master gradients never round through bf16.
+``HETSEQ_GEMM=hip|blas|auto`` selects; ``auto`` (default) times both paths --
+including the epilogue work the fused kernel absorbs -- once per (shape,
+transpose, epilogue) on the GPU and keeps the faster one.  The choice is
+recorded in ``GEMM_CHOICES`` and logged by the benchmark.  In bf16 mode the
+weight-gradient GEMM writes fp32 directly (``out_dtype``), so master gradients
+never round through bf16.
 """
 from __future__ import annotations
 
@@ -24,6 +30,8 @@ from hetseq_amd.ops._C import hip, stream_handle
 GEMM_CHOICES: dict = {}
 _MODE = os.environ.get("HETSEQ_GEMM", "auto")
 
+EPI_NONE, EPI_BIAS, EPI_GELU, EPI_DGELU = 0, 1, 2, 3
+
 
 def set_mode(mode):
     global _MODE
@@ -32,25 +40,41 @@ def set_mode(mode):
     GEMM_CHOICES.clear()
 
 
-def _hip_gemm(a, b, ta, tb, out, bias=None, epi=0, beta=0.0):
+def _dims(a, b, ta, tb):
     M = a.shape[1] if ta else a.shape[0]
     K = a.shape[0] if ta else a.shape[1]
     N = b.shape[0] if tb else b.shape[1]
-    assert out.shape == (M, N) and out.is_contiguous() and a.stride(1) == 1 and b.stride(1) == 1
-    hip().gemm(0, int(ta), int(tb), M, N, K, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), out.data_ptr(),
-               out.stride(0), bias.data_ptr() if bias is not None else 0, epi, float(beta), stream_handle())
-    return out
+    return M, N, K
 
 
-def _blas_gemm(a, b, ta, tb, out, bias=None, epi=0, beta=0.0, out_dtype=None):
+def _hip_ok(a, b, out, *extra):
+    ts = (a, b, out) + tuple(t for t in extra if t is not None)
+    return all(t.is_cuda and t.dtype == torch.float32 for t in ts) and a.stride(1) == 1 and b.stride(1) == 1 \
+        and out.stride(1) == 1
+
+
+def _hip_gemm(a, b, ta, tb, out, bias=None, epi=EPI_NONE, beta=0.0, aux=None, part=None, colsum=None,
+              colsum_acc=False):
+    """Launch the HIP kernel; returns False (nothing launched) if the shape is not served."""
+    M, N, K = _dims(a, b, ta, tb)
+    assert out.shape == (M, N)
+    rc = hip().gemm(0, int(ta), int(tb), M, N, K, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0),
+                    out.data_ptr(), out.stride(0), bias.data_ptr() if bias is not None else 0, epi, float(beta),
+                    aux.data_ptr() if aux is not None else 0, aux.stride(0) if aux is not None else 0,
+                    part.data_ptr() if part is not None else 0, colsum.data_ptr() if colsum is not None else 0,
+                    int(colsum_acc), stream_handle())
+    return rc == 0
+
+
+def _blas_gemm(a, b, ta, tb, out, bias=None, epi=EPI_NONE, beta=0.0, out_dtype=None):
     A = a.t() if ta else a
     B = b.t() if tb else b
     if out_dtype is not None and out_dtype != A.dtype:
+        # library GEMM with bf16 inputs and an fp32 C/D (beta=1 accumulates in place)
         if beta != 0.0:
-            out.add_(torch.mm(A, B, out_dtype=out_dtype))
+            torch.ops.aten.addmm.dtype_out(out, A, B, out_dtype, beta=beta, out=out)
         else:
-            res = torch.mm(A, B, out_dtype=out_dtype)
-            out.copy_(res)
+            torch.ops.aten.mm.dtype_out(A, B, out_dtype, out=out)
         if bias is not None and epi >= 1:
             out.add_(bias)
         return out
@@ -76,45 +100,50 @@ def _bench(fn, iters=5):
     return s.elapsed_time(e) / iters
 
 
-def _choose(key, a, b, ta, tb, out, bias, epi, beta):
+def _choose(key, run_hip, run_blas):
+    """'hip' or 'blas' for this call site; auto mode measures both once (side effects go to scratch)."""
     if _MODE != "auto":
         return _MODE
     c = GEMM_CHOICES.get(key)
-    if c is None:
-        if torch.cuda.is_current_stream_capturing():
-            return "blas"
-        scratch = torch.empty_like(out)
-        if beta != 0.0:
-            scratch.copy_(out)
-        t_hip = _bench(lambda: _hip_gemm(a, b, ta, tb, scratch, bias, epi, beta))
-        t_blas = _bench(lambda: _blas_gemm(a, b, ta, tb, scratch, bias, epi, beta))
-        c = "hip" if t_hip < t_blas else "blas"
-        GEMM_CHOICES[key] = (c, round(t_hip, 4), round(t_blas, 4))
-        return c
-    return c[0]
+    if c is not None:
+        return c[0]
+    if torch.cuda.is_current_stream_capturing():
+        return "blas"
+    t_hip = _bench(run_hip)
+    t_blas = _bench(run_blas)
+    c = "hip" if t_hip < t_blas else "blas"
+    GEMM_CHOICES[key] = (c, round(t_hip, 4), round(t_blas, 4))
+    return c
 
 
-def gemm(a, b, ta=False, tb=False, out=None, bias=None, epi=0, beta=0.0, out_dtype=None):
-    """out = beta*out + op(a) @ op(b) (+bias) (gelu if epi == 2, hip engine only)."""
-    M = a.shape[1] if ta else a.shape[0]
-    N = b.shape[0] if tb else b.shape[1]
+def gemm(a, b, ta=False, tb=False, out=None, bias=None, epi=EPI_NONE, beta=0.0, out_dtype=None):
+    """out = beta*out + op(a) @ op(b) (+bias)."""
+    M, N, K = _dims(a, b, ta, tb)
     odt = out_dtype or a.dtype
     if out is None:
         out = torch.empty((M, N), dtype=odt, device=a.device)
-    hip_ok = (a.is_cuda and a.dtype == torch.float32 and b.dtype == torch.float32 and out.dtype == torch.float32
-              and a.stride(1) == 1 and b.stride(1) == 1 and out.is_contiguous())
-    if epi == 2 and not hip_ok:
-        raise RuntimeError("fused GELU epilogue needs the fp32 HIP GEMM")
-    if a.is_cuda and hip_ok:
-        key = (M, N, a.shape[0] if ta else a.shape[1], ta, tb, epi, beta != 0.0)
-        if epi == 2 or _choose(key, a, b, ta, tb, out, bias, epi, beta) == "hip":
-            return _hip_gemm(a, b, ta, tb, out, bias, epi, beta)
+    if a.is_cuda and _MODE != "blas" and _hip_ok(a, b, out, bias):
+        key = (M, N, K, ta, tb, epi, beta != 0.0)
+        scratch = None
+
+        def run_hip():
+            return _hip_gemm(a, b, ta, tb, scratch, bias, epi, beta)
+
+        def run_blas():
+            _blas_gemm(a, b, ta, tb, scratch, bias, epi, beta, out_dtype)
+
+        if key not in GEMM_CHOICES and _MODE == "auto":
+            scratch = out.clone() if beta != 0.0 else torch.empty_like(out)
+            if not run_hip():
+                GEMM_CHOICES[key] = ("blas", None, None)
+        if _choose(key, run_hip, run_blas) == "hip" and _hip_gemm(a, b, ta, tb, out, bias, epi, beta):
+            return out
     return _blas_gemm(a, b, ta, tb, out, bias, epi, beta, out_dtype)
 
 
 def linear_fwd(x, w, bias=None, out=None):
     """x[T,K] @ w[N,K]^T (+bias)."""
-    return gemm(x, w, ta=False, tb=True, out=out, bias=bias, epi=1 if bias is not None else 0)
+    return gemm(x, w, ta=False, tb=True, out=out, bias=bias, epi=EPI_BIAS if bias is not None else EPI_NONE)
 
 
 def linear_dgrad(dy, w, out=None, accumulate=False):
@@ -125,3 +154,65 @@ def linear_dgrad(dy, w, out=None, accumulate=False):
 def linear_wgrad(dy, x, out=None, accumulate=False):
     """dy[T,N]^T @ x[T,K] -> [N,K] in fp32; accumulate=True adds into ``out`` (flat grad view)."""
     return gemm(dy, x, ta=True, tb=False, out=out, out_dtype=torch.float32, beta=1.0 if accumulate else 0.0)
+
+
+def linear_gelu_fwd(x, w, b):
+    """FFN-in forward: pre = x @ w^T (un-biased, kept for the backward), y = gelu(pre + b).
+
+    Returns (y, pre).  One fused HIP GEMM (epilogue writes both) or library GEMM + bias_gelu kernel.
+    """
+    from hetseq_amd.ops import bert_ops
+
+    T, N = x.shape[0], w.shape[0]
+    pre = torch.empty((T, N), dtype=x.dtype, device=x.device)
+    y = torch.empty_like(pre)
+    if x.is_cuda and _MODE != "blas" and _hip_ok(x, w, y, b, pre):
+        key = (T, N, x.shape[1], "gelu_fwd")
+
+        def run_hip():
+            return _hip_gemm(x, w, False, True, y, b, EPI_GELU, 0.0, aux=pre)
+
+        def run_blas():
+            torch.mm(x, w.t(), out=pre)
+            bert_ops.bias_gelu_fwd(pre, b, out=y)
+
+        if key not in GEMM_CHOICES and _MODE == "auto" and not run_hip():
+            GEMM_CHOICES[key] = ("blas", None, None)
+        if _choose(key, run_hip, run_blas) == "hip" and run_hip():
+            return y, pre
+    torch.mm(x, w.t(), out=pre)
+    return bert_ops.bias_gelu_fwd(pre, b, out=y), pre
+
+
+def linear_dgrad_dgelu(dy, w, pre, b, db_acc=None):
+    """FFN backward through the GELU: dpre = (dy @ w) * gelu'(pre + b), db = colsum(dpre).
+
+    ``db`` is accumulated into ``db_acc`` (flat-store view) when given.  Returns (dpre, db).
+    """
+    from hetseq_amd.ops import bert_ops
+
+    T, N = dy.shape[0], w.shape[1]
+    dpre = torch.empty((T, N), dtype=dy.dtype, device=dy.device)
+    db = db_acc if db_acc is not None else torch.empty(N, dtype=torch.float32, device=dy.device)
+    if dy.is_cuda and _MODE != "blas" and _hip_ok(dy, w, dpre, pre, b):
+        key = (T, N, dy.shape[1], "dgelu")
+        part = torch.empty(((T + 63) // 64, N), dtype=torch.float32, device=dy.device)
+
+        def run_hip(out_db, acc):
+            return _hip_gemm(dy, w, False, False, dpre, b, EPI_DGELU, 0.0, aux=pre, part=part, colsum=out_db,
+                             colsum_acc=acc)
+
+        if key not in GEMM_CHOICES and _MODE == "auto":
+            scratch_db = torch.zeros_like(db)
+
+            def run_blas():
+                bert_ops.gelu_bwd_colsum(torch.mm(dy, w), pre, b, db_acc=scratch_db)
+
+            if not run_hip(scratch_db, True):
+                GEMM_CHOICES[key] = ("blas", None, None)
+            else:
+                _choose(key, lambda: run_hip(scratch_db, True), run_blas)
+        if _choose(key, None, None) == "hip" and run_hip(db, db_acc is not None):
+            return dpre, db
+    df = torch.mm(dy, w)
+    return bert_ops.gelu_bwd_colsum(df, pre, b, db_acc=db_acc)

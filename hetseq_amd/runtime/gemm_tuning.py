@@ -49,9 +49,10 @@ def enable(dtype_tag="fp32", tune_missing=None):
     return True
 
 
-def flush():
-    """Write every tuned result (loaded + newly measured) to the output file now."""
-    if _done:
-        import torch.cuda.tunable as tn
+def results():
+    """The (op, shape, solution, ms) rows TunableOp holds for this process."""
+    if not _done:
+        return []
+    import torch.cuda.tunable as tn
 
-        tn.write_file()
+    return list(tn.get_results())
