@@ -54,7 +54,7 @@ def _hip_ok(a, b, out, *extra):
 
 
 def _hip_gemm(a, b, ta, tb, out, bias=None, epi=EPI_NONE, beta=0.0, aux=None, part=None, colsum=None,
-              colsum_acc=False):
+              colsum_acc=False, tile=-1):
     """Launch the HIP kernel; returns False (nothing launched) if the shape is not served."""
     M, N, K = _dims(a, b, ta, tb)
     assert out.shape == (M, N)
@@ -62,7 +62,7 @@ def _hip_gemm(a, b, ta, tb, out, bias=None, epi=EPI_NONE, beta=0.0, aux=None, pa
                     out.data_ptr(), out.stride(0), bias.data_ptr() if bias is not None else 0, epi, float(beta),
                     aux.data_ptr() if aux is not None else 0, aux.stride(0) if aux is not None else 0,
                     part.data_ptr() if part is not None else 0, colsum.data_ptr() if colsum is not None else 0,
-                    int(colsum_acc), stream_handle())
+                    int(colsum_acc), stream_handle(), tile)
     return rc == 0
 
 
