@@ -41,6 +41,8 @@ def parse():
     p.add_argument("--no-fused", action="store_true")
     p.add_argument("--gemm", default=None, choices=[None, "hip", "blas", "auto"])
     p.add_argument("--profile-phases", action="store_true")
+    p.add_argument("--sync-debug", action="store_true", help="warn (with stack) on every host<->device sync in the timed loop")
+    p.add_argument("--host-profile", default=None, help="cProfile the timed loop into this file")
     return p.parse_args()
 
 
@@ -116,9 +118,29 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    if b.sync_debug:
+        torch.cuda.set_sync_debug_mode("warn")
+    prof = None
+    if b.host_profile:
+        import cProfile
+
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
+    host = 0.0  # host time spent inside train_step (enqueue cost; < ms_per_step means GPU-bound)
+    data_wait = 0.0  # host time blocked on the input pipeline
     for _ in range(b.steps):
-        ctl.train_step(next(gen))
+        d0 = time.perf_counter()
+        batch = next(gen)
+        h0 = time.perf_counter()
+        data_wait += h0 - d0
+        ctl.train_step(batch)
+        host += time.perf_counter() - h0
+    if b.sync_debug:
+        torch.cuda.set_sync_debug_mode(0)
+    if prof is not None:
+        prof.disable()
+        prof.dump_stats(b.host_profile)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -132,10 +154,6 @@ def main():
     from hetseq_amd.ops import bert_ops
 
     bert_ops.check_device_errors()
-    if os.environ.get("HETSEQ_TUNABLEOP_OUT"):
-        from hetseq_amd.runtime import gemm_tuning
-
-        gemm_tuning.flush()
     sec = elapsed / b.steps
     seqs = b.batch * b.update_freq * world
     if rank == 0:
@@ -160,6 +178,8 @@ def main():
                        "update_freq": b.update_freq, "parallelism": "dp%d" % world,
                        "fused_kernels": not b.no_fused, "bucket_cap_mb": b.bucket_cap_mb},
             "final_train_loss_logged": round(loss, 5),
+            "host_ms_per_step": round(host / b.steps * 1000, 3),
+            "data_wait_ms_per_step": round(data_wait / b.steps * 1000, 3),
             "gemm_choices": {str(k): v for k, v in list(G.GEMM_CHOICES.items())[:32]},
         }
         print(json.dumps(out), flush=True)

@@ -186,7 +186,8 @@ class Controller(object):
         if self._dummy_batch is None:
             self._dummy_batch = next((s for s in samples if s is not None and len(s) > 0), None)
         self._set_seed()
-        self.model.train()
+        if not self._model.training:
+            self.model.train()  # (a recursive walk over every module: only when the mode changes)
         self.zero_grad()
         if not dummy_batch:
             self.meters["train_wall"].start()

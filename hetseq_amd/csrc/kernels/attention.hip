@@ -25,6 +25,9 @@
 //    128 rows with a 68-float row stride (16-B reads conflict-free).
 // Backward = two kernels, no atomics: dQ (also emits D = rowsum(dO*O)), then
 // dK/dV.  Supports S % 32 == 0, S <= 512 chunked, head dim 64.
+#include <cstdlib>
+#include <string>
+
 #include "common.h"
 
 namespace hs {
@@ -57,18 +60,57 @@ HS_DEVICE void load_row_half(const T* src, const float* bias, float scale, float
   }
 }
 
-// Stage rows [r0, r0+n) of a head slice (column offset col) into LDS (fp32),
-// adding the (nullable) per-column bias `bias` (already offset to `col`).
-template <typename T>
+// Stage rows [r0, r0+n) (n <= 128) of a head slice (column offset col) into LDS
+// (fp32), adding the (nullable) per-column bias `bias` (already offset to `col`).
+// All of a thread's global loads are issued before any LDS store (one memory
+// round trip per staging instead of one per row group).  NT = block size.
+template <int NT, typename T>
 HS_DEVICE void stage_rows(float* lds, const T* base, int64_t ld, int r0, int n, int col, const float* bias,
                           float scale) {
-  for (int i = threadIdx.x; i < n * 16; i += blockDim.x) {
-    const int r = i >> 4, c4 = (i & 15) * 4;
-    float v[4], b[4] = {0.f, 0.f, 0.f, 0.f};
-    load4(base + (int64_t)(r0 + r) * ld + col + c4, v);
-    if (bias) load4(bias + c4, b);
-    *reinterpret_cast<float4*>(lds + r * kLD + c4) =
-        make_float4((v[0] + b[0]) * scale, (v[1] + b[1]) * scale, (v[2] + b[2]) * scale, (v[3] + b[3]) * scale);
+  constexpr int kPer = 128 * 16 / NT;  // float4 units per thread for a full 128-row chunk
+  const int c4 = (threadIdx.x & 15) * 4;  // NT % 16 == 0: a thread always owns the same 4 columns
+  float b[4] = {0.f, 0.f, 0.f, 0.f};
+  if (bias) load4(bias + c4, b);
+  float v[kPer][4];
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {  // unconditional loads (row clamped): keeps v[] in registers
+    const int r = min((threadIdx.x + i * NT) >> 4, n - 1);
+    load4(base + (int64_t)(r0 + r) * ld + col + c4, v[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    const int r = (threadIdx.x + i * NT) >> 4;
+    if (r < n)
+      *reinterpret_cast<float4*>(lds + r * kLD + c4) = make_float4((v[i][0] + b[0]) * scale, (v[i][1] + b[1]) * scale,
+                                                                   (v[i][2] + b[2]) * scale, (v[i][3] + b[3]) * scale);
+  }
+}
+
+// Two stagings with all loads of both in flight before the first LDS store.
+template <int NT, typename T1, typename T2>
+HS_DEVICE void stage_rows2(float* l1, const T1* b1, int64_t ld1, int col1, const float* bias1, float sc1, float* l2,
+                           const T2* b2, int64_t ld2, int col2, const float* bias2, float sc2, int r0, int n) {
+  constexpr int kPer = 128 * 16 / NT;
+  const int c4 = (threadIdx.x & 15) * 4;
+  float ba[4] = {0.f, 0.f, 0.f, 0.f}, bb[4] = {0.f, 0.f, 0.f, 0.f};
+  if (bias1) load4(bias1 + c4, ba);
+  if (bias2) load4(bias2 + c4, bb);
+  float v1[kPer][4], v2[kPer][4];
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {  // unconditional loads (row clamped): keeps v1/v2 in registers
+    const int r = min((threadIdx.x + i * NT) >> 4, n - 1);
+    load4(b1 + (int64_t)(r0 + r) * ld1 + col1 + c4, v1[i]);
+    load4(b2 + (int64_t)(r0 + r) * ld2 + col2 + c4, v2[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    const int r = (threadIdx.x + i * NT) >> 4;
+    if (r < n) {
+      *reinterpret_cast<float4*>(l1 + r * kLD + c4) = make_float4((v1[i][0] + ba[0]) * sc1, (v1[i][1] + ba[1]) * sc1,
+                                                                  (v1[i][2] + ba[2]) * sc1, (v1[i][3] + ba[3]) * sc1);
+      *reinterpret_cast<float4*>(l2 + r * kLD + c4) = make_float4((v2[i][0] + bb[0]) * sc2, (v2[i][1] + bb[1]) * sc2,
+                                                                  (v2[i][2] + bb[2]) * sc2, (v2[i][3] + bb[3]) * sc2);
+    }
   }
 }
 
@@ -89,7 +131,8 @@ __global__ void __launch_bounds__(256, 2)
   const int q0 = blockIdx.x * 128 + w * 32;
   const bool active = q0 < S;
   const T* rows = qkv + (int64_t)b * S * ld;
-  const float dscale = p < 1.f ? 1.f / (1.f - p) : 0.f;
+  const uint32_t thr = drop_thr16(p);
+  const float dscale = drop_scale16(thr);
 
   float qr[32];
   if (active) load_row_half(rows + (int64_t)(q0 + li) * ld + h * kD + hf * 32, boff(bqkv, h * kD + hf * 32), 0.125f, qr);
@@ -100,8 +143,8 @@ __global__ void __launch_bounds__(256, 2)
   for (int c0 = 0; c0 < S; c0 += kCH) {
     const int clen = min(kCH, S - c0);
     __syncthreads();
-    stage_rows(Ks, rows, ld, c0, clen, H + h * kD, boff(bqkv, H + h * kD), 1.f);
-    stage_rows(Vs, rows, ld, c0, clen, 2 * H + h * kD, boff(bqkv, 2 * H + h * kD), 1.f);
+    stage_rows2<256>(Ks, rows, ld, H + h * kD, boff(bqkv, H + h * kD), 1.f, Vs, rows, ld, 2 * H + h * kD,
+                     boff(bqkv, 2 * H + h * kD), 1.f, c0, clen);
     for (int i = threadIdx.x; i < clen; i += blockDim.x)
       Ms[i] = (1.f - (float)mask[(int64_t)b * S + c0 + i]) * -10000.f;
     __syncthreads();
@@ -139,19 +182,14 @@ __global__ void __launch_bounds__(256, 2)
       o0 *= alpha;
       o1 *= alpha;
       if (p > 0.f) {
-        uint32_t bits = 0u;  // keep-bit of key (c0+t+k) at bit k, this lane's half
+        // keep bits of the 32-key tile: this lane half draws key groups 2hf and 2hf+1 (8 keys
+        // per Philox call, 16-bit uniforms) and swaps them with the partner lane (l ^ 32)
+        const uint64_t e0 = (erow + c0 + t) >> 3;  // group index of key 0 of the tile
+        const uint32_t mine = keep8_bits(seed, off, e0 + 2 * hf, thr) | (keep8_bits(seed, off, e0 + 2 * hf + 1, thr) << 8);
+        const uint32_t other = static_cast<uint32_t>(__shfl_xor(static_cast<int>(mine), 32, 64));
+        const uint32_t bits = hf == 0 ? (mine | (other << 16)) : (other | (mine << 16));  // bit k: key t+k
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          float mk[4];
-          keep4(seed, off, (erow + c0 + t + 8 * g + 4 * hf) >> 2, p, dscale, mk);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            pr[4 * g + j] *= mk[j];
-            bits |= (mk[j] != 0.f ? 1u : 0u) << (8 * g + 4 * hf + j);
-          }
-        }
-        // one 32-bit word per (query, 32-key tile) for the backward kernels
-        bits |= static_cast<uint32_t>(__shfl_xor(static_cast<int>(bits), 32, 64));
+        for (int r = 0; r < 16; ++r) pr[r] = ((bits >> crow(r, hf)) & 1u) ? pr[r] * dscale : 0.f;
         if (dmask && hf == 0) dmask[((uint64_t)bh * S + q0 + li) * (uint64_t)(S >> 5) + ((c0 + t) >> 5)] = bits;
       }
 #pragma unroll
@@ -192,7 +230,7 @@ __global__ void __launch_bounds__(256, 2)
   const int q0 = blockIdx.x * 128 + w * 32;
   const bool active = q0 < S;
   const T* rows = qkv + (int64_t)b * S * ld;
-  const float dscale = p < 1.f ? 1.f / (1.f - p) : 0.f;
+  const float dscale = drop_scale16(drop_thr16(p));
 
   float qr[32], dor[32];
   float dsum = 0.f, lq = 0.f;
@@ -213,8 +251,8 @@ __global__ void __launch_bounds__(256, 2)
   for (int c0 = 0; c0 < S; c0 += kCH) {
     const int clen = min(kCH, S - c0);
     __syncthreads();
-    stage_rows(Ks, rows, ld, c0, clen, H + h * kD, boff(bqkv, H + h * kD), 1.f);
-    stage_rows(Vs, rows, ld, c0, clen, 2 * H + h * kD, boff(bqkv, 2 * H + h * kD), 1.f);
+    stage_rows2<256>(Ks, rows, ld, H + h * kD, boff(bqkv, H + h * kD), 1.f, Vs, rows, ld, 2 * H + h * kD,
+                     boff(bqkv, 2 * H + h * kD), 1.f, c0, clen);
     for (int i = threadIdx.x; i < clen; i += blockDim.x)
       Ms[i] = (1.f - (float)mask[(int64_t)b * S + c0 + i]) * -10000.f;
     __syncthreads();
@@ -282,6 +320,7 @@ __global__ void __launch_bounds__(256, 2)
   __shared__ __attribute__((aligned(16))) float Os[kCH * kLD];
   __shared__ float Ls[kCH];
   __shared__ float Ds[kCH];
+  __shared__ uint32_t Wd[kCH][4];  // keep-bit words of the chunk's queries for this block's 4 key words
   const int H = NH * kD;
   const int64_t ld = 3 * (int64_t)H;
   const int bh = blockIdx.y, b = bh / NH, h = bh % NH;
@@ -291,7 +330,7 @@ __global__ void __launch_bounds__(256, 2)
   const int key = k0 + li;
   const T* rows = qkv + (int64_t)b * S * ld;
   const T* drows = dctx + (int64_t)b * S * H;
-  const float dscale = p < 1.f ? 1.f / (1.f - p) : 0.f;
+  const float dscale = drop_scale16(drop_thr16(p));
 
   float kr[32], vr[32];
   float madd = 0.f;
@@ -306,12 +345,16 @@ __global__ void __launch_bounds__(256, 2)
   for (int c0 = 0; c0 < S; c0 += kCH) {
     const int clen = min(kCH, S - c0);
     __syncthreads();
-    stage_rows(Qs, rows, ld, c0, clen, h * kD, boff(bqkv, h * kD), 0.125f);
-    stage_rows(Os, drows, H, c0, clen, h * kD, nullptr, 1.f);
+    stage_rows2<256>(Qs, rows, ld, h * kD, boff(bqkv, h * kD), 0.125f, Os, drows, H, h * kD, nullptr, 1.f, c0, clen);
     for (int i = threadIdx.x; i < clen; i += blockDim.x) {
       Ls[i] = lse[(int64_t)bh * S + c0 + i];
       Ds[i] = Dd[(int64_t)bh * S + c0 + i];
     }
+    if (p > 0.f)
+      for (int i = threadIdx.x; i < clen * 4; i += blockDim.x) {
+        const int qi = i >> 2, kw = blockIdx.x * 4 + (i & 3);
+        Wd[qi][i & 3] = kw < (S >> 5) ? dmask[((uint64_t)bh * S + c0 + qi) * (uint64_t)(S >> 5) + kw] : 0u;
+      }
     __syncthreads();
     if (!active) continue;
     for (int t = 0; t < clen; t += 32) {
@@ -336,9 +379,7 @@ __global__ void __launch_bounds__(256, 2)
       for (int r = 0; r < 16; ++r) {
         const int qi = t + crow(r, hf);
         const float pv = __expf(s[r] + madd - Ls[qi]);
-        const float mk = p > 0.f ? (((dmask[((uint64_t)bh * S + c0 + qi) * (uint64_t)(S >> 5) + (key >> 5)] >>
-                                       (key & 31)) & 1u) ? dscale : 0.f)
-                                 : 1.f;
+        const float mk = p > 0.f ? (((Wd[qi][w] >> li) & 1u) ? dscale : 0.f) : 1.f;
         pd[r] = pv * mk;
         ds[r] = pv * (dp[r] * mk - Ds[qi]);
       }
@@ -371,9 +412,213 @@ __global__ void __launch_bounds__(256, 2)
   }
 }
 
+// Fused backward for S <= 128: one block per (batch, head) owns every query and
+// every key, so the seven products of the two-kernel path become five.  8 waves
+// (2 per SIMD):
+//   phase 1, wave (kg = w&3, qh = w>>2): keys 32kg..32kg+31, query tiles {64qh, 64qh+32}:
+//     S^T = K Q^T, dP^T = V dO^T, dS^T = P^T o (dP^T - D); dV += P^T dO, dK += dS^T Q
+//     (partials over the two query halves), dS written to LDS ([query][key], 132-float rows);
+//   phase 2, wave (qt = w&3, kh = w>>2): dQ[queries 32qt..] partial over keys 64kh..64kh+63,
+//     dQ = dS K with K re-staged from registers into LDS (72-float rows);
+//   combine: waves 4..7 hand their dK/dV and dQ partials to waves 0..3 through the
+//     freed LDS (fixed order: deterministic), which write the results.
+// No recompute of S and dP, no atomics.  D = rowsum(dO o O) in the prologue.
+// LDS 142 KB -> 1 block (8 waves) per CU.
+constexpr int kLDS = 132;  // dS row stride (floats): conflict-free b128 reads in phase 2
+constexpr int kLDK = 72;   // K row stride in phase 2
+
+template <typename T>
+__global__ void __launch_bounds__(512, 1)
+    attn_bwd_fused_kernel(const T* __restrict__ qkv, const int64_t* __restrict__ mask, const float* __restrict__ bqkv,
+                          const T* __restrict__ ctx, const T* __restrict__ dctx, const float* __restrict__ lse,
+                          T* __restrict__ dqkv, int S, int NH, float p, const uint32_t* __restrict__ dmask) {
+  __shared__ __attribute__((aligned(16))) float QKs[128 * kLDK];  // Q (stride kLD) in phase 1, K (kLDK) in phase 2
+  __shared__ __attribute__((aligned(16))) float Os[128 * kLD];    // dO; then dQ partials
+  __shared__ __attribute__((aligned(16))) float dSs[128 * kLDS];  // dS; then dK/dV partials
+  __shared__ float Ls[128];
+  __shared__ float Ds[128];
+  __shared__ uint32_t Wd[128][4];
+  const int H = NH * kD;
+  const int64_t ld = 3 * (int64_t)H;
+  const int bh = blockIdx.x, b = bh / NH, h = bh % NH;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hf = lane >> 5, li = lane & 31;
+  const int g4 = w & 3, half = w >> 2;  // phase 1: key group / query half; phase 2: query tile / key half
+  const bool kactive = 32 * g4 < S;
+  const int key = 32 * g4 + li;
+  const T* rows = qkv + (int64_t)b * S * ld;
+  const T* drows = dctx + (int64_t)b * S * H;
+  const float dscale = drop_scale16(drop_thr16(p));
+
+  // ---- prologue: stage Q (biased, scaled), dO, lse, keep words; D = rowsum(dO o O)
+  stage_rows2<512>(QKs, rows, ld, h * kD, boff(bqkv, h * kD), 0.125f, Os, drows, H, h * kD, nullptr, 1.f, 0, S);
+  for (int i = threadIdx.x; i < S; i += blockDim.x) Ls[i] = lse[(int64_t)bh * S + i];
+  if (p > 0.f)
+    for (int i = threadIdx.x; i < S * (S >> 5); i += blockDim.x)
+      Wd[i / (S >> 5)][i % (S >> 5)] = dmask[((uint64_t)bh * S) * (uint64_t)(S >> 5) + i];
+  float kr[32], vr[32];
+  float madd = 0.f;
+  if (kactive) {
+    load_row_half(rows + (int64_t)key * ld + H + h * kD + hf * 32, boff(bqkv, H + h * kD + hf * 32), 1.f, kr);
+    load_row_half(rows + (int64_t)key * ld + 2 * H + h * kD + hf * 32, boff(bqkv, 2 * H + h * kD + hf * 32), 1.f,
+                  vr);
+    madd = (1.f - (float)mask[(int64_t)b * S + key]) * -10000.f;
+  }
+  __syncthreads();  // Os staged
+  {
+    const int r = threadIdx.x >> 2, qtr = threadIdx.x & 3;  // 4 threads per query row
+    float dsum = 0.f;
+    if (r < S) {
+      const T* orow = ctx + ((int64_t)b * S + r) * H + h * kD + qtr * 16;
+      const float* dor = Os + r * kLD + qtr * 16;
+#pragma unroll
+      for (int kk = 0; kk < 16; kk += 4) {
+        float o[4];
+        load4(orow + kk, o);
+        dsum = fmaf(dor[kk], o[0], fmaf(dor[kk + 1], o[1], fmaf(dor[kk + 2], o[2], fmaf(dor[kk + 3], o[3], dsum))));
+      }
+    }
+    dsum += __shfl_xor(dsum, 1, 64);
+    dsum += __shfl_xor(dsum, 2, 64);
+    if (r < S && qtr == 0) Ds[r] = dsum;
+  }
+  __syncthreads();
+
+  // ---- phase 1: dK, dV partials for this wave's keys over its query half; dS tiles to LDS
+  f32x16 dk0 = {}, dk1 = {}, dv0 = {}, dv1 = {};
+  if (kactive) {
+    for (int t = 64 * half; t < min(S, 64 * half + 64); t += 32) {
+      f32x16 s = {}, dp = {};
+      const float* qp = QKs + (t + li) * kLD + hf * 32;
+      const float* op = Os + (t + li) * kLD + hf * 32;
+#pragma unroll
+      for (int kk = 0; kk < 32; kk += 4) {
+        const float4 q4 = *reinterpret_cast<const float4*>(qp + kk);
+        const float4 o4 = *reinterpret_cast<const float4*>(op + kk);
+        s = mfma32(q4.x, kr[kk], s);
+        dp = mfma32(o4.x, vr[kk], dp);
+        s = mfma32(q4.y, kr[kk + 1], s);
+        dp = mfma32(o4.y, vr[kk + 1], dp);
+        s = mfma32(q4.z, kr[kk + 2], s);
+        dp = mfma32(o4.z, vr[kk + 2], dp);
+        s = mfma32(q4.w, kr[kk + 3], s);
+        dp = mfma32(o4.w, vr[kk + 3], dp);
+      }
+      float pd[16], ds[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qi = t + crow(r, hf);
+        const float pv = __expf(s[r] + madd - Ls[qi]);
+        const float mk = p > 0.f ? (((Wd[qi][g4] >> li) & 1u) ? dscale : 0.f) : 1.f;
+        pd[r] = pv * mk;
+        ds[r] = pv * (dp[r] * mk - Ds[qi]);
+        dSs[qi * kLDS + key] = ds[r];
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qi = t + crow(r, hf);
+        const float* orow = Os + qi * kLD;
+        const float* qrow = QKs + qi * kLD;
+        dv0 = mfma32(orow[li], pd[r], dv0);
+        dv1 = mfma32(orow[32 + li], pd[r], dv1);
+        dk0 = mfma32(qrow[li], ds[r], dk0);
+        dk1 = mfma32(qrow[32 + li], ds[r], dk1);
+      }
+    }
+  }
+  __syncthreads();  // every wave done with Q and dO; dS complete
+  if (kactive && half == 0) {  // K rows (biased) from registers into LDS for phase 2
+    float* kd = QKs + key * kLDK + hf * 32;
+#pragma unroll
+    for (int kk = 0; kk < 32; kk += 4)
+      *reinterpret_cast<float4*>(kd + kk) = make_float4(kr[kk], kr[kk + 1], kr[kk + 2], kr[kk + 3]);
+  }
+  __syncthreads();
+
+  // ---- phase 2: dQ partial for queries 32*g4.. over keys 64*half..64*half+63
+  const bool qactive = 32 * g4 < S;
+  f32x16 dq0 = {}, dq1 = {};
+  if (qactive) {
+    const float* dsr = dSs + (32 * g4 + li) * kLDS + 4 * hf;
+    for (int k0 = 64 * half; k0 < min(S, 64 * half + 64); k0 += 8) {
+      const float4 b4 = *reinterpret_cast<const float4*>(dsr + k0);
+      const float bv[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) {
+        const float* kp = QKs + (k0 + 4 * hf + s2) * kLDK;
+        dq0 = mfma32(kp[li], bv[s2], dq0);
+        dq1 = mfma32(kp[32 + li], bv[s2], dq1);
+      }
+    }
+  }
+  __syncthreads();  // dS and K consumed: LDS free for the hand-off
+
+  // ---- combine: waves 4..7 hand their partials to waves 0..3 (lane-private slots, fixed order)
+  float* xq = Os + g4 * 64 * 32 + lane;   // dq partial: 32 floats per lane, element r at xq[64 r]
+  float* xk = dSs + g4 * 64 * 64 + lane;  // dk/dv partials: 64 floats per lane (conflict-free slots)
+  if (half == 1) {
+    if (qactive)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        xq[64 * r] = dq0[r];
+        xq[64 * (16 + r)] = dq1[r];
+      }
+    if (kactive)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        xk[64 * r] = dk0[r];
+        xk[64 * (16 + r)] = dk1[r];
+        xk[64 * (32 + r)] = dv0[r];
+        xk[64 * (48 + r)] = dv1[r];
+      }
+  }
+  __syncthreads();
+  if (half == 1) return;
+  if (qactive)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      dq0[r] += xq[64 * r];
+      dq1[r] += xq[64 * (16 + r)];
+    }
+  if (kactive)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      dk0[r] += xk[64 * r];
+      dk1[r] += xk[64 * (16 + r)];
+      dv0[r] += xk[64 * (32 + r)];
+      dv1[r] += xk[64 * (48 + r)];
+    }
+  if (!qactive) return;  // qactive == kactive here (both 32*g4 < S)
+  const int64_t tok = (int64_t)b * S + key;  // key == query index 32*g4 + li
+  T* outq = dqkv + tok * ld + h * kD;
+  T* outk = dqkv + tok * ld + H + h * kD;
+  T* outv = dqkv + tok * ld + 2 * H + h * kD;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int d = 8 * g + 4 * hf;
+    float q0v[4] = {dq0[4 * g] * 0.125f, dq0[4 * g + 1] * 0.125f, dq0[4 * g + 2] * 0.125f, dq0[4 * g + 3] * 0.125f};
+    float q1v[4] = {dq1[4 * g] * 0.125f, dq1[4 * g + 1] * 0.125f, dq1[4 * g + 2] * 0.125f, dq1[4 * g + 3] * 0.125f};
+    float a0[4] = {dk0[4 * g], dk0[4 * g + 1], dk0[4 * g + 2], dk0[4 * g + 3]};
+    float a1[4] = {dk1[4 * g], dk1[4 * g + 1], dk1[4 * g + 2], dk1[4 * g + 3]};
+    float c0v[4] = {dv0[4 * g], dv0[4 * g + 1], dv0[4 * g + 2], dv0[4 * g + 3]};
+    float c1v[4] = {dv1[4 * g], dv1[4 * g + 1], dv1[4 * g + 2], dv1[4 * g + 3]};
+    store4(outq + d, q0v);
+    store4(outq + 32 + d, q1v);
+    store4(outk + d, a0);
+    store4(outk + 32 + d, a1);
+    store4(outv + d, c0v);
+    store4(outv + 32 + d, c1v);
+  }
+}
+
 }  // namespace hs
 
 using namespace hs;
+
+// HETSEQ_ATTN_BWD=split forces the two-kernel backward (A/B and tests)
+static bool fused_bwd_enabled() {
+  const char* e = std::getenv("HETSEQ_ATTN_BWD");
+  return !(e && std::string(e) == "split");
+}
 
 // dmask: uint32 keep-bits [B*NH*S*(S/32)] written by the forward when p > 0
 // and read by both backward kernels (required when p > 0).
@@ -395,6 +640,15 @@ int launch_attn_bwd(int dtype, const void* qkv, const int64_t* mask, const float
                     const void* dctx, const float* lse, float* Dbuf, void* dqkv, const uint32_t* dmask, int B, int S,
                     int NH, int D, float p, hipStream_t st) {
   if (D != kD || S % 32 != 0 || S <= 0 || (p > 0.f && dmask == nullptr)) return -1;
+  if (S <= 128 && fused_bwd_enabled()) {  // one block per (batch, head): 5 products instead of 7
+    if (dtype == 0)
+      hipLaunchKernelGGL(attn_bwd_fused_kernel<float>, dim3(B * NH), dim3(512), 0, st, (const float*)qkv, mask, bqkv,
+                         (const float*)ctx, (const float*)dctx, lse, (float*)dqkv, S, NH, p, dmask);
+    else
+      hipLaunchKernelGGL(attn_bwd_fused_kernel<bf16_t>, dim3(B * NH), dim3(512), 0, st, (const bf16_t*)qkv, mask,
+                         bqkv, (const bf16_t*)ctx, (const bf16_t*)dctx, lse, (bf16_t*)dqkv, S, NH, p, dmask);
+    return 0;
+  }
   dim3 grid((S + 127) / 128, B * NH);
   if (dtype == 0) {
     hipLaunchKernelGGL(attn_bwd_dq_kernel<float>, grid, dim3(256), 0, st, (const float*)qkv, mask, bqkv,

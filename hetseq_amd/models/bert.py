@@ -341,6 +341,17 @@ class BertLayer(nn.Module):
                 o.dense.weight, o.dense.bias, o.LayerNorm.weight, o.LayerNorm.bias]
 
     def _weights(self):
+        """Kernel-side weight views.  With a flat store they are fixed views into its buffers
+        (parameters are updated in place), so they are built once and cached."""
+        cached = getattr(self, "_hs_wcache", None)
+        if cached is not None:
+            return cached
+        W = self._build_weights()
+        if getattr(self, "_hs_store", None) is not None:
+            self._hs_wcache = W
+        return W
+
+    def _build_weights(self):
         from hetseq_amd.ops.bert_ops import LayerWeights
 
         store = getattr(self, "_hs_store", None)
@@ -394,6 +405,14 @@ class BertLayer(nn.Module):
 
     def _grad_views(self):
         """fp32 views of this layer's gradients inside the flat store (accumulated in place)."""
+        cached = getattr(self, "_hs_gcache", None)
+        if cached is not None and cached[0] is self._hs_store:
+            return cached[1]
+        G = self._build_grad_views()
+        self._hs_gcache = (self._hs_store, G)
+        return G
+
+    def _build_grad_views(self):
         from hetseq_amd.ops.bert_ops import LayerWeights
 
         store = self._hs_store
@@ -537,11 +556,13 @@ class BertPreTrainedModel(nn.Module):
         for m in self.modules():
             m._hs_store = store
             m._hs_dtype = compute_dtype
+            m._hs_wcache = None
         self._compute_dtype = compute_dtype
 
     def set_compute_dtype(self, dtype):
         for m in self.modules():
             m._hs_dtype = dtype
+            m._hs_wcache = None
         self._compute_dtype = dtype
 
     @property

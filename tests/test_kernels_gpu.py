@@ -149,6 +149,26 @@ def test_attention_fwd_bwd(cuda, B, S, NH):
     _close(qkv.grad, qkv2.grad, 1e-4, 1e-5, "attn dqkv")
 
 
+@pytest.mark.parametrize("S", [32, 96, 128])
+def test_attention_bwd_fused_matches_split(cuda, S, monkeypatch):
+    """The one-block-per-head fused backward (S <= 128) equals the two-kernel path, with dropout + bias."""
+    from hetseq_amd.ops import bert_ops
+
+    torch.manual_seed(12)
+    B, NH, p = 2, 3, 0.1
+    H = NH * 64
+    qkv = torch.randn(B * S, 3 * H, device=cuda)
+    bias = torch.randn(3 * H, device=cuda) * 0.1
+    mask = torch.ones(B, S, dtype=torch.int64, device=cuda)
+    mask[1, S // 2:] = 0
+    out, lse = bert_ops.attn_fwd(qkv, mask, B, S, NH, p, 5, 7, bias=bias)
+    dout = torch.randn_like(out)
+    g_fused = bert_ops.attn_bwd(qkv, mask, out, dout, lse, B, S, NH, p, bias=bias)
+    monkeypatch.setenv("HETSEQ_ATTN_BWD", "split")
+    g_split = bert_ops.attn_bwd(qkv, mask, out, dout, lse, B, S, NH, p, bias=bias)
+    _close(g_fused, g_split, 1e-5, 1e-6, "fused vs split attention backward")
+
+
 def test_attention_fully_masked_row(cuda):
     """-10000 additive mask (not -inf): a fully masked sequence still attends (Q27)."""
     from hetseq_amd.ops.bert_ops import attention
