@@ -37,7 +37,7 @@ from hetseq_amd.meters import AverageMeter, StopwatchMeter, TimeMeter
 from hetseq_amd.optim import build_lr_scheduler, build_optimizer
 from hetseq_amd.parallel import distributed_utils
 from hetseq_amd.parallel.ddp import BMUF, FlatDDP
-from hetseq_amd.runtime import profiling, rng
+from hetseq_amd.runtime import faults, profiling, rng
 from hetseq_amd.runtime.flat import FlatParamStore
 
 LN2 = math.log(2)
@@ -185,6 +185,7 @@ class Controller(object):
         """Forward, backward and parameter update for one group of micro-batches."""
         if self._dummy_batch is None:
             self._dummy_batch = next((s for s in samples if s is not None and len(s) > 0), None)
+        faults.maybe_inject(getattr(self.args, "distributed_rank", 0) or 0, self._num_updates)
         self._set_seed()
         if not self._model.training:
             self.model.train()  # (a recursive walk over every module: only when the mode changes)

@@ -14,6 +14,8 @@
 // Rows are processed as tiles: a block of 256 threads covers 1024 columns
 // (4 per thread, 16-byte vectors) and a chunk of rows, keeping per-column
 // partial sums in registers -> one partial row per block, no atomics.
+#include <algorithm>
+
 #include "common.h"
 #include "reduce.h"
 
@@ -175,9 +177,48 @@ static int ew_grid(int64_t n) {
   return (int)g;
 }
 
+// Deterministic scatter-add of rows by key: dst[key] += sum of src[order[j]] over the
+// run of equal keys (keys sorted ascending, order = the stable sort permutation).
+// One block per sorted position; only the first position of each run does the
+// work, summing its run in sorted (= original) order -- bitwise reproducible,
+// no atomics, no host sync for the number of distinct keys.  Out-of-range keys
+// are skipped (the forward clamps and flags them).
+__global__ void __launch_bounds__(256) segsum_rows_kernel(const float* __restrict__ src,
+                                                           const int64_t* __restrict__ order,
+                                                           const int64_t* __restrict__ keys, float* __restrict__ dst,
+                                                           int n, int H, int K) {
+  const int i = blockIdx.x;
+  const int64_t key = keys[i];
+  if ((i > 0 && keys[i - 1] == key) || key < 0 || key >= K) return;
+  int end = i + 1;
+  while (end < n && keys[end] == key) ++end;
+  for (int c = threadIdx.x * 4; c < H; c += blockDim.x * 4) {
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int j = i; j < end; ++j) {
+      float v[4];
+      load4(src + order[j] * H + c, v);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[q] += v[q];
+    }
+    float d[4];
+    load4(dst + key * H + c, d);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) d[q] += acc[q];
+    store4(dst + key * H + c, d);
+  }
+}
+
 }  // namespace hs
 
 using namespace hs;
+
+int launch_segsum_rows(const float* src, const int64_t* order, const int64_t* keys, float* dst, int n, int H, int K,
+                       hipStream_t st) {
+  if (H % 4 != 0 || n <= 0) return n == 0 ? 0 : -1;
+  hipLaunchKernelGGL(segsum_rows_kernel, dim3(n), dim3(std::min(256, ((H / 4 + 63) / 64) * 64)), 0, st, src, order,
+                     keys, dst, n, H, K);
+  return 0;
+}
 
 void launch_bias_gelu_fwd(int dtype, const void* x, const float* b, void* y, int64_t rows, int N, hipStream_t st) {
   const int g = ew_grid(rows * N / 4);

@@ -229,36 +229,31 @@ __global__ void __launch_bounds__(256) emb_fwd_kernel(const int64_t* __restrict_
   }
 }
 
-// dword/dpos are accumulated with float atomics (full 256-B wave rows, the
-// fast atomic shape); the token-type gradient (2 rows in BERT) is pre-reduced
-// in registers and LDS first -- 4096 rows into 2 would otherwise serialise.
+// Embedding LayerNorm backward: writes dx = d(word + pos + type) per row (fp32)
+// and the per-block dgamma/dbeta column partials.  The scatter of dx into the
+// three embedding tables is done afterwards by the deterministic sorted-segment
+// reduction (segsum_rows, elementwise.hip) -- no float atomics, so the
+// embedding gradients are bitwise reproducible, and 4096 x 768 x 2 contended
+// atomics (~180 us) become a sort plus ~3 streaming passes.
 template <int NV, typename T>
-__global__ void __launch_bounds__(256) emb_bwd_kernel(const T* __restrict__ dy, const int64_t* __restrict__ ids,
-                                                      const int64_t* __restrict__ tt, const float* __restrict__ zsave,
+__global__ void __launch_bounds__(256) emb_bwd_kernel(const T* __restrict__ dy, const float* __restrict__ zsave,
                                                       const float* __restrict__ mean_in,
                                                       const float* __restrict__ rstd_in,
-                                                      const float* __restrict__ gamma, float* __restrict__ dword,
-                                                      float* __restrict__ dpos, float* __restrict__ dtype,
+                                                      const float* __restrict__ gamma, float* __restrict__ dx_out,
                                                       float* __restrict__ part_gamma, float* __restrict__ part_beta,
-                                                      int rows, int S, int V, int TV, float p, uint64_t seed,
-                                                      uint64_t off) {
+                                                      int rows, float p, uint64_t seed, uint64_t off) {
   constexpr int H = NV * 256;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int lane = threadIdx.x & 63;
   const float scale = p < 1.f ? 1.0f / (1.0f - p) : 0.f;
-  float ag[NV][4], ab[NV][4], at0[NV][4], at1[NV][4];
+  float ag[NV][4], ab[NV][4];
 #pragma unroll
   for (int k = 0; k < NV; ++k)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) ag[k][j] = ab[k][j] = at0[k][j] = at1[k][j] = 0.f;
+    for (int j = 0; j < 4; ++j) ag[k][j] = ab[k][j] = 0.f;
   for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += gridDim.x * 4) {
     const int64_t base = (int64_t)row * H;
     const float mean = mean_in[row], rstd = rstd_in[row];
-    int64_t id = ids[row];
-    int64_t t = tt ? tt[row] : 0;
-    id = id < 0 ? 0 : (id >= V ? V - 1 : id);
-    t = t < 0 ? 0 : (t >= TV ? TV - 1 : t);
-    const int s = row % S;
     float xh[NV][4], g[NV][4];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -285,37 +280,14 @@ __global__ void __launch_bounds__(256) emb_bwd_kernel(const T* __restrict__ dy, 
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
       const int c = (k * 64 + lane) * 4;
+      float dz[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float dz = rstd * (g[k][j] - s1 - xh[k][j] * s2);
-        atomicAdd(dword + id * H + c + j, dz);
-        atomicAdd(dpos + (int64_t)s * H + c + j, dz);
-        if (TV <= 2) {
-          if (t == 0) at0[k][j] += dz; else at1[k][j] += dz;
-        } else {
-          atomicAdd(dtype + t * H + c + j, dz);
-        }
-      }
+      for (int j = 0; j < 4; ++j) dz[j] = rstd * (g[k][j] - s1 - xh[k][j] * s2);
+      store4(dx_out + base + c, dz);
     }
   }
   block_colpart_store<NV>(ag, part_gamma, lds);
   block_colpart_store<NV>(ab, part_beta, lds);
-  if (TV <= 2) {
-    const int w = threadIdx.x >> 6;
-#pragma unroll
-    for (int k = 0; k < NV; ++k) store4(lds + w * H + (k * 64 + lane) * 4, at0[k]);
-    __syncthreads();
-    for (int c = threadIdx.x; c < H; c += blockDim.x)
-      atomicAdd(dtype + c, (lds[c] + lds[H + c]) + (lds[2 * H + c] + lds[3 * H + c]));
-    __syncthreads();
-    if (TV == 2) {
-#pragma unroll
-      for (int k = 0; k < NV; ++k) store4(lds + w * H + (k * 64 + lane) * 4, at1[k]);
-      __syncthreads();
-      for (int c = threadIdx.x; c < H; c += blockDim.x)
-        atomicAdd(dtype + H + c, (lds[c] + lds[H + c]) + (lds[2 * H + c] + lds[3 * H + c]));
-    }
-  }
 }
 
 constexpr int kLnBwdBlocks = 256;
@@ -350,13 +322,11 @@ void emb_fwd_launch(const int64_t* ids, const int64_t* tt, const float* w, const
 }
 
 template <int NV, typename T>
-void emb_bwd_launch(const void* dy, const int64_t* ids, const int64_t* tt, const float* zsave, const float* mean,
-                    const float* rstd, const float* gamma, float* dw, float* dp, float* dt, float* pg, float* pb,
-                    int rows, int S, int V, int TV, float p, uint64_t seed, uint64_t off, hipStream_t st) {
+void emb_bwd_launch(const void* dy, const float* zsave, const float* mean, const float* rstd, const float* gamma,
+                    float* dx, float* pg, float* pb, int rows, float p, uint64_t seed, uint64_t off, hipStream_t st) {
   constexpr int H = NV * 256;
   hipLaunchKernelGGL((emb_bwd_kernel<NV, T>), dim3(kLnBwdBlocks), dim3(256), 4 * H * sizeof(float), st,
-                     (const T*)dy, ids, tt, zsave, mean, rstd, gamma, dw, dp, dt, pg, pb, rows, S, V, TV, p, seed,
-                     off);
+                     (const T*)dy, zsave, mean, rstd, gamma, dx, pg, pb, rows, p, seed, off);
 }
 
 }  // namespace hs
@@ -416,16 +386,13 @@ int launch_emb_fwd(int dtype, const int64_t* ids, const int64_t* tt, const float
   return 0;
 }
 
-int launch_emb_bwd(int dtype, const void* dy, const int64_t* ids, const int64_t* tt, const float* zsave,
-                   const float* mean, const float* rstd, const float* gamma, float* dw, float* dp, float* dt, float* pg,
-                   float* pb, int rows, int S, int H, int V, int TV, float p, uint64_t seed, uint64_t off,
-                   hipStream_t st) {
+int launch_emb_bwd(int dtype, const void* dy, const float* zsave, const float* mean, const float* rstd,
+                   const float* gamma, float* dx, float* pg, float* pb, int rows, int H, float p, uint64_t seed,
+                   uint64_t off, hipStream_t st) {
   if (dtype == 0) {
-    HS_DISPATCH_H(H, (emb_bwd_launch<NV, float>(dy, ids, tt, zsave, mean, rstd, gamma, dw, dp, dt, pg, pb, rows, S, V,
-                                                TV, p, seed, off, st)));
+    HS_DISPATCH_H(H, (emb_bwd_launch<NV, float>(dy, zsave, mean, rstd, gamma, dx, pg, pb, rows, p, seed, off, st)));
   } else {
-    HS_DISPATCH_H(H, (emb_bwd_launch<NV, bf16_t>(dy, ids, tt, zsave, mean, rstd, gamma, dw, dp, dt, pg, pb, rows, S,
-                                                 V, TV, p, seed, off, st)));
+    HS_DISPATCH_H(H, (emb_bwd_launch<NV, bf16_t>(dy, zsave, mean, rstd, gamma, dx, pg, pb, rows, p, seed, off, st)));
   }
   return 0;
 }

@@ -231,6 +231,27 @@ def bias_gelu(x, b):
 
 
 # --------------------------------------------------------------------- embeddings
+_POS_RUNS = {}
+
+
+def _position_runs(B, S, dev):
+    """(sorted keys, order) of the position ids row % S: position s owns rows s, s+S, ..."""
+    k = (B, S, str(dev))
+    if k not in _POS_RUNS:
+        i = torch.arange(B * S, dtype=torch.int64, device=dev)
+        _POS_RUNS[k] = (i // B, (i % B) * S + i // B)
+    return _POS_RUNS[k]
+
+
+def segsum_rows(src, order, keys, dst):
+    """dst[keys[j]] += src[order[j]] for sorted ``keys`` (deterministic run-wise sums; fp32 src/dst)."""
+    n, H = src.shape
+    assert src.dtype == torch.float32 and dst.dtype == torch.float32 and dst.is_contiguous() and src.is_contiguous()
+    hip().segsum_rows(src.data_ptr(), order.data_ptr(), keys.data_ptr(), dst.data_ptr(), n, H, dst.shape[0],
+                      stream_handle())
+    return dst
+
+
 class FusedEmbedding(torch.autograd.Function):
     @staticmethod
     def forward(ctx, ids, tt, wword, wpos, wtype, gamma, beta, p, eps, out_dtype, sink=None):
@@ -273,12 +294,24 @@ class FusedEmbedding(torch.autograd.Function):
             dg, db = outs[0], outs[1]
         nb = hip().ln_bwd_num_blocks()
         part = _colpart_buf(nb, H, dev, 2)
-        hip().emb_bwd(dtype_code(dy), dy.data_ptr(), ids.data_ptr(), tt.data_ptr() if has_tt else 0, z.data_ptr(),
-                      mean.data_ptr(), rstd.data_ptr(), gamma.data_ptr(), dword.data_ptr(), dpos.data_ptr(),
-                      dtype_.data_ptr(), part[0].data_ptr(), part[1].data_ptr(), B * S, S, H, V, TV, float(p), seed,
-                      off, stream_handle())
+        rows = B * S
+        dx = torch.empty((rows, H), dtype=torch.float32, device=dev)
+        hip().emb_bwd(dtype_code(dy), dy.data_ptr(), z.data_ptr(), mean.data_ptr(), rstd.data_ptr(), gamma.data_ptr(),
+                      dx.data_ptr(), part[0].data_ptr(), part[1].data_ptr(), rows, H, float(p), seed, off,
+                      stream_handle())
         hip().colpart_finalize([part[0].data_ptr(), part[1].data_ptr()], [dg.data_ptr(), db.data_ptr()], nb, H,
                                1 if sink is not None else 0, stream_handle())
+        # scatter dx into the three tables by sorted key runs (deterministic, no atomics)
+        word_keys, word_order = torch.sort(ids.view(-1), stable=True)
+        segsum_rows(dx, word_order, word_keys, dword)
+        pos_keys, pos_order = _position_runs(B, S, dev)
+        segsum_rows(dx, pos_order, pos_keys, dpos)
+        if has_tt:
+            tt_keys, tt_order = torch.sort(tt.view(-1), stable=True)
+        else:
+            tt_keys, tt_order = torch.zeros(rows, dtype=torch.int64, device=dev), \
+                torch.arange(rows, dtype=torch.int64, device=dev)
+        segsum_rows(dx, tt_order, tt_keys, dtype_)
         if sink is not None:
             return (None,) * 11
         return None, None, dword, dpos, dtype_, dg, db, None, None, None, None

@@ -20,6 +20,7 @@ change a reference default):
   --json-log PATH           append one JSON object per logged update
   --profile                 roctx ranges + per-phase hipEvent timing
   --no-gemm-tuning          skip the measured GEMM selection table
+  --deterministic           bitwise-reproducible mode (fixed RCCL algorithm, deterministic torch ops)
 """
 from __future__ import annotations
 
@@ -211,6 +212,9 @@ def add_mi355x_args(parser):
     group.add_argument("--json-log", type=str, default=None, metavar="PATH",
                        help="append one JSON object per logged update")
     group.add_argument("--profile", action="store_true", help="roctx ranges and per-phase hipEvent timing")
+    group.add_argument("--deterministic", action="store_true",
+                       help="bitwise-reproducible mode: deterministic torch algorithms, fixed RCCL ring/simple "
+                            "protocol, no tuned GEMM table (library split-K solutions may use atomics)")
     group.add_argument("--no-gemm-tuning", dest="gemm_tuning", action="store_false",
                        help="do not load the measured hipBLASLt/rocBLAS GEMM table (configs/tunableop)")
     group.add_argument("--bmuf-block-momentum", type=float, default=0.875,

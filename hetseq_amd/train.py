@@ -33,6 +33,16 @@ from hetseq_amd.parallel import distributed_utils
 from hetseq_amd.runtime import profiling
 
 
+def enable_deterministic(args):
+    """Bitwise-reproducible training: must run before the process group is created."""
+    import os
+
+    os.environ.setdefault("NCCL_ALGO", "Ring")      # fixed RCCL reduction order
+    os.environ.setdefault("NCCL_PROTO", "Simple")
+    torch.use_deterministic_algorithms(True, warn_only=True)
+    args.gemm_tuning = False  # tuned library solutions may split K with atomics
+
+
 def main(args, init_distributed=False):
     assert args.max_tokens is not None or args.max_sentences is not None, \
         "Must specify batch size either with --max-tokens or --max-sentences"
@@ -42,6 +52,8 @@ def main(args, init_distributed=False):
         profiling.enable(True)
     np.random.seed(args.seed)
     torch.manual_seed(args.seed)
+    if getattr(args, "deterministic", False):
+        enable_deterministic(args)
     if init_distributed:
         args.distributed_rank = distributed_utils.distributed_init(args)
     if distributed_utils.is_master(args):

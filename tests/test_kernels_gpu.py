@@ -240,6 +240,28 @@ def test_embedding_fwd_bwd(cuda):
         _close(t1.grad, t2.grad, 1e-4, 1e-3, "emb d" + n)
 
 
+def test_embedding_backward_bitwise_deterministic(cuda):
+    """Sorted-run scatter (no atomics): repeated ids give bitwise-identical gradients run to run."""
+    from hetseq_amd.ops.bert_ops import FusedEmbedding
+
+    torch.manual_seed(8)
+    B, S, V, H = 8, 128, 50, 768  # 50-word vocab: every id repeats ~20 times
+    ids = torch.randint(0, V, (B, S), device=cuda)
+    tt = torch.randint(0, 2, (B, S), device=cuda)
+    dy = torch.randn(B * S, H, device=cuda)
+    grads = []
+    for _ in range(3):
+        ws = [torch.randn(n, H, device=cuda, generator=torch.Generator(cuda).manual_seed(1)).requires_grad_()
+              for n in (V, 512, 2)]
+        g = torch.ones(H, device=cuda, requires_grad=True)
+        b = torch.zeros(H, device=cuda, requires_grad=True)
+        FusedEmbedding.apply(ids, tt, ws[0], ws[1], ws[2], g, b, 0.1, 1e-12, torch.float32).backward(dy)
+        grads.append([w.grad.clone() for w in ws])
+    for other in grads[1:]:
+        for a, c in zip(grads[0], other):
+            assert torch.equal(a, c)
+
+
 def test_cross_entropy(cuda):
     from hetseq_amd.ops.bert_ops import cross_entropy
 
