@@ -37,9 +37,10 @@ int launch_emb_fwd(int, const int64_t*, const int64_t*, const float*, const floa
                    const float*, void*, float*, float*, float*, int, int, int, int, int, float, float, u64, u64, int*,
                    hipStream_t);
 int launch_emb_bwd(int, const void*, const float*, const float*, const float*, const float*, float*, float*, float*,
-                   int, int, float, u64, u64, hipStream_t);
+                   const int64_t*, float*, int, int, float, u64, u64, hipStream_t);
 void launch_colpart_finalize(const float* const*, float* const*, int, int, int, int, hipStream_t);
-int launch_segsum_rows(const float*, const int64_t*, const int64_t*, float*, int, int, int, hipStream_t);
+int launch_segsum_rows(const float*, const int64_t*, const int64_t*, float*, float*, int, int, int, hipStream_t);
+int launch_pos_grad(const float*, float*, int, int, int, hipStream_t);
 // elementwise.hip
 void launch_bias_gelu_fwd(int, const void*, const float*, void*, int64_t, int, hipStream_t);
 void launch_bias_tanh_fwd(int, const void*, const float*, void*, int64_t, int, hipStream_t);
@@ -125,17 +126,20 @@ PYBIND11_MODULE(_hip, m) {
                          P(int*, err), ST(st)),
           "emb_fwd");
   });
-  m.def("emb_bwd", [](int dt, i64 dy, i64 zsave, i64 mean, i64 rstd, i64 gamma, i64 dx, i64 pg, i64 pb, int rows,
-                      int H, float p, u64 seed, u64 off, i64 st) {
+  m.def("emb_bwd", [](int dt, i64 dy, i64 zsave, i64 mean, i64 rstd, i64 gamma, i64 dx, i64 pg, i64 pb, i64 tt, i64 pt,
+                      int rows, int H, float p, u64 seed, u64 off, i64 st) {
     check(launch_emb_bwd(dt, P(const void*, dy), P(const float*, zsave), P(const float*, mean), P(const float*, rstd),
-                         P(const float*, gamma), P(float*, dx), P(float*, pg), P(float*, pb), rows, H, p, seed, off,
-                         ST(st)),
+                         P(const float*, gamma), P(float*, dx), P(float*, pg), P(float*, pb), P(const int64_t*, tt),
+                         P(float*, pt), rows, H, p, seed, off, ST(st)),
           "emb_bwd");
   });
-  m.def("segsum_rows", [](i64 src, i64 order, i64 keys, i64 dst, int n, int H, int K, i64 st) {
-    check(launch_segsum_rows(P(const float*, src), P(const int64_t*, order), P(const int64_t*, keys), P(float*, dst), n,
-                             H, K, ST(st)),
+  m.def("segsum_rows", [](i64 src, i64 order, i64 keys, i64 scratch, i64 dst, int n, int H, int K, i64 st) {
+    check(launch_segsum_rows(P(const float*, src), P(const int64_t*, order), P(const int64_t*, keys),
+                             P(float*, scratch), P(float*, dst), n, H, K, ST(st)),
           "segsum_rows");
+  });
+  m.def("pos_grad", [](i64 dx, i64 dpos, int B, int S, int H, i64 st) {
+    check(launch_pos_grad(P(const float*, dx), P(float*, dpos), B, S, H, ST(st)), "pos_grad");
   });
   m.def("colpart_finalize", [](py::list parts, py::list outs, int nparts, int H, int accumulate, i64 st) {
     const int n = static_cast<int>(parts.size());

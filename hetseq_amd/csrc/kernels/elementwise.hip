@@ -177,34 +177,110 @@ static int ew_grid(int64_t n) {
   return (int)g;
 }
 
-// Deterministic scatter-add of rows by key: dst[key] += sum of src[order[j]] over the
-// run of equal keys (keys sorted ascending, order = the stable sort permutation).
-// One block per sorted position; only the first position of each run does the
-// work, summing its run in sorted (= original) order -- bitwise reproducible,
-// no atomics, no host sync for the number of distinct keys.  Out-of-range keys
-// are skipped (the forward clamps and flags them).
-__global__ void __launch_bounds__(256) segsum_rows_kernel(const float* __restrict__ src,
+// Deterministic scatter-add of rows by key, dst[key] += sum of src rows with that
+// key, for keys sorted ascending (order = the stable sort permutation of the rows).
+// Two levels, both in fixed order (bitwise reproducible, no atomics, no host sync
+// for the number of distinct keys), and parallel even for very long runs
+// ([PAD] / [MASK] tokens repeat thousands of times in a batch):
+//   1. seg_partial: block b walks sorted rows [32b, 32b+32) and writes the sum of
+//      every run piece inside its chunk to P[piece start];
+//   2. seg_combine: the block at each run start adds the run's pieces (one per
+//      32-row chunk the run touches) into dst[key].
+constexpr int kSegChunk = 32;
+
+__global__ void __launch_bounds__(256) seg_partial_kernel(const float* __restrict__ src,
                                                            const int64_t* __restrict__ order,
-                                                           const int64_t* __restrict__ keys, float* __restrict__ dst,
-                                                           int n, int H, int K) {
+                                                           const int64_t* __restrict__ keys, float* __restrict__ P,
+                                                           int n, int H) {
+  const int r0 = blockIdx.x * kSegChunk, r1 = min(n, r0 + kSegChunk);
+  for (int c = threadIdx.x * 4; c < H; c += blockDim.x * 4) {
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    int start = r0;
+    for (int j = r0; j < r1; ++j) {
+      float v[4];
+      load4(src + order[j] * H + c, v);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[q] += v[q];
+      if (j + 1 == r1 || keys[j + 1] != keys[j]) {  // end of a run piece
+        store4(P + (int64_t)start * H + c, acc);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q] = 0.f;
+        start = j + 1;
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) seg_combine_kernel(const float* __restrict__ P, const int64_t* __restrict__ keys,
+                                                           float* __restrict__ dst, int n, int H, int K) {
   const int i = blockIdx.x;
   const int64_t key = keys[i];
   if ((i > 0 && keys[i - 1] == key) || key < 0 || key >= K) return;
   int end = i + 1;
   while (end < n && keys[end] == key) ++end;
   for (int c = threadIdx.x * 4; c < H; c += blockDim.x * 4) {
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int j = i; j < end; ++j) {
-      float v[4];
-      load4(src + order[j] * H + c, v);
+    // pieces: the run's first chunk, then one per further chunk; 4 independent
+    // accumulators keep 4 loads in flight for long runs (fixed combine order)
+    float acc[4][4];
+    load4(P + (int64_t)i * H + c, acc[0]);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) acc[q] += v[q];
+    for (int u = 1; u < 4; ++u)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[u][q] = 0.f;
+    int j = (i / kSegChunk + 1) * kSegChunk;
+    for (; j + 3 * kSegChunk < end; j += 4 * kSegChunk)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float v[4];
+        load4(P + (int64_t)(j + u * kSegChunk) * H + c, v);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[u][q] += v[q];
+      }
+    for (; j < end; j += kSegChunk) {
+      float v[4];
+      load4(P + (int64_t)j * H + c, v);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[0][q] += v[q];
     }
     float d[4];
     load4(dst + key * H + c, d);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) d[q] += acc[q];
+    for (int q = 0; q < 4; ++q) d[q] += (acc[0][q] + acc[1][q]) + (acc[2][q] + acc[3][q]);
     store4(dst + key * H + c, d);
+  }
+}
+
+// Position-embedding gradient: dpos[s] += sum_b dx[b*S + s] (fixed order, 8 rows in flight).
+__global__ void __launch_bounds__(256) pos_grad_kernel(const float* __restrict__ dx, float* __restrict__ dpos, int B,
+                                                       int S, int H) {
+  const int s = blockIdx.x;
+  for (int c = threadIdx.x * 4; c < H; c += blockDim.x * 4) {
+    float acc[8][4];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[u][q] = 0.f;
+    int b = 0;
+    for (; b + 8 <= B; b += 8)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        float v[4];
+        load4(dx + ((int64_t)(b + u) * S + s) * H + c, v);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[u][q] += v[q];
+      }
+    for (; b < B; ++b) {
+      float v[4];
+      load4(dx + ((int64_t)b * S + s) * H + c, v);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[0][q] += v[q];
+    }
+    float d[4];
+    load4(dpos + (int64_t)s * H + c, d);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      d[q] += ((acc[0][q] + acc[1][q]) + (acc[2][q] + acc[3][q])) + ((acc[4][q] + acc[5][q]) + (acc[6][q] + acc[7][q]));
+    store4(dpos + (int64_t)s * H + c, d);
   }
 }
 
@@ -212,11 +288,21 @@ __global__ void __launch_bounds__(256) segsum_rows_kernel(const float* __restric
 
 using namespace hs;
 
-int launch_segsum_rows(const float* src, const int64_t* order, const int64_t* keys, float* dst, int n, int H, int K,
-                       hipStream_t st) {
-  if (H % 4 != 0 || n <= 0) return n == 0 ? 0 : -1;
-  hipLaunchKernelGGL(segsum_rows_kernel, dim3(n), dim3(std::min(256, ((H / 4 + 63) / 64) * 64)), 0, st, src, order,
-                     keys, dst, n, H, K);
+int launch_segsum_rows(const float* src, const int64_t* order, const int64_t* keys, float* scratch, float* dst, int n,
+                       int H, int K, hipStream_t st) {
+  if (H % 4 != 0 || n < 0) return -1;
+  if (n == 0) return 0;
+  const int threads = std::min(256, ((H / 4 + 63) / 64) * 64);
+  hipLaunchKernelGGL(seg_partial_kernel, dim3((n + kSegChunk - 1) / kSegChunk), dim3(threads), 0, st, src, order, keys,
+                     scratch, n, H);
+  hipLaunchKernelGGL(seg_combine_kernel, dim3(n), dim3(threads), 0, st, scratch, keys, dst, n, H, K);
+  return 0;
+}
+
+int launch_pos_grad(const float* dx, float* dpos, int B, int S, int H, hipStream_t st) {
+  if (H % 4 != 0) return -1;
+  hipLaunchKernelGGL(pos_grad_kernel, dim3(S), dim3(std::min(256, ((H / 4 + 63) / 64) * 64)), 0, st, dx, dpos, B, S,
+                     H);
   return 0;
 }
 

@@ -241,19 +241,21 @@ __global__ void __launch_bounds__(256) emb_bwd_kernel(const T* __restrict__ dy, 
                                                       const float* __restrict__ rstd_in,
                                                       const float* __restrict__ gamma, float* __restrict__ dx_out,
                                                       float* __restrict__ part_gamma, float* __restrict__ part_beta,
+                                                      const int64_t* __restrict__ tt, float* __restrict__ part_type,
                                                       int rows, float p, uint64_t seed, uint64_t off) {
   constexpr int H = NV * 256;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int lane = threadIdx.x & 63;
   const float scale = p < 1.f ? 1.0f / (1.0f - p) : 0.f;
-  float ag[NV][4], ab[NV][4];
+  float ag[NV][4], ab[NV][4], at0[NV][4], at1[NV][4];
 #pragma unroll
   for (int k = 0; k < NV; ++k)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) ag[k][j] = ab[k][j] = 0.f;
+    for (int j = 0; j < 4; ++j) ag[k][j] = ab[k][j] = at0[k][j] = at1[k][j] = 0.f;
   for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += gridDim.x * 4) {
     const int64_t base = (int64_t)row * H;
     const float mean = mean_in[row], rstd = rstd_in[row];
+    const bool type1 = tt != nullptr && tt[row] == 1;
     float xh[NV][4], g[NV][4];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -282,12 +284,19 @@ __global__ void __launch_bounds__(256) emb_bwd_kernel(const T* __restrict__ dy, 
       const int c = (k * 64 + lane) * 4;
       float dz[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) dz[j] = rstd * (g[k][j] - s1 - xh[k][j] * s2);
+      for (int j = 0; j < 4; ++j) {
+        dz[j] = rstd * (g[k][j] - s1 - xh[k][j] * s2);
+        if (type1) at1[k][j] += dz[j]; else at0[k][j] += dz[j];
+      }
       store4(dx_out + base + c, dz);
     }
   }
   block_colpart_store<NV>(ag, part_gamma, lds);
   block_colpart_store<NV>(ab, part_beta, lds);
+  if (part_type) {  // token-type gradient (<= 2 types): per-block partials [2][grid][H]
+    block_colpart_store<NV>(at0, part_type, lds);
+    block_colpart_store<NV>(at1, part_type + (int64_t)gridDim.x * H, lds);
+  }
 }
 
 constexpr int kLnBwdBlocks = 256;
@@ -323,10 +332,11 @@ void emb_fwd_launch(const int64_t* ids, const int64_t* tt, const float* w, const
 
 template <int NV, typename T>
 void emb_bwd_launch(const void* dy, const float* zsave, const float* mean, const float* rstd, const float* gamma,
-                    float* dx, float* pg, float* pb, int rows, float p, uint64_t seed, uint64_t off, hipStream_t st) {
+                    float* dx, float* pg, float* pb, const int64_t* tt, float* pt, int rows, float p, uint64_t seed,
+                    uint64_t off, hipStream_t st) {
   constexpr int H = NV * 256;
   hipLaunchKernelGGL((emb_bwd_kernel<NV, T>), dim3(kLnBwdBlocks), dim3(256), 4 * H * sizeof(float), st,
-                     (const T*)dy, zsave, mean, rstd, gamma, dx, pg, pb, rows, p, seed, off);
+                     (const T*)dy, zsave, mean, rstd, gamma, dx, pg, pb, tt, pt, rows, p, seed, off);
 }
 
 }  // namespace hs
@@ -387,12 +397,14 @@ int launch_emb_fwd(int dtype, const int64_t* ids, const int64_t* tt, const float
 }
 
 int launch_emb_bwd(int dtype, const void* dy, const float* zsave, const float* mean, const float* rstd,
-                   const float* gamma, float* dx, float* pg, float* pb, int rows, int H, float p, uint64_t seed,
-                   uint64_t off, hipStream_t st) {
+                   const float* gamma, float* dx, float* pg, float* pb, const int64_t* tt, float* pt, int rows, int H,
+                   float p, uint64_t seed, uint64_t off, hipStream_t st) {
   if (dtype == 0) {
-    HS_DISPATCH_H(H, (emb_bwd_launch<NV, float>(dy, zsave, mean, rstd, gamma, dx, pg, pb, rows, p, seed, off, st)));
+    HS_DISPATCH_H(H, (emb_bwd_launch<NV, float>(dy, zsave, mean, rstd, gamma, dx, pg, pb, tt, pt, rows, p, seed, off,
+                                                st)));
   } else {
-    HS_DISPATCH_H(H, (emb_bwd_launch<NV, bf16_t>(dy, zsave, mean, rstd, gamma, dx, pg, pb, rows, p, seed, off, st)));
+    HS_DISPATCH_H(H, (emb_bwd_launch<NV, bf16_t>(dy, zsave, mean, rstd, gamma, dx, pg, pb, tt, pt, rows, p, seed, off,
+                                                 st)));
   }
   return 0;
 }

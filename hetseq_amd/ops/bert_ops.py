@@ -231,24 +231,13 @@ def bias_gelu(x, b):
 
 
 # --------------------------------------------------------------------- embeddings
-_POS_RUNS = {}
-
-
-def _position_runs(B, S, dev):
-    """(sorted keys, order) of the position ids row % S: position s owns rows s, s+S, ..."""
-    k = (B, S, str(dev))
-    if k not in _POS_RUNS:
-        i = torch.arange(B * S, dtype=torch.int64, device=dev)
-        _POS_RUNS[k] = (i // B, (i % B) * S + i // B)
-    return _POS_RUNS[k]
-
-
 def segsum_rows(src, order, keys, dst):
     """dst[keys[j]] += src[order[j]] for sorted ``keys`` (deterministic run-wise sums; fp32 src/dst)."""
     n, H = src.shape
     assert src.dtype == torch.float32 and dst.dtype == torch.float32 and dst.is_contiguous() and src.is_contiguous()
-    hip().segsum_rows(src.data_ptr(), order.data_ptr(), keys.data_ptr(), dst.data_ptr(), n, H, dst.shape[0],
-                      stream_handle())
+    scratch = torch.empty_like(src)
+    hip().segsum_rows(src.data_ptr(), order.data_ptr(), keys.data_ptr(), scratch.data_ptr(), dst.data_ptr(), n, H,
+                      dst.shape[0], stream_handle())
     return dst
 
 
@@ -296,22 +285,25 @@ class FusedEmbedding(torch.autograd.Function):
         part = _colpart_buf(nb, H, dev, 2)
         rows = B * S
         dx = torch.empty((rows, H), dtype=torch.float32, device=dev)
+        small_tv = TV <= 2  # token types reduced in-kernel (per-block partials); otherwise by sorted runs
+        ptype = _colpart_buf(nb, H, dev, 2) if small_tv else None
         hip().emb_bwd(dtype_code(dy), dy.data_ptr(), z.data_ptr(), mean.data_ptr(), rstd.data_ptr(), gamma.data_ptr(),
-                      dx.data_ptr(), part[0].data_ptr(), part[1].data_ptr(), rows, H, float(p), seed, off,
-                      stream_handle())
-        hip().colpart_finalize([part[0].data_ptr(), part[1].data_ptr()], [dg.data_ptr(), db.data_ptr()], nb, H,
-                               1 if sink is not None else 0, stream_handle())
-        # scatter dx into the three tables by sorted key runs (deterministic, no atomics)
+                      dx.data_ptr(), part[0].data_ptr(), part[1].data_ptr(),
+                      tt.data_ptr() if (has_tt and small_tv) else 0, ptype.data_ptr() if small_tv else 0, rows, H,
+                      float(p), seed, off, stream_handle())
+        acc = 1 if sink is not None else 0
+        hip().colpart_finalize([part[0].data_ptr(), part[1].data_ptr()], [dg.data_ptr(), db.data_ptr()], nb, H, acc,
+                               stream_handle())
+        if small_tv:
+            tv = [ptype[0].data_ptr()] + ([ptype[1].data_ptr()] if TV == 2 else [])
+            hip().colpart_finalize(tv, [dtype_[i].data_ptr() for i in range(len(tv))], nb, H, 1, stream_handle())
+        else:
+            tt_keys, tt_order = torch.sort(tt.view(-1), stable=True)
+            segsum_rows(dx, tt_order, tt_keys, dtype_)
+        # word rows: deterministic sorted-run sums; positions: fixed-order column sums
         word_keys, word_order = torch.sort(ids.view(-1), stable=True)
         segsum_rows(dx, word_order, word_keys, dword)
-        pos_keys, pos_order = _position_runs(B, S, dev)
-        segsum_rows(dx, pos_order, pos_keys, dpos)
-        if has_tt:
-            tt_keys, tt_order = torch.sort(tt.view(-1), stable=True)
-        else:
-            tt_keys, tt_order = torch.zeros(rows, dtype=torch.int64, device=dev), \
-                torch.arange(rows, dtype=torch.int64, device=dev)
-        segsum_rows(dx, tt_order, tt_keys, dtype_)
+        hip().pos_grad(dx.data_ptr(), dpos.data_ptr(), B, S, H, stream_handle())
         if sink is not None:
             return (None,) * 11
         return None, None, dword, dpos, dtype_, dg, db, None, None, None, None

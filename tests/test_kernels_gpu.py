@@ -249,8 +249,11 @@ def test_embedding_backward_bitwise_deterministic(cuda):
     ids = torch.randint(0, V, (B, S), device=cuda)
     tt = torch.randint(0, 2, (B, S), device=cuda)
     dy = torch.randn(B * S, H, device=cuda)
+    from hetseq_amd.runtime import rng
+
     grads = []
     for _ in range(3):
+        rng.set_seed(123)  # same dropout stream every repetition
         ws = [torch.randn(n, H, device=cuda, generator=torch.Generator(cuda).manual_seed(1)).requires_grad_()
               for n in (V, 512, 2)]
         g = torch.ones(H, device=cuda, requires_grad=True)
