@@ -77,6 +77,36 @@ __global__ void norm_finalize_kernel(const double* __restrict__ partial, int npa
   }
 }
 
+// Streaming (non-temporal) 16-B accesses: the optimizer touches every byte of
+// p/g/m/v exactly once, so keep them out of L2/MALL.
+typedef float f4v __attribute__((ext_vector_type(4)));
+HS_DEVICE float4 ld_nt(const float* p) {
+  const f4v t = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
+  return make_float4(t.x, t.y, t.z, t.w);
+}
+HS_DEVICE void st_nt(float* p, float4 v) {
+  const f4v t = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(t, reinterpret_cast<f4v*>(p));
+}
+
+template <bool kShadow>
+HS_DEVICE void adam4(float4& pp, const float4 gg, float4& mm, float4& vv, float mul, float b1, float b2, float omb1,
+                     float omb2, float eps, float wd, float decay, float step_size) {
+  float* P = reinterpret_cast<float*>(&pp);
+  const float* Gr = reinterpret_cast<const float*>(&gg);
+  float* M = reinterpret_cast<float*>(&mm);
+  float* V = reinterpret_cast<float*>(&vv);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float gk = Gr[k] * mul;
+    M[k] = M[k] * b1 + omb1 * gk;
+    V[k] = V[k] * b2 + omb2 * gk * gk;
+    const float denom = sqrtf(V[k]) + eps;
+    if (wd != 0.f) P[k] = P[k] + decay * P[k];
+    P[k] = P[k] - step_size * (M[k] / denom);
+  }
+}
+
 template <bool kShadow>
 __global__ void __launch_bounds__(256) adam_flat_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                         float* __restrict__ m, float* __restrict__ v,
@@ -86,25 +116,33 @@ __global__ void __launch_bounds__(256) adam_flat_kernel(float* __restrict__ p, c
   const float mul = gmul ? gmul[0] : 1.0f;
   const float omb1 = 1.0f - b1, omb2 = 1.0f - b2, decay = -wd * lr;
   const int64_t n4 = n >> 2;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-    float pp[4], gg[4], mm[4], vv[4];
-    load4(p + 4 * i, pp);
-    load4(g + 4 * i, gg);
-    load4(m + 4 * i, mm);
-    load4(v + 4 * i, vv);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float gk = gg[k] * mul;
-      mm[k] = mm[k] * b1 + omb1 * gk;
-      vv[k] = vv[k] * b2 + omb2 * gk * gk;
-      const float denom = sqrtf(vv[k]) + eps;
-      if (wd != 0.f) pp[k] = pp[k] + decay * pp[k];
-      pp[k] = pp[k] - step_size * (mm[k] / denom);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  // two float4 groups per thread per iteration: 8 independent 16-B loads in flight
+  for (; i + stride < n4; i += 2 * stride) {
+    float4 p0 = ld_nt(p + 4 * i), g0 = ld_nt(g + 4 * i), m0 = ld_nt(m + 4 * i), v0 = ld_nt(v + 4 * i);
+    const int64_t j = i + stride;
+    float4 p1 = ld_nt(p + 4 * j), g1 = ld_nt(g + 4 * j), m1 = ld_nt(m + 4 * j), v1 = ld_nt(v + 4 * j);
+    adam4<kShadow>(p0, g0, m0, v0, mul, b1, b2, omb1, omb2, eps, wd, decay, step_size);
+    adam4<kShadow>(p1, g1, m1, v1, mul, b1, b2, omb1, omb2, eps, wd, decay, step_size);
+    st_nt(p + 4 * i, p0);
+    st_nt(m + 4 * i, m0);
+    st_nt(v + 4 * i, v0);
+    st_nt(p + 4 * j, p1);
+    st_nt(m + 4 * j, m1);
+    st_nt(v + 4 * j, v1);
+    if (kShadow) {
+      store4(shadow + 4 * i, reinterpret_cast<const float*>(&p0));
+      store4(shadow + 4 * j, reinterpret_cast<const float*>(&p1));
     }
-    store4(p + 4 * i, pp);
-    store4(m + 4 * i, mm);
-    store4(v + 4 * i, vv);
-    if (kShadow) store4(shadow + 4 * i, pp);
+  }
+  for (; i < n4; i += stride) {
+    float4 p0 = ld_nt(p + 4 * i), g0 = ld_nt(g + 4 * i), m0 = ld_nt(m + 4 * i), v0 = ld_nt(v + 4 * i);
+    adam4<kShadow>(p0, g0, m0, v0, mul, b1, b2, omb1, omb2, eps, wd, decay, step_size);
+    st_nt(p + 4 * i, p0);
+    st_nt(m + 4 * i, m0);
+    st_nt(v + 4 * i, v0);
+    if (kShadow) store4(shadow + 4 * i, reinterpret_cast<const float*>(&p0));
   }
   // scalar tail
   const int64_t tail = n - (n4 << 2);
