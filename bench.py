@@ -41,6 +41,7 @@ def parse():
     p.add_argument("--no-fused", action="store_true")
     p.add_argument("--gemm", default=None, choices=[None, "hip", "blas", "auto"])
     p.add_argument("--profile-phases", action="store_true")
+    p.add_argument("--hip-graph", action="store_true", help="replay the captured update as one HIP graph (1 GPU)")
     p.add_argument("--sync-debug", action="store_true", help="warn (with stack) on every host<->device sync in the timed loop")
     p.add_argument("--host-profile", default=None, help="cProfile the timed loop into this file")
     return p.parse_args()
@@ -85,6 +86,8 @@ def main():
             "--update-freq", str(b.update_freq)]
     if b.no_fused:
         argv.append("--no-fused")
+    if b.hip_graph:
+        argv.append("--hip-graph")
     args = options.parse_cli(argv)
     args.distributed_rank = rank
     args.device_id = local_rank
@@ -176,7 +179,8 @@ def main():
             "config": {"model": "bert-base-uncased (L12 H768 A12, %d params)" % nparams,
                        "global_batch": seqs, "seq_len": b.seq_len, "per_gpu_batch": b.batch,
                        "update_freq": b.update_freq, "parallelism": "dp%d" % world,
-                       "fused_kernels": not b.no_fused, "bucket_cap_mb": b.bucket_cap_mb},
+                       "fused_kernels": not b.no_fused, "bucket_cap_mb": b.bucket_cap_mb,
+                       "hip_graph": bool(b.hip_graph and world == 1)},
             "final_train_loss_logged": round(loss, 5),
             "host_ms_per_step": round(host / b.steps * 1000, 3),
             "data_wait_ms_per_step": round(data_wait / b.steps * 1000, 3),

@@ -75,6 +75,8 @@ class Controller(object):
         self._all_reduce_list = [0.0] * 6
         self.fast_stat_sync = args.fast_stat_sync
         self.phase_timer = profiling.PhaseTimer()
+        self._graph = None  # runtime.graphs.GraphedStep once --hip-graph captured the update
+        self._graph_warmup = 3  # eager updates first: GEMM autotuning, TunableOp, allocator warm-up
         self.init_meters(args)
 
     def init_meters(self, args):
@@ -183,6 +185,10 @@ class Controller(object):
     # ------------------------------------------------------------------ training
     def train_step(self, samples, dummy_batch=False, raise_oom=False):
         """Forward, backward and parameter update for one group of micro-batches."""
+        if self._graph_eligible(samples, dummy_batch):
+            out = self._train_step_graphed(samples[0])
+            if out is not None:
+                return out
         if self._dummy_batch is None:
             self._dummy_batch = next((s for s in samples if s is not None and len(s) > 0), None)
         faults.maybe_inject(getattr(self.args, "distributed_rank", 0) or 0, self._num_updates)
@@ -296,6 +302,76 @@ class Controller(object):
             self.zero_grad()
             logging_output = None
         self.clear_buffered_stats()
+        self.meters["train_wall"].stop()
+        return logging_output
+
+    # ------------------------------------------------------------------ HIP graph path
+    def _graph_eligible(self, samples, dummy_batch):
+        a = self.args
+        return (getattr(a, "hip_graph", False) and self.cuda and self.fast_stat_sync and not dummy_batch
+                and len(samples) == 1 and samples[0] is not None and len(samples[0]) > 0
+                and not (a.distributed_world_size > 1 and dist.is_initialized())
+                and getattr(self.optimizer, "supports_device_hyper", False)
+                and self._num_updates >= self._graph_warmup)
+
+    def _graph_body(self, sample):
+        """The captured update (fast-stat path of train_step, single process)."""
+        self.zero_grad()
+        stats = torch.zeros(6, dtype=torch.float64, device=self.device)
+        _, sample_size, lo = self.task.train_step(sample, self.model, self.optimizer, False)
+        stats[0] += sample_size
+        stats[1] += lo.get("nsentences", 0.0)
+        stats[2] += _as_f64(lo.get("loss", 0.0), self.device)
+        stats[3] += _as_f64(lo.get("nll_loss", 0.0), self.device)
+        stats[4] += lo.get("ntokens", 0.0)
+        stats[2:4].div_(stats[0:1] * LN2)
+        scale = torch.where(stats[0] > 0, 1.0 / stats[0].clamp(min=1e-30), torch.ones_like(stats[0])).float()
+        self.optimizer.multiply_grads(scale)
+        grad_norm = self.optimizer.clip_grad_norm(self.args.clip_norm)
+        self.optimizer.step(launch_only=True)
+        return stats, grad_norm.reshape(1)
+
+    def _train_step_graphed(self, sample):
+        from hetseq_amd.runtime.graphs import GraphedStep
+
+        sample = self._prepare_sample(sample)
+        if self._graph is False:
+            return None  # capture failed once: stay eager
+        if self._graph is None:
+            rng.enable_device_seed(self.device)
+            self.optimizer.enable_device_hyper(self.device)
+            self._graph = GraphedStep(self._graph_body)
+        elif not self._graph.matches(sample):
+            return None  # e.g. a short last batch: run it eagerly
+        faults.maybe_inject(getattr(self.args, "distributed_rank", 0) or 0, self._num_updates)
+        self._set_seed()
+        self.optimizer.graph_prepare()
+        self.meters["train_wall"].start()
+        try:
+            stats, grad_norm = self._graph.run(list(sample))
+        except RuntimeError as e:
+            if self._graph.graph is not None and self._graph.static_out is not None:
+                raise  # a replay failure is a real error
+            # capture failed (nothing ran): undo the host half of the update and fall back to eager
+            print("| WARNING: HIP graph capture failed ({}); continuing eagerly".format(str(e).splitlines()[0]),
+                  flush=True)
+            self.optimizer.step_count -= 1
+            self._graph = False
+            return None
+        grad_norm = grad_norm[0]
+        self.set_num_updates(self.get_num_updates() + 1)
+        self.task.update_step(self._num_updates)
+        logging_output = {"nsentences": stats[1], "loss": stats[2], "nll_loss": stats[3], "ntokens": stats[4]}
+        self._prev_grad_norm = grad_norm
+        self.meters["wps"].update(stats[4])
+        self.meters["ups"].update(1.0)
+        self.meters["wpb"].update(stats[4])
+        self.meters["bsz"].update(stats[1])
+        self.meters["gnorm"].update(grad_norm)
+        self.meters["clip"].update((grad_norm > self.args.clip_norm).float() if self.args.clip_norm > 0 else 0.0)
+        self.meters["train_loss"].update(stats[2], stats[0])
+        if self.args.check_consistency and self._num_updates % self.args.check_consistency == 0:
+            self.check_consistency()
         self.meters["train_wall"].stop()
         return logging_output
 

@@ -120,7 +120,8 @@ template <typename T>
 __global__ void __launch_bounds__(256, 2)
     attn_fwd_kernel(const T* __restrict__ qkv, const int64_t* __restrict__ mask, const float* __restrict__ bqkv,
                     T* __restrict__ ctx, float* __restrict__ lse, uint32_t* __restrict__ dmask, int S, int NH, float p,
-                    uint64_t seed, uint64_t off) {
+                    uint64_t seed, uint64_t off, const uint64_t* __restrict__ seed_dev) {
+  seed = resolve_seed(seed, seed_dev);
   __shared__ __attribute__((aligned(16))) float Ks[kCH * kLD];
   __shared__ __attribute__((aligned(16))) float Vs[kCH * kLD];
   __shared__ float Ms[kCH];
@@ -614,6 +615,16 @@ __global__ void __launch_bounds__(512, 1)
 
 using namespace hs;
 
+int launch_attn_fwd_bf16(const void* qkv, const int64_t* mask, const float* bqkv, void* ctx, float* lse,
+                         uint32_t* dmask, int B, int S, int NH, int D, float p, uint64_t seed, uint64_t off,
+                         hipStream_t st);
+
+// HETSEQ_ATTN_BF16_MFMA=0 keeps bf16 attention on the fp32-MFMA kernels (A/B and tests)
+static bool bf16_mfma_enabled() {
+  const char* e = std::getenv("HETSEQ_ATTN_BF16_MFMA");
+  return !(e && std::string(e) == "0");
+}
+
 // HETSEQ_ATTN_BWD=split forces the two-kernel backward (A/B and tests)
 static bool fused_bwd_enabled() {
   const char* e = std::getenv("HETSEQ_ATTN_BWD");
@@ -627,12 +638,14 @@ int launch_attn_fwd(int dtype, const void* qkv, const int64_t* mask, const float
                     hipStream_t st) {
   if (D != kD || S % 32 != 0 || S <= 0) return -1;
   dim3 grid((S + 127) / 128, B * NH);
+  if (dtype != 0 && bf16_mfma_enabled())  // bf16 matrix cores (attention_bf16.hip)
+    return launch_attn_fwd_bf16(qkv, mask, bqkv, ctx, lse, dmask, B, S, NH, D, p, seed, off, st);
   if (dtype == 0)
     hipLaunchKernelGGL(attn_fwd_kernel<float>, grid, dim3(256), 0, st, (const float*)qkv, mask, bqkv, (float*)ctx,
-                       lse, dmask, S, NH, p, seed, off);
+                       lse, dmask, S, NH, p, seed, off, g_seed_dev);
   else
     hipLaunchKernelGGL(attn_fwd_kernel<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)qkv, mask, bqkv,
-                       (bf16_t*)ctx, lse, dmask, S, NH, p, seed, off);
+                       (bf16_t*)ctx, lse, dmask, S, NH, p, seed, off, g_seed_dev);
   return 0;
 }
 

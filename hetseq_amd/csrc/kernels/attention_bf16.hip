@@ -1,0 +1,207 @@
+// bf16 attention on the bf16 matrix cores (v_mfma_f32_32x32x16_bf16) for
+// --dtype bf16.  Same contract as attention.hip (reference bert_modeling.py:
+// 351-377): Q/K/V read from the fused QKV projection output [B*S, 3H] with the
+// projection bias folded into the loads, additive -10000 mask, Philox dropout
+// on the probabilities with a 1-bit keep mask for the backward, context out in
+// [B*S, H], per-row log-sum-exp saved.  fp32 accumulation and softmax
+// statistics; MFMA operands bf16 (the QK scale 1/8 is exact in bf16).
+//
+// Orientation (same as the fp32 kernels): a wave owns 32 queries; the score
+// tile is S^T[key][query] so a lane holds one query's scores in registers.
+//   S^T = K Q^T : A = K rows from LDS (16-B reads, 144-B rows: conflict-free),
+//                 B = the lane's own Q row (registers, 4 k-steps of 16 dims);
+//   O^T = V^T P^T: B = the probability accumulator itself, converted to bf16 --
+//                 registers 8s..8s+7 are exactly the B fragment of k-step s
+//                 (key 16s + 8(j>>2) + 4*half + (j&3) for element j);
+//                 A = V^T from a transposed LDS image (two 8-B reads per step).
+// 8 MFMAs per 32-key tile instead of 128 fp32 ones: the kernel is bound by the
+// softmax/dropout VALU work, not the matrix cores.
+#include "common.h"
+
+namespace hs {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int kBD = 64;        // head dim
+constexpr int kKLD = 72;       // K image row stride (bf16): 144 B
+constexpr int kVLD = 132;      // V^T image row stride (bf16): 264 B -> lanes d, d+1 on adjacent bank pairs
+constexpr int kBCH = 128;      // keys per LDS chunk
+
+HS_DEVICE f32x16 mfma16(bf16x8 a, bf16x8 b, f32x16 c) { return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0); }
+HS_DEVICE int crow16(int r, int hf) { return (r & 3) + 8 * (r >> 2) + 4 * hf; }
+HS_DEVICE short bfbits(float v) { return static_cast<short>(from_f<bf16_t>(v).x); }
+HS_DEVICE float bfval(uint16_t b) { return __uint_as_float(static_cast<uint32_t>(b) << 16); }
+
+// 8 consecutive bf16 of a row (16-B load) -> fp32, + bias, * scale
+HS_DEVICE void load8(const bf16_t* src, const float* bias, float scale, float (&v)[8]) {
+  const uint4 t = *reinterpret_cast<const uint4*>(src);
+  const uint32_t w[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+  if (bias) {
+    const float4 b0 = *reinterpret_cast<const float4*>(bias), b1 = *reinterpret_cast<const float4*>(bias + 4);
+    v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
+    v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] *= scale;
+}
+
+HS_DEVICE bf16x8 pack8(const float (&v)[8]) {
+  bf16x8 r;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r[i] = bfbits(v[i]);
+  return r;
+}
+
+HS_DEVICE const float* boff16(const float* b, int off) { return b ? b + off : nullptr; }
+
+__global__ void __launch_bounds__(256, 2)
+    attn_fwd_bf16_kernel(const bf16_t* __restrict__ qkv, const int64_t* __restrict__ mask,
+                         const float* __restrict__ bqkv, bf16_t* __restrict__ ctx, float* __restrict__ lse,
+                         uint32_t* __restrict__ dmask, int S, int NH, float p, uint64_t seed, uint64_t off,
+                         const uint64_t* __restrict__ seed_dev) {
+  seed = resolve_seed(seed, seed_dev);
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[kBCH * kKLD];
+  __shared__ __attribute__((aligned(16))) uint16_t Vt[kBD * kVLD];
+  __shared__ float Ms[kBCH];
+  const int H = NH * kBD;
+  const int64_t ld = 3 * (int64_t)H;
+  const int bh = blockIdx.y, b = bh / NH, h = bh % NH;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hf = lane >> 5, li = lane & 31;
+  const int q0 = blockIdx.x * 128 + w * 32;
+  const bool active = q0 < S;
+  const bf16_t* rows = qkv + (int64_t)b * S * ld;
+  const uint32_t thr = drop_thr16(p);
+  const float dscale = drop_scale16(thr);
+
+  // the lane's Q row, dims 16s + 8hf + j (k-step s), biased and scaled by 1/sqrt(64)
+  bf16x8 qf[4];
+  if (active) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      float v[8];
+      const int d = 16 * s + 8 * hf;
+      load8(rows + (int64_t)(q0 + li) * ld + h * kBD + d, boff16(bqkv, h * kBD + d), 0.125f, v);
+      qf[s] = pack8(v);
+    }
+  }
+  f32x16 o0 = {}, o1 = {};
+  float m = -1e30f, l = 0.f;
+  const uint64_t erow = ((uint64_t)bh * S + (q0 + li)) * (uint64_t)S;
+
+  for (int c0 = 0; c0 < S; c0 += kBCH) {
+    const int clen = min(kBCH, S - c0);
+    __syncthreads();
+    // K chunk: row-major image; thread unit = (row, 8-dim chunk)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int u = threadIdx.x + 256 * i, r = u >> 3, c8 = (u & 7) * 8;
+      if (r < clen) {
+        float v[8];
+        load8(rows + (int64_t)(c0 + r) * ld + H + h * kBD + c8, boff16(bqkv, H + h * kBD + c8), 1.f, v);
+        *reinterpret_cast<bf16x8*>(Ks + r * kKLD + c8) = pack8(v);
+      }
+    }
+    // V chunk, transposed: Vt[d][key]; consecutive lanes take consecutive keys (conflict-free 2-B writes)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int u = threadIdx.x + 256 * i, r = u & 127, c8 = (u >> 7) * 8;
+      if (r < clen) {
+        float v[8];
+        load8(rows + (int64_t)(c0 + r) * ld + 2 * H + h * kBD + c8, boff16(bqkv, 2 * H + h * kBD + c8), 1.f, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) Vt[(c8 + j) * kVLD + r] = static_cast<uint16_t>(bfbits(v[j]));
+      }
+    }
+    for (int i = threadIdx.x; i < clen; i += blockDim.x)
+      Ms[i] = (1.f - (float)mask[(int64_t)b * S + c0 + i]) * -10000.f;
+    __syncthreads();
+    if (!active) continue;
+    for (int t = 0; t < clen; t += 32) {
+      f32x16 s = {};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+        s = mfma16(*reinterpret_cast<const bf16x8*>(Ks + (t + li) * kKLD + 16 * ks + 8 * hf), qf[ks], s);
+      float mt = -1e30f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        s[r] += Ms[t + crow16(r, hf)];
+        mt = fmaxf(mt, s[r]);
+      }
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      const float mn = fmaxf(m, mt);
+      const float alpha = __expf(m - mn);
+      m = mn;
+      float pr[16];
+      float ps = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        pr[r] = __expf(s[r] - mn);
+        ps += pr[r];
+      }
+      ps += __shfl_xor(ps, 32, 64);
+      l = l * alpha + ps;
+      o0 *= alpha;
+      o1 *= alpha;
+      if (p > 0.f) {  // same keep-bit stream and word layout as the fp32 kernel
+        const uint64_t e0 = (erow + c0 + t) >> 3;
+        const uint32_t mine = keep8_bits(seed, off, e0 + 2 * hf, thr) | (keep8_bits(seed, off, e0 + 2 * hf + 1, thr) << 8);
+        const uint32_t other = static_cast<uint32_t>(__shfl_xor(static_cast<int>(mine), 32, 64));
+        const uint32_t bits = hf == 0 ? (mine | (other << 16)) : (other | (mine << 16));
+#pragma unroll
+        for (int r = 0; r < 16; ++r) pr[r] = ((bits >> crow16(r, hf)) & 1u) ? pr[r] * dscale : 0.f;
+        if (dmask && hf == 0) dmask[((uint64_t)bh * S + q0 + li) * (uint64_t)(S >> 5) + ((c0 + t) >> 5)] = bits;
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 pf;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pf[j] = bfbits(pr[8 * ks + j]);
+        const int k0 = t + 16 * ks + 4 * hf;
+        // A = V^T rows d = li (o0) and 32 + li (o1), keys k0..k0+3 and k0+8..k0+11
+        const uint16_t* v0 = Vt + li * kVLD + k0;
+        const uint16_t* v1 = Vt + (32 + li) * kVLD + k0;
+        bf16x8 a0, a1;
+        const uint2 x0 = *reinterpret_cast<const uint2*>(v0), y0 = *reinterpret_cast<const uint2*>(v0 + 8);
+        const uint2 x1 = *reinterpret_cast<const uint2*>(v1), y1 = *reinterpret_cast<const uint2*>(v1 + 8);
+        a0[0] = (short)(x0.x & 0xffff); a0[1] = (short)(x0.x >> 16); a0[2] = (short)(x0.y & 0xffff); a0[3] = (short)(x0.y >> 16);
+        a0[4] = (short)(y0.x & 0xffff); a0[5] = (short)(y0.x >> 16); a0[6] = (short)(y0.y & 0xffff); a0[7] = (short)(y0.y >> 16);
+        a1[0] = (short)(x1.x & 0xffff); a1[1] = (short)(x1.x >> 16); a1[2] = (short)(x1.y & 0xffff); a1[3] = (short)(x1.y >> 16);
+        a1[4] = (short)(y1.x & 0xffff); a1[5] = (short)(y1.x >> 16); a1[6] = (short)(y1.y & 0xffff); a1[7] = (short)(y1.y >> 16);
+        o0 = mfma16(a0, pf, o0);
+        o1 = mfma16(a1, pf, o1);
+      }
+    }
+  }
+  if (!active) return;
+  const float inv = 1.f / l;
+  bf16_t* out = ctx + ((int64_t)b * S + q0 + li) * H + h * kBD;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int d = 8 * g + 4 * hf;
+    float v0[4] = {o0[4 * g] * inv, o0[4 * g + 1] * inv, o0[4 * g + 2] * inv, o0[4 * g + 3] * inv};
+    float v1[4] = {o1[4 * g] * inv, o1[4 * g + 1] * inv, o1[4 * g + 2] * inv, o1[4 * g + 3] * inv};
+    store4(out + d, v0);
+    store4(out + 32 + d, v1);
+  }
+  if (hf == 0) lse[(int64_t)bh * S + q0 + li] = m + __logf(l);
+}
+
+}  // namespace hs
+
+using namespace hs;
+
+int launch_attn_fwd_bf16(const void* qkv, const int64_t* mask, const float* bqkv, void* ctx, float* lse,
+                         uint32_t* dmask, int B, int S, int NH, int D, float p, uint64_t seed, uint64_t off,
+                         hipStream_t st) {
+  if (D != kBD || S % 32 != 0 || S <= 0) return -1;
+  dim3 grid((S + 127) / 128, B * NH);
+  hipLaunchKernelGGL(attn_fwd_bf16_kernel, grid, dim3(256), 0, st, (const bf16_t*)qkv, mask, bqkv, (bf16_t*)ctx, lse,
+                     dmask, S, NH, p, seed, off, g_seed_dev);
+  return 0;
+}

@@ -21,7 +21,7 @@ using i64 = int64_t;
 // optim.hip
 void launch_grad_norm(const float*, int64_t, double*, const float*, float, float*, hipStream_t);
 void launch_adam_flat(float*, const float*, float*, float*, void*, int64_t, const float*, float, float, float, float,
-                      float, float, hipStream_t);
+                      float, float, const float*, hipStream_t);
 void launch_adadelta_flat(float*, const float*, float*, float*, void*, int64_t, const float*, float, float, float,
                           float, hipStream_t);
 void launch_lamb_flat(float*, const float*, float*, float*, float*, void*, const int64_t*, int, float*, const float*,
@@ -63,6 +63,11 @@ int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, i
                 int64_t ldb, void* C, int64_t ldc, const float* bias, int epi, float beta, float* aux, int64_t ldaux,
                 float* part, float* colsum_out, int colsum_acc, int tile_override, hipStream_t st);
 
+// HIP-graph mode: device word holding the dropout seed (see common.h resolve_seed)
+namespace hs {
+const uint64_t* g_seed_dev = nullptr;
+}
+
 static void check(int rc, const char* what) {
   if (rc != 0) throw std::invalid_argument(std::string(what) + ": unsupported shape for the HIP kernel");
   hipError_t e = hipGetLastError();
@@ -79,11 +84,14 @@ PYBIND11_MODULE(_hip, m) {
     check_launch("grad_norm");
   });
   m.def("adam_flat", [](i64 p, i64 g, i64 mm, i64 v, i64 shadow, i64 n, i64 gmul, float lr, float b1, float b2,
-                        float eps, float wd, float step_size, i64 st) {
+                        float eps, float wd, float step_size, i64 st, i64 hyper) {
     launch_adam_flat(P(float*, p), P(const float*, g), P(float*, mm), P(float*, v), P(void*, shadow), n,
-                     P(const float*, gmul), lr, b1, b2, eps, wd, step_size, ST(st));
+                     P(const float*, gmul), lr, b1, b2, eps, wd, step_size, P(const float*, hyper), ST(st));
     check_launch("adam_flat");
-  });
+  }, pybind11::arg("p"), pybind11::arg("g"), pybind11::arg("m"), pybind11::arg("v"), pybind11::arg("shadow"),
+     pybind11::arg("n"), pybind11::arg("gmul"), pybind11::arg("lr"), pybind11::arg("b1"), pybind11::arg("b2"),
+     pybind11::arg("eps"), pybind11::arg("wd"), pybind11::arg("step_size"), pybind11::arg("st"),
+     pybind11::arg("hyper") = 0);
   m.def("adadelta_flat", [](i64 p, i64 g, i64 sq, i64 acc, i64 shadow, i64 n, i64 gmul, float lr, float rho, float eps,
                             float wd, i64 st) {
     launch_adadelta_flat(P(float*, p), P(const float*, g), P(float*, sq), P(float*, acc), P(void*, shadow), n,
@@ -210,6 +218,7 @@ PYBIND11_MODULE(_hip, m) {
   });
 
   // returns 0 when launched, -1 when the shape/epilogue is not served (caller falls back)
+  m.def("set_seed_ptr", [](i64 ptr) { hs::g_seed_dev = reinterpret_cast<const uint64_t*>(ptr); });
   m.def("gemm", [](int dt, int ta, int tb, int M, int N, int K, i64 A, i64 lda, i64 B, i64 ldb, i64 C, i64 ldc, i64 bias,
                    int epi, float beta, i64 aux, i64 ldaux, i64 part, i64 colsum, int colsum_acc, i64 st,
                    int tile) {

@@ -96,6 +96,13 @@ HS_DEVICE void keep4(uint64_t seed, uint64_t offset, uint64_t q, float p, float 
   m[3] = u01(r.w) >= p ? scale : 0.f;
 }
 
+// Dropout seed source.  Normally the per-update seed is a kernel argument; in
+// HIP-graph mode (runtime/graphs.py) the captured launches must not bake it in,
+// so launchers pass g_seed_dev -- a device word the host refreshes before every
+// replay -- and kernels read it instead.  Set through the `set_seed_ptr` binding.
+extern const uint64_t* g_seed_dev;
+HS_DEVICE uint64_t resolve_seed(uint64_t seed, const uint64_t* seed_dev) { return seed_dev ? *seed_dev : seed; }
+
 // 16-bit dropout decisions: one Philox call -> 8 keep bits (bit e: element e of the
 // group), keep iff the 16-bit uniform >= thr16 = round(p * 65536).  Halves the RNG
 // cost of keep4 where a kernel needs bits rather than 24-bit uniforms.

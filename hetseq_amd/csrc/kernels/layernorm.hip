@@ -46,10 +46,12 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const T* __restrict__ a, co
                                                      const float* __restrict__ beta, T* __restrict__ y,
                                                      float* __restrict__ zsave, float* __restrict__ mean_out,
                                                      float* __restrict__ rstd_out, int rows, float eps, float p,
-                                                     uint64_t seed, uint64_t off, int mode) {
+                                                     uint64_t seed, uint64_t off, int mode,
+                                                     const uint64_t* __restrict__ seed_dev) {
   constexpr int H = NV * 256;
   const int lane = threadIdx.x & 63;
   const float scale = p < 1.f ? 1.0f / (1.0f - p) : 0.f;
+  seed = resolve_seed(seed, seed_dev);
   for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += gridDim.x * 4) {
     const int64_t base = (int64_t)row * H;
     float x[NV][4];
@@ -116,11 +118,13 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, c
                                                      const float* __restrict__ gamma, T* __restrict__ dz_out,
                                                      T* __restrict__ da_out, float* __restrict__ part_gamma,
                                                      float* __restrict__ part_beta, float* __restrict__ part_bias,
-                                                     int rows, float p, uint64_t seed, uint64_t off, int mode) {
+                                                     int rows, float p, uint64_t seed, uint64_t off, int mode,
+                                                     const uint64_t* __restrict__ seed_dev) {
   constexpr int H = NV * 256;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int lane = threadIdx.x & 63;
   const float scale = p < 1.f ? 1.0f / (1.0f - p) : 0.f;
+  seed = resolve_seed(seed, seed_dev);
   float ag[NV][4], ab[NV][4], abias[NV][4];
 #pragma unroll
   for (int k = 0; k < NV; ++k)
@@ -183,10 +187,11 @@ __global__ void __launch_bounds__(256) emb_fwd_kernel(const int64_t* __restrict_
                                                       float* __restrict__ zsave, float* __restrict__ mean_out,
                                                       float* __restrict__ rstd_out, int rows, int S, int V, int TV,
                                                       float eps, float p, uint64_t seed, uint64_t off,
-                                                      int* __restrict__ err) {
+                                                      int* __restrict__ err, const uint64_t* __restrict__ seed_dev) {
   constexpr int H = NV * 256;
   const int lane = threadIdx.x & 63;
   const float scale = p < 1.f ? 1.0f / (1.0f - p) : 0.f;
+  seed = resolve_seed(seed, seed_dev);
   for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += gridDim.x * 4) {
     const int64_t base = (int64_t)row * H;
     int64_t id = ids[row];
@@ -242,11 +247,13 @@ __global__ void __launch_bounds__(256) emb_bwd_kernel(const T* __restrict__ dy, 
                                                       const float* __restrict__ gamma, float* __restrict__ dx_out,
                                                       float* __restrict__ part_gamma, float* __restrict__ part_beta,
                                                       const int64_t* __restrict__ tt, float* __restrict__ part_type,
-                                                      int rows, float p, uint64_t seed, uint64_t off) {
+                                                      int rows, float p, uint64_t seed, uint64_t off,
+                                                      const uint64_t* __restrict__ seed_dev) {
   constexpr int H = NV * 256;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int lane = threadIdx.x & 63;
   const float scale = p < 1.f ? 1.0f / (1.0f - p) : 0.f;
+  seed = resolve_seed(seed, seed_dev);
   float ag[NV][4], ab[NV][4], at0[NV][4], at1[NV][4];
 #pragma unroll
   for (int k = 0; k < NV; ++k)
@@ -308,7 +315,7 @@ void ln_fwd_launch(const void* a, const float* bias, const void* resid, const fl
   int grid = (rows + 3) / 4;
   if (grid > 4096) grid = 4096;
   hipLaunchKernelGGL((ln_fwd_kernel<NV, T>), dim3(grid), dim3(256), 0, st, (const T*)a, bias, (const T*)resid, gamma,
-                     beta, (T*)y, zsave, mean, rstd, rows, eps, p, seed, off, mode);
+                     beta, (T*)y, zsave, mean, rstd, rows, eps, p, seed, off, mode, g_seed_dev);
 }
 
 template <int NV, typename T>
@@ -317,7 +324,7 @@ void ln_bwd_launch(const void* dy, const float* zsave, const float* mean, const 
                    uint64_t off, int mode, hipStream_t st) {
   constexpr int H = NV * 256;
   hipLaunchKernelGGL((ln_bwd_kernel<NV, T>), dim3(kLnBwdBlocks), dim3(256), 4 * H * sizeof(float), st, (const T*)dy,
-                     zsave, mean, rstd, gamma, (T*)dz, (T*)da, pg, pb, pbias, rows, p, seed, off, mode);
+                     zsave, mean, rstd, gamma, (T*)dz, (T*)da, pg, pb, pbias, rows, p, seed, off, mode, g_seed_dev);
 }
 
 template <int NV, typename T>
@@ -327,7 +334,7 @@ void emb_fwd_launch(const int64_t* ids, const int64_t* tt, const float* w, const
   int grid = (rows + 3) / 4;
   if (grid > 4096) grid = 4096;
   hipLaunchKernelGGL((emb_fwd_kernel<NV, T>), dim3(grid), dim3(256), 0, st, ids, tt, w, pe, te, gamma, beta, (T*)y,
-                     zsave, mean, rstd, rows, S, V, TV, eps, p, seed, off, err);
+                     zsave, mean, rstd, rows, S, V, TV, eps, p, seed, off, err, g_seed_dev);
 }
 
 template <int NV, typename T>
@@ -336,7 +343,7 @@ void emb_bwd_launch(const void* dy, const float* zsave, const float* mean, const
                     uint64_t off, hipStream_t st) {
   constexpr int H = NV * 256;
   hipLaunchKernelGGL((emb_bwd_kernel<NV, T>), dim3(kLnBwdBlocks), dim3(256), 4 * H * sizeof(float), st,
-                     (const T*)dy, zsave, mean, rstd, gamma, dx, pg, pb, tt, pt, rows, p, seed, off);
+                     (const T*)dy, zsave, mean, rstd, gamma, dx, pg, pb, tt, pt, rows, p, seed, off, g_seed_dev);
 }
 
 }  // namespace hs

@@ -112,8 +112,13 @@ __global__ void __launch_bounds__(256) adam_flat_kernel(float* __restrict__ p, c
                                                         float* __restrict__ m, float* __restrict__ v,
                                                         bf16_t* __restrict__ shadow, int64_t n,
                                                         const float* __restrict__ gmul, float lr, float b1,
-                                                        float b2, float eps, float wd, float step_size) {
+                                                        float b2, float eps, float wd, float step_size,
+                                                        const float* __restrict__ hyper) {
   const float mul = gmul ? gmul[0] : 1.0f;
+  if (hyper) {  // HIP-graph mode: per-update lr and bias-corrected step size from device memory
+    lr = hyper[0];
+    step_size = hyper[1];
+  }
   const float omb1 = 1.0f - b1, omb2 = 1.0f - b2, decay = -wd * lr;
   const int64_t n4 = n >> 2;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -255,14 +260,15 @@ void launch_grad_norm(const float* g, int64_t n, double* partial, const float* s
 }
 
 void launch_adam_flat(float* p, const float* g, float* m, float* v, void* shadow, int64_t n, const float* gmul,
-                      float lr, float b1, float b2, float eps, float wd, float step_size, hipStream_t st) {
+                      float lr, float b1, float b2, float eps, float wd, float step_size, const float* hyper,
+                      hipStream_t st) {
   const int grid = grid_for(n / 4 + 1, 256, 8192);
   if (shadow)
     hipLaunchKernelGGL(adam_flat_kernel<true>, dim3(grid), dim3(256), 0, st, p, g, m, v,
-                       reinterpret_cast<bf16_t*>(shadow), n, gmul, lr, b1, b2, eps, wd, step_size);
+                       reinterpret_cast<bf16_t*>(shadow), n, gmul, lr, b1, b2, eps, wd, step_size, hyper);
   else
     hipLaunchKernelGGL(adam_flat_kernel<false>, dim3(grid), dim3(256), 0, st, p, g, m, v, nullptr, n, gmul, lr, b1,
-                       b2, eps, wd, step_size);
+                       b2, eps, wd, step_size, hyper);
 }
 
 void launch_adadelta_flat(float* p, const float* g, float* sq, float* acc, void* shadow, int64_t n,

@@ -127,9 +127,34 @@ class _Optimizer(object):
                 self._dev_scalars[2] = self._scale_tensor()[0]
         return self._dev_scalars[2:3]
 
-    def step(self, closure=None):
-        loss = closure() if closure is not None else None
+    # ------------------------------------------------------------ HIP-graph support
+    supports_device_hyper = False
+    _hyper = None
+
+    def enable_device_hyper(self, device):
+        """Per-update hyper-parameters come from device memory (HIP-graph replay)."""
+        from hetseq_amd.runtime.graphs import HostToDevice
+
+        if not self.supports_device_hyper:
+            raise NotImplementedError("%s has no device hyper-parameter path" % type(self).__name__)
+        self._hyper = HostToDevice(4, torch.float32, device)
+
+    def graph_prepare(self):
+        """Host half of step() for a graph replay: count the step, publish lr / step size."""
         self.step_count += 1
+        self._hyper.push(self._device_hyper_values())
+
+    def _device_hyper_values(self):
+        raise NotImplementedError
+
+    def step(self, closure=None, launch_only=False):
+        """``launch_only``: the step counter / hyper-parameters were already published by
+        :meth:`graph_prepare` (graph capture); only the kernel is launched."""
+        loss = closure() if closure is not None else None
+        if not launch_only:
+            self.step_count += 1
+            if self._hyper is not None:
+                self._hyper.push(self._device_hyper_values())
         if self.store is None:
             self._step_unfused()
         else:
@@ -222,12 +247,18 @@ class _Adam(_Optimizer):
     def optimizer_config(self):
         return {k: v for k, v in self.defaults().items() if k != "amsgrad"}
 
+    supports_device_hyper = True
+
     def _coeffs(self):
         g = self.param_groups[0]
         b1, b2 = g["betas"]
-        t = self.step_count
+        t = max(self.step_count, 1)
         step_size = g["lr"] * math.sqrt(1 - b2 ** t) / (1 - b1 ** t)
         return g["lr"], b1, b2, g["eps"], g["weight_decay"], step_size
+
+    def _device_hyper_values(self):
+        lr, _, _, _, _, step_size = self._coeffs()
+        return [lr, step_size, 0.0, 0.0]
 
     def _step_hip(self, gmul):
         lr, b1, b2, eps, wd, step_size = self._coeffs()
@@ -235,7 +266,7 @@ class _Adam(_Optimizer):
         shadow = s.shadow.data_ptr() if s.shadow is not None else 0
         hip().adam_flat(s.param.data_ptr(), s.grad.data_ptr(), self._state["exp_avg"].data_ptr(),
                         self._state["exp_avg_sq"].data_ptr(), shadow, s.numel, gmul.data_ptr(), lr, b1, b2, eps, wd,
-                        step_size, stream_handle())
+                        step_size, stream_handle(), self._hyper.dev.data_ptr() if self._hyper is not None else 0)
 
     def _step_cpu(self, gmul):
         lr, b1, b2, eps, wd, step_size = self._coeffs()

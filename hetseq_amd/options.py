@@ -21,6 +21,7 @@ change a reference default):
   --profile                 roctx ranges + per-phase hipEvent timing
   --no-gemm-tuning          skip the measured GEMM selection table
   --deterministic           bitwise-reproducible mode (fixed RCCL algorithm, deterministic torch ops)
+  --hip-graph               replay the captured update as one HIP graph (launch-bound configurations)
 """
 from __future__ import annotations
 
@@ -212,6 +213,9 @@ def add_mi355x_args(parser):
     group.add_argument("--json-log", type=str, default=None, metavar="PATH",
                        help="append one JSON object per logged update")
     group.add_argument("--profile", action="store_true", help="roctx ranges and per-phase hipEvent timing")
+    group.add_argument("--hip-graph", action="store_true",
+                       help="capture the whole update (forward, backward, clip, Adam) in a HIP graph after a few "
+                            "eager warm-up updates and replay it (single process, --fast-stat-sync, update-freq 1)")
     group.add_argument("--deterministic", action="store_true",
                        help="bitwise-reproducible mode: deterministic torch algorithms, fixed RCCL ring/simple "
                             "protocol, no tuned GEMM table (library split-K solutions may use atomics)")

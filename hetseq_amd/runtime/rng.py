@@ -9,12 +9,45 @@ backward pass, which regenerates the mask bit-identically.
 """
 import threading
 
+import torch
+
 _state = threading.local()
+
+
+_device_seed = None  # HostToDevice when the kernels read the seed from device memory (HIP graphs)
+
+
+def enable_device_seed(device):
+    """Make every dropout kernel read the seed from a device word (graph replays re-seed through it)."""
+    global _device_seed
+    from hetseq_amd.ops._C import hip
+    from hetseq_amd.runtime.graphs import HostToDevice
+
+    if _device_seed is None:
+        _device_seed = HostToDevice(1, torch.int64, device)
+        hip().set_seed_ptr(_device_seed.dev.data_ptr())
+    if hasattr(_state, "seed"):
+        _device_seed.push([_to_i64(_state.seed)])
+
+
+def disable_device_seed():
+    global _device_seed
+    if _device_seed is not None:
+        from hetseq_amd.ops._C import hip
+
+        hip().set_seed_ptr(0)
+        _device_seed = None
+
+
+def _to_i64(u):
+    return u - (1 << 64) if u >= (1 << 63) else u
 
 
 def set_seed(seed: int):
     _state.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
     _state.offset = 0
+    if _device_seed is not None:
+        _device_seed.push([_to_i64(_state.seed)])
 
 
 def get_seed() -> int:

@@ -75,7 +75,8 @@ class Task(object):
         raise NotImplementedError
 
     def train_step(self, sample, model, optimizer, ignore_grad=False):
-        model.train()
+        if not model.training:  # train() walks every submodule: only on a mode change
+            model.train()
         loss = model(*sample)
         if ignore_grad:
             loss = loss * 0

@@ -149,6 +149,40 @@ def test_attention_fwd_bwd(cuda, B, S, NH):
     _close(qkv.grad, qkv2.grad, 1e-4, 1e-5, "attn dqkv")
 
 
+@pytest.mark.parametrize("B,S,NH", [(2, 128, 12), (2, 96, 2), (1, 512, 2)])
+def test_attention_fwd_bf16_mfma(cuda, B, S, NH, monkeypatch):
+    """bf16 matrix-core forward vs an fp64 reference on the same bf16 inputs (+ bias), and vs the fp32-MFMA path."""
+    from hetseq_amd.ops import bert_ops
+
+    torch.manual_seed(21)
+    H = NH * 64
+    qkv = torch.randn(B * S, 3 * H, device=cuda).bfloat16()
+    bias = torch.randn(3 * H, device=cuda) * 0.1
+    mask = torch.ones(B, S, dtype=torch.int64, device=cuda)
+    mask[-1, S // 3:] = 0
+    out, (lse, _) = bert_ops.attn_fwd(qkv, mask, B, S, NH, 0.0, 0, 0, bias=bias)
+    ref = _ref_attention((qkv.double() + bias.double()), mask, B, S, NH)
+    _close(out, ref, 2e-2, 2e-2, "bf16 mfma attention fwd")
+    monkeypatch.setenv("HETSEQ_ATTN_BF16_MFMA", "0")
+    out32, (lse32, _) = bert_ops.attn_fwd(qkv, mask, B, S, NH, 0.0, 0, 0, bias=bias)
+    _close(out, out32, 2e-2, 2e-2, "bf16 mfma vs fp32-mfma path")
+    _close(lse, lse32, 1e-2, 2e-2, "lse")
+
+
+def test_attention_bf16_mfma_dropout_bits_match(cuda, monkeypatch):
+    """The bf16 forward draws the same keep bits as the fp32 forward (shared Philox stream)."""
+    from hetseq_amd.ops import bert_ops
+
+    torch.manual_seed(22)
+    B, S, NH = 2, 128, 4
+    qkv = torch.randn(B * S, 3 * NH * 64, device=cuda).bfloat16()
+    mask = torch.ones(B, S, dtype=torch.int64, device=cuda)
+    _, (_, bits) = bert_ops.attn_fwd(qkv, mask, B, S, NH, 0.1, 9, 4)
+    monkeypatch.setenv("HETSEQ_ATTN_BF16_MFMA", "0")
+    _, (_, bits32) = bert_ops.attn_fwd(qkv, mask, B, S, NH, 0.1, 9, 4)
+    assert torch.equal(bits, bits32)
+
+
 @pytest.mark.parametrize("S", [32, 96, 128])
 def test_attention_bwd_fused_matches_split(cuda, S, monkeypatch):
     """The one-block-per-head fused backward (S <= 128) equals the two-kernel path, with dropout + bias."""
