@@ -619,6 +619,10 @@ int launch_attn_fwd_bf16(const void* qkv, const int64_t* mask, const float* bqkv
                          uint32_t* dmask, int B, int S, int NH, int D, float p, uint64_t seed, uint64_t off,
                          hipStream_t st);
 
+int launch_attn_bwd_fused_bf16(const void* qkv, const int64_t* mask, const float* bqkv, const void* ctx,
+                               const void* dctx, const float* lse, void* dqkv, const uint32_t* dmask, int B, int S,
+                               int NH, int D, float p, hipStream_t st);
+
 // HETSEQ_ATTN_BF16_MFMA=0 keeps bf16 attention on the fp32-MFMA kernels (A/B and tests)
 static bool bf16_mfma_enabled() {
   const char* e = std::getenv("HETSEQ_ATTN_BF16_MFMA");
@@ -654,6 +658,8 @@ int launch_attn_bwd(int dtype, const void* qkv, const int64_t* mask, const float
                     int NH, int D, float p, hipStream_t st) {
   if (D != kD || S % 32 != 0 || S <= 0 || (p > 0.f && dmask == nullptr)) return -1;
   if (S <= 128 && fused_bwd_enabled()) {  // one block per (batch, head): 5 products instead of 7
+    if (dtype != 0 && bf16_mfma_enabled())
+      return launch_attn_bwd_fused_bf16(qkv, mask, bqkv, ctx, dctx, lse, dqkv, dmask, B, S, NH, D, p, st);
     if (dtype == 0)
       hipLaunchKernelGGL(attn_bwd_fused_kernel<float>, dim3(B * NH), dim3(512), 0, st, (const float*)qkv, mask, bqkv,
                          (const float*)ctx, (const float*)dctx, lse, (float*)dqkv, S, NH, p, dmask);

@@ -169,6 +169,30 @@ def test_attention_fwd_bf16_mfma(cuda, B, S, NH, monkeypatch):
     _close(lse, lse32, 1e-2, 2e-2, "lse")
 
 
+@pytest.mark.parametrize("S,p", [(128, 0.0), (128, 0.1), (96, 0.1), (32, 0.0)])
+def test_attention_bwd_bf16_mfma(cuda, S, p, monkeypatch):
+    """bf16 matrix-core fused backward vs the fp32-MFMA fused backward on the same bf16 inputs."""
+    from hetseq_amd.ops import bert_ops
+
+    torch.manual_seed(23)
+    B, NH = 2, 4
+    H = NH * 64
+    qkv = torch.randn(B * S, 3 * H, device=cuda).bfloat16()
+    bias = torch.randn(3 * H, device=cuda) * 0.1
+    mask = torch.ones(B, S, dtype=torch.int64, device=cuda)
+    mask[1, S // 2:] = 0
+    out, lse = bert_ops.attn_fwd(qkv, mask, B, S, NH, p, 5, 7, bias=bias)
+    dout = torch.randn_like(out)
+    g16 = bert_ops.attn_bwd(qkv, mask, out, dout, lse, B, S, NH, p, bias=bias)
+    monkeypatch.setenv("HETSEQ_ATTN_BF16_MFMA", "0")
+    g32 = bert_ops.attn_bwd(qkv, mask, out, dout, lse, B, S, NH, p, bias=bias)
+    _close(g16, g32, 3e-2, 3e-2, "bf16 mfma attention backward")
+    if p == 0.0:  # and against fp64 autograd on the bf16 inputs
+        x = (qkv.double() + bias.double()).requires_grad_()
+        _ref_attention(x, mask, B, S, NH).backward(dout.double())
+        _close(g16, x.grad, 3e-2, 3e-2, "bf16 mfma attention backward vs fp64")
+
+
 def test_attention_bf16_mfma_dropout_bits_match(cuda, monkeypatch):
     """The bf16 forward draws the same keep bits as the fp32 forward (shared Philox stream)."""
     from hetseq_amd.ops import bert_ops
