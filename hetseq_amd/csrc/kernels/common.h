@@ -66,8 +66,10 @@ struct Philox {
              c3 = static_cast<uint32_t>(counter_hi >> 32);
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-      const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
-      const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+      // one 32x32->64 multiply each (v_mad_u64_u32) instead of separate mul_hi / mul_lo
+      const uint64_t p0 = static_cast<uint64_t>(0xD2511F53u) * c0, p1 = static_cast<uint64_t>(0xCD9E8D57u) * c2;
+      const uint32_t hi0 = static_cast<uint32_t>(p0 >> 32), lo0 = static_cast<uint32_t>(p0);
+      const uint32_t hi1 = static_cast<uint32_t>(p1 >> 32), lo1 = static_cast<uint32_t>(p1);
       c0 = hi1 ^ c1 ^ k0;
       c1 = lo1;
       c2 = hi0 ^ c3 ^ k1;
