@@ -97,3 +97,38 @@ def write_mnist(root, n_train=512, n_test=128, seed=0):
             images[sel, 2 + 2 * c : 6 + 2 * c, 4:24] += 180
         torch.save((images.clamp(0, 255).to(torch.uint8), labels), os.path.join(d, name))
     return root
+
+
+def main(argv=None):
+    """``python -m hetseq_amd.data.synthetic OUT_DIR``: a ready-to-train synthetic BERT corpus
+    (train/test shards, vocab.txt, bert_config.json) or MNIST tensors (``--mnist``)."""
+    import argparse
+
+    ap = argparse.ArgumentParser(description=main.__doc__)
+    ap.add_argument("out_dir")
+    ap.add_argument("--mnist", action="store_true", help="write MNIST/processed/{training,test}.pt instead")
+    ap.add_argument("--shards", type=int, default=4)
+    ap.add_argument("--per-shard", type=int, default=4096, help="sequences per shard")
+    ap.add_argument("--seq-len", type=int, default=128)
+    ap.add_argument("--max-pred", type=int, default=20, help="20 for phase 1 (seq 128), 80 for phase 2 (seq 512)")
+    ap.add_argument("--vocab-size", type=int, default=30522)
+    ap.add_argument("--gzip", type=int, default=0, help="gzip level of the HDF5 datasets (0 = contiguous)")
+    ap.add_argument("--seed", type=int, default=0)
+    a = ap.parse_args(argv)
+    if a.mnist:
+        write_mnist(a.out_dir, seed=a.seed)
+        print("| wrote %s/MNIST/processed" % a.out_dir)
+        return
+    data = os.path.join(a.out_dir, "data")
+    for split, n in (("train", a.shards), ("test", 1)):
+        write_bert_shards(data, num_shards=n, per_shard=a.per_shard, seq_len=a.seq_len, max_pred=a.max_pred,
+                          vocab_size=a.vocab_size, seed=a.seed + (0 if split == "train" else 7919), split=split,
+                          gzip_level=a.gzip)
+    write_vocab(os.path.join(a.out_dir, "vocab.txt"), a.vocab_size)
+    write_bert_config(os.path.join(a.out_dir, "bert_config.json"), vocab_size=a.vocab_size)
+    print("| wrote %s: --data %s --dict %s --config_file %s" % (a.out_dir, data, os.path.join(a.out_dir, "vocab.txt"),
+                                                             os.path.join(a.out_dir, "bert_config.json")))
+
+
+if __name__ == "__main__":
+    main()

@@ -158,3 +158,16 @@ def test_mnist_dataset_transform(tmp_path):
     assert img.shape == (1, 28, 28) and torch.allclose(img[0], ref) and y == int(labels[3])
     x, t = ds.collater([ds[0], ds[1]])
     assert x.shape == (2, 1, 28, 28) and t.dtype == torch.int64
+
+
+def test_synthetic_corpus_cli(tmp_path):
+    """python -m hetseq_amd.data.synthetic produces a corpus the BERT task loads."""
+    from hetseq_amd.data.bert_dataset import BertH5Dataset
+    from hetseq_amd.data.synthetic import main
+
+    main([str(tmp_path), "--shards", "2", "--per-shard", "40", "--vocab-size", "500"])
+    files = sorted(os.listdir(tmp_path / "data"))
+    assert sum("train" in f for f in files) == 2 and sum("test" in f for f in files) == 1
+    ds = BertH5Dataset(str(tmp_path / "data" / [f for f in files if "train" in f][0]), 20)
+    assert len(ds) == 40
+    assert (tmp_path / "vocab.txt").exists() and (tmp_path / "bert_config.json").exists()
