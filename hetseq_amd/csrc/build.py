@@ -105,8 +105,56 @@ def build_h5(verbose=False, jobs=4):
     objs, changed = _compile_objs("g++", flags, [src], [], os.path.join(BUILD_DIR, "h5"), verbose, jobs)
     out = os.path.join(PKG, "_h5" + EXT)
     # Link the real soname file so the loader never needs the dev symlink.
-    _link("g++", objs, out, ["-pthread", "-L" + lib, "-lhdf5", "-Wl,-rpath," + lib], verbose, changed)
+    # static libstdc++: the rpath to the HDF5 prefix would otherwise pick its older libstdc++
+    _link("g++", objs, out, ["-pthread", "-static-libstdc++", "-static-libgcc", "-L" + lib, "-lhdf5", "-Wl,-rpath," + lib],
+          verbose, changed)
     return out
+
+
+SAN_FLAGS = ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined",
+             "-shared-libsan"]
+SAN_CXX = os.path.join(ROCM, "lib", "llvm", "bin", "clang++")
+
+
+def asan_runtime():
+    """Path of the clang ASan runtime the sanitized modules need preloaded."""
+    import glob
+
+    hits = sorted(glob.glob(os.path.join(ROCM, "lib", "llvm", "lib", "clang", "*", "lib", "linux",
+                                         "libclang_rt.asan-x86_64.so")))
+    return hits[-1] if hits else None
+
+
+def build_sanitized(outdir=None, verbose=False, jobs=4):
+    """ASan+UBSan builds of the host runtime (batcher, HDF5 IO) for the sanitizer test.
+
+    Built with the ROCm LLVM clang (its runtime copes with this kernel's
+    high-entropy mmap layout; the gcc 11 runtime does not).  The modules keep
+    their import names (``_native``, ``_h5``) but land in ``outdir`` (default
+    ``build/native/asan``) so they never shadow the in-tree ones;
+    ``tools/asan_native.py`` loads them with ``LD_PRELOAD=asan_runtime()``.
+    Host code only: GPU sanitizers are not used on this platform.
+    """
+    outdir = outdir or os.path.join(BUILD_DIR, "asan")
+    os.makedirs(outdir, exist_ok=True)
+    pyinc = ["-I" + p for p in _py_includes()]
+    base = ["-std=c++17", "-fPIC", "-Wall"] + SAN_FLAGS
+    nsrc = os.path.join(HERE, "native", "batcher.cpp")
+    objs, changed = _compile_objs(SAN_CXX, base + pyinc, [nsrc], [], os.path.join(outdir, "obj-native"), verbose, jobs)
+    outs = [os.path.join(outdir, "_native" + EXT)]
+    _link(SAN_CXX, objs, outs[0], ["-pthread"] + SAN_FLAGS, verbose, changed)
+    inc, lib = os.path.join(HDF5_ROOT, "include"), os.path.join(HDF5_ROOT, "lib")
+    if os.path.exists(os.path.join(inc, "hdf5.h")):
+        hsrc = os.path.join(HERE, "native", "h5shard.cpp")
+        objs, changed = _compile_objs(SAN_CXX, base + ["-I" + inc] + pyinc, [hsrc], [],
+                                      os.path.join(outdir, "obj-h5"), verbose, jobs)
+        outs.append(os.path.join(outdir, "_h5" + EXT))
+        # libhdf5 by path, not -L (the HDF5 prefix ships older sanitizer runtimes and libstdc++);
+        # the system libstdc++ directory is searched before the HDF5 prefix at run time
+        sysdir = "/usr/lib/x86_64-linux-gnu"
+        _link(SAN_CXX, objs, outs[1], ["-pthread"] + SAN_FLAGS + [os.path.join(lib, "libhdf5.so"),
+              "-Wl,-rpath," + sysdir + ":" + lib], verbose, changed)
+    return outs
 
 
 def hip_sources():

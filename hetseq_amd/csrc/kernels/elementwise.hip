@@ -61,7 +61,27 @@ __global__ void __launch_bounds__(256) colsum_tile_kernel(const T* __restrict__ 
   float bb[4] = {0.f, 0.f, 0.f, 0.f};
   if (kGelu) load4(b + c, bb);
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int64_t r = r0; r < r1; ++r) {
+  int64_t r = r0;
+  // 4 rows per step with every load issued first: the strip walk is latency-bound otherwise
+  for (; r + 4 <= r1; r += 4) {
+    float d[4][4], v[4][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      load4(dy + (r + u) * N + c, d[u]);
+      if (kGelu) load4(x + (r + u) * N + c, v[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (kGelu) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d[u][j] *= gelu_grad_f(v[u][j] + bb[j]);
+        store4(dx + (r + u) * N + c, d[u]);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] += d[u][j];
+    }
+  }
+  for (; r < r1; ++r) {
     const int64_t o = r * N + c;
     float d[4];
     load4(dy + o, d);
@@ -216,8 +236,13 @@ __global__ void __launch_bounds__(256) seg_combine_kernel(const float* __restric
   const int i = blockIdx.x;
   const int64_t key = keys[i];
   if ((i > 0 && keys[i - 1] == key) || key < 0 || key >= K) return;
-  int end = i + 1;
-  while (end < n && keys[end] == key) ++end;
+  // keys are sorted: binary-search the run end instead of walking it (runs like [PAD] span thousands of rows)
+  int lo = i + 1, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (keys[mid] == key) lo = mid + 1; else hi = mid;
+  }
+  const int end = lo;
   for (int c = threadIdx.x * 4; c < H; c += blockDim.x * 4) {
     // pieces: the run's first chunk, then one per further chunk; 4 independent
     // accumulators keep 4 loads in flight for long runs (fixed combine order)
@@ -325,8 +350,8 @@ void launch_bias_tanh_fwd(int dtype, const void* x, const float* b, void* y, int
 }
 
 int colsum_row_chunks(int64_t rows) {
-  int chunks = (int)((rows + 31) / 32);
-  if (chunks > 256) chunks = 256;
+  int chunks = (int)((rows + 15) / 16);  // >= 2 blocks per CU for the 3072-wide FFN strip
+  if (chunks > 512) chunks = 512;
   if (chunks < 1) chunks = 1;
   return chunks;
 }

@@ -482,10 +482,12 @@ class FusedMLMLoss(torch.autograd.Function):
         acc = Gv is not None
         dlogits = xent_bwd_(logits, lab, lse, dloss.reshape(1).float().contiguous(), out)  # in place, fp32
         # tied decoder weight: accumulates into the word-embedding gradient
-        dWdec = G.linear_wgrad(dlogits, t2.float() if t2.dtype != torch.float32 else t2,
-                               out=Gv[4] if acc else None, accumulate=acc)
+        # bf16 mode: both decoder GEMMs take bf16 operands (fp32 C for the weight gradient);
+        # the fp32-operand weight GEMM cost 268 us vs 72 us (tools/bench_mlm_head.py)
+        dl_c = dlogits.to(t2.dtype) if t2.dtype != torch.float32 else dlogits
+        dWdec = G.linear_wgrad(dl_c, t2, out=Gv[4] if acc else None, accumulate=acc)
         dbdec = colsum(dlogits, acc=Gv[5] if acc else None)
-        dt2 = G.gemm(dlogits.to(t2.dtype) if t2.dtype != torch.float32 else dlogits, Wd)
+        dt2 = G.gemm(dl_c, Wd)
         dt1, _, dg, db, _ = ln_bwd(dt2, z, mean, rstd, g, 0.0, 0, acc=(Gv[2], Gv[3]) if acc else None)
         dt1pre, dbt = gelu_bwd_colsum(dt1, t1pre, bt, db_acc=Gv[1] if acc else None)
         dWt = G.linear_wgrad(dt1pre, hsel, out=Gv[0] if acc else None, accumulate=acc)
