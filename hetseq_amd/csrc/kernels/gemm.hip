@@ -31,6 +31,8 @@
 // The launcher only serves shapes that tile exactly (M % BM, N % BN, K % 32,
 // 16-B aligned operands); anything else returns -1 and the caller uses the
 // library GEMM.
+#include <algorithm>
+
 #include "common.h"
 #include "reduce.h"
 
@@ -72,6 +74,8 @@ struct GemmArgs {
   int64_t lda, ldb, ldc, ldaux;
   int M, N, K;
   float beta;
+  int ksplit;   // >1: K is cut into ksplit slices, each writes a plain slab (no epilogue)
+  float* slab;  // [ksplit][M][N] partial products (summed by splitk_reduce_kernel)
 };
 
 // LDS image geometry of one operand (rows = BM or BN).  The [k][mn] image is
@@ -129,75 +133,58 @@ HS_DEVICE float4 frag(const float* __restrict__ S, int row, int g, int lr, int q
 
 HS_DEVICE float comp(const float4& v, int s) { return s == 0 ? v.x : s == 1 ? v.y : s == 2 ? v.z : v.w; }
 
-template <int BM, int BN, int MF, bool TA, bool TB, int EPI, int ABL = 0>
-__global__ void __launch_bounds__(256, 2) gemm_f32_kernel(GemmArgs p) {
-  using IA = Img<BM, !TA, MF>;
-  using IB = Img<BN, TB, MF>;
-  using M_ = Mf<MF>;
-  constexpr int TM = BM / 2 / MF, TN = BN / 2 / MF, NQ = 64 / MF, KG = 4 * NQ;
-  __shared__ __attribute__((aligned(16))) float smem[2 * (IA::size + IB::size)];
-  float* const As0 = smem;                 // A buffers at [0, 2*IA::size)
-  float* const Bs0 = smem + 2 * IA::size;  // B buffers after them
+// ---------------------------------------------------------------------------
+// fp32 products on the bf16 matrix cores.  CDNA4 runs v_mfma_f32_32x32x2_f32 at
+// 1/16 of the bf16 rate (64 vs 1024 FLOP/clk/SIMD) and has no xf32, so an fp32
+// operand x is split (round-to-nearest-even each time) into three bf16 terms
+//   x = hi + mid + lo + r,   |r| <= 2^-27 |x|
+// and a*b is summed from the 6 cross products of order <= 2^-16 (hi*hi, hi*mid,
+// mid*hi, hi*lo, lo*hi, mid*mid; the dropped mid*lo, lo*mid, lo*lo are
+// <= 2^-24 |a b|, the size of one fp32 rounding).  Every bf16 x bf16 product is
+// exact in the fp32 accumulator, so the result carries fp32-level error
+// (tests/test_gemm_x6_gpu.py measures it against fp64 next to the exact-fp32
+// MFMA kernel) at 6/16 of the f32 MFMA's cycles.  NT = 3 keeps only
+// hi*hi + hi*mid + mid*hi (two-term split, ~2^-16 relative: NOT fp32 accuracy,
+// a benchmarking variant only).
+typedef __bf16 bfx8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bfx2 __attribute__((ext_vector_type(2)));
+typedef float fx2 __attribute__((ext_vector_type(2)));
 
-  const int tiles_m = p.M / BM, tiles_n = p.N / BN, nwg = tiles_m * tiles_n;
-  const int orig = blockIdx.x;
-  const int xcd = orig % 8, qq = nwg / 8, rr = nwg % 8;
-  const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + orig / 8;
-  const int tm = wg % tiles_m, tn = wg / tiles_m;  // M fastest: neighbours share the B panel
-  const int m0 = tm * BM, n0 = tn * BN;
-
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int wr = w >> 1, wc = w & 1;
-  const int wm = wr * (BM / 2), wn = wc * (BN / 2);
-  const int lr = lane % MF, q = lane / MF;
-
-  typename M_::acc_t acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = typename M_::acc_t{};
-
-  float4 ra[IA::nld], rb[IB::nld];
-  const int KT = p.K / GBK;
-  g_load<BM, !TA>(p.A, p.lda, m0, 0, ra);
-  g_load<BN, TB>(p.B, p.ldb, n0, 0, rb);
-  s_store<BM, !TA, MF>(As0, ra);
-  s_store<BN, TB, MF>(Bs0, rb);
-  __syncthreads();
-  for (int kt = 0; kt < KT; ++kt) {
-    const int cur = kt & 1;
-    // prefetch the next K tile (the last iteration re-reads the final tile into the idle
-    // buffer: keeps the staging registers unconditional, so they stay in VGPRs)
-    const int kn = (kt + 1 < KT ? kt + 1 : kt) * GBK;
-    if (ABL == 0) {  // ABL: ablation builds for the microbenchmark (1: no global loads, 2: + no LDS writes/barrier)
-      g_load<BM, !TA>(p.A, p.lda, m0, kn, ra);
-      g_load<BN, TB>(p.B, p.ldb, n0, kn, rb);
-    }
-    const float* as = As0 + cur * IA::size;
-    const float* bs = Bs0 + cur * IB::size;
-#pragma unroll
-    for (int g = 0; g < GBK / KG; ++g) {
-      float4 av[TM], bv[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) av[i] = frag<BM, !TA, MF>(as, wm + MF * i, g, lr, q);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) bv[j] = frag<BN, TB, MF>(bs, wn + MF * j, g, lr, q);
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) acc[i][j] = M_::mma(comp(av[i], s), comp(bv[j], s), acc[i][j]);
-    }
-    // the other buffer was last read before the previous barrier
-    if (ABL < 2) {
-      s_store<BM, !TA, MF>(As0 + (cur ^ 1) * IA::size, ra);
-      s_store<BN, TB, MF>(Bs0 + (cur ^ 1) * IB::size, rb);
-    }
-    if (ABL < 2) __syncthreads();
+template <int NT>
+HS_DEVICE void split4(float4 x, uint2& hi, uint2& mi, uint2& lo) {
+  const fx2 x0 = {x.x, x.y}, x1 = {x.z, x.w};
+  const bfx2 h0 = __builtin_convertvector(x0, bfx2), h1 = __builtin_convertvector(x1, bfx2);
+  const fx2 r0 = x0 - __builtin_convertvector(h0, fx2), r1 = x1 - __builtin_convertvector(h1, fx2);
+  const bfx2 m0 = __builtin_convertvector(r0, bfx2), m1 = __builtin_convertvector(r1, bfx2);
+  hi = make_uint2(__builtin_bit_cast(uint32_t, h0), __builtin_bit_cast(uint32_t, h1));
+  mi = make_uint2(__builtin_bit_cast(uint32_t, m0), __builtin_bit_cast(uint32_t, m1));
+  if (NT >= 6) {
+    const bfx2 l0 = __builtin_convertvector(r0 - __builtin_convertvector(m0, fx2), bfx2);
+    const bfx2 l1 = __builtin_convertvector(r1 - __builtin_convertvector(m1, fx2), bfx2);
+    lo = make_uint2(__builtin_bit_cast(uint32_t, l0), __builtin_bit_cast(uint32_t, l1));
   }
+}
 
-  // epilogue: acc[i][j] register r -> row m0+wm+MF*i+Mf::row(r,q), col n0+wn+MF*j+lr
+HS_DEVICE f32x16 mma_bf(bfx8 a, bfx8 b, f32x16 c) { return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0); }
+
+// Shared GEMM epilogue (both kernels): split-K slab, or C = acc (+bias) (+beta*C) / GELU /
+// dGELU + column partial sums.  acc[i][j] register r -> row m0+wm+MF*i+Mf::row(r,q), col n0+wn+MF*j+lr.
+template <int BM, int BN, int MF, int EPI>
+HS_DEVICE void epilogue(const GemmArgs& p, typename Mf<MF>::acc_t (&acc)[BM / 2 / MF][BN / 2 / MF], float* smem, int m0,
+                        int n0, int tm, int slice, int wm, int wn, int wr, int lr, int q) {
+  using M_ = Mf<MF>;
+  constexpr int TM = BM / 2 / MF, TN = BN / 2 / MF;
+  if (p.ksplit > 1) {  // split-K: plain partial slab, bias / beta / sum in splitk_reduce_kernel
+    float* sl = p.slab + (int64_t)slice * p.M * p.N;
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < M_::nreg; ++r)
+          sl[(int64_t)(m0 + wm + MF * i + M_::row(r, q)) * p.N + n0 + wn + MF * j + lr] = acc[i][j][r];
+    return;
+  }
   float csum[TN];
   const bool use_beta = (EPI == kEpiNone || EPI == kEpiBias) && p.beta != 0.f;
 #pragma unroll
@@ -259,37 +246,312 @@ __global__ void __launch_bounds__(256, 2) gemm_f32_kernel(GemmArgs p) {
   }
 }
 
-static int g_ablation = 0;  // microbenchmark hook (tile_override bits 3-4)
+template <int BM, int BN, int MF, bool TA, bool TB, int EPI, int ABL = 0>
+__global__ void __launch_bounds__(256, 2) gemm_f32_kernel(GemmArgs p) {
+  using IA = Img<BM, !TA, MF>;
+  using IB = Img<BN, TB, MF>;
+  using M_ = Mf<MF>;
+  constexpr int TM = BM / 2 / MF, TN = BN / 2 / MF, NQ = 64 / MF, KG = 4 * NQ;
+  __shared__ __attribute__((aligned(16))) float smem[2 * (IA::size + IB::size)];
+  float* const As0 = smem;                 // A buffers at [0, 2*IA::size)
+  float* const Bs0 = smem + 2 * IA::size;  // B buffers after them
 
-template <int BM, int BN, int MF, bool TA, bool TB, int EPI>
-void launch_cfg(const GemmArgs& a, hipStream_t st) {
-  const int tiles = (a.M / BM) * (a.N / BN);
-  if (EPI == kEpiNone && g_ablation == 1)
-    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, MF, TA, TB, EPI, 1>), dim3(tiles), dim3(256), 0, st, a);
-  else if (EPI == kEpiNone && g_ablation == 2)
-    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, MF, TA, TB, EPI, 2>), dim3(tiles), dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, MF, TA, TB, EPI>), dim3(tiles), dim3(256), 0, st, a);
+  const int tiles_m = p.M / BM, tiles_n = p.N / BN, nwg = tiles_m * tiles_n * p.ksplit;
+  const int orig = blockIdx.x;
+  const int xcd = orig % 8, qq = nwg / 8, rr = nwg % 8;
+  const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + orig / 8;
+  // the K slices of one tile sit next to each other (same XCD); M fastest: neighbours share the B panel
+  const int slice = wg % p.ksplit, tile = wg / p.ksplit;
+  const int tm = tile % tiles_m, tn = tile / tiles_m;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kofs = slice * (p.K / p.ksplit);
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wr = w >> 1, wc = w & 1;
+  const int wm = wr * (BM / 2), wn = wc * (BN / 2);
+  const int lr = lane % MF, q = lane / MF;
+
+  typename M_::acc_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = typename M_::acc_t{};
+
+  float4 ra[IA::nld], rb[IB::nld];
+  const int KT = p.K / p.ksplit / GBK;
+  g_load<BM, !TA>(p.A, p.lda, m0, kofs, ra);
+  g_load<BN, TB>(p.B, p.ldb, n0, kofs, rb);
+  s_store<BM, !TA, MF>(As0, ra);
+  s_store<BN, TB, MF>(Bs0, rb);
+  __syncthreads();
+  for (int kt = 0; kt < KT; ++kt) {
+    const int cur = kt & 1;
+    // prefetch the next K tile (the last iteration re-reads the final tile into the idle
+    // buffer: keeps the staging registers unconditional, so they stay in VGPRs)
+    const int kn = kofs + (kt + 1 < KT ? kt + 1 : kt) * GBK;
+    if (ABL == 0) {  // ABL: ablation builds for the microbenchmark (1: no global loads, 2: + no LDS writes/barrier)
+      g_load<BM, !TA>(p.A, p.lda, m0, kn, ra);
+      g_load<BN, TB>(p.B, p.ldb, n0, kn, rb);
+    }
+    const float* as = As0 + cur * IA::size;
+    const float* bs = Bs0 + cur * IB::size;
+#pragma unroll
+    for (int g = 0; g < GBK / KG; ++g) {
+      float4 av[TM], bv[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) av[i] = frag<BM, !TA, MF>(as, wm + MF * i, g, lr, q);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bv[j] = frag<BN, TB, MF>(bs, wn + MF * j, g, lr, q);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = M_::mma(comp(av[i], s), comp(bv[j], s), acc[i][j]);
+    }
+    // the other buffer was last read before the previous barrier
+    if (ABL < 2) {
+      s_store<BM, !TA, MF>(As0 + (cur ^ 1) * IA::size, ra);
+      s_store<BN, TB, MF>(Bs0 + (cur ^ 1) * IB::size, rb);
+    }
+    if (ABL < 2) __syncthreads();
+  }
+
+  epilogue<BM, BN, MF, EPI>(p, acc, smem, m0, n0, tm, slice, wm, wn, wr, lr, q);
 }
 
-template <int BM, int BN, int MF>
+// ---------------------------------------------------------------------------
+// Split-bf16 kernel: 128x128 block tile, 4 waves (2x2, 64x64 each = 2x2 MFMA
+// tiles of 32x32x16), BK = 32.  The fp32 tile of each operand is split ONCE per
+// block while it is staged: each thread loads a 4(mn) x 4(k) micro-block (16-B
+// global loads, coalesced for either operand layout; the mn-contiguous case is
+// transposed in registers), splits it and writes three 8-B bf16 quads per row
+// into a k-contiguous LDS image
+//   row r (208 B): [hi k0..31 | mid k0..31 | lo k0..31 | 16 B pad]
+// so every MFMA fragment (8 consecutive k of one plane) is one ds_read_b128.
+// The 16-B k-chunks of the images staged from mn-contiguous sources are
+// XOR-swizzled by (r ^ r>>3) & 3: 2-way instead of 8-way bank conflicts on the
+// transposing ds_write_b64 for 2-way on the reads; k-contiguous sources need no
+// swizzle (conflict-free both ways; tools/lds_banks.py checks all four cases).
+// One LDS buffer (53 KB) + a register prefetch of the next K tile: two barriers
+// per K tile, two blocks per CU, so one block's staging overlaps the other's MFMAs.
+constexpr int XROW = 208;  // bytes per LDS image row
+
+template <bool SWZ>
+HS_DEVICE int xchunk(int r, int kc) { return SWZ ? kc ^ ((r ^ (r >> 3)) & 3) : kc; }
+
+// per-thread byte offsets of the 4 rows (k-contiguous) / k rows (mn-contiguous) a thread stages;
+// the K-tile base is a wave-uniform pointer, so the loads use the scalar-base addressing mode
+template <bool KCONTIG>
+HS_DEVICE void x_offsets(int64_t ldx, int r0, uint32_t (&o)[4]) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    o[i] = KCONTIG ? (uint32_t)(((int64_t)(r0 + 4 * (t >> 3) + i) * ldx + 4 * (t & 7)) * 4)
+                   : (uint32_t)(((int64_t)(4 * (t >> 5) + i) * ldx + r0 + 4 * (t & 31)) * 4);
+}
+
+template <bool KCONTIG>
+HS_DEVICE void x_load(const char* __restrict__ base, const uint32_t (&o)[4], float4 (&v)[4]) {
+  if (KCONTIG) {  // v[i] = k 4c..4c+3 of row 4g+i; 8 lanes per 128-B row segment
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = *reinterpret_cast<const float4*>(base + o[i]);
+  } else {  // 32 lanes per 512-B k row, then a 4x4 register transpose
+    float4 w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = *reinterpret_cast<const float4*>(base + o[j]);
+    v[0] = make_float4(w[0].x, w[1].x, w[2].x, w[3].x);
+    v[1] = make_float4(w[0].y, w[1].y, w[2].y, w[3].y);
+    v[2] = make_float4(w[0].z, w[1].z, w[2].z, w[3].z);
+    v[3] = make_float4(w[0].w, w[1].w, w[2].w, w[3].w);
+  }
+}
+
+template <bool KCONTIG, int NT>
+HS_DEVICE void x_store(char* __restrict__ S, const float4 (&v)[4]) {
+  const int t = threadIdx.x;
+  const int g = KCONTIG ? t >> 3 : t & 31, c = KCONTIG ? t & 7 : t >> 5;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = 4 * g + i;
+    uint2 h, m, l;
+    split4<NT>(v[i], h, m, l);
+    char* row = S + r * XROW + 16 * xchunk<!KCONTIG>(r, c >> 1) + 8 * (c & 1);
+    *reinterpret_cast<uint2*>(row) = h;
+    *reinterpret_cast<uint2*>(row + 64) = m;
+    if (NT >= 6) *reinterpret_cast<uint2*>(row + 128) = l;
+  }
+}
+
+// fragment of plane p (0 hi, 1 mid, 2 lo), k-slice ks, for the 32-row tile at `row`
+template <bool SWZ>
+HS_DEVICE bfx8 x_frag(const char* __restrict__ S, int row, int p, int ks, int lr, int h) {
+  const int r = row + lr;
+  return *reinterpret_cast<const bfx8*>(S + r * XROW + 64 * p + 16 * xchunk<SWZ>(r, 2 * ks + h));
+}
+
+template <bool TA, bool TB, int EPI, int NT, int ABL = 0>
+__global__ void __launch_bounds__(256, 2) gemm_x6s_kernel(GemmArgs p) {
+  constexpr int BM = 128, BN = 128, TM = 2, TN = 2;
+  __shared__ __attribute__((aligned(16))) char smem[2 * 128 * XROW];
+  char* const As = smem;
+  char* const Bs = smem + 128 * XROW;
+
+  const int tiles_m = p.M / BM, tiles_n = p.N / BN, nwg = tiles_m * tiles_n * p.ksplit;
+  const int orig = blockIdx.x;
+  const int xcd = orig % 8, qq = nwg / 8, rr = nwg % 8;
+  const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + orig / 8;
+  const int slice = wg % p.ksplit, tile = wg / p.ksplit;
+  // grouped order: 8 M-tiles x all N-tiles per group, N fastest inside it, so the 64 blocks an
+  // XCD runs at a time cover an ~8x8 tile square (A and B panels each re-read 8x from its L2)
+  const int gsz = 8 * tiles_n, grp = tile / gsz, gm = min(8, tiles_m - 8 * grp);
+  const int tm = 8 * grp + (tile % gsz) % gm, tn = (tile % gsz) / gm;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kofs = slice * (p.K / p.ksplit);
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wr = w >> 1, wc = w & 1;
+  const int wm = wr * (BM / 2), wn = wc * (BN / 2);
+  const int lr = lane & 31, q = lane >> 5;
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
+
+  // staging: 32-bit per-thread offsets + a uniform K-tile base pointer (advanced per tile)
+  uint32_t oa[4], ob[4];
+  x_offsets<!TA>(p.lda, m0, oa);
+  x_offsets<TB>(p.ldb, n0, ob);
+  const int64_t sa = TA ? (int64_t)GBK * p.lda * 4 : GBK * 4, sb = TB ? GBK * 4 : (int64_t)GBK * p.ldb * 4;
+  const char* ab = reinterpret_cast<const char*>(p.A) + (TA ? (int64_t)kofs * p.lda : kofs) * 4;
+  const char* bb = reinterpret_cast<const char*>(p.B) + (TB ? kofs : (int64_t)kofs * p.ldb) * 4;
+  float4 va[4], vb[4];
+  const int KT = p.K / p.ksplit / GBK;
+  x_load<!TA>(ab, oa, va);
+  x_load<TB>(bb, ob, vb);
+  x_store<!TA, NT>(As, va);
+  x_store<TB, NT>(Bs, vb);
+  __syncthreads();
+  constexpr int NPL = NT >= 6 ? 3 : 2, NTERM = NT >= 6 ? 6 : 3;
+  constexpr int PA[6] = {2, 0, 1, 1, 0, 0}, PB[6] = {0, 2, 1, 0, 1, 0};  // smallest terms first
+  for (int kt = 0; kt < KT; ++kt) {
+    // fragments of both k-slices first (one wait each), then the next tile's global loads
+    // (the last iteration re-reads its own tile: unconditional, so the registers stay static)
+    bfx8 af[2][3][TM], bf[2][3][TN];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int pl = 0; pl < NPL; ++pl) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af[ks][pl][i] = x_frag<TA>(As, wm + 32 * i, pl, ks, lr, q);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bf[ks][pl][j] = x_frag<!TB>(Bs, wn + 32 * j, pl, ks, lr, q);
+      }
+    if (kt + 1 < KT) {
+      ab += sa;
+      bb += sb;
+    }
+    if (ABL < 1) {  // ablation builds (tools/bench_gemm_x6.py --ablate; timing only, wrong results):
+      x_load<!TA>(ab, oa, va);  // 1 no global loads in the loop, 2 + no staging, 3 + no barriers
+      x_load<TB>(bb, ob, vb);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int tt = 6 - NTERM; tt < 6; ++tt)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mma_bf(af[ks][PA[tt]][i], bf[ks][PB[tt]][j], acc[i][j]);
+    if (ABL < 3) __syncthreads();  // every wave is done reading this K tile
+    if (ABL < 2) {
+      x_store<!TA, NT>(As, va);
+      x_store<TB, NT>(Bs, vb);
+    }
+    if (ABL < 3) __syncthreads();
+  }
+  epilogue<BM, BN, 32, EPI>(p, acc, reinterpret_cast<float*>(smem), m0, n0, tm, slice, wm, wn, wr, lr, q);
+}
+
+static int g_ablation = 0;  // microbenchmark hook (tile_override bits 3-4)
+
+// split-K finish: C = sum_s slab[s] (+ bias) (+ beta * C), fixed slice order (deterministic)
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ slab, int ksplit, int M, int N,
+                                                            float* __restrict__ C, int64_t ldc,
+                                                            const float* __restrict__ bias, float beta) {
+  const int n4 = N / 4;
+  const int64_t total = (int64_t)M * n4, plane = (int64_t)M * N;
+  for (int64_t u = blockIdx.x * 256ll + threadIdx.x; u < total; u += (int64_t)gridDim.x * 256) {
+    const int m = (int)(u / n4), n = (int)(u % n4) * 4;
+    const float* s0 = slab + (int64_t)m * N + n;
+    float4 a = *reinterpret_cast<const float4*>(s0);
+    for (int s = 1; s < ksplit; ++s) {
+      const float4 b = *reinterpret_cast<const float4*>(s0 + s * plane);
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    if (bias) {
+      const float4 b = *reinterpret_cast<const float4*>(bias + n);
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    float4* c = reinterpret_cast<float4*>(C + (int64_t)m * ldc + n);
+    if (beta != 0.f) {
+      const float4 o = *c;
+      a.x += beta * o.x; a.y += beta * o.y; a.z += beta * o.z; a.w += beta * o.w;
+    }
+    *c = a;
+  }
+}
+
+template <int BM, int BN, int MF, bool TA, bool TB, int EPI, int NT>
+void launch_cfg(const GemmArgs& a, hipStream_t st) {
+  const int blocks = (a.M / BM) * (a.N / BN) * a.ksplit;
+  if constexpr (NT > 0) {
+    if (EPI == kEpiNone && g_ablation == 1)
+      hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 1>), dim3(blocks), dim3(256), 0, st, a);
+    else if (EPI == kEpiNone && g_ablation == 2)
+      hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 2>), dim3(blocks), dim3(256), 0, st, a);
+    else if (EPI == kEpiNone && g_ablation == 3)
+      hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 3>), dim3(blocks), dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT>), dim3(blocks), dim3(256), 0, st, a);
+  }
+  else if (EPI == kEpiNone && g_ablation == 1)
+    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, MF, TA, TB, EPI, 1>), dim3(blocks), dim3(256), 0, st, a);
+  else if (EPI == kEpiNone && g_ablation == 2)
+    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, MF, TA, TB, EPI, 2>), dim3(blocks), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, MF, TA, TB, EPI, 0>), dim3(blocks), dim3(256), 0, st, a);
+}
+
+template <int BM, int BN, int MF, int NT>
 int launch_tile(int ta, int tb, int epi, const GemmArgs& a, hipStream_t st) {
+  if (a.ksplit > 1) epi = kEpiNone;  // bias / beta are applied by the split-K reduction
   if (!ta && tb) {  // forward X * W^T
-    if (epi == kEpiNone) launch_cfg<BM, BN, MF, false, true, kEpiNone>(a, st);
-    else if (epi == kEpiBias) launch_cfg<BM, BN, MF, false, true, kEpiBias>(a, st);
-    else if (epi == kEpiGelu) launch_cfg<BM, BN, MF, false, true, kEpiGelu>(a, st);
+    if (epi == kEpiNone) launch_cfg<BM, BN, MF, false, true, kEpiNone, NT>(a, st);
+    else if (epi == kEpiBias) launch_cfg<BM, BN, MF, false, true, kEpiBias, NT>(a, st);
+    else if (epi == kEpiGelu) launch_cfg<BM, BN, MF, false, true, kEpiGelu, NT>(a, st);
     else return -1;
   } else if (!ta && !tb) {  // dgrad dY * W
-    if (epi == kEpiNone) launch_cfg<BM, BN, MF, false, false, kEpiNone>(a, st);
-    else if (epi == kEpiDGelu) launch_cfg<BM, BN, MF, false, false, kEpiDGelu>(a, st);
+    if (epi == kEpiNone) launch_cfg<BM, BN, MF, false, false, kEpiNone, NT>(a, st);
+    else if (epi == kEpiDGelu) launch_cfg<BM, BN, MF, false, false, kEpiDGelu, NT>(a, st);
     else return -1;
   } else if (ta && !tb) {  // wgrad dY^T * X
-    if (epi == kEpiNone) launch_cfg<BM, BN, MF, true, false, kEpiNone>(a, st);
+    if (epi == kEpiNone) launch_cfg<BM, BN, MF, true, false, kEpiNone, NT>(a, st);
     else return -1;
   } else {
     return -1;
   }
   return 0;
+}
+
+template <int NT>
+int launch_split(int tile, int ta, int tb, int epi, const GemmArgs& a, hipStream_t st) {
+  if constexpr (NT > 0) return tile == 0 ? launch_tile<128, 128, 32, NT>(ta, tb, epi, a, st) : -1;
+  else return tile == 0 ? launch_tile<128, 128, 32, 0>(ta, tb, epi, a, st)
+         : tile == 1 ? launch_tile<128, 64, 32, 0>(ta, tb, epi, a, st)
+                     : launch_tile<64, 64, 32, 0>(ta, tb, epi, a, st);
 }
 
 }  // namespace hs
@@ -304,20 +566,44 @@ static int pick_tile(int M, int N) {
   return -1;
 }
 
+// bf16-split products: 128x128 tiles (each wave 64x64: 4 accumulators share every split
+// fragment) and K slices until the grid covers the 256 CUs about twice.
+static int pick_tile_split(int M, int N, int K, int* ksplit) {
+  if (M % 128 || N % 128) return -1;
+  const int tile = 0, tiles = (M / 128) * (N / 128);
+  int s = 1;
+  while (tiles * s < 384 && s < 8 && K % (2 * s * GBK) == 0 && K / (2 * s) >= 256) s *= 2;
+  *ksplit = s;
+  return tile;
+}
+
+// dtype: 0 fp32 on the exact-fp32 MFMA; 2 fp32 as 6 bf16 split products (fp32-level
+// error, see split8); 3 two-term split (3 products, ~2^-16: benchmarking only).
 // epi: 0 none, 1 +bias, 2 gelu(+bias) writing the pre-activation to aux,
 // 3 dgelu (aux = pre-activation) with column sums of C written (or added,
 // colsum_acc) to colsum_out.  part: scratch of (M/64)*N floats (epi 3 only).
+// ksplit: 0 = automatic (split dtypes only), 1 = none, >1 forced; slab: ksplit*M*N floats
+// of scratch when the split is >1 (epi 0/1 only).
 // Returns -1 when the request is not served (caller falls back to the library).
 int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, int64_t lda, const void* B,
                 int64_t ldb, void* C, int64_t ldc, const float* bias, int epi, float beta, float* aux, int64_t ldaux,
-                float* part, float* colsum_out, int colsum_acc, int tile_override, hipStream_t st) {
-  if (dtype != 0 || M <= 0 || N <= 0 || K <= 0 || K % GBK != 0) return -1;
+                float* part, float* colsum_out, int colsum_acc, int tile_override, hipStream_t st, int ksplit,
+                float* slab, int64_t slab_floats) {
+  if ((dtype != 0 && dtype != 2 && dtype != 3) || M <= 0 || N <= 0 || K <= 0 || K % GBK != 0) return -1;
   auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
   if (!al16(A) || !al16(B) || lda % 4 || ldb % 4) return -1;
   if ((epi >= 1 && !bias) || (epi >= 2 && (!aux || beta != 0.f)) || (epi == 3 && (!part || !colsum_out)))
     return -1;
-  int tile = pick_tile(M, N);
-  const bool mfma16 = tile_override >= 0 && (tile_override & 4);  // benchmarking hook: 16x16x4 MFMA
+  const int nt = dtype == 2 ? 6 : dtype == 3 ? 3 : 0;
+  int tile, ks = 1;
+  if (nt) {
+    tile = pick_tile_split(M, N, K, &ks);
+    if (ksplit > 0) ks = ksplit;
+    if (epi >= 2 || !slab) ks = 1;  // fused GELU epilogues need the whole K in one block
+  } else {
+    tile = pick_tile(M, N);
+  }
+  const bool mfma16 = !nt && tile_override >= 0 && (tile_override & 4);  // benchmarking hook: 16x16x4 MFMA
   g_ablation = tile_override >= 0 ? (tile_override >> 3) & 3 : 0;
   tile_override = tile_override >= 0 ? (tile_override & 3) : -1;
   if (tile_override >= 0) {  // benchmarking hook: force a tile shape (must divide the problem)
@@ -325,18 +611,28 @@ int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, i
     tile = (M % bm == 0 && N % bn == 0) ? tile_override : -1;
   }
   if (tile < 0) return -1;
+  if (ks > 1 && (K % (ks * GBK) != 0 || (int64_t)ks * M * N > slab_floats || N % 4 || ldc % 4 || !al16(C)))
+    return -1;
   GemmArgs a{static_cast<const float*>(A), static_cast<const float*>(B), static_cast<float*>(C), bias, aux, part,
-             lda, ldb, ldc, ldaux, M, N, K, beta};
+             lda, ldb, ldc, ldaux, M, N, K, beta, ks, slab};
   int rc;
-  if (mfma16)
-    rc = tile == 0 ? launch_tile<128, 128, 16>(ta, tb, epi, a, st)
-         : tile == 1 ? launch_tile<128, 64, 16>(ta, tb, epi, a, st)
-                     : launch_tile<64, 64, 16>(ta, tb, epi, a, st);
+  if (nt == 6)
+    rc = launch_split<6>(tile, ta, tb, epi, a, st);
+  else if (nt == 3)
+    rc = launch_split<3>(tile, ta, tb, epi, a, st);
+  else if (mfma16)
+    rc = tile == 0 ? launch_tile<128, 128, 16, 0>(ta, tb, epi, a, st)
+         : tile == 1 ? launch_tile<128, 64, 16, 0>(ta, tb, epi, a, st)
+                     : launch_tile<64, 64, 16, 0>(ta, tb, epi, a, st);
   else
-    rc = tile == 0 ? launch_tile<128, 128, 32>(ta, tb, epi, a, st)
-         : tile == 1 ? launch_tile<128, 64, 32>(ta, tb, epi, a, st)
-                     : launch_tile<64, 64, 32>(ta, tb, epi, a, st);
+    rc = launch_split<0>(tile, ta, tb, epi, a, st);
   if (rc != 0) return rc;
+  if (ks > 1) {
+    const int64_t n4 = (int64_t)M * (N / 4);
+    const int grid = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid), dim3(256), 0, st, slab, ks, M, N, static_cast<float*>(C), ldc,
+                       epi >= 1 ? bias : nullptr, beta);
+  }
   if (epi == kEpiDGelu) {
     const int bm = tile == 2 ? 64 : 128;
     const float* parts[1] = {part};

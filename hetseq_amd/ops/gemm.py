@@ -12,6 +12,11 @@ epilogue.  Two engines:
              per-shape solution comes from the measured TunableOp table, see
              runtime/gemm_tuning.py), followed by the separate HIP epilogue kernels.
 
+fp32 products on the HIP engine run on the bf16 matrix cores as six split-bf16
+products (``HETSEQ_FP32_GEMM=x6``, default: fp32-level error at ~2.7x the exact-fp32
+MFMA rate, see gemm.hip ``split8``) or on the exact-fp32 MFMA (``native``); ``x3``
+(two-term split, ~2^-16 relative error) exists for benchmarking only.
+
 ``HETSEQ_GEMM=hip|blas|auto`` selects; ``auto`` (default) times both paths --
 including the epilogue work the fused kernel absorbs -- once per (shape,
 transpose, epilogue) on the GPU and keeps the faster one.  The choice is
@@ -29,6 +34,10 @@ from hetseq_amd.ops._C import hip, stream_handle
 
 GEMM_CHOICES: dict = {}
 _MODE = os.environ.get("HETSEQ_GEMM", "auto")
+_FP32_DT = {"native": 0, "x6": 2, "x3": 3}
+_FP32 = os.environ.get("HETSEQ_FP32_GEMM", "x6")
+assert _FP32 in _FP32_DT, "HETSEQ_FP32_GEMM must be one of native|x6|x3"
+_SLABS: dict = {}  # (device, stream) -> split-K partial-sum workspace
 
 EPI_NONE, EPI_BIAS, EPI_GELU, EPI_DGELU = 0, 1, 2, 3
 
@@ -38,6 +47,31 @@ def set_mode(mode):
     assert mode in ("hip", "blas", "auto")
     _MODE = mode
     GEMM_CHOICES.clear()
+
+
+def set_fp32_mode(mode):
+    """'x6' (split-bf16 products, fp32-level error), 'native' (exact-fp32 MFMA) or 'x3' (benchmark only)."""
+    global _FP32
+    assert mode in _FP32_DT
+    _FP32 = mode
+    GEMM_CHOICES.clear()
+
+
+def fp32_mode():
+    return _FP32
+
+
+def _slab(M, N, ksplit, device):
+    """Split-K workspace for ksplit partial [M,N] fp32 planes (grown on demand, reused per stream)."""
+    key = (device, torch.cuda.current_stream(device).cuda_stream)
+    need = 8 * M * N if ksplit <= 0 else ksplit * M * N
+    buf = _SLABS.get(key)
+    if buf is None or buf.numel() < need:
+        if torch.cuda.is_current_stream_capturing():
+            return None  # never allocate inside a graph capture: run without split-K
+        buf = torch.empty(need, dtype=torch.float32, device=device)
+        _SLABS[key] = buf
+    return buf
 
 
 def _dims(a, b, ta, tb):
@@ -54,15 +88,22 @@ def _hip_ok(a, b, out, *extra):
 
 
 def _hip_gemm(a, b, ta, tb, out, bias=None, epi=EPI_NONE, beta=0.0, aux=None, part=None, colsum=None,
-              colsum_acc=False, tile=-1):
-    """Launch the HIP kernel; returns False (nothing launched) if the shape is not served."""
+              colsum_acc=False, tile=-1, fp32=None, ksplit=0):
+    """Launch the HIP kernel; returns False (nothing launched) if the shape is not served.
+
+    ``fp32`` picks the product engine (default: the HETSEQ_FP32_GEMM policy); ``ksplit``
+    0 = automatic split-K for the split-bf16 engines, 1 = none, >1 forced.
+    """
     M, N, K = _dims(a, b, ta, tb)
     assert out.shape == (M, N)
-    rc = hip().gemm(0, int(ta), int(tb), M, N, K, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0),
+    dt = _FP32_DT[fp32 or _FP32]
+    slab = _slab(M, N, ksplit, a.device) if dt and epi <= EPI_BIAS and ksplit != 1 else None
+    rc = hip().gemm(dt, int(ta), int(tb), M, N, K, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0),
                     out.data_ptr(), out.stride(0), bias.data_ptr() if bias is not None else 0, epi, float(beta),
                     aux.data_ptr() if aux is not None else 0, aux.stride(0) if aux is not None else 0,
                     part.data_ptr() if part is not None else 0, colsum.data_ptr() if colsum is not None else 0,
-                    int(colsum_acc), stream_handle(), tile)
+                    int(colsum_acc), stream_handle(), tile, ksplit,
+                    slab.data_ptr() if slab is not None else 0, slab.numel() if slab is not None else 0)
     return rc == 0
 
 
@@ -125,18 +166,35 @@ def gemm(a, b, ta=False, tb=False, out=None, bias=None, epi=EPI_NONE, beta=0.0, 
     if a.is_cuda and _MODE != "blas" and _hip_ok(a, b, out, bias):
         key = (M, N, K, ta, tb, epi, beta != 0.0)
         scratch = None
+        ks = [0]  # split-K of the HIP engine: 0 = kernel heuristic, else measured (auto mode)
 
         def run_hip():
-            return _hip_gemm(a, b, ta, tb, scratch, bias, epi, beta)
+            return _hip_gemm(a, b, ta, tb, scratch, bias, epi, beta, ksplit=ks[0])
 
         def run_blas():
             _blas_gemm(a, b, ta, tb, scratch, bias, epi, beta, out_dtype)
 
-        if key not in GEMM_CHOICES and _MODE == "auto":
+        if key not in GEMM_CHOICES and _MODE == "auto" and not torch.cuda.is_current_stream_capturing():
             scratch = out.clone() if beta != 0.0 else torch.empty_like(out)
             if not run_hip():
                 GEMM_CHOICES[key] = ("blas", None, None)
-        if _choose(key, run_hip, run_blas) == "hip" and _hip_gemm(a, b, ta, tb, out, bias, epi, beta):
+            elif _FP32 != "native" and epi <= EPI_BIAS:
+                # the split-bf16 engines: measure the K split too (wave quantisation vs slab traffic)
+                best = None
+                for cand in (0, 1, 2, 4):
+                    ks[0] = cand
+                    if run_hip():
+                        t = _bench(run_hip)
+                        if best is None or t < best[0]:
+                            best = (t, cand)
+                ks[0] = best[1]
+                t_blas = _bench(run_blas)
+                c = "hip" if best[0] < t_blas else "blas"
+                GEMM_CHOICES[key] = (c, round(best[0], 4), round(t_blas, 4), best[1])
+        c = GEMM_CHOICES.get(key)
+        if c is not None and len(c) > 3:
+            ks[0] = c[3]
+        if _choose(key, run_hip, run_blas) == "hip" and _hip_gemm(a, b, ta, tb, out, bias, epi, beta, ksplit=ks[0]):
             return out
     return _blas_gemm(a, b, ta, tb, out, bias, epi, beta, out_dtype)
 

@@ -340,20 +340,24 @@ def test_cross_entropy(cuda):
         _close(x.grad, x2.grad, 1e-4, 1e-8, "xent bwd")
 
 
+@pytest.mark.parametrize("engine,ksplit", [("native", 1), ("x6", 1), ("x6", 2), ("x6", 0)])
 @pytest.mark.parametrize("ta,tb", [(0, 1), (0, 0), (1, 0)])
 @pytest.mark.parametrize("M,N,K", [(256, 384, 128), (4096, 768, 768), (4096, 3072, 768), (768, 3072, 4096),
                                    (300, 130, 72), (640, 30522, 64)])
-def test_gemm_hip(cuda, ta, tb, M, N, K):
+def test_gemm_hip(cuda, engine, ksplit, ta, tb, M, N, K):
     from hetseq_amd.models.bert import f_gelu
     from hetseq_amd.ops import gemm as G
 
+    if engine == "native" and ksplit != 1:
+        pytest.skip("split-K is a split-bf16 engine feature")
     torch.manual_seed(9)
     a = torch.randn((K, M) if ta else (M, K), device=cuda)
     b = torch.randn((N, K) if tb else (K, N), device=cuda)
     bias = torch.randn(N, device=cuda)
     ref = (a.t() if ta else a).double() @ (b.t() if tb else b).double()
     out = torch.full((M, N), float("nan"), device=cuda)
-    served = G._hip_gemm(a, b, ta, tb, out)
+    kw = dict(fp32=engine, ksplit=ksplit)
+    served = G._hip_gemm(a, b, ta, tb, out, **kw)
     if M % 64 or N % 64 or K % 32:
         assert not served and torch.isnan(out).all()  # unsupported shape: nothing launched
         return
@@ -362,13 +366,16 @@ def test_gemm_hip(cuda, ta, tb, M, N, K):
     _close(out, ref, 1e-5, 1e-4, "gemm")
     c0 = torch.randn(M, N, device=cuda)
     out.copy_(c0)
-    assert G._hip_gemm(a, b, ta, tb, out, beta=1.0)
+    assert G._hip_gemm(a, b, ta, tb, out, beta=1.0, **kw)
     _close(out, ref + c0.double(), 1e-5, 1e-4, "gemm beta")
     if (ta, tb) == (0, 1):
-        assert G._hip_gemm(a, b, ta, tb, out, bias=bias, epi=G.EPI_BIAS)
+        assert G._hip_gemm(a, b, ta, tb, out, bias=bias, epi=G.EPI_BIAS, **kw)
         _close(out, ref + bias.double(), 1e-5, 1e-4, "gemm+bias")
+        out.copy_(c0)
+        assert G._hip_gemm(a, b, ta, tb, out, bias=bias, epi=G.EPI_BIAS, beta=1.0, **kw)
+        _close(out, ref + bias.double() + c0.double(), 1e-5, 1e-4, "gemm+bias beta")
         aux = torch.empty_like(out)
-        assert G._hip_gemm(a, b, ta, tb, out, bias=bias, epi=G.EPI_GELU, aux=aux)
+        assert G._hip_gemm(a, b, ta, tb, out, bias=bias, epi=G.EPI_GELU, aux=aux, **kw)
         _close(aux, ref, 1e-5, 1e-4, "gemm gelu pre")
         _close(out, f_gelu(ref + bias.double()), 1e-5, 1e-4, "gemm gelu")
     if (ta, tb) == (0, 0):
@@ -377,11 +384,42 @@ def test_gemm_hip(cuda, ta, tb, M, N, K):
         db = torch.randn(N, device=cuda)
         db0 = db.clone()
         assert G._hip_gemm(a, b, ta, tb, out, bias=bias, epi=G.EPI_DGELU, aux=pre, part=part, colsum=db,
-                           colsum_acc=True)
+                           colsum_acc=True, **kw)
         x = (pre.double() + bias.double()).requires_grad_()
         f_gelu(x).backward(ref)
         _close(out, x.grad, 1e-5, 1e-4, "gemm dgelu")
         _close(db, db0.double() + x.grad.sum(0), 1e-5, 1e-3, "gemm dgelu colsum")
+
+
+@pytest.mark.parametrize("ta,tb,M,N,K", [(0, 1, 4096, 2304, 768), (0, 0, 4096, 768, 3072), (1, 0, 768, 3072, 4096)])
+def test_gemm_x6_error_matches_fp32(cuda, ta, tb, M, N, K):
+    """Split-bf16 products carry fp32-level error: within 2x of the exact-fp32 MFMA kernel and of
+    the library SGEMM, measured against fp64 in units of |A|@|B| (the scale a K-long fp32 dot
+    product rounds on), and far below the two-term split and plain bf16."""
+    from hetseq_amd.ops import gemm as G
+
+    torch.manual_seed(12)
+    a = torch.rand((K, M) if ta else (M, K), device=cuda) * 2 - 1
+    b = torch.rand((N, K) if tb else (K, N), device=cuda) * 2 - 1
+    At, Bt = (a.t() if ta else a), (b.t() if tb else b)
+    ref = At.double() @ Bt.double()
+    mag = At.double().abs() @ Bt.double().abs()
+    out = torch.empty(M, N, device=cuda)
+
+    def err():
+        return float(((out.double() - ref).abs() / mag).max())
+
+    errs = {}
+    torch.mm(At, Bt, out=out)
+    errs["blas"] = err()
+    for eng in ("native", "x6", "x3"):
+        assert G._hip_gemm(a, b, ta, tb, out, fp32=eng)
+        errs[eng] = err()
+    out.copy_(At.bfloat16().float() @ Bt.bfloat16().float())
+    errs["bf16"] = err()
+    assert errs["x6"] <= 2.0 * max(errs["native"], errs["blas"]), errs
+    assert errs["x6"] < 5e-7, errs
+    assert errs["x3"] > 2 * errs["x6"] and errs["bf16"] > 100 * errs["x6"], errs
 
 
 @pytest.mark.parametrize("mode", ["hip", "blas", "auto"])
