@@ -44,6 +44,11 @@ def parse():
     p.add_argument("--hip-graph", action="store_true", help="replay the captured update as one HIP graph (1 GPU)")
     p.add_argument("--sync-debug", action="store_true", help="warn (with stack) on every host<->device sync in the timed loop")
     p.add_argument("--host-profile", default=None, help="cProfile the timed loop into this file")
+    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                   help="process-group backend for N > 1 (nccl = RCCL; gloo only to rehearse several ranks on one GPU)")
+    p.add_argument("--gemm-choices", default=None,
+                   help="JSON of measured GEMM engine choices: loaded if it exists (no measuring in warm-up), "
+                        "else written after the run (profiling runs use it to keep tuning out of the trace)")
     return p.parse_args()
 
 
@@ -64,11 +69,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if b.dist_backend == "gloo":
+        local_rank = 0  # rehearsal: every rank shares GPU 0
     torch.cuda.set_device(local_rank)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", init_method="env://", world_size=world, rank=rank,
-                                device_id=torch.device("cuda", local_rank))
+        if b.dist_backend == "nccl":
+            dist.init_process_group("nccl", init_method="env://", world_size=world, rank=rank,
+                                    device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group("gloo", init_method="env://", world_size=world, rank=rank)
         dist.all_reduce(torch.zeros(1, device="cuda"))
     work = tempfile.mkdtemp(prefix="hetseq_bench_r%d_" % rank)
     data_dir = os.path.join(work, "data")
@@ -114,6 +124,8 @@ def main():
                     group = []
 
     gen = batches()
+    if b.gemm_choices and os.path.exists(b.gemm_choices):
+        G.load_choices(b.gemm_choices)
     ctl.optimizer  # build optimizer/scheduler (and the DP engine) before timing
     for _ in range(b.warmup):
         ctl.train_step(next(gen))
@@ -159,6 +171,8 @@ def main():
     bert_ops.check_device_errors()
     sec = elapsed / b.steps
     seqs = b.batch * b.update_freq * world
+    if rank == 0 and b.gemm_choices and not os.path.exists(b.gemm_choices):
+        G.save_choices(b.gemm_choices)
     if rank == 0:
         out = {
             "metric": "avg sec/step, BERT-base seq128 bs=32/GPU",

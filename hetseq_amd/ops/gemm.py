@@ -49,6 +49,28 @@ def set_mode(mode):
     GEMM_CHOICES.clear()
 
 
+def save_choices(path):
+    """Write the measured per-call-site engine choices (JSON) so a later run can skip the measuring."""
+    import json
+
+    with open(path, "w") as f:
+        json.dump({"fp32": _FP32, "choices": {repr(k): v for k, v in GEMM_CHOICES.items()}}, f, indent=0)
+
+
+def load_choices(path):
+    """Load choices written by save_choices (only when they were measured under the same fp32 policy)."""
+    import ast
+    import json
+
+    with open(path) as f:
+        d = json.load(f)
+    if d.get("fp32") != _FP32:
+        return False
+    for k, v in d["choices"].items():
+        GEMM_CHOICES[ast.literal_eval(k)] = tuple(v)
+    return True
+
+
 def set_fp32_mode(mode):
     """'x6' (split-bf16 products, fp32-level error), 'native' (exact-fp32 MFMA) or 'x3' (benchmark only)."""
     global _FP32

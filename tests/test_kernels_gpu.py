@@ -350,6 +350,7 @@ def test_gemm_hip(cuda, engine, ksplit, ta, tb, M, N, K):
 
     if engine == "native" and ksplit != 1:
         pytest.skip("split-K is a split-bf16 engine feature")
+
     torch.manual_seed(9)
     a = torch.randn((K, M) if ta else (M, K), device=cuda)
     b = torch.randn((N, K) if tb else (K, N), device=cuda)
@@ -389,6 +390,25 @@ def test_gemm_hip(cuda, engine, ksplit, ta, tb, M, N, K):
         f_gelu(x).backward(ref)
         _close(out, x.grad, 1e-5, 1e-4, "gemm dgelu")
         _close(db, db0.double() + x.grad.sum(0), 1e-5, 1e-3, "gemm dgelu colsum")
+
+
+@pytest.mark.parametrize("engine", ["x6"])
+def test_gemm_splitk_deterministic(cuda, engine):
+    """Split-K partial slabs are summed in slice order by one reduction pass: repeated runs are
+    bitwise identical."""
+    from hetseq_amd.ops import gemm as G
+
+    torch.manual_seed(5)
+    a = torch.randn(4096, 768, device=cuda)
+    b = torch.randn(4096, 1024, device=cuda)
+    first = torch.empty(768, 1024, device=cuda)
+    assert G._hip_gemm(a, b, 1, 0, first, fp32=engine, ksplit=4)
+    ref = a.double().t() @ b.double()
+    _close(first, ref, 1e-5, 1e-4, "splitk")
+    for _ in range(20):
+        out = torch.empty_like(first)
+        assert G._hip_gemm(a, b, 1, 0, out, fp32=engine, ksplit=4)
+        assert torch.equal(out, first)
 
 
 @pytest.mark.parametrize("ta,tb,M,N,K", [(0, 1, 4096, 2304, 768), (0, 0, 4096, 768, 3072), (1, 0, 768, 3072, 4096)])

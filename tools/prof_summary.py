@@ -11,7 +11,8 @@ def main():
     path, steps, title = sys.argv[1], float(sys.argv[2]), sys.argv[3]
     rows = list(csv.DictReader(open(path)))
     tot = sum(float(r["TotalDurationNs"]) for r in rows)
-    gemm = sum(float(r["TotalDurationNs"]) for r in rows if r["Name"].startswith("Cijk") or "gemm" in r["Name"])
+    gemm = sum(float(r["TotalDurationNs"]) for r in rows if r["Name"].startswith("Cijk"))
+    hsg = sum(float(r["TotalDurationNs"]) for r in rows if "hs::" in r["Name"] and "gemm" in r["Name"])
     hs = sum(float(r["TotalDurationNs"]) for r in rows if "hs::" in r["Name"])
     print("# %s\n" % title)
     print("Source: `rocprofv3 --kernel-trace --stats` (`%s`), %d profiled steps (incl. warmup).\n" % (path, steps))
@@ -19,6 +20,7 @@ def main():
     print("| all kernels | %.3f | 100%% |" % (tot / 1e6 / steps))
     print("| library GEMM (hipBLASLt Cijk_*) | %.3f | %.0f%% |" % (gemm / 1e6 / steps, 100 * gemm / tot))
     print("| hetseq_amd HIP kernels (hs::*) | %.3f | %.0f%% |" % (hs / 1e6 / steps, 100 * hs / tot))
+    print("| of which hand-written GEMM (hs::gemm_*) | %.3f | %.0f%% |" % (hsg / 1e6 / steps, 100 * hsg / tot))
     print("| other (torch elementwise, copies) | %.3f | %.0f%% |\n" % ((tot - gemm - hs) / 1e6 / steps,
                                                                   100 * (tot - gemm - hs) / tot))
     print("| kernel | calls/step | avg us | ms/step |\n|---|---|---|---|")
