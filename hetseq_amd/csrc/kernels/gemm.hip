@@ -343,8 +343,7 @@ HS_DEVICE int xchunk(int r, int kc) { return SWZ ? kc ^ ((r ^ (r >> 3)) & 3) : k
 // per-thread byte offsets of the 4 rows (k-contiguous) / k rows (mn-contiguous) a thread stages;
 // the K-tile base is a wave-uniform pointer, so the loads use the scalar-base addressing mode
 template <bool KCONTIG>
-HS_DEVICE void x_offsets(int64_t ldx, int r0, uint32_t (&o)[4]) {
-  const int t = threadIdx.x;
+HS_DEVICE void x_offsets(int64_t ldx, int r0, uint32_t (&o)[4], int t) {
 #pragma unroll
   for (int i = 0; i < 4; ++i)
     o[i] = KCONTIG ? (uint32_t)(((int64_t)(r0 + 4 * (t >> 3) + i) * ldx + 4 * (t & 7)) * 4)
@@ -368,8 +367,7 @@ HS_DEVICE void x_load(const char* __restrict__ base, const uint32_t (&o)[4], flo
 }
 
 template <bool KCONTIG, int NT>
-HS_DEVICE void x_store(char* __restrict__ S, const float4 (&v)[4]) {
-  const int t = threadIdx.x;
+HS_DEVICE void x_store(char* __restrict__ S, const float4 (&v)[4], int t) {
   const int g = KCONTIG ? t >> 3 : t & 31, c = KCONTIG ? t & 7 : t >> 5;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -390,9 +388,12 @@ HS_DEVICE bfx8 x_frag(const char* __restrict__ S, int row, int p, int ks, int lr
   return *reinterpret_cast<const bfx8*>(S + r * XROW + 64 * p + 16 * xchunk<SWZ>(r, 2 * ks + h));
 }
 
-template <bool TA, bool TB, int EPI, int NT, int ABL = 0>
-__global__ void __launch_bounds__(256, 2) gemm_x6s_kernel(GemmArgs p) {
-  constexpr int BM = 128, BN = 128, TM = 2, TN = 2;
+// WV = 4: 2x2 waves of 64x64, every thread stages 4x4 of A and of B.
+// WV = 8: 2x4 waves of 64x32 (twice the waves per CU to hide each other's staging), threads
+//         0-255 stage A and 256-511 stage B with the same 4x4 micro-blocks.
+template <bool TA, bool TB, int EPI, int NT, int ABL = 0, int WV = 4>
+__global__ void __launch_bounds__(64 * WV, 2) gemm_x6s_kernel(GemmArgs p) {
+  constexpr int BM = 128, BN = 128, WC = WV / 2, TM = 2, TN = BN / WC / 32;
   __shared__ __attribute__((aligned(16))) char smem[2 * 128 * XROW];
   char* const As = smem;
   char* const Bs = smem + 128 * XROW;
@@ -410,8 +411,8 @@ __global__ void __launch_bounds__(256, 2) gemm_x6s_kernel(GemmArgs p) {
   const int kofs = slice * (p.K / p.ksplit);
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int wr = w >> 1, wc = w & 1;
-  const int wm = wr * (BM / 2), wn = wc * (BN / 2);
+  const int wr = w / WC, wc = w % WC;
+  const int wm = wr * (BM / 2), wn = wc * (BN / WC);
   const int lr = lane & 31, q = lane >> 5;
 
   f32x16 acc[TM][TN];
@@ -421,18 +422,39 @@ __global__ void __launch_bounds__(256, 2) gemm_x6s_kernel(GemmArgs p) {
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
 
   // staging: 32-bit per-thread offsets + a uniform K-tile base pointer (advanced per tile)
+  const int st = threadIdx.x & 255;
+  const bool stA = WV == 4 || threadIdx.x < 256, stB = WV == 4 || threadIdx.x >= 256;
   uint32_t oa[4], ob[4];
-  x_offsets<!TA>(p.lda, m0, oa);
-  x_offsets<TB>(p.ldb, n0, ob);
+  x_offsets<!TA>(p.lda, m0, oa, st);
+  x_offsets<TB>(p.ldb, n0, ob, st);
   const int64_t sa = TA ? (int64_t)GBK * p.lda * 4 : GBK * 4, sb = TB ? GBK * 4 : (int64_t)GBK * p.ldb * 4;
   const char* ab = reinterpret_cast<const char*>(p.A) + (TA ? (int64_t)kofs * p.lda : kofs) * 4;
   const char* bb = reinterpret_cast<const char*>(p.B) + (TB ? kofs : (int64_t)kofs * p.ldb) * 4;
   float4 va[4], vb[4];
+  auto load = [&]() {
+    if (WV == 4) {
+      x_load<!TA>(ab, oa, va);
+      x_load<TB>(bb, ob, vb);
+    } else if (stA) {  // wave-uniform branch: one operand per half of the block
+      x_load<!TA>(ab, oa, va);
+    } else {
+      x_load<TB>(bb, ob, va);
+    }
+  };
+  auto store = [&]() {
+    if (WV == 4) {
+      x_store<!TA, NT>(As, va, st);
+      x_store<TB, NT>(Bs, vb, st);
+    } else if (stA) {
+      x_store<!TA, NT>(As, va, st);
+    } else {
+      x_store<TB, NT>(Bs, va, st);
+    }
+  };
+  (void)stB;
   const int KT = p.K / p.ksplit / GBK;
-  x_load<!TA>(ab, oa, va);
-  x_load<TB>(bb, ob, vb);
-  x_store<!TA, NT>(As, va);
-  x_store<TB, NT>(Bs, vb);
+  load();
+  store();
   __syncthreads();
   constexpr int NPL = NT >= 6 ? 3 : 2, NTERM = NT >= 6 ? 6 : 3;
   constexpr int PA[6] = {2, 0, 1, 1, 0, 0}, PB[6] = {0, 2, 1, 0, 1, 0};  // smallest terms first
@@ -453,10 +475,8 @@ __global__ void __launch_bounds__(256, 2) gemm_x6s_kernel(GemmArgs p) {
       ab += sa;
       bb += sb;
     }
-    if (ABL < 1) {  // ablation builds (tools/bench_gemm_x6.py --ablate; timing only, wrong results):
-      x_load<!TA>(ab, oa, va);  // 1 no global loads in the loop, 2 + no staging, 3 + no barriers
-      x_load<TB>(bb, ob, vb);
-    }
+    if (ABL < 1) load();  // ablation builds (tools/bench_gemm_x6.py --ablate; timing only, wrong
+                          // results): 1 no global loads in the loop, 2 + no staging, 3 + no barriers
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -466,16 +486,18 @@ __global__ void __launch_bounds__(256, 2) gemm_x6s_kernel(GemmArgs p) {
 #pragma unroll
           for (int j = 0; j < TN; ++j) acc[i][j] = mma_bf(af[ks][PA[tt]][i], bf[ks][PB[tt]][j], acc[i][j]);
     if (ABL < 3) __syncthreads();  // every wave is done reading this K tile
-    if (ABL < 2) {
-      x_store<!TA, NT>(As, va);
-      x_store<TB, NT>(Bs, vb);
-    }
+    if (ABL < 2) store();
     if (ABL < 3) __syncthreads();
   }
-  epilogue<BM, BN, 32, EPI>(p, acc, reinterpret_cast<float*>(smem), m0, n0, tm, slice, wm, wn, wr, lr, q);
+  // the epilogue's tile geometry: TM x TN 32x32 accumulators per wave, two wave rows
+  epilogue<BM, 2 * 32 * TN, 32, EPI>(p, acc, reinterpret_cast<float*>(smem), m0, n0, tm, slice, wm, wn, wr, lr, q);
 }
 
 static int g_ablation = 0;  // microbenchmark hook (tile_override bits 3-4)
+// split-bf16 kernel waves per block: 8 for the weight gradient (both operands mn-contiguous:
+// twice the waves hide its transposing staging; measured +8-12%), 4 elsewhere (the 8-wave
+// dgrad needs 160 VGPRs = one block per CU, -25%).  tile_override bit 5 forces 4, bit 6 forces 8.
+static int g_x6_waves = 4;
 
 // split-K finish: C = sum_s slab[s] (+ bias) (+ beta * C), fixed slice order (deterministic)
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ slab, int ksplit, int M, int N,
@@ -508,14 +530,25 @@ template <int BM, int BN, int MF, bool TA, bool TB, int EPI, int NT>
 void launch_cfg(const GemmArgs& a, hipStream_t st) {
   const int blocks = (a.M / BM) * (a.N / BN) * a.ksplit;
   if constexpr (NT > 0) {
-    if (EPI == kEpiNone && g_ablation == 1)
-      hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 1>), dim3(blocks), dim3(256), 0, st, a);
-    else if (EPI == kEpiNone && g_ablation == 2)
-      hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 2>), dim3(blocks), dim3(256), 0, st, a);
-    else if (EPI == kEpiNone && g_ablation == 3)
-      hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 3>), dim3(blocks), dim3(256), 0, st, a);
-    else
-      hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT>), dim3(blocks), dim3(256), 0, st, a);
+    if (g_x6_waves == 4) {
+      if (EPI == kEpiNone && g_ablation == 1)
+        hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 1, 4>), dim3(blocks), dim3(256), 0, st, a);
+      else if (EPI == kEpiNone && g_ablation == 2)
+        hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 2, 4>), dim3(blocks), dim3(256), 0, st, a);
+      else if (EPI == kEpiNone && g_ablation == 3)
+        hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 3, 4>), dim3(blocks), dim3(256), 0, st, a);
+      else
+        hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 0, 4>), dim3(blocks), dim3(256), 0, st, a);
+    } else {
+      if (EPI == kEpiNone && g_ablation == 1)
+        hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 1, 8>), dim3(blocks), dim3(512), 0, st, a);
+      else if (EPI == kEpiNone && g_ablation == 2)
+        hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 2, 8>), dim3(blocks), dim3(512), 0, st, a);
+      else if (EPI == kEpiNone && g_ablation == 3)
+        hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 3, 8>), dim3(blocks), dim3(512), 0, st, a);
+      else
+        hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 0, 8>), dim3(blocks), dim3(512), 0, st, a);
+    }
   }
   else if (EPI == kEpiNone && g_ablation == 1)
     hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, MF, TA, TB, EPI, 1>), dim3(blocks), dim3(256), 0, st, a);
@@ -605,6 +638,8 @@ int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, i
   }
   const bool mfma16 = !nt && tile_override >= 0 && (tile_override & 4);  // benchmarking hook: 16x16x4 MFMA
   g_ablation = tile_override >= 0 ? (tile_override >> 3) & 3 : 0;
+  g_x6_waves = tile_override >= 0 && (tile_override & 32) ? 4 : tile_override >= 0 && (tile_override & 64) ? 8
+                                                              : ta ? 8 : 4;
   tile_override = tile_override >= 0 ? (tile_override & 3) : -1;
   if (tile_override >= 0) {  // benchmarking hook: force a tile shape (must divide the problem)
     const int bm = tile_override == 2 ? 64 : 128, bn = tile_override == 0 ? 128 : 64;

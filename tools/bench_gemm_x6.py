@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--ksplit", default="0", help="comma list of split-K settings for x6 (0 = automatic)")
     ap.add_argument("--only", default=None, help="profile mode: 'M,N,K,ta,tb,engine' run --reps times, nothing else")
     ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--waves", type=int, default=8, help="with --only: waves per block of the split kernel (4/8)")
     ap.add_argument("--ablate", type=int, default=0, help="with --only: 1 no global loads, 2 + no staging, 3 + no barriers")
     a = ap.parse_args()
     if a.only:
@@ -36,9 +37,10 @@ def main():
         B = torch.rand((N, K) if tb else (K, N), device="cuda") * 2 - 1
         C = torch.empty(M, N, device="cuda")
         f = (lambda: torch.mm(A.t() if ta else A, B.t() if tb else B, out=C)) if eng == "blas" else \
-            (lambda: G._hip_gemm(A, B, ta, tb, C, fp32=eng, ksplit=1, tile=(a.ablate << 3) if a.ablate else -1))
+            (lambda: G._hip_gemm(A, B, ta, tb, C, fp32=eng, ksplit=1,
+                                 tile=(a.ablate << 3) | (32 if a.waves == 4 else 64)))
         t = timeit(f, a.reps)
-        print("%s%s %dx%dx%d %.1fus %.1fTF" % (eng, " ablate=%d" % a.ablate if a.ablate else "", M, N, K, t,
+        print("%s w%d%s %dx%dx%d %.1fus %.1fTF" % (eng, a.waves, " ablate=%d" % a.ablate if a.ablate else "", M, N, K, t,
                                               2.0 * M * N * K / t / 1e6))
         return
     from hetseq_amd.runtime import gemm_tuning

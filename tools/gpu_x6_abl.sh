@@ -3,8 +3,10 @@ export TMPDIR=/tmp HETSEQ_GEMM_TUNE_MISSING=0
 timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q -k "gemm" --timeout 120 --timeout-method thread > gpurun_out/t_x6.log 2>&1; rc=$?
 tail -3 gpurun_out/t_x6.log
 [ $rc -eq 0 ] || { tail -40 gpurun_out/t_x6.log; exit $rc; }
-for e in x6 x3; do for ab in 0 1 2 3; do
-timeout -k 10 120 python3 tools/bench_gemm_x6.py --only 4096,2048,768,0,1,$e --reps 50 --ablate $ab 2>/dev/null || exit 1
-done; done
+for w in 4 8; do for ab in 0 1 2 3; do
+timeout -k 10 120 python3 tools/bench_gemm_x6.py --only 4096,2048,768,0,1,x6 --reps 50 --ablate $ab --waves $w 2>/dev/null || exit 1
+done
+for s in 4096,2048,3072,0,0 2048,2048,4096,1,0; do timeout -k 10 120 python3 tools/bench_gemm_x6.py --only $s,x6 --reps 50 --waves $w 2>/dev/null || exit 1; done
+done
 timeout -k 10 300 python tools/bench_gemm_x6.py --ksplit 0,1,2,4 --md gpurun_out/gemm_x6.md > gpurun_out/gemm_x6.log 2>&1 || { tail -20 gpurun_out/gemm_x6.log; exit 1; }
 cut -c1-330 gpurun_out/gemm_x6.log
