@@ -86,6 +86,8 @@ def _link(compiler, objs, out, ldflags, verbose, force):
 
 def build_native(verbose=False, jobs=4):
     src = os.path.join(HERE, "native", "batcher.cpp")
+    if not _newer(os.path.join(PKG, "_native" + EXT), [src]):
+        return os.path.join(PKG, "_native" + EXT)
     flags = ["-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall"] + ["-I" + p for p in _py_includes()]
     objs, changed = _compile_objs("g++", flags, [src], [], os.path.join(BUILD_DIR, "native"), verbose, jobs)
     out = os.path.join(PKG, "_native" + EXT)
@@ -99,6 +101,8 @@ def build_h5(verbose=False, jobs=4):
     if not os.path.exists(os.path.join(inc, "hdf5.h")):
         raise RuntimeError("libhdf5 headers not found under %s (set HETSEQ_HDF5_ROOT)" % HDF5_ROOT)
     src = os.path.join(HERE, "native", "h5shard.cpp")
+    if not _newer(os.path.join(PKG, "_h5" + EXT), [src]):
+        return os.path.join(PKG, "_h5" + EXT)
     flags = ["-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall", "-I" + inc] + [
         "-I" + p for p in _py_includes()
     ]
@@ -165,6 +169,9 @@ def hip_sources():
 def build_hip(verbose=False, jobs=8):
     hipcc = shutil.which("hipcc") or os.path.join(ROCM, "bin", "hipcc")
     kdir = os.path.join(HERE, "kernels")
+    out = os.path.join(PKG, "_hip" + EXT)
+    if not _newer(out, hip_sources() + _headers(kdir)):
+        return out  # the shipped module is current (object files need not travel with the tree)
     flags = [
         "-O3",
         "-std=c++17",

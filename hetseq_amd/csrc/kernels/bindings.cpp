@@ -76,6 +76,24 @@ static void check(int rc, const char* what) {
 }
 static void check_launch(const char* what) { check(0, what); }
 
+// Stream fork/join for the weight-gradient side stream (runtime/streams.py): record an event on
+// `signal`, make `waiter` wait for it.  A ring of timing-free events, created once; an event is
+// re-recorded only after 64 later forks, long after the wait that used it was enqueued (a wait
+// captures the event's state at enqueue time).
+static void stream_wait(hipStream_t waiter, hipStream_t signal) {
+  static hipEvent_t ring[64];
+  static int n = 0;
+  static bool init = false;
+  if (!init) {
+    for (auto& e : ring)
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) throw std::runtime_error("hipEventCreate");
+    init = true;
+  }
+  hipEvent_t e = ring[n++ & 63];
+  if (hipEventRecord(e, signal) != hipSuccess || hipStreamWaitEvent(waiter, e, 0) != hipSuccess)
+    throw std::runtime_error("stream_wait: hipEventRecord/hipStreamWaitEvent failed");
+}
+
 PYBIND11_MODULE(_hip, m) {
   m.doc() = "hetseq_amd CDNA4 (gfx950) kernels";
   m.attr("arch") = "gfx950";
@@ -220,6 +238,7 @@ PYBIND11_MODULE(_hip, m) {
 
   // returns 0 when launched, -1 when the shape/epilogue is not served (caller falls back)
   m.def("set_seed_ptr", [](i64 ptr) { hs::g_seed_dev = reinterpret_cast<const uint64_t*>(ptr); });
+  m.def("stream_wait", [](i64 waiter, i64 signal) { stream_wait(ST(waiter), ST(signal)); });
   m.def("gemm", [](int dt, int ta, int tb, int M, int N, int K, i64 A, i64 lda, i64 B, i64 ldb, i64 C, i64 ldc, i64 bias,
                    int epi, float beta, i64 aux, i64 ldaux, i64 part, i64 colsum, int colsum_acc, i64 st,
                    int tile, int ksplit, i64 slab, i64 slab_floats) {

@@ -334,11 +334,15 @@ class BertLayer(nn.Module):
 
     # ------------------------------------------------------------- fused path
     def fused_params(self):
+        cached = self.__dict__.get("_hs_pcache")  # parameter objects never change identity
+        if cached is not None:
+            return cached
         a, o = self.attention, self.output
-        return [a.self.query.weight, a.self.query.bias, a.self.key.weight, a.self.key.bias, a.self.value.weight,
+        self.__dict__["_hs_pcache"] = ps = [a.self.query.weight, a.self.query.bias, a.self.key.weight, a.self.key.bias, a.self.value.weight,
                 a.self.value.bias, a.output.dense.weight, a.output.dense.bias, a.output.LayerNorm.weight,
                 a.output.LayerNorm.bias, self.intermediate.dense_act.weight, self.intermediate.dense_act.bias,
                 o.dense.weight, o.dense.bias, o.LayerNorm.weight, o.LayerNorm.bias]
+        return ps
 
     def _weights(self):
         """Kernel-side weight views.  With a flat store they are fixed views into its buffers

@@ -24,7 +24,7 @@ import torch
 
 from hetseq_amd.ops import gemm as G
 from hetseq_amd.ops._C import dtype_code, hip, stream_handle
-from hetseq_amd.runtime import rng
+from hetseq_amd.runtime import rng, streams
 
 LN_WIDTHS = (256, 512, 768, 1024, 1536, 2048)
 
@@ -370,16 +370,26 @@ class FusedBertLayer(torch.autograd.Function):
         # LN2 (bias-dropout-residual) backward
         dz2, do_, dg2, dbb2, db2 = ln_bwd(dh2, z2, m2, r2, W.g2, p_h, 1, s_2, o_2, True, True,
                                           acc=(Gv.g2, Gv.bb2, Gv.b2) if acc else None)
-        dW2 = G.linear_wgrad(do_, f1, out=Gv.w2 if acc else None, accumulate=acc)
+        # weight gradients go into the flat store on the side stream (runtime/streams.py) and
+        # overlap the data-gradient chain; without a flat store they stay in order
+        side = acc and streams.enabled()
+
+        def wgrad(dy, xin, out):
+            if not side:
+                return G.linear_wgrad(dy, xin, out=out, accumulate=acc)
+            with torch.cuda.stream(streams.fork(dy.device, dy, xin)):
+                return G.linear_wgrad(dy, xin, out=out, accumulate=acc, ksplit=streams.SIDE_KSPLIT)
+
+        dW2 = wgrad(do_, f1, Gv.w2 if acc else None)
         df1pre, dbi = G.linear_dgrad_dgelu(do_, W.w2, f1pre, W.bi, db_acc=Gv.bi if acc else None)
-        dW1 = G.linear_wgrad(df1pre, h1, out=Gv.w1 if acc else None, accumulate=acc)
+        dW1 = wgrad(df1pre, h1, Gv.w1 if acc else None)
         dh1 = G.linear_dgrad(df1pre, W.w1, out=dz2, accumulate=True)  # dz2 + df1pre @ W1
         dz1, da1, dg1, db1, dbo = ln_bwd(dh1, z1, m1, r1, W.g1, p_h, 1, s_1, o_1, True, True,
                                          acc=(Gv.g1, Gv.b1, Gv.bo) if acc else None)
-        dWo = G.linear_wgrad(da1, ctx_, out=Gv.wo if acc else None, accumulate=acc)
+        dWo = wgrad(da1, ctx_, Gv.wo if acc else None)
         dctx = G.linear_dgrad(da1, W.wo)
         dqkv = attn_bwd(qkv, mask, ctx_, dctx, (lse, dmask), B, S, NH, p_a, bias=W.bqkv)
-        dWqkv = G.linear_wgrad(dqkv, x, out=Gv.wqkv if acc else None, accumulate=acc)
+        dWqkv = wgrad(dqkv, x, Gv.wqkv if acc else None)
         dbqkv = colsum(dqkv, acc=Gv.bqkv if acc else None)
         dx = G.linear_dgrad(dqkv, W.wqkv, out=dz1, accumulate=True)  # dz1 + dqkv @ Wqkv
         if acc:

@@ -179,8 +179,8 @@ def _choose(key, run_hip, run_blas):
     return c
 
 
-def gemm(a, b, ta=False, tb=False, out=None, bias=None, epi=EPI_NONE, beta=0.0, out_dtype=None):
-    """out = beta*out + op(a) @ op(b) (+bias)."""
+def gemm(a, b, ta=False, tb=False, out=None, bias=None, epi=EPI_NONE, beta=0.0, out_dtype=None, ksplit=None):
+    """out = beta*out + op(a) @ op(b) (+bias).  ``ksplit`` overrides the measured split-K of the HIP engine."""
     M, N, K = _dims(a, b, ta, tb)
     odt = out_dtype or a.dtype
     if out is None:
@@ -216,6 +216,8 @@ def gemm(a, b, ta=False, tb=False, out=None, bias=None, epi=EPI_NONE, beta=0.0, 
         c = GEMM_CHOICES.get(key)
         if c is not None and len(c) > 3:
             ks[0] = c[3]
+        if ksplit is not None:
+            ks[0] = ksplit
         if _choose(key, run_hip, run_blas) == "hip" and _hip_gemm(a, b, ta, tb, out, bias, epi, beta, ksplit=ks[0]):
             return out
     return _blas_gemm(a, b, ta, tb, out, bias, epi, beta, out_dtype)
@@ -231,9 +233,10 @@ def linear_dgrad(dy, w, out=None, accumulate=False):
     return gemm(dy, w, ta=False, tb=False, out=out, beta=1.0 if accumulate else 0.0)
 
 
-def linear_wgrad(dy, x, out=None, accumulate=False):
+def linear_wgrad(dy, x, out=None, accumulate=False, ksplit=None):
     """dy[T,N]^T @ x[T,K] -> [N,K] in fp32; accumulate=True adds into ``out`` (flat grad view)."""
-    return gemm(dy, x, ta=True, tb=False, out=out, out_dtype=torch.float32, beta=1.0 if accumulate else 0.0)
+    return gemm(dy, x, ta=True, tb=False, out=out, out_dtype=torch.float32, beta=1.0 if accumulate else 0.0,
+                ksplit=ksplit)
 
 
 def linear_gelu_fwd(x, w, b):

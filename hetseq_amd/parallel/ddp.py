@@ -34,7 +34,7 @@ import contextlib
 import torch
 import torch.distributed as dist
 
-from hetseq_amd.runtime import profiling
+from hetseq_amd.runtime import profiling, streams
 
 
 class FlatDDP(torch.nn.Module):
@@ -123,7 +123,17 @@ class FlatDDP(torch.nn.Module):
     def _launch(self, b):
         lo, hi = self.ranges[b]
         profiling.range_push("allreduce_bucket%d" % b)
-        work = dist.all_reduce(self.store.grad[lo:hi], group=self.process_group, async_op=True)
+        g = self.store.grad
+        side = streams.active(g.device) if g.is_cuda else None
+        if side is not None:
+            # the bucket's weight gradients come from the wgrad side stream, its biases / LN
+            # from the compute stream: issue the collective from the side stream after it
+            # waits for the compute stream, so RCCL orders after both without stalling compute
+            side.wait_stream(torch.cuda.current_stream(g.device))
+            with torch.cuda.stream(side):
+                work = dist.all_reduce(g[lo:hi], group=self.process_group, async_op=True)
+        else:
+            work = dist.all_reduce(g[lo:hi], group=self.process_group, async_op=True)
         profiling.range_pop()
         self.works.append(work)
 
@@ -138,6 +148,8 @@ class FlatDDP(torch.nn.Module):
             for i in missing:
                 self.ready[i] = True
             self._launch_ready()
+        if self.store.grad.is_cuda:
+            streams.join()  # compute stream after the wgrad stream (and the collectives issued on it)
         for w in self.works:
             w.wait()
         self.works = []

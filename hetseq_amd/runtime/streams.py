@@ -1,0 +1,93 @@
+"""Weight-gradient side stream: overlap the wgrad GEMMs with the data-gradient chain.
+
+In a layer's backward only the data gradient (dgrad) is on the critical path:
+layer i-1 needs dX of layer i, nothing needs dW until the all-reduce / optimizer.
+The BERT GEMMs are small for a 256-CU chip (M = 4096 tokens -> 192..768 tiles of
+128x128), so a single stream leaves CUs idle in every GEMM tail.  The fused
+layer backward therefore enqueues its four weight-gradient GEMMs on a second
+HIP stream (forked from the compute stream with an event wait) and lets the next
+dgrad run concurrently; blocks of both fill the machine.
+
+Ordering rules kept here:
+* ``fork(device, *tensors)`` -- the side stream waits for everything enqueued on
+  the compute stream so far (one event record + wait in C++, a few microseconds),
+  and the inputs are kept referenced until the join, so the caching allocator
+  cannot hand their memory to new compute-stream work while the side stream still
+  reads it (cheaper than ``record_stream`` and no allocator-side event polling);
+* ``join()`` -- the compute stream waits for the side stream and the kept inputs
+  are released.  It is queued as an autograd-engine callback the first time a
+  backward forks, so any consumer of the gradients after ``backward()``
+  (grad-norm, optimizer, tests) is ordered;
+* the data-parallel engine launches a bucket's all-reduce *on the side stream*
+  after making it wait for the compute stream, so RCCL waits for both producers
+  without stalling the compute stream (parallel/ddp.py).
+
+Only gradients that go straight into the flat store use the side stream; graph
+capture (--hip-graph) keeps the single-stream order.  ``HETSEQ_WGRAD_STREAM=0``
+disables it.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+_ENABLED = os.environ.get("HETSEQ_WGRAD_STREAM", "1") == "1"
+# split-K of the side-stream wgrad GEMMs.  The per-call-site choice is measured with the GEMM
+# alone on the chip (4 slices for most weight gradients); running beside the dgrad chain, 2 slices
+# measured best (BERT-base fp32: 16.6 ms/step vs 17.6 with the isolated choice, 19.2 with 1).
+# "auto" = use the isolated measurement.
+_ks = os.environ.get("HETSEQ_SIDE_KSPLIT", "2")
+SIDE_KSPLIT = None if _ks == "auto" else int(_ks)
+_STREAMS: dict = {}
+_state = {"queued": False}
+
+
+def set_enabled(flag: bool):
+    global _ENABLED
+    _ENABLED = bool(flag)
+
+
+def enabled() -> bool:
+    return _ENABLED and torch.cuda.is_available() and not torch.cuda.is_current_stream_capturing()
+
+
+def side(device) -> "torch.cuda.Stream":
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    s = _STREAMS.get(idx)
+    if s is None:
+        s = torch.cuda.Stream(device=torch.device("cuda", idx))
+        _STREAMS[idx] = s
+    return s
+
+
+def active(device) -> "torch.cuda.Stream | None":
+    """The side stream if one has been forked in the current backward, else None."""
+    return _STREAMS.get(device.index) if _state["queued"] else None
+
+
+_KEEP: list = []
+
+
+def fork(device, *tensors) -> "torch.cuda.Stream":
+    from hetseq_amd.ops._C import hip, stream_handle
+
+    s = side(device)
+    hip().stream_wait(s.cuda_stream, stream_handle())
+    _KEEP.extend(tensors)
+    if not _state["queued"]:
+        _state["queued"] = True
+        torch.autograd.Variable._execution_engine.queue_callback(join)
+    return s
+
+
+def join():
+    """Make the current stream wait for every side stream (end of backward); release kept inputs."""
+    if not _state["queued"] and not _KEEP:
+        return
+    from hetseq_amd.ops._C import hip
+
+    _state["queued"] = False
+    for idx, s in _STREAMS.items():
+        hip().stream_wait(torch._C._cuda_getCurrentRawStream(idx), s.cuda_stream)
+    _KEEP.clear()
