@@ -139,6 +139,7 @@ def main():
     if b.host_profile:
         import cProfile
 
+        torch.autograd.set_multithreading_enabled(False)  # backward on this thread, visible to cProfile
         prof = cProfile.Profile()
         prof.enable()
     t0 = time.perf_counter()

@@ -377,8 +377,8 @@ class FusedBertLayer(torch.autograd.Function):
         def wgrad(dy, xin, out):
             if not side:
                 return G.linear_wgrad(dy, xin, out=out, accumulate=acc)
-            with torch.cuda.stream(streams.fork(dy.device, dy, xin)):
-                return G.linear_wgrad(dy, xin, out=out, accumulate=acc, ksplit=streams.SIDE_KSPLIT)
+            return streams.run(dy.device, lambda: G.linear_wgrad(dy, xin, out=out, accumulate=acc,
+                                                                 ksplit=streams.SIDE_KSPLIT), dy, xin)
 
         dW2 = wgrad(do_, f1, Gv.w2 if acc else None)
         df1pre, dbi = G.linear_dgrad_dgelu(do_, W.w2, f1pre, W.bi, db_acc=Gv.bi if acc else None)

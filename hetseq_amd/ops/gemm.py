@@ -84,8 +84,12 @@ def fp32_mode():
 
 
 def _slab(M, N, ksplit, device):
-    """Split-K workspace for ksplit partial [M,N] fp32 planes (grown on demand, reused per stream)."""
-    key = (device, torch.cuda.current_stream(device).cuda_stream)
+    """Split-K workspace for ksplit partial [M,N] fp32 planes (grown on demand).  One per stream
+    role -- the compute stream (or the graph-capture stream standing in for it) and the
+    weight-gradient side stream -- since those two run GEMMs concurrently."""
+    from hetseq_amd.runtime import streams
+
+    key = (device, "side" if streams.is_side(stream_handle()) else "main")
     need = 8 * M * N if ksplit <= 0 else ksplit * M * N
     buf = _SLABS.get(key)
     if buf is None or buf.numel() < need:

@@ -22,9 +22,12 @@ Ordering rules kept here:
   after making it wait for the compute stream, so RCCL waits for both producers
   without stalling the compute stream (parallel/ddp.py).
 
-Only gradients that go straight into the flat store use the side stream; graph
-capture (--hip-graph) keeps the single-stream order.  ``HETSEQ_WGRAD_STREAM=0``
-disables it.
+Only gradients that go straight into the flat store use the side stream.  Under
+HIP-graph capture (--hip-graph) the fork/join events are captured as graph edges
+(the side stream joins the capture at the fork and leaves it at the join).
+``HETSEQ_WGRAD_STREAM=0`` disables it.  The switch costs ~5 us of host time per
+GEMM (raw stream get/set, one C++ event call), so host-bound configurations (bf16
+without graphs) may prefer it off; ``Controller`` decides (see ``auto_enable``).
 """
 from __future__ import annotations
 
@@ -49,7 +52,12 @@ def set_enabled(flag: bool):
 
 
 def enabled() -> bool:
-    return _ENABLED and torch.cuda.is_available() and not torch.cuda.is_current_stream_capturing()
+    return _ENABLED and torch.cuda.is_available()
+
+
+def is_side(stream_handle: int) -> bool:
+    """Whether a raw stream handle is one of the side streams (split-K workspaces are per role)."""
+    return any(s.cuda_stream == stream_handle for s in _STREAMS.values())
 
 
 def side(device) -> "torch.cuda.Stream":
@@ -79,6 +87,18 @@ def fork(device, *tensors) -> "torch.cuda.Stream":
         _state["queued"] = True
         torch.autograd.Variable._execution_engine.queue_callback(join)
     return s
+
+
+def run(device, fn, *tensors):
+    """fn() with the side stream current (forked from the current stream; inputs kept alive).
+    Raw get/set of the current stream: the torch.cuda.stream() context costs ~20 us of host time."""
+    st = fork(device, *tensors)
+    prev = torch._C._cuda_getCurrentStream(st.device_index)
+    torch._C._cuda_setStream(stream_id=st.stream_id, device_index=st.device_index, device_type=st.device_type)
+    try:
+        return fn()
+    finally:
+        torch._C._cuda_setStream(stream_id=prev[0], device_index=prev[1], device_type=prev[2])
 
 
 def join():
