@@ -1,9 +1,11 @@
-# the other BASELINE.md configs that fit on one GPU: phase-2 seq512 bs8, update-freq 4, bf16
+# smoke + the BASELINE configurations on one GPU (phase 1 / phase 2, fp32 / bf16, update-freq 4)
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp HETSEQ_GEMM_TUNE_MISSING=0
-run() {  # name, args...
-  n=$1; shift
-  timeout -k 10 600 python3 bench.py --steps 20 --warmup 5 "$@" > gpurun_out/cfg_$n.log 2>&1 || { echo "$n failed"; tail -20 gpurun_out/cfg_$n.log; return 1; }
-  tail -1 gpurun_out/cfg_$n.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$n', d['dtype'], d['ms_per_step'], 'ms/step', d['tokens_per_s'], 'tok/s host', d['host_ms_per_step'])"
-}
-run ph2_fp32 --seq-len 512 --batch 8 --max-pred 80 && run uf4_fp32 --update-freq 4 && run ph2_bf16 --seq-len 512 --batch 8 --max-pred 80 --dtype bf16 && run uf4_bf16 --update-freq 4 --dtype bf16
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1
+run() { timeout -k 10 400 python bench.py --steps 20 --warmup 5 "$@" > gpurun_out/cfg.log 2>&1 || { tail -20 gpurun_out/cfg.log; exit 1; }
+  tail -1 gpurun_out/cfg.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); c=d['config']; print(d['dtype'], 'seq', c['seq_len'], 'bs', c['per_gpu_batch'], 'uf', c['update_freq'], d['ms_per_step'], 'ms/step', d['seq_per_s'], 'seq/s')"; }
+run --dtype fp32
+run --dtype fp32 --update-freq 4
+run --dtype fp32 --seq-len 512 --batch 8 --max-pred 80
+run --dtype bf16 --seq-len 512 --batch 8 --max-pred 80
+run --dtype bf16 --hip-graph
