@@ -72,9 +72,11 @@ def ln_fwd(a, gamma, beta, eps=1e-12, bias=None, resid=None, p=0.0, mode=0, seed
 
 
 def ln_bwd(dy, z, mean, rstd, gamma, p=0.0, mode=0, seed=0, off=0, want_dz=True, want_da=False, dz_out=None,
-           acc=None):
+           acc=None, side=False):
     """LN backward.  ``acc`` = (dgamma, dbeta[, dbias]) fp32 tensors to ACCUMULATE into
-    (flat-store gradient views); otherwise fresh tensors are returned."""
+    (flat-store gradient views); otherwise fresh tensors are returned.  ``side``: run the
+    parameter-gradient finalisation on the weight-gradient stream (runtime/streams.py) --
+    only dz / da are on the critical path."""
     rows, H = dy.shape
     nb = hip().ln_bwd_num_blocks()
     part = _colpart_buf(nb, H, dy.device)
@@ -87,8 +89,15 @@ def ln_bwd(dy, z, mean, rstd, gamma, p=0.0, mode=0, seed=0, off=0, want_dz=True,
     if acc is not None:
         outs = list(acc[:n])
         assert all(o.is_contiguous() and o.dtype == torch.float32 for o in outs)
-        hip().colpart_finalize([part[i].data_ptr() for i in range(n)], [o.data_ptr() for o in outs], nb, H, 1,
-                               stream_handle())
+
+        def fin():
+            hip().colpart_finalize([part[i].data_ptr() for i in range(n)], [o.data_ptr() for o in outs], nb, H, 1,
+                                   stream_handle())
+
+        if side:
+            streams.run(dy.device, fin, part)
+        else:
+            fin()
     else:
         outs = torch.empty((n, H), dtype=torch.float32, device=dy.device)
         hip().colpart_finalize([part[i].data_ptr() for i in range(n)], [outs[i].data_ptr() for i in range(n)], nb, H,
@@ -275,6 +284,7 @@ class FusedEmbedding(torch.autograd.Function):
         sink = ctx.sink
         if sink is not None:  # accumulate straight into the flat gradient buffer
             dword, dpos, dtype_, dg, db = sink["views"]()
+            streams.wait(dev)  # the tied decoder's weight gradient (side stream) also lands in dword
         else:
             dword = torch.zeros((V, H), dtype=torch.float32, device=dev)
             dpos = torch.zeros((P, H), dtype=torch.float32, device=dev)
@@ -368,11 +378,12 @@ class FusedBertLayer(torch.autograd.Function):
         Gv = sink() if sink is not None else None  # flat-store gradient views (accumulate in place)
         acc = Gv is not None
         # LN2 (bias-dropout-residual) backward
-        dz2, do_, dg2, dbb2, db2 = ln_bwd(dh2, z2, m2, r2, W.g2, p_h, 1, s_2, o_2, True, True,
-                                          acc=(Gv.g2, Gv.bb2, Gv.b2) if acc else None)
-        # weight gradients go into the flat store on the side stream (runtime/streams.py) and
-        # overlap the data-gradient chain; without a flat store they stay in order
+        # weight / bias / LN-parameter gradients go into the flat store on the side stream
+        # (runtime/streams.py) and overlap the data-gradient chain; without a flat store they
+        # stay in order
         side = acc and streams.enabled()
+        dz2, do_, dg2, dbb2, db2 = ln_bwd(dh2, z2, m2, r2, W.g2, p_h, 1, s_2, o_2, True, True,
+                                          acc=(Gv.g2, Gv.bb2, Gv.b2) if acc else None, side=side)
 
         def wgrad(dy, xin, out):
             if not side:
@@ -385,12 +396,15 @@ class FusedBertLayer(torch.autograd.Function):
         dW1 = wgrad(df1pre, h1, Gv.w1 if acc else None)
         dh1 = G.linear_dgrad(df1pre, W.w1, out=dz2, accumulate=True)  # dz2 + df1pre @ W1
         dz1, da1, dg1, db1, dbo = ln_bwd(dh1, z1, m1, r1, W.g1, p_h, 1, s_1, o_1, True, True,
-                                         acc=(Gv.g1, Gv.b1, Gv.bo) if acc else None)
+                                         acc=(Gv.g1, Gv.b1, Gv.bo) if acc else None, side=side)
         dWo = wgrad(da1, ctx_, Gv.wo if acc else None)
         dctx = G.linear_dgrad(da1, W.wo)
         dqkv = attn_bwd(qkv, mask, ctx_, dctx, (lse, dmask), B, S, NH, p_a, bias=W.bqkv)
         dWqkv = wgrad(dqkv, x, Gv.wqkv if acc else None)
-        dbqkv = colsum(dqkv, acc=Gv.bqkv if acc else None)
+        if side:
+            dbqkv = streams.run(dqkv.device, lambda: colsum(dqkv, acc=Gv.bqkv), dqkv)
+        else:
+            dbqkv = colsum(dqkv, acc=Gv.bqkv if acc else None)
         dx = G.linear_dgrad(dqkv, W.wqkv, out=dz1, accumulate=True)  # dz1 + dqkv @ Wqkv
         if acc:
             return (dx, None, None) + (None,) * 16
@@ -495,12 +509,23 @@ class FusedMLMLoss(torch.autograd.Function):
         # bf16 mode: both decoder GEMMs take bf16 operands (fp32 C for the weight gradient);
         # the fp32-operand weight GEMM cost 268 us vs 72 us (tools/bench_mlm_head.py)
         dl_c = dlogits.to(t2.dtype) if t2.dtype != torch.float32 else dlogits
-        dWdec = G.linear_wgrad(dl_c, t2, out=Gv[4] if acc else None, accumulate=acc)
-        dbdec = colsum(dlogits, acc=Gv[5] if acc else None)
+        # parameter gradients on the weight-gradient stream when they go to the flat store (the
+        # decoder one lands in the tied word-embedding gradient: FusedEmbedding.backward waits)
+        side = acc and streams.enabled()
+        if side:
+            dWdec = streams.run(dl_c.device, lambda: G.linear_wgrad(dl_c, t2, out=Gv[4], accumulate=True), dl_c, t2)
+            dbdec = streams.run(dl_c.device, lambda: colsum(dlogits, acc=Gv[5]), dlogits)
+        else:
+            dWdec = G.linear_wgrad(dl_c, t2, out=Gv[4] if acc else None, accumulate=acc)
+            dbdec = colsum(dlogits, acc=Gv[5] if acc else None)
         dt2 = G.gemm(dl_c, Wd)
-        dt1, _, dg, db, _ = ln_bwd(dt2, z, mean, rstd, g, 0.0, 0, acc=(Gv[2], Gv[3]) if acc else None)
+        dt1, _, dg, db, _ = ln_bwd(dt2, z, mean, rstd, g, 0.0, 0, acc=(Gv[2], Gv[3]) if acc else None, side=side)
         dt1pre, dbt = gelu_bwd_colsum(dt1, t1pre, bt, db_acc=Gv[1] if acc else None)
-        dWt = G.linear_wgrad(dt1pre, hsel, out=Gv[0] if acc else None, accumulate=acc)
+        if side:
+            dWt = streams.run(dt1pre.device, lambda: G.linear_wgrad(dt1pre, hsel, out=Gv[0], accumulate=True),
+                              dt1pre, hsel)
+        else:
+            dWt = G.linear_wgrad(dt1pre, hsel, out=Gv[0] if acc else None, accumulate=acc)
         dhsel = G.linear_dgrad(dt1pre, Wt)
         dseq = torch.zeros((ctx.T, hsel.shape[1]), dtype=hsel.dtype, device=hsel.device)
         hip().scatter_add_rows(dtype_code(dseq), dhsel.data_ptr(), idx.data_ptr(), dseq.data_ptr(), idx.numel(),

@@ -101,6 +101,17 @@ def run(device, fn, *tensors):
         torch._C._cuda_setStream(stream_id=prev[0], device_index=prev[1], device_type=prev[2])
 
 
+def wait(device):
+    """Current stream waits for the side stream (mid-backward ordering point, e.g. before the
+    embedding backward accumulates into the word-embedding gradient the tied decoder's
+    side-stream GEMM also writes).  Keeps the backward's join pending."""
+    s = _STREAMS.get(device.index)
+    if s is not None and _state["queued"]:
+        from hetseq_amd.ops._C import hip, stream_handle
+
+        hip().stream_wait(stream_handle(), s.cuda_stream)
+
+
 def join():
     """Make the current stream wait for every side stream (end of backward); release kept inputs."""
     if not _state["queued"] and not _KEEP:
