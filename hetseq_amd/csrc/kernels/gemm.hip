@@ -32,6 +32,7 @@
 // 16-B aligned operands); anything else returns -1 and the caller uses the
 // library GEMM.
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 #include "reduce.h"
@@ -391,10 +392,11 @@ HS_DEVICE bfx8 x_frag(const char* __restrict__ S, int row, int p, int ks, int lr
 // WV = 4: 2x2 waves of 64x64, every thread stages 4x4 of A and of B.
 // WV = 8: 2x4 waves of 64x32 (twice the waves per CU to hide each other's staging), threads
 //         0-255 stage A and 256-511 stage B with the same 4x4 micro-blocks.
-template <bool TA, bool TB, int EPI, int NT, int ABL = 0, int WV = 4>
-__global__ void __launch_bounds__(64 * WV, 2) gemm_x6s_kernel(GemmArgs p) {
+template <bool TA, bool TB, int EPI, int NT, int ABL = 0, int WV = 4, int NBUF = 1>
+__global__ void __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(NBUF == 2 ? 2 : WV / 2, NBUF == 2 ? 2 : WV / 2))) gemm_x6s_kernel(GemmArgs p) {
   constexpr int BM = 128, BN = 128, WC = WV / 2, TM = 2, TN = BN / WC / 32;
-  __shared__ __attribute__((aligned(16))) char smem[2 * 128 * XROW];
+  static_assert(NBUF == 1 || WV == 8, "double-buffered images: 8-wave variant only");
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * 128 * XROW];
   char* const As = smem;
   char* const Bs = smem + 128 * XROW;
 
@@ -453,30 +455,22 @@ __global__ void __launch_bounds__(64 * WV, 2) gemm_x6s_kernel(GemmArgs p) {
   };
   (void)stB;
   const int KT = p.K / p.ksplit / GBK;
-  load();
-  store();
-  __syncthreads();
   constexpr int NPL = NT >= 6 ? 3 : 2, NTERM = NT >= 6 ? 6 : 3;
   constexpr int PA[6] = {2, 0, 1, 1, 0, 0}, PB[6] = {0, 2, 1, 0, 1, 0};  // smallest terms first
-  for (int kt = 0; kt < KT; ++kt) {
-    // fragments of both k-slices first (one wait each), then the next tile's global loads
-    // (the last iteration re-reads its own tile: unconditional, so the registers stay static)
+  // one K tile of MFMA work from the LDS images: fragments of both k-slices first (one wait
+  // each), then `between()` (the next global loads) so they fly under the MFMAs
+  auto compute = [&](auto between, const char* Ab, const char* Bb) {
     bfx8 af[2][3][TM], bf[2][3][TN];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int pl = 0; pl < NPL; ++pl) {
 #pragma unroll
-        for (int i = 0; i < TM; ++i) af[ks][pl][i] = x_frag<TA>(As, wm + 32 * i, pl, ks, lr, q);
+        for (int i = 0; i < TM; ++i) af[ks][pl][i] = x_frag<TA>(Ab, wm + 32 * i, pl, ks, lr, q);
 #pragma unroll
-        for (int j = 0; j < TN; ++j) bf[ks][pl][j] = x_frag<!TB>(Bs, wn + 32 * j, pl, ks, lr, q);
+        for (int j = 0; j < TN; ++j) bf[ks][pl][j] = x_frag<!TB>(Bb, wn + 32 * j, pl, ks, lr, q);
       }
-    if (kt + 1 < KT) {
-      ab += sa;
-      bb += sb;
-    }
-    if (ABL < 1) load();  // ablation builds (tools/bench_gemm_x6.py --ablate; timing only, wrong
-                          // results): 1 no global loads in the loop, 2 + no staging, 3 + no barriers
+    between();
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -485,9 +479,63 @@ __global__ void __launch_bounds__(64 * WV, 2) gemm_x6s_kernel(GemmArgs p) {
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j) acc[i][j] = mma_bf(af[ks][PA[tt]][i], bf[ks][PB[tt]][j], acc[i][j]);
-    if (ABL < 3) __syncthreads();  // every wave is done reading this K tile
-    if (ABL < 2) store();
-    if (ABL < 3) __syncthreads();
+  };
+  // (ABL: ablation builds for tools/bench_gemm_x6.py --ablate, timing only, wrong results:
+  //  1 no global loads in the loop, 2 + no staging, 3 + no barriers)
+  if constexpr (NBUF == 2) {
+    // 8 waves: a thread stages ONE operand, so two register sets fit -- tile kt+1 waits in
+    // registers while tile kt+2 is in flight -- and the LDS images are double-buffered: staging
+    // tile kt+1 into the other buffer needs no barrier before it and overlaps this tile's MFMAs
+    // (the weight gradient runs at ~1 block per CU, with no second block to hide a staging
+    // phase).  Unrolled by two so the register sets and buffers keep fixed roles.
+    char* const As1 = smem + 2 * 128 * XROW;
+    char* const Bs1 = As1 + 128 * XROW;
+    const char* gp = stA ? ab : bb;
+    const int64_t gs = stA ? sa : sb;
+    auto ld = [&](float4(&v)[4], int t) {
+      const char* base = gp + (int64_t)min(t, KT - 1) * gs;  // clamped: unconditional loads
+      if (stA) x_load<!TA>(base, oa, v);
+      else x_load<TB>(base, ob, v);
+    };
+    auto sto = [&](char* A_, char* B_, const float4(&v)[4]) {
+      if (stA) x_store<!TA, NT>(A_, v, st);
+      else x_store<TB, NT>(B_, v, st);
+    };
+    float4 r1[4];
+    ld(va, 0);
+    sto(As, Bs, va);
+    __syncthreads();
+    ld(va, 1);
+    ld(r1, 2);
+    int kt = 0;
+    for (; kt + 1 < KT; kt += 2) {  // buffer 0 = tile kt, va = kt+1, r1 = kt+2
+      compute([] {}, As, Bs);
+      if (ABL < 2) sto(As1, Bs1, va);  // buffer 1 was last read before the previous barrier
+      if (ABL < 1) ld(va, kt + 3);
+      if (ABL < 3) __syncthreads();
+      compute([] {}, As1, Bs1);
+      if (ABL < 2) sto(As, Bs, r1);
+      if (ABL < 1) ld(r1, kt + 4);
+      if (ABL < 3) __syncthreads();
+    }
+    if (kt < KT) compute([] {}, As, Bs);  // odd tile count: the last tile is already in buffer 0
+  } else {
+    load();
+    store();
+    __syncthreads();
+    for (int kt = 0; kt < KT; ++kt) {
+      // the last iteration re-reads its own tile: unconditional, so the registers stay static
+      compute([&] {
+        if (kt + 1 < KT) {
+          ab += sa;
+          bb += sb;
+        }
+        if (ABL < 1) load();
+      }, As, Bs);
+      if (ABL < 3) __syncthreads();  // every wave is done reading this K tile
+      if (ABL < 2) store();
+      if (ABL < 3) __syncthreads();
+    }
   }
   // the epilogue's tile geometry: TM x TN 32x32 accumulators per wave, two wave rows
   epilogue<BM, 2 * 32 * TN, 32, EPI>(p, acc, reinterpret_cast<float*>(smem), m0, n0, tm, slice, wm, wn, wr, lr, q);
@@ -498,6 +546,12 @@ static int g_ablation = 0;  // microbenchmark hook (tile_override bits 3-4)
 // twice the waves hide its transposing staging; measured +8-12%), 4 elsewhere (the 8-wave
 // dgrad needs 160 VGPRs = one block per CU, -25%).  tile_override bit 5 forces 4, bit 6 forces 8.
 static int g_x6_waves = 4;
+// 8-wave variant with double-buffered LDS images (106 KB: one block per CU, one barrier per K
+// tile) -- HETSEQ_X6_DBUF=1; default single buffer (53 KB, blocks of other kernels co-reside).
+static const int g_x6_dbuf = [] {
+  const char* e = std::getenv("HETSEQ_X6_DBUF");
+  return e && e[0] == '1' ? 1 : 0;
+}();
 
 // split-K finish: C = sum_s slab[s] (+ bias) (+ beta * C), fixed slice order (deterministic)
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ slab, int ksplit, int M, int N,
@@ -539,13 +593,18 @@ void launch_cfg(const GemmArgs& a, hipStream_t st) {
         hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 3, 4>), dim3(blocks), dim3(256), 0, st, a);
       else
         hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 0, 4>), dim3(blocks), dim3(256), 0, st, a);
+    } else if (g_x6_dbuf) {
+      if (EPI == kEpiNone && g_ablation == 1)
+        hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 1, 8, 2>), dim3(blocks), dim3(512), 0, st, a);
+      else if (EPI == kEpiNone && g_ablation == 2)
+        hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 2, 8, 2>), dim3(blocks), dim3(512), 0, st, a);
+      else if (EPI == kEpiNone && g_ablation == 3)
+        hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 3, 8, 2>), dim3(blocks), dim3(512), 0, st, a);
+      else
+        hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 0, 8, 2>), dim3(blocks), dim3(512), 0, st, a);
     } else {
       if (EPI == kEpiNone && g_ablation == 1)
         hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 1, 8>), dim3(blocks), dim3(512), 0, st, a);
-      else if (EPI == kEpiNone && g_ablation == 2)
-        hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 2, 8>), dim3(blocks), dim3(512), 0, st, a);
-      else if (EPI == kEpiNone && g_ablation == 3)
-        hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 3, 8>), dim3(blocks), dim3(512), 0, st, a);
       else
         hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 0, 8>), dim3(blocks), dim3(512), 0, st, a);
     }

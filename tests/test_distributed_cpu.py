@@ -129,3 +129,31 @@ def test_bert_tiny_two_ranks(tmp_path):
              "--bucket-cap-mb", "1"] for r in range(2)]
     out0, _ = _run_all(cmds)
     assert "num_updates=4," in out0 and "(epoch 1 @ 5 updates)" in out0
+
+
+def test_bert_tiny_eight_ranks_hetero_3_plus_5(tmp_path):
+    """The driver's 8-rank data-parallel shape rehearsed on CPU/gloo: BERT (tiny) through the
+    flat-store DP engine with several buckets, two heterogeneous launches (3 + 5 spawned
+    processes, tcp:// rendezvous), update-freq 2 (no_sync on the first micro-batch), and a
+    parameter-checksum consistency check after every update."""
+    from hetseq_amd.data.synthetic import write_bert_config, write_bert_shards, write_vocab
+
+    d = tmp_path / "bert"
+    write_bert_shards(str(d), num_shards=2, per_shard=80, seq_len=32, max_pred=5, vocab_size=300, split="train")
+    write_bert_shards(str(d), num_shards=1, per_shard=8, seq_len=32, max_pred=5, vocab_size=300, split="test")
+    write_vocab(str(tmp_path / "vocab.txt"), 300)
+    cfg = write_bert_config(str(tmp_path / "cfg.json"), vocab_size=300, hidden_size=64, num_hidden_layers=2,
+                            num_attention_heads=2, intermediate_size=128)
+    init = "tcp://127.0.0.1:%d" % _free_port()
+    base = [sys.executable, os.path.join(ROOT, "train.py"), "--task", "bert", "--data", str(d), "--dict",
+            str(tmp_path / "vocab.txt"), "--config_file", cfg, "--max-sentences", "4", "--valid-subset", "test",
+            "--max-update", "3", "--cpu", "--distributed-backend", "gloo", "--save-dir", str(tmp_path / "ck"),
+            "--distributed-init-method", init, "--distributed-world-size", "8", "--check-consistency", "1",
+            "--fast-stat-sync", "--lr", "1e-3", "--bucket-cap-mb", "1", "--update-freq", "2", "--num-workers", "0",
+            "--log-format", "simple", "--log-interval", "1"]
+    cmds = [base + ["--distributed-gpus", "3", "--distributed-rank", "0"],
+            base + ["--distributed-gpus", "5", "--distributed-rank", "3"]]
+    out0, _ = _run_all(cmds, timeout=400)
+    assert "(epoch 1 @ 3 updates)" in out0, out0[-2000:]
+    # fast-stat sample size = seq_len x 8 ranks x update-freq 2 (reference bsz semantics, Q03)
+    assert "bsz=512.000" in out0, out0[-2000:]
