@@ -63,6 +63,7 @@ class Controller(object):
             from hetseq_amd.runtime import gemm_tuning
 
             gemm_tuning.enable(getattr(args, "dtype", "fp32"))
+            gemm_tuning.load_engine_choices(getattr(args, "dtype", "fp32"))
         shadow = torch.bfloat16 if self.compute_dtype == torch.bfloat16 else None
         self.store = FlatParamStore(self._model, device=self.device, shadow_dtype=shadow)
         if hasattr(self._model, "attach_store"):

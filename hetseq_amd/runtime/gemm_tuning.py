@@ -49,6 +49,25 @@ def enable(dtype_tag="fp32", tune_missing=None):
     return True
 
 
+CHOICE_DIR = os.path.join(ROOT, "configs", "gemm_choices")
+
+
+def load_engine_choices(dtype_tag="fp32"):
+    """Preload the per-call-site engine choices (HIP kernel vs library, split-K) measured on
+    gfx950 and committed under ``configs/gemm_choices/`` (written by ``bench.py
+    --gemm-choices``), so a run needs no measuring in its first step.  Sites missing from
+    the file are still measured on first use; ``HETSEQ_GEMM_CHOICES=measure`` ignores the
+    file.  Entries measured under another fp32 engine policy are skipped."""
+    if os.environ.get("HETSEQ_GEMM_CHOICES", "") == "measure" or not torch.cuda.is_available():
+        return False
+    path = os.path.join(CHOICE_DIR, "gfx950_%s.json" % dtype_tag)
+    if not os.path.exists(path):
+        return False
+    from hetseq_amd.ops import gemm as G
+
+    return G.load_choices(path)
+
+
 def results():
     """The (op, shape, solution, ms) rows TunableOp holds for this process."""
     if not _done:
