@@ -50,9 +50,13 @@ def main():
           "(`%s`).  TF/s = MFMA FLOPs (512 x MFMA MOPS) / kernel time (counter runs serialise kernels, so times "
           "are indicative); %% of peak against the sustained rates measured by tools/micro/mfma_peak.hip "
           "(155 TF/s fp32, 2170 TF/s bf16); LDS conflict = bank-conflict cycles / LDS-active cycles.\n" % path)
-    print("| kernel | dispatches | total ms | MFMA TF/s | % of sustained MFMA peak | LDS conflict % |\n|---|---|---|---|---|---|")
+    print("Split-bf16 fp32 GEMMs (`gemm_x6s_kernel<..., 6, ...>`) issue six bf16 products per fp32 product: their "
+          "effective fp32 rate is the bf16 MFMA rate / 6 (last column).\n")
+    print("| kernel | dispatches | total ms | MFMA TF/s | % of sustained MFMA peak | LDS conflict % | effective fp32 TF/s |\n"
+          "|---|---|---|---|---|---|---|")
     for t, k, n, u, tf, cf in rows[:top]:
-        print("| `%s` | %d | %.3f | %.1f | %.1f | %.1f |" % (k.replace("|", "/")[:90], n, t / 1e6, tf, u, cf))
+        eff = "%.1f" % (tf / 6.0) if "gemm_x6s_kernel" in k and ", 6," in k else ""
+        print("| `%s` | %d | %.3f | %.1f | %.1f | %.1f | %s |" % (k.replace("|", "/")[:90], n, t / 1e6, tf, u, cf, eff))
 
 
 if __name__ == "__main__":
