@@ -60,7 +60,7 @@ def load_engine_choices(dtype_tag="fp32"):
     file.  Entries measured under another fp32 engine policy are skipped."""
     if os.environ.get("HETSEQ_GEMM_CHOICES", "") == "measure" or not torch.cuda.is_available():
         return False
-    path = os.path.join(CHOICE_DIR, "gfx950_%s.json" % dtype_tag)
+    path = os.environ.get("HETSEQ_GEMM_CHOICES_FILE") or os.path.join(CHOICE_DIR, "gfx950_%s.json" % dtype_tag)
     if not os.path.exists(path):
         return False
     from hetseq_amd.ops import gemm as G
