@@ -62,7 +62,7 @@ void launch_xent_bwd(int, void*, const int64_t*, const float*, int, int, int64_t
 int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, int64_t lda, const void* B,
                 int64_t ldb, void* C, int64_t ldc, const float* bias, int epi, float beta, float* aux, int64_t ldaux,
                 float* part, float* colsum_out, int colsum_acc, int tile_override, hipStream_t st, int ksplit,
-                float* slab, int64_t slab_floats);
+                float* slab, int64_t slab_floats, int mv, int nv, int kv);
 
 // HIP-graph mode: device word holding the dropout seed (see common.h resolve_seed)
 namespace hs {
@@ -241,10 +241,11 @@ PYBIND11_MODULE(_hip, m) {
   m.def("stream_wait", [](i64 waiter, i64 signal) { stream_wait(ST(waiter), ST(signal)); });
   m.def("gemm", [](int dt, int ta, int tb, int M, int N, int K, i64 A, i64 lda, i64 B, i64 ldb, i64 C, i64 ldc, i64 bias,
                    int epi, float beta, i64 aux, i64 ldaux, i64 part, i64 colsum, int colsum_acc, i64 st,
-                   int tile, int ksplit, i64 slab, i64 slab_floats) {
+                   int tile, int ksplit, i64 slab, i64 slab_floats, int mv, int nv, int kv) {
     const int rc = launch_gemm(dt, ta, tb, M, N, K, P(const void*, A), lda, P(const void*, B), ldb, P(void*, C), ldc,
                                P(const float*, bias), epi, beta, P(float*, aux), ldaux, P(float*, part),
-                               P(float*, colsum), colsum_acc, tile, ST(st), ksplit, P(float*, slab), slab_floats);
+                               P(float*, colsum), colsum_acc, tile, ST(st), ksplit, P(float*, slab), slab_floats, mv, nv,
+                               kv);
     if (rc == 0) check_launch("gemm");
     return rc;
   }, pybind11::arg("dt"), pybind11::arg("ta"), pybind11::arg("tb"), pybind11::arg("M"), pybind11::arg("N"),
@@ -252,5 +253,6 @@ PYBIND11_MODULE(_hip, m) {
      pybind11::arg("C"), pybind11::arg("ldc"), pybind11::arg("bias"), pybind11::arg("epi"), pybind11::arg("beta"),
      pybind11::arg("aux"), pybind11::arg("ldaux"), pybind11::arg("part"), pybind11::arg("colsum"),
      pybind11::arg("colsum_acc"), pybind11::arg("st"), pybind11::arg("tile") = -1, pybind11::arg("ksplit") = 0,
-     pybind11::arg("slab") = 0, pybind11::arg("slab_floats") = 0);
+     pybind11::arg("slab") = 0, pybind11::arg("slab_floats") = 0, pybind11::arg("mv") = 0, pybind11::arg("nv") = 0,
+     pybind11::arg("kv") = 0);
 }

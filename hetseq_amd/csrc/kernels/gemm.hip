@@ -77,6 +77,9 @@ struct GemmArgs {
   float beta;
   int ksplit;   // >1: K is cut into ksplit slices, each writes a plain slab (no epilogue)
   float* slab;  // [ksplit][M][N] partial products (summed by splitk_reduce_kernel)
+  // valid extents (EDGE launches only, else = M, N, K): the padded problem is M x N x K; operand
+  // rows past them read as zeros, C rows past Mv are not written, bias past Nv reads as zero
+  int Mv, Nv, Kv;
 };
 
 // LDS image geometry of one operand (rows = BM or BN).  The [k][mn] image is
@@ -170,7 +173,7 @@ HS_DEVICE f32x16 mma_bf(bfx8 a, bfx8 b, f32x16 c) { return __builtin_amdgcn_mfma
 
 // Shared GEMM epilogue (both kernels): split-K slab, or C = acc (+bias) (+beta*C) / GELU /
 // dGELU + column partial sums.  acc[i][j] register r -> row m0+wm+MF*i+Mf::row(r,q), col n0+wn+MF*j+lr.
-template <int BM, int BN, int MF, int EPI>
+template <int BM, int BN, int MF, int EPI, bool EDGE = false>
 HS_DEVICE void epilogue(const GemmArgs& p, typename Mf<MF>::acc_t (&acc)[BM / 2 / MF][BN / 2 / MF], float* smem, int m0,
                         int n0, int tm, int slice, int wm, int wn, int wr, int lr, int q) {
   using M_ = Mf<MF>;
@@ -192,7 +195,7 @@ HS_DEVICE void epilogue(const GemmArgs& p, typename Mf<MF>::acc_t (&acc)[BM / 2 
   for (int j = 0; j < TN; ++j) {
     csum[j] = 0.f;
     const int n = n0 + wn + MF * j + lr;
-    const float bv = (EPI != kEpiNone) ? p.bias[n] : 0.f;
+    const float bv = (EPI != kEpiNone && (!EDGE || n < p.Nv)) ? p.bias[n] : 0.f;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int mb = m0 + wm + MF * i;
@@ -216,13 +219,16 @@ HS_DEVICE void epilogue(const GemmArgs& p, typename Mf<MF>::acc_t (&acc)[BM / 2 
       } else if (use_beta) {
         float old[M_::nreg];
 #pragma unroll
-        for (int r = 0; r < M_::nreg; ++r) old[r] = p.C[(int64_t)(mb + M_::row(r, q)) * p.ldc + n];
+        for (int r = 0; r < M_::nreg; ++r)
+          old[r] = (!EDGE || mb + M_::row(r, q) < p.Mv) ? p.C[(int64_t)(mb + M_::row(r, q)) * p.ldc + n] : 0.f;
 #pragma unroll
         for (int r = 0; r < M_::nreg; ++r)
-          p.C[(int64_t)(mb + M_::row(r, q)) * p.ldc + n] = acc[i][j][r] + bv + p.beta * old[r];
+          if (!EDGE || mb + M_::row(r, q) < p.Mv)
+            p.C[(int64_t)(mb + M_::row(r, q)) * p.ldc + n] = acc[i][j][r] + bv + p.beta * old[r];
       } else {
 #pragma unroll
-        for (int r = 0; r < M_::nreg; ++r) p.C[(int64_t)(mb + M_::row(r, q)) * p.ldc + n] = acc[i][j][r] + bv;
+        for (int r = 0; r < M_::nreg; ++r)
+          if (!EDGE || mb + M_::row(r, q) < p.Mv) p.C[(int64_t)(mb + M_::row(r, q)) * p.ldc + n] = acc[i][j][r] + bv;
       }
     }
   }
@@ -351,15 +357,20 @@ HS_DEVICE void x_offsets(int64_t ldx, int r0, uint32_t (&o)[4], int t) {
                    : (uint32_t)(((int64_t)(4 * (t >> 5) + i) * ldx + r0 + 4 * (t & 31)) * 4);
 }
 
+// lim (EDGE launches): rows of this operand tile that exist -- mn rows from the tile origin for
+// k-contiguous sources, k rows from the K-tile origin for mn-contiguous ones; the rest read as 0
 template <bool KCONTIG>
-HS_DEVICE void x_load(const char* __restrict__ base, const uint32_t (&o)[4], float4 (&v)[4]) {
+HS_DEVICE void x_load(const char* __restrict__ base, const uint32_t (&o)[4], float4 (&v)[4], int lim = 1 << 30) {
+  const int t = threadIdx.x & 255;
   if (KCONTIG) {  // v[i] = k 4c..4c+3 of row 4g+i; 8 lanes per 128-B row segment
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = *reinterpret_cast<const float4*>(base + o[i]);
+    for (int i = 0; i < 4; ++i)
+      v[i] = 4 * (t >> 3) + i < lim ? *reinterpret_cast<const float4*>(base + o[i]) : make_float4(0.f, 0.f, 0.f, 0.f);
   } else {  // 32 lanes per 512-B k row, then a 4x4 register transpose
     float4 w[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) w[j] = *reinterpret_cast<const float4*>(base + o[j]);
+    for (int j = 0; j < 4; ++j)
+      w[j] = 4 * (t >> 5) + j < lim ? *reinterpret_cast<const float4*>(base + o[j]) : make_float4(0.f, 0.f, 0.f, 0.f);
     v[0] = make_float4(w[0].x, w[1].x, w[2].x, w[3].x);
     v[1] = make_float4(w[0].y, w[1].y, w[2].y, w[3].y);
     v[2] = make_float4(w[0].z, w[1].z, w[2].z, w[3].z);
@@ -392,10 +403,11 @@ HS_DEVICE bfx8 x_frag(const char* __restrict__ S, int row, int p, int ks, int lr
 // WV = 4: 2x2 waves of 64x64, every thread stages 4x4 of A and of B.
 // WV = 8: 2x4 waves of 64x32 (twice the waves per CU to hide each other's staging), threads
 //         0-255 stage A and 256-511 stage B with the same 4x4 micro-blocks.
-template <bool TA, bool TB, int EPI, int NT, int ABL = 0, int WV = 4, int NBUF = 1>
+template <bool TA, bool TB, int EPI, int NT, int ABL = 0, int WV = 4, int NBUF = 1, bool EDGE = false>
 __global__ void __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(NBUF == 2 ? 2 : WV / 2, NBUF == 2 ? 2 : WV / 2))) gemm_x6s_kernel(GemmArgs p) {
   constexpr int BM = 128, BN = 128, WC = WV / 2, TM = 2, TN = BN / WC / 32;
   static_assert(NBUF == 1 || WV == 8, "double-buffered images: 8-wave variant only");
+  static_assert(!EDGE || (WV == 4 && EPI <= kEpiBias), "edge-masked launches: 4 waves, plain / bias epilogue");
   __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * 128 * XROW];
   char* const As = smem;
   char* const Bs = smem + 128 * XROW;
@@ -433,8 +445,12 @@ __global__ void __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(NB
   const char* ab = reinterpret_cast<const char*>(p.A) + (TA ? (int64_t)kofs * p.lda : kofs) * 4;
   const char* bb = reinterpret_cast<const char*>(p.B) + (TB ? kofs : (int64_t)kofs * p.ldb) * 4;
   float4 va[4], vb[4];
+  int kld = kofs;  // absolute k of the tile ab / bb point at (edge guards of k-row operands)
   auto load = [&]() {
-    if (WV == 4) {
+    if (EDGE) {
+      x_load<!TA>(ab, oa, va, TA ? p.Kv - kld : p.Mv - m0);
+      x_load<TB>(bb, ob, vb, TB ? p.Nv - n0 : p.Kv - kld);
+    } else if (WV == 4) {
       x_load<!TA>(ab, oa, va);
       x_load<TB>(bb, ob, vb);
     } else if (stA) {  // wave-uniform branch: one operand per half of the block
@@ -529,6 +545,7 @@ __global__ void __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(NB
         if (kt + 1 < KT) {
           ab += sa;
           bb += sb;
+          kld += GBK;
         }
         if (ABL < 1) load();
       }, As, Bs);
@@ -538,7 +555,8 @@ __global__ void __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(NB
     }
   }
   // the epilogue's tile geometry: TM x TN 32x32 accumulators per wave, two wave rows
-  epilogue<BM, 2 * 32 * TN, 32, EPI>(p, acc, reinterpret_cast<float*>(smem), m0, n0, tm, slice, wm, wn, wr, lr, q);
+  epilogue<BM, 2 * 32 * TN, 32, EPI, EDGE>(p, acc, reinterpret_cast<float*>(smem), m0, n0, tm, slice, wm, wn, wr, lr,
+                                           q);
 }
 
 static int g_ablation = 0;  // microbenchmark hook (tile_override bits 3-4)
@@ -556,9 +574,9 @@ static const int g_x6_dbuf = [] {
 // split-K finish: C = sum_s slab[s] (+ bias) (+ beta * C), fixed slice order (deterministic)
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ slab, int ksplit, int M, int N,
                                                             float* __restrict__ C, int64_t ldc,
-                                                            const float* __restrict__ bias, float beta) {
+                                                            const float* __restrict__ bias, float beta, int Mv, int Nv) {
   const int n4 = N / 4;
-  const int64_t total = (int64_t)M * n4, plane = (int64_t)M * N;
+  const int64_t total = (int64_t)Mv * n4, plane = (int64_t)M * N;  // rows past Mv are padding: not written
   for (int64_t u = blockIdx.x * 256ll + threadIdx.x; u < total; u += (int64_t)gridDim.x * 256) {
     const int m = (int)(u / n4), n = (int)(u % n4) * 4;
     const float* s0 = slab + (int64_t)m * N + n;
@@ -567,9 +585,14 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
       const float4 b = *reinterpret_cast<const float4*>(s0 + s * plane);
       a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
     }
-    if (bias) {
+    if (bias && n + 3 < Nv) {
       const float4 b = *reinterpret_cast<const float4*>(bias + n);
       a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    } else if (bias) {  // the quad straddling the valid width (bias past Nv reads as zero)
+      a.x += n < Nv ? bias[n] : 0.f;
+      a.y += n + 1 < Nv ? bias[n + 1] : 0.f;
+      a.z += n + 2 < Nv ? bias[n + 2] : 0.f;
+      a.w += n + 3 < Nv ? bias[n + 3] : 0.f;
     }
     float4* c = reinterpret_cast<float4*>(C + (int64_t)m * ldc + n);
     if (beta != 0.f) {
@@ -584,7 +607,10 @@ template <int BM, int BN, int MF, bool TA, bool TB, int EPI, int NT>
 void launch_cfg(const GemmArgs& a, hipStream_t st) {
   const int blocks = (a.M / BM) * (a.N / BN) * a.ksplit;
   if constexpr (NT > 0) {
-    if (g_x6_waves == 4) {
+    if (a.Mv != a.M || a.Nv != a.N || a.Kv != a.K) {  // padded problem (launch_gemm checked epi)
+      if constexpr (EPI <= kEpiBias)
+        hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 0, 4, 1, true>), dim3(blocks), dim3(256), 0, st, a);
+    } else if (g_x6_waves == 4) {
       if (EPI == kEpiNone && g_ablation == 1)
         hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 1, 4>), dim3(blocks), dim3(256), 0, st, a);
       else if (EPI == kEpiNone && g_ablation == 2)
@@ -675,12 +701,12 @@ static int pick_tile_split(int M, int N, int K, int* ksplit) {
 // 3 dgelu (aux = pre-activation) with column sums of C written (or added,
 // colsum_acc) to colsum_out.  part: scratch of (M/64)*N floats (epi 3 only).
 // ksplit: 0 = automatic (split dtypes only), 1 = none, >1 forced; slab: ksplit*M*N floats
-// of scratch when the split is >1 (epi 0/1 only).
+// of scratch when the split is >1 (epi 0/1 only).  mv/nv/kv: valid extents of a padded problem.
 // Returns -1 when the request is not served (caller falls back to the library).
 int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, int64_t lda, const void* B,
                 int64_t ldb, void* C, int64_t ldc, const float* bias, int epi, float beta, float* aux, int64_t ldaux,
                 float* part, float* colsum_out, int colsum_acc, int tile_override, hipStream_t st, int ksplit,
-                float* slab, int64_t slab_floats) {
+                float* slab, int64_t slab_floats, int mv, int nv, int kv) {
   if ((dtype != 0 && dtype != 2 && dtype != 3) || M <= 0 || N <= 0 || K <= 0 || K % GBK != 0) return -1;
   auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
   if (!al16(A) || !al16(B) || lda % 4 || ldb % 4) return -1;
@@ -707,8 +733,14 @@ int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, i
   if (tile < 0) return -1;
   if (ks > 1 && (K % (ks * GBK) != 0 || (int64_t)ks * M * N > slab_floats || N % 4 || ldc % 4 || !al16(C)))
     return -1;
+  // valid extents of a padded problem (0 = the whole dimension): split-bf16 engine, plain / bias
+  // epilogue only; the caller guarantees the operand pads it does not guard are allocated
+  mv = mv > 0 ? mv : M;
+  nv = nv > 0 ? nv : N;
+  kv = kv > 0 ? kv : K;
+  if ((mv != M || nv != N || kv != K) && (!nt || epi > kEpiBias || mv > M || nv > N || kv > K)) return -1;
   GemmArgs a{static_cast<const float*>(A), static_cast<const float*>(B), static_cast<float*>(C), bias, aux, part,
-             lda, ldb, ldc, ldaux, M, N, K, beta, ks, slab};
+             lda, ldb, ldc, ldaux, M, N, K, beta, ks, slab, mv, nv, kv};
   int rc;
   if (nt == 6)
     rc = launch_split<6>(tile, ta, tb, epi, a, st);
@@ -725,7 +757,7 @@ int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, i
     const int64_t n4 = (int64_t)M * (N / 4);
     const int grid = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid), dim3(256), 0, st, slab, ks, M, N, static_cast<float*>(C), ldc,
-                       epi >= 1 ? bias : nullptr, beta);
+                       epi >= 1 ? bias : nullptr, beta, a.Mv, a.Nv);
   }
   if (epi == kEpiDGelu) {
     const int bm = tile == 2 ? 64 : 128;

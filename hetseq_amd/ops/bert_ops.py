@@ -489,10 +489,16 @@ class FusedMLMLoss(torch.autograd.Function):
         t1pre = G.linear_fwd(hsel, Wt)
         t1 = bias_gelu_fwd(t1pre, bt)
         t2, z, mean, rstd = ln_fwd(t1, g, b, eps)
-        logits = G.gemm(t2, Wd, ta=False, tb=True, bias=bdec, epi=1, out_dtype=torch.float32) \
-            if t2.dtype == torch.float32 else G.gemm(t2, Wd, tb=True, bias=bdec, epi=1, out_dtype=torch.float32)
+        # tied decoder on the compacted rows; fp32: split-bf16 kernel on the vocabulary padded to
+        # 512 (logits is a view of a zero-padded buffer the backward reuses), else library GEMM
+        if t2.dtype == torch.float32:
+            logits, lbuf = G.decoder_logits(t2, Wd, bdec)
+        else:
+            logits, lbuf = G.gemm(t2, Wd, tb=True, bias=bdec, epi=1, out_dtype=torch.float32), None
         out, lse = xent_fwd(logits, lab)
-        ctx.save_for_backward(idx, lab, hsel, t1pre, t1, z, mean, rstd, t2, logits, lse, out, g, bt)
+        ctx.padded = lbuf is not None
+        ctx.save_for_backward(idx, lab, hsel, t1pre, t1, z, mean, rstd, t2, lbuf if lbuf is not None else logits, lse,
+                              out, g, bt)
         ctx.meta = meta
         ctx.T = T
         return out[0]
@@ -500,6 +506,9 @@ class FusedMLMLoss(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dloss):
         idx, lab, hsel, t1pre, t1, z, mean, rstd, t2, logits, lse, out, g, bt = ctx.saved_tensors
+        lbuf = None
+        if ctx.padded:  # zero-padded [R, pad512(V)] buffer: the loss works on its [:, :V] view
+            lbuf, logits = logits, logits[:, :ctx.meta["weights"]()[1].shape[0]]
         Wt, Wd = ctx.meta["weights"]()
         sink = ctx.meta.get("grad_sink")
         Gv = sink() if sink is not None else None  # (wt, bt, g, b, wdec, bdec) flat-store views
@@ -512,13 +521,27 @@ class FusedMLMLoss(torch.autograd.Function):
         # parameter gradients on the weight-gradient stream when they go to the flat store (the
         # decoder one lands in the tied word-embedding gradient: FusedEmbedding.backward waits)
         side = acc and streams.enabled()
-        if side:
-            dWdec = streams.run(dl_c.device, lambda: G.linear_wgrad(dl_c, t2, out=Gv[4], accumulate=True), dl_c, t2)
-            dbdec = streams.run(dl_c.device, lambda: colsum(dlogits, acc=Gv[5]), dlogits)
+        V = dlogits.shape[1]
+        if lbuf is not None:  # padded split-bf16 decoder products (pad columns of dlogits stay zero)
+            def dwdec():
+                out_w = Gv[4] if acc else torch.zeros((V, t2.shape[1]), dtype=torch.float32, device=t2.device)
+                return G.decoder_wgrad(lbuf, t2, V, out_w, accumulate=True)
         else:
-            dWdec = G.linear_wgrad(dl_c, t2, out=Gv[4] if acc else None, accumulate=acc)
-            dbdec = colsum(dlogits, acc=Gv[5] if acc else None)
-        dt2 = G.gemm(dl_c, Wd)
+            def dwdec():
+                return G.linear_wgrad(dl_c, t2, out=Gv[4] if acc else None, accumulate=acc)
+        def dbias():
+            if lbuf is None:
+                return colsum(dlogits, acc=Gv[5] if acc else None)
+            full = colsum(lbuf)[:V]  # column sums of the padded buffer (pad columns are zero)
+            return Gv[5].add_(full) if acc else full
+
+        if side:
+            dWdec = streams.run(dl_c.device, dwdec, dl_c, t2, lbuf)
+            dbdec = streams.run(dl_c.device, dbias, dlogits, lbuf)
+        else:
+            dWdec = dwdec()
+            dbdec = dbias()
+        dt2 = G.decoder_dgrad(lbuf, Wd, V) if lbuf is not None else G.gemm(dl_c, Wd)
         dt1, _, dg, db, _ = ln_bwd(dt2, z, mean, rstd, g, 0.0, 0, acc=(Gv[2], Gv[3]) if acc else None, side=side)
         dt1pre, dbt = gelu_bwd_colsum(dt1, t1pre, bt, db_acc=Gv[1] if acc else None)
         if side:

@@ -114,14 +114,17 @@ def _hip_ok(a, b, out, *extra):
 
 
 def _hip_gemm(a, b, ta, tb, out, bias=None, epi=EPI_NONE, beta=0.0, aux=None, part=None, colsum=None,
-              colsum_acc=False, tile=-1, fp32=None, ksplit=0):
+              colsum_acc=False, tile=-1, fp32=None, ksplit=0, dims=None, valid=None):
     """Launch the HIP kernel; returns False (nothing launched) if the shape is not served.
 
     ``fp32`` picks the product engine (default: the HETSEQ_FP32_GEMM policy); ``ksplit``
-    0 = automatic split-K for the split-bf16 engines, 1 = none, >1 forced.
+    0 = automatic split-K for the split-bf16 engines, 1 = none, >1 forced.  ``dims`` /
+    ``valid``: (M, N, K) of a padded problem and its valid extents (split-bf16 engine only):
+    operand rows past the valid extents read as zero, C rows past valid M are not written.
     """
-    M, N, K = _dims(a, b, ta, tb)
-    assert out.shape == (M, N)
+    M, N, K = dims if dims is not None else _dims(a, b, ta, tb)
+    mv, nv, kv = valid if valid is not None else (0, 0, 0)
+    assert dims is not None or out.shape == (M, N)
     dt = _FP32_DT[fp32 or _FP32]
     slab = _slab(M, N, ksplit, a.device) if dt and epi <= EPI_BIAS and ksplit != 1 else None
     rc = hip().gemm(dt, int(ta), int(tb), M, N, K, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0),
@@ -129,7 +132,7 @@ def _hip_gemm(a, b, ta, tb, out, bias=None, epi=EPI_NONE, beta=0.0, aux=None, pa
                     aux.data_ptr() if aux is not None else 0, aux.stride(0) if aux is not None else 0,
                     part.data_ptr() if part is not None else 0, colsum.data_ptr() if colsum is not None else 0,
                     int(colsum_acc), stream_handle(), tile, ksplit,
-                    slab.data_ptr() if slab is not None else 0, slab.numel() if slab is not None else 0)
+                    slab.data_ptr() if slab is not None else 0, slab.numel() if slab is not None else 0, mv, nv, kv)
     return rc == 0
 
 
@@ -225,6 +228,115 @@ def gemm(a, b, ta=False, tb=False, out=None, bias=None, epi=EPI_NONE, beta=0.0, 
         if _choose(key, run_hip, run_blas) == "hip" and _hip_gemm(a, b, ta, tb, out, bias, epi, beta, ksplit=ks[0]):
             return out
     return _blas_gemm(a, b, ta, tb, out, bias, epi, beta, out_dtype)
+
+
+# ------------------------------------------------------------------ tied MLM decoder (V = 30522)
+def _pad_vocab(n):
+    # a multiple of 512: 128-wide tiles for the logits / weight-gradient products, and K-splits
+    # of up to 16 slices for the data-gradient product (K = vocab, only 30 output tiles)
+    return (n + 511) // 512 * 512
+
+
+def _padded_ok(*ts):
+    return (_MODE != "blas" and _FP32 != "native" and all(t.is_cuda and t.dtype == torch.float32 for t in ts)
+            and ts[0].shape[0] % 128 == 0)
+
+
+def decoder_logits(t2, w, bias):
+    """logits [R, V] = t2 [R, H] @ w[V, H]^T + bias, returned as a view of a [R, pad512(V)]
+    buffer whose pad columns are zero -- the split-bf16 engine runs the padded problem with the
+    missing weight rows / bias entries read as zero.  Library GEMM when faster or not served."""
+    R, H = t2.shape
+    V = w.shape[0]
+    if not _padded_ok(t2, w, bias):
+        return gemm(t2, w, tb=True, bias=bias, epi=EPI_BIAS, out_dtype=torch.float32), None
+    Vp = _pad_vocab(V)
+    buf = torch.empty((R, Vp), dtype=torch.float32, device=t2.device)
+    key = (R, V, H, "decoder_fwd")
+
+    def run_hip():
+        return _hip_gemm(t2, w, False, True, buf, bias, EPI_BIAS, 0.0, dims=(R, Vp, H), valid=(R, V, H))
+
+    def run_blas():
+        buf[:, V:].zero_()
+        torch.addmm(bias, t2, w.t(), out=buf[:, :V])
+
+    if _choose_padded(key, run_hip, run_blas) == "hip" and run_hip():
+        return buf[:, :V], buf
+    run_blas()
+    return buf[:, :V], buf
+
+
+def decoder_dgrad(dlogits_buf, w, V):
+    """dt2 [R, H] = dlogits [R, V] @ w [V, H] from the zero-padded [R, pad512(V)] buffer."""
+    R, Vp = dlogits_buf.shape
+    H = w.shape[1]
+    out = torch.empty((R, H), dtype=torch.float32, device=w.device)
+    key = (R, H, V, "decoder_dgrad")
+    ks = [0]
+
+    def run_hip():
+        return _hip_gemm(dlogits_buf, w, False, False, out, dims=(R, H, Vp), valid=(R, H, V), ksplit=ks[0])
+
+    def run_blas():
+        torch.mm(dlogits_buf[:, :V], w, out=out)
+
+    if key not in GEMM_CHOICES and _MODE == "auto" and not torch.cuda.is_current_stream_capturing():
+        best = None  # K = vocab over only (R/128) x (H/128) tiles: measure the split
+        for cand in (4, 8, 16):
+            ks[0] = cand
+            if run_hip():
+                t = _bench(run_hip)
+                best = (t, cand) if best is None or t < best[0] else best
+        t_blas = _bench(run_blas)
+        if best is None:
+            GEMM_CHOICES[key] = ("blas", None, round(t_blas, 4))
+        else:
+            GEMM_CHOICES[key] = ("hip" if best[0] < t_blas else "blas", round(best[0], 4), round(t_blas, 4), best[1])
+    c = GEMM_CHOICES.get(key)
+    if c is not None and len(c) > 3:
+        ks[0] = c[3]
+    if _choose_padded(key, run_hip, run_blas) == "hip" and run_hip():
+        return out
+    run_blas()
+    return out
+
+
+def decoder_wgrad(dlogits_buf, t2, V, out, accumulate):
+    """dW [V, H] (+)= dlogits^T @ t2 from the zero-padded buffer (rows past V are not written)."""
+    R, Vp = dlogits_buf.shape
+    H = t2.shape[1]
+    key = (V, H, R, "decoder_wgrad", bool(accumulate))
+    beta = 1.0 if accumulate else 0.0
+
+    def run_hip(dst):
+        return _hip_gemm(dlogits_buf, t2, True, False, dst, beta=beta, dims=(Vp, H, R), valid=(V, H, R))
+
+    def run_blas(dst):
+        if accumulate:
+            dst.addmm_(dlogits_buf[:, :V].t(), t2)
+        else:
+            torch.mm(dlogits_buf[:, :V].t(), t2, out=dst)
+
+    if key not in GEMM_CHOICES and _MODE == "auto" and not torch.cuda.is_current_stream_capturing():
+        scratch = out.clone()  # measuring must not accumulate into the real gradient
+        _choose_padded(key, lambda: run_hip(scratch), lambda: run_blas(scratch))
+    if _choose_padded(key, None, None) == "hip" and run_hip(out):
+        return out
+    run_blas(out)
+    return out
+
+
+def _choose_padded(key, run_hip, run_blas):
+    """Engine choice for the padded decoder products: measured once per site in auto mode
+    (side effects only into buffers the caller overwrites afterwards), else the mode."""
+    if _MODE == "hip":
+        return "hip"
+    if key in GEMM_CHOICES:
+        return GEMM_CHOICES[key][0]
+    if torch.cuda.is_current_stream_capturing():
+        return "blas"
+    return _choose(key, run_hip, run_blas)
 
 
 def linear_fwd(x, w, bias=None, out=None):

@@ -617,3 +617,36 @@ def test_attention_dropout_bitmask_matches_philox(cuda):
     v = qkv0[:, 2 * NH * 64: 2 * NH * 64 + 64]
     expect = (keep[:, None] * v).sum(0) / S / (1 - p)
     _close(out[5, :64], expect, 1e-4, 1e-5, "bitmask row")
+
+
+def test_decoder_padded_vocab_products(cuda):
+    """Tied-decoder products on the split-bf16 engine with a vocabulary that is not a multiple of
+    the tile (padded to 128; missing weight rows / bias read as zero, gradient rows past V never
+    written) against fp64, on the HIP engine explicitly."""
+    from hetseq_amd.ops import gemm as G
+
+    torch.manual_seed(31)
+    R, H, V = 256, 192, 1000
+    t2 = torch.randn(R, H, device=cuda)
+    w = torch.randn(V, H, device=cuda) * 0.05
+    bias = torch.randn(V, device=cuda)
+    old = G._MODE
+    try:
+        G.set_mode("hip")
+        logits, buf = G.decoder_logits(t2, w, bias)
+        assert buf is not None and buf.shape == (R, 1024) and logits.shape == (R, V)  # pad to 512
+        ref = t2.double() @ w.double().t() + bias.double()
+        _close(logits, ref, 1e-5, 1e-4, "decoder logits")
+        assert torch.count_nonzero(buf[:, V:]) == 0
+        buf[:, :V].copy_(torch.randn(R, V, device=cuda))  # stands in for dlogits (pad columns stay zero)
+        dl = buf[:, :V].double()
+        dt2 = G.decoder_dgrad(buf, w, V)
+        _close(dt2, dl @ w.double(), 1e-5, 1e-4, "decoder dgrad")
+        guard = torch.full((V + 64, H), 7.0, device=cuda)  # rows past V must stay untouched
+        g0 = torch.randn(V, H, device=cuda)
+        guard[:V].copy_(g0)
+        G.decoder_wgrad(buf, t2, V, guard[:V], accumulate=True)
+        _close(guard[:V], g0.double() + dl.t() @ t2.double(), 1e-5, 1e-4, "decoder wgrad")
+        assert torch.all(guard[V:] == 7.0)
+    finally:
+        G.set_mode(old)
