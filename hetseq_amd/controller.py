@@ -57,6 +57,10 @@ class Controller(object):
         # (BERT-base 18.4 -> 16.6 ms); off for bf16, whose eager step is host-bound (the stream
         # switches cost ~1 ms of host time per step there) and under --hip-graph (HIP graph
         # replay does not run the two branches concurrently).  HETSEQ_WGRAD_STREAM overrides.
+        if getattr(args, "fp32_gemm", None):
+            from hetseq_amd.ops import gemm as G
+
+            G.set_fp32_mode(args.fp32_gemm)
         if "HETSEQ_WGRAD_STREAM" not in os.environ:
             streams.set_enabled(self.compute_dtype == torch.float32 and not getattr(args, "hip_graph", False))
         if self.cuda and getattr(args, "gemm_tuning", True):
