@@ -46,6 +46,8 @@ def parse():
     p.add_argument("--host-profile", default=None, help="cProfile the timed loop into this file")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="process-group backend for N > 1 (nccl = RCCL; gloo only to rehearse several ranks on one GPU)")
+    p.add_argument("--comm-engine", default="auto", choices=["auto", "native", "c10d"],
+                   help="gradient collectives for N > 1: native RCCL engine (auto with nccl) or torch c10d")
     p.add_argument("--gemm-choices", default=None,
                    help="JSON of measured GEMM engine choices: loaded if it exists (no measuring in warm-up), "
                         "else written after the run (profiling runs use it to keep tuning out of the trace)")
@@ -93,7 +95,7 @@ def main():
             "--max-sentences", str(b.batch), "--lr", "1e-4", "--warmup-updates", "100", "--weight-decay", "0.01",
             "--fast-stat-sync", "--clip-norm", "25", "--dtype", b.dtype, "--bucket-cap-mb", str(b.bucket_cap_mb),
             "--distributed-world-size", str(world), "--num-workers", "2", "--log-format", "none",
-            "--update-freq", str(b.update_freq)]
+            "--update-freq", str(b.update_freq), "--comm-engine", b.comm_engine]
     if b.no_fused:
         argv.append("--no-fused")
     if b.hip_graph:
@@ -175,6 +177,8 @@ def main():
     if rank == 0 and b.gemm_choices and not os.path.exists(b.gemm_choices):
         G.save_choices(b.gemm_choices)
     if rank == 0:
+        comm_kind = "none" if world == 1 else (
+            "rccl-native" if getattr(ctl.model, "comm", None) is not None else "c10d-" + b.dist_backend)
         out = {
             "metric": "avg sec/step, BERT-base seq128 bs=32/GPU",
             "value": round(sec, 6),
@@ -195,7 +199,7 @@ def main():
                        "global_batch": seqs, "seq_len": b.seq_len, "per_gpu_batch": b.batch,
                        "update_freq": b.update_freq, "parallelism": "dp%d" % world,
                        "fused_kernels": not b.no_fused, "bucket_cap_mb": b.bucket_cap_mb,
-                       "hip_graph": bool(b.hip_graph and world == 1)},
+                       "hip_graph": bool(b.hip_graph and world == 1), "comm": comm_kind},
             "final_train_loss_logged": round(loss, 5),
             "host_ms_per_step": round(host / b.steps * 1000, 3),
             "data_wait_ms_per_step": round(data_wait / b.steps * 1000, 3),
@@ -204,6 +208,8 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
+        if getattr(ctl.model, "comm", None) is not None:
+            ctl.model.comm.close()
         dist.destroy_process_group()
     return 0
 

@@ -111,7 +111,9 @@ class Controller(object):
         if self._wrapped_model is None:
             if self.args.distributed_world_size > 1 and dist.is_initialized() and not self.args.use_bmuf:
                 self._wrapped_model = FlatDDP(self._model, self.store, bucket_cap_mb=self.args.bucket_cap_mb,
-                                              find_unused_parameters=self.args.find_unused_parameters)
+                                              find_unused_parameters=self.args.find_unused_parameters,
+                                              comm_engine=getattr(self.args, "comm_engine", "auto"),
+                                              timeout_s=getattr(self.args, "collective_timeout", 1800.0))
             else:
                 self._wrapped_model = self._model
                 if self.args.distributed_world_size > 1 and dist.is_initialized() and self.args.use_bmuf:
@@ -251,7 +253,10 @@ class Controller(object):
         scale = None  # grad multiplier: W/sample_size of the reference, divided by W (we sum, not average)
         if self.fast_stat_sync:
             if self._sync_stats():
-                dist.all_reduce(stats)
+                if isinstance(self.model, FlatDDP):
+                    self.model.all_reduce_(stats)  # native engine: in-stream RCCL, no c10d bookkeeping
+                else:
+                    dist.all_reduce(stats)
             stats[2:4].div_(stats[0:1] * LN2)
             sample_size_t = stats[0]
             logging_output = {"nsentences": stats[1], "loss": stats[2], "nll_loss": stats[3], "ntokens": stats[4]}

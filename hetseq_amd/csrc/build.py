@@ -1,11 +1,12 @@
 """In-tree native build for hetseq_amd (no setuptools, no hipify, no JIT cache).
 
-Three extension modules are produced next to the package sources so that
+Four extension modules are produced next to the package sources so that
 they travel with the repository snapshot to the GPU box:
 
 * ``hetseq_amd/_native*.so`` -- host runtime (batcher), plain g++.
 * ``hetseq_amd/_h5*.so``     -- HDF5 shard reader/writer/prefetcher, g++ + libhdf5.
 * ``hetseq_amd/_hip*.so``    -- CDNA4 kernels, ``hipcc --offload-arch=gfx950``.
+* ``hetseq_amd/_comm*.so``   -- RCCL gradient-communication engine (comm stream, watchdog).
 
 The HIP module does not include any torch header: kernels are launched
 through a thin pybind11 layer that takes raw device addresses and a
@@ -190,12 +191,42 @@ def build_hip(verbose=False, jobs=8):
     return out
 
 
+def _torch_lib():
+    """torch's bundled ROCm runtime directory: the comm engine links the SAME librccl / libamdhip64
+    that torch loaded (one RCCL instance per process)."""
+    import importlib.util
+
+    spec = importlib.util.find_spec("torch")
+    return os.path.join(os.path.dirname(spec.origin), "lib")
+
+
+def build_comm(verbose=False, jobs=4):
+    """``hetseq_amd/_comm*.so`` -- the RCCL gradient-communication engine (host C++, g++)."""
+    src = os.path.join(HERE, "comm", "comm.cpp")
+    out = os.path.join(PKG, "_comm" + EXT)
+    if not _newer(out, [src]):
+        return out
+    tlib = _torch_lib()
+    rccl = os.path.join(tlib, "librccl.so")
+    if not os.path.exists(rccl):
+        rccl = os.path.join(ROCM, "lib", "librccl.so")
+    hip = os.path.join(tlib, "libamdhip64.so")
+    if not os.path.exists(hip):
+        hip = os.path.join(ROCM, "lib", "libamdhip64.so")
+    flags = ["-O2", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall", "-D__HIP_PLATFORM_AMD__",
+             "-I" + os.path.join(ROCM, "include")] + ["-I" + p for p in _py_includes()]
+    objs, changed = _compile_objs("g++", flags, [src], [], os.path.join(BUILD_DIR, "comm"), verbose, jobs)
+    _link("g++", objs, out, ["-pthread", rccl, hip, "-Wl,-rpath," + os.path.dirname(rccl)], verbose, changed)
+    return out
+
+
 def build_all(verbose=False, hip=True, h5=True):
     outs = [build_native(verbose)]
     if h5:
         outs.append(build_h5(verbose))
     if hip:
         outs.append(build_hip(verbose))
+        outs.append(build_comm(verbose))
     return outs
 
 

@@ -15,7 +15,8 @@ change a reference default):
   --device-id-offset N      map local rank i -> device i+N (heterogeneous launches on one node, Q24)
   --per-rank-seed           different dropout streams per rank (reference: identical, Q14)
   --check-consistency N     all-reduce a parameter checksum every N updates
-  --collective-timeout S    timeout (seconds) for process-group collectives
+  --collective-timeout S    timeout (seconds) for process-group collectives (and the RCCL watchdog)
+  --comm-engine E           gradient collectives: native RCCL engine (auto on GPU+nccl) or c10d
   --checkpoint-activations  recompute encoder layers in backward
   --json-log PATH           append one JSON object per logged update
   --profile                 roctx ranges + per-phase hipEvent timing
@@ -210,7 +211,12 @@ def add_mi355x_args(parser):
     group.add_argument("--check-consistency", type=int, default=0, metavar="N",
                        help="every N updates all-reduce a parameter checksum and fail on divergence")
     group.add_argument("--collective-timeout", type=float, default=1800.0, metavar="SEC",
-                       help="timeout for process-group collectives")
+                       help="timeout for process-group collectives; the native engine's watchdog aborts the "
+                            "communicator when a collective outlives it")
+    group.add_argument("--comm-engine", default="auto", choices=["auto", "native", "c10d"],
+                       help="gradient / stats collectives: the native RCCL engine (greatest-priority comm "
+                            "stream, event-gated buckets, watchdog; auto = on GPUs with the nccl backend) or "
+                            "torch.distributed (c10d)")
     group.add_argument("--checkpoint-activations", action="store_true",
                        help="recompute encoder layers during backward to save activation memory")
     group.add_argument("--json-log", type=str, default=None, metavar="PATH",

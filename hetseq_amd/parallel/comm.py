@@ -1,0 +1,151 @@
+"""Python facade of the native RCCL communication engine (``hetseq_amd/_comm``).
+
+SURVEY §2.3 / §5.8: the reference's gradient exchange is torch DDP's C++ reducer
+over NCCL (controller.py:74-89) and its stats go through c10d
+(controller.py:294-296).  Here the data-parallel engine (``parallel/ddp.py``)
+drives a communicator of its own (``csrc/comm/comm.cpp``): bucket all-reduces
+on a greatest-priority comm stream gated by events on the producer streams,
+a consumer-side join, in-stream small collectives, and a watchdog that aborts
+the communicator when an operation outlives ``--collective-timeout`` (or RCCL
+reports an async error) so the job fails loudly instead of hanging.
+
+Rendezvous: rank 0 draws the RCCL unique id and publishes it through the
+process group's store (the job's ``tcp://`` / ``file://`` / env rendezvous),
+so no extra port or file is needed.  Engine selection (``--comm-engine``):
+``native`` (default on GPUs with the nccl backend) or ``c10d`` (torch's
+ProcessGroupNCCL / gloo; always used on CPU).
+"""
+from __future__ import annotations
+
+import itertools
+import os
+import warnings
+
+import torch
+import torch.distributed as dist
+
+DTYPES = {torch.float32: 0, torch.bfloat16: 1, torch.float64: 2, torch.int64: 3, torch.uint8: 4, torch.int32: 5}
+OPS = {"sum": 0, "min": 1, "max": 2}
+_ids = itertools.count()
+
+
+def module():
+    """The compiled engine, or None when it is not built (CPU-only checkouts)."""
+    try:
+        from hetseq_amd import _comm
+    except ImportError:
+        return None
+    return _comm
+
+
+def _stream(s=None):
+    return (s if s is not None else torch.cuda.current_stream()).cuda_stream
+
+
+class NativeComm(object):
+    """One RCCL communicator over the ranks of ``group`` (all of them take part in construction)."""
+
+    def __init__(self, group=None, timeout_s=1800.0, device=None):
+        mod = module()
+        if mod is None:
+            raise RuntimeError("hetseq_amd._comm is not built (python -m hetseq_amd.csrc.build)")
+        self.group = group or dist.group.WORLD
+        self.rank = dist.get_rank(self.group)
+        self.size = dist.get_world_size(self.group)
+        self.device = torch.cuda.current_device() if device is None else device
+        key = "hetseq_comm_uid_%d" % next(_ids)
+        store = dist.distributed_c10d._get_default_store()
+        if self.rank == 0:
+            store.set(key, mod.unique_id())
+        uid = store.get(key)  # blocks until rank 0 published it (the store's own timeout applies)
+        self._c = mod.Comm(uid, self.size, self.rank, self.device, float(timeout_s))
+
+    # ------------------------------------------------------------------ bucket path
+    def all_reduce_async(self, t, producers=(), op="sum"):
+        """In-place all-reduce of contiguous ``t`` on the comm stream, ordered after the work
+        enqueued so far on every stream in ``producers`` (default: the current stream)."""
+        hs = [_stream(s) for s in producers] or [_stream()]
+        self._c.all_reduce_async(t.data_ptr(), t.numel(), DTYPES[t.dtype], OPS[op], hs)
+
+    def wait(self, stream=None):
+        """``stream`` (default current) waits for every collective issued on the comm stream."""
+        self._c.wait(_stream(stream))
+
+    # ------------------------------------------------------------------ in-stream collectives
+    def all_reduce(self, t, op="sum", stream=None):
+        assert t.is_contiguous()
+        self._c.all_reduce(t.data_ptr(), t.numel(), DTYPES[t.dtype], OPS[op], _stream(stream))
+        return t
+
+    def broadcast(self, t, src=0, stream=None):
+        assert t.is_contiguous()
+        self._c.broadcast(t.data_ptr(), t.numel(), DTYPES[t.dtype], src, _stream(stream))
+        return t
+
+    def all_gather(self, out, t, stream=None):
+        """``out`` = concatenation over ranks of ``t`` (``out.numel() == size * t.numel()``)."""
+        assert out.is_contiguous() and t.is_contiguous() and out.numel() == self.size * t.numel()
+        self._c.all_gather(t.data_ptr(), out.data_ptr(), t.numel(), DTYPES[t.dtype], _stream(stream))
+        return out
+
+    # ------------------------------------------------------------------ health
+    def check(self):
+        """Raise if the watchdog aborted the communicator (timeout or async RCCL error)."""
+        self._c.check()
+
+    @property
+    def aborted(self):
+        return self._c.aborted
+
+    @property
+    def stream_handle(self):
+        return self._c.stream
+
+    def inject_stall(self, n=1):
+        """Fault-injection hook: the watchdog treats the next ``n`` collectives as stuck."""
+        self._c.inject_stall(n)
+
+    def outstanding(self):
+        return self._c.outstanding()
+
+    def close(self):
+        self._c.close()
+
+
+def want_native(engine, device_is_cuda, group=None):
+    """Resolve ``--comm-engine`` ('auto' | 'native' | 'c10d') for a process group."""
+    engine = os.environ.get("HETSEQ_COMM_ENGINE", engine or "auto")
+    if engine == "c10d" or not device_is_cuda:
+        return False
+    backend = dist.get_backend(group or dist.group.WORLD)
+    if backend != "nccl":
+        if engine == "native":
+            warnings.warn("--comm-engine native needs the nccl (RCCL) backend; using c10d (%s)" % backend)
+        return False
+    if module() is None:
+        if engine == "native":
+            raise RuntimeError("--comm-engine native: hetseq_amd._comm is not built")
+        return False
+    return True
+
+
+def create(engine, device_is_cuda, group=None, timeout_s=1800.0):
+    """A NativeComm when the engine resolves to native on EVERY rank, else None (c10d path).
+    The ranks agree first (one c10d all-reduce of an availability flag), because the RCCL
+    initialisation itself blocks until all ranks join it."""
+    engine = os.environ.get("HETSEQ_COMM_ENGINE", engine or "auto")
+    if engine == "c10d" or not device_is_cuda or dist.get_backend(group or dist.group.WORLD) != "nccl":
+        want_native(engine, device_is_cuda, group)  # (warns on an explicit native request)
+        return None
+    local = 1.0
+    try:
+        local = 0.0 if want_native(engine, device_is_cuda, group) else 1.0
+    except RuntimeError as e:
+        warnings.warn(str(e))
+    flag = torch.tensor([local], device="cuda")
+    dist.all_reduce(flag, group=group)
+    if float(flag.item()) != 0.0:
+        if local == 0.0:
+            warnings.warn("native RCCL engine unavailable on some rank; using c10d")
+        return None
+    return NativeComm(group, timeout_s=timeout_s)

@@ -20,7 +20,14 @@ controller.py:74-89) with an engine built on the flat gradient buffer
 * ``no_sync()`` skips communication for the first update_freq-1 micro
   batches (reference: controller.py:245-258);
 * the constructor broadcasts rank 0's parameters (one collective on the flat
-  buffer, X3).
+  buffer, X3);
+* on GPUs with the nccl backend the collectives go through the native RCCL
+  engine (``parallel/comm.py`` over ``csrc/comm/comm.cpp``): a bucket's
+  all-reduce is enqueued on a greatest-priority comm stream behind events on
+  BOTH producer streams (compute and weight-gradient), the end of backward
+  makes the compute stream wait for the comm stream, and a watchdog turns a
+  stuck collective into an error.  ``--comm-engine c10d`` (and every CPU/gloo
+  run) uses ``torch.distributed`` instead.
 
 Bucket sizing for MI355X: with 7 xGMI links per GPU a ring all-reduce is
 per-link bound; the default 25 MB (reference default) yields one bucket per
@@ -34,17 +41,22 @@ import contextlib
 import torch
 import torch.distributed as dist
 
+from hetseq_amd.parallel import comm as native_comm
 from hetseq_amd.runtime import profiling, streams
 
 
 class FlatDDP(torch.nn.Module):
     def __init__(self, module, store, process_group=None, bucket_cap_mb=25, find_unused_parameters=False,
-                 broadcast=True):
+                 broadcast=True, comm_engine="auto", timeout_s=1800.0):
         super().__init__()
         self.module = module
         self.store = store
         self.process_group = process_group or dist.group.WORLD
         self.world_size = dist.get_world_size(self.process_group)
+        # native RCCL engine (None: torch.distributed); chosen identically on every rank
+        # (a 1-rank group gets one only on an explicit "native" request: the single-GPU tests)
+        self.comm = native_comm.create(comm_engine, store.grad.is_cuda, self.process_group, timeout_s) \
+            if self.world_size > 1 or comm_engine == "native" else None
         self.find_unused_parameters = find_unused_parameters
         self.require_sync = True
         cap = max(1, int(bucket_cap_mb * 1024 * 1024 / 4))
@@ -75,9 +87,12 @@ class FlatDDP(torch.nn.Module):
         # directly into the flat buffer (the AccumulateGrad node still runs, after
         # that Function's kernels were enqueued), so one signal covers both paths.
         self._hooks = [p.register_post_accumulate_grad_hook(self._grad_ready) for p in params]
-        if broadcast and self.world_size > 1:
+        if broadcast and (self.world_size > 1 or self.comm is not None):
             with torch.no_grad():
-                dist.broadcast(store.param, src=0, group=self.process_group)
+                if self.comm is not None:
+                    self.comm.broadcast(store.param, src=0)
+                else:
+                    dist.broadcast(store.param, src=0, group=self.process_group)
             store.sync_shadow()
 
     def _reset_state(self):
@@ -125,7 +140,12 @@ class FlatDDP(torch.nn.Module):
         profiling.range_push("allreduce_bucket%d" % b)
         g = self.store.grad
         side = streams.active(g.device) if g.is_cuda else None
-        if side is not None:
+        if self.comm is not None:
+            # the comm stream waits for both producers; neither producer stream is stalled
+            cur = torch.cuda.current_stream(g.device)
+            self.comm.all_reduce_async(g[lo:hi], producers=(cur, side) if side is not None else (cur,))
+            work = None
+        elif side is not None:
             # the bucket's weight gradients come from the wgrad side stream, its biases / LN
             # from the compute stream: issue the collective from the side stream after it
             # waits for the compute stream, so RCCL orders after both without stalling compute
@@ -135,7 +155,8 @@ class FlatDDP(torch.nn.Module):
         else:
             work = dist.all_reduce(g[lo:hi], group=self.process_group, async_op=True)
         profiling.range_pop()
-        self.works.append(work)
+        if work is not None:
+            self.works.append(work)
 
     def _finalize(self):
         if self.next_launch < len(self.buckets):
@@ -150,9 +171,19 @@ class FlatDDP(torch.nn.Module):
             self._launch_ready()
         if self.store.grad.is_cuda:
             streams.join()  # compute stream after the wgrad stream (and the collectives issued on it)
+        if self.comm is not None:
+            self.comm.wait()  # compute stream after the comm stream (no host synchronisation)
+            self.comm.check()  # raises if the watchdog aborted a stuck / failed collective
         for w in self.works:
             w.wait()
         self.works = []
+
+    def all_reduce_(self, t):
+        """In-place SUM of a small device tensor across the data-parallel group (fast stats)."""
+        if self.comm is not None and t.is_cuda:
+            return self.comm.all_reduce(t)
+        dist.all_reduce(t, group=self.process_group)
+        return t
 
     def parameters(self, recurse=True):
         return self.module.parameters(recurse)

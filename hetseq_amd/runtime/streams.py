@@ -18,9 +18,10 @@ Ordering rules kept here:
   are released.  It is queued as an autograd-engine callback the first time a
   backward forks, so any consumer of the gradients after ``backward()``
   (grad-norm, optimizer, tests) is ordered;
-* the data-parallel engine launches a bucket's all-reduce *on the side stream*
-  after making it wait for the compute stream, so RCCL waits for both producers
-  without stalling the compute stream (parallel/ddp.py).
+* the data-parallel engine orders a bucket's all-reduce after both producers
+  without stalling the compute stream: the native RCCL engine's comm stream
+  waits on events of both streams; the c10d path issues the collective from
+  the side stream after it waits for the compute stream (parallel/ddp.py).
 
 Only gradients that go straight into the flat store use the side stream.  Under
 HIP-graph capture (--hip-graph) the fork/join events are captured as graph edges

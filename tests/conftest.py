@@ -25,6 +25,7 @@ def _native_built():
 
         if torch.cuda.is_available():
             build.build_hip()
+            build.build_comm()
     except Exception:
         pass
     yield
