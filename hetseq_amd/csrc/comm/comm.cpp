@@ -91,9 +91,12 @@ class Comm {
     watchdog_ = std::thread([this] { watch(); });
   }
 
-  ~Comm() { close(); }
+  ~Comm() { close(false); }
 
-  void close() {
+  // graceful: destroy the communicator when every operation has completed (all ranks close at
+  // the same point); otherwise -- operations still outstanding (a peer died) or process exit --
+  // abort it, which never waits for peers.
+  void close(bool graceful) {
     {
       std::lock_guard<std::mutex> g(mu_);
       if (closed_.load()) return;
@@ -104,8 +107,14 @@ class Comm {
     if (comm_) {
       if (!aborted_.load()) {  // (an aborted communicator was freed by ncclCommAbort)
         hipSetDevice(device_);
-        hipStreamSynchronize(stream_);
-        ncclCommDestroy(comm_);
+        bool done = true;
+        for (auto& p : pending_) done = done && !p.stalled && hipEventQuery(p.ev) == hipSuccess;
+        if (graceful && done) {
+          hipStreamSynchronize(stream_);
+          ncclCommDestroy(comm_);
+        } else {
+          ncclCommAbort(comm_);
+        }
       }
       comm_ = nullptr;
     }
@@ -332,7 +341,7 @@ PYBIND11_MODULE(_comm, m) {
       .def("all_gather", &Comm::all_gather, py::arg("send"), py::arg("recv"), py::arg("count"), py::arg("dtype"),
            py::arg("stream"))
       .def("check", &Comm::check)
-      .def("close", &Comm::close)
+      .def("close", &Comm::close, py::arg("graceful") = true)
       .def("inject_stall", &Comm::inject_stall)
       .def("outstanding", &Comm::outstanding)
       .def_property_readonly("stream", &Comm::stream)

@@ -40,6 +40,7 @@ from torch.utils import checkpoint
 
 logger = logging.getLogger(__name__)
 
+TF_WEIGHTS_NAME = "model.ckpt"
 CONFIG_NAME = "bert_config.json"
 WEIGHTS_NAME = "pytorch_model.bin"
 
@@ -602,7 +603,14 @@ class BertPreTrainedModel(nn.Module):
 
             shutil.rmtree(tempdir, ignore_errors=True)
         if from_tf:
-            raise NotImplementedError("TensorFlow checkpoint import needs TensorFlow, which is not installed")
+            # reference: bert_modeling.py:685-688 (TF_WEIGHTS_NAME = 'model.ckpt'); read without TensorFlow
+            from hetseq_amd.utils.tf_checkpoint import load_tf_weights_in_bert
+
+            prefix = os.path.join(serialization_dir, TF_WEIGHTS_NAME)
+            if not os.path.exists(prefix + ".index") and os.path.exists(os.path.join(serialization_dir,
+                                                                                    "bert_model.ckpt.index")):
+                prefix = os.path.join(serialization_dir, "bert_model.ckpt")  # Google's release name
+            return load_tf_weights_in_bert(model, prefix)
         renamed = {}
         for k, v in state_dict.items():
             nk = k.replace("gamma", "weight").replace("beta", "bias")

@@ -17,9 +17,11 @@ ProcessGroupNCCL / gloo; always used on CPU).
 """
 from __future__ import annotations
 
+import atexit
 import itertools
 import os
 import warnings
+import weakref
 
 import torch
 import torch.distributed as dist
@@ -59,6 +61,10 @@ class NativeComm(object):
             store.set(key, mod.unique_id())
         uid = store.get(key)  # blocks until rank 0 published it (the store's own timeout applies)
         self._c = mod.Comm(uid, self.size, self.rank, self.device, float(timeout_s))
+        # at interpreter exit (no explicit close): abort -- frees the communicator without waiting
+        # for peers, while the HIP runtime is still alive (never from static destructors)
+        ref = weakref.ref(self)
+        atexit.register(lambda: ref() is not None and ref()._c.close(False))
 
     # ------------------------------------------------------------------ bucket path
     def all_reduce_async(self, t, producers=(), op="sum"):
@@ -108,8 +114,10 @@ class NativeComm(object):
     def outstanding(self):
         return self._c.outstanding()
 
-    def close(self):
-        self._c.close()
+    def close(self, graceful=True):
+        """Destroy the communicator (every rank at the same point), or abort it when operations
+        are still outstanding / ``graceful`` is False."""
+        self._c.close(graceful)
 
 
 def want_native(engine, device_is_cuda, group=None):
