@@ -623,6 +623,20 @@ int launch_attn_bwd_fused_bf16(const void* qkv, const int64_t* mask, const float
                                const void* dctx, const float* lse, void* dqkv, const uint32_t* dmask, int B, int S,
                                int NH, int D, float p, hipStream_t st);
 
+int launch_attn_fwd_x6(const float* qkv, const int64_t* mask, const float* bqkv, float* ctx, float* lse,
+                       uint32_t* dmask, int B, int S, int NH, int D, float p, uint64_t seed, uint64_t off,
+                       hipStream_t st);
+
+// fp32 attention products: "x6" (split-bf16 on the bf16 matrix cores, attention_x6.hip) or
+// "native" (exact-fp32 MFMA) -- HETSEQ_ATTN_FP32, default x6
+static int g_attn_fp32_x6 = [] {
+  const char* e = std::getenv("HETSEQ_ATTN_FP32");
+  return e && std::string(e) == "native" ? 0 : 1;
+}();
+
+void set_attn_fp32_mode(int x6) { g_attn_fp32_x6 = x6; }
+int attn_fp32_mode() { return g_attn_fp32_x6; }
+
 // HETSEQ_ATTN_BF16_MFMA=0 keeps bf16 attention on the fp32-MFMA kernels (A/B and tests)
 static bool bf16_mfma_enabled() {
   const char* e = std::getenv("HETSEQ_ATTN_BF16_MFMA");
@@ -644,6 +658,8 @@ int launch_attn_fwd(int dtype, const void* qkv, const int64_t* mask, const float
   dim3 grid((S + 127) / 128, B * NH);
   if (dtype != 0 && bf16_mfma_enabled())  // bf16 matrix cores (attention_bf16.hip)
     return launch_attn_fwd_bf16(qkv, mask, bqkv, ctx, lse, dmask, B, S, NH, D, p, seed, off, st);
+  if (dtype == 0 && g_attn_fp32_x6)  // fp32 as split-bf16 products (attention_x6.hip)
+    return launch_attn_fwd_x6((const float*)qkv, mask, bqkv, (float*)ctx, lse, dmask, B, S, NH, D, p, seed, off, st);
   if (dtype == 0)
     hipLaunchKernelGGL(attn_fwd_kernel<float>, grid, dim3(256), 0, st, (const float*)qkv, mask, bqkv, (float*)ctx,
                        lse, dmask, S, NH, p, seed, off, g_seed_dev);

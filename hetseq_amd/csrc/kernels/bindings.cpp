@@ -50,6 +50,8 @@ void launch_mlm_compact(const int64_t*, int, int, int, int32_t*, int64_t*, int32
 void launch_gather_rows(int, const void*, const int32_t*, void*, int, int, hipStream_t);
 void launch_scatter_add_rows(int, const void*, const int32_t*, void*, int, int, hipStream_t);
 // attention.hip
+void set_attn_fp32_mode(int x6);
+int attn_fp32_mode();
 int launch_attn_fwd(int, const void*, const int64_t*, const float*, void*, float*, uint32_t*, int, int, int, int, float,
                     u64, u64, hipStream_t);
 int launch_attn_bwd(int, const void*, const int64_t*, const float*, const void*, const void*, const float*, float*,
@@ -209,6 +211,8 @@ PYBIND11_MODULE(_hip, m) {
     check_launch("scatter_add_rows");
   });
 
+  m.def("set_attn_fp32_mode", &set_attn_fp32_mode, "fp32 attention products: 1 split-bf16 (x6), 0 exact-fp32 MFMA");
+  m.def("attn_fp32_mode", &attn_fp32_mode);
   m.def("attn_fwd", [](int dt, i64 qkv, i64 mask, i64 bqkv, i64 ctx, i64 lse, i64 dmask, int B, int S, int NH, int D,
                        float p, u64 seed, u64 off, i64 st) {
     check(launch_attn_fwd(dt, P(const void*, qkv), P(const int64_t*, mask), P(const float*, bqkv), P(void*, ctx),

@@ -149,6 +149,38 @@ def test_attention_fwd_bwd(cuda, B, S, NH):
     _close(qkv.grad, qkv2.grad, 1e-4, 1e-5, "attn dqkv")
 
 
+@pytest.mark.parametrize("B,S,NH,p", [(2, 128, 12, 0.0), (2, 96, 2, 0.1), (1, 512, 2, 0.0), (2, 192, 2, 0.1)])
+def test_attention_fwd_x6_fp32_level(cuda, B, S, NH, p):
+    """fp32 forward on split-bf16 products: the same keep bits as the exact-fp32 MFMA kernel,
+    and an error against fp64 at the exact-fp32 kernel's level (not bf16's)."""
+    from hetseq_amd.ops import bert_ops
+    from hetseq_amd.ops._C import hip
+
+    torch.manual_seed(31)
+    H = NH * 64
+    qkv = torch.randn(B * S, 3 * H, device=cuda)
+    bias = torch.randn(3 * H, device=cuda) * 0.1
+    mask = torch.ones(B, S, dtype=torch.int64, device=cuda)
+    mask[-1, S // 3:] = 0
+    old = hip().attn_fp32_mode()
+    try:
+        hip().set_attn_fp32_mode(1)
+        out6, (lse6, bits6) = bert_ops.attn_fwd(qkv, mask, B, S, NH, p, 3, 11, bias=bias)
+        hip().set_attn_fp32_mode(0)
+        out32, (lse32, bits32) = bert_ops.attn_fwd(qkv, mask, B, S, NH, p, 3, 11, bias=bias)
+    finally:
+        hip().set_attn_fp32_mode(old)
+    if p > 0:
+        assert torch.equal(bits6, bits32)
+    _close(lse6, lse32, 1e-5, 1e-5, "x6 lse")
+    _close(out6, out32, 1e-5, 1e-6, "x6 vs exact-fp32 attention")
+    if p == 0.0:
+        ref = _ref_attention(qkv.double() + bias.double(), mask, B, S, NH)
+        e6 = float((out6.double() - ref).abs().max())
+        e32 = float((out32.double() - ref).abs().max())
+        assert e6 <= 2 * e32 + 1e-7, (e6, e32)
+
+
 @pytest.mark.parametrize("B,S,NH", [(2, 128, 12), (2, 96, 2), (1, 512, 2)])
 def test_attention_fwd_bf16_mfma(cuda, B, S, NH, monkeypatch):
     """bf16 matrix-core forward vs an fp64 reference on the same bf16 inputs (+ bias), and vs the fp32-MFMA path."""
