@@ -16,7 +16,6 @@ from __future__ import annotations
 import collections
 import os
 
-import numpy as np
 import torch
 
 from hetseq_amd.data import data_utils, iterators
