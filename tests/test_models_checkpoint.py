@@ -143,3 +143,35 @@ def test_load_reference_format_checkpoint_with_empty_extra_state(tmp_path):
     torch.save(state, tmp_path / "ref.pt")
     st = load_checkpoint_to_cpu(str(tmp_path / "ref.pt"))
     assert st["optimizer_history"][0]["num_updates"] == 3 and st["extra_state"] == {}
+
+
+def test_token_classification_task_trains(tmp_path):
+    """The working replacement of the reference's unreachable BertFineTuningTask (tasks.py:261-285, Q13)."""
+    import argparse
+    import json
+
+    from hetseq_amd.tasks import BertTokenClassificationTask
+
+    cfg = tmp_path / "bert_config.json"
+    cfg.write_text(json.dumps(dict(vocab_size=64, hidden_size=32, num_hidden_layers=1, num_attention_heads=2,
+                                   intermediate_size=64, hidden_act="gelu", hidden_dropout_prob=0.0,
+                                   attention_probs_dropout_prob=0.0, max_position_embeddings=32,
+                                   type_vocab_size=2, initializer_range=0.02)))
+    vocab = tmp_path / "vocab.txt"
+    vocab.write_text("\n".join("tok%d" % i for i in range(64)) + "\n")
+    args = argparse.Namespace(config_file=str(cfg), dict=str(vocab), num_label=5)
+    task = BertTokenClassificationTask.setup_task(args)
+    assert len(task.dictionary) == 64
+    model = task.build_model(args)
+
+    class _Opt(object):
+        def backward(self, loss):
+            loss.backward()
+
+    torch.manual_seed(0)
+    ids = torch.randint(0, 64, (3, 12))
+    sample = [ids, torch.zeros_like(ids), torch.ones_like(ids), torch.randint(0, 5, (3, 12))]
+    loss, sample_size, log = task.train_step(sample, model, _Opt())
+    # the reference's sample_size is len(sample[0][0]): the sequence length (tasks.py:164)
+    assert torch.isfinite(loss) and sample_size == 12 and log["nsentences"] == 12
+    assert model.classifier.weight.grad is not None and model.classifier.weight.grad.abs().sum() > 0
