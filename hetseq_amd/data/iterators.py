@@ -1,23 +1,27 @@
 """Epoch / shard / group iterators (reference: data/iterators.py:10-275).
 
-Index randomisation and assignment across ranks are kept exactly (the heart
-of HetSeq): the frozen global batch list is shuffled per epoch
-with ``seed + epoch`` (identical on every rank), sharded STRIDED
-(``batches[shard_id::num_shards]``), and short shards are padded with ``[]``
-so that every rank runs the same number of updates; ``state_dict`` /
-``load_state_dict`` fast-forward inside an epoch.
+Behaviour kept from the reference (the cross-rank "index
+randomisation and assignment"):
 
-MI355X-native data path: when the dataset can build a native prefetcher
-(``BertH5Dataset``), batches are read by C++ worker threads straight into
+* the global batch list is frozen once;
+* epoch ``e`` visits it in the order of a legacy-NumPy shuffle seeded with
+  ``seed + e`` -- the same permutation on every rank;
+* rank ``r`` of ``W`` takes every W-th batch starting at ``r`` and pads its
+  share with ``[]`` up to ``ceil(len / W)``, so every rank runs the same number
+  of updates (the controller turns ``[]`` into a dummy ``loss * 0`` batch);
+* ``state_dict`` stores (epoch, iterations_in_epoch) and resuming skips the
+  batches already consumed in that epoch.
+
+MI355X-native data path: datasets that can build a native prefetcher
+(``BertH5Dataset.make_batch_stream``) are read by C++ worker threads into
 pinned staging slots and copied to the GPU with ``non_blocking`` copies on a
 dedicated HIP stream, event-fenced to the compute stream -- no DataLoader
-worker processes and no pageable blocking copies.  Other datasets use a
-``torch.utils.data.DataLoader`` exactly like the reference.
+worker processes and no pageable blocking copies.  Any other dataset goes
+through a ``torch.utils.data.DataLoader`` over this rank's batch list.
 """
 from __future__ import annotations
 
 import itertools
-import math
 import os
 
 import numpy as np
@@ -26,35 +30,55 @@ import torch
 from hetseq_amd.data import data_utils
 
 
+def shard_batches(batches, num_shards, shard_id, fill_value=None):
+    """Strided share ``batches[shard_id::num_shards]`` padded to ``ceil(len / num_shards)``."""
+    if not 0 <= shard_id < num_shards:
+        raise ValueError("shard_id must be between 0 and num_shards")
+    share = list(batches[shard_id::num_shards])
+    want = -(-len(batches) // num_shards)
+    return share + [fill_value] * (want - len(share))
+
+
+def epoch_order(batches, seed):
+    """``batches`` permuted by the legacy global NumPy RNG seeded with ``seed`` (RNG state restored)."""
+    out = list(batches)
+    with data_utils.numpy_seed(seed):
+        np.random.shuffle(out)
+    return out
+
+
 class CountingIterator(object):
-    """Wrapper around an iterable that maintains the iteration count."""
+    """Iterator over ``iterable`` that counts the items handed out (``count``), starting at ``start``."""
 
     def __init__(self, iterable, start=0):
         self.iterable = iterable
         self.count = start
-        self.itr = iter(self)
         self.len = start + len(iterable)
+        self._src = iter(iterable)
 
     def __len__(self):
         return self.len
 
     def __iter__(self):
-        for x in self.iterable:
-            self.count += 1
-            yield x
+        return self
 
     def __next__(self):
-        return next(self.itr)
+        item = next(self._src)
+        self.count += 1
+        return item
 
     def has_next(self):
-        return self.count < len(self)
+        return self.count < self.len
 
     def skip(self, num_to_skip):
-        next(itertools.islice(self.itr, num_to_skip, num_to_skip), None)
+        for _ in itertools.islice(self, num_to_skip):
+            pass
         return self
 
 
 class EpochBatchIterating(object):
+    """Interface of a resumable multi-epoch batch iterator."""
+
     def __len__(self) -> int:
         raise NotImplementedError
 
@@ -76,7 +100,7 @@ class EpochBatchIterating(object):
 
 
 class EpochBatchIterator(EpochBatchIterating):
-    """A multi-epoch, sharded, resumable iterator over a dataset."""
+    """Multi-epoch, sharded, resumable iterator over ``dataset`` with frozen batches."""
 
     def __init__(self, dataset, collate_fn, batch_sampler, seed=1, num_shards=1, shard_id=0, num_workers=0, epoch=0,
                  device=None):
@@ -92,23 +116,27 @@ class EpochBatchIterator(EpochBatchIterating):
         self.epoch = epoch
         self.shuffle = True
         self._cur_epoch_itr = None
-        self._next_epoch_itr = None
+        self._next_epoch_itr = None  # set by load_state_dict: the resumed, partly consumed epoch
         self._supports_prefetch = getattr(dataset, "supports_prefetch", False)
 
     def __len__(self):
         return len(self.frozen_batches)
 
+    @property
+    def resuming(self) -> bool:
+        """True between ``load_state_dict`` of a mid-epoch position and the next ``next_epoch_itr``."""
+        return self._next_epoch_itr is not None
+
     def next_epoch_itr(self, shuffle=True, fix_batches_to_gpus=False):
-        if self._next_epoch_itr is not None:
-            self._cur_epoch_itr = self._next_epoch_itr
-            self._next_epoch_itr = None
+        if self.resuming:
+            self._cur_epoch_itr, self._next_epoch_itr = self._next_epoch_itr, None
         else:
             self.epoch += 1
             self.shuffle = shuffle
-            self._cur_epoch_itr = self._get_iterator_for_epoch(self.epoch, shuffle,
-                                                               fix_batches_to_gpus=fix_batches_to_gpus)
-        if hasattr(self.dataset, "set_epoch"):
-            self.dataset.set_epoch(self.epoch)
+            self._cur_epoch_itr = self._open(self.epoch, shuffle, fix_batches_to_gpus=fix_batches_to_gpus)
+        set_epoch = getattr(self.dataset, "set_epoch", None)
+        if set_epoch is not None:
+            set_epoch(self.epoch)
         return self._cur_epoch_itr
 
     def end_of_epoch(self) -> bool:
@@ -116,72 +144,53 @@ class EpochBatchIterator(EpochBatchIterating):
 
     @property
     def iterations_in_epoch(self):
-        if self._cur_epoch_itr is not None:
-            return self._cur_epoch_itr.count
-        elif self._next_epoch_itr is not None:
-            return self._next_epoch_itr.count
-        return 0
+        itr = self._cur_epoch_itr if self._cur_epoch_itr is not None else self._next_epoch_itr
+        return 0 if itr is None else itr.count
 
     def state_dict(self):
         return {"epoch": self.epoch, "iterations_in_epoch": self.iterations_in_epoch, "shuffle": self.shuffle}
 
     def load_state_dict(self, state_dict):
         self.epoch = state_dict["epoch"]
-        itr_pos = state_dict.get("iterations_in_epoch", 0)
-        if itr_pos > 0:
-            self._next_epoch_itr = self._get_iterator_for_epoch(self.epoch, shuffle=state_dict.get("shuffle", True),
-                                                                offset=itr_pos)
+        done = state_dict.get("iterations_in_epoch", 0)
+        if done > 0:
+            self._next_epoch_itr = self._open(self.epoch, state_dict.get("shuffle", True), offset=done)
 
     def epoch_batches(self, epoch, shuffle, fix_batches_to_gpus=False):
         """This rank's batch list for ``epoch`` (exposed for tests/tools)."""
-
-        def shuffle_batches(batches, seed):
-            with data_utils.numpy_seed(seed):
-                np.random.shuffle(batches)
-            return batches
-
+        order = epoch_order(self.frozen_batches, self.seed + epoch) if shuffle and not (
+            self._supports_prefetch and fix_batches_to_gpus) else list(self.frozen_batches)
+        mine = shard_batches(order, self.num_shards, self.shard_id, fill_value=[])
         if self._supports_prefetch:
-            batches = self.frozen_batches
-            if shuffle and not fix_batches_to_gpus:
-                batches = shuffle_batches(list(batches), self.seed + epoch)
-            batches = list(ShardedIterator(batches, self.num_shards, self.shard_id, fill_value=[]))
-            self.dataset.prefetch([i for s in batches for i in s])
+            self.dataset.prefetch([i for b in mine for i in b])
             if shuffle and fix_batches_to_gpus:
-                batches = shuffle_batches(batches, self.seed + epoch + self.shard_id)
-        else:
-            if shuffle:
-                batches = shuffle_batches(list(self.frozen_batches), self.seed + epoch)
-            else:
-                batches = self.frozen_batches
-            batches = list(ShardedIterator(batches, self.num_shards, self.shard_id, fill_value=[]))
-        return batches
+                mine = epoch_order(mine, self.seed + epoch + self.shard_id)
+        return mine
 
-    def _get_iterator_for_epoch(self, epoch, shuffle, fix_batches_to_gpus=False, offset=0):
-        batches = self.epoch_batches(epoch, shuffle, fix_batches_to_gpus)
-        if offset > 0 and offset >= len(batches):
+    def _open(self, epoch, shuffle, fix_batches_to_gpus=False, offset=0):
+        mine = self.epoch_batches(epoch, shuffle, fix_batches_to_gpus)
+        if offset > 0 and offset >= len(mine):
             return None
-        remaining = batches[offset:]
-        maker = getattr(self.dataset, "make_batch_stream", None)
-        if maker is not None:
-            stream = maker(remaining, num_threads=max(1, self.num_workers), device=self.device)
-            return CountingIterator(stream, start=offset)
-        if self.num_workers > 0:
-            os.environ["PYTHONWARNINGS"] = "ignore:semaphore_tracker:UserWarning"
-        return CountingIterator(
-            torch.utils.data.DataLoader(self.dataset, collate_fn=self.collate_fn, batch_sampler=remaining,
-                                        num_workers=self.num_workers),
-            start=offset,
-        )
+        todo = mine[offset:]
+        make_stream = getattr(self.dataset, "make_batch_stream", None)
+        if make_stream is not None:
+            src = make_stream(todo, num_threads=max(1, self.num_workers), device=self.device)
+        else:
+            if self.num_workers > 0:
+                os.environ["PYTHONWARNINGS"] = "ignore:semaphore_tracker:UserWarning"
+            src = torch.utils.data.DataLoader(self.dataset, collate_fn=self.collate_fn, batch_sampler=todo,
+                                              num_workers=self.num_workers)
+        return CountingIterator(src, start=offset)
 
 
 class GroupedIterator(object):
-    """Wrapper around an iterable that returns groups (chunks) of items."""
+    """Yields lists of ``chunk_size`` consecutive items (the last one may be shorter): update-freq groups."""
 
     def __init__(self, iterable, chunk_size):
-        self._len = int(math.ceil(len(iterable) / float(chunk_size)))
-        self.offset = int(math.ceil(getattr(iterable, "count", 0) / float(chunk_size)))
         self.itr = iterable
         self.chunk_size = chunk_size
+        self._len = -(-len(iterable) // chunk_size)
+        self.offset = -(-getattr(iterable, "count", 0) // chunk_size)
 
     def __len__(self):
         return self._len
@@ -190,36 +199,25 @@ class GroupedIterator(object):
         return self
 
     def __next__(self):
-        chunk = []
-        try:
-            for _ in range(self.chunk_size):
-                chunk.append(next(self.itr))
-        except StopIteration as e:
-            if len(chunk) == 0:
-                raise e
-        return chunk
+        group = list(itertools.islice(self.itr, self.chunk_size))
+        if not group:
+            raise StopIteration
+        return group
 
 
 class ShardedIterator(object):
-    """A sharded wrapper around an iterable, padded to length."""
+    """Iterator over this shard's strided share of ``iterable``, padded with ``fill_value``."""
 
     def __init__(self, iterable, num_shards, shard_id, fill_value=None):
-        if shard_id < 0 or shard_id >= num_shards:
-            raise ValueError("shard_id must be between 0 and num_shards")
-        self._sharded_len = len(iterable) // num_shards
-        if len(iterable) % num_shards > 0:
-            self._sharded_len += 1
-        self.itr = itertools.zip_longest(
-            range(self._sharded_len),
-            itertools.islice(iterable, shard_id, len(iterable), num_shards),
-            fillvalue=fill_value,
-        )
+        items = iterable if hasattr(iterable, "__getitem__") else list(iterable)
+        self._items = shard_batches(items, num_shards, shard_id, fill_value)
+        self._pos = iter(self._items)
 
     def __len__(self):
-        return self._sharded_len
+        return len(self._items)
 
     def __iter__(self):
         return self
 
     def __next__(self):
-        return next(self.itr)[1]
+        return next(self._pos)

@@ -81,7 +81,7 @@ def main(args, init_distributed=False):
     train_meter = StopwatchMeter()
     train_meter.start()
     while (lr > args.min_lr
-           and (epoch_itr.epoch < max_epoch or (epoch_itr.epoch == max_epoch and epoch_itr._next_epoch_itr is not None))
+           and (epoch_itr.epoch < max_epoch or (epoch_itr.epoch == max_epoch and epoch_itr.resuming))
            and controller.get_num_updates() < max_update):
         train(args, controller, task, epoch_itr)
         valid_losses = [None]

@@ -171,3 +171,16 @@ def test_synthetic_corpus_cli(tmp_path):
     ds = BertH5Dataset(str(tmp_path / "data" / [f for f in files if "train" in f][0]), 20)
     assert len(ds) == 40
     assert (tmp_path / "vocab.txt").exists() and (tmp_path / "bert_config.json").exists()
+
+
+def test_counting_and_sharded_iterators():
+    c = iterators.CountingIterator(list(range(10)), start=0)
+    assert next(c) == 0 and c.count == 1 and c.has_next()
+    c.skip(3)
+    assert c.count == 4 and next(c) == 4
+    assert list(c) == [5, 6, 7, 8, 9] and not c.has_next() and len(c) == 10
+    assert list(iterators.ShardedIterator(range(7), 3, 2, fill_value=-1)) == [2, 5, -1]
+    assert list(iterators.ShardedIterator((x for x in range(7)), 3, 0)) == [0, 3, 6]
+    assert len(iterators.ShardedIterator(range(7), 3, 1)) == 3
+    with pytest.raises(ValueError):
+        iterators.ShardedIterator(range(7), 3, 3)
