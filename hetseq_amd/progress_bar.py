@@ -1,52 +1,44 @@
-"""Progress bars / loggers (reference: progress_bar.py:13-138).
+"""Training-log bars (reference: progress_bar.py:13-138).
 
-``simple`` reproduces the reference line format byte-for-byte:
-``| epoch 001:      5 / 100 loss=..., ppl=...``.  ``none`` is silent.
-``json`` (defined here; the reference names it but never implements it, Q22)
-prints one JSON object per logged step.  An optional JSON-lines sink
-(``--json-log``) records every logged step for benchmark harnesses.
+Formats:
+* ``simple`` -- the reference's text lines, byte for byte:
+  ``| epoch 001:      5 / 100 loss=1.234, ...`` every ``--log-interval``
+  items (after the consumer handled item i, never for i = 0), and
+  ``| epoch 001 | loss 1.234 | ...`` for end-of-epoch summaries;
+* ``none`` -- silent;
+* ``json`` -- one JSON object per logged step (the reference names it but
+  never defines it, Q22).
+``--json-log FILE`` additionally appends every ``log()`` call as a JSON line
+(numbers only), for benchmark harnesses.  Stats handed to ``log()`` may hold
+lazy device meters: the text is only rendered when a line is actually printed,
+so logging never forces a host-device sync.
 """
 import json
-import sys
 from collections import OrderedDict
 from numbers import Number
 
 from hetseq_amd.meters import AverageMeter, StopwatchMeter, TimeMeter
 
-
-def build_progress_bar(args, iterator, epoch=None, prefix=None, default="simple", no_progress_bar="none"):
-    if args.log_format is None:
-        args.log_format = no_progress_bar if args.no_progress_bar else default
-    if args.log_format == "none":
-        bar = noop_progress_bar(iterator, epoch, prefix)
-    elif args.log_format == "simple":
-        bar = simple_progress_bar(iterator, epoch, prefix, args.log_interval)
-    elif args.log_format == "json":
-        bar = json_progress_bar(iterator, epoch, prefix, args.log_interval)
-    else:
-        raise ValueError("Unknown log format: {}".format(args.log_format))
-    sink = getattr(args, "json_log", None)
-    if sink:
-        bar.json_sink = sink
-    return bar
+_TEXT = (
+    (AverageMeter, lambda m: "{:.3f}".format(m.avg)),
+    (TimeMeter, lambda m: "{:g}".format(round(m.avg))),
+    (StopwatchMeter, lambda m: "{:.4f}".format(m.sum)),
+)
 
 
 def format_stat(stat):
+    """Text of one stat: numbers with ``%g``, meters by their reference rule, anything else unchanged."""
     if isinstance(stat, Number):
-        stat = "{:g}".format(stat)
-    elif isinstance(stat, AverageMeter):
-        stat = "{:.3f}".format(stat.avg)
-    elif isinstance(stat, TimeMeter):
-        stat = "{:g}".format(round(stat.avg))
-    elif isinstance(stat, StopwatchMeter):
-        stat = "{:.4f}".format(stat.sum)
+        return "{:g}".format(stat)
+    for cls, fmt in _TEXT:
+        if isinstance(stat, cls):
+            return fmt(stat)
     return stat
 
 
-def _plain(stat):
-    if isinstance(stat, AverageMeter):
-        return stat.avg
-    if isinstance(stat, TimeMeter):
+def _value(stat):
+    """Plain JSON-able value of one stat (meters -> their average / total)."""
+    if isinstance(stat, (AverageMeter, TimeMeter)):
         return stat.avg
     if isinstance(stat, StopwatchMeter):
         return stat.sum
@@ -55,8 +47,13 @@ def _plain(stat):
     return stat
 
 
+def _rendered(stats):
+    return OrderedDict((k, str(format_stat(v)).strip()) for k, v in stats.items())
+
+
 class progress_bar(object):
-    """Abstract class for progress bars."""
+    """Base bar: wraps an iterable, numbers its items from the iterable's ``offset`` and calls
+    ``_after(i, size)`` once the consumer is done with item ``i``."""
 
     json_sink = None
 
@@ -64,11 +61,12 @@ class progress_bar(object):
         self.iterable = iterable
         self.offset = getattr(iterable, "offset", 0)
         self.epoch = epoch
-        self.prefix = ""
+        parts = []
         if epoch is not None:
-            self.prefix += "| epoch {:03d}".format(epoch)
+            parts.append("| epoch {:03d}".format(epoch))
         if prefix is not None:
-            self.prefix += " | {}".format(prefix)
+            parts.append(" | {}".format(prefix))
+        self.prefix = "".join(parts)
 
     def __len__(self):
         return len(self.iterable)
@@ -80,92 +78,71 @@ class progress_bar(object):
         return False
 
     def __iter__(self):
-        raise NotImplementedError
+        size = len(self.iterable)
+        for i, item in enumerate(self.iterable, start=self.offset):
+            yield item
+            self._after(i, size)
+
+    def _after(self, i, size):
+        pass
+
+    def _due(self, i):
+        return getattr(self, "stats", None) is not None and i > 0 and self.log_interval is not None \
+            and i % self.log_interval == 0
 
     def log(self, stats, tag="", step=None):
-        raise NotImplementedError
-
-    def print(self, stats, tag="", step=None):
-        raise NotImplementedError
-
-    def _str_commas(self, stats):
-        return ", ".join(key + "=" + stats[key].strip() for key in stats.keys())
-
-    def _str_pipes(self, stats):
-        return " | ".join(key + " " + stats[key].strip() for key in stats.keys())
-
-    def _format_stats(self, stats):
-        postfix = OrderedDict(stats)
-        for key in postfix.keys():
-            postfix[key] = str(format_stat(postfix[key]))
-        return postfix
-
-    def _sink(self, stats, step):
-        if self.json_sink:
-            rec = OrderedDict(epoch=self.epoch, step=step)
-            for k, v in stats.items():
-                v = _plain(v)
-                if isinstance(v, Number) or v is None:
-                    rec[k] = v
-            with open(self.json_sink, "a") as f:
-                f.write(json.dumps(rec) + "\n")
-
-
-class noop_progress_bar(progress_bar):
-    def __iter__(self):
-        for obj in self.iterable:
-            yield obj
-
-    def log(self, stats, tag="", step=None):
+        """Record intermediate stats (printed at the next log-interval boundary)."""
         self._sink(stats, step)
 
     def print(self, stats, tag="", step=None):
-        pass
+        """Print end-of-epoch stats."""
+
+    def _sink(self, stats, step):
+        if not self.json_sink:
+            return
+        rec = OrderedDict(epoch=self.epoch, step=step)
+        rec.update((k, v) for k, v in ((k, _value(v)) for k, v in stats.items())
+                   if v is None or isinstance(v, Number))
+        with open(self.json_sink, "a") as f:
+            f.write(json.dumps(rec) + "\n")
+
+
+class noop_progress_bar(progress_bar):
+    """Iterates without printing (``--log-format none`` / ``--no-progress-bar``)."""
+
+
+class _Deferred(object):
+    """Stats whose text is rendered on first use (keeps lazy device meters lazy)."""
+
+    def __init__(self, stats):
+        self._stats, self._text = stats, None
+
+    def text(self):
+        if self._text is None:
+            self._text = _rendered(self._stats)
+        return self._text
 
 
 class simple_progress_bar(progress_bar):
-    """A minimal logger for non-TTY environments."""
+    """Plain text lines for non-TTY logs."""
 
     def __init__(self, iterable, epoch=None, prefix=None, log_interval=1000):
         super().__init__(iterable, epoch, prefix)
         self.log_interval = log_interval
         self.stats = None
 
-    def __iter__(self):
-        size = len(self.iterable)
-        for i, obj in enumerate(self.iterable, start=self.offset):
-            yield obj
-            if self.stats is not None and i > 0 and self.log_interval is not None and i % self.log_interval == 0:
-                postfix = self._str_commas(self.stats)
-                print("{}:  {:5d} / {:d} {}".format(self.prefix, i, size, postfix), flush=True)
+    def _after(self, i, size):
+        if self._due(i):
+            body = ", ".join("{}={}".format(k, v) for k, v in self.stats.text().items())
+            print("{}:  {:5d} / {:d} {}".format(self.prefix, i, size, body), flush=True)
 
     def log(self, stats, tag="", step=None):
-        # formatting resolves lazy (device) meters; only do it when a line will be printed
-        self._raw = stats
-        self.stats = _LazyFormat(self, stats)
+        self.stats = _Deferred(stats)
         self._sink(stats, step)
 
     def print(self, stats, tag="", step=None):
-        postfix = self._str_pipes(self._format_stats(stats))
-        print("{} | {}".format(self.prefix, postfix), flush=True)
-
-
-class _LazyFormat(object):
-    """Formats the stats only when the progress bar actually prints them."""
-
-    def __init__(self, bar, stats):
-        self._bar, self._stats, self._cache = bar, stats, None
-
-    def _get(self):
-        if self._cache is None:
-            self._cache = self._bar._format_stats(self._stats)
-        return self._cache
-
-    def keys(self):
-        return self._get().keys()
-
-    def __getitem__(self, k):
-        return self._get()[k]
+        body = " | ".join("{} {}".format(k, v) for k, v in _rendered(stats).items())
+        print("{} | {}".format(self.prefix, body), flush=True)
 
 
 class json_progress_bar(progress_bar):
@@ -175,18 +152,14 @@ class json_progress_bar(progress_bar):
         super().__init__(iterable, epoch, prefix)
         self.log_interval = log_interval
         self.stats = None
-        self._step = None
 
-    def __iter__(self):
-        for i, obj in enumerate(self.iterable, start=self.offset):
-            yield obj
-            if self.stats is not None and i > 0 and self.log_interval is not None and i % self.log_interval == 0:
-                rec = OrderedDict(epoch=self.epoch, update=i)
-                for k, v in self.stats.items():
-                    v = _plain(v)
-                    rec[k] = round(v, 6) if isinstance(v, float) else v
-                print(json.dumps(rec), flush=True)
-                sys.stdout.flush()
+    def _after(self, i, size):
+        if self._due(i):
+            rec = OrderedDict(epoch=self.epoch, update=i)
+            for k, v in self.stats.items():
+                v = _value(v)
+                rec[k] = round(v, 6) if isinstance(v, float) else v
+            print(json.dumps(rec), flush=True)
 
     def log(self, stats, tag="", step=None):
         self.stats = stats
@@ -194,6 +167,20 @@ class json_progress_bar(progress_bar):
 
     def print(self, stats, tag="", step=None):
         rec = OrderedDict(epoch=self.epoch)
-        for k, v in stats.items():
-            rec[k] = _plain(v)
+        rec.update((k, _value(v)) for k, v in stats.items())
         print(json.dumps(rec), flush=True)
+
+
+_BARS = {"none": noop_progress_bar, "simple": simple_progress_bar, "json": json_progress_bar}
+
+
+def build_progress_bar(args, iterator, epoch=None, prefix=None, default="simple", no_progress_bar="none"):
+    if args.log_format is None:
+        args.log_format = no_progress_bar if args.no_progress_bar else default
+    cls = _BARS.get(args.log_format)
+    if cls is None:
+        raise ValueError("Unknown log format: {}".format(args.log_format))
+    bar = cls(iterator, epoch, prefix) if cls is noop_progress_bar else cls(iterator, epoch, prefix, args.log_interval)
+    if getattr(args, "json_log", None):
+        bar.json_sink = args.json_log
+    return bar
