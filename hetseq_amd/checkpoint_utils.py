@@ -33,50 +33,59 @@ from hetseq_amd import meters as meters_mod
 from hetseq_amd.parallel import distributed_utils
 
 
+def _checkpoint_names(args, epoch, updates, end_of_epoch, val_loss, improved):
+    """File names this save writes, in priority order (the first is written, the rest copied)."""
+    names = []
+    if end_of_epoch and not args.no_epoch_checkpoints and epoch % args.save_interval == 0:
+        names.append("checkpoint%d.pt" % epoch)
+    if not end_of_epoch and args.save_interval_updates > 0 and updates % args.save_interval_updates == 0:
+        names.append("checkpoint_%d_%d.pt" % (epoch, updates))
+    if val_loss is not None and improved:
+        names.append("checkpoint_best.pt")
+    if not args.no_last_checkpoints:
+        names.append("checkpoint_last.pt")
+    return names
+
+
+def _prune(save_dir, pattern, keep):
+    """Delete all but the ``keep`` newest checkpoints whose names match ``pattern``."""
+    for stale in checkpoint_paths(save_dir, pattern=pattern)[keep:]:
+        if os.path.lexists(stale):
+            os.remove(stale)
+
+
 def save_checkpoint(args, controller, epoch_itr, val_loss, end_of_epoch=None):
+    """Master-only save of the training state (reference: checkpoint_utils.py:14-83, with Q01/Q07 fixed)."""
+    higher = args.maximize_best_checkpoint_metric
     prev_best = getattr(save_checkpoint, "best", val_loss)
     if val_loss is not None:
-        best_function = max if args.maximize_best_checkpoint_metric else min
-        save_checkpoint.best = best_function(val_loss, prev_best)
+        save_checkpoint.best = max(val_loss, prev_best) if higher else min(val_loss, prev_best)
     if args.no_save or not distributed_utils.is_master(args):
         return
-
-    def is_better(a, b):
-        return a >= b if args.maximize_best_checkpoint_metric else a <= b
-
-    write_timer = meters_mod.StopwatchMeter()
-    write_timer.start()
-    epoch = epoch_itr.epoch
+    clock = meters_mod.StopwatchMeter()
+    clock.start()
+    epoch, updates = epoch_itr.epoch, controller.get_num_updates()
     if end_of_epoch is None:
         end_of_epoch = epoch_itr.end_of_epoch()
-    updates = controller.get_num_updates()
-    conds = collections.OrderedDict()
-    conds["checkpoint{}.pt".format(epoch)] = (end_of_epoch and not args.no_epoch_checkpoints
-                                             and epoch % args.save_interval == 0)
-    conds["checkpoint_{}_{}.pt".format(epoch, updates)] = (not end_of_epoch and args.save_interval_updates > 0
-                                                          and updates % args.save_interval_updates == 0)
-    conds["checkpoint_best.pt"] = val_loss is not None and (
-        not hasattr(save_checkpoint, "best") or is_better(val_loss, save_checkpoint.best))
-    conds["checkpoint_last.pt"] = not args.no_last_checkpoints
+    best = getattr(save_checkpoint, "best", None)
+    improved = val_loss is not None and (not hasattr(save_checkpoint, "best") or (
+        val_loss >= best if higher else val_loss <= best))
     extra_state = {"train_iterator": epoch_itr.state_dict(), "val_loss": val_loss}
     if hasattr(save_checkpoint, "best"):
-        extra_state.update({"best": save_checkpoint.best})
-    checkpoints = [os.path.join(args.save_dir, fn) for fn, cond in conds.items() if cond]
-    if len(checkpoints) > 0:
-        controller.save_checkpoint(checkpoints[0], extra_state)
-        for cp in checkpoints[1:]:
-            shutil.copyfile(checkpoints[0], cp)
-        write_timer.stop()
+        extra_state["best"] = save_checkpoint.best
+    paths = [os.path.join(args.save_dir, n) for n in
+             _checkpoint_names(args, epoch, updates, end_of_epoch, val_loss, improved)]
+    if paths:
+        controller.save_checkpoint(paths[0], extra_state)
+        for dup in paths[1:]:
+            shutil.copyfile(paths[0], dup)
+        clock.stop()
         print("| saved checkpoint {} (epoch {} @ {} updates) (writing took {} seconds)".format(
-            checkpoints[0], epoch, updates, write_timer.sum))
+            paths[0], epoch, updates, clock.sum))
     if not end_of_epoch and args.keep_interval_updates > 0:
-        for old in checkpoint_paths(args.save_dir, pattern=r"checkpoint_\d+_(\d+)\.pt")[args.keep_interval_updates:]:
-            if os.path.lexists(old):
-                os.remove(old)
+        _prune(args.save_dir, r"checkpoint_\d+_(\d+)\.pt", args.keep_interval_updates)
     if args.keep_last_epochs > 0:
-        for old in checkpoint_paths(args.save_dir, pattern=r"checkpoint(\d+)\.pt")[args.keep_last_epochs:]:
-            if os.path.lexists(old):
-                os.remove(old)
+        _prune(args.save_dir, r"checkpoint(\d+)\.pt", args.keep_last_epochs)
 
 
 def load_checkpoint(args, controller):
@@ -125,14 +134,12 @@ def _meter_classes():
 
 
 def checkpoint_paths(path, pattern=r"checkpoint(\d+)\.pt"):
-    pt_regexp = re.compile(pattern)
-    entries = []
-    for i, f in enumerate(os.listdir(path)):
-        m = pt_regexp.fullmatch(f)
-        if m is not None:
-            idx = int(m.group(1)) if len(m.groups()) > 0 else i
-            entries.append((idx, m.group(0)))
-    return [os.path.join(path, x[1]) for x in sorted(entries, reverse=True)]
+    """Files in ``path`` fully matching ``pattern``, newest first by the captured number
+    (by directory position when the pattern captures nothing)."""
+    rx = re.compile(pattern)
+    found = [(pos, rx.fullmatch(name)) for pos, name in enumerate(os.listdir(path))]
+    keyed = sorted(((int(m.group(1)) if m.groups() else pos, m.group(0)) for pos, m in found if m), reverse=True)
+    return [os.path.join(path, name) for _, name in keyed]
 
 
 def torch_persistent_save(obj, filename):
@@ -212,14 +219,12 @@ def save_state(filename, args, model_state_dict, criterion, optimizer, lr_schedu
 
 
 def verify_checkpoint_directory(save_dir):
-    if not os.path.exists(save_dir):
-        os.makedirs(save_dir, exist_ok=True)
-    temp_file_path = os.path.join(save_dir, "dummy")
+    """Create ``save_dir`` if needed and prove it is writable (fails early, before training)."""
+    os.makedirs(save_dir, exist_ok=True)
+    probe = os.path.join(save_dir, "dummy")
     try:
-        with open(temp_file_path, "w"):
-            pass
-    except OSError as e:
+        open(probe, "w").close()
+    except OSError:
         print("| Unable to access checkpoint save directory: {}".format(save_dir))
-        raise e
-    else:
-        os.remove(temp_file_path)
+        raise
+    os.remove(probe)

@@ -175,3 +175,25 @@ def test_token_classification_task_trains(tmp_path):
     # the reference's sample_size is len(sample[0][0]): the sequence length (tasks.py:164)
     assert torch.isfinite(loss) and sample_size == 12 and log["nsentences"] == 12
     assert model.classifier.weight.grad is not None and model.classifier.weight.grad.abs().sum() > 0
+
+
+def test_checkpoint_names_and_pruning(tmp_path):
+    """Which files a save writes (reference checkpoint_utils.py:36-55, Q07 fixed) and --keep-* pruning."""
+    import argparse
+
+    from hetseq_amd import checkpoint_utils as cu
+
+    a = argparse.Namespace(no_epoch_checkpoints=False, save_interval=1, save_interval_updates=5,
+                           no_last_checkpoints=False)
+    assert cu._checkpoint_names(a, 3, 40, True, None, False) == ["checkpoint3.pt", "checkpoint_last.pt"]
+    assert cu._checkpoint_names(a, 3, 40, False, None, False) == ["checkpoint_3_40.pt", "checkpoint_last.pt"]
+    assert cu._checkpoint_names(a, 3, 41, False, 1.0, True) == ["checkpoint_best.pt", "checkpoint_last.pt"]
+    for n in ["checkpoint1.pt", "checkpoint2.pt", "checkpoint10.pt", "checkpoint_1_5.pt", "checkpoint_1_15.pt",
+              "checkpoint_last.pt"]:
+        (tmp_path / n).write_text("x")
+    assert [p.rsplit("/", 1)[1] for p in cu.checkpoint_paths(str(tmp_path))] == \
+        ["checkpoint10.pt", "checkpoint2.pt", "checkpoint1.pt"]
+    cu._prune(str(tmp_path), r"checkpoint(\d+)\.pt", 2)
+    cu._prune(str(tmp_path), r"checkpoint_\d+_(\d+)\.pt", 1)
+    assert sorted(p.name for p in tmp_path.iterdir()) == \
+        ["checkpoint10.pt", "checkpoint2.pt", "checkpoint_1_15.pt", "checkpoint_last.pt"]
