@@ -30,22 +30,34 @@ class _LRScheduler(object):
         return self.optimizer.get_lr()
 
 
+def polynomial_decay(n, base_lr, warmup, total, end_lr, power):
+    """LR at update ``n`` after warmup: polynomial from ``base_lr`` (at ``warmup``) to ``end_lr`` (at ``total``)."""
+    if n >= total:
+        return end_lr
+    frac_left = 1 - (n - warmup) / (total - warmup)
+    return (base_lr - end_lr) * frac_left ** power + end_lr
+
+
 class PolynomialDecayScheduler(_LRScheduler):
+    """Warmup (from LR 0 at update 0) then polynomial decay; per-epoch base LR from ``--lr``."""
+
     def __init__(self, args, optimizer):
         super().__init__(args, optimizer)
         args.warmup_updates = getattr(args, "warmup_updates", 0) or 0
         self.lr = args.lr[0]
-        self.warmup_factor = 1.0 / args.warmup_updates if args.warmup_updates > 0 else 1
         self.end_learning_rate = args.end_learning_rate
         self.total_num_update = args.total_num_update
         self.power = args.power
+        # scale of the base LR applied by step(epoch); only the warmup branch of step_update moves it
+        self.warmup_factor = 1.0 / args.warmup_updates if args.warmup_updates > 0 else 1
         self.optimizer.set_lr(self.warmup_factor * self.lr)
 
     def get_next_lr(self, epoch):
-        lrs = self.args.lr
-        if self.args.force_anneal is None or epoch < self.args.force_anneal:
-            return lrs[min(epoch, len(lrs) - 1)]
-        return self.optimizer.get_lr()
+        anneal_from = self.args.force_anneal
+        if anneal_from is not None and epoch >= anneal_from:
+            return self.optimizer.get_lr()  # annealing: keep whatever the updates reached
+        per_epoch = self.args.lr
+        return per_epoch[epoch] if epoch < len(per_epoch) else per_epoch[-1]
 
     def step(self, epoch, val_loss=None):
         super().step(epoch, val_loss)
@@ -54,16 +66,12 @@ class PolynomialDecayScheduler(_LRScheduler):
         return self.optimizer.get_lr()
 
     def step_update(self, num_updates):
-        w = self.args.warmup_updates
-        if w > 0 and num_updates <= w:
-            self.warmup_factor = num_updates / float(w)
-            lr = self.warmup_factor * self.lr
-        elif num_updates >= self.total_num_update:
-            lr = self.end_learning_rate
-        else:
-            lr_range = self.lr - self.end_learning_rate
-            pct_remaining = 1 - (num_updates - w) / (self.total_num_update - w)
-            lr = lr_range * pct_remaining ** self.power + self.end_learning_rate
+        warmup = self.args.warmup_updates
+        in_warmup = 0 < warmup and num_updates <= warmup
+        if in_warmup:
+            self.warmup_factor = num_updates / float(warmup)
+        lr = self.warmup_factor * self.lr if in_warmup else polynomial_decay(
+            num_updates, self.lr, warmup, self.total_num_update, self.end_learning_rate, self.power)
         self.optimizer.set_lr(lr)
         return self.optimizer.get_lr()
 
