@@ -107,6 +107,9 @@ def main():
     task = LanguageModelingTask.setup_task(args)
     model = task.build_model(args)
     nparams = sum(p.numel() for p in model.parameters())
+    from hetseq_amd.runtime import gemm_tuning
+
+    gemm_tuning.configure(args)
     ctl = Controller(args, task, model)
     task.load_dataset("train")
     task.prepare_model_for_data(ctl.get_model(), "train")

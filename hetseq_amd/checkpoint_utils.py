@@ -106,14 +106,38 @@ def load_checkpoint(args, controller):
         save_checkpoint.best = extra_state["best"]
     if extra_state is not None and not args.reset_dataloader:
         itr_state = extra_state.get("train_iterator")
-        if itr_state is None:  # reference checkpoints carry extra_state == {}
-            itr_state = {"epoch": extra_state.get("_epoch_hint", 0), "iterations_in_epoch": 0}
-        epoch_itr = controller.get_train_iterator(epoch=itr_state["epoch"], load_dataset=True)
+        if itr_state is None:
+            # reference-format checkpoints carry extra_state == {} (reference checkpoint_utils.py:204,
+            # SURVEY Q01): rebuild the position the reference meant to save (its :50-55) from the
+            # update count in optimizer_history and this run's batches per epoch
+            epoch_itr = controller.get_train_iterator(epoch=0, load_dataset=True)
+            per_rank = -(-len(epoch_itr) // max(1, epoch_itr.num_shards))
+            itr_state = iterator_state_from_updates(controller.get_num_updates(), per_rank, args.update_freq)
+        else:
+            epoch_itr = controller.get_train_iterator(epoch=itr_state["epoch"], load_dataset=True)
         epoch_itr.load_state_dict(itr_state)
     else:
         epoch_itr = controller.get_train_iterator(epoch=0, load_dataset=True)
     controller.lr_step(epoch_itr.epoch)
     return extra_state, epoch_itr
+
+
+def iterator_state_from_updates(num_updates, batches_per_epoch, update_freq):
+    """Iterator position after ``num_updates`` updates of ``batches_per_epoch`` micro-batches per
+    epoch and rank, grouped by the per-epoch ``update_freq`` list (the last entry repeats), as the
+    reference's ``EpochBatchIterator.state_dict`` would have recorded it: a finished epoch E gives
+    ``{'epoch': E, 'iterations_in_epoch': 0}`` (the next run starts epoch E+1), a mid-epoch save
+    the micro-batches consumed so far."""
+    update_freq = list(update_freq) if isinstance(update_freq, (list, tuple)) else [int(update_freq)]
+    epoch, left = 0, int(num_updates)
+    while left > 0 and batches_per_epoch > 0:
+        uf = update_freq[min(epoch, len(update_freq) - 1)]
+        per_epoch = -(-batches_per_epoch // uf)
+        if left < per_epoch:
+            return {"epoch": epoch + 1, "iterations_in_epoch": left * uf}
+        left -= per_epoch
+        epoch += 1
+    return {"epoch": epoch, "iterations_in_epoch": 0}
 
 
 _SAFE = [argparse.Namespace, OrderedDict, collections.defaultdict]

@@ -63,11 +63,8 @@ class Controller(object):
             G.set_fp32_mode(args.fp32_gemm)
         if "HETSEQ_WGRAD_STREAM" not in os.environ:
             streams.set_enabled(self.compute_dtype == torch.float32 and not getattr(args, "hip_graph", False))
-        if self.cuda and getattr(args, "gemm_tuning", True):
-            from hetseq_amd.runtime import gemm_tuning
-
-            gemm_tuning.enable(getattr(args, "dtype", "fp32"))
-            gemm_tuning.load_engine_choices(getattr(args, "dtype", "fp32"))
+        # library-GEMM tables (TunableOp) are process-global: loaded by the entry points
+        # (train.py / bench.py -> runtime.gemm_tuning.configure), never here
         shadow = torch.bfloat16 if self.compute_dtype == torch.bfloat16 else None
         self.store = FlatParamStore(self._model, device=self.device, shadow_dtype=shadow)
         if hasattr(self._model, "attach_store"):

@@ -146,7 +146,7 @@ HS_DEVICE float comp(const float4& v, int s) { return s == 0 ? v.x : s == 1 ? v.
 // mid*hi, hi*lo, lo*hi, mid*mid; the dropped mid*lo, lo*mid, lo*lo are
 // <= 2^-24 |a b|, the size of one fp32 rounding).  Every bf16 x bf16 product is
 // exact in the fp32 accumulator, so the result carries fp32-level error
-// (tests/test_gemm_x6_gpu.py measures it against fp64 next to the exact-fp32
+// (tests/test_kernels_gpu.py::test_gemm_x6_error_matches_fp32 measures it against fp64 next to the exact-fp32
 // MFMA kernel) at 6/16 of the f32 MFMA's cycles.  NT = 3 keeps only
 // hi*hi + hi*mid + mid*hi (two-term split, ~2^-16 relative: NOT fp32 accuracy,
 // a benchmarking variant only).

@@ -12,7 +12,7 @@
 //  * a constant-length fast path never materialises per-sample lengths;
 //  * the output is a list of int64 numpy arrays (one per batch).
 // The cut rule is reproduced exactly so the batch lists match the reference
-// element for element (tests/test_batcher.py checks golden lists).
+// element for element (tests/test_data.py::test_batcher_* check golden lists).
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 

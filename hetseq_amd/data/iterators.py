@@ -54,7 +54,7 @@ class CountingIterator(object):
         self.iterable = iterable
         self.count = start
         self.len = start + len(iterable)
-        self._src = iter(iterable)
+        self._src = None  # started lazily on the first item (DataLoader workers fork after set_epoch)
 
     def __len__(self):
         return self.len
@@ -63,6 +63,8 @@ class CountingIterator(object):
         return self
 
     def __next__(self):
+        if self._src is None:
+            self._src = iter(self.iterable)
         item = next(self._src)
         self.count += 1
         return item

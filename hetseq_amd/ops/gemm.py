@@ -36,6 +36,7 @@ GEMM_CHOICES: dict = {}
 _MODE = os.environ.get("HETSEQ_GEMM", "auto")
 _FP32_DT = {"native": 0, "x6": 2, "x3": 3}
 _FP32 = os.environ.get("HETSEQ_FP32_GEMM", "x6")
+FP32_DEFAULT = _FP32
 assert _FP32 in _FP32_DT, "HETSEQ_FP32_GEMM must be one of native|x6|x3"
 _SLABS: dict = {}  # (device, stream) -> split-K partial-sum workspace
 

@@ -230,6 +230,9 @@ def add_mi355x_args(parser):
                             "protocol, no tuned GEMM table (library split-K solutions may use atomics)")
     group.add_argument("--no-gemm-tuning", dest="gemm_tuning", action="store_false",
                        help="do not load the measured hipBLASLt/rocBLAS GEMM table (configs/tunableop)")
+    group.add_argument("--gemm-tune-missing", action="store_true",
+                       help="let TunableOp time library GEMM shapes missing from the table on first use "
+                            "(off by default: live tuning runs untested candidate solutions mid-training)")
     group.add_argument("--bmuf-block-momentum", type=float, default=0.875,
                        help="block momentum for --use-bmuf")
     group.add_argument("--bmuf-sync-interval", type=int, default=1,

@@ -30,7 +30,7 @@ def enable(dtype_tag="fp32", tune_missing=None):
     import torch.cuda.tunable as tn
 
     if tune_missing is None:
-        tune_missing = os.environ.get("HETSEQ_GEMM_TUNE_MISSING", "1") == "1"
+        tune_missing = os.environ.get("HETSEQ_GEMM_TUNE_MISSING", "0") == "1"
     tn.enable(True)
     tn.tuning_enable(bool(tune_missing))
     if "PYTORCH_TUNABLEOP_MAX_TUNING_DURATION_MS" not in os.environ:
@@ -47,6 +47,28 @@ def enable(dtype_tag="fp32", tune_missing=None):
             tn.read_file(path)
     _done = True
     return True
+
+
+def configure(args):
+    """Entry-point hook (train.py, bench.py): load the measured library-GEMM table and the
+    per-call-site engine choices for ``args.dtype`` unless ``--no-gemm-tuning``."""
+    if not torch.cuda.is_available() or getattr(args, "cpu", False) or not getattr(args, "gemm_tuning", True):
+        return False
+    dt = getattr(args, "dtype", "fp32")
+    enable(dt, tune_missing=True if getattr(args, "gemm_tune_missing", False) else None)
+    load_engine_choices(dt)
+    return True
+
+
+def reset():
+    """Undo :func:`enable` (tests: no TunableOp state leaks from one test into the next)."""
+    global _done
+    if torch.cuda.is_available():
+        import torch.cuda.tunable as tn
+
+        tn.tuning_enable(False)
+        tn.enable(False)
+    _done = False
 
 
 CHOICE_DIR = os.path.join(ROOT, "configs", "gemm_choices")

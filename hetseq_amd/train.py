@@ -67,6 +67,9 @@ def main(args, init_distributed=False):
     print("| num. model params: {} (num. trained: {})".format(
         sum(p.numel() for p in model.parameters()), sum(p.numel() for p in model.parameters() if p.requires_grad)))
 
+    from hetseq_amd.runtime import gemm_tuning
+
+    gemm_tuning.configure(args)  # process-global library-GEMM table: an entry-point decision
     controller = Controller(args, task, model)
     print("| training on {} GPUs".format(args.distributed_world_size))
     print("| max tokens per GPU = {} and max sentences per GPU = {}".format(args.max_tokens, args.max_sentences))

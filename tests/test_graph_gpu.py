@@ -56,3 +56,13 @@ def test_graph_replay_matches_eager(cuda, tmp_path, dtype):
         assert abs(a - b) <= 1e-5 * abs(a) + 1e-6, (l_eager, l_graph)
     err = (p_eager - p_graph).abs().max().item()
     assert err <= 1e-5 * p_eager.abs().max().item(), err
+
+
+def test_controller_leaves_tunableop_off(cuda, tmp_path):
+    """Building and stepping a default Controller must not switch on process-global TunableOp
+    (the library-GEMM table is an entry-point decision: runtime.gemm_tuning.configure)."""
+    import torch.cuda.tunable as tn
+
+    _run(tmp_path, False, 1)
+    assert not tn.is_enabled()
+    assert not tn.tuning_is_enabled()

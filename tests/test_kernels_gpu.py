@@ -149,6 +149,53 @@ def test_attention_fwd_bwd(cuda, B, S, NH):
     _close(qkv.grad, qkv2.grad, 1e-4, 1e-5, "attn dqkv")
 
 
+def _keep_mask(dmask, BH, S):
+    """[BH, S(query), S(key)] float keep mask unpacked from the forward's packed keep bits."""
+    w = dmask.view(BH, S, S // 32, 1)
+    sh = torch.arange(32, device=dmask.device, dtype=torch.int32)
+    return ((w >> sh) & 1).reshape(BH, S, S).double()
+
+
+def _ref_attention_drop(qkv, mask, B, S, NH, keep, p):
+    H = qkv.shape[1] // 3
+    q, k, v = qkv.view(B, S, 3, NH, 64).permute(2, 0, 3, 1, 4)
+    scores = torch.matmul(q, k.transpose(-1, -2)) / 8.0
+    scores = scores + ((1.0 - mask.to(qkv.dtype)) * -10000.0)[:, None, None, :]
+    prob = torch.softmax(scores, -1)
+    if p > 0:
+        thr = min(65536, int(p * 65536.0 + 0.5))
+        prob = prob * keep.view(B, NH, S, S) * (65536.0 / (65536 - thr))
+    return torch.matmul(prob, v).permute(0, 2, 1, 3).reshape(B * S, H)
+
+
+@pytest.mark.parametrize("S", [256, 384, 512])
+@pytest.mark.parametrize("B,NH", [(1, 2), (8, 12)])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_attention_long_seq_fwd_bwd_vs_fp64(cuda, S, B, NH, p):
+    """Phase-2 lengths (S > 128: chunked forward, two-kernel backward) against an fp64 autograd
+    reference that applies the forward's own keep bits (regression grid of the round-1 fault)."""
+    from hetseq_amd.ops import bert_ops
+
+    torch.manual_seed(40 + S + B)
+    H = NH * 64
+    qkv = torch.randn(B * S, 3 * H, device=cuda)
+    bias = torch.randn(3 * H, device=cuda) * 0.1
+    mask = torch.ones(B, S, dtype=torch.int64, device=cuda)
+    mask[0, S - 37:] = 0
+    if B > 1:
+        mask[B - 1, 3:11] = 0
+    out, (lse, dmask) = bert_ops.attn_fwd(qkv, mask, B, S, NH, p, 17, 5, bias=bias)
+    dout = torch.randn_like(out)
+    dqkv = bert_ops.attn_bwd(qkv, mask, out, dout, (lse, dmask), B, S, NH, p, bias=bias)
+    torch.cuda.synchronize()
+    keep = _keep_mask(dmask, B * NH, S) if p > 0 else None
+    x = (qkv.double() + bias.double()).requires_grad_()
+    ref = _ref_attention_drop(x, mask, B, S, NH, keep, p)
+    ref.backward(dout.double())
+    _close(out, ref, 1e-4, 1e-6, "long-seq attn fwd")
+    _close(dqkv, x.grad, 1e-4, 1e-6, "long-seq attn dqkv")
+
+
 @pytest.mark.parametrize("B,S,NH,p", [(2, 128, 12, 0.0), (2, 96, 2, 0.1), (1, 512, 2, 0.0), (2, 192, 2, 0.1)])
 def test_attention_fwd_x6_fp32_level(cuda, B, S, NH, p):
     """fp32 forward on split-bf16 products: the same keep bits as the exact-fp32 MFMA kernel,

@@ -145,6 +145,43 @@ def test_load_reference_format_checkpoint_with_empty_extra_state(tmp_path):
     assert st["optimizer_history"][0]["num_updates"] == 3 and st["extra_state"] == {}
 
 
+def test_iterator_state_from_updates():
+    from hetseq_amd.checkpoint_utils import iterator_state_from_updates as f
+
+    assert f(0, 6, [1]) == {"epoch": 0, "iterations_in_epoch": 0}
+    assert f(6, 6, [1]) == {"epoch": 1, "iterations_in_epoch": 0}   # epoch 1 finished
+    assert f(8, 6, [1]) == {"epoch": 2, "iterations_in_epoch": 2}   # mid-epoch 2
+    assert f(3, 6, [2]) == {"epoch": 1, "iterations_in_epoch": 0}   # 6 batches / uf 2 = 3 updates
+    assert f(4, 7, [2]) == {"epoch": 1, "iterations_in_epoch": 0}   # ceil(7/2) = 4
+    assert f(5, 6, [1, 2]) == {"epoch": 1, "iterations_in_epoch": 5}
+    assert f(8, 6, [1, 2]) == {"epoch": 2, "iterations_in_epoch": 4}  # epoch 2 groups by 2
+
+
+def test_resume_reference_checkpoint_keeps_epoch(tmp_path):
+    """A reference-written checkpoint (extra_state == {}) resumes at the epoch its update count
+    implies instead of replaying finished epochs (reference checkpoint_utils.py:115-119)."""
+    from hetseq_amd.checkpoint_utils import load_checkpoint_to_cpu
+    from hetseq_amd.data.synthetic import write_bert_config, write_bert_shards, write_vocab
+    from hetseq_amd.parallel import distributed_utils
+
+    d = tmp_path / "data"
+    write_bert_shards(str(d), num_shards=1, per_shard=24, seq_len=16, max_pred=3, vocab_size=200, split="train")
+    write_bert_shards(str(d), num_shards=1, per_shard=4, seq_len=16, max_pred=3, vocab_size=200, split="test")
+    vocab = write_vocab(str(tmp_path / "v.txt"), 200)
+    cfg = write_bert_config(str(tmp_path / "c.json"), vocab_size=200, hidden_size=64, num_hidden_layers=1,
+                            num_attention_heads=2, intermediate_size=128)
+    run = tmp_path / "r"
+    c1 = _train_cli(run, ["--max-epoch", "1"], str(d), cfg, vocab)
+    assert c1.get_num_updates() == 6  # 24 samples / 4 per batch
+    ck = run / "ck" / "checkpoint_last.pt"
+    st = load_checkpoint_to_cpu(str(ck))
+    st["extra_state"] = {}  # what the reference's save_state writes (Q01)
+    torch.save(st, ck)
+    c2 = _train_cli(run, ["--max-epoch", "2"], str(d), cfg, vocab)
+    assert c2.get_num_updates() == 12  # epoch 2 only, not epochs 1 and 2 again
+    distributed_utils.restore_output()
+
+
 def test_token_classification_task_trains(tmp_path):
     """The working replacement of the reference's unreachable BertFineTuningTask (tasks.py:261-285, Q13)."""
     import argparse
