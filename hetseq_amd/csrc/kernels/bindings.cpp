@@ -43,12 +43,17 @@ int launch_segsum_rows(const float*, const int64_t*, const int64_t*, float*, flo
 int launch_pos_grad(const float*, float*, int, int, int, hipStream_t);
 // elementwise.hip
 void launch_bias_gelu_fwd(int, const void*, const float*, void*, int64_t, int, hipStream_t);
-void launch_bias_tanh_fwd(int, const void*, const float*, void*, int64_t, int, hipStream_t);
 int colsum_row_chunks(int64_t);
 void launch_colsum(int, const void*, const void*, const float*, void*, float*, float*, int64_t, int, int, hipStream_t);
 void launch_mlm_compact(const int64_t*, int, int, int, int32_t*, int64_t*, int32_t*, int*, hipStream_t);
 void launch_gather_rows(int, const void*, const int32_t*, void*, int, int, hipStream_t);
 void launch_scatter_add_rows(int, const void*, const int32_t*, void*, int, int, hipStream_t);
+// pool_nsp.hip
+int launch_pool_nsp_fwd(int, const void*, int, int, int, const float*, const float*, const float*, const float*,
+                        const int64_t*, const float*, float*, float*, float*, float*, float*, hipStream_t);
+int launch_pool_nsp_bwd(int, const float*, const void*, void*, int, int, int, const float*, const float*,
+                        const int64_t*, const float*, const float*, const float*, const float*, float*, float*,
+                        float*, float*, float*, float*, int, hipStream_t);
 // attention.hip
 void set_attn_fp32_mode(int x6);
 int attn_fp32_mode();
@@ -187,9 +192,23 @@ PYBIND11_MODULE(_hip, m) {
     launch_bias_gelu_fwd(dt, P(const void*, x), P(const float*, b), P(void*, y), rows, N, ST(st));
     check_launch("bias_gelu_fwd");
   });
-  m.def("bias_tanh_fwd", [](int dt, i64 x, i64 b, i64 y, i64 rows, int N, i64 st) {
-    launch_bias_tanh_fwd(dt, P(const void*, x), P(const float*, b), P(void*, y), rows, N, ST(st));
-    check_launch("bias_tanh_fwd");
+  m.def("pool_nsp_fwd", [](int dt, i64 seq, int B, int S, int H, i64 Wp, i64 bp, i64 Wn, i64 bn, i64 label,
+                           i64 mlm_loss, i64 pooled, i64 logits, i64 lse, i64 stats, i64 total, i64 st) {
+    check(launch_pool_nsp_fwd(dt, P(const void*, seq), B, S, H, P(const float*, Wp), P(const float*, bp),
+                              P(const float*, Wn), P(const float*, bn), P(const int64_t*, label),
+                              P(const float*, mlm_loss), P(float*, pooled), P(float*, logits), P(float*, lse),
+                              P(float*, stats), P(float*, total), ST(st)),
+          "pool_nsp_fwd");
+  });
+  m.def("pool_nsp_bwd", [](int dt, i64 dloss, i64 seq, i64 dseq, int B, int S, int H, i64 Wp, i64 Wn, i64 label,
+                           i64 pooled, i64 logits, i64 lse, i64 stats, i64 dlogits, i64 dpre, i64 dWp, i64 dbp,
+                           i64 dWn, i64 dbn, int accumulate, i64 st) {
+    check(launch_pool_nsp_bwd(dt, P(const float*, dloss), P(const void*, seq), P(void*, dseq), B, S, H,
+                              P(const float*, Wp), P(const float*, Wn), P(const int64_t*, label),
+                              P(const float*, pooled), P(const float*, logits), P(const float*, lse),
+                              P(const float*, stats), P(float*, dlogits), P(float*, dpre), P(float*, dWp),
+                              P(float*, dbp), P(float*, dWn), P(float*, dbn), accumulate, ST(st)),
+          "pool_nsp_bwd");
   });
   m.def("colsum_row_chunks", &colsum_row_chunks);
   m.def("colsum", [](int dt, i64 dy, i64 x, i64 b, i64 dx, i64 part, i64 out, i64 rows, int N, int accumulate, i64 st) {

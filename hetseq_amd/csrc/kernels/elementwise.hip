@@ -37,16 +37,6 @@ __global__ void __launch_bounds__(256) bias_gelu_fwd_kernel(const T* __restrict_
   }
 }
 
-template <typename T>
-__global__ void __launch_bounds__(256) bias_tanh_fwd_kernel(const T* __restrict__ x, const float* __restrict__ b,
-                                                            T* __restrict__ y, int64_t rows, int N) {
-  const int64_t total = rows * N;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int c = (int)(i % N);
-    y[i] = from_f<T>(tanhf(to_f(x[i]) + b[c]));
-  }
-}
-
 // grid = (ceil(N/1024), row_chunks); part is [row_chunks, N]
 template <typename T, bool kGelu>
 __global__ void __launch_bounds__(256) colsum_tile_kernel(const T* __restrict__ dy, const T* __restrict__ x,
@@ -337,15 +327,6 @@ void launch_bias_gelu_fwd(int dtype, const void* x, const float* b, void* y, int
     hipLaunchKernelGGL(bias_gelu_fwd_kernel<float>, dim3(g), dim3(256), 0, st, (const float*)x, b, (float*)y, rows, N);
   else
     hipLaunchKernelGGL(bias_gelu_fwd_kernel<bf16_t>, dim3(g), dim3(256), 0, st, (const bf16_t*)x, b, (bf16_t*)y, rows,
-                       N);
-}
-
-void launch_bias_tanh_fwd(int dtype, const void* x, const float* b, void* y, int64_t rows, int N, hipStream_t st) {
-  const int g = ew_grid(rows * N);
-  if (dtype == 0)
-    hipLaunchKernelGGL(bias_tanh_fwd_kernel<float>, dim3(g), dim3(256), 0, st, (const float*)x, b, (float*)y, rows, N);
-  else
-    hipLaunchKernelGGL(bias_tanh_fwd_kernel<bf16_t>, dim3(g), dim3(256), 0, st, (const bf16_t*)x, b, (bf16_t*)y, rows,
                        N);
 }
 

@@ -1,24 +1,25 @@
-"""BERT model family.
+"""BERT model family (reference: bert_modeling.py).
 
-Module tree, parameter names (207 state-dict keys for BERT-base, tied MLM
-decoder), initialisation and forward semantics follow the reference
-(reference: bert_modeling.py:180-1301):
-  * post-LN encoder, separate Q/K/V Linear layers, additive (1-mask)*-10000
-    attention mask (Q27), dropout on attention probabilities;
-  * erf-GELU with the 1.41421 constant (Q18); TF-style LayerNorm, eps 1e-12;
-  * ``LinearActivation`` keeps kaiming-uniform init with non-zero bias and is
-    deep-copied across layers (Q17); ``init_bert_weights`` N(0, 0.02) for
-    Linear/Embedding, applied by BertModel and again by the heads model;
-  * ``BertForPreTraining(...)`` returns MLM CE(ignore -1) + NSP CE.
-  * fine-tuning heads: MaskedLM, NextSentencePrediction, SequenceClassification,
-    MultipleChoice, TokenClassification, QuestionAnswering.
+What must match the reference, and why:
+  * the module tree and parameter names -- 207 state-dict keys for BERT-base,
+    tied MLM decoder -- because checkpoints and ``from_pretrained`` archives
+    are exchanged with it (reference :292-888);
+  * the numerics of the pre-training forward: post-LN encoder, separate
+    Q/K/V projections, additive (1 - mask) * -10000 attention mask (Q27),
+    dropout on the attention probabilities, erf-GELU with the 1.41421
+    constant (Q18), TF-style LayerNorm with eps 1e-12, MLM CE(ignore -1) +
+    NSP CE as the returned loss (reference :875-888);
+  * the initialisation quirks: N(0, 0.02) for Linear / Embedding weights via
+    ``init_bert_weights`` (applied by BertModel and again by each heads
+    model), while ``LinearActivation`` keeps its uniform(+-1/sqrt(fan_in))
+    weight AND bias and is deep-copied across encoder layers (Q17).
 
-Two execution paths share these modules:
-  * fused (GPU): ``FusedEmbedding`` -> 12 x ``FusedBertLayer`` -> ``FusedMLMLoss``
-    over the gfx950 HIP kernels (hetseq_amd/ops/bert_ops.py), fp32 or bf16
-    compute (``attach_store``/``set_compute_dtype``);
-  * reference (CPU or ``--no-fused``): plain torch ops, mathematically the
-    reference model; also the numerical oracle for the kernel tests.
+Two execution paths share the modules:
+  * fused (GPU): ``FusedEmbedding`` -> L x ``FusedBertLayer`` -> the fused
+    pre-training heads (sparse MLM + pooler/NSP) over the gfx950 HIP kernels
+    in hetseq_amd/ops/bert_ops.py, fp32 or bf16 compute;
+  * torch-op oracle (CPU, ``--no-fused``, fine-tuning heads): plain PyTorch,
+    the numerical reference the kernel tests compare against.
 """
 from __future__ import annotations
 
@@ -27,14 +28,13 @@ import json
 import logging
 import math
 import os
+import shutil
 import tarfile
 import tempfile
 
 import torch
 import torch.nn.functional as F
 from torch import nn
-from torch.nn import CrossEntropyLoss
-from torch.nn import init
 from torch.nn.parameter import Parameter
 from torch.utils import checkpoint
 
@@ -43,31 +43,33 @@ logger = logging.getLogger(__name__)
 TF_WEIGHTS_NAME = "model.ckpt"
 CONFIG_NAME = "bert_config.json"
 WEIGHTS_NAME = "pytorch_model.bin"
+FUSED_HIDDEN = (256, 512, 768, 1024, 1536, 2048)  # widths the LayerNorm / embedding kernels serve
 
 
-# ----------------------------------------------------------------- activations
+# ----------------------------------------------------------------- activations (reference :104-130)
+_ERF_DIV = 1.41421  # the reference's constant, not sqrt(2) (Q18)
+
+
 def f_gelu(x):
-    return x * 0.5 * (1.0 + torch.erf(x / 1.41421))
+    return 0.5 * x * (1.0 + torch.erf(x / _ERF_DIV))
+
+
+gelu = f_gelu
 
 
 def bias_gelu(bias, y):
-    x = bias + y
-    return x * 0.5 * (1.0 + torch.erf(x / 1.41421))
+    return f_gelu(y + bias)
 
 
 def bias_tanh(bias, y):
-    return torch.tanh(bias + y)
-
-
-def gelu(x):
-    return f_gelu(x)
+    return torch.tanh(y + bias)
 
 
 def swish(x):
-    return x * torch.sigmoid(x)
+    return torch.sigmoid(x) * x
 
 
-ACT2FN = {"gelu": gelu, "relu": torch.nn.functional.relu, "swish": swish}
+ACT2FN = {"gelu": gelu, "relu": F.relu, "swish": swish, "tanh": torch.tanh}
 
 
 def _fused_ok(t):
@@ -76,27 +78,21 @@ def _fused_ok(t):
     return use_fused(t)
 
 
-class LinearActivation(nn.Module):
-    """Linear (bias-free GEMM) followed by a fused bias+activation."""
+def _cw(w, x):
+    """``w`` in the compute dtype of ``x`` (autograd-transparent cast)."""
+    return w if w.dtype == x.dtype else w.to(x.dtype)
 
-    __constants__ = ["bias"]
+
+class LinearActivation(nn.Module):
+    """act(x @ W^T + b) with the bias added by the activation step (reference :132-177).
+
+    Parameters are initialised like ``torch.nn.Linear`` (uniform, bound 1/sqrt(fan_in) for weight
+    and bias), and ``init_bert_weights`` does not touch this class -- the reference quirk kept."""
 
     def __init__(self, in_features, out_features, act="gelu", bias=True):
         super().__init__()
-        self.in_features = in_features
-        self.out_features = out_features
-        self.fused_gelu = False
-        self.fused_tanh = False
+        self.in_features, self.out_features = in_features, out_features
         self.act = act
-        if isinstance(act, str):
-            if bias and act == "gelu":
-                self.fused_gelu = True
-            elif bias and act == "tanh":
-                self.fused_tanh = True
-            else:
-                self.act_fn = ACT2FN[act]
-        else:
-            self.act_fn = act
         self.weight = Parameter(torch.empty(out_features, in_features))
         if bias:
             self.bias = Parameter(torch.empty(out_features))
@@ -104,78 +100,82 @@ class LinearActivation(nn.Module):
             self.register_parameter("bias", None)
         self.reset_parameters()
 
+    @property
+    def fused_gelu(self):
+        return self.act == "gelu" and self.bias is not None
+
     def reset_parameters(self):
-        init.kaiming_uniform_(self.weight, a=math.sqrt(5))
+        nn.init.kaiming_uniform_(self.weight, a=math.sqrt(5))
         if self.bias is not None:
-            fan_in, _ = init._calculate_fan_in_and_fan_out(self.weight)
-            bound = 1 / math.sqrt(fan_in)
-            init.uniform_(self.bias, -bound, bound)
+            lim = self.in_features ** -0.5
+            nn.init.uniform_(self.bias, -lim, lim)
 
-    def forward(self, input):
-        if self.fused_gelu:
-            if _fused_ok(input) and input.dim() == 2 and self.out_features % 4 == 0:
-                from hetseq_amd.ops.bert_ops import bias_gelu as fused_bias_gelu
+    def forward(self, x):
+        y = F.linear(x, _cw(self.weight, x))
+        if self.bias is None:
+            return (ACT2FN[self.act] if isinstance(self.act, str) else self.act)(y)
+        if self.act == "gelu":
+            if _fused_ok(x) and x.dim() == 2 and self.out_features % 4 == 0:
+                from hetseq_amd.ops.bert_ops import bias_gelu as hip_bias_gelu
 
-                return fused_bias_gelu(F.linear(input, _cw(self.weight, input)), self.bias)
-            return bias_gelu(self.bias, F.linear(input, _cw(self.weight, input), None))
-        elif self.fused_tanh:
-            return bias_tanh(self.bias, F.linear(input, _cw(self.weight, input), None))
-        return self.act_fn(F.linear(input, _cw(self.weight, input), self.bias))
+                return hip_bias_gelu(y, self.bias)
+            return bias_gelu(self.bias, y)
+        if self.act == "tanh":
+            return bias_tanh(self.bias, y)
+        fn = ACT2FN[self.act] if isinstance(self.act, str) else self.act
+        return fn(y + self.bias)
 
     def extra_repr(self):
-        return "in_features={}, out_features={}, bias={}".format(self.in_features, self.out_features,
-                                                                  self.bias is not None)
+        return "in_features=%d, out_features=%d, bias=%s" % (self.in_features, self.out_features,
+                                                               self.bias is not None)
 
 
-def _cw(w, x):
-    """Weight in the compute dtype of ``x`` (autograd-transparent cast)."""
-    return w if w.dtype == x.dtype else w.to(x.dtype)
+# ----------------------------------------------------------------- configuration (reference :180-266)
+# (JSON key, default) -- the reference's config schema, in its positional order
+_CONFIG_FIELDS = (("hidden_size", 768), ("num_hidden_layers", 12), ("num_attention_heads", 12),
+                  ("intermediate_size", 3072), ("hidden_act", "gelu"), ("hidden_dropout_prob", 0.1),
+                  ("attention_probs_dropout_prob", 0.1), ("max_position_embeddings", 512),
+                  ("type_vocab_size", 2), ("initializer_range", 0.02))
 
 
-# ----------------------------------------------------------------- config
+def _read_json(path):
+    with open(path, "r", encoding="utf-8") as f:
+        return json.load(f)
+
+
 class BertConfig(object):
-    """Configuration of a BertModel (same JSON keys as the reference)."""
+    """BERT hyper-parameters.  ``BertConfig(vocab_size, **fields)`` or ``BertConfig(path.json)``;
+    the JSON keys are those of Google's ``bert_config.json``."""
 
-    def __init__(self, vocab_size_or_config_json_file, hidden_size=768, num_hidden_layers=12,
-                 num_attention_heads=12, intermediate_size=3072, hidden_act="gelu", hidden_dropout_prob=0.1,
-                 attention_probs_dropout_prob=0.1, max_position_embeddings=512, type_vocab_size=2,
-                 initializer_range=0.02):
-        if isinstance(vocab_size_or_config_json_file, str):
-            with open(vocab_size_or_config_json_file, "r", encoding="utf-8") as reader:
-                json_config = json.loads(reader.read())
-            for key, value in json_config.items():
-                self.__dict__[key] = value
-        elif isinstance(vocab_size_or_config_json_file, int):
-            self.vocab_size = vocab_size_or_config_json_file
-            self.hidden_size = hidden_size
-            self.num_hidden_layers = num_hidden_layers
-            self.num_attention_heads = num_attention_heads
-            self.hidden_act = hidden_act
-            self.intermediate_size = intermediate_size
-            self.hidden_dropout_prob = hidden_dropout_prob
-            self.attention_probs_dropout_prob = attention_probs_dropout_prob
-            self.max_position_embeddings = max_position_embeddings
-            self.type_vocab_size = type_vocab_size
-            self.initializer_range = initializer_range
-        else:
+    def __init__(self, vocab_size_or_config_json_file, *args, **kwargs):
+        src = vocab_size_or_config_json_file
+        if isinstance(src, str):
+            self.__dict__.update(_read_json(src))
+            return
+        if not isinstance(src, int):
             raise ValueError("First argument must be either a vocabulary size (int) or the path to a pretrained "
                              "model config file (str)")
+        names = [n for n, _ in _CONFIG_FIELDS]
+        if len(args) > len(names):
+            raise TypeError("BertConfig takes at most %d positional fields" % len(names))
+        unknown = sorted(set(kwargs) - set(names))
+        if unknown:
+            raise TypeError("unknown BertConfig field(s): %s" % ", ".join(unknown))
+        fields = dict(_CONFIG_FIELDS)
+        fields.update(zip(names, args))
+        fields.update(kwargs)
+        self.vocab_size = src
+        self.__dict__.update(fields)
 
     @classmethod
     def from_dict(cls, json_object):
-        config = BertConfig(vocab_size_or_config_json_file=-1)
-        for key, value in json_object.items():
-            config.__dict__[key] = value
-        return config
+        cfg = cls.__new__(cls)
+        cfg.__dict__.update(copy.deepcopy(dict(json_object)))
+        return cfg
 
     @classmethod
     def from_json_file(cls, json_file):
-        with open(json_file, "r", encoding="utf-8") as reader:
-            text = reader.read()
-        return cls.from_dict(json.loads(text))
-
-    def __repr__(self):
-        return str(self.to_json_string())
+        return cls.from_dict(_read_json(json_file))
 
     def to_dict(self):
         return copy.deepcopy(self.__dict__)
@@ -183,9 +183,12 @@ class BertConfig(object):
     def to_json_string(self):
         return json.dumps(self.to_dict(), indent=2, sort_keys=True) + "\n"
 
+    def __repr__(self):
+        return self.to_json_string()
+
 
 class BertLayerNorm(nn.Module):
-    """TF-style LayerNorm (epsilon inside the square root), eps=1e-12."""
+    """TF-style LayerNorm: (x - mean) / sqrt(biased var + eps) * weight + bias (reference :277-289)."""
 
     def __init__(self, hidden_size, eps=1e-12):
         super().__init__()
@@ -194,38 +197,36 @@ class BertLayerNorm(nn.Module):
         self.variance_epsilon = eps
 
     def forward(self, x):
-        if _fused_ok(x) and x.shape[-1] in (256, 512, 768, 1024, 1536, 2048):
+        if _fused_ok(x) and x.shape[-1] in FUSED_HIDDEN:
             from hetseq_amd.ops.bert_ops import layer_norm
 
-            shp = x.shape
-            return layer_norm(x.reshape(-1, shp[-1]).contiguous(), self.weight, self.bias,
-                              self.variance_epsilon).view(shp)
-        u = x.mean(-1, keepdim=True)
-        s = (x - u).pow(2).mean(-1, keepdim=True)
-        x = (x - u) / torch.sqrt(s + self.variance_epsilon)
-        return self.weight * x + self.bias
+            flat = x.reshape(-1, x.shape[-1]).contiguous()
+            return layer_norm(flat, self.weight, self.bias, self.variance_epsilon).view(x.shape)
+        centered = x - x.mean(-1, keepdim=True)
+        inv = torch.rsqrt(centered.pow(2).mean(-1, keepdim=True) + self.variance_epsilon)
+        return centered * inv * self.weight + self.bias
 
 
-# ----------------------------------------------------------------- modules
+# ----------------------------------------------------------------- encoder modules
 class BertEmbeddings(nn.Module):
+    """word + position + token-type embeddings -> LayerNorm -> dropout (reference :292-320)."""
+
     def __init__(self, config):
         super().__init__()
-        self.word_embeddings = nn.Embedding(config.vocab_size, config.hidden_size)
-        self.position_embeddings = nn.Embedding(config.max_position_embeddings, config.hidden_size)
-        self.token_type_embeddings = nn.Embedding(config.type_vocab_size, config.hidden_size)
-        self.LayerNorm = BertLayerNorm(config.hidden_size, eps=1e-12)
+        H = config.hidden_size
+        self.word_embeddings = nn.Embedding(config.vocab_size, H)
+        self.position_embeddings = nn.Embedding(config.max_position_embeddings, H)
+        self.token_type_embeddings = nn.Embedding(config.type_vocab_size, H)
+        self.LayerNorm = BertLayerNorm(H, eps=1e-12)
         self.dropout = nn.Dropout(config.hidden_dropout_prob)
 
     def forward(self, input_ids, token_type_ids=None):
-        seq_length = input_ids.size(1)
-        position_ids = torch.arange(seq_length, dtype=torch.long, device=input_ids.device)
-        position_ids = position_ids.unsqueeze(0).expand_as(input_ids)
+        S = input_ids.shape[1]
         if token_type_ids is None:
             token_type_ids = torch.zeros_like(input_ids)
-        embeddings = (self.word_embeddings(input_ids) + self.position_embeddings(position_ids)
-                      + self.token_type_embeddings(token_type_ids))
-        embeddings = self.LayerNorm(embeddings)
-        return self.dropout(embeddings)
+        pos = self.position_embeddings.weight[:S].unsqueeze(0)  # positions 0..S-1, broadcast over B
+        summed = self.word_embeddings(input_ids) + pos + self.token_type_embeddings(token_type_ids)
+        return self.dropout(self.LayerNorm(summed))
 
     def fused(self, input_ids, token_type_ids, out_dtype):
         from hetseq_amd.ops.bert_ops import FusedEmbedding
@@ -234,60 +235,65 @@ class BertEmbeddings(nn.Module):
         params = [self.word_embeddings.weight, self.position_embeddings.weight, self.token_type_embeddings.weight,
                   self.LayerNorm.weight, self.LayerNorm.bias]
         store = getattr(self, "_hs_store", None)
-        sink = None
-        if store is not None:
-            sink = {"views": lambda: [store.grad_view(q) for q in params]}
+        sink = {"views": lambda: [store.grad_view(q) for q in params]} if store is not None else None
         return FusedEmbedding.apply(input_ids, token_type_ids, *params, p, self.LayerNorm.variance_epsilon,
                                     out_dtype, sink)
 
 
 class BertSelfAttention(nn.Module):
+    """Multi-head scaled dot-product attention with separate Q/K/V projections (reference :323-377)."""
+
     def __init__(self, config):
         super().__init__()
-        if config.hidden_size % config.num_attention_heads != 0:
-            raise ValueError("The hidden size (%d) is not a multiple of the number of attention heads (%d)"
-                             % (config.hidden_size, config.num_attention_heads))
-        self.num_attention_heads = config.num_attention_heads
-        self.attention_head_size = int(config.hidden_size / config.num_attention_heads)
-        self.all_head_size = self.num_attention_heads * self.attention_head_size
-        self.query = nn.Linear(config.hidden_size, self.all_head_size)
-        self.key = nn.Linear(config.hidden_size, self.all_head_size)
-        self.value = nn.Linear(config.hidden_size, self.all_head_size)
+        H, nh = config.hidden_size, config.num_attention_heads
+        if H % nh:
+            raise ValueError("The hidden size (%d) is not a multiple of the number of attention heads (%d)" % (H, nh))
+        self.num_attention_heads = nh
+        self.attention_head_size = H // nh
+        self.all_head_size = nh * self.attention_head_size
+        self.query = nn.Linear(H, self.all_head_size)
+        self.key = nn.Linear(H, self.all_head_size)
+        self.value = nn.Linear(H, self.all_head_size)
         self.dropout = nn.Dropout(config.attention_probs_dropout_prob)
-        self.softmax = nn.Softmax(dim=-1)
         # Q/K/V weights (and biases) adjacent in the flat store -> one [3H, H] GEMM operand
         self._flat_groups = [[self.query.weight, self.key.weight, self.value.weight],
                              [self.query.bias, self.key.bias, self.value.bias]]
 
-    def transpose_for_scores(self, x):
-        new_x_shape = x.size()[:-1] + (self.num_attention_heads, self.attention_head_size)
-        return x.view(*new_x_shape).permute(0, 2, 1, 3)
-
-    def transpose_key_for_scores(self, x):
-        new_x_shape = x.size()[:-1] + (self.num_attention_heads, self.attention_head_size)
-        return x.view(*new_x_shape).permute(0, 2, 3, 1)
+    def _heads(self, t):
+        """[B, S, nh * dh] -> [B, nh, S, dh]"""
+        B, S, _ = t.shape
+        return t.reshape(B, S, self.num_attention_heads, self.attention_head_size).transpose(1, 2)
 
     def forward(self, hidden_states, attention_mask):
-        q = self.transpose_for_scores(self.query(hidden_states))
-        k = self.transpose_key_for_scores(self.key(hidden_states))
-        v = self.transpose_for_scores(self.value(hidden_states))
-        scores = torch.matmul(q, k) / math.sqrt(self.attention_head_size)
-        scores = scores + attention_mask
-        probs = self.dropout(self.softmax(scores))
-        ctx = torch.matmul(probs, v).permute(0, 2, 1, 3).contiguous()
-        return ctx.view(*(ctx.size()[:-2] + (self.all_head_size,)))
+        q, k, v = (self._heads(proj(hidden_states)) for proj in (self.query, self.key, self.value))
+        scores = q.matmul(k.transpose(-1, -2)) / math.sqrt(self.attention_head_size) + attention_mask
+        probs = self.dropout(torch.softmax(scores, dim=-1))
+        ctx = probs.matmul(v).transpose(1, 2)
+        return ctx.reshape(ctx.shape[0], ctx.shape[1], self.all_head_size)
 
 
-class BertSelfOutput(nn.Module):
-    def __init__(self, config):
+class _DenseDropoutAddNorm(nn.Module):
+    """LayerNorm(dropout(dense(x)) + residual): the shared shape of BertSelfOutput (reference
+    :380-391) and BertOutput (:416-427)."""
+
+    def __init__(self, in_features, config):
         super().__init__()
-        self.dense = nn.Linear(config.hidden_size, config.hidden_size)
+        self.dense = nn.Linear(in_features, config.hidden_size)
         self.LayerNorm = BertLayerNorm(config.hidden_size, eps=1e-12)
         self.dropout = nn.Dropout(config.hidden_dropout_prob)
 
     def forward(self, hidden_states, input_tensor):
-        hidden_states = self.dropout(self.dense(hidden_states))
-        return self.LayerNorm(hidden_states + input_tensor)
+        return self.LayerNorm(input_tensor + self.dropout(self.dense(hidden_states)))
+
+
+class BertSelfOutput(_DenseDropoutAddNorm):
+    def __init__(self, config):
+        super().__init__(config.hidden_size, config)
+
+
+class BertOutput(_DenseDropoutAddNorm):
+    def __init__(self, config):
+        super().__init__(config.intermediate_size, config)
 
 
 class BertAttention(nn.Module):
@@ -309,19 +315,9 @@ class BertIntermediate(nn.Module):
         return self.dense_act(hidden_states)
 
 
-class BertOutput(nn.Module):
-    def __init__(self, config):
-        super().__init__()
-        self.dense = nn.Linear(config.intermediate_size, config.hidden_size)
-        self.LayerNorm = BertLayerNorm(config.hidden_size, eps=1e-12)
-        self.dropout = nn.Dropout(config.hidden_dropout_prob)
-
-    def forward(self, hidden_states, input_tensor):
-        hidden_states = self.dropout(self.dense(hidden_states))
-        return self.LayerNorm(hidden_states + input_tensor)
-
-
 class BertLayer(nn.Module):
+    """Post-LN transformer block (reference :430-441) plus the fused-kernel plumbing."""
+
     def __init__(self, config):
         super().__init__()
         self.attention = BertAttention(config)
@@ -329,21 +325,21 @@ class BertLayer(nn.Module):
         self.output = BertOutput(config)
 
     def forward(self, hidden_states, attention_mask):
-        attention_output = self.attention(hidden_states, attention_mask)
-        intermediate_output = self.intermediate(attention_output)
-        return self.output(intermediate_output, attention_output)
+        attended = self.attention(hidden_states, attention_mask)
+        return self.output(self.intermediate(attended), attended)
 
     # ------------------------------------------------------------- fused path
     def fused_params(self):
-        cached = self.__dict__.get("_hs_pcache")  # parameter objects never change identity
-        if cached is not None:
-            return cached
-        a, o = self.attention, self.output
-        self.__dict__["_hs_pcache"] = ps = [a.self.query.weight, a.self.query.bias, a.self.key.weight, a.self.key.bias, a.self.value.weight,
-                a.self.value.bias, a.output.dense.weight, a.output.dense.bias, a.output.LayerNorm.weight,
-                a.output.LayerNorm.bias, self.intermediate.dense_act.weight, self.intermediate.dense_act.bias,
-                o.dense.weight, o.dense.bias, o.LayerNorm.weight, o.LayerNorm.bias]
-        return ps
+        """The 16 parameters in reference order (q.w, q.b, k.w, k.b, v.w, v.b, o.w, o.b, ln1.w,
+        ln1.b, i.w, i.b, out.w, out.b, ln2.w, ln2.b); parameter objects never change identity."""
+        cached = self.__dict__.get("_hs_pcache")
+        if cached is None:
+            sa, so, o = self.attention.self, self.attention.output, self.output
+            mods = (sa.query, sa.key, sa.value, so.dense, so.LayerNorm, self.intermediate.dense_act, o.dense,
+                    o.LayerNorm)
+            cached = [t for m in mods for t in (m.weight, m.bias)]
+            self.__dict__["_hs_pcache"] = cached
+        return cached
 
     def _weights(self):
         """Kernel-side weight views.  With a flat store they are fixed views into its buffers
@@ -391,7 +387,7 @@ class BertLayer(nn.Module):
     def fused_ok(self, x, S):
         sa = self.attention.self
         H = sa.query.weight.shape[1]
-        return (sa.attention_head_size == 64 and H in (256, 512, 768, 1024, 1536, 2048) and S % 32 == 0
+        return (sa.attention_head_size == 64 and H in FUSED_HIDDEN and S % 32 == 0
                 and self.intermediate.dense_act.fused_gelu and self.intermediate.dense_act.out_features % 4 == 0)
 
     def fused(self, x2d, mask_i64, B, S, recompute=False):
@@ -403,8 +399,7 @@ class BertLayer(nn.Module):
         seeds = tuple(rng.fork() if p > 0 else (0, 0) for p in (p_a, p_h, p_h))
         cfg = (B, S, self.attention.self.num_attention_heads, p_h, p_a, self.output.LayerNorm.variance_epsilon, seeds)
         meta = {"weights": self._weights, "cfg": cfg, "recompute": recompute}
-        store = getattr(self, "_hs_store", None)
-        if store is not None:
+        if getattr(self, "_hs_store", None) is not None:
             meta["grad_sink"] = self._grad_views
         return FusedBertLayer.apply(x2d, mask_i64, meta, *self.fused_params())
 
@@ -437,41 +432,41 @@ class BertLayer(nn.Module):
 
 
 class BertEncoder(nn.Module):
+    """L identical (deep-copied) layers; optional activation checkpointing over ceil(sqrt(L))-layer
+    segments (reference :444-487)."""
+
     def __init__(self, config):
         super().__init__()
-        layer = BertLayer(config)
-        self.layer = nn.ModuleList([copy.deepcopy(layer) for _ in range(config.num_hidden_layers)])
+        proto = BertLayer(config)
+        self.layer = nn.ModuleList([copy.deepcopy(proto) for _ in range(config.num_hidden_layers)])
+
+    def _run(self, first, last):
+        def segment(h, mask):
+            for blk in self.layer[first:last]:
+                h = blk(h, mask)
+            return h
+
+        return segment
 
     def forward(self, hidden_states, attention_mask, output_all_encoded_layers=True, checkpoint_activations=False):
-        all_encoder_layers = []
-
-        def custom(start, end):
-            def custom_forward(*inputs):
-                x_ = inputs[0]
-                for layer in self.layer[start:end]:
-                    x_ = layer(x_, inputs[1])
-                return x_
-
-            return custom_forward
-
         if checkpoint_activations:
-            l, num_layers = 0, len(self.layer)
-            chunk_length = math.ceil(math.sqrt(num_layers))
-            while l < num_layers:
-                hidden_states = checkpoint.checkpoint(custom(l, l + chunk_length), hidden_states, attention_mask * 1,
-                                                      use_reentrant=False)
-                l += chunk_length
-        else:
-            for layer_module in self.layer:
-                hidden_states = layer_module(hidden_states, attention_mask)
-                if output_all_encoded_layers:
-                    all_encoder_layers.append(hidden_states)
-        if not output_all_encoded_layers or checkpoint_activations:
-            all_encoder_layers.append(hidden_states)
-        return all_encoder_layers
+            L = len(self.layer)
+            step = math.ceil(math.sqrt(L))
+            for first in range(0, L, step):
+                hidden_states = checkpoint.checkpoint(self._run(first, first + step), hidden_states,
+                                                      attention_mask * 1, use_reentrant=False)
+            return [hidden_states]
+        outs = []
+        for blk in self.layer:
+            hidden_states = blk(hidden_states, attention_mask)
+            outs.append(hidden_states)
+        return outs if output_all_encoded_layers else outs[-1:]
 
 
+# ----------------------------------------------------------------- heads (reference :506-581)
 class BertPooler(nn.Module):
+    """tanh(dense(first token))."""
+
     def __init__(self, config):
         super().__init__()
         self.dense_act = LinearActivation(config.hidden_size, config.hidden_size, act="tanh")
@@ -491,22 +486,25 @@ class BertPredictionHeadTransform(nn.Module):
 
 
 class BertLMPredictionHead(nn.Module):
+    """transform -> decoder tied to the word embeddings (no bias of its own) + a separate bias."""
+
     def __init__(self, config, bert_model_embedding_weights):
         super().__init__()
+        V, H = bert_model_embedding_weights.shape
         self.transform = BertPredictionHeadTransform(config)
-        self.decoder = nn.Linear(bert_model_embedding_weights.size(1), bert_model_embedding_weights.size(0),
-                                 bias=False)
+        self.decoder = nn.Linear(H, V, bias=False)
         self.decoder.weight = bert_model_embedding_weights
-        self.bias = nn.Parameter(torch.zeros(bert_model_embedding_weights.size(0)))
+        self.bias = nn.Parameter(torch.zeros(V))
 
     def forward(self, hidden_states):
-        hidden_states = self.transform(hidden_states)
-        from hetseq_amd.runtime.profiling import range_push, range_pop
+        from hetseq_amd.runtime.profiling import range_pop, range_push
 
+        h = self.transform(hidden_states)
         range_push("decoder")
-        out = self.decoder(hidden_states) + self.bias
-        range_pop()
-        return out
+        try:
+            return F.linear(h, self.decoder.weight, self.bias)
+        finally:
+            range_pop()
 
 
 class BertOnlyMLMHead(nn.Module):
@@ -528,6 +526,9 @@ class BertOnlyNSPHead(nn.Module):
 
 
 class BertPreTrainingHeads(nn.Module):
+    """MLM prediction head + NSP classifier (registered in that order: it fixes the parameter
+    order, hence the optimizer-state indices of reference checkpoints)."""
+
     def __init__(self, config, bert_model_embedding_weights):
         super().__init__()
         self.predictions = BertLMPredictionHead(config, bert_model_embedding_weights)
@@ -537,24 +538,51 @@ class BertPreTrainingHeads(nn.Module):
         return self.predictions(sequence_output), self.seq_relationship(pooled_output)
 
 
+# ----------------------------------------------------------------- checkpoint import
+def _pretrained_key(name):
+    """Names of pre-PyTorch-era BERT archives (LayerNorm gamma/beta) -> this module tree."""
+    return name.replace("gamma", "weight").replace("beta", "bias")
+
+
+def load_pretrained_state(model, state_dict):
+    """Load an archive state dict into ``model`` (non-strict: heads absent from the archive keep
+    their fresh init).  Renames gamma/beta, and drops a leading ``bert.`` when ``model`` is the bare
+    encoder.  Shape mismatches raise; missing / unused keys are logged (reference :690-733)."""
+    remapped = {_pretrained_key(k): v for k, v in state_dict.items()}
+    if not hasattr(model, "bert") and any(k.startswith("bert.") for k in remapped):
+        remapped = {k[len("bert."):] if k.startswith("bert.") else k: v for k, v in remapped.items()}
+    result = model.load_state_dict(remapped, strict=False)
+    if result.missing_keys:
+        logger.info("Weights of %s not initialized from pretrained model: %s", type(model).__name__,
+                    result.missing_keys)
+    if result.unexpected_keys:
+        logger.info("Weights from pretrained model not used in %s: %s", type(model).__name__,
+                    result.unexpected_keys)
+    return model
+
+
 class BertPreTrainedModel(nn.Module):
-    """Weight init + (local-only) ``from_pretrained``."""
+    """Weight init, runtime plumbing (flat store, compute dtype) and local ``from_pretrained``."""
 
     def __init__(self, config, *inputs, **kwargs):
         super().__init__()
         if not isinstance(config, BertConfig):
             raise ValueError("Parameter config in `{}(config)` should be an instance of class `BertConfig`."
-                             .format(self.__class__.__name__))
+                             .format(type(self).__name__))
         self.config = config
 
     def init_bert_weights(self, module):
+        """N(0, initializer_range) for Linear / Embedding weights, zero Linear biases, identity
+        LayerNorm; LinearActivation is deliberately not matched (reference :599-610)."""
+        std = self.config.initializer_range
+        if isinstance(module, BertLayerNorm):
+            nn.init.ones_(module.weight)
+            nn.init.zeros_(module.bias)
+            return
         if isinstance(module, (nn.Linear, nn.Embedding)):
-            module.weight.data.normal_(mean=0.0, std=self.config.initializer_range)
-        elif isinstance(module, BertLayerNorm):
-            module.bias.data.zero_()
-            module.weight.data.fill_(1.0)
+            module.weight.data.normal_(0.0, std)
         if isinstance(module, nn.Linear) and module.bias is not None:
-            module.bias.data.zero_()
+            nn.init.zeros_(module.bias)
 
     # --- runtime plumbing (flat store / compute dtype / fused switch)
     def attach_store(self, store, compute_dtype=torch.float32):
@@ -577,72 +605,40 @@ class BertPreTrainedModel(nn.Module):
     @classmethod
     def from_pretrained(cls, pretrained_model_name_or_path, state_dict=None, cache_dir=None, from_tf=False, *inputs,
                         **kwargs):
-        """Load from a local directory or .tar.gz archive holding bert_config.json + pytorch_model.bin.
-
-        There is no network here: remote names go through
-        :func:`hetseq_amd.utils.file_utils.cached_path`, which only resolves
-        cached or local files.  Weights load with ``weights_only=True``."""
+        """Build from a local directory or ``.tar.gz`` archive (bert_config.json + pytorch_model.bin,
+        or a TF checkpoint with ``from_tf``).  There is no network: remote names resolve only through
+        :func:`hetseq_amd.utils.file_utils.cached_path`'s cache.  Weights load with
+        ``weights_only=True``; TF checkpoints are read without TensorFlow."""
         from hetseq_amd.utils.file_utils import cached_path
 
         resolved = cached_path(pretrained_model_name_or_path, cache_dir=cache_dir)
-        tempdir = None
-        if os.path.isdir(resolved) or from_tf:
-            serialization_dir = resolved
-        else:
-            tempdir = tempfile.mkdtemp()
+        unpacked = None
+        if not (os.path.isdir(resolved) or from_tf):
+            unpacked = tempfile.mkdtemp()
             with tarfile.open(resolved, "r:gz") as archive:
-                archive.extractall(tempdir, filter="data")
-            serialization_dir = tempdir
-        config = BertConfig.from_json_file(os.path.join(serialization_dir, CONFIG_NAME))
-        model = cls(config, *inputs, **kwargs)
-        if state_dict is None and not from_tf:
-            state_dict = torch.load(os.path.join(serialization_dir, WEIGHTS_NAME), map_location="cpu",
-                                    weights_only=True)
-        if tempdir:
-            import shutil
+                archive.extractall(unpacked, filter="data")
+        root = unpacked or resolved
+        try:
+            model = cls(BertConfig.from_json_file(os.path.join(root, CONFIG_NAME)), *inputs, **kwargs)
+            if from_tf:
+                from hetseq_amd.utils.tf_checkpoint import load_tf_weights_in_bert
 
-            shutil.rmtree(tempdir, ignore_errors=True)
-        if from_tf:
-            # reference: bert_modeling.py:685-688 (TF_WEIGHTS_NAME = 'model.ckpt'); read without TensorFlow
-            from hetseq_amd.utils.tf_checkpoint import load_tf_weights_in_bert
-
-            prefix = os.path.join(serialization_dir, TF_WEIGHTS_NAME)
-            if not os.path.exists(prefix + ".index") and os.path.exists(os.path.join(serialization_dir,
-                                                                                    "bert_model.ckpt.index")):
-                prefix = os.path.join(serialization_dir, "bert_model.ckpt")  # Google's release name
-            return load_tf_weights_in_bert(model, prefix)
-        renamed = {}
-        for k, v in state_dict.items():
-            nk = k.replace("gamma", "weight").replace("beta", "bias")
-            renamed[nk] = v
-        missing, unexpected, errors = [], [], []
-        metadata = getattr(state_dict, "_metadata", None)
-        state_dict = renamed
-        if metadata is not None:
-            state_dict._metadata = metadata
-
-        def load(module, prefix=""):
-            local_metadata = {} if metadata is None else metadata.get(prefix[:-1], {})
-            module._load_from_state_dict(state_dict, prefix, local_metadata, True, missing, unexpected, errors)
-            for name, child in module._modules.items():
-                if child is not None:
-                    load(child, prefix + name + ".")
-
-        start_prefix = ""
-        if not hasattr(model, "bert") and any(s.startswith("bert.") for s in state_dict.keys()):
-            start_prefix = "bert."
-        load(model, prefix=start_prefix)
-        if missing:
-            logger.info("Weights of %s not initialized from pretrained model: %s", model.__class__.__name__, missing)
-        if unexpected:
-            logger.info("Weights from pretrained model not used in %s: %s", model.__class__.__name__, unexpected)
-        if errors:
-            raise RuntimeError("Error(s) in loading state_dict for {}:\n\t{}".format(model.__class__.__name__,
-                                                                                      "\n\t".join(errors)))
-        return model
+                prefix = os.path.join(root, TF_WEIGHTS_NAME)
+                if not os.path.exists(prefix + ".index") and os.path.exists(os.path.join(root,
+                                                                                        "bert_model.ckpt.index")):
+                    prefix = os.path.join(root, "bert_model.ckpt")  # Google's release name
+                return load_tf_weights_in_bert(model, prefix)
+            if state_dict is None:
+                state_dict = torch.load(os.path.join(root, WEIGHTS_NAME), map_location="cpu", weights_only=True)
+        finally:
+            if unpacked:
+                shutil.rmtree(unpacked, ignore_errors=True)
+        return load_pretrained_state(model, state_dict)
 
 
 class BertModel(BertPreTrainedModel):
+    """Embeddings + encoder + pooler; returns (encoded layers, pooled first token)."""
+
     def __init__(self, config):
         super().__init__(config)
         self.embeddings = BertEmbeddings(config)
@@ -654,8 +650,12 @@ class BertModel(BertPreTrainedModel):
         if not _fused_ok(input_ids) or getattr(self, "_hs_disable_fused", False):
             return False
         S = input_ids.shape[-1]
-        H = self.config.hidden_size
-        return (H in (256, 512, 768, 1024, 1536, 2048) and all(l.fused_ok(None, S) for l in self.encoder.layer))
+        return self.config.hidden_size in FUSED_HIDDEN and all(blk.fused_ok(None, S) for blk in self.encoder.layer)
+
+    @staticmethod
+    def additive_mask(attention_mask, dtype):
+        """[B, S] 0/1 mask -> [B, 1, 1, S] additive (1 - m) * -10000 (reference :798-806, Q27)."""
+        return (1.0 - attention_mask[:, None, None, :].to(dtype)) * -10000.0
 
     def forward(self, input_ids, token_type_ids=None, attention_mask=None, output_all_encoded_layers=True,
                 checkpoint_activations=False):
@@ -665,23 +665,17 @@ class BertModel(BertPreTrainedModel):
             token_type_ids = torch.zeros_like(input_ids)
         if self._can_fuse(input_ids):
             seq2d, pooled = self.fused_forward(input_ids, token_type_ids, attention_mask, checkpoint_activations)
-            B, S = input_ids.shape
-            seq = seq2d.view(B, S, -1)
-            return (seq if not output_all_encoded_layers else [seq]), pooled
-        extended = attention_mask.unsqueeze(1).unsqueeze(2)
-        extended = extended.to(dtype=next(self.parameters()).dtype)
-        extended = (1.0 - extended) * -10000.0
-        embedding_output = self.embeddings(input_ids, token_type_ids)
-        encoded_layers = self.encoder(embedding_output, extended, output_all_encoded_layers=output_all_encoded_layers,
-                                      checkpoint_activations=checkpoint_activations)
-        sequence_output = encoded_layers[-1]
-        pooled_output = self.pooler(sequence_output)
-        if not output_all_encoded_layers:
-            encoded_layers = encoded_layers[-1]
-        return encoded_layers, pooled_output
+            seq = seq2d.view(*input_ids.shape, -1)
+            return ([seq] if output_all_encoded_layers else seq), pooled
+        mask = self.additive_mask(attention_mask, self.embeddings.word_embeddings.weight.dtype)
+        layers = self.encoder(self.embeddings(input_ids, token_type_ids), mask,
+                              output_all_encoded_layers=output_all_encoded_layers,
+                              checkpoint_activations=checkpoint_activations)
+        pooled = self.pooler(layers[-1])
+        return (layers if output_all_encoded_layers else layers[-1]), pooled
 
-    def fused_forward(self, input_ids, token_type_ids, attention_mask, checkpoint_activations=False):
-        """Fused encoder: returns (sequence_output [B*S, H], pooled [B, H])."""
+    def fused_encoder(self, input_ids, token_type_ids, attention_mask, checkpoint_activations=False):
+        """Fused embeddings + encoder: the sequence output [B*S, H] in the compute dtype."""
         from hetseq_amd.runtime.profiling import range_pop, range_push
 
         B, S = input_ids.shape
@@ -689,17 +683,26 @@ class BertModel(BertPreTrainedModel):
         range_push("embeddings")
         x = self.embeddings.fused(input_ids, token_type_ids, self.compute_dtype)
         range_pop()
-        for i, layer in enumerate(self.encoder.layer):
+        for i, blk in enumerate(self.encoder.layer):
             range_push("layer%d" % i)
-            x = layer.fused(x, mask, B, S, recompute=checkpoint_activations)
+            x = blk.fused(x, mask, B, S, recompute=checkpoint_activations)
             range_pop()
-        first = x.view(B, S, -1)[:, 0]
-        pooled = self.pooler.dense_act(first)
-        return x, pooled
+        return x
+
+    def fused_forward(self, input_ids, token_type_ids, attention_mask, checkpoint_activations=False):
+        """Fused encoder + pooler: (sequence output [B*S, H], pooled [B, H])."""
+        x = self.fused_encoder(input_ids, token_type_ids, attention_mask, checkpoint_activations)
+        B, S = input_ids.shape
+        return x, self.pooler.dense_act(x.view(B, S, -1)[:, 0])
+
+
+def _xent(logits, target, ignore_index=-100):
+    """Cross-entropy in fp32 whatever the compute dtype."""
+    return F.cross_entropy(logits.float(), target, ignore_index=ignore_index)
 
 
 class BertForPreTraining(BertPreTrainedModel):
-    """BERT with the MLM + NSP pre-training heads; returns the summed loss."""
+    """BERT with the MLM + NSP pre-training heads; with labels, returns the summed loss."""
 
     def __init__(self, config):
         super().__init__(config)
@@ -710,171 +713,162 @@ class BertForPreTraining(BertPreTrainedModel):
 
     def forward(self, input_ids, token_type_ids=None, attention_mask=None, masked_lm_labels=None,
                 next_sentence_label=None, checkpoint_activations=False):
-        if (masked_lm_labels is not None and next_sentence_label is not None
-                and self.bert._can_fuse(input_ids)):
+        labelled = masked_lm_labels is not None and next_sentence_label is not None
+        if labelled and self.bert._can_fuse(input_ids):
             return self._fused_loss(input_ids, token_type_ids, attention_mask, masked_lm_labels, next_sentence_label,
                                     checkpoint_activations)
-        sequence_output, pooled_output = self.bert(input_ids, token_type_ids, attention_mask,
-                                                   output_all_encoded_layers=False,
-                                                   checkpoint_activations=checkpoint_activations)
-        prediction_scores, seq_relationship_score = self.cls(sequence_output, pooled_output)
-        if masked_lm_labels is not None and next_sentence_label is not None:
-            loss_fct = CrossEntropyLoss(ignore_index=-1)
-            masked_lm_loss = loss_fct(prediction_scores.view(-1, self.config.vocab_size).float(),
-                                      masked_lm_labels.view(-1))
-            next_sentence_loss = loss_fct(seq_relationship_score.view(-1, 2).float(), next_sentence_label.view(-1))
-            return masked_lm_loss + next_sentence_loss
-        return prediction_scores, seq_relationship_score
+        seq, pooled = self.bert(input_ids, token_type_ids, attention_mask, output_all_encoded_layers=False,
+                                checkpoint_activations=checkpoint_activations)
+        mlm_scores, nsp_scores = self.cls(seq, pooled)
+        if not labelled:
+            return mlm_scores, nsp_scores
+        return (_xent(mlm_scores.reshape(-1, self.config.vocab_size), masked_lm_labels.reshape(-1), -1)
+                + _xent(nsp_scores.reshape(-1, 2), next_sentence_label.reshape(-1), -1))
 
     def _mlm_weights(self):
         t = self.cls.predictions.transform
+        wt, wd = t.dense_act.weight, self.cls.predictions.decoder.weight
+        if self.compute_dtype != torch.bfloat16:
+            return wt.detach(), wd.detach()
         store = getattr(self, "_hs_store", None)
-        if self.compute_dtype == torch.bfloat16:
-            if store is not None:
-                return store.shadow_view(t.dense_act.weight), store.shadow_view(self.cls.predictions.decoder.weight)
-            return t.dense_act.weight.detach().bfloat16(), self.cls.predictions.decoder.weight.detach().bfloat16()
-        return t.dense_act.weight.detach(), self.cls.predictions.decoder.weight.detach()
+        if store is not None:
+            return store.shadow_view(wt), store.shadow_view(wd)
+        return wt.detach().bfloat16(), wd.detach().bfloat16()
 
     def _fused_loss(self, input_ids, token_type_ids, attention_mask, labels, nsp_label, checkpoint_activations):
-        from hetseq_amd.ops.bert_ops import FusedMLMLoss
+        from hetseq_amd.ops.bert_ops import FusedPreTrainingLoss
 
         if token_type_ids is None:
             token_type_ids = torch.zeros_like(input_ids)
         if attention_mask is None:
             attention_mask = torch.ones_like(input_ids)
         B, S = input_ids.shape
-        seq2d, pooled = self.bert.fused_forward(input_ids, token_type_ids, attention_mask, checkpoint_activations)
+        seq2d = self.bert.fused_encoder(input_ids, token_type_ids, attention_mask, checkpoint_activations)
         cap = B * S if self.max_predictions_per_seq is None else min(B * S, B * int(self.max_predictions_per_seq))
-        t = self.cls.predictions.transform
-        meta = {"cap": cap, "eps": t.LayerNorm.variance_epsilon, "weights": self._mlm_weights}
+        t, pred = self.cls.predictions.transform, self.cls.predictions
+        pooler, nsp = self.bert.pooler.dense_act, self.cls.seq_relationship
+        params = [t.dense_act.weight, t.dense_act.bias, t.LayerNorm.weight, t.LayerNorm.bias, pred.decoder.weight,
+                  pred.bias, pooler.weight, pooler.bias, nsp.weight, nsp.bias]
+        meta = {"cap": cap, "eps": t.LayerNorm.variance_epsilon, "weights": self._mlm_weights, "B": B, "S": S}
         store = getattr(self, "_hs_store", None)
         if store is not None:
-            cls_params = [t.dense_act.weight, t.dense_act.bias, t.LayerNorm.weight, t.LayerNorm.bias,
-                          self.cls.predictions.decoder.weight, self.cls.predictions.bias]
-            meta["grad_sink"] = lambda: [store.grad_view(q) for q in cls_params]
-        mlm_loss = FusedMLMLoss.apply(seq2d, labels.reshape(-1).contiguous(), meta, t.dense_act.weight,
-                                      t.dense_act.bias, t.LayerNorm.weight, t.LayerNorm.bias,
-                                      self.cls.predictions.decoder.weight, self.cls.predictions.bias)
-        nsp_logits = self.cls.seq_relationship(pooled.float() if pooled.dtype != torch.float32 else pooled)
-        nsp_loss = F.cross_entropy(nsp_logits.view(-1, 2), nsp_label.view(-1), ignore_index=-1)
-        return mlm_loss + nsp_loss
+            meta["grad_sink"] = lambda: [store.grad_view(q) for q in params]
+        return FusedPreTrainingLoss.apply(seq2d, labels.reshape(-1).contiguous(), nsp_label.reshape(-1).contiguous(),
+                                          meta, *params)
 
 
-class BertForMaskedLM(BertPreTrainedModel):
+# ----------------------------------------------------------------- fine-tuning heads (reference :891-1301)
+class _BertFineTune(BertPreTrainedModel):
+    """An encoder plus a task head; subclasses define the head modules and ``_head``."""
+
     def __init__(self, config):
         super().__init__(config)
         self.bert = BertModel(config)
+
+    def _encode(self, input_ids, token_type_ids, attention_mask):
+        return self.bert(input_ids, token_type_ids, attention_mask, output_all_encoded_layers=False)
+
+
+class BertForMaskedLM(_BertFineTune):
+    def __init__(self, config):
+        super().__init__(config)
         self.cls = BertOnlyMLMHead(config, self.bert.embeddings.word_embeddings.weight)
         self.apply(self.init_bert_weights)
 
     def forward(self, input_ids, token_type_ids=None, attention_mask=None, masked_lm_labels=None,
                 checkpoint_activations=False):
-        sequence_output, _ = self.bert(input_ids, token_type_ids, attention_mask, output_all_encoded_layers=False)
-        prediction_scores = self.cls(sequence_output)
-        if masked_lm_labels is not None:
-            return CrossEntropyLoss(ignore_index=-1)(prediction_scores.view(-1, self.config.vocab_size).float(),
-                                                     masked_lm_labels.view(-1))
-        return prediction_scores
+        scores = self.cls(self._encode(input_ids, token_type_ids, attention_mask)[0])
+        if masked_lm_labels is None:
+            return scores
+        return _xent(scores.reshape(-1, self.config.vocab_size), masked_lm_labels.reshape(-1), -1)
 
 
-class BertForNextSentencePrediction(BertPreTrainedModel):
+class BertForNextSentencePrediction(_BertFineTune):
     def __init__(self, config):
         super().__init__(config)
-        self.bert = BertModel(config)
         self.cls = BertOnlyNSPHead(config)
         self.apply(self.init_bert_weights)
 
     def forward(self, input_ids, token_type_ids=None, attention_mask=None, next_sentence_label=None,
                 checkpoint_activations=False):
-        _, pooled_output = self.bert(input_ids, token_type_ids, attention_mask, output_all_encoded_layers=False)
-        seq_relationship_score = self.cls(pooled_output)
-        if next_sentence_label is not None:
-            return CrossEntropyLoss(ignore_index=-1)(seq_relationship_score.view(-1, 2).float(),
-                                                     next_sentence_label.view(-1))
-        return seq_relationship_score
+        scores = self.cls(self._encode(input_ids, token_type_ids, attention_mask)[1])
+        if next_sentence_label is None:
+            return scores
+        return _xent(scores.reshape(-1, 2), next_sentence_label.reshape(-1), -1)
 
 
-class BertForSequenceClassification(BertPreTrainedModel):
-    def __init__(self, config, num_labels):
+class _PooledClassifier(_BertFineTune):
+    """dropout(pooled) -> Linear(H, width)."""
+
+    def __init__(self, config, width):
         super().__init__(config)
-        self.num_labels = num_labels
-        self.bert = BertModel(config)
         self.dropout = nn.Dropout(config.hidden_dropout_prob)
-        self.classifier = nn.Linear(config.hidden_size, num_labels)
+        self.classifier = nn.Linear(config.hidden_size, width)
         self.apply(self.init_bert_weights)
 
+    def _logits(self, input_ids, token_type_ids, attention_mask):
+        return self.classifier(self.dropout(self._encode(input_ids, token_type_ids, attention_mask)[1]))
+
+
+class BertForSequenceClassification(_PooledClassifier):
+    def __init__(self, config, num_labels):
+        super().__init__(config, num_labels)
+        self.num_labels = num_labels
+
     def forward(self, input_ids, token_type_ids=None, attention_mask=None, labels=None, checkpoint_activations=False):
-        _, pooled_output = self.bert(input_ids, token_type_ids, attention_mask, output_all_encoded_layers=False)
-        logits = self.classifier(self.dropout(pooled_output))
-        if labels is not None:
-            return CrossEntropyLoss()(logits.view(-1, self.num_labels).float(), labels.view(-1))
-        return logits
+        logits = self._logits(input_ids, token_type_ids, attention_mask)
+        return logits if labels is None else _xent(logits.reshape(-1, self.num_labels), labels.reshape(-1))
 
 
-class BertForMultipleChoice(BertPreTrainedModel):
+class BertForMultipleChoice(_PooledClassifier):
+    """Scores each of ``num_choices`` [B, C, S] candidates with a 1-wide classifier."""
+
     def __init__(self, config, num_choices):
-        super().__init__(config)
+        super().__init__(config, 1)
         self.num_choices = num_choices
-        self.bert = BertModel(config)
-        self.dropout = nn.Dropout(config.hidden_dropout_prob)
-        self.classifier = nn.Linear(config.hidden_size, 1)
-        self.apply(self.init_bert_weights)
 
     def forward(self, input_ids, token_type_ids=None, attention_mask=None, labels=None, checkpoint_activations=False):
-        flat_input_ids = input_ids.reshape(-1, input_ids.size(-1))
-        flat_token_type_ids = token_type_ids.reshape(-1, token_type_ids.size(-1))
-        flat_attention_mask = attention_mask.reshape(-1, attention_mask.size(-1))
-        _, pooled_output = self.bert(flat_input_ids, flat_token_type_ids, flat_attention_mask,
-                                     output_all_encoded_layers=False)
-        logits = self.classifier(self.dropout(pooled_output))
-        reshaped_logits = logits.view(-1, self.num_choices)
-        if labels is not None:
-            return CrossEntropyLoss()(reshaped_logits.float(), labels)
-        return reshaped_logits
+        S = input_ids.shape[-1]
+        flat = [t.reshape(-1, S) if t is not None else None for t in (input_ids, token_type_ids, attention_mask)]
+        logits = self._logits(*flat).reshape(-1, self.num_choices)
+        return logits if labels is None else _xent(logits, labels)
 
 
-class BertForTokenClassification(BertPreTrainedModel):
+class BertForTokenClassification(_BertFineTune):
     def __init__(self, config, num_labels):
         super().__init__(config)
         self.num_labels = num_labels
-        self.bert = BertModel(config)
         self.dropout = nn.Dropout(config.hidden_dropout_prob)
         self.classifier = nn.Linear(config.hidden_size, num_labels)
         self.apply(self.init_bert_weights)
 
     def forward(self, input_ids, token_type_ids=None, attention_mask=None, labels=None, checkpoint_activations=False):
-        sequence_output, _ = self.bert(input_ids, token_type_ids, attention_mask, output_all_encoded_layers=False)
-        logits = self.classifier(self.dropout(sequence_output))
-        if labels is not None:
-            loss_fct = CrossEntropyLoss()
-            if attention_mask is not None:
-                active = attention_mask.view(-1) == 1
-                return loss_fct(logits.view(-1, self.num_labels)[active].float(), labels.view(-1)[active])
-            return loss_fct(logits.view(-1, self.num_labels).float(), labels.view(-1))
-        return logits
+        seq = self._encode(input_ids, token_type_ids, attention_mask)[0]
+        logits = self.classifier(self.dropout(seq)).reshape(-1, self.num_labels)
+        if labels is None:
+            return logits.view(*seq.shape[:-1], self.num_labels)
+        labels = labels.reshape(-1)
+        if attention_mask is not None:  # only positions the mask keeps
+            keep = attention_mask.reshape(-1) == 1
+            logits, labels = logits[keep], labels[keep]
+        return _xent(logits, labels)
 
 
-class BertForQuestionAnswering(BertPreTrainedModel):
+class BertForQuestionAnswering(_BertFineTune):
+    """Span start / end logits; positions outside the sequence are clamped to S and ignored."""
+
     def __init__(self, config):
         super().__init__(config)
-        self.bert = BertModel(config)
         self.qa_outputs = nn.Linear(config.hidden_size, 2)
         self.apply(self.init_bert_weights)
 
     def forward(self, input_ids, token_type_ids=None, attention_mask=None, start_positions=None, end_positions=None,
                 checkpoint_activations=False):
-        sequence_output, _ = self.bert(input_ids, token_type_ids, attention_mask, output_all_encoded_layers=False)
-        logits = self.qa_outputs(sequence_output)
-        start_logits, end_logits = logits.split(1, dim=-1)
-        start_logits, end_logits = start_logits.squeeze(-1), end_logits.squeeze(-1)
-        if start_positions is not None and end_positions is not None:
-            if len(start_positions.size()) > 1:
-                start_positions = start_positions.squeeze(-1)
-            if len(end_positions.size()) > 1:
-                end_positions = end_positions.squeeze(-1)
-            ignored_index = start_logits.size(1)
-            start_positions = start_positions.clamp(0, ignored_index)
-            end_positions = end_positions.clamp(0, ignored_index)
-            loss_fct = CrossEntropyLoss(ignore_index=ignored_index)
-            return (loss_fct(start_logits.float(), start_positions) + loss_fct(end_logits.float(), end_positions)) / 2
-        return start_logits, end_logits
+        seq = self._encode(input_ids, token_type_ids, attention_mask)[0]
+        start_logits, end_logits = self.qa_outputs(seq).unbind(-1)
+        if start_positions is None or end_positions is None:
+            return start_logits, end_logits
+        S = start_logits.shape[1]
+        losses = [_xent(lg, pos.reshape(pos.shape[0], -1)[:, 0].clamp(0, S), ignore_index=S)
+                  for lg, pos in ((start_logits, start_positions), (end_logits, end_positions))]
+        return sum(losses) / 2

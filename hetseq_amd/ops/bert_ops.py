@@ -9,9 +9,10 @@ control:
                        -> FFN1 -> bias+GELU -> FFN2 -> bias/dropout/residual/LN
                        (bert_modeling.py:323-441), with in-Function activation
                        recomputation for ``--checkpoint-activations``
-* ``FusedMLMLoss``     masked-row compaction -> transform(GEMM+GELU+LN) -> tied decoder
-                       GEMM on masked rows only -> fused cross-entropy
-                       (bert_modeling.py:519-549, 880-882)
+* ``FusedPreTrainingLoss``  masked-row compaction -> transform(GEMM+GELU+LN) -> tied
+                       decoder GEMM on masked rows only -> fused cross-entropy, plus
+                       pooler(tanh) -> NSP -> CE -> loss sum in the pool_nsp kernels
+                       (bert_modeling.py:506-581, 875-888)
 Standalone ops used by tests and other models: ``attention``, ``layer_norm``,
 ``bias_dropout_residual_ln``, ``bias_gelu``.
 
@@ -474,14 +475,21 @@ def cross_entropy(logits, labels, ignore_index=-1):
     return FusedCrossEntropy.apply(logits, labels, ignore_index)
 
 
-class FusedMLMLoss(torch.autograd.Function):
-    """Sparse masked-LM head + loss.  Exact w.r.t. the dense reference: rows with
-    label -1 contribute neither loss nor gradient, so only the (at most ``cap``)
-    labelled rows go through the transform, the tied decoder GEMM and the CE."""
+class FusedPreTrainingLoss(torch.autograd.Function):
+    """Both pre-training heads and their losses: sparse masked-LM head + CE and pooler + NSP head
+    + CE, returning mlm_loss + nsp_loss (reference bert_modeling.py:875-888).
+
+    MLM: exact w.r.t. the dense reference -- rows with label -1 contribute neither loss nor
+    gradient, so only the (at most ``cap``) labelled rows go through the transform, the tied
+    decoder GEMM and the CE.  Pooler/NSP (K08, pool_nsp.hip): first-token rows read in place,
+    fp32 whatever the compute dtype, the final sum done in the NSP loss kernel; its input gradient
+    is added straight into the first-token rows of the MLM path's sequence gradient."""
 
     @staticmethod
-    def forward(ctx, seq, labels, meta, wt, bt, g, b, wdec, bdec):
+    def forward(ctx, seq, labels, nsp_labels, meta, wt, bt, g, b, wdec, bdec, wp, bp, wn, bn):
         T, H = seq.shape
+        B, S = meta["B"], meta["S"]
+        assert T == B * S and H % 4 == 0 and nsp_labels.dtype == torch.int64 and nsp_labels.numel() == B
         cap, eps = meta["cap"], meta["eps"]
         Wt, Wd = meta["weights"]()
         idx, lab, cnt = mlm_compact(labels.reshape(-1), cap)
@@ -496,24 +504,37 @@ class FusedMLMLoss(torch.autograd.Function):
         else:
             logits, lbuf = G.gemm(t2, Wd, tb=True, bias=bdec, epi=1, out_dtype=torch.float32), None
         out, lse = xent_fwd(logits, lab)
+        # pooler + NSP + CE; total = out[0] + nsp mean loss
+        dev = seq.device
+        pooled = torch.empty((B, H), dtype=torch.float32, device=dev)
+        nsp_small = torch.empty((B, 4), dtype=torch.float32, device=dev)  # [:, :2] logits, [:, 2] lse
+        stats = torch.empty(3, dtype=torch.float32, device=dev)  # count, nsp loss, total
+        nsp_logits, nsp_lse = nsp_small[:, :2].contiguous(), nsp_small[:, 2].contiguous()
+        hip().pool_nsp_fwd(dtype_code(seq), seq.data_ptr(), B, S, H, wp.data_ptr(), bp.data_ptr(), wn.data_ptr(),
+                           bn.data_ptr(), nsp_labels.data_ptr(), out.data_ptr(), pooled.data_ptr(),
+                           nsp_logits.data_ptr(), nsp_lse.data_ptr(), stats.data_ptr(), stats[2:].data_ptr(),
+                           stream_handle())
         ctx.padded = lbuf is not None
         ctx.save_for_backward(idx, lab, hsel, t1pre, t1, z, mean, rstd, t2, lbuf if lbuf is not None else logits, lse,
-                              out, g, bt)
+                              out, g, bt, seq, nsp_labels, pooled, nsp_logits, nsp_lse, stats, wp, wn)
         ctx.meta = meta
         ctx.T = T
-        return out[0]
+        return stats[2]
 
     @staticmethod
     def backward(ctx, dloss):
-        idx, lab, hsel, t1pre, t1, z, mean, rstd, t2, logits, lse, out, g, bt = ctx.saved_tensors
+        (idx, lab, hsel, t1pre, t1, z, mean, rstd, t2, logits, lse, out, g, bt, seq, nsp_labels, pooled, nsp_logits,
+         nsp_lse, stats, wp, wn) = ctx.saved_tensors
+        meta = ctx.meta
         lbuf = None
         if ctx.padded:  # zero-padded [R, pad512(V)] buffer: the loss works on its [:, :V] view
-            lbuf, logits = logits, logits[:, :ctx.meta["weights"]()[1].shape[0]]
-        Wt, Wd = ctx.meta["weights"]()
-        sink = ctx.meta.get("grad_sink")
-        Gv = sink() if sink is not None else None  # (wt, bt, g, b, wdec, bdec) flat-store views
+            lbuf, logits = logits, logits[:, :meta["weights"]()[1].shape[0]]
+        Wt, Wd = meta["weights"]()
+        sink = meta.get("grad_sink")
+        Gv = sink() if sink is not None else None  # (wt, bt, g, b, wdec, bdec, wp, bp, wn, bn) flat-store views
         acc = Gv is not None
-        dlogits = xent_bwd_(logits, lab, lse, dloss.reshape(1).float().contiguous(), out)  # in place, fp32
+        dloss = dloss.reshape(1).float().contiguous()
+        dlogits = xent_bwd_(logits, lab, lse, dloss, out)  # in place, fp32
         # tied decoder weight: accumulates into the word-embedding gradient
         # bf16 mode: both decoder GEMMs take bf16 operands (fp32 C for the weight gradient);
         # the fp32-operand weight GEMM cost 268 us vs 72 us (tools/bench_mlm_head.py)
@@ -529,6 +550,7 @@ class FusedMLMLoss(torch.autograd.Function):
         else:
             def dwdec():
                 return G.linear_wgrad(dl_c, t2, out=Gv[4] if acc else None, accumulate=acc)
+
         def dbias():
             if lbuf is None:
                 return colsum(dlogits, acc=Gv[5] if acc else None)
@@ -553,6 +575,24 @@ class FusedMLMLoss(torch.autograd.Function):
         dseq = torch.zeros((ctx.T, hsel.shape[1]), dtype=hsel.dtype, device=hsel.device)
         hip().scatter_add_rows(dtype_code(dseq), dhsel.data_ptr(), idx.data_ptr(), dseq.data_ptr(), idx.numel(),
                                hsel.shape[1], stream_handle())
+        # pooler / NSP: input gradient added into dseq's first-token rows; parameter gradients
+        # written (or accumulated into the flat store) by the deterministic column kernel
+        B, S, H = meta["B"], meta["S"], seq.shape[1]
+        dev = seq.device
         if acc:
-            return dseq, None, None, None, None, None, None, None, None
-        return dseq, None, None, dWt, dbt, dg, db, dWdec, dbdec
+            dWp, dbp, dWn, dbn = Gv[6], Gv[7], Gv[8], Gv[9]
+        else:
+            dWp = torch.empty((H, H), dtype=torch.float32, device=dev)
+            dbp = torch.empty(H, dtype=torch.float32, device=dev)
+            dWn = torch.empty((2, H), dtype=torch.float32, device=dev)
+            dbn = torch.empty(2, dtype=torch.float32, device=dev)
+        dpre = torch.empty((B, H), dtype=torch.float32, device=dev)
+        dnsp = torch.empty((B, 2), dtype=torch.float32, device=dev)
+        hip().pool_nsp_bwd(dtype_code(seq), dloss.data_ptr(), seq.data_ptr(), dseq.data_ptr(), B, S, H,
+                           wp.data_ptr(), wn.data_ptr(), nsp_labels.data_ptr(), pooled.data_ptr(),
+                           nsp_logits.data_ptr(), nsp_lse.data_ptr(), stats.data_ptr(), dnsp.data_ptr(),
+                           dpre.data_ptr(), dWp.data_ptr(), dbp.data_ptr(), dWn.data_ptr(), dbn.data_ptr(), int(acc),
+                           stream_handle())
+        if acc:
+            return (dseq,) + (None,) * 13
+        return (dseq, None, None, None, dWt, dbt, dg, db, dWdec, dbdec, dWp, dbp, dWn, dbn)
