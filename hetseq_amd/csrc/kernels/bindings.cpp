@@ -106,11 +106,13 @@ PYBIND11_MODULE(_hip, m) {
   m.attr("arch") = "gfx950";
 
   m.def("grad_norm", [](i64 g, i64 n, i64 partial, i64 scale, float max_norm, i64 out, i64 st) {
+    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
     launch_grad_norm(P(const float*, g), n, P(double*, partial), P(const float*, scale), max_norm, P(float*, out), ST(st));
     check_launch("grad_norm");
   });
   m.def("adam_flat", [](i64 p, i64 g, i64 mm, i64 v, i64 shadow, i64 n, i64 gmul, float lr, float b1, float b2,
                         float eps, float wd, float step_size, i64 st, i64 hyper) {
+    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
     launch_adam_flat(P(float*, p), P(const float*, g), P(float*, mm), P(float*, v), P(void*, shadow), n,
                      P(const float*, gmul), lr, b1, b2, eps, wd, step_size, P(const float*, hyper), ST(st));
     check_launch("adam_flat");
@@ -120,18 +122,21 @@ PYBIND11_MODULE(_hip, m) {
      pybind11::arg("hyper") = 0);
   m.def("adadelta_flat", [](i64 p, i64 g, i64 sq, i64 acc, i64 shadow, i64 n, i64 gmul, float lr, float rho, float eps,
                             float wd, i64 st) {
+    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
     launch_adadelta_flat(P(float*, p), P(const float*, g), P(float*, sq), P(float*, acc), P(void*, shadow), n,
                          P(const float*, gmul), lr, rho, eps, wd, ST(st));
     check_launch("adadelta_flat");
   });
   m.def("lamb_flat", [](i64 p, i64 g, i64 mm, i64 v, i64 upd, i64 shadow, i64 seg_off, int nseg, i64 seg_norms, i64 gmul,
                         float lr, float b1, float b2, float eps, float wd, float bc1, float bc2, i64 st) {
+    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
     launch_lamb_flat(P(float*, p), P(const float*, g), P(float*, mm), P(float*, v), P(float*, upd), P(void*, shadow),
                      P(const int64_t*, seg_off), nseg, P(float*, seg_norms), P(const float*, gmul), lr, b1, b2, eps, wd,
                      bc1, bc2, ST(st));
     check_launch("lamb_flat");
   });
   m.def("cast_f32_bf16", [](i64 x, i64 y, i64 n, i64 st) {
+    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
     launch_cast_f32_bf16(P(const float*, x), P(void*, y), n, ST(st));
     check_launch("cast_f32_bf16");
   });
@@ -139,6 +144,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("ln_bwd_num_blocks", &ln_bwd_num_blocks);
   m.def("ln_fwd", [](int dt, i64 a, i64 bias, i64 resid, i64 gamma, i64 beta, i64 y, i64 zsave, i64 mean, i64 rstd,
                      int rows, int H, float eps, float p, u64 seed, u64 off, int mode, i64 st) {
+    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
     check(launch_ln_fwd(dt, P(const void*, a), P(const float*, bias), P(const void*, resid), P(const float*, gamma),
                         P(const float*, beta), P(void*, y), P(float*, zsave), P(float*, mean), P(float*, rstd), rows, H,
                         eps, p, seed, off, mode, ST(st)),
@@ -146,6 +152,7 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("ln_bwd", [](int dt, i64 dy, i64 zsave, i64 mean, i64 rstd, i64 gamma, i64 dz, i64 da, i64 pg, i64 pb, i64 pbias,
                      int rows, int H, float p, u64 seed, u64 off, int mode, i64 st) {
+    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
     check(launch_ln_bwd(dt, P(const void*, dy), P(const float*, zsave), P(const float*, mean), P(const float*, rstd),
                         P(const float*, gamma), P(void*, dz), P(void*, da), P(float*, pg), P(float*, pb),
                         P(float*, pbias), rows, H, p, seed, off, mode, ST(st)),
@@ -154,6 +161,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("emb_fwd", [](int dt, i64 ids, i64 tt, i64 w, i64 pe, i64 te, i64 gamma, i64 beta, i64 y, i64 zsave, i64 mean,
                       i64 rstd, int rows, int S, int H, int V, int TV, float eps, float p, u64 seed, u64 off, i64 err,
                       i64 st) {
+    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
     check(launch_emb_fwd(dt, P(const int64_t*, ids), P(const int64_t*, tt), P(const float*, w), P(const float*, pe),
                          P(const float*, te), P(const float*, gamma), P(const float*, beta), P(void*, y),
                          P(float*, zsave), P(float*, mean), P(float*, rstd), rows, S, H, V, TV, eps, p, seed, off,
@@ -162,20 +170,24 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("emb_bwd", [](int dt, i64 dy, i64 zsave, i64 mean, i64 rstd, i64 gamma, i64 dx, i64 pg, i64 pb, i64 tt, i64 pt,
                       int rows, int H, float p, u64 seed, u64 off, i64 st) {
+    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
     check(launch_emb_bwd(dt, P(const void*, dy), P(const float*, zsave), P(const float*, mean), P(const float*, rstd),
                          P(const float*, gamma), P(float*, dx), P(float*, pg), P(float*, pb), P(const int64_t*, tt),
                          P(float*, pt), rows, H, p, seed, off, ST(st)),
           "emb_bwd");
   });
   m.def("segsum_rows", [](i64 src, i64 order, i64 keys, i64 scratch, i64 dst, int n, int H, int K, i64 st) {
+    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
     check(launch_segsum_rows(P(const float*, src), P(const int64_t*, order), P(const int64_t*, keys),
                              P(float*, scratch), P(float*, dst), n, H, K, ST(st)),
           "segsum_rows");
   });
   m.def("pos_grad", [](i64 dx, i64 dpos, int B, int S, int H, i64 st) {
+    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
     check(launch_pos_grad(P(const float*, dx), P(float*, dpos), B, S, H, ST(st)), "pos_grad");
   });
   m.def("colpart_finalize", [](py::list parts, py::list outs, int nparts, int H, int accumulate, i64 st) {
+    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
     const int n = static_cast<int>(parts.size());
     if (n < 1 || n > 3 || outs.size() != parts.size()) throw std::invalid_argument("colpart_finalize: 1..3 pairs");
     const float* pp[3];
@@ -189,11 +201,13 @@ PYBIND11_MODULE(_hip, m) {
   });
 
   m.def("bias_gelu_fwd", [](int dt, i64 x, i64 b, i64 y, i64 rows, int N, i64 st) {
+    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
     launch_bias_gelu_fwd(dt, P(const void*, x), P(const float*, b), P(void*, y), rows, N, ST(st));
     check_launch("bias_gelu_fwd");
   });
   m.def("pool_nsp_fwd", [](int dt, i64 seq, int B, int S, int H, i64 Wp, i64 bp, i64 Wn, i64 bn, i64 label,
                            i64 mlm_loss, i64 pooled, i64 logits, i64 lse, i64 stats, i64 total, i64 st) {
+    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
     check(launch_pool_nsp_fwd(dt, P(const void*, seq), B, S, H, P(const float*, Wp), P(const float*, bp),
                               P(const float*, Wn), P(const float*, bn), P(const int64_t*, label),
                               P(const float*, mlm_loss), P(float*, pooled), P(float*, logits), P(float*, lse),
@@ -203,6 +217,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("pool_nsp_bwd", [](int dt, i64 dloss, i64 seq, i64 dseq, int B, int S, int H, i64 Wp, i64 Wn, i64 label,
                            i64 pooled, i64 logits, i64 lse, i64 stats, i64 dlogits, i64 dpre, i64 dWp, i64 dbp,
                            i64 dWn, i64 dbn, int accumulate, i64 st) {
+    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
     check(launch_pool_nsp_bwd(dt, P(const float*, dloss), P(const void*, seq), P(void*, dseq), B, S, H,
                               P(const float*, Wp), P(const float*, Wn), P(const int64_t*, label),
                               P(const float*, pooled), P(const float*, logits), P(const float*, lse),
@@ -212,20 +227,24 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("colsum_row_chunks", &colsum_row_chunks);
   m.def("colsum", [](int dt, i64 dy, i64 x, i64 b, i64 dx, i64 part, i64 out, i64 rows, int N, int accumulate, i64 st) {
+    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
     launch_colsum(dt, P(const void*, dy), P(const void*, x), P(const float*, b), P(void*, dx), P(float*, part),
                   P(float*, out), rows, N, accumulate, ST(st));
     check_launch("colsum");
   });
   m.def("mlm_compact", [](i64 labels, int rows, int ignore, int cap, i64 idx, i64 lab_out, i64 count, i64 err, i64 st) {
+    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
     launch_mlm_compact(P(const int64_t*, labels), rows, ignore, cap, P(int32_t*, idx), P(int64_t*, lab_out),
                        P(int32_t*, count), P(int*, err), ST(st));
     check_launch("mlm_compact");
   });
   m.def("gather_rows", [](int dt, i64 src, i64 idx, i64 out, int n, int H, i64 st) {
+    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
     launch_gather_rows(dt, P(const void*, src), P(const int32_t*, idx), P(void*, out), n, H, ST(st));
     check_launch("gather_rows");
   });
   m.def("scatter_add_rows", [](int dt, i64 src, i64 idx, i64 dst, int n, int H, i64 st) {
+    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
     launch_scatter_add_rows(dt, P(const void*, src), P(const int32_t*, idx), P(void*, dst), n, H, ST(st));
     check_launch("scatter_add_rows");
   });
@@ -234,12 +253,14 @@ PYBIND11_MODULE(_hip, m) {
   m.def("attn_fp32_mode", &attn_fp32_mode);
   m.def("attn_fwd", [](int dt, i64 qkv, i64 mask, i64 bqkv, i64 ctx, i64 lse, i64 dmask, int B, int S, int NH, int D,
                        float p, u64 seed, u64 off, i64 st) {
+    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
     check(launch_attn_fwd(dt, P(const void*, qkv), P(const int64_t*, mask), P(const float*, bqkv), P(void*, ctx),
                           P(float*, lse), P(uint32_t*, dmask), B, S, NH, D, p, seed, off, ST(st)),
           "attn_fwd");
   });
   m.def("attn_bwd", [](int dt, i64 qkv, i64 mask, i64 bqkv, i64 ctx, i64 dctx, i64 lse, i64 dbuf, i64 dqkv, i64 dmask,
                        int B, int S, int NH, int D, float p, i64 st) {
+    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
     check(launch_attn_bwd(dt, P(const void*, qkv), P(const int64_t*, mask), P(const float*, bqkv),
                           P(const void*, ctx), P(const void*, dctx), P(const float*, lse), P(float*, dbuf),
                           P(void*, dqkv), P(const uint32_t*, dmask), B, S, NH, D, p, ST(st)),
@@ -248,12 +269,14 @@ PYBIND11_MODULE(_hip, m) {
 
   m.def("xent_fwd", [](int dt, i64 logits, i64 labels, int rows, int V, i64 ldv, int ignore, i64 row_loss, i64 lse,
                        i64 out, i64 st) {
+    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
     launch_xent_fwd(dt, P(const void*, logits), P(const int64_t*, labels), rows, V, ldv, ignore, P(float*, row_loss),
                     P(float*, lse), P(float*, out), ST(st));
     check_launch("xent_fwd");
   });
   m.def("xent_bwd", [](int dt, i64 logits, i64 labels, i64 lse, int rows, int V, i64 ldv, int ignore, i64 dloss,
                        i64 stats, i64 st) {
+    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
     launch_xent_bwd(dt, P(void*, logits), P(const int64_t*, labels), P(const float*, lse), rows, V, ldv, ignore,
                     P(const float*, dloss), P(const float*, stats), ST(st));
     check_launch("xent_bwd");
@@ -265,6 +288,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("gemm", [](int dt, int ta, int tb, int M, int N, int K, i64 A, i64 lda, i64 B, i64 ldb, i64 C, i64 ldc, i64 bias,
                    int epi, float beta, i64 aux, i64 ldaux, i64 part, i64 colsum, int colsum_acc, i64 st,
                    int tile, int ksplit, i64 slab, i64 slab_floats, int mv, int nv, int kv) {
+    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
     const int rc = launch_gemm(dt, ta, tb, M, N, K, P(const void*, A), lda, P(const void*, B), ldb, P(void*, C), ldc,
                                P(const float*, bias), epi, beta, P(float*, aux), ldaux, P(float*, part),
                                P(float*, colsum), colsum_acc, tile, ST(st), ksplit, P(float*, slab), slab_floats, mv, nv,
