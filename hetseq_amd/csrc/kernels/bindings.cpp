@@ -71,6 +71,14 @@ int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, i
                 float* part, float* colsum_out, int colsum_acc, int tile_override, hipStream_t st, int ksplit,
                 float* slab, int64_t slab_floats, int mv, int nv, int kv);
 
+// gemm_planes.hip
+int launch_gemm_planes(int planes, int c_dtype, int ta, int tb, int M, int N, int K, const void* A, int64_t lda,
+                       int64_t a_ps, const void* B, int64_t ldb, int64_t b_ps, void* C, int64_t ldc,
+                       const float* bias, int epi, float beta, void* aux, int64_t ldaux, float* part,
+                       float* colsum_out, int colsum_acc, int ksplit, float* slab, int64_t slab_floats,
+                       hipStream_t st);
+void launch_split_planes(const float* x, void* out, int64_t n, int64_t ps, hipStream_t st);
+
 // HIP-graph mode: device word holding the dropout seed (see common.h resolve_seed)
 namespace hs {
 const uint64_t* g_seed_dev = nullptr;
@@ -204,6 +212,24 @@ PYBIND11_MODULE(_hip, m) {
     (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
     launch_bias_gelu_fwd(dt, P(const void*, x), P(const float*, b), P(void*, y), rows, N, ST(st));
     check_launch("bias_gelu_fwd");
+  });
+  m.def("gemm_planes", [](int planes, int c_dtype, int ta, int tb, int M, int N, int K, i64 A, i64 lda, i64 a_ps,
+                          i64 B, i64 ldb, i64 b_ps, i64 C, i64 ldc, i64 bias, int epi, float beta, i64 aux,
+                          i64 ldaux, i64 part, i64 colsum, int colsum_acc, int ksplit, i64 slab, i64 slab_floats,
+                          i64 st) {
+    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
+    const int rc = launch_gemm_planes(planes, c_dtype, ta, tb, M, N, K, P(const void*, A), lda, a_ps,
+                                      P(const void*, B), ldb, b_ps, P(void*, C), ldc, P(const float*, bias), epi,
+                                      beta, P(void*, aux), ldaux, P(float*, part), P(float*, colsum), colsum_acc,
+                                      ksplit, P(float*, slab), slab_floats, ST(st));
+    if (rc == 0) check_launch("gemm_planes");
+    return rc;
+  });
+  m.def("split_planes", [](i64 x, i64 out, i64 n, i64 ps, i64 st) {
+    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
+    if (n % 4 || ps % 4) throw std::invalid_argument("split_planes: n and the plane stride must be multiples of 4");
+    launch_split_planes(P(const float*, x), P(void*, out), n, ps, ST(st));
+    check_launch("split_planes");
   });
   m.def("pool_nsp_fwd", [](int dt, i64 seq, int B, int S, int H, i64 Wp, i64 bp, i64 Wn, i64 bn, i64 label,
                            i64 mlm_loss, i64 pooled, i64 logits, i64 lse, i64 stats, i64 total, i64 st) {

@@ -676,6 +676,13 @@ int launch_split(int tile, int ta, int tb, int epi, const GemmArgs& a, hipStream
 
 using namespace hs;
 
+void launch_splitk_reduce(const float* slab, int ksplit, int M, int N, float* C, int64_t ldc, const float* bias,
+                          float beta, int Mv, int Nv, hipStream_t st) {
+  const int64_t n4 = (int64_t)Mv * (N / 4);
+  const int grid = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid), dim3(256), 0, st, slab, ksplit, M, N, C, ldc, bias, beta, Mv, Nv);
+}
+
 // Tile choice: the largest tile that still gives >= 2 blocks per CU (256 CUs).
 static int pick_tile(int M, int N) {
   if (M % 128 == 0 && N % 128 == 0 && (M / 128) * (N / 128) >= 512) return 0;
@@ -753,12 +760,7 @@ int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, i
   else
     rc = launch_split<0>(tile, ta, tb, epi, a, st);
   if (rc != 0) return rc;
-  if (ks > 1) {
-    const int64_t n4 = (int64_t)M * (N / 4);
-    const int grid = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid), dim3(256), 0, st, slab, ks, M, N, static_cast<float*>(C), ldc,
-                       epi >= 1 ? bias : nullptr, beta, a.Mv, a.Nv);
-  }
+  if (ks > 1) launch_splitk_reduce(slab, ks, M, N, static_cast<float*>(C), ldc, epi >= 1 ? bias : nullptr, beta, a.Mv, a.Nv, st);
   if (epi == kEpiDGelu) {
     const int bm = tile == 2 ? 64 : 128;
     const float* parts[1] = {part};

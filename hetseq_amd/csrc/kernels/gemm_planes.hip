@@ -1,0 +1,393 @@
+// bf16-plane MFMA GEMM: the engine behind both precision modes (K01/K03/K04 GEMM parts).
+//
+//   C[M,N] = beta*C + op(A)[M,K] * op(B)[K,N]  (+ bias / GELU / dGELU epilogue)
+//
+// Operands arrive as P bf16 "planes" of the same shape (plane stride ps elements):
+//   P = 1  --dtype bf16: the bf16 activation / weight shadow itself, one product;
+//   P = 3  fp32 (the reference's precision) as split-bf16: x = hi + mid + lo + r,
+//          |r| <= 2^-27 |x| (RNE each time), and a*b summed from the six cross
+//          terms of order <= 2^-16 (lo*hi, hi*lo, mid*mid, mid*hi, hi*mid, hi*hi,
+//          smallest first).  Every bf16 x bf16 product is exact in the fp32
+//          accumulator, so the result carries fp32-level error.
+// The planes are produced ONCE per tensor (split_planes_kernel below, or the
+// optimizer for the weights), not once per GEMM block as in gemm_x6s_kernel
+// (gemm.hip), whose in-block splitting VALU work co-issued with -- and capped --
+// its MFMAs.  Here the K loop is pure data movement + MFMA:
+//
+//  * tiles of 128x128, 4 waves (2x2, 64x64 each = 2x2 v_mfma_f32_32x32x16_bf16
+//    accumulators), BK = 32 (P = 3) or 64 (P = 1);
+//  * both operand layouts are served from LDS without any transpose pass:
+//      k-contiguous source (A for TA=0, B for TB=1): image [128 rows][BK] read with
+//        ds_read_b128, 16-B chunks XOR-swizzled by row (conflict-free for the
+//        32x32x16 operand map);
+//      mn-contiguous source (TA=1 / TB=0: the dgrad weight and both weight-gradient
+//        operands): image [BK rows][128] read with ds_read_b64_tr_b16 (the gfx950
+//        transposing LDS read: 4 k-rows of 16 columns per 16-lane group), chunks
+//        XOR-swizzled by 4*(row & 3) (conflict-free per 32-lane half);
+//  * staging is global_load_lds_dwordx4 (LDS-DMA, no VGPR round trip): the LDS image
+//    is written lane-linearly, so the swizzle lives in each lane's SOURCE address;
+//    two LDS stages, the next K tile in flight under the current tile's MFMAs, one
+//    vmcnt(0) + barrier per K tile, all LDS in one __shared__ array;
+//  * block ids are remapped XCD-contiguously (bijective for any grid) and grouped
+//    8 M-tiles x all N-tiles so an XCD's resident blocks share operand panels in
+//    its private L2;
+//  * optional split-K into fp32 slabs (summed in fixed order by splitk_reduce_kernel
+//    in gemm.hip) for the K = 4096 weight gradients whose tile grids are small.
+// Epilogue (shared by both P): C in fp32 or bf16, + bias, beta-accumulate, GELU
+// (pre-activation kept in aux), dGELU with per-block column partials of the bias
+// gradient (finalised by reduce_rows).
+#include <algorithm>
+
+#include "common.h"
+#include "reduce.h"
+
+namespace hs {
+
+typedef __bf16 pbf8 __attribute__((ext_vector_type(8)));
+typedef short ps4 __attribute__((ext_vector_type(4)));
+typedef float pf16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_void_t;
+
+enum { kPEpiNone = 0, kPEpiBias = 1, kPEpiGelu = 2, kPEpiDGelu = 3 };
+constexpr int kPB = 128;  // block tile (rows and columns)
+
+struct PlanesArgs {
+  const uint16_t* A;  // plane 0 of op(A)'s storage; plane p at A + p * a_ps
+  const uint16_t* B;
+  void* C;
+  const float* bias;
+  void* aux;    // kEpiGelu: pre-activation out; kEpiDGelu: pre-activation in (same dtype as C)
+  float* part;  // kEpiDGelu: [M/128][N] column partial sums
+  float* slab;  // split-K: [ksplit][M][N] fp32 partial products
+  int64_t lda, ldb, ldc, ldaux, a_ps, b_ps;
+  int M, N, K, ksplit;
+  float beta;
+};
+
+// LDS image geometry of one operand plane (128 x BK bf16 elements either way).
+template <int BK, bool KCONTIG>
+struct PImg {
+  static constexpr int bytes = kPB * BK * 2;
+  static constexpr int row_bytes = KCONTIG ? BK * 2 : kPB * 2;  // 64 / 128 or 256
+  static constexpr int chunks = row_bytes / 16;                 // 16-B chunks per row
+  // chunk swizzle of row r: k-contiguous rows spread the b128 row reads of 16 lanes over
+  // all 16 bank quads; mn-contiguous (256-B) rows put the 4 k-rows of a transposed read
+  // into 4 different quarters of the bank row
+  HS_DEVICE static int swz(int r) {
+    if (KCONTIG) return (r >> (row_bytes == 64 ? 2 : 1)) & (chunks - 1);
+    return 4 * (r & 3);
+  }
+};
+
+// Per-lane source byte offsets (from the plane-0 base at k = 0) of this wave's LDS-DMA
+// instructions for one operand: instruction j writes image bytes [1024 * (4 j + w), +1024)
+// of the operand's P planes.
+template <int BK, bool KCONTIG, int NJ>
+HS_DEVICE void dma_offsets(uint32_t* off, int64_t ld, int64_t ps, int mn0, int w, int lane) {
+  using I = PImg<BK, KCONTIG>;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int byte = 1024 * (4 * j + w) + 16 * lane;
+    const int plane = byte / I::bytes, ib = byte % I::bytes;
+    const int row = ib / I::row_bytes, cl = (ib % I::row_bytes) / 16;
+    const int gc = cl ^ I::swz(row);  // the chunk this LDS position holds
+    const int64_t e = KCONTIG ? (int64_t)(mn0 + row) * ld + 8 * gc   // [mn][k]: row = mn, chunk = 8 k
+                              : (int64_t)row * ld + mn0 + 8 * gc;    // [k][mn]: row = k, chunk = 8 mn
+    off[j] = static_cast<uint32_t>(2 * (e + plane * ps));
+  }
+}
+
+template <int NJ>
+HS_DEVICE void dma_issue(const char* base, const uint32_t* off, char* img, int w) {
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+    __builtin_amdgcn_global_load_lds((gbl_void_t*)(base + off[j]), (lds_void_t*)(img + 1024 * (4 * j + w)), 16, 0, 0);
+}
+
+// MFMA operand (8 consecutive k of one row / column) of plane p for the 32-wide tile at
+// `rc` (row of op(A) or column of op(B)), k-slice ks of the stage.
+template <int BK, bool KCONTIG>
+HS_DEVICE pbf8 frag(const char* img, int p, int rc, int ks, int lane) {
+  using I = PImg<BK, KCONTIG>;
+  const char* pl = img + p * I::bytes;
+  if (KCONTIG) {
+    const int r = rc + (lane & 31), c = 2 * ks + (lane >> 5);
+    return *reinterpret_cast<const pbf8*>(pl + r * I::row_bytes + 16 * (c ^ I::swz(r)));
+  } else {
+    // transposed read: lane 4q+p' of a 16-lane group addresses k-row k0+q, columns c0+4p'..+3
+    const int l16 = lane & 15, q = l16 >> 2, pp = l16 & 3, g = lane >> 4;
+    const int col = rc + 16 * (g & 1) + 4 * pp;
+    ps4 v[2];
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int row = 16 * ks + 8 * (g >> 1) + 4 * jj + q;
+      const char* a = pl + row * I::row_bytes + 16 * ((col >> 3) ^ I::swz(row)) + 2 * (col & 7);
+      v[jj] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) ps4*)(a));
+    }
+    typedef short ps8 __attribute__((ext_vector_type(8)));
+    const ps8 u = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w};
+    return __builtin_bit_cast(pbf8, u);
+  }
+}
+
+HS_DEVICE pf16 mma16(pbf8 a, pbf8 b, pf16 c) { return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0); }
+HS_DEVICE int acc_row(int r, int q) { return (r & 3) + 8 * (r >> 2) + 4 * q; }
+
+HS_DEVICE void store_c(float* p, float v) { *p = v; }
+HS_DEVICE void store_c(bf16_t* p, float v) { *p = from_f<bf16_t>(v); }
+HS_DEVICE float load_c(const float* p) { return *p; }
+HS_DEVICE float load_c(const bf16_t* p) { return to_f(*p); }
+template <typename TC>
+HS_DEVICE float round_c(float v) { return to_f(from_f<TC>(v)); }
+
+template <int P, int BK, bool TA, bool TB, int EPI, typename TC>
+__global__ void __launch_bounds__(256) gemm_planes_kernel(PlanesArgs p) {
+  constexpr bool AK = !TA, BKc = TB;  // k-contiguous storage?
+  using IA = PImg<BK, AK>;
+  using IB = PImg<BK, BKc>;
+  constexpr int STAGE = P * (IA::bytes + IB::bytes);
+  constexpr int NA = P * IA::bytes / 4096, NB = P * IB::bytes / 4096;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+  const int tiles_m = p.M / kPB, tiles_n = p.N / kPB, nwg = tiles_m * tiles_n * p.ksplit;
+  const int orig = blockIdx.x;
+  const int xcd = orig % 8, qq = nwg / 8, rr = nwg % 8;
+  const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + orig / 8;
+  const int slice = wg % p.ksplit, tile = wg / p.ksplit;
+  const int gsz = 8 * tiles_n, grp = tile / gsz, gm = min(8, tiles_m - 8 * grp);
+  const int tm = 8 * grp + (tile % gsz) % gm, tn = (tile % gsz) / gm;
+  const int m0 = tm * kPB, n0 = tn * kPB;
+  const int kofs = slice * (p.K / p.ksplit);
+  const int KT = p.K / p.ksplit / BK;
+
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = w >> 1, wc = w & 1, wm = 64 * wr, wn = 64 * wc;
+
+  uint32_t offA[NA], offB[NB];
+  dma_offsets<BK, AK, NA>(offA, p.lda, p.a_ps, m0, w, lane);
+  dma_offsets<BK, BKc, NB>(offB, p.ldb, p.b_ps, n0, w, lane);
+  // K-tile advance of the (wave-uniform) source bases, in bytes
+  const int64_t stepA = AK ? 2 * BK : 2 * (int64_t)BK * p.lda, stepB = BKc ? 2 * BK : 2 * (int64_t)BK * p.ldb;
+  const char* ga = reinterpret_cast<const char*>(p.A) + (AK ? 2 * (int64_t)kofs : 2 * (int64_t)kofs * p.lda);
+  const char* gb = reinterpret_cast<const char*>(p.B) + (BKc ? 2 * (int64_t)kofs : 2 * (int64_t)kofs * p.ldb);
+
+  pf16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = pf16{};
+
+  // product terms (plane of A, plane of B), smallest first
+  constexpr int NTERM = P == 3 ? 6 : 1;
+  constexpr int TA_[6] = {2, 0, 1, 1, 0, 0}, TB_[6] = {0, 2, 1, 0, 1, 0};
+  constexpr int T0 = P == 3 ? 0 : 5;
+
+  // One wave per SIMD (the x6 image needs 96 KB of LDS): the fragment reads of k-slice ks+1 are
+  // issued before the MFMAs of slice ks, and the next tile's first slice right after the
+  // barrier that publishes its DMA, so LDS latency hides under MFMAs.
+  constexpr int NKS = BK / 16;
+  struct Frags {
+    pbf8 a[P][2], b[P][2];
+  };
+  auto read = [&](Frags& f, const char* stage, int ks) {
+#pragma unroll
+    for (int pl = 0; pl < P; ++pl)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        f.a[pl][i] = frag<BK, AK>(stage, pl, wm + 32 * i, ks, lane);
+        f.b[pl][i] = frag<BK, BKc>(stage + P * IA::bytes, pl, wn + 32 * i, ks, lane);
+      }
+  };
+  auto mma = [&](const Frags& f) {
+#pragma unroll
+    for (int tt = T0; tt < T0 + NTERM; ++tt)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mma16(f.a[TA_[tt]][i], f.b[TB_[tt]][j], acc[i][j]);
+  };
+
+  dma_issue<NA>(ga, offA, smem, w);
+  dma_issue<NB>(gb, offB, smem + P * IA::bytes, w);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  Frags f[2];
+  read(f[0], smem, 0);
+  for (int t = 0; t < KT; ++t) {
+    const char* cur = smem + (t & 1) * STAGE;
+    char* nxt = smem + ((t + 1) & 1) * STAGE;
+    if (t + 1 < KT) {  // the other stage was last read before the previous barrier
+      dma_issue<NA>(ga + (t + 1) * stepA, offA, nxt, w);
+      dma_issue<NB>(gb + (t + 1) * stepB, offB, nxt + P * IA::bytes, w);
+    }
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      if (ks + 1 < NKS) {
+        read(f[(ks + 1) & 1], cur, ks + 1);
+        mma(f[ks & 1]);
+      } else {
+        // keep the previous slice's MFMAs ahead of the barrier (the scheduler would sink them
+        // past it, exposing the last slice's LDS reads to the barrier's lgkmcnt(0))
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // tile t+1 landed in every wave's share; nobody reads tile t any more
+        if (t + 1 < KT) read(f[(ks + 1) & 1], nxt, 0);
+        mma(f[ks & 1]);
+      }
+    }
+  }
+
+  // ---------------- epilogue: register r of acc[i][j] -> row m0+wm+32i+acc_row(r,q), col n0+wn+32j+lr
+  const int lr = lane & 31, q = lane >> 5;
+  if (p.ksplit > 1) {  // plain fp32 partial slab; bias / beta / sum in splitk_reduce_kernel
+    float* sl = p.slab + (int64_t)slice * p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          sl[(int64_t)(m0 + wm + 32 * i + acc_row(r, q)) * p.N + n0 + wn + 32 * j + lr] = acc[i][j][r];
+    return;
+  }
+  TC* C = static_cast<TC*>(p.C);
+  TC* aux = static_cast<TC*>(p.aux);
+  float csum[2] = {0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = n0 + wn + 32 * j + lr;
+    const float bv = EPI != kPEpiNone ? p.bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t m = m0 + wm + 32 * i + acc_row(r, q);
+        const float a = acc[i][j][r];
+        if (EPI == kPEpiGelu) {  // GELU of the STORED pre-activation (what the backward will see)
+          store_c(aux + m * p.ldaux + n, a);
+          store_c(C + m * p.ldc + n, gelu_f(round_c<TC>(a) + bv));
+        } else if (EPI == kPEpiDGelu) {
+          const float v = a * gelu_grad_f(load_c(aux + m * p.ldaux + n) + bv);
+          csum[j] += v;
+          store_c(C + m * p.ldc + n, v);
+        } else if (p.beta != 0.f) {
+          store_c(C + m * p.ldc + n, a + bv + p.beta * load_c(C + m * p.ldc + n));
+        } else {
+          store_c(C + m * p.ldc + n, a + bv);
+        }
+      }
+    }
+  }
+  if (EPI == kPEpiDGelu) {  // column sums over the block's 128 rows: lane halves, then wave rows via LDS
+    float* red = reinterpret_cast<float*>(smem);  // the K loop ended with a barrier
+#pragma unroll
+    for (int j = 0; j < 2; ++j) csum[j] += __shfl_xor(csum[j], 32, 64);
+    if (wr == 1 && q == 0)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) red[wn + 32 * j + lr] = csum[j];
+    __syncthreads();
+    if (wr == 0 && q == 0)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int c = wn + 32 * j + lr;
+        p.part[(int64_t)tm * p.N + n0 + c] = csum[j] + red[c];
+      }
+  }
+}
+
+// fp32 -> three bf16 planes (hi, mid, lo), RNE at each step: out[p * n + i].
+__global__ void __launch_bounds__(256) split_planes_kernel(const float* __restrict__ x, uint16_t* __restrict__ out,
+                                                           int64_t n4, int64_t ps) {
+  typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const float4 v = reinterpret_cast<const float4*>(x)[i];
+    const f2 x0 = {v.x, v.y}, x1 = {v.z, v.w};
+    const b2 h0 = __builtin_convertvector(x0, b2), h1 = __builtin_convertvector(x1, b2);
+    const f2 r0 = x0 - __builtin_convertvector(h0, f2), r1 = x1 - __builtin_convertvector(h1, f2);
+    const b2 m0 = __builtin_convertvector(r0, b2), m1 = __builtin_convertvector(r1, b2);
+    const b2 l0 = __builtin_convertvector(r0 - __builtin_convertvector(m0, f2), b2);
+    const b2 l1 = __builtin_convertvector(r1 - __builtin_convertvector(m1, f2), b2);
+    uint2* o = reinterpret_cast<uint2*>(out);
+    o[i] = make_uint2(__builtin_bit_cast(uint32_t, h0), __builtin_bit_cast(uint32_t, h1));
+    o[i + ps / 4] = make_uint2(__builtin_bit_cast(uint32_t, m0), __builtin_bit_cast(uint32_t, m1));
+    o[i + ps / 2] = make_uint2(__builtin_bit_cast(uint32_t, l0), __builtin_bit_cast(uint32_t, l1));
+  }
+}
+
+template <int P, int BK, typename TC>
+int launch_planes_cfg(int ta, int tb, int epi, const PlanesArgs& a, hipStream_t st) {
+  const dim3 grid((a.M / kPB) * (a.N / kPB) * a.ksplit), blk(256);
+#define HS_PL(TA_, TB_, E_) hipLaunchKernelGGL((gemm_planes_kernel<P, BK, TA_, TB_, E_, TC>), grid, blk, 0, st, a)
+  if (!ta && tb) {  // forward X W^T
+    if (epi == kPEpiNone) HS_PL(false, true, kPEpiNone);
+    else if (epi == kPEpiBias) HS_PL(false, true, kPEpiBias);
+    else if (epi == kPEpiGelu) HS_PL(false, true, kPEpiGelu);
+    else return -1;
+  } else if (!ta && !tb) {  // dgrad dY W
+    if (epi == kPEpiNone) HS_PL(false, false, kPEpiNone);
+    else if (epi == kPEpiDGelu) HS_PL(false, false, kPEpiDGelu);
+    else return -1;
+  } else if (ta && !tb) {  // wgrad dY^T X
+    if (epi == kPEpiNone) HS_PL(true, false, kPEpiNone);
+    else return -1;
+  } else {
+    return -1;
+  }
+#undef HS_PL
+  return 0;
+}
+
+}  // namespace hs
+
+// gemm.hip: C = sum of the ksplit fp32 slabs (fixed order) (+ bias) (+ beta * C)
+void launch_splitk_reduce(const float* slab, int ksplit, int M, int N, float* C, int64_t ldc, const float* bias,
+                          float beta, int Mv, int Nv, hipStream_t st);
+
+using namespace hs;
+
+// planes: 1 (bf16) or 3 (split fp32); c_dtype: 0 fp32 C, 1 bf16 C.  Operand strides / plane
+// strides in elements.  Returns -1 (nothing launched) for shapes it does not serve: M, N
+// multiples of 128, K a multiple of BK * ksplit, 16-B aligned rows.
+int launch_gemm_planes(int planes, int c_dtype, int ta, int tb, int M, int N, int K, const void* A, int64_t lda,
+                       int64_t a_ps, const void* B, int64_t ldb, int64_t b_ps, void* C, int64_t ldc,
+                       const float* bias, int epi, float beta, void* aux, int64_t ldaux, float* part,
+                       float* colsum_out, int colsum_acc, int ksplit, float* slab, int64_t slab_floats,
+                       hipStream_t st) {
+  if (planes != 1 && planes != 3) return -1;
+  const int BK = planes == 3 ? 32 : 64;
+  ksplit = std::max(1, ksplit);
+  if (M <= 0 || N <= 0 || K <= 0 || M % kPB || N % kPB || K % (BK * ksplit)) return -1;
+  auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  if (!al16(A) || !al16(B) || lda % 8 || ldb % 8 || (planes == 3 && (a_ps % 8 || b_ps % 8))) return -1;
+  if ((epi >= 1 && !bias) || (epi >= 2 && (!aux || beta != 0.f)) || (epi == 3 && (!part || !colsum_out))) return -1;
+  if (ksplit > 1 && (epi != 0 || c_dtype != 0 || !slab || (int64_t)ksplit * M * N > slab_floats || ldc % 4 || N % 4))
+    return -1;
+  // 32-bit per-lane DMA offsets: the operand span (all planes) must stay below 4 GiB
+  const int64_t spanA = 2 * ((planes - 1) * a_ps + (int64_t)(ta ? K : M) * lda);
+  const int64_t spanB = 2 * ((planes - 1) * b_ps + (int64_t)(tb ? N : K) * ldb);
+  if (spanA >= (1ll << 32) || spanB >= (1ll << 32)) return -1;
+  PlanesArgs a{static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), C, bias, aux, part, slab,
+               lda, ldb, ldc, ldaux, a_ps, b_ps, M, N, K, ksplit, beta};
+  int rc;
+  if (planes == 3)
+    rc = c_dtype ? launch_planes_cfg<3, 32, bf16_t>(ta, tb, epi, a, st) : launch_planes_cfg<3, 32, float>(ta, tb, epi, a, st);
+  else
+    rc = c_dtype ? launch_planes_cfg<1, 64, bf16_t>(ta, tb, epi, a, st) : launch_planes_cfg<1, 64, float>(ta, tb, epi, a, st);
+  if (rc) return rc;
+  if (ksplit > 1) launch_splitk_reduce(slab, ksplit, M, N, static_cast<float*>(C), ldc, nullptr, beta, M, N, st);
+  if (epi == kPEpiDGelu) {
+    const float* parts[1] = {part};
+    float* outs[1] = {colsum_out};
+    launch_reduce_rows(parts, outs, 1, M / kPB, N, colsum_acc, st);
+  }
+  return 0;
+}
+
+void launch_split_planes(const float* x, void* out, int64_t n, int64_t ps, hipStream_t st) {
+  const int64_t n4 = n / 4;
+  const int grid = (int)std::min<int64_t>((n4 + 255) / 256, 4096);
+  hipLaunchKernelGGL(split_planes_kernel, dim3(grid), dim3(256), 0, st, x, static_cast<uint16_t*>(out), n4, ps);
+}

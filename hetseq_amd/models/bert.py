@@ -382,6 +382,15 @@ class BertLayer(nn.Module):
         W.w1, W.bi = cw(self.intermediate.dense_act.weight), self.intermediate.dense_act.bias.detach()
         W.w2, W.b2 = cw(o.dense.weight), o.dense.bias.detach()
         W.g2, W.bb2 = o.LayerNorm.weight.detach(), o.LayerNorm.bias.detach()
+        W.planes = False
+        if not bf16 and store is not None and store.planes is not None:
+            # fp32 on the plane engine: GEMM weights as their split-bf16 planes (refreshed by the optimizer)
+            W.wqkv = store.planes_view(qkv, (3 * sa.all_head_size, H))
+            W.wo = store.planes_view([ao.dense.weight], tuple(ao.dense.weight.shape))
+            W.w1 = store.planes_view([self.intermediate.dense_act.weight],
+                                     tuple(self.intermediate.dense_act.weight.shape))
+            W.w2 = store.planes_view([o.dense.weight], tuple(o.dense.weight.shape))
+            W.planes = True
         return W
 
     def fused_ok(self, x, S):
@@ -586,6 +595,11 @@ class BertPreTrainedModel(nn.Module):
 
     # --- runtime plumbing (flat store / compute dtype / fused switch)
     def attach_store(self, store, compute_dtype=torch.float32):
+        if compute_dtype == torch.float32 and store.param.is_cuda:
+            from hetseq_amd.ops import gemm as G
+
+            if G.planes_enabled():
+                store.enable_planes()  # fp32 GEMM weights as split-bf16 planes (plane engine)
         for m in self.modules():
             m._hs_store = store
             m._hs_dtype = compute_dtype
@@ -728,9 +742,11 @@ class BertForPreTraining(BertPreTrainedModel):
     def _mlm_weights(self):
         t = self.cls.predictions.transform
         wt, wd = t.dense_act.weight, self.cls.predictions.decoder.weight
-        if self.compute_dtype != torch.bfloat16:
-            return wt.detach(), wd.detach()
         store = getattr(self, "_hs_store", None)
+        if self.compute_dtype != torch.bfloat16:
+            if store is not None and store.planes is not None:  # transform weight on the plane engine
+                return store.planes_view([wt], tuple(wt.shape)), wd.detach()
+            return wt.detach(), wd.detach()
         if store is not None:
             return store.shadow_view(wt), store.shadow_view(wd)
         return wt.detach().bfloat16(), wd.detach().bfloat16()

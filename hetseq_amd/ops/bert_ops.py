@@ -322,23 +322,37 @@ class FusedEmbedding(torch.autograd.Function):
 
 # --------------------------------------------------------------------- encoder layer
 class LayerWeights(object):
-    """Compute views of one encoder layer's weights (fp32 master or bf16 shadow)."""
+    """Compute views of one encoder layer's weights: fp32 master, bf16 shadow, or (fp32 plane
+    engine, ``planes`` True) the split-bf16 plane views (ops.gemm.Planes) of the GEMM weights."""
 
-    __slots__ = ("wqkv", "bqkv", "wo", "bo", "g1", "b1", "w1", "bi", "w2", "b2", "g2", "bb2")
+    __slots__ = ("wqkv", "bqkv", "wo", "bo", "g1", "b1", "w1", "bi", "w2", "b2", "g2", "bb2", "planes")
+
+
+def _planes_of(buf):
+    """Planes over a [3, rows, cols] split buffer (what G.split returns / the layer saves)."""
+    return G.Planes(buf, buf.shape[1], buf.shape[2], buf.shape[2], buf.shape[1] * buf.shape[2], 3)
 
 
 def _layer_forward(x, mask, W, cfg, save):
+    """GEMM operands are split once into bf16 planes when the weights are planes (fp32 mode on
+    the plane engine): each activation feeds its forward GEMM and, saved, its weight gradient."""
     B, S, NH, p_h, p_a, eps, seeds = cfg
     (s_a, o_a), (s_1, o_1), (s_2, o_2) = seeds
-    qkv = G.linear_fwd(x, W.wqkv)  # bias folded into the attention kernels' Q/K/V loads
+    sp = G.split if getattr(W, "planes", False) else (lambda t: t)
+    xin = sp(x)
+    qkv = G.linear_fwd(xin, W.wqkv)  # bias folded into the attention kernels' Q/K/V loads
     ctx_, (lse, dmask) = attn_fwd(qkv, mask, B, S, NH, p_a, s_a, o_a, bias=W.bqkv)
-    a = G.linear_fwd(ctx_, W.wo)
+    cin = sp(ctx_)
+    a = G.linear_fwd(cin, W.wo)
     h1, z1, m1, r1 = ln_fwd(a, W.g1, W.b1, eps, bias=W.bo, resid=x, p=p_h, mode=1, seed=s_1, off=o_1)
-    f1, f1pre = G.linear_gelu_fwd(h1, W.w1, W.bi)  # f1pre: un-biased pre-activation (for the backward)
-    o = G.linear_fwd(f1, W.w2)
+    hin = sp(h1)
+    f1, f1pre = G.linear_gelu_fwd(hin, W.w1, W.bi)  # f1pre: un-biased pre-activation (for the backward)
+    fin = sp(f1)
+    o = G.linear_fwd(fin, W.w2)
     h2, z2, m2, r2 = ln_fwd(o, W.g2, W.bb2, eps, bias=W.b2, resid=h1, p=p_h, mode=1, seed=s_2, off=o_2)
     if save:
-        return h2, (qkv, ctx_, lse, dmask, z1, m1, r1, h1, f1pre, f1, z2, m2, r2)
+        keep = (lambda t: t.buf) if getattr(W, "planes", False) else (lambda t: t)
+        return h2, (qkv, ctx_, lse, dmask, z1, m1, r1, keep(hin), f1pre, keep(fin), z2, m2, r2, keep(xin), keep(cin))
     return h2, None
 
 
@@ -370,7 +384,11 @@ class FusedBertLayer(torch.autograd.Function):
         else:
             x, mask = ctx.saved_tensors[:2]
             saved = ctx.saved_tensors[2:]
-        qkv, ctx_, lse, dmask, z1, m1, r1, h1, f1pre, f1, z2, m2, r2 = saved
+        qkv, ctx_, lse, dmask, z1, m1, r1, h1, f1pre, f1, z2, m2, r2, xin, cin = saved
+        pl = getattr(W, "planes", False)
+        sp = G.split if pl else (lambda t: t)
+        if pl:  # GEMM operands saved as split planes
+            h1, f1, xin, cin = (_planes_of(t) for t in (h1, f1, xin, cin))
         B, S, NH, p_h, p_a, eps, seeds = cfg
         (s_a, o_a), (s_1, o_1), (s_2, o_2) = seeds
         dh2 = dh2.contiguous()
@@ -386,27 +404,31 @@ class FusedBertLayer(torch.autograd.Function):
         dz2, do_, dg2, dbb2, db2 = ln_bwd(dh2, z2, m2, r2, W.g2, p_h, 1, s_2, o_2, True, True,
                                           acc=(Gv.g2, Gv.bb2, Gv.b2) if acc else None, side=side)
 
-        def wgrad(dy, xin, out):
+        def wgrad(dy, xin_, out):
             if not side:
-                return G.linear_wgrad(dy, xin, out=out, accumulate=acc)
-            return streams.run(dy.device, lambda: G.linear_wgrad(dy, xin, out=out, accumulate=acc,
-                                                                 ksplit=streams.SIDE_KSPLIT), dy, xin)
+                return G.linear_wgrad(dy, xin_, out=out, accumulate=acc)
+            return streams.run(dy.device, lambda: G.linear_wgrad(dy, xin_, out=out, accumulate=acc,
+                                                                 ksplit=streams.SIDE_KSPLIT), dy, xin_)
 
-        dW2 = wgrad(do_, f1, Gv.w2 if acc else None)
-        df1pre, dbi = G.linear_dgrad_dgelu(do_, W.w2, f1pre, W.bi, db_acc=Gv.bi if acc else None)
-        dW1 = wgrad(df1pre, h1, Gv.w1 if acc else None)
-        dh1 = G.linear_dgrad(df1pre, W.w1, out=dz2, accumulate=True)  # dz2 + df1pre @ W1
+        do_p = sp(do_)
+        dW2 = wgrad(do_p, f1, Gv.w2 if acc else None)
+        df1pre, dbi = G.linear_dgrad_dgelu(do_p, W.w2, f1pre, W.bi, db_acc=Gv.bi if acc else None)
+        df1p = sp(df1pre)
+        dW1 = wgrad(df1p, h1, Gv.w1 if acc else None)
+        dh1 = G.linear_dgrad(df1p, W.w1, out=dz2, accumulate=True)  # dz2 + df1pre @ W1
         dz1, da1, dg1, db1, dbo = ln_bwd(dh1, z1, m1, r1, W.g1, p_h, 1, s_1, o_1, True, True,
                                          acc=(Gv.g1, Gv.b1, Gv.bo) if acc else None, side=side)
-        dWo = wgrad(da1, ctx_, Gv.wo if acc else None)
-        dctx = G.linear_dgrad(da1, W.wo)
+        da1p = sp(da1)
+        dWo = wgrad(da1p, cin, Gv.wo if acc else None)
+        dctx = G.linear_dgrad(da1p, W.wo)
         dqkv = attn_bwd(qkv, mask, ctx_, dctx, (lse, dmask), B, S, NH, p_a, bias=W.bqkv)
-        dWqkv = wgrad(dqkv, x, Gv.wqkv if acc else None)
+        dqkvp = sp(dqkv)
+        dWqkv = wgrad(dqkvp, xin, Gv.wqkv if acc else None)
         if side:
             dbqkv = streams.run(dqkv.device, lambda: colsum(dqkv, acc=Gv.bqkv), dqkv)
         else:
             dbqkv = colsum(dqkv, acc=Gv.bqkv if acc else None)
-        dx = G.linear_dgrad(dqkv, W.wqkv, out=dz1, accumulate=True)  # dz1 + dqkv @ Wqkv
+        dx = G.linear_dgrad(dqkvp, W.wqkv, out=dz1, accumulate=True)  # dz1 + dqkv @ Wqkv
         if acc:
             return (dx, None, None) + (None,) * 16
         return (dx, None, None,
@@ -494,7 +516,9 @@ class FusedPreTrainingLoss(torch.autograd.Function):
         Wt, Wd = meta["weights"]()
         idx, lab, cnt = mlm_compact(labels.reshape(-1), cap)
         hsel = gather_rows(seq, idx)
-        t1pre = G.linear_fwd(hsel, Wt)
+        pl = isinstance(Wt, G.Planes)  # fp32 on the plane engine: transform GEMM operands split once
+        hsel_in = G.split(hsel) if pl else hsel
+        t1pre = G.linear_fwd(hsel_in, Wt)
         t1 = bias_gelu_fwd(t1pre, bt)
         t2, z, mean, rstd = ln_fwd(t1, g, b, eps)
         # tied decoder on the compacted rows; fp32: split-bf16 kernel on the vocabulary padded to
@@ -515,8 +539,10 @@ class FusedPreTrainingLoss(torch.autograd.Function):
                            nsp_logits.data_ptr(), nsp_lse.data_ptr(), stats.data_ptr(), stats[2:].data_ptr(),
                            stream_handle())
         ctx.padded = lbuf is not None
-        ctx.save_for_backward(idx, lab, hsel, t1pre, t1, z, mean, rstd, t2, lbuf if lbuf is not None else logits, lse,
-                              out, g, bt, seq, nsp_labels, pooled, nsp_logits, nsp_lse, stats, wp, wn)
+        ctx.save_for_backward(idx, lab, hsel_in.buf if pl else hsel, t1pre, t1, z, mean, rstd, t2,
+                              lbuf if lbuf is not None else logits, lse, out, g, bt, seq, nsp_labels, pooled,
+                              nsp_logits, nsp_lse, stats, wp, wn)
+        ctx.planes = pl
         ctx.meta = meta
         ctx.T = T
         return stats[2]
@@ -566,15 +592,18 @@ class FusedPreTrainingLoss(torch.autograd.Function):
         dt2 = G.decoder_dgrad(lbuf, Wd, V) if lbuf is not None else G.gemm(dl_c, Wd)
         dt1, _, dg, db, _ = ln_bwd(dt2, z, mean, rstd, g, 0.0, 0, acc=(Gv[2], Gv[3]) if acc else None, side=side)
         dt1pre, dbt = gelu_bwd_colsum(dt1, t1pre, bt, db_acc=Gv[1] if acc else None)
+        hsel_in = _planes_of(hsel) if ctx.planes else hsel
+        dt1pre_in = G.split(dt1pre) if ctx.planes else dt1pre
         if side:
-            dWt = streams.run(dt1pre.device, lambda: G.linear_wgrad(dt1pre, hsel, out=Gv[0], accumulate=True),
-                              dt1pre, hsel)
+            dWt = streams.run(dt1pre.device, lambda: G.linear_wgrad(dt1pre_in, hsel_in, out=Gv[0], accumulate=True),
+                              dt1pre_in, hsel_in)
         else:
-            dWt = G.linear_wgrad(dt1pre, hsel, out=Gv[0] if acc else None, accumulate=acc)
-        dhsel = G.linear_dgrad(dt1pre, Wt)
-        dseq = torch.zeros((ctx.T, hsel.shape[1]), dtype=hsel.dtype, device=hsel.device)
+            dWt = G.linear_wgrad(dt1pre_in, hsel_in, out=Gv[0] if acc else None, accumulate=acc)
+        dhsel = G.linear_dgrad(dt1pre_in, Wt)
+        H_ = seq.shape[1]
+        dseq = torch.zeros((ctx.T, H_), dtype=seq.dtype, device=seq.device)
         hip().scatter_add_rows(dtype_code(dseq), dhsel.data_ptr(), idx.data_ptr(), dseq.data_ptr(), idx.numel(),
-                               hsel.shape[1], stream_handle())
+                               H_, stream_handle())
         # pooler / NSP: input gradient added into dseq's first-token rows; parameter gradients
         # written (or accumulated into the flat store) by the deterministic column kernel
         B, S, H = meta["B"], meta["S"], seq.shape[1]

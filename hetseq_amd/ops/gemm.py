@@ -101,6 +101,118 @@ def _slab(M, N, ksplit, device):
     return buf
 
 
+# ------------------------------------------------------------------ bf16-plane operands
+class Planes(object):
+    """A [rows, cols] GEMM operand as P bf16 planes (csrc/kernels/gemm_planes.hip):
+    P = 3 -- an fp32 matrix split once into hi + mid + lo (the fp32 engine's operand);
+    P = 1 -- a bf16 matrix as it is (--dtype bf16).
+    ``buf`` owns the storage; element (r, c) of plane p sits at flat index
+    ``offset + p * ps + r * ld + c`` of it."""
+
+    __slots__ = ("buf", "rows", "cols", "ld", "ps", "P", "offset")
+
+    def __init__(self, buf, rows, cols, ld, ps, P, offset=0):
+        self.buf, self.rows, self.cols, self.ld, self.ps, self.P, self.offset = buf, rows, cols, ld, ps, P, offset
+
+    @property
+    def shape(self):
+        return (self.rows, self.cols)
+
+    @property
+    def device(self):
+        return self.buf.device
+
+    @property
+    def is_cuda(self):
+        return self.buf.is_cuda
+
+    def data_ptr(self):
+        return self.buf.data_ptr() + 2 * self.offset
+
+    @staticmethod
+    def of_bf16(x):
+        """P = 1 view of a row-major bf16 matrix (rows may be strided)."""
+        assert x.dtype == torch.bfloat16 and x.dim() == 2 and x.stride(1) == 1
+        return Planes(x, x.shape[0], x.shape[1], x.stride(0), 0, 1)
+
+    def unsplit(self):
+        """fp32 value of the planes (tests / debugging)."""
+        v = self.buf.reshape(-1)[self.offset:]
+        if self.P == 1:
+            return torch.as_strided(v, (self.rows, self.cols), (self.ld, 1)).float()
+        parts = [torch.as_strided(v[p * self.ps:], (self.rows, self.cols), (self.ld, 1)).float() for p in range(3)]
+        return parts[2] + parts[1] + parts[0]
+
+
+def planes_enabled():
+    """fp32 GEMMs on pre-split planes (HETSEQ_GEMM_PLANES=0 keeps the in-kernel-split x6 engine)."""
+    return _PLANES and _FP32 == "x6" and _MODE != "blas"
+
+
+_PLANES = os.environ.get("HETSEQ_GEMM_PLANES", "1") != "0"
+
+
+def split(x, out=None):
+    """fp32 [rows, cols] (contiguous) -> P = 3 Planes (one elementwise pass: read 4 B, write 6 B)."""
+    assert x.dtype == torch.float32 and x.dim() == 2 and x.is_contiguous() and x.numel() % 4 == 0
+    rows, cols = x.shape
+    if out is None:
+        out = torch.empty((3, rows, cols), dtype=torch.bfloat16, device=x.device)
+    hip().split_planes(x.data_ptr(), out.data_ptr(), x.numel(), rows * cols, stream_handle())
+    return Planes(out, rows, cols, cols, rows * cols, 3)
+
+
+def _unplane(x):
+    """fp32 value of a P = 3 operand for the engines that take fp32 (shapes the plane engine does
+    not tile, e.g. a 40-row masked-LM head in a test); other operands unchanged."""
+    return x.unsplit() if isinstance(x, Planes) and x.P == 3 else (x.buf if isinstance(x, Planes) else x)
+
+
+def _as_planes(x):
+    if isinstance(x, Planes):
+        return x
+    if x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 2 and x.stride(1) == 1:
+        return Planes.of_bf16(x)
+    return None
+
+
+def gemm_planes(a, b, ta, tb, out, bias=None, epi=EPI_NONE, beta=0.0, aux=None, part=None, colsum=None,
+                colsum_acc=False, ksplit=1):
+    """Launch the bf16-plane engine on Planes operands; False (nothing launched) if not served."""
+    if a.P != b.P or not out.is_cuda or out.stride(1) != 1 or out.dtype not in (torch.float32, torch.bfloat16):
+        return False
+    M, N, K = _dims(a, b, ta, tb)
+    if out.shape != (M, N):
+        return False
+    slab = _slab(M, N, ksplit, out.device) if ksplit > 1 else None
+    if ksplit > 1 and slab is None:
+        ksplit = 1
+    rc = hip().gemm_planes(a.P, 1 if out.dtype == torch.bfloat16 else 0, int(ta), int(tb), M, N, K, a.data_ptr(),
+                           a.ld, a.ps, b.data_ptr(), b.ld, b.ps, out.data_ptr(), out.stride(0),
+                           bias.data_ptr() if bias is not None else 0, epi, float(beta),
+                           aux.data_ptr() if aux is not None else 0, aux.stride(0) if aux is not None else 0,
+                           part.data_ptr() if part is not None else 0, colsum.data_ptr() if colsum is not None else 0,
+                           int(colsum_acc), int(ksplit), slab.data_ptr() if slab is not None else 0,
+                           slab.numel() if slab is not None else 0, stream_handle())
+    return rc == 0
+
+
+# split-K of the plane engine's weight gradients (K = tokens): slices so the tile grid covers the
+# chip about twice; measured choices can override per shape (PLANES_KSPLIT)
+PLANES_KSPLIT: dict = {}
+
+
+def _planes_ksplit(M, N, K, P):
+    key = (M, N, K, P)
+    if key in PLANES_KSPLIT:
+        return PLANES_KSPLIT[key]
+    tiles, s = (M // 128) * (N // 128), 1
+    bk = 32 if P == 3 else 64
+    while tiles * s < 384 and s < 8 and K % (2 * s * bk) == 0 and K // (2 * s) >= 512:
+        s *= 2
+    return s
+
+
 def _dims(a, b, ta, tb):
     M = a.shape[1] if ta else a.shape[0]
     K = a.shape[0] if ta else a.shape[1]
@@ -188,8 +300,21 @@ def _choose(key, run_hip, run_blas):
 
 
 def gemm(a, b, ta=False, tb=False, out=None, bias=None, epi=EPI_NONE, beta=0.0, out_dtype=None, ksplit=None):
-    """out = beta*out + op(a) @ op(b) (+bias).  ``ksplit`` overrides the measured split-K of the HIP engine."""
+    """out = beta*out + op(a) @ op(b) (+bias).  ``ksplit`` overrides the measured split-K of the HIP engine.
+
+    Operands that are :class:`Planes` (fp32 split once) or bf16 matrices run on the bf16-plane
+    engine (gemm_planes.hip); fp32 tensors on the in-kernel-split engine (gemm.hip) or the library."""
     M, N, K = _dims(a, b, ta, tb)
+    pa, pb = _as_planes(a), _as_planes(b)
+    if pa is not None and pb is not None and _MODE != "blas":
+        odt = out_dtype or (torch.float32 if pa.P == 3 else torch.bfloat16)
+        if out is None:
+            out = torch.empty((M, N), dtype=odt, device=pa.device)
+        ks = ksplit if ksplit is not None else (_planes_ksplit(M, N, K, pa.P) if ta and epi == EPI_NONE
+                                                and out.dtype == torch.float32 else 1)
+        if gemm_planes(pa, pb, ta, tb, out, bias, epi, beta, ksplit=ks):
+            return out
+        a, b = _unplane(a), _unplane(b)  # a shape the plane engine does not serve
     odt = out_dtype or a.dtype
     if out is None:
         out = torch.empty((M, N), dtype=odt, device=a.device)
@@ -364,6 +489,14 @@ def linear_gelu_fwd(x, w, b):
     from hetseq_amd.ops import bert_ops
 
     T, N = x.shape[0], w.shape[0]
+    px, pw = _as_planes(x), _as_planes(w)
+    if px is not None and pw is not None and _MODE != "blas":
+        dt = torch.float32 if px.P == 3 else torch.bfloat16
+        pre = torch.empty((T, N), dtype=dt, device=px.device)
+        y = torch.empty_like(pre)
+        if gemm_planes(px, pw, False, True, y, b, EPI_GELU, 0.0, aux=pre):
+            return y, pre
+        x, w = _unplane(x), _unplane(w)
     pre = torch.empty((T, N), dtype=x.dtype, device=x.device)
     y = torch.empty_like(pre)
     if x.is_cuda and _MODE != "blas" and _hip_ok(x, w, y, b, pre):
@@ -392,8 +525,16 @@ def linear_dgrad_dgelu(dy, w, pre, b, db_acc=None):
     from hetseq_amd.ops import bert_ops
 
     T, N = dy.shape[0], w.shape[1]
-    dpre = torch.empty((T, N), dtype=dy.dtype, device=dy.device)
     db = db_acc if db_acc is not None else torch.empty(N, dtype=torch.float32, device=dy.device)
+    pd, pw = _as_planes(dy), _as_planes(w)
+    if pd is not None and pw is not None and _MODE != "blas":
+        dpre = torch.empty((T, N), dtype=pre.dtype, device=pre.device)
+        part = torch.empty(((T + 127) // 128, N), dtype=torch.float32, device=pre.device)
+        if gemm_planes(pd, pw, False, False, dpre, b, EPI_DGELU, 0.0, aux=pre, part=part, colsum=db,
+                       colsum_acc=db_acc is not None):
+            return dpre, db
+        dy, w = _unplane(dy), _unplane(w)
+    dpre = torch.empty((T, N), dtype=dy.dtype, device=dy.device)
     if dy.is_cuda and _MODE != "blas" and _hip_ok(dy, w, dpre, pre, b):
         key = (T, N, dy.shape[1], "dgelu")
         part = torch.empty(((T + 63) // 64, N), dtype=torch.float32, device=dy.device)

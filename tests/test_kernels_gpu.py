@@ -815,3 +815,93 @@ def test_pretraining_heads_launch_no_torch_kernels(cuda):
     # the reference's pooler/NSP ops as torch kernels: bias+tanh, log-softmax / NLL (cross-entropy)
     bad = [n for n in names if "at::native" in n and any(k in n for k in ("tanh", "nll_loss", "log_softmax"))]
     assert not bad, bad
+
+
+def test_split_planes_exact(cuda):
+    """fp32 -> hi/mid/lo bf16 planes: each plane is the RNE bf16 of the remaining residual, and
+    hi + mid + lo reproduces x to 2^-24 relative (gemm_planes.hip)."""
+    from hetseq_amd.ops import gemm as G
+
+    torch.manual_seed(60)
+    x = torch.randn(300, 512, device=cuda) * torch.logspace(-20, 20, 512, base=2.0, device=cuda)
+    pl = G.split(x)
+    hi = x.bfloat16()
+    mid = (x - hi.float()).bfloat16()
+    lo = (x - hi.float() - mid.float()).bfloat16()
+    assert torch.equal(pl.buf[0], hi) and torch.equal(pl.buf[1], mid) and torch.equal(pl.buf[2], lo)
+    back = pl.unsplit()
+    assert ((back - x).abs() <= x.abs() * 2.0 ** -24).all()
+
+
+def _planes_operand(x, P):
+    from hetseq_amd.ops import gemm as G
+
+    return G.split(x.contiguous()) if P == 3 else G.Planes.of_bf16(x.bfloat16().contiguous())
+
+
+@pytest.mark.parametrize("P", [3, 1])
+@pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False)])
+@pytest.mark.parametrize("M,N,K,ks", [(256, 384, 512, 1), (640, 768, 768, 1), (384, 256, 1024, 4),
+                                      (128, 128, 4096, 2)])
+def test_gemm_planes_vs_fp64(cuda, P, ta, tb, M, N, K, ks):
+    """The bf16-plane engine in both layouts of each operand (k-contiguous b128 reads and
+    mn-contiguous transposed reads) and with split-K, against fp64.  P = 3 (fp32 as split bf16)
+    must carry fp32-level error: within 2x of torch's own fp32 GEMM error; P = 1 is exact bf16
+    products with fp32 accumulation."""
+    from hetseq_amd.ops import gemm as G
+
+    torch.manual_seed(61 + M + N + K)
+    a = torch.randn((K, M) if ta else (M, K), device=cuda)
+    b = torch.randn((N, K) if tb else (K, N), device=cuda)
+    pa, pb = _planes_operand(a, P), _planes_operand(b, P)
+    out = torch.empty(M, N, device=cuda)
+    assert G.gemm_planes(pa, pb, ta, tb, out, ksplit=ks)
+    ad, bd = (a.double(), b.double()) if P == 3 else (a.bfloat16().double(), b.bfloat16().double())
+    ref = (ad.t() if ta else ad) @ (bd.t() if tb else bd)
+    mag = (ad.abs().t() if ta else ad.abs()) @ (bd.abs().t() if tb else bd.abs())
+    err = float(((out.double() - ref).abs() / mag).max())  # in units of |A|@|B| (test_gemm_x6_error_...)
+    if P == 3:
+        f32 = (a.t() if ta else a) @ (b.t() if tb else b)
+        e32 = float(((f32.double() - ref).abs() / mag).max())
+        assert err <= 2.0 * e32 and err < 5e-7, (err, e32)
+    else:
+        assert err < 1e-5, err
+
+
+@pytest.mark.parametrize("P", [3, 1])
+def test_gemm_planes_epilogues(cuda, P):
+    """bias, beta-accumulate, GELU (pre-activation kept) and dGELU + bias-gradient column sums."""
+    from hetseq_amd.models.bert import f_gelu
+    from hetseq_amd.ops import gemm as G
+
+    torch.manual_seed(62)
+    T, K, N = 256, 512, 384
+    x, w, bias = torch.randn(T, K, device=cuda), torch.randn(N, K, device=cuda) * 0.05, torch.randn(N, device=cuda)
+    px, pw = _planes_operand(x, P), _planes_operand(w, P)
+    dt = torch.float32 if P == 3 else torch.bfloat16
+    xd, wd = (x.double(), w.double()) if P == 3 else (x.bfloat16().double(), w.bfloat16().double())
+    tol = 1e-5 if P == 3 else 1e-2
+    # bias
+    y = torch.empty(T, N, device=cuda, dtype=dt)
+    assert G.gemm_planes(px, pw, False, True, y, bias, G.EPI_BIAS)
+    _close(y, xd @ wd.t() + bias.double(), tol, tol, "planes bias")
+    # beta accumulate (fp32 C)
+    c0 = torch.randn(T, N, device=cuda)
+    c = c0.clone()
+    assert G.gemm_planes(px, pw, False, True, c, beta=1.0)
+    _close(c, xd @ wd.t() + c0.double(), tol, tol, "planes beta")
+    # GELU forward: y = gelu(pre + b), pre stored
+    y, pre = G.linear_gelu_fwd(px, pw, bias)
+    _close(pre, xd @ wd.t(), tol, tol, "planes gelu pre")
+    _close(y, f_gelu(pre.double() + bias.double()), tol, tol, "planes gelu")
+    # dGELU: dpre = (dy @ W) * gelu'(pre + b), db = colsum(dpre)
+    dy = torch.randn(T, N, device=cuda)
+    w2 = torch.randn(N, K, device=cuda) * 0.05  # dgrad operand [N][K]: dy[T,N] @ w2 -> [T, K]
+    prek = torch.randn(T, K, device=cuda).to(dt)
+    bk = torch.randn(K, device=cuda)
+    dpre, db = G.linear_dgrad_dgelu(_planes_operand(dy, P), _planes_operand(w2, P), prek, bk)
+    dyd, w2d = (dy.double(), w2.double()) if P == 3 else (dy.bfloat16().double(), w2.bfloat16().double())
+    pk = prek.double().requires_grad_()
+    f_gelu(pk + bk.double()).backward(dyd @ w2d)
+    _close(dpre, pk.grad, tol, tol, "planes dgelu")
+    _close(db, pk.grad.sum(0), tol, tol, "planes dgelu colsum")
