@@ -53,7 +53,7 @@ int launch_pool_nsp_fwd(int, const void*, int, int, int, const float*, const flo
                         const int64_t*, const float*, float*, float*, float*, float*, float*, hipStream_t);
 int launch_pool_nsp_bwd(int, const float*, const void*, void*, int, int, int, const float*, const float*,
                         const int64_t*, const float*, const float*, const float*, const float*, float*, float*,
-                        float*, float*, float*, float*, int, hipStream_t);
+                        float*, float*, float*, float*, float*, int, hipStream_t);
 // attention.hip
 void set_attn_fp32_mode(int x6);
 int attn_fp32_mode();
@@ -76,8 +76,9 @@ int launch_gemm_planes(int planes, int c_dtype, int ta, int tb, int M, int N, in
                        int64_t a_ps, const void* B, int64_t ldb, int64_t b_ps, void* C, int64_t ldc,
                        const float* bias, int epi, float beta, void* aux, int64_t ldaux, float* part,
                        float* colsum_out, int colsum_acc, int ksplit, float* slab, int64_t slab_floats,
-                       hipStream_t st);
+                       int variant, hipStream_t st);
 void launch_split_planes(const float* x, void* out, int64_t n, int64_t ps, hipStream_t st);
+void set_planes_variant(int v);
 
 // HIP-graph mode: device word holding the dropout seed (see common.h resolve_seed)
 namespace hs {
@@ -216,15 +217,16 @@ PYBIND11_MODULE(_hip, m) {
   m.def("gemm_planes", [](int planes, int c_dtype, int ta, int tb, int M, int N, int K, i64 A, i64 lda, i64 a_ps,
                           i64 B, i64 ldb, i64 b_ps, i64 C, i64 ldc, i64 bias, int epi, float beta, i64 aux,
                           i64 ldaux, i64 part, i64 colsum, int colsum_acc, int ksplit, i64 slab, i64 slab_floats,
-                          i64 st) {
+                          int variant, i64 st) {
     (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
     const int rc = launch_gemm_planes(planes, c_dtype, ta, tb, M, N, K, P(const void*, A), lda, a_ps,
                                       P(const void*, B), ldb, b_ps, P(void*, C), ldc, P(const float*, bias), epi,
                                       beta, P(void*, aux), ldaux, P(float*, part), P(float*, colsum), colsum_acc,
-                                      ksplit, P(float*, slab), slab_floats, ST(st));
+                                      ksplit, P(float*, slab), slab_floats, variant, ST(st));
     if (rc == 0) check_launch("gemm_planes");
     return rc;
   });
+  m.def("set_planes_variant", &set_planes_variant, "plane GEMM variant: 0 default, 1 one LDS stage, 2 half K depth");
   m.def("split_planes", [](i64 x, i64 out, i64 n, i64 ps, i64 st) {
     (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
     if (n % 4 || ps % 4) throw std::invalid_argument("split_planes: n and the plane stride must be multiples of 4");
@@ -241,13 +243,14 @@ PYBIND11_MODULE(_hip, m) {
           "pool_nsp_fwd");
   });
   m.def("pool_nsp_bwd", [](int dt, i64 dloss, i64 seq, i64 dseq, int B, int S, int H, i64 Wp, i64 Wn, i64 label,
-                           i64 pooled, i64 logits, i64 lse, i64 stats, i64 dlogits, i64 dpre, i64 dWp, i64 dbp,
-                           i64 dWn, i64 dbn, int accumulate, i64 st) {
+                           i64 pooled, i64 logits, i64 lse, i64 stats, i64 dlogits, i64 dpre, i64 part, i64 dWp,
+                           i64 dbp, i64 dWn, i64 dbn, int accumulate, i64 st) {
     (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
     check(launch_pool_nsp_bwd(dt, P(const float*, dloss), P(const void*, seq), P(void*, dseq), B, S, H,
                               P(const float*, Wp), P(const float*, Wn), P(const int64_t*, label),
                               P(const float*, pooled), P(const float*, logits), P(const float*, lse),
-                              P(const float*, stats), P(float*, dlogits), P(float*, dpre), P(float*, dWp),
+                              P(const float*, stats), P(float*, dlogits), P(float*, dpre), P(float*, part),
+                              P(float*, dWp),
                               P(float*, dbp), P(float*, dWn), P(float*, dbn), accumulate, ST(st)),
           "pool_nsp_bwd");
   });

@@ -37,6 +37,7 @@
 // (pre-activation kept in aux), dGELU with per-block column partials of the bias
 // gradient (finalised by reduce_rows).
 #include <algorithm>
+#include <type_traits>
 
 #include "common.h"
 #include "reduce.h"
@@ -75,7 +76,7 @@ struct PImg {
   // all 16 bank quads; mn-contiguous (256-B) rows put the 4 k-rows of a transposed read
   // into 4 different quarters of the bank row
   HS_DEVICE static int swz(int r) {
-    if (KCONTIG) return (r >> (row_bytes == 64 ? 2 : 1)) & (chunks - 1);
+    if (KCONTIG) return (r >> (row_bytes == 32 ? 3 : row_bytes == 64 ? 2 : 1)) & (chunks - 1);
     return 4 * (r & 3);
   }
 };
@@ -83,12 +84,12 @@ struct PImg {
 // Per-lane source byte offsets (from the plane-0 base at k = 0) of this wave's LDS-DMA
 // instructions for one operand: instruction j writes image bytes [1024 * (4 j + w), +1024)
 // of the operand's P planes.
-template <int BK, bool KCONTIG, int NJ>
+template <int BK, bool KCONTIG, int NJ, int WV>
 HS_DEVICE void dma_offsets(uint32_t* off, int64_t ld, int64_t ps, int mn0, int w, int lane) {
   using I = PImg<BK, KCONTIG>;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
-    const int byte = 1024 * (4 * j + w) + 16 * lane;
+    const int byte = 1024 * (WV * j + w) + 16 * lane;
     const int plane = byte / I::bytes, ib = byte % I::bytes;
     const int row = ib / I::row_bytes, cl = (ib % I::row_bytes) / 16;
     const int gc = cl ^ I::swz(row);  // the chunk this LDS position holds
@@ -98,11 +99,11 @@ HS_DEVICE void dma_offsets(uint32_t* off, int64_t ld, int64_t ps, int mn0, int w
   }
 }
 
-template <int NJ>
+template <int NJ, int WV>
 HS_DEVICE void dma_issue(const char* base, const uint32_t* off, char* img, int w) {
 #pragma unroll
   for (int j = 0; j < NJ; ++j)
-    __builtin_amdgcn_global_load_lds((gbl_void_t*)(base + off[j]), (lds_void_t*)(img + 1024 * (4 * j + w)), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((gbl_void_t*)(base + off[j]), (lds_void_t*)(img + 1024 * (WV * j + w)), 16, 0, 0);
 }
 
 // MFMA operand (8 consecutive k of one row / column) of plane p for the 32-wide tile at
@@ -141,14 +142,29 @@ HS_DEVICE float load_c(const bf16_t* p) { return to_f(*p); }
 template <typename TC>
 HS_DEVICE float round_c(float v) { return to_f(from_f<TC>(v)); }
 
-template <int P, int BK, bool TA, bool TB, int EPI, typename TC>
-__global__ void __launch_bounds__(256) gemm_planes_kernel(PlanesArgs p) {
+// waves per SIMD the block may count on: the blocks per CU its LDS image allows, capped so the
+// register budget stays >= 128 VGPRs (4 waves: 3 blocks, 8 waves: 2 blocks); WV / 4 waves per SIMD
+// per block
+template <int P, int BK, int STAGES, int WV>
+constexpr int planes_waves_per_simd() {
+  constexpr int by_lds = (160 * 1024) / (STAGES * P * 2 * kPB * BK * 2);
+  constexpr int cap = WV == 8 ? 2 : 3;
+  return (by_lds < cap ? by_lds : cap) * (WV / 4);
+}
+
+// WV = 4: 2x2 waves of 64x64 (2x2 accumulators each, one wave per SIMD per block);
+// WV = 8: 2x4 waves of 64x32 (2x1 accumulators, two waves per SIMD: one wave's LDS-DMA issue
+//         overlaps its partner's MFMAs)
+template <int P, int BK, int STAGES, int WV, bool TA, bool TB, int EPI, typename TC>
+__global__ void __launch_bounds__(64 * WV, (planes_waves_per_simd<P, BK, STAGES, WV>()))
+    gemm_planes_kernel(PlanesArgs p) {
   constexpr bool AK = !TA, BKc = TB;  // k-contiguous storage?
   using IA = PImg<BK, AK>;
   using IB = PImg<BK, BKc>;
   constexpr int STAGE = P * (IA::bytes + IB::bytes);
-  constexpr int NA = P * IA::bytes / 4096, NB = P * IB::bytes / 4096;
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  constexpr int NA = P * IA::bytes / (1024 * WV), NB = P * IB::bytes / (1024 * WV);
+  constexpr int WC = WV / 2, TN = 2 / (WV / 4);  // wave columns, 32-wide accumulator columns per wave
+  __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE];
 
   const int tiles_m = p.M / kPB, tiles_n = p.N / kPB, nwg = tiles_m * tiles_n * p.ksplit;
   const int orig = blockIdx.x;
@@ -163,21 +179,21 @@ __global__ void __launch_bounds__(256) gemm_planes_kernel(PlanesArgs p) {
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = w >> 1, wc = w & 1, wm = 64 * wr, wn = 64 * wc;
+  const int wr = w / WC, wc = w % WC, wm = 64 * wr, wn = (kPB / WC) * wc;
 
   uint32_t offA[NA], offB[NB];
-  dma_offsets<BK, AK, NA>(offA, p.lda, p.a_ps, m0, w, lane);
-  dma_offsets<BK, BKc, NB>(offB, p.ldb, p.b_ps, n0, w, lane);
+  dma_offsets<BK, AK, NA, WV>(offA, p.lda, p.a_ps, m0, w, lane);
+  dma_offsets<BK, BKc, NB, WV>(offB, p.ldb, p.b_ps, n0, w, lane);
   // K-tile advance of the (wave-uniform) source bases, in bytes
   const int64_t stepA = AK ? 2 * BK : 2 * (int64_t)BK * p.lda, stepB = BKc ? 2 * BK : 2 * (int64_t)BK * p.ldb;
   const char* ga = reinterpret_cast<const char*>(p.A) + (AK ? 2 * (int64_t)kofs : 2 * (int64_t)kofs * p.lda);
   const char* gb = reinterpret_cast<const char*>(p.B) + (BKc ? 2 * (int64_t)kofs : 2 * (int64_t)kofs * p.ldb);
 
-  pf16 acc[2][2];
+  pf16 acc[2][TN];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = pf16{};
+    for (int j = 0; j < TN; ++j) acc[i][j] = pf16{};
 
   // product terms (plane of A, plane of B), smallest first
   constexpr int NTERM = P == 3 ? 6 : 1;
@@ -189,7 +205,7 @@ __global__ void __launch_bounds__(256) gemm_planes_kernel(PlanesArgs p) {
   // barrier that publishes its DMA, so LDS latency hides under MFMAs.
   constexpr int NKS = BK / 16;
   struct Frags {
-    pbf8 a[P][2], b[P][2];
+    pbf8 a[P][2], b[P][TN];
   };
   auto read = [&](Frags& f, const char* stage, int ks) {
 #pragma unroll
@@ -197,7 +213,7 @@ __global__ void __launch_bounds__(256) gemm_planes_kernel(PlanesArgs p) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         f.a[pl][i] = frag<BK, AK>(stage, pl, wm + 32 * i, ks, lane);
-        f.b[pl][i] = frag<BK, BKc>(stage + P * IA::bytes, pl, wn + 32 * i, ks, lane);
+        if (i < TN) f.b[pl][i] = frag<BK, BKc>(stage + P * IA::bytes, pl, wn + 32 * i, ks, lane);
       }
   };
   auto mma = [&](const Frags& f) {
@@ -206,38 +222,63 @@ __global__ void __launch_bounds__(256) gemm_planes_kernel(PlanesArgs p) {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mma16(f.a[TA_[tt]][i], f.b[TB_[tt]][j], acc[i][j]);
+        for (int j = 0; j < TN; ++j) acc[i][j] = mma16(f.a[TA_[tt]][i], f.b[TB_[tt]][j], acc[i][j]);
   };
 
-  dma_issue<NA>(ga, offA, smem, w);
-  dma_issue<NB>(gb, offB, smem + P * IA::bytes, w);
+  Frags f[2];
+  if constexpr (STAGES == 1) {
+    // one LDS image: DMA, wait, compute, and a barrier before the next DMA overwrites it; the
+    // other blocks resident on the CU (LDS allows 3) fill the MFMA pipe meanwhile
+    for (int t = 0; t < KT; ++t) {
+      dma_issue<NA, WV>(ga + t * stepA, offA, smem, w);
+      dma_issue<NB, WV>(gb + t * stepB, offB, smem + P * IA::bytes, w);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      read(f[0], smem, 0);
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        if (ks + 1 < NKS) read(f[(ks + 1) & 1], smem, ks + 1);
+        mma(f[ks & 1]);
+      }
+      __syncthreads();
+    }
+  } else {
+  dma_issue<NA, WV>(ga, offA, smem, w);
+  dma_issue<NB, WV>(gb, offB, smem + P * IA::bytes, w);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  Frags f[2];
   read(f[0], smem, 0);
-  for (int t = 0; t < KT; ++t) {
+  // one K tile; the fragment set a slice uses alternates, so with an odd slice count the parity
+  // flips per tile: PAR (the tile's parity, compile-time) keeps every index static
+  auto tile = [&](int t, auto par) {
+    constexpr int F0 = decltype(par)::value * NKS;
     const char* cur = smem + (t & 1) * STAGE;
     char* nxt = smem + ((t + 1) & 1) * STAGE;
     if (t + 1 < KT) {  // the other stage was last read before the previous barrier
-      dma_issue<NA>(ga + (t + 1) * stepA, offA, nxt, w);
-      dma_issue<NB>(gb + (t + 1) * stepB, offB, nxt + P * IA::bytes, w);
+      dma_issue<NA, WV>(ga + (t + 1) * stepA, offA, nxt, w);
+      dma_issue<NB, WV>(gb + (t + 1) * stepB, offB, nxt + P * IA::bytes, w);
     }
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
       if (ks + 1 < NKS) {
-        read(f[(ks + 1) & 1], cur, ks + 1);
-        mma(f[ks & 1]);
+        read(f[(F0 + ks + 1) & 1], cur, ks + 1);
+        mma(f[(F0 + ks) & 1]);
       } else {
         // keep the previous slice's MFMAs ahead of the barrier (the scheduler would sink them
         // past it, exposing the last slice's LDS reads to the barrier's lgkmcnt(0))
         __builtin_amdgcn_sched_barrier(0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // tile t+1 landed in every wave's share; nobody reads tile t any more
-        if (t + 1 < KT) read(f[(ks + 1) & 1], nxt, 0);
-        mma(f[ks & 1]);
+        if (t + 1 < KT) read(f[(F0 + ks + 1) & 1], nxt, 0);
+        mma(f[(F0 + ks) & 1]);
       }
     }
+  };
+  for (int t = 0; t < KT; t += 2) {
+    tile(t, std::integral_constant<int, 0>{});
+    if (t + 1 < KT) tile(t + 1, std::integral_constant<int, 1>{});
   }
+  }  // STAGES == 2
 
   // ---------------- epilogue: register r of acc[i][j] -> row m0+wm+32i+acc_row(r,q), col n0+wn+32j+lr
   const int lr = lane & 31, q = lane >> 5;
@@ -246,7 +287,7 @@ __global__ void __launch_bounds__(256) gemm_planes_kernel(PlanesArgs p) {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r)
           sl[(int64_t)(m0 + wm + 32 * i + acc_row(r, q)) * p.N + n0 + wn + 32 * j + lr] = acc[i][j][r];
@@ -254,9 +295,11 @@ __global__ void __launch_bounds__(256) gemm_planes_kernel(PlanesArgs p) {
   }
   TC* C = static_cast<TC*>(p.C);
   TC* aux = static_cast<TC*>(p.aux);
-  float csum[2] = {0.f, 0.f};
+  float csum[TN];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
+  for (int j = 0; j < TN; ++j) csum[j] = 0.f;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
     const int n = n0 + wn + 32 * j + lr;
     const float bv = EPI != kPEpiNone ? p.bias[n] : 0.f;
 #pragma unroll
@@ -283,14 +326,14 @@ __global__ void __launch_bounds__(256) gemm_planes_kernel(PlanesArgs p) {
   if (EPI == kPEpiDGelu) {  // column sums over the block's 128 rows: lane halves, then wave rows via LDS
     float* red = reinterpret_cast<float*>(smem);  // the K loop ended with a barrier
 #pragma unroll
-    for (int j = 0; j < 2; ++j) csum[j] += __shfl_xor(csum[j], 32, 64);
+    for (int j = 0; j < TN; ++j) csum[j] += __shfl_xor(csum[j], 32, 64);
     if (wr == 1 && q == 0)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) red[wn + 32 * j + lr] = csum[j];
+      for (int j = 0; j < TN; ++j) red[wn + 32 * j + lr] = csum[j];
     __syncthreads();
     if (wr == 0 && q == 0)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < TN; ++j) {
         const int c = wn + 32 * j + lr;
         p.part[(int64_t)tm * p.N + n0 + c] = csum[j] + red[c];
       }
@@ -317,10 +360,11 @@ __global__ void __launch_bounds__(256) split_planes_kernel(const float* __restri
   }
 }
 
-template <int P, int BK, typename TC>
+template <int P, int BK, int STAGES, int WV, typename TC>
 int launch_planes_cfg(int ta, int tb, int epi, const PlanesArgs& a, hipStream_t st) {
-  const dim3 grid((a.M / kPB) * (a.N / kPB) * a.ksplit), blk(256);
-#define HS_PL(TA_, TB_, E_) hipLaunchKernelGGL((gemm_planes_kernel<P, BK, TA_, TB_, E_, TC>), grid, blk, 0, st, a)
+  const dim3 grid((a.M / kPB) * (a.N / kPB) * a.ksplit), blk(64 * WV);
+#define HS_PL(TA_, TB_, E_) \
+  hipLaunchKernelGGL((gemm_planes_kernel<P, BK, STAGES, WV, TA_, TB_, E_, TC>), grid, blk, 0, st, a)
   if (!ta && tb) {  // forward X W^T
     if (epi == kPEpiNone) HS_PL(false, true, kPEpiNone);
     else if (epi == kPEpiBias) HS_PL(false, true, kPEpiBias);
@@ -348,6 +392,9 @@ void launch_splitk_reduce(const float* slab, int ksplit, int M, int N, float* C,
 
 using namespace hs;
 
+static int g_planes_variant = 0;  // microbenchmark / tuning hook (tools/bench_planes.py)
+void set_planes_variant(int v) { g_planes_variant = v; }
+
 // planes: 1 (bf16) or 3 (split fp32); c_dtype: 0 fp32 C, 1 bf16 C.  Operand strides / plane
 // strides in elements.  Returns -1 (nothing launched) for shapes it does not serve: M, N
 // multiples of 128, K a multiple of BK * ksplit, 16-B aligned rows.
@@ -355,9 +402,12 @@ int launch_gemm_planes(int planes, int c_dtype, int ta, int tb, int M, int N, in
                        int64_t a_ps, const void* B, int64_t ldb, int64_t b_ps, void* C, int64_t ldc,
                        const float* bias, int epi, float beta, void* aux, int64_t ldaux, float* part,
                        float* colsum_out, int colsum_acc, int ksplit, float* slab, int64_t slab_floats,
-                       hipStream_t st) {
+                       int variant, hipStream_t st) {
   if (planes != 1 && planes != 3) return -1;
-  const int BK = planes == 3 ? 32 : 64;
+  // variant (tile K depth, LDS stages, waves): 0 = two stages, 4 waves; 1 = one stage; 2 = half
+  // depth; 3 = 8 waves; 4 = 8 waves + one stage.  < 0: the process default (set_planes_variant)
+  if (variant < 0) variant = g_planes_variant;
+  const int BK = planes == 3 ? (variant == 2 ? 16 : 32) : (variant == 2 ? 32 : 64);
   ksplit = std::max(1, ksplit);
   if (M <= 0 || N <= 0 || K <= 0 || M % kPB || N % kPB || K % (BK * ksplit)) return -1;
   auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
@@ -372,10 +422,16 @@ int launch_gemm_planes(int planes, int c_dtype, int ta, int tb, int M, int N, in
   PlanesArgs a{static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), C, bias, aux, part, slab,
                lda, ldb, ldc, ldaux, a_ps, b_ps, M, N, K, ksplit, beta};
   int rc;
+#define HS_CFG(P_, BK_, S_, W_)                                                        \
+  (c_dtype ? launch_planes_cfg<P_, BK_, S_, W_, bf16_t>(ta, tb, epi, a, st) \
+           : launch_planes_cfg<P_, BK_, S_, W_, float>(ta, tb, epi, a, st))
   if (planes == 3)
-    rc = c_dtype ? launch_planes_cfg<3, 32, bf16_t>(ta, tb, epi, a, st) : launch_planes_cfg<3, 32, float>(ta, tb, epi, a, st);
+    rc = variant == 1 ? HS_CFG(3, 32, 1, 4) : variant == 2 ? HS_CFG(3, 16, 2, 4) : variant == 3 ? HS_CFG(3, 32, 2, 8)
+       : variant == 4 ? HS_CFG(3, 32, 1, 8) : HS_CFG(3, 32, 2, 4);
   else
-    rc = c_dtype ? launch_planes_cfg<1, 64, bf16_t>(ta, tb, epi, a, st) : launch_planes_cfg<1, 64, float>(ta, tb, epi, a, st);
+    rc = variant == 1 ? HS_CFG(1, 64, 1, 4) : variant == 2 ? HS_CFG(1, 32, 2, 4) : variant == 3 ? HS_CFG(1, 64, 2, 8)
+       : variant == 4 ? HS_CFG(1, 64, 1, 8) : HS_CFG(1, 64, 2, 4);
+#undef HS_CFG
   if (rc) return rc;
   if (ksplit > 1) launch_splitk_reduce(slab, ksplit, M, N, static_cast<float*>(C), ldc, nullptr, beta, M, N, st);
   if (epi == kPEpiDGelu) {

@@ -6,16 +6,16 @@
 //   loss   = mlm_loss + CE(logits, label, ignore_index=-1)
 // There the pooler is a GEMM + a TorchScript bias-tanh kernel, the NSP head
 // another GEMM + bias, the CE two more kernels and the final add a fifth.  The
-// work is tiny ([B, H] x [H, H] with B = 32 or 8), so it is launch- and
-// latency-bound: here it is four kernels for forward + backward together,
+// work is tiny ([B, H] x [H, H] with B = 32 or 8), so it is latency-bound: the
+// kernels below spread it over hundreds of waves (one per pooler row / row chunk),
 // all in fp32 whatever the encoder's compute dtype, reading the first-token
 // rows straight out of the [B*S, H] sequence output (no gather copy).
 //
-//   pool_nsp_fwd_kernel   grid B: pooled[b], logits[b] (one workgroup per sequence;
-//                         Wp rows are dotted by whole waves, 4 rows per pass)
-//   nsp_loss_kernel       1 wave: mean CE over labelled rows, + mlm_loss -> total
-//   pool_nsp_bwd_kernel   grid B: dlogits, dpre = (dlogits Wn) o (1 - pooled^2),
-//                         dx = dpre Wp added into dseq's first-token row
+//   pool_fwd_kernel       grid H/4: one wave per pooler row, all B first-token rows past it
+//   nsp_loss_kernel       1 workgroup: logits, mean CE over labelled rows, + mlm_loss -> total
+//   nsp_bwd_kernel        grid B: dlogits, dpre = (dlogits Wn) o (1 - pooled^2)
+//   pool_dx_partial/finish grid (B, 8) + B: dx = dpre Wp in 8 row chunks, summed in fixed
+//                         order and added into dseq's first-token rows
 //   pool_nsp_wgrad_kernel grid H + 2: dWp / dbp rows, then dWn / dbn, summed over b
 //                         in a fixed order (deterministic), written or accumulated
 //                         into the flat gradient buffer
@@ -25,96 +25,108 @@ namespace hs {
 
 constexpr int kPoolThreads = 256;
 
-// pooled[b, :] and logits[b, :].  x = seq row b*S (the first token).
+// pooled[b, i] = tanh(x_b . Wp[i] + bp[i]) for every b: one wave per row i (its Wp row stays in
+// registers, 3 x 16 B per lane at H = 768) and the B first-token rows streamed past it, four in
+// flight; grid H / 4 workgroups of 4 waves fill the chip instead of one workgroup per sequence.
 template <typename T>
 __global__ void __launch_bounds__(kPoolThreads)
-    pool_nsp_fwd_kernel(const T* __restrict__ seq, int S, int H, const float* __restrict__ Wp,
-                        const float* __restrict__ bp, const float* __restrict__ Wn, const float* __restrict__ bn,
-                        float* __restrict__ pooled, float* __restrict__ logits) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* xs = sm;      // [H] first-token row
-  float* ps = sm + H;  // [H] pooled row
-  const int b = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = kPoolThreads / 64;
-  const T* x = seq + (int64_t)b * S * H;
-  for (int k = threadIdx.x * 4; k < H; k += kPoolThreads * 4) {
-    float v[4];
-    load4(x + k, v);
-    *reinterpret_cast<float4*>(xs + k) = make_float4(v[0], v[1], v[2], v[3]);
-  }
-  __syncthreads();
-  // each wave takes 4 rows of Wp at a time: 4 independent dot products per lane, one shuffle tree
-  for (int i0 = 4 * w; i0 < H; i0 += 4 * nw) {
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int k = lane * 4; k < H; k += 256) {
-      const float4 xv = *reinterpret_cast<const float4*>(xs + k);
+    pool_fwd_kernel(const T* __restrict__ seq, int B, int S, int H, const float* __restrict__ Wp,
+                    const float* __restrict__ bp, float* __restrict__ pooled) {
+  constexpr int kMaxV = 4;  // float4 per lane: H <= 1024
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * (kPoolThreads / 64) + (threadIdx.x >> 6);
+  if (i >= H) return;
+  float w[kMaxV][4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (i0 + r < H) {
-          const float4 wv = *reinterpret_cast<const float4*>(Wp + (int64_t)(i0 + r) * H + k);
-          acc[r] = fmaf(wv.x, xv.x, fmaf(wv.y, xv.y, fmaf(wv.z, xv.z, fmaf(wv.w, xv.w, acc[r]))));
+  for (int v = 0; v < kMaxV; ++v) {
+    const int k = 4 * (lane + 64 * v);
+    if (k < H) load4(Wp + (int64_t)i * H + k, w[v]);
+    else w[v][0] = w[v][1] = w[v][2] = w[v][3] = 0.f;
+  }
+  const float bias = bp[i];
+  for (int b0 = 0; b0 < B; b0 += 4) {
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int b = min(b0 + u, B - 1);
+#pragma unroll
+      for (int v = 0; v < kMaxV; ++v) {
+        const int k = 4 * (lane + 64 * v);
+        if (k < H) {
+          float x[4];
+          load4(seq + (int64_t)b * S * H + k, x);
+          acc[u] = fmaf(w[v][0], x[0], fmaf(w[v][1], x[1], fmaf(w[v][2], x[2], fmaf(w[v][3], x[3], acc[u]))));
         }
       }
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) acc[r] = wave_sum(acc[r]);
-    if (lane < 4 && i0 + lane < H) {
+    for (int u = 0; u < 4; ++u) acc[u] = wave_sum(acc[u]);
+    if (lane < 4 && b0 + lane < B) {
       const float a = lane == 0 ? acc[0] : lane == 1 ? acc[1] : lane == 2 ? acc[2] : acc[3];
-      const float y = tanhf(a + bp[i0 + lane]);
-      ps[i0 + lane] = y;
-      pooled[(int64_t)b * H + i0 + lane] = y;
+      pooled[(int64_t)(b0 + lane) * H + i] = tanhf(a + bias);
     }
-  }
-  __syncthreads();
-  if (w < 2) {  // wave c: logit c
-    float acc = 0.f;
-    for (int k = lane; k < H; k += 64) acc = fmaf(ps[k], Wn[(int64_t)w * H + k], acc);
-    acc = wave_sum(acc);
-    if (lane == 0) logits[b * 2 + w] = acc + bn[w];
   }
 }
 
-// total[0] = mlm_loss[0] + mean_b CE(logits[b], label[b]) over labels != -1 (NaN if none, as
-// torch); lse[b] kept for the backward, stats[0] = count of labelled rows.
-__global__ void __launch_bounds__(64)
-    nsp_loss_kernel(const float* __restrict__ logits, const int64_t* __restrict__ label, int B,
-                    const float* __restrict__ mlm_loss, float* __restrict__ lse, float* __restrict__ stats,
+// logits[b] = pooled[b] Wn^T + bn (one wave per b), then total[0] = mlm_loss[0] + mean_b
+// CE(logits[b], label[b]) over labels != -1 (NaN if none, as torch); lse[b] kept for the
+// backward, stats[0] = count of labelled rows, stats[1] = NSP loss.  One workgroup.
+__global__ void __launch_bounds__(kPoolThreads)
+    nsp_loss_kernel(const float* __restrict__ pooled, const float* __restrict__ Wn, const float* __restrict__ bn,
+                    const int64_t* __restrict__ label, int B, int H, const float* __restrict__ mlm_loss,
+                    float* __restrict__ logits, float* __restrict__ lse, float* __restrict__ stats,
                     float* __restrict__ total) {
+  __shared__ float red[2][kPoolThreads / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = kPoolThreads / 64;
   float s = 0.f, c = 0.f;
-  for (int b = threadIdx.x; b < B; b += 64) {
-    const float l0 = logits[2 * b], l1 = logits[2 * b + 1];
+  for (int b = w; b < B; b += nw) {
+    float a0 = 0.f, a1 = 0.f;
+    for (int k = lane; k < H; k += 64) {
+      const float p = pooled[(int64_t)b * H + k];
+      a0 = fmaf(p, Wn[k], a0);
+      a1 = fmaf(p, Wn[H + k], a1);
+    }
+    const float l0 = wave_sum(a0) + bn[0], l1 = wave_sum(a1) + bn[1];
     const float m = fmaxf(l0, l1);
     const float z = m + __logf(__expf(l0 - m) + __expf(l1 - m));
-    lse[b] = z;
     const int64_t y = label[b];
-    if (y == 0 || y == 1) {
-      s += z - (y == 0 ? l0 : l1);
-      c += 1.f;
+    if (lane == 0) {
+      logits[2 * b] = l0;
+      logits[2 * b + 1] = l1;
+      lse[b] = z;
+      if (y == 0 || y == 1) {
+        s += z - (y == 0 ? l0 : l1);
+        c += 1.f;
+      }
     }
   }
-  s = wave_sum(s);
-  c = wave_sum(c);
+  if (lane == 0) {
+    red[0][w] = s;
+    red[1][w] = c;
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
-    stats[0] = c;
-    stats[1] = s / c;
-    total[0] = (mlm_loss ? mlm_loss[0] : 0.f) + s / c;
+    float ts = 0.f, tc = 0.f;
+    for (int i = 0; i < nw; ++i) {  // fixed order: deterministic
+      ts += red[0][i];
+      tc += red[1][i];
+    }
+    stats[0] = tc;
+    stats[1] = ts / tc;
+    total[0] = (mlm_loss ? mlm_loss[0] : 0.f) + ts / tc;
   }
 }
 
-// dlogits[b] = dloss / count * (softmax - onehot) (0 for ignored rows); dpre[b] = (dlogits Wn) o
-// (1 - pooled^2); dseq[b*S, :] += dpre Wp.
-template <typename T>
+// dlogits[b] = dloss / count * (softmax - onehot) (0 for ignored rows);
+// dpre[b] = (dlogits Wn) o (1 - pooled^2).  Grid B.
 __global__ void __launch_bounds__(kPoolThreads)
-    pool_nsp_bwd_kernel(const float* __restrict__ dloss, const float* __restrict__ logits,
-                        const float* __restrict__ lse, const int64_t* __restrict__ label,
-                        const float* __restrict__ stats, const float* __restrict__ pooled,
-                        const float* __restrict__ Wn, const float* __restrict__ Wp, int S, int H,
-                        float* __restrict__ dlogits, float* __restrict__ dpre, T* __restrict__ dseq) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* dps = sm;  // [H]
+    nsp_bwd_kernel(const float* __restrict__ dloss, const float* __restrict__ logits, const float* __restrict__ lse,
+                   const int64_t* __restrict__ label, const float* __restrict__ stats,
+                   const float* __restrict__ pooled, const float* __restrict__ Wn, int H,
+                   float* __restrict__ dlogits, float* __restrict__ dpre) {
   const int b = blockIdx.x;
   const int64_t y = label[b];
-  const bool valid = y == 0 || y == 1;
-  const float g = valid ? dloss[0] / stats[0] : 0.f;
+  const float g = (y == 0 || y == 1) ? dloss[0] / stats[0] : 0.f;
   const float z = lse[b];
   const float d0 = g * (__expf(logits[2 * b] - z) - (y == 0 ? 1.f : 0.f));
   const float d1 = g * (__expf(logits[2 * b + 1] - z) - (y == 1 ? 1.f : 0.f));
@@ -124,27 +136,69 @@ __global__ void __launch_bounds__(kPoolThreads)
   }
   for (int k = threadIdx.x; k < H; k += kPoolThreads) {
     const float p = pooled[(int64_t)b * H + k];
-    const float d = (d0 * Wn[k] + d1 * Wn[H + k]) * (1.f - p * p);
-    dps[k] = d;
-    dpre[(int64_t)b * H + k] = d;
+    dpre[(int64_t)b * H + k] = (d0 * Wn[k] + d1 * Wn[H + k]) * (1.f - p * p);
+  }
+}
+
+// dx = dpre Wp in kChunks row chunks of Wp: workgroup (b, c) sums rows [c H/kChunks, (c+1) H/kChunks)
+// of Wp weighted by dpre[b] (each wave a quarter of them, lanes over all columns, then the waves
+// combined in LDS in fixed order) -> part[b][c][:]
+constexpr int kChunks = 8;
+
+__global__ void __launch_bounds__(kPoolThreads)
+    pool_dx_partial_kernel(const float* __restrict__ dpre, const float* __restrict__ Wp, int H,
+                           float* __restrict__ part) {
+  constexpr int kMaxV = 4;  // H <= 1024
+  extern __shared__ __attribute__((aligned(16))) float smp[];  // [4 waves][H]
+  const int b = blockIdx.x, c = blockIdx.y, lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = kPoolThreads / 64;
+  const int rows = H / kChunks, r0 = c * rows + w * (rows / nw), r1 = (w == nw - 1) ? (c + 1) * rows : r0 + rows / nw;
+  float acc[kMaxV][4] = {};
+  for (int i = r0; i < r1; ++i) {
+    const float d = dpre[(int64_t)b * H + i];
+#pragma unroll
+    for (int v = 0; v < kMaxV; ++v) {
+      const int k = 4 * (lane + 64 * v);
+      if (k < H) {
+        float wv[4];
+        load4(Wp + (int64_t)i * H + k, wv);
+        acc[v][0] = fmaf(d, wv[0], acc[v][0]);
+        acc[v][1] = fmaf(d, wv[1], acc[v][1]);
+        acc[v][2] = fmaf(d, wv[2], acc[v][2]);
+        acc[v][3] = fmaf(d, wv[3], acc[v][3]);
+      }
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < kMaxV; ++v) {
+    const int k = 4 * (lane + 64 * v);
+    if (k < H) store4(smp + w * H + k, acc[v]);
   }
   __syncthreads();
-  // dx[j] = sum_i dpre[i] Wp[i][j]: threads own 4 consecutive columns, rows streamed in order
+  for (int k = threadIdx.x; k < H; k += kPoolThreads) {
+    float t = 0.f;
+    for (int q = 0; q < nw; ++q) t += smp[q * H + k];
+    part[((int64_t)b * kChunks + c) * H + k] = t;
+  }
+}
+
+// dseq[b*S, :] += sum_c part[b][c][:] (fixed order).  Grid B.
+template <typename T>
+__global__ void __launch_bounds__(kPoolThreads)
+    pool_dx_finish_kernel(const float* __restrict__ part, int S, int H, T* __restrict__ dseq) {
+  const int b = blockIdx.x;
   T* row = dseq + (int64_t)b * S * H;
   for (int j = threadIdx.x * 4; j < H; j += kPoolThreads * 4) {
-    float a[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int i = 0; i < H; ++i) {
-      const float4 wv = *reinterpret_cast<const float4*>(Wp + (int64_t)i * H + j);
-      const float d = dps[i];
-      a[0] = fmaf(d, wv.x, a[0]);
-      a[1] = fmaf(d, wv.y, a[1]);
-      a[2] = fmaf(d, wv.z, a[2]);
-      a[3] = fmaf(d, wv.w, a[3]);
+    float a[4];
+    load4(row + j, a);
+    for (int c = 0; c < kChunks; ++c) {
+      float v[4];
+      load4(part + ((int64_t)b * kChunks + c) * H + j, v);
+      a[0] += v[0];
+      a[1] += v[1];
+      a[2] += v[2];
+      a[3] += v[3];
     }
-    float old[4];
-    load4(row + j, old);
-    const float v[4] = {old[0] + a[0], old[1] + a[1], old[2] + a[2], old[3] + a[3]};
-    store4(row + j, v);
+    store4(row + j, a);
   }
 }
 
@@ -193,36 +247,40 @@ __global__ void __launch_bounds__(kPoolThreads)
 
 using namespace hs;
 
-// dtype: 0 fp32, 1 bf16 sequence output.  H % 4 == 0 (checked by the caller too).
+// dtype: 0 fp32, 1 bf16 sequence output.  H % 4 == 0, H <= 1024 (checked by the caller too).
 int launch_pool_nsp_fwd(int dtype, const void* seq, int B, int S, int H, const float* Wp, const float* bp,
                         const float* Wn, const float* bn, const int64_t* label, const float* mlm_loss, float* pooled,
                         float* logits, float* lse, float* stats, float* total, hipStream_t st) {
-  if (B <= 0 || H <= 0 || H % 4) return -1;
-  const size_t lds = 2 * (size_t)H * sizeof(float);
+  if (B <= 0 || H <= 0 || H % 4 || H > 1024) return -1;
+  const dim3 grid((H + 3) / 4);
   if (dtype == 0)
-    hipLaunchKernelGGL(pool_nsp_fwd_kernel<float>, dim3(B), dim3(kPoolThreads), lds, st, (const float*)seq, S, H, Wp,
-                       bp, Wn, bn, pooled, logits);
+    hipLaunchKernelGGL(pool_fwd_kernel<float>, grid, dim3(kPoolThreads), 0, st, (const float*)seq, B, S, H, Wp, bp,
+                       pooled);
   else
-    hipLaunchKernelGGL(pool_nsp_fwd_kernel<bf16_t>, dim3(B), dim3(kPoolThreads), lds, st, (const bf16_t*)seq, S, H,
-                       Wp, bp, Wn, bn, pooled, logits);
-  hipLaunchKernelGGL(nsp_loss_kernel, dim3(1), dim3(64), 0, st, logits, label, B, mlm_loss, lse, stats, total);
+    hipLaunchKernelGGL(pool_fwd_kernel<bf16_t>, grid, dim3(kPoolThreads), 0, st, (const bf16_t*)seq, B, S, H, Wp,
+                       bp, pooled);
+  hipLaunchKernelGGL(nsp_loss_kernel, dim3(1), dim3(kPoolThreads), 0, st, pooled, Wn, bn, label, B, H, mlm_loss,
+                     logits, lse, stats, total);
   return 0;
 }
 
+// scratch: dlogits [B, 2], dpre [B, H], part [B, 8, H] floats
 int launch_pool_nsp_bwd(int dtype, const float* dloss, const void* seq, void* dseq, int B, int S, int H,
                         const float* Wp, const float* Wn, const int64_t* label, const float* pooled,
                         const float* logits, const float* lse, const float* stats, float* dlogits, float* dpre,
-                        float* dWp, float* dbp, float* dWn, float* dbn, int accumulate, hipStream_t st) {
-  if (B <= 0 || H <= 0 || H % 4) return -1;
-  const size_t lds = (size_t)H * sizeof(float);
+                        float* part, float* dWp, float* dbp, float* dWn, float* dbn, int accumulate,
+                        hipStream_t st) {
+  if (B <= 0 || H <= 0 || H % 4 || H > 1024 || H % (kChunks * 4)) return -1;
+  hipLaunchKernelGGL(nsp_bwd_kernel, dim3(B), dim3(kPoolThreads), 0, st, dloss, logits, lse, label, stats, pooled, Wn,
+                     H, dlogits, dpre);
+  hipLaunchKernelGGL(pool_dx_partial_kernel, dim3(B, kChunks), dim3(kPoolThreads), 4 * (size_t)H * sizeof(float), st,
+                     dpre, Wp, H, part);
   if (dtype == 0) {
-    hipLaunchKernelGGL(pool_nsp_bwd_kernel<float>, dim3(B), dim3(kPoolThreads), lds, st, dloss, logits, lse, label,
-                       stats, pooled, Wn, Wp, S, H, dlogits, dpre, (float*)dseq);
+    hipLaunchKernelGGL(pool_dx_finish_kernel<float>, dim3(B), dim3(kPoolThreads), 0, st, part, S, H, (float*)dseq);
     hipLaunchKernelGGL(pool_nsp_wgrad_kernel<float>, dim3(H + 2), dim3(kPoolThreads), 0, st, (const float*)seq, dpre,
                        dlogits, pooled, B, S, H, dWp, dbp, dWn, dbn, accumulate);
   } else {
-    hipLaunchKernelGGL(pool_nsp_bwd_kernel<bf16_t>, dim3(B), dim3(kPoolThreads), lds, st, dloss, logits, lse, label,
-                       stats, pooled, Wn, Wp, S, H, dlogits, dpre, (bf16_t*)dseq);
+    hipLaunchKernelGGL(pool_dx_finish_kernel<bf16_t>, dim3(B), dim3(kPoolThreads), 0, st, part, S, H, (bf16_t*)dseq);
     hipLaunchKernelGGL(pool_nsp_wgrad_kernel<bf16_t>, dim3(H + 2), dim3(kPoolThreads), 0, st, (const bf16_t*)seq,
                        dpre, dlogits, pooled, B, S, H, dWp, dbp, dWn, dbn, accumulate);
   }

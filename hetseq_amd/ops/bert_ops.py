@@ -615,13 +615,13 @@ class FusedPreTrainingLoss(torch.autograd.Function):
             dbp = torch.empty(H, dtype=torch.float32, device=dev)
             dWn = torch.empty((2, H), dtype=torch.float32, device=dev)
             dbn = torch.empty(2, dtype=torch.float32, device=dev)
-        dpre = torch.empty((B, H), dtype=torch.float32, device=dev)
-        dnsp = torch.empty((B, 2), dtype=torch.float32, device=dev)
+        scratch = torch.empty(B * (2 + 9 * H), dtype=torch.float32, device=dev)  # dlogits, dpre, 8 dx chunks
+        dnsp, dpre, part = scratch[:2 * B], scratch[2 * B:2 * B + B * H], scratch[2 * B + B * H:]
         hip().pool_nsp_bwd(dtype_code(seq), dloss.data_ptr(), seq.data_ptr(), dseq.data_ptr(), B, S, H,
                            wp.data_ptr(), wn.data_ptr(), nsp_labels.data_ptr(), pooled.data_ptr(),
                            nsp_logits.data_ptr(), nsp_lse.data_ptr(), stats.data_ptr(), dnsp.data_ptr(),
-                           dpre.data_ptr(), dWp.data_ptr(), dbp.data_ptr(), dWn.data_ptr(), dbn.data_ptr(), int(acc),
-                           stream_handle())
+                           dpre.data_ptr(), part.data_ptr(), dWp.data_ptr(), dbp.data_ptr(), dWn.data_ptr(),
+                           dbn.data_ptr(), int(acc), stream_handle())
         if acc:
             return (dseq,) + (None,) * 13
         return (dseq, None, None, None, dWt, dbt, dg, db, dWdec, dbdec, dWp, dbp, dWn, dbn)

@@ -149,7 +149,10 @@ def planes_enabled():
     return _PLANES and _FP32 == "x6" and _MODE != "blas"
 
 
-_PLANES = os.environ.get("HETSEQ_GEMM_PLANES", "1") != "0"
+# fp32 GEMMs on pre-split planes are opt-in: on the BERT-base shapes the in-kernel-split engine is
+# faster for the forward / data-gradient products and the planes win only the weight gradients,
+# by less than the standalone split passes cost (profiles/r2_gemm_engines.md)
+_PLANES = os.environ.get("HETSEQ_GEMM_PLANES", "0") == "1"
 
 
 def split(x, out=None):
@@ -177,8 +180,10 @@ def _as_planes(x):
 
 
 def gemm_planes(a, b, ta, tb, out, bias=None, epi=EPI_NONE, beta=0.0, aux=None, part=None, colsum=None,
-                colsum_acc=False, ksplit=1):
-    """Launch the bf16-plane engine on Planes operands; False (nothing launched) if not served."""
+                colsum_acc=False, ksplit=1, variant=-1):
+    """Launch the bf16-plane engine on Planes operands; False (nothing launched) if not served.
+    ``variant``: kernel variant (gemm_planes.hip: 0 two LDS stages, 1 one stage, 2 half K depth,
+    3 eight waves, 4 eight waves + one stage); -1 = :func:`planes_variant` for the shape."""
     if a.P != b.P or not out.is_cuda or out.stride(1) != 1 or out.dtype not in (torch.float32, torch.bfloat16):
         return False
     M, N, K = _dims(a, b, ta, tb)
@@ -187,14 +192,26 @@ def gemm_planes(a, b, ta, tb, out, bias=None, epi=EPI_NONE, beta=0.0, aux=None, 
     slab = _slab(M, N, ksplit, out.device) if ksplit > 1 else None
     if ksplit > 1 and slab is None:
         ksplit = 1
+    if variant < 0:
+        variant = planes_variant(M, N, K, a.P, ta)
     rc = hip().gemm_planes(a.P, 1 if out.dtype == torch.bfloat16 else 0, int(ta), int(tb), M, N, K, a.data_ptr(),
                            a.ld, a.ps, b.data_ptr(), b.ld, b.ps, out.data_ptr(), out.stride(0),
                            bias.data_ptr() if bias is not None else 0, epi, float(beta),
                            aux.data_ptr() if aux is not None else 0, aux.stride(0) if aux is not None else 0,
                            part.data_ptr() if part is not None else 0, colsum.data_ptr() if colsum is not None else 0,
                            int(colsum_acc), int(ksplit), slab.data_ptr() if slab is not None else 0,
-                           slab.numel() if slab is not None else 0, stream_handle())
+                           slab.numel() if slab is not None else 0, int(variant), stream_handle())
     return rc == 0
+
+
+def planes_variant(M, N, K, P, ta):
+    """Default kernel variant per shape, from tools/bench_planes.py on MI355X (profiles/
+    r2_gemm_engines.md): one LDS stage (3 workgroups per CU) for the split-fp32 planes, except
+    the small-grid 768 x 768-class products (8 waves); bf16 sites are measured (gemm())."""
+    tiles = (M // 128) * (N // 128)
+    if tiles <= 256 and K <= 1024 and not ta:
+        return 3
+    return 1
 
 
 # split-K of the plane engine's weight gradients (K = tokens): slices so the tile grid covers the
@@ -211,6 +228,32 @@ def _planes_ksplit(M, N, K, P):
     while tiles * s < 384 and s < 8 and K % (2 * s * bk) == 0 and K // (2 * s) >= 512:
         s *= 2
     return s
+
+
+def _bf16_choice(key, pa, pb, ta, tb, out, bias, epi, beta, ks, out_dtype):
+    """bf16 operands: the plane engine (best measured variant) or the library, chosen per call site
+    by timing both once (auto mode; results in GEMM_CHOICES); 'hip' mode always takes the engine.
+    Returns ``out`` when the engine ran, None when the caller should use the library."""
+    if _MODE == "hip":
+        return out if gemm_planes(pa, pb, ta, tb, out, bias, epi, beta, ksplit=ks) else None
+    c = GEMM_CHOICES.get(key)
+    if c is None and not torch.cuda.is_current_stream_capturing():
+        scratch = out.clone() if beta != 0.0 else torch.empty_like(out)
+        best = None
+        for v in (0, 1, 3, 4):
+            if gemm_planes(pa, pb, ta, tb, scratch, bias, epi, beta, ksplit=ks, variant=v):
+                t = _bench(lambda: gemm_planes(pa, pb, ta, tb, scratch, bias, epi, beta, ksplit=ks, variant=v))
+                best = (t, v) if best is None or t < best[0] else best
+        a, b = pa.buf if pa.P == 1 else None, pb.buf if pb.P == 1 else None
+        t_blas = _bench(lambda: _blas_gemm(a, b, ta, tb, scratch, bias, epi, beta, out_dtype))
+        if best is None:
+            c = ("blas", None, round(t_blas, 4))
+        else:
+            c = ("hip" if best[0] < t_blas else "blas", round(best[0], 4), round(t_blas, 4), ks, best[1])
+        GEMM_CHOICES[key] = c
+    if c is None or c[0] != "hip":
+        return None
+    return out if gemm_planes(pa, pb, ta, tb, out, bias, epi, beta, ksplit=ks, variant=c[4]) else None
 
 
 def _dims(a, b, ta, tb):
@@ -312,9 +355,13 @@ def gemm(a, b, ta=False, tb=False, out=None, bias=None, epi=EPI_NONE, beta=0.0, 
             out = torch.empty((M, N), dtype=odt, device=pa.device)
         ks = ksplit if ksplit is not None else (_planes_ksplit(M, N, K, pa.P) if ta and epi == EPI_NONE
                                                 and out.dtype == torch.float32 else 1)
-        if gemm_planes(pa, pb, ta, tb, out, bias, epi, beta, ksplit=ks):
+        if pa.P == 3:
+            if gemm_planes(pa, pb, ta, tb, out, bias, epi, beta, ksplit=ks):
+                return out
+        elif _bf16_choice((M, N, K, ta, tb, epi, beta != 0.0, "bf16"), pa, pb, ta, tb, out, bias, epi, beta, ks,
+                          out_dtype) is not None:
             return out
-        a, b = _unplane(a), _unplane(b)  # a shape the plane engine does not serve
+        a, b = _unplane(a), _unplane(b)  # a shape the plane engine does not serve, or the library
     odt = out_dtype or a.dtype
     if out is None:
         out = torch.empty((M, N), dtype=odt, device=a.device)

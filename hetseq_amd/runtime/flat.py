@@ -80,10 +80,10 @@ class FlatParamStore(object):
                     self.params.append(q)
                     self.names.append(name_of[id(q)])
         self.shadow = None
+        self.planes = None  # [3, total] bf16 hi/mid/lo split of ``param`` (enable_planes)
         if shadow_dtype is not None:
             self.shadow = torch.empty(total, dtype=shadow_dtype, device=dev)
             self.sync_shadow()
-        self.planes = None  # [3, total] bf16 hi/mid/lo split of ``param`` (enable_planes)
 
     # ------------------------------------------------------------ views
     def offset(self, p):

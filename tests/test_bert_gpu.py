@@ -133,3 +133,35 @@ def test_base_model_param_count(cuda):
     m = BertForPreTraining(cfg)
     assert sum(p.numel() for p in m.parameters()) == 110106428
     assert len(m.state_dict()) == 207
+
+
+def test_fp32_plane_engine_matches_reference(cuda, monkeypatch):
+    """fp32 on the opt-in bf16-plane engine (HETSEQ_GEMM_PLANES=1: operands split once into
+    hi/mid/lo planes, weight planes refreshed by the optimizer) tracks the torch-op reference."""
+    from hetseq_amd.ops import gemm as G
+    from hetseq_amd.runtime.flat import FlatParamStore
+
+    monkeypatch.setattr(G, "_PLANES", True)
+    model, cfg = _tiny(cuda)
+    model.eval()
+    model.max_predictions_per_seq = 32  # 4 x 32 = 128 masked-LM rows: the transform GEMMs tile
+    ref = copy.deepcopy(model)
+    store = FlatParamStore(model)
+    model.attach_store(store, torch.float32)
+    assert store.planes is not None
+    batch = _batch(cuda, 4, 64, cfg.vocab_size, P=32)
+    l1 = model(*batch)
+    l2 = ref(*batch)
+    assert abs(l1.item() - l2.item()) < 1e-4 * abs(l2.item()) + 1e-5, (l1.item(), l2.item())
+    l1.backward()
+    l2.backward()
+    for (n, p1), (_, p2) in zip(model.named_parameters(), ref.named_parameters()):
+        d = (p1.grad - p2.grad).abs().max().item()
+        assert d <= 2e-3 * (p2.grad.abs().max().item() + 1e-6) + 1e-6, (n, d)
+    # the weight planes follow an in-place parameter update
+    with torch.no_grad():
+        store.param.mul_(0.5)
+    store.refresh_planes()
+    w = model.bert.encoder.layer[0].attention.output.dense.weight
+    pv = store.planes_view([w], tuple(w.shape)).unsplit()
+    assert torch.allclose(pv, w, rtol=2 ** -22, atol=0)

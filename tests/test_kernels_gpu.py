@@ -772,9 +772,10 @@ def test_pool_nsp_kernels_vs_fp64(cuda, dt, acc):
     base = [g.clone() for g in grads]
     dnsp = torch.empty(B, 2, device=cuda)
     dpre = torch.empty(B, H, device=cuda)
+    part = torch.empty(B, 8, H, device=cuda)
     hip().pool_nsp_bwd(dtype_code(seq), P(dl), P(seq), P(dseq), B, S, H, P(Wp), P(Wn), P(lab), P(pooled), P(logits),
-                       P(lse), P(stats), P(dnsp), P(dpre), P(grads[0]), P(grads[1]), P(grads[2]), P(grads[3]),
-                       int(acc), stream_handle())
+                       P(lse), P(stats), P(dnsp), P(dpre), P(part), P(grads[0]), P(grads[1]), P(grads[2]),
+                       P(grads[3]), int(acc), stream_handle())
     old_first = dseq0.view(B, S, H)[:, 0].double()
     expect = old_first + x.grad
     # bf16 dseq: the sum is rounded once to bf16 (relative 2^-8 of its magnitude)
@@ -839,11 +840,12 @@ def _planes_operand(x, P):
     return G.split(x.contiguous()) if P == 3 else G.Planes.of_bf16(x.bfloat16().contiguous())
 
 
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("P", [3, 1])
 @pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False)])
 @pytest.mark.parametrize("M,N,K,ks", [(256, 384, 512, 1), (640, 768, 768, 1), (384, 256, 1024, 4),
                                       (128, 128, 4096, 2)])
-def test_gemm_planes_vs_fp64(cuda, P, ta, tb, M, N, K, ks):
+def test_gemm_planes_vs_fp64(cuda, P, ta, tb, M, N, K, ks, variant):
     """The bf16-plane engine in both layouts of each operand (k-contiguous b128 reads and
     mn-contiguous transposed reads) and with split-K, against fp64.  P = 3 (fp32 as split bf16)
     must carry fp32-level error: within 2x of torch's own fp32 GEMM error; P = 1 is exact bf16
@@ -855,7 +857,13 @@ def test_gemm_planes_vs_fp64(cuda, P, ta, tb, M, N, K, ks):
     b = torch.randn((N, K) if tb else (K, N), device=cuda)
     pa, pb = _planes_operand(a, P), _planes_operand(b, P)
     out = torch.empty(M, N, device=cuda)
-    assert G.gemm_planes(pa, pb, ta, tb, out, ksplit=ks)
+    from hetseq_amd.ops._C import hip
+
+    hip().set_planes_variant(variant)  # (0 two LDS stages, 1 one stage, 2 half K depth)
+    try:
+        assert G.gemm_planes(pa, pb, ta, tb, out, ksplit=ks)
+    finally:
+        hip().set_planes_variant(0)
     ad, bd = (a.double(), b.double()) if P == 3 else (a.bfloat16().double(), b.bfloat16().double())
     ref = (ad.t() if ta else ad) @ (bd.t() if tb else bd)
     mag = (ad.abs().t() if ta else ad.abs()) @ (bd.abs().t() if tb else bd.abs())
