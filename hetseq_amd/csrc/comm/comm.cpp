@@ -72,6 +72,18 @@ ncclRedOp_t nccl_op(int code) {
 
 hipStream_t as_stream(uintptr_t h) { return reinterpret_cast<hipStream_t>(h); }
 
+size_t elem_size(int code) {
+  switch (code) {
+    case 0: return 4;
+    case 1: return 2;
+    case 2: return 8;
+    case 3: return 8;
+    case 4: return 1;
+    case 5: return 4;
+  }
+  throw std::invalid_argument("hetseq comm: unsupported dtype code");
+}
+
 class Comm {
  public:
   Comm(py::bytes uid, int nranks, int rank, int device, double timeout_s)
@@ -137,12 +149,31 @@ class Comm {
       give_event(e);  // recorded + waited: reusable once the comm stream passes it (ordered)
     }
     void* p = reinterpret_cast<void*>(ptr);
+    if (snap_dst_) {
+      // test mode: copy the bucket as it stands when the collective would read it (the copy is
+      // ordered exactly like the all-reduce: on the comm stream, behind the producer events)
+      if (ptr < snap_src_ || ptr + (uintptr_t)count * elem_size(dtype) > snap_src_ + snap_bytes_)
+        throw std::invalid_argument("hetseq comm: snapshot range outside the registered buffer");
+      hip_check(hipMemcpyAsync(reinterpret_cast<void*>(snap_dst_ + (ptr - snap_src_)), p,
+                               (size_t)count * elem_size(dtype), hipMemcpyDeviceToDevice, stream_),
+                "hipMemcpyAsync(snapshot)");
+      track(stream_);
+      return;
+    }
     {
       std::lock_guard<std::mutex> g(op_mu_);
       check();
       nccl_check(ncclAllReduce(p, p, (size_t)count, nccl_type(dtype), nccl_op(op), comm_, stream_), "ncclAllReduce");
     }
     track(stream_);
+  }
+
+  // Test hook (single-GPU ordering check): while set, all_reduce_async copies each bucket of
+  // [src, src + bytes) into the same offset of `dst` on the comm stream instead of reducing it.
+  void set_snapshot(uintptr_t dst, uintptr_t src, int64_t bytes) {
+    snap_dst_ = dst;
+    snap_src_ = src;
+    snap_bytes_ = (uintptr_t)bytes;
   }
 
   // The consumer stream waits for every collective issued on the comm stream so far.
@@ -213,6 +244,8 @@ class Comm {
   bool aborted() const { return aborted_.load(); }
 
  private:
+  uintptr_t snap_dst_ = 0, snap_src_ = 0, snap_bytes_ = 0;
+
   struct Pending {
     hipEvent_t ev;
     std::chrono::steady_clock::time_point t0;
@@ -343,6 +376,7 @@ PYBIND11_MODULE(_comm, m) {
       .def("check", &Comm::check)
       .def("close", &Comm::close, py::arg("graceful") = true)
       .def("inject_stall", &Comm::inject_stall)
+      .def("set_snapshot", &Comm::set_snapshot, py::arg("dst"), py::arg("src"), py::arg("bytes"))
       .def("outstanding", &Comm::outstanding)
       .def_property_readonly("stream", &Comm::stream)
       .def_property_readonly("rank", &Comm::rank)

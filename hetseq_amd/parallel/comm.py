@@ -73,6 +73,15 @@ class NativeComm(object):
         hs = [_stream(s) for s in producers] or [_stream()]
         self._c.all_reduce_async(t.data_ptr(), t.numel(), DTYPES[t.dtype], OPS[op], hs)
 
+    def set_snapshot(self, dst, src):
+        """Test mode: every all_reduce_async of a slice of ``src`` copies it into the same offsets
+        of ``dst`` on the comm stream instead (ordering check on one GPU); ``dst=None`` ends it."""
+        if dst is None:
+            self._c.set_snapshot(0, 0, 0)
+        else:
+            assert dst.numel() == src.numel() and dst.dtype == src.dtype
+            self._c.set_snapshot(dst.data_ptr(), src.data_ptr(), src.numel() * src.element_size())
+
     def wait(self, stream=None):
         """``stream`` (default current) waits for every collective issued on the comm stream."""
         self._c.wait(_stream(stream))

@@ -145,3 +145,64 @@ def test_flatddp_native_engine_matches_local(group):
     finally:
         streams.set_enabled(old)
     assert torch.equal(grads[0], grads[1])
+
+
+def _snapshot_run(group, gate_side_stream):
+    """Fused BERT backward through FlatDDP on the native engine in snapshot mode, with the
+    weight-gradient side stream delayed so an ungated bucket copy would see unfinished grads.
+    Returns (snapshot, final gradient, bucket ranges)."""
+    from hetseq_amd.parallel.ddp import FlatDDP
+    from hetseq_amd.runtime import streams
+    from hetseq_amd.runtime.flat import FlatParamStore
+    from tests.test_bert_gpu import _batch, _tiny
+
+    cuda = torch.device("cuda", 0)
+    model, cfg = _tiny(cuda)
+    model.eval()
+    model.max_predictions_per_seq = 10
+    store = FlatParamStore(model)
+    model.attach_store(store, torch.float32)
+    net = FlatDDP(model, store, bucket_cap_mb=0.25, comm_engine="native", timeout_s=60)
+    snap = torch.full_like(store.grad, float("nan"))
+    net.comm.set_snapshot(snap, store.grad)
+    orig_fork, orig_active = streams.fork, streams.active
+
+    def slow_fork(device, *tensors):  # every side-stream task starts ~1 ms late
+        s = orig_fork(device, *tensors)
+        with torch.cuda.stream(s):
+            torch.cuda._sleep(2_000_000)
+        return s
+
+    streams.fork = slow_fork
+    if not gate_side_stream:  # remove the side-stream producer event from the bucket launches
+        streams.active = lambda device: None
+    try:
+        batch = _batch(cuda, 4, 64, cfg.vocab_size)
+        store.grad.zero_()
+        net(*batch).backward()
+        torch.cuda.synchronize()
+    finally:
+        streams.fork, streams.active = orig_fork, orig_active
+        net.comm.set_snapshot(None, None)
+        net.comm.check()
+        net.comm.close()
+    return snap, store.grad.clone(), net.ranges
+
+
+def test_bucket_snapshots_equal_final_gradients(group):
+    """Every bucket, copied on the comm stream exactly when its all-reduce would read it, already
+    holds its final gradient: the producer events on BOTH streams (compute and weight-gradient)
+    gate the launch.  Control: without the side-stream event the same run snapshots unfinished
+    buckets, so this test would catch a missing producer event."""
+    from hetseq_amd.runtime import streams
+
+    old = streams.enabled()
+    streams.set_enabled(True)
+    try:
+        snap, grad, ranges = _snapshot_run(group, True)
+        for lo, hi in ranges:
+            assert torch.equal(snap[lo:hi], grad[lo:hi]), (lo, hi)
+        snap_bad, grad_bad, ranges = _snapshot_run(group, False)
+        assert any(not torch.equal(snap_bad[lo:hi], grad_bad[lo:hi]) for lo, hi in ranges)
+    finally:
+        streams.set_enabled(old)
