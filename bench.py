@@ -147,6 +147,7 @@ def main():
         torch.autograd.set_multithreading_enabled(False)  # backward on this thread, visible to cProfile
         prof = cProfile.Profile()
         prof.enable()
+    ms0 = torch.cuda.memory_stats()
     t0 = time.perf_counter()
     host = 0.0  # host time spent inside train_step (enqueue cost; < ms_per_step means GPU-bound)
     data_wait = 0.0  # host time blocked on the input pipeline
@@ -167,6 +168,10 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    ms1 = torch.cuda.memory_stats()
+    # device-level allocator events inside the timed loop (each hipMalloc / hipFree can stall the host)
+    alloc_events = {k: ms1.get(k, 0) - ms0.get(k, 0) for k in ("num_device_alloc", "num_device_free",
+                                                             "num_alloc_retries", "num_sync_all_streams")}
     t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -206,6 +211,7 @@ def main():
             "final_train_loss_logged": round(loss, 5),
             "host_ms_per_step": round(host / b.steps * 1000, 3),
             "data_wait_ms_per_step": round(data_wait / b.steps * 1000, 3),
+            "allocator_events": alloc_events,
             "gemm_choices": {str(k): v for k, v in list(G.GEMM_CHOICES.items())[:32]},
         }
         print(json.dumps(out), flush=True)

@@ -84,6 +84,132 @@ HS_DEVICE bfx8 frag2x4(const __bf16* p) {
 
 HS_DEVICE const float* bofs(const float* b, int off) { return b ? b + off : nullptr; }
 
+// ---- backward helpers (fp32 tiles in LDS, split into planes as fragments are read) ----
+constexpr int kBLD = 68;    // fp32 row stride of staged Q / dO / K / V rows: conflict-free b128 fragment reads
+constexpr int kBLS = 132;   // fp32 row stride of dS [query][key] and K^T [d][key] (fused kernel)
+
+// 8 consecutive fp32 of an LDS row (two b128 reads) -> hi/mid/lo fragment planes
+HS_DEVICE void lds_planes(const float* p, bfx8 (&f)[3]) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  split8(v, f[0], f[1], f[2]);
+}
+
+// k-step fragment of a transposed operand: column `col` of rows r0 + {0..3, 8..11} (the
+// accumulator-register order of a 16-row k-step) -> planes
+HS_DEVICE void lds_col_planes(const float* base, int r0, int col, bfx8 (&f)[3]) {
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = base[(r0 + (j & 3) + 8 * (j >> 2)) * kBLD + col];
+  split8(v, f[0], f[1], f[2]);
+}
+
+// rows [r0, r0 + n) of a head slice -> LDS (fp32, kBLD stride), (x + bias) * scale; 256 or 512
+// threads, 16 per row (4 floats each); rows past n are not written
+template <int NT>
+HS_DEVICE void stage_x6(float* lds, const float* base, int64_t ld, int r0, int n, const float* bias, float scale) {
+  const int c4 = (threadIdx.x & 15) * 4;
+  float4 bb = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (bias) bb = *reinterpret_cast<const float4*>(bias + c4);
+  constexpr int kPer = 128 * 16 / NT;
+  float4 v[kPer];
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    const int r = min((int)(threadIdx.x + i * NT) >> 4, n - 1);
+    v[i] = *reinterpret_cast<const float4*>(base + (int64_t)(r0 + r) * ld + c4);
+  }
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    const int r = (threadIdx.x + i * NT) >> 4;
+    if (r < n)
+      *reinterpret_cast<float4*>(lds + r * kBLD + c4) = make_float4((v[i].x + bb.x) * scale, (v[i].y + bb.y) * scale,
+                                                                    (v[i].z + bb.z) * scale, (v[i].w + bb.w) * scale);
+  }
+}
+
+// One 32-key x 32-query tile of the key-side backward (dK / dV), lane = key:
+//   S^T-tile sc[query][key] = Q K^T, dp = dO V^T (A = Q / dO rows from LDS, B = the lane's K / V row),
+//   P and dS = P o (dP o keep - D) in registers, then dV^T += dO^T P, dK^T += Q^T dS with the
+//   registers as the B operand and dO^T / Q^T gathered from the row-major LDS images.
+// Qs / Os: staged rows (Q scaled by 1/8), t: tile's first row in them; Lq / Dq / keep: per-row
+// lse, D and keep word of row t + i.  ds_out: optional dS sink (fused kernel), row stride kBLS.
+struct KeyTile {
+  const float* Qs;
+  const float* Os;
+  const float* Ls;
+  const float* Ds;
+  const uint32_t* Wd;  // keep word of (row, this wave's key word), stride wstride
+  int wstride;
+  float p, dscale;
+};
+
+HS_DEVICE void key_tile(const KeyTile& k, int t, const float (&kr)[4][8], const float (&vr)[4][8], float madd, int li,
+                        int hf, f32x16& dk0, f32x16& dk1, f32x16& dv0, f32x16& dv1, float* ds_out, int key) {
+  // one product at a time and P / dS built per k-step: the live fragments stay under the
+  // 256-VGPR budget of two waves per SIMD
+  f32x16 sc = {}, dp = {};
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    bfx8 a[3], bb[3];
+    lds_planes(k.Qs + (t + li) * kBLD + 16 * ks + 8 * hf, a);
+    split8(kr[ks], bb[0], bb[1], bb[2]);
+    sc = mma6(a, bb, sc);
+  }
+  __builtin_amdgcn_sched_barrier(0);  // bound the live fragments (no spills at 256 VGPRs)
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    bfx8 a[3], bb[3];
+    lds_planes(k.Os + (t + li) * kBLD + 16 * ks + 8 * hf, a);
+    split8(vr[ks], bb[0], bb[1], bb[2]);
+    dp = mma6(a, bb, dp);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    float pd[8], ds[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int r = 8 * ks + j, qi = t + xrow(r, hf);
+      const float pv = __expf(sc[r] + madd - k.Ls[qi]);
+      const float mk = k.p > 0.f ? (((k.Wd[qi * k.wstride] >> li) & 1u) ? k.dscale : 0.f) : 1.f;
+      pd[j] = pv * mk;
+      ds[j] = pv * (dp[r] * mk - k.Ds[qi]);
+      if (ds_out) ds_out[qi * kBLS + key] = ds[j];
+    }
+    bfx8 pb[3], a[3];
+    split8(pd, pb[0], pb[1], pb[2]);
+    const int q = t + 16 * ks + 4 * hf;
+    lds_col_planes(k.Os, q, li, a);
+    dv0 = mma6(a, pb, dv0);
+    lds_col_planes(k.Os, q, 32 + li, a);
+    dv1 = mma6(a, pb, dv1);
+    split8(ds, pb[0], pb[1], pb[2]);
+    lds_col_planes(k.Qs, q, li, a);
+    dk0 = mma6(a, pb, dk0);
+    lds_col_planes(k.Qs, q, 32 + li, a);
+    dk1 = mma6(a, pb, dk1);
+  }
+}
+
+// the lane's K / V row halves in fragment order: r[s][j] = row[16 s + 8 hf + j] (+ bias)
+HS_DEVICE void row_frags(const float* row, const float* bias, int hf, float (&r)[4][8]) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) ld8(row + 16 * s + 8 * hf, bias ? bias + 16 * s + 8 * hf : nullptr, 1.f, r[s]);
+}
+
+// 16 accumulator registers of two 32x32 C tiles (rows d = crow, lane column) -> 64 fp32 of a
+// token row: out[d] for d = 8g + 4hf + (0..3), out[32 + d]
+HS_DEVICE void store_rows(float* out, const f32x16& c0, const f32x16& c1, int hf, float scale) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int d = 8 * g + 4 * hf;
+    *reinterpret_cast<float4*>(out + d) =
+        make_float4(c0[4 * g] * scale, c0[4 * g + 1] * scale, c0[4 * g + 2] * scale, c0[4 * g + 3] * scale);
+    *reinterpret_cast<float4*>(out + 32 + d) =
+        make_float4(c1[4 * g] * scale, c1[4 * g + 1] * scale, c1[4 * g + 2] * scale, c1[4 * g + 3] * scale);
+  }
+}
+
 }  // namespace
 
 __global__ void __launch_bounds__(256, 2)
@@ -230,9 +356,297 @@ __global__ void __launch_bounds__(256, 2)
   if (hf == 0) lse[(int64_t)bh * S + q0 + li] = m + __logf(l);
 }
 
+// ---------------------------------------------------------------------------
+// Backward, fp32 operands as split-bf16 products (the forward's scheme; reference
+// bert_modeling.py:361-376).  Staged tiles stay fp32 in LDS (the most compact image: one
+// plane set would take 1.5x the bytes) and every fragment is split into hi/mid/lo planes in
+// registers as it is read, so a 32x32 product costs 6 x 2 bf16 MFMAs per 16-deep k-step
+// (24 x 32 cycles per 64-deep tile) instead of 32 exact-fp32 v_mfma_f32_32x32x2_f32 (2048).
+//
+// Fused, S <= 128: one block (8 waves) per (batch, head), the x6 counterpart of
+// attn_bwd_fused_kernel (attention.hip): phase 1 wave (kg = w & 3, half = w >> 2) runs key_tile
+// over query tiles {64 half, 64 half + 32} for keys 32 kg.. and stores dS [query][key]; phase 2
+// dQ^T = K^T dS^T for queries 32 kg.. over keys 64 half.. with K^T staged from the registers;
+// waves 4..7 hand their partials to waves 0..3 (fixed order).  LDS 140 KB, one block per CU.
+__global__ void __launch_bounds__(512, 1)
+    attn_bwd_fused_x6_kernel(const float* __restrict__ qkv, const int64_t* __restrict__ mask,
+                             const float* __restrict__ bqkv, const float* __restrict__ ctx,
+                             const float* __restrict__ dctx, const float* __restrict__ lse, float* __restrict__ dqkv,
+                             int S, int NH, float p, const uint32_t* __restrict__ dmask) {
+  __shared__ __attribute__((aligned(16))) float QKs[128 * kBLD];  // Q rows; K^T [64][kBLS] in phase 2
+  __shared__ __attribute__((aligned(16))) float Os[128 * kBLD];   // dO rows; then dQ partials
+  __shared__ __attribute__((aligned(16))) float dSs[128 * kBLS];  // dS; then dK / dV partials
+  __shared__ float Ls[128];
+  __shared__ float Ds[128];
+  __shared__ uint32_t Wd[128][4];
+  static_assert(64 * kBLS <= 128 * kBLD, "K^T image fits the Q region");
+  const int H = NH * kXD;
+  const int64_t ld = 3 * (int64_t)H;
+  const int bh = blockIdx.x, b = bh / NH, h = bh % NH;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hf = lane >> 5, li = lane & 31;
+  const int g4 = w & 3, half = w >> 2;
+  const bool kactive = 32 * g4 < S;
+  const int key = 32 * g4 + li;
+  const float* rows = qkv + (int64_t)b * S * ld;
+  const float* drows = dctx + (int64_t)b * S * H;
+
+  stage_x6<512>(QKs, rows + h * kXD, ld, 0, S, bofs(bqkv, h * kXD), 0.125f);
+  stage_x6<512>(Os, drows + h * kXD, H, 0, S, nullptr, 1.f);
+  for (int i = threadIdx.x; i < S; i += blockDim.x) Ls[i] = lse[(int64_t)bh * S + i];
+  if (p > 0.f)
+    for (int i = threadIdx.x; i < S * (S >> 5); i += blockDim.x)
+      Wd[i / (S >> 5)][i % (S >> 5)] = dmask[((uint64_t)bh * S) * (uint64_t)(S >> 5) + i];
+  float kr[4][8], vr[4][8];
+  float madd = 0.f;
+  if (kactive) {
+    row_frags(rows + (int64_t)key * ld + H + h * kXD, bofs(bqkv, H + h * kXD), hf, kr);
+    row_frags(rows + (int64_t)key * ld + 2 * H + h * kXD, bofs(bqkv, 2 * H + h * kXD), hf, vr);
+    madd = (1.f - (float)mask[(int64_t)b * S + key]) * -10000.f;
+  }
+  {  // D = rowsum(dO o O), 4 threads per query row
+    const int r = threadIdx.x >> 2, qtr = threadIdx.x & 3;
+    float dsum = 0.f;
+    if (r < S) {
+      const float* orow = ctx + ((int64_t)b * S + r) * H + h * kXD + qtr * 16;
+      const float* grow = drows + (int64_t)r * H + h * kXD + qtr * 16;
+#pragma unroll
+      for (int c = 0; c < 16; c += 4) {
+        const float4 o = *reinterpret_cast<const float4*>(orow + c), g = *reinterpret_cast<const float4*>(grow + c);
+        dsum = fmaf(g.x, o.x, fmaf(g.y, o.y, fmaf(g.z, o.z, fmaf(g.w, o.w, dsum))));
+      }
+    }
+    dsum += __shfl_xor(dsum, 1, 64);
+    dsum += __shfl_xor(dsum, 2, 64);
+    if (r < S && qtr == 0) Ds[r] = dsum;
+  }
+  __syncthreads();
+
+  // ---- phase 1
+  f32x16 dk0 = {}, dk1 = {}, dv0 = {}, dv1 = {};
+  if (kactive) {
+    const KeyTile kt{QKs, Os, Ls, Ds, &Wd[0][g4], 4, p, drop_scale16(drop_thr16(p))};
+    for (int t = 64 * half; t < min(S, 64 * half + 64); t += 32)
+      key_tile(kt, t, kr, vr, madd, li, hf, dk0, dk1, dv0, dv1, dSs, key);
+  }
+  __syncthreads();  // Q, dO consumed; dS complete
+  if (kactive && half == 0)  // K^T [d][key] from the lanes' K rows
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) QKs[(16 * s + 8 * hf + j) * kBLS + key] = kr[s][j];
+  __syncthreads();
+
+  // ---- phase 2: dQ^T partial for queries 32 g4.. over keys 64 half..
+  f32x16 dq0 = {}, dq1 = {};
+  if (kactive) {
+    const float* dsr = dSs + (32 * g4 + li) * kBLS + 8 * hf;
+    for (int k0 = 64 * half; k0 < min(S, 64 * half + 64); k0 += 16) {
+      bfx8 bq[3], a[3];
+      lds_planes(dsr + k0, bq);
+      lds_planes(QKs + li * kBLS + k0 + 8 * hf, a);
+      dq0 = mma6(a, bq, dq0);
+      lds_planes(QKs + (32 + li) * kBLS + k0 + 8 * hf, a);
+      dq1 = mma6(a, bq, dq1);
+    }
+  }
+  __syncthreads();  // LDS free for the hand-off
+
+  // ---- combine (fixed order) and store
+  float* xq = Os + g4 * 64 * 32 + lane;
+  float* xk = dSs + g4 * 64 * 64 + lane;
+  if (half == 1 && kactive) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      xq[64 * r] = dq0[r];
+      xq[64 * (16 + r)] = dq1[r];
+      xk[64 * r] = dk0[r];
+      xk[64 * (16 + r)] = dk1[r];
+      xk[64 * (32 + r)] = dv0[r];
+      xk[64 * (48 + r)] = dv1[r];
+    }
+  }
+  __syncthreads();
+  if (half == 1 || !kactive) return;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    dq0[r] += xq[64 * r];
+    dq1[r] += xq[64 * (16 + r)];
+    dk0[r] += xk[64 * r];
+    dk1[r] += xk[64 * (16 + r)];
+    dv0[r] += xk[64 * (32 + r)];
+    dv1[r] += xk[64 * (48 + r)];
+  }
+  float* out = dqkv + ((int64_t)b * S + key) * ld + h * kXD;  // key == query index 32 g4 + li
+  store_rows(out, dq0, dq1, hf, 0.125f);
+  store_rows(out + H, dk0, dk1, hf, 1.f);
+  store_rows(out + 2 * H, dv0, dv1, hf, 1.f);
+}
+
+// S > 128, kernel 1 of 2: dQ for 32 queries per wave (lane = query) over 128-key chunks of
+// K / V staged fp32 in LDS; also writes D = rowsum(dO o O) for kernel 2.
+//   sc[key][query] = K Q^T, dp = V dO^T (A = K / V rows from LDS, B = the lane's Q / dO row);
+//   dQ^T += K^T dS^T (A gathered from the K rows, B = the dS registers).
+__global__ void __launch_bounds__(256, 2)
+    attn_bwd_dq_x6_kernel(const float* __restrict__ qkv, const int64_t* __restrict__ mask,
+                          const float* __restrict__ bqkv, const float* __restrict__ ctx,
+                          const float* __restrict__ dctx, const float* __restrict__ lse, float* __restrict__ Dout,
+                          float* __restrict__ dqkv, int S, int NH, float p, const uint32_t* __restrict__ dmask) {
+  __shared__ __attribute__((aligned(16))) float Ks[128 * kBLD];
+  __shared__ __attribute__((aligned(16))) float Vs[128 * kBLD];
+  __shared__ float Ms[128];
+  const int H = NH * kXD;
+  const int64_t ld = 3 * (int64_t)H;
+  const int bh = blockIdx.y, b = bh / NH, h = bh % NH;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hf = lane >> 5, li = lane & 31;
+  const int q0 = blockIdx.x * 128 + w * 32;
+  const bool active = q0 < S;
+  const float* rows = qkv + (int64_t)b * S * ld;
+  const float dscale = drop_scale16(drop_thr16(p));
+
+  float qr[4][8], dor[4][8];
+  float dsum = 0.f, lq = 0.f;
+  if (active) {
+    const int64_t tok = (int64_t)b * S + q0 + li;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int d = 16 * s + 8 * hf;
+      ld8(rows + (int64_t)(q0 + li) * ld + h * kXD + d, bofs(bqkv, h * kXD + d), 0.125f, qr[s]);
+      ld8(dctx + tok * H + h * kXD + d, nullptr, 1.f, dor[s]);
+      float o[8];
+      ld8(ctx + tok * H + h * kXD + d, nullptr, 1.f, o);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dsum = fmaf(dor[s][j], o[j], dsum);
+    }
+    dsum += __shfl_xor(dsum, 32, 64);
+    if (hf == 0) Dout[(int64_t)bh * S + q0 + li] = dsum;
+    lq = lse[(int64_t)bh * S + q0 + li];
+  }
+  f32x16 dq0 = {}, dq1 = {};
+  for (int c0 = 0; c0 < S; c0 += 128) {
+    const int clen = min(128, S - c0);
+    __syncthreads();
+    stage_x6<256>(Ks, rows + H + h * kXD, ld, c0, clen, bofs(bqkv, H + h * kXD), 1.f);
+    stage_x6<256>(Vs, rows + 2 * H + h * kXD, ld, c0, clen, bofs(bqkv, 2 * H + h * kXD), 1.f);
+    for (int i = threadIdx.x; i < clen; i += blockDim.x) Ms[i] = (1.f - (float)mask[(int64_t)b * S + c0 + i]) * -10000.f;
+    __syncthreads();
+    if (!active) continue;
+    for (int t = 0; t < clen; t += 32) {
+      f32x16 sc = {}, dp = {};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        bfx8 a[3], bb[3];
+        lds_planes(Ks + (t + li) * kBLD + 16 * ks + 8 * hf, a);
+        split8(qr[ks], bb[0], bb[1], bb[2]);
+        sc = mma6(a, bb, sc);
+      }
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        bfx8 a[3], bb[3];
+        lds_planes(Vs + (t + li) * kBLD + 16 * ks + 8 * hf, a);
+        split8(dor[ks], bb[0], bb[1], bb[2]);
+        dp = mma6(a, bb, dp);
+      }
+      const uint32_t word = p > 0.f ? dmask[((uint64_t)bh * S + q0 + li) * (uint64_t)(S >> 5) + ((c0 + t) >> 5)] : 0u;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        float ds[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int r = 8 * ks + j, kj = xrow(r, hf);
+          const float mk = p > 0.f ? (((word >> kj) & 1u) ? dscale : 0.f) : 1.f;
+          const float pv = __expf(sc[r] + Ms[t + kj] - lq);
+          ds[j] = pv * (dp[r] * mk - dsum);
+        }
+        bfx8 sb[3], a[3];
+        split8(ds, sb[0], sb[1], sb[2]);
+        const int kk = t + 16 * ks + 4 * hf;
+        lds_col_planes(Ks, kk, li, a);
+        dq0 = mma6(a, sb, dq0);
+        lds_col_planes(Ks, kk, 32 + li, a);
+        dq1 = mma6(a, sb, dq1);
+      }
+    }
+  }
+  if (!active) return;
+  store_rows(dqkv + ((int64_t)b * S + q0 + li) * ld + h * kXD, dq0, dq1, hf, 0.125f);
+}
+
+// S > 128, kernel 2 of 2: dK / dV for 32 keys per wave (lane = key) over 128-query chunks of
+// Q (biased, * 1/8) and dO staged fp32 in LDS (key_tile per 32-query tile).
+__global__ void __launch_bounds__(256, 2)
+    attn_bwd_dkv_x6_kernel(const float* __restrict__ qkv, const int64_t* __restrict__ mask,
+                           const float* __restrict__ bqkv, const float* __restrict__ dctx,
+                           const float* __restrict__ lse, const float* __restrict__ Dd, float* __restrict__ dqkv, int S,
+                           int NH, float p, const uint32_t* __restrict__ dmask) {
+  __shared__ __attribute__((aligned(16))) float Qs[128 * kBLD];
+  __shared__ __attribute__((aligned(16))) float Os[128 * kBLD];
+  __shared__ float Ls[128];
+  __shared__ float Ds[128];
+  __shared__ uint32_t Wd[128][4];  // keep words of the chunk's queries for this block's 4 key words
+  const int H = NH * kXD;
+  const int64_t ld = 3 * (int64_t)H;
+  const int bh = blockIdx.y, b = bh / NH, h = bh % NH;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hf = lane >> 5, li = lane & 31;
+  const int k0 = blockIdx.x * 128 + w * 32;
+  const bool active = k0 < S;
+  const int key = k0 + li;
+  const float* rows = qkv + (int64_t)b * S * ld;
+  const float* drows = dctx + (int64_t)b * S * H;
+
+  float kr[4][8], vr[4][8];
+  float madd = 0.f;
+  if (active) {
+    row_frags(rows + (int64_t)key * ld + H + h * kXD, bofs(bqkv, H + h * kXD), hf, kr);
+    row_frags(rows + (int64_t)key * ld + 2 * H + h * kXD, bofs(bqkv, 2 * H + h * kXD), hf, vr);
+    madd = (1.f - (float)mask[(int64_t)b * S + key]) * -10000.f;
+  }
+  f32x16 dk0 = {}, dk1 = {}, dv0 = {}, dv1 = {};
+  const KeyTile kt{Qs, Os, Ls, Ds, &Wd[0][w], 4, p, drop_scale16(drop_thr16(p))};
+  for (int c0 = 0; c0 < S; c0 += 128) {
+    const int clen = min(128, S - c0);
+    __syncthreads();
+    stage_x6<256>(Qs, rows + h * kXD, ld, c0, clen, bofs(bqkv, h * kXD), 0.125f);
+    stage_x6<256>(Os, drows + h * kXD, H, c0, clen, nullptr, 1.f);
+    for (int i = threadIdx.x; i < clen; i += blockDim.x) {
+      Ls[i] = lse[(int64_t)bh * S + c0 + i];
+      Ds[i] = Dd[(int64_t)bh * S + c0 + i];
+    }
+    if (p > 0.f)
+      for (int i = threadIdx.x; i < clen * 4; i += blockDim.x) {
+        const int qi = i >> 2, kw = blockIdx.x * 4 + (i & 3);
+        Wd[qi][i & 3] = kw < (S >> 5) ? dmask[((uint64_t)bh * S + c0 + qi) * (uint64_t)(S >> 5) + kw] : 0u;
+      }
+    __syncthreads();
+    if (!active) continue;
+    for (int t = 0; t < clen; t += 32) key_tile(kt, t, kr, vr, madd, li, hf, dk0, dk1, dv0, dv1, nullptr, key);
+  }
+  if (!active) return;
+  float* out = dqkv + ((int64_t)b * S + key) * ld + h * kXD;
+  store_rows(out + H, dk0, dk1, hf, 1.f);
+  store_rows(out + 2 * H, dv0, dv1, hf, 1.f);
+}
+
 }  // namespace hs
 
 using namespace hs;
+
+// fused S <= 128 (grid B*NH x 512) or the dQ / dKV pair (grid (S/128, B*NH) x 256 each)
+int launch_attn_bwd_x6(const float* qkv, const int64_t* mask, const float* bqkv, const float* ctx, const float* dctx,
+                       const float* lse, float* Dbuf, float* dqkv, const uint32_t* dmask, int B, int S, int NH,
+                       int D, float p, bool fused, hipStream_t st) {
+  if (D != kXD || S % 32 != 0 || S <= 0 || (p > 0.f && dmask == nullptr)) return -1;
+  if (fused && S <= 128) {
+    hipLaunchKernelGGL(attn_bwd_fused_x6_kernel, dim3(B * NH), dim3(512), 0, st, qkv, mask, bqkv, ctx, dctx, lse, dqkv,
+                       S, NH, p, dmask);
+    return 0;
+  }
+  dim3 grid((S + 127) / 128, B * NH);
+  hipLaunchKernelGGL(attn_bwd_dq_x6_kernel, grid, dim3(256), 0, st, qkv, mask, bqkv, ctx, dctx, lse, Dbuf, dqkv, S, NH,
+                     p, dmask);
+  hipLaunchKernelGGL(attn_bwd_dkv_x6_kernel, grid, dim3(256), 0, st, qkv, mask, bqkv, dctx, lse, Dbuf, dqkv, S, NH, p,
+                     dmask);
+  return 0;
+}
 
 int launch_attn_fwd_x6(const float* qkv, const int64_t* mask, const float* bqkv, float* ctx, float* lse,
                        uint32_t* dmask, int B, int S, int NH, int D, float p, uint64_t seed, uint64_t off,

@@ -403,11 +403,14 @@ HS_DEVICE bfx8 x_frag(const char* __restrict__ S, int row, int p, int ks, int lr
 // WV = 4: 2x2 waves of 64x64, every thread stages 4x4 of A and of B.
 // WV = 8: 2x4 waves of 64x32 (twice the waves per CU to hide each other's staging), threads
 //         0-255 stage A and 256-511 stage B with the same 4x4 micro-blocks.
-template <bool TA, bool TB, int EPI, int NT, int ABL = 0, int WV = 4, int NBUF = 1, bool EDGE = false>
+// PF (4 waves, single buffer): register prefetch depth -- 1 = the next K tile, loaded under the
+// MFMAs of this one; 2 = two register sets, each tile's loads issued two tiles ahead.
+template <bool TA, bool TB, int EPI, int NT, int ABL = 0, int WV = 4, int NBUF = 1, bool EDGE = false, int PF = 1>
 __global__ void __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(NBUF == 2 ? 2 : WV / 2, NBUF == 2 ? 2 : WV / 2))) gemm_x6s_kernel(GemmArgs p) {
   constexpr int BM = 128, BN = 128, WC = WV / 2, TM = 2, TN = BN / WC / 32;
   static_assert(NBUF == 1 || WV == 8, "double-buffered images: 8-wave variant only");
   static_assert(!EDGE || (WV == 4 && EPI <= kEpiBias), "edge-masked launches: 4 waves, plain / bias epilogue");
+  static_assert(PF == 1 || (WV == 4 && NBUF == 1 && !EDGE), "two-deep prefetch: 4-wave, single-buffer, unmasked");
   __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * 128 * XROW];
   char* const As = smem;
   char* const Bs = smem + 128 * XROW;
@@ -535,6 +538,39 @@ __global__ void __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(NB
       if (ABL < 3) __syncthreads();
     }
     if (kt < KT) compute([] {}, As, Bs);  // odd tile count: the last tile is already in buffer 0
+  } else if constexpr (PF == 2) {
+    // LDS = tile kt, (va, vb) = kt+1, (wa, wb) = kt+2: a tile's loads are issued right after the
+    // set that will hold it is staged, so their latency spans two compute phases.  Unrolled by two
+    // so the register sets keep fixed roles; loads past the end re-read the last tile (clamped).
+    float4 wa[4], wb[4];
+    auto ldt = [&](float4(&xa)[4], float4(&xb)[4], int t) {
+      const int64_t tt = min(t, KT - 1);
+      x_load<!TA>(ab + tt * sa, oa, xa);
+      x_load<TB>(bb + tt * sb, ob, xb);
+    };
+    auto stt = [&](const float4(&xa)[4], const float4(&xb)[4]) {
+      x_store<!TA, NT>(As, xa, st);
+      x_store<TB, NT>(Bs, xb, st);
+    };
+    ldt(va, vb, 0);
+    stt(va, vb);
+    __syncthreads();
+    ldt(va, vb, 1);
+    ldt(wa, wb, 2);
+    int kt = 0;
+    for (; kt + 1 < KT; kt += 2) {
+      compute([] {}, As, Bs);
+      __syncthreads();
+      stt(va, vb);
+      ldt(va, vb, kt + 3);
+      __syncthreads();
+      compute([] {}, As, Bs);
+      __syncthreads();
+      stt(wa, wb);
+      ldt(wa, wb, kt + 4);
+      __syncthreads();
+    }
+    if (kt < KT) compute([] {}, As, Bs);  // odd tile count: the last tile is staged already
   } else {
     load();
     store();
@@ -564,6 +600,12 @@ static int g_ablation = 0;  // microbenchmark hook (tile_override bits 3-4)
 // twice the waves hide its transposing staging; measured +8-12%), 4 elsewhere (the 8-wave
 // dgrad needs 160 VGPRs = one block per CU, -25%).  tile_override bit 5 forces 4, bit 6 forces 8.
 static int g_x6_waves = 4;
+// 4-wave register prefetch depth (PF above): HETSEQ_X6_PF=1/2, tile_override bit 7 forces 2
+static const int g_x6_pf_env = [] {
+  const char* e = std::getenv("HETSEQ_X6_PF");
+  return e && e[0] == '2' ? 2 : 1;
+}();
+static int g_x6_pf = 1;
 // 8-wave variant with double-buffered LDS images (106 KB: one block per CU, one barrier per K
 // tile) -- HETSEQ_X6_DBUF=1; default single buffer (53 KB, blocks of other kernels co-reside).
 static const int g_x6_dbuf = [] {
@@ -617,6 +659,8 @@ void launch_cfg(const GemmArgs& a, hipStream_t st) {
         hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 2, 4>), dim3(blocks), dim3(256), 0, st, a);
       else if (EPI == kEpiNone && g_ablation == 3)
         hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 3, 4>), dim3(blocks), dim3(256), 0, st, a);
+      else if (g_x6_pf == 2)
+        hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 0, 4, 1, false, 2>), dim3(blocks), dim3(256), 0, st, a);
       else
         hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 0, 4>), dim3(blocks), dim3(256), 0, st, a);
     } else if (g_x6_dbuf) {
@@ -732,6 +776,7 @@ int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, i
   g_ablation = tile_override >= 0 ? (tile_override >> 3) & 3 : 0;
   g_x6_waves = tile_override >= 0 && (tile_override & 32) ? 4 : tile_override >= 0 && (tile_override & 64) ? 8
                                                               : ta ? 8 : 4;
+  g_x6_pf = tile_override >= 0 && (tile_override & 128) ? 2 : g_x6_pf_env;
   tile_override = tile_override >= 0 ? (tile_override & 3) : -1;
   if (tile_override >= 0) {  // benchmarking hook: force a tile shape (must divide the problem)
     const int bm = tile_override == 2 ? 64 : 128, bn = tile_override == 0 ? 128 : 64;

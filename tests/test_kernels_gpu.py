@@ -228,6 +228,44 @@ def test_attention_fwd_x6_fp32_level(cuda, B, S, NH, p):
         assert e6 <= 2 * e32 + 1e-7, (e6, e32)
 
 
+@pytest.mark.parametrize("B,S,NH,p", [(2, 128, 12, 0.0), (2, 96, 2, 0.1), (1, 512, 2, 0.0), (2, 192, 2, 0.1),
+                                       (3, 64, 4, 0.1), (2, 256, 12, 0.0)])
+@pytest.mark.parametrize("fused", [True, False])
+def test_attention_bwd_x6_fp32_level(cuda, B, S, NH, p, fused, monkeypatch):
+    """fp32 backward on split-bf16 products (fused S <= 128 and the dQ / dKV pair) against the
+    exact-fp32 MFMA backward on the same forward, and against fp64 autograd: error at the
+    exact-fp32 kernel's level."""
+    from hetseq_amd.ops import bert_ops
+    from hetseq_amd.ops._C import hip
+
+    if not fused:
+        monkeypatch.setenv("HETSEQ_ATTN_BWD", "split")
+    torch.manual_seed(32 + S)
+    H = NH * 64
+    qkv = torch.randn(B * S, 3 * H, device=cuda)
+    bias = torch.randn(3 * H, device=cuda) * 0.1
+    mask = torch.ones(B, S, dtype=torch.int64, device=cuda)
+    mask[-1, S // 3:] = 0
+    old = hip().attn_fp32_mode()
+    try:
+        hip().set_attn_fp32_mode(0)
+        out, saved = bert_ops.attn_fwd(qkv, mask, B, S, NH, p, 3, 11, bias=bias)
+        dout = torch.randn_like(out)
+        g32 = bert_ops.attn_bwd(qkv, mask, out, dout, saved, B, S, NH, p, bias=bias)
+        hip().set_attn_fp32_mode(1)
+        g6 = bert_ops.attn_bwd(qkv, mask, out, dout, saved, B, S, NH, p, bias=bias)
+    finally:
+        hip().set_attn_fp32_mode(old)
+    torch.cuda.synchronize()
+    _close(g6, g32, 1e-4, 1e-6, "x6 vs exact-fp32 attention backward")
+    keep = _keep_mask(saved[1], B * NH, S) if p > 0 else None
+    x = (qkv.double() + bias.double()).requires_grad_()
+    _ref_attention_drop(x, mask, B, S, NH, keep, p).backward(dout.double())
+    e6 = float((g6.double() - x.grad).abs().max())
+    e32 = float((g32.double() - x.grad).abs().max())
+    assert e6 <= 2 * e32 + 1e-7, (e6, e32)
+
+
 @pytest.mark.parametrize("B,S,NH", [(2, 128, 12), (2, 96, 2), (1, 512, 2)])
 def test_attention_fwd_bf16_mfma(cuda, B, S, NH, monkeypatch):
     """bf16 matrix-core forward vs an fp64 reference on the same bf16 inputs (+ bias), and vs the fp32-MFMA path."""
