@@ -40,6 +40,7 @@ int launch_emb_bwd(int, const void*, const float*, const float*, const float*, c
                    const int64_t*, float*, int, int, float, u64, u64, hipStream_t);
 void launch_colpart_finalize(const float* const*, float* const*, int, int, int, int, hipStream_t);
 int launch_segsum_rows(const float*, const int64_t*, const int64_t*, float*, float*, int, int, int, hipStream_t);
+int launch_sort_keys(const int64_t*, int, int64_t, int64_t*, int64_t*, hipStream_t);
 int launch_pos_grad(const float*, float*, int, int, int, hipStream_t);
 // elementwise.hip
 void launch_bias_gelu_fwd(int, const void*, const float*, void*, int64_t, int, hipStream_t);
@@ -185,6 +186,10 @@ PYBIND11_MODULE(_hip, m) {
                          P(float*, pt), rows, H, p, seed, off, ST(st)),
           "emb_bwd");
   });
+  m.def("sort_keys", [](i64 keys, int n, i64 bound, i64 out_keys, i64 out_order, i64 st) {
+    (void)hipGetLastError();
+    return launch_sort_keys(P(const int64_t*, keys), n, bound, P(int64_t*, out_keys), P(int64_t*, out_order), ST(st));
+  }, "stable sort of n int64 keys in [0, bound): sorted keys + source indices; -1 = unsupported size");
   m.def("segsum_rows", [](i64 src, i64 order, i64 keys, i64 scratch, i64 dst, int n, int H, int K, i64 st) {
     (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
     check(launch_segsum_rows(P(const float*, src), P(const int64_t*, order), P(const int64_t*, keys),

@@ -314,6 +314,48 @@ int launch_segsum_rows(const float* src, const int64_t* order, const int64_t* ke
   return 0;
 }
 
+// Stable key sort for the embedding backward's sorted-run gradient sums (replaces torch.sort).
+// Every element's output slot is its rank: the number of composite words (key << ib) | index
+// (ib = bits of n - 1; unique, so the order is total and stable) smaller than its own.  A block
+// ranks 64 elements; its 4 waves each count over a quarter of all n words (broadcast LDS reads)
+// and the quarter counts are summed (integers: exact in any order).  O(n^2) compares, but n is
+// a batch's token count: 4096 -> 64 blocks of 1024 compares per thread, a few microseconds.
+// n <= 16384 and key bits + index bits <= 32; other sizes return -1 (library sort fallback).
+constexpr int kSortMax = 16384;
+
+__global__ void __launch_bounds__(256) sort_keys_kernel(const int64_t* __restrict__ keys, int n, int ib,
+                                                        int64_t* __restrict__ out_keys,
+                                                        int64_t* __restrict__ out_order) {
+  __shared__ uint32_t s[kSortMax];
+  __shared__ int part[4][64];
+  for (int i = threadIdx.x; i < n; i += blockDim.x) s[i] = (static_cast<uint32_t>(keys[i]) << ib) | static_cast<uint32_t>(i);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + lane;
+  const uint32_t me = i < n ? s[i] : 0u;
+  const int q = (n + 3) / 4, j0 = w * q, j1 = min(n, j0 + q);
+  int cnt = 0;
+  for (int j = j0; j < j1; ++j) cnt += s[j] < me ? 1 : 0;
+  part[w][lane] = cnt;
+  __syncthreads();
+  if (w == 0 && i < n) {
+    const int r = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
+    out_keys[r] = static_cast<int64_t>(me >> ib);
+    out_order[r] = static_cast<int64_t>(i);
+  }
+}
+
+int launch_sort_keys(const int64_t* keys, int n, int64_t key_bound, int64_t* out_keys, int64_t* out_order,
+                     hipStream_t st) {
+  if (n <= 0 || n > kSortMax || key_bound <= 0) return -1;
+  int ib = 0, kb = 0;
+  while ((1 << ib) < n) ++ib;
+  while ((int64_t(1) << kb) < key_bound) ++kb;
+  if (ib + kb > 32) return -1;
+  hipLaunchKernelGGL(sort_keys_kernel, dim3((n + 63) / 64), dim3(256), 0, st, keys, n, ib, out_keys, out_order);
+  return 0;
+}
+
 int launch_pos_grad(const float* dx, float* dpos, int B, int S, int H, hipStream_t st) {
   if (H % 4 != 0) return -1;
   hipLaunchKernelGGL(pos_grad_kernel, dim3(S), dim3(std::min(256, ((H / 4 + 63) / 64) * 64)), 0, st, dx, dpos, B, S,

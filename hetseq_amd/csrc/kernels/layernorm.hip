@@ -15,6 +15,8 @@
 // Backward kernels produce the row gradient and per-block column partials of
 // dgamma/dbeta/dbias; `colpart_finalize` reduces the partials (no atomics,
 // deterministic).  Dropout masks are regenerated from Philox (seed, offset).
+#include <cstdlib>
+
 #include "common.h"
 #include "reduce.h"
 
@@ -98,84 +100,115 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const T* __restrict__ a, co
   }
 }
 
-// Column partials are written as part[blockIdx.x][H] (one row per block).
-template <int NV>
+// Column partials are written as part[blockIdx.x][H] (one row per block); the WV waves'
+// register partials are summed in a fixed pairwise order (deterministic).
+template <int NV, int WV = 4>
 HS_DEVICE void block_colpart_store(float (&acc)[NV][4], float* __restrict__ part, float* lds) {
   constexpr int H = NV * 256;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  // lds: [4][H]
+  // lds: [WV][H]
 #pragma unroll
   for (int k = 0; k < NV; ++k) store4(lds + w * H + (k * 64 + lane) * 4, acc[k]);
   __syncthreads();
-  for (int c = threadIdx.x; c < H; c += blockDim.x)
-    part[(int64_t)blockIdx.x * H + c] = (lds[c] + lds[H + c]) + (lds[2 * H + c] + lds[3 * H + c]);
+  for (int c = threadIdx.x; c < H; c += blockDim.x) {
+    float v = (lds[c] + lds[H + c]) + (lds[2 * H + c] + lds[3 * H + c]);
+    if (WV == 8) v += (lds[4 * H + c] + lds[5 * H + c]) + (lds[6 * H + c] + lds[7 * H + c]);
+    part[(int64_t)blockIdx.x * H + c] = v;
+  }
   __syncthreads();
 }
 
+// One row per wave at a time, with the NEXT row's dy / z / statistics loaded before this row's
+// reductions (two rows of loads in flight per wave); gamma is loaded once per wave.  Small
+// blocks (4 waves) so the kernel still finds room on CUs that run weight-gradient GEMM blocks of
+// the side stream (an 8-wave, 156-VGPR variant waited for whole GEMM blocks to drain: 3x slower
+// inside the training step).
+constexpr int kLnBwdWaves = 4;
+
 template <int NV, typename T>
-__global__ void __launch_bounds__(256) ln_bwd_kernel(const T* __restrict__ dy, const float* __restrict__ zsave,
-                                                     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
-                                                     const float* __restrict__ gamma, T* __restrict__ dz_out,
-                                                     T* __restrict__ da_out, float* __restrict__ part_gamma,
-                                                     float* __restrict__ part_beta, float* __restrict__ part_bias,
-                                                     int rows, float p, uint64_t seed, uint64_t off, int mode,
-                                                     const uint64_t* __restrict__ seed_dev) {
+__global__ void __launch_bounds__(64 * kLnBwdWaves) ln_bwd_kernel(
+    const T* __restrict__ dy, const float* __restrict__ zsave, const float* __restrict__ mean_in,
+    const float* __restrict__ rstd_in, const float* __restrict__ gamma, T* __restrict__ dz_out, T* __restrict__ da_out,
+    float* __restrict__ part_gamma, float* __restrict__ part_beta, float* __restrict__ part_bias, int rows, float p,
+    uint64_t seed, uint64_t off, int mode, const uint64_t* __restrict__ seed_dev) {
   constexpr int H = NV * 256;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int lane = threadIdx.x & 63;
   const float scale = p < 1.f ? 1.0f / (1.0f - p) : 0.f;
   seed = resolve_seed(seed, seed_dev);
-  float ag[NV][4], ab[NV][4], abias[NV][4];
+  float ag[NV][4], ab[NV][4], abias[NV][4], gw[NV][4];
 #pragma unroll
-  for (int k = 0; k < NV; ++k)
+  for (int k = 0; k < NV; ++k) {
+    load4(gamma + (k * 64 + lane) * 4, gw[k]);
 #pragma unroll
     for (int j = 0; j < 4; ++j) ag[k][j] = ab[k][j] = abias[k][j] = 0.f;
-  for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += gridDim.x * 4) {
+  }
+  const int stride = gridDim.x * kLnBwdWaves;
+  int row = blockIdx.x * kLnBwdWaves + (threadIdx.x >> 6);
+  float d[NV][4], z[NV][4], mean = 0.f, rstd = 0.f;
+  auto fetch = [&](int r, float (&dd)[NV][4], float (&zz)[NV][4], float& mu, float& rs) {
+    const int64_t base = (int64_t)r * H;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      load4(dy + base + (k * 64 + lane) * 4, dd[k]);
+      load4(zsave + base + (k * 64 + lane) * 4, zz[k]);
+    }
+    mu = mean_in[r];
+    rs = rstd_in[r];
+  };
+  if (row < rows) fetch(row, d, z, mean, rstd);
+  while (row < rows) {
+    const int nxt = row + stride;
+    float dn[NV][4], zn[NV][4], mn = 0.f, rn = 0.f;
+    if (nxt < rows) fetch(nxt, dn, zn, mn, rn);
     const int64_t base = (int64_t)row * H;
-    const float mean = mean_in[row], rstd = rstd_in[row];
     float xh[NV][4], g[NV][4];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int k = 0; k < NV; ++k) {
-      const int c = (k * 64 + lane) * 4;
-      float d[4], z[4], gw[4];
-      load4(dy + base + c, d);
-      load4(zsave + base + c, z);
-      load4(gamma + c, gw);
+    for (int k = 0; k < NV; ++k)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        xh[k][j] = (z[j] - mean) * rstd;
-        g[k][j] = d[j] * gw[j];
-        ag[k][j] = fmaf(d[j], xh[k][j], ag[k][j]);
-        ab[k][j] += d[j];
+        xh[k][j] = (z[k][j] - mean) * rstd;
+        g[k][j] = d[k][j] * gw[k][j];
+        ag[k][j] = fmaf(d[k][j], xh[k][j], ag[k][j]);
+        ab[k][j] += d[k][j];
         s1 += g[k][j];
         s2 = fmaf(g[k][j], xh[k][j], s2);
       }
-    }
     s1 = wave_sum(s1) / H;
     s2 = wave_sum(s2) / H;
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
       const int c = (k * 64 + lane) * 4;
-      float dz[4];
+      float dzv[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) dz[j] = rstd * (g[k][j] - s1 - xh[k][j] * s2);
-      if (dz_out) store4(dz_out + base + c, dz);
+      for (int j = 0; j < 4; ++j) dzv[j] = rstd * (g[k][j] - s1 - xh[k][j] * s2);
+      if (dz_out) store4(dz_out + base + c, dzv);
       if (mode == kBDR) {
         float m[4] = {1.f, 1.f, 1.f, 1.f};
         if (p > 0.f) keep4(seed, off, (uint64_t)(base + c) >> 2, p, scale, m);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          dz[j] *= m[j];
-          abias[k][j] += dz[j];
+          dzv[j] *= m[j];
+          abias[k][j] += dzv[j];
         }
-        if (da_out) store4(da_out + base + c, dz);
+        if (da_out) store4(da_out + base + c, dzv);
       }
     }
+#pragma unroll
+    for (int k = 0; k < NV; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        d[k][j] = dn[k][j];
+        z[k][j] = zn[k][j];
+      }
+    mean = mn;
+    rstd = rn;
+    row = nxt;
   }
-  block_colpart_store<NV>(ag, part_gamma, lds);
-  block_colpart_store<NV>(ab, part_beta, lds);
-  if (mode == kBDR && part_bias) block_colpart_store<NV>(abias, part_bias, lds);
+  block_colpart_store<NV, kLnBwdWaves>(ag, part_gamma, lds);
+  block_colpart_store<NV, kLnBwdWaves>(ab, part_beta, lds);
+  if (mode == kBDR && part_bias) block_colpart_store<NV, kLnBwdWaves>(abias, part_bias, lds);
 }
 
 // ------------------------------------------------------------ embeddings
@@ -306,7 +339,12 @@ __global__ void __launch_bounds__(256) emb_bwd_kernel(const T* __restrict__ dy, 
   }
 }
 
-constexpr int kLnBwdBlocks = 256;
+// column-partial blocks of the LN / embedding backward: HETSEQ_LNBWD_BLOCKS (default 512)
+static const int kLnBwdBlocks = [] {
+  const char* e = std::getenv("HETSEQ_LNBWD_BLOCKS");
+  const int v = e ? std::atoi(e) : 512;
+  return v >= 64 && v <= 4096 ? v : 512;
+}();
 
 template <int NV, typename T>
 void ln_fwd_launch(const void* a, const float* bias, const void* resid, const float* gamma, const float* beta, void* y,
@@ -323,7 +361,7 @@ void ln_bwd_launch(const void* dy, const float* zsave, const float* mean, const 
                    void* dz, void* da, float* pg, float* pb, float* pbias, int rows, float p, uint64_t seed,
                    uint64_t off, int mode, hipStream_t st) {
   constexpr int H = NV * 256;
-  hipLaunchKernelGGL((ln_bwd_kernel<NV, T>), dim3(kLnBwdBlocks), dim3(256), 4 * H * sizeof(float), st, (const T*)dy,
+  hipLaunchKernelGGL((ln_bwd_kernel<NV, T>), dim3(kLnBwdBlocks), dim3(64 * kLnBwdWaves), kLnBwdWaves * H * sizeof(float), st, (const T*)dy,
                      zsave, mean, rstd, gamma, (T*)dz, (T*)da, pg, pb, pbias, rows, p, seed, off, mode, g_seed_dev);
 }
 

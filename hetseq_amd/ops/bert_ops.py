@@ -251,6 +251,19 @@ def segsum_rows(src, order, keys, dst):
     return dst
 
 
+def sort_keys(keys, bound):
+    """Stable ascending sort of int64 ``keys`` in [0, bound): (sorted keys, source indices), by the
+    one-block LDS sort (elementwise.hip sort_keys_kernel); sizes it does not serve (n > 16384 or
+    too many key + index bits) use torch.sort(stable=True), which returns the same pair."""
+    keys = keys.contiguous().view(-1)
+    n = keys.numel()
+    out_k = torch.empty_like(keys)
+    out_o = torch.empty_like(keys)
+    if hip().sort_keys(keys.data_ptr(), n, int(bound), out_k.data_ptr(), out_o.data_ptr(), stream_handle()) == 0:
+        return out_k, out_o
+    return torch.sort(keys, stable=True)
+
+
 class FusedEmbedding(torch.autograd.Function):
     @staticmethod
     def forward(ctx, ids, tt, wword, wpos, wtype, gamma, beta, p, eps, out_dtype, sink=None):
@@ -309,10 +322,10 @@ class FusedEmbedding(torch.autograd.Function):
             tv = [ptype[0].data_ptr()] + ([ptype[1].data_ptr()] if TV == 2 else [])
             hip().colpart_finalize(tv, [dtype_[i].data_ptr() for i in range(len(tv))], nb, H, 1, stream_handle())
         else:
-            tt_keys, tt_order = torch.sort(tt.view(-1), stable=True)
+            tt_keys, tt_order = sort_keys(tt, TV)
             segsum_rows(dx, tt_order, tt_keys, dtype_)
         # word rows: deterministic sorted-run sums; positions: fixed-order column sums
-        word_keys, word_order = torch.sort(ids.view(-1), stable=True)
+        word_keys, word_order = sort_keys(ids, V)
         segsum_rows(dx, word_order, word_keys, dword)
         hip().pos_grad(dx.data_ptr(), dpos.data_ptr(), B, S, H, stream_handle())
         if sink is not None:

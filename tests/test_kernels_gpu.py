@@ -266,6 +266,23 @@ def test_attention_bwd_x6_fp32_level(cuda, B, S, NH, p, fused, monkeypatch):
     assert e6 <= 2 * e32 + 1e-7, (e6, e32)
 
 
+@pytest.mark.parametrize("n,bound", [(4096, 30522), (1, 5), (777, 2), (16384, 30522), (5000, 100000)])
+def test_sort_keys_matches_stable_sort(cuda, n, bound):
+    """The one-block LDS key sort returns torch.sort(stable=True)'s keys and indices exactly."""
+    from hetseq_amd.ops import bert_ops
+    from hetseq_amd.ops._C import hip
+
+    torch.manual_seed(n)
+    keys = torch.randint(0, bound, (n,), device=cuda, dtype=torch.int64)
+    ok = torch.empty_like(keys)
+    oo = torch.empty_like(keys)
+    served = hip().sort_keys(keys.data_ptr(), n, bound, ok.data_ptr(), oo.data_ptr(), 0) == 0
+    assert served == (n <= 16384 and (n - 1).bit_length() + (bound - 1).bit_length() <= 32)
+    k, o = bert_ops.sort_keys(keys, bound)
+    rk, ro = torch.sort(keys, stable=True)
+    assert torch.equal(k, rk) and torch.equal(o, ro)
+
+
 @pytest.mark.parametrize("B,S,NH", [(2, 128, 12), (2, 96, 2), (1, 512, 2)])
 def test_attention_fwd_bf16_mfma(cuda, B, S, NH, monkeypatch):
     """bf16 matrix-core forward vs an fp64 reference on the same bf16 inputs (+ bias), and vs the fp32-MFMA path."""
