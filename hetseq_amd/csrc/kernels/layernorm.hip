@@ -339,11 +339,12 @@ __global__ void __launch_bounds__(256) emb_bwd_kernel(const T* __restrict__ dy, 
   }
 }
 
-// column-partial blocks of the LN / embedding backward: HETSEQ_LNBWD_BLOCKS (default 512)
+// column-partial blocks of the LN / embedding backward: HETSEQ_LNBWD_BLOCKS (default 256: 4 rows
+// per wave; 512 / 1024 blocks measured 25.0 / 27.0 us isolated vs 25.3, and slower in the step)
 static const int kLnBwdBlocks = [] {
   const char* e = std::getenv("HETSEQ_LNBWD_BLOCKS");
-  const int v = e ? std::atoi(e) : 512;
-  return v >= 64 && v <= 4096 ? v : 512;
+  const int v = e ? std::atoi(e) : 256;
+  return v >= 64 && v <= 4096 ? v : 256;
 }();
 
 template <int NV, typename T>
