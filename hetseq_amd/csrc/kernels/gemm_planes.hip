@@ -295,6 +295,96 @@ __global__ void __launch_bounds__(64 * WV, (planes_waves_per_simd<P, BK, STAGES,
   }
   TC* C = static_cast<TC*>(p.C);
   TC* aux = static_cast<TC*>(p.aux);
+  if constexpr (sizeof(TC) == 2) {
+    // bf16 C: stage the fp32 tile through LDS in two 64-row halves (32 KB, the smallest stage of
+    // any variant) and finish it row-contiguously: 8 columns per thread, one 16-B load of the
+    // bias / pre-activation / old C and one 16-B store per 8 outputs instead of per-register
+    // 2-B accesses.  dGELU column sums: per-thread partials over its rows, then a fixed-order
+    // LDS reduction (deterministic).
+    static_assert(STAGES * STAGE >= 64 * kPB * 4, "epilogue staging fits the operand buffers");
+    float* T = reinterpret_cast<float*>(smem);
+    constexpr int NT = 64 * WV, GRP = NT / 16;  // threads; threads sharing a column group
+    const int cg = (threadIdx.x & 15) * 8;
+    float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (EPI != kPEpiNone) {
+      const float4 b0 = *reinterpret_cast<const float4*>(p.bias + n0 + cg);
+      const float4 b1 = *reinterpret_cast<const float4*>(p.bias + n0 + cg + 4);
+      bv[0] = b0.x; bv[1] = b0.y; bv[2] = b0.z; bv[3] = b0.w; bv[4] = b1.x; bv[5] = b1.y; bv[6] = b1.z; bv[7] = b1.w;
+    }
+    auto unpack = [](uint4 u, float (&v)[8]) {
+      const uint32_t x[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        v[2 * k] = __uint_as_float(x[k] << 16);
+        v[2 * k + 1] = __uint_as_float(x[k] & 0xffff0000u);
+      }
+    };
+    auto pack = [](const float (&v)[8]) {
+      uint32_t x[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        x[k] = (uint32_t)from_f<bf16_t>(v[2 * k]).x | ((uint32_t)from_f<bf16_t>(v[2 * k + 1]).x << 16);
+      return make_uint4(x[0], x[1], x[2], x[3]);
+    };
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      __syncthreads();  // operand buffers (or the previous half) no longer read
+      if (wr == hh)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) T[(32 * i + acc_row(r, q)) * kPB + wn + 32 * j + lr] = acc[i][j][r];
+      __syncthreads();
+      for (int row = threadIdx.x >> 4; row < 64; row += GRP) {
+        const int64_t m = m0 + 64 * hh + row;
+        const float4 a0 = *reinterpret_cast<const float4*>(T + row * kPB + cg);
+        const float4 a1 = *reinterpret_cast<const float4*>(T + row * kPB + cg + 4);
+        const float a[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        float o[8];
+        uint4* cp = reinterpret_cast<uint4*>(C + m * p.ldc + n0 + cg);
+        if (EPI == kPEpiGelu) {  // GELU of the STORED (rounded) pre-activation, as the backward sees it
+          const uint4 pre = pack(a);
+          *reinterpret_cast<uint4*>(aux + m * p.ldaux + n0 + cg) = pre;
+          float ar[8];
+          unpack(pre, ar);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) o[k] = gelu_f(ar[k] + bv[k]);
+        } else if (EPI == kPEpiDGelu) {
+          float pre[8];
+          unpack(*reinterpret_cast<const uint4*>(aux + m * p.ldaux + n0 + cg), pre);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            o[k] = a[k] * gelu_grad_f(pre[k] + bv[k]);
+            cs[k] += o[k];
+          }
+        } else if (p.beta != 0.f) {
+          float old[8];
+          unpack(*cp, old);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) o[k] = a[k] + bv[k] + p.beta * old[k];
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) o[k] = a[k] + bv[k];
+        }
+        *cp = pack(o);
+      }
+    }
+    if (EPI == kPEpiDGelu) {  // column partials of the block's 128 rows: GRP thread partials per column
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < 8; ++k) T[(threadIdx.x >> 4) * kPB + cg + k] = cs[k];
+      __syncthreads();
+      if (threadIdx.x < kPB) {
+        float t = 0.f;
+        for (int g = 0; g < GRP; ++g) t += T[g * kPB + threadIdx.x];  // fixed order
+        p.part[(int64_t)tm * p.N + n0 + threadIdx.x] = t;
+      }
+    }
+    return;
+  }
   float csum[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) csum[j] = 0.f;
@@ -337,6 +427,47 @@ __global__ void __launch_bounds__(64 * WV, (planes_waves_per_simd<P, BK, STAGES,
         const int c = wn + 32 * j + lr;
         p.part[(int64_t)tm * p.N + n0 + c] = csum[j] + red[c];
       }
+  }
+}
+
+// split-K finish for a bf16 C: C = bf16(sum_s slab[s] (+ bias) (+ beta * C)), slices in fixed
+// order (deterministic); 8 columns per thread (16-B bf16 stores)
+__global__ void __launch_bounds__(256) splitk_reduce_bf16_kernel(const float* __restrict__ slab, int ksplit, int M,
+                                                                 int N, bf16_t* __restrict__ C, int64_t ldc,
+                                                                 const float* __restrict__ bias, float beta) {
+  const int n8 = N / 8;
+  const int64_t total = (int64_t)M * n8, plane = (int64_t)M * N;
+  for (int64_t u = blockIdx.x * 256ll + threadIdx.x; u < total; u += (int64_t)gridDim.x * 256) {
+    const int m = (int)(u / n8), n = (int)(u % n8) * 8;
+    const float* s0 = slab + (int64_t)m * N + n;
+    float a[8];
+    {
+      const float4 x = *reinterpret_cast<const float4*>(s0), y = *reinterpret_cast<const float4*>(s0 + 4);
+      a[0] = x.x; a[1] = x.y; a[2] = x.z; a[3] = x.w; a[4] = y.x; a[5] = y.y; a[6] = y.z; a[7] = y.w;
+    }
+    for (int sl = 1; sl < ksplit; ++sl) {
+      const float4 x = *reinterpret_cast<const float4*>(s0 + sl * plane);
+      const float4 y = *reinterpret_cast<const float4*>(s0 + sl * plane + 4);
+      a[0] += x.x; a[1] += x.y; a[2] += x.z; a[3] += x.w; a[4] += y.x; a[5] += y.y; a[6] += y.z; a[7] += y.w;
+    }
+    if (bias)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) a[k] += bias[n + k];
+    uint4* c = reinterpret_cast<uint4*>(C + (int64_t)m * ldc + n);
+    if (beta != 0.f) {
+      const uint4 o = *c;
+      const uint32_t w[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        a[2 * k] += beta * __uint_as_float(w[k] << 16);
+        a[2 * k + 1] += beta * __uint_as_float(w[k] & 0xffff0000u);
+      }
+    }
+    uint32_t w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      w[k] = (uint32_t)from_f<bf16_t>(a[2 * k]).x | ((uint32_t)from_f<bf16_t>(a[2 * k + 1]).x << 16);
+    *c = make_uint4(w[0], w[1], w[2], w[3]);
   }
 }
 
@@ -413,7 +544,13 @@ int launch_gemm_planes(int planes, int c_dtype, int ta, int tb, int M, int N, in
   auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
   if (!al16(A) || !al16(B) || lda % 8 || ldb % 8 || (planes == 3 && (a_ps % 8 || b_ps % 8))) return -1;
   if ((epi >= 1 && !bias) || (epi >= 2 && (!aux || beta != 0.f)) || (epi == 3 && (!part || !colsum_out))) return -1;
-  if (ksplit > 1 && (epi != 0 || c_dtype != 0 || !slab || (int64_t)ksplit * M * N > slab_floats || ldc % 4 || N % 4))
+  // split-K: fp32 slabs, then a fixed-order reduction applying bias / beta (fp32 or bf16 C)
+  if (ksplit > 1 && (epi > 1 || !slab || (int64_t)ksplit * M * N > slab_floats || ldc % 8 || N % 8 ||
+                     (c_dtype && !al16(C))))
+    return -1;
+  // bf16 C: the epilogue moves 8 columns per 16-B access (C, pre-activation, old C)
+  if (c_dtype && ksplit == 1 && (!al16(C) || ldc % 8 || (epi >= 2 && (!al16(aux) || ldaux % 8)) ||
+                                 (epi >= 1 && !al16(bias))))
     return -1;
   // 32-bit per-lane DMA offsets: the operand span (all planes) must stay below 4 GiB
   const int64_t spanA = 2 * ((planes - 1) * a_ps + (int64_t)(ta ? K : M) * lda);
@@ -433,7 +570,13 @@ int launch_gemm_planes(int planes, int c_dtype, int ta, int tb, int M, int N, in
        : variant == 4 ? HS_CFG(1, 64, 1, 8) : HS_CFG(1, 64, 2, 4);
 #undef HS_CFG
   if (rc) return rc;
-  if (ksplit > 1) launch_splitk_reduce(slab, ksplit, M, N, static_cast<float*>(C), ldc, nullptr, beta, M, N, st);
+  if (ksplit > 1 && c_dtype) {
+    const int64_t units = (int64_t)M * (N / 8);
+    hipLaunchKernelGGL(splitk_reduce_bf16_kernel, dim3((int)std::min<int64_t>((units + 255) / 256, 2048)), dim3(256),
+                       0, st, slab, ksplit, M, N, static_cast<bf16_t*>(C), ldc, epi == 1 ? bias : nullptr, beta);
+  } else if (ksplit > 1) {
+    launch_splitk_reduce(slab, ksplit, M, N, static_cast<float*>(C), ldc, epi == 1 ? bias : nullptr, beta, M, N, st);
+  }
   if (epi == kPEpiDGelu) {
     const float* parts[1] = {part};
     float* outs[1] = {colsum_out};

@@ -931,6 +931,26 @@ def test_gemm_planes_vs_fp64(cuda, P, ta, tb, M, N, K, ks, variant):
         assert err < 1e-5, err
 
 
+@pytest.mark.parametrize("ks", [2, 4])
+@pytest.mark.parametrize("epi_bias,beta", [(False, 0.0), (True, 0.0), (True, 1.0)])
+def test_gemm_planes_bf16_splitk(cuda, ks, epi_bias, beta):
+    """bf16 C through K slices: fp32 slabs summed in fixed order with the bias and beta applied
+    once, rounded to bf16 at the end (the small-grid N = 768 products of the bf16 step)."""
+    from hetseq_amd.ops import gemm as G
+
+    torch.manual_seed(63 + ks)
+    T, K, N = 256, 1024, 384
+    x, w = torch.randn(T, K, device=cuda).bfloat16(), (torch.randn(N, K, device=cuda) * 0.05).bfloat16()
+    bias = torch.randn(N, device=cuda) if epi_bias else None
+    c0 = torch.randn(T, N, device=cuda).bfloat16()
+    y = c0.clone()
+    ok = G.gemm_planes(G.Planes.of_bf16(x), G.Planes.of_bf16(w), False, True, y, bias,
+                       G.EPI_BIAS if epi_bias else G.EPI_NONE, beta, ksplit=ks)
+    assert ok
+    ref = x.double() @ w.double().t() + (bias.double() if epi_bias else 0.0) + beta * c0.double()
+    _close(y, ref, 1e-2, 1e-2, "bf16 split-K planes")
+
+
 @pytest.mark.parametrize("P", [3, 1])
 def test_gemm_planes_epilogues(cuda, P):
     """bias, beta-accumulate, GELU (pre-activation kept) and dGELU + bias-gradient column sums."""
