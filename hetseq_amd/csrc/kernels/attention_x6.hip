@@ -16,6 +16,8 @@
 // fragment of k-step s).  K and V^T are split once per block while staged into LDS (three
 // planes each, 64-key chunks: 54 KB, two blocks per CU); the lane's Q row is split once in
 // registers; probabilities are split in registers per tile.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace hs {
@@ -208,6 +210,64 @@ HS_DEVICE void store_rows(float* out, const f32x16& c0, const f32x16& c1, int hf
     *reinterpret_cast<float4*>(out + 32 + d) =
         make_float4(c1[4 * g] * scale, c1[4 * g + 1] * scale, c1[4 * g + 2] * scale, c1[4 * g + 3] * scale);
   }
+}
+
+// ---- pre-split plane images of 64-row chunks (the "p" backward kernels) ----
+// A chunk of Q / dO (or K / V) rows is split ONCE per block into three bf16 planes [row][64 d]
+// (128-B rows, 8 KB per plane), read two ways: row fragments (k = d) by one ds_read_b128 each,
+// transposed fragments (rows = d, k = rows of the chunk, in the score-register order) by two
+// ds_read_b64_tr_b16.  The 16-B chunk swizzle pswz makes both patterns conflict-free (searched
+// exhaustively over 3-bit row-bit selections: the b128 lane groups and the 32-lane tr16 halves).
+constexpr int kPRow = 128;            // bytes per plane row
+constexpr int kPPlane = 64 * kPRow;   // bytes per plane (64 rows)
+constexpr int kPImg = 3 * kPPlane;    // one operand's three planes: 24 KB
+
+typedef short ps4 __attribute__((ext_vector_type(4)));
+typedef short ps8 __attribute__((ext_vector_type(8)));
+
+HS_DEVICE int pswz(int r) { return ((r >> 2) & 1) | (((r >> 3) & 1) << 1) | (((r >> 1) & 1) << 2); }
+
+// rows [r0, r0 + n) (n <= 64) of a head slice, (x + bias) * scale, split into the plane image;
+// unit = (row, 16-d segment): four float4 loads, two 16-B chunks per plane
+template <int NT>
+HS_DEVICE void stage_planes(char* img, const float* base, int64_t ld, int r0, int n, const float* bias, float scale) {
+  for (int u = threadIdx.x; u < 64 * 4; u += NT) {
+    const int row = u >> 2, seg = u & 3;
+    if (row >= n) continue;
+    float v[2][8];
+    ld8(base + (int64_t)(r0 + row) * ld + 16 * seg, bias ? bias + 16 * seg : nullptr, scale, v[0]);
+    ld8(base + (int64_t)(r0 + row) * ld + 16 * seg + 8, bias ? bias + 16 * seg + 8 : nullptr, scale, v[1]);
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      bfx8 f[3];
+      split8(v[e], f[0], f[1], f[2]);
+      const int off = row * kPRow + 16 * ((2 * seg + e) ^ pswz(row));
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<bfx8*>(img + pl * kPPlane + off) = f[pl];
+    }
+  }
+}
+
+// row fragment of plane pl: row `row` (this lane's), 16-B chunk c (= 2 ks + lane half)
+HS_DEVICE bfx8 prow_frag(const char* img, int pl, int row, int c) {
+  return *reinterpret_cast<const bfx8*>(img + pl * kPPlane + row * kPRow + 16 * (c ^ pswz(row)));
+}
+
+// transposed fragment of plane pl: lane (r, h) gets column d0 + r of rows q0 + 4h + 8(j>>2) + (j&3)
+// (j = 0..7: the order of score registers 8ks..8ks+7, so it pairs with P / dS as the B operand)
+HS_DEVICE bfx8 ptr_frag(const char* img, int pl, int d0, int q0, int lane) {
+  const int l16 = lane & 15, qq = l16 >> 2, pp = l16 & 3, g = lane >> 4;
+  const int col = d0 + 16 * (g & 1) + 4 * pp;
+  const char* plb = img + pl * kPPlane;
+  ps4 v[2];
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj) {
+    const int row = q0 + 4 * (g >> 1) + 8 * jj + qq;
+    const char* a = plb + row * kPRow + 16 * ((col >> 3) ^ pswz(row)) + 2 * (col & 7);
+    v[jj] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) ps4*)(a));
+  }
+  const ps8 u = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w};
+  return __builtin_bit_cast(bfx8, u);
 }
 
 }  // namespace
@@ -626,15 +686,245 @@ __global__ void __launch_bounds__(256, 2)
   store_rows(out + 2 * H, dv0, dv1, hf, 1.f);
 }
 
+// ---------------------------------------------------------------------------
+// Backward on pre-split plane images ("p" kernels; any S % 32 == 0): like the dQ / dKV pair
+// above, but each 64-row chunk of the shared operand is split into planes once per block
+// (instead of once per wave and fragment) and the transposed fragments come from the same
+// image through ds_read_b64_tr_b16 (no scalar gathers, no second split).  Per 32x32 tile a
+// wave splits only its own K / V (or Q / dO) fragments and the P / dS registers.  48 KB of
+// LDS, two blocks per CU.
+
+// dK / dV for 32 keys per wave (lane = key) over 64-query chunks of Q (biased, * 1/8) and dO.
+__global__ void __launch_bounds__(256, 2)
+    attn_bwd_dkv_x6p_kernel(const float* __restrict__ qkv, const int64_t* __restrict__ mask,
+                            const float* __restrict__ bqkv, const float* __restrict__ dctx,
+                            const float* __restrict__ lse, const float* __restrict__ Dd, float* __restrict__ dqkv,
+                            int S, int NH, float p, const uint32_t* __restrict__ dmask) {
+  __shared__ __attribute__((aligned(16))) char Qp[kPImg];
+  __shared__ __attribute__((aligned(16))) char Op[kPImg];
+  __shared__ float Ls[64];
+  __shared__ float Ds[64];
+  __shared__ uint32_t Wd[64][4];
+  const int H = NH * kXD;
+  const int64_t ld = 3 * (int64_t)H;
+  const int bh = blockIdx.y, b = bh / NH, h = bh % NH;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hf = lane >> 5, li = lane & 31;
+  const int k0 = blockIdx.x * 128 + w * 32;
+  const bool active = k0 < S;
+  const int key = k0 + li;
+  const float* rows = qkv + (int64_t)b * S * ld;
+  const float* drows = dctx + (int64_t)b * S * H;
+  const float dscale = drop_scale16(drop_thr16(p));
+
+  // the lane's K / V rows, split once (they are the B operand of every tile)
+  bfx8 kb[4][3], vb[4][3];
+  float madd = 0.f;
+  {
+    float kr[4][8], vr[4][8];
+    if (active) {
+      row_frags(rows + (int64_t)key * ld + H + h * kXD, bofs(bqkv, H + h * kXD), hf, kr);
+      row_frags(rows + (int64_t)key * ld + 2 * H + h * kXD, bofs(bqkv, 2 * H + h * kXD), hf, vr);
+      madd = (1.f - (float)mask[(int64_t)b * S + key]) * -10000.f;
+    } else {
+#pragma unroll
+      for (int ss = 0; ss < 4; ++ss)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) kr[ss][j] = vr[ss][j] = 0.f;
+    }
+#pragma unroll
+    for (int ss = 0; ss < 4; ++ss) {
+      split8(kr[ss], kb[ss][0], kb[ss][1], kb[ss][2]);
+      split8(vr[ss], vb[ss][0], vb[ss][1], vb[ss][2]);
+    }
+  }
+  f32x16 dk0 = {}, dk1 = {}, dv0 = {}, dv1 = {};
+  for (int c0 = 0; c0 < S; c0 += 64) {
+    const int clen = min(64, S - c0);
+    __syncthreads();
+    stage_planes<256>(Qp, rows + h * kXD, ld, c0, clen, bofs(bqkv, h * kXD), 0.125f);
+    stage_planes<256>(Op, drows + h * kXD, H, c0, clen, nullptr, 1.f);
+    for (int i = threadIdx.x; i < clen; i += blockDim.x) {
+      Ls[i] = lse[(int64_t)bh * S + c0 + i];
+      Ds[i] = Dd[(int64_t)bh * S + c0 + i];
+    }
+    if (p > 0.f)
+      for (int i = threadIdx.x; i < clen * 4; i += blockDim.x) {
+        const int qi = i >> 2, kw = blockIdx.x * 4 + (i & 3);
+        Wd[qi][i & 3] = kw < (S >> 5) ? dmask[((uint64_t)bh * S + c0 + qi) * (uint64_t)(S >> 5) + kw] : 0u;
+      }
+    __syncthreads();
+    if (!active) continue;
+    for (int t = 0; t < clen; t += 32) {
+      f32x16 sc = {}, dp = {};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        bfx8 a[3];
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) a[pl] = prow_frag(Qp, pl, t + li, 2 * ks + hf);
+        sc = mma6(a, kb[ks], sc);
+      }
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        bfx8 a[3];
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) a[pl] = prow_frag(Op, pl, t + li, 2 * ks + hf);
+        dp = mma6(a, vb[ks], dp);
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        float pd[8], ds[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int r = 8 * ks + j, qi = t + xrow(r, hf);
+          const float pv = __expf(sc[r] + madd - Ls[qi]);
+          const float mk = p > 0.f ? (((Wd[qi][w] >> li) & 1u) ? dscale : 0.f) : 1.f;
+          pd[j] = pv * mk;
+          ds[j] = pv * (dp[r] * mk - Ds[qi]);
+        }
+        bfx8 pb[3], a[3];
+        split8(pd, pb[0], pb[1], pb[2]);
+        const int q0 = t + 16 * ks;
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) a[pl] = ptr_frag(Op, pl, 0, q0, lane);
+        dv0 = mma6(a, pb, dv0);
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) a[pl] = ptr_frag(Op, pl, 32, q0, lane);
+        dv1 = mma6(a, pb, dv1);
+        split8(ds, pb[0], pb[1], pb[2]);
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) a[pl] = ptr_frag(Qp, pl, 0, q0, lane);
+        dk0 = mma6(a, pb, dk0);
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) a[pl] = ptr_frag(Qp, pl, 32, q0, lane);
+        dk1 = mma6(a, pb, dk1);
+      }
+    }
+  }
+  if (!active) return;
+  float* out = dqkv + ((int64_t)b * S + key) * ld + h * kXD;
+  store_rows(out + H, dk0, dk1, hf, 1.f);
+  store_rows(out + 2 * H, dv0, dv1, hf, 1.f);
+}
+
+// dQ for 32 queries per wave (lane = query) over 64-key chunks of K / V (biased); writes D.
+__global__ void __launch_bounds__(256, 2)
+    attn_bwd_dq_x6p_kernel(const float* __restrict__ qkv, const int64_t* __restrict__ mask,
+                           const float* __restrict__ bqkv, const float* __restrict__ ctx,
+                           const float* __restrict__ dctx, const float* __restrict__ lse, float* __restrict__ Dout,
+                           float* __restrict__ dqkv, int S, int NH, float p, const uint32_t* __restrict__ dmask) {
+  __shared__ __attribute__((aligned(16))) char Kp[kPImg];
+  __shared__ __attribute__((aligned(16))) char Vp[kPImg];
+  __shared__ float Ms[64];
+  const int H = NH * kXD;
+  const int64_t ld = 3 * (int64_t)H;
+  const int bh = blockIdx.y, b = bh / NH, h = bh % NH;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hf = lane >> 5, li = lane & 31;
+  const int q0 = blockIdx.x * 128 + w * 32;
+  const bool active = q0 < S;
+  const float* rows = qkv + (int64_t)b * S * ld;
+  const float dscale = drop_scale16(drop_thr16(p));
+
+  // the lane's Q (biased, * 1/8) and dO rows, split once (the B operand of every tile)
+  bfx8 qb[4][3], ob[4][3];
+  float dsum = 0.f, lq = 0.f;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    float qr[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, dor[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (active) {
+      const int64_t tok = (int64_t)b * S + q0 + li;
+      const int d = 16 * s + 8 * hf;
+      ld8(rows + (int64_t)(q0 + li) * ld + h * kXD + d, bofs(bqkv, h * kXD + d), 0.125f, qr);
+      ld8(dctx + tok * H + h * kXD + d, nullptr, 1.f, dor);
+      float o[8];
+      ld8(ctx + tok * H + h * kXD + d, nullptr, 1.f, o);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dsum = fmaf(dor[j], o[j], dsum);
+    }
+    split8(qr, qb[s][0], qb[s][1], qb[s][2]);
+    split8(dor, ob[s][0], ob[s][1], ob[s][2]);
+  }
+  if (active) {
+    dsum += __shfl_xor(dsum, 32, 64);
+    if (hf == 0) Dout[(int64_t)bh * S + q0 + li] = dsum;
+    lq = lse[(int64_t)bh * S + q0 + li];
+  }
+  f32x16 dq0 = {}, dq1 = {};
+  for (int c0 = 0; c0 < S; c0 += 64) {
+    const int clen = min(64, S - c0);
+    __syncthreads();
+    stage_planes<256>(Kp, rows + H + h * kXD, ld, c0, clen, bofs(bqkv, H + h * kXD), 1.f);
+    stage_planes<256>(Vp, rows + 2 * H + h * kXD, ld, c0, clen, bofs(bqkv, 2 * H + h * kXD), 1.f);
+    for (int i = threadIdx.x; i < clen; i += blockDim.x) Ms[i] = (1.f - (float)mask[(int64_t)b * S + c0 + i]) * -10000.f;
+    __syncthreads();
+    if (!active) continue;
+    for (int t = 0; t < clen; t += 32) {
+      f32x16 sc = {}, dp = {};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        bfx8 a[3];
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) a[pl] = prow_frag(Kp, pl, t + li, 2 * ks + hf);
+        sc = mma6(a, qb[ks], sc);
+      }
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        bfx8 a[3];
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) a[pl] = prow_frag(Vp, pl, t + li, 2 * ks + hf);
+        dp = mma6(a, ob[ks], dp);
+      }
+      const uint32_t word = p > 0.f ? dmask[((uint64_t)bh * S + q0 + li) * (uint64_t)(S >> 5) + ((c0 + t) >> 5)] : 0u;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        float ds[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int r = 8 * ks + j, kj = xrow(r, hf);
+          const float mk = p > 0.f ? (((word >> kj) & 1u) ? dscale : 0.f) : 1.f;
+          const float pv = __expf(sc[r] + Ms[t + kj] - lq);
+          ds[j] = pv * (dp[r] * mk - dsum);
+        }
+        bfx8 sb[3], a[3];
+        split8(ds, sb[0], sb[1], sb[2]);
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) a[pl] = ptr_frag(Kp, pl, 0, t + 16 * ks, lane);
+        dq0 = mma6(a, sb, dq0);
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) a[pl] = ptr_frag(Kp, pl, 32, t + 16 * ks, lane);
+        dq1 = mma6(a, sb, dq1);
+      }
+    }
+  }
+  if (!active) return;
+  store_rows(dqkv + ((int64_t)b * S + q0 + li) * ld + h * kXD, dq0, dq1, hf, 0.125f);
+}
+
 }  // namespace hs
 
 using namespace hs;
+
+// fp32 backward kernel family: HETSEQ_ATTN_BWD_X6=p (plane-image dQ / dKV pair, default) or g
+// (fused S <= 128 / gather dQ / dKV pair)
+static int g_bwd_planes_env = [] {
+  const char* e = std::getenv("HETSEQ_ATTN_BWD_X6");
+  return e && e[0] == 'g' ? 0 : 1;
+}();
+static int g_bwd_planes = g_bwd_planes_env;
+void set_attn_bwd_x6_planes(int on) { g_bwd_planes = on < 0 ? g_bwd_planes_env : on; }
 
 // fused S <= 128 (grid B*NH x 512) or the dQ / dKV pair (grid (S/128, B*NH) x 256 each)
 int launch_attn_bwd_x6(const float* qkv, const int64_t* mask, const float* bqkv, const float* ctx, const float* dctx,
                        const float* lse, float* Dbuf, float* dqkv, const uint32_t* dmask, int B, int S, int NH,
                        int D, float p, bool fused, hipStream_t st) {
   if (D != kXD || S % 32 != 0 || S <= 0 || (p > 0.f && dmask == nullptr)) return -1;
+  if (g_bwd_planes) {  // plane-image kernels (default)
+    dim3 grid((S + 127) / 128, B * NH);
+    hipLaunchKernelGGL(attn_bwd_dq_x6p_kernel, grid, dim3(256), 0, st, qkv, mask, bqkv, ctx, dctx, lse, Dbuf, dqkv, S,
+                       NH, p, dmask);
+    hipLaunchKernelGGL(attn_bwd_dkv_x6p_kernel, grid, dim3(256), 0, st, qkv, mask, bqkv, dctx, lse, Dbuf, dqkv, S, NH,
+                       p, dmask);
+    return 0;
+  }
   if (fused && S <= 128) {
     hipLaunchKernelGGL(attn_bwd_fused_x6_kernel, dim3(B * NH), dim3(512), 0, st, qkv, mask, bqkv, ctx, dctx, lse, dqkv,
                        S, NH, p, dmask);

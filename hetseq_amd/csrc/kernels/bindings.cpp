@@ -57,6 +57,7 @@ int launch_pool_nsp_bwd(int, const float*, const void*, void*, int, int, int, co
                         float*, float*, float*, float*, float*, int, hipStream_t);
 // attention.hip
 void set_attn_fp32_mode(int x6);
+void set_attn_bwd_x6_planes(int on);
 int attn_fp32_mode();
 int launch_attn_fwd(int, const void*, const int64_t*, const float*, void*, float*, uint32_t*, int, int, int, int, float,
                     u64, u64, hipStream_t);
@@ -284,6 +285,8 @@ PYBIND11_MODULE(_hip, m) {
   });
 
   m.def("set_attn_fp32_mode", &set_attn_fp32_mode, "fp32 attention products: 1 split-bf16 (x6), 0 exact-fp32 MFMA");
+  m.def("set_attn_bwd_x6_planes", &set_attn_bwd_x6_planes,
+        "fp32 split-bf16 attention backward: 1 plane-image dQ / dKV kernels, 0 fused / gather kernels");
   m.def("attn_fp32_mode", &attn_fp32_mode);
   m.def("attn_fwd", [](int dt, i64 qkv, i64 mask, i64 bqkv, i64 ctx, i64 lse, i64 dmask, int B, int S, int NH, int D,
                        float p, u64 seed, u64 off, i64 st) {

@@ -230,16 +230,17 @@ def test_attention_fwd_x6_fp32_level(cuda, B, S, NH, p):
 
 @pytest.mark.parametrize("B,S,NH,p", [(2, 128, 12, 0.0), (2, 96, 2, 0.1), (1, 512, 2, 0.0), (2, 192, 2, 0.1),
                                        (3, 64, 4, 0.1), (2, 256, 12, 0.0)])
-@pytest.mark.parametrize("fused", [True, False])
-def test_attention_bwd_x6_fp32_level(cuda, B, S, NH, p, fused, monkeypatch):
-    """fp32 backward on split-bf16 products (fused S <= 128 and the dQ / dKV pair) against the
-    exact-fp32 MFMA backward on the same forward, and against fp64 autograd: error at the
-    exact-fp32 kernel's level."""
+@pytest.mark.parametrize("family", ["planes", "fused", "gather"])
+def test_attention_bwd_x6_fp32_level(cuda, B, S, NH, p, family, monkeypatch):
+    """fp32 backward on split-bf16 products -- the plane-image dQ / dKV pair (default), the fused
+    S <= 128 kernel and the gather dQ / dKV pair -- against the exact-fp32 MFMA backward on the
+    same forward, and against fp64 autograd: error at the exact-fp32 kernel's level."""
     from hetseq_amd.ops import bert_ops
     from hetseq_amd.ops._C import hip
 
-    if not fused:
+    if family == "gather":
         monkeypatch.setenv("HETSEQ_ATTN_BWD", "split")
+    hip().set_attn_bwd_x6_planes(1 if family == "planes" else 0)
     torch.manual_seed(32 + S)
     H = NH * 64
     qkv = torch.randn(B * S, 3 * H, device=cuda)
@@ -256,6 +257,7 @@ def test_attention_bwd_x6_fp32_level(cuda, B, S, NH, p, fused, monkeypatch):
         g6 = bert_ops.attn_bwd(qkv, mask, out, dout, saved, B, S, NH, p, bias=bias)
     finally:
         hip().set_attn_fp32_mode(old)
+        hip().set_attn_bwd_x6_planes(-1)
     torch.cuda.synchronize()
     _close(g6, g32, 1e-4, 1e-6, "x6 vs exact-fp32 attention backward")
     keep = _keep_mask(saved[1], B * NH, S) if p > 0 else None
