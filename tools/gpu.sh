@@ -4,6 +4,7 @@
 #   tools/gpu.sh pmc   [dtypes] [tag]  MFMA / LDS counters per kernel          -> gpurun_out/pmc_<tag>_<dtype>.md
 #   tools/gpu.sh bench [dtypes]        bench.py per dtype                      -> gpurun_out/bench_<dtype>.json
 #   tools/gpu.sh tests [pytest args]   the GPU test suite (one process)        -> gpurun_out/gputests.log
+#   tools/gpu.sh configs               every single-GPU BASELINE.md configuration -> gpurun_out/configs.jsonl
 # Every GPU step runs under its own time limit; the first failure ends the job (no retries).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
@@ -33,6 +34,22 @@ case "$cmd" in
       timeout -k 10 300 python3 bench.py --steps 30 --warmup 5 --dtype "$D" ${BENCH_ARGS:-} > "gpurun_out/bench_$D.log" 2>&1 || { tail -20 "gpurun_out/bench_$D.log"; exit 1; }
       tail -1 "gpurun_out/bench_$D.log" > "gpurun_out/bench_$D.json"; cut -c1-220 "gpurun_out/bench_$D.json"
     done ;;
+  configs)  # the BASELINE.md table: every single-GPU configuration, one bench.py run each
+    : > gpurun_out/configs.jsonl
+    while read -r name args; do
+      [ -z "$name" ] && continue
+      timeout -k 10 400 python3 bench.py $args > "gpurun_out/cfg_$name.log" 2>&1 || { tail -20 "gpurun_out/cfg_$name.log"; exit 1; }
+      echo "{\"config\": \"$name\", \"result\": $(tail -1 "gpurun_out/cfg_$name.log")}" >> gpurun_out/configs.jsonl
+      echo "$name $(tail -1 "gpurun_out/cfg_$name.log" | cut -c1-160)"
+    done <<'CFG'
+ph1_fp32 --steps 30 --warmup 5
+ph1_bf16 --steps 30 --warmup 5 --dtype bf16
+ph1_bf16_graph --steps 30 --warmup 5 --dtype bf16 --hip-graph
+ph1_fp32_uf4 --steps 10 --warmup 3 --update-freq 4
+ph2_fp32 --steps 20 --warmup 4 --seq-len 512 --batch 8 --max-pred 80
+ph2_bf16 --steps 20 --warmup 4 --seq-len 512 --batch 8 --max-pred 80 --dtype bf16
+CFG
+    ;;
   tests)
     timeout -k 10 1100 python3 -u -m pytest tests -m gpu -v --timeout 180 --timeout-method thread "$@" > gpurun_out/gputests.log 2>&1
     rc=$?; grep -E "passed|failed" gpurun_out/gputests.log | tail -3; exit $rc ;;
