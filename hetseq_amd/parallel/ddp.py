@@ -80,7 +80,9 @@ class FlatDDP(torch.nn.Module):
             self.ranges.append((lo, hi))
             for p in ps:
                 self.bucket_of[id(p)] = bi
-        # extend ranges to cover alignment gaps so the buckets tile the buffer
+        # a bucket covers [first offset, last end) of its parameters, alignment gaps between them
+        # included; gaps between buckets (<= 63 elements of 256-B padding, runtime/flat.py) are in no
+        # range: their gradient entries stay zero on every rank and no parameter reads them
         self._reset_state()
         # Readiness = post-accumulate-grad hooks.  They also fire when a fused
         # Function returned None for a parameter whose gradient it accumulated
