@@ -188,7 +188,7 @@ def main():
         comm_kind = "none" if world == 1 else (
             "rccl-native" if getattr(ctl.model, "comm", None) is not None else "c10d-" + b.dist_backend)
         out = {
-            "metric": "avg sec/step, BERT-base seq128 bs=32/GPU",
+            "metric": "avg sec/step, BERT-base seq%d bs=%d/GPU" % (b.seq_len, b.batch),
             "value": round(sec, 6),
             "unit": "s/step",
             "n_gpus": world,
