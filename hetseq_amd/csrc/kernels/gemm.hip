@@ -400,20 +400,77 @@ HS_DEVICE bfx8 x_frag(const char* __restrict__ S, int row, int p, int ks, int lr
   return *reinterpret_cast<const bfx8*>(S + r * XROW + 64 * p + 16 * xchunk<SWZ>(r, 2 * ks + h));
 }
 
+// Transposed-read layout ("TR", mn-contiguous sources): instead of a register 4x4 transpose into
+// the k-contiguous image, the split planes are stored as read -- [k row][128 mn] bf16, 256-B rows,
+// 16-B chunks XOR-swizzled by 4 (r & 3) -- and each MFMA fragment (8 consecutive k of one mn) is
+// gathered by two ds_read_b64_tr_b16.  The stores are row-contiguous (16 lanes = 128 B of one k
+// row: conflict-free) and the transposed reads hit 4 different bank quarters per k-row quad.
+constexpr int TROW = 256;                // bytes per k row of one plane
+constexpr int TIMG = 3 * GBK * TROW;     // the three planes of one operand tile: 24 KB
+typedef short sx4 __attribute__((ext_vector_type(4)));
+typedef short sx8 __attribute__((ext_vector_type(8)));
+
+HS_DEVICE int tr_swz(int k) { return 4 * (k & 3); }
+
+// v[j] = mn 4g..4g+3 of k row 4c + j (g = t & 31, c = t >> 5): 32 lanes per 512-B k row
+HS_DEVICE void x_load_rows(const char* __restrict__ base, const uint32_t (&o)[4], float4 (&v)[4], int lim = 1 << 30) {
+  const int t = threadIdx.x & 255;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    v[j] = 4 * (t >> 5) + j < lim ? *reinterpret_cast<const float4*>(base + o[j]) : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+template <int NT>
+HS_DEVICE void x_store_tr(char* __restrict__ S, const float4 (&v)[4], int t) {
+  const int g = t & 31, c = t >> 5;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int k = 4 * c + j;
+    uint2 h, m, l;
+    split4<NT>(v[j], h, m, l);
+    char* row = S + k * TROW + 16 * ((g >> 1) ^ tr_swz(k)) + 8 * (g & 1);
+    *reinterpret_cast<uint2*>(row) = h;
+    *reinterpret_cast<uint2*>(row + GBK * TROW) = m;
+    if (NT >= 6) *reinterpret_cast<uint2*>(row + 2 * GBK * TROW) = l;
+  }
+}
+
+// fragment of plane p, k-slice ks, for the 32-wide mn tile at rc: lane 4qq + pp of a 16-lane group
+// addresses k row 16 ks + 8 (g >> 1) + 4 jj + qq, mn columns rc + 16 (g & 1) + 4 pp .. + 3
+HS_DEVICE bfx8 x_frag_tr(const char* __restrict__ S, int rc, int p, int ks, int lane) {
+  const int l16 = lane & 15, qq = l16 >> 2, pp = l16 & 3, g = lane >> 4;
+  const int col = rc + 16 * (g & 1) + 4 * pp;
+  const char* pl = S + p * GBK * TROW;
+  sx4 v[2];
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj) {
+    const int k = 16 * ks + 8 * (g >> 1) + 4 * jj + qq;
+    const char* a = pl + k * TROW + 16 * ((col >> 3) ^ tr_swz(k)) + 2 * (col & 7);
+    v[jj] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) sx4*)(a));
+  }
+  const sx8 u = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w};
+  return __builtin_bit_cast(bfx8, u);
+}
+
 // WV = 4: 2x2 waves of 64x64, every thread stages 4x4 of A and of B.
 // WV = 8: 2x4 waves of 64x32 (twice the waves per CU to hide each other's staging), threads
 //         0-255 stage A and 256-511 stage B with the same 4x4 micro-blocks.
 // PF (4 waves, single buffer): register prefetch depth -- 1 = the next K tile, loaded under the
 // MFMAs of this one; 2 = two register sets, each tile's loads issued two tiles ahead.
-template <bool TA, bool TB, int EPI, int NT, int ABL = 0, int WV = 4, int NBUF = 1, bool EDGE = false, int PF = 1>
+// TRL: mn-contiguous operands in the transposed-read layout (above) instead of the register
+// transpose into k-contiguous images.
+template <bool TA, bool TB, int EPI, int NT, int ABL = 0, int WV = 4, int NBUF = 1, bool EDGE = false, int PF = 1,
+          bool TRL = false>
 __global__ void __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(NBUF == 2 ? 2 : WV / 2, NBUF == 2 ? 2 : WV / 2))) gemm_x6s_kernel(GemmArgs p) {
   constexpr int BM = 128, BN = 128, WC = WV / 2, TM = 2, TN = BN / WC / 32;
   static_assert(NBUF == 1 || WV == 8, "double-buffered images: 8-wave variant only");
   static_assert(!EDGE || (WV == 4 && EPI <= kEpiBias), "edge-masked launches: 4 waves, plain / bias epilogue");
   static_assert(PF == 1 || (WV == 4 && NBUF == 1 && !EDGE), "two-deep prefetch: 4-wave, single-buffer, unmasked");
-  __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * 128 * XROW];
+  constexpr bool TRA = TRL && TA, TRB = TRL && !TB;  // operands staged in the transposed-read layout
+  constexpr int IA = TRA ? TIMG : 128 * XROW, IB = TRB ? TIMG : 128 * XROW;
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * (IA + IB)];
   char* const As = smem;
-  char* const Bs = smem + 128 * XROW;
+  char* const Bs = smem + IA;
 
   const int tiles_m = p.M / BM, tiles_n = p.N / BN, nwg = tiles_m * tiles_n * p.ksplit;
   const int orig = blockIdx.x;
@@ -449,27 +506,45 @@ __global__ void __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(NB
   const char* bb = reinterpret_cast<const char*>(p.B) + (TB ? kofs : (int64_t)kofs * p.ldb) * 4;
   float4 va[4], vb[4];
   int kld = kofs;  // absolute k of the tile ab / bb point at (edge guards of k-row operands)
+  // per-operand staging: k-contiguous image (register transpose for mn-contiguous sources) or,
+  // with TRL, the transposed-read layout
+  auto ldA = [&](const char* base, float4(&v)[4], int lim = 1 << 30) {
+    if (TRA) x_load_rows(base, oa, v, lim);
+    else x_load<!TA>(base, oa, v, lim);
+  };
+  auto ldB = [&](const char* base, float4(&v)[4], int lim = 1 << 30) {
+    if (TRB) x_load_rows(base, ob, v, lim);
+    else x_load<TB>(base, ob, v, lim);
+  };
+  auto stoA = [&](char* S_, const float4(&v)[4]) {
+    if (TRA) x_store_tr<NT>(S_, v, st);
+    else x_store<!TA, NT>(S_, v, st);
+  };
+  auto stoB = [&](char* S_, const float4(&v)[4]) {
+    if (TRB) x_store_tr<NT>(S_, v, st);
+    else x_store<TB, NT>(S_, v, st);
+  };
   auto load = [&]() {
     if (EDGE) {
-      x_load<!TA>(ab, oa, va, TA ? p.Kv - kld : p.Mv - m0);
-      x_load<TB>(bb, ob, vb, TB ? p.Nv - n0 : p.Kv - kld);
+      ldA(ab, va, TA ? p.Kv - kld : p.Mv - m0);
+      ldB(bb, vb, TB ? p.Nv - n0 : p.Kv - kld);
     } else if (WV == 4) {
-      x_load<!TA>(ab, oa, va);
-      x_load<TB>(bb, ob, vb);
+      ldA(ab, va);
+      ldB(bb, vb);
     } else if (stA) {  // wave-uniform branch: one operand per half of the block
-      x_load<!TA>(ab, oa, va);
+      ldA(ab, va);
     } else {
-      x_load<TB>(bb, ob, va);
+      ldB(bb, va);
     }
   };
   auto store = [&]() {
     if (WV == 4) {
-      x_store<!TA, NT>(As, va, st);
-      x_store<TB, NT>(Bs, vb, st);
+      stoA(As, va);
+      stoB(Bs, vb);
     } else if (stA) {
-      x_store<!TA, NT>(As, va, st);
+      stoA(As, va);
     } else {
-      x_store<TB, NT>(Bs, va, st);
+      stoB(Bs, va);
     }
   };
   (void)stB;
@@ -485,9 +560,11 @@ __global__ void __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(NB
 #pragma unroll
       for (int pl = 0; pl < NPL; ++pl) {
 #pragma unroll
-        for (int i = 0; i < TM; ++i) af[ks][pl][i] = x_frag<TA>(Ab, wm + 32 * i, pl, ks, lr, q);
+        for (int i = 0; i < TM; ++i)
+          af[ks][pl][i] = TRA ? x_frag_tr(Ab, wm + 32 * i, pl, ks, lane) : x_frag<TA>(Ab, wm + 32 * i, pl, ks, lr, q);
 #pragma unroll
-        for (int j = 0; j < TN; ++j) bf[ks][pl][j] = x_frag<!TB>(Bb, wn + 32 * j, pl, ks, lr, q);
+        for (int j = 0; j < TN; ++j)
+          bf[ks][pl][j] = TRB ? x_frag_tr(Bb, wn + 32 * j, pl, ks, lane) : x_frag<!TB>(Bb, wn + 32 * j, pl, ks, lr, q);
       }
     between();
 #pragma unroll
@@ -507,18 +584,18 @@ __global__ void __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(NB
     // tile kt+1 into the other buffer needs no barrier before it and overlaps this tile's MFMAs
     // (the weight gradient runs at ~1 block per CU, with no second block to hide a staging
     // phase).  Unrolled by two so the register sets and buffers keep fixed roles.
-    char* const As1 = smem + 2 * 128 * XROW;
-    char* const Bs1 = As1 + 128 * XROW;
+    char* const As1 = smem + IA + IB;
+    char* const Bs1 = As1 + IA;
     const char* gp = stA ? ab : bb;
     const int64_t gs = stA ? sa : sb;
     auto ld = [&](float4(&v)[4], int t) {
       const char* base = gp + (int64_t)min(t, KT - 1) * gs;  // clamped: unconditional loads
-      if (stA) x_load<!TA>(base, oa, v);
-      else x_load<TB>(base, ob, v);
+      if (stA) ldA(base, v);
+      else ldB(base, v);
     };
     auto sto = [&](char* A_, char* B_, const float4(&v)[4]) {
-      if (stA) x_store<!TA, NT>(A_, v, st);
-      else x_store<TB, NT>(B_, v, st);
+      if (stA) stoA(A_, v);
+      else stoB(B_, v);
     };
     float4 r1[4];
     ld(va, 0);
@@ -545,12 +622,12 @@ __global__ void __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(NB
     float4 wa[4], wb[4];
     auto ldt = [&](float4(&xa)[4], float4(&xb)[4], int t) {
       const int64_t tt = min(t, KT - 1);
-      x_load<!TA>(ab + tt * sa, oa, xa);
-      x_load<TB>(bb + tt * sb, ob, xb);
+      ldA(ab + tt * sa, xa);
+      ldB(bb + tt * sb, xb);
     };
     auto stt = [&](const float4(&xa)[4], const float4(&xb)[4]) {
-      x_store<!TA, NT>(As, xa, st);
-      x_store<TB, NT>(Bs, xb, st);
+      stoA(As, xa);
+      stoB(Bs, xb);
     };
     ldt(va, vb, 0);
     stt(va, vb);
@@ -606,6 +683,15 @@ static const int g_x6_pf_env = [] {
   return e && e[0] == '2' ? 2 : 1;
 }();
 static int g_x6_pf = 1;
+// mn-contiguous operands in the transposed-read layout (default; HETSEQ_X6_TR=0 restores the
+// register transpose): weight gradients 7-12 % and NN data gradients 3-10 % faster on the BERT
+// shapes (profiles/r2_gemm_experiments.md).  tile_override bit 8 forces it, bit 9 forces the
+// register-transpose layout.
+static const int g_x6_tr_env = [] {
+  const char* e = std::getenv("HETSEQ_X6_TR");
+  return e && e[0] == '0' ? 0 : 1;
+}();
+static int g_x6_tr = 0;
 // 8-wave variant with double-buffered LDS images (106 KB: one block per CU, one barrier per K
 // tile) -- HETSEQ_X6_DBUF=1; default single buffer (53 KB, blocks of other kernels co-reside).
 static const int g_x6_dbuf = [] {
@@ -661,6 +747,9 @@ void launch_cfg(const GemmArgs& a, hipStream_t st) {
         hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 3, 4>), dim3(blocks), dim3(256), 0, st, a);
       else if (g_x6_pf == 2)
         hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 0, 4, 1, false, 2>), dim3(blocks), dim3(256), 0, st, a);
+      else if (g_x6_tr && (TA || !TB))
+        hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 0, 4, 1, false, 1, true>), dim3(blocks), dim3(256), 0, st,
+                           a);
       else
         hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 0, 4>), dim3(blocks), dim3(256), 0, st, a);
     } else if (g_x6_dbuf) {
@@ -675,6 +764,9 @@ void launch_cfg(const GemmArgs& a, hipStream_t st) {
     } else {
       if (EPI == kEpiNone && g_ablation == 1)
         hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 1, 8>), dim3(blocks), dim3(512), 0, st, a);
+      else if (g_x6_tr && (TA || !TB))
+        hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 0, 8, 1, false, 1, true>), dim3(blocks), dim3(512), 0, st,
+                           a);
       else
         hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 0, 8>), dim3(blocks), dim3(512), 0, st, a);
     }
@@ -777,6 +869,8 @@ int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, i
   g_x6_waves = tile_override >= 0 && (tile_override & 32) ? 4 : tile_override >= 0 && (tile_override & 64) ? 8
                                                               : ta ? 8 : 4;
   g_x6_pf = tile_override >= 0 && (tile_override & 128) ? 2 : g_x6_pf_env;
+  g_x6_tr = tile_override >= 0 && (tile_override & 256) ? 1 : tile_override >= 0 && (tile_override & 512) ? 0
+                                                              : g_x6_tr_env;
   tile_override = tile_override >= 0 ? (tile_override & 3) : -1;
   if (tile_override >= 0) {  // benchmarking hook: force a tile shape (must divide the problem)
     const int bm = tile_override == 2 ? 64 : 128, bn = tile_override == 0 ? 128 : 64;

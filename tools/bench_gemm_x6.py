@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--waves", type=int, default=8, help="with --only: waves per block of the split kernel (4/8)")
     ap.add_argument("--ablate", type=int, default=0, help="with --only: 1 no global loads, 2 + no staging, 3 + no barriers")
     ap.add_argument("--pf", type=int, default=1, help="with --only: 4-wave register prefetch depth (1/2)")
+    ap.add_argument("--tr", type=int, default=-1, help="with --only: 1 transposed-read layout, 0 register transpose")
+    ap.add_argument("--ks", type=int, default=1, help="with --only: split-K slices")
     a = ap.parse_args()
     if a.only:
         M, N, K, ta, tb, eng = a.only.split(",")
@@ -38,13 +40,14 @@ def main():
         B = torch.rand((N, K) if tb else (K, N), device="cuda") * 2 - 1
         C = torch.empty(M, N, device="cuda")
         f = (lambda: torch.mm(A.t() if ta else A, B.t() if tb else B, out=C)) if eng == "blas" else \
-            (lambda: G._hip_gemm(A, B, ta, tb, C, fp32=eng, ksplit=1,
-                                 tile=(a.ablate << 3) | (32 if a.waves == 4 else 64) | (128 if a.pf == 2 else 0)))
+            (lambda: G._hip_gemm(A, B, ta, tb, C, fp32=eng, ksplit=a.ks,
+                                 tile=(a.ablate << 3) | (32 if a.waves == 4 else 64) | (128 if a.pf == 2 else 0)
+                                 | (256 if a.tr == 1 else 512 if a.tr == 0 else 0)))
         t = timeit(f, a.reps)
         f()
         At, Bt = (A.t() if ta else A).double(), (B.t() if tb else B).double()
         err = float(((C.double() - At @ Bt).abs() / (At.abs() @ Bt.abs())).max())
-        print("%s w%d pf%d%s %dx%dx%d %.1fus %.1fTF err %.2e" % (eng, a.waves, a.pf, " ablate=%d" % a.ablate if a.ablate
+        print("%s tr%d ks%d w%d pf%d%s %dx%dx%d %.1fus %.1fTF err %.2e" % (eng, a.tr, a.ks, a.waves, a.pf, " ablate=%d" % a.ablate if a.ablate
                                                                 else "", M, N, K, t, 2.0 * M * N * K / t / 1e6, err))
         return
     from hetseq_amd.runtime import gemm_tuning
