@@ -2,12 +2,13 @@
 //
 // Used to finalize the per-block column partials written by the LayerNorm /
 // GELU / bias-gradient kernels (no atomics, deterministic order).  A block of
-// 32 columns x 32 row-groups (1024 threads): each wave reads 2 x 128-B
-// coalesced row segments per step, each thread sums nparts/32 rows with 4
-// independent accumulators (the loads issue back to back instead of forming
-// one dependent chain), and the 32 partial sums are combined through LDS.
-// grid = (ceil(N/32), n_arrays).  The finalize is latency-bound (a few hundred
-// partial rows), so the aim is many loads in flight, not bandwidth.
+// 32 columns x 8 row-groups (256 threads): each thread sums nparts/8 rows with
+// 4 independent accumulators (the loads issue back to back instead of forming
+// one dependent chain), and the 8 partial sums are combined through LDS in a
+// fixed order.  grid = (ceil(N/32), n_arrays).  Small blocks on purpose: these
+// run beside the weight-gradient GEMM blocks of the side stream, where a
+// 1024-thread block waits for a whole CU to drain (12 us per call inside the
+// step vs 4.6 us alone).
 #pragma once
 #include "common.h"
 
@@ -19,8 +20,8 @@ struct ReduceArgs {
   float* out[3];
 };
 
-__global__ void __launch_bounds__(1024) reduce_rows_kernel(ReduceArgs args, int nparts, int N, int accumulate) {
-  __shared__ float red[32][33];
+__global__ void __launch_bounds__(256) reduce_rows_kernel(ReduceArgs args, int nparts, int N, int accumulate) {
+  __shared__ float red[8][33];
   const float* part = args.part[blockIdx.y];
   float* out = args.out[blockIdx.y];
   const int cx = threadIdx.x & 31, ry = threadIdx.x >> 5;
@@ -28,20 +29,20 @@ __global__ void __launch_bounds__(1024) reduce_rows_kernel(ReduceArgs args, int 
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   if (c < N) {
     int r = ry;
-    for (; r + 96 < nparts; r += 128) {
+    for (; r + 24 < nparts; r += 32) {
       s0 += part[(int64_t)r * N + c];
-      s1 += part[(int64_t)(r + 32) * N + c];
-      s2 += part[(int64_t)(r + 64) * N + c];
-      s3 += part[(int64_t)(r + 96) * N + c];
+      s1 += part[(int64_t)(r + 8) * N + c];
+      s2 += part[(int64_t)(r + 16) * N + c];
+      s3 += part[(int64_t)(r + 24) * N + c];
     }
-    for (; r < nparts; r += 32) s0 += part[(int64_t)r * N + c];
+    for (; r < nparts; r += 8) s0 += part[(int64_t)r * N + c];
   }
   red[ry][cx] = (s0 + s1) + (s2 + s3);
   __syncthreads();
   if (ry == 0 && c < N) {
     float t = 0.f;
 #pragma unroll
-    for (int i = 0; i < 32; ++i) t += red[i][cx];
+    for (int i = 0; i < 8; ++i) t += red[i][cx];
     out[c] = accumulate ? out[c] + t : t;
   }
 }
@@ -53,7 +54,7 @@ inline void launch_reduce_rows(const float* const* parts, float* const* outs, in
     a.part[i] = parts[i];
     a.out[i] = outs[i];
   }
-  hipLaunchKernelGGL(reduce_rows_kernel, dim3((N + 31) / 32, n), dim3(1024), 0, st, a, nparts, N, accumulate);
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3((N + 31) / 32, n), dim3(256), 0, st, a, nparts, N, accumulate);
 }
 
 }  // namespace
