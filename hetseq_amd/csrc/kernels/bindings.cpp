@@ -82,6 +82,21 @@ int launch_gemm_planes(int planes, int c_dtype, int ta, int tb, int M, int N, in
 void launch_split_planes(const float* x, void* out, int64_t n, int64_t ps, hipStream_t st);
 void set_planes_variant(int v);
 
+// mnist.hip
+void launch_mnist_conv1_fwd(const float*, const float*, const float*, float*, int, hipStream_t);
+void launch_mnist_im2col(const float*, float*, int, int, hipStream_t);
+void launch_mnist_perm(const float*, float*, int, int, hipStream_t);
+void launch_mnist_pool_fwd(const float*, float*, uint8_t*, int, int, float, uint64_t, uint64_t, hipStream_t);
+void launch_mnist_pool_bwd(const float*, const uint8_t*, float*, int, int, float, hipStream_t);
+void launch_mnist_head_fwd(const float*, const float*, const float*, const int64_t*, float*, float*, float*, int, float,
+                           uint64_t, uint64_t, hipStream_t);
+void launch_mnist_loss(const float*, const float*, const int64_t*, int, int, float*, float*, float*, hipStream_t);
+void launch_mnist_head_bwd(const float*, const float*, const float*, const int64_t*, const float*, const float*,
+                           const float*, float*, float*, int, int, int, float, hipStream_t);
+void launch_mnist_fc2_wgrad(const float*, const float*, float*, float*, float*, int, hipStream_t);
+void launch_mnist_col2im(const float*, const float*, float*, int, hipStream_t);
+void launch_mnist_conv1_wgrad(const float*, const float*, float*, float*, float*, int, hipStream_t);
+
 // HIP-graph mode: device word holding the dropout seed (see common.h resolve_seed)
 namespace hs {
 const uint64_t* g_seed_dev = nullptr;
@@ -191,6 +206,73 @@ PYBIND11_MODULE(_hip, m) {
     (void)hipGetLastError();
     return launch_sort_keys(P(const int64_t*, keys), n, bound, P(int64_t*, out_keys), P(int64_t*, out_order), ST(st));
   }, "stable sort of n int64 keys in [0, bound): sorted keys + source indices; -1 = unsupported size");
+  // ---- MNISTNet (mnist.hip); every entry raw pointers + batch size + stream
+  m.def("mnist_conv1_fwd", [](i64 x, i64 w, i64 b, i64 y, int B, i64 st) {
+    (void)hipGetLastError();
+    launch_mnist_conv1_fwd(P(const float*, x), P(const float*, w), P(const float*, b), P(float*, y), B, ST(st));
+    check_launch("mnist_conv1_fwd");
+  });
+  m.def("mnist_im2col", [](i64 h1, i64 col, int B, int R, i64 st) {
+    (void)hipGetLastError();
+    check(R >= B * 576 ? 0 : -1, "mnist_im2col");
+    launch_mnist_im2col(P(const float*, h1), P(float*, col), B, R, ST(st));
+    check_launch("mnist_im2col");
+  });
+  m.def("mnist_perm", [](i64 src, i64 dst, int rows, int mode, i64 st) {
+    (void)hipGetLastError();
+    check(mode >= 0 && mode <= 3 ? 0 : -1, "mnist_perm");
+    launch_mnist_perm(P(const float*, src), P(float*, dst), rows, mode, ST(st));
+    check_launch("mnist_perm");
+  });
+  m.def("mnist_pool_fwd", [](i64 c2, i64 pooled, i64 arg, int B, int Bp, float p, u64 seed, u64 off, i64 st) {
+    (void)hipGetLastError();
+    launch_mnist_pool_fwd(P(const float*, c2), P(float*, pooled), P(uint8_t*, arg), B, Bp, p, seed, off, ST(st));
+    check_launch("mnist_pool_fwd");
+  });
+  m.def("mnist_pool_bwd", [](i64 dpooled, i64 arg, i64 dc2, int B, int R, float p, i64 st) {
+    (void)hipGetLastError();
+    check(R >= B * 576 ? 0 : -1, "mnist_pool_bwd");
+    launch_mnist_pool_bwd(P(const float*, dpooled), P(const uint8_t*, arg), P(float*, dc2), B, R, p, ST(st));
+    check_launch("mnist_pool_bwd");
+  });
+  m.def("mnist_head_fwd", [](i64 pre, i64 w2, i64 b2, i64 target, i64 h, i64 logp, i64 nll, int B, float p, u64 seed,
+                             u64 off, i64 st) {
+    (void)hipGetLastError();
+    launch_mnist_head_fwd(P(const float*, pre), P(const float*, w2), P(const float*, b2), P(const int64_t*, target),
+                          P(float*, h), P(float*, logp), P(float*, nll), B, p, seed, off, ST(st));
+    check_launch("mnist_head_fwd");
+  });
+  m.def("mnist_loss", [](i64 nll, i64 logp, i64 target, int B, int mean, i64 loss, i64 correct, i64 count, i64 st) {
+    (void)hipGetLastError();
+    launch_mnist_loss(P(const float*, nll), P(const float*, logp), P(const int64_t*, target), B, mean, P(float*, loss),
+                      P(float*, correct), P(float*, count), ST(st));
+    check_launch("mnist_loss");
+  });
+  m.def("mnist_head_bwd", [](i64 dloss, i64 count, i64 logp, i64 target, i64 pre, i64 h, i64 w2, i64 dlogits,
+                             i64 dpre, int B, int Bp, int mean, float p, i64 st) {
+    (void)hipGetLastError();
+    launch_mnist_head_bwd(P(const float*, dloss), P(const float*, count), P(const float*, logp),
+                          P(const int64_t*, target), P(const float*, pre), P(const float*, h), P(const float*, w2),
+                          P(float*, dlogits), P(float*, dpre), B, Bp, mean, p, ST(st));
+    check_launch("mnist_head_bwd");
+  });
+  m.def("mnist_fc2_wgrad", [](i64 dlogits, i64 h, i64 part, i64 dw2, i64 db2, int B, i64 st) {
+    (void)hipGetLastError();  // part: 64 * 1290 floats of scratch
+    launch_mnist_fc2_wgrad(P(const float*, dlogits), P(const float*, h), P(float*, part), P(float*, dw2),
+                           P(float*, db2), B, ST(st));
+    check_launch("mnist_fc2_wgrad");
+  });
+  m.def("mnist_col2im", [](i64 dcol, i64 h1, i64 dh1, int B, i64 st) {
+    (void)hipGetLastError();
+    launch_mnist_col2im(P(const float*, dcol), P(const float*, h1), P(float*, dh1), B, ST(st));
+    check_launch("mnist_col2im");
+  });
+  m.def("mnist_conv1_wgrad", [](i64 dh1, i64 x, i64 part, i64 dw1, i64 db1, int B, i64 st) {
+    (void)hipGetLastError();  // part: 1024 * 320 floats of scratch
+    launch_mnist_conv1_wgrad(P(const float*, dh1), P(const float*, x), P(float*, part), P(float*, dw1),
+                             P(float*, db1), B, ST(st));
+    check_launch("mnist_conv1_wgrad");
+  });
   m.def("segsum_rows", [](i64 src, i64 order, i64 keys, i64 scratch, i64 dst, int n, int H, int K, i64 st) {
     (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
     check(launch_segsum_rows(P(const float*, src), P(const int64_t*, order), P(const int64_t*, keys),

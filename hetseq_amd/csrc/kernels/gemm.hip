@@ -843,7 +843,7 @@ static int pick_tile_split(int M, int N, int K, int* ksplit) {
 // epi: 0 none, 1 +bias, 2 gelu(+bias) writing the pre-activation to aux,
 // 3 dgelu (aux = pre-activation) with column sums of C written (or added,
 // colsum_acc) to colsum_out.  part: scratch of (M/64)*N floats (epi 3 only).
-// ksplit: 0 = automatic (split dtypes only), 1 = none, >1 forced; slab: ksplit*M*N floats
+// ksplit: 0 = automatic (split dtypes only), 1 = none, >1 forced (any dtype); slab: ksplit*M*N floats
 // of scratch when the split is >1 (epi 0/1 only).  mv/nv/kv: valid extents of a padded problem.
 // Returns -1 when the request is not served (caller falls back to the library).
 int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, int64_t lda, const void* B,
@@ -863,6 +863,7 @@ int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, i
     if (epi >= 2 || !slab) ks = 1;  // fused GELU epilogues need the whole K in one block
   } else {
     tile = pick_tile(M, N);
+    if (ksplit > 1 && epi <= kEpiBias && slab) ks = ksplit;  // exact-fp32 engine: forced split only
   }
   const bool mfma16 = !nt && tile_override >= 0 && (tile_override & 4);  // benchmarking hook: 16x16x4 MFMA
   g_ablation = tile_override >= 0 ? (tile_override >> 3) & 3 : 0;

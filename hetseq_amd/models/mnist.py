@@ -4,7 +4,9 @@ conv(1->32,3) -> ReLU -> conv(32->64,3) -> ReLU -> maxpool2 -> Dropout2d(.25)
 -> flatten -> fc(9216->128) -> ReLU -> Dropout2d(.5) -> fc(128->10) ->
 log_softmax -> NLL.  ``forward(x, target)`` returns the loss (task contract);
 ``eval=True`` returns (loss summed over the batch, number correct) for the
-evaluator.
+evaluator.  On a GPU the whole network runs on the gfx950 kernels of
+``ops/mnist_ops.py`` (K15); ``logits`` is the torch-op path (CPU, and the
+numerics oracle of tests/test_mnist_gpu.py).
 """
 import torch
 import torch.nn.functional as F
@@ -34,6 +36,13 @@ class MNISTNet(nn.Module):
         return self.fc2(x)
 
     def forward(self, x, target, eval=False):
+        from hetseq_amd.ops._C import use_fused
+
+        if use_fused(x) and x.shape[1:] == (1, 28, 28):  # K15: the whole network on the gfx950 kernels
+            from hetseq_amd.ops.mnist_ops import mnist_loss
+
+            loss, correct = mnist_loss(self, x, target, eval=eval)
+            return (loss, correct) if eval else loss
         output = F.log_softmax(self.logits(x), dim=1)
         if eval:
             loss = F.nll_loss(output, target, reduction="sum")

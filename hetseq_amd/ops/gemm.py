@@ -297,7 +297,7 @@ def _hip_gemm(a, b, ta, tb, out, bias=None, epi=EPI_NONE, beta=0.0, aux=None, pa
     mv, nv, kv = valid if valid is not None else (0, 0, 0)
     assert dims is not None or out.shape == (M, N)
     dt = _FP32_DT[fp32 or _FP32]
-    slab = _slab(M, N, ksplit, a.device) if dt and epi <= EPI_BIAS and ksplit != 1 else None
+    slab = _slab(M, N, ksplit, a.device) if (dt or ksplit > 1) and epi <= EPI_BIAS and ksplit != 1 else None
     rc = hip().gemm(dt, int(ta), int(tb), M, N, K, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0),
                     out.data_ptr(), out.stride(0), bias.data_ptr() if bias is not None else 0, epi, float(beta),
                     aux.data_ptr() if aux is not None else 0, aux.stride(0) if aux is not None else 0,

@@ -1,0 +1,141 @@
+"""MNISTNet on the gfx950 kernels (K15, ops/mnist_ops.py) against the torch-op network."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref_loss(model, x, target, eval=False):
+    out = F.log_softmax(model.logits(x), dim=1)
+    if eval:
+        return F.nll_loss(out, target, reduction="sum"), out.argmax(1).eq(target).sum()
+    return F.nll_loss(out, target)
+
+
+def _routed_ref_loss(model, ref, x, t):
+    """fp64 loss of the torch-op network whose ReLU masks and 2x2-max choices are the ones the fused
+    fp32 forward made.  A conv output within fp32 rounding of zero, or two window entries within
+    rounding of each other, routes the gradient differently in fp32 and fp64 (seed 128 has a conv2
+    value of 2.4e-8 that fp32 evaluates as <= 0): pinning the discrete decisions to the kernel's own
+    keeps the comparison about arithmetic, not about which side of a tie fp32 lands on."""
+    from hetseq_amd.ops import mnist_ops as MO
+    from hetseq_amd.ops._C import hip, stream_handle
+
+    B = x.shape[0]
+    st = stream_handle()
+    R = (B * 576 + MO.ROWS - 1) // MO.ROWS * MO.ROWS
+    with torch.no_grad():
+        h1 = torch.empty(B, 26, 26, 32, device=x.device)
+        hip().mnist_conv1_fwd(x.data_ptr(), model.conv1.weight.data_ptr(), model.conv1.bias.data_ptr(),
+                              h1.data_ptr(), B, st)
+        col = torch.empty(R, MO.KP, device=x.device)
+        hip().mnist_im2col(h1.data_ptr(), col.data_ptr(), B, R, st)
+        c2 = MO._mm(col, MO._perm(model.conv2.weight.contiguous(), 64, MO.KP, 0), False, True,
+                    torch.empty(R, 64, device=x.device), model.conv2.bias)
+        c2 = F.relu(c2[:B * 576].view(B, 24, 24, 64).permute(0, 3, 1, 2))
+        pooled32, idx = F.max_pool2d(c2, 2, return_indices=True)
+        h1 = h1.permute(0, 3, 1, 2)
+    a1 = F.conv2d(x.double(), ref.conv1.weight, ref.conv1.bias) * (h1 > 0)
+    a2 = F.conv2d(a1, ref.conv2.weight, ref.conv2.bias).flatten(2)
+    p = torch.gather(a2, 2, idx.flatten(2)).view_as(pooled32) * (pooled32 > 0)
+    hid = F.relu(ref.fc1(p.flatten(1)))
+    return F.nll_loss(F.log_softmax(ref.fc2(hid), dim=1), t)
+
+
+@pytest.mark.parametrize("B", [64, 37, 128])
+def test_mnist_fused_matches_torch(cuda, B):
+    """Loss and every parameter gradient (dropout off) against an fp64 run of the torch-op network
+    (with the fused forward's ReLU / max-pool decisions, see _routed_ref_loss), at the error level
+    of the torch fp32 path (the conv1 weight gradient sums B * 676 terms with heavy cancellation, so
+    a fixed relative bound would only measure fp32 itself)."""
+    from hetseq_amd.models.mnist import MNISTNet
+    from hetseq_amd.ops.mnist_ops import mnist_loss
+
+    torch.manual_seed(B)
+    model = MNISTNet().to(cuda).eval()  # eval: no dropout, so every path sees the same network
+    ref = MNISTNet().to(cuda).double().eval()
+    ref.load_state_dict({k: v.double() for k, v in model.state_dict().items()})
+    plain = MNISTNet().to(cuda).double().eval()
+    plain.load_state_dict(ref.state_dict())
+    f32 = MNISTNet().to(cuda).eval()
+    f32.load_state_dict(model.state_dict())
+    x = torch.randn(B, 1, 28, 28, device=cuda)
+    t = torch.randint(0, 10, (B,), device=cuda)
+    loss, _ = mnist_loss(model, x, t, eval=False)
+    loss.backward()
+    rl = _routed_ref_loss(model, ref, x, t)
+    rl.backward()
+    pl = _ref_loss(plain, x.double(), t)
+    pl.backward()
+    assert abs(float(pl.detach()) - float(rl.detach())) <= 1e-6
+    _ref_loss(f32, x, t).backward()
+    assert abs(float(loss.detach()) - float(rl.detach())) <= 1e-5 * max(1.0, abs(float(rl.detach())))
+    named = zip(model.named_parameters(), ref.parameters(), plain.parameters(), f32.parameters())
+    for (n, p), q, u, r in named:
+        # ours against the routed fp64 reference; torch fp32 against the plain one (its own routing)
+        err = float((p.grad.double() - q.grad).abs().max())
+        err32 = float((r.grad.double() - u.grad).abs().max())
+        scale = float(q.grad.abs().max()) + 1e-12
+        assert err <= max(4 * err32, 2e-5 * scale), (n, err, err32, scale)
+
+
+def test_mnist_fused_eval_sum_and_correct(cuda):
+    from hetseq_amd.models.mnist import MNISTNet
+
+    torch.manual_seed(3)
+    model = MNISTNet().to(cuda).eval()
+    x = torch.randn(200, 1, 28, 28, device=cuda)
+    t = torch.randint(0, 10, (200,), device=cuda)
+    with torch.no_grad():
+        loss, correct = model(x, t, eval=True)
+        rl, rc = _ref_loss(model, x, t, eval=True)
+    assert abs(float(loss) - float(rl)) <= 1e-4 * abs(float(rl))
+    assert int(correct) == int(rc)
+
+
+def test_mnist_fused_dropout_training(cuda):
+    """Training mode: dropout draws are reproducible from the seed, drop about p of the units, and a
+    few SGD steps on one batch lower its loss."""
+    from hetseq_amd.models.mnist import MNISTNet
+    from hetseq_amd.runtime import rng
+
+    torch.manual_seed(5)
+    model = MNISTNet().to(cuda).train()
+    x = torch.randn(64, 1, 28, 28, device=cuda)
+    t = torch.randint(0, 10, (64,), device=cuda)
+    rng.set_seed(11)
+    l1 = model(x, t)
+    rng.set_seed(11)
+    l2 = model(x, t)
+    assert float(l1) == float(l2)
+    opt = torch.optim.SGD(model.parameters(), lr=0.05)
+    losses = []
+    for i in range(8):
+        rng.set_seed(100 + i)
+        opt.zero_grad()
+        loss = model(x, t)
+        loss.backward()
+        opt.step()
+        losses.append(float(loss))
+    assert losses[-1] < losses[0]
+
+
+def test_mnist_fused_launches_no_torch_conv(cuda):
+    """The fused path runs no at::native / MIOpen convolution, pooling or softmax kernels."""
+    from torch.profiler import ProfilerActivity, profile
+
+    from hetseq_amd.models.mnist import MNISTNet
+
+    model = MNISTNet().to(cuda).train()
+    x = torch.randn(64, 1, 28, 28, device=cuda)
+    t = torch.randint(0, 10, (64,), device=cuda)
+    model(x, t).backward()
+    torch.cuda.synchronize()
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        model(x, t).backward()
+        torch.cuda.synchronize()
+    names = [e.name for e in prof.events() if e.device_type.name == "CUDA"]
+    bad = [n for n in names if any(s in n.lower() for s in ("miopen", "conv", "max_pool", "softmax", "nll_loss"))
+           and "hs::" not in n and "Cijk" not in n]
+    assert not bad, bad[:5]
