@@ -139,3 +139,35 @@ def test_mnist_fused_launches_no_torch_conv(cuda):
     bad = [n for n in names if any(s in n.lower() for s in ("miopen", "conv", "max_pool", "softmax", "nll_loss"))
            and "hs::" not in n and "Cijk" not in n]
     assert not bad, bad[:5]
+
+
+def test_mnist_train_and_eval_scripts_on_gpu(tmp_path):
+    """train.py --task mnist on the GPU (K15 kernels, flat-store Adadelta) for two epochs of a
+    synthetic set, then eval_mnist.py on the saved checkpoint: the whole user-facing MNIST flow."""
+    import os
+    import re
+    import subprocess
+    import sys
+
+    from hetseq_amd.data.synthetic import write_mnist
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    d = tmp_path / "mnist"
+    write_mnist(str(d), n_train=512, n_test=128, seed=4)
+    env = dict(os.environ)
+    env["PYTHONPATH"] = root + os.pathsep + env.get("PYTHONPATH", "")
+    save = str(tmp_path / "ck")
+    out = subprocess.run([sys.executable, os.path.join(root, "train.py"), "--task", "mnist", "--optimizer", "adadelta",
+                          "--lr", "1.0", "--data", str(d), "--max-sentences", "64", "--valid-subset", "test",
+                          "--max-epoch", "2", "--save-dir", save, "--clip-norm", "0", "--log-format", "simple",
+                          "--log-interval", "1", "--device-id", "0"],
+                         stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env, timeout=300)
+    assert out.returncode == 0, out.stdout[-3000:]
+    losses = [float(m) for m in re.findall(r"loss=([0-9.]+)", out.stdout)]
+    assert losses and losses[-1] < losses[0], losses
+    ck = os.path.join(save, "checkpoint_last.pt")
+    assert os.path.exists(ck)
+    ev = subprocess.run([sys.executable, os.path.join(root, "eval_mnist.py"), "--model_ckpt", ck, "--mnist_dir",
+                         str(d)], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env, timeout=300)
+    assert ev.returncode == 0, ev.stdout[-3000:]
+    assert "Accuracy" in ev.stdout or "accuracy" in ev.stdout, ev.stdout[-2000:]
