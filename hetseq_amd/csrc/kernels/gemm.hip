@@ -736,8 +736,13 @@ void launch_cfg(const GemmArgs& a, hipStream_t st) {
   const int blocks = (a.M / BM) * (a.N / BN) * a.ksplit;
   if constexpr (NT > 0) {
     if (a.Mv != a.M || a.Nv != a.N || a.Kv != a.K) {  // padded problem (launch_gemm checked epi)
-      if constexpr (EPI <= kEpiBias)
-        hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 0, 4, 1, true>), dim3(blocks), dim3(256), 0, st, a);
+      if constexpr (EPI <= kEpiBias) {
+        if (g_x6_tr && (TA || !TB))
+          hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 0, 4, 1, true, 1, true>), dim3(blocks), dim3(256), 0, st,
+                             a);
+        else
+          hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 0, 4, 1, true>), dim3(blocks), dim3(256), 0, st, a);
+      }
     } else if (g_x6_waves == 4) {
       if (EPI == kEpiNone && g_ablation == 1)
         hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 1, 4>), dim3(blocks), dim3(256), 0, st, a);
