@@ -43,6 +43,8 @@ def main():
     acc = (torch.zeros(H, device="cuda"), torch.zeros(H, device="cuda"), torch.zeros(H, device="cuda"))
     t = timeit(lambda: bert_ops.ln_bwd(dy, z, mean, rstd, g, 0.1, 1, 1, 2, True, True, acc=acc), a.reps)
     print("ln_bwd (BDR, dz + da, accumulate): %.1f us = %.2f TB/s" % (t, 4 * rows * H * 4 / t / 1e6))
+    t = timeit(lambda: bert_ops.ln_bwd(dy, z, mean, rstd, g, 0.0, 1, 1, 2, True, True, acc=acc), a.reps)
+    print("ln_bwd (BDR, p = 0): %.1f us" % t)
     ids = torch.randint(0, 30522, (rows,), device="cuda")
     t = timeit(lambda: bert_ops.sort_keys(ids, 30522), a.reps)
     tt = timeit(lambda: torch.sort(ids, stable=True), a.reps)
