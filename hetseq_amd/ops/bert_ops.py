@@ -414,6 +414,7 @@ class FusedBertLayer(torch.autograd.Function):
         # (runtime/streams.py) and overlap the data-gradient chain; without a flat store they
         # stay in order
         side = acc and streams.enabled()
+        dks = streams.DGRAD_KSPLIT if side else None  # K split of the dgrads beside the side stream
         dz2, do_, dg2, dbb2, db2 = ln_bwd(dh2, z2, m2, r2, W.g2, p_h, 1, s_2, o_2, True, True,
                                           acc=(Gv.g2, Gv.bb2, Gv.b2) if acc else None, side=side)
 
@@ -428,12 +429,12 @@ class FusedBertLayer(torch.autograd.Function):
         df1pre, dbi = G.linear_dgrad_dgelu(do_p, W.w2, f1pre, W.bi, db_acc=Gv.bi if acc else None)
         df1p = sp(df1pre)
         dW1 = wgrad(df1p, h1, Gv.w1 if acc else None)
-        dh1 = G.linear_dgrad(df1p, W.w1, out=dz2, accumulate=True)  # dz2 + df1pre @ W1
+        dh1 = G.linear_dgrad(df1p, W.w1, out=dz2, accumulate=True, ksplit=dks)  # dz2 + df1pre @ W1
         dz1, da1, dg1, db1, dbo = ln_bwd(dh1, z1, m1, r1, W.g1, p_h, 1, s_1, o_1, True, True,
                                          acc=(Gv.g1, Gv.b1, Gv.bo) if acc else None, side=side)
         da1p = sp(da1)
         dWo = wgrad(da1p, cin, Gv.wo if acc else None)
-        dctx = G.linear_dgrad(da1p, W.wo)
+        dctx = G.linear_dgrad(da1p, W.wo, ksplit=dks)
         dqkv = attn_bwd(qkv, mask, ctx_, dctx, (lse, dmask), B, S, NH, p_a, bias=W.bqkv)
         dqkvp = sp(dqkv)
         dWqkv = wgrad(dqkvp, xin, Gv.wqkv if acc else None)
@@ -441,7 +442,7 @@ class FusedBertLayer(torch.autograd.Function):
             dbqkv = streams.run(dqkv.device, lambda: colsum(dqkv, acc=Gv.bqkv), dqkv)
         else:
             dbqkv = colsum(dqkv, acc=Gv.bqkv if acc else None)
-        dx = G.linear_dgrad(dqkvp, W.wqkv, out=dz1, accumulate=True)  # dz1 + dqkv @ Wqkv
+        dx = G.linear_dgrad(dqkvp, W.wqkv, out=dz1, accumulate=True, ksplit=dks)  # dz1 + dqkv @ Wqkv
         if acc:
             return (dx, None, None) + (None,) * 16
         return (dx, None, None,

@@ -533,9 +533,9 @@ def linear_fwd(x, w, bias=None, out=None):
     return gemm(x, w, ta=False, tb=True, out=out, bias=bias, epi=EPI_BIAS if bias is not None else EPI_NONE)
 
 
-def linear_dgrad(dy, w, out=None, accumulate=False):
+def linear_dgrad(dy, w, out=None, accumulate=False, ksplit=None):
     """dy[T,N] @ w[N,K]; accumulate=True adds into ``out``."""
-    return gemm(dy, w, ta=False, tb=False, out=out, beta=1.0 if accumulate else 0.0)
+    return gemm(dy, w, ta=False, tb=False, out=out, beta=1.0 if accumulate else 0.0, ksplit=ksplit)
 
 
 def linear_wgrad(dy, x, out=None, accumulate=False, ksplit=None):

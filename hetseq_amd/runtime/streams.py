@@ -43,6 +43,13 @@ _ENABLED = os.environ.get("HETSEQ_WGRAD_STREAM", "1") == "1"
 # "auto" = use the isolated measurement.
 _ks = os.environ.get("HETSEQ_SIDE_KSPLIT", "2")
 SIDE_KSPLIT = None if _ks == "auto" else int(_ks)
+# split-K of the compute-stream data-gradient GEMMs while the side stream runs the weight
+# gradients beside them: the two streams fill the chip together, so the K split the isolated
+# measurement picks (4 slices for the N = 768 products) only adds slab traffic and a reduction
+# pass.  1 measured best (BERT-base fp32, interleaved runs: 15.53 / 15.55 ms/step vs 15.72 with the
+# isolated choice, profiles/r2_gemm_experiments.md); "auto" = use the isolated measurement.
+_dks = os.environ.get("HETSEQ_DGRAD_KSPLIT", "1")
+DGRAD_KSPLIT = None if _dks == "auto" else int(_dks)
 _STREAMS: dict = {}
 _state = {"queued": False}
 
