@@ -694,22 +694,27 @@ __global__ void __launch_bounds__(256, 2)
 // wave splits only its own K / V (or Q / dO) fragments and the P / dS registers.  48 KB of
 // LDS, two blocks per CU.
 
-// dK / dV for 32 keys per wave (lane = key) over 64-query chunks of Q (biased, * 1/8) and dO.
-__global__ void __launch_bounds__(256, 2)
-    attn_bwd_dkv_x6p_kernel(const float* __restrict__ qkv, const int64_t* __restrict__ mask,
-                            const float* __restrict__ bqkv, const float* __restrict__ dctx,
-                            const float* __restrict__ lse, const float* __restrict__ Dd, float* __restrict__ dqkv,
-                            int S, int NH, float p, const uint32_t* __restrict__ dmask) {
-  __shared__ __attribute__((aligned(16))) char Qp[kPImg];
-  __shared__ __attribute__((aligned(16))) char Op[kPImg];
-  __shared__ float Ls[64];
-  __shared__ float Ds[64];
-  __shared__ uint32_t Wd[64][4];
+// LDS of one block of the backward pair: the dKV role's Q / dO plane images + per-query lse, D
+// and keep words, or the dQ role's K / V plane images + key mask (the larger layout: 50.7 KB)
+constexpr int kBwdSmem = 2 * kPImg + 64 * 4 * 2 + 64 * 4 * 4;
+
+// dK / dV for 32 keys per wave (lane = key) over 64-query chunks of Q (biased, * 1/8) and dO;
+// bx = the block's 128-key group.
+HS_DEVICE void dkv_x6p_body(char* __restrict__ smem, int bx, const float* __restrict__ qkv,
+                            const int64_t* __restrict__ mask, const float* __restrict__ bqkv,
+                            const float* __restrict__ dctx, const float* __restrict__ lse,
+                            const float* __restrict__ Dd, float* __restrict__ dqkv, int S, int NH, float p,
+                            const uint32_t* __restrict__ dmask) {
+  char* const Qp = smem;
+  char* const Op = smem + kPImg;
+  float* const Ls = reinterpret_cast<float*>(smem + 2 * kPImg);
+  float* const Ds = Ls + 64;
+  uint32_t(*const Wd)[4] = reinterpret_cast<uint32_t(*)[4]>(Ds + 64);
   const int H = NH * kXD;
   const int64_t ld = 3 * (int64_t)H;
   const int bh = blockIdx.y, b = bh / NH, h = bh % NH;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hf = lane >> 5, li = lane & 31;
-  const int k0 = blockIdx.x * 128 + w * 32;
+  const int k0 = bx * 128 + w * 32;
   const bool active = k0 < S;
   const int key = k0 + li;
   const float* rows = qkv + (int64_t)b * S * ld;
@@ -749,7 +754,7 @@ __global__ void __launch_bounds__(256, 2)
     }
     if (p > 0.f)
       for (int i = threadIdx.x; i < clen * 4; i += blockDim.x) {
-        const int qi = i >> 2, kw = blockIdx.x * 4 + (i & 3);
+        const int qi = i >> 2, kw = bx * 4 + (i & 3);
         Wd[qi][i & 3] = kw < (S >> 5) ? dmask[((uint64_t)bh * S + c0 + qi) * (uint64_t)(S >> 5) + kw] : 0u;
       }
     __syncthreads();
@@ -806,20 +811,20 @@ __global__ void __launch_bounds__(256, 2)
   store_rows(out + 2 * H, dv0, dv1, hf, 1.f);
 }
 
-// dQ for 32 queries per wave (lane = query) over 64-key chunks of K / V (biased); writes D.
-__global__ void __launch_bounds__(256, 2)
-    attn_bwd_dq_x6p_kernel(const float* __restrict__ qkv, const int64_t* __restrict__ mask,
-                           const float* __restrict__ bqkv, const float* __restrict__ ctx,
-                           const float* __restrict__ dctx, const float* __restrict__ lse, float* __restrict__ Dout,
+// dQ for 32 queries per wave (lane = query) over 64-key chunks of K / V (biased); bx = the
+// block's 128-query group; D = rowsum(dO o O) read from attn_bwd_dsum_kernel's output.
+HS_DEVICE void dq_x6p_body(char* __restrict__ smem, int bx, const float* __restrict__ qkv,
+                           const int64_t* __restrict__ mask, const float* __restrict__ bqkv,
+                           const float* __restrict__ dctx, const float* __restrict__ lse, const float* __restrict__ Dd,
                            float* __restrict__ dqkv, int S, int NH, float p, const uint32_t* __restrict__ dmask) {
-  __shared__ __attribute__((aligned(16))) char Kp[kPImg];
-  __shared__ __attribute__((aligned(16))) char Vp[kPImg];
-  __shared__ float Ms[64];
+  char* const Kp = smem;
+  char* const Vp = smem + kPImg;
+  float* const Ms = reinterpret_cast<float*>(smem + 2 * kPImg);
   const int H = NH * kXD;
   const int64_t ld = 3 * (int64_t)H;
   const int bh = blockIdx.y, b = bh / NH, h = bh % NH;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hf = lane >> 5, li = lane & 31;
-  const int q0 = blockIdx.x * 128 + w * 32;
+  const int q0 = bx * 128 + w * 32;
   const bool active = q0 < S;
   const float* rows = qkv + (int64_t)b * S * ld;
   const float dscale = drop_scale16(drop_thr16(p));
@@ -835,17 +840,12 @@ __global__ void __launch_bounds__(256, 2)
       const int d = 16 * s + 8 * hf;
       ld8(rows + (int64_t)(q0 + li) * ld + h * kXD + d, bofs(bqkv, h * kXD + d), 0.125f, qr);
       ld8(dctx + tok * H + h * kXD + d, nullptr, 1.f, dor);
-      float o[8];
-      ld8(ctx + tok * H + h * kXD + d, nullptr, 1.f, o);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) dsum = fmaf(dor[j], o[j], dsum);
     }
     split8(qr, qb[s][0], qb[s][1], qb[s][2]);
     split8(dor, ob[s][0], ob[s][1], ob[s][2]);
   }
   if (active) {
-    dsum += __shfl_xor(dsum, 32, 64);
-    if (hf == 0) Dout[(int64_t)bh * S + q0 + li] = dsum;
+    dsum = Dd[(int64_t)bh * S + q0 + li];
     lq = lse[(int64_t)bh * S + q0 + li];
   }
   f32x16 dq0 = {}, dq1 = {};
@@ -899,6 +899,47 @@ __global__ void __launch_bounds__(256, 2)
   store_rows(dqkv + ((int64_t)b * S + q0 + li) * ld + h * kXD, dq0, dq1, hf, 0.125f);
 }
 
+// D[bh][q] = rowsum(dO o O) over the head's 64 dims: 16 lanes per (token, head), float4 each.
+__global__ void __launch_bounds__(256) attn_bwd_dsum_kernel(const float* __restrict__ ctx,
+                                                            const float* __restrict__ dctx, float* __restrict__ Dout,
+                                                            int B, int S, int NH) {
+  const int64_t u = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);  // (token, head) unit
+  const int l = threadIdx.x & 15;
+  const int64_t units = (int64_t)B * S * NH;
+  const int64_t tok = u / NH;
+  const int h = (int)(u % NH);
+  float v = 0.f;
+  if (u < units) {
+    const int64_t o = tok * NH * kXD + h * kXD + 4 * l;
+    const float4 a = *reinterpret_cast<const float4*>(dctx + o), c = *reinterpret_cast<const float4*>(ctx + o);
+    v = a.x * c.x + a.y * c.y + a.z * c.z + a.w * c.w;
+  }
+#pragma unroll
+  for (int m = 8; m >= 1; m >>= 1) v += __shfl_xor(v, m, 16);
+  if (u < units && l == 0) {
+    const int64_t b = tok / S, q = tok % S;
+    Dout[(b * NH + h) * S + q] = v;
+  }
+}
+
+// The backward pair as ONE launch: blocks x < nq run the dQ role, the rest the dK / dV role (both
+// only read D, computed beforehand).  Sequential dQ and dKV launches each ran (S/128) * B*NH blocks
+// on 512 two-per-CU slots -- 0.75 of a round at S = 512, B = 8, NH = 12, half the CUs holding one
+// block -- and waited for each other; one launch of both roles fills the slots the first round
+// leaves and backfills the second.
+__global__ void __launch_bounds__(256, 2)
+    attn_bwd_x6p_kernel(const float* __restrict__ qkv, const int64_t* __restrict__ mask,
+                        const float* __restrict__ bqkv, const float* __restrict__ dctx,
+                        const float* __restrict__ lse, const float* __restrict__ Dd, float* __restrict__ dqkv, int S,
+                        int NH, float p, const uint32_t* __restrict__ dmask) {
+  __shared__ __attribute__((aligned(16))) char smem[kBwdSmem];
+  const int nq = (S + 127) / 128;
+  if ((int)blockIdx.x < nq)
+    dq_x6p_body(smem, blockIdx.x, qkv, mask, bqkv, dctx, lse, Dd, dqkv, S, NH, p, dmask);
+  else
+    dkv_x6p_body(smem, blockIdx.x - nq, qkv, mask, bqkv, dctx, lse, Dd, dqkv, S, NH, p, dmask);
+}
+
 }  // namespace hs
 
 using namespace hs;
@@ -917,12 +958,13 @@ int launch_attn_bwd_x6(const float* qkv, const int64_t* mask, const float* bqkv,
                        const float* lse, float* Dbuf, float* dqkv, const uint32_t* dmask, int B, int S, int NH,
                        int D, float p, bool fused, hipStream_t st) {
   if (D != kXD || S % 32 != 0 || S <= 0 || (p > 0.f && dmask == nullptr)) return -1;
-  if (g_bwd_planes) {  // plane-image kernels (default)
-    dim3 grid((S + 127) / 128, B * NH);
-    hipLaunchKernelGGL(attn_bwd_dq_x6p_kernel, grid, dim3(256), 0, st, qkv, mask, bqkv, ctx, dctx, lse, Dbuf, dqkv, S,
-                       NH, p, dmask);
-    hipLaunchKernelGGL(attn_bwd_dkv_x6p_kernel, grid, dim3(256), 0, st, qkv, mask, bqkv, dctx, lse, Dbuf, dqkv, S, NH,
-                       p, dmask);
+  if (g_bwd_planes) {  // plane-image kernels (default): D, then both roles in one launch
+    const int64_t units = (int64_t)B * S * NH;
+    hipLaunchKernelGGL(attn_bwd_dsum_kernel, dim3((unsigned)((units + 15) / 16)), dim3(256), 0, st, ctx, dctx, Dbuf, B,
+                       S, NH);
+    dim3 grid(2 * ((S + 127) / 128), B * NH);
+    hipLaunchKernelGGL(attn_bwd_x6p_kernel, grid, dim3(256), 0, st, qkv, mask, bqkv, dctx, lse, Dbuf, dqkv, S, NH, p,
+                       dmask);
     return 0;
   }
   if (fused && S <= 128) {
