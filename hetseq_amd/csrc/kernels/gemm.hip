@@ -673,10 +673,17 @@ __global__ void __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(NB
 }
 
 static int g_ablation = 0;  // microbenchmark hook (tile_override bits 3-4)
-// split-bf16 kernel waves per block: 8 for the weight gradient (both operands mn-contiguous:
-// twice the waves hide its transposing staging; measured +8-12%), 4 elsewhere (the 8-wave
-// dgrad needs 160 VGPRs = one block per CU, -25%).  tile_override bit 5 forces 4, bit 6 forces 8.
+// split-bf16 kernel waves per block: 4 (the weight gradient's 8-wave variant hid the register
+// transpose of its mn-contiguous staging, +8-12 % before the transposed-read layout; now it loses
+// in the step, see g_x6_wgrad_waves).  tile_override bit 5 forces 4, bit 6 forces 8.
 static int g_x6_waves = 4;
+// waves per block of the weight-gradient (TA) launches: HETSEQ_X6_WGRAD_WAVES=4 / 8.  4 since the
+// transposed-read layout: beside the data-gradient chain (side stream, 2 K slices) the BERT-base fp32
+// step runs 15.20-15.28 ms vs 15.52-15.56 with 8 (interleaved, profiles/r2_gemm_experiments.md)
+static const int g_x6_wgrad_waves = [] {
+  const char* e = std::getenv("HETSEQ_X6_WGRAD_WAVES");
+  return e && e[0] == '8' ? 8 : 4;
+}();
 // 4-wave register prefetch depth (PF above): HETSEQ_X6_PF=1/2, tile_override bit 7 forces 2
 static const int g_x6_pf_env = [] {
   const char* e = std::getenv("HETSEQ_X6_PF");
@@ -873,7 +880,7 @@ int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, i
   const bool mfma16 = !nt && tile_override >= 0 && (tile_override & 4);  // benchmarking hook: 16x16x4 MFMA
   g_ablation = tile_override >= 0 ? (tile_override >> 3) & 3 : 0;
   g_x6_waves = tile_override >= 0 && (tile_override & 32) ? 4 : tile_override >= 0 && (tile_override & 64) ? 8
-                                                              : ta ? 8 : 4;
+                                                              : ta ? g_x6_wgrad_waves : 4;
   g_x6_pf = tile_override >= 0 && (tile_override & 128) ? 2 : g_x6_pf_env;
   g_x6_tr = tile_override >= 0 && (tile_override & 256) ? 1 : tile_override >= 0 && (tile_override & 512) ? 0
                                                               : g_x6_tr_env;
