@@ -21,6 +21,8 @@ parameters are produced in fp32 (master precision) in both --dtype modes.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from hetseq_amd.ops import gemm as G
@@ -421,8 +423,9 @@ class FusedBertLayer(torch.autograd.Function):
         def wgrad(dy, xin_, out):
             if not side:
                 return G.linear_wgrad(dy, xin_, out=out, accumulate=acc)
+            ks = streams.side_ksplit(dy.shape[1], xin_.shape[1])
             return streams.run(dy.device, lambda: G.linear_wgrad(dy, xin_, out=out, accumulate=acc,
-                                                                 ksplit=streams.SIDE_KSPLIT), dy, xin_)
+                                                                 ksplit=ks), dy, xin_)
 
         do_p = sp(do_)
         dW2 = wgrad(do_p, f1, Gv.w2 if acc else None)

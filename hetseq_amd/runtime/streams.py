@@ -43,6 +43,17 @@ _ENABLED = os.environ.get("HETSEQ_WGRAD_STREAM", "1") == "1"
 # "auto" = use the isolated measurement.
 _ks = os.environ.get("HETSEQ_SIDE_KSPLIT", "2")
 SIDE_KSPLIT = None if _ks == "auto" else int(_ks)
+# ... except the small ones (output <= 768 x 768, the attention-output projection: 36 tiles, 72
+# blocks at 2 slices), which take 4: 15.431 / 15.442 / 15.451 ms/step vs 15.491 / 15.540 / 15.511
+# with 2 and 15.46-15.50 with 8 (interleaved, profiles/r2_gemm_experiments.md)
+SIDE_KSPLIT_SMALL = int(os.environ.get("HETSEQ_SIDE_KSPLIT_SMALL", "4"))
+
+
+def side_ksplit(M, N):
+    """K split of an M x N weight-gradient GEMM on the side stream (None: the isolated measurement)."""
+    if SIDE_KSPLIT is None:
+        return None
+    return SIDE_KSPLIT_SMALL if M * N <= 768 * 768 else SIDE_KSPLIT
 # split-K of the compute-stream data-gradient GEMMs while the side stream runs the weight
 # gradients beside them: the two streams fill the chip together, so the K split the isolated
 # measurement picks (4 slices for the N = 768 products) only adds slab traffic and a reduction
