@@ -21,8 +21,6 @@ parameters are produced in fp32 (master precision) in both --dtype modes.
 """
 from __future__ import annotations
 
-import os
-
 import torch
 
 from hetseq_amd.ops import gemm as G
