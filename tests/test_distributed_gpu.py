@@ -48,3 +48,47 @@ def test_two_ranks_fused_bert_on_one_gpu(tmp_path):
     for p, o in zip(procs, outs):
         assert p.returncode == 0, o[-3000:]
     assert "(epoch 1 @ 6 updates)" in outs[0]
+
+
+def test_bert_resume_mid_epoch_matches_uninterrupted(tmp_path):
+    """train.py on the fused GPU path: 3 updates, stop, resume from checkpoint_last.pt to 6 updates
+    == 6 updates in one run (same parameters, optimizer state and iterator position; deterministic
+    kernels, per-update dropout seeds)."""
+    import subprocess
+
+    import torch
+
+    from hetseq_amd.data.synthetic import write_bert_config, write_bert_shards, write_vocab
+
+    d = tmp_path / "bert"
+    write_bert_shards(str(d), num_shards=2, per_shard=64, seq_len=64, max_pred=8, vocab_size=1000, split="train")
+    write_bert_shards(str(d), num_shards=1, per_shard=8, seq_len=64, max_pred=8, vocab_size=1000, split="test")
+    write_vocab(str(tmp_path / "vocab.txt"), 1000)
+    cfg = write_bert_config(str(tmp_path / "cfg.json"), vocab_size=1000, hidden_size=256, num_hidden_layers=2,
+                            num_attention_heads=4, intermediate_size=1024)
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    env["HETSEQ_GEMM"] = "hip"  # no timing-based engine choice between the runs
+
+    def run(save_dir, max_update):
+        cmd = [sys.executable, os.path.join(ROOT, "train.py"), "--task", "bert", "--data", str(d), "--dict",
+               str(tmp_path / "vocab.txt"), "--config_file", cfg, "--max-sentences", "8", "--max-update",
+               str(max_update), "--save-dir", str(save_dir), "--distributed-world-size", "1", "--fast-stat-sync",
+               "--valid-subset", "test",
+               "--lr", "1e-3", "--warmup-updates", "2", "--log-format", "simple", "--log-interval", "1"]
+        p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env, timeout=300)
+        assert p.returncode == 0, p.stdout[-3000:]
+        return p.stdout
+
+    run(tmp_path / "a", 6)
+    run(tmp_path / "b", 3)
+    out = run(tmp_path / "b", 6)
+    assert "loaded checkpoint" in out, out[-2000:]
+    sa = torch.load(str(tmp_path / "a" / "checkpoint_last.pt"), map_location="cpu", weights_only=False)
+    sb = torch.load(str(tmp_path / "b" / "checkpoint_last.pt"), map_location="cpu", weights_only=False)
+    assert sa["optimizer_history"][-1]["num_updates"] == sb["optimizer_history"][-1]["num_updates"] == 6
+    for k, v in sa["model"].items():
+        assert torch.equal(v, sb["model"][k]), k
+    ea, eb = sa["last_optimizer_state"]["state"], sb["last_optimizer_state"]["state"]
+    for i in ea:
+        assert torch.equal(ea[i]["exp_avg"], eb[i]["exp_avg"]) and torch.equal(ea[i]["exp_avg_sq"], eb[i]["exp_avg_sq"])
