@@ -282,9 +282,9 @@ __global__ void __launch_bounds__(256, 2)
   __shared__ float Ms[kXCH];
   const int H = NH * kXD;
   const int64_t ld = 3 * (int64_t)H;
-  const int bh = blockIdx.y, b = bh / NH, h = bh % NH;
+  const int bh = blockIdx.x, b = bh / NH, h = bh % NH;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hf = lane >> 5, li = lane & 31;
-  const int q0 = blockIdx.x * 128 + w * 32;
+  const int q0 = blockIdx.y * 128 + w * 32;
   const bool active = q0 < S;
   const float* rows = qkv + (int64_t)b * S * ld;
   const uint32_t thr = drop_thr16(p);
@@ -700,7 +700,7 @@ constexpr int kBwdSmem = 2 * kPImg + 64 * 4 * 2 + 64 * 4 * 4;
 
 // dK / dV for 32 keys per wave (lane = key) over 64-query chunks of Q (biased, * 1/8) and dO;
 // bx = the block's 128-key group.
-HS_DEVICE void dkv_x6p_body(char* __restrict__ smem, int bx, const float* __restrict__ qkv,
+HS_DEVICE void dkv_x6p_body(char* __restrict__ smem, int bx, int bh, const float* __restrict__ qkv,
                             const int64_t* __restrict__ mask, const float* __restrict__ bqkv,
                             const float* __restrict__ dctx, const float* __restrict__ lse,
                             const float* __restrict__ Dd, float* __restrict__ dqkv, int S, int NH, float p,
@@ -712,7 +712,7 @@ HS_DEVICE void dkv_x6p_body(char* __restrict__ smem, int bx, const float* __rest
   uint32_t(*const Wd)[4] = reinterpret_cast<uint32_t(*)[4]>(Ds + 64);
   const int H = NH * kXD;
   const int64_t ld = 3 * (int64_t)H;
-  const int bh = blockIdx.y, b = bh / NH, h = bh % NH;
+  const int b = bh / NH, h = bh % NH;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hf = lane >> 5, li = lane & 31;
   const int k0 = bx * 128 + w * 32;
   const bool active = k0 < S;
@@ -813,7 +813,7 @@ HS_DEVICE void dkv_x6p_body(char* __restrict__ smem, int bx, const float* __rest
 
 // dQ for 32 queries per wave (lane = query) over 64-key chunks of K / V (biased); bx = the
 // block's 128-query group; D = rowsum(dO o O) read from attn_bwd_dsum_kernel's output.
-HS_DEVICE void dq_x6p_body(char* __restrict__ smem, int bx, const float* __restrict__ qkv,
+HS_DEVICE void dq_x6p_body(char* __restrict__ smem, int bx, int bh, const float* __restrict__ qkv,
                            const int64_t* __restrict__ mask, const float* __restrict__ bqkv,
                            const float* __restrict__ dctx, const float* __restrict__ lse, const float* __restrict__ Dd,
                            float* __restrict__ dqkv, int S, int NH, float p, const uint32_t* __restrict__ dmask) {
@@ -822,7 +822,7 @@ HS_DEVICE void dq_x6p_body(char* __restrict__ smem, int bx, const float* __restr
   float* const Ms = reinterpret_cast<float*>(smem + 2 * kPImg);
   const int H = NH * kXD;
   const int64_t ld = 3 * (int64_t)H;
-  const int bh = blockIdx.y, b = bh / NH, h = bh % NH;
+  const int b = bh / NH, h = bh % NH;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hf = lane >> 5, li = lane & 31;
   const int q0 = bx * 128 + w * 32;
   const bool active = q0 < S;
@@ -931,13 +931,16 @@ __global__ void __launch_bounds__(256, 2)
     attn_bwd_x6p_kernel(const float* __restrict__ qkv, const int64_t* __restrict__ mask,
                         const float* __restrict__ bqkv, const float* __restrict__ dctx,
                         const float* __restrict__ lse, const float* __restrict__ Dd, float* __restrict__ dqkv, int S,
-                        int NH, float p, const uint32_t* __restrict__ dmask) {
+                        int NH, float p, const uint32_t* __restrict__ dmask, int dkv_first) {
   __shared__ __attribute__((aligned(16))) char smem[kBwdSmem];
-  const int nq = (S + 127) / 128;
-  if ((int)blockIdx.x < nq)
-    dq_x6p_body(smem, blockIdx.x, qkv, mask, bqkv, dctx, lse, Dd, dqkv, S, NH, p, dmask);
+  // grid (B*NH, 2 * nq): blocks dispatch x-fastest, so every head's dK / dV blocks (the longer
+  // role) go out before the dQ ones and the shorter blocks fill the tail of the last round
+  const int nq = (S + 127) / 128, bh = blockIdx.x;
+  const int y = blockIdx.y, first = y < nq, g = first ? y : y - nq;  // role group, block in the role
+  if (first == (dkv_first != 0))
+    dkv_x6p_body(smem, g, bh, qkv, mask, bqkv, dctx, lse, Dd, dqkv, S, NH, p, dmask);
   else
-    dkv_x6p_body(smem, blockIdx.x - nq, qkv, mask, bqkv, dctx, lse, Dd, dqkv, S, NH, p, dmask);
+    dq_x6p_body(smem, g, bh, qkv, mask, bqkv, dctx, lse, Dd, dqkv, S, NH, p, dmask);
 }
 
 }  // namespace hs
@@ -951,6 +954,12 @@ static int g_bwd_planes_env = [] {
   return e && e[0] == 'g' ? 0 : 1;
 }();
 static int g_bwd_planes = g_bwd_planes_env;
+// dispatch order of the merged backward's roles: dK / dV blocks first (default) or dQ first
+// (HETSEQ_ATTN_BWD_DKV_FIRST=0)
+static const int g_bwd_dkv_first = [] {
+  const char* e = std::getenv("HETSEQ_ATTN_BWD_DKV_FIRST");
+  return e && e[0] == '0' ? 0 : 1;
+}();
 void set_attn_bwd_x6_planes(int on) { g_bwd_planes = on < 0 ? g_bwd_planes_env : on; }
 
 // fused S <= 128 (grid B*NH x 512) or the dQ / dKV pair (grid (S/128, B*NH) x 256 each)
@@ -962,9 +971,9 @@ int launch_attn_bwd_x6(const float* qkv, const int64_t* mask, const float* bqkv,
     const int64_t units = (int64_t)B * S * NH;
     hipLaunchKernelGGL(attn_bwd_dsum_kernel, dim3((unsigned)((units + 15) / 16)), dim3(256), 0, st, ctx, dctx, Dbuf, B,
                        S, NH);
-    dim3 grid(2 * ((S + 127) / 128), B * NH);
+    dim3 grid(B * NH, 2 * ((S + 127) / 128));
     hipLaunchKernelGGL(attn_bwd_x6p_kernel, grid, dim3(256), 0, st, qkv, mask, bqkv, dctx, lse, Dbuf, dqkv, S, NH, p,
-                       dmask);
+                       dmask, g_bwd_dkv_first);
     return 0;
   }
   if (fused && S <= 128) {
@@ -984,7 +993,9 @@ int launch_attn_fwd_x6(const float* qkv, const int64_t* mask, const float* bqkv,
                        uint32_t* dmask, int B, int S, int NH, int D, float p, uint64_t seed, uint64_t off,
                        hipStream_t st) {
   if (D != kXD || S % 32 != 0 || S <= 0) return -1;
-  dim3 grid((S + 127) / 128, B * NH);
+  // grid (B*NH, S/128): consecutive blocks are different heads, so (B*NH a multiple of 8) every
+  // query block of a head lands on the same XCD and its K / V come through one L2
+  dim3 grid(B * NH, (S + 127) / 128);
   hipLaunchKernelGGL(attn_fwd_x6_kernel, grid, dim3(256), 0, st, qkv, mask, bqkv, ctx, lse, dmask, S, NH, p, seed, off,
                      g_seed_dev);
   return 0;
