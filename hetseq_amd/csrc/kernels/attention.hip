@@ -127,9 +127,9 @@ __global__ void __launch_bounds__(256, 2)
   __shared__ float Ms[kCH];
   const int H = NH * kD;
   const int64_t ld = 3 * (int64_t)H;
-  const int bh = blockIdx.y, b = bh / NH, h = bh % NH;
+  const int bh = blockIdx.x, b = bh / NH, h = bh % NH;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hf = lane >> 5, li = lane & 31;
-  const int q0 = blockIdx.x * 128 + w * 32;
+  const int q0 = blockIdx.y * 128 + w * 32;
   const bool active = q0 < S;
   const T* rows = qkv + (int64_t)b * S * ld;
   const uint32_t thr = drop_thr16(p);
@@ -226,9 +226,9 @@ __global__ void __launch_bounds__(256, 2)
   __shared__ float Ms[kCH];
   const int H = NH * kD;
   const int64_t ld = 3 * (int64_t)H;
-  const int bh = blockIdx.y, b = bh / NH, h = bh % NH;
+  const int bh = blockIdx.x, b = bh / NH, h = bh % NH;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hf = lane >> 5, li = lane & 31;
-  const int q0 = blockIdx.x * 128 + w * 32;
+  const int q0 = blockIdx.y * 128 + w * 32;
   const bool active = q0 < S;
   const T* rows = qkv + (int64_t)b * S * ld;
   const float dscale = drop_scale16(drop_thr16(p));
@@ -324,9 +324,9 @@ __global__ void __launch_bounds__(256, 2)
   __shared__ uint32_t Wd[kCH][4];  // keep-bit words of the chunk's queries for this block's 4 key words
   const int H = NH * kD;
   const int64_t ld = 3 * (int64_t)H;
-  const int bh = blockIdx.y, b = bh / NH, h = bh % NH;
+  const int bh = blockIdx.x, b = bh / NH, h = bh % NH;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hf = lane >> 5, li = lane & 31;
-  const int k0 = blockIdx.x * 128 + w * 32;
+  const int k0 = blockIdx.y * 128 + w * 32;
   const bool active = k0 < S;
   const int key = k0 + li;
   const T* rows = qkv + (int64_t)b * S * ld;
@@ -353,7 +353,7 @@ __global__ void __launch_bounds__(256, 2)
     }
     if (p > 0.f)
       for (int i = threadIdx.x; i < clen * 4; i += blockDim.x) {
-        const int qi = i >> 2, kw = blockIdx.x * 4 + (i & 3);
+        const int qi = i >> 2, kw = blockIdx.y * 4 + (i & 3);
         Wd[qi][i & 3] = kw < (S >> 5) ? dmask[((uint64_t)bh * S + c0 + qi) * (uint64_t)(S >> 5) + kw] : 0u;
       }
     __syncthreads();
@@ -659,7 +659,7 @@ int launch_attn_fwd(int dtype, const void* qkv, const int64_t* mask, const float
                     uint32_t* dmask, int B, int S, int NH, int D, float p, uint64_t seed, uint64_t off,
                     hipStream_t st) {
   if (D != kD || S % 32 != 0 || S <= 0) return -1;
-  dim3 grid((S + 127) / 128, B * NH);
+  dim3 grid(B * NH, (S + 127) / 128);  // head-major: a head's blocks share one XCD's L2
   if (dtype != 0 && bf16_mfma_enabled())  // bf16 matrix cores (attention_bf16.hip)
     return launch_attn_fwd_bf16(qkv, mask, bqkv, ctx, lse, dmask, B, S, NH, D, p, seed, off, st);
   if (dtype == 0 && g_attn_fp32_x6)  // fp32 as split-bf16 products (attention_x6.hip)
@@ -691,7 +691,7 @@ int launch_attn_bwd(int dtype, const void* qkv, const int64_t* mask, const float
                          bqkv, (const bf16_t*)ctx, (const bf16_t*)dctx, lse, (bf16_t*)dqkv, S, NH, p, dmask);
     return 0;
   }
-  dim3 grid((S + 127) / 128, B * NH);
+  dim3 grid(B * NH, (S + 127) / 128);  // head-major: a head's blocks share one XCD's L2
   if (dtype == 0) {
     hipLaunchKernelGGL(attn_bwd_dq_kernel<float>, grid, dim3(256), 0, st, (const float*)qkv, mask, bqkv,
                        (const float*)ctx, (const float*)dctx, lse, Dbuf, (float*)dqkv, S, NH, p, dmask);

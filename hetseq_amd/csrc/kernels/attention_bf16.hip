@@ -71,9 +71,9 @@ __global__ void __launch_bounds__(256, 2)
   __shared__ float Ms[kBCH];
   const int H = NH * kBD;
   const int64_t ld = 3 * (int64_t)H;
-  const int bh = blockIdx.y, b = bh / NH, h = bh % NH;
+  const int bh = blockIdx.x, b = bh / NH, h = bh % NH;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hf = lane >> 5, li = lane & 31;
-  const int q0 = blockIdx.x * 128 + w * 32;
+  const int q0 = blockIdx.y * 128 + w * 32;
   const bool active = q0 < S;
   const bf16_t* rows = qkv + (int64_t)b * S * ld;
   const uint32_t thr = drop_thr16(p);
@@ -418,7 +418,7 @@ int launch_attn_fwd_bf16(const void* qkv, const int64_t* mask, const float* bqkv
                          uint32_t* dmask, int B, int S, int NH, int D, float p, uint64_t seed, uint64_t off,
                          hipStream_t st) {
   if (D != kBD || S % 32 != 0 || S <= 0) return -1;
-  dim3 grid((S + 127) / 128, B * NH);
+  dim3 grid(B * NH, (S + 127) / 128);  // head-major: a head's blocks share one XCD's L2
   hipLaunchKernelGGL(attn_fwd_bf16_kernel, grid, dim3(256), 0, st, (const bf16_t*)qkv, mask, bqkv, (bf16_t*)ctx, lse,
                      dmask, S, NH, p, seed, off, g_seed_dev);
   return 0;

@@ -556,9 +556,9 @@ __global__ void __launch_bounds__(256, 2)
   __shared__ float Ms[128];
   const int H = NH * kXD;
   const int64_t ld = 3 * (int64_t)H;
-  const int bh = blockIdx.y, b = bh / NH, h = bh % NH;
+  const int bh = blockIdx.x, b = bh / NH, h = bh % NH;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hf = lane >> 5, li = lane & 31;
-  const int q0 = blockIdx.x * 128 + w * 32;
+  const int q0 = blockIdx.y * 128 + w * 32;
   const bool active = q0 < S;
   const float* rows = qkv + (int64_t)b * S * ld;
   const float dscale = drop_scale16(drop_thr16(p));
@@ -645,9 +645,9 @@ __global__ void __launch_bounds__(256, 2)
   __shared__ uint32_t Wd[128][4];  // keep words of the chunk's queries for this block's 4 key words
   const int H = NH * kXD;
   const int64_t ld = 3 * (int64_t)H;
-  const int bh = blockIdx.y, b = bh / NH, h = bh % NH;
+  const int bh = blockIdx.x, b = bh / NH, h = bh % NH;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hf = lane >> 5, li = lane & 31;
-  const int k0 = blockIdx.x * 128 + w * 32;
+  const int k0 = blockIdx.y * 128 + w * 32;
   const bool active = k0 < S;
   const int key = k0 + li;
   const float* rows = qkv + (int64_t)b * S * ld;
@@ -673,7 +673,7 @@ __global__ void __launch_bounds__(256, 2)
     }
     if (p > 0.f)
       for (int i = threadIdx.x; i < clen * 4; i += blockDim.x) {
-        const int qi = i >> 2, kw = blockIdx.x * 4 + (i & 3);
+        const int qi = i >> 2, kw = blockIdx.y * 4 + (i & 3);
         Wd[qi][i & 3] = kw < (S >> 5) ? dmask[((uint64_t)bh * S + c0 + qi) * (uint64_t)(S >> 5) + kw] : 0u;
       }
     __syncthreads();
@@ -981,7 +981,7 @@ int launch_attn_bwd_x6(const float* qkv, const int64_t* mask, const float* bqkv,
                        S, NH, p, dmask);
     return 0;
   }
-  dim3 grid((S + 127) / 128, B * NH);
+  dim3 grid(B * NH, (S + 127) / 128);  // head-major: a head's blocks share one XCD's L2
   hipLaunchKernelGGL(attn_bwd_dq_x6_kernel, grid, dim3(256), 0, st, qkv, mask, bqkv, ctx, dctx, lse, Dbuf, dqkv, S, NH,
                      p, dmask);
   hipLaunchKernelGGL(attn_bwd_dkv_x6_kernel, grid, dim3(256), 0, st, qkv, mask, bqkv, dctx, lse, Dbuf, dqkv, S, NH, p,
