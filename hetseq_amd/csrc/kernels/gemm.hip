@@ -80,6 +80,7 @@ struct GemmArgs {
   // valid extents (EDGE launches only, else = M, N, K): the padded problem is M x N x K; operand
   // rows past them read as zeros, C rows past Mv are not written, bias past Nv reads as zero
   int Mv, Nv, Kv;
+  int slice_major;  // split-K block order: 1 = all tiles of slice 0, then slice 1, ... (else tile-major)
 };
 
 // LDS image geometry of one operand (rows = BM or BN).  The [k][mn] image is
@@ -476,7 +477,10 @@ __global__ void __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(NB
   const int orig = blockIdx.x;
   const int xcd = orig % 8, qq = nwg / 8, rr = nwg % 8;
   const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + orig / 8;
-  const int slice = wg % p.ksplit, tile = wg / p.ksplit;
+  const int ntile = tiles_m * tiles_n;
+  // slice-major: an XCD's contiguous range of blocks is (mostly) one K slice over a group of tiles,
+  // so its L2 holds that slice's panels once instead of every slice of a few tiles
+  const int slice = p.slice_major ? wg / ntile : wg % p.ksplit, tile = p.slice_major ? wg % ntile : wg / p.ksplit;
   // grouped order: 8 M-tiles x all N-tiles per group, N fastest inside it, so the 64 blocks an
   // XCD runs at a time cover an ~8x8 tile square (A and B panels each re-read 8x from its L2)
   const int gsz = 8 * tiles_n, grp = tile / gsz, gm = min(8, tiles_m - 8 * grp);
@@ -677,6 +681,12 @@ static int g_ablation = 0;  // microbenchmark hook (tile_override bits 3-4)
 // transpose of its mn-contiguous staging, +8-12 % before the transposed-read layout; now it loses
 // in the step, see g_x6_wgrad_waves).  tile_override bit 5 forces 4, bit 6 forces 8.
 static int g_x6_waves = 4;
+// split-K block order of the split-bf16 kernel: slice-major (default; BERT-base fp32 step 15.04 vs
+// 15.13 ms tile-major, interleaved) or HETSEQ_X6_SLICE_MAJOR=0 tile-major
+static const int g_slice_major = [] {
+  const char* e = std::getenv("HETSEQ_X6_SLICE_MAJOR");
+  return e && e[0] == '0' ? 0 : 1;
+}();
 // waves per block of the weight-gradient (TA) launches: HETSEQ_X6_WGRAD_WAVES=4 / 8.  4 since the
 // transposed-read layout: beside the data-gradient chain (side stream, 2 K slices) the BERT-base fp32
 // step runs 15.20-15.28 ms vs 15.52-15.56 with 8 (interleaved, profiles/r2_gemm_experiments.md)
@@ -899,7 +909,7 @@ int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, i
   kv = kv > 0 ? kv : K;
   if ((mv != M || nv != N || kv != K) && (!nt || epi > kEpiBias || mv > M || nv > N || kv > K)) return -1;
   GemmArgs a{static_cast<const float*>(A), static_cast<const float*>(B), static_cast<float*>(C), bias, aux, part,
-             lda, ldb, ldc, ldaux, M, N, K, beta, ks, slab, mv, nv, kv};
+             lda, ldb, ldc, ldaux, M, N, K, beta, ks, slab, mv, nv, kv, g_slice_major};
   int rc;
   if (nt == 6)
     rc = launch_split<6>(tile, ta, tb, epi, a, st);

@@ -64,6 +64,7 @@ struct PlanesArgs {
   int64_t lda, ldb, ldc, ldaux, a_ps, b_ps;
   int M, N, K, ksplit;
   float beta;
+  int slice_major;  // split-K block order (see gemm.hip): 1 = slice-major
 };
 
 // LDS image geometry of one operand plane (128 x BK bf16 elements either way).
@@ -170,7 +171,8 @@ __global__ void __launch_bounds__(64 * WV, (planes_waves_per_simd<P, BK, STAGES,
   const int orig = blockIdx.x;
   const int xcd = orig % 8, qq = nwg / 8, rr = nwg % 8;
   const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + orig / 8;
-  const int slice = wg % p.ksplit, tile = wg / p.ksplit;
+  const int ntile = tiles_m * tiles_n;
+  const int slice = p.slice_major ? wg / ntile : wg % p.ksplit, tile = p.slice_major ? wg % ntile : wg / p.ksplit;
   const int gsz = 8 * tiles_n, grp = tile / gsz, gm = min(8, tiles_m - 8 * grp);
   const int tm = 8 * grp + (tile % gsz) % gm, tn = (tile % gsz) / gm;
   const int m0 = tm * kPB, n0 = tn * kPB;
@@ -528,6 +530,12 @@ void set_planes_variant(int v) { g_planes_variant = v; }
 
 // planes: 1 (bf16) or 3 (split fp32); c_dtype: 0 fp32 C, 1 bf16 C.  Operand strides / plane
 // strides in elements.  Returns -1 (nothing launched) for shapes it does not serve: M, N
+// split-K block order (HETSEQ_PLANES_SLICE_MAJOR=1 slice-major, default tile-major)
+static const int g_planes_slice_major = [] {
+  const char* e = std::getenv("HETSEQ_PLANES_SLICE_MAJOR");
+  return e && e[0] == '1' ? 1 : 0;
+}();
+
 // multiples of 128, K a multiple of BK * ksplit, 16-B aligned rows.
 int launch_gemm_planes(int planes, int c_dtype, int ta, int tb, int M, int N, int K, const void* A, int64_t lda,
                        int64_t a_ps, const void* B, int64_t ldb, int64_t b_ps, void* C, int64_t ldc,
@@ -557,7 +565,7 @@ int launch_gemm_planes(int planes, int c_dtype, int ta, int tb, int M, int N, in
   const int64_t spanB = 2 * ((planes - 1) * b_ps + (int64_t)(tb ? N : K) * ldb);
   if (spanA >= (1ll << 32) || spanB >= (1ll << 32)) return -1;
   PlanesArgs a{static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), C, bias, aux, part, slab,
-               lda, ldb, ldc, ldaux, a_ps, b_ps, M, N, K, ksplit, beta};
+               lda, ldb, ldc, ldaux, a_ps, b_ps, M, N, K, ksplit, beta, g_planes_slice_major};
   int rc;
 #define HS_CFG(P_, BK_, S_, W_)                                                        \
   (c_dtype ? launch_planes_cfg<P_, BK_, S_, W_, bf16_t>(ta, tb, epi, a, st) \
