@@ -1,4 +1,3 @@
-#!/usr/bin/env python3
 """Headline benchmark: avg sec/step of BERT-base phase-1 pre-training.
 
 Config (BASELINE.json): BERT-base (110,106,428 params, random init),
@@ -6,9 +5,23 @@ seq_len 128, 32 sequences per GPU per step (update-freq 1), synthetic
 NVIDIA-format HDF5 shards read through the native loader, fused Adam,
 --fast-stat-sync (as in every documented reference run), weak scaling.
 
-    python bench.py --gpus N --steps K --warmup W [--dtype fp32|bf16]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype fp32|bf16] [--hetero 2,6]
 
-For N > 1 launch with torch.distributed.run (one rank per GPU, RCCL).
+Launch modes (one process per GPU, RCCL over xGMI):
+
+* ``torchrun --nproc-per-node N bench.py --gpus N`` -- the ranks come from
+  RANK / LOCAL_RANK / WORLD_SIZE; a ``--gpus`` that disagrees with WORLD_SIZE is
+  an error (exit 2), never a silently smaller run.
+* ``python bench.py --gpus N`` (N > 1, no WORLD_SIZE) -- this process becomes a
+  launcher: it starts N fresh rank processes (env:// rendezvous on 127.0.0.1),
+  never touches the GPU itself, relays their output and exits non-zero if any
+  rank fails.
+* ``python bench.py --hetero 2,6`` -- the heterogeneous launch of BASELINE.json
+  config 4: one launch group per entry (here 2 and 6 GPUs of one node), each
+  with its own ``--distributed-gpus`` / first global rank / ``--device-id-offset``,
+  joined by a ``tcp://`` rendezvous, exactly like separate ``train.py`` launches
+  on two nodes (reference train.py:189-236).
+
 Timed region: K full training steps (data -> H2D -> fwd -> bwd -> bucketed
 all-reduce -> stats all-reduce -> clip -> Adam), bracketed by a barrier and
 device synchronisation on both sides; the reported time is the MAX over
@@ -19,6 +32,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import tempfile
 import time
@@ -28,7 +43,10 @@ BASELINE_SEC_PER_STEP = 2.60  # README.md:65, 1 node x 4 GPUs, 32 seq/GPU/step
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="GPUs (= ranks); default WORLD_SIZE under torchrun, else 1")
+    p.add_argument("--hetero", default=None,
+                   help="heterogeneous launch groups, e.g. 2,6: one launch per group (tcp:// rendezvous)")
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
@@ -48,14 +66,111 @@ def parse():
                    help="process-group backend for N > 1 (nccl = RCCL; gloo only to rehearse several ranks on one GPU)")
     p.add_argument("--comm-engine", default="auto", choices=["auto", "native", "c10d"],
                    help="gradient collectives for N > 1: native RCCL engine (auto with nccl) or torch c10d")
+    p.add_argument("--dry-run", type=int, default=None, help=argparse.SUPPRESS)  # launcher test: fail this rank
     p.add_argument("--gemm-choices", default=None,
                    help="JSON of measured GEMM engine choices: loaded if it exists (no measuring in warm-up), "
                         "else written after the run (profiling runs use it to keep tuning out of the trace)")
     return p.parse_args()
 
 
+
+
+def _free_port():
+    s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _groups(b):
+    """Launch groups: [(n_ranks, first_global_rank)]."""
+    if b.hetero:
+        sizes = [int(x) for x in b.hetero.split(",") if x.strip()]
+        if not sizes or min(sizes) < 1:
+            raise SystemExit("bench.py: bad --hetero %r" % b.hetero)
+        out, r = [], 0
+        for n in sizes:
+            out.append((n, r))
+            r += n
+        return out
+    return [(b.gpus, 0)]
+
+
+def launch(b):
+    """Parent of a self-launched multi-rank run: starts one fresh process per rank, relays their
+    output, fails if any rank fails.  This process never initialises the GPU (no torch import)."""
+    groups = _groups(b)
+    world = sum(n for n, _ in groups)
+    port = _free_port()
+    procs = []
+    for gi, (n, first) in enumerate(groups):
+        for i in range(n):
+            env = dict(os.environ)
+            env.update({"RANK": str(first + i), "WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1",
+                        "MASTER_PORT": str(port), "HETSEQ_BENCH_CHILD": "1"})
+            if b.hetero:
+                # one launch group = one "node" of the heterogeneous job: local index i inside it,
+                # devices from the group's offset, tcp:// rendezvous (reference train.py:213-225)
+                env.update({"LOCAL_RANK": str(i), "LOCAL_WORLD_SIZE": str(n), "HETSEQ_GROUP": str(gi),
+                            "HETSEQ_GROUP_GPUS": str(n), "HETSEQ_DEVICE_OFFSET": str(first),
+                            "HETSEQ_INIT_METHOD": "tcp://127.0.0.1:%d" % port})
+            else:
+                env.update({"LOCAL_RANK": str(first + i), "LOCAL_WORLD_SIZE": str(world)})
+            cmd = [sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:]
+            procs.append(subprocess.Popen(cmd, env=env))
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                r = p.poll()
+                if r is None:
+                    continue
+                live.remove(p)
+                if r != 0 and rc == 0:
+                    rc = r
+                    print("bench.py: rank process %d exited with %d; stopping the others" % (procs.index(p), r),
+                          file=sys.stderr, flush=True)
+                    for q in live:
+                        q.terminate()
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc
+
+
 def main():
     b = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if b.hetero and b.gpus is not None and b.gpus != sum(n for n, _ in _groups(b)):
+        print("bench.py: --gpus %d disagrees with --hetero %s" % (b.gpus, b.hetero), file=sys.stderr)
+        return 2
+    if env_world is None:
+        if b.hetero:
+            return launch(b)
+        b.gpus = 1 if b.gpus is None else b.gpus
+        if b.gpus > 1:
+            return launch(b)
+    elif b.gpus is not None and b.gpus != int(env_world) and not b.hetero:
+        print("bench.py: --gpus %d disagrees with WORLD_SIZE=%s (the launcher started a different number of "
+              "ranks); refusing to time a different job" % (b.gpus, env_world), file=sys.stderr)
+        return 2
+    return run_rank(b)
+
+
+def run_rank(b):
+    if b.dry_run is not None:
+        # launcher test hook (tests/test_bench_launch.py): report the rank layout, touch nothing
+        rank = int(os.environ.get("RANK", "0"))
+        info = {k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_PORT", "HETSEQ_GROUP",
+                                               "HETSEQ_GROUP_GPUS", "HETSEQ_DEVICE_OFFSET", "HETSEQ_INIT_METHOD")}
+        sys.stdout.write("DRYRUN " + json.dumps(info) + "\n")  # one write: ranks share the pipe
+        sys.stdout.flush()
+        return 3 if b.dry_run == rank else 0
     if b.gemm:
         os.environ["HETSEQ_GEMM"] = b.gemm
     import torch
@@ -71,17 +186,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if b.dist_backend == "gloo":
-        local_rank = 0  # rehearsal: every rank shares GPU 0
-    torch.cuda.set_device(local_rank)
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if b.dist_backend == "nccl":
-            dist.init_process_group("nccl", init_method="env://", world_size=world, rank=rank,
-                                    device_id=torch.device("cuda", local_rank))
-        else:
-            dist.init_process_group("gloo", init_method="env://", world_size=world, rank=rank)
-        dist.all_reduce(torch.zeros(1, device="cuda"))
+    hetero = os.environ.get("HETSEQ_INIT_METHOD") is not None
     work = tempfile.mkdtemp(prefix="hetseq_bench_r%d_" % rank)
     data_dir = os.path.join(work, "data")
     # every rank writes the SAME shards (same seed) and takes its strided share of the
@@ -100,9 +205,24 @@ def main():
         argv.append("--no-fused")
     if b.hip_graph:
         argv.append("--hip-graph")
+    if world > 1:
+        argv += ["--distributed-backend", b.dist_backend, "--distributed-rank", str(rank)]
+        if hetero:  # this rank's launch group: its GPU count and device offset on the node
+            argv += ["--distributed-init-method", os.environ["HETSEQ_INIT_METHOD"],
+                     "--distributed-gpus", os.environ["HETSEQ_GROUP_GPUS"],
+                     "--device-id-offset", os.environ["HETSEQ_DEVICE_OFFSET"]]
+        else:
+            argv += ["--distributed-init-method", "env://"]
     args = options.parse_cli(argv)
     args.distributed_rank = rank
-    args.device_id = local_rank
+    # local index -> device (group offset for heterogeneous launches); gloo rehearsal: all on GPU 0
+    args.device_id = 0 if b.dist_backend == "gloo" else distributed_utils.local_device_id(args, local_rank)
+    torch.cuda.set_device(args.device_id)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        distributed_utils.distributed_init(args)  # the training launcher's own rendezvous + warm-up
+        if b.dist_backend == "gloo":
+            dist.all_reduce(torch.zeros(1, device="cuda"))  # (touch the device as the nccl path does)
     torch.manual_seed(args.seed)
     task = LanguageModelingTask.setup_task(args)
     model = task.build_model(args)
@@ -185,8 +305,11 @@ def main():
     if rank == 0 and b.gemm_choices and not os.path.exists(b.gemm_choices):
         G.save_choices(b.gemm_choices)
     if rank == 0:
+        from hetseq_amd.parallel import comm as native_comm
+
         comm_kind = "none" if world == 1 else (
             "rccl-native" if getattr(ctl.model, "comm", None) is not None else "c10d-" + b.dist_backend)
+        par = "dp%d" % world + (" (hetero %s)" % "+".join(str(n) for n, _ in _groups(b)) if b.hetero else "")
         out = {
             "metric": "avg sec/step, BERT-base seq%d bs=%d/GPU" % (b.seq_len, b.batch),
             "value": round(sec, 6),
@@ -205,16 +328,18 @@ def main():
             "data": "synthetic NVIDIA-format HDF5 shards (random tokens), random-init weights",
             "config": {"model": "bert-base-uncased (L12 H768 A12, %d params)" % nparams,
                        "global_batch": seqs, "seq_len": b.seq_len, "per_gpu_batch": b.batch,
-                       "update_freq": b.update_freq, "parallelism": "dp%d" % world,
+                       "update_freq": b.update_freq, "parallelism": par,
                        "fused_kernels": not b.no_fused, "bucket_cap_mb": b.bucket_cap_mb,
-                       "hip_graph": bool(b.hip_graph and world == 1), "comm": comm_kind},
+                       "hip_graph": bool(b.hip_graph and world == 1), "comm": comm_kind,
+                       "comm_fallback_reason": native_comm.LAST_STATUS.get("reason") if world > 1 else None},
             "final_train_loss_logged": round(loss, 5),
             "host_ms_per_step": round(host / b.steps * 1000, 3),
             "data_wait_ms_per_step": round(data_wait / b.steps * 1000, 3),
             "allocator_events": alloc_events,
             "gemm_choices": {str(k): v for k, v in list(G.GEMM_CHOICES.items())[:32]},
         }
-        print(json.dumps(out), flush=True)
+        sys.stdout.write(json.dumps(out) + "\n")  # one write: other ranks may share this pipe
+        sys.stdout.flush()
     if world > 1:
         dist.barrier()
         if getattr(ctl.model, "comm", None) is not None:

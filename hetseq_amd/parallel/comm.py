@@ -146,23 +146,89 @@ def want_native(engine, device_is_cuda, group=None):
     return True
 
 
-def create(engine, device_is_cuda, group=None, timeout_s=1800.0):
-    """A NativeComm when the engine resolves to native on EVERY rank, else None (c10d path).
-    The ranks agree first (one c10d all-reduce of an availability flag), because the RCCL
-    initialisation itself blocks until all ranks join it."""
-    engine = os.environ.get("HETSEQ_COMM_ENGINE", engine or "auto")
-    if engine == "c10d" or not device_is_cuda or dist.get_backend(group or dist.group.WORLD) != "nccl":
-        want_native(engine, device_is_cuda, group)  # (warns on an explicit native request)
-        return None
-    local = 1.0
-    try:
-        local = 0.0 if want_native(engine, device_is_cuda, group) else 1.0
-    except RuntimeError as e:
-        warnings.warn(str(e))
-    flag = torch.tensor([local], device="cuda")
+# What the last create() call decided, for logs and the benchmark record:
+# {"engine": "rccl-native" | "c10d", "reason": why the native engine is not in use (or None)}
+LAST_STATUS = {"engine": "c10d", "reason": "not created"}
+
+
+def _agree(ok, group, device):
+    """True when ``ok`` holds on EVERY rank of ``group`` (one c10d all-reduce of a failure count)."""
+    flag = torch.tensor([0.0 if ok else 1.0], device=device)
     dist.all_reduce(flag, group=group)
-    if float(flag.item()) != 0.0:
-        if local == 0.0:
-            warnings.warn("native RCCL engine unavailable on some rank; using c10d")
+    return float(flag.item()) == 0.0
+
+
+def _fault(point, rank):
+    """Fault injection for the fallback tests: ``HETSEQ_COMM_FAULT=<point>:<rank>`` with point
+    ``init`` (this rank fails before the RCCL rendezvous) or ``first`` (this rank's first
+    all-reduce reports a wrong result)."""
+    spec = os.environ.get("HETSEQ_COMM_FAULT", "")
+    for item in filter(None, spec.split(";")):
+        p, _, r = item.partition(":")
+        if p == point and (r == "" or int(r) == rank):
+            return True
+    return False
+
+
+def create(engine, device_is_cuda, group=None, timeout_s=1800.0, factory=None):
+    """A NativeComm when the native engine works on EVERY rank, else None (c10d path).
+
+    Construction is a cross-rank-agreed, two-round protocol, so one rank's failure never leaves
+    the others inside the RCCL rendezvous or with a half-working engine:
+
+    1. every rank checks what it can without the rendezvous (module built, backend, device,
+       injected ``init`` fault); the ranks agree (c10d all-reduce) before anyone calls
+       ncclCommInitRank, which blocks until all ranks join it;
+    2. every rank builds the communicator and runs one all-reduce through it, checking the
+       result on the host; the ranks agree again, and on any failure every rank aborts its
+       communicator (never waits for peers) and falls back to c10d.
+
+    The outcome and the failure reason land in :data:`LAST_STATUS`.  ``factory`` replaces the
+    NativeComm constructor (tests drive the protocol over gloo with a stand-in engine).
+    """
+    global LAST_STATUS
+    engine = os.environ.get("HETSEQ_COMM_ENGINE", engine or "auto")
+    backend = dist.get_backend(group or dist.group.WORLD)
+    if factory is None and (engine == "c10d" or not device_is_cuda or backend != "nccl"):
+        want_native(engine, device_is_cuda, group)  # (warns on an explicit native request)
+        LAST_STATUS = {"engine": "c10d", "reason": "engine=%s backend=%s cuda=%s" % (engine, backend, device_is_cuda)}
         return None
-    return NativeComm(group, timeout_s=timeout_s)
+    rank = dist.get_rank(group)
+    size = dist.get_world_size(group)
+    dev = "cuda" if backend == "nccl" else "cpu"
+    reason = None
+    try:  # round 1: local checks only
+        if factory is None and not want_native(engine, device_is_cuda, group):
+            reason = "native engine not requested or not built"
+        elif _fault("init", rank):
+            reason = "injected init fault on rank %d" % rank
+    except RuntimeError as e:
+        reason = str(e)
+    if not _agree(reason is None, group, dev):
+        LAST_STATUS = {"engine": "c10d", "reason": reason or "native engine unavailable on another rank"}
+        warnings.warn("native RCCL engine not used: %s; using c10d" % LAST_STATUS["reason"])
+        return None
+    nc = None
+    try:  # round 2: rendezvous + one verified collective
+        nc = (factory or NativeComm)(group, timeout_s=timeout_s)
+        t = torch.ones(1, device=dev)
+        nc.all_reduce(t)
+        if _fault("first", rank):
+            t.fill_(-1.0)
+        got = float(t.item())  # one host synchronisation, at setup only
+        nc.check()
+        if got != float(size):
+            raise RuntimeError("first all-reduce returned %g, expected %d" % (got, size))
+    except Exception as e:  # noqa: BLE001 - any failure turns into the agreed fallback
+        reason = "%s: %s" % (type(e).__name__, e)
+    if not _agree(reason is None, group, dev):
+        if nc is not None:
+            try:
+                nc.close(False)  # abort: frees the communicator without waiting for peers
+            except Exception:  # noqa: BLE001
+                pass
+        LAST_STATUS = {"engine": "c10d", "reason": reason or "native engine failed on another rank"}
+        warnings.warn("native RCCL engine not used: %s; using c10d" % LAST_STATUS["reason"])
+        return None
+    LAST_STATUS = {"engine": "rccl-native", "reason": None}
+    return nc
