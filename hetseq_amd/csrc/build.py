@@ -14,14 +14,22 @@ through a thin pybind11 layer that takes raw device addresses and a
 ``torch.cuda.current_stream().cuda_stream``).  That keeps compile times in
 seconds and avoids the torch C++ ABI altogether.
 
-Each translation unit is compiled to an object file only when its source
-(or any shared header) is newer than the object; objects compile in a
-process pool.  ``python -m hetseq_amd.csrc.build`` builds everything.
+Build integrity is content-based, not mtime-based: every module carries a
+stamp ``HETSEQ_SRC_HASH=<sha256>`` (a data symbol linked into the ``.so``)
+over its sources, shared headers, compiler flags and target arch.  A module is
+rebuilt exactly when its embedded stamp differs from the hash of the tree it
+sits in, and ``hetseq_amd/ops/_C.py`` refuses to import a module whose stamp
+does not match (it rebuilds first, or raises with HETSEQ_NO_AUTOBUILD=1), so a
+loaded ``_hip.so`` is always the code of the sources next to it.  Objects are
+cached per translation unit under ``build/native`` with the same content hash.
+``python -m hetseq_amd.csrc.build`` builds everything.
 """
 from __future__ import annotations
 
 import concurrent.futures as cf
+import hashlib
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -42,11 +50,30 @@ def _py_includes():
     return [sysconfig.get_paths()["include"], pybind11.get_include()]
 
 
-def _newer(target, deps):
-    if not os.path.exists(target):
-        return True
-    t = os.path.getmtime(target)
-    return any(os.path.getmtime(d) > t for d in deps)
+def _digest(paths, flags, extra=""):
+    """sha256 over the contents of ``paths`` (sorted by name), the compiler flags and ``extra``."""
+    h = hashlib.sha256()
+    h.update(extra.encode())
+    for f in flags:
+        h.update(b"\0F" + f.encode())
+    for p in sorted(paths, key=os.path.basename):
+        h.update(b"\0P" + os.path.basename(p).encode() + b"\0")
+        with open(p, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+_STAMP_RE = re.compile(rb"HETSEQ_SRC_HASH=([0-9a-f]{64})")
+
+
+def embedded_hash(so_path):
+    """The source stamp linked into a built module (None: missing file or no stamp)."""
+    try:
+        with open(so_path, "rb") as fh:
+            m = _STAMP_RE.search(fh.read())
+    except OSError:
+        return None
+    return m.group(1).decode() if m else None
 
 
 def _run(cmd, verbose):
@@ -63,56 +90,60 @@ def _headers(dirpath):
 
 
 def _compile_objs(compiler, flags, sources, headers, objdir, verbose, jobs):
+    """Compile each source whose content hash (source + headers + flags) differs from the one
+    recorded next to its object file."""
     os.makedirs(objdir, exist_ok=True)
     todo, objs = [], []
     for src in sources:
         obj = os.path.join(objdir, os.path.basename(src) + ".o")
         objs.append(obj)
-        if _newer(obj, [src] + headers):
-            todo.append((src, obj))
+        want = _digest([src] + headers, [compiler] + flags)
+        try:
+            with open(obj + ".hash") as fh:
+                have = fh.read().strip()
+        except OSError:
+            have = None
+        if have != want or not os.path.exists(obj):
+            todo.append((src, obj, want))
     if todo:
         with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-            futs = [ex.submit(_run, [compiler] + flags + ["-c", s, "-o", o], verbose) for s, o in todo]
+            futs = [ex.submit(_run, [compiler] + flags + ["-c", s, "-o", o], verbose) for s, o, _ in todo]
             for f in futs:
                 f.result()
-    return objs, bool(todo)
+        for _, o, want in todo:
+            with open(o + ".hash", "w") as fh:
+                fh.write(want)
+    return objs
 
 
-def _link(compiler, objs, out, ldflags, verbose, force):
-    if force or _newer(out, objs):
-        tmp = out + ".tmp"
-        _run([compiler, "-shared", "-o", tmp] + objs + ldflags, verbose)
-        os.replace(tmp, out)  # atomic: a running process never sees a half-written .so
+def _stamp_obj(name, digest, objdir, verbose):
+    """Object file defining the module's source stamp (a plain data symbol, kept by the linker)."""
+    os.makedirs(objdir, exist_ok=True)
+    src = os.path.join(objdir, "stamp_%s.cpp" % name)
+    with open(src, "w") as fh:
+        fh.write('extern "C" __attribute__((visibility("default"), used)) const char hetseq_src_stamp_%s[] = '
+                 '"HETSEQ_SRC_HASH=%s";\n' % (name.strip("_"), digest))
+    obj = src[:-4] + ".o"
+    _run(["g++", "-fPIC", "-c", src, "-o", obj], verbose)
+    return obj
 
 
-def build_native(verbose=False, jobs=4):
-    src = os.path.join(HERE, "native", "batcher.cpp")
-    if not _newer(os.path.join(PKG, "_native" + EXT), [src]):
-        return os.path.join(PKG, "_native" + EXT)
-    flags = ["-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall"] + ["-I" + p for p in _py_includes()]
-    objs, changed = _compile_objs("g++", flags, [src], [], os.path.join(BUILD_DIR, "native"), verbose, jobs)
-    out = os.path.join(PKG, "_native" + EXT)
-    _link("g++", objs, out, ["-pthread"], verbose, changed)
-    return out
+def _link(compiler, objs, out, ldflags, verbose):
+    tmp = out + ".tmp"
+    _run([compiler, "-shared", "-o", tmp] + objs + ldflags, verbose)
+    os.replace(tmp, out)  # atomic: a running process never sees a half-written .so
 
 
-def build_h5(verbose=False, jobs=4):
-    inc = os.path.join(HDF5_ROOT, "include")
-    lib = os.path.join(HDF5_ROOT, "lib")
-    if not os.path.exists(os.path.join(inc, "hdf5.h")):
-        raise RuntimeError("libhdf5 headers not found under %s (set HETSEQ_HDF5_ROOT)" % HDF5_ROOT)
-    src = os.path.join(HERE, "native", "h5shard.cpp")
-    if not _newer(os.path.join(PKG, "_h5" + EXT), [src]):
-        return os.path.join(PKG, "_h5" + EXT)
-    flags = ["-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall", "-I" + inc] + [
-        "-I" + p for p in _py_includes()
-    ]
-    objs, changed = _compile_objs("g++", flags, [src], [], os.path.join(BUILD_DIR, "h5"), verbose, jobs)
-    out = os.path.join(PKG, "_h5" + EXT)
-    # Link the real soname file so the loader never needs the dev symlink.
-    # static libstdc++: the rpath to the HDF5 prefix would otherwise pick its older libstdc++
-    _link("g++", objs, out, ["-pthread", "-static-libstdc++", "-static-libgcc", "-L" + lib, "-lhdf5", "-Wl,-rpath," + lib],
-          verbose, changed)
+def _build_module(name, compiler, flags, sources, headers, ldflags, objdir, verbose, jobs, out=None,
+                  link_compiler=None):
+    """Build ``hetseq_amd/<name>.so`` unless its embedded stamp already matches the tree."""
+    out = out or os.path.join(PKG, name + EXT)
+    digest = module_hash(name)
+    if embedded_hash(out) == digest:
+        return out
+    objs = _compile_objs(compiler, flags, sources, headers, objdir, verbose, jobs)
+    objs.append(_stamp_obj(name, digest, objdir, verbose))
+    _link(link_compiler or compiler, objs, out, ldflags, verbose)
     return out
 
 
@@ -145,50 +176,26 @@ def build_sanitized(outdir=None, verbose=False, jobs=4):
     pyinc = ["-I" + p for p in _py_includes()]
     base = ["-std=c++17", "-fPIC", "-Wall"] + SAN_FLAGS
     nsrc = os.path.join(HERE, "native", "batcher.cpp")
-    objs, changed = _compile_objs(SAN_CXX, base + pyinc, [nsrc], [], os.path.join(outdir, "obj-native"), verbose, jobs)
+    objs = _compile_objs(SAN_CXX, base + pyinc, [nsrc], [], os.path.join(outdir, "obj-native"), verbose, jobs)
     outs = [os.path.join(outdir, "_native" + EXT)]
-    _link(SAN_CXX, objs, outs[0], ["-pthread"] + SAN_FLAGS, verbose, changed)
+    _link(SAN_CXX, objs, outs[0], ["-pthread"] + SAN_FLAGS, verbose)
     inc, lib = os.path.join(HDF5_ROOT, "include"), os.path.join(HDF5_ROOT, "lib")
     if os.path.exists(os.path.join(inc, "hdf5.h")):
         hsrc = os.path.join(HERE, "native", "h5shard.cpp")
-        objs, changed = _compile_objs(SAN_CXX, base + ["-I" + inc] + pyinc, [hsrc], [],
+        objs = _compile_objs(SAN_CXX, base + ["-I" + inc] + pyinc, [hsrc], [],
                                       os.path.join(outdir, "obj-h5"), verbose, jobs)
         outs.append(os.path.join(outdir, "_h5" + EXT))
         # libhdf5 by path, not -L (the HDF5 prefix ships older sanitizer runtimes and libstdc++);
         # the system libstdc++ directory is searched before the HDF5 prefix at run time
         sysdir = "/usr/lib/x86_64-linux-gnu"
         _link(SAN_CXX, objs, outs[1], ["-pthread"] + SAN_FLAGS + [os.path.join(lib, "libhdf5.so"),
-              "-Wl,-rpath," + sysdir + ":" + lib], verbose, changed)
+              "-Wl,-rpath," + sysdir + ":" + lib], verbose)
     return outs
 
 
 def hip_sources():
     kdir = os.path.join(HERE, "kernels")
     return sorted(os.path.join(kdir, f) for f in os.listdir(kdir) if f.endswith((".hip", ".cpp")))
-
-
-def build_hip(verbose=False, jobs=8):
-    hipcc = shutil.which("hipcc") or os.path.join(ROCM, "bin", "hipcc")
-    kdir = os.path.join(HERE, "kernels")
-    out = os.path.join(PKG, "_hip" + EXT)
-    if not _newer(out, hip_sources() + _headers(kdir)):
-        return out  # the shipped module is current (object files need not travel with the tree)
-    flags = [
-        "-O3",
-        "-std=c++17",
-        "-fPIC",
-        "-fvisibility=hidden",
-        "--offload-arch=" + ARCH,
-        "-munsafe-fp-atomics",
-        "-Wno-unused-result",
-        "-I" + kdir,
-    ] + ["-I" + p for p in _py_includes()]
-    objs, changed = _compile_objs(
-        hipcc, flags, hip_sources(), _headers(kdir), os.path.join(BUILD_DIR, "hip-" + ARCH), verbose, jobs
-    )
-    out = os.path.join(PKG, "_hip" + EXT)
-    _link(hipcc, objs, out, ["--offload-arch=" + ARCH, "-L" + os.path.join(ROCM, "lib"), "-lamdhip64"], verbose, changed)
-    return out
 
 
 def _torch_lib():
@@ -200,24 +207,82 @@ def _torch_lib():
     return os.path.join(os.path.dirname(spec.origin), "lib")
 
 
+def _spec(name):
+    """(compiler, flags, sources, headers, ldflags, objdir) of one in-tree module."""
+    pyinc = ["-I" + p for p in _py_includes()]
+    host = ["-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall"]
+    if name == "_native":
+        return ("g++", host + pyinc, [os.path.join(HERE, "native", "batcher.cpp")], [], ["-pthread"],
+                os.path.join(BUILD_DIR, "native"))
+    if name == "_h5":
+        inc, lib = os.path.join(HDF5_ROOT, "include"), os.path.join(HDF5_ROOT, "lib")
+        if not os.path.exists(os.path.join(inc, "hdf5.h")):
+            raise RuntimeError("libhdf5 headers not found under %s (set HETSEQ_HDF5_ROOT)" % HDF5_ROOT)
+        # Link the real soname file so the loader never needs the dev symlink.  static libstdc++:
+        # the rpath to the HDF5 prefix would otherwise pick its older libstdc++
+        return ("g++", host + ["-I" + inc] + pyinc, [os.path.join(HERE, "native", "h5shard.cpp")], [],
+                ["-pthread", "-static-libstdc++", "-static-libgcc", "-L" + lib, "-lhdf5", "-Wl,-rpath," + lib],
+                os.path.join(BUILD_DIR, "h5"))
+    if name == "_hip":
+        hipcc = shutil.which("hipcc") or os.path.join(ROCM, "bin", "hipcc")
+        kdir = os.path.join(HERE, "kernels")
+        flags = ["-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "--offload-arch=" + ARCH, "-munsafe-fp-atomics",
+                 "-Wno-unused-result", "-I" + kdir] + pyinc
+        return (hipcc, flags, hip_sources(), _headers(kdir),
+                ["--offload-arch=" + ARCH, "-L" + os.path.join(ROCM, "lib"), "-lamdhip64"],
+                os.path.join(BUILD_DIR, "hip-" + ARCH))
+    if name == "_comm":
+        tlib = _torch_lib()
+        rccl = os.path.join(tlib, "librccl.so")
+        if not os.path.exists(rccl):
+            rccl = os.path.join(ROCM, "lib", "librccl.so")
+        hip = os.path.join(tlib, "libamdhip64.so")
+        if not os.path.exists(hip):
+            hip = os.path.join(ROCM, "lib", "libamdhip64.so")
+        flags = ["-O2", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall", "-D__HIP_PLATFORM_AMD__",
+                 "-I" + os.path.join(ROCM, "include")] + pyinc
+        return ("g++", flags, [os.path.join(HERE, "comm", "comm.cpp")], [],
+                ["-pthread", rccl, hip, "-Wl,-rpath," + os.path.dirname(rccl)], os.path.join(BUILD_DIR, "comm"))
+    raise KeyError(name)
+
+
+MODULES = ("_native", "_h5", "_hip", "_comm")
+
+
+def module_hash(name):
+    """Content hash the module's embedded stamp must equal: its sources, shared headers,
+    compiler, flags (include paths and target arch among them) and link flags."""
+    cc, flags, srcs, hdrs, ld, _ = _spec(name)
+    # directories dropped (same toolchain, different install prefix or PATH entry -> same stamp)
+    norm = [re.sub(r"/[^\s:]*/", "", f) for f in [cc] + flags + ["LD"] + ld]
+    return _digest(srcs + hdrs, norm, extra=name)
+
+
+def stamp_status(name, so_path=None):
+    """(embedded stamp, expected hash) of an in-tree module; equal means the .so is current."""
+    return embedded_hash(so_path or os.path.join(PKG, name + EXT)), module_hash(name)
+
+
+def _build(name, verbose, jobs):
+    cc, flags, srcs, hdrs, ld, objdir = _spec(name)
+    return _build_module(name, cc, flags, srcs, hdrs, ld, objdir, verbose, jobs)
+
+
+def build_native(verbose=False, jobs=4):
+    return _build("_native", verbose, jobs)
+
+
+def build_h5(verbose=False, jobs=4):
+    return _build("_h5", verbose, jobs)
+
+
+def build_hip(verbose=False, jobs=8):
+    return _build("_hip", verbose, jobs)
+
+
 def build_comm(verbose=False, jobs=4):
     """``hetseq_amd/_comm*.so`` -- the RCCL gradient-communication engine (host C++, g++)."""
-    src = os.path.join(HERE, "comm", "comm.cpp")
-    out = os.path.join(PKG, "_comm" + EXT)
-    if not _newer(out, [src]):
-        return out
-    tlib = _torch_lib()
-    rccl = os.path.join(tlib, "librccl.so")
-    if not os.path.exists(rccl):
-        rccl = os.path.join(ROCM, "lib", "librccl.so")
-    hip = os.path.join(tlib, "libamdhip64.so")
-    if not os.path.exists(hip):
-        hip = os.path.join(ROCM, "lib", "libamdhip64.so")
-    flags = ["-O2", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall", "-D__HIP_PLATFORM_AMD__",
-             "-I" + os.path.join(ROCM, "include")] + ["-I" + p for p in _py_includes()]
-    objs, changed = _compile_objs("g++", flags, [src], [], os.path.join(BUILD_DIR, "comm"), verbose, jobs)
-    _link("g++", objs, out, ["-pthread", rccl, hip, "-Wl,-rpath," + os.path.dirname(rccl)], verbose, changed)
-    return out
+    return _build("_comm", verbose, jobs)
 
 
 def build_all(verbose=False, hip=True, h5=True):

@@ -40,7 +40,7 @@ int launch_emb_bwd(int, const void*, const float*, const float*, const float*, c
                    const int64_t*, float*, int, int, float, u64, u64, hipStream_t);
 void launch_colpart_finalize(const float* const*, float* const*, int, int, int, int, hipStream_t);
 int launch_segsum_rows(const float*, const int64_t*, const int64_t*, float*, float*, int, int, int, hipStream_t);
-int launch_sort_keys(const int64_t*, int, int64_t, int64_t*, int64_t*, hipStream_t);
+int launch_sort_keys(const int64_t*, int, int64_t, int64_t*, int64_t*, int*, hipStream_t);
 int launch_pos_grad(const float*, float*, int, int, int, hipStream_t);
 // elementwise.hip
 void launch_bias_gelu_fwd(int, const void*, const float*, void*, int64_t, int, hipStream_t);
@@ -108,6 +108,18 @@ static void check(int rc, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
 static void check_launch(const char* what) { check(0, what); }
+// An error left pending by an EARLIER HIP call (torch's or ours) is raised here, named against the
+// op about to launch, instead of being cleared and lost.  Only the status codes torch's own
+// queries and P2P probes leave behind are benign and cleared: hipErrorNotReady (event / stream
+// queries), peer access already enabled / not enabled.
+static void pre_launch(const char* what) {
+  const hipError_t e = hipGetLastError();
+  if (e == hipSuccess || e == hipErrorNotReady || e == hipErrorPeerAccessAlreadyEnabled ||
+      e == hipErrorPeerAccessNotEnabled)
+    return;
+  throw std::runtime_error(std::string("HIP error pending before ") + what + " (left by an earlier call): " +
+                           hipGetErrorString(e));
+}
 
 // Stream fork/join for the weight-gradient side stream (runtime/streams.py): record an event on
 // `signal`, make `waiter` wait for it.  A ring of timing-free events, created once; an event is
@@ -132,13 +144,13 @@ PYBIND11_MODULE(_hip, m) {
   m.attr("arch") = "gfx950";
 
   m.def("grad_norm", [](i64 g, i64 n, i64 partial, i64 scale, float max_norm, i64 out, i64 st) {
-    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
+    pre_launch("grad_norm");
     launch_grad_norm(P(const float*, g), n, P(double*, partial), P(const float*, scale), max_norm, P(float*, out), ST(st));
     check_launch("grad_norm");
   });
   m.def("adam_flat", [](i64 p, i64 g, i64 mm, i64 v, i64 shadow, i64 n, i64 gmul, float lr, float b1, float b2,
                         float eps, float wd, float step_size, i64 st, i64 hyper) {
-    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
+    pre_launch("adam_flat");
     launch_adam_flat(P(float*, p), P(const float*, g), P(float*, mm), P(float*, v), P(void*, shadow), n,
                      P(const float*, gmul), lr, b1, b2, eps, wd, step_size, P(const float*, hyper), ST(st));
     check_launch("adam_flat");
@@ -148,21 +160,21 @@ PYBIND11_MODULE(_hip, m) {
      pybind11::arg("hyper") = 0);
   m.def("adadelta_flat", [](i64 p, i64 g, i64 sq, i64 acc, i64 shadow, i64 n, i64 gmul, float lr, float rho, float eps,
                             float wd, i64 st) {
-    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
+    pre_launch("adadelta_flat");
     launch_adadelta_flat(P(float*, p), P(const float*, g), P(float*, sq), P(float*, acc), P(void*, shadow), n,
                          P(const float*, gmul), lr, rho, eps, wd, ST(st));
     check_launch("adadelta_flat");
   });
   m.def("lamb_flat", [](i64 p, i64 g, i64 mm, i64 v, i64 upd, i64 shadow, i64 seg_off, int nseg, i64 seg_norms, i64 gmul,
                         float lr, float b1, float b2, float eps, float wd, float bc1, float bc2, i64 st) {
-    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
+    pre_launch("lamb_flat");
     launch_lamb_flat(P(float*, p), P(const float*, g), P(float*, mm), P(float*, v), P(float*, upd), P(void*, shadow),
                      P(const int64_t*, seg_off), nseg, P(float*, seg_norms), P(const float*, gmul), lr, b1, b2, eps, wd,
                      bc1, bc2, ST(st));
     check_launch("lamb_flat");
   });
   m.def("cast_f32_bf16", [](i64 x, i64 y, i64 n, i64 st) {
-    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
+    pre_launch("cast_f32_bf16");
     launch_cast_f32_bf16(P(const float*, x), P(void*, y), n, ST(st));
     check_launch("cast_f32_bf16");
   });
@@ -170,7 +182,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("ln_bwd_num_blocks", &ln_bwd_num_blocks);
   m.def("ln_fwd", [](int dt, i64 a, i64 bias, i64 resid, i64 gamma, i64 beta, i64 y, i64 zsave, i64 mean, i64 rstd,
                      int rows, int H, float eps, float p, u64 seed, u64 off, int mode, i64 st) {
-    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
+    pre_launch("ln_fwd");
     check(launch_ln_fwd(dt, P(const void*, a), P(const float*, bias), P(const void*, resid), P(const float*, gamma),
                         P(const float*, beta), P(void*, y), P(float*, zsave), P(float*, mean), P(float*, rstd), rows, H,
                         eps, p, seed, off, mode, ST(st)),
@@ -178,7 +190,7 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("ln_bwd", [](int dt, i64 dy, i64 zsave, i64 mean, i64 rstd, i64 gamma, i64 dz, i64 da, i64 pg, i64 pb, i64 pbias,
                      int rows, int H, float p, u64 seed, u64 off, int mode, i64 st) {
-    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
+    pre_launch("ln_bwd");
     check(launch_ln_bwd(dt, P(const void*, dy), P(const float*, zsave), P(const float*, mean), P(const float*, rstd),
                         P(const float*, gamma), P(void*, dz), P(void*, da), P(float*, pg), P(float*, pb),
                         P(float*, pbias), rows, H, p, seed, off, mode, ST(st)),
@@ -187,7 +199,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("emb_fwd", [](int dt, i64 ids, i64 tt, i64 w, i64 pe, i64 te, i64 gamma, i64 beta, i64 y, i64 zsave, i64 mean,
                       i64 rstd, int rows, int S, int H, int V, int TV, float eps, float p, u64 seed, u64 off, i64 err,
                       i64 st) {
-    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
+    pre_launch("emb_fwd");
     check(launch_emb_fwd(dt, P(const int64_t*, ids), P(const int64_t*, tt), P(const float*, w), P(const float*, pe),
                          P(const float*, te), P(const float*, gamma), P(const float*, beta), P(void*, y),
                          P(float*, zsave), P(float*, mean), P(float*, rstd), rows, S, H, V, TV, eps, p, seed, off,
@@ -196,95 +208,99 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("emb_bwd", [](int dt, i64 dy, i64 zsave, i64 mean, i64 rstd, i64 gamma, i64 dx, i64 pg, i64 pb, i64 tt, i64 pt,
                       int rows, int H, float p, u64 seed, u64 off, i64 st) {
-    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
+    pre_launch("emb_bwd");
     check(launch_emb_bwd(dt, P(const void*, dy), P(const float*, zsave), P(const float*, mean), P(const float*, rstd),
                          P(const float*, gamma), P(float*, dx), P(float*, pg), P(float*, pb), P(const int64_t*, tt),
                          P(float*, pt), rows, H, p, seed, off, ST(st)),
           "emb_bwd");
   });
-  m.def("sort_keys", [](i64 keys, int n, i64 bound, i64 out_keys, i64 out_order, i64 st) {
-    (void)hipGetLastError();
-    return launch_sort_keys(P(const int64_t*, keys), n, bound, P(int64_t*, out_keys), P(int64_t*, out_order), ST(st));
-  }, "stable sort of n int64 keys in [0, bound): sorted keys + source indices; -1 = unsupported size");
+  m.def("sort_keys", [](i64 keys, int n, i64 bound, i64 out_keys, i64 out_order, i64 err, i64 st) {
+    pre_launch("sort_keys");
+    const int rc = launch_sort_keys(P(const int64_t*, keys), n, bound, P(int64_t*, out_keys), P(int64_t*, out_order),
+                                    P(int*, err), ST(st));
+    if (rc == 0) check_launch("sort_keys");  // a failed launch must not leave out_keys / out_order unwritten
+    return rc;
+  }, "stable sort of n int64 keys in [0, bound): sorted keys + source indices; -1 = unsupported size; a key "
+     "outside [0, bound) sets bit 2 of *err and sorts as clamped");
   // ---- MNISTNet (mnist.hip); every entry raw pointers + batch size + stream
   m.def("mnist_conv1_fwd", [](i64 x, i64 w, i64 b, i64 y, int B, i64 st) {
-    (void)hipGetLastError();
+    pre_launch("mnist_conv1_fwd");
     launch_mnist_conv1_fwd(P(const float*, x), P(const float*, w), P(const float*, b), P(float*, y), B, ST(st));
     check_launch("mnist_conv1_fwd");
   });
   m.def("mnist_im2col", [](i64 h1, i64 col, int B, int R, i64 st) {
-    (void)hipGetLastError();
+    pre_launch("mnist_im2col");
     check(R >= B * 576 ? 0 : -1, "mnist_im2col");
     launch_mnist_im2col(P(const float*, h1), P(float*, col), B, R, ST(st));
     check_launch("mnist_im2col");
   });
   m.def("mnist_perm", [](i64 src, i64 dst, int rows, int mode, i64 st) {
-    (void)hipGetLastError();
+    pre_launch("mnist_perm");
     check(mode >= 0 && mode <= 3 ? 0 : -1, "mnist_perm");
     launch_mnist_perm(P(const float*, src), P(float*, dst), rows, mode, ST(st));
     check_launch("mnist_perm");
   });
   m.def("mnist_pool_fwd", [](i64 c2, i64 pooled, i64 arg, int B, int Bp, float p, u64 seed, u64 off, i64 st) {
-    (void)hipGetLastError();
+    pre_launch("mnist_pool_fwd");
     launch_mnist_pool_fwd(P(const float*, c2), P(float*, pooled), P(uint8_t*, arg), B, Bp, p, seed, off, ST(st));
     check_launch("mnist_pool_fwd");
   });
   m.def("mnist_pool_bwd", [](i64 dpooled, i64 arg, i64 dc2, int B, int R, float p, i64 st) {
-    (void)hipGetLastError();
+    pre_launch("mnist_pool_bwd");
     check(R >= B * 576 ? 0 : -1, "mnist_pool_bwd");
     launch_mnist_pool_bwd(P(const float*, dpooled), P(const uint8_t*, arg), P(float*, dc2), B, R, p, ST(st));
     check_launch("mnist_pool_bwd");
   });
   m.def("mnist_head_fwd", [](i64 pre, i64 w2, i64 b2, i64 target, i64 h, i64 logp, i64 nll, int B, float p, u64 seed,
                              u64 off, i64 st) {
-    (void)hipGetLastError();
+    pre_launch("mnist_head_fwd");
     launch_mnist_head_fwd(P(const float*, pre), P(const float*, w2), P(const float*, b2), P(const int64_t*, target),
                           P(float*, h), P(float*, logp), P(float*, nll), B, p, seed, off, ST(st));
     check_launch("mnist_head_fwd");
   });
   m.def("mnist_loss", [](i64 nll, i64 logp, i64 target, int B, int mean, i64 loss, i64 correct, i64 count, i64 st) {
-    (void)hipGetLastError();
+    pre_launch("mnist_loss");
     launch_mnist_loss(P(const float*, nll), P(const float*, logp), P(const int64_t*, target), B, mean, P(float*, loss),
                       P(float*, correct), P(float*, count), ST(st));
     check_launch("mnist_loss");
   });
   m.def("mnist_head_bwd", [](i64 dloss, i64 count, i64 logp, i64 target, i64 pre, i64 h, i64 w2, i64 dlogits,
                              i64 dpre, int B, int Bp, int mean, float p, i64 st) {
-    (void)hipGetLastError();
+    pre_launch("mnist_head_bwd");
     launch_mnist_head_bwd(P(const float*, dloss), P(const float*, count), P(const float*, logp),
                           P(const int64_t*, target), P(const float*, pre), P(const float*, h), P(const float*, w2),
                           P(float*, dlogits), P(float*, dpre), B, Bp, mean, p, ST(st));
     check_launch("mnist_head_bwd");
   });
   m.def("mnist_fc2_wgrad", [](i64 dlogits, i64 h, i64 part, i64 dw2, i64 db2, int B, i64 st) {
-    (void)hipGetLastError();  // part: 64 * 1290 floats of scratch
+    pre_launch("mnist_fc2_wgrad");
     launch_mnist_fc2_wgrad(P(const float*, dlogits), P(const float*, h), P(float*, part), P(float*, dw2),
                            P(float*, db2), B, ST(st));
     check_launch("mnist_fc2_wgrad");
   });
   m.def("mnist_col2im", [](i64 dcol, i64 h1, i64 dh1, int B, i64 st) {
-    (void)hipGetLastError();
+    pre_launch("mnist_col2im");
     launch_mnist_col2im(P(const float*, dcol), P(const float*, h1), P(float*, dh1), B, ST(st));
     check_launch("mnist_col2im");
   });
   m.def("mnist_conv1_wgrad", [](i64 dh1, i64 x, i64 part, i64 dw1, i64 db1, int B, i64 st) {
-    (void)hipGetLastError();  // part: 1024 * 320 floats of scratch
+    pre_launch("mnist_conv1_wgrad");
     launch_mnist_conv1_wgrad(P(const float*, dh1), P(const float*, x), P(float*, part), P(float*, dw1),
                              P(float*, db1), B, ST(st));
     check_launch("mnist_conv1_wgrad");
   });
   m.def("segsum_rows", [](i64 src, i64 order, i64 keys, i64 scratch, i64 dst, int n, int H, int K, i64 st) {
-    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
+    pre_launch("segsum_rows");
     check(launch_segsum_rows(P(const float*, src), P(const int64_t*, order), P(const int64_t*, keys),
                              P(float*, scratch), P(float*, dst), n, H, K, ST(st)),
           "segsum_rows");
   });
   m.def("pos_grad", [](i64 dx, i64 dpos, int B, int S, int H, i64 st) {
-    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
+    pre_launch("pos_grad");
     check(launch_pos_grad(P(const float*, dx), P(float*, dpos), B, S, H, ST(st)), "pos_grad");
   });
   m.def("colpart_finalize", [](py::list parts, py::list outs, int nparts, int H, int accumulate, i64 st) {
-    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
+    pre_launch("colpart_finalize");
     const int n = static_cast<int>(parts.size());
     if (n < 1 || n > 3 || outs.size() != parts.size()) throw std::invalid_argument("colpart_finalize: 1..3 pairs");
     const float* pp[3];
@@ -298,7 +314,7 @@ PYBIND11_MODULE(_hip, m) {
   });
 
   m.def("bias_gelu_fwd", [](int dt, i64 x, i64 b, i64 y, i64 rows, int N, i64 st) {
-    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
+    pre_launch("bias_gelu_fwd");
     launch_bias_gelu_fwd(dt, P(const void*, x), P(const float*, b), P(void*, y), rows, N, ST(st));
     check_launch("bias_gelu_fwd");
   });
@@ -306,7 +322,7 @@ PYBIND11_MODULE(_hip, m) {
                           i64 B, i64 ldb, i64 b_ps, i64 C, i64 ldc, i64 bias, int epi, float beta, i64 aux,
                           i64 ldaux, i64 part, i64 colsum, int colsum_acc, int ksplit, i64 slab, i64 slab_floats,
                           int variant, i64 st) {
-    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
+    pre_launch("gemm_planes");
     const int rc = launch_gemm_planes(planes, c_dtype, ta, tb, M, N, K, P(const void*, A), lda, a_ps,
                                       P(const void*, B), ldb, b_ps, P(void*, C), ldc, P(const float*, bias), epi,
                                       beta, P(void*, aux), ldaux, P(float*, part), P(float*, colsum), colsum_acc,
@@ -316,14 +332,14 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("set_planes_variant", &set_planes_variant, "plane GEMM variant: 0 default, 1 one LDS stage, 2 half K depth");
   m.def("split_planes", [](i64 x, i64 out, i64 n, i64 ps, i64 st) {
-    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
+    pre_launch("split_planes");
     if (n % 4 || ps % 4) throw std::invalid_argument("split_planes: n and the plane stride must be multiples of 4");
     launch_split_planes(P(const float*, x), P(void*, out), n, ps, ST(st));
     check_launch("split_planes");
   });
   m.def("pool_nsp_fwd", [](int dt, i64 seq, int B, int S, int H, i64 Wp, i64 bp, i64 Wn, i64 bn, i64 label,
                            i64 mlm_loss, i64 pooled, i64 logits, i64 lse, i64 stats, i64 total, i64 st) {
-    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
+    pre_launch("pool_nsp_fwd");
     check(launch_pool_nsp_fwd(dt, P(const void*, seq), B, S, H, P(const float*, Wp), P(const float*, bp),
                               P(const float*, Wn), P(const float*, bn), P(const int64_t*, label),
                               P(const float*, mlm_loss), P(float*, pooled), P(float*, logits), P(float*, lse),
@@ -333,7 +349,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("pool_nsp_bwd", [](int dt, i64 dloss, i64 seq, i64 dseq, int B, int S, int H, i64 Wp, i64 Wn, i64 label,
                            i64 pooled, i64 logits, i64 lse, i64 stats, i64 dlogits, i64 dpre, i64 part, i64 dWp,
                            i64 dbp, i64 dWn, i64 dbn, int accumulate, i64 st) {
-    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
+    pre_launch("pool_nsp_bwd");
     check(launch_pool_nsp_bwd(dt, P(const float*, dloss), P(const void*, seq), P(void*, dseq), B, S, H,
                               P(const float*, Wp), P(const float*, Wn), P(const int64_t*, label),
                               P(const float*, pooled), P(const float*, logits), P(const float*, lse),
@@ -344,24 +360,24 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("colsum_row_chunks", &colsum_row_chunks);
   m.def("colsum", [](int dt, i64 dy, i64 x, i64 b, i64 dx, i64 part, i64 out, i64 rows, int N, int accumulate, i64 st) {
-    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
+    pre_launch("colsum");
     launch_colsum(dt, P(const void*, dy), P(const void*, x), P(const float*, b), P(void*, dx), P(float*, part),
                   P(float*, out), rows, N, accumulate, ST(st));
     check_launch("colsum");
   });
   m.def("mlm_compact", [](i64 labels, int rows, int ignore, int cap, i64 idx, i64 lab_out, i64 count, i64 err, i64 st) {
-    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
+    pre_launch("mlm_compact");
     launch_mlm_compact(P(const int64_t*, labels), rows, ignore, cap, P(int32_t*, idx), P(int64_t*, lab_out),
                        P(int32_t*, count), P(int*, err), ST(st));
     check_launch("mlm_compact");
   });
   m.def("gather_rows", [](int dt, i64 src, i64 idx, i64 out, int n, int H, i64 st) {
-    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
+    pre_launch("gather_rows");
     launch_gather_rows(dt, P(const void*, src), P(const int32_t*, idx), P(void*, out), n, H, ST(st));
     check_launch("gather_rows");
   });
   m.def("scatter_add_rows", [](int dt, i64 src, i64 idx, i64 dst, int n, int H, i64 st) {
-    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
+    pre_launch("scatter_add_rows");
     launch_scatter_add_rows(dt, P(const void*, src), P(const int32_t*, idx), P(void*, dst), n, H, ST(st));
     check_launch("scatter_add_rows");
   });
@@ -372,14 +388,14 @@ PYBIND11_MODULE(_hip, m) {
   m.def("attn_fp32_mode", &attn_fp32_mode);
   m.def("attn_fwd", [](int dt, i64 qkv, i64 mask, i64 bqkv, i64 ctx, i64 lse, i64 dmask, int B, int S, int NH, int D,
                        float p, u64 seed, u64 off, i64 st) {
-    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
+    pre_launch("attn_fwd");
     check(launch_attn_fwd(dt, P(const void*, qkv), P(const int64_t*, mask), P(const float*, bqkv), P(void*, ctx),
                           P(float*, lse), P(uint32_t*, dmask), B, S, NH, D, p, seed, off, ST(st)),
           "attn_fwd");
   });
   m.def("attn_bwd", [](int dt, i64 qkv, i64 mask, i64 bqkv, i64 ctx, i64 dctx, i64 lse, i64 dbuf, i64 dqkv, i64 dmask,
                        int B, int S, int NH, int D, float p, i64 st) {
-    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
+    pre_launch("attn_bwd");
     check(launch_attn_bwd(dt, P(const void*, qkv), P(const int64_t*, mask), P(const float*, bqkv),
                           P(const void*, ctx), P(const void*, dctx), P(const float*, lse), P(float*, dbuf),
                           P(void*, dqkv), P(const uint32_t*, dmask), B, S, NH, D, p, ST(st)),
@@ -388,14 +404,14 @@ PYBIND11_MODULE(_hip, m) {
 
   m.def("xent_fwd", [](int dt, i64 logits, i64 labels, int rows, int V, i64 ldv, int ignore, i64 row_loss, i64 lse,
                        i64 out, i64 st) {
-    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
+    pre_launch("xent_fwd");
     launch_xent_fwd(dt, P(const void*, logits), P(const int64_t*, labels), rows, V, ldv, ignore, P(float*, row_loss),
                     P(float*, lse), P(float*, out), ST(st));
     check_launch("xent_fwd");
   });
   m.def("xent_bwd", [](int dt, i64 logits, i64 labels, i64 lse, int rows, int V, i64 ldv, int ignore, i64 dloss,
                        i64 stats, i64 st) {
-    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
+    pre_launch("xent_bwd");
     launch_xent_bwd(dt, P(void*, logits), P(const int64_t*, labels), P(const float*, lse), rows, V, ldv, ignore,
                     P(const float*, dloss), P(const float*, stats), ST(st));
     check_launch("xent_bwd");
@@ -407,7 +423,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("gemm", [](int dt, int ta, int tb, int M, int N, int K, i64 A, i64 lda, i64 B, i64 ldb, i64 C, i64 ldc, i64 bias,
                    int epi, float beta, i64 aux, i64 ldaux, i64 part, i64 colsum, int colsum_acc, i64 st,
                    int tile, int ksplit, i64 slab, i64 slab_floats, int mv, int nv, int kv) {
-    (void)hipGetLastError();  // a stale error of an earlier (e.g. torch) HIP call is not ours
+    pre_launch("gemm");
     const int rc = launch_gemm(dt, ta, tb, M, N, K, P(const void*, A), lda, P(const void*, B), ldb, P(void*, C), ldc,
                                P(const float*, bias), epi, beta, P(float*, aux), ldaux, P(float*, part),
                                P(float*, colsum), colsum_acc, tile, ST(st), ksplit, P(float*, slab), slab_floats, mv, nv,

@@ -324,11 +324,18 @@ int launch_segsum_rows(const float* src, const int64_t* order, const int64_t* ke
 constexpr int kSortMax = 16384;
 
 __global__ void __launch_bounds__(256) sort_keys_kernel(const int64_t* __restrict__ keys, int n, int ib,
-                                                        int64_t* __restrict__ out_keys,
-                                                        int64_t* __restrict__ out_order) {
+                                                        int64_t bound, int64_t* __restrict__ out_keys,
+                                                        int64_t* __restrict__ out_order, int* __restrict__ err) {
   __shared__ uint32_t s[kSortMax];
   __shared__ int part[4][64];
-  for (int i = threadIdx.x; i < n; i += blockDim.x) s[i] = (static_cast<uint32_t>(keys[i]) << ib) | static_cast<uint32_t>(i);
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    int64_t k = keys[i];
+    if (k < 0 || k >= bound) {  // would wrap inside the packed word: flag it, sort it clamped
+      if (err && blockIdx.x == 0) atomicOr(err, 4);
+      k = k < 0 ? 0 : bound - 1;
+    }
+    s[i] = (static_cast<uint32_t>(k) << ib) | static_cast<uint32_t>(i);
+  }
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int i = blockIdx.x * 64 + lane;
@@ -345,14 +352,15 @@ __global__ void __launch_bounds__(256) sort_keys_kernel(const int64_t* __restric
   }
 }
 
-int launch_sort_keys(const int64_t* keys, int n, int64_t key_bound, int64_t* out_keys, int64_t* out_order,
+int launch_sort_keys(const int64_t* keys, int n, int64_t key_bound, int64_t* out_keys, int64_t* out_order, int* err,
                      hipStream_t st) {
   if (n <= 0 || n > kSortMax || key_bound <= 0) return -1;
   int ib = 0, kb = 0;
   while ((1 << ib) < n) ++ib;
   while ((int64_t(1) << kb) < key_bound) ++kb;
   if (ib + kb > 32) return -1;
-  hipLaunchKernelGGL(sort_keys_kernel, dim3((n + 63) / 64), dim3(256), 0, st, keys, n, ib, out_keys, out_order);
+  hipLaunchKernelGGL(sort_keys_kernel, dim3((n + 63) / 64), dim3(256), 0, st, keys, n, ib, key_bound, out_keys,
+                     out_order, err);
   return 0;
 }
 

@@ -8,6 +8,12 @@ Policy for the GPU path: when a CUDA/HIP device is present and the fused
 kernels are requested, a missing or unloadable ``_hip`` module is a hard
 error (``HipKernelsUnavailable``) -- there is no silent eager fallback on a
 GPU box.  On CPU-only hosts the model runs its torch-op reference path.
+
+Integrity: before a module is imported its embedded source stamp
+(``csrc/build.py``) is compared with the hash of the sources next to it.  A
+stale module is rebuilt first, or -- with ``HETSEQ_NO_AUTOBUILD=1`` -- refused
+with an error that names both hashes; a ``.so`` that does not belong to the
+tree is never loaded.
 """
 from __future__ import annotations
 
@@ -25,20 +31,38 @@ class HipKernelsUnavailable(RuntimeError):
     pass
 
 
+class StaleModule(ImportError):
+    pass
+
+
+def verify_stamp(name, builder=None, so_path=None):
+    """Make sure ``hetseq_amd/<name>.so`` was built from the sources in this tree: rebuild it
+    (``builder``) when its stamp differs, or raise :class:`StaleModule` when rebuilding is off
+    (``HETSEQ_NO_AUTOBUILD=1``) or does not help.  No-op when the sources are not present."""
+    from hetseq_amd.csrc import build as _build
+
+    try:
+        have, want = _build.stamp_status(name, so_path)
+    except (OSError, RuntimeError, KeyError):
+        return  # sources / toolchain headers not in this checkout: nothing to compare against
+    if have == want:
+        return
+    what = "hetseq_amd.%s: embedded source stamp %s does not match the tree (%s)" % (name, have, want)
+    if builder is None or os.environ.get("HETSEQ_NO_AUTOBUILD"):
+        raise StaleModule(what + "; rebuild with python -m hetseq_amd.csrc.build")
+    getattr(_build, builder)()
+    have = _build.embedded_hash(so_path) if so_path else _build.stamp_status(name)[0]
+    if have != want:
+        raise StaleModule(what + " even after a rebuild")
+
+
 def _load(name, builder):
     with _LOCK:
         if name in _CACHE:
             return _CACHE[name]
-        try:
-            mod = importlib.import_module("hetseq_amd." + name)
-        except ImportError:
-            if os.environ.get("HETSEQ_NO_AUTOBUILD"):
-                raise
-            from hetseq_amd.csrc import build as _build
-
-            getattr(_build, builder)()
-            importlib.invalidate_caches()
-            mod = importlib.import_module("hetseq_amd." + name)
+        verify_stamp(name, builder)
+        importlib.invalidate_caches()
+        mod = importlib.import_module("hetseq_amd." + name)
         _CACHE[name] = mod
         return mod
 
@@ -49,6 +73,14 @@ def native():
 
 def h5():
     return _load("_h5", "build_h5")
+
+
+def comm():
+    """The RCCL engine module, or None when it cannot be built / loaded here."""
+    try:
+        return _load("_comm", "build_comm")
+    except (ImportError, RuntimeError):
+        return None
 
 
 def hip():

@@ -31,7 +31,8 @@ LN_WIDTHS = (256, 512, 768, 1024, 1536, 2048)
 
 
 def _err_flag(device):
-    """Device-side error word (bit0: embedding id out of range, bit1: MLM overflow)."""
+    """Device-side error word (bit0: embedding id out of range, bit1: MLM overflow, bit2: sort key
+    out of range)."""
     key = ("err", device.index)
     buf = _BUFS.get(key)
     if buf is None:
@@ -51,6 +52,8 @@ def check_device_errors(device=None):
                 raise RuntimeError("embedding lookup got an id outside the vocabulary / type range")
             if e & 2:
                 raise RuntimeError("masked-LM rows exceeded the configured capacity (max_predictions_per_seq)")
+            if e & 4:
+                raise RuntimeError("sort_keys got a key outside [0, bound) (gradient rows would be misplaced)")
 
 
 def _colpart_buf(nparts, H, device, n=3):
@@ -259,7 +262,9 @@ def sort_keys(keys, bound):
     n = keys.numel()
     out_k = torch.empty_like(keys)
     out_o = torch.empty_like(keys)
-    if hip().sort_keys(keys.data_ptr(), n, int(bound), out_k.data_ptr(), out_o.data_ptr(), stream_handle()) == 0:
+    err = _err_flag(keys.device)  # bit 2: a key outside [0, bound) (sorted as clamped; raised by check_device_errors)
+    if hip().sort_keys(keys.data_ptr(), n, int(bound), out_k.data_ptr(), out_o.data_ptr(), err.data_ptr(),
+                       stream_handle()) == 0:
         return out_k, out_o
     return torch.sort(keys, stable=True)
 

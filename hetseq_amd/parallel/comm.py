@@ -33,11 +33,9 @@ _ids = itertools.count()
 
 def module():
     """The compiled engine, or None when it is not built (CPU-only checkouts)."""
-    try:
-        from hetseq_amd import _comm
-    except ImportError:
-        return None
-    return _comm
+    from hetseq_amd.ops import _C
+
+    return _C.comm()  # stamp-verified load (ops/_C.py)
 
 
 def _stream(s=None):

@@ -278,11 +278,27 @@ def test_sort_keys_matches_stable_sort(cuda, n, bound):
     keys = torch.randint(0, bound, (n,), device=cuda, dtype=torch.int64)
     ok = torch.empty_like(keys)
     oo = torch.empty_like(keys)
-    served = hip().sort_keys(keys.data_ptr(), n, bound, ok.data_ptr(), oo.data_ptr(), 0) == 0
+    err = torch.zeros(1, dtype=torch.int32, device=cuda)
+    served = hip().sort_keys(keys.data_ptr(), n, bound, ok.data_ptr(), oo.data_ptr(), err.data_ptr(), 0) == 0
     assert served == (n <= 16384 and (n - 1).bit_length() + (bound - 1).bit_length() <= 32)
     k, o = bert_ops.sort_keys(keys, bound)
     rk, ro = torch.sort(keys, stable=True)
     assert torch.equal(k, rk) and torch.equal(o, ro)
+    assert int(err.item()) == 0
+
+
+def test_sort_keys_flags_out_of_range_keys(cuda):
+    """A key outside [0, bound) no longer wraps silently: bit 2 of the error word is set (raised
+    by check_device_errors) and the key sorts as clamped, so the output stays a permutation."""
+    from hetseq_amd.ops._C import hip
+
+    keys = torch.tensor([3, -1, 7, 2, 9, 0], device=cuda, dtype=torch.int64)
+    ok, oo = torch.empty_like(keys), torch.empty_like(keys)
+    err = torch.zeros(1, dtype=torch.int32, device=cuda)
+    assert hip().sort_keys(keys.data_ptr(), 6, 8, ok.data_ptr(), oo.data_ptr(), err.data_ptr(), 0) == 0
+    assert int(err.item()) & 4
+    assert sorted(oo.tolist()) == list(range(6))
+    assert ok.tolist() == [0, 0, 2, 3, 7, 7]
 
 
 @pytest.mark.parametrize("B,S,NH", [(2, 128, 12), (2, 96, 2), (1, 512, 2)])
