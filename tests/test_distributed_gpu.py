@@ -92,3 +92,22 @@ def test_bert_resume_mid_epoch_matches_uninterrupted(tmp_path):
     ea, eb = sa["last_optimizer_state"]["state"], sb["last_optimizer_state"]["state"]
     for i in ea:
         assert torch.equal(ea[i]["exp_avg"], eb[i]["exp_avg"]) and torch.equal(ea[i]["exp_avg_sq"], eb[i]["exp_avg_sq"])
+
+
+def test_bench_self_launches_two_ranks(tmp_path):
+    """``python bench.py --gpus 2`` with no launcher: the parent starts two rank processes (never
+    touching the GPU itself), they time BERT-base data-parallel steps, rank 0 reports n_gpus 2 /
+    dp2.  Two ranks share the box's one GPU over gloo (RCCL refuses two ranks on one device)."""
+    import json
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+                        "--steps", "5", "--warmup", "2"], env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = lines[0]
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 64
+    assert out["config"]["comm"] == "c10d-gloo" and out["steps"] == 5
+    assert out["value"] > 0
