@@ -80,6 +80,11 @@ int launch_gemm_planes(int planes, int c_dtype, int ta, int tb, int M, int N, in
                        float* colsum_out, int colsum_acc, int ksplit, float* slab, int64_t slab_floats,
                        int variant, hipStream_t st);
 void launch_split_planes(const float* x, void* out, int64_t n, int64_t ps, hipStream_t st);
+// gemm_ring.hip
+int launch_gemm_ring(int ta, int tb, int M, int N, int K, const void* A, int64_t lda, int64_t a_ps, const void* B,
+                     int64_t ldb, int64_t b_ps, float* C, int64_t ldc, const float* bias, int epi, float beta,
+                     float* aux, int64_t ldaux, float* part, float* colsum_out, int colsum_acc, int ksplit,
+                     float* slab, int64_t slab_floats, void* outp, int64_t o_ps, int bn, hipStream_t st);
 void set_planes_variant(int v);
 
 // mnist.hip
@@ -330,6 +335,17 @@ PYBIND11_MODULE(_hip, m) {
     if (rc == 0) check_launch("gemm_planes");
     return rc;
   });
+  m.def("gemm_ring", [](int ta, int tb, int M, int N, int K, i64 A, i64 lda, i64 a_ps, i64 B, i64 ldb, i64 b_ps, i64 C,
+                        i64 ldc, i64 bias, int epi, float beta, i64 aux, i64 ldaux, i64 part, i64 colsum,
+                        int colsum_acc, int ksplit, i64 slab, i64 slab_floats, i64 outp, i64 o_ps, int bn, i64 st) {
+    pre_launch("gemm_ring");
+    const int rc = launch_gemm_ring(ta, tb, M, N, K, P(const void*, A), lda, a_ps, P(const void*, B), ldb, b_ps,
+                                    P(float*, C), ldc, P(const float*, bias), epi, beta, P(float*, aux), ldaux,
+                                    P(float*, part), P(float*, colsum), colsum_acc, ksplit, P(float*, slab),
+                                    slab_floats, P(void*, outp), o_ps, bn, ST(st));
+    if (rc == 0) check_launch("gemm_ring");
+    return rc;
+  }, "fp32 GEMM on split-bf16 planes, 3-stage LDS-DMA ring (gemm_ring.hip); -1 = shape not served");
   m.def("set_planes_variant", &set_planes_variant, "plane GEMM variant: 0 default, 1 one LDS stage, 2 half K depth");
   m.def("split_planes", [](i64 x, i64 out, i64 n, i64 ps, i64 st) {
     pre_launch("split_planes");

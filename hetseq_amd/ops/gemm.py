@@ -188,20 +188,80 @@ def _as_planes(x):
     return None
 
 
+RING = 5  # gemm_planes variant id of the 3-stage LDS-DMA ring kernel (csrc/kernels/gemm_ring.hip)
+_RING_OFF = os.environ.get("HETSEQ_GEMM_RING", "1") == "0"
+
+
+def _ring_bn(M, N, ta):
+    """Tile width the ring launcher picks (mirror of gemm_ring.hip pick_bn)."""
+    ok96, ok128 = N % 96 == 0, N % 128 == 0
+    if not (ok96 or ok128):
+        return 0
+    if ta and ok96:
+        return 96
+    if not ok96:
+        return 128
+    if not ok128:
+        return 96
+    t96, t128 = (M // 128) * (N // 96), (M // 128) * (N // 128)
+    return 128 if -(-t128 // 256) * 128 <= -(-t96 // 256) * 96 else 96
+
+
+def ring_ksplit(M, N, K, ta):
+    """K slices for a ring launch: minimise (rounds of one-per-CU blocks) x (K per block) plus the
+    fp32 slab traffic of the split (written and read once): t ~ rounds * 128 * BN * K/s * 12 FLOP at
+    ~5 TF/s per CU  +  s * M * N * 8 B at ~5 TB/s."""
+    bn = _ring_bn(M, N, ta)
+    if bn == 0 or M % 128:
+        return 1
+    tiles = (M // 128) * (N // bn)
+    best = None
+    for s in (1, 2, 4, 8):
+        if K % (32 * s) or (s > 1 and K // s < 256):
+            continue
+        t = -(-tiles * s // 256) * 128 * bn * (K // s) * 12 / 5.1e12 + (s * M * N * 8 / 5e12 if s > 1 else 0.0)
+        if best is None or t < best[0]:
+            best = (t, s)
+    return best[1] if best else 1
+
+
 def gemm_planes(a, b, ta, tb, out, bias=None, epi=EPI_NONE, beta=0.0, aux=None, part=None, colsum=None,
-                colsum_acc=False, ksplit=1, variant=-1):
+                colsum_acc=False, ksplit=1, variant=-1, outp=None, ring_bn=0):
     """Launch the bf16-plane engine on Planes operands; False (nothing launched) if not served.
     ``variant``: kernel variant (gemm_planes.hip: 0 two LDS stages, 1 one stage, 2 half K depth,
-    3 eight waves, 4 eight waves + one stage); -1 = :func:`planes_variant` for the shape."""
+    3 eight waves, 4 eight waves + one stage; 5 = RING, gemm_ring.hip); -1 = the ring kernel for
+    split-fp32 planes when it serves the shape, else :func:`planes_variant`.  ``outp``: a [3, M, N]
+    bf16 buffer that receives the result again as split planes (ring kernel, GELU / dGELU
+    epilogues: the output is the next GEMM's operand)."""
     if a.P != b.P or not out.is_cuda or out.stride(1) != 1 or out.dtype not in (torch.float32, torch.bfloat16):
         return False
     M, N, K = _dims(a, b, ta, tb)
     if out.shape != (M, N):
         return False
+    if a.P == 3 and out.dtype == torch.float32 and variant in (-1, RING) and not _RING_OFF:
+        ks = ksplit if ksplit and ksplit > 0 else 1
+        slab = _slab(M, N, ks, out.device) if ks > 1 else None
+        if ks > 1 and slab is None:
+            ks = 1
+        if outp is None or (outp.shape == (3, M, N) and out.stride(0) == N):
+            rc = hip().gemm_ring(int(ta), int(tb), M, N, K, a.data_ptr(), a.ld, a.ps, b.data_ptr(), b.ld, b.ps,
+                                 out.data_ptr(), out.stride(0), bias.data_ptr() if bias is not None else 0, epi,
+                                 float(beta), aux.data_ptr() if aux is not None else 0,
+                                 aux.stride(0) if aux is not None else 0, part.data_ptr() if part is not None else 0,
+                                 colsum.data_ptr() if colsum is not None else 0, int(colsum_acc), int(ks),
+                                 slab.data_ptr() if slab is not None else 0, slab.numel() if slab is not None else 0,
+                                 outp.data_ptr() if outp is not None else 0, M * N if outp is not None else 0,
+                                 int(ring_bn), stream_handle())
+            if rc == 0:
+                return True
+        if variant == RING:
+            return False
+    if outp is not None:
+        return False
     slab = _slab(M, N, ksplit, out.device) if ksplit > 1 else None
     if ksplit > 1 and slab is None:
         ksplit = 1
-    if variant < 0:
+    if variant < 0 or variant == RING:
         variant = planes_variant(M, N, K, a.P, ta)
     rc = hip().gemm_planes(a.P, 1 if out.dtype == torch.bfloat16 else 0, int(ta), int(tb), M, N, K, a.data_ptr(),
                            a.ld, a.ps, b.data_ptr(), b.ld, b.ps, out.data_ptr(), out.stride(0),
@@ -232,6 +292,8 @@ def _planes_ksplit(M, N, K, P):
     key = (M, N, K, P)
     if key in PLANES_KSPLIT:
         return PLANES_KSPLIT[key]
+    if P == 3 and not _RING_OFF and _ring_bn(M, N, True):
+        return ring_ksplit(M, N, K, True)
     tiles, s = (M // 128) * (N // 128), 1
     bk = 32 if P == 3 else 64
     while tiles * s < 384 and s < 8 and K % (2 * s * bk) == 0 and K // (2 * s) >= 512:

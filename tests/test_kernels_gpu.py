@@ -1006,3 +1006,91 @@ def test_gemm_planes_epilogues(cuda, P):
     f_gelu(pk + bk.double()).backward(dyd @ w2d)
     _close(dpre, pk.grad, tol, tol, "planes dgelu")
     _close(db, pk.grad.sum(0), tol, tol, "planes dgelu colsum")
+
+
+# ------------------------------------------------------------------ ring plane kernel (gemm_ring.hip)
+def _ring_err(a, b, ta, tb, out):
+    ad, bd = a.double(), b.double()
+    At, Bt = (ad.t() if ta else ad), (bd.t() if tb else bd)
+    ref = At @ Bt
+    mag = At.abs() @ Bt.abs()
+    f32 = (a.t() if ta else a) @ (b.t() if tb else b)
+    return float(((out.double() - ref).abs() / mag).max()), float(((f32.double() - ref).abs() / mag).max())
+
+
+@pytest.mark.parametrize("bn", [96, 128])
+@pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False)])
+@pytest.mark.parametrize("M,N,K,ks", [(256, 384, 512, 1), (128, 768, 96, 1), (384, 768, 1024, 4), (256, 384, 2048, 2),
+                                      (128, 384, 32, 1), (128, 384, 64, 1)])
+def test_gemm_ring_vs_fp64(cuda, bn, ta, tb, M, N, K, ks):
+    """Ring kernel, every operand layout (k-contiguous b128 images, mn-contiguous transposed
+    images), both tile widths, K of 1..64 tiles (prologue / odd tile counts) and split-K:
+    fp32-level error, within 2x of torch's own fp32 GEMM against fp64."""
+    from hetseq_amd.ops import gemm as G
+
+    torch.manual_seed(70 + M + N + K + bn)
+    a = torch.randn((K, M) if ta else (M, K), device=cuda)
+    b = torch.randn((N, K) if tb else (K, N), device=cuda)
+    out = torch.full((M, N), float("nan"), device=cuda)
+    assert G.gemm_planes(G.split(a.contiguous()), G.split(b.contiguous()), ta, tb, out, ksplit=ks,
+                         variant=G.RING, ring_bn=bn)
+    err, e32 = _ring_err(a, b, ta, tb, out)
+    assert err <= 2.0 * e32 and err < 5e-7, (err, e32)
+
+
+@pytest.mark.parametrize("ta,tb,M,N,K", [(0, 1, 4096, 2304, 768), (0, 1, 4096, 768, 768), (0, 1, 4096, 3072, 768),
+                                         (0, 0, 4096, 768, 3072), (0, 0, 4096, 768, 2304),
+                                         (1, 0, 768, 3072, 4096), (1, 0, 2304, 768, 4096)])
+def test_gemm_ring_bert_shapes(cuda, ta, tb, M, N, K):
+    """The BERT-base products on the ring kernel (the launcher's own tile and the K split of
+    the step): fp32-level error against fp64."""
+    from hetseq_amd.ops import gemm as G
+
+    torch.manual_seed(77)
+    a = torch.rand((K, M) if ta else (M, K), device=cuda) * 2 - 1
+    b = torch.rand((N, K) if tb else (K, N), device=cuda) * 2 - 1
+    out = torch.empty(M, N, device=cuda)
+    ks = G.ring_ksplit(M, N, K, bool(ta)) if ta else 1
+    assert G.gemm_planes(G.split(a), G.split(b), bool(ta), bool(tb), out, ksplit=ks, variant=G.RING)
+    err, e32 = _ring_err(a, b, ta, tb, out)
+    assert err <= 2.0 * e32 and err < 5e-7, (err, e32)
+
+
+def test_gemm_ring_epilogues_and_plane_output(cuda):
+    """bias, beta-accumulate, GELU (pre-activation kept, output planes) and dGELU + bias-gradient
+    column sums (output planes) on the ring kernel; the plane output equals split(C) bit for bit."""
+    from hetseq_amd.models.bert import f_gelu
+    from hetseq_amd.ops import gemm as G
+
+    torch.manual_seed(78)
+    T, K, N = 256, 512, 384
+    x, w, bias = torch.randn(T, K, device=cuda), torch.randn(N, K, device=cuda) * 0.05, torch.randn(N, device=cuda)
+    px, pw = G.split(x), G.split(w)
+    xd, wd = x.double(), w.double()
+    y = torch.empty(T, N, device=cuda)
+    assert G.gemm_planes(px, pw, False, True, y, bias, G.EPI_BIAS, variant=G.RING)
+    _close(y, xd @ wd.t() + bias.double(), 1e-5, 1e-5, "ring bias")
+    c0 = torch.randn(T, N, device=cuda)
+    c = c0.clone()
+    assert G.gemm_planes(px, pw, False, True, c, bias, G.EPI_BIAS, beta=1.0, variant=G.RING)
+    _close(c, xd @ wd.t() + bias.double() + c0.double(), 1e-5, 1e-5, "ring beta")
+    pre = torch.empty(T, N, device=cuda)
+    yp = torch.empty((3, T, N), dtype=torch.bfloat16, device=cuda)
+    assert G.gemm_planes(px, pw, False, True, y, bias, G.EPI_GELU, aux=pre, variant=G.RING, outp=yp)
+    _close(pre, xd @ wd.t(), 1e-5, 1e-5, "ring gelu pre")
+    _close(y, f_gelu(pre.double() + bias.double()), 1e-5, 1e-5, "ring gelu")
+    assert torch.equal(yp, G.split(y).buf.view(3, T, N))
+    dy = torch.randn(T, N, device=cuda)
+    w2 = torch.randn(N, K, device=cuda) * 0.05
+    prek, bk = torch.randn(T, K, device=cuda), torch.randn(K, device=cuda)
+    dpre = torch.empty(T, K, device=cuda)
+    dp = torch.empty((3, T, K), dtype=torch.bfloat16, device=cuda)
+    part = torch.empty((T // 128, K), device=cuda)
+    db = torch.empty(K, device=cuda)
+    assert G.gemm_planes(G.split(dy), G.split(w2), False, False, dpre, bk, G.EPI_DGELU, aux=prek, part=part,
+                         colsum=db, variant=G.RING, outp=dp)
+    pk = prek.double().requires_grad_()
+    f_gelu(pk + bk.double()).backward(dy.double() @ w2.double())
+    _close(dpre, pk.grad, 1e-5, 1e-5, "ring dgelu")
+    _close(db, pk.grad.sum(0), 1e-5, 1e-5, "ring dgelu colsum")
+    assert torch.equal(dp, G.split(dpre).buf.view(3, T, K))

@@ -1,62 +1,82 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 --pmc counter CSVs per kernel: MFMA utilisation, achieved MFMA FLOP rate,
-LDS bank-conflict rate.
+"""Per-kernel summary of rocprofv3 counter databases (rocpd sqlite, ROCm 7.x).
 
-usage: pmc_summary.py <run_counter_collection.csv> <title> [top_n]
-Counters expected: SQ_VALU_MFMA_BUSY_CYCLES, SQ_INSTS_VALU_MFMA_MOPS_{F32,BF16}, GRBM_GUI_ACTIVE,
-SQ_LDS_BANK_CONFLICT, SQ_LDS_IDX_ACTIVE.  MI355X: 256 CUs x 4 SIMDs; 1 MOP = 512 FLOP.
+    python tools/pmc_summary.py gpurun_out/pmc_a/run_results.db [more.db ...] [--match gemm_ring] [--top 20]
+
+Counters of several single-pass runs of the same program are joined by kernel name (each pass is
+its own run: rocprofv3 does not split counters over passes).  Per kernel: dispatches, mean
+duration, the mean of every counter per dispatch, and derived columns when their inputs exist:
+bf16 MFMA TF/s (512 FLOP per MOPS unit), MFMA busy % of the dispatch's SQ busy cycles, LDS
+bank-conflict % of LDS-active cycles, L2 hit %, wait % of wave cycles.
 """
-import csv
-import sys
-from collections import defaultdict
+import argparse
+import collections
+import re
+import sqlite3
 
-# sustained MFMA rates measured by tools/micro/mfma_peak.hip (profiles/r1_mfma_peak.md), TF/s
-PEAK_F32 = 155.0
-PEAK_BF16 = 2170.0
+
+def short(name, n=70):
+    name = re.sub(r"\(.*", "", name)
+    return name if len(name) <= n else name[:n - 3] + "..."
+
+
+def load(db):
+    c = sqlite3.connect(db)
+    per = collections.defaultdict(lambda: collections.defaultdict(list))
+    durs = collections.defaultdict(dict)
+    for name, disp, counter, value, dur in c.execute(
+            "select kernel_name, dispatch_id, counter_name, value, duration from counters_collection"):
+        per[name][counter].append((disp, value))
+        durs[name][disp] = dur
+    return per, durs
 
 
 def main():
-    path, title = sys.argv[1], sys.argv[2]
-    top = int(sys.argv[3]) if len(sys.argv) > 3 else 25
-    per = defaultdict(lambda: defaultdict(float))
-    ns = defaultdict(float)
-    calls = defaultdict(set)
-    gui = defaultdict(float)  # per dispatch: GRBM_GUI_ACTIVE is reported per XCD -> take the max
-    for r in csv.DictReader(open(path)):
-        k = r["Kernel_Name"]
-        d = r["Dispatch_Id"]
-        if r["Counter_Name"] == "GRBM_GUI_ACTIVE":
-            gui[(k, d)] = max(gui[(k, d)], float(r["Counter_Value"]))
-        else:
-            per[k][r["Counter_Name"]] += float(r["Counter_Value"])
-        if d not in calls[k]:
-            calls[k].add(d)
-            ns[k] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-    for (k, d), v in gui.items():
-        per[k]["GRBM_GUI_ACTIVE"] += v
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dbs", nargs="+")
+    ap.add_argument("--match", default=None)
+    ap.add_argument("--top", type=int, default=25)
+    a = ap.parse_args()
+    counters = collections.defaultdict(dict)  # kernel -> counter -> mean per dispatch
+    ndisp, dur = {}, {}
+    for db in a.dbs:
+        per, durs = load(db)
+        for k, cs in per.items():
+            if a.match and not re.search(a.match, k):
+                continue
+            for cn, vals in cs.items():
+                bydisp = collections.defaultdict(float)
+                for d, v in vals:
+                    bydisp[d] += v
+                counters[k][cn] = sum(bydisp.values()) / len(bydisp)
+            ndisp[k] = max(ndisp.get(k, 0), len(durs[k]))
+            dur.setdefault(k, []).extend(durs[k].values())
     rows = []
-    for k, c in per.items():
-        f32, b16 = 512.0 * c["SQ_INSTS_VALU_MFMA_MOPS_F32"], 512.0 * c["SQ_INSTS_VALU_MFMA_MOPS_BF16"]
-        tf = (f32 + b16) / (ns[k] * 1e-9) / 1e12 if ns[k] else 0.0
-        peak = PEAK_BF16 if b16 > f32 else PEAK_F32
-        util = 100.0 * tf / peak
-        lds = c["SQ_LDS_IDX_ACTIVE"]
-        conf = 100.0 * c["SQ_LDS_BANK_CONFLICT"] / lds if lds else 0.0
-        rows.append((ns[k], k, len(calls[k]), util, tf, conf))
-    rows.sort(reverse=True)
-    print("# %s\n" % title)
-    print("Source: `rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_INSTS_VALU_MFMA_MOPS_BF16 "
-          "GRBM_GUI_ACTIVE SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --kernel-trace` over `bench.py --steps 3` "
-          "(`%s`).  TF/s = MFMA FLOPs (512 x MFMA MOPS) / kernel time (counter runs serialise kernels, so times "
-          "are indicative); %% of peak against the sustained rates measured by tools/micro/mfma_peak.hip "
-          "(155 TF/s fp32, 2170 TF/s bf16); LDS conflict = bank-conflict cycles / LDS-active cycles.\n" % path)
-    print("Split-bf16 fp32 GEMMs (`gemm_x6s_kernel<..., 6, ...>`) issue six bf16 products per fp32 product: their "
-          "effective fp32 rate is the bf16 MFMA rate / 6 (last column).\n")
-    print("| kernel | dispatches | total ms | MFMA TF/s | % of sustained MFMA peak | LDS conflict % | effective fp32 TF/s |\n"
-          "|---|---|---|---|---|---|---|")
-    for t, k, n, u, tf, cf in rows[:top]:
-        eff = "%.1f" % (tf / 6.0) if "gemm_x6s_kernel" in k and ", 6," in k else ""
-        print("| `%s` | %d | %.3f | %.1f | %.1f | %.1f | %s |" % (k.replace("|", "/")[:90], n, t / 1e6, tf, u, cf, eff))
+    for k, cs in counters.items():
+        d = sum(dur[k]) / len(dur[k])  # ns
+        row = {"kernel": short(k), "n": ndisp[k], "us": d / 1000.0}
+        if "SQ_INSTS_VALU_MFMA_MOPS_BF16" in cs:
+            row["bf16 TF/s"] = cs["SQ_INSTS_VALU_MFMA_MOPS_BF16"] * 512 / d / 1000.0
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in cs and "SQ_BUSY_CYCLES" in cs and cs["SQ_BUSY_CYCLES"]:
+            row["mfma busy/SQ busy %"] = 100.0 * cs["SQ_VALU_MFMA_BUSY_CYCLES"] / (cs["SQ_BUSY_CYCLES"] * 4 * 4)
+        if "SQ_LDS_BANK_CONFLICT" in cs and cs.get("SQ_LDS_IDX_ACTIVE"):
+            row["lds conflict %"] = 100.0 * cs["SQ_LDS_BANK_CONFLICT"] / cs["SQ_LDS_IDX_ACTIVE"]
+        if "TCC_HIT_sum" in cs and (cs["TCC_HIT_sum"] + cs.get("TCC_MISS_sum", 0)):
+            row["L2 hit %"] = 100.0 * cs["TCC_HIT_sum"] / (cs["TCC_HIT_sum"] + cs.get("TCC_MISS_sum", 0))
+        if "SQ_WAVE_CYCLES" in cs and cs["SQ_WAVE_CYCLES"]:
+            for w in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_LDS"):
+                if w in cs:
+                    row[w.replace("SQ_", "").lower() + " %"] = 100.0 * cs[w] / cs["SQ_WAVE_CYCLES"]
+        if "GRBM_GUI_ACTIVE" in cs:
+            row["clock GHz"] = cs["GRBM_GUI_ACTIVE"] / 8 / d
+        rows.append(row)
+    rows.sort(key=lambda r: -r["us"] * r["n"])
+    cols = ["kernel", "n", "us"] + sorted({c for r in rows for c in r} - {"kernel", "n", "us"})
+    print("| " + " | ".join(cols) + " |")
+    print("|" + "---|" * len(cols))
+    for r in rows[:a.top]:
+        print("| " + " | ".join(("%.1f" % r[c]) if isinstance(r.get(c), float) else str(r.get(c, "")) for c in cols)
+              + " |")
 
 
 if __name__ == "__main__":
