@@ -89,6 +89,14 @@ def _headers(dirpath):
     return [os.path.join(dirpath, f) for f in os.listdir(dirpath) if f.endswith((".h", ".hpp", ".cuh"))]
 
 
+# per-translation-unit extra flags (kept in the object and module hashes)
+SOURCE_FLAGS = {
+    # MFMA accumulators in VGPRs: with AGPR accumulators hipcc rotates the ring kernel's 48-64
+    # accumulator registers through v_accvgpr moves on every loop iteration (72-96 per two K tiles)
+    "gemm_ring.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
+}
+
+
 def _compile_objs(compiler, flags, sources, headers, objdir, verbose, jobs):
     """Compile each source whose content hash (source + headers + flags) differs from the one
     recorded next to its object file."""
@@ -97,7 +105,7 @@ def _compile_objs(compiler, flags, sources, headers, objdir, verbose, jobs):
     for src in sources:
         obj = os.path.join(objdir, os.path.basename(src) + ".o")
         objs.append(obj)
-        want = _digest([src] + headers, [compiler] + flags)
+        want = _digest([src] + headers, [compiler] + flags + SOURCE_FLAGS.get(os.path.basename(src), []))
         try:
             with open(obj + ".hash") as fh:
                 have = fh.read().strip()
@@ -107,7 +115,8 @@ def _compile_objs(compiler, flags, sources, headers, objdir, verbose, jobs):
             todo.append((src, obj, want))
     if todo:
         with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-            futs = [ex.submit(_run, [compiler] + flags + ["-c", s, "-o", o], verbose) for s, o, _ in todo]
+            futs = [ex.submit(_run, [compiler] + flags + SOURCE_FLAGS.get(os.path.basename(s), []) + ["-c", s, "-o", o],
+                              verbose) for s, o, _ in todo]
             for f in futs:
                 f.result()
         for _, o, want in todo:
@@ -254,7 +263,8 @@ def module_hash(name):
     compiler, flags (include paths and target arch among them) and link flags."""
     cc, flags, srcs, hdrs, ld, _ = _spec(name)
     # directories dropped (same toolchain, different install prefix or PATH entry -> same stamp)
-    norm = [re.sub(r"/[^\s:]*/", "", f) for f in [cc] + flags + ["LD"] + ld]
+    extra = [f for src in srcs for f in ["SRC:" + os.path.basename(src)] + SOURCE_FLAGS.get(os.path.basename(src), [])]
+    norm = [re.sub(r"/[^\s:]*/", "", f) for f in [cc] + flags + ["LD"] + ld + extra]
     return _digest(srcs + hdrs, norm, extra=name)
 
 

@@ -318,8 +318,8 @@ __global__ void __launch_bounds__(NT, 1) gemm_ring_kernel(Args p) {
   for (int j = 0; j < TN; ++j) csum[j] = 0.f;
   // the runtime options (beta-accumulate, plane output) are hoisted out of the element loops: a
   // per-element branch around a load makes hipcc wait vmcnt(0) for every element
-  auto store = [&](auto use_beta, auto use_planes) __attribute__((always_inline)) {
-    constexpr bool UB = decltype(use_beta)::value, UP = decltype(use_planes)::value;
+  auto store = [&](auto use_beta, auto use_planes, auto write_c) __attribute__((always_inline)) {
+    constexpr bool UB = decltype(use_beta)::value, UP = decltype(use_planes)::value, WC = decltype(write_c)::value;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int n = n0 + wn + 16 * j + lr;
@@ -347,7 +347,7 @@ __global__ void __launch_bounds__(NT, 1) gemm_ring_kernel(Args p) {
             v = a + bv;
             if (UB) v += p.beta * in[r];
           }
-          p.C[m * p.ldc + n] = v;
+          if (WC) p.C[m * p.ldc + n] = v;
           if (UP) {  // the value again as planes, for the GEMMs that consume it
 #pragma clang fp contract(off)  // residuals of the STORED v (no fma with the product that made it)
             const b1 h = (b1)v;
@@ -365,13 +365,14 @@ __global__ void __launch_bounds__(NT, 1) gemm_ring_kernel(Args p) {
   };
   using T_ = std::true_type;
   using F_ = std::false_type;
-  if (EPI >= kGelu) {
-    if (p.outp) store(F_{}, T_{});
-    else store(F_{}, F_{});
+  if (EPI >= kGelu) {  // fused-activation outputs: planes only when the fp32 copy has no reader (C null)
+    if (p.outp && p.C) store(F_{}, T_{}, T_{});
+    else if (p.outp) store(F_{}, T_{}, F_{});
+    else store(F_{}, F_{}, T_{});
   } else if (p.beta != 0.f) {
-    store(T_{}, F_{});
+    store(T_{}, F_{}, T_{});
   } else {
-    store(F_{}, F_{});
+    store(F_{}, F_{}, T_{});
   }
   if (EPI == kDGelu) {  // column sums over the block's 128 rows: the 4 lane groups, then the 2 wave rows
     float* red = reinterpret_cast<float*>(smem);
@@ -452,6 +453,7 @@ int launch_gemm_ring(int ta, int tb, int M, int N, int K, const void* A, int64_t
   if (ksplit > 1 && (epi > 1 || outp || !slab || (int64_t)ksplit * M * N > slab_floats || N % 4 || ldc % 4))
     return -1;
   if (outp && (epi < 2 || o_ps <= 0)) return -1;  // plane outputs: the GELU / dGELU epilogues only
+  if (!C && !outp) return -1;
   // 32-bit per-lane DMA offsets: the operand span (all planes) must stay below 4 GiB
   const int64_t spanA = 2 * (2 * a_ps + (int64_t)(ta ? K : M) * lda);
   const int64_t spanB = 2 * (2 * b_ps + (int64_t)(tb ? N : K) * ldb);

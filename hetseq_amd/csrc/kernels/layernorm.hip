@@ -49,7 +49,8 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const T* __restrict__ a, co
                                                      float* __restrict__ zsave, float* __restrict__ mean_out,
                                                      float* __restrict__ rstd_out, int rows, float eps, float p,
                                                      uint64_t seed, uint64_t off, int mode,
-                                                     const uint64_t* __restrict__ seed_dev) {
+                                                     const uint64_t* __restrict__ seed_dev,
+                                                     uint16_t* __restrict__ yp, int64_t yps) {
   constexpr int H = NV * 256;
   const int lane = threadIdx.x & 63;
   const float scale = p < 1.f ? 1.0f / (1.0f - p) : 0.f;
@@ -92,6 +93,7 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const T* __restrict__ a, co
 #pragma unroll
       for (int j = 0; j < 4; ++j) o[j] = gw[j] * ((x[k][j] - mean) * rstd) + gb[j];
       store4(y + base + c, o);
+      if (yp) store4_planes(yp, yps, base + c, o);  // y again as the next GEMM's split-bf16 operand
     }
     if (lane == 0) {
       mean_out[row] = mean;
@@ -130,7 +132,8 @@ __global__ void __launch_bounds__(64 * kLnBwdWaves) ln_bwd_kernel(
     const T* __restrict__ dy, const float* __restrict__ zsave, const float* __restrict__ mean_in,
     const float* __restrict__ rstd_in, const float* __restrict__ gamma, T* __restrict__ dz_out, T* __restrict__ da_out,
     float* __restrict__ part_gamma, float* __restrict__ part_beta, float* __restrict__ part_bias, int rows, float p,
-    uint64_t seed, uint64_t off, int mode, const uint64_t* __restrict__ seed_dev) {
+    uint64_t seed, uint64_t off, int mode, const uint64_t* __restrict__ seed_dev, uint16_t* __restrict__ dap,
+    int64_t daps) {
   constexpr int H = NV * 256;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int lane = threadIdx.x & 63;
@@ -193,6 +196,7 @@ __global__ void __launch_bounds__(64 * kLnBwdWaves) ln_bwd_kernel(
           abias[k][j] += dzv[j];
         }
         if (da_out) store4(da_out + base + c, dzv);
+        if (dap) store4_planes(dap, daps, base + c, dzv);  // da as the dgrad / wgrad GEMMs' operand
       }
     }
 #pragma unroll
@@ -350,20 +354,21 @@ static const int kLnBwdBlocks = [] {
 template <int NV, typename T>
 void ln_fwd_launch(const void* a, const float* bias, const void* resid, const float* gamma, const float* beta, void* y,
                    float* zsave, float* mean, float* rstd, int rows, float eps, float p, uint64_t seed, uint64_t off,
-                   int mode, hipStream_t st) {
+                   int mode, uint16_t* yp, int64_t yps, hipStream_t st) {
   int grid = (rows + 3) / 4;
   if (grid > 4096) grid = 4096;
   hipLaunchKernelGGL((ln_fwd_kernel<NV, T>), dim3(grid), dim3(256), 0, st, (const T*)a, bias, (const T*)resid, gamma,
-                     beta, (T*)y, zsave, mean, rstd, rows, eps, p, seed, off, mode, g_seed_dev);
+                     beta, (T*)y, zsave, mean, rstd, rows, eps, p, seed, off, mode, g_seed_dev, yp, yps);
 }
 
 template <int NV, typename T>
 void ln_bwd_launch(const void* dy, const float* zsave, const float* mean, const float* rstd, const float* gamma,
                    void* dz, void* da, float* pg, float* pb, float* pbias, int rows, float p, uint64_t seed,
-                   uint64_t off, int mode, hipStream_t st) {
+                   uint64_t off, int mode, uint16_t* dap, int64_t daps, hipStream_t st) {
   constexpr int H = NV * 256;
   hipLaunchKernelGGL((ln_bwd_kernel<NV, T>), dim3(kLnBwdBlocks), dim3(64 * kLnBwdWaves), kLnBwdWaves * H * sizeof(float), st, (const T*)dy,
-                     zsave, mean, rstd, gamma, (T*)dz, (T*)da, pg, pb, pbias, rows, p, seed, off, mode, g_seed_dev);
+                     zsave, mean, rstd, gamma, (T*)dz, (T*)da, pg, pb, pbias, rows, p, seed, off, mode, g_seed_dev,
+                     dap, daps);
 }
 
 template <int NV, typename T>
@@ -404,26 +409,28 @@ int ln_bwd_num_blocks() { return kLnBwdBlocks; }
 
 int launch_ln_fwd(int dtype, const void* a, const float* bias, const void* resid, const float* gamma,
                   const float* beta, void* y, float* zsave, float* mean, float* rstd, int rows, int H, float eps,
-                  float p, uint64_t seed, uint64_t off, int mode, hipStream_t st) {
+                  float p, uint64_t seed, uint64_t off, int mode, void* yp, int64_t yps, hipStream_t st) {
+  if (yp && dtype != 0) return -1;  // plane output: fp32 mode only
   if (dtype == 0) {
     HS_DISPATCH_H(H, (ln_fwd_launch<NV, float>(a, bias, resid, gamma, beta, y, zsave, mean, rstd, rows, eps, p, seed,
-                                               off, mode, st)));
+                                               off, mode, (uint16_t*)yp, yps, st)));
   } else {
     HS_DISPATCH_H(H, (ln_fwd_launch<NV, bf16_t>(a, bias, resid, gamma, beta, y, zsave, mean, rstd, rows, eps, p, seed,
-                                                off, mode, st)));
+                                                off, mode, nullptr, 0, st)));
   }
   return 0;
 }
 
 int launch_ln_bwd(int dtype, const void* dy, const float* zsave, const float* mean, const float* rstd,
                   const float* gamma, void* dz, void* da, float* pg, float* pb, float* pbias, int rows, int H, float p,
-                  uint64_t seed, uint64_t off, int mode, hipStream_t st) {
+                  uint64_t seed, uint64_t off, int mode, void* dap, int64_t daps, hipStream_t st) {
+  if (dap && (dtype != 0 || mode != kBDR)) return -1;  // plane output of da: fp32, bias-dropout-residual mode
   if (dtype == 0) {
     HS_DISPATCH_H(H, (ln_bwd_launch<NV, float>(dy, zsave, mean, rstd, gamma, dz, da, pg, pb, pbias, rows, p, seed, off,
-                                               mode, st)));
+                                               mode, (uint16_t*)dap, daps, st)));
   } else {
     HS_DISPATCH_H(H, (ln_bwd_launch<NV, bf16_t>(dy, zsave, mean, rstd, gamma, dz, da, pg, pb, pbias, rows, p, seed,
-                                                off, mode, st)));
+                                                off, mode, nullptr, 0, st)));
   }
   return 0;
 }

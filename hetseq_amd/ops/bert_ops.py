@@ -61,7 +61,13 @@ def _colpart_buf(nparts, H, device, n=3):
 
 
 # --------------------------------------------------------------------- basic ops
-def ln_fwd(a, gamma, beta, eps=1e-12, bias=None, resid=None, p=0.0, mode=0, seed=0, off=0, save_z=True):
+def _planes_buf(rows, cols, device):
+    return torch.empty((3, rows, cols), dtype=torch.bfloat16, device=device)
+
+
+def ln_fwd(a, gamma, beta, eps=1e-12, bias=None, resid=None, p=0.0, mode=0, seed=0, off=0, save_z=True, planes=None):
+    """LayerNorm forward (+ bias / dropout / residual in mode 1).  ``planes``: a [3, rows, H] bf16
+    buffer that also receives y as split-bf16 planes (the fp32 GEMM engine's operand format)."""
     rows, H = a.shape
     assert H in LN_WIDTHS and a.is_contiguous() and (resid is None or resid.shape == a.shape)
     y = torch.empty_like(a)
@@ -71,16 +77,18 @@ def ln_fwd(a, gamma, beta, eps=1e-12, bias=None, resid=None, p=0.0, mode=0, seed
     hip().ln_fwd(dtype_code(a), a.data_ptr(), bias.data_ptr() if bias is not None else 0,
                  resid.data_ptr() if resid is not None else 0, gamma.data_ptr(), beta.data_ptr(), y.data_ptr(),
                  z.data_ptr() if z is not None else 0, mean.data_ptr(), rstd.data_ptr(), rows, H, float(eps), float(p),
-                 seed, off, mode, stream_handle())
+                 seed, off, mode, stream_handle(), planes.data_ptr() if planes is not None else 0,
+                 rows * H if planes is not None else 0)
     return y, z, mean, rstd
 
 
 def ln_bwd(dy, z, mean, rstd, gamma, p=0.0, mode=0, seed=0, off=0, want_dz=True, want_da=False, dz_out=None,
-           acc=None, side=False):
+           acc=None, side=False, da_planes=None):
     """LN backward.  ``acc`` = (dgamma, dbeta[, dbias]) fp32 tensors to ACCUMULATE into
     (flat-store gradient views); otherwise fresh tensors are returned.  ``side``: run the
     parameter-gradient finalisation on the weight-gradient stream (runtime/streams.py) --
-    only dz / da are on the critical path."""
+    only dz / da are on the critical path.  ``da_planes``: [3, rows, H] bf16 buffer receiving da
+    as split-bf16 planes (mode 1; with ``want_da`` False the fp32 da is not written at all)."""
     rows, H = dy.shape
     nb = hip().ln_bwd_num_blocks()
     part = _colpart_buf(nb, H, dy.device)
@@ -88,7 +96,8 @@ def ln_bwd(dy, z, mean, rstd, gamma, p=0.0, mode=0, seed=0, off=0, want_dz=True,
     da = torch.empty_like(dy) if want_da else None
     hip().ln_bwd(dtype_code(dy), dy.data_ptr(), z.data_ptr(), mean.data_ptr(), rstd.data_ptr(), gamma.data_ptr(),
                  dz.data_ptr() if dz is not None else 0, da.data_ptr() if da is not None else 0, part[0].data_ptr(),
-                 part[1].data_ptr(), part[2].data_ptr(), rows, H, float(p), seed, off, mode, stream_handle())
+                 part[1].data_ptr(), part[2].data_ptr(), rows, H, float(p), seed, off, mode, stream_handle(),
+                 da_planes.data_ptr() if da_planes is not None else 0, rows * H if da_planes is not None else 0)
     n = 3 if mode == 1 else 2
     if acc is not None:
         outs = list(acc[:n])
@@ -352,24 +361,32 @@ def _planes_of(buf):
 
 
 def _layer_forward(x, mask, W, cfg, save):
-    """GEMM operands are split once into bf16 planes when the weights are planes (fp32 mode on
-    the plane engine): each activation feeds its forward GEMM and, saved, its weight gradient."""
+    """fp32 on the plane engine (``W.planes``): every GEMM operand is split-bf16 planes, written by
+    the kernel that produces the tensor where it can -- the LN forwards (h1, h2: h2's planes wait
+    in gemm.remember_planes for the next layer), the GELU epilogue (f1, planes only) -- and by a
+    split pass for the attention output and the embedding output; saved planes feed the weight
+    gradients of the backward."""
     B, S, NH, p_h, p_a, eps, seeds = cfg
     (s_a, o_a), (s_1, o_1), (s_2, o_2) = seeds
-    sp = G.split if getattr(W, "planes", False) else (lambda t: t)
-    xin = sp(x)
+    pl = getattr(W, "planes", False)
+    rows, H = x.shape
+    xin = G.split_cached(x) if pl else x
     qkv = G.linear_fwd(xin, W.wqkv)  # bias folded into the attention kernels' Q/K/V loads
     ctx_, (lse, dmask) = attn_fwd(qkv, mask, B, S, NH, p_a, s_a, o_a, bias=W.bqkv)
-    cin = sp(ctx_)
+    cin = G.split(ctx_) if pl else ctx_
     a = G.linear_fwd(cin, W.wo)
-    h1, z1, m1, r1 = ln_fwd(a, W.g1, W.b1, eps, bias=W.bo, resid=x, p=p_h, mode=1, seed=s_1, off=o_1)
-    hin = sp(h1)
-    f1, f1pre = G.linear_gelu_fwd(hin, W.w1, W.bi)  # f1pre: un-biased pre-activation (for the backward)
-    fin = sp(f1)
+    h1p = _planes_buf(rows, H, x.device) if pl else None
+    h1, z1, m1, r1 = ln_fwd(a, W.g1, W.b1, eps, bias=W.bo, resid=x, p=p_h, mode=1, seed=s_1, off=o_1, planes=h1p)
+    hin = _planes_of(h1p) if pl else h1
+    f1, f1pre = G.linear_gelu_fwd(hin, W.w1, W.bi, planes_out=pl)  # f1pre: un-biased pre-activation
+    fin = f1
     o = G.linear_fwd(fin, W.w2)
-    h2, z2, m2, r2 = ln_fwd(o, W.g2, W.bb2, eps, bias=W.b2, resid=h1, p=p_h, mode=1, seed=s_2, off=o_2)
+    h2p = _planes_buf(rows, H, x.device) if pl else None
+    h2, z2, m2, r2 = ln_fwd(o, W.g2, W.bb2, eps, bias=W.b2, resid=h1, p=p_h, mode=1, seed=s_2, off=o_2, planes=h2p)
+    if pl:
+        G.remember_planes(h2, _planes_of(h2p))  # the next layer's QKV operand
     if save:
-        keep = (lambda t: t.buf) if getattr(W, "planes", False) else (lambda t: t)
+        keep = (lambda t: t.buf) if pl else (lambda t: t)
         return h2, (qkv, ctx_, lse, dmask, z1, m1, r1, keep(hin), f1pre, keep(fin), z2, m2, r2, keep(xin), keep(cin))
     return h2, None
 
@@ -404,7 +421,6 @@ class FusedBertLayer(torch.autograd.Function):
             saved = ctx.saved_tensors[2:]
         qkv, ctx_, lse, dmask, z1, m1, r1, h1, f1pre, f1, z2, m2, r2, xin, cin = saved
         pl = getattr(W, "planes", False)
-        sp = G.split if pl else (lambda t: t)
         if pl:  # GEMM operands saved as split planes
             h1, f1, xin, cin = (_planes_of(t) for t in (h1, f1, xin, cin))
         B, S, NH, p_h, p_a, eps, seeds = cfg
@@ -420,8 +436,10 @@ class FusedBertLayer(torch.autograd.Function):
         # stay in order
         side = acc and streams.enabled()
         dks = streams.DGRAD_KSPLIT if side else None  # K split of the dgrads beside the side stream
-        dz2, do_, dg2, dbb2, db2 = ln_bwd(dh2, z2, m2, r2, W.g2, p_h, 1, s_2, o_2, True, True,
-                                          acc=(Gv.g2, Gv.bb2, Gv.b2) if acc else None, side=side)
+        rows = dh2.shape[0]
+        dop = _planes_buf(rows, H, dh2.device) if pl else None  # the LN backwards write da as planes
+        dz2, do_, dg2, dbb2, db2 = ln_bwd(dh2, z2, m2, r2, W.g2, p_h, 1, s_2, o_2, True, not pl,
+                                          acc=(Gv.g2, Gv.bb2, Gv.b2) if acc else None, side=side, da_planes=dop)
 
         def wgrad(dy, xin_, out):
             if not side:
@@ -430,19 +448,19 @@ class FusedBertLayer(torch.autograd.Function):
             return streams.run(dy.device, lambda: G.linear_wgrad(dy, xin_, out=out, accumulate=acc,
                                                                  ksplit=ks), dy, xin_)
 
-        do_p = sp(do_)
+        do_p = _planes_of(dop) if pl else do_
         dW2 = wgrad(do_p, f1, Gv.w2 if acc else None)
-        df1pre, dbi = G.linear_dgrad_dgelu(do_p, W.w2, f1pre, W.bi, db_acc=Gv.bi if acc else None)
-        df1p = sp(df1pre)
+        df1p, dbi = G.linear_dgrad_dgelu(do_p, W.w2, f1pre, W.bi, db_acc=Gv.bi if acc else None, planes_out=pl)
         dW1 = wgrad(df1p, h1, Gv.w1 if acc else None)
         dh1 = G.linear_dgrad(df1p, W.w1, out=dz2, accumulate=True, ksplit=dks)  # dz2 + df1pre @ W1
-        dz1, da1, dg1, db1, dbo = ln_bwd(dh1, z1, m1, r1, W.g1, p_h, 1, s_1, o_1, True, True,
-                                         acc=(Gv.g1, Gv.b1, Gv.bo) if acc else None, side=side)
-        da1p = sp(da1)
+        dap = _planes_buf(rows, H, dh2.device) if pl else None
+        dz1, da1, dg1, db1, dbo = ln_bwd(dh1, z1, m1, r1, W.g1, p_h, 1, s_1, o_1, True, not pl,
+                                         acc=(Gv.g1, Gv.b1, Gv.bo) if acc else None, side=side, da_planes=dap)
+        da1p = _planes_of(dap) if pl else da1
         dWo = wgrad(da1p, cin, Gv.wo if acc else None)
         dctx = G.linear_dgrad(da1p, W.wo, ksplit=dks)
         dqkv = attn_bwd(qkv, mask, ctx_, dctx, (lse, dmask), B, S, NH, p_a, bias=W.bqkv)
-        dqkvp = sp(dqkv)
+        dqkvp = G.split(dqkv) if pl else dqkv
         dWqkv = wgrad(dqkvp, xin, Gv.wqkv if acc else None)
         if side:
             dbqkv = streams.run(dqkv.device, lambda: colsum(dqkv, acc=Gv.bqkv), dqkv)

@@ -164,6 +164,29 @@ def planes_enabled():
 _PLANES = os.environ.get("HETSEQ_GEMM_PLANES", "0") == "1"
 
 
+# Tensors whose split-bf16 planes a producer kernel already wrote (an LN forward emitting its
+# output in both formats): the consumer's split() is then free.  Keyed by the tensor object and
+# its version counter, so an in-place update invalidates the entry.
+_KNOWN_PLANES: dict = {}
+
+
+def remember_planes(t, planes):
+    import weakref
+
+    _KNOWN_PLANES[id(t)] = (weakref.ref(t), t._version, planes)
+
+
+def split_cached(x):
+    """:func:`split` unless a producer already emitted ``x``'s planes (entry consumed once)."""
+    e = _KNOWN_PLANES.pop(id(x), None)
+    if e is not None and e[0]() is x and e[1] == x._version:
+        return e[2]
+    if len(_KNOWN_PLANES) > 8:  # entries of tensors that were never consumed (the last layer's output)
+        for k in [k for k, v in _KNOWN_PLANES.items() if v[0]() is None]:
+            del _KNOWN_PLANES[k]
+    return split(x.contiguous())
+
+
 def split(x, out=None):
     """fp32 [rows, cols] (contiguous) -> P = 3 Planes (one elementwise pass: read 4 B, write 6 B)."""
     assert x.dtype == torch.float32 and x.dim() == 2 and x.is_contiguous() and x.numel() % 4 == 0
@@ -233,19 +256,24 @@ def gemm_planes(a, b, ta, tb, out, bias=None, epi=EPI_NONE, beta=0.0, aux=None, 
     split-fp32 planes when it serves the shape, else :func:`planes_variant`.  ``outp``: a [3, M, N]
     bf16 buffer that receives the result again as split planes (ring kernel, GELU / dGELU
     epilogues: the output is the next GEMM's operand)."""
-    if a.P != b.P or not out.is_cuda or out.stride(1) != 1 or out.dtype not in (torch.float32, torch.bfloat16):
-        return False
     M, N, K = _dims(a, b, ta, tb)
-    if out.shape != (M, N):
+    if out is None:  # plane output only (ring kernel, fused-activation epilogues)
+        if outp is None or a.P != 3 or variant not in (-1, RING) or _RING_OFF:
+            return False
+    elif a.P != b.P or not out.is_cuda or out.stride(1) != 1 or out.dtype not in (torch.float32, torch.bfloat16) \
+            or out.shape != (M, N):
         return False
-    if a.P == 3 and out.dtype == torch.float32 and variant in (-1, RING) and not _RING_OFF:
+    if a.P == 3 and (out is None or out.dtype == torch.float32) and variant in (-1, RING) and not _RING_OFF:
         ks = ksplit if ksplit and ksplit > 0 else 1
-        slab = _slab(M, N, ks, out.device) if ks > 1 else None
+        dev = a.device
+        slab = _slab(M, N, ks, dev) if ks > 1 else None
         if ks > 1 and slab is None:
             ks = 1
-        if outp is None or (outp.shape == (3, M, N) and out.stride(0) == N):
+        ldc = out.stride(0) if out is not None else N
+        if outp is None or (tuple(outp.shape) == (3, M, N) and ldc == N):
             rc = hip().gemm_ring(int(ta), int(tb), M, N, K, a.data_ptr(), a.ld, a.ps, b.data_ptr(), b.ld, b.ps,
-                                 out.data_ptr(), out.stride(0), bias.data_ptr() if bias is not None else 0, epi,
+                                 out.data_ptr() if out is not None else 0, ldc,
+                                 bias.data_ptr() if bias is not None else 0, epi,
                                  float(beta), aux.data_ptr() if aux is not None else 0,
                                  aux.stride(0) if aux is not None else 0, part.data_ptr() if part is not None else 0,
                                  colsum.data_ptr() if colsum is not None else 0, int(colsum_acc), int(ks),
@@ -256,7 +284,7 @@ def gemm_planes(a, b, ta, tb, out, bias=None, epi=EPI_NONE, beta=0.0, aux=None, 
                 return True
         if variant == RING:
             return False
-    if outp is not None:
+    if outp is not None or out is None:
         return False
     slab = _slab(M, N, ksplit, out.device) if ksplit > 1 else None
     if ksplit > 1 and slab is None:
@@ -606,10 +634,12 @@ def linear_wgrad(dy, x, out=None, accumulate=False, ksplit=None):
                 ksplit=ksplit)
 
 
-def linear_gelu_fwd(x, w, b):
+def linear_gelu_fwd(x, w, b, planes_out=False):
     """FFN-in forward: pre = x @ w^T (un-biased, kept for the backward), y = gelu(pre + b).
 
     Returns (y, pre).  One fused HIP GEMM (epilogue writes both) or library GEMM + bias_gelu kernel.
+    ``planes_out`` (fp32 plane engine): y is returned as split-bf16 :class:`Planes` written by the
+    epilogue (no fp32 copy).
     """
     from hetseq_amd.ops import bert_ops
 
@@ -618,9 +648,14 @@ def linear_gelu_fwd(x, w, b):
     if px is not None and pw is not None and _MODE != "blas":
         dt = torch.float32 if px.P == 3 else torch.bfloat16
         pre = torch.empty((T, N), dtype=dt, device=px.device)
+        if px.P == 3 and planes_out:
+            # y only as split planes (its one use is the next GEMM's operand): Planes, pre
+            yp = torch.empty((3, T, N), dtype=torch.bfloat16, device=px.device)
+            if gemm_planes(px, pw, False, True, None, b, EPI_GELU, 0.0, aux=pre, outp=yp):
+                return Planes(yp, T, N, N, T * N, 3), pre
         y = torch.empty_like(pre)
         if gemm_planes(px, pw, False, True, y, b, EPI_GELU, 0.0, aux=pre):
-            return y, pre
+            return (split(y) if planes_out else y), pre
         x, w = _unplane(x), _unplane(w)
     pre = torch.empty((T, N), dtype=x.dtype, device=x.device)
     y = torch.empty_like(pre)
@@ -642,10 +677,11 @@ def linear_gelu_fwd(x, w, b):
     return bert_ops.bias_gelu_fwd(pre, b, out=y), pre
 
 
-def linear_dgrad_dgelu(dy, w, pre, b, db_acc=None):
+def linear_dgrad_dgelu(dy, w, pre, b, db_acc=None, planes_out=False):
     """FFN backward through the GELU: dpre = (dy @ w) * gelu'(pre + b), db = colsum(dpre).
 
-    ``db`` is accumulated into ``db_acc`` (flat-store view) when given.  Returns (dpre, db).
+    ``db`` is accumulated into ``db_acc`` (flat-store view) when given.  Returns (dpre, db);
+    ``planes_out`` (fp32 plane engine): dpre as split-bf16 :class:`Planes` (no fp32 copy).
     """
     from hetseq_amd.ops import bert_ops
 
@@ -653,11 +689,16 @@ def linear_dgrad_dgelu(dy, w, pre, b, db_acc=None):
     db = db_acc if db_acc is not None else torch.empty(N, dtype=torch.float32, device=dy.device)
     pd, pw = _as_planes(dy), _as_planes(w)
     if pd is not None and pw is not None and _MODE != "blas":
-        dpre = torch.empty((T, N), dtype=pre.dtype, device=pre.device)
         part = torch.empty(((T + 127) // 128, N), dtype=torch.float32, device=pre.device)
+        if pd.P == 3 and planes_out:
+            dp = torch.empty((3, T, N), dtype=torch.bfloat16, device=pre.device)
+            if gemm_planes(pd, pw, False, False, None, b, EPI_DGELU, 0.0, aux=pre, part=part, colsum=db,
+                           colsum_acc=db_acc is not None, outp=dp):
+                return Planes(dp, T, N, N, T * N, 3), db
+        dpre = torch.empty((T, N), dtype=pre.dtype, device=pre.device)
         if gemm_planes(pd, pw, False, False, dpre, b, EPI_DGELU, 0.0, aux=pre, part=part, colsum=db,
                        colsum_acc=db_acc is not None):
-            return dpre, db
+            return (split(dpre) if planes_out else dpre), db
         dy, w = _unplane(dy), _unplane(w)
     dpre = torch.empty((T, N), dtype=dy.dtype, device=dy.device)
     if dy.is_cuda and _MODE != "blas" and _hip_ok(dy, w, dpre, pre, b):

@@ -46,6 +46,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--only", default=None, help="comma-separated product names (e.g. 'out fwd,qkv dgrad')")
     ap.add_argument("--engines", default="x6s,ring")
+    ap.add_argument("--ks-sweep", action="store_true", help="also time the ring with K splits 1/2/4/8 (wgrads)")
     a = ap.parse_args()
     rows = []
     only = set(x.strip() for x in a.only.split(",")) if a.only else None
@@ -68,6 +69,13 @@ def main():
         t6, tg = min(tx), min(tr)
         fl = 2.0 * M * N * K
         rows.append((name, M, N, K, ks, t6, tg, fl / t6 / 1e6, fl / tg / 1e6))
+        if a.ks_sweep and ta:
+            sweep = {}
+            for s_ in (1, 2, 4, 8):
+                f_ = lambda: G.gemm_planes(pa, pb, bool(ta), bool(tb), out, ksplit=s_, variant=G.RING)  # noqa: E731
+                if f_():
+                    sweep[s_] = round(timeit(f_, a.reps), 1)
+            print("ks sweep %s: %s" % (name, sweep), flush=True)
     print("| product | M | N | K | ring ks | x6s us | ring us | x6s fp32 TF/s | ring fp32 TF/s | ring bf16-MFMA TF/s |")
     print("|---|---|---|---|---|---|---|---|---|---|")
     for r in rows:
