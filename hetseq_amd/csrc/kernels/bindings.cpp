@@ -21,11 +21,11 @@ using i64 = int64_t;
 // optim.hip
 void launch_grad_norm(const float*, int64_t, double*, const float*, float, float*, hipStream_t);
 void launch_adam_flat(float*, const float*, float*, float*, void*, int64_t, const float*, float, float, float, float,
-                      float, float, const float*, hipStream_t);
+                      float, float, float, float, const float*, hipStream_t);
 void launch_adadelta_flat(float*, const float*, float*, float*, void*, int64_t, const float*, float, float, float,
-                          float, hipStream_t);
+                          float, float, hipStream_t);
 void launch_lamb_flat(float*, const float*, float*, float*, float*, void*, const int64_t*, int, float*, const float*,
-                      float, float, float, float, float, float, float, hipStream_t);
+                      float, float, float, float, float, float, float, float, float, hipStream_t);
 void launch_cast_f32_bf16(const float*, void*, int64_t, hipStream_t);
 // layernorm.hip
 int ln_bwd_num_blocks();
@@ -153,29 +153,31 @@ PYBIND11_MODULE(_hip, m) {
     launch_grad_norm(P(const float*, g), n, P(double*, partial), P(const float*, scale), max_norm, P(float*, out), ST(st));
     check_launch("grad_norm");
   });
-  m.def("adam_flat", [](i64 p, i64 g, i64 mm, i64 v, i64 shadow, i64 n, i64 gmul, float lr, float b1, float b2,
+  // betas / rho arrive as Python doubles: 1 - beta is formed in double and rounded once (see optim.hip)
+  m.def("adam_flat", [](i64 p, i64 g, i64 mm, i64 v, i64 shadow, i64 n, i64 gmul, float lr, double b1, double b2,
                         float eps, float wd, float step_size, i64 st, i64 hyper) {
     pre_launch("adam_flat");
     launch_adam_flat(P(float*, p), P(const float*, g), P(float*, mm), P(float*, v), P(void*, shadow), n,
-                     P(const float*, gmul), lr, b1, b2, eps, wd, step_size, P(const float*, hyper), ST(st));
+                     P(const float*, gmul), lr, (float)b1, (float)b2, (float)(1.0 - b1), (float)(1.0 - b2), eps, wd,
+                     step_size, P(const float*, hyper), ST(st));
     check_launch("adam_flat");
   }, pybind11::arg("p"), pybind11::arg("g"), pybind11::arg("m"), pybind11::arg("v"), pybind11::arg("shadow"),
      pybind11::arg("n"), pybind11::arg("gmul"), pybind11::arg("lr"), pybind11::arg("b1"), pybind11::arg("b2"),
      pybind11::arg("eps"), pybind11::arg("wd"), pybind11::arg("step_size"), pybind11::arg("st"),
      pybind11::arg("hyper") = 0);
-  m.def("adadelta_flat", [](i64 p, i64 g, i64 sq, i64 acc, i64 shadow, i64 n, i64 gmul, float lr, float rho, float eps,
-                            float wd, i64 st) {
+  m.def("adadelta_flat", [](i64 p, i64 g, i64 sq, i64 acc, i64 shadow, i64 n, i64 gmul, float lr, double rho,
+                            float eps, float wd, i64 st) {
     pre_launch("adadelta_flat");
     launch_adadelta_flat(P(float*, p), P(const float*, g), P(float*, sq), P(float*, acc), P(void*, shadow), n,
-                         P(const float*, gmul), lr, rho, eps, wd, ST(st));
+                         P(const float*, gmul), lr, (float)rho, (float)(1.0 - rho), eps, wd, ST(st));
     check_launch("adadelta_flat");
   });
   m.def("lamb_flat", [](i64 p, i64 g, i64 mm, i64 v, i64 upd, i64 shadow, i64 seg_off, int nseg, i64 seg_norms, i64 gmul,
-                        float lr, float b1, float b2, float eps, float wd, float bc1, float bc2, i64 st) {
+                        float lr, double b1, double b2, float eps, float wd, float bc1, float bc2, i64 st) {
     pre_launch("lamb_flat");
     launch_lamb_flat(P(float*, p), P(const float*, g), P(float*, mm), P(float*, v), P(float*, upd), P(void*, shadow),
-                     P(const int64_t*, seg_off), nseg, P(float*, seg_norms), P(const float*, gmul), lr, b1, b2, eps, wd,
-                     bc1, bc2, ST(st));
+                     P(const int64_t*, seg_off), nseg, P(float*, seg_norms), P(const float*, gmul), lr, (float)b1,
+                     (float)b2, (float)(1.0 - b1), (float)(1.0 - b2), eps, wd, bc1, bc2, ST(st));
     check_launch("lamb_flat");
   });
   m.def("cast_f32_bf16", [](i64 x, i64 y, i64 n, i64 st) {

@@ -299,99 +299,97 @@ __global__ void __launch_bounds__(NT, 1) gemm_ring_kernel(Args p) {
   wait_vm<0>();  // the trailing re-read DMAs land before LDS is reused or released
   barrier_lds();
 
-  // ---- epilogue: acc[i][j][r] -> row m0 + wm + 16 i + 4 (lane >> 4) + r, col n0 + wn + 16 j + (lane & 15)
-  const int lr = lane & 15, lq = lane >> 4;
-  if (p.ksplit > 1) {
-    float* sl = p.slab + (int64_t)slice * p.M * p.N;
+  // ---- epilogue.  The accumulators are staged through LDS (the ring's stages, free now) as the fp32
+  // tile T[128][BN], then finished row-contiguously: each thread owns 8 consecutive columns of a
+  // row, so every global access -- C, the pre-activation, the split-K slab, the three output planes
+  // -- is a 16-B (or 3 x 16-B) vector instead of a 4-B (2-B for planes) access per MFMA register.
+  // acc[i][j][r] is row wm + 16 i + 4 (lane >> 4) + r, column wn + 16 j + (lane & 15) of the tile.
+  constexpr int LDT = BN + 4;  // padded rows: the four 16-lane groups' rows 4 apart hit disjoint banks
+  static_assert(BM * LDT * 4 <= NS * STAGE, "epilogue tile fits the ring");
+  float* T = reinterpret_cast<float*>(smem);
+  {
+    const int lr = lane & 15, lq = lane >> 4;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          sl[(int64_t)(m0 + wm + 16 * i + 4 * lq + r) * p.N + n0 + wn + 16 * j + lr] = acc[i][j][r];
+        for (int r = 0; r < 4; ++r) T[(wm + 16 * i + 4 * lq + r) * LDT + wn + 16 * j + lr] = acc[i][j][r];
+  }
+  barrier_lds();
+  constexpr int NG = BN / 8;  // 8-column groups per row
+  typedef float f8 __attribute__((ext_vector_type(8)));
+  auto ld8 = [](const float* q) __attribute__((always_inline)) {
+    const f4 x = *reinterpret_cast<const f4*>(q), y = *reinterpret_cast<const f4*>(q + 4);
+    return f8{x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+  };
+  auto st8 = [](float* q, f8 v) __attribute__((always_inline)) {
+    *reinterpret_cast<f4*>(q) = f4{v[0], v[1], v[2], v[3]};
+    *reinterpret_cast<f4*>(q + 4) = f4{v[4], v[5], v[6], v[7]};
+  };
+  if (p.ksplit > 1) {  // plain fp32 partial slab; bias / beta / the sum in splitk_reduce_kernel
+    float* sl = p.slab + (int64_t)slice * p.M * p.N;
+    for (int u = threadIdx.x; u < BM * NG; u += NT) {
+      const int row = u / NG, c = (u % NG) * 8;
+      st8(sl + (int64_t)(m0 + row) * p.N + n0 + c, ld8(T + row * LDT + c));
+    }
     return;
   }
-  typedef __bf16 b1;
-  float csum[TN];
-#pragma unroll
-  for (int j = 0; j < TN; ++j) csum[j] = 0.f;
-  // the runtime options (beta-accumulate, plane output) are hoisted out of the element loops: a
+  // the runtime options (beta-accumulate, plane output, fp32 output) become template flags: a
   // per-element branch around a load makes hipcc wait vmcnt(0) for every element
-  auto store = [&](auto use_beta, auto use_planes, auto write_c) __attribute__((always_inline)) {
+  auto finish = [&](auto use_beta, auto use_planes, auto write_c) __attribute__((always_inline)) {
     constexpr bool UB = decltype(use_beta)::value, UP = decltype(use_planes)::value, WC = decltype(write_c)::value;
+    for (int u = threadIdx.x; u < BM * NG; u += NT) {
+      const int row = u / NG, c = (u % NG) * 8;
+      const int64_t m = m0 + row;
+      const int n = n0 + c;
+      const f8 a = ld8(T + row * LDT + c);
+      const f8 bv = EPI != kNone ? ld8(p.bias + n) : f8{};
+      f8 v;
+      if (EPI == kGelu) {
+        st8(p.aux + m * p.ldaux + n, a);  // the un-biased pre-activation, for the backward
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wn + 16 * j + lr;
-      const float bv = EPI != kNone ? p.bias[n] : 0.f;
+        for (int k = 0; k < 8; ++k) v[k] = gelu_f(a[k] + bv[k]);
+      } else if (EPI == kDGelu) {
+        const f8 pre = ld8(p.aux + m * p.ldaux + n);
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        float in[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int64_t m = m0 + wm + 16 * i + 4 * lq + r;
-          in[r] = EPI == kDGelu ? p.aux[m * p.ldaux + n] : UB ? p.C[m * p.ldc + n] : 0.f;
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int64_t m = m0 + wm + 16 * i + 4 * lq + r;
-          const float a = acc[i][j][r];
-          float v;
-          if (EPI == kGelu) {
-            p.aux[m * p.ldaux + n] = a;
-            v = gelu_f(a + bv);
-          } else if (EPI == kDGelu) {
-            v = a * gelu_grad_f(in[r] + bv);
-            csum[j] += v;
-          } else {
-            v = a + bv;
-            if (UB) v += p.beta * in[r];
-          }
-          if (WC) p.C[m * p.ldc + n] = v;
-          if (UP) {  // the value again as planes, for the GEMMs that consume it
-#pragma clang fp contract(off)  // residuals of the STORED v (no fma with the product that made it)
-            const b1 h = (b1)v;
-            const float r1 = v - (float)h;
-            const b1 md = (b1)r1;
-            const b1 lo = (b1)(r1 - (float)md);
-            b1* o = reinterpret_cast<b1*>(p.outp) + m * p.ldc + n;
-            o[0] = h;
-            o[p.o_ps] = md;
-            o[2 * p.o_ps] = lo;
-          }
-        }
+        for (int k = 0; k < 8; ++k) v[k] = a[k] * gelu_grad_f(pre[k] + bv[k]);
+        st8(T + row * LDT + c, v);  // kept for the bias-gradient column sums below
+      } else {
+        v = a + bv;
+        if (UB) v += p.beta * ld8(p.C + m * p.ldc + n);
+      }
+      if (WC) st8(p.C + m * p.ldc + n, v);
+      if (UP) {  // the value again as planes, for the GEMMs that consume it
+        const float lo4[4] = {v[0], v[1], v[2], v[3]}, hi4[4] = {v[4], v[5], v[6], v[7]};
+        store4_planes(p.outp, p.o_ps, m * p.ldc + n, lo4);
+        store4_planes(p.outp, p.o_ps, m * p.ldc + n + 4, hi4);
       }
     }
   };
   using T_ = std::true_type;
   using F_ = std::false_type;
   if (EPI >= kGelu) {  // fused-activation outputs: planes only when the fp32 copy has no reader (C null)
-    if (p.outp && p.C) store(F_{}, T_{}, T_{});
-    else if (p.outp) store(F_{}, T_{}, F_{});
-    else store(F_{}, F_{}, T_{});
+    if (p.outp && p.C) finish(F_{}, T_{}, T_{});
+    else if (p.outp) finish(F_{}, T_{}, F_{});
+    else finish(F_{}, F_{}, T_{});
   } else if (p.beta != 0.f) {
-    store(T_{}, F_{}, T_{});
+    finish(T_{}, F_{}, T_{});
   } else {
-    store(F_{}, F_{}, T_{});
+    finish(F_{}, F_{}, T_{});
   }
-  if (EPI == kDGelu) {  // column sums over the block's 128 rows: the 4 lane groups, then the 2 wave rows
-    float* red = reinterpret_cast<float*>(smem);
-    barrier_lds();  // every wave is past its last LDS read
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      csum[j] += __shfl_xor(csum[j], 16, 64);
-      csum[j] += __shfl_xor(csum[j], 32, 64);
-    }
-    if (wr == 1 && lq == 0)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) red[wn + 16 * j + lr] = csum[j];
+  if (EPI == kDGelu) {  // column sums of the block's 128 rows, fixed order (deterministic)
     barrier_lds();
-    if (wr == 0 && lq == 0)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int c = wn + 16 * j + lr;
-        p.part[(int64_t)tm * p.N + n0 + c] = csum[j] + red[c];
+    for (int c = threadIdx.x; c < BN; c += NT) {
+      float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+      for (int row = 0; row < BM; row += 4) {
+        s0 += T[row * LDT + c];
+        s1 += T[(row + 1) * LDT + c];
+        s2 += T[(row + 2) * LDT + c];
+        s3 += T[(row + 3) * LDT + c];
       }
+      p.part[(int64_t)tm * p.N + n0 + c] = (s0 + s1) + (s2 + s3);
+    }
   }
 }
 
@@ -454,6 +452,10 @@ int launch_gemm_ring(int ta, int tb, int M, int N, int K, const void* A, int64_t
     return -1;
   if (outp && (epi < 2 || o_ps <= 0)) return -1;  // plane outputs: the GELU / dGELU epilogues only
   if (!C && !outp) return -1;
+  // the row-contiguous epilogue moves 8 columns per thread as 16-B vectors (planes: 8-B pieces)
+  if ((C && (!al16(C) || ldc % 4)) || (aux && (!al16(aux) || ldaux % 4)) || (bias && !al16(bias)) ||
+      (outp && ((reinterpret_cast<uintptr_t>(outp) & 7) || o_ps % 4 || ldc % 4)) || (slab && !al16(slab)))
+    return -1;
   // 32-bit per-lane DMA offsets: the operand span (all planes) must stay below 4 GiB
   const int64_t spanA = 2 * (2 * a_ps + (int64_t)(ta ? K : M) * lda);
   const int64_t spanB = 2 * (2 * b_ps + (int64_t)(tb ? N : K) * ldb);

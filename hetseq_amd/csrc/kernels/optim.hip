@@ -112,14 +112,14 @@ __global__ void __launch_bounds__(256) adam_flat_kernel(float* __restrict__ p, c
                                                         float* __restrict__ m, float* __restrict__ v,
                                                         bf16_t* __restrict__ shadow, int64_t n,
                                                         const float* __restrict__ gmul, float lr, float b1,
-                                                        float b2, float eps, float wd, float step_size,
-                                                        const float* __restrict__ hyper) {
+                                                        float b2, float omb1, float omb2, float eps, float wd,
+                                                        float step_size, const float* __restrict__ hyper) {
   const float mul = gmul ? gmul[0] : 1.0f;
   if (hyper) {  // HIP-graph mode: per-update lr and bias-corrected step size from device memory
     lr = hyper[0];
     step_size = hyper[1];
   }
-  const float omb1 = 1.0f - b1, omb2 = 1.0f - b2, decay = -wd * lr;
+  const float decay = -wd * lr;
   const int64_t n4 = n >> 2;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -171,17 +171,17 @@ __global__ void __launch_bounds__(256) adadelta_flat_kernel(float* __restrict__ 
                                                             float* __restrict__ sq, float* __restrict__ acc,
                                                             bf16_t* __restrict__ shadow, int64_t n,
                                                             const float* __restrict__ gmul, float lr, float rho,
-                                                            float eps, float wd) {
+                                                            float omr, float eps, float wd) {
   const float mul = gmul ? gmul[0] : 1.0f;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     float gk = g[i] * mul;
     float pk = p[i];
     if (wd != 0.f) gk = gk + wd * pk;
-    const float s = sq[i] * rho + (1.f - rho) * gk * gk;
+    const float s = sq[i] * rho + omr * gk * gk;
     const float stdv = sqrtf(s + eps);
     const float delta = sqrtf(acc[i] + eps) / stdv * gk;
     pk = pk - lr * delta;
-    acc[i] = acc[i] * rho + (1.f - rho) * delta * delta;
+    acc[i] = acc[i] * rho + omr * delta * delta;
     sq[i] = s;
     p[i] = pk;
     if (kShadow) shadow[i] = from_f<bf16_t>(pk);
@@ -197,15 +197,16 @@ __global__ void __launch_bounds__(256) lamb_stage1_kernel(const float* __restric
                                                           float* __restrict__ upd, const int64_t* __restrict__ seg_off,
                                                           int nseg, float* __restrict__ seg_norms,
                                                           const float* __restrict__ gmul, float b1, float b2,
-                                                          float eps, float wd, float bc1, float bc2) {
+                                                          float omb1, float omb2, float eps, float wd, float bc1,
+                                                          float bc2) {
   const int s = blockIdx.y;
   const int64_t beg = seg_off[s], end = seg_off[s + 1];
   const float mul = gmul ? gmul[0] : 1.0f;
   float pn = 0.f, un = 0.f;
   for (int64_t i = beg + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < end; i += (int64_t)gridDim.x * blockDim.x) {
     const float gk = g[i] * mul;
-    const float mk = m[i] * b1 + (1.f - b1) * gk;
-    const float vk = v[i] * b2 + (1.f - b2) * gk * gk;
+    const float mk = m[i] * b1 + omb1 * gk;
+    const float vk = v[i] * b2 + omb2 * gk * gk;
     m[i] = mk;
     v[i] = vk;
     const float u = (mk / bc1) / (sqrtf(vk / bc2) + eps) + wd * p[i];
@@ -259,35 +260,38 @@ void launch_grad_norm(const float* g, int64_t n, double* partial, const float* s
   hipLaunchKernelGGL(norm_finalize_kernel, dim3(1), dim3(1024), 0, st, partial, kRedBlocks, scale, max_norm, out);
 }
 
+// omb1 = 1 - b1, omb2 = 1 - b2 (and omr = 1 - rho below) come from the host, computed in double from
+// the Python hyper-parameters and rounded once: 1.0f - 0.999f is 0.00100004673, 4.7e-5 off the
+// reference's (1 - beta2) = 0.001 (optim.py:205-206 multiplies by the Python double).
 void launch_adam_flat(float* p, const float* g, float* m, float* v, void* shadow, int64_t n, const float* gmul,
-                      float lr, float b1, float b2, float eps, float wd, float step_size, const float* hyper,
-                      hipStream_t st) {
+                      float lr, float b1, float b2, float omb1, float omb2, float eps, float wd, float step_size,
+                      const float* hyper, hipStream_t st) {
   const int grid = grid_for(n / 4 + 1, 256, 8192);
   if (shadow)
     hipLaunchKernelGGL(adam_flat_kernel<true>, dim3(grid), dim3(256), 0, st, p, g, m, v,
-                       reinterpret_cast<bf16_t*>(shadow), n, gmul, lr, b1, b2, eps, wd, step_size, hyper);
+                       reinterpret_cast<bf16_t*>(shadow), n, gmul, lr, b1, b2, omb1, omb2, eps, wd, step_size, hyper);
   else
     hipLaunchKernelGGL(adam_flat_kernel<false>, dim3(grid), dim3(256), 0, st, p, g, m, v, nullptr, n, gmul, lr, b1,
-                       b2, eps, wd, step_size, hyper);
+                       b2, omb1, omb2, eps, wd, step_size, hyper);
 }
 
 void launch_adadelta_flat(float* p, const float* g, float* sq, float* acc, void* shadow, int64_t n,
-                          const float* gmul, float lr, float rho, float eps, float wd, hipStream_t st) {
+                          const float* gmul, float lr, float rho, float omr, float eps, float wd, hipStream_t st) {
   const int grid = grid_for(n, 256, 8192);
   if (shadow)
     hipLaunchKernelGGL(adadelta_flat_kernel<true>, dim3(grid), dim3(256), 0, st, p, g, sq, acc,
-                       reinterpret_cast<bf16_t*>(shadow), n, gmul, lr, rho, eps, wd);
+                       reinterpret_cast<bf16_t*>(shadow), n, gmul, lr, rho, omr, eps, wd);
   else
     hipLaunchKernelGGL(adadelta_flat_kernel<false>, dim3(grid), dim3(256), 0, st, p, g, sq, acc, nullptr, n, gmul,
-                       lr, rho, eps, wd);
+                       lr, rho, omr, eps, wd);
 }
 
 void launch_lamb_flat(float* p, const float* g, float* m, float* v, float* upd, void* shadow, const int64_t* seg_off,
-                      int nseg, float* seg_norms, const float* gmul, float lr, float b1, float b2, float eps, float wd,
-                      float bc1, float bc2, hipStream_t st) {
+                      int nseg, float* seg_norms, const float* gmul, float lr, float b1, float b2, float omb1,
+                      float omb2, float eps, float wd, float bc1, float bc2, hipStream_t st) {
   hipMemsetAsync(seg_norms, 0, sizeof(float) * 2 * nseg, st);
   hipLaunchKernelGGL(lamb_stage1_kernel, dim3(32, nseg), dim3(256), 0, st, p, g, m, v, upd, seg_off, nseg, seg_norms,
-                     gmul, b1, b2, eps, wd, bc1, bc2);
+                     gmul, b1, b2, omb1, omb2, eps, wd, bc1, bc2);
   if (shadow)
     hipLaunchKernelGGL(lamb_stage2_kernel<true>, dim3(32, nseg), dim3(256), 0, st, p, upd,
                        reinterpret_cast<bf16_t*>(shadow), seg_off, seg_norms, lr);

@@ -168,11 +168,15 @@ def test_fp32_plane_engine_matches_reference(cuda, monkeypatch):
 
 
 def _grad_report(model, ref):
-    """Worst per-parameter gradient difference relative to the oracle's largest entry."""
+    """Worst per-parameter gradient difference relative to the oracle's largest entry of that
+    parameter -- floored at 1e-3 of the model's largest gradient entry: the key biases' gradient
+    is exactly zero in exact arithmetic (a per-query constant shift of the scores cancels in the
+    softmax), so both paths hold rounding noise there and a ratio of noises means nothing."""
+    gmax = max(p.grad.abs().max().item() for p in ref.parameters())
     worst, where = 0.0, None
     for (n, p1), (_, p2) in zip(model.named_parameters(), ref.named_parameters()):
         d = (p1.grad.double() - p2.grad.double()).abs().max().item()
-        r = d / (p2.grad.abs().max().item() + 1e-30)
+        r = d / max(p2.grad.abs().max().item(), 1e-3 * gmax)
         if r > worst:
             worst, where = r, n
     return worst, where
@@ -273,8 +277,11 @@ def test_lamb_hip_step_matches_cpu_math(cuda):
     net2 = copy.deepcopy(net)
     s1, s2 = FlatParamStore(net), FlatParamStore(net2)
     o1, o2 = _Lamb(args, list(net.parameters()), s1), _Lamb(args, list(net2.parameters()), s2)
+    covered = torch.zeros(s1.numel, dtype=torch.bool, device=cuda)  # parameter elements (not alignment gaps)
+    for q in net.parameters():
+        covered[s1.offset(q):s1.offset(q) + q.numel()] = True
     for step in range(5):
-        g = torch.randn_like(s1.grad) * (0.1 + step)
+        g = torch.randn_like(s1.grad) * (0.1 + step) * covered
         s1.grad.copy_(g)
         s2.grad.copy_(g)
         o1.step_count += 1
@@ -285,4 +292,5 @@ def test_lamb_hip_step_matches_cpu_math(cuda):
         torch.cuda.synchronize()
         for a, b, what in ((s1.param, s2.param, "param"), (o1._state["exp_avg"], o2._state["exp_avg"], "m"),
                            (o1._state["exp_avg_sq"], o2._state["exp_avg_sq"], "v")):
-            torch.testing.assert_close(a, b, rtol=2e-6, atol=1e-7, msg=lambda m: "%s step %d: %s" % (what, step, m))
+            torch.testing.assert_close(a[covered], b[covered], rtol=2e-6, atol=1e-7,
+                                       msg=lambda m: "%s step %d: %s" % (what, step, m))
