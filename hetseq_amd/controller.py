@@ -110,13 +110,22 @@ class Controller(object):
                 self._wrapped_model = FlatDDP(self._model, self.store, bucket_cap_mb=self.args.bucket_cap_mb,
                                               find_unused_parameters=self.args.find_unused_parameters,
                                               comm_engine=getattr(self.args, "comm_engine", "auto"),
-                                              timeout_s=getattr(self.args, "collective_timeout", 1800.0))
+                                              timeout_s=getattr(self.args, "collective_timeout", 1800.0),
+                                              sparse_embedding=self._sparse_embedding())
             else:
                 self._wrapped_model = self._model
                 if self.args.distributed_world_size > 1 and dist.is_initialized() and self.args.use_bmuf:
                     self._bmuf = BMUF(self.store, block_momentum=self.args.bmuf_block_momentum,
                                       sync_interval=self.args.bmuf_sync_interval)
         return self._wrapped_model
+
+    def _sparse_embedding(self):
+        """Embedding tables the data-parallel engine exchanges sparsely (parallel/tied.py), when the
+        model declares them and the fused BERT path (the only one handing rows over) is on."""
+        fn = getattr(self._model, "sparse_embedding", None)
+        if fn is None or getattr(self.args, "sparse_embedding_exchange", True) is False:
+            return None
+        return fn()
 
     @property
     def optimizer(self):

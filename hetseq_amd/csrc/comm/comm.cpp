@@ -168,6 +168,26 @@ class Comm {
     track(stream_);
   }
 
+  // All-gather of `count` elements per rank into `recv` on the comm stream, ordered after the
+  // work enqueued so far on every producer stream (the tied-embedding key / row exchange).
+  void all_gather_async(uintptr_t send, uintptr_t recv, int64_t count, int dtype, std::vector<uintptr_t> producers) {
+    check();
+    for (uintptr_t s : producers) {
+      hipEvent_t e = take_event();
+      hip_check(hipEventRecord(e, as_stream(s)), "hipEventRecord(producer)");
+      hip_check(hipStreamWaitEvent(stream_, e, 0), "hipStreamWaitEvent(comm)");
+      give_event(e);
+    }
+    {
+      std::lock_guard<std::mutex> g(op_mu_);
+      check();
+      nccl_check(ncclAllGather(reinterpret_cast<void*>(send), reinterpret_cast<void*>(recv), (size_t)count,
+                               nccl_type(dtype), comm_, stream_),
+                 "ncclAllGather");
+    }
+    track(stream_);
+  }
+
   // Test hook (single-GPU ordering check): while set, all_reduce_async copies each bucket of
   // [src, src + bytes) into the same offset of `dst` on the comm stream instead of reducing it.
   void set_snapshot(uintptr_t dst, uintptr_t src, int64_t bytes) {
@@ -366,6 +386,8 @@ PYBIND11_MODULE(_comm, m) {
            py::arg("device"), py::arg("timeout_s"))
       .def("all_reduce_async", &Comm::all_reduce_async, py::arg("ptr"), py::arg("count"), py::arg("dtype"),
            py::arg("op"), py::arg("producers"))
+      .def("all_gather_async", &Comm::all_gather_async, py::arg("send"), py::arg("recv"), py::arg("count"),
+           py::arg("dtype"), py::arg("producers"))
       .def("wait", &Comm::wait, py::arg("consumer"))
       .def("all_reduce", &Comm::all_reduce, py::arg("ptr"), py::arg("count"), py::arg("dtype"), py::arg("op"),
            py::arg("stream"))

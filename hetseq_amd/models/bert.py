@@ -751,6 +751,15 @@ class BertForPreTraining(BertPreTrainedModel):
             return store.shadow_view(wt), store.shadow_view(wd)
         return wt.detach().bfloat16(), wd.detach().bfloat16()
 
+    def sparse_embedding(self):
+        """(tables, rest) for the data-parallel engine's sparse table exchange (parallel/tied.py):
+        the word / position / token-type tables, whose gradient rows the fused embedding backward
+        hands over (the word table also takes the tied decoder's dense gradient, signalled by the
+        fused loss), and the rest of the embedding module (its LayerNorm)."""
+        e = self.bert.embeddings
+        return ([e.word_embeddings.weight, e.position_embeddings.weight, e.token_type_embeddings.weight],
+                [e.LayerNorm.weight, e.LayerNorm.bias])
+
     def _fused_loss(self, input_ids, token_type_ids, attention_mask, labels, nsp_label, checkpoint_activations):
         from hetseq_amd.ops.bert_ops import FusedPreTrainingLoss
 

@@ -25,6 +25,7 @@ import torch
 
 from hetseq_amd.ops import gemm as G
 from hetseq_amd.ops._C import dtype_code, hip, stream_handle
+from hetseq_amd.parallel import tied
 from hetseq_amd.runtime import rng, streams
 
 LN_WIDTHS = (256, 512, 768, 1024, 1536, 2048)
@@ -253,11 +254,17 @@ def bias_gelu(x, b):
 
 
 # --------------------------------------------------------------------- embeddings
-def segsum_rows(src, order, keys, dst):
-    """dst[keys[j]] += src[order[j]] for sorted ``keys`` (deterministic run-wise sums; fp32 src/dst)."""
-    n, H = src.shape
+def segsum_rows(src, order, keys, dst, scratch=None):
+    """dst[keys[j]] += src[order[j]] for sorted ``keys`` (deterministic run-wise sums; fp32 src/dst).
+    Keys outside [0, dst rows) are skipped; there may be more keys than source rows (one row summed
+    into several tables of a concatenated region).  ``scratch``: >= [keys, H] fp32 (run pieces)."""
+    H = src.shape[1]
+    n = keys.numel()
     assert src.dtype == torch.float32 and dst.dtype == torch.float32 and dst.is_contiguous() and src.is_contiguous()
-    scratch = torch.empty_like(src)
+    assert order.numel() == n and dst.shape[1] == H
+    if scratch is None:
+        scratch = torch.empty((n, H), dtype=torch.float32, device=src.device)
+    assert scratch.numel() >= n * H and scratch.dtype == torch.float32
     hip().segsum_rows(src.data_ptr(), order.data_ptr(), keys.data_ptr(), scratch.data_ptr(), dst.data_ptr(), n, H,
                       dst.shape[0], stream_handle())
     return dst
@@ -301,6 +308,12 @@ class FusedEmbedding(torch.autograd.Function):
         ctx.save_for_backward(ids, tt if tt is not None else ids.new_zeros(0), z, mean, rstd, gamma)
         ctx.cfg = (B, S, V, H, TV, wpos.shape[0], p, seed, off, tt is not None)
         ctx.sink = sink
+        # data-parallel sparse exchange of the tables' rows (parallel/tied.py): keys gathered now
+        ctx.tables = None
+        if sink is not None and tied._HANDLERS:
+            h = tied.lookup(sink["views"]()[0])
+            if h is not None and h.begin(ids, tt, bool(ctx.needs_input_grad[2])):
+                ctx.tables = h
         return y
 
     @staticmethod
@@ -310,9 +323,11 @@ class FusedEmbedding(torch.autograd.Function):
         dy = dy.contiguous()
         dev = dy.device
         sink = ctx.sink
+        tables = ctx.tables  # rows exchanged by the data-parallel engine: no local table updates
         if sink is not None:  # accumulate straight into the flat gradient buffer
             dword, dpos, dtype_, dg, db = sink["views"]()
-            streams.wait(dev)  # the tied decoder's weight gradient (side stream) also lands in dword
+            if tables is None:
+                streams.wait(dev)  # the tied decoder's weight gradient (side stream) also lands in dword
         else:
             dword = torch.zeros((V, H), dtype=torch.float32, device=dev)
             dpos = torch.zeros((P, H), dtype=torch.float32, device=dev)
@@ -322,16 +337,20 @@ class FusedEmbedding(torch.autograd.Function):
         nb = hip().ln_bwd_num_blocks()
         part = _colpart_buf(nb, H, dev, 2)
         rows = B * S
-        dx = torch.empty((rows, H), dtype=torch.float32, device=dev)
+        dx = tables.row_buffer(rows, H) if tables is not None else torch.empty((rows, H), dtype=torch.float32,
+                                                                                device=dev)
         small_tv = TV <= 2  # token types reduced in-kernel (per-block partials); otherwise by sorted runs
-        ptype = _colpart_buf(nb, H, dev, 2) if small_tv else None
+        ptype = _colpart_buf(nb, H, dev, 2) if (small_tv and tables is None) else None
         hip().emb_bwd(dtype_code(dy), dy.data_ptr(), z.data_ptr(), mean.data_ptr(), rstd.data_ptr(), gamma.data_ptr(),
                       dx.data_ptr(), part[0].data_ptr(), part[1].data_ptr(),
-                      tt.data_ptr() if (has_tt and small_tv) else 0, ptype.data_ptr() if small_tv else 0, rows, H,
-                      float(p), seed, off, stream_handle())
+                      tt.data_ptr() if (has_tt and ptype is not None) else 0,
+                      ptype.data_ptr() if ptype is not None else 0, rows, H, float(p), seed, off, stream_handle())
         acc = 1 if sink is not None else 0
         hip().colpart_finalize([part[0].data_ptr(), part[1].data_ptr()], [dg.data_ptr(), db.data_ptr()], nb, H, acc,
                                stream_handle())
+        if tables is not None:
+            tables.rows_ready()  # word / position / type rows: gathered and summed after the exchange
+            return (None,) * 11
         if small_tv:
             tv = [ptype[0].data_ptr()] + ([ptype[1].data_ptr()] if TV == 2 else [])
             hip().colpart_finalize(tv, [dtype_[i].data_ptr() for i in range(len(tv))], nb, H, 1, stream_handle())
@@ -627,6 +646,10 @@ class FusedPreTrainingLoss(torch.autograd.Function):
         else:
             dWdec = dwdec()
             dbdec = dbias()
+        if acc:  # the tied table's dense part is complete: the data-parallel engine reduces it now
+            h = tied.lookup(Gv[4])
+            if h is not None:
+                h.dense_ready(dl_c.device)
         dt2 = G.decoder_dgrad(lbuf, Wd, V) if lbuf is not None else G.gemm(dl_c, Wd)
         dt1, _, dg, db, _ = ln_bwd(dt2, z, mean, rstd, g, 0.0, 0, acc=(Gv[2], Gv[3]) if acc else None, side=side)
         dt1pre, dbt = gelu_bwd_colsum(dt1, t1pre, bt, db_acc=Gv[1] if acc else None)

@@ -17,6 +17,8 @@ change a reference default):
   --check-consistency N     all-reduce a parameter checksum every N updates
   --collective-timeout S    timeout (seconds) for process-group collectives (and the RCCL watchdog)
   --comm-engine E           gradient collectives: native RCCL engine (auto on GPU+nccl) or c10d
+  --no-sparse-embedding-exchange  all-reduce the embedding tables densely in the last bucket
+                            (default: early dense bucket + sparse row exchange, parallel/tied.py)
   --checkpoint-activations  recompute encoder layers in backward
   --json-log PATH           append one JSON object per logged update
   --profile                 roctx ranges + per-phase hipEvent timing
@@ -217,6 +219,9 @@ def add_mi355x_args(parser):
                        help="gradient / stats collectives: the native RCCL engine (greatest-priority comm "
                             "stream, event-gated buckets, watchdog; auto = on GPUs with the nccl backend) or "
                             "torch.distributed (c10d)")
+    group.add_argument("--no-sparse-embedding-exchange", dest="sparse_embedding_exchange", action="store_false",
+                       help="all-reduce the embedding tables densely in the last bucket instead of the early "
+                            "dense bucket (tied decoder part) + all-gather of the per-token rows")
     group.add_argument("--checkpoint-activations", action="store_true",
                        help="recompute encoder layers during backward to save activation memory")
     group.add_argument("--json-log", type=str, default=None, metavar="PATH",

@@ -71,6 +71,15 @@ class NativeComm(object):
         hs = [_stream(s) for s in producers] or [_stream()]
         self._c.all_reduce_async(t.data_ptr(), t.numel(), DTYPES[t.dtype], OPS[op], hs)
 
+    def all_gather_async(self, out, t, producers=()):
+        """``out`` = concatenation over ranks of ``t``, on the comm stream after the work enqueued
+        so far on every stream in ``producers`` (default: the current stream)."""
+        assert out.is_contiguous() and t.is_contiguous() and out.numel() == self.size * t.numel()
+        assert out.dtype == t.dtype
+        hs = [_stream(s) for s in producers] or [_stream()]
+        self._c.all_gather_async(t.data_ptr(), out.data_ptr(), t.numel(), DTYPES[t.dtype], hs)
+        return out
+
     def set_snapshot(self, dst, src):
         """Test mode: every all_reduce_async of a slice of ``src`` copies it into the same offsets
         of ``dst`` on the comm stream instead (ordering check on one GPU); ``dst=None`` ends it."""

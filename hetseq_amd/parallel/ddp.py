@@ -42,12 +42,13 @@ import torch
 import torch.distributed as dist
 
 from hetseq_amd.parallel import comm as native_comm
+from hetseq_amd.parallel.tied import SparseTableSync
 from hetseq_amd.runtime import profiling, streams
 
 
 class FlatDDP(torch.nn.Module):
     def __init__(self, module, store, process_group=None, bucket_cap_mb=25, find_unused_parameters=False,
-                 broadcast=True, comm_engine="auto", timeout_s=1800.0):
+                 broadcast=True, comm_engine="auto", timeout_s=1800.0, sparse_embedding=None, sparse_capacity=None):
         super().__init__()
         self.module = module
         self.store = store
@@ -61,10 +62,23 @@ class FlatDDP(torch.nn.Module):
         self.require_sync = True
         cap = max(1, int(bucket_cap_mb * 1024 * 1024 / 4))
         params = list(store.params)
-        order = sorted(params, key=lambda p: store.offset(p), reverse=True)
+        # embedding tables exchanged sparsely (parallel/tied.py): out of the buckets; the rest of
+        # their module (LayerNorm) is a bucket of its own so that nothing else waits for the
+        # embedding backward
+        self.tables = None
+        own = set()
+        if sparse_embedding is not None and SparseTableSync.supported(store, list(sparse_embedding[0])):
+            tables, rest = sparse_embedding
+            self.tables = SparseTableSync(self, list(tables), sparse_capacity)
+            own = {id(p) for p in rest}
+        skip = {id(p) for p in self.tables.tables} if self.tables is not None else set()
+        order = sorted((p for p in params if id(p) not in skip), key=lambda p: store.offset(p), reverse=True)
         self.buckets = []  # (lo, hi, [params])
         cur, size = [], 0
         for p in order:
+            if id(p) in own and cur and not any(id(q) in own for q in cur):
+                self.buckets.append(cur)
+                cur, size = [], 0
             cur.append(p)
             size += p.numel()
             if size >= cap:
@@ -103,11 +117,27 @@ class FlatDDP(torch.nn.Module):
         self.next_launch = 0
         self.works = []
         self.callback_queued = False
+        # collectives of this step: (what, bytes per rank, issued after the last backward kernel)
+        self.comm_log = []
+        self._in_tail = False
+
+    def _log(self, what, t):
+        self.comm_log.append((what, t.numel() * t.element_size(), self._in_tail))
+
+    def _tail_started(self):
+        """Called once the last backward Function enqueued its kernels (the embedding backward)."""
+        self._in_tail = True
+
+    def tail_bytes(self):
+        """Bytes per rank of the collectives issued after the last backward kernel (this step)."""
+        return sum(b for _, b, tail in self.comm_log if tail)
 
     # ------------------------------------------------------------- forward
     def forward(self, *inputs, **kwargs):
         if self.require_sync:
             self._reset_state()
+            if self.tables is not None:
+                self.tables.reset()
         return self.module(*inputs, **kwargs)
 
     @contextlib.contextmanager
@@ -126,7 +156,9 @@ class FlatDDP(torch.nn.Module):
         if not self.callback_queued:
             self.callback_queued = True
             torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
-        b = self.bucket_of[id(p)]
+        b = self.bucket_of.get(id(p))
+        if b is None:  # a sparsely exchanged table (parallel/tied.py)
+            return
         self.pending[b] -= 1
         if self.pending[b] == 0:
             self.ready[b] = True
@@ -139,8 +171,14 @@ class FlatDDP(torch.nn.Module):
 
     def _launch(self, b):
         lo, hi = self.ranges[b]
-        profiling.range_push("allreduce_bucket%d" % b)
+        if b == len(self.buckets) - 1 and (self.tables is None or not self.tables.armed):
+            self._tail_started()  # the last bucket waited for the embedding backward (dense tables)
+        self._launch_range(lo, hi, "allreduce_bucket%d" % b)
+
+    def _launch_range(self, lo, hi, name):
+        profiling.range_push(name)
         g = self.store.grad
+        self._log(name, g[lo:hi])
         side = streams.active(g.device) if g.is_cuda else None
         if self.comm is not None:
             # the comm stream waits for both producers; neither producer stream is stalled
@@ -171,6 +209,8 @@ class FlatDDP(torch.nn.Module):
             for i in missing:
                 self.ready[i] = True
             self._launch_ready()
+        if self.tables is not None:
+            self.tables.launch_pending()
         if self.store.grad.is_cuda:
             streams.join()  # compute stream after the wgrad stream (and the collectives issued on it)
         if self.comm is not None:
@@ -179,6 +219,8 @@ class FlatDDP(torch.nn.Module):
         for w in self.works:
             w.wait()
         self.works = []
+        if self.tables is not None:
+            self.tables.scatter()  # gathered embedding rows into the reduced tables
 
     def all_reduce_(self, t):
         """In-place SUM of a small device tensor across the data-parallel group (fast stats)."""

@@ -1,0 +1,258 @@
+"""Sparse exchange of the embedding tables' gradient for the data-parallel engine.
+
+BERT's word-embedding table (V x H: 23.4 M floats for BERT-base) receives two gradient
+contributions per step (reference: bert_modeling.py ties the MLM decoder to it, and torch DDP
+all-reduces it as one dense tensor in the LAST bucket, controller.py:74-89):
+
+* the tied MLM decoder's dense weight gradient -- produced FIRST in backward (the MLM head is the
+  first Function autograd runs), by one GEMM on the weight-gradient stream;
+* the embedding layer's per-token rows -- produced LAST (the embedding is the last Function):
+  B*S rows of H, plus the same rows summed by position and by token type.
+
+In an ordinary bucket the table's 94 MB all-reduce can only start after the embedding backward,
+a tail no backward compute overlaps.  ``SparseTableSync`` splits it:
+
+1. forward: every rank builds the keys of its tokens into the concatenated [word | position |
+   type] table region (int64 [3, cap]; padding keys point past the region) and all-gathers them
+   on the comm stream -- they are known long before backward;
+2. MLM-head backward, right after the decoder weight GEMM is enqueued
+   (``FusedPreTrainingLoss.backward`` -> ``dense_ready``): the whole region is all-reduced as its
+   own early bucket, ordered after the GEMM by producer events, overlapping the encoder's
+   backward; the gathered keys are sorted (stable) on the weight-gradient stream;
+3. embedding backward (``FusedEmbedding.backward`` -> ``row_buffer`` / ``rows_ready``): the
+   per-token rows are not scattered locally -- they land in a persistent [cap, H] buffer that is
+   all-gathered: cap*H*4 bytes per rank, the only exchange issued after the last backward kernel
+   besides the embedding LayerNorm's 2*H parameters;
+4. end of backward (``scatter``): after the comm stream, every rank adds the W*cap gathered rows
+   into the reduced region with the deterministic sorted-run kernel (``segsum_rows``) -- the
+   same inputs in the same order on every rank, so the replicas stay bit-identical.
+
+The result is the dense path's sum (decoder + all ranks' rows) up to fp32 summation order.
+``cap`` (tokens per rank per micro-batch) is agreed once, as the maximum over ranks of the first
+synchronised micro-batch, unless given; a later, larger micro-batch raises.  ``no_sync`` micro
+batches, non-fused models and inference take the dense path: the region is then reduced at the
+end of backward like an ordinary bucket.
+"""
+from __future__ import annotations
+
+import weakref
+
+import torch
+import torch.distributed as dist
+
+from hetseq_amd.runtime import profiling, streams
+
+# data_ptr of the first table's flat-gradient view -> weak reference to its SparseTableSync (a
+# live handler keeps its store alive, so the address cannot be reused while the entry resolves)
+_HANDLERS: dict = {}
+
+
+def lookup(grad_view):
+    """The sync handler owning the table whose flat-gradient view is ``grad_view`` (or None)."""
+    if not _HANDLERS or grad_view is None:
+        return None
+    ref = _HANDLERS.get(grad_view.data_ptr())
+    return ref() if ref is not None else None
+
+
+class SparseTableSync(object):
+    @staticmethod
+    def supported(store, tables):
+        """The tables (word, position, token type) are [rows, H] and adjacent in the flat buffer:
+        one region, one collective, one key space."""
+        H = tables[0].shape[1]
+        end = store.offset(tables[0])
+        for p in tables:
+            if p.dim() != 2 or p.shape[1] != H or store.offset(p) != end or p.dtype != torch.float32:
+                return False
+            end += p.numel()
+        return len(tables) == 3
+
+    def __init__(self, ddp, tables, capacity=None):
+        store = ddp.store
+        self._ddp = weakref.ref(ddp)  # the engine owns this object
+        self.store = store
+        assert self.supported(store, tables)
+        H = tables[0].shape[1]
+        lo = store.offset(tables[0])
+        end = lo + sum(p.numel() for p in tables)
+        kept = list(tables)
+        self.tables = kept
+        self.lo, self.hi, self.H = lo, end, H
+        self.bases = []
+        base = 0
+        for p in kept:
+            self.bases.append(base)
+            base += p.shape[0]
+        self.K = base  # region rows; key K = padding (skipped by the scatter)
+        self.cap = int(capacity) if capacity else None
+        self.world = ddp.world_size
+        self.device = store.grad.device
+        self._pos_keys = {}
+        self._bufs = None
+        self.key = store.grad_view(kept[0]).data_ptr()
+        _HANDLERS[self.key] = weakref.ref(self)
+        self.reset()
+
+    @property
+    def ddp(self):
+        return self._ddp()
+
+    def close(self):
+        if self.key in _HANDLERS and _HANDLERS[self.key]() is self:
+            del _HANDLERS[self.key]
+
+    def reset(self):
+        self.armed = False  # keys gathered this step: the embedding backward hands its rows over
+        self.dense_launched = False
+        self.rows_launched = False
+        self.work_keys = None
+        self.works = []
+        self.sorted = None
+
+    # ---------------------------------------------------------------- buffers
+    def _agree_capacity(self, n):
+        t = torch.tensor([n], dtype=torch.int64, device=self.device)
+        comm = self.ddp.comm
+        if comm is not None and t.is_cuda:
+            comm.all_reduce(t, op="max")
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.ddp.process_group)
+        return int(t.item())  # once per job (host sync)
+
+    def _buffers(self):
+        if self._bufs is None:
+            cap, W, H, dev = self.cap, self.world, self.H, self.device
+            nk = len(self.tables)
+            self._bufs = {
+                "keys": torch.full((nk, cap), self.K, dtype=torch.int64, device=dev),
+                "keys_all": torch.empty((W, nk, cap), dtype=torch.int64, device=dev),
+                "rows": torch.zeros((cap, H), dtype=torch.float32, device=dev),
+                "rows_all": torch.empty((W * cap, H), dtype=torch.float32, device=dev),
+                "scratch": torch.empty((W * nk * cap, H), dtype=torch.float32, device=dev)
+                if dev.type == "cuda" else None,
+            }
+        return self._bufs
+
+    def region(self):
+        return self.store.grad[self.lo:self.hi].view(self.K, self.H)
+
+    # ---------------------------------------------------------------- forward
+    def begin(self, ids, tt, needs_grad):
+        """Forward of the fused embedding: ids / tt [B, S] int64.  Returns True when this
+        micro-batch's rows go through the sparse exchange (the caller then uses ``row_buffer``)."""
+        self.reset()
+        if not (needs_grad and self.ddp.require_sync):
+            return False
+        B, S = ids.shape
+        n = B * S
+        if self.cap is None:
+            self.cap = self._agree_capacity(n)
+        if n > self.cap:
+            raise RuntimeError("sparse embedding exchange: a micro-batch of %d tokens exceeds the agreed capacity %d "
+                               "(pass sparse_capacity to FlatDDP)" % (n, self.cap))
+        b = self._buffers()
+        keys = b["keys"]
+        keys[0, :n].copy_(ids.reshape(-1))
+        pk = self._pos_keys.get((n, S))
+        if pk is None:  # position of token r is r % S (positions 0..S-1 of every sequence)
+            pk = (torch.arange(n, dtype=torch.int64, device=ids.device) % S) + self.bases[1]
+            self._pos_keys[(n, S)] = pk
+        keys[1, :n].copy_(pk)
+        if tt is None:
+            keys[2, :n].fill_(self.bases[2])
+        else:
+            torch.add(tt.reshape(-1), self.bases[2], out=keys[2, :n])
+        if n < self.cap:
+            keys[:, n:].fill_(self.K)
+        comm = self.ddp.comm
+        self.ddp._log("keys", keys)
+        if comm is not None and keys.is_cuda:
+            comm.all_gather_async(b["keys_all"], keys, producers=(torch.cuda.current_stream(keys.device),))
+        else:
+            self.work_keys = dist.all_gather_into_tensor(b["keys_all"].view(-1), keys.view(-1), group=self.ddp.process_group,
+                                                         async_op=True)
+        self.armed = True
+        return True
+
+    # ---------------------------------------------------------------- backward
+    def _sort(self):
+        """Stable sort of the gathered keys (same order on every rank) and their source rows."""
+        b = self._bufs
+        comm = self.ddp.comm
+        if comm is not None and b["keys_all"].is_cuda:
+            comm.wait()  # this stream after the key gather (the only collective issued since forward)
+        elif self.work_keys is not None:
+            self.work_keys.wait()
+            self.work_keys = None
+        flat = b["keys_all"].view(-1)
+        skeys, order = torch.sort(flat, stable=True)
+        nk, cap = len(self.tables), self.cap
+        rows = torch.div(order, nk * cap, rounding_mode="floor") * cap + torch.remainder(order, cap)
+        self.sorted = (skeys, rows)
+
+    def _reduce_region(self):
+        self.ddp._launch_range(self.lo, self.hi, "allreduce_tables")
+        self.dense_launched = True
+
+    def dense_ready(self, device):
+        """MLM-head backward, after the tied decoder's weight GEMM was enqueued: reduce the region
+        (its dense part is final now) and sort the gathered keys on the weight-gradient stream."""
+        if not self.armed or self.dense_launched:
+            return
+        if device.type == "cuda" and streams.active(device) is not None:
+            b = self._bufs
+            streams.run(device, self._sort, b["keys_all"])
+        else:
+            self._sort()
+        self._reduce_region()
+
+    def row_buffer(self, n, H):
+        assert self.armed and H == self.H and n <= self.cap
+        return self._bufs["rows"][:n]
+
+    def rows_ready(self):
+        """End of the embedding backward (its kernels wrote ``row_buffer``): gather every rank's rows."""
+        assert self.armed and not self.rows_launched
+        if not self.dense_launched:  # the tied decoder did not signal (non-fused head): reduce now
+            self._sort()
+            self._reduce_region()
+        self.ddp._tail_started()
+        b = self._bufs
+        comm = self.ddp.comm
+        profiling.range_push("allgather_rows")
+        self.ddp._log("rows", b["rows"])
+        if comm is not None and b["rows"].is_cuda:
+            comm.all_gather_async(b["rows_all"], b["rows"], producers=(torch.cuda.current_stream(self.device),))
+        else:
+            self.works.append(dist.all_gather_into_tensor(b["rows_all"], b["rows"], group=self.ddp.process_group,
+                                                          async_op=True))
+        profiling.range_pop()
+        self.rows_launched = True
+
+    def launch_pending(self):
+        """End of backward, before the engine's waits: the dense fallback when no rows came."""
+        if self.armed and not self.rows_launched:
+            raise RuntimeError("sparse embedding exchange: keys were gathered but the embedding backward never "
+                               "handed its rows over")
+        if not self.armed and not self.dense_launched:
+            self._reduce_region()
+
+    def scatter(self):
+        """After the engine waited for the comm stream: add the gathered rows into the region."""
+        for w in self.works:
+            w.wait()
+        self.works = []
+        if not self.armed:
+            return
+        b = self._bufs
+        skeys, rows = self.sorted
+        region = self.region()
+        if region.is_cuda:
+            from hetseq_amd.ops.bert_ops import segsum_rows
+
+            segsum_rows(b["rows_all"], rows, skeys, region, scratch=b["scratch"])
+        else:
+            valid = skeys < self.K
+            region.index_add_(0, skeys[valid], b["rows_all"].index_select(0, rows[valid]))
+        self.armed = False

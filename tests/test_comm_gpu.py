@@ -206,3 +206,69 @@ def test_bucket_snapshots_equal_final_gradients(group):
         assert any(not torch.equal(snap_bad[lo:hi], grad_bad[lo:hi]) for lo, hi in ranges)
     finally:
         streams.set_enabled(old)
+
+
+def test_tied_tables_early_bucket_and_sparse_rows(group):
+    """Tied word-embedding tail (parallel/tied.py) on the fused BERT path, native engine in
+    snapshot mode: the tables' early bucket is read (snapshot copy on the comm stream, where the
+    all-reduce would read it) after the tied decoder's weight GEMM and BEFORE any embedding row is
+    added -- so the position / token-type tables are still zero there and every word row no token
+    touched already holds its final value; the bytes issued after the last backward kernel are the
+    row gather (B*S*H*4) plus the embedding LayerNorm's 2*H*4; and the gradient equals the
+    engine-free fused backward's."""
+    from hetseq_amd.parallel.ddp import FlatDDP
+    from hetseq_amd.runtime import streams
+    from hetseq_amd.runtime.flat import FlatParamStore
+    from tests.test_bert_gpu import _batch, _tiny
+
+    cuda = torch.device("cuda", 0)
+    B, S = 4, 64
+    old = streams.enabled()
+    streams.set_enabled(True)
+    try:
+        grads = []
+        for use_ddp in (False, True):
+            model, cfg = _tiny(cuda)
+            model.eval()
+            model.max_predictions_per_seq = 10
+            store = FlatParamStore(model)
+            model.attach_store(store, torch.float32)
+            batch = _batch(cuda, B, S, cfg.vocab_size)
+            store.grad.zero_()
+            if not use_ddp:
+                model(*batch).backward()
+                torch.cuda.synchronize()
+                grads.append(store.grad.clone())
+                continue
+            net = FlatDDP(model, store, bucket_cap_mb=0.25, comm_engine="native", timeout_s=60,
+                          sparse_embedding=model.sparse_embedding())
+            assert net.tables is not None
+            snap = torch.full_like(store.grad, float("nan"))
+            net.comm.set_snapshot(snap, store.grad)
+            try:
+                net(*batch).backward()
+                torch.cuda.synchronize()
+            finally:
+                net.comm.set_snapshot(None, None)
+                net.comm.check()
+                net.comm.close()
+            grads.append(store.grad.clone())
+            t = net.tables
+            H = cfg.hidden_size
+            V = cfg.vocab_size
+            region_snap = snap[t.lo:t.hi].view(t.K, H)
+            region = store.grad[t.lo:t.hi].view(t.K, H)
+            assert torch.all(region_snap[V:] == 0)  # position + type rows: no embedding row added yet
+            touched = torch.zeros(V, dtype=torch.bool, device=cuda)
+            touched[batch[0].reshape(-1)] = True
+            assert torch.equal(region_snap[:V][~touched], region[:V][~touched])
+            assert not torch.equal(region_snap[:V][touched], region[:V][touched])
+            names = [w for w, _, _ in net.comm_log]
+            assert names[:2] == ["keys", "allreduce_tables"], names
+            tail = [(w, b) for w, b, late in net.comm_log if late]
+            assert tail[0] == ("rows", B * S * H * 4), tail
+            assert net.tail_bytes() <= B * S * H * 4 + 2 * H * 4, tail
+    finally:
+        streams.set_enabled(old)
+    ref, got = grads
+    assert torch.allclose(got, ref, rtol=1e-5, atol=1e-6), (got - ref).abs().max().item()

@@ -111,3 +111,69 @@ def test_bench_self_launches_two_ranks(tmp_path):
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 64
     assert out["config"]["comm"] == "c10d-gloo" and out["steps"] == 5
     assert out["value"] > 0
+
+
+def _tied_worker(rank, port, q, sparse):
+    try:
+        import torch
+        import torch.distributed as dist
+
+        from hetseq_amd.parallel.ddp import FlatDDP
+        from hetseq_amd.runtime.flat import FlatParamStore
+        from tests.test_bert_gpu import _batch, _tiny
+
+        dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, world_size=2, rank=rank)
+        cuda = torch.device("cuda", 0)
+        torch.cuda.set_device(cuda)
+        model, cfg = _tiny(cuda)
+        model.eval()
+        model.max_predictions_per_seq = 10
+        store = FlatParamStore(model)
+        model.attach_store(store, torch.float32)
+        net = FlatDDP(model, store, bucket_cap_mb=0.25, comm_engine="c10d",
+                      sparse_embedding=model.sparse_embedding() if sparse else None)
+        assert (net.tables is not None) == sparse
+        ids, tt, mask, labels, nsp = _batch(cuda, 4, 64, cfg.vocab_size)
+        ids = (ids + 37 * rank) % cfg.vocab_size  # different tokens per rank, some shared
+        store.grad.zero_()
+        for micro in range(2):  # update_freq 2: a no_sync micro-batch first (dense local tables)
+            with (net.no_sync() if micro == 0 else torch.enable_grad()):
+                net(ids, tt, mask, labels, nsp).backward()
+        torch.cuda.synchronize()
+        q.put((rank, store.grad.cpu().numpy().copy(), [w for w, _, late in net.comm_log if late]))
+        dist.destroy_process_group()
+    except BaseException as e:
+        q.put((rank, None, repr(e)))
+        raise
+
+
+def test_tied_tables_sparse_exchange_two_ranks_fused_bert():
+    """Fused BERT backward, 2 ranks sharing the GPU over gloo (c10d engine): the sparse table
+    exchange (early dense bucket + row gather + sorted-run scatter, parallel/tied.py) gives the
+    dense-bucket engine's gradient, after a no_sync micro-batch too, with identical replicas."""
+    import multiprocessing as mp
+
+    import torch
+
+    res = {}
+    for sparse in (True, False):
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_tied_worker, args=(r, port, q, sparse)) for r in range(2)]
+        for p in procs:
+            p.start()
+        out = {}
+        for _ in range(2):
+            r, g, tail = q.get(timeout=300)
+            assert g is not None, "rank %d: %s" % (r, tail)
+            out[r] = (torch.from_numpy(g), tail)
+        for p in procs:
+            p.join(60)
+            assert p.exitcode == 0
+        res[sparse] = out
+    g_sp, g_dn = res[True][0][0], res[False][0][0]
+    assert torch.equal(g_sp, res[True][1][0])
+    assert torch.equal(g_dn, res[False][1][0])
+    assert torch.allclose(g_sp, g_dn, rtol=1e-5, atol=1e-6), (g_sp - g_dn).abs().max().item()
+    assert res[True][0][1][0] == "rows", res[True][0][1]
