@@ -59,7 +59,7 @@ def parse():
     p.add_argument("--no-fused", action="store_true")
     p.add_argument("--gemm", default=None, choices=[None, "hip", "blas", "auto"])
     p.add_argument("--profile-phases", action="store_true")
-    p.add_argument("--hip-graph", action="store_true", help="replay the captured update as one HIP graph (1 GPU)")
+    p.add_argument("--hip-graph", action="store_true", help="replay the captured update as one HIP graph (1 GPU, or data-parallel on the native RCCL engine)")
     p.add_argument("--sync-debug", action="store_true", help="warn (with stack) on every host<->device sync in the timed loop")
     p.add_argument("--host-profile", default=None, help="cProfile the timed loop into this file")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -67,6 +67,9 @@ def parse():
     p.add_argument("--comm-engine", default="auto", choices=["auto", "native", "c10d"],
                    help="gradient collectives for N > 1: native RCCL engine (auto with nccl) or torch c10d")
     p.add_argument("--dry-run", type=int, default=None, help=argparse.SUPPRESS)  # launcher test: fail this rank
+    # profiling aid: the data-parallel engine (FlatDDP + native RCCL comm stream) on a 1-rank world,
+    # so the stream / HW-queue layout of a DP step can be traced on one GPU (profiles/r3_stream_queues.md)
+    p.add_argument("--ddp-world1", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--gemm-choices", default=None,
                    help="JSON of measured GEMM engine choices: loaded if it exists (no measuring in warm-up), "
                         "else written after the run (profiling runs use it to keep tuning out of the trace)")
@@ -215,9 +218,16 @@ def run_rank(b):
             argv += ["--distributed-init-method", "env://"]
     args = options.parse_cli(argv)
     args.distributed_rank = rank
+    args.force_ddp = bool(b.ddp_world1 and world == 1)
     # local index -> device (group offset for heterogeneous launches); gloo rehearsal: all on GPU 0
     args.device_id = 0 if b.dist_backend == "gloo" else distributed_utils.local_device_id(args, local_rank)
     torch.cuda.set_device(args.device_id)
+    from hetseq_amd.runtime import streams
+
+    streams.reserve(torch.device("cuda", args.device_id))  # hardware queues before RCCL's streams
+    if args.force_ddp:
+        dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % _free_port(), world_size=1, rank=0,
+                                device_id=torch.device("cuda", args.device_id))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         distributed_utils.distributed_init(args)  # the training launcher's own rendezvous + warm-up
@@ -307,9 +317,10 @@ def run_rank(b):
     if rank == 0:
         from hetseq_amd.parallel import comm as native_comm
 
-        comm_kind = "none" if world == 1 else (
+        comm_kind = "none" if (world == 1 and not args.force_ddp) else (
             "rccl-native" if getattr(ctl.model, "comm", None) is not None else "c10d-" + b.dist_backend)
-        par = "dp%d" % world + (" (hetero %s)" % "+".join(str(n) for n, _ in _groups(b)) if b.hetero else "")
+        par = "dp%d" % world + (" (hetero %s)" % "+".join(str(n) for n, _ in _groups(b)) if b.hetero else "") + (
+            " (DP engine on a 1-rank world)" if args.force_ddp else "")
         out = {
             "metric": "avg sec/step, BERT-base seq%d bs=%d/GPU" % (b.seq_len, b.batch),
             "value": round(sec, 6),
@@ -330,7 +341,7 @@ def run_rank(b):
                        "global_batch": seqs, "seq_len": b.seq_len, "per_gpu_batch": b.batch,
                        "update_freq": b.update_freq, "parallelism": par,
                        "fused_kernels": not b.no_fused, "bucket_cap_mb": b.bucket_cap_mb,
-                       "hip_graph": bool(b.hip_graph and world == 1), "comm": comm_kind,
+                       "hip_graph": bool(getattr(ctl, "_graph", None)), "comm": comm_kind,
                        "comm_fallback_reason": native_comm.LAST_STATUS.get("reason") if world > 1 else None},
             "final_train_loss_logged": round(loss, 5),
             "host_ms_per_step": round(host / b.steps * 1000, 3),
@@ -340,7 +351,7 @@ def run_rank(b):
         }
         sys.stdout.write(json.dumps(out) + "\n")  # one write: other ranks may share this pipe
         sys.stdout.flush()
-    if world > 1:
+    if world > 1 or args.force_ddp:
         dist.barrier()
         if getattr(ctl.model, "comm", None) is not None:
             ctl.model.comm.close()

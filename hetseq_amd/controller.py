@@ -106,7 +106,8 @@ class Controller(object):
     @property
     def model(self):
         if self._wrapped_model is None:
-            if self.args.distributed_world_size > 1 and dist.is_initialized() and not self.args.use_bmuf:
+            multi = self.args.distributed_world_size > 1 or getattr(self.args, "force_ddp", False)
+            if multi and dist.is_initialized() and not self.args.use_bmuf:
                 self._wrapped_model = FlatDDP(self._model, self.store, bucket_cap_mb=self.args.bucket_cap_mb,
                                               find_unused_parameters=self.args.find_unused_parameters,
                                               comm_engine=getattr(self.args, "comm_engine", "auto"),
@@ -330,14 +331,19 @@ class Controller(object):
     # ------------------------------------------------------------------ HIP graph path
     def _graph_eligible(self, samples, dummy_batch):
         a = self.args
+        # data-parallel runs capture too when the gradients go through the native RCCL engine: its
+        # collectives are enqueued on streams (captured into the graph, replayed in the same order
+        # on every rank); c10d / gloo and BMUF stay eager
+        dp = self._sync_stats() or isinstance(self.model, FlatDDP)
+        dp_ok = not dp or (isinstance(self.model, FlatDDP) and self.model.comm is not None and not a.use_bmuf)
         return (getattr(a, "hip_graph", False) and self.cuda and self.fast_stat_sync and not dummy_batch
-                and len(samples) == 1 and samples[0] is not None and len(samples[0]) > 0
-                and not (a.distributed_world_size > 1 and dist.is_initialized())
+                and len(samples) == 1 and samples[0] is not None and len(samples[0]) > 0 and dp_ok
                 and getattr(self.optimizer, "supports_device_hyper", False)
                 and self._num_updates >= self._graph_warmup)
 
     def _graph_body(self, sample):
-        """The captured update (fast-stat path of train_step, single process)."""
+        """The captured update (fast-stat path of train_step; data-parallel: the bucket, table and
+        statistics collectives of the native engine are captured with it)."""
         self.zero_grad()
         stats = torch.zeros(6, dtype=torch.float64, device=self.device)
         _, sample_size, lo = self.task.train_step(sample, self.model, self.optimizer, False)
@@ -346,6 +352,8 @@ class Controller(object):
         stats[2] += _as_f64(lo.get("loss", 0.0), self.device)
         stats[3] += _as_f64(lo.get("nll_loss", 0.0), self.device)
         stats[4] += lo.get("ntokens", 0.0)
+        if self._sync_stats():
+            self.model.all_reduce_(stats)  # in-stream RCCL (captured)
         stats[2:4].div_(stats[0:1] * LN2)
         scale = torch.where(stats[0] > 0, 1.0 / stats[0].clamp(min=1e-30), torch.ones_like(stats[0])).float()
         self.optimizer.multiply_grads(scale)
@@ -362,7 +370,10 @@ class Controller(object):
         if self._graph is None:
             rng.enable_device_seed(self.device)
             self.optimizer.enable_device_hyper(self.device)
-            self._graph = GraphedStep(self._graph_body)
+            comm = getattr(self.model, "comm", None)
+            # with a communicator the watchdog thread queries events during capture: errors of other
+            # threads must not invalidate it (thread-local capture mode)
+            self._graph = GraphedStep(self._graph_body, capture_error_mode="thread_local" if comm else "global")
         elif not self._graph.matches(sample):
             return None  # e.g. a short last batch: run it eagerly
         faults.maybe_inject(getattr(self.args, "distributed_rank", 0) or 0, self._num_updates)
@@ -380,6 +391,10 @@ class Controller(object):
             self.optimizer.step_count -= 1
             self._graph = False
             return None
+        comm = getattr(self.model, "comm", None)
+        if comm is not None:
+            comm.watch()  # the replayed collectives under the watchdog
+            comm.check()
         grad_norm = grad_norm[0]
         self.set_num_updates(self.get_num_updates() + 1)
         self.task.update_step(self._num_updates)

@@ -241,6 +241,13 @@ class Comm {
     track(as_stream(stream));
   }
 
+  // The watchdog also covers the work enqueued on `stream` so far (a replayed HIP graph whose
+  // collectives were captured: their completion is the replay's).
+  void watch_stream(uintptr_t stream) {
+    check();
+    track(as_stream(stream));
+  }
+
   // Raises if the watchdog aborted the communicator (timeout / async RCCL error).
   void check() {
     if (aborted_.load()) {
@@ -289,8 +296,13 @@ class Comm {
     free_.push_back(e);
   }
 
-  // completion event of the collective just enqueued on `s`, watched by the watchdog
+  // completion event of the collective just enqueued on `s`, watched by the watchdog.  Not while
+  // `s` is being captured into a HIP graph: an event recorded there never completes outside the
+  // graph (the replay is watched instead: watch_stream() after each launch).
   void track(hipStream_t s) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    hip_check(hipStreamIsCapturing(s, &cs), "hipStreamIsCapturing");
+    if (cs != hipStreamCaptureStatusNone) return;
     hipEvent_t e = take_event();
     hip_check(hipEventRecord(e, s), "hipEventRecord(done)");
     bool stalled = false;
@@ -396,6 +408,7 @@ PYBIND11_MODULE(_comm, m) {
       .def("all_gather", &Comm::all_gather, py::arg("send"), py::arg("recv"), py::arg("count"), py::arg("dtype"),
            py::arg("stream"))
       .def("check", &Comm::check)
+      .def("watch_stream", &Comm::watch_stream, py::arg("stream"))
       .def("close", &Comm::close, py::arg("graceful") = true)
       .def("inject_stall", &Comm::inject_stall)
       .def("set_snapshot", &Comm::set_snapshot, py::arg("dst"), py::arg("src"), py::arg("bytes"))

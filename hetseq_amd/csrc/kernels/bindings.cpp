@@ -442,6 +442,18 @@ PYBIND11_MODULE(_hip, m) {
   // returns 0 when launched, -1 when the shape/epilogue is not served (caller falls back)
   m.def("set_seed_ptr", [](i64 ptr) { hs::g_seed_dev = reinterpret_cast<const uint64_t*>(ptr); });
   m.def("stream_wait", [](i64 waiter, i64 signal) { stream_wait(ST(waiter), ST(signal)); });
+  // A non-blocking stream of the current device that lives for the whole process (runtime/streams.py
+  // creates the engine's streams with it before RCCL and torch's stream pool create theirs, so each
+  // role gets a hardware queue of its own; never destroyed).
+  m.def("stream_create", [](int greatest_priority) {
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess)
+      throw std::runtime_error("hipDeviceGetStreamPriorityRange failed");
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithPriority(&s, hipStreamNonBlocking, greatest_priority ? greatest : least) != hipSuccess)
+      throw std::runtime_error("hipStreamCreateWithPriority failed");
+    return reinterpret_cast<i64>(s);
+  });
   m.def("gemm", [](int dt, int ta, int tb, int M, int N, int K, i64 A, i64 lda, i64 B, i64 ldb, i64 C, i64 ldc, i64 bias,
                    int epi, float beta, i64 aux, i64 ldaux, i64 part, i64 colsum, int colsum_acc, i64 st,
                    int tile, int ksplit, i64 slab, i64 slab_floats, int mv, int nv, int kv) {

@@ -167,7 +167,9 @@ class NativeBatchStream(object):
         ptrs = [[t.data_ptr() for t in s] for s in self._slots]
         self._pf = _h5().Prefetcher(self.dataset._set, self.batches, ptrs, max_bsz, self.num_threads)
         if pin:
-            self._copy_stream = torch.cuda.Stream(device=self.device)
+            from hetseq_amd.runtime import streams
+
+            self._copy_stream = streams.copy_stream(self.device)  # one per device for the job
         self._inflight = []  # (slot, event)
 
     def __iter__(self):

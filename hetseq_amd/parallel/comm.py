@@ -111,6 +111,11 @@ class NativeComm(object):
         return out
 
     # ------------------------------------------------------------------ health
+    def watch(self, stream=None):
+        """Put the work enqueued on ``stream`` (default current) so far under the watchdog -- after
+        a HIP-graph replay whose collectives were captured (capture itself registers nothing)."""
+        self._c.watch_stream(_stream(stream))
+
     def check(self):
         """Raise if the watchdog aborted the communicator (timeout or async RCCL error)."""
         self._c.check()

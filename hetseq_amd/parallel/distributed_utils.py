@@ -48,6 +48,11 @@ def distributed_init(args):
             kw = {}
         else:
             kw = dict(world_size=args.distributed_world_size, rank=args.distributed_rank)
+        if torch.cuda.is_available() and backend == "nccl":
+            from hetseq_amd.runtime import streams
+
+            # the engine's streams take their hardware queues before RCCL creates its streams
+            streams.reserve(torch.device("cuda", torch.cuda.current_device()))
         timeout = datetime.timedelta(seconds=float(getattr(args, "collective_timeout", 1800.0)))
         if backend == "nccl" and torch.cuda.is_available():
             kw["device_id"] = torch.device("cuda", torch.cuda.current_device())

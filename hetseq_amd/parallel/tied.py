@@ -14,11 +14,12 @@ a tail no backward compute overlaps.  ``SparseTableSync`` splits it:
 
 1. forward: every rank builds the keys of its tokens into the concatenated [word | position |
    type] table region (int64 [3, cap]; padding keys point past the region) and all-gathers them
-   on the comm stream -- they are known long before backward;
+   on the comm stream -- they are known long before backward -- and sorts them (stable) right
+   behind the gather on the same stream;
 2. MLM-head backward, right after the decoder weight GEMM is enqueued
    (``FusedPreTrainingLoss.backward`` -> ``dense_ready``): the whole region is all-reduced as its
    own early bucket, ordered after the GEMM by producer events, overlapping the encoder's
-   backward; the gathered keys are sorted (stable) on the weight-gradient stream;
+   backward;
 3. embedding backward (``FusedEmbedding.backward`` -> ``row_buffer`` / ``rows_ready``): the
    per-token rows are not scattered locally -- they land in a persistent [cap, H] buffer that is
    all-gathered: cap*H*4 bytes per rank, the only exchange issued after the last backward kernel
@@ -90,6 +91,7 @@ class SparseTableSync(object):
         self.device = store.grad.device
         self._pos_keys = {}
         self._bufs = None
+        self._comm_stream = None
         self.key = store.grad_view(kept[0]).data_ptr()
         _HANDLERS[self.key] = weakref.ref(self)
         self.reset()
@@ -169,6 +171,13 @@ class SparseTableSync(object):
         self.ddp._log("keys", keys)
         if comm is not None and keys.is_cuda:
             comm.all_gather_async(b["keys_all"], keys, producers=(torch.cuda.current_stream(keys.device),))
+            # sort right behind the gather on the comm stream itself (idle during forward): no other
+            # stream waits on the comm stream before the end of backward -- a mid-step wait on it
+            # also breaks HIP-graph capture (tools/graph_probe.py seq_b)
+            if self._comm_stream is None:
+                self._comm_stream = torch.cuda.ExternalStream(comm.stream_handle, device=self.device)
+            with torch.cuda.stream(self._comm_stream):
+                self._sort_keys()
         else:
             self.work_keys = dist.all_gather_into_tensor(b["keys_all"].view(-1), keys.view(-1), group=self.ddp.process_group,
                                                          async_op=True)
@@ -177,14 +186,15 @@ class SparseTableSync(object):
 
     # ---------------------------------------------------------------- backward
     def _sort(self):
-        """Stable sort of the gathered keys (same order on every rank) and their source rows."""
-        b = self._bufs
-        comm = self.ddp.comm
-        if comm is not None and b["keys_all"].is_cuda:
-            comm.wait()  # this stream after the key gather (the only collective issued since forward)
-        elif self.work_keys is not None:
+        """c10d path: after the key gather, the sort on the current stream."""
+        if self.work_keys is not None:
             self.work_keys.wait()
             self.work_keys = None
+        self._sort_keys()
+
+    def _sort_keys(self):
+        """Stable sort of the gathered keys (same order on every rank) and their source rows."""
+        b = self._bufs
         flat = b["keys_all"].view(-1)
         skeys, order = torch.sort(flat, stable=True)
         nk, cap = len(self.tables), self.cap
@@ -200,11 +210,11 @@ class SparseTableSync(object):
         (its dense part is final now) and sort the gathered keys on the weight-gradient stream."""
         if not self.armed or self.dense_launched:
             return
-        if device.type == "cuda" and streams.active(device) is not None:
-            b = self._bufs
-            streams.run(device, self._sort, b["keys_all"])
-        else:
-            self._sort()
+        if self.sorted is None:  # c10d path
+            if device.type == "cuda" and streams.active(device) is not None:
+                streams.run(device, self._sort, self._bufs["keys_all"])
+            else:
+                self._sort()
         self._reduce_region()
 
     def row_buffer(self, n, H):
@@ -215,7 +225,8 @@ class SparseTableSync(object):
         """End of the embedding backward (its kernels wrote ``row_buffer``): gather every rank's rows."""
         assert self.armed and not self.rows_launched
         if not self.dense_launched:  # the tied decoder did not signal (non-fused head): reduce now
-            self._sort()
+            if self.sorted is None:
+                self._sort()
             self._reduce_region()
         self.ddp._tail_started()
         b = self._bufs

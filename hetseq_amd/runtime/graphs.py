@@ -53,8 +53,9 @@ class GraphedStep(object):
     ``outputs`` is a tuple of device tensors; ``run`` returns clones of them.
     """
 
-    def __init__(self, fn):
+    def __init__(self, fn, capture_error_mode="global"):
         self.fn = fn
+        self.mode = capture_error_mode
         self.graph = None
         self.static_in = None
         self.static_out = None
@@ -73,7 +74,7 @@ class GraphedStep(object):
             self.signature = self._sig(inputs)
             torch.cuda.synchronize()
             self.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph):
+            with torch.cuda.graph(self.graph, capture_error_mode=self.mode):
                 self.static_out = self.fn(self.static_in)
         else:
             for dst, src in zip(self.static_in, inputs):

@@ -79,13 +79,65 @@ def is_side(stream_handle: int) -> bool:
     return any(s.cuda_stream == stream_handle for s in _STREAMS.values())
 
 
+def _new_stream(idx):
+    """A process-lifetime non-blocking HIP stream of device ``idx`` (not from torch's pool)."""
+    from hetseq_amd.ops._C import hip
+
+    prev = torch.cuda.current_device()
+    torch.cuda.set_device(idx)
+    try:
+        return torch.cuda.ExternalStream(hip().stream_create(0), device=torch.device("cuda", idx))
+    finally:
+        torch.cuda.set_device(prev)
+
+
 def side(device) -> "torch.cuda.Stream":
     idx = device.index if device.index is not None else torch.cuda.current_device()
     s = _STREAMS.get(idx)
     if s is None:
-        s = torch.cuda.Stream(device=torch.device("cuda", idx))
+        s = _new_stream(idx)
         _STREAMS[idx] = s
     return s
+
+
+def reserve(device):
+    """Create the weight-gradient and copy streams of ``device`` now -- before RCCL (torch's process
+    group, the native engine) and torch's stream pool create theirs.  HIP hands the first
+    GPU_MAX_HW_QUEUES streams of a process a hardware queue each and makes later ones share the
+    least-used queue: created after RCCL's ten internal streams, the side stream landed on the
+    compute stream's queue and the two serialised (BERT-base DP step 19.3 ms vs 15.1,
+    profiles/r3_stream_queues.md).  The comm stream (greatest priority) gets a priority queue."""
+    if device is None or device.type != "cuda" or not torch.cuda.is_available():
+        return
+    side(device)
+    copy_stream(device)
+
+
+_COPY: dict = {}
+
+
+def copy_stream(device) -> "torch.cuda.Stream":
+    """The process's host-to-device copy stream of ``device`` (the data loader's batch uploads).
+    One per device for the whole job: a stream per epoch iterator would draw new pool streams
+    and, past GPU_MAX_HW_QUEUES, land on a hardware queue shared with the compute / side / comm
+    streams (profiles/r3_stream_queues.md)."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    s = _COPY.get(idx)
+    if s is None:
+        s = _new_stream(idx)
+        _COPY[idx] = s
+    return s
+
+
+def engine_streams(device) -> dict:
+    """Raw handles of the streams this process runs work on, by role (created ones only)."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    out = {"compute": torch.cuda.current_stream(torch.device("cuda", idx)).cuda_stream}
+    if idx in _STREAMS:
+        out["wgrad"] = _STREAMS[idx].cuda_stream
+    if idx in _COPY:
+        out["copy"] = _COPY[idx].cuda_stream
+    return out
 
 
 def active(device) -> "torch.cuda.Stream | None":

@@ -48,6 +48,9 @@ def main(args, init_distributed=False):
         "Must specify batch size either with --max-tokens or --max-sentences"
     if torch.cuda.is_available() and not args.cpu:
         torch.cuda.set_device(args.device_id)
+        from hetseq_amd.runtime import streams
+
+        streams.reserve(torch.device("cuda", args.device_id))  # hardware queues before RCCL's streams
     if getattr(args, "profile", False):
         profiling.enable(True)
     np.random.seed(args.seed)

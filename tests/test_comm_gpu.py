@@ -272,3 +272,90 @@ def test_tied_tables_early_bucket_and_sparse_rows(group):
         streams.set_enabled(old)
     ref, got = grads
     assert torch.allclose(got, ref, rtol=1e-5, atol=1e-6), (got - ref).abs().max().item()
+
+
+def test_engine_stream_roles_are_distinct_and_fit_hw_queues(group):
+    """The data-parallel step runs on exactly four streams -- compute, weight-gradient side
+    stream, the native engine's greatest-priority comm stream and the loader's copy stream (one
+    per device for the whole job, not one per epoch iterator) -- all distinct and no more than
+    GPU_MAX_HW_QUEUES, so each gets its own hardware queue (profiles/r3_stream_queues.md shows
+    the placement and overlap from a kernel trace)."""
+    from hetseq_amd.parallel.ddp import FlatDDP
+    from hetseq_amd.runtime import streams
+    from hetseq_amd.runtime.flat import FlatParamStore
+    from tests.test_bert_gpu import _batch, _tiny
+
+    cuda = torch.device("cuda", 0)
+    old = streams.enabled()
+    streams.set_enabled(True)
+    try:
+        model, cfg = _tiny(cuda)
+        model.max_predictions_per_seq = 10
+        store = FlatParamStore(model)
+        model.attach_store(store, torch.float32)
+        net = FlatDDP(model, store, bucket_cap_mb=0.25, comm_engine="native", timeout_s=60,
+                      sparse_embedding=model.sparse_embedding())
+        copy = streams.copy_stream(cuda)
+        assert streams.copy_stream(cuda) is copy  # a second epoch iterator reuses it
+        for _ in range(2):
+            store.grad.zero_()
+            net(*_batch(cuda, 4, 64, cfg.vocab_size)).backward()
+        torch.cuda.synchronize()
+        roles = streams.engine_streams(cuda)
+        roles["comm"] = net.comm.stream_handle
+        net.comm.check()
+        net.comm.close()
+    finally:
+        streams.set_enabled(old)
+    assert set(roles) == {"compute", "wgrad", "copy", "comm"}, roles
+    assert len(set(roles.values())) == 4, roles
+    assert len(roles) <= int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+
+
+def test_graph_captured_dp_step_matches_eager(group):
+    """HIP-graph capture of a data-parallel backward on the native engine (1-rank communicator):
+    the bucket all-reduces, the tables' early bucket, the key / row gathers and the stream joins
+    are captured; replays give the eager step's gradient, and the watchdog registered nothing
+    during capture (its events would never complete outside the graph)."""
+    from hetseq_amd.parallel.ddp import FlatDDP
+    from hetseq_amd.runtime import streams
+    from hetseq_amd.runtime.flat import FlatParamStore
+    from hetseq_amd.runtime.graphs import GraphedStep
+    from tests.test_bert_gpu import _batch, _tiny
+
+    cuda = torch.device("cuda", 0)
+    old = streams.enabled()
+    streams.set_enabled(True)
+    try:
+        model, cfg = _tiny(cuda)
+        model.eval()
+        model.max_predictions_per_seq = 10
+        store = FlatParamStore(model)
+        model.attach_store(store, torch.float32)
+        net = FlatDDP(model, store, bucket_cap_mb=0.25, comm_engine="native", timeout_s=60,
+                      sparse_embedding=model.sparse_embedding())
+        batch = list(_batch(cuda, 4, 64, cfg.vocab_size))
+        for _ in range(2):  # eager warm-up (capacity agreement, buffers, GEMM choices)
+            store.grad.zero_()
+            net(*batch).backward()
+        torch.cuda.synchronize()
+        eager = store.grad.clone()
+
+        def body(inputs):
+            store.grad.zero_()
+            net(*inputs).backward()
+            return (store.grad,)
+
+        step = GraphedStep(body, capture_error_mode="thread_local")
+        outs = [step.run(batch)[0] for _ in range(3)]
+        net.comm.watch()
+        torch.cuda.synchronize()
+        net.comm.check()
+        assert step.graph is not None
+        names = [w for w, _, _ in net.comm_log]  # the captured step's collectives
+        assert names[:2] == ["keys", "allreduce_tables"] and "rows" in names, names
+        net.comm.close()
+    finally:
+        streams.set_enabled(old)
+    for g in outs:
+        assert torch.equal(g, eager), (g - eager).abs().max().item()
