@@ -112,7 +112,8 @@ def load_checkpoint(args, controller):
             # update count in optimizer_history and this run's batches per epoch
             epoch_itr = controller.get_train_iterator(epoch=0, load_dataset=True)
             per_rank = -(-len(epoch_itr) // max(1, epoch_itr.num_shards))
-            itr_state = iterator_state_from_updates(controller.get_num_updates(), per_rank, args.update_freq)
+            # (the history's count, not the controller's: --reset-optimizer restarts the latter at 0)
+            itr_state = iterator_state_from_updates(controller.checkpoint_num_updates(), per_rank, args.update_freq)
         else:
             epoch_itr = controller.get_train_iterator(epoch=itr_state["epoch"], load_dataset=True)
         epoch_itr.load_state_dict(itr_state)

@@ -191,6 +191,11 @@ class Controller(object):
             print("| no existing checkpoint found {}".format(filename))
         return extra_state
 
+    def checkpoint_num_updates(self):
+        """Update count recorded in the loaded checkpoint's optimizer history (0 if none) -- also
+        under --reset-optimizer, where the controller's own count restarts at 0."""
+        return int(self._optim_history[-1].get("num_updates", 0)) if self._optim_history else 0
+
     def get_train_iterator(self, epoch, combine=True, load_dataset=True):
         if load_dataset:
             print("| loading train data for epoch {}".format(epoch))
@@ -334,8 +339,10 @@ class Controller(object):
         # data-parallel runs capture too when the gradients go through the native RCCL engine: its
         # collectives are enqueued on streams (captured into the graph, replayed in the same order
         # on every rank); c10d / gloo and BMUF stay eager
+        # (c10d / gloo: the collectives cannot be captured, so forward+backward and the update are
+        # two graphs with the gradient exchange between them -- _graph_split)
         dp = self._sync_stats() or isinstance(self.model, FlatDDP)
-        dp_ok = not dp or (isinstance(self.model, FlatDDP) and self.model.comm is not None and not a.use_bmuf)
+        dp_ok = not dp or (isinstance(self.model, FlatDDP) and not a.use_bmuf)
         return (getattr(a, "hip_graph", False) and self.cuda and self.fast_stat_sync and not dummy_batch
                 and len(samples) == 1 and samples[0] is not None and len(samples[0]) > 0 and dp_ok
                 and getattr(self.optimizer, "supports_device_hyper", False)
@@ -361,30 +368,69 @@ class Controller(object):
         self.optimizer.step(launch_only=True)
         return stats, grad_norm.reshape(1)
 
+    def _graph_split(self):
+        """Data-parallel through torch.distributed (c10d / gloo): collectives cannot be captured."""
+        return isinstance(self.model, FlatDDP) and self.model.comm is None
+
+    def _graph_fwd_bwd(self, sample):
+        """Split graph 1: forward + backward with no collective (gradients stay local)."""
+        self.zero_grad()
+        stats = torch.zeros(6, dtype=torch.float64, device=self.device)
+        with self.model.no_sync():
+            _, sample_size, lo = self.task.train_step(sample, self.model, self.optimizer, False)
+        stats[0] += sample_size
+        stats[1] += lo.get("nsentences", 0.0)
+        stats[2] += _as_f64(lo.get("loss", 0.0), self.device)
+        stats[3] += _as_f64(lo.get("nll_loss", 0.0), self.device)
+        stats[4] += lo.get("ntokens", 0.0)
+        return (stats,)
+
+    def _graph_update(self, inputs):
+        """Split graph 2: the update from the exchanged gradients and statistics."""
+        stats = inputs[0]
+        stats[2:4].div_(stats[0:1] * LN2)
+        scale = torch.where(stats[0] > 0, 1.0 / stats[0].clamp(min=1e-30), torch.ones_like(stats[0])).float()
+        self.optimizer.multiply_grads(scale)
+        grad_norm = self.optimizer.clip_grad_norm(self.args.clip_norm)
+        self.optimizer.step(launch_only=True)
+        return stats, grad_norm.reshape(1)
+
+    def _run_split_graphs(self, sample):
+        g1, g2 = self._graph
+        (stats,) = g1.run(list(sample))
+        self.model.all_reduce_grads()  # eager c10d exchange of the flat gradient buffer
+        self.model.all_reduce_(stats)
+        return g2.run([stats])
+
     def _train_step_graphed(self, sample):
         from hetseq_amd.runtime.graphs import GraphedStep
 
         sample = self._prepare_sample(sample)
         if self._graph is False:
             return None  # capture failed once: stay eager
+        split = self._graph_split()
         if self._graph is None:
             rng.enable_device_seed(self.device)
             self.optimizer.enable_device_hyper(self.device)
             comm = getattr(self.model, "comm", None)
-            # with a communicator the watchdog thread queries events during capture: errors of other
-            # threads must not invalidate it (thread-local capture mode)
-            self._graph = GraphedStep(self._graph_body, capture_error_mode="thread_local" if comm else "global")
-        elif not self._graph.matches(sample):
+            if split:
+                self._graph = (GraphedStep(self._graph_fwd_bwd), GraphedStep(self._graph_update))
+            else:
+                # with a communicator the watchdog thread queries events during capture: errors of
+                # other threads must not invalidate it (thread-local capture mode)
+                self._graph = GraphedStep(self._graph_body, capture_error_mode="thread_local" if comm else "global")
+        elif not (self._graph[0] if split else self._graph).matches(sample):
             return None  # e.g. a short last batch: run it eagerly
         faults.maybe_inject(getattr(self.args, "distributed_rank", 0) or 0, self._num_updates)
         self._set_seed()
         self.optimizer.graph_prepare()
         self.meters["train_wall"].start()
         try:
-            stats, grad_norm = self._graph.run(list(sample))
+            stats, grad_norm = self._run_split_graphs(sample) if split else self._graph.run(list(sample))
         except RuntimeError as e:
-            if self._graph.graph is not None and self._graph.static_out is not None:
-                raise  # a replay failure is a real error
+            first = self._graph[0] if split else self._graph
+            if first.graph is not None and first.static_out is not None:
+                raise  # a replay failure (or a failure after the first graph ran) is a real error
             # capture failed (nothing ran): undo the host half of the update and fall back to eager
             print("| WARNING: HIP graph capture failed ({}); continuing eagerly".format(str(e).splitlines()[0]),
                   flush=True)

@@ -222,6 +222,16 @@ class FlatDDP(torch.nn.Module):
         if self.tables is not None:
             self.tables.scatter()  # gathered embedding rows into the reduced tables
 
+    def all_reduce_grads(self):
+        """SUM the whole flat gradient buffer across the group in one collective (the split-graph
+        path: backward ran without communication, parallel bucket overlap is not available)."""
+        g = self.store.grad
+        if self.comm is not None and g.is_cuda:
+            self.comm.all_reduce(g)
+        else:
+            dist.all_reduce(g, group=self.process_group)
+        return g
+
     def all_reduce_(self, t):
         """In-place SUM of a small device tensor across the data-parallel group (fast stats)."""
         if self.comm is not None and t.is_cuda:

@@ -177,3 +177,19 @@ def test_tied_tables_sparse_exchange_two_ranks_fused_bert():
     assert torch.equal(g_dn, res[False][1][0])
     assert torch.allclose(g_sp, g_dn, rtol=1e-5, atol=1e-6), (g_sp - g_dn).abs().max().item()
     assert res[True][0][1][0] == "rows", res[True][0][1]
+
+
+def test_bench_two_ranks_gloo_bf16_hip_graph(tmp_path):
+    """``bench.py --gpus 2 --dist-backend gloo --dtype bf16 --hip-graph``: data-parallel over c10d
+    runs the split-graph path (forward+backward graph, eager gradient exchange, update graph)."""
+    import json
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+                        "--dtype", "bf16", "--hip-graph", "--steps", "5", "--warmup", "4"], env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    out = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")][0]
+    assert out["n_gpus"] == 2 and out["config"]["hip_graph"] is True and out["dtype"] == "bf16"
+    assert out["value"] > 0

@@ -177,8 +177,20 @@ def test_resume_reference_checkpoint_keeps_epoch(tmp_path):
     st = load_checkpoint_to_cpu(str(ck))
     st["extra_state"] = {}  # what the reference's save_state writes (Q01)
     torch.save(st, ck)
+    import shutil
+
+    shutil.copy(ck, tmp_path / "ref_last.pt")
     c2 = _train_cli(run, ["--max-epoch", "2"], str(d), cfg, vocab)
     assert c2.get_num_updates() == 12  # epoch 2 only, not epochs 1 and 2 again
+    # --reset-optimizer: the update count restarts at 0, the iterator position still comes from the
+    # checkpoint's optimizer history (epoch 1 finished -> epoch 2 runs, once)
+    run2 = tmp_path / "r2"
+    (run2 / "ck").mkdir(parents=True)
+    shutil.copy(tmp_path / "ref_last.pt", run2 / "ck" / "checkpoint_last.pt")
+    c3 = _train_cli(run2, ["--max-epoch", "2", "--reset-optimizer"], str(d), cfg, vocab)
+    assert c3.get_num_updates() == 6  # epoch 2's six updates, counted from 0
+    st3 = load_checkpoint_to_cpu(str(run2 / "ck" / "checkpoint_last.pt"))
+    assert st3["extra_state"]["train_iterator"]["epoch"] == 2
     distributed_utils.restore_output()
 
 
