@@ -383,7 +383,17 @@ class BertLayer(nn.Module):
         W.w2, W.b2 = cw(o.dense.weight), o.dense.bias.detach()
         W.g2, W.bb2 = o.LayerNorm.weight.detach(), o.LayerNorm.bias.detach()
         W.planes = False
+        W.bwd = W
         if not bf16 and store is not None and store.planes is not None:
+            from hetseq_amd.ops import gemm as G
+
+            if not G.planes_backward():  # forward-only planes: the backward keeps the fp32 views
+                Wb = LayerWeights()
+                for k in LayerWeights.__slots__:
+                    if k != "bwd":
+                        setattr(Wb, k, getattr(W, k))
+                Wb.bwd = Wb
+                W.bwd = Wb
             # fp32 on the plane engine: GEMM weights as their split-bf16 planes (refreshed by the optimizer)
             W.wqkv = store.planes_view(qkv, (3 * sa.all_head_size, H))
             W.wo = store.planes_view([ao.dense.weight], tuple(ao.dense.weight.shape))
@@ -744,7 +754,9 @@ class BertForPreTraining(BertPreTrainedModel):
         wt, wd = t.dense_act.weight, self.cls.predictions.decoder.weight
         store = getattr(self, "_hs_store", None)
         if self.compute_dtype != torch.bfloat16:
-            if store is not None and store.planes is not None:  # transform weight on the plane engine
+            from hetseq_amd.ops import gemm as G
+
+            if store is not None and store.planes is not None and G.planes_backward():  # transform on planes
                 return store.planes_view([wt], tuple(wt.shape)), wd.detach()
             return wt.detach(), wd.detach()
         if store is not None:

@@ -371,7 +371,7 @@ class LayerWeights(object):
     """Compute views of one encoder layer's weights: fp32 master, bf16 shadow, or (fp32 plane
     engine, ``planes`` True) the split-bf16 plane views (ops.gemm.Planes) of the GEMM weights."""
 
-    __slots__ = ("wqkv", "bqkv", "wo", "bo", "g1", "b1", "w1", "bi", "w2", "b2", "g2", "bb2", "planes")
+    __slots__ = ("wqkv", "bqkv", "wo", "bo", "g1", "b1", "w1", "bi", "w2", "b2", "g2", "bb2", "planes", "bwd")
 
 
 def _planes_of(buf):
@@ -388,6 +388,7 @@ def _layer_forward(x, mask, W, cfg, save):
     B, S, NH, p_h, p_a, eps, seeds = cfg
     (s_a, o_a), (s_1, o_1), (s_2, o_2) = seeds
     pl = getattr(W, "planes", False)
+    plb = pl and W.bwd is W  # the backward's GEMMs on planes too (else: fp32 operands saved)
     rows, H = x.shape
     xin = G.split_cached(x) if pl else x
     qkv = G.linear_fwd(xin, W.wqkv)  # bias folded into the attention kernels' Q/K/V loads
@@ -397,16 +398,23 @@ def _layer_forward(x, mask, W, cfg, save):
     h1p = _planes_buf(rows, H, x.device) if pl else None
     h1, z1, m1, r1 = ln_fwd(a, W.g1, W.b1, eps, bias=W.bo, resid=x, p=p_h, mode=1, seed=s_1, off=o_1, planes=h1p)
     hin = _planes_of(h1p) if pl else h1
-    f1, f1pre = G.linear_gelu_fwd(hin, W.w1, W.bi, planes_out=pl)  # f1pre: un-biased pre-activation
-    fin = f1
+    if pl and not plb:  # forward-only planes: f1 in fp32 (saved) and as planes (the next product)
+        f1, f1pre = G.linear_gelu_fwd(hin, W.w1, W.bi, emit_planes=True)
+        fin = G.split_cached(f1)
+    else:
+        f1, f1pre = G.linear_gelu_fwd(hin, W.w1, W.bi, planes_out=pl)  # f1pre: un-biased pre-activation
+        fin = f1
     o = G.linear_fwd(fin, W.w2)
     h2p = _planes_buf(rows, H, x.device) if pl else None
     h2, z2, m2, r2 = ln_fwd(o, W.g2, W.bb2, eps, bias=W.b2, resid=h1, p=p_h, mode=1, seed=s_2, off=o_2, planes=h2p)
     if pl:
         G.remember_planes(h2, _planes_of(h2p))  # the next layer's QKV operand
     if save:
-        keep = (lambda t: t.buf) if pl else (lambda t: t)
-        return h2, (qkv, ctx_, lse, dmask, z1, m1, r1, keep(hin), f1pre, keep(fin), z2, m2, r2, keep(xin), keep(cin))
+        if plb:
+            keep = lambda t: t.buf  # noqa: E731
+            return h2, (qkv, ctx_, lse, dmask, z1, m1, r1, keep(hin), f1pre, keep(fin), z2, m2, r2, keep(xin),
+                        keep(cin))
+        return h2, (qkv, ctx_, lse, dmask, z1, m1, r1, h1, f1pre, f1, z2, m2, r2, x, ctx_)
     return h2, None
 
 
@@ -439,6 +447,8 @@ class FusedBertLayer(torch.autograd.Function):
             x, mask = ctx.saved_tensors[:2]
             saved = ctx.saved_tensors[2:]
         qkv, ctx_, lse, dmask, z1, m1, r1, h1, f1pre, f1, z2, m2, r2, xin, cin = saved
+        if getattr(W, "planes", False) and W.bwd is not W:
+            W = W.bwd  # forward-only planes: the backward on the in-kernel-split engine (fp32 operands)
         pl = getattr(W, "planes", False)
         if pl:  # GEMM operands saved as split planes
             h1, f1, xin, cin = (_planes_of(t) for t in (h1, f1, xin, cin))

@@ -155,13 +155,26 @@ class Planes(object):
 
 def planes_enabled():
     """fp32 GEMMs on pre-split planes (HETSEQ_GEMM_PLANES=0 keeps the in-kernel-split x6 engine)."""
-    return _PLANES and _FP32 == "x6" and _MODE != "blas"
+    return _PLANES != "off" and _FP32 == "x6" and _MODE != "blas"
 
 
-# fp32 GEMMs on pre-split planes are opt-in: on the BERT-base shapes the in-kernel-split engine is
-# faster for the forward / data-gradient products and the planes win only the weight gradients,
-# by less than the standalone split passes cost (profiles/r2_gemm_engines.md)
-_PLANES = os.environ.get("HETSEQ_GEMM_PLANES", "0") == "1"
+def planes_backward():
+    """The backward's GEMMs on the plane engine too (HETSEQ_GEMM_PLANES=1), or only the forward's
+    (HETSEQ_GEMM_PLANES=fwd: the backward stays on the in-kernel-split engine, whose blocks share
+    CUs with the weight-gradient side stream's -- profiles/r3_gemm_ring.md)."""
+    return planes_enabled() and _PLANES == "all"
+
+
+def set_planes_mode(mode):
+    """'off' | 'fwd' | 'all' (tests / benchmarks; takes effect for weights built afterwards)."""
+    global _PLANES
+    assert mode in ("off", "fwd", "all")
+    _PLANES = mode
+
+
+# HETSEQ_GEMM_PLANES: 0 (in-kernel-split engine everywhere), fwd (forward products on the ring
+# plane kernel, fed by producers that emit planes), 1 (every product on planes)
+_PLANES = {"0": "off", "1": "all", "all": "all", "fwd": "fwd"}.get(os.environ.get("HETSEQ_GEMM_PLANES", "0"), "off")
 
 
 # Tensors whose split-bf16 planes a producer kernel already wrote (an LN forward emitting its
@@ -634,12 +647,13 @@ def linear_wgrad(dy, x, out=None, accumulate=False, ksplit=None):
                 ksplit=ksplit)
 
 
-def linear_gelu_fwd(x, w, b, planes_out=False):
+def linear_gelu_fwd(x, w, b, planes_out=False, emit_planes=False):
     """FFN-in forward: pre = x @ w^T (un-biased, kept for the backward), y = gelu(pre + b).
 
     Returns (y, pre).  One fused HIP GEMM (epilogue writes both) or library GEMM + bias_gelu kernel.
     ``planes_out`` (fp32 plane engine): y is returned as split-bf16 :class:`Planes` written by the
-    epilogue (no fp32 copy).
+    epilogue (no fp32 copy).  ``emit_planes``: y fp32 AND its planes from the same epilogue, the
+    planes left for :func:`split_cached` (forward-only plane mode: the backward reads fp32 y).
     """
     from hetseq_amd.ops import bert_ops
 
@@ -653,6 +667,12 @@ def linear_gelu_fwd(x, w, b, planes_out=False):
             yp = torch.empty((3, T, N), dtype=torch.bfloat16, device=px.device)
             if gemm_planes(px, pw, False, True, None, b, EPI_GELU, 0.0, aux=pre, outp=yp):
                 return Planes(yp, T, N, N, T * N, 3), pre
+        if px.P == 3 and emit_planes:
+            y = torch.empty_like(pre)
+            yp = torch.empty((3, T, N), dtype=torch.bfloat16, device=px.device)
+            if gemm_planes(px, pw, False, True, y, b, EPI_GELU, 0.0, aux=pre, outp=yp):
+                remember_planes(y, Planes(yp, T, N, N, T * N, 3))
+                return y, pre
         y = torch.empty_like(pre)
         if gemm_planes(px, pw, False, True, y, b, EPI_GELU, 0.0, aux=pre):
             return (split(y) if planes_out else y), pre

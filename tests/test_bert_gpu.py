@@ -141,7 +141,7 @@ def test_fp32_plane_engine_matches_reference(cuda, monkeypatch):
     from hetseq_amd.ops import gemm as G
     from hetseq_amd.runtime.flat import FlatParamStore
 
-    monkeypatch.setattr(G, "_PLANES", True)
+    monkeypatch.setattr(G, "_PLANES", "all")
     model, cfg = _tiny(cuda)
     model.eval()
     model.max_predictions_per_seq = 32  # 4 x 32 = 128 masked-LM rows: the transform GEMMs tile
@@ -182,10 +182,11 @@ def _grad_report(model, ref):
     return worst, where
 
 
-@pytest.mark.parametrize("planes", [False, True])
+@pytest.mark.parametrize("planes", ["off", "fwd", "all"])
 def test_bert_base_shape_matches_reference_1e4(cuda, monkeypatch, planes):
     """BERT-base (H 768, L 12, 12 heads, S 128, B 8), dropout off: the fused fp32 path -- in-kernel
-    split engine, or split-bf16 planes on the ring kernel -- against the fp32 torch-op oracle (the
+    split engine, split-bf16 planes on the ring kernel for the forward only or for every product --
+    against the fp32 torch-op oracle (the
     reference module graph, bert_modeling.py:819-888).  Loss to 1e-5 relative; every parameter's
     gradient within 1e-4 of the oracle's largest gradient entry of that parameter."""
     from hetseq_amd.models.bert import BertConfig, BertForPreTraining
@@ -201,7 +202,7 @@ def test_bert_base_shape_matches_reference_1e4(cuda, monkeypatch, planes):
     ref = copy.deepcopy(model)
     store = FlatParamStore(model)
     model.attach_store(store, torch.float32)
-    assert (store.planes is not None) == planes
+    assert (store.planes is not None) == (planes != "off")
     batch = _batch(cuda, 8, 128, cfg.vocab_size, P=20)
     assert model.bert._can_fuse(batch[0])
     l1 = model(*batch)
