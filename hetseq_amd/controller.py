@@ -34,6 +34,7 @@ import torch.distributed as dist
 
 from hetseq_amd import checkpoint_utils, utils
 from hetseq_amd.meters import AverageMeter, StopwatchMeter, TimeMeter
+from hetseq_amd.ops._C import hip, stream_handle
 from hetseq_amd.optim import build_lr_scheduler, build_optimizer
 from hetseq_amd.parallel import distributed_utils
 from hetseq_amd.parallel.ddp import BMUF, FlatDDP
@@ -84,6 +85,7 @@ class Controller(object):
         self.fast_stat_sync = args.fast_stat_sync
         self.phase_timer = profiling.PhaseTimer()
         self._graph = None  # runtime.graphs.GraphedStep once --hip-graph captured the update
+        self._scale_buf = None  # fp32 device scalar: the gradient scale of the fast-stat path
         self._graph_warmup = 3  # eager updates first: GEMM autotuning, TunableOp, allocator warm-up
         self.init_meters(args)
 
@@ -249,7 +251,7 @@ class Controller(object):
                 if not ignore_grad:
                     logging_outputs.append(logging_output)
                     sample_sizes.append(sample_size)
-                    if self.fast_stat_sync:
+                    if self.fast_stat_sync and not _stats_accum_fused(stats, sample_size, logging_output):
                         stats[0] += sample_size
                         stats[1] += logging_output.get("nsentences", 0.0)
                         stats[2] += _as_f64(logging_output.get("loss", 0.0), self.device)
@@ -269,13 +271,18 @@ class Controller(object):
                     self.model.all_reduce_(stats)  # native engine: in-stream RCCL, no c10d bookkeeping
                 else:
                     dist.all_reduce(stats)
-            stats[2:4].div_(stats[0:1] * LN2)
+            w = 1.0 if isinstance(self.model, FlatDDP) else float(self.args.distributed_world_size)
+            if stats.is_cuda:  # one launch: division + gradient scale (the step's tail is host-bound)
+                if self._scale_buf is None:
+                    self._scale_buf = torch.empty(1, dtype=torch.float32, device=stats.device)
+                hip().stats_finalize(stats.data_ptr(), LN2, w, self._scale_buf.data_ptr(), stream_handle())
+                scale = self._scale_buf[0]
+            else:
+                stats[2:4].div_(stats[0:1] * LN2)
+                scale = torch.where(stats[0] > 0, w / stats[0].clamp(min=1e-30), torch.ones_like(stats[0])).float()
             sample_size_t = stats[0]
             logging_output = {"nsentences": stats[1], "loss": stats[2], "nll_loss": stats[3], "ntokens": stats[4]}
             ooms = stats[5]
-            w = 1.0 if isinstance(self.model, FlatDDP) else float(self.args.distributed_world_size)
-            scale = torch.where(sample_size_t > 0, w / sample_size_t.clamp(min=1e-30),
-                                torch.ones_like(sample_size_t)).float()
             sample_size_for_meter = sample_size_t
         else:
             if self._sync_stats():
@@ -516,6 +523,24 @@ class Controller(object):
 
     def _sync_stats(self):
         return self.args.distributed_world_size > 1 and dist.is_initialized()
+
+
+def _stats_accum_fused(stats, sample_size, lo):
+    """stats[0..4] += this micro-batch's (sample_size, nsentences, loss, nll_loss, ntokens) in one HIP
+    launch when the losses are fp32 device scalars and the counts host numbers; False otherwise."""
+    if stats is None or not stats.is_cuda:
+        return False
+    vals = [lo.get("nsentences", 0.0), lo.get("ntokens", 0.0), sample_size]
+    losses = [lo.get("loss", 0.0), lo.get("nll_loss", 0.0)]
+    if any(torch.is_tensor(v) for v in vals):
+        return False
+    for t in losses:
+        if not (torch.is_tensor(t) and t.is_cuda and t.dtype == torch.float32 and t.numel() == 1
+                and t.is_contiguous() and t.device == stats.device):
+            return False
+    hip().stats_accum(stats.data_ptr(), losses[0].data_ptr(), losses[1].data_ptr(), float(sample_size),
+                      float(vals[0]), float(vals[1]), stream_handle())
+    return True
 
 
 def _as_f64(v, device):

@@ -20,6 +20,8 @@ using i64 = int64_t;
 
 // optim.hip
 void launch_grad_norm(const float*, int64_t, double*, const float*, float, float*, hipStream_t);
+void launch_stats_accum(double*, const float*, const float*, double, double, double, hipStream_t);
+void launch_stats_finalize(double*, double, double, float*, hipStream_t);
 void launch_adam_flat(float*, const float*, float*, float*, void*, int64_t, const float*, float, float, float, float,
                       float, float, float, float, const float*, hipStream_t);
 void launch_adadelta_flat(float*, const float*, float*, float*, void*, int64_t, const float*, float, float, float,
@@ -152,6 +154,16 @@ PYBIND11_MODULE(_hip, m) {
     pre_launch("grad_norm");
     launch_grad_norm(P(const float*, g), n, P(double*, partial), P(const float*, scale), max_norm, P(float*, out), ST(st));
     check_launch("grad_norm");
+  });
+  m.def("stats_accum", [](i64 st, i64 loss, i64 nll, double ss, double ns, double nt, i64 stream) {
+    pre_launch("stats_accum");
+    launch_stats_accum(P(double*, st), P(const float*, loss), P(const float*, nll), ss, ns, nt, ST(stream));
+    check_launch("stats_accum");
+  });
+  m.def("stats_finalize", [](i64 st, double ln2, double w, i64 scale, i64 stream) {
+    pre_launch("stats_finalize");
+    launch_stats_finalize(P(double*, st), ln2, w, P(float*, scale), ST(stream));
+    check_launch("stats_finalize");
   });
   // betas / rho arrive as Python doubles: 1 - beta is formed in double and rounded once (see optim.hip)
   m.def("adam_flat", [](i64 p, i64 g, i64 mm, i64 v, i64 shadow, i64 n, i64 gmul, float lr, double b1, double b2,

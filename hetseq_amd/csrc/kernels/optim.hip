@@ -254,6 +254,39 @@ static int grid_for(int64_t n_items, int threads, int cap = 4096) {
 
 using namespace hs;
 
+// Fast-stat bookkeeping of the controller (controller.py train_step): one launch per micro-batch
+// instead of the ~8 small torch ops (casts, five in-place adds), one for the end-of-update division
+// and gradient scale instead of ~6 -- the step's tail is host-bound, each launch costs host time.
+// st[0..4] += (sample_size, nsentences, loss, nll_loss, ntokens); loss / nll: fp32 device scalars
+__global__ void stats_accum_kernel(double* __restrict__ st, const float* __restrict__ loss,
+                                   const float* __restrict__ nll, double ss, double ns, double nt) {
+  if (threadIdx.x != 0) return;
+  st[0] += ss;
+  st[1] += ns;
+  st[2] += loss ? static_cast<double>(loss[0]) : 0.0;
+  st[3] += nll ? static_cast<double>(nll[0]) : 0.0;
+  st[4] += nt;
+}
+
+// st[2:4] /= st[0] * ln2 (double, as the torch ops did); scale = st[0] > 0 ? w / max(st[0], 1e-30) : 1
+// computed in double, rounded once to fp32
+__global__ void stats_finalize_kernel(double* __restrict__ st, double ln2, double w, float* __restrict__ scale) {
+  if (threadIdx.x != 0) return;
+  const double s0 = st[0], d = s0 * ln2;
+  st[2] = st[2] / d;
+  st[3] = st[3] / d;
+  scale[0] = static_cast<float>(s0 > 0.0 ? w / (s0 > 1e-30 ? s0 : 1e-30) : 1.0);
+}
+
+void launch_stats_accum(double* st, const float* loss, const float* nll, double ss, double ns, double nt,
+                        hipStream_t stream) {
+  hipLaunchKernelGGL(stats_accum_kernel, dim3(1), dim3(64), 0, stream, st, loss, nll, ss, ns, nt);
+}
+
+void launch_stats_finalize(double* st, double ln2, double w, float* scale, hipStream_t stream) {
+  hipLaunchKernelGGL(stats_finalize_kernel, dim3(1), dim3(64), 0, stream, st, ln2, w, scale);
+}
+
 void launch_grad_norm(const float* g, int64_t n, double* partial, const float* scale, float max_norm, float* out,
                       hipStream_t st) {
   hipLaunchKernelGGL(sumsq_partial_kernel, dim3(kRedBlocks), dim3(kRedThreads), 0, st, g, n, partial);

@@ -327,7 +327,7 @@ class FusedEmbedding(torch.autograd.Function):
         if sink is not None:  # accumulate straight into the flat gradient buffer
             dword, dpos, dtype_, dg, db = sink["views"]()
             if tables is None:
-                streams.wait(dev)  # the tied decoder's weight gradient (side stream) also lands in dword
+                streams.wait_mark(dev, "tied")  # the tied decoder's weight GEMM (side stream) also writes dword
         else:
             dword = torch.zeros((V, H), dtype=torch.float32, device=dev)
             dpos = torch.zeros((P, H), dtype=torch.float32, device=dev)
@@ -652,6 +652,7 @@ class FusedPreTrainingLoss(torch.autograd.Function):
 
         if side:
             dWdec = streams.run(dl_c.device, dwdec, dl_c, t2, lbuf)
+            streams.mark(dl_c.device, "tied")  # the embedding backward waits for this GEMM only
             dbdec = streams.run(dl_c.device, dbias, dlogits, lbuf)
         else:
             dWdec = dwdec()

@@ -183,6 +183,38 @@ def wait(device):
         hip().stream_wait(stream_handle(), s.cuda_stream)
 
 
+_MARKS: dict = {}  # (device index, key) -> event recorded on the side stream in this backward
+
+
+def mark(device, key):
+    """Record an event on the side stream now (e.g. right after the tied decoder's weight GEMM was
+    enqueued), so a later consumer waits for exactly that work (:func:`wait_mark`) instead of for
+    everything the side stream holds by then."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    s = _STREAMS.get(idx)
+    if s is None or not _state["queued"]:
+        return
+    ev = _MARKS.get((idx, key))
+    if ev is None:
+        ev = torch.cuda.Event()
+    ev.record(s)
+    _MARKS[(idx, key)] = ev
+    _MARKED.add((idx, key))
+
+
+_MARKED: set = set()
+
+
+def wait_mark(device, key):
+    """Current stream waits for the event :func:`mark` recorded under ``key`` in this backward (or,
+    without one, for the whole side stream, as :func:`wait`)."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    if (idx, key) in _MARKED:
+        torch.cuda.current_stream(torch.device("cuda", idx)).wait_event(_MARKS[(idx, key)])
+        return
+    wait(device)
+
+
 def join():
     """Make the current stream wait for every side stream (end of backward); release kept inputs."""
     if not _state["queued"] and not _KEEP:
@@ -190,6 +222,7 @@ def join():
     from hetseq_amd.ops._C import hip
 
     _state["queued"] = False
+    _MARKED.clear()
     for idx, s in _STREAMS.items():
         hip().stream_wait(torch._C._cuda_getCurrentRawStream(idx), s.cuda_stream)
     _KEEP.clear()

@@ -1094,3 +1094,35 @@ def test_gemm_ring_epilogues_and_plane_output(cuda):
     _close(dpre, pk.grad, 1e-5, 1e-5, "ring dgelu")
     _close(db, pk.grad.sum(0), 1e-5, 1e-5, "ring dgelu colsum")
     assert torch.equal(dp, G.split(dpre).buf.view(3, T, K))
+
+
+def test_fast_stat_kernels_match_torch_ops(cuda):
+    """stats_accum / stats_finalize (optim.hip) == the controller's torch-op bookkeeping, bit for bit."""
+    import math
+
+    from hetseq_amd.ops._C import hip, stream_handle
+
+    st = torch.zeros(6, dtype=torch.float64, device=cuda)
+    ref = torch.zeros(6, dtype=torch.float64, device=cuda)
+    for i, (ss, ns, nt) in enumerate([(128, 32, 0), (128, 32, 7), (96, 24, 3)]):
+        loss = torch.tensor(3.1 + i, dtype=torch.float32, device=cuda)
+        nll = torch.tensor(2.7 - i, dtype=torch.float32, device=cuda)
+        hip().stats_accum(st.data_ptr(), loss.data_ptr(), nll.data_ptr(), float(ss), float(ns), float(nt),
+                          stream_handle())
+        ref[0] += ss
+        ref[1] += ns
+        ref[2] += loss.double()
+        ref[3] += nll.double()
+        ref[4] += nt
+    ln2 = math.log(2)
+    scale = torch.empty(1, dtype=torch.float32, device=cuda)
+    hip().stats_finalize(st.data_ptr(), ln2, 1.0, scale.data_ptr(), stream_handle())
+    ref[2:4].div_(ref[0:1] * ln2)
+    rs = torch.where(ref[0] > 0, 1.0 / ref[0].clamp(min=1e-30), torch.ones_like(ref[0])).float()
+    torch.cuda.synchronize()
+    assert torch.equal(st, ref), (st, ref)
+    assert torch.equal(scale[0], rs), (scale, rs)
+    z = torch.zeros(6, dtype=torch.float64, device=cuda)  # no samples: scale 1
+    hip().stats_finalize(z.data_ptr(), ln2, 1.0, scale.data_ptr(), stream_handle())
+    torch.cuda.synchronize()
+    assert scale.item() == 1.0
