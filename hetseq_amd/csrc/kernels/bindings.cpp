@@ -32,7 +32,7 @@ void launch_cast_f32_bf16(const float*, void*, int64_t, hipStream_t);
 // layernorm.hip
 int ln_bwd_num_blocks();
 int launch_ln_fwd(int, const void*, const float*, const void*, const float*, const float*, void*, float*, float*,
-                  float*, int, int, float, float, u64, u64, int, void*, int64_t, hipStream_t);
+                  float*, int, int, float, float, u64, u64, int, void*, int64_t, int, int64_t, hipStream_t);
 int launch_ln_bwd(int, const void*, const float*, const float*, const float*, const float*, void*, void*, float*,
                   float*, float*, int, int, float, u64, u64, int, void*, int64_t, hipStream_t);
 int launch_emb_fwd(int, const int64_t*, const int64_t*, const float*, const float*, const float*, const float*,
@@ -60,6 +60,7 @@ int launch_pool_nsp_bwd(int, const float*, const void*, void*, int, int, int, co
 // attention.hip
 void set_attn_fp32_mode(int x6);
 void set_attn_bwd_x6_planes(int on);
+void set_attn_timing(uint64_t* buf);
 int attn_fp32_mode();
 int launch_attn_fwd(int, const void*, const int64_t*, const float*, void*, float*, uint32_t*, int, int, int, int, float,
                     u64, u64, hipStream_t);
@@ -70,6 +71,7 @@ void launch_xent_fwd(int, const void*, const int64_t*, int, int, int64_t, int, f
 void launch_xent_bwd(int, void*, const int64_t*, const float*, int, int, int64_t, int, const float*, const float*,
                      hipStream_t);
 // gemm.hip
+int gemm_last_ksplit();
 int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, int64_t lda, const void* B,
                 int64_t ldb, void* C, int64_t ldc, const float* bias, int epi, float beta, float* aux, int64_t ldaux,
                 float* part, float* colsum_out, int colsum_acc, int tile_override, hipStream_t st, int ksplit,
@@ -200,15 +202,17 @@ PYBIND11_MODULE(_hip, m) {
 
   m.def("ln_bwd_num_blocks", &ln_bwd_num_blocks);
   m.def("ln_fwd", [](int dt, i64 a, i64 bias, i64 resid, i64 gamma, i64 beta, i64 y, i64 zsave, i64 mean, i64 rstd,
-                     int rows, int H, float eps, float p, u64 seed, u64 off, int mode, i64 st, i64 yp, i64 yps) {
+                     int rows, int H, float eps, float p, u64 seed, u64 off, int mode, i64 st, i64 yp, i64 yps,
+                     int nslab, i64 slab_stride) {
     pre_launch("ln_fwd");
     check(launch_ln_fwd(dt, P(const void*, a), P(const float*, bias), P(const void*, resid), P(const float*, gamma),
                         P(const float*, beta), P(void*, y), P(float*, zsave), P(float*, mean), P(float*, rstd), rows, H,
-                        eps, p, seed, off, mode, P(void*, yp), yps, ST(st)),
+                        eps, p, seed, off, mode, P(void*, yp), yps, nslab, slab_stride, ST(st)),
           "ln_fwd");
   }, py::arg("dt"), py::arg("a"), py::arg("bias"), py::arg("resid"), py::arg("gamma"), py::arg("beta"), py::arg("y"),
      py::arg("zsave"), py::arg("mean"), py::arg("rstd"), py::arg("rows"), py::arg("H"), py::arg("eps"), py::arg("p"),
-     py::arg("seed"), py::arg("off"), py::arg("mode"), py::arg("st"), py::arg("yp") = 0, py::arg("yps") = 0);
+     py::arg("seed"), py::arg("off"), py::arg("mode"), py::arg("st"), py::arg("yp") = 0, py::arg("yps") = 0,
+     py::arg("nslab") = 1, py::arg("slab_stride") = 0);
   m.def("ln_bwd", [](int dt, i64 dy, i64 zsave, i64 mean, i64 rstd, i64 gamma, i64 dz, i64 da, i64 pg, i64 pb, i64 pbias,
                      int rows, int H, float p, u64 seed, u64 off, int mode, i64 st, i64 dap, i64 daps) {
     pre_launch("ln_bwd");
@@ -418,8 +422,11 @@ PYBIND11_MODULE(_hip, m) {
 
   m.def("set_attn_fp32_mode", &set_attn_fp32_mode, "fp32 attention products: 1 split-bf16 (x6), 0 exact-fp32 MFMA");
   m.def("set_attn_bwd_x6_planes", &set_attn_bwd_x6_planes,
-        "fp32 split-bf16 attention backward: 1 plane-image dQ / dKV kernels, 0 fused / gather kernels");
+        "fp32 split-bf16 attention backward: 2 key-block kernel (S <= 128) / plane-image pair, 1 plane-image dQ / dKV "
+        "pair, 0 fused / gather kernels, -1 the HETSEQ_ATTN_BWD_X6 default");
   m.def("attn_fp32_mode", &attn_fp32_mode);
+  m.def("set_attn_timing", [](i64 buf) { set_attn_timing(P(uint64_t*, buf)); },
+        "diagnostic: buffer of 16 uint64 per block for the key-block backward's phase clock stamps (0 = off)");
   m.def("attn_fwd", [](int dt, i64 qkv, i64 mask, i64 bqkv, i64 ctx, i64 lse, i64 dmask, int B, int S, int NH, int D,
                        float p, u64 seed, u64 off, i64 st) {
     pre_launch("attn_fwd");
@@ -466,6 +473,8 @@ PYBIND11_MODULE(_hip, m) {
       throw std::runtime_error("hipStreamCreateWithPriority failed");
     return reinterpret_cast<i64>(s);
   });
+  m.def("gemm_last_ksplit", &gemm_last_ksplit,
+        "K slices of the last split-bf16 GEMM launch (with C = 0 its partials stay in the slab)");
   m.def("gemm", [](int dt, int ta, int tb, int M, int N, int K, i64 A, i64 lda, i64 B, i64 ldb, i64 C, i64 ldc, i64 bias,
                    int epi, float beta, i64 aux, i64 ldaux, i64 part, i64 colsum, int colsum_acc, i64 st,
                    int tile, int ksplit, i64 slab, i64 slab_floats, int mv, int nv, int kv) {

@@ -867,7 +867,12 @@ static int pick_tile_split(int M, int N, int K, int* ksplit) {
 // colsum_acc) to colsum_out.  part: scratch of (M/64)*N floats (epi 3 only).
 // ksplit: 0 = automatic (split dtypes only), 1 = none, >1 forced (any dtype); slab: ksplit*M*N floats
 // of scratch when the split is >1 (epi 0/1 only).  mv/nv/kv: valid extents of a padded problem.
+// C == nullptr (no epilogue, split dtypes): the result stays in the slab -- ksplit partial
+// [M][N] planes the consumer sums in slice order (gemm_last_ksplit() says how many), no reduce pass.
 // Returns -1 when the request is not served (caller falls back to the library).
+static thread_local int g_last_ks = 1;
+int gemm_last_ksplit() { return g_last_ks; }
+
 int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, int64_t lda, const void* B,
                 int64_t ldb, void* C, int64_t ldc, const float* bias, int epi, float beta, float* aux, int64_t ldaux,
                 float* part, float* colsum_out, int colsum_acc, int tile_override, hipStream_t st, int ksplit,
@@ -900,6 +905,13 @@ int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, i
     tile = (M % bm == 0 && N % bn == 0) ? tile_override : -1;
   }
   if (tile < 0) return -1;
+  const bool keep_slab = C == nullptr;
+  if (keep_slab && (!nt || epi != kEpiNone || !slab || beta != 0.f)) return -1;  // no bias: the consumer adds it
+  if (keep_slab && ks == 1) {  // one slice: the slab's plane 0 is C
+    if ((int64_t)M * N > slab_floats) return -1;
+    C = slab;
+    ldc = N;
+  }
   if (ks > 1 && (K % (ks * GBK) != 0 || (int64_t)ks * M * N > slab_floats || N % 4 || ldc % 4 || !al16(C)))
     return -1;
   // valid extents of a padded problem (0 = the whole dimension): split-bf16 engine, plain / bias
@@ -922,7 +934,8 @@ int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, i
   else
     rc = launch_split<0>(tile, ta, tb, epi, a, st);
   if (rc != 0) return rc;
-  if (ks > 1) launch_splitk_reduce(slab, ks, M, N, static_cast<float*>(C), ldc, epi >= 1 ? bias : nullptr, beta, a.Mv, a.Nv, st);
+  g_last_ks = ks;
+  if (ks > 1 && !keep_slab) launch_splitk_reduce(slab, ks, M, N, static_cast<float*>(C), ldc, epi >= 1 ? bias : nullptr, beta, a.Mv, a.Nv, st);
   if (epi == kEpiDGelu) {
     const int bm = tile == 2 ? 64 : 128;
     const float* parts[1] = {part};

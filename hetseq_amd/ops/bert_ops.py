@@ -21,9 +21,15 @@ parameters are produced in fp32 (master precision) in both --dtype modes.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from hetseq_amd.ops import gemm as G
+
+# the FFN-out product's split-K partials summed by the LN forward instead of a reduce pass
+# (HETSEQ_LN_PARTIALS=0: reduce in the GEMM as before)
+_LN_PARTIALS = os.environ.get("HETSEQ_LN_PARTIALS", "1") == "1"
 from hetseq_amd.ops._C import dtype_code, hip, stream_handle
 from hetseq_amd.parallel import tied
 from hetseq_amd.runtime import rng, streams
@@ -68,7 +74,14 @@ def _planes_buf(rows, cols, device):
 
 def ln_fwd(a, gamma, beta, eps=1e-12, bias=None, resid=None, p=0.0, mode=0, seed=0, off=0, save_z=True, planes=None):
     """LayerNorm forward (+ bias / dropout / residual in mode 1).  ``planes``: a [3, rows, H] bf16
-    buffer that also receives y as split-bf16 planes (the fp32 GEMM engine's operand format)."""
+    buffer that also receives y as split-bf16 planes (the fp32 GEMM engine's operand format).
+    ``a`` may be [ks, rows, H] split-K partials of the producing GEMM (gemm.linear_fwd_partials),
+    summed in slice order as the GEMM's own reduce pass would."""
+    nslab = 1
+    if a.dim() == 3:
+        nslab = a.shape[0]
+        stride = a.stride(0)
+        a = a[0]
     rows, H = a.shape
     assert H in LN_WIDTHS and a.is_contiguous() and (resid is None or resid.shape == a.shape)
     y = torch.empty_like(a)
@@ -79,7 +92,7 @@ def ln_fwd(a, gamma, beta, eps=1e-12, bias=None, resid=None, p=0.0, mode=0, seed
                  resid.data_ptr() if resid is not None else 0, gamma.data_ptr(), beta.data_ptr(), y.data_ptr(),
                  z.data_ptr() if z is not None else 0, mean.data_ptr(), rstd.data_ptr(), rows, H, float(eps), float(p),
                  seed, off, mode, stream_handle(), planes.data_ptr() if planes is not None else 0,
-                 rows * H if planes is not None else 0)
+                 rows * H if planes is not None else 0, nslab, stride if nslab > 1 else 0)
     return y, z, mean, rstd
 
 
@@ -404,7 +417,8 @@ def _layer_forward(x, mask, W, cfg, save):
     else:
         f1, f1pre = G.linear_gelu_fwd(hin, W.w1, W.bi, planes_out=pl)  # f1pre: un-biased pre-activation
         fin = f1
-    o = G.linear_fwd(fin, W.w2)
+    # FFN-out product: its split-K partials go straight into the LN (no reduce pass)
+    o = G.linear_fwd(fin, W.w2) if (pl or not _LN_PARTIALS) else G.linear_fwd_partials(fin, W.w2)[0]
     h2p = _planes_buf(rows, H, x.device) if pl else None
     h2, z2, m2, r2 = ln_fwd(o, W.g2, W.bb2, eps, bias=W.b2, resid=h1, p=p_h, mode=1, seed=s_2, off=o_2, planes=h2p)
     if pl:

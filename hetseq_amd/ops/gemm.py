@@ -636,6 +636,31 @@ def linear_fwd(x, w, bias=None, out=None):
     return gemm(x, w, ta=False, tb=True, out=out, bias=bias, epi=EPI_BIAS if bias is not None else EPI_NONE)
 
 
+def linear_fwd_partials(x, w):
+    """x[T,K] @ w[N,K]^T for a consumer that sums split-K partials itself (the LN forward after the
+    FFN-out product): ``(partials [ks, T, N], ks)`` with the split-bf16 engine's K slices left in the
+    stream's slab -- no reduce pass, the LN reads the slices in the reduce kernel's order, so the
+    result is bitwise the same -- or ``(out, 1)`` from any other path (first, measuring call;
+    library choice; plane operands).  The view aliases the slab: consume it before the next GEMM
+    on this stream."""
+    M, K = x.shape
+    N = w.shape[0]
+    if (_MODE != "blas" and _FP32 != "native" and x.is_cuda and isinstance(x, torch.Tensor)
+            and isinstance(w, torch.Tensor) and _hip_ok(x, w, x)):
+        c = GEMM_CHOICES.get((M, N, K, False, True, EPI_NONE, False))
+        if c is not None and c[0] == "hip":
+            ks = c[3] if len(c) > 3 else 0
+            slab = _slab(M, N, ks, x.device)
+            if slab is not None:
+                rc = hip().gemm(_FP32_DT[_FP32], 0, 1, M, N, K, x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0),
+                                0, N, 0, EPI_NONE, 0.0, 0, 0, 0, 0, 0, stream_handle(), -1, ks, slab.data_ptr(),
+                                slab.numel(), 0, 0, 0)
+                if rc == 0:
+                    n = hip().gemm_last_ksplit()
+                    return slab[:n * M * N].view(n, M, N), n
+    return linear_fwd(x, w), 1
+
+
 def linear_dgrad(dy, w, out=None, accumulate=False, ksplit=None):
     """dy[T,N] @ w[N,K]; accumulate=True adds into ``out``."""
     return gemm(dy, w, ta=False, tb=False, out=out, beta=1.0 if accumulate else 0.0, ksplit=ksplit)

@@ -41,6 +41,31 @@ def test_layernorm_fwd_bwd(cuda, H):
     _close(b.grad, b2.grad, 1e-4, 1e-3, "ln dbeta")
 
 
+def test_ffn_out_partials_into_ln_bitwise(cuda):
+    """FFN-out product with its split-K partials summed by the LN forward (no reduce pass) gives
+    bitwise the LN of the reduced product: same slice order, same bias / dropout / residual."""
+    from hetseq_amd.ops import bert_ops
+    from hetseq_amd.ops import gemm as G
+
+    torch.manual_seed(3)
+    T, H, F_ = 1024, 768, 3072
+    x = torch.randn(T, F_, device=cuda)
+    w = torch.randn(H, F_, device=cuda) * 0.02
+    b = torch.randn(H, device=cuda) * 0.1
+    r = torch.randn(T, H, device=cuda)
+    g = torch.rand(H, device=cuda) + 0.5
+    be = torch.randn(H, device=cuda) * 0.1
+    G.linear_fwd(x, w)  # first call measures the engine and K split
+    parts, n = G.linear_fwd_partials(x, w)
+    if G.GEMM_CHOICES[(T, H, F_, False, True, 0, False)][0] == "hip":
+        assert parts.dim() == 3 and parts.shape[1:] == (T, H) and n == parts.shape[0]
+    y1, z1, m1, r1 = bert_ops.ln_fwd(parts, g, be, bias=b, resid=r, p=0.1, mode=1, seed=5, off=9)
+    y2, z2, m2, r2 = bert_ops.ln_fwd(G.linear_fwd(x, w), g, be, bias=b, resid=r, p=0.1, mode=1, seed=5, off=9)
+    assert torch.equal(y1, y2) and torch.equal(z1, z2) and torch.equal(m1, m2) and torch.equal(r1, r2)
+    ref = x.double() @ w.double().t()
+    _close(parts.sum(0) if parts.dim() == 3 else parts, ref, 1e-5, 1e-5, "partials sum")
+
+
 def test_bias_dropout_residual_ln_nodrop(cuda):
     from hetseq_amd.ops.bert_ops import bias_dropout_residual_ln
 
@@ -230,17 +255,18 @@ def test_attention_fwd_x6_fp32_level(cuda, B, S, NH, p):
 
 @pytest.mark.parametrize("B,S,NH,p", [(2, 128, 12, 0.0), (2, 96, 2, 0.1), (1, 512, 2, 0.0), (2, 192, 2, 0.1),
                                        (3, 64, 4, 0.1), (2, 256, 12, 0.0)])
-@pytest.mark.parametrize("family", ["planes", "fused", "gather"])
+@pytest.mark.parametrize("family", ["keyblock", "planes", "fused", "gather"])
 def test_attention_bwd_x6_fp32_level(cuda, B, S, NH, p, family, monkeypatch):
-    """fp32 backward on split-bf16 products -- the plane-image dQ / dKV pair (default), the fused
-    S <= 128 kernel and the gather dQ / dKV pair -- against the exact-fp32 MFMA backward on the
-    same forward, and against fp64 autograd: error at the exact-fp32 kernel's level."""
+    """fp32 backward on split-bf16 products -- the key-block kernel (default for S <= 128; the
+    plane-image pair above), the plane-image dQ / dKV pair, the fused S <= 128 kernel and the
+    gather dQ / dKV pair -- against the exact-fp32 MFMA backward on the same forward, and against
+    fp64 autograd: error at the exact-fp32 kernel's level."""
     from hetseq_amd.ops import bert_ops
     from hetseq_amd.ops._C import hip
 
     if family == "gather":
         monkeypatch.setenv("HETSEQ_ATTN_BWD", "split")
-    hip().set_attn_bwd_x6_planes(1 if family == "planes" else 0)
+    hip().set_attn_bwd_x6_planes({"keyblock": 2, "planes": 1}.get(family, 0))
     torch.manual_seed(32 + S)
     H = NH * 64
     qkv = torch.randn(B * S, 3 * H, device=cuda)
