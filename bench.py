@@ -70,6 +70,11 @@ def parse():
     # profiling aid: the data-parallel engine (FlatDDP + native RCCL comm stream) on a 1-rank world,
     # so the stream / HW-queue layout of a DP step can be traced on one GPU (profiles/r3_stream_queues.md)
     p.add_argument("--ddp-world1", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--ab", default=None,
+                   help="A/B mode (1 GPU): alternate these runtime variants (comma list of " + ",".join(sorted(_AB))
+                        + ") in --ab-rounds rounds of --steps steps each, one process, and print each variant's "
+                        "median ms per step (interleaving cancels drift in the box's clock / thermal state)")
+    p.add_argument("--ab-rounds", type=int, default=6, help=argparse.SUPPRESS)
     p.add_argument("--gemm-choices", default=None,
                    help="JSON of measured GEMM engine choices: loaded if it exists (no measuring in warm-up), "
                         "else written after the run (profiling runs use it to keep tuning out of the trace)")
@@ -277,6 +282,8 @@ def run_rank(b):
         torch.autograd.set_multithreading_enabled(False)  # backward on this thread, visible to cProfile
         prof = cProfile.Profile()
         prof.enable()
+    if b.ab:
+        return _ab_run(b, ctl, gen)
     ms0 = torch.cuda.memory_stats()
     t0 = time.perf_counter()
     host = 0.0  # host time spent inside train_step (enqueue cost; < ms_per_step means GPU-bound)
@@ -356,6 +363,48 @@ def run_rank(b):
         if getattr(ctl.model, "comm", None) is not None:
             ctl.model.comm.close()
         dist.destroy_process_group()
+    return 0
+
+
+def _set_attn(code):
+    from hetseq_amd.ops._C import hip
+
+    hip().set_attn_bwd_x6_planes(code)
+
+
+def _set_ln_partials(on):
+    from hetseq_amd.ops import bert_ops
+
+    bert_ops._LN_PARTIALS = on
+
+
+# runtime variants for --ab (switches that take effect on the next step without a rebuild)
+_AB = {
+    "attn_k": lambda: _set_attn(2),    # key-block fp32 attention backward (S <= 128)
+    "attn_k1": lambda: _set_attn(3),   # its first version (A/B reference)
+    "attn_p": lambda: _set_attn(1),    # plane-image dQ / dKV pair
+    "lnp_on": lambda: _set_ln_partials(True),    # FFN-out split-K partials summed in the LN forward
+    "lnp_off": lambda: _set_ln_partials(False),  # ... or reduced by the GEMM's own pass
+}
+
+
+def _ab_run(b, ctl, gen):
+    import torch
+
+    names = b.ab.split(",")
+    times = {n: [] for n in names}
+    for r in range(b.ab_rounds):
+        for n in (names if r % 2 == 0 else names[::-1]):  # alternate the order too
+            _AB[n]()
+            ctl.train_step(next(gen))  # one untimed step after a switch
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(b.steps):
+                ctl.train_step(next(gen))
+            torch.cuda.synchronize()
+            times[n].append((time.perf_counter() - t0) / b.steps * 1000)
+    out = {n: {"median_ms": round(sorted(v)[len(v) // 2], 3), "all": [round(x, 3) for x in v]} for n, v in times.items()}
+    sys.stdout.write(json.dumps({"ab": out, "steps_per_segment": b.steps, "rounds": b.ab_rounds}) + "\n")
     return 0
 
 

@@ -963,7 +963,7 @@ __global__ void __launch_bounds__(256, 2)
 constexpr int kKRows = 128;                  // keys per block
 constexpr int kKPlane = kKRows * kPRow;      // 16 KB: one plane of a 128-row image
 constexpr int kKImg = 3 * kKPlane;           // 48 KB
-constexpr int kKSmem = 2 * kKImg + 2 * kPImg + 64 * 4 * 2 + 4 * 64 * 4;
+constexpr int kKSmem = 2 * kKImg + 2 * kPImg + 64 * 4 * 2 + 4 * 64 * 4 + kXD * 4;
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -996,6 +996,34 @@ HS_DEVICE bfx8 ptr16_frag(const char* plb, int c0, int r0, int lane) {
     const char* a = plb + row * kPRow + 16 * ((col >> 3) ^ pswz(row)) + 2 * (col & 7);
     v[jj] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) ps4*)(a));
   }
+  const ps8 u = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w};
+  return __builtin_bit_cast(bfx8, u);
+}
+
+// Lane byte offsets of ptr_frag's two ds_read_b64_tr_b16 per (d0 = 0 / 32, jj) in a 64-d plane image,
+// relative to row q0 (a multiple of 16: the swizzle depends on row bits 1..3 only), so every
+// transposed fragment of a phase is one of four base registers + an immediate offset.
+struct TrBase {
+  int o[2][2];
+};
+HS_DEVICE TrBase tr_base(int lane) {
+  TrBase t;
+  const int l16 = lane & 15, qq = l16 >> 2, pp = l16 & 3, g = lane >> 4;
+#pragma unroll
+  for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int row = 4 * (g >> 1) + 8 * jj + qq, col = 32 * dh + 16 * (g & 1) + 4 * pp;
+      t.o[dh][jj] = row * kPRow + 16 * ((col >> 3) ^ pswz(row)) + 2 * (col & 7);
+    }
+  return t;
+}
+// ptr_frag with the offsets precomputed: plb = plane base + q0 rows
+HS_DEVICE bfx8 ptr_frag_b(const char* plb, const TrBase& t, int dh) {
+  ps4 v[2];
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj)
+    v[jj] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) ps4*)(plb + t.o[dh][jj]));
   const ps8 u = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w};
   return __builtin_bit_cast(bfx8, u);
 }
@@ -1057,6 +1085,357 @@ __global__ void __launch_bounds__(512, 1)
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = w >> 2, wg = w & 3;
+  const int nkw = S >> 5;  // 32-key words of a keep-mask row
+  const bool kactive = 32 * wg < S;
+  const float* rows = qkv + (int64_t)b * S * ld;
+  const float dscale = drop_scale16(drop_thr16(p));
+  // staging unit of this thread: chunk row sr, d = 8 sc8 .. 8 sc8 + 7
+  const int sr = tid >> 3, sc8 = tid & 7;
+  float* const Qb = reinterpret_cast<float*>(Wd + 4 * 64);  // the head's Q bias (64 floats)
+  if (tid < kXD) Qb[tid] = bqkv ? bqkv[h * kXD + tid] : 0.f;
+  auto stage_ptrs = [&](int c0, const float*& qr, const float*& orw, const float*& cr) {
+    const int64_t tok = (int64_t)b * S + c0 + sr;
+    qr = qkv + tok * ld + h * kXD + 8 * sc8;
+    orw = dctx + tok * H + h * kXD + 8 * sc8;
+    cr = ctx + tok * H + h * kXD + 8 * sc8;
+  };
+
+  // ---- prologue: chunk 0's Q / dO / O loads in flight with the K image and the lane's V row
+  StageRegs st;
+  {
+    const float *qr, *orw, *cr;
+    stage_ptrs(0, qr, orw, cr);
+    stage_load(st, qr, orw, cr, sr < S);
+  }
+  {  // K image (biased): rows sr and sr + 64
+    const float* bk = bofs(bqkv, H + h * kXD + 8 * sc8);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = sr + 64 * i;
+      float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // rows past S: zero (phase B sums all 128 keys)
+      if (r < S) ld8(rows + (int64_t)r * ld + H + h * kXD + 8 * sc8, bk, 1.f, v);
+      put_planes(Kimg, kKPlane, r, sc8, v);
+    }
+    if (32 * wg >= S) {  // keys past S: their dS rows stay zero
+      const int row = 32 * wg + (lane >> 1);
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          *reinterpret_cast<uint4*>(Simg + pl * kKPlane + row * kPRow + 16 * (4 * (lane & 1) + j)) = make_uint4(0, 0, 0, 0);
+    }
+  }
+  bfx8 vb[4][3];
+  float madd = 0.f;
+  {
+    const int li = lane & 31, hf = lane >> 5, key = 32 * wg + li;
+    float vr[4][8];
+    if (kactive) {
+      row_frags(rows + (int64_t)key * ld + 2 * H + h * kXD, bofs(bqkv, 2 * H + h * kXD), hf, vr);
+      madd = (1.f - (float)mask[(int64_t)b * S + key]) * -10000.f;
+    } else {
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) vr[s][j] = 0.f;
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) split8(vr[s], vb[s][0], vb[s][1], vb[s][2]);
+  }
+  f32x16 dk0 = {}, dk1 = {}, dv0 = {}, dv1 = {};
+  __syncthreads();  // Qb visible to the staging threads
+
+  for (int c0 = 0; c0 < S; c0 += 64) {
+    const int clen = min(64, S - c0);
+    stamp();
+    // ---- the chunk's staged registers -> Q (biased, * 1/8) / dO plane images, D, lse, keep words.
+    // Nothing written here is read by the previous chunk's dQ phase: no barrier before it.
+    {
+      float v[8];
+      const float* q = reinterpret_cast<const float*>(st.q);
+      const float* o = reinterpret_cast<const float*>(st.o);
+      const float* c = reinterpret_cast<const float*>(st.c);
+      float dsum = 0.f;
+      const float4 b0 = *reinterpret_cast<const float4*>(Qb + 8 * sc8), b1 = *reinterpret_cast<const float4*>(Qb + 8 * sc8 + 4);
+      const float qb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        v[j] = (q[j] + qb[j]) * 0.125f;
+        dsum = fmaf(o[j], c[j], dsum);
+      }
+      if (sr < clen) put_planes(Qimg, kPPlane, sr, sc8, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = o[j];
+      if (sr < clen) put_planes(Oimg, kPPlane, sr, sc8, v);
+      dsum += __shfl_xor(dsum, 1, 64);
+      dsum += __shfl_xor(dsum, 2, 64);
+      dsum += __shfl_xor(dsum, 4, 64);
+      if (sr < clen && sc8 == 0) Ds[sr] = dsum;
+    }
+    if (tid < clen) Ls[tid] = lse[(int64_t)bh * S + c0 + tid];
+    if (p > 0.f && tid < 256) {
+      const int q = tid & 63, kw = tid >> 6;
+      if (q < clen && kw < nkw) Wd[kw * 64 + q] = dmask[((uint64_t)bh * S + c0 + q) * (uint64_t)nkw + kw];
+    }
+    __syncthreads();
+    stamp();
+    // the next chunk's loads fly under this chunk's MFMA phases
+    if (c0 + 64 < S) {
+      const float *qr, *orw, *cr;
+      stage_ptrs(c0 + 64, qr, orw, cr);
+      stage_load(st, qr, orw, cr, c0 + 64 + sr < S);
+    }
+
+    // ---- phase A: S, dP, P, dS, dV^T, dK^T for slice g (rows 32 g .. of the chunk's images)
+    const bool has = c0 + 32 * g < S;
+    if (has && kactive) {
+      const int ln = opaque(lane), li = ln & 31, hf = ln >> 5, key = 32 * wg + li;
+      const int qr = 32 * g;
+      const int sw = pswz(li);  // = pswz(qr + li) = pswz(key): both rows share the chunk swizzle
+      const char* qa = Qimg + (qr + li) * kPRow;
+      const char* ka = Kimg + key * kPRow;
+      f32x16 sc = {}, dp = {};
+      // S then dP: 8 k-steps, each step's fragments read one step ahead of its MFMAs
+      bfx8 fa[2][3], fk[2][3];
+      auto frag_load = [&](int st, bfx8 (&a)[3], bfx8 (&k)[3]) {
+        const int o = 16 * ((2 * (st & 3) + hf) ^ sw);
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+          a[pl] = *reinterpret_cast<const bfx8*>(qa + (st >> 2) * kPImg + pl * kPPlane + o);
+          if (st < 4) k[pl] = *reinterpret_cast<const bfx8*>(ka + pl * kKPlane + o);
+        }
+      };
+      __builtin_amdgcn_sched_barrier(0);
+      frag_load(0, fa[0], fk[0]);
+#pragma unroll
+      for (int st = 0; st < 8; ++st) {
+        if (st + 1 < 8) frag_load(st + 1, fa[(st + 1) & 1], fk[(st + 1) & 1]);
+        if (st < 4)
+          sc = mma6(fa[st & 1], fk[st & 1], sc);
+        else
+          dp = mma6(fa[st & 1], vb[st & 3], dp);
+      }
+      // pinned order: step st + 1's LDS reads issue before step st's six MFMAs
+#define HS_RD(n) __builtin_amdgcn_sched_group_barrier(0x100, n, 0)
+#define HS_MM() __builtin_amdgcn_sched_group_barrier(0x008, 6, 0)
+      HS_RD(6); HS_RD(6); HS_MM(); HS_RD(6); HS_MM(); HS_RD(6); HS_MM(); HS_RD(3); HS_MM();
+      HS_RD(3); HS_MM(); HS_RD(3); HS_MM(); HS_RD(3); HS_MM(); HS_MM();
+#undef HS_RD
+#undef HS_MM
+      __builtin_amdgcn_sched_barrier(0);
+      // P, dS (registers; split into planes), then dV^T / dK^T: 8 units (ks, product), each six
+      // transposed-fragment reads + six MFMAs, reads pinned one unit ahead
+      // P and dS of both k-steps (score registers 8 ks .. 8 ks + 7) split into planes; sc / dp die here
+      bfx8 pb[2][3], sb[2][3];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        float pd[8], ds[8];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {  // runs of four consecutive queries: rows 8 (2 ks + i) + 4 hf + 0..3
+          const int q0 = qr + 8 * (2 * ks + i) + 4 * hf;
+          const float4 L4 = *reinterpret_cast<const float4*>(Ls + q0);
+          const float4 D4 = *reinterpret_cast<const float4*>(Ds + q0);
+          uint4 W4 = make_uint4(0u, 0u, 0u, 0u);
+          if (p > 0.f) W4 = *reinterpret_cast<const uint4*>(Wd + wg * 64 + q0);
+          const float Lv[4] = {L4.x, L4.y, L4.z, L4.w}, Dv[4] = {D4.x, D4.y, D4.z, D4.w};
+          const uint32_t Wv[4] = {W4.x, W4.y, W4.z, W4.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = 8 * ks + 4 * i + e;
+            const float pv = __expf(sc[r] + madd - Lv[e]);
+            const float mk = p > 0.f ? (((Wv[e] >> li) & 1u) ? dscale : 0.f) : 1.f;
+            pd[4 * i + e] = pv * mk;
+            ds[4 * i + e] = pv * (dp[r] * mk - Dv[e]);
+          }
+        }
+        split8(pd, pb[ks][0], pb[ks][1], pb[ks][2]);
+        split8(ds, sb[ks][0], sb[ks][1], sb[ks][2]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // dV^T / dK^T: 8 units (ks, product), each six transposed-fragment reads + six MFMAs, the
+      // reads pinned one unit ahead
+      bfx8 fu[2][3];
+      const TrBase tb = tr_base(ln);
+      auto unit_frag = [&](int u, bfx8 (&f)[3]) {  // u = 4 ks + {dO^T d 0-31, dO^T 32-63, Q^T 0-31, Q^T 32-63}
+        const char* img = ((u & 2) ? Qimg : Oimg) + (qr + 16 * (u >> 2)) * kPRow;
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) f[pl] = ptr_frag_b(img + pl * kPPlane, tb, u & 1);
+      };
+      unit_frag(0, fu[0]);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (u + 1 < 8) unit_frag(u + 1, fu[(u + 1) & 1]);
+        const int ks = u >> 2;
+        switch (u & 3) {
+          case 0: dv0 = mma6(fu[u & 1], pb[ks], dv0); break;
+          case 1: dv1 = mma6(fu[u & 1], pb[ks], dv1); break;
+          case 2: dk0 = mma6(fu[u & 1], sb[ks], dk0); break;
+          default: dk1 = mma6(fu[u & 1], sb[ks], dk1); break;
+        }
+      }
+#define HS_RD() __builtin_amdgcn_sched_group_barrier(0x100, 6, 0)
+#define HS_MM() __builtin_amdgcn_sched_group_barrier(0x008, 6, 0)
+      HS_RD(); HS_RD(); HS_MM(); HS_RD(); HS_MM(); HS_RD(); HS_MM(); HS_RD(); HS_MM();
+      HS_RD(); HS_MM(); HS_RD(); HS_MM(); HS_RD(); HS_MM(); HS_MM();
+#undef HS_RD
+#undef HS_MM
+      __builtin_amdgcn_sched_barrier(0);
+      // dS planes -> the [key][query] image: elements 0..3 of k-step ks are queries 16 ks + 4 hf + 0..3,
+      // 4..7 are 16 ks + 8 + 4 hf + 0..3 (8-B runs of the image row `key`)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+          const uint4 u = __builtin_bit_cast(uint4, sb[ks][pl]);
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            const int col = qr + 16 * ks + 8 * i + 4 * hf;
+            *reinterpret_cast<uint2*>(Simg + pl * kKPlane + key * kPRow + 16 * ((col >> 3) ^ sw) + 2 * (col & 7)) =
+                i == 0 ? make_uint2(u.x, u.y) : make_uint2(u.z, u.w);
+          }
+        }
+    }
+    __syncthreads();
+    stamp();
+
+    // ---- phase B: dQ of slice g = dS K (16 x 16 tiles: q halves x this wave's 16-wide d quarter)
+    if (has) {
+      const int ln = opaque(lane);
+      f32x4 q0acc = {}, q1acc = {};
+      // four 32-key k-steps (keys past S read as zero), each step's 18 transposed reads pinned
+      // ahead of the previous step's 12 MFMAs
+      bfx8 kf[2][3], a0[2][3], a1[2][3];
+      auto qfrag = [&](int ks, bfx8 (&k)[3], bfx8 (&x0)[3], bfx8 (&x1)[3]) {
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+          k[pl] = ptr16_frag(Kimg + pl * kKPlane, 16 * wg, 32 * ks, ln);
+          x0[pl] = ptr16_frag(Simg + pl * kKPlane, 32 * g, 32 * ks, ln);
+          x1[pl] = ptr16_frag(Simg + pl * kKPlane, 32 * g + 16, 32 * ks, ln);
+        }
+      };
+      __builtin_amdgcn_sched_barrier(0);
+      qfrag(0, kf[0], a0[0], a1[0]);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        if (ks + 1 < 4) qfrag(ks + 1, kf[(ks + 1) & 1], a0[(ks + 1) & 1], a1[(ks + 1) & 1]);
+        q0acc = mma16_6(a0[ks & 1], kf[ks & 1], q0acc);
+        q1acc = mma16_6(a1[ks & 1], kf[ks & 1], q1acc);
+      }
+#define HS_RD() __builtin_amdgcn_sched_group_barrier(0x100, 18, 0)
+#define HS_MM() __builtin_amdgcn_sched_group_barrier(0x008, 12, 0)
+      HS_RD(); HS_RD(); HS_MM(); HS_RD(); HS_MM(); HS_RD(); HS_MM(); HS_MM();
+#undef HS_RD
+#undef HS_MM
+      __builtin_amdgcn_sched_barrier(0);
+      // C of a 16x16 tile: lane column = d, rows 4 (lane >> 4) + e = queries
+      float* out = dqkv + ((int64_t)b * S + c0 + 32 * g + 4 * (ln >> 4)) * ld + h * kXD + 16 * wg + (ln & 15);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        out[(int64_t)e * ld] = q0acc[e] * 0.125f;
+        out[(int64_t)(16 + e) * ld] = q1acc[e] * 0.125f;
+      }
+    }
+  }
+  __syncthreads();  // every dQ phase is done with the images: reuse the LDS for the hand-off
+  stamp();
+
+  // ---- dK / dV: group 1 hands its partials to group 0 (fixed order), group 0 stores
+  // the two groups swap halves: group 1 hands its dK partial to group 0, group 0 its dV partial to
+  // group 1 ([register quad][lane] float4 images), each adds the other's half in the fixed order
+  // (group 0 + group 1) and stores it
+  float4* xk = reinterpret_cast<float4*>(smem) + (g * 4 + wg) * 8 * 64 + lane;  // written by group g
+  if (kactive) {
+    const f32x16& s0 = g ? dk0 : dv0;
+    const f32x16& s1 = g ? dk1 : dv1;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      xk[64 * r] = make_float4(s0[4 * r], s0[4 * r + 1], s0[4 * r + 2], s0[4 * r + 3]);
+      xk[64 * (4 + r)] = make_float4(s1[4 * r], s1[4 * r + 1], s1[4 * r + 2], s1[4 * r + 3]);
+    }
+  }
+  __syncthreads();
+  if (!kactive) return;
+  const float4* xo = reinterpret_cast<const float4*>(smem) + ((1 - g) * 4 + wg) * 8 * 64 + lane;  // the other group's
+  f32x16& d0 = g ? dv0 : dk0;
+  f32x16& d1 = g ? dv1 : dk1;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float4 u = xo[64 * r], v = xo[64 * (4 + r)];
+    // group 0's partial first: d = g0 + g1 in both groups
+    if (g == 0) {
+      d0[4 * r] += u.x; d0[4 * r + 1] += u.y; d0[4 * r + 2] += u.z; d0[4 * r + 3] += u.w;
+      d1[4 * r] += v.x; d1[4 * r + 1] += v.y; d1[4 * r + 2] += v.z; d1[4 * r + 3] += v.w;
+    } else {
+      d0[4 * r] = u.x + d0[4 * r]; d0[4 * r + 1] = u.y + d0[4 * r + 1];
+      d0[4 * r + 2] = u.z + d0[4 * r + 2]; d0[4 * r + 3] = u.w + d0[4 * r + 3];
+      d1[4 * r] = v.x + d1[4 * r]; d1[4 * r + 1] = v.y + d1[4 * r + 1];
+      d1[4 * r + 2] = v.z + d1[4 * r + 2]; d1[4 * r + 3] = v.w + d1[4 * r + 3];
+    }
+  }
+  const int li = lane & 31, hf = lane >> 5;
+  float* out = dqkv + ((int64_t)b * S + 32 * wg + li) * ld + h * kXD + (g ? 2 * H : H);
+  store_rows(out, d0, d1, hf, 1.f);
+  stamp();
+}
+
+// ---- A/B reference: the first key-block kernel (round 3 commit 2bf9dab), HETSEQ_ATTN_BWD_X6=1 / mode 3
+// A value the compiler must treat as new at this point: lane-derived LDS addresses are recomputed
+// per phase instead of being hoisted out of the slice loop (and spilled around it).
+HS_DEVICE int opaque_v1(int x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
+// 8 fp32 -> planes at 16-B chunk c of row `row` of a plane image (plane stride ps)
+HS_DEVICE void put_planes_v1(char* img, int ps, int row, int c, const float (&v)[8]) {
+  bfx8 f[3];
+  split8(v, f[0], f[1], f[2]);
+  const int off = row * kPRow + 16 * (c ^ pswz(row));
+#pragma unroll
+  for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<bfx8*>(img + pl * ps + off) = f[pl];
+}
+
+// per-thread staging registers of one 64-query chunk: row t >> 3, 8-wide d chunk t & 7 of Q (raw),
+// dO and O
+struct StageRegsV1 {
+  float4 q[2], o[2], c[2];
+};
+
+HS_DEVICE void stage_load_v1(StageRegsV1& r, const float* qrow, const float* orow, const float* crow, bool ok) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    r.q[i] = ok ? *reinterpret_cast<const float4*>(qrow + 4 * i) : make_float4(0.f, 0.f, 0.f, 0.f);
+    r.o[i] = ok ? *reinterpret_cast<const float4*>(orow + 4 * i) : make_float4(0.f, 0.f, 0.f, 0.f);
+    r.c[i] = ok ? *reinterpret_cast<const float4*>(crow + 4 * i) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+__global__ void __launch_bounds__(512, 1)
+    attn_bwd_x6k_v1_kernel(const float* __restrict__ qkv, const int64_t* __restrict__ mask,
+                        const float* __restrict__ bqkv, const float* __restrict__ ctx,
+                        const float* __restrict__ dctx, const float* __restrict__ lse, float* __restrict__ dqkv, int S,
+                        int NH, float p, const uint32_t* __restrict__ dmask, uint64_t* __restrict__ tbuf) {
+  __shared__ __attribute__((aligned(16))) char smem[kKSmem];
+  // diagnostic phase clock (tools/bench_attention.py --phases): shader-clock stamps of block 0..
+  int tn = 0;
+  auto stamp = [&]() {
+    if (tbuf && threadIdx.x == 0) tbuf[blockIdx.x * 16 + tn] = __builtin_amdgcn_s_memtime();
+    ++tn;
+  };
+  stamp();
+  char* const Kimg = smem;                     // [key][d] planes, 128 rows
+  char* const Qimg = Kimg + kKImg;             // [query of the chunk][d], 64 rows
+  char* const Oimg = Qimg + kPImg;             // dO rows, same layout
+  char* const Simg = Oimg + kPImg;             // dS planes [key][query of the chunk], 128 rows
+  float* const Ls = reinterpret_cast<float*>(Simg + kKImg);
+  float* const Ds = Ls + 64;
+  uint32_t* const Wd = reinterpret_cast<uint32_t*>(Ds + 64);  // [key word][query]
+  const int H = NH * kXD;
+  const int64_t ld = 3 * (int64_t)H;
+  const int bh = blockIdx.x, b = bh / NH, h = bh % NH;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = w >> 2, wg = w & 3;
   const int nkw = S >> 5;
   const bool kactive = 32 * wg < S;
   const float* rows = qkv + (int64_t)b * S * ld;
@@ -1077,11 +1456,11 @@ __global__ void __launch_bounds__(512, 1)
   };
 
   // ---- prologue: chunk 0's Q / dO / O loads in flight with the K image and the lane's V row
-  StageRegs st;
+  StageRegsV1 st;
   {
     const float *qr, *orw, *cr;
     stage_ptrs(0, qr, orw, cr);
-    stage_load(st, qr, orw, cr, sr < S);
+    stage_load_v1(st, qr, orw, cr, sr < S);
   }
   {  // K image (biased): rows sr and sr + 64
     const float* bk = bofs(bqkv, H + h * kXD + 8 * sc8);
@@ -1091,7 +1470,7 @@ __global__ void __launch_bounds__(512, 1)
       if (r < S) {
         float v[8];
         ld8(rows + (int64_t)r * ld + H + h * kXD + 8 * sc8, bk, 1.f, v);
-        put_planes(Kimg, kKPlane, r, sc8, v);
+        put_planes_v1(Kimg, kKPlane, r, sc8, v);
       }
     }
   }
@@ -1130,10 +1509,10 @@ __global__ void __launch_bounds__(512, 1)
         v[j] = (q[j] + qb[j]) * 0.125f;
         dsum = fmaf(o[j], c[j], dsum);
       }
-      if (sr < clen) put_planes(Qimg, kPPlane, sr, sc8, v);
+      if (sr < clen) put_planes_v1(Qimg, kPPlane, sr, sc8, v);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = o[j];
-      if (sr < clen) put_planes(Oimg, kPPlane, sr, sc8, v);
+      if (sr < clen) put_planes_v1(Oimg, kPPlane, sr, sc8, v);
       dsum += __shfl_xor(dsum, 1, 64);
       dsum += __shfl_xor(dsum, 2, 64);
       dsum += __shfl_xor(dsum, 4, 64);
@@ -1150,13 +1529,13 @@ __global__ void __launch_bounds__(512, 1)
     if (c0 + 64 < S) {
       const float *qr, *orw, *cr;
       stage_ptrs(c0 + 64, qr, orw, cr);
-      stage_load(st, qr, orw, cr, c0 + 64 + sr < S);
+      stage_load_v1(st, qr, orw, cr, c0 + 64 + sr < S);
     }
 
     // ---- phase A: S, dP, P, dS, dV^T, dK^T for slice g (rows 32 g .. of the chunk's images)
     const bool has = c0 + 32 * g < S;
     if (has && kactive) {
-      const int ln = opaque(lane), li = ln & 31, hf = ln >> 5, key = 32 * wg + li;
+      const int ln = opaque_v1(lane), li = ln & 31, hf = ln >> 5, key = 32 * wg + li;
       const int qr = 32 * g;
       const int sw = pswz(li);  // = pswz(qr + li) = pswz(key): both rows share the chunk swizzle
       const char* qa = Qimg + (qr + li) * kPRow;
@@ -1237,7 +1616,7 @@ __global__ void __launch_bounds__(512, 1)
 
     // ---- phase B: dQ of slice g = dS K (16 x 16 tiles: q halves x this wave's 16-wide d quarter)
     if (has) {
-      const int ln = opaque(lane);
+      const int ln = opaque_v1(lane);
       f32x4 q0acc = {}, q1acc = {};
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
@@ -1296,12 +1675,14 @@ __global__ void __launch_bounds__(512, 1)
 
 using namespace hs;
 
-// fp32 backward kernel family: HETSEQ_ATTN_BWD_X6=k (key-block kernel for S <= 128, the plane-image
-// dQ / dKV pair above that; default), p (the plane-image pair at every S) or g (fused S <= 128 /
-// gather dQ / dKV pair)
+// fp32 backward kernel family: HETSEQ_ATTN_BWD_X6=p (the plane-image dQ / dKV pair; default), k (key-block
+// kernel for S <= 128, the pair above that), 1 (the key-block kernel's first version) or g (fused
+// S <= 128 / gather dQ / dKV pair).  The key-block kernel is 0.8x the pair's time alone on the chip but
+// takes whole CUs (145 KB LDS, 512 VGPRs a block): beside the weight-gradient side stream the BERT-base
+// step measured 15.65 ms with it vs 15.34 with the pair (bench.py --ab, profiles/r3_attention.md).
 static int g_bwd_planes_env = [] {
   const char* e = std::getenv("HETSEQ_ATTN_BWD_X6");
-  return e && e[0] == 'g' ? 0 : (e && e[0] == 'p' ? 1 : 2);
+  return e && e[0] == 'g' ? 0 : (e && e[0] == 'k' ? 2 : (e && e[0] == '1' ? 3 : 1));
 }();
 static int g_bwd_planes = g_bwd_planes_env;
 // dispatch order of the merged backward's roles: dK / dV blocks first (default) or dQ first
@@ -1320,6 +1701,11 @@ int launch_attn_bwd_x6(const float* qkv, const int64_t* mask, const float* bqkv,
                        const float* lse, float* Dbuf, float* dqkv, const uint32_t* dmask, int B, int S, int NH,
                        int D, float p, bool fused, hipStream_t st) {
   if (D != kXD || S % 32 != 0 || S <= 0 || (p > 0.f && dmask == nullptr)) return -1;
+  if (g_bwd_planes == 3 && S <= kKRows) {
+    hipLaunchKernelGGL(attn_bwd_x6k_v1_kernel, dim3(B * NH), dim3(512), 0, st, qkv, mask, bqkv, ctx, dctx, lse, dqkv,
+                       S, NH, p, dmask, nullptr);
+    return 0;
+  }
   if (g_bwd_planes == 2 && S <= kKRows) {  // key-block kernel: one block per (batch, head)
     hipLaunchKernelGGL(attn_bwd_x6k_kernel, dim3(B * NH), dim3(512), 0, st, qkv, mask, bqkv, ctx, dctx, lse, dqkv, S,
                        NH, p, dmask, g_attn_tbuf);
