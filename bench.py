@@ -378,8 +378,17 @@ def _set_ln_partials(on):
     bert_ops._LN_PARTIALS = on
 
 
+def _set_side_ks(big, small):
+    from hetseq_amd.runtime import streams
+
+    streams.SIDE_KSPLIT, streams.SIDE_KSPLIT_SMALL = big, small
+
+
 # runtime variants for --ab (switches that take effect on the next step without a rebuild)
 _AB = {
+    "wks2": lambda: _set_side_ks(2, 4),  # side-stream weight-gradient K split (default), small products 4
+    "wks1": lambda: _set_side_ks(1, 1),  # no split-K (no reduce pass, fewer longer blocks)
+    "wks1s4": lambda: _set_side_ks(1, 4),
     "attn_k": lambda: _set_attn(2),    # key-block fp32 attention backward (S <= 128)
     "attn_k1": lambda: _set_attn(3),   # its first version (A/B reference)
     "attn_p": lambda: _set_attn(1),    # plane-image dQ / dKV pair
