@@ -384,8 +384,16 @@ def _set_side_ks(big, small):
     streams.SIDE_KSPLIT, streams.SIDE_KSPLIT_SMALL = big, small
 
 
+def _set_flag(mod, name, v):
+    import importlib
+
+    setattr(importlib.import_module(mod), name, v)
+
+
 # runtime variants for --ab (switches that take effect on the next step without a rebuild)
 _AB = {
+    "fsplit_on": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FWD_SPLIT", True),  # half-batch forward chains
+    "fsplit_off": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FWD_SPLIT", False),
     "wks2": lambda: _set_side_ks(2, 4),  # side-stream weight-gradient K split (default), small products 4
     "wks1": lambda: _set_side_ks(1, 1),  # no split-K (no reduce pass, fewer longer blocks)
     "wks1s4": lambda: _set_side_ks(1, 4),

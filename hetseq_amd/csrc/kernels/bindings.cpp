@@ -32,7 +32,7 @@ void launch_cast_f32_bf16(const float*, void*, int64_t, hipStream_t);
 // layernorm.hip
 int ln_bwd_num_blocks();
 int launch_ln_fwd(int, const void*, const float*, const void*, const float*, const float*, void*, float*, float*,
-                  float*, int, int, float, float, u64, u64, int, void*, int64_t, int, int64_t, hipStream_t);
+                  float*, int, int, float, float, u64, u64, int, void*, int64_t, int, int64_t, int, hipStream_t);
 int launch_ln_bwd(int, const void*, const float*, const float*, const float*, const float*, void*, void*, float*,
                   float*, float*, int, int, float, u64, u64, int, void*, int64_t, hipStream_t);
 int launch_emb_fwd(int, const int64_t*, const int64_t*, const float*, const float*, const float*, const float*,
@@ -203,16 +203,16 @@ PYBIND11_MODULE(_hip, m) {
   m.def("ln_bwd_num_blocks", &ln_bwd_num_blocks);
   m.def("ln_fwd", [](int dt, i64 a, i64 bias, i64 resid, i64 gamma, i64 beta, i64 y, i64 zsave, i64 mean, i64 rstd,
                      int rows, int H, float eps, float p, u64 seed, u64 off, int mode, i64 st, i64 yp, i64 yps,
-                     int nslab, i64 slab_stride) {
+                     int nslab, i64 slab_stride, int row0) {
     pre_launch("ln_fwd");
     check(launch_ln_fwd(dt, P(const void*, a), P(const float*, bias), P(const void*, resid), P(const float*, gamma),
                         P(const float*, beta), P(void*, y), P(float*, zsave), P(float*, mean), P(float*, rstd), rows, H,
-                        eps, p, seed, off, mode, P(void*, yp), yps, nslab, slab_stride, ST(st)),
+                        eps, p, seed, off, mode, P(void*, yp), yps, nslab, slab_stride, row0, ST(st)),
           "ln_fwd");
   }, py::arg("dt"), py::arg("a"), py::arg("bias"), py::arg("resid"), py::arg("gamma"), py::arg("beta"), py::arg("y"),
      py::arg("zsave"), py::arg("mean"), py::arg("rstd"), py::arg("rows"), py::arg("H"), py::arg("eps"), py::arg("p"),
      py::arg("seed"), py::arg("off"), py::arg("mode"), py::arg("st"), py::arg("yp") = 0, py::arg("yps") = 0,
-     py::arg("nslab") = 1, py::arg("slab_stride") = 0);
+     py::arg("nslab") = 1, py::arg("slab_stride") = 0, py::arg("row0") = 0);
   m.def("ln_bwd", [](int dt, i64 dy, i64 zsave, i64 mean, i64 rstd, i64 gamma, i64 dz, i64 da, i64 pg, i64 pb, i64 pbias,
                      int rows, int H, float p, u64 seed, u64 off, int mode, i64 st, i64 dap, i64 daps) {
     pre_launch("ln_bwd");

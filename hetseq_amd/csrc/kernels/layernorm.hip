@@ -51,7 +51,7 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const T* __restrict__ a, co
                                                      uint64_t seed, uint64_t off, int mode,
                                                      const uint64_t* __restrict__ seed_dev,
                                                      uint16_t* __restrict__ yp, int64_t yps, int nslab,
-                                                     int64_t slab_stride) {
+                                                     int64_t slab_stride, int row0) {
   constexpr int H = NV * 256;
   const int lane = threadIdx.x & 63;
   const float scale = p < 1.f ? 1.0f / (1.0f - p) : 0.f;
@@ -75,9 +75,9 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const T* __restrict__ a, co
 #pragma unroll
         for (int j = 0; j < 4; ++j) x[k][j] += b[j];
       }
-      if (mode == kBDR && p > 0.f) {
+      if (mode == kBDR && p > 0.f) {  // counter of the element's row in the whole batch (row0: a row slice)
         float m[4];
-        keep4(seed, off, (uint64_t)(base + c) >> 2, p, scale, m);
+        keep4(seed, off, (uint64_t)((int64_t)(row0 + row) * H + c) >> 2, p, scale, m);
 #pragma unroll
         for (int j = 0; j < 4; ++j) x[k][j] *= m[j];
       }
@@ -361,12 +361,12 @@ static const int kLnBwdBlocks = [] {
 template <int NV, typename T>
 void ln_fwd_launch(const void* a, const float* bias, const void* resid, const float* gamma, const float* beta, void* y,
                    float* zsave, float* mean, float* rstd, int rows, float eps, float p, uint64_t seed, uint64_t off,
-                   int mode, uint16_t* yp, int64_t yps, int nslab, int64_t slab_stride, hipStream_t st) {
+                   int mode, uint16_t* yp, int64_t yps, int nslab, int64_t slab_stride, int row0, hipStream_t st) {
   int grid = (rows + 3) / 4;
   if (grid > 4096) grid = 4096;
   hipLaunchKernelGGL((ln_fwd_kernel<NV, T>), dim3(grid), dim3(256), 0, st, (const T*)a, bias, (const T*)resid, gamma,
                      beta, (T*)y, zsave, mean, rstd, rows, eps, p, seed, off, mode, g_seed_dev, yp, yps, nslab,
-                     slab_stride);
+                     slab_stride, row0);
 }
 
 template <int NV, typename T>
@@ -418,15 +418,15 @@ int ln_bwd_num_blocks() { return kLnBwdBlocks; }
 int launch_ln_fwd(int dtype, const void* a, const float* bias, const void* resid, const float* gamma,
                   const float* beta, void* y, float* zsave, float* mean, float* rstd, int rows, int H, float eps,
                   float p, uint64_t seed, uint64_t off, int mode, void* yp, int64_t yps, int nslab,
-                  int64_t slab_stride, hipStream_t st) {
+                  int64_t slab_stride, int row0, hipStream_t st) {
   if (yp && dtype != 0) return -1;  // plane output: fp32 mode only
   if (nslab < 1 || (nslab > 1 && (dtype != 0 || slab_stride < (int64_t)rows * H || slab_stride % 4))) return -1;
   if (dtype == 0) {
     HS_DISPATCH_H(H, (ln_fwd_launch<NV, float>(a, bias, resid, gamma, beta, y, zsave, mean, rstd, rows, eps, p, seed,
-                                               off, mode, (uint16_t*)yp, yps, nslab, slab_stride, st)));
+                                               off, mode, (uint16_t*)yp, yps, nslab, slab_stride, row0, st)));
   } else {
     HS_DISPATCH_H(H, (ln_fwd_launch<NV, bf16_t>(a, bias, resid, gamma, beta, y, zsave, mean, rstd, rows, eps, p, seed,
-                                                off, mode, nullptr, 0, 1, 0, st)));
+                                                off, mode, nullptr, 0, 1, 0, row0, st)));
   }
   return 0;
 }

@@ -72,11 +72,14 @@ def _planes_buf(rows, cols, device):
     return torch.empty((3, rows, cols), dtype=torch.bfloat16, device=device)
 
 
-def ln_fwd(a, gamma, beta, eps=1e-12, bias=None, resid=None, p=0.0, mode=0, seed=0, off=0, save_z=True, planes=None):
+def ln_fwd(a, gamma, beta, eps=1e-12, bias=None, resid=None, p=0.0, mode=0, seed=0, off=0, save_z=True, planes=None,
+           outs=None, row0=0):
     """LayerNorm forward (+ bias / dropout / residual in mode 1).  ``planes``: a [3, rows, H] bf16
     buffer that also receives y as split-bf16 planes (the fp32 GEMM engine's operand format).
     ``a`` may be [ks, rows, H] split-K partials of the producing GEMM (gemm.linear_fwd_partials),
-    summed in slice order as the GEMM's own reduce pass would."""
+    summed in slice order as the GEMM's own reduce pass would.  ``outs`` = (y, z, mean, rstd) buffers to
+    write (row slices of whole-batch tensors); ``row0``: the first row's index in the whole batch
+    (the dropout mask is drawn by whole-batch element index, as the backward regenerates it)."""
     nslab = 1
     if a.dim() == 3:
         nslab = a.shape[0]
@@ -84,15 +87,18 @@ def ln_fwd(a, gamma, beta, eps=1e-12, bias=None, resid=None, p=0.0, mode=0, seed
         a = a[0]
     rows, H = a.shape
     assert H in LN_WIDTHS and a.is_contiguous() and (resid is None or resid.shape == a.shape)
-    y = torch.empty_like(a)
-    z = torch.empty((rows, H), dtype=torch.float32, device=a.device) if save_z else None
-    mean = torch.empty(rows, dtype=torch.float32, device=a.device)
-    rstd = torch.empty_like(mean)
+    if outs is not None:
+        y, z, mean, rstd = outs
+    else:
+        y = torch.empty_like(a)
+        z = torch.empty((rows, H), dtype=torch.float32, device=a.device) if save_z else None
+        mean = torch.empty(rows, dtype=torch.float32, device=a.device)
+        rstd = torch.empty_like(mean)
     hip().ln_fwd(dtype_code(a), a.data_ptr(), bias.data_ptr() if bias is not None else 0,
                  resid.data_ptr() if resid is not None else 0, gamma.data_ptr(), beta.data_ptr(), y.data_ptr(),
                  z.data_ptr() if z is not None else 0, mean.data_ptr(), rstd.data_ptr(), rows, H, float(eps), float(p),
                  seed, off, mode, stream_handle(), planes.data_ptr() if planes is not None else 0,
-                 rows * H if planes is not None else 0, nslab, stride if nslab > 1 else 0)
+                 rows * H if planes is not None else 0, nslab, stride if nslab > 1 else 0, int(row0))
     return y, z, mean, rstd
 
 
@@ -167,17 +173,21 @@ def colsum(x, acc=None):
     return out
 
 
-def attn_fwd(qkv, mask, B, S, NH, p, seed, off, bias=None):
-    """qkv [B*S, 3H] (un-biased projection output if ``bias`` [3H] fp32 is given)."""
+def attn_fwd(qkv, mask, B, S, NH, p, seed, off, bias=None, outs=None):
+    """qkv [B*S, 3H] (un-biased projection output if ``bias`` [3H] fp32 is given).  ``outs`` =
+    (ctx, lse, dmask) buffers to write (slices of whole-batch tensors)."""
     T, H3 = qkv.shape
     H = H3 // 3
     assert T == B * S and H == NH * 64 and S % 32 == 0 and qkv.is_contiguous()
     assert mask.dtype == torch.int64 and mask.shape == (B, S) and mask.is_contiguous()
     assert bias is None or (bias.shape == (H3,) and bias.dtype == torch.float32 and bias.is_contiguous())
-    ctx = torch.empty((T, H), dtype=qkv.dtype, device=qkv.device)
-    lse = torch.empty((B * NH * S,), dtype=torch.float32, device=qkv.device)
-    # 1 keep-bit per attention probability, packed 32 keys per word, for the backward
-    dmask = torch.empty((B * NH * S * (S // 32),), dtype=torch.int32, device=qkv.device) if p > 0 else None
+    if outs is not None:
+        ctx, lse, dmask = outs
+    else:
+        ctx = torch.empty((T, H), dtype=qkv.dtype, device=qkv.device)
+        lse = torch.empty((B * NH * S,), dtype=torch.float32, device=qkv.device)
+        # 1 keep-bit per attention probability, packed 32 keys per word, for the backward
+        dmask = torch.empty((B * NH * S * (S // 32),), dtype=torch.int32, device=qkv.device) if p > 0 else None
     hip().attn_fwd(dtype_code(qkv), qkv.data_ptr(), mask.data_ptr(), bias.data_ptr() if bias is not None else 0,
                    ctx.data_ptr(), lse.data_ptr(), dmask.data_ptr() if dmask is not None else 0, B, S, NH, 64,
                    float(p), seed, off, stream_handle())
@@ -392,12 +402,66 @@ def _planes_of(buf):
     return G.Planes(buf, buf.shape[1], buf.shape[2], buf.shape[2], buf.shape[1] * buf.shape[2], 3)
 
 
+# The fp32 encoder-layer forward runs the batch as two half-batch chains on two streams (the compute
+# stream and streams.fwd2): a single chain leaves the GEMMs' last partial round of tiles on a mostly
+# idle chip (QKV: 576 tiles of 128 x 128 for 512 block slots), and the other half's kernels fill it
+# (12 BERT-base layers 4.96 -> 4.42 ms, tools/fwd_split_probe.py).  HETSEQ_FWD_SPLIT=0 turns it off.
+_FWD_SPLIT = os.environ.get("HETSEQ_FWD_SPLIT", "1") == "1"
+
+
+def _fwd_split_ok(x, mask, W, cfg):
+    B, S = cfg[0], cfg[1]
+    return (_FWD_SPLIT and x.is_cuda and x.dtype == torch.float32 and not getattr(W, "planes", False)
+            and B % 2 == 0 and B * S >= 1024 and streams.enabled() and x.is_contiguous()
+            and not torch.cuda.is_current_stream_capturing())
+
+
+def _layer_forward_split(x, mask, W, cfg, save):
+    """_layer_forward with the batch in two halves on two streams, every op writing its half of the
+    whole-batch tensors (the backward sees the same saved tensors as an unsplit forward).  Dropout:
+    the LN masks by whole-batch element index (``row0``, what the backward regenerates), the second
+    half's attention keep bits from counter offset + 1 (stored for the backward, never regenerated)."""
+    B, S, NH, p_h, p_a, eps, seeds = cfg
+    (s_a, o_a), (s_1, o_1), (s_2, o_2) = seeds
+    rows, H = x.shape
+    F = W.w1.shape[0]
+    dev, f32 = x.device, torch.float32
+    qkv = torch.empty((rows, 3 * H), dtype=f32, device=dev)
+    ctx_ = torch.empty((rows, H), dtype=f32, device=dev)
+    lse = torch.empty((B * NH * S,), dtype=f32, device=dev)
+    dmask = torch.empty((B * NH * S * (S // 32),), dtype=torch.int32, device=dev) if p_a > 0 else None
+    h1, z1, h2, z2 = (torch.empty((rows, H), dtype=f32, device=dev) for _ in range(4))
+    m1, r1, m2, r2 = (torch.empty((rows,), dtype=f32, device=dev) for _ in range(4))
+    f1, f1pre = torch.empty((rows, F), dtype=f32, device=dev), torch.empty((rows, F), dtype=f32, device=dev)
+    hr, hb = rows // 2, B // 2
+    nl, nm = hb * NH * S, hb * NH * S * (S // 32)
+    with streams.fwd_halves(dev) as halves:
+        for h in halves:
+            r = slice(h * hr, (h + 1) * hr)
+            xh = x[r]
+            G.linear_fwd(xh, W.wqkv, out=qkv[r])
+            attn_fwd(qkv[r], mask[h * hb:(h + 1) * hb], hb, S, NH, p_a, s_a, o_a + h, bias=W.bqkv,
+                     outs=(ctx_[r], lse[h * nl:(h + 1) * nl], dmask[h * nm:(h + 1) * nm] if dmask is not None else None))
+            a = G.linear_fwd(ctx_[r], W.wo)
+            ln_fwd(a, W.g1, W.b1, eps, bias=W.bo, resid=xh, p=p_h, mode=1, seed=s_1, off=o_1, row0=h * hr,
+                   outs=(h1[r], z1[r], m1[r], r1[r]))
+            G.linear_gelu_fwd(h1[r], W.w1, W.bi, out=(f1[r], f1pre[r]))
+            o = G.linear_fwd_partials(f1[r], W.w2)[0] if _LN_PARTIALS else G.linear_fwd(f1[r], W.w2)
+            ln_fwd(o, W.g2, W.bb2, eps, bias=W.b2, resid=h1[r], p=p_h, mode=1, seed=s_2, off=o_2, row0=h * hr,
+                   outs=(h2[r], z2[r], m2[r], r2[r]))
+    if save:
+        return h2, (qkv, ctx_, lse, dmask, z1, m1, r1, h1, f1pre, f1, z2, m2, r2, x, ctx_)
+    return h2, None
+
+
 def _layer_forward(x, mask, W, cfg, save):
     """fp32 on the plane engine (``W.planes``): every GEMM operand is split-bf16 planes, written by
     the kernel that produces the tensor where it can -- the LN forwards (h1, h2: h2's planes wait
     in gemm.remember_planes for the next layer), the GELU epilogue (f1, planes only) -- and by a
     split pass for the attention output and the embedding output; saved planes feed the weight
     gradients of the backward."""
+    if _fwd_split_ok(x, mask, W, cfg):
+        return _layer_forward_split(x, mask, W, cfg, save)
     B, S, NH, p_h, p_a, eps, seeds = cfg
     (s_a, o_a), (s_1, o_1), (s_2, o_2) = seeds
     pl = getattr(W, "planes", False)

@@ -99,7 +99,7 @@ def _slab(M, N, ksplit, device):
     weight-gradient side stream -- since those two run GEMMs concurrently."""
     from hetseq_amd.runtime import streams
 
-    key = (device, "side" if streams.is_side(stream_handle()) else "main")
+    key = (device, streams.role(stream_handle()))
     need = 8 * M * N if ksplit <= 0 else ksplit * M * N
     buf = _SLABS.get(key)
     if buf is None or buf.numel() < need:
@@ -672,13 +672,14 @@ def linear_wgrad(dy, x, out=None, accumulate=False, ksplit=None):
                 ksplit=ksplit)
 
 
-def linear_gelu_fwd(x, w, b, planes_out=False, emit_planes=False):
+def linear_gelu_fwd(x, w, b, planes_out=False, emit_planes=False, out=None):
     """FFN-in forward: pre = x @ w^T (un-biased, kept for the backward), y = gelu(pre + b).
 
     Returns (y, pre).  One fused HIP GEMM (epilogue writes both) or library GEMM + bias_gelu kernel.
     ``planes_out`` (fp32 plane engine): y is returned as split-bf16 :class:`Planes` written by the
     epilogue (no fp32 copy).  ``emit_planes``: y fp32 AND its planes from the same epilogue, the
     planes left for :func:`split_cached` (forward-only plane mode: the backward reads fp32 y).
+    ``out`` = (y, pre) buffers to write (fp32 operands; row slices of whole-batch tensors).
     """
     from hetseq_amd.ops import bert_ops
 
@@ -702,8 +703,11 @@ def linear_gelu_fwd(x, w, b, planes_out=False, emit_planes=False):
         if gemm_planes(px, pw, False, True, y, b, EPI_GELU, 0.0, aux=pre):
             return (split(y) if planes_out else y), pre
         x, w = _unplane(x), _unplane(w)
-    pre = torch.empty((T, N), dtype=x.dtype, device=x.device)
-    y = torch.empty_like(pre)
+    if out is not None:
+        y, pre = out
+    else:
+        pre = torch.empty((T, N), dtype=x.dtype, device=x.device)
+        y = torch.empty_like(pre)
     if x.is_cuda and _MODE != "blas" and _hip_ok(x, w, y, b, pre):
         key = (T, N, x.shape[1], "gelu_fwd")
 

@@ -100,6 +100,64 @@ def side(device) -> "torch.cuda.Stream":
     return s
 
 
+_FWD2: dict = {}
+
+
+def fwd2(device) -> "torch.cuda.Stream":
+    """The second forward stream of ``device``: the other half-batch chain of the encoder forward
+    (ops/bert_ops.py ``_layer_forward_split``)."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    s = _FWD2.get(idx)
+    if s is None:
+        s = _new_stream(idx)
+        _FWD2[idx] = s
+    return s
+
+
+def role(stream_handle: int) -> str:
+    """'side', 'fwd2' or 'main': which engine stream a raw handle is (per-role scratch: split-K slabs)."""
+    if any(s.cuda_stream == stream_handle for s in _STREAMS.values()):
+        return "side"
+    if any(s.cuda_stream == stream_handle for s in _FWD2.values()):
+        return "fwd2"
+    return "main"
+
+
+class fwd_halves(object):
+    """``with fwd_halves(dev) as halves: for h in halves: ...`` -- iteration 0 on the current stream,
+    iteration 1 on :func:`fwd2` (forked from the current stream with an event wait); on exit the
+    current stream waits for fwd2.  Tensors the second half allocates come from fwd2's pool."""
+
+    def __init__(self, device):
+        self.device = device
+        self.gen = None
+
+    def __enter__(self):
+        from hetseq_amd.ops._C import hip, stream_handle
+
+        self.st = fwd2(self.device)
+        hip().stream_wait(self.st.cuda_stream, stream_handle())
+        self.gen = self._halves()
+        return self.gen
+
+    def _halves(self):
+        yield 0
+        st = self.st
+        prev = torch._C._cuda_getCurrentStream(st.device_index)
+        torch._C._cuda_setStream(stream_id=st.stream_id, device_index=st.device_index, device_type=st.device_type)
+        try:
+            yield 1
+        finally:
+            torch._C._cuda_setStream(stream_id=prev[0], device_index=prev[1], device_type=prev[2])
+
+    def __exit__(self, *exc):
+        from hetseq_amd.ops._C import hip, stream_handle
+
+        self.gen.close()  # restores the current stream if the loop left early
+        hip().stream_wait(stream_handle(), self.st.cuda_stream)
+        return False
+
+
 def reserve(device):
     """Create the weight-gradient and copy streams of ``device`` now -- before RCCL (torch's process
     group, the native engine) and torch's stream pool create theirs.  HIP hands the first
@@ -110,6 +168,7 @@ def reserve(device):
     if device is None or device.type != "cuda" or not torch.cuda.is_available():
         return
     side(device)
+    fwd2(device)
     copy_stream(device)
 
 
@@ -137,6 +196,8 @@ def engine_streams(device) -> dict:
         out["wgrad"] = _STREAMS[idx].cuda_stream
     if idx in _COPY:
         out["copy"] = _COPY[idx].cuda_stream
+    if idx in _FWD2:
+        out["fwd2"] = _FWD2[idx].cuda_stream
     return out
 
 

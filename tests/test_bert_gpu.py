@@ -295,3 +295,38 @@ def test_lamb_hip_step_matches_cpu_math(cuda):
                            (o1._state["exp_avg_sq"], o2._state["exp_avg_sq"], "v")):
             torch.testing.assert_close(a[covered], b[covered], rtol=2e-6, atol=1e-7,
                                        msg=lambda m: "%s step %d: %s" % (what, step, m))
+
+
+def test_layer_forward_half_batch_streams_match(cuda, monkeypatch):
+    """The encoder layer forward as two half-batch chains on two streams writes the same tensors as
+    the one-chain forward: LN dropout masks drawn by whole-batch element index (the backward
+    regenerates them that way), every saved tensor equal to GEMM tolerance."""
+    from hetseq_amd.models.bert import BertConfig, BertForPreTraining
+    from hetseq_amd.ops import bert_ops
+    from hetseq_amd.runtime.flat import FlatParamStore
+
+    torch.manual_seed(5)
+    cfg = BertConfig(vocab_size_or_config_json_file=512, hidden_size=768, num_hidden_layers=1,
+                     num_attention_heads=12, intermediate_size=3072)
+    model = BertForPreTraining(cfg).cuda()
+    model.attach_store(FlatParamStore(model), torch.float32)
+    W = model.bert.encoder.layer[0]._weights()
+    B, S = 16, 128
+    x = torch.randn(B * S, 768, device=cuda)
+    mask = torch.ones(B, S, dtype=torch.int64, device=cuda)
+    mask[3, 100:] = 0
+    c = (B, S, 12, 0.1, 0.0, 1e-12, ((7, 0), (7, 256), (7, 512)))  # hidden dropout on, attention off
+    monkeypatch.setattr(bert_ops, "_FWD_SPLIT", True)
+    assert bert_ops._fwd_split_ok(x, mask, W, c)
+    h_s, sv_s = bert_ops._layer_forward(x, mask, W, c, save=True)
+    monkeypatch.setattr(bert_ops, "_FWD_SPLIT", False)
+    h_1, sv_1 = bert_ops._layer_forward(x, mask, W, c, save=True)
+    torch.cuda.synchronize()
+    names = ["qkv", "ctx", "lse", "dmask", "z1", "m1", "r1", "h1", "f1pre", "f1", "z2", "m2", "r2", "x", "ctx2"]
+    for n, a, b in zip(names, sv_s, sv_1):
+        if a is None:
+            assert b is None
+            continue
+        tol = 1e-5 * float(b.abs().max()) + 1e-6
+        assert float((a - b).abs().max()) <= tol, n
+    assert float((h_s - h_1).abs().max()) <= 1e-5 * float(h_1.abs().max())  # (a different mask: O(1) apart)
