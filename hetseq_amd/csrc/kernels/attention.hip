@@ -120,7 +120,7 @@ template <typename T>
 __global__ void __launch_bounds__(256, 2)
     attn_fwd_kernel(const T* __restrict__ qkv, const int64_t* __restrict__ mask, const float* __restrict__ bqkv,
                     T* __restrict__ ctx, float* __restrict__ lse, uint32_t* __restrict__ dmask, int S, int NH, float p,
-                    uint64_t seed, uint64_t off, const uint64_t* __restrict__ seed_dev) {
+                    uint64_t seed, uint64_t off, const uint64_t* __restrict__ seed_dev, int bh0) {
   seed = resolve_seed(seed, seed_dev);
   __shared__ __attribute__((aligned(16))) float Ks[kCH * kLD];
   __shared__ __attribute__((aligned(16))) float Vs[kCH * kLD];
@@ -139,7 +139,7 @@ __global__ void __launch_bounds__(256, 2)
   if (active) load_row_half(rows + (int64_t)(q0 + li) * ld + h * kD + hf * 32, boff(bqkv, h * kD + hf * 32), 0.125f, qr);
   f32x16 o0 = {}, o1 = {};
   float m = -1e30f, l = 0.f;
-  const uint64_t erow = ((uint64_t)bh * S + (q0 + li)) * (uint64_t)S;
+  const uint64_t erow = ((uint64_t)(bh0 + bh) * S + (q0 + li)) * (uint64_t)S;  // bh0: a batch slice's first head
 
   for (int c0 = 0; c0 < S; c0 += kCH) {
     const int clen = min(kCH, S - c0);
@@ -617,7 +617,7 @@ using namespace hs;
 
 int launch_attn_fwd_bf16(const void* qkv, const int64_t* mask, const float* bqkv, void* ctx, float* lse,
                          uint32_t* dmask, int B, int S, int NH, int D, float p, uint64_t seed, uint64_t off,
-                         hipStream_t st);
+                         hipStream_t st, int bh0);
 
 int launch_attn_bwd_fused_bf16(const void* qkv, const int64_t* mask, const float* bqkv, const void* ctx,
                                const void* dctx, const float* lse, void* dqkv, const uint32_t* dmask, int B, int S,
@@ -625,7 +625,7 @@ int launch_attn_bwd_fused_bf16(const void* qkv, const int64_t* mask, const float
 
 int launch_attn_fwd_x6(const float* qkv, const int64_t* mask, const float* bqkv, float* ctx, float* lse,
                        uint32_t* dmask, int B, int S, int NH, int D, float p, uint64_t seed, uint64_t off,
-                       hipStream_t st);
+                       hipStream_t st, int bh0);
 
 int launch_attn_bwd_x6(const float* qkv, const int64_t* mask, const float* bqkv, const float* ctx, const float* dctx,
                        const float* lse, float* Dbuf, float* dqkv, const uint32_t* dmask, int B, int S, int NH,
@@ -655,21 +655,24 @@ static bool fused_bwd_enabled() {
 
 // dmask: uint32 keep-bits [B*NH*S*(S/32)] written by the forward when p > 0
 // and read by both backward kernels (required when p > 0).
+// bh0: index of the launch's first (batch, head) in the whole batch -- the dropout keep bits of a
+// batch slice are the ones the whole-batch launch would draw for those heads.
 int launch_attn_fwd(int dtype, const void* qkv, const int64_t* mask, const float* bqkv, void* ctx, float* lse,
                     uint32_t* dmask, int B, int S, int NH, int D, float p, uint64_t seed, uint64_t off,
-                    hipStream_t st) {
-  if (D != kD || S % 32 != 0 || S <= 0) return -1;
+                    hipStream_t st, int bh0) {
+  if (D != kD || S % 32 != 0 || S <= 0 || bh0 < 0) return -1;
   dim3 grid(B * NH, (S + 127) / 128);  // head-major: a head's blocks share one XCD's L2
   if (dtype != 0 && bf16_mfma_enabled())  // bf16 matrix cores (attention_bf16.hip)
-    return launch_attn_fwd_bf16(qkv, mask, bqkv, ctx, lse, dmask, B, S, NH, D, p, seed, off, st);
+    return launch_attn_fwd_bf16(qkv, mask, bqkv, ctx, lse, dmask, B, S, NH, D, p, seed, off, st, bh0);
   if (dtype == 0 && g_attn_fp32_x6)  // fp32 as split-bf16 products (attention_x6.hip)
-    return launch_attn_fwd_x6((const float*)qkv, mask, bqkv, (float*)ctx, lse, dmask, B, S, NH, D, p, seed, off, st);
+    return launch_attn_fwd_x6((const float*)qkv, mask, bqkv, (float*)ctx, lse, dmask, B, S, NH, D, p, seed, off, st,
+                              bh0);
   if (dtype == 0)
     hipLaunchKernelGGL(attn_fwd_kernel<float>, grid, dim3(256), 0, st, (const float*)qkv, mask, bqkv, (float*)ctx,
-                       lse, dmask, S, NH, p, seed, off, g_seed_dev);
+                       lse, dmask, S, NH, p, seed, off, g_seed_dev, bh0);
   else
     hipLaunchKernelGGL(attn_fwd_kernel<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)qkv, mask, bqkv,
-                       (bf16_t*)ctx, lse, dmask, S, NH, p, seed, off, g_seed_dev);
+                       (bf16_t*)ctx, lse, dmask, S, NH, p, seed, off, g_seed_dev, bh0);
   return 0;
 }
 

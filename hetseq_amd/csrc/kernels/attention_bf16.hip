@@ -64,7 +64,7 @@ __global__ void __launch_bounds__(256, 2)
     attn_fwd_bf16_kernel(const bf16_t* __restrict__ qkv, const int64_t* __restrict__ mask,
                          const float* __restrict__ bqkv, bf16_t* __restrict__ ctx, float* __restrict__ lse,
                          uint32_t* __restrict__ dmask, int S, int NH, float p, uint64_t seed, uint64_t off,
-                         const uint64_t* __restrict__ seed_dev) {
+                         const uint64_t* __restrict__ seed_dev, int bh0) {
   seed = resolve_seed(seed, seed_dev);
   __shared__ __attribute__((aligned(16))) uint16_t Ks[kBCH * kKLD];
   __shared__ __attribute__((aligned(16))) uint16_t Vt[kBD * kVLD];
@@ -92,7 +92,7 @@ __global__ void __launch_bounds__(256, 2)
   }
   f32x16 o0 = {}, o1 = {};
   float m = -1e30f, l = 0.f;
-  const uint64_t erow = ((uint64_t)bh * S + (q0 + li)) * (uint64_t)S;
+  const uint64_t erow = ((uint64_t)(bh0 + bh) * S + (q0 + li)) * (uint64_t)S;  // bh0: a batch slice's first head
 
   for (int c0 = 0; c0 < S; c0 += kBCH) {
     const int clen = min(kBCH, S - c0);
@@ -416,11 +416,11 @@ using namespace hs;
 
 int launch_attn_fwd_bf16(const void* qkv, const int64_t* mask, const float* bqkv, void* ctx, float* lse,
                          uint32_t* dmask, int B, int S, int NH, int D, float p, uint64_t seed, uint64_t off,
-                         hipStream_t st) {
+                         hipStream_t st, int bh0) {
   if (D != kBD || S % 32 != 0 || S <= 0) return -1;
   dim3 grid(B * NH, (S + 127) / 128);  // head-major: a head's blocks share one XCD's L2
   hipLaunchKernelGGL(attn_fwd_bf16_kernel, grid, dim3(256), 0, st, (const bf16_t*)qkv, mask, bqkv, (bf16_t*)ctx, lse,
-                     dmask, S, NH, p, seed, off, g_seed_dev);
+                     dmask, S, NH, p, seed, off, g_seed_dev, bh0);
   return 0;
 }
 

@@ -275,7 +275,7 @@ HS_DEVICE bfx8 ptr_frag(const char* img, int pl, int d0, int q0, int lane) {
 __global__ void __launch_bounds__(256, 2)
     attn_fwd_x6_kernel(const float* __restrict__ qkv, const int64_t* __restrict__ mask, const float* __restrict__ bqkv,
                        float* __restrict__ ctx, float* __restrict__ lse, uint32_t* __restrict__ dmask, int S, int NH,
-                       float p, uint64_t seed, uint64_t off, const uint64_t* __restrict__ seed_dev) {
+                       float p, uint64_t seed, uint64_t off, const uint64_t* __restrict__ seed_dev, int bh0) {
   seed = resolve_seed(seed, seed_dev);
   __shared__ __attribute__((aligned(16))) __bf16 Ks[3][kXCH * kXKLD];
   __shared__ __attribute__((aligned(16))) __bf16 Vt[3][kXD * kXVLD];
@@ -303,7 +303,7 @@ __global__ void __launch_bounds__(256, 2)
   }
   f32x16 o0 = {}, o1 = {};
   float m = -1e30f, l = 0.f;
-  const uint64_t erow = ((uint64_t)bh * S + (q0 + li)) * (uint64_t)S;
+  const uint64_t erow = ((uint64_t)(bh0 + bh) * S + (q0 + li)) * (uint64_t)S;  // bh0: a batch slice's first head
 
   for (int c0 = 0; c0 < S; c0 += kXCH) {
     const int clen = min(kXCH, S - c0);
@@ -1735,12 +1735,12 @@ int launch_attn_bwd_x6(const float* qkv, const int64_t* mask, const float* bqkv,
 
 int launch_attn_fwd_x6(const float* qkv, const int64_t* mask, const float* bqkv, float* ctx, float* lse,
                        uint32_t* dmask, int B, int S, int NH, int D, float p, uint64_t seed, uint64_t off,
-                       hipStream_t st) {
+                       hipStream_t st, int bh0) {
   if (D != kXD || S % 32 != 0 || S <= 0) return -1;
   // grid (B*NH, S/128): consecutive blocks are different heads, so (B*NH a multiple of 8) every
   // query block of a head lands on the same XCD and its K / V come through one L2
   dim3 grid(B * NH, (S + 127) / 128);
   hipLaunchKernelGGL(attn_fwd_x6_kernel, grid, dim3(256), 0, st, qkv, mask, bqkv, ctx, lse, dmask, S, NH, p, seed, off,
-                     g_seed_dev);
+                     g_seed_dev, bh0);
   return 0;
 }

@@ -63,7 +63,7 @@ void set_attn_bwd_x6_planes(int on);
 void set_attn_timing(uint64_t* buf);
 int attn_fp32_mode();
 int launch_attn_fwd(int, const void*, const int64_t*, const float*, void*, float*, uint32_t*, int, int, int, int, float,
-                    u64, u64, hipStream_t);
+                    u64, u64, hipStream_t, int);
 int launch_attn_bwd(int, const void*, const int64_t*, const float*, const void*, const void*, const float*, float*,
                     void*, const uint32_t*, int, int, int, int, float, hipStream_t);
 // xent.hip
@@ -428,12 +428,14 @@ PYBIND11_MODULE(_hip, m) {
   m.def("set_attn_timing", [](i64 buf) { set_attn_timing(P(uint64_t*, buf)); },
         "diagnostic: buffer of 16 uint64 per block for the key-block backward's phase clock stamps (0 = off)");
   m.def("attn_fwd", [](int dt, i64 qkv, i64 mask, i64 bqkv, i64 ctx, i64 lse, i64 dmask, int B, int S, int NH, int D,
-                       float p, u64 seed, u64 off, i64 st) {
+                       float p, u64 seed, u64 off, i64 st, int bh0) {
     pre_launch("attn_fwd");
     check(launch_attn_fwd(dt, P(const void*, qkv), P(const int64_t*, mask), P(const float*, bqkv), P(void*, ctx),
-                          P(float*, lse), P(uint32_t*, dmask), B, S, NH, D, p, seed, off, ST(st)),
+                          P(float*, lse), P(uint32_t*, dmask), B, S, NH, D, p, seed, off, ST(st), bh0),
           "attn_fwd");
-  });
+  }, py::arg("dt"), py::arg("qkv"), py::arg("mask"), py::arg("bqkv"), py::arg("ctx"), py::arg("lse"), py::arg("dmask"),
+     py::arg("B"), py::arg("S"), py::arg("NH"), py::arg("D"), py::arg("p"), py::arg("seed"), py::arg("off"),
+     py::arg("st"), py::arg("bh0") = 0);
   m.def("attn_bwd", [](int dt, i64 qkv, i64 mask, i64 bqkv, i64 ctx, i64 dctx, i64 lse, i64 dbuf, i64 dqkv, i64 dmask,
                        int B, int S, int NH, int D, float p, i64 st) {
     pre_launch("attn_bwd");

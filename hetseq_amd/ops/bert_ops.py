@@ -173,9 +173,10 @@ def colsum(x, acc=None):
     return out
 
 
-def attn_fwd(qkv, mask, B, S, NH, p, seed, off, bias=None, outs=None):
+def attn_fwd(qkv, mask, B, S, NH, p, seed, off, bias=None, outs=None, b0=0):
     """qkv [B*S, 3H] (un-biased projection output if ``bias`` [3H] fp32 is given).  ``outs`` =
-    (ctx, lse, dmask) buffers to write (slices of whole-batch tensors)."""
+    (ctx, lse, dmask) buffers to write (slices of whole-batch tensors); ``b0``: the slice's first
+    sequence in the whole batch (its dropout keep bits are the whole-batch launch's)."""
     T, H3 = qkv.shape
     H = H3 // 3
     assert T == B * S and H == NH * 64 and S % 32 == 0 and qkv.is_contiguous()
@@ -190,7 +191,7 @@ def attn_fwd(qkv, mask, B, S, NH, p, seed, off, bias=None, outs=None):
         dmask = torch.empty((B * NH * S * (S // 32),), dtype=torch.int32, device=qkv.device) if p > 0 else None
     hip().attn_fwd(dtype_code(qkv), qkv.data_ptr(), mask.data_ptr(), bias.data_ptr() if bias is not None else 0,
                    ctx.data_ptr(), lse.data_ptr(), dmask.data_ptr() if dmask is not None else 0, B, S, NH, 64,
-                   float(p), seed, off, stream_handle())
+                   float(p), seed, off, stream_handle(), int(b0) * NH)
     return ctx, (lse, dmask)
 
 
@@ -403,7 +404,7 @@ def _planes_of(buf):
 
 
 # The fp32 encoder-layer forward runs the batch as two half-batch chains on two streams (the compute
-# stream and streams.fwd2): a single chain leaves the GEMMs' last partial round of tiles on a mostly
+# stream and streams.fwd2, the idle weight-gradient stream): a single chain leaves the GEMMs' last partial round of tiles on a mostly
 # idle chip (QKV: 576 tiles of 128 x 128 for 512 block slots), and the other half's kernels fill it
 # (12 BERT-base layers 4.96 -> 4.42 ms, tools/fwd_split_probe.py).  HETSEQ_FWD_SPLIT=0 turns it off.
 _FWD_SPLIT = os.environ.get("HETSEQ_FWD_SPLIT", "1") == "1"
@@ -413,14 +414,13 @@ def _fwd_split_ok(x, mask, W, cfg):
     B, S = cfg[0], cfg[1]
     return (_FWD_SPLIT and x.is_cuda and x.dtype == torch.float32 and not getattr(W, "planes", False)
             and B % 2 == 0 and B * S >= 1024 and streams.enabled() and x.is_contiguous()
-            and not torch.cuda.is_current_stream_capturing())
+            and not torch.cuda.is_current_stream_capturing())  # (graphs: one chain; the same dropout masks)
 
 
 def _layer_forward_split(x, mask, W, cfg, save):
     """_layer_forward with the batch in two halves on two streams, every op writing its half of the
-    whole-batch tensors (the backward sees the same saved tensors as an unsplit forward).  Dropout:
-    the LN masks by whole-batch element index (``row0``, what the backward regenerates), the second
-    half's attention keep bits from counter offset + 1 (stored for the backward, never regenerated)."""
+    whole-batch tensors (the backward sees the same saved tensors as an unsplit forward).  Dropout is
+    drawn by whole-batch index (LN: ``row0``, attention: ``b0``): the same masks as one chain."""
     B, S, NH, p_h, p_a, eps, seeds = cfg
     (s_a, o_a), (s_1, o_1), (s_2, o_2) = seeds
     rows, H = x.shape
@@ -440,7 +440,7 @@ def _layer_forward_split(x, mask, W, cfg, save):
             r = slice(h * hr, (h + 1) * hr)
             xh = x[r]
             G.linear_fwd(xh, W.wqkv, out=qkv[r])
-            attn_fwd(qkv[r], mask[h * hb:(h + 1) * hb], hb, S, NH, p_a, s_a, o_a + h, bias=W.bqkv,
+            attn_fwd(qkv[r], mask[h * hb:(h + 1) * hb], hb, S, NH, p_a, s_a, o_a, bias=W.bqkv, b0=h * hb,
                      outs=(ctx_[r], lse[h * nl:(h + 1) * nl], dmask[h * nm:(h + 1) * nm] if dmask is not None else None))
             a = G.linear_fwd(ctx_[r], W.wo)
             ln_fwd(a, W.g1, W.b1, eps, bias=W.bo, resid=xh, p=p_h, mode=1, seed=s_1, off=o_1, row0=h * hr,

@@ -100,27 +100,17 @@ def side(device) -> "torch.cuda.Stream":
     return s
 
 
-_FWD2: dict = {}
-
-
 def fwd2(device) -> "torch.cuda.Stream":
     """The second forward stream of ``device``: the other half-batch chain of the encoder forward
-    (ops/bert_ops.py ``_layer_forward_split``)."""
-    idx = device.index if device.index is not None else torch.cuda.current_device()
-    s = _FWD2.get(idx)
-    if s is None:
-        s = _new_stream(idx)
-        _FWD2[idx] = s
-    return s
+    (ops/bert_ops.py ``_layer_forward_split``).  It IS the weight-gradient side stream: that one has
+    no work during the forward (the previous backward joined it), and a fifth stream would share a
+    hardware queue with a busy one (GPU_MAX_HW_QUEUES = 4: compute, side, comm, copy)."""
+    return side(device)
 
 
 def role(stream_handle: int) -> str:
-    """'side', 'fwd2' or 'main': which engine stream a raw handle is (per-role scratch: split-K slabs)."""
-    if any(s.cuda_stream == stream_handle for s in _STREAMS.values()):
-        return "side"
-    if any(s.cuda_stream == stream_handle for s in _FWD2.values()):
-        return "fwd2"
-    return "main"
+    """'side' or 'main': which engine stream a raw handle is (per-role scratch: split-K slabs)."""
+    return "side" if is_side(stream_handle) else "main"
 
 
 class fwd_halves(object):
@@ -168,7 +158,6 @@ def reserve(device):
     if device is None or device.type != "cuda" or not torch.cuda.is_available():
         return
     side(device)
-    fwd2(device)
     copy_stream(device)
 
 
@@ -196,8 +185,6 @@ def engine_streams(device) -> dict:
         out["wgrad"] = _STREAMS[idx].cuda_stream
     if idx in _COPY:
         out["copy"] = _COPY[idx].cuda_stream
-    if idx in _FWD2:
-        out["fwd2"] = _FWD2[idx].cuda_stream
     return out
 
 

@@ -299,8 +299,9 @@ def test_lamb_hip_step_matches_cpu_math(cuda):
 
 def test_layer_forward_half_batch_streams_match(cuda, monkeypatch):
     """The encoder layer forward as two half-batch chains on two streams writes the same tensors as
-    the one-chain forward: LN dropout masks drawn by whole-batch element index (the backward
-    regenerates them that way), every saved tensor equal to GEMM tolerance."""
+    the one-chain forward: LN and attention dropout masks drawn by whole-batch index (the backward
+    regenerates the LN ones that way; the attention keep bits are bitwise the same), every saved
+    tensor equal to GEMM tolerance."""
     from hetseq_amd.models.bert import BertConfig, BertForPreTraining
     from hetseq_amd.ops import bert_ops
     from hetseq_amd.runtime.flat import FlatParamStore
@@ -315,7 +316,7 @@ def test_layer_forward_half_batch_streams_match(cuda, monkeypatch):
     x = torch.randn(B * S, 768, device=cuda)
     mask = torch.ones(B, S, dtype=torch.int64, device=cuda)
     mask[3, 100:] = 0
-    c = (B, S, 12, 0.1, 0.0, 1e-12, ((7, 0), (7, 256), (7, 512)))  # hidden dropout on, attention off
+    c = (B, S, 12, 0.1, 0.1, 1e-12, ((7, 0), (7, 256), (7, 512)))  # hidden and attention dropout on
     monkeypatch.setattr(bert_ops, "_FWD_SPLIT", True)
     assert bert_ops._fwd_split_ok(x, mask, W, c)
     h_s, sv_s = bert_ops._layer_forward(x, mask, W, c, save=True)
@@ -330,3 +331,4 @@ def test_layer_forward_half_batch_streams_match(cuda, monkeypatch):
         tol = 1e-5 * float(b.abs().max()) + 1e-6
         assert float((a - b).abs().max()) <= tol, n
     assert float((h_s - h_1).abs().max()) <= 1e-5 * float(h_1.abs().max())  # (a different mask: O(1) apart)
+    assert torch.equal(sv_s[3], sv_1[3])  # attention keep bits
