@@ -392,6 +392,8 @@ def _set_flag(mod, name, v):
 
 # runtime variants for --ab (switches that take effect on the next step without a rebuild)
 _AB = {
+    "dks1": lambda: _set_flag("hetseq_amd.runtime.streams", "DGRAD_KSPLIT", 1),  # data-gradient K split
+    "dks2": lambda: _set_flag("hetseq_amd.runtime.streams", "DGRAD_KSPLIT", 2),
     "fsplit_on": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FWD_SPLIT", True),  # half-batch forward chains
     "fsplit_off": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FWD_SPLIT", False),
     "wks2": lambda: _set_side_ks(2, 4),  # side-stream weight-gradient K split (default), small products 4

@@ -58,16 +58,34 @@ def main():
                 h1, _ = bert_ops._layer_forward(h1, mask[B // 2:], W, c, save=True)
         cur.wait_stream(s2)
 
+    s3, s4 = torch.cuda.Stream(), torch.cuda.Stream()
+
+    def split4():  # four quarter-batch chains on four streams
+        cur = torch.cuda.current_stream()
+        sts = [cur, s2, s3, s4]
+        for st in sts[1:]:
+            st.wait_stream(cur)
+        q, qb = B * S // 4, B // 4
+        c = (qb, S, NH, 0.1, 0.1, 1e-12, seeds)
+        hs = [x[i * q:(i + 1) * q] for i in range(4)]
+        for W in Ws:
+            for i in range(4):
+                with torch.cuda.stream(sts[i]):
+                    hs[i], _ = bert_ops._layer_forward(hs[i], mask[i * qb:(i + 1) * qb], W, c, save=True)
+        for st in sts[1:]:
+            cur.wait_stream(st)
+
     def half_only():
         run(x[:B * S // 2], mask[:B // 2], B // 2)
 
-    for fn in (full, split, half_only):
+    bert_ops._FWD_SPLIT = False  # the probe does its own splitting
+    for fn in (full, split, split4, half_only):
         for _ in range(3):
             fn()
     torch.cuda.synchronize()
     res = {}
     for rep in range(6):
-        for name, fn in (("full", full), ("split2", split), ("one_half", half_only)):
+        for name, fn in (("full", full), ("split2", split), ("split4", split4), ("one_half", half_only)):
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
             fn()
