@@ -332,3 +332,37 @@ def test_layer_forward_half_batch_streams_match(cuda, monkeypatch):
         assert float((a - b).abs().max()) <= tol, n
     assert float((h_s - h_1).abs().max()) <= 1e-5 * float(h_1.abs().max())  # (a different mask: O(1) apart)
     assert torch.equal(sv_s[3], sv_1[3])  # attention keep bits
+
+
+def test_checkpoint_activations_with_split_forward_matches(cuda):
+    """--checkpoint-activations on the fused path: the backward recomputes each layer's forward (as
+    two half-batch chains, the second on the side stream that already holds the later layers'
+    weight-gradient GEMMs) and must give the stored-activation run's loss and gradients."""
+    from hetseq_amd.ops import bert_ops
+    from hetseq_amd.runtime import streams
+    from hetseq_amd.runtime.flat import FlatParamStore
+
+    old = streams.enabled()
+    streams.set_enabled(True)
+    try:
+        model, cfg = _tiny(cuda, H=256, L=3)
+        model.eval()
+        model.max_predictions_per_seq = 10
+        store = FlatParamStore(model)
+        model.attach_store(store, torch.float32)
+        batch = _batch(cuda, 16, 64, cfg.vocab_size)
+        x = torch.zeros(16 * 64, 256, device=cuda)
+        W = model.bert.encoder.layer[0]._weights()
+        assert bert_ops._fwd_split_ok(x, batch[2], W, (16, 64, 4, 0.0, 0.0, 1e-12, ((0, 0),) * 3))
+        outs = []
+        for ck in (False, True):
+            store.grad.zero_()
+            loss = model(*batch, checkpoint_activations=ck)
+            loss.backward()
+            torch.cuda.synchronize()
+            outs.append((loss.item(), store.grad.clone()))
+        (l0, g0), (l1, g1) = outs
+        assert abs(l0 - l1) <= 1e-6 * abs(l0)
+        assert float((g0 - g1).abs().max()) <= 1e-6 * float(g0.abs().max())
+    finally:
+        streams.set_enabled(old)
