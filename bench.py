@@ -394,6 +394,10 @@ def _set_flag(mod, name, v):
 _AB = {
     "dks1": lambda: _set_flag("hetseq_amd.runtime.streams", "DGRAD_KSPLIT", 1),  # data-gradient K split
     "dks2": lambda: _set_flag("hetseq_amd.runtime.streams", "DGRAD_KSPLIT", 2),
+    "fks_auto": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FWD_KS", None),  # forward chains' K split
+    "fks1": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FWD_KS", 1),
+    "fks2": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FWD_KS", 2),
+    "fks4": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FWD_KS", 4),
     "fsplit_on": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FWD_SPLIT", True),  # half-batch forward chains
     "fsplit_off": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FWD_SPLIT", False),
     "wks2": lambda: _set_side_ks(2, 4),  # side-stream weight-gradient K split (default), small products 4

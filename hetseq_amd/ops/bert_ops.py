@@ -408,6 +408,8 @@ def _planes_of(buf):
 # idle chip (QKV: 576 tiles of 128 x 128 for 512 block slots), and the other half's kernels fill it
 # (12 BERT-base layers 4.96 -> 4.42 ms, tools/fwd_split_probe.py).  HETSEQ_FWD_SPLIT=0 turns it off.
 _FWD_SPLIT = os.environ.get("HETSEQ_FWD_SPLIT", "1") == "1"
+# K split of the half-batch chains' plain GEMMs (None: the per-shape isolated measurement)
+_FWD_KS = None
 
 
 def _fwd_split_ok(x, mask, W, cfg):
@@ -439,14 +441,15 @@ def _layer_forward_split(x, mask, W, cfg, save):
         for h in halves:
             r = slice(h * hr, (h + 1) * hr)
             xh = x[r]
-            G.linear_fwd(xh, W.wqkv, out=qkv[r])
+            G.linear_fwd(xh, W.wqkv, out=qkv[r], ksplit=_FWD_KS)
             attn_fwd(qkv[r], mask[h * hb:(h + 1) * hb], hb, S, NH, p_a, s_a, o_a, bias=W.bqkv, b0=h * hb,
                      outs=(ctx_[r], lse[h * nl:(h + 1) * nl], dmask[h * nm:(h + 1) * nm] if dmask is not None else None))
-            a = G.linear_fwd(ctx_[r], W.wo)
+            a = G.linear_fwd(ctx_[r], W.wo, ksplit=_FWD_KS)
             ln_fwd(a, W.g1, W.b1, eps, bias=W.bo, resid=xh, p=p_h, mode=1, seed=s_1, off=o_1, row0=h * hr,
                    outs=(h1[r], z1[r], m1[r], r1[r]))
             G.linear_gelu_fwd(h1[r], W.w1, W.bi, out=(f1[r], f1pre[r]))
-            o = G.linear_fwd_partials(f1[r], W.w2)[0] if _LN_PARTIALS else G.linear_fwd(f1[r], W.w2)
+            o = (G.linear_fwd_partials(f1[r], W.w2, ksplit=_FWD_KS)[0] if _LN_PARTIALS
+                 else G.linear_fwd(f1[r], W.w2, ksplit=_FWD_KS))
             ln_fwd(o, W.g2, W.bb2, eps, bias=W.b2, resid=h1[r], p=p_h, mode=1, seed=s_2, off=o_2, row0=h * hr,
                    outs=(h2[r], z2[r], m2[r], r2[r]))
     if save:

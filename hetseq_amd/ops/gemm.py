@@ -631,12 +631,13 @@ def _choose_padded(key, run_hip, run_blas):
     return _choose(key, run_hip, run_blas)
 
 
-def linear_fwd(x, w, bias=None, out=None):
+def linear_fwd(x, w, bias=None, out=None, ksplit=None):
     """x[T,K] @ w[N,K]^T (+bias)."""
-    return gemm(x, w, ta=False, tb=True, out=out, bias=bias, epi=EPI_BIAS if bias is not None else EPI_NONE)
+    return gemm(x, w, ta=False, tb=True, out=out, bias=bias, epi=EPI_BIAS if bias is not None else EPI_NONE,
+                ksplit=ksplit)
 
 
-def linear_fwd_partials(x, w):
+def linear_fwd_partials(x, w, ksplit=None):
     """x[T,K] @ w[N,K]^T for a consumer that sums split-K partials itself (the LN forward after the
     FFN-out product): ``(partials [ks, T, N], ks)`` with the split-bf16 engine's K slices left in the
     stream's slab -- no reduce pass, the LN reads the slices in the reduce kernel's order, so the
@@ -649,7 +650,7 @@ def linear_fwd_partials(x, w):
             and isinstance(w, torch.Tensor) and _hip_ok(x, w, x)):
         c = GEMM_CHOICES.get((M, N, K, False, True, EPI_NONE, False))
         if c is not None and c[0] == "hip":
-            ks = c[3] if len(c) > 3 else 0
+            ks = ksplit if ksplit is not None else (c[3] if len(c) > 3 else 0)
             slab = _slab(M, N, ks, x.device)
             if slab is not None:
                 rc = hip().gemm(_FP32_DT[_FP32], 0, 1, M, N, K, x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0),
