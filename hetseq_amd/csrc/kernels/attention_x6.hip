@@ -248,6 +248,35 @@ HS_DEVICE void stage_planes(char* img, const float* base, int64_t ld, int r0, in
   }
 }
 
+// stage_planes for dO rows that also writes D[row] = rowsum(dO o O) of the head (O rows at orows,
+// row stride ld): the four threads of a row (16 d each) reduce their partial dots by shuffles
+template <int NT>
+HS_DEVICE void stage_planes_dsum(char* img, const float* base, const float* obase, int64_t ld, int r0, int n,
+                                 float* Dsm) {
+  for (int u = threadIdx.x; u < 64 * 4; u += NT) {
+    const int row = u >> 2, seg = u & 3;
+    float dsum = 0.f;
+    if (row < n) {
+      float v[2][8], o[8];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        ld8(base + (int64_t)(r0 + row) * ld + 16 * seg + 8 * e, nullptr, 1.f, v[e]);
+        ld8(obase + (int64_t)(r0 + row) * ld + 16 * seg + 8 * e, nullptr, 1.f, o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dsum = fmaf(v[e][j], o[j], dsum);
+        bfx8 f[3];
+        split8(v[e], f[0], f[1], f[2]);
+        const int off = row * kPRow + 16 * ((2 * seg + e) ^ pswz(row));
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<bfx8*>(img + pl * kPPlane + off) = f[pl];
+      }
+    }
+    dsum += __shfl_xor(dsum, 1, 64);
+    dsum += __shfl_xor(dsum, 2, 64);
+    if (row < n && seg == 0) Dsm[row] = dsum;
+  }
+}
+
 // row fragment of plane pl: row `row` (this lane's), 16-B chunk c (= 2 ks + lane half)
 HS_DEVICE bfx8 prow_frag(const char* img, int pl, int row, int c) {
   return *reinterpret_cast<const bfx8*>(img + pl * kPPlane + row * kPRow + 16 * (c ^ pswz(row)));
@@ -704,7 +733,7 @@ HS_DEVICE void dkv_x6p_body(char* __restrict__ smem, int bx, int bh, const float
                             const int64_t* __restrict__ mask, const float* __restrict__ bqkv,
                             const float* __restrict__ dctx, const float* __restrict__ lse,
                             const float* __restrict__ Dd, float* __restrict__ dqkv, int S, int NH, float p,
-                            const uint32_t* __restrict__ dmask) {
+                            const uint32_t* __restrict__ dmask, const float* __restrict__ ctx) {
   char* const Qp = smem;
   char* const Op = smem + kPImg;
   float* const Ls = reinterpret_cast<float*>(smem + 2 * kPImg);
@@ -747,10 +776,15 @@ HS_DEVICE void dkv_x6p_body(char* __restrict__ smem, int bx, int bh, const float
     const int clen = min(64, S - c0);
     __syncthreads();
     stage_planes<256>(Qp, rows + h * kXD, ld, c0, clen, bofs(bqkv, h * kXD), 0.125f);
-    stage_planes<256>(Op, drows + h * kXD, H, c0, clen, nullptr, 1.f);
-    for (int i = threadIdx.x; i < clen; i += blockDim.x) {
-      Ls[i] = lse[(int64_t)bh * S + c0 + i];
-      Ds[i] = Dd[(int64_t)bh * S + c0 + i];
+    if (ctx) {  // D = rowsum(dO o O) of the chunk's queries computed while dO is staged
+      stage_planes_dsum<256>(Op, drows + h * kXD, ctx + (int64_t)b * S * H + h * kXD, H, c0, clen, Ds);
+      for (int i = threadIdx.x; i < clen; i += blockDim.x) Ls[i] = lse[(int64_t)bh * S + c0 + i];
+    } else {
+      stage_planes<256>(Op, drows + h * kXD, H, c0, clen, nullptr, 1.f);
+      for (int i = threadIdx.x; i < clen; i += blockDim.x) {
+        Ls[i] = lse[(int64_t)bh * S + c0 + i];
+        Ds[i] = Dd[(int64_t)bh * S + c0 + i];
+      }
     }
     if (p > 0.f)
       for (int i = threadIdx.x; i < clen * 4; i += blockDim.x) {
@@ -816,7 +850,8 @@ HS_DEVICE void dkv_x6p_body(char* __restrict__ smem, int bx, int bh, const float
 HS_DEVICE void dq_x6p_body(char* __restrict__ smem, int bx, int bh, const float* __restrict__ qkv,
                            const int64_t* __restrict__ mask, const float* __restrict__ bqkv,
                            const float* __restrict__ dctx, const float* __restrict__ lse, const float* __restrict__ Dd,
-                           float* __restrict__ dqkv, int S, int NH, float p, const uint32_t* __restrict__ dmask) {
+                           float* __restrict__ dqkv, int S, int NH, float p, const uint32_t* __restrict__ dmask,
+                           const float* __restrict__ ctx) {
   char* const Kp = smem;
   char* const Vp = smem + kPImg;
   float* const Ms = reinterpret_cast<float*>(smem + 2 * kPImg);
@@ -840,12 +875,19 @@ HS_DEVICE void dq_x6p_body(char* __restrict__ smem, int bx, int bh, const float*
       const int d = 16 * s + 8 * hf;
       ld8(rows + (int64_t)(q0 + li) * ld + h * kXD + d, bofs(bqkv, h * kXD + d), 0.125f, qr);
       ld8(dctx + tok * H + h * kXD + d, nullptr, 1.f, dor);
+      if (ctx) {  // D = rowsum(dO o O): this lane's half of the row, the other half from lane ^ 32
+        float o[8];
+        ld8(ctx + tok * H + h * kXD + d, nullptr, 1.f, o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dsum = fmaf(dor[j], o[j], dsum);
+      }
     }
     split8(qr, qb[s][0], qb[s][1], qb[s][2]);
     split8(dor, ob[s][0], ob[s][1], ob[s][2]);
   }
+  if (ctx) dsum += __shfl_xor(dsum, 32, 64);
   if (active) {
-    dsum = Dd[(int64_t)bh * S + q0 + li];
+    if (!ctx) dsum = Dd[(int64_t)bh * S + q0 + li];
     lq = lse[(int64_t)bh * S + q0 + li];
   }
   f32x16 dq0 = {}, dq1 = {};
@@ -931,16 +973,19 @@ __global__ void __launch_bounds__(256, 2)
     attn_bwd_x6p_kernel(const float* __restrict__ qkv, const int64_t* __restrict__ mask,
                         const float* __restrict__ bqkv, const float* __restrict__ dctx,
                         const float* __restrict__ lse, const float* __restrict__ Dd, float* __restrict__ dqkv, int S,
-                        int NH, float p, const uint32_t* __restrict__ dmask, int dkv_first) {
+                        int NH, float p, const uint32_t* __restrict__ dmask, int dkv_first,
+                        const float* __restrict__ ctx) {
+  // ctx != nullptr: both roles compute D = rowsum(dO o O) themselves (no attn_bwd_dsum pass; S <= 128,
+  // where each head's one dK / dV block stages every query once)
   __shared__ __attribute__((aligned(16))) char smem[kBwdSmem];
   // grid (B*NH, 2 * nq): blocks dispatch x-fastest, so every head's dK / dV blocks (the longer
   // role) go out before the dQ ones and the shorter blocks fill the tail of the last round
   const int nq = (S + 127) / 128, bh = blockIdx.x;
   const int y = blockIdx.y, first = y < nq, g = first ? y : y - nq;  // role group, block in the role
   if (first == (dkv_first != 0))
-    dkv_x6p_body(smem, g, bh, qkv, mask, bqkv, dctx, lse, Dd, dqkv, S, NH, p, dmask);
+    dkv_x6p_body(smem, g, bh, qkv, mask, bqkv, dctx, lse, Dd, dqkv, S, NH, p, dmask, ctx);
   else
-    dq_x6p_body(smem, g, bh, qkv, mask, bqkv, dctx, lse, Dd, dqkv, S, NH, p, dmask);
+    dq_x6p_body(smem, g, bh, qkv, mask, bqkv, dctx, lse, Dd, dqkv, S, NH, p, dmask, ctx);
 }
 
 // ---------------------------------------------------------------------------
@@ -1691,6 +1736,12 @@ static const int g_bwd_dkv_first = [] {
   const char* e = std::getenv("HETSEQ_ATTN_BWD_DKV_FIRST");
   return e && e[0] == '0' ? 0 : 1;
 }();
+// the plane pair computes D itself at S <= 128 (HETSEQ_ATTN_BWD_DSUM=1: the separate attn_bwd_dsum pass)
+static int g_bwd_fused_d = [] {
+  const char* e = std::getenv("HETSEQ_ATTN_BWD_DSUM");
+  return e && e[0] == '1' ? 0 : 1;
+}();
+void set_attn_bwd_fused_d(int on) { g_bwd_fused_d = on; }
 // diagnostic: per-block shader-clock stamps of the key-block backward (16 per block; nullptr = off)
 static uint64_t* g_attn_tbuf = nullptr;
 void set_attn_timing(uint64_t* buf) { g_attn_tbuf = buf; }
@@ -1711,13 +1762,16 @@ int launch_attn_bwd_x6(const float* qkv, const int64_t* mask, const float* bqkv,
                        NH, p, dmask, g_attn_tbuf);
     return 0;
   }
-  if (g_bwd_planes) {  // plane-image kernels: D, then both roles in one launch
-    const int64_t units = (int64_t)B * S * NH;
-    hipLaunchKernelGGL(attn_bwd_dsum_kernel, dim3((unsigned)((units + 15) / 16)), dim3(256), 0, st, ctx, dctx, Dbuf, B,
-                       S, NH);
+  if (g_bwd_planes) {  // plane-image kernels: D (in the roles for S <= 128), both roles in one launch
+    const bool fused_d = g_bwd_fused_d && S <= 128;
+    if (!fused_d) {
+      const int64_t units = (int64_t)B * S * NH;
+      hipLaunchKernelGGL(attn_bwd_dsum_kernel, dim3((unsigned)((units + 15) / 16)), dim3(256), 0, st, ctx, dctx, Dbuf,
+                         B, S, NH);
+    }
     dim3 grid(B * NH, 2 * ((S + 127) / 128));
     hipLaunchKernelGGL(attn_bwd_x6p_kernel, grid, dim3(256), 0, st, qkv, mask, bqkv, dctx, lse, Dbuf, dqkv, S, NH, p,
-                       dmask, g_bwd_dkv_first);
+                       dmask, g_bwd_dkv_first, fused_d ? ctx : nullptr);
     return 0;
   }
   if (fused && S <= 128) {
