@@ -406,6 +406,8 @@ _AB = {
     "attn_k": lambda: _set_attn(2),    # key-block fp32 attention backward (S <= 128)
     "attn_k1": lambda: _set_attn(3),   # its first version (A/B reference)
     "attn_p": lambda: _set_attn(1),    # plane-image dQ / dKV pair
+    "afwd_p": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_fwd_x6_planes(1),
+    "afwd_old": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_fwd_x6_planes(0),
     "dsum_in": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_bwd_fused_d(1),
     "dsum_sep": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_bwd_fused_d(0),
     "lnp_on": lambda: _set_ln_partials(True),    # FFN-out split-K partials summed in the LN forward

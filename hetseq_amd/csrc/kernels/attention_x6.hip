@@ -1423,6 +1423,160 @@ __global__ void __launch_bounds__(512, 1)
   stamp();
 }
 
+// ---------------------------------------------------------------------------
+// Forward on plane images ("p" forward, fp32 default): attn_fwd_x6_kernel's algorithm (a wave owns
+// 32 queries, S^T tiles with the key on the registers, online softmax, the same keep bits) with
+// the backward kernels' operand staging: each 64-key chunk of K and of V is split once into
+// [key][64 d] plane images (16-B b128 stores, the pswz swizzle) -- S = K Q^T reads K fragments by
+// rows, P V reads V^T fragments transposed (ds_read_b64_tr_b16) from the same row-major image.
+// The first x6 forward staged V^T by 2-byte scalar stores (48 per thread and chunk, 28 % LDS bank
+// conflicts).  The next chunk's K / V rows are loaded under the current chunk's MFMAs.  48 KB LDS.
+__global__ void __launch_bounds__(256, 2)
+    attn_fwd_x6p_kernel(const float* __restrict__ qkv, const int64_t* __restrict__ mask,
+                        const float* __restrict__ bqkv, float* __restrict__ ctx, float* __restrict__ lse,
+                        uint32_t* __restrict__ dmask, int S, int NH, float p, uint64_t seed, uint64_t off,
+                        const uint64_t* __restrict__ seed_dev, int bh0) {
+  seed = resolve_seed(seed, seed_dev);
+  __shared__ __attribute__((aligned(16))) char smem[2 * kPImg];
+  __shared__ float Ms[kXCH];
+  __shared__ __attribute__((aligned(16))) float KVb[2 * kXD];  // K and V bias of the head
+  char* const Kimg = smem;
+  char* const Vimg = smem + kPImg;
+  const int H = NH * kXD;
+  const int64_t ld = 3 * (int64_t)H;
+  const int bh = blockIdx.x, b = bh / NH, h = bh % NH;
+  const int tid = threadIdx.x, lane = tid & 63, hf = lane >> 5, li = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q0 = blockIdx.y * 128 + w * 32;
+  const bool active = q0 < S;
+  const float* rows = qkv + (int64_t)b * S * ld;
+  const uint32_t thr = drop_thr16(p);
+  const float dscale = drop_scale16(thr);
+  if (tid < 2 * kXD) KVb[tid] = bqkv ? bqkv[(1 + (tid >> 6)) * H + h * kXD + (tid & 63)] : 0.f;
+
+  // the lane's Q row, dims 16s + 8hf + j (k-step s), biased, * 1/sqrt(64) (exact), split
+  bfx8 qf[4][3];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const int d = 16 * s + 8 * hf;
+    if (active) ld8(rows + (int64_t)(q0 + li) * ld + h * kXD + d, bofs(bqkv, h * kXD + d), 0.125f, v);
+    split8(v, qf[s][0], qf[s][1], qf[s][2]);
+  }
+  f32x16 o0 = {}, o1 = {};
+  float m = -1e30f, l = 0.f;
+  const uint64_t erow = ((uint64_t)(bh0 + bh) * S + (q0 + li)) * (uint64_t)S;  // bh0: a batch slice's first head
+
+  // staging units of this thread: (key row u >> 3, 8-d chunk u & 7) for u = tid, tid + 256, of K and V
+  float4 kv[2][2][2];  // [K / V][unit][half]
+  auto load = [&](int c0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int u = tid + 256 * i, r = u >> 3, c8 = (u & 7) * 8;
+      const bool ok = c0 + r < S;
+#pragma unroll
+      for (int kvs = 0; kvs < 2; ++kvs) {
+        const float* src = rows + (int64_t)(c0 + r) * ld + (1 + kvs) * H + h * kXD + c8;
+        kv[kvs][i][0] = ok ? *reinterpret_cast<const float4*>(src) : make_float4(0.f, 0.f, 0.f, 0.f);
+        kv[kvs][i][1] = ok ? *reinterpret_cast<const float4*>(src + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+  };
+  load(0);
+  __syncthreads();  // KVb
+  for (int c0 = 0; c0 < S; c0 += kXCH) {
+    const int clen = min(kXCH, S - c0);
+    if (c0 > 0) __syncthreads();  // every wave done with the previous chunk's images
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int u = tid + 256 * i, r = u >> 3, c = u & 7;
+#pragma unroll
+      for (int kvs = 0; kvs < 2; ++kvs) {
+        const float* bb = KVb + kvs * kXD + 8 * c;
+        const float4 x = kv[kvs][i][0], y = kv[kvs][i][1];
+        const float v[8] = {x.x + bb[0], x.y + bb[1], x.z + bb[2], x.w + bb[3],
+                            y.x + bb[4], y.y + bb[5], y.z + bb[6], y.w + bb[7]};
+        put_planes(kvs ? Vimg : Kimg, kPPlane, r, c, v);
+      }
+    }
+    for (int i = tid; i < clen; i += blockDim.x) Ms[i] = (1.f - (float)mask[(int64_t)b * S + c0 + i]) * -10000.f;
+    __syncthreads();
+    if (c0 + kXCH < S) load(c0 + kXCH);  // the next chunk's rows fly under this chunk's MFMAs
+    if (!active) continue;
+    const int ln = opaque(lane);
+    const TrBase tb = tr_base(ln);
+    for (int t = 0; t < clen; t += 32) {
+      f32x16 s = {};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        bfx8 kf[3];
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) kf[pl] = prow_frag(Kimg, pl, t + li, 2 * ks + hf);
+        s = mma6(kf, qf[ks], s);
+      }
+      float mt = -1e30f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        s[r] += Ms[t + xrow(r, hf)];
+        mt = fmaxf(mt, s[r]);
+      }
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      const float mn = fmaxf(m, mt);
+      const float alpha = __expf(m - mn);
+      m = mn;
+      float pr[16];
+      float ps = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        pr[r] = __expf(s[r] - mn);
+        ps += pr[r];
+      }
+      ps += __shfl_xor(ps, 32, 64);
+      l = l * alpha + ps;
+      o0 *= alpha;
+      o1 *= alpha;
+      if (p > 0.f) {  // the fp32 kernel's keep-bit stream and word layout (the backward reads them)
+        const uint64_t e0 = (erow + c0 + t) >> 3;
+        const uint32_t mine = keep8_bits(seed, off, e0 + 2 * hf, thr) | (keep8_bits(seed, off, e0 + 2 * hf + 1, thr) << 8);
+        const uint32_t other = static_cast<uint32_t>(__shfl_xor(static_cast<int>(mine), 32, 64));
+        const uint32_t bits = hf == 0 ? (mine | (other << 16)) : (other | (mine << 16));
+#pragma unroll
+        for (int r = 0; r < 16; ++r) pr[r] = ((bits >> xrow(r, hf)) & 1u) ? pr[r] * dscale : 0.f;
+        if (dmask && hf == 0) dmask[((uint64_t)bh * S + q0 + li) * (uint64_t)(S >> 5) + ((c0 + t) >> 5)] = bits;
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        float pv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pv[j] = pr[8 * ks + j];
+        bfx8 pf[3];
+        split8(pv, pf[0], pf[1], pf[2]);
+        const char* vb = Vimg + (t + 16 * ks) * kPRow;
+        bfx8 a0[3], a1[3];
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+          a0[pl] = ptr_frag_b(vb + pl * kPPlane, tb, 0);
+          a1[pl] = ptr_frag_b(vb + pl * kPPlane, tb, 1);
+        }
+        o0 = mma6(a0, pf, o0);
+        o1 = mma6(a1, pf, o1);
+      }
+    }
+  }
+  if (!active) return;
+  const float inv = 1.f / l;
+  float* out = ctx + ((int64_t)b * S + q0 + li) * H + h * kXD;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int d = 8 * g + 4 * hf;
+    *reinterpret_cast<float4*>(out + d) = make_float4(o0[4 * g] * inv, o0[4 * g + 1] * inv, o0[4 * g + 2] * inv,
+                                                      o0[4 * g + 3] * inv);
+    *reinterpret_cast<float4*>(out + 32 + d) = make_float4(o1[4 * g] * inv, o1[4 * g + 1] * inv,
+                                                           o1[4 * g + 2] * inv, o1[4 * g + 3] * inv);
+  }
+  if (hf == 0) lse[(int64_t)bh * S + q0 + li] = m + __logf(l);
+}
+
 // ---- A/B reference: the first key-block kernel (round 3 commit 2bf9dab), HETSEQ_ATTN_BWD_X6=1 / mode 3
 // A value the compiler must treat as new at this point: lane-derived LDS addresses are recomputed
 // per phase instead of being hoisted out of the slice loop (and spilled around it).
@@ -1736,6 +1890,12 @@ static const int g_bwd_dkv_first = [] {
   const char* e = std::getenv("HETSEQ_ATTN_BWD_DKV_FIRST");
   return e && e[0] == '0' ? 0 : 1;
 }();
+// fp32 forward: plane-image kernel (default) or the first x6 forward (HETSEQ_ATTN_FWD_X6=old)
+static int g_fwd_planes = [] {
+  const char* e = std::getenv("HETSEQ_ATTN_FWD_X6");
+  return e && e[0] == 'o' ? 0 : 1;
+}();
+void set_attn_fwd_x6_planes(int on) { g_fwd_planes = on; }
 // the plane pair computes D itself at S <= 128 (HETSEQ_ATTN_BWD_DSUM=1: the separate attn_bwd_dsum pass)
 static int g_bwd_fused_d = [] {
   const char* e = std::getenv("HETSEQ_ATTN_BWD_DSUM");
@@ -1794,7 +1954,11 @@ int launch_attn_fwd_x6(const float* qkv, const int64_t* mask, const float* bqkv,
   // grid (B*NH, S/128): consecutive blocks are different heads, so (B*NH a multiple of 8) every
   // query block of a head lands on the same XCD and its K / V come through one L2
   dim3 grid(B * NH, (S + 127) / 128);
-  hipLaunchKernelGGL(attn_fwd_x6_kernel, grid, dim3(256), 0, st, qkv, mask, bqkv, ctx, lse, dmask, S, NH, p, seed, off,
-                     g_seed_dev, bh0);
+  if (g_fwd_planes)
+    hipLaunchKernelGGL(attn_fwd_x6p_kernel, grid, dim3(256), 0, st, qkv, mask, bqkv, ctx, lse, dmask, S, NH, p, seed,
+                       off, g_seed_dev, bh0);
+  else
+    hipLaunchKernelGGL(attn_fwd_x6_kernel, grid, dim3(256), 0, st, qkv, mask, bqkv, ctx, lse, dmask, S, NH, p, seed,
+                       off, g_seed_dev, bh0);
   return 0;
 }

@@ -62,6 +62,7 @@ void set_attn_fp32_mode(int x6);
 void set_attn_bwd_x6_planes(int on);
 void set_attn_timing(uint64_t* buf);
 void set_attn_bwd_fused_d(int on);
+void set_attn_fwd_x6_planes(int on);
 int attn_fp32_mode();
 int launch_attn_fwd(int, const void*, const int64_t*, const float*, void*, float*, uint32_t*, int, int, int, int, float,
                     u64, u64, hipStream_t, int);
@@ -428,6 +429,8 @@ PYBIND11_MODULE(_hip, m) {
   m.def("attn_fp32_mode", &attn_fp32_mode);
   m.def("set_attn_bwd_fused_d", &set_attn_bwd_fused_d,
         "fp32 plane-pair attention backward: 1 = D = rowsum(dO o O) inside the kernel (S <= 128), 0 = separate pass");
+  m.def("set_attn_fwd_x6_planes", &set_attn_fwd_x6_planes,
+        "fp32 attention forward: 1 = plane-image kernel (default), 0 = the first x6 forward");
   m.def("set_attn_timing", [](i64 buf) { set_attn_timing(P(uint64_t*, buf)); },
         "diagnostic: buffer of 16 uint64 per block for the key-block backward's phase clock stamps (0 = off)");
   m.def("attn_fwd", [](int dt, i64 qkv, i64 mask, i64 bqkv, i64 ctx, i64 lse, i64 dmask, int B, int S, int NH, int D,

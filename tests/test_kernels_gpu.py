@@ -222,12 +222,15 @@ def test_attention_long_seq_fwd_bwd_vs_fp64(cuda, S, B, NH, p):
 
 
 @pytest.mark.parametrize("B,S,NH,p", [(2, 128, 12, 0.0), (2, 96, 2, 0.1), (1, 512, 2, 0.0), (2, 192, 2, 0.1)])
-def test_attention_fwd_x6_fp32_level(cuda, B, S, NH, p):
-    """fp32 forward on split-bf16 products: the same keep bits as the exact-fp32 MFMA kernel,
-    and an error against fp64 at the exact-fp32 kernel's level (not bf16's)."""
+@pytest.mark.parametrize("family", ["planes", "old"])
+def test_attention_fwd_x6_fp32_level(cuda, B, S, NH, p, family):
+    """fp32 forward on split-bf16 products (the plane-image kernel, default, and the first x6
+    forward): the same keep bits as the exact-fp32 MFMA kernel, and an error against fp64 at the
+    exact-fp32 kernel's level (not bf16's)."""
     from hetseq_amd.ops import bert_ops
     from hetseq_amd.ops._C import hip
 
+    hip().set_attn_fwd_x6_planes(1 if family == "planes" else 0)
     torch.manual_seed(31)
     H = NH * 64
     qkv = torch.randn(B * S, 3 * H, device=cuda)
@@ -242,6 +245,7 @@ def test_attention_fwd_x6_fp32_level(cuda, B, S, NH, p):
         out32, (lse32, bits32) = bert_ops.attn_fwd(qkv, mask, B, S, NH, p, 3, 11, bias=bias)
     finally:
         hip().set_attn_fp32_mode(old)
+        hip().set_attn_fwd_x6_planes(1)
     if p > 0:
         assert torch.equal(bits6, bits32)
     _close(lse6, lse32, 1e-5, 1e-5, "x6 lse")

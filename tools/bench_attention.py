@@ -59,6 +59,11 @@ def main():
         hip().set_attn_fp32_mode(1)
         out, saved = bert_ops.attn_fwd(qkv, mask, B, S, NH, 0.1, 1, 2, bias=bias)
         dout = torch.randn_like(out)
+        for fam, code in (("planes", 1), ("old", 0)):  # fp32 forward kernels
+            hip().set_attn_fwd_x6_planes(code)
+            tf = timeit(lambda: bert_ops.attn_fwd(qkv, mask, B, S, NH, 0.1, 1, 2, bias=bias), a.reps)
+            row.append("x6 fwd[%s] %.1f us" % (fam, tf))
+        hip().set_attn_fwd_x6_planes(1)
         for fam, code in (("keyblock", 2), ("planes", 1)):  # fp32 backward kernel families
             hip().set_attn_bwd_x6_planes(code)
             tb = timeit(lambda: bert_ops.attn_bwd(qkv, mask, out, dout, saved, B, S, NH, 0.1, bias=bias), a.reps)
