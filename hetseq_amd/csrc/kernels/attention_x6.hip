@@ -1577,311 +1577,18 @@ __global__ void __launch_bounds__(256, 2)
   if (hf == 0) lse[(int64_t)bh * S + q0 + li] = m + __logf(l);
 }
 
-// ---- A/B reference: the first key-block kernel (round 3 commit 2bf9dab), HETSEQ_ATTN_BWD_X6=1 / mode 3
-// A value the compiler must treat as new at this point: lane-derived LDS addresses are recomputed
-// per phase instead of being hoisted out of the slice loop (and spilled around it).
-HS_DEVICE int opaque_v1(int x) {
-  asm volatile("" : "+v"(x));
-  return x;
-}
-
-// 8 fp32 -> planes at 16-B chunk c of row `row` of a plane image (plane stride ps)
-HS_DEVICE void put_planes_v1(char* img, int ps, int row, int c, const float (&v)[8]) {
-  bfx8 f[3];
-  split8(v, f[0], f[1], f[2]);
-  const int off = row * kPRow + 16 * (c ^ pswz(row));
-#pragma unroll
-  for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<bfx8*>(img + pl * ps + off) = f[pl];
-}
-
-// per-thread staging registers of one 64-query chunk: row t >> 3, 8-wide d chunk t & 7 of Q (raw),
-// dO and O
-struct StageRegsV1 {
-  float4 q[2], o[2], c[2];
-};
-
-HS_DEVICE void stage_load_v1(StageRegsV1& r, const float* qrow, const float* orow, const float* crow, bool ok) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    r.q[i] = ok ? *reinterpret_cast<const float4*>(qrow + 4 * i) : make_float4(0.f, 0.f, 0.f, 0.f);
-    r.o[i] = ok ? *reinterpret_cast<const float4*>(orow + 4 * i) : make_float4(0.f, 0.f, 0.f, 0.f);
-    r.c[i] = ok ? *reinterpret_cast<const float4*>(crow + 4 * i) : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-}
-
-__global__ void __launch_bounds__(512, 1)
-    attn_bwd_x6k_v1_kernel(const float* __restrict__ qkv, const int64_t* __restrict__ mask,
-                        const float* __restrict__ bqkv, const float* __restrict__ ctx,
-                        const float* __restrict__ dctx, const float* __restrict__ lse, float* __restrict__ dqkv, int S,
-                        int NH, float p, const uint32_t* __restrict__ dmask, uint64_t* __restrict__ tbuf) {
-  __shared__ __attribute__((aligned(16))) char smem[kKSmem];
-  // diagnostic phase clock (tools/bench_attention.py --phases): shader-clock stamps of block 0..
-  int tn = 0;
-  auto stamp = [&]() {
-    if (tbuf && threadIdx.x == 0) tbuf[blockIdx.x * 16 + tn] = __builtin_amdgcn_s_memtime();
-    ++tn;
-  };
-  stamp();
-  char* const Kimg = smem;                     // [key][d] planes, 128 rows
-  char* const Qimg = Kimg + kKImg;             // [query of the chunk][d], 64 rows
-  char* const Oimg = Qimg + kPImg;             // dO rows, same layout
-  char* const Simg = Oimg + kPImg;             // dS planes [key][query of the chunk], 128 rows
-  float* const Ls = reinterpret_cast<float*>(Simg + kKImg);
-  float* const Ds = Ls + 64;
-  uint32_t* const Wd = reinterpret_cast<uint32_t*>(Ds + 64);  // [key word][query]
-  const int H = NH * kXD;
-  const int64_t ld = 3 * (int64_t)H;
-  const int bh = blockIdx.x, b = bh / NH, h = bh % NH;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = w >> 2, wg = w & 3;
-  const int nkw = S >> 5;
-  const bool kactive = 32 * wg < S;
-  const float* rows = qkv + (int64_t)b * S * ld;
-  const float dscale = drop_scale16(drop_thr16(p));
-  // staging unit of this thread: chunk row sr, d = 8 sc8 .. 8 sc8 + 7
-  const int sr = tid >> 3, sc8 = tid & 7;
-  float qb[8];  // the Q bias of the thread's 8 dims (constant over chunks)
-  {
-    const float* bq = bofs(bqkv, h * kXD + 8 * sc8);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) qb[j] = bq ? bq[j] : 0.f;
-  }
-  auto stage_ptrs = [&](int c0, const float*& qr, const float*& orw, const float*& cr) {
-    const int64_t tok = (int64_t)b * S + c0 + sr;
-    qr = qkv + tok * ld + h * kXD + 8 * sc8;
-    orw = dctx + tok * H + h * kXD + 8 * sc8;
-    cr = ctx + tok * H + h * kXD + 8 * sc8;
-  };
-
-  // ---- prologue: chunk 0's Q / dO / O loads in flight with the K image and the lane's V row
-  StageRegsV1 st;
-  {
-    const float *qr, *orw, *cr;
-    stage_ptrs(0, qr, orw, cr);
-    stage_load_v1(st, qr, orw, cr, sr < S);
-  }
-  {  // K image (biased): rows sr and sr + 64
-    const float* bk = bofs(bqkv, H + h * kXD + 8 * sc8);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int r = sr + 64 * i;
-      if (r < S) {
-        float v[8];
-        ld8(rows + (int64_t)r * ld + H + h * kXD + 8 * sc8, bk, 1.f, v);
-        put_planes_v1(Kimg, kKPlane, r, sc8, v);
-      }
-    }
-  }
-  bfx8 vb[4][3];
-  float madd = 0.f;
-  {
-    const int li = lane & 31, hf = lane >> 5, key = 32 * wg + li;
-    float vr[4][8];
-    if (kactive) {
-      row_frags(rows + (int64_t)key * ld + 2 * H + h * kXD, bofs(bqkv, 2 * H + h * kXD), hf, vr);
-      madd = (1.f - (float)mask[(int64_t)b * S + key]) * -10000.f;
-    } else {
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) vr[s][j] = 0.f;
-    }
-#pragma unroll
-    for (int s = 0; s < 4; ++s) split8(vr[s], vb[s][0], vb[s][1], vb[s][2]);
-  }
-  f32x16 dk0 = {}, dk1 = {}, dv0 = {}, dv1 = {};
-
-  for (int c0 = 0; c0 < S; c0 += 64) {
-    const int clen = min(64, S - c0);
-    stamp();
-    // ---- the chunk's staged registers -> Q (biased, * 1/8) / dO plane images, D, lse, keep words.
-    // Nothing written here is read by the previous chunk's dQ phase: no barrier before it.
-    {
-      float v[8];
-      const float* q = reinterpret_cast<const float*>(st.q);
-      const float* o = reinterpret_cast<const float*>(st.o);
-      const float* c = reinterpret_cast<const float*>(st.c);
-      float dsum = 0.f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        v[j] = (q[j] + qb[j]) * 0.125f;
-        dsum = fmaf(o[j], c[j], dsum);
-      }
-      if (sr < clen) put_planes_v1(Qimg, kPPlane, sr, sc8, v);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = o[j];
-      if (sr < clen) put_planes_v1(Oimg, kPPlane, sr, sc8, v);
-      dsum += __shfl_xor(dsum, 1, 64);
-      dsum += __shfl_xor(dsum, 2, 64);
-      dsum += __shfl_xor(dsum, 4, 64);
-      if (sr < clen && sc8 == 0) Ds[sr] = dsum;
-    }
-    if (tid < clen) Ls[tid] = lse[(int64_t)bh * S + c0 + tid];
-    if (p > 0.f && tid < 256) {
-      const int q = tid & 63, kw = tid >> 6;
-      if (q < clen && kw < nkw) Wd[kw * 64 + q] = dmask[((uint64_t)bh * S + c0 + q) * (uint64_t)nkw + kw];
-    }
-    __syncthreads();
-    stamp();
-    // the next chunk's loads fly under this chunk's MFMA phases
-    if (c0 + 64 < S) {
-      const float *qr, *orw, *cr;
-      stage_ptrs(c0 + 64, qr, orw, cr);
-      stage_load_v1(st, qr, orw, cr, c0 + 64 + sr < S);
-    }
-
-    // ---- phase A: S, dP, P, dS, dV^T, dK^T for slice g (rows 32 g .. of the chunk's images)
-    const bool has = c0 + 32 * g < S;
-    if (has && kactive) {
-      const int ln = opaque_v1(lane), li = ln & 31, hf = ln >> 5, key = 32 * wg + li;
-      const int qr = 32 * g;
-      const int sw = pswz(li);  // = pswz(qr + li) = pswz(key): both rows share the chunk swizzle
-      const char* qa = Qimg + (qr + li) * kPRow;
-      const char* ka = Kimg + key * kPRow;
-      f32x16 sc = {}, dp = {};
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const int o = 16 * ((2 * ks + hf) ^ sw);
-        bfx8 a[3], kf[3];
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl) {
-          a[pl] = *reinterpret_cast<const bfx8*>(qa + pl * kPPlane + o);
-          kf[pl] = *reinterpret_cast<const bfx8*>(ka + pl * kKPlane + o);
-        }
-        sc = mma6(a, kf, sc);
-      }
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const int o = 16 * ((2 * ks + hf) ^ sw);
-        bfx8 a[3];
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl) a[pl] = *reinterpret_cast<const bfx8*>(qa + kPImg + pl * kPPlane + o);
-        dp = mma6(a, vb[ks], dp);
-      }
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        float pd[8], ds[8];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {  // runs of four consecutive queries: rows 8 (2 ks + i) + 4 hf + 0..3
-          const int q0 = qr + 8 * (2 * ks + i) + 4 * hf;
-          const float4 L4 = *reinterpret_cast<const float4*>(Ls + q0);
-          const float4 D4 = *reinterpret_cast<const float4*>(Ds + q0);
-          uint4 W4 = make_uint4(0u, 0u, 0u, 0u);
-          if (p > 0.f) W4 = *reinterpret_cast<const uint4*>(Wd + wg * 64 + q0);
-          const float Lv[4] = {L4.x, L4.y, L4.z, L4.w}, Dv[4] = {D4.x, D4.y, D4.z, D4.w};
-          const uint32_t Wv[4] = {W4.x, W4.y, W4.z, W4.w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int r = 8 * ks + 4 * i + e;
-            const float pv = __expf(sc[r] + madd - Lv[e]);
-            const float mk = p > 0.f ? (((Wv[e] >> li) & 1u) ? dscale : 0.f) : 1.f;
-            pd[4 * i + e] = pv * mk;
-            ds[4 * i + e] = pv * (dp[r] * mk - Dv[e]);
-          }
-        }
-        bfx8 pb[3], a[3];
-        split8(pd, pb[0], pb[1], pb[2]);
-        const int q0 = qr + 16 * ks;
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl) a[pl] = ptr_frag(Oimg, pl, 0, q0, ln);
-        dv0 = mma6(a, pb, dv0);
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl) a[pl] = ptr_frag(Oimg, pl, 32, q0, ln);
-        dv1 = mma6(a, pb, dv1);
-        split8(ds, pb[0], pb[1], pb[2]);
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl) a[pl] = ptr_frag(Qimg, pl, 0, q0, ln);
-        dk0 = mma6(a, pb, dk0);
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl) a[pl] = ptr_frag(Qimg, pl, 32, q0, ln);
-        dk1 = mma6(a, pb, dk1);
-        // dS planes -> the [key][query] image: elements 0..3 are queries q0 + 4 hf + 0..3, 4..7 are
-        // q0 + 8 + 4 hf + 0..3 (8-B runs of the image row `key`)
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl) {
-          const uint4 u = __builtin_bit_cast(uint4, pb[pl]);
-#pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            const int col = q0 + 8 * i + 4 * hf;
-            *reinterpret_cast<uint2*>(Simg + pl * kKPlane + key * kPRow + 16 * ((col >> 3) ^ sw) + 2 * (col & 7)) =
-                i == 0 ? make_uint2(u.x, u.y) : make_uint2(u.z, u.w);
-          }
-        }
-      }
-    }
-    __syncthreads();
-    stamp();
-
-    // ---- phase B: dQ of slice g = dS K (16 x 16 tiles: q halves x this wave's 16-wide d quarter)
-    if (has) {
-      const int ln = opaque_v1(lane);
-      f32x4 q0acc = {}, q1acc = {};
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        if (ks < nkw) {
-          bfx8 kf[3], a0[3], a1[3];
-#pragma unroll
-          for (int pl = 0; pl < 3; ++pl) {
-            kf[pl] = ptr16_frag(Kimg + pl * kKPlane, 16 * wg, 32 * ks, ln);
-            a0[pl] = ptr16_frag(Simg + pl * kKPlane, 32 * g, 32 * ks, ln);
-            a1[pl] = ptr16_frag(Simg + pl * kKPlane, 32 * g + 16, 32 * ks, ln);
-          }
-          q0acc = mma16_6(a0, kf, q0acc);
-          q1acc = mma16_6(a1, kf, q1acc);
-        }
-      }
-      // C of a 16x16 tile: lane column = d, rows 4 (lane >> 4) + e = queries
-      float* out = dqkv + ((int64_t)b * S + c0 + 32 * g + 4 * (ln >> 4)) * ld + h * kXD + 16 * wg + (ln & 15);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        out[(int64_t)e * ld] = q0acc[e] * 0.125f;
-        out[(int64_t)(16 + e) * ld] = q1acc[e] * 0.125f;
-      }
-    }
-  }
-  __syncthreads();  // every dQ phase is done with the images: reuse the LDS for the hand-off
-  stamp();
-
-  // ---- dK / dV: group 1 hands its partials to group 0 (fixed order), group 0 stores
-  float* xk = reinterpret_cast<float*>(smem) + wg * 64 * 64 + lane;
-  if (g == 1 && kactive) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      xk[64 * r] = dk0[r];
-      xk[64 * (16 + r)] = dk1[r];
-      xk[64 * (32 + r)] = dv0[r];
-      xk[64 * (48 + r)] = dv1[r];
-    }
-  }
-  __syncthreads();
-  if (g == 1 || !kactive) return;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    dk0[r] += xk[64 * r];
-    dk1[r] += xk[64 * (16 + r)];
-    dv0[r] += xk[64 * (32 + r)];
-    dv1[r] += xk[64 * (48 + r)];
-  }
-  const int li = lane & 31, hf = lane >> 5;
-  float* out = dqkv + ((int64_t)b * S + 32 * wg + li) * ld + h * kXD;
-  store_rows(out + H, dk0, dk1, hf, 1.f);
-  store_rows(out + 2 * H, dv0, dv1, hf, 1.f);
-  stamp();
-}
-
 }  // namespace hs
 
 using namespace hs;
 
 // fp32 backward kernel family: HETSEQ_ATTN_BWD_X6=p (the plane-image dQ / dKV pair; default), k (key-block
-// kernel for S <= 128, the pair above that), 1 (the key-block kernel's first version) or g (fused
-// S <= 128 / gather dQ / dKV pair).  The key-block kernel is 0.8x the pair's time alone on the chip but
-// takes whole CUs (145 KB LDS, 512 VGPRs a block): beside the weight-gradient side stream the BERT-base
-// step measured 15.65 ms with it vs 15.34 with the pair (bench.py --ab, profiles/r3_attention.md).
+// kernel for S <= 128, the pair above that) or g (fused S <= 128 / gather dQ / dKV pair).  The key-block
+// kernel is 0.8x the pair's time alone on the chip but takes whole CUs (145 KB LDS, 512 VGPRs a block):
+// beside the weight-gradient side stream the BERT-base step measured 15.65 ms with it vs 15.34 with the
+// pair (bench.py --ab, profiles/r3_attention.md).
 static int g_bwd_planes_env = [] {
   const char* e = std::getenv("HETSEQ_ATTN_BWD_X6");
-  return e && e[0] == 'g' ? 0 : (e && e[0] == 'k' ? 2 : (e && e[0] == '1' ? 3 : 1));
+  return e && e[0] == 'g' ? 0 : (e && e[0] == 'k' ? 2 : 1);
 }();
 static int g_bwd_planes = g_bwd_planes_env;
 // dispatch order of the merged backward's roles: dK / dV blocks first (default) or dQ first
@@ -1912,11 +1619,6 @@ int launch_attn_bwd_x6(const float* qkv, const int64_t* mask, const float* bqkv,
                        const float* lse, float* Dbuf, float* dqkv, const uint32_t* dmask, int B, int S, int NH,
                        int D, float p, bool fused, hipStream_t st) {
   if (D != kXD || S % 32 != 0 || S <= 0 || (p > 0.f && dmask == nullptr)) return -1;
-  if (g_bwd_planes == 3 && S <= kKRows) {
-    hipLaunchKernelGGL(attn_bwd_x6k_v1_kernel, dim3(B * NH), dim3(512), 0, st, qkv, mask, bqkv, ctx, dctx, lse, dqkv,
-                       S, NH, p, dmask, nullptr);
-    return 0;
-  }
   if (g_bwd_planes == 2 && S <= kKRows) {  // key-block kernel: one block per (batch, head)
     hipLaunchKernelGGL(attn_bwd_x6k_kernel, dim3(B * NH), dim3(512), 0, st, qkv, mask, bqkv, ctx, dctx, lse, dqkv, S,
                        NH, p, dmask, g_attn_tbuf);
