@@ -404,6 +404,7 @@ _AB = {
     "wks1": lambda: _set_side_ks(1, 1),  # no split-K (no reduce pass, fewer longer blocks)
     "wks1s4": lambda: _set_side_ks(1, 4),
     "attn_k": lambda: _set_attn(2),    # key-block fp32 attention backward (S <= 128)
+    "attn_c": lambda: _set_attn(4),    # the key-block kernel in one 4-wave group (co-resides with a GEMM block)
     "attn_p": lambda: _set_attn(1),    # plane-image dQ / dKV pair
     "afwd_p": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_fwd_x6_planes(1),
     "afwd_old": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_fwd_x6_planes(0),

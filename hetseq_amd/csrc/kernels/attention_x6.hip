@@ -1424,6 +1424,296 @@ __global__ void __launch_bounds__(512, 1)
 }
 
 // ---------------------------------------------------------------------------
+// Key-block backward in ONE 4-wave group ("c" kernel, HETSEQ_ATTN_BWD_X6=c): the key-block kernel's
+// algorithm with 32-query chunks, so its LDS (97 KB: K image 48 KB, Q / dO images of 32 rows 24 KB, a
+// 24 KB dS image that keeps keys 0-63 in columns 0-31 and keys 64-127 in columns 32-63 of a 64-row
+// plane image) and its 4 x 256 VGPRs leave room on the CU for one GEMM block of the weight-gradient
+// stream: the 8-wave kernel took whole CUs and lost in the step (profiles/r3_attention.md).
+constexpr int kCPlane = 32 * kPRow;   // 4 KB: one plane of a 32-row image
+constexpr int kCImg = 3 * kCPlane;    // 12 KB
+constexpr int kCSmem = kKImg + 2 * kCImg + kPImg + 32 * 4 * 2 + 4 * 32 * 4 + kXD * 4;
+
+__global__ void __launch_bounds__(256, 2)
+    attn_bwd_x6c_kernel(const float* __restrict__ qkv, const int64_t* __restrict__ mask,
+                        const float* __restrict__ bqkv, const float* __restrict__ ctx,
+                        const float* __restrict__ dctx, const float* __restrict__ lse, float* __restrict__ dqkv, int S,
+                        int NH, float p, const uint32_t* __restrict__ dmask) {
+  __shared__ __attribute__((aligned(16))) char smem[kCSmem];
+  auto stamp = [] {};
+  char* const Kimg = smem;                     // [key][d] planes, 128 rows
+  char* const Qimg = Kimg + kKImg;             // [query of the chunk][d], 32 rows (plane stride kCPlane)
+  char* const Oimg = Qimg + kCImg;             // dO rows, same layout
+  char* const Simg = Oimg + kCImg;             // dS planes: row key & 63, columns 32 (key >> 6) + query
+  float* const Ls = reinterpret_cast<float*>(Simg + kPImg);
+  float* const Ds = Ls + 32;
+  uint32_t* const Wd = reinterpret_cast<uint32_t*>(Ds + 32);  // [key word][query]
+  const int H = NH * kXD;
+  const int64_t ld = 3 * (int64_t)H;
+  const int bh = blockIdx.x, b = bh / NH, h = bh % NH;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = 0, wg = w;
+  const int nkw = S >> 5;  // 32-key words of a keep-mask row
+  const bool kactive = 32 * wg < S;
+  const float* rows = qkv + (int64_t)b * S * ld;
+  const float dscale = drop_scale16(drop_thr16(p));
+  // staging unit of this thread: chunk row sr, d = 8 sc8 .. 8 sc8 + 7
+  const int sr = tid >> 3, sc8 = tid & 7;
+  float* const Qb = reinterpret_cast<float*>(Wd + 4 * 32);  // the head's Q bias (64 floats)
+  if (tid < kXD) Qb[tid] = bqkv ? bqkv[h * kXD + tid] : 0.f;
+  auto stage_ptrs = [&](int c0, const float*& qr, const float*& orw, const float*& cr) {
+    const int64_t tok = (int64_t)b * S + c0 + sr;
+    qr = qkv + tok * ld + h * kXD + 8 * sc8;
+    orw = dctx + tok * H + h * kXD + 8 * sc8;
+    cr = ctx + tok * H + h * kXD + 8 * sc8;
+  };
+
+  // ---- prologue: chunk 0's Q / dO / O loads in flight with the K image and the lane's V row
+  StageRegs st;
+  {
+    const float *qr, *orw, *cr;
+    stage_ptrs(0, qr, orw, cr);
+    stage_load(st, qr, orw, cr, sr < S);
+  }
+  {  // K image (biased): rows sr + 32 i (256 threads, 32 staging rows)
+    const float* bk = bofs(bqkv, H + h * kXD + 8 * sc8);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = sr + 32 * i;
+      float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // rows past S: zero (phase B sums all 128 keys)
+      if (r < S) ld8(rows + (int64_t)r * ld + H + h * kXD + 8 * sc8, bk, 1.f, v);
+      put_planes(Kimg, kKPlane, r, sc8, v);
+    }
+    if (32 * wg >= S && lane < 32) {  // keys past S: their dS entries stay zero
+      const int key = 32 * wg + lane, row = key & 63, h2 = key >> 6;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          *reinterpret_cast<uint4*>(Simg + pl * kPPlane + row * kPRow + 16 * ((4 * h2 + j) ^ pswz(row))) =
+              make_uint4(0, 0, 0, 0);
+    }
+  }
+  bfx8 vb[4][3];
+  float madd = 0.f;
+  {
+    const int li = lane & 31, hf = lane >> 5, key = 32 * wg + li;
+    float vr[4][8];
+    if (kactive) {
+      row_frags(rows + (int64_t)key * ld + 2 * H + h * kXD, bofs(bqkv, 2 * H + h * kXD), hf, vr);
+      madd = (1.f - (float)mask[(int64_t)b * S + key]) * -10000.f;
+    } else {
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) vr[s][j] = 0.f;
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) split8(vr[s], vb[s][0], vb[s][1], vb[s][2]);
+  }
+  f32x16 dk0 = {}, dk1 = {}, dv0 = {}, dv1 = {};
+  __syncthreads();  // Qb visible to the staging threads
+
+  for (int c0 = 0; c0 < S; c0 += 32) {
+    const int clen = min(32, S - c0);
+    stamp();
+    // ---- the chunk's staged registers -> Q (biased, * 1/8) / dO plane images, D, lse, keep words.
+    // Nothing written here is read by the previous chunk's dQ phase: no barrier before it.
+    {
+      float v[8];
+      const float* q = reinterpret_cast<const float*>(st.q);
+      const float* o = reinterpret_cast<const float*>(st.o);
+      const float* c = reinterpret_cast<const float*>(st.c);
+      float dsum = 0.f;
+      const float4 b0 = *reinterpret_cast<const float4*>(Qb + 8 * sc8), b1 = *reinterpret_cast<const float4*>(Qb + 8 * sc8 + 4);
+      const float qb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        v[j] = (q[j] + qb[j]) * 0.125f;
+        dsum = fmaf(o[j], c[j], dsum);
+      }
+      if (sr < clen) put_planes(Qimg, kCPlane, sr, sc8, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = o[j];
+      if (sr < clen) put_planes(Oimg, kCPlane, sr, sc8, v);
+      dsum += __shfl_xor(dsum, 1, 64);
+      dsum += __shfl_xor(dsum, 2, 64);
+      dsum += __shfl_xor(dsum, 4, 64);
+      if (sr < clen && sc8 == 0) Ds[sr] = dsum;
+    }
+    if (tid < clen) Ls[tid] = lse[(int64_t)bh * S + c0 + tid];
+    if (p > 0.f && tid < 128) {
+      const int q = tid & 31, kw = tid >> 5;
+      if (q < clen && kw < nkw) Wd[kw * 32 + q] = dmask[((uint64_t)bh * S + c0 + q) * (uint64_t)nkw + kw];
+    }
+    __syncthreads();
+    stamp();
+    // the next chunk's loads fly under this chunk's MFMA phases
+    if (c0 + 32 < S) {
+      const float *qr, *orw, *cr;
+      stage_ptrs(c0 + 32, qr, orw, cr);
+      stage_load(st, qr, orw, cr, c0 + 32 + sr < S);
+    }
+
+    // ---- phase A: S, dP, P, dS, dV^T, dK^T for slice g (rows 32 g .. of the chunk's images)
+    const bool has = c0 + 32 * g < S;
+    if (has && kactive) {
+      const int ln = opaque(lane), li = ln & 31, hf = ln >> 5, key = 32 * wg + li;
+      const int qr = 32 * g;
+      const int sw = pswz(li);  // = pswz(qr + li) = pswz(key): both rows share the chunk swizzle
+      const char* qa = Qimg + (qr + li) * kPRow;
+      const char* ka = Kimg + key * kPRow;
+      f32x16 sc = {}, dp = {};
+      // S then dP: 8 k-steps, each step's fragments read one step ahead of its MFMAs
+      bfx8 fa[2][3], fk[2][3];
+      auto frag_load = [&](int st, bfx8 (&a)[3], bfx8 (&k)[3]) {
+        const int o = 16 * ((2 * (st & 3) + hf) ^ sw);
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+          a[pl] = *reinterpret_cast<const bfx8*>(qa + (st >> 2) * kCImg + pl * kCPlane + o);
+          if (st < 4) k[pl] = *reinterpret_cast<const bfx8*>(ka + pl * kKPlane + o);
+        }
+      };
+      __builtin_amdgcn_sched_barrier(0);
+      frag_load(0, fa[0], fk[0]);
+#pragma unroll
+      for (int st = 0; st < 8; ++st) {
+        if (st + 1 < 8) frag_load(st + 1, fa[(st + 1) & 1], fk[(st + 1) & 1]);
+        if (st < 4)
+          sc = mma6(fa[st & 1], fk[st & 1], sc);
+        else
+          dp = mma6(fa[st & 1], vb[st & 3], dp);
+      }
+      // pinned order: step st + 1's LDS reads issue before step st's six MFMAs
+#define HS_RD(n) __builtin_amdgcn_sched_group_barrier(0x100, n, 0)
+#define HS_MM() __builtin_amdgcn_sched_group_barrier(0x008, 6, 0)
+      HS_RD(6); HS_RD(6); HS_MM(); HS_RD(6); HS_MM(); HS_RD(6); HS_MM(); HS_RD(3); HS_MM();
+      HS_RD(3); HS_MM(); HS_RD(3); HS_MM(); HS_RD(3); HS_MM(); HS_MM();
+#undef HS_RD
+#undef HS_MM
+      __builtin_amdgcn_sched_barrier(0);
+      // P, dS (registers; split into planes), then dV^T / dK^T: 8 units (ks, product), each six
+      // transposed-fragment reads + six MFMAs, reads pinned one unit ahead
+      // P and dS of both k-steps (score registers 8 ks .. 8 ks + 7) split into planes; sc / dp die here
+      bfx8 pb[2][3], sb[2][3];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        float pd[8], ds[8];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {  // runs of four consecutive queries: rows 8 (2 ks + i) + 4 hf + 0..3
+          const int q0 = qr + 8 * (2 * ks + i) + 4 * hf;
+          const float4 L4 = *reinterpret_cast<const float4*>(Ls + q0);
+          const float4 D4 = *reinterpret_cast<const float4*>(Ds + q0);
+          uint4 W4 = make_uint4(0u, 0u, 0u, 0u);
+          if (p > 0.f) W4 = *reinterpret_cast<const uint4*>(Wd + wg * 32 + q0);
+          const float Lv[4] = {L4.x, L4.y, L4.z, L4.w}, Dv[4] = {D4.x, D4.y, D4.z, D4.w};
+          const uint32_t Wv[4] = {W4.x, W4.y, W4.z, W4.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = 8 * ks + 4 * i + e;
+            const float pv = __expf(sc[r] + madd - Lv[e]);
+            const float mk = p > 0.f ? (((Wv[e] >> li) & 1u) ? dscale : 0.f) : 1.f;
+            pd[4 * i + e] = pv * mk;
+            ds[4 * i + e] = pv * (dp[r] * mk - Dv[e]);
+          }
+        }
+        split8(pd, pb[ks][0], pb[ks][1], pb[ks][2]);
+        split8(ds, sb[ks][0], sb[ks][1], sb[ks][2]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // dV^T / dK^T: 8 units (ks, product), each six transposed-fragment reads + six MFMAs, the
+      // reads pinned one unit ahead
+      bfx8 fu[2][3];
+      const TrBase tb = tr_base(ln);
+      auto unit_frag = [&](int u, bfx8 (&f)[3]) {  // u = 4 ks + {dO^T d 0-31, dO^T 32-63, Q^T 0-31, Q^T 32-63}
+        const char* img = ((u & 2) ? Qimg : Oimg) + (qr + 16 * (u >> 2)) * kPRow;
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) f[pl] = ptr_frag_b(img + pl * kCPlane, tb, u & 1);
+      };
+      unit_frag(0, fu[0]);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (u + 1 < 8) unit_frag(u + 1, fu[(u + 1) & 1]);
+        const int ks = u >> 2;
+        switch (u & 3) {
+          case 0: dv0 = mma6(fu[u & 1], pb[ks], dv0); break;
+          case 1: dv1 = mma6(fu[u & 1], pb[ks], dv1); break;
+          case 2: dk0 = mma6(fu[u & 1], sb[ks], dk0); break;
+          default: dk1 = mma6(fu[u & 1], sb[ks], dk1); break;
+        }
+      }
+#define HS_RD() __builtin_amdgcn_sched_group_barrier(0x100, 6, 0)
+#define HS_MM() __builtin_amdgcn_sched_group_barrier(0x008, 6, 0)
+      HS_RD(); HS_RD(); HS_MM(); HS_RD(); HS_MM(); HS_RD(); HS_MM(); HS_RD(); HS_MM();
+      HS_RD(); HS_MM(); HS_RD(); HS_MM(); HS_RD(); HS_MM(); HS_MM();
+#undef HS_RD
+#undef HS_MM
+      __builtin_amdgcn_sched_barrier(0);
+      // dS planes -> the [key][query] image: elements 0..3 of k-step ks are queries 16 ks + 4 hf + 0..3,
+      // 4..7 are 16 ks + 8 + 4 hf + 0..3 (8-B runs of the image row `key`)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+          const uint4 u = __builtin_bit_cast(uint4, sb[ks][pl]);
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            const int col = 32 * (key >> 6) + 16 * ks + 8 * i + 4 * hf;  // row key & 63: its swizzle is sw
+            *reinterpret_cast<uint2*>(Simg + pl * kPPlane + (key & 63) * kPRow + 16 * ((col >> 3) ^ sw) +
+                                      2 * (col & 7)) = i == 0 ? make_uint2(u.x, u.y) : make_uint2(u.z, u.w);
+          }
+        }
+    }
+    __syncthreads();
+    stamp();
+
+    // ---- phase B: dQ of slice g = dS K (16 x 16 tiles: q halves x this wave's 16-wide d quarter)
+    if (has) {
+      const int ln = opaque(lane);
+      f32x4 q0acc = {}, q1acc = {};
+      // four 32-key k-steps (keys past S read as zero), each step's 18 transposed reads pinned
+      // ahead of the previous step's 12 MFMAs
+      bfx8 kf[2][3], a0[2][3], a1[2][3];
+      auto qfrag = [&](int ks, bfx8 (&k)[3], bfx8 (&x0)[3], bfx8 (&x1)[3]) {
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+          k[pl] = ptr16_frag(Kimg + pl * kKPlane, 16 * wg, 32 * ks, ln);
+          x0[pl] = ptr16_frag(Simg + pl * kPPlane, 32 * (ks >> 1), 32 * (ks & 1), ln);
+          x1[pl] = ptr16_frag(Simg + pl * kPPlane, 32 * (ks >> 1) + 16, 32 * (ks & 1), ln);
+        }
+      };
+      __builtin_amdgcn_sched_barrier(0);
+      qfrag(0, kf[0], a0[0], a1[0]);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        if (ks + 1 < 4) qfrag(ks + 1, kf[(ks + 1) & 1], a0[(ks + 1) & 1], a1[(ks + 1) & 1]);
+        q0acc = mma16_6(a0[ks & 1], kf[ks & 1], q0acc);
+        q1acc = mma16_6(a1[ks & 1], kf[ks & 1], q1acc);
+      }
+#define HS_RD() __builtin_amdgcn_sched_group_barrier(0x100, 18, 0)
+#define HS_MM() __builtin_amdgcn_sched_group_barrier(0x008, 12, 0)
+      HS_RD(); HS_RD(); HS_MM(); HS_RD(); HS_MM(); HS_RD(); HS_MM(); HS_MM();
+#undef HS_RD
+#undef HS_MM
+      __builtin_amdgcn_sched_barrier(0);
+      // C of a 16x16 tile: lane column = d, rows 4 (lane >> 4) + e = queries
+      float* out = dqkv + ((int64_t)b * S + c0 + 32 * g + 4 * (ln >> 4)) * ld + h * kXD + 16 * wg + (ln & 15);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        out[(int64_t)e * ld] = q0acc[e] * 0.125f;
+        out[(int64_t)(16 + e) * ld] = q1acc[e] * 0.125f;
+      }
+    }
+  }
+  // ---- dK / dV: every wave holds its keys' whole sums (one group): store them
+  if (!kactive) return;
+  const int li = lane & 31, hf = lane >> 5;
+  float* out = dqkv + ((int64_t)b * S + 32 * wg + li) * ld + h * kXD;
+  store_rows(out + H, dk0, dk1, hf, 1.f);
+  store_rows(out + 2 * H, dv0, dv1, hf, 1.f);
+}
+
+// ---------------------------------------------------------------------------
 // Forward on plane images ("p" forward, fp32 default): attn_fwd_x6_kernel's algorithm (a wave owns
 // 32 queries, S^T tiles with the key on the registers, online softmax, the same keep bits) with
 // the backward kernels' operand staging: each 64-key chunk of K and of V is split once into
@@ -1588,7 +1878,7 @@ using namespace hs;
 // pair (bench.py --ab, profiles/r3_attention.md).
 static int g_bwd_planes_env = [] {
   const char* e = std::getenv("HETSEQ_ATTN_BWD_X6");
-  return e && e[0] == 'g' ? 0 : (e && e[0] == 'k' ? 2 : 1);
+  return e && e[0] == 'g' ? 0 : (e && e[0] == 'k' ? 2 : (e && e[0] == 'c' ? 4 : 1));
 }();
 static int g_bwd_planes = g_bwd_planes_env;
 // dispatch order of the merged backward's roles: dK / dV blocks first (default) or dQ first
@@ -1619,6 +1909,11 @@ int launch_attn_bwd_x6(const float* qkv, const int64_t* mask, const float* bqkv,
                        const float* lse, float* Dbuf, float* dqkv, const uint32_t* dmask, int B, int S, int NH,
                        int D, float p, bool fused, hipStream_t st) {
   if (D != kXD || S % 32 != 0 || S <= 0 || (p > 0.f && dmask == nullptr)) return -1;
+  if (g_bwd_planes == 4 && S <= kKRows) {  // one-group key-block kernel: one 4-wave block per (batch, head)
+    hipLaunchKernelGGL(attn_bwd_x6c_kernel, dim3(B * NH), dim3(256), 0, st, qkv, mask, bqkv, ctx, dctx, lse, dqkv, S,
+                       NH, p, dmask);
+    return 0;
+  }
   if (g_bwd_planes == 2 && S <= kKRows) {  // key-block kernel: one block per (batch, head)
     hipLaunchKernelGGL(attn_bwd_x6k_kernel, dim3(B * NH), dim3(512), 0, st, qkv, mask, bqkv, ctx, dctx, lse, dqkv, S,
                        NH, p, dmask, g_attn_tbuf);

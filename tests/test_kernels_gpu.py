@@ -259,7 +259,7 @@ def test_attention_fwd_x6_fp32_level(cuda, B, S, NH, p, family):
 
 @pytest.mark.parametrize("B,S,NH,p", [(2, 128, 12, 0.0), (2, 96, 2, 0.1), (1, 512, 2, 0.0), (2, 192, 2, 0.1),
                                        (3, 64, 4, 0.1), (2, 256, 12, 0.0)])
-@pytest.mark.parametrize("family", ["keyblock", "planes", "planes_dsum", "fused", "gather"])
+@pytest.mark.parametrize("family", ["keyblock", "keyblock4", "planes", "planes_dsum", "fused", "gather"])
 def test_attention_bwd_x6_fp32_level(cuda, B, S, NH, p, family, monkeypatch):
     """fp32 backward on split-bf16 products -- the key-block kernel (default for S <= 128; the
     plane-image pair above), the plane-image dQ / dKV pair, the fused S <= 128 kernel and the
@@ -270,7 +270,7 @@ def test_attention_bwd_x6_fp32_level(cuda, B, S, NH, p, family, monkeypatch):
 
     if family == "gather":
         monkeypatch.setenv("HETSEQ_ATTN_BWD", "split")
-    hip().set_attn_bwd_x6_planes({"keyblock": 2, "planes": 1, "planes_dsum": 1}.get(family, 0))
+    hip().set_attn_bwd_x6_planes({"keyblock": 2, "keyblock4": 4, "planes": 1, "planes_dsum": 1}.get(family, 0))
     hip().set_attn_bwd_fused_d(0 if family == "planes_dsum" else 1)  # D inside the pair vs the separate pass
     torch.manual_seed(32 + S)
     H = NH * 64

@@ -64,7 +64,7 @@ def main():
             tf = timeit(lambda: bert_ops.attn_fwd(qkv, mask, B, S, NH, 0.1, 1, 2, bias=bias), a.reps)
             row.append("x6 fwd[%s] %.1f us" % (fam, tf))
         hip().set_attn_fwd_x6_planes(1)
-        for fam, code in (("keyblock", 2), ("planes", 1)):  # fp32 backward kernel families
+        for fam, code in (("keyblock", 2), ("keyblock4", 4), ("planes", 1)):  # fp32 backward kernel families
             hip().set_attn_bwd_x6_planes(code)
             tb = timeit(lambda: bert_ops.attn_bwd(qkv, mask, out, dout, saved, B, S, NH, 0.1, bias=bias), a.reps)
             row.append("x6 bwd[%s] %.1f us" % (fam, tb))
