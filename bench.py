@@ -412,6 +412,8 @@ _AB = {
     "dsum_sep": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_bwd_fused_d(0),
     "lnp_on": lambda: _set_ln_partials(True),    # FFN-out split-K partials summed in the LN forward
     "lnp_off": lambda: _set_ln_partials(False),  # ... or reduced by the GEMM's own pass
+    "lnpo_on": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_LN_PARTIALS_WO", True),  # attention-output part
+    "lnpo_off": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_LN_PARTIALS_WO", False),
 }
 
 

@@ -27,9 +27,10 @@ import torch
 
 from hetseq_amd.ops import gemm as G
 
-# the FFN-out product's split-K partials summed by the LN forward instead of a reduce pass
-# (HETSEQ_LN_PARTIALS=0: reduce in the GEMM as before)
+# the attention-output and FFN-out products' split-K partials summed by the LN forward instead of a
+# reduce pass (HETSEQ_LN_PARTIALS=0: reduce in the GEMM as before)
 _LN_PARTIALS = os.environ.get("HETSEQ_LN_PARTIALS", "1") == "1"
+_LN_PARTIALS_WO = _LN_PARTIALS  # (the attention-output product's part of the switch, for bench --ab)
 from hetseq_amd.ops._C import dtype_code, hip, stream_handle
 from hetseq_amd.parallel import tied
 from hetseq_amd.runtime import rng, streams
@@ -444,7 +445,8 @@ def _layer_forward_split(x, mask, W, cfg, save):
             G.linear_fwd(xh, W.wqkv, out=qkv[r], ksplit=_FWD_KS)
             attn_fwd(qkv[r], mask[h * hb:(h + 1) * hb], hb, S, NH, p_a, s_a, o_a, bias=W.bqkv, b0=h * hb,
                      outs=(ctx_[r], lse[h * nl:(h + 1) * nl], dmask[h * nm:(h + 1) * nm] if dmask is not None else None))
-            a = G.linear_fwd(ctx_[r], W.wo, ksplit=_FWD_KS)
+            a = (G.linear_fwd_partials(ctx_[r], W.wo, ksplit=_FWD_KS)[0] if _LN_PARTIALS_WO
+                 else G.linear_fwd(ctx_[r], W.wo, ksplit=_FWD_KS))
             ln_fwd(a, W.g1, W.b1, eps, bias=W.bo, resid=xh, p=p_h, mode=1, seed=s_1, off=o_1, row0=h * hr,
                    outs=(h1[r], z1[r], m1[r], r1[r]))
             G.linear_gelu_fwd(h1[r], W.w1, W.bi, out=(f1[r], f1pre[r]))
@@ -474,7 +476,7 @@ def _layer_forward(x, mask, W, cfg, save):
     qkv = G.linear_fwd(xin, W.wqkv)  # bias folded into the attention kernels' Q/K/V loads
     ctx_, (lse, dmask) = attn_fwd(qkv, mask, B, S, NH, p_a, s_a, o_a, bias=W.bqkv)
     cin = G.split(ctx_) if pl else ctx_
-    a = G.linear_fwd(cin, W.wo)
+    a = G.linear_fwd(cin, W.wo) if (pl or not _LN_PARTIALS_WO) else G.linear_fwd_partials(cin, W.wo)[0]
     h1p = _planes_buf(rows, H, x.device) if pl else None
     h1, z1, m1, r1 = ln_fwd(a, W.g1, W.b1, eps, bias=W.bo, resid=x, p=p_h, mode=1, seed=s_1, off=o_1, planes=h1p)
     hin = _planes_of(h1p) if pl else h1

@@ -41,14 +41,16 @@ def test_layernorm_fwd_bwd(cuda, H):
     _close(b.grad, b2.grad, 1e-4, 1e-3, "ln dbeta")
 
 
-def test_ffn_out_partials_into_ln_bitwise(cuda):
-    """FFN-out product with its split-K partials summed by the LN forward (no reduce pass) gives
-    bitwise the LN of the reduced product: same slice order, same bias / dropout / residual."""
+@pytest.mark.parametrize("T,F_", [(1024, 3072), (2048, 768)])
+def test_ffn_out_partials_into_ln_bitwise(cuda, T, F_):
+    """FFN-out (K 3072) and attention-output (K 768, the half-batch forward's shape) products with
+    their split-K partials summed by the LN forward (no reduce pass) give bitwise the LN of the
+    reduced product: same slice order, same bias / dropout / residual."""
     from hetseq_amd.ops import bert_ops
     from hetseq_amd.ops import gemm as G
 
     torch.manual_seed(3)
-    T, H, F_ = 1024, 768, 3072
+    H = 768
     x = torch.randn(T, F_, device=cuda)
     w = torch.randn(H, F_, device=cuda) * 0.02
     b = torch.randn(H, device=cuda) * 0.1
