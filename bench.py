@@ -412,6 +412,12 @@ _AB = {
     "dsum_sep": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_bwd_fused_d(0),
     "lnp_on": lambda: _set_ln_partials(True),    # FFN-out split-K partials summed in the LN forward
     "lnp_off": lambda: _set_ln_partials(False),  # ... or reduced by the GEMM's own pass
+    "lnb_chunk": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_ln_bwd_lds(1),  # 3 KB LDS
+    "lnb_full": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_ln_bwd_lds(0),   # 12 KB LDS
+    "fork_co": lambda: _set_flag("hetseq_amd.runtime.streams", "COALESCE", True),  # one event per fork point
+    "fork_each": lambda: _set_flag("hetseq_amd.runtime.streams", "COALESCE", False),  # one per side launch
+    "swf0": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_stream_wait_flags(0),
+    "swf1": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_stream_wait_flags(1),
     "lnpo_on": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_LN_PARTIALS_WO", True),  # attention-output part
     "lnpo_off": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_LN_PARTIALS_WO", False),
 }

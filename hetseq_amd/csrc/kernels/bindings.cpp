@@ -63,6 +63,7 @@ void set_attn_bwd_x6_planes(int on);
 void set_attn_timing(uint64_t* buf);
 void set_attn_bwd_fused_d(int on);
 void set_attn_fwd_x6_planes(int on);
+void set_ln_bwd_lds(int chunked);
 int attn_fp32_mode();
 int launch_attn_fwd(int, const void*, const int64_t*, const float*, void*, float*, uint32_t*, int, int, int, int, float,
                     u64, u64, hipStream_t, int);
@@ -136,14 +137,23 @@ static void pre_launch(const char* what) {
 // `signal`, make `waiter` wait for it.  A ring of timing-free events, created once; an event is
 // re-recorded only after 64 later forks, long after the wait that used it was enqueued (a wait
 // captures the event's state at enqueue time).
+// Cross-stream ordering point: `waiter` runs nothing enqueued after this until `signal` has
+// finished everything enqueued so far.  Events from a ring of 64, created with
+// g_wait_flags (hipEventDisableTiming by default; tools/probes/fork_gap.py measures the flag
+// choices, set_stream_wait_flags switches them).
+static unsigned g_wait_flags = hipEventDisableTiming;
 static void stream_wait(hipStream_t waiter, hipStream_t signal) {
   static hipEvent_t ring[64];
   static int n = 0;
-  static bool init = false;
-  if (!init) {
+  static unsigned made = ~0u;
+  if (made != g_wait_flags) {
+    if (made != ~0u) {
+      if (hipDeviceSynchronize() != hipSuccess) throw std::runtime_error("stream_wait: hipDeviceSynchronize");
+      for (auto& e : ring) (void)hipEventDestroy(e);
+    }
     for (auto& e : ring)
-      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) throw std::runtime_error("hipEventCreate");
-    init = true;
+      if (hipEventCreateWithFlags(&e, g_wait_flags) != hipSuccess) throw std::runtime_error("hipEventCreate");
+    made = g_wait_flags;
   }
   hipEvent_t e = ring[n++ & 63];
   if (hipEventRecord(e, signal) != hipSuccess || hipStreamWaitEvent(waiter, e, 0) != hipSuccess)
@@ -429,6 +439,8 @@ PYBIND11_MODULE(_hip, m) {
   m.def("attn_fp32_mode", &attn_fp32_mode);
   m.def("set_attn_bwd_fused_d", &set_attn_bwd_fused_d,
         "fp32 plane-pair attention backward: 1 = D = rowsum(dO o O) inside the kernel (S <= 128), 0 = separate pass");
+  m.def("set_ln_bwd_lds", &set_ln_bwd_lds,
+        "LN backward column partials: 1 = through a 3 KB LDS window (default), 0 = the [waves][H] LDS image");
   m.def("set_attn_fwd_x6_planes", &set_attn_fwd_x6_planes,
         "fp32 attention forward: 1 = plane-image kernel (default), 0 = the first x6 forward");
   m.def("set_attn_timing", [](i64 buf) { set_attn_timing(P(uint64_t*, buf)); },
@@ -469,6 +481,11 @@ PYBIND11_MODULE(_hip, m) {
   // returns 0 when launched, -1 when the shape/epilogue is not served (caller falls back)
   m.def("set_seed_ptr", [](i64 ptr) { hs::g_seed_dev = reinterpret_cast<const uint64_t*>(ptr); });
   m.def("stream_wait", [](i64 waiter, i64 signal) { stream_wait(ST(waiter), ST(signal)); });
+  m.def("set_stream_wait_flags", [](int mode) {
+    // 0: DisableTiming; 1: + DisableSystemFence; 2: + ReleaseToDevice; 3: + both
+    g_wait_flags = hipEventDisableTiming | (mode & 1 ? hipEventDisableSystemFence : 0u) |
+                   (mode & 2 ? hipEventReleaseToDevice : 0u);
+  }, "event flags of stream_wait's ordering events (synchronises the device when they change)");
   // A non-blocking stream of the current device that lives for the whole process (runtime/streams.py
   // creates the engine's streams with it before RCCL and torch's stream pool create theirs, so each
   // role gets a hardware queue of its own; never destroyed).

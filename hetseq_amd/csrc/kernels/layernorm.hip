@@ -127,6 +127,37 @@ HS_DEVICE void block_colpart_store(float (&acc)[NV][4], float* __restrict__ part
   __syncthreads();
 }
 
+// The same per-block column partials through a 3 KB LDS window instead of [WV][H]: waves 1-3 hand
+// wave 0 one 256-column chunk at a time and wave 0 sums ((w0 + w1) + (w2 + w3)) -- the LN backward
+// then needs 3 KB of LDS instead of 12 KB, so it still finds room on a CU whose LDS is taken by three
+// 53 KB split-bf16 GEMM blocks of the other stream (160 KB - 3 x 53 KB = 4 KB left).
+template <int NV>
+HS_DEVICE void colpart_chunked_store(float (&acc)[NV][4], float* __restrict__ part, float* lds) {
+  constexpr int H = NV * 256;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    if (w > 0) store4(lds + (w - 1) * 256 + lane * 4, acc[k]);
+    __syncthreads();
+    if (w == 0) {
+      float a[4], b[4], c[4], o[4];
+      load4(lds + lane * 4, a);
+      load4(lds + 256 + lane * 4, b);
+      load4(lds + 512 + lane * 4, c);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = (acc[k][j] + a[j]) + (b[j] + c[j]);
+      store4(part + (int64_t)blockIdx.x * H + (k * 64 + lane) * 4, o);
+    }
+    __syncthreads();
+  }
+}
+
+// 0: [WV][H] LDS reduction (12 KB at H 768); 1: the 3 KB chunked one (default) -- set_ln_bwd_lds
+static int g_lnbwd_chunked = [] {
+  const char* e = std::getenv("HETSEQ_LNBWD_LDS");
+  return e && e[0] == 'f' ? 0 : 1;
+}();
+
 // One row per wave at a time, with the NEXT row's dy / z / statistics loaded before this row's
 // reductions (two rows of loads in flight per wave); gamma is loaded once per wave.  Small
 // blocks (4 waves) so the kernel still finds room on CUs that run weight-gradient GEMM blocks of
@@ -134,7 +165,7 @@ HS_DEVICE void block_colpart_store(float (&acc)[NV][4], float* __restrict__ part
 // inside the training step).
 constexpr int kLnBwdWaves = 4;
 
-template <int NV, typename T>
+template <int NV, typename T, bool CHUNK = false>
 __global__ void __launch_bounds__(64 * kLnBwdWaves) ln_bwd_kernel(
     const T* __restrict__ dy, const float* __restrict__ zsave, const float* __restrict__ mean_in,
     const float* __restrict__ rstd_in, const float* __restrict__ gamma, T* __restrict__ dz_out, T* __restrict__ da_out,
@@ -217,9 +248,17 @@ __global__ void __launch_bounds__(64 * kLnBwdWaves) ln_bwd_kernel(
     rstd = rn;
     row = nxt;
   }
-  block_colpart_store<NV, kLnBwdWaves>(ag, part_gamma, lds);
-  block_colpart_store<NV, kLnBwdWaves>(ab, part_beta, lds);
-  if (mode == kBDR && part_bias) block_colpart_store<NV, kLnBwdWaves>(abias, part_bias, lds);
+  if constexpr (CHUNK) {
+    static_assert(kLnBwdWaves == 4, "chunked partials: 4 waves");
+    __shared__ __attribute__((aligned(16))) float win[768];
+    colpart_chunked_store<NV>(ag, part_gamma, win);
+    colpart_chunked_store<NV>(ab, part_beta, win);
+    if (mode == kBDR && part_bias) colpart_chunked_store<NV>(abias, part_bias, win);
+  } else {
+    block_colpart_store<NV, kLnBwdWaves>(ag, part_gamma, lds);
+    block_colpart_store<NV, kLnBwdWaves>(ab, part_beta, lds);
+    if (mode == kBDR && part_bias) block_colpart_store<NV, kLnBwdWaves>(abias, part_bias, lds);
+  }
 }
 
 // ------------------------------------------------------------ embeddings
@@ -374,6 +413,14 @@ void ln_bwd_launch(const void* dy, const float* zsave, const float* mean, const 
                    void* dz, void* da, float* pg, float* pb, float* pbias, int rows, float p, uint64_t seed,
                    uint64_t off, int mode, uint16_t* dap, int64_t daps, hipStream_t st) {
   constexpr int H = NV * 256;
+  if constexpr (NV <= 3) {
+    if (g_lnbwd_chunked) {
+      hipLaunchKernelGGL((ln_bwd_kernel<NV, T, true>), dim3(kLnBwdBlocks), dim3(64 * kLnBwdWaves), 0, st,
+                         (const T*)dy, zsave, mean, rstd, gamma, (T*)dz, (T*)da, pg, pb, pbias, rows, p, seed, off, mode,
+                         g_seed_dev, dap, daps);
+      return;
+    }
+  }
   hipLaunchKernelGGL((ln_bwd_kernel<NV, T>), dim3(kLnBwdBlocks), dim3(64 * kLnBwdWaves), kLnBwdWaves * H * sizeof(float), st, (const T*)dy,
                      zsave, mean, rstd, gamma, (T*)dz, (T*)da, pg, pb, pbias, rows, p, seed, off, mode, g_seed_dev,
                      dap, daps);
@@ -414,6 +461,7 @@ using namespace hs;
   }
 
 int ln_bwd_num_blocks() { return kLnBwdBlocks; }
+void set_ln_bwd_lds(int chunked) { g_lnbwd_chunked = chunked; }
 
 int launch_ln_fwd(int dtype, const void* a, const float* bias, const void* resid, const float* gamma,
                   const float* beta, void* y, float* zsave, float* mean, float* rstd, int rows, int H, float eps,

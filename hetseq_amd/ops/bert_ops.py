@@ -550,8 +550,6 @@ class FusedBertLayer(torch.autograd.Function):
         dks = streams.DGRAD_KSPLIT if side else None  # K split of the dgrads beside the side stream
         rows = dh2.shape[0]
         dop = _planes_buf(rows, H, dh2.device) if pl else None  # the LN backwards write da as planes
-        dz2, do_, dg2, dbb2, db2 = ln_bwd(dh2, z2, m2, r2, W.g2, p_h, 1, s_2, o_2, True, not pl,
-                                          acc=(Gv.g2, Gv.bb2, Gv.b2) if acc else None, side=side, da_planes=dop)
 
         def wgrad(dy, xin_, out):
             if not side:
@@ -560,24 +558,30 @@ class FusedBertLayer(torch.autograd.Function):
             return streams.run(dy.device, lambda: G.linear_wgrad(dy, xin_, out=out, accumulate=acc,
                                                                  ksplit=ks), dy, xin_)
 
-        do_p = _planes_of(dop) if pl else do_
-        dW2 = wgrad(do_p, f1, Gv.w2 if acc else None)
+        # side-stream work forks at three points per layer; the launches at one point share one event
+        with streams.coalesced():  # LN2 parameter gradients + the FFN-out weight gradient
+            dz2, do_, dg2, dbb2, db2 = ln_bwd(dh2, z2, m2, r2, W.g2, p_h, 1, s_2, o_2, True, not pl,
+                                              acc=(Gv.g2, Gv.bb2, Gv.b2) if acc else None, side=side, da_planes=dop)
+            do_p = _planes_of(dop) if pl else do_
+            dW2 = wgrad(do_p, f1, Gv.w2 if acc else None)
         df1p, dbi = G.linear_dgrad_dgelu(do_p, W.w2, f1pre, W.bi, db_acc=Gv.bi if acc else None, planes_out=pl)
         dW1 = wgrad(df1p, h1, Gv.w1 if acc else None)
         dh1 = G.linear_dgrad(df1p, W.w1, out=dz2, accumulate=True, ksplit=dks)  # dz2 + df1pre @ W1
         dap = _planes_buf(rows, H, dh2.device) if pl else None
-        dz1, da1, dg1, db1, dbo = ln_bwd(dh1, z1, m1, r1, W.g1, p_h, 1, s_1, o_1, True, not pl,
-                                         acc=(Gv.g1, Gv.b1, Gv.bo) if acc else None, side=side, da_planes=dap)
-        da1p = _planes_of(dap) if pl else da1
-        dWo = wgrad(da1p, cin, Gv.wo if acc else None)
+        with streams.coalesced():  # LN1 parameter gradients + the attention-output weight gradient
+            dz1, da1, dg1, db1, dbo = ln_bwd(dh1, z1, m1, r1, W.g1, p_h, 1, s_1, o_1, True, not pl,
+                                             acc=(Gv.g1, Gv.b1, Gv.bo) if acc else None, side=side, da_planes=dap)
+            da1p = _planes_of(dap) if pl else da1
+            dWo = wgrad(da1p, cin, Gv.wo if acc else None)
         dctx = G.linear_dgrad(da1p, W.wo, ksplit=dks)
         dqkv = attn_bwd(qkv, mask, ctx_, dctx, (lse, dmask), B, S, NH, p_a, bias=W.bqkv)
         dqkvp = G.split(dqkv) if pl else dqkv
-        dWqkv = wgrad(dqkvp, xin, Gv.wqkv if acc else None)
-        if side:
-            dbqkv = streams.run(dqkv.device, lambda: colsum(dqkv, acc=Gv.bqkv), dqkv)
-        else:
-            dbqkv = colsum(dqkv, acc=Gv.bqkv if acc else None)
+        with streams.coalesced():  # QKV weight and bias gradients
+            dWqkv = wgrad(dqkvp, xin, Gv.wqkv if acc else None)
+            if side:
+                dbqkv = streams.run(dqkv.device, lambda: colsum(dqkv, acc=Gv.bqkv), dqkv)
+            else:
+                dbqkv = colsum(dqkv, acc=Gv.bqkv if acc else None)
         dx = G.linear_dgrad(dqkvp, W.wqkv, out=dz1, accumulate=True, ksplit=dks)  # dz1 + dqkv @ Wqkv
         if acc:
             return (dx, None, None) + (None,) * 16
@@ -734,9 +738,10 @@ class FusedPreTrainingLoss(torch.autograd.Function):
             return Gv[5].add_(full) if acc else full
 
         if side:
-            dWdec = streams.run(dl_c.device, dwdec, dl_c, t2, lbuf)
-            streams.mark(dl_c.device, "tied")  # the embedding backward waits for this GEMM only
-            dbdec = streams.run(dl_c.device, dbias, dlogits, lbuf)
+            with streams.coalesced():  # (the mark records on the side stream: one fork serves both)
+                dWdec = streams.run(dl_c.device, dwdec, dl_c, t2, lbuf)
+                streams.mark(dl_c.device, "tied")  # the embedding backward waits for this GEMM only
+                dbdec = streams.run(dl_c.device, dbias, dlogits, lbuf)
         else:
             dWdec = dwdec()
             dbdec = dbias()

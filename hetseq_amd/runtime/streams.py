@@ -62,7 +62,9 @@ def side_ksplit(M, N):
 _dks = os.environ.get("HETSEQ_DGRAD_KSPLIT", "1")
 DGRAD_KSPLIT = None if _dks == "auto" else int(_dks)
 _STREAMS: dict = {}
-_state = {"queued": False}
+_state = {"queued": False, "coalesce": 0}
+# share one fork event between consecutive side-stream launches (bench --ab fork_co / fork_each)
+COALESCE = os.environ.get("HETSEQ_FORK_COALESCE", "1") == "1"
 
 
 def set_enabled(flag: bool):
@@ -111,6 +113,12 @@ def fwd2(device) -> "torch.cuda.Stream":
 def role(stream_handle: int) -> str:
     """'side' or 'main': which engine stream a raw handle is (per-role scratch: split-K slabs)."""
     return "side" if is_side(stream_handle) else "main"
+
+
+# An ordering point between two streams costs the recording stream ~6.5 us of GPU time between two
+# dependent kernels (a round trip compute -> side -> compute ~27 us, tools/probes/fork_gap.py), so
+# consecutive forks share one event (:class:`coalesced`).  In the training step the other stream
+# fills most of that bubble (profiles/r3_forks.md).
 
 
 class fwd_halves(object):
@@ -196,11 +204,30 @@ def active(device) -> "torch.cuda.Stream | None":
 _KEEP: list = []
 
 
+class coalesced(object):
+    """``with coalesced(): ...`` -- forks inside it after the first reuse its event: the caller
+    guarantees that nothing is enqueued on the current stream between them (e.g. an LN backward's
+    parameter-gradient finalisation and the weight gradient that follows it)."""
+
+    def __enter__(self):
+        self.prev = _state.get("coalesce", 0)
+        _state["coalesce"] = 1
+        return self
+
+    def __exit__(self, *exc):
+        _state["coalesce"] = self.prev
+        return False
+
+
 def fork(device, *tensors) -> "torch.cuda.Stream":
     from hetseq_amd.ops._C import hip, stream_handle
 
     s = side(device)
-    hip().stream_wait(s.cuda_stream, stream_handle())
+    c = _state.get("coalesce", 0)
+    if c != 2 or not COALESCE:
+        hip().stream_wait(s.cuda_stream, stream_handle())
+        if c == 1:
+            _state["coalesce"] = 2
     _KEEP.extend(tensors)
     if not _state["queued"]:
         _state["queued"] = True

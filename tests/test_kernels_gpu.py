@@ -68,6 +68,28 @@ def test_ffn_out_partials_into_ln_bitwise(cuda, T, F_):
     _close(parts.sum(0) if parts.dim() == 3 else parts, ref, 1e-5, 1e-5, "partials sum")
 
 
+def test_ln_bwd_chunked_partials_bitwise(cuda):
+    """The LN backward's 3 KB-LDS column partials sum the four waves in the same pairwise order as
+    the [waves][H] LDS image: dgamma / dbeta / dbias and dz / da are bitwise equal."""
+    from hetseq_amd.ops import bert_ops
+    from hetseq_amd.ops._C import hip
+
+    torch.manual_seed(4)
+    rows, H = 4096, 768
+    dy, z = torch.randn(rows, H, device=cuda), torch.randn(rows, H, device=cuda)
+    mean, rstd = torch.randn(rows, device=cuda), torch.rand(rows, device=cuda) + 0.5
+    g = torch.randn(H, device=cuda)
+    outs = []
+    try:
+        for chunked in (1, 0):
+            hip().set_ln_bwd_lds(chunked)
+            outs.append(bert_ops.ln_bwd(dy, z, mean, rstd, g, 0.1, 1, 1, 2, True, True))
+    finally:
+        hip().set_ln_bwd_lds(1)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 def test_bias_dropout_residual_ln_nodrop(cuda):
     from hetseq_amd.ops.bert_ops import bias_dropout_residual_ln
 
