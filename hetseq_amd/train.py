@@ -102,6 +102,8 @@ def main(args, init_distributed=False):
     if controller.cuda:
         bert_ops.check_device_errors()
     print("| done training in {:.1f} seconds".format(train_meter.sum))
+    if init_distributed:
+        distributed_utils.shutdown(controller)
     return controller
 
 
