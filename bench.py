@@ -418,6 +418,8 @@ _AB = {
     "fork_each": lambda: _set_flag("hetseq_amd.runtime.streams", "COALESCE", False),  # one per side launch
     "swf0": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_stream_wait_flags(0),
     "swf1": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_stream_wait_flags(1),
+    "wcol_on": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_WGRAD_COLSUM", True),  # QKV bias grad in the wgrad
+    "wcol_off": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_WGRAD_COLSUM", False),  # separate column sum
     "lnpo_on": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_LN_PARTIALS_WO", True),  # attention-output part
     "lnpo_off": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_LN_PARTIALS_WO", False),
 }

@@ -552,6 +552,20 @@ __global__ void __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(NB
     }
   };
   (void)stB;
+  // weight gradient with p.part (TA only; the launcher admits it for the 4-wave single-buffer PF-1
+  // loop): the blocks of the first column tile also sum A over this slice's K -- the bias gradient
+  // of the same product (QKV: db = sum over tokens of dqkv) -- from the registers they stage anyway.
+  // Thread st holds columns m0 + 4 (st & 31) + e of k rows 4 (st >> 5) + 0..3 in both A layouts.
+  const bool csum = TA && WV == 4 && NBUF == 1 && PF == 1 && !EDGE && p.part != nullptr && tn == 0;
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};
+  auto acc_cols = [&]() {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float a0 = TRA ? comp(va[0], e) : comp(va[e], 0), a1 = TRA ? comp(va[1], e) : comp(va[e], 1);
+      const float a2 = TRA ? comp(va[2], e) : comp(va[e], 2), a3 = TRA ? comp(va[3], e) : comp(va[e], 3);
+      cs[e] += (a0 + a1) + (a2 + a3);
+    }
+  };
   const int KT = p.K / p.ksplit / GBK;
   constexpr int NPL = NT >= 6 ? 3 : 2, NTERM = NT >= 6 ? 6 : 3;
   constexpr int PA[6] = {2, 0, 1, 1, 0, 0}, PB[6] = {0, 2, 1, 0, 1, 0};  // smallest terms first
@@ -654,6 +668,7 @@ __global__ void __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(NB
     if (kt < KT) compute([] {}, As, Bs);  // odd tile count: the last tile is staged already
   } else {
     load();
+    if (csum) acc_cols();
     store();
     __syncthreads();
     for (int kt = 0; kt < KT; ++kt) {
@@ -667,8 +682,22 @@ __global__ void __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(NB
         if (ABL < 1) load();
       }, As, Bs);
       if (ABL < 3) __syncthreads();  // every wave is done reading this K tile
+      if (csum && kt + 1 < KT) acc_cols();  // (not the re-read last tile)
       if (ABL < 2) store();
       if (ABL < 3) __syncthreads();
+    }
+    if (csum) {  // block-uniform: the 8 k-row groups' sums in a fixed order -> part[slice][m]
+      float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red[(st >> 5) * 128 + 4 * (st & 31) + e] = cs[e];
+      __syncthreads();
+      if (st < 128) {
+        float v = 0.f;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) v += red[c * 128 + st];
+        p.part[(int64_t)slice * p.M + m0 + st] = v;
+      }
+      __syncthreads();
     }
   }
   // the epilogue's tile geometry: TM x TN 32x32 accumulators per wave, two wave rows
@@ -920,6 +949,12 @@ int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, i
   nv = nv > 0 ? nv : N;
   kv = kv > 0 ? kv : K;
   if ((mv != M || nv != N || kv != K) && (!nt || epi > kEpiBias || mv > M || nv > N || kv > K)) return -1;
+  // weight gradient + the column sums of A (its bias gradient) in the same launch: split-bf16
+  // engine, 4-wave single-buffer PF-1 kernel, unpadded; part = [ks][M] partials, summed into
+  // colsum_out (added if colsum_acc) below
+  const bool wcol = ta && epi == kEpiNone && part != nullptr;
+  if (wcol && (!nt || !colsum_out || g_x6_waves != 4 || g_x6_pf != 1 || g_ablation || mv != M || nv != N || kv != K))
+    return -1;
   GemmArgs a{static_cast<const float*>(A), static_cast<const float*>(B), static_cast<float*>(C), bias, aux, part,
              lda, ldb, ldc, ldaux, M, N, K, beta, ks, slab, mv, nv, kv, g_slice_major};
   int rc;
@@ -941,6 +976,10 @@ int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, i
     const float* parts[1] = {part};
     float* outs[1] = {colsum_out};
     launch_reduce_rows(parts, outs, 1, M / bm, N, colsum_acc, st);
+  } else if (wcol) {
+    const float* parts[1] = {part};
+    float* outs[1] = {colsum_out};
+    launch_reduce_rows(parts, outs, 1, ks, M, colsum_acc, st);
   }
   return 0;
 }

@@ -31,6 +31,9 @@ from hetseq_amd.ops import gemm as G
 # reduce pass (HETSEQ_LN_PARTIALS=0: reduce in the GEMM as before)
 _LN_PARTIALS = os.environ.get("HETSEQ_LN_PARTIALS", "1") == "1"
 _LN_PARTIALS_WO = _LN_PARTIALS  # (the attention-output product's part of the switch, for bench --ab)
+# the QKV bias gradient summed by the QKV weight-gradient kernel (gemm.linear_wgrad_colsum) instead of
+# a column-sum pass over dqkv (HETSEQ_WGRAD_COLSUM=0: separate pass)
+_WGRAD_COLSUM = os.environ.get("HETSEQ_WGRAD_COLSUM", "1") == "1"
 from hetseq_amd.ops._C import dtype_code, hip, stream_handle
 from hetseq_amd.parallel import tied
 from hetseq_amd.runtime import rng, streams
@@ -577,11 +580,19 @@ class FusedBertLayer(torch.autograd.Function):
         dqkv = attn_bwd(qkv, mask, ctx_, dctx, (lse, dmask), B, S, NH, p_a, bias=W.bqkv)
         dqkvp = G.split(dqkv) if pl else dqkv
         with streams.coalesced():  # QKV weight and bias gradients
-            dWqkv = wgrad(dqkvp, xin, Gv.wqkv if acc else None)
-            if side:
-                dbqkv = streams.run(dqkv.device, lambda: colsum(dqkv, acc=Gv.bqkv), dqkv)
+            fused = False
+            if side and not pl and _WGRAD_COLSUM:  # one launch: the bias gradient from the wgrad's staging
+                ks = streams.side_ksplit(dqkv.shape[1], xin.shape[1])
+                fused = streams.run(dqkv.device, lambda: G.linear_wgrad_colsum(dqkv, xin, Gv.wqkv, Gv.bqkv, ksplit=ks),
+                                    dqkv, xin)
+            if fused:
+                dWqkv, dbqkv = Gv.wqkv, Gv.bqkv
             else:
-                dbqkv = colsum(dqkv, acc=Gv.bqkv if acc else None)
+                dWqkv = wgrad(dqkvp, xin, Gv.wqkv if acc else None)
+                if side:
+                    dbqkv = streams.run(dqkv.device, lambda: colsum(dqkv, acc=Gv.bqkv), dqkv)
+                else:
+                    dbqkv = colsum(dqkv, acc=Gv.bqkv if acc else None)
         dx = G.linear_dgrad(dqkvp, W.wqkv, out=dz1, accumulate=True, ksplit=dks)  # dz1 + dqkv @ Wqkv
         if acc:
             return (dx, None, None) + (None,) * 16

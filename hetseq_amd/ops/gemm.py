@@ -673,6 +673,27 @@ def linear_wgrad(dy, x, out=None, accumulate=False, ksplit=None):
                 ksplit=ksplit)
 
 
+def linear_wgrad_colsum(dy, x, out, colsum_out, ksplit=None):
+    """``out += dy^T @ x`` and ``colsum_out += dy.sum(0)`` (a Linear's weight and bias gradients) in
+    one split-bf16 launch: the weight-gradient blocks of the first column tile sum dy's columns from
+    the registers they stage (gemm.hip, ``wcol``), and one small pass adds the K slices' partials
+    into ``colsum_out``.  Returns False when not served (library choice, first measuring call, other
+    layouts): the caller then runs :func:`linear_wgrad` and a column sum."""
+    T, M = dy.shape
+    N = x.shape[1]
+    if not (_MODE != "blas" and _FP32 == "x6" and isinstance(dy, torch.Tensor) and isinstance(x, torch.Tensor)
+            and dy.is_cuda and dy.dtype == torch.float32 and x.dtype == torch.float32 and out.is_contiguous()
+            and colsum_out.is_contiguous() and colsum_out.numel() == M and _hip_ok(dy, x, out)):
+        return False
+    c = GEMM_CHOICES.get((M, N, T, True, False, EPI_NONE, True))
+    if c is None or c[0] != "hip":
+        return False
+    ks = ksplit if ksplit is not None else (c[3] if len(c) > 3 else 0)
+    part = torch.empty((max(ks, 1) if ks > 0 else 8, M), dtype=torch.float32, device=dy.device)
+    return _hip_gemm(dy, x, True, False, out, beta=1.0, part=part, colsum=colsum_out, colsum_acc=True,
+                     fp32="x6", ksplit=ks)
+
+
 def linear_gelu_fwd(x, w, b, planes_out=False, emit_planes=False, out=None):
     """FFN-in forward: pre = x @ w^T (un-biased, kept for the backward), y = gelu(pre + b).
 

@@ -68,6 +68,29 @@ def test_ffn_out_partials_into_ln_bitwise(cuda, T, F_):
     _close(parts.sum(0) if parts.dim() == 3 else parts, ref, 1e-5, 1e-5, "partials sum")
 
 
+@pytest.mark.parametrize("tile", [-1, 512])  # transposed-read A layout (default) / register transpose
+@pytest.mark.parametrize("ks", [2, 4])
+def test_wgrad_colsum_fused(cuda, tile, ks):
+    """QKV-shaped weight gradient with the bias gradient summed by the same launch (the first column
+    tile's blocks add up the dy columns they stage): dW += dy^T x and db += sum_rows(dy), both
+    accumulated, against fp64."""
+    from hetseq_amd.ops import gemm as G
+
+    torch.manual_seed(6)
+    T, M, N = 4096, 2304, 768
+    dy, x = torch.randn(T, M, device=cuda), torch.randn(T, N, device=cuda)
+    w0, c0 = torch.randn(M, N, device=cuda), torch.randn(M, device=cuda)
+    w, c = w0.clone(), c0.clone()
+    part = torch.empty((ks, M), dtype=torch.float32, device=cuda)
+    assert G._hip_gemm(dy, x, True, False, w, beta=1.0, part=part, colsum=c, colsum_acc=True, fp32="x6", ksplit=ks,
+                       tile=tile)
+    d, xd = dy.double(), x.double()
+    scale = w0.double().abs() + d.abs().t() @ xd.abs()
+    assert float(((w.double() - (w0.double() + d.t() @ xd)).abs() / scale).max()) < 1e-6
+    cscale = c0.double().abs() + d.abs().sum(0)
+    assert float(((c.double() - (c0.double() + d.sum(0))).abs() / cscale).max()) < 1e-6
+
+
 def test_ln_bwd_chunked_partials_bitwise(cuda):
     """The LN backward's 3 KB-LDS column partials sum the four waves in the same pairwise order as
     the [waves][H] LDS image: dgamma / dbeta / dbias and dz / da are bitwise equal."""
