@@ -481,24 +481,6 @@ PYBIND11_MODULE(_hip, m) {
   // returns 0 when launched, -1 when the shape/epilogue is not served (caller falls back)
   m.def("set_seed_ptr", [](i64 ptr) { hs::g_seed_dev = reinterpret_cast<const uint64_t*>(ptr); });
   m.def("stream_wait", [](i64 waiter, i64 signal) { stream_wait(ST(waiter), ST(signal)); });
-  // Probe (tools/probes/fork_gap.py): an ordering point made of stream memory operations instead of
-  // an event -- `signal` writes an increasing 64-bit value to signal memory, `waiter` waits for >= it.
-  m.def("stream_wait_value", [](i64 waiter, i64 signal) {
-    static uint64_t* flag = nullptr;
-    static uint64_t seq = 0;
-    if (!flag) {
-      void* q = nullptr;
-      if (hipExtMallocWithFlags(&q, 64, hipMallocSignalMemory) != hipSuccess)
-        throw std::runtime_error("hipExtMallocWithFlags(signal) failed");
-      flag = static_cast<uint64_t*>(q);
-      if (hipMemset(flag, 0, 64) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
-        throw std::runtime_error("signal memory init failed");
-    }
-    ++seq;
-    if (hipStreamWriteValue64(ST(signal), flag, seq, 0) != hipSuccess ||
-        hipStreamWaitValue64(ST(waiter), flag, seq, hipStreamWaitValueGte, ~0ull) != hipSuccess)
-      throw std::runtime_error("stream_wait_value: hipStreamWriteValue64/hipStreamWaitValue64 failed");
-  });
   m.def("set_stream_wait_flags", [](int mode) {
     // 0: DisableTiming; 1: + DisableSystemFence; 2: + ReleaseToDevice; 3: + both
     g_wait_flags = hipEventDisableTiming | (mode & 1 ? hipEventDisableSystemFence : 0u) |

@@ -685,10 +685,21 @@ def linear_wgrad_colsum(dy, x, out, colsum_out, ksplit=None):
             and dy.is_cuda and dy.dtype == torch.float32 and x.dtype == torch.float32 and out.is_contiguous()
             and colsum_out.is_contiguous() and colsum_out.numel() == M and _hip_ok(dy, x, out)):
         return False
-    c = GEMM_CHOICES.get((M, N, T, True, False, EPI_NONE, True))
-    if c is None or c[0] != "hip":
-        return False
-    ks = ksplit if ksplit is not None else (c[3] if len(c) > 3 else 0)
+    # the same engine decision as linear_wgrad's (so a run takes the fused path from its first step
+    # on, whatever the choice table held: the bias gradient's summation order never switches)
+    key = (M, N, T, True, False, EPI_NONE, True)
+    ks = ksplit if ksplit is not None else 0
+    if _MODE == "auto":
+        if key not in GEMM_CHOICES:
+            if torch.cuda.is_current_stream_capturing():
+                return False
+            gemm(dy, x, ta=True, tb=False, out=torch.empty_like(out), beta=1.0, out_dtype=torch.float32,
+                 ksplit=ksplit)  # first call: measures the engines (into scratch)
+        c = GEMM_CHOICES.get(key)
+        if c is None or c[0] != "hip":
+            return False
+        if ksplit is None and len(c) > 3:
+            ks = c[3]
     part = torch.empty((max(ks, 1) if ks > 0 else 8, M), dtype=torch.float32, device=dy.device)
     return _hip_gemm(dy, x, True, False, out, beta=1.0, part=part, colsum=colsum_out, colsum_acc=True,
                      fp32="x6", ksplit=ks)

@@ -28,8 +28,6 @@ def run(mode, n=200):
         x.add_(1.0)
         if mode == "record":
             hip().stream_wait(side.cuda_stream, stream_handle())  # record on compute, side waits
-        elif mode == "wvalue":
-            hip().stream_wait_value(side.cuda_stream, stream_handle())  # write value on compute, side waits
         elif mode == "roundtrip":
             hip().stream_wait(side.cuda_stream, stream_handle())
             hip().stream_wait(stream_handle(), side.cuda_stream)  # and compute waits for side
@@ -42,9 +40,6 @@ def run(mode, n=200):
 
 if __name__ == "__main__":
     streams.reserve(torch.device("cuda", 0))
-    for m in ("plain", "wvalue", "record"):
-        ts = sorted(run(m) for _ in range(5))
-        print("%-12s %.2f us per step (median of 5)" % (m, ts[2]))
     for flags in (0, 1, 2):
         hip().set_stream_wait_flags(flags)
         for m in ("plain", "record", "roundtrip"):
