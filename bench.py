@@ -390,6 +390,15 @@ def _set_flag(mod, name, v):
     setattr(importlib.import_module(mod), name, v)
 
 
+def _set_head_engine(engine):
+    from hetseq_amd.ops import gemm as G
+
+    for k in list(G.GEMM_CHOICES):
+        if len(k) == 7 and 640 in k[:3] and 30522 not in k[:3]:  # (M, N, K, ta, tb, epi, beta)
+            c = G.GEMM_CHOICES[k]
+            G.GEMM_CHOICES[k] = (engine,) + tuple(c[1:])
+
+
 # runtime variants for --ab (switches that take effect on the next step without a rebuild)
 _AB = {
     "dks1": lambda: _set_flag("hetseq_amd.runtime.streams", "DGRAD_KSPLIT", 1),  # data-gradient K split
@@ -420,6 +429,8 @@ _AB = {
     "swf1": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_stream_wait_flags(1),
     "wcol_on": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_WGRAD_COLSUM", True),  # QKV bias grad in the wgrad
     "wcol_off": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_WGRAD_COLSUM", False),  # separate column sum
+    "head_hip": lambda: _set_head_engine("hip"),  # the MLM transform's 640-row products on the split-bf16 kernel
+    "head_blas": lambda: _set_head_engine("blas"),  # ... or the library (the isolated measurement's choice)
     "lnpo_on": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_LN_PARTIALS_WO", True),  # attention-output part
     "lnpo_off": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_LN_PARTIALS_WO", False),
 }
