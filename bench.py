@@ -431,6 +431,8 @@ _AB = {
     "wcol_off": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_WGRAD_COLSUM", False),  # separate column sum
     "head_hip": lambda: _set_head_engine("hip"),  # the MLM transform's 640-row products on the split-bf16 kernel
     "head_blas": lambda: _set_head_engine("blas"),  # ... or the library (the isolated measurement's choice)
+    "fresh_on": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FRESH_WGRAD", True),  # store after zero_grad
+    "fresh_off": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FRESH_WGRAD", False),  # always accumulate
     "lnpo_on": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_LN_PARTIALS_WO", True),  # attention-output part
     "lnpo_off": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_LN_PARTIALS_WO", False),
 }

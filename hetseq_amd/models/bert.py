@@ -420,6 +420,7 @@ class BertLayer(nn.Module):
         meta = {"weights": self._weights, "cfg": cfg, "recompute": recompute}
         if getattr(self, "_hs_store", None) is not None:
             meta["grad_sink"] = self._grad_views
+            meta["store"] = self._hs_store
         return FusedBertLayer.apply(x2d, mask_i64, meta, *self.fused_params())
 
     def _grad_views(self):

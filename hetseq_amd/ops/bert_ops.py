@@ -34,6 +34,8 @@ _LN_PARTIALS_WO = _LN_PARTIALS  # (the attention-output product's part of the sw
 # the QKV bias gradient summed by the QKV weight-gradient kernel (gemm.linear_wgrad_colsum) instead of
 # a column-sum pass over dqkv (HETSEQ_WGRAD_COLSUM=0: separate pass)
 _WGRAD_COLSUM = os.environ.get("HETSEQ_WGRAD_COLSUM", "1") == "1"
+# weight gradients store (beta 0) in the first backward after zero_grad (HETSEQ_FRESH_WGRAD=0: always add)
+_FRESH_WGRAD = os.environ.get("HETSEQ_FRESH_WGRAD", "1") == "1"
 from hetseq_amd.ops._C import dtype_code, hip, stream_handle
 from hetseq_amd.parallel import tied
 from hetseq_amd.runtime import rng, streams
@@ -553,12 +555,16 @@ class FusedBertLayer(torch.autograd.Function):
         dks = streams.DGRAD_KSPLIT if side else None  # K split of the dgrads beside the side stream
         rows = dh2.shape[0]
         dop = _planes_buf(rows, H, dh2.device) if pl else None  # the LN backwards write da as planes
+        # first backward after zero_grad: the weight gradients are the only writers of their regions
+        # and store instead of accumulating (the split-K reduce does not read the zeros back)
+        store = meta.get("store")
+        wacc = acc and not (side and _FRESH_WGRAD and store is not None and store.claim_fresh())
 
         def wgrad(dy, xin_, out):
             if not side:
                 return G.linear_wgrad(dy, xin_, out=out, accumulate=acc)
             ks = streams.side_ksplit(dy.shape[1], xin_.shape[1])
-            return streams.run(dy.device, lambda: G.linear_wgrad(dy, xin_, out=out, accumulate=acc,
+            return streams.run(dy.device, lambda: G.linear_wgrad(dy, xin_, out=out, accumulate=wacc,
                                                                  ksplit=ks), dy, xin_)
 
         # side-stream work forks at three points per layer; the launches at one point share one event
@@ -583,8 +589,8 @@ class FusedBertLayer(torch.autograd.Function):
             fused = False
             if side and not pl and _WGRAD_COLSUM:  # one launch: the bias gradient from the wgrad's staging
                 ks = streams.side_ksplit(dqkv.shape[1], xin.shape[1])
-                fused = streams.run(dqkv.device, lambda: G.linear_wgrad_colsum(dqkv, xin, Gv.wqkv, Gv.bqkv, ksplit=ks),
-                                    dqkv, xin)
+                fused = streams.run(dqkv.device, lambda: G.linear_wgrad_colsum(dqkv, xin, Gv.wqkv, Gv.bqkv, ksplit=ks,
+                                                                               accumulate=wacc), dqkv, xin)
             if fused:
                 dWqkv, dbqkv = Gv.wqkv, Gv.bqkv
             else:

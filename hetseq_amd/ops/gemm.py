@@ -673,8 +673,8 @@ def linear_wgrad(dy, x, out=None, accumulate=False, ksplit=None):
                 ksplit=ksplit)
 
 
-def linear_wgrad_colsum(dy, x, out, colsum_out, ksplit=None):
-    """``out += dy^T @ x`` and ``colsum_out += dy.sum(0)`` (a Linear's weight and bias gradients) in
+def linear_wgrad_colsum(dy, x, out, colsum_out, ksplit=None, accumulate=True):
+    """``out (+)= dy^T @ x`` and ``colsum_out (+)= dy.sum(0)`` (a Linear's weight and bias gradients) in
     one split-bf16 launch: the weight-gradient blocks of the first column tile sum dy's columns from
     the registers they stage (gemm.hip, ``wcol``), and one small pass adds the K slices' partials
     into ``colsum_out``.  Returns False when not served (library choice, first measuring call, other
@@ -701,8 +701,8 @@ def linear_wgrad_colsum(dy, x, out, colsum_out, ksplit=None):
         if ksplit is None and len(c) > 3:
             ks = c[3]
     part = torch.empty((max(ks, 1) if ks > 0 else 8, M), dtype=torch.float32, device=dy.device)
-    return _hip_gemm(dy, x, True, False, out, beta=1.0, part=part, colsum=colsum_out, colsum_acc=True,
-                     fp32="x6", ksplit=ks)
+    return _hip_gemm(dy, x, True, False, out, beta=1.0 if accumulate else 0.0, part=part, colsum=colsum_out,
+                     colsum_acc=accumulate, fp32="x6", ksplit=ks)
 
 
 def linear_gelu_fwd(x, w, b, planes_out=False, emit_planes=False, out=None):

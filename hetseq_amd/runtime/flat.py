@@ -132,8 +132,30 @@ class FlatParamStore(object):
     # post-accumulate-grad hook is the data-parallel readiness signal.
 
     # ------------------------------------------------------------ ops
+    # True from zero_grad() until the end of the first backward after it (end_fresh, queued by the
+    # first consumer): a weight gradient that is the only writer of its region may store instead of
+    # accumulating (the fused layer backward's weight-gradient products, ops/bert_ops.py) -- the
+    # zeros need not be read back.
+    grads_zero = False
+    _fresh_end_queued = False
+
     def zero_grad(self):
         self.grad.zero_()
+        self.grads_zero = True
+
+    def claim_fresh(self):
+        """Inside a backward: whether gradients are still all zero from zero_grad(); the first call
+        queues end_fresh() for the end of this backward (later backwards accumulate)."""
+        if not self.grads_zero:
+            return False
+        if not self._fresh_end_queued:
+            self._fresh_end_queued = True
+            torch.autograd.Variable._execution_engine.queue_callback(self.end_fresh)
+        return True
+
+    def end_fresh(self):
+        self.grads_zero = False
+        self._fresh_end_queued = False
         # re-attach views in case something replaced p.grad
         for p in self.params:
             if p.grad is None or p.grad.data_ptr() != self.grad.data_ptr() + 4 * self.offsets[id(p)]:
