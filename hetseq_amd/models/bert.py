@@ -791,6 +791,7 @@ class BertForPreTraining(BertPreTrainedModel):
         store = getattr(self, "_hs_store", None)
         if store is not None:
             meta["grad_sink"] = lambda: [store.grad_view(q) for q in params]
+            meta["store"] = store
         return FusedPreTrainingLoss.apply(seq2d, labels.reshape(-1).contiguous(), nsp_label.reshape(-1).contiguous(),
                                           meta, *params)
 

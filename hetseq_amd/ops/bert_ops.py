@@ -740,10 +740,14 @@ class FusedPreTrainingLoss(torch.autograd.Function):
         # decoder one lands in the tied word-embedding gradient: FusedEmbedding.backward waits)
         side = acc and streams.enabled()
         V = dlogits.shape[1]
+        # first backward after zero_grad: the decoder GEMM is the first writer of the tied table's
+        # gradient (the embedding backward adds its rows later): it stores, the 94 MB of zeros unread
+        store = meta.get("store")
+        dec_acc = not (side and _FRESH_WGRAD and store is not None and store.claim_fresh())
         if lbuf is not None:  # padded split-bf16 decoder products (pad columns of dlogits stay zero)
             def dwdec():
                 out_w = Gv[4] if acc else torch.zeros((V, t2.shape[1]), dtype=torch.float32, device=t2.device)
-                return G.decoder_wgrad(lbuf, t2, V, out_w, accumulate=True)
+                return G.decoder_wgrad(lbuf, t2, V, out_w, accumulate=dec_acc)
         else:
             def dwdec():
                 return G.linear_wgrad(dl_c, t2, out=Gv[4] if acc else None, accumulate=acc)

@@ -1,6 +1,7 @@
-"""Ordering-point bookkeeping of runtime/streams.py, on CPU with the HIP calls stubbed: consecutive
-forks inside ``streams.coalesced()`` record one event (the compute stream pays ~6.5 us of GPU time
-per ordering point, profiles/r3_forks.md), and a fork after the block records again."""
+"""Step bookkeeping on CPU: the ordering points of runtime/streams.py with the HIP calls stubbed
+(consecutive forks inside ``streams.coalesced()`` record one event -- the compute stream pays
+~6.5 us of GPU time per ordering point, profiles/r3_forks.md -- and a fork after the block records
+again), and the flat store's fresh-gradient window (runtime/flat.py claim_fresh)."""
 import pytest
 
 from hetseq_amd.runtime import streams
@@ -63,3 +64,33 @@ def test_nested_blocks_restore_the_outer_state(stub):
         streams.fork(None)
     assert len(stub.waits) == 2
     assert streams._state["coalesce"] == 0
+
+
+def test_fresh_gradients_claimed_for_one_backward_only():
+    """FlatParamStore.claim_fresh: True throughout the first backward after zero_grad (weight
+    gradients may store instead of accumulate), False from the end of that backward on."""
+    import torch
+
+    from hetseq_amd.runtime.flat import FlatParamStore
+
+    lin = torch.nn.Linear(4, 3)
+    store = FlatParamStore(lin)
+    seen = []
+
+    class Probe(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x):
+            return x * 1.0
+
+        @staticmethod
+        def backward(ctx, g):
+            seen.append((store.claim_fresh(), store.claim_fresh()))
+            return g
+
+    x = torch.randn(2, 4, requires_grad=True)
+    assert not store.claim_fresh()  # nothing zeroed yet: accumulate
+    store.zero_grad()
+    Probe.apply(x).sum().backward()
+    assert seen[-1] == (True, True) and not store.grads_zero
+    Probe.apply(x).sum().backward()  # a second micro-batch accumulates
+    assert seen[-1] == (False, False)
