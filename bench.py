@@ -410,6 +410,8 @@ _AB = {
     "fsplit_on": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FWD_SPLIT", True),  # half-batch forward chains
     "fsplit_off": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FWD_SPLIT", False),
     "wks2": lambda: _set_side_ks(2, 4),  # side-stream weight-gradient K split (default), small products 4
+    "wks4": lambda: _set_side_ks(4, 4),  # 4 slices for every weight gradient
+    "wks2s2": lambda: _set_side_ks(2, 2),
     "wks1": lambda: _set_side_ks(1, 1),  # no split-K (no reduce pass, fewer longer blocks)
     "wks1s4": lambda: _set_side_ks(1, 4),
     "attn_k": lambda: _set_attn(2),    # key-block fp32 attention backward (S <= 128)
