@@ -399,6 +399,14 @@ def _set_head_engine(engine):
             G.GEMM_CHOICES[k] = (engine,) + tuple(c[1:])
 
 
+def _set_decoder_dgrad_ks(ks):
+    from hetseq_amd.ops import gemm as G
+
+    for k, c in list(G.GEMM_CHOICES.items()):
+        if len(k) == 4 and k[3] == "decoder_dgrad" and c[0] == "hip":
+            G.GEMM_CHOICES[k] = tuple(c[:3]) + (ks,)
+
+
 # runtime variants for --ab (switches that take effect on the next step without a rebuild)
 _AB = {
     "dks1": lambda: _set_flag("hetseq_amd.runtime.streams", "DGRAD_KSPLIT", 1),  # data-gradient K split
@@ -435,6 +443,9 @@ _AB = {
     "head_blas": lambda: _set_head_engine("blas"),  # ... or the library (the isolated measurement's choice)
     "fresh_on": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FRESH_WGRAD", True),  # store after zero_grad
     "fresh_off": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FRESH_WGRAD", False),  # always accumulate
+    "ddec8": lambda: _set_decoder_dgrad_ks(8),  # K split of the tied decoder's data gradient (K = vocab)
+    "ddec16": lambda: _set_decoder_dgrad_ks(16),
+    "ddec32": lambda: _set_decoder_dgrad_ks(32),
     "lnpo_on": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_LN_PARTIALS_WO", True),  # attention-output part
     "lnpo_off": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_LN_PARTIALS_WO", False),
 }
