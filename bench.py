@@ -407,6 +407,14 @@ def _set_decoder_dgrad_ks(ks):
             G.GEMM_CHOICES[k] = tuple(c[:3]) + (ks,)
 
 
+def _set_site_ks(key, ks):
+    from hetseq_amd.ops import gemm as G
+
+    c = G.GEMM_CHOICES.get(key)
+    if c is not None:
+        G.GEMM_CHOICES[key] = tuple(c[:3]) + (ks,)
+
+
 # runtime variants for --ab (switches that take effect on the next step without a rebuild)
 _AB = {
     "dks1": lambda: _set_flag("hetseq_amd.runtime.streams", "DGRAD_KSPLIT", 1),  # data-gradient K split
@@ -446,6 +454,13 @@ _AB = {
     "ddec8": lambda: _set_decoder_dgrad_ks(8),  # K split of the tied decoder's data gradient (K = vocab)
     "ddec16": lambda: _set_decoder_dgrad_ks(16),
     "ddec32": lambda: _set_decoder_dgrad_ks(32),
+    # K split of the half-batch attention-output product (its partials go to the LN forward)
+    "wo_ks1": lambda: _set_site_ks((2048, 768, 768, False, True, 0, False), 1),
+    "wo_ks2": lambda: _set_site_ks((2048, 768, 768, False, True, 0, False), 2),
+    "wo_ks4": lambda: _set_site_ks((2048, 768, 768, False, True, 0, False), 4),
+    # ... and of the half-batch FFN-out product
+    "fo_ks2": lambda: _set_site_ks((2048, 768, 3072, False, True, 0, False), 2),
+    "fo_ks4": lambda: _set_site_ks((2048, 768, 3072, False, True, 0, False), 4),
     "lnpo_on": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_LN_PARTIALS_WO", True),  # attention-output part
     "lnpo_off": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_LN_PARTIALS_WO", False),
 }
