@@ -70,10 +70,11 @@ def test_ffn_out_partials_into_ln_bitwise(cuda, T, F_):
 
 @pytest.mark.parametrize("tile", [-1, 512])  # transposed-read A layout (default) / register transpose
 @pytest.mark.parametrize("ks", [2, 4])
-def test_wgrad_colsum_fused(cuda, tile, ks):
+@pytest.mark.parametrize("acc", [True, False])  # accumulate / store (first backward after zero_grad)
+def test_wgrad_colsum_fused(cuda, tile, ks, acc):
     """QKV-shaped weight gradient with the bias gradient summed by the same launch (the first column
-    tile's blocks add up the dy columns they stage): dW += dy^T x and db += sum_rows(dy), both
-    accumulated, against fp64."""
+    tile's blocks add up the dy columns they stage): dW (+)= dy^T x and db (+)= sum_rows(dy),
+    against fp64."""
     from hetseq_amd.ops import gemm as G
 
     torch.manual_seed(6)
@@ -82,8 +83,11 @@ def test_wgrad_colsum_fused(cuda, tile, ks):
     w0, c0 = torch.randn(M, N, device=cuda), torch.randn(M, device=cuda)
     w, c = w0.clone(), c0.clone()
     part = torch.empty((ks, M), dtype=torch.float32, device=cuda)
-    assert G._hip_gemm(dy, x, True, False, w, beta=1.0, part=part, colsum=c, colsum_acc=True, fp32="x6", ksplit=ks,
-                       tile=tile)
+    assert G._hip_gemm(dy, x, True, False, w, beta=1.0 if acc else 0.0, part=part, colsum=c, colsum_acc=acc,
+                       fp32="x6", ksplit=ks, tile=tile)
+    if not acc:
+        w0.zero_()
+        c0.zero_()
     d, xd = dy.double(), x.double()
     scale = w0.double().abs() + d.abs().t() @ xd.abs()
     assert float(((w.double() - (w0.double() + d.t() @ xd)).abs() / scale).max()) < 1e-6
