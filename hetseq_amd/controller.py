@@ -110,11 +110,12 @@ class Controller(object):
         if self._wrapped_model is None:
             multi = self.args.distributed_world_size > 1 or getattr(self.args, "force_ddp", False)
             if multi and dist.is_initialized() and not self.args.use_bmuf:
+                sparse, cap = self._sparse_embedding()
                 self._wrapped_model = FlatDDP(self._model, self.store, bucket_cap_mb=self.args.bucket_cap_mb,
                                               find_unused_parameters=self.args.find_unused_parameters,
                                               comm_engine=getattr(self.args, "comm_engine", "auto"),
                                               timeout_s=getattr(self.args, "collective_timeout", 1800.0),
-                                              sparse_embedding=self._sparse_embedding())
+                                              sparse_embedding=sparse, sparse_capacity=cap)
             else:
                 self._wrapped_model = self._model
                 if self.args.distributed_world_size > 1 and dist.is_initialized() and self.args.use_bmuf:
@@ -124,11 +125,23 @@ class Controller(object):
 
     def _sparse_embedding(self):
         """Embedding tables the data-parallel engine exchanges sparsely (parallel/tied.py), when the
-        model declares them and the fused BERT path (the only one handing rows over) is on."""
+        model declares them and the fused BERT path (the only one handing rows over) is on, and the
+        row capacity per micro-batch: the configured bound (``--max-sentences`` x the training data's
+        sequence length, or ``--max-tokens``), identical on every rank by construction, so no batch
+        can overflow it on one rank only.  (None, None) when no bound is known: dense tables."""
         fn = getattr(self._model, "sparse_embedding", None)
         if fn is None or getattr(self.args, "sparse_embedding_exchange", True) is False:
-            return None
-        return fn()
+            return None, None
+        ds = getattr(self.task, "datasets", {}).get(getattr(self.args, "train_subset", "train"))
+        S = getattr(ds, "seq_len", None)
+        cap = None
+        if getattr(self.args, "max_sentences", None) and S:
+            cap = int(self.args.max_sentences) * int(S)
+        elif getattr(self.args, "max_tokens", None):
+            cap = int(self.args.max_tokens)
+        if cap is None:
+            return None, None
+        return fn(), cap
 
     @property
     def optimizer(self):

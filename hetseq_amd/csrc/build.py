@@ -138,9 +138,40 @@ def _stamp_obj(name, digest, objdir, verbose):
 
 
 def _link(compiler, objs, out, ldflags, verbose):
-    tmp = out + ".tmp"
-    _run([compiler, "-shared", "-o", tmp] + objs + ldflags, verbose)
-    os.replace(tmp, out)  # atomic: a running process never sees a half-written .so
+    tmp = "%s.tmp.%d" % (out, os.getpid())  # per-process: two builders never share a half-written file
+    try:
+        _run([compiler, "-shared", "-o", tmp] + objs + ldflags, verbose)
+        os.replace(tmp, out)  # atomic: a running process never sees a half-written .so
+    finally:
+        if os.path.exists(tmp):
+            os.unlink(tmp)
+
+
+class _BuildLock(object):
+    """Inter-process lock around one module's build (``fcntl.flock`` on a file in BUILD_DIR).
+
+    Every rank of a multi-process launch may find the same stale stamp at import; without the lock
+    they would compile into the same object directory and link over each other.  The holder builds;
+    the others wait, then find the fresh stamp and return without building."""
+
+    def __init__(self, name):
+        os.makedirs(BUILD_DIR, exist_ok=True)
+        self.path = os.path.join(BUILD_DIR, ".lock" + name)
+        self.fh = None
+
+    def __enter__(self):
+        import fcntl
+
+        self.fh = open(self.path, "a+")
+        fcntl.flock(self.fh.fileno(), fcntl.LOCK_EX)
+        return self
+
+    def __exit__(self, *exc):
+        import fcntl
+
+        fcntl.flock(self.fh.fileno(), fcntl.LOCK_UN)
+        self.fh.close()
+        return False
 
 
 def _build_module(name, compiler, flags, sources, headers, ldflags, objdir, verbose, jobs, out=None,
@@ -150,9 +181,12 @@ def _build_module(name, compiler, flags, sources, headers, ldflags, objdir, verb
     digest = module_hash(name)
     if embedded_hash(out) == digest:
         return out
-    objs = _compile_objs(compiler, flags, sources, headers, objdir, verbose, jobs)
-    objs.append(_stamp_obj(name, digest, objdir, verbose))
-    _link(link_compiler or compiler, objs, out, ldflags, verbose)
+    with _BuildLock(name):
+        if embedded_hash(out) == digest:  # another process built it while this one waited
+            return out
+        objs = _compile_objs(compiler, flags, sources, headers, objdir, verbose, jobs)
+        objs.append(_stamp_obj(name, digest, objdir, verbose))
+        _link(link_compiler or compiler, objs, out, ldflags, verbose)
     return out
 
 

@@ -86,16 +86,27 @@ size_t elem_size(int code) {
 
 class Comm {
  public:
-  Comm(py::bytes uid, int nranks, int rank, int device, double timeout_s)
+  // Two-phase construction: the local part (device, comm stream) here, the blocking rendezvous in
+  // init() -- so every rank can report a local failure (parallel/comm.py create(), round 1) before
+  // any rank enters ncclCommInitRank, which waits for all of them.
+  Comm(int nranks, int rank, int device, double timeout_s)
       : nranks_(nranks), rank_(rank), device_(device), timeout_(timeout_s) {
+    hip_check(hipSetDevice(device_), "hipSetDevice");
+    int least = 0, greatest = 0;
+    hip_check(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
+    hip_check(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, greatest), "hipStreamCreateWithPriority");
+  }
+  Comm(py::bytes uid, int nranks, int rank, int device, double timeout_s) : Comm(nranks, rank, device, timeout_s) {
+    init(uid);
+  }
+
+  void init(py::bytes uid) {
+    if (comm_) throw std::logic_error("hetseq comm: init called twice");
     std::string u = uid;
     if (u.size() != sizeof(ncclUniqueId)) throw std::invalid_argument("hetseq comm: bad unique id size");
     ncclUniqueId id;
     std::memcpy(&id, u.data(), sizeof(id));
     hip_check(hipSetDevice(device_), "hipSetDevice");
-    int least = 0, greatest = 0;
-    hip_check(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
-    hip_check(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, greatest), "hipStreamCreateWithPriority");
     {
       py::gil_scoped_release nogil;  // a blocking rendezvous among the ranks
       nccl_check(ncclCommInitRank(&comm_, nranks_, id, rank_), "ncclCommInitRank");
@@ -396,6 +407,9 @@ PYBIND11_MODULE(_comm, m) {
   py::class_<Comm>(m, "Comm")
       .def(py::init<py::bytes, int, int, int, double>(), py::arg("uid"), py::arg("nranks"), py::arg("rank"),
            py::arg("device"), py::arg("timeout_s"))
+      .def(py::init<int, int, int, double>(), py::arg("nranks"), py::arg("rank"), py::arg("device"),
+           py::arg("timeout_s"))
+      .def("init", &Comm::init, py::arg("uid"), "the blocking RCCL rendezvous of a two-phase construction")
       .def("all_reduce_async", &Comm::all_reduce_async, py::arg("ptr"), py::arg("count"), py::arg("dtype"),
            py::arg("op"), py::arg("producers"))
       .def("all_gather_async", &Comm::all_gather_async, py::arg("send"), py::arg("recv"), py::arg("count"),

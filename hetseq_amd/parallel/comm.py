@@ -45,7 +45,10 @@ def _stream(s=None):
 class NativeComm(object):
     """One RCCL communicator over the ranks of ``group`` (all of them take part in construction)."""
 
-    def __init__(self, group=None, timeout_s=1800.0, device=None):
+    def __init__(self, group=None, timeout_s=1800.0, device=None, rendezvous=True):
+        """``rendezvous=False``: only the local part (device, comm stream) and the unique-id
+        exchange through the c10d store; :meth:`rendezvous` then enters ncclCommInitRank (create()
+        agrees across ranks in between)."""
         mod = module()
         if mod is None:
             raise RuntimeError("hetseq_amd._comm is not built (python -m hetseq_amd.csrc.build)")
@@ -57,12 +60,18 @@ class NativeComm(object):
         store = dist.distributed_c10d._get_default_store()
         if self.rank == 0:
             store.set(key, mod.unique_id())
-        uid = store.get(key)  # blocks until rank 0 published it (the store's own timeout applies)
-        self._c = mod.Comm(uid, self.size, self.rank, self.device, float(timeout_s))
+        self._uid = store.get(key)  # blocks until rank 0 published it (the store's own timeout applies)
+        self._c = mod.Comm(self.size, self.rank, self.device, float(timeout_s))
         # at interpreter exit (no explicit close): abort -- frees the communicator without waiting
         # for peers, while the HIP runtime is still alive (never from static destructors)
         ref = weakref.ref(self)
         atexit.register(lambda: ref() is not None and ref()._c.close(False))
+        if rendezvous:
+            self.rendezvous()
+
+    def rendezvous(self):
+        """The blocking RCCL rendezvous (every rank of the group must call it)."""
+        self._c.init(self._uid)
 
     # ------------------------------------------------------------------ bucket path
     def all_reduce_async(self, t, producers=(), op="sum"):
@@ -185,15 +194,20 @@ def _fault(point, rank):
 def create(engine, device_is_cuda, group=None, timeout_s=1800.0, factory=None):
     """A NativeComm when the native engine works on EVERY rank, else None (c10d path).
 
-    Construction is a cross-rank-agreed, two-round protocol, so one rank's failure never leaves
-    the others inside the RCCL rendezvous or with a half-working engine:
+    Construction is a cross-rank-agreed, two-round protocol, so a local failure on one rank never
+    leaves the others inside the RCCL rendezvous or with a half-working engine:
 
-    1. every rank checks what it can without the rendezvous (module built, backend, device,
-       injected ``init`` fault); the ranks agree (c10d all-reduce) before anyone calls
-       ncclCommInitRank, which blocks until all ranks join it;
-    2. every rank builds the communicator and runs one all-reduce through it, checking the
-       result on the host; the ranks agree again, and on any failure every rank aborts its
-       communicator (never waits for peers) and falls back to c10d.
+    1. every rank does everything that needs no rendezvous -- module built, backend, injected
+       ``init`` fault, and the engine's local construction (device, greatest-priority comm stream,
+       rank 0's unique id published through the c10d store and fetched by all); the ranks agree
+       (c10d all-reduce) before anyone calls ncclCommInitRank, which blocks until all ranks join;
+    2. every rank enters the rendezvous and runs one all-reduce through the communicator,
+       checking the result on the host; the ranks agree again, and on any failure every rank
+       aborts its communicator (never waits for peers) and falls back to c10d.
+
+    What round 1 cannot cover is a failure INSIDE ncclCommInitRank on some ranks only (the
+    library's own bootstrap, whose failures normally reach every rank): the others then wait in
+    the rendezvous until RCCL's bootstrap timeout, not the collective timeout.
 
     The outcome and the failure reason land in :data:`LAST_STATUS`.  ``factory`` replaces the
     NativeComm constructor (tests drive the protocol over gloo with a stand-in engine).
@@ -209,20 +223,27 @@ def create(engine, device_is_cuda, group=None, timeout_s=1800.0, factory=None):
     size = dist.get_world_size(group)
     dev = "cuda" if backend == "nccl" else "cpu"
     reason = None
-    try:  # round 1: local checks only
+    nc = None
+    try:  # round 1: everything local (no rendezvous)
         if factory is None and not want_native(engine, device_is_cuda, group):
             reason = "native engine not requested or not built"
         elif _fault("init", rank):
             reason = "injected init fault on rank %d" % rank
-    except RuntimeError as e:
-        reason = str(e)
+        else:
+            nc = (factory or NativeComm)(group, timeout_s=timeout_s, rendezvous=False)
+    except Exception as e:  # noqa: BLE001 - any local failure turns into the agreed fallback
+        reason = "%s: %s" % (type(e).__name__, e)
     if not _agree(reason is None, group, dev):
+        if nc is not None:
+            try:
+                nc.close(False)  # never entered the rendezvous: frees the local stream
+            except Exception:  # noqa: BLE001
+                pass
         LAST_STATUS = {"engine": "c10d", "reason": reason or "native engine unavailable on another rank"}
         warnings.warn("native RCCL engine not used: %s; using c10d" % LAST_STATUS["reason"])
         return None
-    nc = None
     try:  # round 2: rendezvous + one verified collective
-        nc = (factory or NativeComm)(group, timeout_s=timeout_s)
+        nc.rendezvous()
         t = torch.ones(1, device=dev)
         nc.all_reduce(t)
         if _fault("first", rank):

@@ -67,7 +67,8 @@ class FlatDDP(torch.nn.Module):
         # embedding backward
         self.tables = None
         own = set()
-        if sparse_embedding is not None and SparseTableSync.supported(store, list(sparse_embedding[0])):
+        if (sparse_embedding is not None and SparseTableSync.supported(store, list(sparse_embedding[0]))
+                and SparseTableSync.pays(self.world_size, sparse_capacity, list(sparse_embedding[0]))):
             tables, rest = sparse_embedding
             self.tables = SparseTableSync(self, list(tables), sparse_capacity)
             own = {id(p) for p in rest}
@@ -117,20 +118,27 @@ class FlatDDP(torch.nn.Module):
         self.next_launch = 0
         self.works = []
         self.callback_queued = False
-        # collectives of this step: (what, bytes per rank, issued after the last backward kernel)
+        # collectives of this step: (what, payload bytes per rank, issued after the last backward
+        # kernel, bytes each rank RECEIVES over the links)
         self.comm_log = []
         self._in_tail = False
 
-    def _log(self, what, t):
-        self.comm_log.append((what, t.numel() * t.element_size(), self._in_tail))
+    def _log(self, what, t, kind="allreduce"):
+        n = t.numel() * t.element_size()
+        W = self.world_size
+        # ring collectives: an all-reduce receives 2(W-1)/W of the payload, an all-gather the other
+        # W-1 ranks' payloads
+        recv = (W - 1) * n if kind == "allgather" else 2 * (W - 1) * n // max(W, 1)
+        self.comm_log.append((what, n, self._in_tail, recv))
 
     def _tail_started(self):
         """Called once the last backward Function enqueued its kernels (the embedding backward)."""
         self._in_tail = True
 
     def tail_bytes(self):
-        """Bytes per rank of the collectives issued after the last backward kernel (this step)."""
-        return sum(b for _, b, tail in self.comm_log if tail)
+        """Bytes each rank receives in the collectives issued after the last backward kernel (this
+        step): what the exposed communication tail has to move over the links."""
+        return sum(r for _, _, tail, r in self.comm_log if tail)
 
     # ------------------------------------------------------------- forward
     def forward(self, *inputs, **kwargs):

@@ -29,10 +29,14 @@ a tail no backward compute overlaps.  ``SparseTableSync`` splits it:
    same inputs in the same order on every rank, so the replicas stay bit-identical.
 
 The result is the dense path's sum (decoder + all ranks' rows) up to fp32 summation order.
-``cap`` (tokens per rank per micro-batch) is agreed once, as the maximum over ranks of the first
-synchronised micro-batch, unless given; a later, larger micro-batch raises.  ``no_sync`` micro
-batches, non-fused models and inference take the dense path: the region is then reduced at the
-end of backward like an ordinary bucket.
+``cap`` (tokens per rank per micro-batch) is the configured bound the controller passes
+(``--max-sentences`` x sequence length, or ``--max-tokens``): the same on every rank, and no batch
+the batcher builds can exceed it.  Only a caller that passes no capacity gets the older rule (the
+maximum over ranks of the first synchronised micro-batch; a later, larger micro-batch raises).
+The engine uses the exchange only while it moves fewer bytes after backward than the dense
+bucket would (``pays``: W x cap < 2 x region rows).  ``no_sync`` micro batches, non-fused models
+and inference take the dense path: the region is then reduced at the end of backward like an
+ordinary bucket.
 """
 from __future__ import annotations
 
@@ -68,6 +72,22 @@ class SparseTableSync(object):
                 return False
             end += p.numel()
         return len(tables) == 3
+
+    @staticmethod
+    def pays(world, capacity, tables):
+        """Whether the sparse exchange beats the dense last bucket at this world size.
+
+        After the last backward kernel the dense path all-reduces the whole region (each rank
+        receives 2(W-1)/W x K x H floats over its links); the sparse path all-gathers the rows
+        ((W-1) x cap x H floats received) -- and on top of that holds W x 3 x cap x H floats of
+        scratch for the sorted-run scatter.  It pays while (W-1) x cap < 2(W-1)/W x K, i.e.
+        W x cap < 2K: BERT-base (K = 31,036 rows) at cap 4,096 tokens up to W = 15.  Without a
+        capacity (tests, or a caller that lets the first synchronised micro-batch set it) the
+        caller opted in explicitly."""
+        if capacity is None:
+            return True
+        K = sum(int(p.shape[0]) for p in tables)
+        return world * int(capacity) < 2 * K
 
     def __init__(self, ddp, tables, capacity=None):
         store = ddp.store
@@ -168,7 +188,7 @@ class SparseTableSync(object):
         if n < self.cap:
             keys[:, n:].fill_(self.K)
         comm = self.ddp.comm
-        self.ddp._log("keys", keys)
+        self.ddp._log("keys", keys, "allgather")
         if comm is not None and keys.is_cuda:
             comm.all_gather_async(b["keys_all"], keys, producers=(torch.cuda.current_stream(keys.device),))
             # sort right behind the gather on the comm stream itself (idle during forward): no other
@@ -232,7 +252,7 @@ class SparseTableSync(object):
         b = self._bufs
         comm = self.ddp.comm
         profiling.range_push("allgather_rows")
-        self.ddp._log("rows", b["rows"])
+        self.ddp._log("rows", b["rows"], "allgather")
         if comm is not None and b["rows"].is_cuda:
             comm.all_gather_async(b["rows_all"], b["rows"], producers=(torch.cuda.current_stream(self.device),))
         else:

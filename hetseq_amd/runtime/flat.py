@@ -142,6 +142,11 @@ class FlatParamStore(object):
     def zero_grad(self):
         self.grad.zero_()
         self.grads_zero = True
+        # re-attach views in case something replaced p.grad (pointer compares, every path)
+        for p in self.params:
+            if p.grad is None or p.grad.data_ptr() != self.grad.data_ptr() + 4 * self.offsets[id(p)]:
+                off = self.offsets[id(p)]
+                p.grad = self.grad[off : off + p.numel()].view(p.shape)
 
     def claim_fresh(self):
         """Inside a backward: whether gradients are still all zero from zero_grad(); the first call
@@ -156,11 +161,6 @@ class FlatParamStore(object):
     def end_fresh(self):
         self.grads_zero = False
         self._fresh_end_queued = False
-        # re-attach views in case something replaced p.grad
-        for p in self.params:
-            if p.grad is None or p.grad.data_ptr() != self.grad.data_ptr() + 4 * self.offsets[id(p)]:
-                off = self.offsets[id(p)]
-                p.grad = self.grad[off : off + p.numel()].view(p.shape)
 
     def sync_shadow(self):
         if self.shadow is None:

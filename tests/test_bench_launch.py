@@ -98,9 +98,15 @@ def _fallback_worker(rank, world, path, fault, q):
         """Stand-in engine: all-reduce through gloo, records that it was closed."""
 
         closed = None
+        entered = False  # the (blocking) rendezvous was entered
 
-        def __init__(self, group, timeout_s=0.0):
+        def __init__(self, group, timeout_s=0.0, rendezvous=True):
             self.group = group
+            if rendezvous:
+                self.rendezvous()
+
+        def rendezvous(self):
+            FakeComm.entered = True
 
         def all_reduce(self, t, op="sum", stream=None):
             dist.all_reduce(t, group=self.group)
@@ -114,7 +120,7 @@ def _fallback_worker(rank, world, path, fault, q):
 
     try:
         c = comm.create("native", False, factory=FakeComm)
-        q.put((rank, c is not None, comm.LAST_STATUS, FakeComm.closed))
+        q.put((rank, c is not None, comm.LAST_STATUS, FakeComm.closed, FakeComm.entered))
     finally:
         dist.destroy_process_group()
 
@@ -149,7 +155,8 @@ def test_init_fault_on_one_rank_falls_back_everywhere(tmp_path):
     assert all(o[2]["engine"] == "c10d" for o in out)
     assert "injected init fault on rank 1" in out[1][2]["reason"]
     assert "another rank" in out[0][2]["reason"]
-    assert all(o[3] is None for o in out)  # no engine was built, so none to close
+    assert not any(o[4] for o in out)  # nobody entered the rendezvous
+    assert out[0][3] is False and out[1][3] is None  # rank 0 freed its local part (abort), rank 1 built none
 
 
 @pytest.mark.slow
@@ -158,3 +165,4 @@ def test_bad_first_collective_aborts_on_every_rank(tmp_path):
     assert [o[1] for o in out] == [False, False]
     assert "first all-reduce returned" in out[0][2]["reason"]
     assert all(o[3] is False for o in out)  # every rank aborted (never a graceful, peer-waiting close)
+    assert all(o[4] for o in out)  # after both entered the rendezvous

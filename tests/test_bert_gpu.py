@@ -57,24 +57,37 @@ def test_fused_matches_reference_loss_and_grads(cuda):
         assert d <= 2e-3 * scale + 1e-6, (n, d, scale)
 
 
-def test_direct_flat_grads_match_autograd_grads(cuda):
-    """With a flat store attached, fused kernels accumulate grads in place; values must match."""
+@pytest.mark.parametrize("side", [False, True])
+def test_direct_flat_grads_match_autograd_grads(cuda, side):
+    """With a flat store attached, fused kernels accumulate grads in place; values must match.
+    Run the way a real update does: zero_grad() opens the fresh-gradient window, so with the side
+    stream on the first backward STORES the weight / fused QKV-bias / tied-decoder gradients (the
+    embedding rows then add onto the decoder's store) and the second backward accumulates."""
+    from hetseq_amd.runtime import streams
     from hetseq_amd.runtime.flat import FlatParamStore
 
-    model, cfg = _tiny(cuda)
-    model.eval()
-    model.max_predictions_per_seq = 10
-    ref = copy.deepcopy(model)
-    store = FlatParamStore(model)
-    model.attach_store(store, torch.float32)
-    batch = _batch(cuda, 4, 64, cfg.vocab_size)
-    for _ in range(2):  # two micro-batches: in-place accumulation must add up
-        model(*batch).backward()
-        ref(*batch).backward()
-    for (n, p1), (_, p2) in zip(model.named_parameters(), ref.named_parameters()):
-        assert p1.grad.data_ptr() == store.grad_view(p1).data_ptr(), n
-        d = (p1.grad - p2.grad).abs().max().item()
-        assert d <= 1e-4 * (p2.grad.abs().max().item() + 1e-6) + 1e-7, (n, d)
+    old = streams.enabled()
+    streams.set_enabled(side)
+    try:
+        model, cfg = _tiny(cuda)
+        model.eval()
+        model.max_predictions_per_seq = 10
+        ref = copy.deepcopy(model)
+        store = FlatParamStore(model)
+        model.attach_store(store, torch.float32)
+        batch = _batch(cuda, 4, 64, cfg.vocab_size)
+        store.grad.fill_(123.0)  # stale values: only a store or zero_grad may remove them
+        store.zero_grad()
+        for _ in range(2):  # two micro-batches: the first stores (side), the second accumulates
+            model(*batch).backward()
+            ref(*batch).backward()
+        torch.cuda.synchronize()
+        for (n, p1), (_, p2) in zip(model.named_parameters(), ref.named_parameters()):
+            assert p1.grad.data_ptr() == store.grad_view(p1).data_ptr(), n
+            d = (p1.grad - p2.grad).abs().max().item()
+            assert d <= 1e-4 * (p2.grad.abs().max().item() + 1e-6) + 1e-7, (n, d)
+    finally:
+        streams.set_enabled(old)
 
 
 def test_fused_train_step_with_store_and_dropout(cuda):

@@ -135,12 +135,12 @@ def _tied_worker(rank, port, q, sparse):
         assert (net.tables is not None) == sparse
         ids, tt, mask, labels, nsp = _batch(cuda, 4, 64, cfg.vocab_size)
         ids = (ids + 37 * rank) % cfg.vocab_size  # different tokens per rank, some shared
-        store.grad.zero_()
+        store.zero_grad()  # opens the fresh-gradient window (store-mode weight gradients)
         for micro in range(2):  # update_freq 2: a no_sync micro-batch first (dense local tables)
             with (net.no_sync() if micro == 0 else torch.enable_grad()):
                 net(ids, tt, mask, labels, nsp).backward()
         torch.cuda.synchronize()
-        q.put((rank, store.grad.cpu().numpy().copy(), [w for w, _, late in net.comm_log if late]))
+        q.put((rank, store.grad.cpu().numpy().copy(), [w for w, _, late, _ in net.comm_log if late]))
         dist.destroy_process_group()
     except BaseException as e:
         q.put((rank, None, repr(e)))

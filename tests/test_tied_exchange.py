@@ -186,12 +186,13 @@ def test_sparse_tables_match_dense_engine(micro_batches):
     assert torch.equal(g0, sp[1][0])  # replicas identical
     assert torch.allclose(g0, dn[0][0], atol=1e-5, rtol=1e-5)
     assert torch.allclose(g0, ref, atol=1e-5, rtol=1e-5)
-    names = [w for w, _, _ in log]
+    names = [w for w, *_ in log]
     # keys in forward, the tables' dense bucket before every encoder bucket, rows after backward
     assert names[0] == "keys" and names[1] == "allreduce_tables", names
-    tail = [(w, b) for w, b, t in log if t]
+    tail = [(w, b) for w, b, t, _ in log if t]
     assert [w for w, _ in tail][0] == "rows", tail
     assert sum(b for w, b in tail if w == "rows") == 15 * H * 4  # B*S*H*4 per rank
+    assert sum(r for w, _, t, r in log if t and w == "rows") == 15 * H * 4  # received: (W-1) x payload
     # at most the embedding LayerNorm's own bucket (two H-vectors, each padded to 256 B in the flat buffer)
     assert sum(b for w, b in tail if w != "rows") <= 2 * 256
 
@@ -202,5 +203,42 @@ def test_sparse_tables_pad_small_micro_batch():
     g0 = sp[0][0]
     assert torch.equal(g0, sp[1][0])
     assert torch.allclose(g0, ref, atol=1e-5, rtol=1e-5)
-    rows = [b for w, b, _ in sp[0][1] if w == "rows"]
+    rows = [b for w, b, *_ in sp[0][1] if w == "rows"]
     assert rows == [15 * H * 4]  # the agreed capacity, 10 real rows + 5 padding rows
+
+
+def test_sparse_policy_by_world_size():
+    """The sparse exchange is used only while its tail (the row all-gather, (W-1) x cap x H received
+    per rank) is smaller than the dense bucket's all-reduce of the region (2(W-1)/W x K x H):
+    BERT-base tables at 4,096 tokens per rank pay up to W = 15, not at 16; without a configured
+    capacity the caller opted in."""
+    from hetseq_amd.parallel.tied import SparseTableSync
+
+    tables = [torch.empty(30522, 1), torch.empty(512, 1), torch.empty(2, 1)]
+    assert SparseTableSync.pays(2, 4096, tables)
+    assert SparseTableSync.pays(8, 4096, tables)
+    assert SparseTableSync.pays(15, 4096, tables)
+    assert not SparseTableSync.pays(16, 4096, tables)
+    assert not SparseTableSync.pays(8, 8 * 4096, tables)  # seq 512 x 64 sentences per rank: dense
+    assert SparseTableSync.pays(64, None, tables)
+
+
+def test_received_bytes_accounting():
+    """comm_log records what each rank RECEIVES: all-gather (W-1) x payload, ring all-reduce
+    2(W-1)/W x payload; tail_bytes sums the received bytes of the collectives after backward."""
+    from hetseq_amd.parallel.ddp import FlatDDP
+
+    class _Fake(object):
+        world_size = 8
+        comm_log = []
+        _in_tail = False
+
+    f = _Fake()
+    t = torch.empty(1000)
+    FlatDDP._log(f, "keys", t, "allgather")
+    f._in_tail = True
+    FlatDDP._log(f, "rows", t, "allgather")
+    FlatDDP._log(f, "allreduce_bucket9", t)
+    assert f.comm_log[1] == ("rows", 4000, True, 7 * 4000)
+    assert f.comm_log[2] == ("allreduce_bucket9", 4000, True, 2 * 7 * 4000 // 8)
+    assert FlatDDP.tail_bytes(f) == 7 * 4000 + 7000
