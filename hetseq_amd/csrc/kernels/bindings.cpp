@@ -32,12 +32,13 @@ void launch_cast_f32_bf16(const float*, void*, int64_t, hipStream_t);
 // layernorm.hip
 int ln_bwd_num_blocks();
 int launch_ln_fwd(int, const void*, const float*, const void*, const float*, const float*, void*, float*, float*,
-                  float*, int, int, float, float, u64, u64, int, void*, int64_t, int, int64_t, int, hipStream_t);
+                  float*, int, int, float, float, u64, u64, int, void*, int64_t, int, int64_t, int, float*,
+                  hipStream_t);
 int launch_ln_bwd(int, const void*, const float*, const float*, const float*, const float*, void*, void*, float*,
-                  float*, float*, int, int, float, u64, u64, int, void*, int64_t, hipStream_t);
+                  float*, float*, int, int, float, u64, u64, int, void*, int64_t, float*, hipStream_t);
 int launch_emb_fwd(int, const int64_t*, const int64_t*, const float*, const float*, const float*, const float*,
                    const float*, void*, float*, float*, float*, int, int, int, int, int, float, float, u64, u64, int*,
-                   hipStream_t);
+                   float*, hipStream_t);
 int launch_emb_bwd(int, const void*, const float*, const float*, const float*, const float*, float*, float*, float*,
                    const int64_t*, float*, int, int, float, u64, u64, hipStream_t);
 void launch_colpart_finalize(const float* const*, float* const*, int, int, int, int, hipStream_t);
@@ -51,6 +52,8 @@ void launch_colsum(int, const void*, const void*, const float*, void*, float*, f
 void launch_mlm_compact(const int64_t*, int, int, int, int32_t*, int64_t*, int32_t*, int*, hipStream_t);
 void launch_gather_rows(int, const void*, const int32_t*, void*, int, int, hipStream_t);
 void launch_scatter_add_rows(int, const void*, const int32_t*, void*, int, int, hipStream_t);
+int launch_amax(const float*, int64_t, float*, int, hipStream_t);
+void launch_amax_seg(const float*, const int64_t*, int, float*, hipStream_t);
 // pool_nsp.hip
 int launch_pool_nsp_fwd(int, const void*, int, int, int, const float*, const float*, const float*, const float*,
                         const int64_t*, const float*, float*, float*, float*, float*, float*, hipStream_t);
@@ -78,7 +81,8 @@ int gemm_last_ksplit();
 int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, int64_t lda, const void* B,
                 int64_t ldb, void* C, int64_t ldc, const float* bias, int epi, float beta, float* aux, int64_t ldaux,
                 float* part, float* colsum_out, int colsum_acc, int tile_override, hipStream_t st, int ksplit,
-                float* slab, int64_t slab_floats, int mv, int nv, int kv);
+                float* slab, int64_t slab_floats, int mv, int nv, int kv, const float* amax_a, int namax_a,
+                const float* amax_b, int namax_b, float* amax_c);
 
 // gemm_planes.hip
 int launch_gemm_planes(int planes, int c_dtype, int ta, int tb, int M, int N, int K, const void* A, int64_t lda,
@@ -215,36 +219,40 @@ PYBIND11_MODULE(_hip, m) {
   m.def("ln_bwd_num_blocks", &ln_bwd_num_blocks);
   m.def("ln_fwd", [](int dt, i64 a, i64 bias, i64 resid, i64 gamma, i64 beta, i64 y, i64 zsave, i64 mean, i64 rstd,
                      int rows, int H, float eps, float p, u64 seed, u64 off, int mode, i64 st, i64 yp, i64 yps,
-                     int nslab, i64 slab_stride, int row0) {
+                     int nslab, i64 slab_stride, int row0, i64 amax) {
     pre_launch("ln_fwd");
     check(launch_ln_fwd(dt, P(const void*, a), P(const float*, bias), P(const void*, resid), P(const float*, gamma),
                         P(const float*, beta), P(void*, y), P(float*, zsave), P(float*, mean), P(float*, rstd), rows, H,
-                        eps, p, seed, off, mode, P(void*, yp), yps, nslab, slab_stride, row0, ST(st)),
+                        eps, p, seed, off, mode, P(void*, yp), yps, nslab, slab_stride, row0, P(float*, amax), ST(st)),
           "ln_fwd");
   }, py::arg("dt"), py::arg("a"), py::arg("bias"), py::arg("resid"), py::arg("gamma"), py::arg("beta"), py::arg("y"),
      py::arg("zsave"), py::arg("mean"), py::arg("rstd"), py::arg("rows"), py::arg("H"), py::arg("eps"), py::arg("p"),
      py::arg("seed"), py::arg("off"), py::arg("mode"), py::arg("st"), py::arg("yp") = 0, py::arg("yps") = 0,
-     py::arg("nslab") = 1, py::arg("slab_stride") = 0, py::arg("row0") = 0);
+     py::arg("nslab") = 1, py::arg("slab_stride") = 0, py::arg("row0") = 0, py::arg("amax") = 0);
   m.def("ln_bwd", [](int dt, i64 dy, i64 zsave, i64 mean, i64 rstd, i64 gamma, i64 dz, i64 da, i64 pg, i64 pb, i64 pbias,
-                     int rows, int H, float p, u64 seed, u64 off, int mode, i64 st, i64 dap, i64 daps) {
+                     int rows, int H, float p, u64 seed, u64 off, int mode, i64 st, i64 dap, i64 daps, i64 amax) {
     pre_launch("ln_bwd");
     check(launch_ln_bwd(dt, P(const void*, dy), P(const float*, zsave), P(const float*, mean), P(const float*, rstd),
                         P(const float*, gamma), P(void*, dz), P(void*, da), P(float*, pg), P(float*, pb),
-                        P(float*, pbias), rows, H, p, seed, off, mode, P(void*, dap), daps, ST(st)),
+                        P(float*, pbias), rows, H, p, seed, off, mode, P(void*, dap), daps, P(float*, amax), ST(st)),
           "ln_bwd");
   }, py::arg("dt"), py::arg("dy"), py::arg("zsave"), py::arg("mean"), py::arg("rstd"), py::arg("gamma"), py::arg("dz"),
      py::arg("da"), py::arg("pg"), py::arg("pb"), py::arg("pbias"), py::arg("rows"), py::arg("H"), py::arg("p"),
-     py::arg("seed"), py::arg("off"), py::arg("mode"), py::arg("st"), py::arg("dap") = 0, py::arg("daps") = 0);
+     py::arg("seed"), py::arg("off"), py::arg("mode"), py::arg("st"), py::arg("dap") = 0, py::arg("daps") = 0,
+     py::arg("amax") = 0);
   m.def("emb_fwd", [](int dt, i64 ids, i64 tt, i64 w, i64 pe, i64 te, i64 gamma, i64 beta, i64 y, i64 zsave, i64 mean,
                       i64 rstd, int rows, int S, int H, int V, int TV, float eps, float p, u64 seed, u64 off, i64 err,
-                      i64 st) {
+                      i64 st, i64 amax) {
     pre_launch("emb_fwd");
     check(launch_emb_fwd(dt, P(const int64_t*, ids), P(const int64_t*, tt), P(const float*, w), P(const float*, pe),
                          P(const float*, te), P(const float*, gamma), P(const float*, beta), P(void*, y),
                          P(float*, zsave), P(float*, mean), P(float*, rstd), rows, S, H, V, TV, eps, p, seed, off,
-                         P(int*, err), ST(st)),
+                         P(int*, err), P(float*, amax), ST(st)),
           "emb_fwd");
-  });
+  }, py::arg("dt"), py::arg("ids"), py::arg("tt"), py::arg("w"), py::arg("pe"), py::arg("te"), py::arg("gamma"),
+     py::arg("beta"), py::arg("y"), py::arg("zsave"), py::arg("mean"), py::arg("rstd"), py::arg("rows"), py::arg("S"),
+     py::arg("H"), py::arg("V"), py::arg("TV"), py::arg("eps"), py::arg("p"), py::arg("seed"), py::arg("off"),
+     py::arg("err"), py::arg("st"), py::arg("amax") = 0);
   m.def("emb_bwd", [](int dt, i64 dy, i64 zsave, i64 mean, i64 rstd, i64 gamma, i64 dx, i64 pg, i64 pb, i64 tt, i64 pt,
                       int rows, int H, float p, u64 seed, u64 off, i64 st) {
     pre_launch("emb_bwd");
@@ -432,6 +440,17 @@ PYBIND11_MODULE(_hip, m) {
     check_launch("scatter_add_rows");
   });
 
+  m.def("amax", [](i64 x, i64 n, i64 out, int zero_first, i64 st) {
+    pre_launch("amax");
+    check(launch_amax(P(const float*, x), n, P(float*, out), zero_first, ST(st)), "amax");
+  }, "|max| of n fp32 values (n % 4 == 0, 16-B aligned) atomically maxed into *out (cleared first if zero_first)");
+  m.def("amax_seg", [](i64 base, i64 tab, int nblk, i64 out, i64 st) {
+    pre_launch("amax_seg");
+    launch_amax_seg(P(const float*, base), P(const int64_t*, tab), nblk, P(float*, out), ST(st));
+    check_launch("amax_seg");
+  }, "per-segment |max| over a flat fp32 buffer: tab = [nblk][3] int64 (segment, first float4, end float4); out "
+     "must be zeroed");
+
   m.def("set_attn_fp32_mode", &set_attn_fp32_mode, "fp32 attention products: 1 split-bf16 (x6), 0 exact-fp32 MFMA");
   m.def("set_attn_bwd_x6_planes", &set_attn_bwd_x6_planes,
         "fp32 split-bf16 attention backward: 2 key-block kernel (S <= 128) / plane-image pair, 1 plane-image dQ / dKV "
@@ -502,12 +521,14 @@ PYBIND11_MODULE(_hip, m) {
         "K slices of the last split-bf16 GEMM launch (with C = 0 its partials stay in the slab)");
   m.def("gemm", [](int dt, int ta, int tb, int M, int N, int K, i64 A, i64 lda, i64 B, i64 ldb, i64 C, i64 ldc, i64 bias,
                    int epi, float beta, i64 aux, i64 ldaux, i64 part, i64 colsum, int colsum_acc, i64 st,
-                   int tile, int ksplit, i64 slab, i64 slab_floats, int mv, int nv, int kv) {
+                   int tile, int ksplit, i64 slab, i64 slab_floats, int mv, int nv, int kv, i64 amax_a, int namax_a,
+                   i64 amax_b, int namax_b, i64 amax_c) {
     pre_launch("gemm");
     const int rc = launch_gemm(dt, ta, tb, M, N, K, P(const void*, A), lda, P(const void*, B), ldb, P(void*, C), ldc,
                                P(const float*, bias), epi, beta, P(float*, aux), ldaux, P(float*, part),
                                P(float*, colsum), colsum_acc, tile, ST(st), ksplit, P(float*, slab), slab_floats, mv, nv,
-                               kv);
+                               kv, P(const float*, amax_a), namax_a, P(const float*, amax_b), namax_b,
+                               P(float*, amax_c));
     if (rc == 0) check_launch("gemm");
     return rc;
   }, pybind11::arg("dt"), pybind11::arg("ta"), pybind11::arg("tb"), pybind11::arg("M"), pybind11::arg("N"),
@@ -516,5 +537,6 @@ PYBIND11_MODULE(_hip, m) {
      pybind11::arg("aux"), pybind11::arg("ldaux"), pybind11::arg("part"), pybind11::arg("colsum"),
      pybind11::arg("colsum_acc"), pybind11::arg("st"), pybind11::arg("tile") = -1, pybind11::arg("ksplit") = 0,
      pybind11::arg("slab") = 0, pybind11::arg("slab_floats") = 0, pybind11::arg("mv") = 0, pybind11::arg("nv") = 0,
-     pybind11::arg("kv") = 0);
+     pybind11::arg("kv") = 0, pybind11::arg("amax_a") = 0, pybind11::arg("namax_a") = 0, pybind11::arg("amax_b") = 0,
+     pybind11::arg("namax_b") = 0, pybind11::arg("amax_c") = 0);
 }

@@ -51,6 +51,14 @@ HS_DEVICE float wave_max(float v) {
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
   return v;
 }
+HS_DEVICE uint32_t wave_umax(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), o, 64)));
+  return v;
+}
+// |max| of a lane's values, kept as bits of |x| (integer max = float max, NaN above inf): amax_bits
+// folds one value in; the wave's result goes out with one atomic max (gemm.hip amax_commit)
+HS_DEVICE uint32_t amax_bits(uint32_t m, float x) { return max(m, __float_as_uint(x) & 0x7fffffffu); }
 HS_DEVICE double wave_sum_d(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

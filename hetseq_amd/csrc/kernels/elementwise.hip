@@ -444,3 +444,52 @@ void launch_scatter_add_rows(int dtype, const void* src, const int32_t* idx, voi
     hipLaunchKernelGGL(scatter_add_rows_kernel<bf16_t>, dim3(n), dim3(64), 0, st, (const bf16_t*)src, idx,
                        (bf16_t*)dst, n, H);
 }
+
+// ---------------------------------------------------------------------------
+// Per-tensor |max| for the fp16-split GEMM engine (gemm.hip split4h): the operand scale is a power
+// of two from it.  Producers that write an operand fold this reduction into their own epilogue
+// (one atomic max per wave); these kernels serve the rest -- the weights once per update, and
+// operands no fused producer wrote.  Non-negative floats order as their bit patterns, so an
+// unsigned atomic max is exact and order-independent (deterministic); NaN sorts above inf.
+namespace hs {
+
+// |x| as bits: integer max over them is the float max of |x|, with any NaN above inf
+HS_DEVICE uint32_t absbits4(uint4 v) {
+  return max(max(v.x & 0x7fffffffu, v.y & 0x7fffffffu), max(v.z & 0x7fffffffu, v.w & 0x7fffffffu));
+}
+
+__global__ void __launch_bounds__(256) amax_kernel(const float* __restrict__ x, int64_t n4, float* __restrict__ out) {
+  uint32_t m = 0u;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256)
+    m = max(m, absbits4(reinterpret_cast<const uint4*>(x)[i]));
+  m = wave_umax(m);
+  if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned int*>(out), m);
+}
+
+// block b reduces float4 range [tab[3b+1], tab[3b+2]) of the flat buffer into out[tab[3b]]
+__global__ void __launch_bounds__(256) amax_seg_kernel(const float* __restrict__ base, const int64_t* __restrict__ tab,
+                                                       float* __restrict__ out) {
+  const int64_t seg = tab[3 * blockIdx.x], lo = tab[3 * blockIdx.x + 1], hi = tab[3 * blockIdx.x + 2];
+  uint32_t m = 0u;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += 256) m = max(m, absbits4(reinterpret_cast<const uint4*>(base)[i]));
+  m = wave_umax(m);
+  if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned int*>(out + seg), m);
+}
+
+}  // namespace hs
+
+// |max| of x[0, n) (n % 4 == 0, 16-B aligned) into *out; zero_first: out is cleared on the stream first
+int launch_amax(const float* x, int64_t n, float* out, int zero_first, hipStream_t st) {
+  if (n % 4 || (reinterpret_cast<uintptr_t>(x) & 15)) return -1;
+  if (zero_first && hipMemsetAsync(out, 0, sizeof(float), st) != hipSuccess) return -1;
+  if (n == 0) return 0;
+  const int64_t n4 = n / 4;
+  const int grid = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
+  hipLaunchKernelGGL(amax_kernel, dim3(grid), dim3(256), 0, st, x, n4, out);
+  return 0;
+}
+
+// per-segment |max| over a flat buffer: tab = [nblk][3] int64 (segment, first float4, end float4)
+void launch_amax_seg(const float* base, const int64_t* tab, int nblk, float* out, hipStream_t st) {
+  if (nblk > 0) hipLaunchKernelGGL(amax_seg_kernel, dim3(nblk), dim3(256), 0, st, base, tab, out);
+}

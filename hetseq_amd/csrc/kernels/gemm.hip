@@ -81,6 +81,12 @@ struct GemmArgs {
   // rows past them read as zeros, C rows past Mv are not written, bias past Nv reads as zero
   int Mv, Nv, Kv;
   int slice_major;  // split-K block order: 1 = all tiles of slice 0, then slice 1, ... (else tile-major)
+  // fp16 two-term split (NT == 4): per-tensor |max| of op(A) / op(B), na / nb partial maxima each
+  // (e.g. one per half-batch producer); the kernel scales each operand by a power of two from them
+  const float* amax_a;
+  const float* amax_b;
+  int namax_a, namax_b;
+  float* amax_c;  // GELU / dGELU epilogues: |max| of the written C (atomic max), the next product's operand
 };
 
 // LDS image geometry of one operand (rows = BM or BN).  The [k][mn] image is
@@ -172,6 +178,60 @@ HS_DEVICE void split4(float4 x, uint2& hi, uint2& mi, uint2& lo) {
 
 HS_DEVICE f32x16 mma_bf(bfx8 a, bfx8 b, f32x16 c) { return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0); }
 
+// ---------------------------------------------------------------------------
+// fp32 products as THREE fp16 products (NT == 4, "h3").  fp16 carries 11 significant bits against
+// bf16's 8, so two terms hold 22 of fp32's 24:  s*x = hi + lo + r,  |r| <= 2^-22 |s*x|,  and
+//   s_a s_b a*b = hi_a hi_b + hi_a lo_b + lo_a hi_b   (dropped: lo_a lo_b ~ 2^-22 |ab|)
+// -- half the MFMA work of the six-term bf16 split (NT == 6).  fp16's range is what the per-tensor
+// scale s (a power of two, exact) is for: s = 2^(14 - e) with 2^e <= amax < 2^(e+1) maps the
+// operand's largest |x| into [2^14, 2^15) (no overflow; 65504 is fp16's largest) and keeps every
+// element down to 2^-18 amax at the full 22 bits (below that lo is subnormal: absolute error
+// <= 2^-25 / s = 2^-39 amax).  Per-element representation error is random in sign, so over a
+// K-long dot product it grows as sqrt(K) x 2^-22 |a||b| -- under the fp32 accumulation's own
+// rounding for K >= ~64 (tests/test_kernels_gpu.py::test_gemm_h3_error_matches_fp32 measures both
+// against fp64).  Every fp16 x fp16 product is exact in the fp32 accumulator.
+typedef _Float16 hx2 __attribute__((ext_vector_type(2)));
+typedef _Float16 hx8 __attribute__((ext_vector_type(8)));
+
+HS_DEVICE int h16_exp(const float* am, int n) {
+  uint32_t b = 0u;  // max over the partial maxima as |x| bits (a NaN partial wins)
+  for (int i = 0; i < n; ++i) b = max(b, __float_as_uint(am[i]) & 0x7fffffffu);
+  const float m = __uint_as_float(b);
+  if (!(m > 0.f) || !(m <= 3.4028235e38f)) return 0;  // zero, NaN or inf: unscaled (NaN / inf propagate)
+  return min(126, max(-126, 14 - ilogbf(m)));
+}
+
+HS_DEVICE void split4h(float4 x, float s, uint2& hi, uint2& lo) {
+  const fx2 x0 = {x.x * s, x.y * s}, x1 = {x.z * s, x.w * s};  // exact: s is a power of two
+  const hx2 h0 = __builtin_convertvector(x0, hx2), h1 = __builtin_convertvector(x1, hx2);
+  const fx2 r0 = x0 - __builtin_convertvector(h0, fx2), r1 = x1 - __builtin_convertvector(h1, fx2);  // exact
+  const hx2 l0 = __builtin_convertvector(r0, hx2), l1 = __builtin_convertvector(r1, hx2);
+  hi = make_uint2(__builtin_bit_cast(uint32_t, h0), __builtin_bit_cast(uint32_t, h1));
+  lo = make_uint2(__builtin_bit_cast(uint32_t, l0), __builtin_bit_cast(uint32_t, l1));
+}
+
+// the split of one float4 for engine NT: bf16 hi / mid / lo (NT 3, 6) or fp16 hi / lo (NT 4, planes 0, 1)
+template <int NT>
+HS_DEVICE void split_nt(float4 x, float s, uint2& p0, uint2& p1, uint2& p2) {
+  if constexpr (NT == 4) split4h(x, s, p0, p1);
+  else split4<NT>(x, p0, p1, p2);
+}
+
+template <int NT>
+HS_DEVICE f32x16 mma_nt(bfx8 a, bfx8 b, f32x16 c) {
+  if constexpr (NT == 4)
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(hx8, a), __builtin_bit_cast(hx8, b), c, 0, 0, 0);
+  else
+    return mma_bf(a, b, c);
+}
+
+// |max| of the values a lane wrote (amax_bits) -> one atomic max per wave (non-negative floats order as
+// their bit patterns; NaN's pattern sorts above inf, so a NaN output reaches the consumer's scale as NaN)
+HS_DEVICE void amax_commit(float* out, uint32_t m) {
+  m = wave_umax(m);
+  if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned int*>(out), m);
+}
+
 // Shared GEMM epilogue (both kernels): split-K slab, or C = acc (+bias) (+beta*C) / GELU /
 // dGELU + column partial sums.  acc[i][j] register r -> row m0+wm+MF*i+Mf::row(r,q), col n0+wn+MF*j+lr.
 template <int BM, int BN, int MF, int EPI, bool EDGE = false>
@@ -191,6 +251,7 @@ HS_DEVICE void epilogue(const GemmArgs& p, typename Mf<MF>::acc_t (&acc)[BM / 2 
     return;
   }
   float csum[TN];
+  uint32_t cmax = 0u;  // |max| of the written C as bits (GELU / dGELU epilogues, when p.amax_c is set)
   const bool use_beta = (EPI == kEpiNone || EPI == kEpiBias) && p.beta != 0.f;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -205,7 +266,9 @@ HS_DEVICE void epilogue(const GemmArgs& p, typename Mf<MF>::acc_t (&acc)[BM / 2 
         for (int r = 0; r < M_::nreg; ++r) {
           const int64_t m = mb + M_::row(r, q);
           p.aux[m * p.ldaux + n] = acc[i][j][r];
-          p.C[m * p.ldc + n] = gelu_f(acc[i][j][r] + bv);
+          const float y = gelu_f(acc[i][j][r] + bv);
+          cmax = amax_bits(cmax, y);
+          p.C[m * p.ldc + n] = y;
         }
       } else if (EPI == kEpiDGelu) {
         float pre[M_::nreg];
@@ -215,6 +278,7 @@ HS_DEVICE void epilogue(const GemmArgs& p, typename Mf<MF>::acc_t (&acc)[BM / 2 
         for (int r = 0; r < M_::nreg; ++r) {
           const float v = acc[i][j][r] * gelu_grad_f(pre[r] + bv);
           csum[j] += v;
+          cmax = amax_bits(cmax, v);
           p.C[(int64_t)(mb + M_::row(r, q)) * p.ldc + n] = v;
         }
       } else if (use_beta) {
@@ -233,6 +297,7 @@ HS_DEVICE void epilogue(const GemmArgs& p, typename Mf<MF>::acc_t (&acc)[BM / 2 
       }
     }
   }
+  if ((EPI == kEpiGelu || EPI == kEpiDGelu) && p.amax_c) amax_commit(p.amax_c, cmax);
   if (EPI == kEpiDGelu) {
     // column sums over the block's BM rows: lane groups, then the two wave rows via LDS
     float* red = smem;  // [BN] floats; the K loop ended with a barrier
@@ -380,13 +445,13 @@ HS_DEVICE void x_load(const char* __restrict__ base, const uint32_t (&o)[4], flo
 }
 
 template <bool KCONTIG, int NT>
-HS_DEVICE void x_store(char* __restrict__ S, const float4 (&v)[4], int t) {
+HS_DEVICE void x_store(char* __restrict__ S, const float4 (&v)[4], int t, float sc = 1.f) {
   const int g = KCONTIG ? t >> 3 : t & 31, c = KCONTIG ? t & 7 : t >> 5;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int r = 4 * g + i;
     uint2 h, m, l;
-    split4<NT>(v[i], h, m, l);
+    split_nt<NT>(v[i], sc, h, m, l);
     char* row = S + r * XROW + 16 * xchunk<!KCONTIG>(r, c >> 1) + 8 * (c & 1);
     *reinterpret_cast<uint2*>(row) = h;
     *reinterpret_cast<uint2*>(row + 64) = m;
@@ -422,13 +487,13 @@ HS_DEVICE void x_load_rows(const char* __restrict__ base, const uint32_t (&o)[4]
 }
 
 template <int NT>
-HS_DEVICE void x_store_tr(char* __restrict__ S, const float4 (&v)[4], int t) {
+HS_DEVICE void x_store_tr(char* __restrict__ S, const float4 (&v)[4], int t, float sc = 1.f) {
   const int g = t & 31, c = t >> 5;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int k = 4 * c + j;
     uint2 h, m, l;
-    split4<NT>(v[j], h, m, l);
+    split_nt<NT>(v[j], sc, h, m, l);
     char* row = S + k * TROW + 16 * ((g >> 1) ^ tr_swz(k)) + 8 * (g & 1);
     *reinterpret_cast<uint2*>(row) = h;
     *reinterpret_cast<uint2*>(row + GBK * TROW) = m;
@@ -520,13 +585,20 @@ __global__ void __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(NB
     if (TRB) x_load_rows(base, ob, v, lim);
     else x_load<TB>(base, ob, v, lim);
   };
+  // fp16 split (NT == 4): power-of-two operand scales from the producers' |max| (h16_exp)
+  int ea = 0, eb = 0;
+  if constexpr (NT == 4) {
+    ea = h16_exp(p.amax_a, p.namax_a);
+    eb = h16_exp(p.amax_b, p.namax_b);
+  }
+  const float sca = ldexpf(1.f, ea), scb = ldexpf(1.f, eb);
   auto stoA = [&](char* S_, const float4(&v)[4]) {
-    if (TRA) x_store_tr<NT>(S_, v, st);
-    else x_store<!TA, NT>(S_, v, st);
+    if (TRA) x_store_tr<NT>(S_, v, st, sca);
+    else x_store<!TA, NT>(S_, v, st, sca);
   };
   auto stoB = [&](char* S_, const float4(&v)[4]) {
-    if (TRB) x_store_tr<NT>(S_, v, st);
-    else x_store<TB, NT>(S_, v, st);
+    if (TRB) x_store_tr<NT>(S_, v, st, scb);
+    else x_store<TB, NT>(S_, v, st, scb);
   };
   auto load = [&]() {
     if (EDGE) {
@@ -592,7 +664,7 @@ __global__ void __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(NB
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int j = 0; j < TN; ++j) acc[i][j] = mma_bf(af[ks][PA[tt]][i], bf[ks][PB[tt]][j], acc[i][j]);
+          for (int j = 0; j < TN; ++j) acc[i][j] = mma_nt<NT>(af[ks][PA[tt]][i], bf[ks][PB[tt]][j], acc[i][j]);
   };
   // (ABL: ablation builds for tools/bench_gemm_x6.py --ablate, timing only, wrong results:
   //  1 no global loads in the loop, 2 + no staging, 3 + no barriers)
@@ -699,6 +771,13 @@ __global__ void __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(NB
       }
       __syncthreads();
     }
+  }
+  if constexpr (NT == 4) {  // undo the operand scales (powers of two: exact unless subnormal)
+    const float ia = ldexpf(1.f, -ea), ib = ldexpf(1.f, -eb);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = acc[i][j] * ia * ib;
   }
   // the epilogue's tile geometry: TM x TN 32x32 accumulators per wave, two wave rows
   epilogue<BM, 2 * 32 * TN, 32, EPI, EDGE>(p, acc, reinterpret_cast<float*>(smem), m0, n0, tm, slice, wm, wn, wr, lr,
@@ -890,7 +969,9 @@ static int pick_tile_split(int M, int N, int K, int* ksplit) {
 }
 
 // dtype: 0 fp32 on the exact-fp32 MFMA; 2 fp32 as 6 bf16 split products (fp32-level
-// error, see split8); 3 two-term split (3 products, ~2^-16: benchmarking only).
+// error, see split8); 3 two-term split (3 products, ~2^-16: benchmarking only); 4 fp32 as 3 fp16
+// split products with per-tensor power-of-two scales (split4h; amax_a / amax_b required: na / nb
+// partial |max| values each, up to 8).  amax_c: GELU / dGELU epilogues atomically max |C| into it.
 // epi: 0 none, 1 +bias, 2 gelu(+bias) writing the pre-activation to aux,
 // 3 dgelu (aux = pre-activation) with column sums of C written (or added,
 // colsum_acc) to colsum_out.  part: scratch of (M/64)*N floats (epi 3 only).
@@ -905,13 +986,15 @@ int gemm_last_ksplit() { return g_last_ks; }
 int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, int64_t lda, const void* B,
                 int64_t ldb, void* C, int64_t ldc, const float* bias, int epi, float beta, float* aux, int64_t ldaux,
                 float* part, float* colsum_out, int colsum_acc, int tile_override, hipStream_t st, int ksplit,
-                float* slab, int64_t slab_floats, int mv, int nv, int kv) {
-  if ((dtype != 0 && dtype != 2 && dtype != 3) || M <= 0 || N <= 0 || K <= 0 || K % GBK != 0) return -1;
+                float* slab, int64_t slab_floats, int mv, int nv, int kv, const float* amax_a, int namax_a,
+                const float* amax_b, int namax_b, float* amax_c) {
+  if ((dtype != 0 && dtype != 2 && dtype != 3 && dtype != 4) || M <= 0 || N <= 0 || K <= 0 || K % GBK != 0) return -1;
+  if (dtype == 4 && (!amax_a || !amax_b || namax_a < 1 || namax_b < 1 || namax_a > 8 || namax_b > 8)) return -1;
   auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
   if (!al16(A) || !al16(B) || lda % 4 || ldb % 4) return -1;
   if ((epi >= 1 && !bias) || (epi >= 2 && (!aux || beta != 0.f)) || (epi == 3 && (!part || !colsum_out)))
     return -1;
-  const int nt = dtype == 2 ? 6 : dtype == 3 ? 3 : 0;
+  const int nt = dtype == 2 ? 6 : dtype == 3 ? 3 : dtype == 4 ? 4 : 0;
   int tile, ks = 1;
   if (nt) {
     tile = pick_tile_split(M, N, K, &ks);
@@ -956,10 +1039,13 @@ int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, i
   if (wcol && (!nt || !colsum_out || g_x6_waves != 4 || g_x6_pf != 1 || g_ablation || mv != M || nv != N || kv != K))
     return -1;
   GemmArgs a{static_cast<const float*>(A), static_cast<const float*>(B), static_cast<float*>(C), bias, aux, part,
-             lda, ldb, ldc, ldaux, M, N, K, beta, ks, slab, mv, nv, kv, g_slice_major};
+             lda, ldb, ldc, ldaux, M, N, K, beta, ks, slab, mv, nv, kv, g_slice_major,
+             amax_a, amax_b, namax_a, namax_b, amax_c};
   int rc;
   if (nt == 6)
     rc = launch_split<6>(tile, ta, tb, epi, a, st);
+  else if (nt == 4)
+    rc = launch_split<4>(tile, ta, tb, epi, a, st);
   else if (nt == 3)
     rc = launch_split<3>(tile, ta, tb, epi, a, st);
   else if (mfma16)

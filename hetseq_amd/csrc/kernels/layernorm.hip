@@ -51,11 +51,12 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const T* __restrict__ a, co
                                                      uint64_t seed, uint64_t off, int mode,
                                                      const uint64_t* __restrict__ seed_dev,
                                                      uint16_t* __restrict__ yp, int64_t yps, int nslab,
-                                                     int64_t slab_stride, int row0) {
+                                                     int64_t slab_stride, int row0, float* __restrict__ amax_y) {
   constexpr int H = NV * 256;
   const int lane = threadIdx.x & 63;
   const float scale = p < 1.f ? 1.0f / (1.0f - p) : 0.f;
   seed = resolve_seed(seed, seed_dev);
+  uint32_t am = 0u;  // |max| of y as bits (amax_y: the next fp16-split GEMM's operand scale)
   for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += gridDim.x * 4) {
     const int64_t base = (int64_t)row * H;
     float x[NV][4];
@@ -98,7 +99,10 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const T* __restrict__ a, co
       load4(gamma + c, gw);
       load4(beta + c, gb);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = gw[j] * ((x[k][j] - mean) * rstd) + gb[j];
+      for (int j = 0; j < 4; ++j) {
+        o[j] = gw[j] * ((x[k][j] - mean) * rstd) + gb[j];
+        am = amax_bits(am, o[j]);
+      }
       store4(y + base + c, o);
       if (yp) store4_planes(yp, yps, base + c, o);  // y again as the next GEMM's split-bf16 operand
     }
@@ -106,6 +110,10 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const T* __restrict__ a, co
       mean_out[row] = mean;
       rstd_out[row] = rstd;
     }
+  }
+  if (amax_y) {
+    am = wave_umax(am);
+    if (lane == 0) atomicMax(reinterpret_cast<unsigned int*>(amax_y), am);
   }
 }
 
@@ -171,10 +179,11 @@ __global__ void __launch_bounds__(64 * kLnBwdWaves) ln_bwd_kernel(
     const float* __restrict__ rstd_in, const float* __restrict__ gamma, T* __restrict__ dz_out, T* __restrict__ da_out,
     float* __restrict__ part_gamma, float* __restrict__ part_beta, float* __restrict__ part_bias, int rows, float p,
     uint64_t seed, uint64_t off, int mode, const uint64_t* __restrict__ seed_dev, uint16_t* __restrict__ dap,
-    int64_t daps) {
+    int64_t daps, float* __restrict__ amax_out) {
   constexpr int H = NV * 256;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int lane = threadIdx.x & 63;
+  uint32_t am = 0u;  // |max| of da (mode kBDR) or dz (kPlain): the next fp16-split GEMM's operand scale
   const float scale = p < 1.f ? 1.0f / (1.0f - p) : 0.f;
   seed = resolve_seed(seed, seed_dev);
   float ag[NV][4], ab[NV][4], abias[NV][4], gw[NV][4];
@@ -225,6 +234,10 @@ __global__ void __launch_bounds__(64 * kLnBwdWaves) ln_bwd_kernel(
 #pragma unroll
       for (int j = 0; j < 4; ++j) dzv[j] = rstd * (g[k][j] - s1 - xh[k][j] * s2);
       if (dz_out) store4(dz_out + base + c, dzv);
+      if (mode != kBDR) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) am = amax_bits(am, dzv[j]);
+      }
       if (mode == kBDR) {
         float m[4] = {1.f, 1.f, 1.f, 1.f};
         if (p > 0.f) keep4(seed, off, (uint64_t)(base + c) >> 2, p, scale, m);
@@ -232,6 +245,7 @@ __global__ void __launch_bounds__(64 * kLnBwdWaves) ln_bwd_kernel(
         for (int j = 0; j < 4; ++j) {
           dzv[j] *= m[j];
           abias[k][j] += dzv[j];
+          am = amax_bits(am, dzv[j]);
         }
         if (da_out) store4(da_out + base + c, dzv);
         if (dap) store4_planes(dap, daps, base + c, dzv);  // da as the dgrad / wgrad GEMMs' operand
@@ -247,6 +261,10 @@ __global__ void __launch_bounds__(64 * kLnBwdWaves) ln_bwd_kernel(
     mean = mn;
     rstd = rn;
     row = nxt;
+  }
+  if (amax_out) {
+    am = wave_umax(am);
+    if (lane == 0) atomicMax(reinterpret_cast<unsigned int*>(amax_out), am);
   }
   if constexpr (CHUNK) {
     static_assert(kLnBwdWaves == 4, "chunked partials: 4 waves");
@@ -270,11 +288,13 @@ __global__ void __launch_bounds__(256) emb_fwd_kernel(const int64_t* __restrict_
                                                       float* __restrict__ zsave, float* __restrict__ mean_out,
                                                       float* __restrict__ rstd_out, int rows, int S, int V, int TV,
                                                       float eps, float p, uint64_t seed, uint64_t off,
-                                                      int* __restrict__ err, const uint64_t* __restrict__ seed_dev) {
+                                                      int* __restrict__ err, const uint64_t* __restrict__ seed_dev,
+                                                      float* __restrict__ amax_y) {
   constexpr int H = NV * 256;
   const int lane = threadIdx.x & 63;
   const float scale = p < 1.f ? 1.0f / (1.0f - p) : 0.f;
   seed = resolve_seed(seed, seed_dev);
+  uint32_t am = 0u;  // |max| of y (the first layer's fp16-split GEMM operand scale)
   for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += gridDim.x * 4) {
     const int64_t base = (int64_t)row * H;
     int64_t id = ids[row];
@@ -307,13 +327,20 @@ __global__ void __launch_bounds__(256) emb_fwd_kernel(const int64_t* __restrict_
       load4(beta + c, gb);
       if (p > 0.f) keep4(seed, off, (uint64_t)(base + c) >> 2, p, scale, m);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = (gw[j] * ((x[k][j] - mean) * rstd) + gb[j]) * m[j];
+      for (int j = 0; j < 4; ++j) {
+        o[j] = (gw[j] * ((x[k][j] - mean) * rstd) + gb[j]) * m[j];
+        am = amax_bits(am, o[j]);
+      }
       store4(y + base + c, o);
     }
     if (lane == 0) {
       mean_out[row] = mean;
       rstd_out[row] = rstd;
     }
+  }
+  if (amax_y) {
+    am = wave_umax(am);
+    if (lane == 0) atomicMax(reinterpret_cast<unsigned int*>(amax_y), am);
   }
 }
 
@@ -400,40 +427,42 @@ static const int kLnBwdBlocks = [] {
 template <int NV, typename T>
 void ln_fwd_launch(const void* a, const float* bias, const void* resid, const float* gamma, const float* beta, void* y,
                    float* zsave, float* mean, float* rstd, int rows, float eps, float p, uint64_t seed, uint64_t off,
-                   int mode, uint16_t* yp, int64_t yps, int nslab, int64_t slab_stride, int row0, hipStream_t st) {
+                   int mode, uint16_t* yp, int64_t yps, int nslab, int64_t slab_stride, int row0, float* amax,
+                   hipStream_t st) {
   int grid = (rows + 3) / 4;
   if (grid > 4096) grid = 4096;
   hipLaunchKernelGGL((ln_fwd_kernel<NV, T>), dim3(grid), dim3(256), 0, st, (const T*)a, bias, (const T*)resid, gamma,
                      beta, (T*)y, zsave, mean, rstd, rows, eps, p, seed, off, mode, g_seed_dev, yp, yps, nslab,
-                     slab_stride, row0);
+                     slab_stride, row0, amax);
 }
 
 template <int NV, typename T>
 void ln_bwd_launch(const void* dy, const float* zsave, const float* mean, const float* rstd, const float* gamma,
                    void* dz, void* da, float* pg, float* pb, float* pbias, int rows, float p, uint64_t seed,
-                   uint64_t off, int mode, uint16_t* dap, int64_t daps, hipStream_t st) {
+                   uint64_t off, int mode, uint16_t* dap, int64_t daps, float* amax, hipStream_t st) {
   constexpr int H = NV * 256;
   if constexpr (NV <= 3) {
     if (g_lnbwd_chunked) {
       hipLaunchKernelGGL((ln_bwd_kernel<NV, T, true>), dim3(kLnBwdBlocks), dim3(64 * kLnBwdWaves), 0, st,
                          (const T*)dy, zsave, mean, rstd, gamma, (T*)dz, (T*)da, pg, pb, pbias, rows, p, seed, off, mode,
-                         g_seed_dev, dap, daps);
+                         g_seed_dev, dap, daps, amax);
       return;
     }
   }
   hipLaunchKernelGGL((ln_bwd_kernel<NV, T>), dim3(kLnBwdBlocks), dim3(64 * kLnBwdWaves), kLnBwdWaves * H * sizeof(float), st, (const T*)dy,
                      zsave, mean, rstd, gamma, (T*)dz, (T*)da, pg, pb, pbias, rows, p, seed, off, mode, g_seed_dev,
-                     dap, daps);
+                     dap, daps, amax);
 }
 
 template <int NV, typename T>
 void emb_fwd_launch(const int64_t* ids, const int64_t* tt, const float* w, const float* pe, const float* te,
                     const float* gamma, const float* beta, void* y, float* zsave, float* mean, float* rstd, int rows,
-                    int S, int V, int TV, float eps, float p, uint64_t seed, uint64_t off, int* err, hipStream_t st) {
+                    int S, int V, int TV, float eps, float p, uint64_t seed, uint64_t off, int* err, float* amax,
+                    hipStream_t st) {
   int grid = (rows + 3) / 4;
   if (grid > 4096) grid = 4096;
   hipLaunchKernelGGL((emb_fwd_kernel<NV, T>), dim3(grid), dim3(256), 0, st, ids, tt, w, pe, te, gamma, beta, (T*)y,
-                     zsave, mean, rstd, rows, S, V, TV, eps, p, seed, off, err, g_seed_dev);
+                     zsave, mean, rstd, rows, S, V, TV, eps, p, seed, off, err, g_seed_dev, amax);
 }
 
 template <int NV, typename T>
@@ -466,29 +495,29 @@ void set_ln_bwd_lds(int chunked) { g_lnbwd_chunked = chunked; }
 int launch_ln_fwd(int dtype, const void* a, const float* bias, const void* resid, const float* gamma,
                   const float* beta, void* y, float* zsave, float* mean, float* rstd, int rows, int H, float eps,
                   float p, uint64_t seed, uint64_t off, int mode, void* yp, int64_t yps, int nslab,
-                  int64_t slab_stride, int row0, hipStream_t st) {
+                  int64_t slab_stride, int row0, float* amax, hipStream_t st) {
   if (yp && dtype != 0) return -1;  // plane output: fp32 mode only
   if (nslab < 1 || (nslab > 1 && (dtype != 0 || slab_stride < (int64_t)rows * H || slab_stride % 4))) return -1;
   if (dtype == 0) {
     HS_DISPATCH_H(H, (ln_fwd_launch<NV, float>(a, bias, resid, gamma, beta, y, zsave, mean, rstd, rows, eps, p, seed,
-                                               off, mode, (uint16_t*)yp, yps, nslab, slab_stride, row0, st)));
+                                               off, mode, (uint16_t*)yp, yps, nslab, slab_stride, row0, amax, st)));
   } else {
     HS_DISPATCH_H(H, (ln_fwd_launch<NV, bf16_t>(a, bias, resid, gamma, beta, y, zsave, mean, rstd, rows, eps, p, seed,
-                                                off, mode, nullptr, 0, 1, 0, row0, st)));
+                                                off, mode, nullptr, 0, 1, 0, row0, amax, st)));
   }
   return 0;
 }
 
 int launch_ln_bwd(int dtype, const void* dy, const float* zsave, const float* mean, const float* rstd,
                   const float* gamma, void* dz, void* da, float* pg, float* pb, float* pbias, int rows, int H, float p,
-                  uint64_t seed, uint64_t off, int mode, void* dap, int64_t daps, hipStream_t st) {
+                  uint64_t seed, uint64_t off, int mode, void* dap, int64_t daps, float* amax, hipStream_t st) {
   if (dap && (dtype != 0 || mode != kBDR)) return -1;  // plane output of da: fp32, bias-dropout-residual mode
   if (dtype == 0) {
     HS_DISPATCH_H(H, (ln_bwd_launch<NV, float>(dy, zsave, mean, rstd, gamma, dz, da, pg, pb, pbias, rows, p, seed, off,
-                                               mode, (uint16_t*)dap, daps, st)));
+                                               mode, (uint16_t*)dap, daps, amax, st)));
   } else {
     HS_DISPATCH_H(H, (ln_bwd_launch<NV, bf16_t>(dy, zsave, mean, rstd, gamma, dz, da, pg, pb, pbias, rows, p, seed,
-                                                off, mode, nullptr, 0, st)));
+                                                off, mode, nullptr, 0, amax, st)));
   }
   return 0;
 }
@@ -496,13 +525,13 @@ int launch_ln_bwd(int dtype, const void* dy, const float* zsave, const float* me
 int launch_emb_fwd(int dtype, const int64_t* ids, const int64_t* tt, const float* w, const float* pe, const float* te,
                    const float* gamma, const float* beta, void* y, float* zsave, float* mean, float* rstd, int rows,
                    int S, int H, int V, int TV, float eps, float p, uint64_t seed, uint64_t off, int* err,
-                   hipStream_t st) {
+                   float* amax, hipStream_t st) {
   if (dtype == 0) {
     HS_DISPATCH_H(H, (emb_fwd_launch<NV, float>(ids, tt, w, pe, te, gamma, beta, y, zsave, mean, rstd, rows, S, V, TV,
-                                                eps, p, seed, off, err, st)));
+                                                eps, p, seed, off, err, amax, st)));
   } else {
     HS_DISPATCH_H(H, (emb_fwd_launch<NV, bf16_t>(ids, tt, w, pe, te, gamma, beta, y, zsave, mean, rstd, rows, S, V,
-                                                 TV, eps, p, seed, off, err, st)));
+                                                 TV, eps, p, seed, off, err, amax, st)));
   }
   return 0;
 }

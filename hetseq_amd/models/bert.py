@@ -228,7 +228,7 @@ class BertEmbeddings(nn.Module):
         summed = self.word_embeddings(input_ids) + pos + self.token_type_embeddings(token_type_ids)
         return self.dropout(self.LayerNorm(summed))
 
-    def fused(self, input_ids, token_type_ids, out_dtype):
+    def fused(self, input_ids, token_type_ids, out_dtype, amax=None):
         from hetseq_amd.ops.bert_ops import FusedEmbedding
 
         p = self.dropout.p if self.training else 0.0
@@ -237,7 +237,7 @@ class BertEmbeddings(nn.Module):
         store = getattr(self, "_hs_store", None)
         sink = {"views": lambda: [store.grad_view(q) for q in params]} if store is not None else None
         return FusedEmbedding.apply(input_ids, token_type_ids, *params, p, self.LayerNorm.variance_epsilon,
-                                    out_dtype, sink)
+                                    out_dtype, sink, amax)
 
 
 class BertSelfAttention(nn.Module):
@@ -409,7 +409,8 @@ class BertLayer(nn.Module):
         return (sa.attention_head_size == 64 and H in FUSED_HIDDEN and S % 32 == 0
                 and self.intermediate.dense_act.fused_gelu and self.intermediate.dense_act.out_features % 4 == 0)
 
-    def fused(self, x2d, mask_i64, B, S, recompute=False):
+    def fused(self, x2d, mask_i64, B, S, recompute=False, amax=None):
+        """``amax``: this layer's bert_ops.LayerAmax (h3 GEMM engine operand scales) or None."""
         from hetseq_amd.ops.bert_ops import FusedBertLayer
         from hetseq_amd.runtime import rng
 
@@ -417,7 +418,7 @@ class BertLayer(nn.Module):
         p_a = self.attention.self.dropout.p if self.training else 0.0
         seeds = tuple(rng.fork() if p > 0 else (0, 0) for p in (p_a, p_h, p_h))
         cfg = (B, S, self.attention.self.num_attention_heads, p_h, p_a, self.output.LayerNorm.variance_epsilon, seeds)
-        meta = {"weights": self._weights, "cfg": cfg, "recompute": recompute}
+        meta = {"weights": self._weights, "cfg": cfg, "recompute": recompute, "amax": amax}
         if getattr(self, "_hs_store", None) is not None:
             meta["grad_sink"] = self._grad_views
             meta["store"] = self._hs_store
@@ -699,18 +700,52 @@ class BertModel(BertPreTrainedModel):
         pooled = self.pooler(layers[-1])
         return (layers if output_all_encoded_layers else layers[-1]), pooled
 
-    def fused_encoder(self, input_ids, token_type_ids, attention_mask, checkpoint_activations=False):
-        """Fused embeddings + encoder: the sequence output [B*S, H] in the compute dtype."""
+    def _amax_plan(self, extra_weights=(), extra_slots=0):
+        """h3 GEMM engine: this forward's ops.gemm.AmaxPool (every GEMM weight's |max| measured now,
+        one launch) and the per-layer bert_ops.LayerAmax slot maps; (None, None) on other engines.
+        Slots: 0-1 the embedding output (one producer; the second stays zero), then LayerAmax.NS
+        per layer, then ``extra_slots`` for the caller (the pre-training head)."""
+        from hetseq_amd.ops import gemm as G
+
+        if not G.h3_active(self.compute_dtype) or not self.embeddings.word_embeddings.weight.is_cuda:
+            return None, None
+        from hetseq_amd.ops.bert_ops import LayerAmax
+
+        Ws = [blk._weights() for blk in self.encoder.layer]
+        if any(getattr(W, "planes", False) for W in Ws):
+            return None, None
+        weights = [w for W in Ws for w in (W.wqkv, W.wo, W.w1, W.w2)] + list(extra_weights)
+        L, NS = len(Ws), LayerAmax.NS
+        pool = G.AmaxPool(weights, 2 + L * NS + extra_slots, self.embeddings.word_embeddings.weight.device)
+        plan = []
+        for i in range(L):
+            la = LayerAmax()
+            la.pool, la.base = pool, 2 + i * NS
+            la.w = tuple(pool.w(4 * i + k) for k in range(4))
+            if i == 0:  # both half-batch chains read the embedding's slot (written before the fork)
+                la.x, la.xw = (pool.act(0), pool.act(0)), pool.act(0, 2)
+            else:
+                o = 2 + (i - 1) * NS + 6  # the previous layer's h2 halves
+                la.x, la.xw = (pool.act(o), pool.act(o + 1)), pool.act(o, 2)
+            plan.append(la)
+        return pool, plan
+
+    def fused_encoder(self, input_ids, token_type_ids, attention_mask, checkpoint_activations=False, amax=None):
+        """Fused embeddings + encoder: the sequence output [B*S, H] in the compute dtype.  ``amax``:
+        (pool, per-layer slot maps) from :meth:`_amax_plan` (h3 engine); planned here when None."""
         from hetseq_amd.runtime.profiling import range_pop, range_push
 
         B, S = input_ids.shape
         mask = attention_mask.to(torch.int64).contiguous()
+        pool, plan = amax if amax is not None else self._amax_plan()
         range_push("embeddings")
-        x = self.embeddings.fused(input_ids, token_type_ids, self.compute_dtype)
+        x = self.embeddings.fused(input_ids, token_type_ids, self.compute_dtype,
+                                  amax=pool.act(0) if pool is not None else None)
         range_pop()
         for i, blk in enumerate(self.encoder.layer):
             range_push("layer%d" % i)
-            x = blk.fused(x, mask, B, S, recompute=checkpoint_activations)
+            x = blk.fused(x, mask, B, S, recompute=checkpoint_activations,
+                          amax=plan[i] if plan is not None else None)
             range_pop()
         return x
 
@@ -781,13 +816,24 @@ class BertForPreTraining(BertPreTrainedModel):
         if attention_mask is None:
             attention_mask = torch.ones_like(input_ids)
         B, S = input_ids.shape
-        seq2d = self.bert.fused_encoder(input_ids, token_type_ids, attention_mask, checkpoint_activations)
+        wt_, wd_ = self._mlm_weights()
+        head_w = (wt_, wd_) if isinstance(wt_, torch.Tensor) and wt_.dtype == torch.float32 else ()
+        pool, plan = self.bert._amax_plan(extra_weights=head_w, extra_slots=1)
+        seq2d = self.bert.fused_encoder(input_ids, token_type_ids, attention_mask, checkpoint_activations,
+                                        amax=(pool, plan))
         cap = B * S if self.max_predictions_per_seq is None else min(B * S, B * int(self.max_predictions_per_seq))
         t, pred = self.cls.predictions.transform, self.cls.predictions
         pooler, nsp = self.bert.pooler.dense_act, self.cls.seq_relationship
         params = [t.dense_act.weight, t.dense_act.bias, t.LayerNorm.weight, t.LayerNorm.bias, pred.decoder.weight,
                   pred.bias, pooler.weight, pooler.bias, nsp.weight, nsp.bias]
         meta = {"cap": cap, "eps": t.LayerNorm.variance_epsilon, "weights": self._mlm_weights, "B": B, "S": S}
+        if pool is not None and head_w:
+            L = len(plan)
+            last = plan[-1]
+            # h3 slots of the head: the sequence output (last layer's h2 halves), the transform and
+            # decoder weights, and the transform LN output t2 (the decoder's A operand)
+            meta["amax"] = {"seq": last.a(6, 2), "wt": pool.w(4 * L), "wd": pool.w(4 * L + 1),
+                            "t2": pool.act(2 + L * last.NS)}
         store = getattr(self, "_hs_store", None)
         if store is not None:
             meta["grad_sink"] = lambda: [store.grad_view(q) for q in params]

@@ -79,13 +79,15 @@ def _planes_buf(rows, cols, device):
 
 
 def ln_fwd(a, gamma, beta, eps=1e-12, bias=None, resid=None, p=0.0, mode=0, seed=0, off=0, save_z=True, planes=None,
-           outs=None, row0=0):
+           outs=None, row0=0, amax=None):
     """LayerNorm forward (+ bias / dropout / residual in mode 1).  ``planes``: a [3, rows, H] bf16
     buffer that also receives y as split-bf16 planes (the fp32 GEMM engine's operand format).
     ``a`` may be [ks, rows, H] split-K partials of the producing GEMM (gemm.linear_fwd_partials),
     summed in slice order as the GEMM's own reduce pass would.  ``outs`` = (y, z, mean, rstd) buffers to
     write (row slices of whole-batch tensors); ``row0``: the first row's index in the whole batch
-    (the dropout mask is drawn by whole-batch element index, as the backward regenerates it)."""
+    (the dropout mask is drawn by whole-batch element index, as the backward regenerates it).
+    ``amax``: a 1-element slot (ops.gemm.AmaxPool) the kernel atomically maxes |y| into (the h3
+    GEMM engine's operand scale for the next product)."""
     nslab = 1
     if a.dim() == 3:
         nslab = a.shape[0]
@@ -104,17 +106,19 @@ def ln_fwd(a, gamma, beta, eps=1e-12, bias=None, resid=None, p=0.0, mode=0, seed
                  resid.data_ptr() if resid is not None else 0, gamma.data_ptr(), beta.data_ptr(), y.data_ptr(),
                  z.data_ptr() if z is not None else 0, mean.data_ptr(), rstd.data_ptr(), rows, H, float(eps), float(p),
                  seed, off, mode, stream_handle(), planes.data_ptr() if planes is not None else 0,
-                 rows * H if planes is not None else 0, nslab, stride if nslab > 1 else 0, int(row0))
+                 rows * H if planes is not None else 0, nslab, stride if nslab > 1 else 0, int(row0),
+                 amax.data_ptr() if amax is not None else 0)
     return y, z, mean, rstd
 
 
 def ln_bwd(dy, z, mean, rstd, gamma, p=0.0, mode=0, seed=0, off=0, want_dz=True, want_da=False, dz_out=None,
-           acc=None, side=False, da_planes=None):
+           acc=None, side=False, da_planes=None, amax=None):
     """LN backward.  ``acc`` = (dgamma, dbeta[, dbias]) fp32 tensors to ACCUMULATE into
     (flat-store gradient views); otherwise fresh tensors are returned.  ``side``: run the
     parameter-gradient finalisation on the weight-gradient stream (runtime/streams.py) --
     only dz / da are on the critical path.  ``da_planes``: [3, rows, H] bf16 buffer receiving da
-    as split-bf16 planes (mode 1; with ``want_da`` False the fp32 da is not written at all)."""
+    as split-bf16 planes (mode 1; with ``want_da`` False the fp32 da is not written at all).
+    ``amax``: slot receiving |max| of da (mode 1) or dz (mode 0) -- the next GEMMs' operand."""
     rows, H = dy.shape
     nb = hip().ln_bwd_num_blocks()
     part = _colpart_buf(nb, H, dy.device)
@@ -123,7 +127,8 @@ def ln_bwd(dy, z, mean, rstd, gamma, p=0.0, mode=0, seed=0, off=0, want_dz=True,
     hip().ln_bwd(dtype_code(dy), dy.data_ptr(), z.data_ptr(), mean.data_ptr(), rstd.data_ptr(), gamma.data_ptr(),
                  dz.data_ptr() if dz is not None else 0, da.data_ptr() if da is not None else 0, part[0].data_ptr(),
                  part[1].data_ptr(), part[2].data_ptr(), rows, H, float(p), seed, off, mode, stream_handle(),
-                 da_planes.data_ptr() if da_planes is not None else 0, rows * H if da_planes is not None else 0)
+                 da_planes.data_ptr() if da_planes is not None else 0, rows * H if da_planes is not None else 0,
+                 amax.data_ptr() if amax is not None else 0)
     n = 3 if mode == 1 else 2
     if acc is not None:
         outs = list(acc[:n])
@@ -179,10 +184,11 @@ def colsum(x, acc=None):
     return out
 
 
-def attn_fwd(qkv, mask, B, S, NH, p, seed, off, bias=None, outs=None, b0=0):
+def attn_fwd(qkv, mask, B, S, NH, p, seed, off, bias=None, outs=None, b0=0, amax=None):
     """qkv [B*S, 3H] (un-biased projection output if ``bias`` [3H] fp32 is given).  ``outs`` =
     (ctx, lse, dmask) buffers to write (slices of whole-batch tensors); ``b0``: the slice's first
-    sequence in the whole batch (its dropout keep bits are the whole-batch launch's)."""
+    sequence in the whole batch (its dropout keep bits are the whole-batch launch's).  ``amax``:
+    slot receiving |max| of ctx (one pass right behind the kernel)."""
     T, H3 = qkv.shape
     H = H3 // 3
     assert T == B * S and H == NH * 64 and S % 32 == 0 and qkv.is_contiguous()
@@ -198,11 +204,14 @@ def attn_fwd(qkv, mask, B, S, NH, p, seed, off, bias=None, outs=None, b0=0):
     hip().attn_fwd(dtype_code(qkv), qkv.data_ptr(), mask.data_ptr(), bias.data_ptr() if bias is not None else 0,
                    ctx.data_ptr(), lse.data_ptr(), dmask.data_ptr() if dmask is not None else 0, B, S, NH, 64,
                    float(p), seed, off, stream_handle(), int(b0) * NH)
+    if amax is not None:
+        hip().amax(ctx.data_ptr(), ctx.numel(), amax.data_ptr(), 0, stream_handle())
     return ctx, (lse, dmask)
 
 
-def attn_bwd(qkv, mask, ctx, dctx, lse, B, S, NH, p, seed=0, off=0, bias=None):
-    """``lse`` is the (lse, dropout-bitmask) pair returned by :func:`attn_fwd`."""
+def attn_bwd(qkv, mask, ctx, dctx, lse, B, S, NH, p, seed=0, off=0, bias=None, amax=None):
+    """``lse`` is the (lse, dropout-bitmask) pair returned by :func:`attn_fwd`; ``amax``: slot
+    receiving |max| of dqkv."""
     lse, dmask = lse
     assert dctx.is_contiguous() and dctx.shape == ctx.shape
     assert p == 0 or dmask is not None
@@ -211,6 +220,8 @@ def attn_bwd(qkv, mask, ctx, dctx, lse, B, S, NH, p, seed=0, off=0, bias=None):
     hip().attn_bwd(dtype_code(qkv), qkv.data_ptr(), mask.data_ptr(), bias.data_ptr() if bias is not None else 0,
                    ctx.data_ptr(), dctx.data_ptr(), lse.data_ptr(), dbuf.data_ptr(), dqkv.data_ptr(),
                    dmask.data_ptr() if dmask is not None else 0, B, S, NH, 64, float(p), stream_handle())
+    if amax is not None:
+        hip().amax(dqkv.data_ptr(), dqkv.numel(), amax.data_ptr(), 0, stream_handle())
     return dqkv
 
 
@@ -317,7 +328,7 @@ def sort_keys(keys, bound):
 
 class FusedEmbedding(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, ids, tt, wword, wpos, wtype, gamma, beta, p, eps, out_dtype, sink=None):
+    def forward(ctx, ids, tt, wword, wpos, wtype, gamma, beta, p, eps, out_dtype, sink=None, amax=None):
         B, S = ids.shape
         V, H = wword.shape
         TV = wtype.shape[0]
@@ -334,7 +345,7 @@ class FusedEmbedding(torch.autograd.Function):
         hip().emb_fwd(dtype_code(y), ids.data_ptr(), tt.data_ptr() if tt is not None else 0, wword.data_ptr(),
                       wpos.data_ptr(), wtype.data_ptr(), gamma.data_ptr(), beta.data_ptr(), y.data_ptr(), z.data_ptr(),
                       mean.data_ptr(), rstd.data_ptr(), rows, S, H, V, TV, float(eps), float(p), seed, off,
-                      err.data_ptr(), stream_handle())
+                      err.data_ptr(), stream_handle(), amax.data_ptr() if amax is not None else 0)
         ctx.save_for_backward(ids, tt if tt is not None else ids.new_zeros(0), z, mean, rstd, gamma)
         ctx.cfg = (B, S, V, H, TV, wpos.shape[0], p, seed, off, tt is not None)
         ctx.sink = sink
@@ -380,7 +391,7 @@ class FusedEmbedding(torch.autograd.Function):
                                stream_handle())
         if tables is not None:
             tables.rows_ready()  # word / position / type rows: gathered and summed after the exchange
-            return (None,) * 11
+            return (None,) * 12
         if small_tv:
             tv = [ptype[0].data_ptr()] + ([ptype[1].data_ptr()] if TV == 2 else [])
             hip().colpart_finalize(tv, [dtype_[i].data_ptr() for i in range(len(tv))], nb, H, 1, stream_handle())
@@ -392,8 +403,8 @@ class FusedEmbedding(torch.autograd.Function):
         segsum_rows(dx, word_order, word_keys, dword)
         hip().pos_grad(dx.data_ptr(), dpos.data_ptr(), B, S, H, stream_handle())
         if sink is not None:
-            return (None,) * 11
-        return None, None, dword, dpos, dtype_, dg, db, None, None, None, None
+            return (None,) * 12
+        return None, None, dword, dpos, dtype_, dg, db, None, None, None, None, None
 
 
 # --------------------------------------------------------------------- encoder layer
@@ -402,6 +413,25 @@ class LayerWeights(object):
     engine, ``planes`` True) the split-bf16 plane views (ops.gemm.Planes) of the GEMM weights."""
 
     __slots__ = ("wqkv", "bqkv", "wo", "bo", "g1", "b1", "w1", "bi", "w2", "b2", "g2", "bb2", "planes", "bwd")
+
+
+class LayerAmax(object):
+    """The h3 GEMM engine's |max| slots for one encoder layer (in a forward's ops.gemm.AmaxPool):
+    ``w`` = (wqkv, wo, w1, w2) weight slots; ``x`` = the input's slot per half-batch chain (both
+    halves read the embedding's one slot in layer 0), ``xw`` = the input's whole-batch partials;
+    activation slots at ``base`` + 0 h1, 2 ctx, 4 f1, 6 h2 (one per half each; the un-split
+    forward uses the first) and the backward's 8 do, 9 df1, 10 da1, 11 dqkv."""
+
+    NS = 12
+    __slots__ = ("pool", "w", "x", "xw", "base")
+
+    def a(self, off, n=1):
+        return self.pool.act(self.base + off, n)
+
+
+def _am(am, *pairs):
+    """(A's, B's) slots for a GEMM when ``am`` is set (None: the GEMM wrapper measures the operands)."""
+    return None if am is None else pairs
 
 
 def _planes_of(buf):
@@ -425,7 +455,7 @@ def _fwd_split_ok(x, mask, W, cfg):
             and not torch.cuda.is_current_stream_capturing())  # (graphs: one chain; the same dropout masks)
 
 
-def _layer_forward_split(x, mask, W, cfg, save):
+def _layer_forward_split(x, mask, W, cfg, save, am=None):
     """_layer_forward with the batch in two halves on two streams, every op writing its half of the
     whole-batch tensors (the backward sees the same saved tensors as an unsplit forward).  Dropout is
     drawn by whole-batch index (LN: ``row0``, attention: ``b0``): the same masks as one chain."""
@@ -447,54 +477,69 @@ def _layer_forward_split(x, mask, W, cfg, save):
         for h in halves:
             r = slice(h * hr, (h + 1) * hr)
             xh = x[r]
-            G.linear_fwd(xh, W.wqkv, out=qkv[r], ksplit=_FWD_KS)
+            sl = (lambda off: am.a(off + h)) if am is not None else (lambda off: None)  # this half's slot
+            G.linear_fwd(xh, W.wqkv, out=qkv[r], ksplit=_FWD_KS, amax=_am(am, am and am.x[h], am and am.w[0]))
             attn_fwd(qkv[r], mask[h * hb:(h + 1) * hb], hb, S, NH, p_a, s_a, o_a, bias=W.bqkv, b0=h * hb,
-                     outs=(ctx_[r], lse[h * nl:(h + 1) * nl], dmask[h * nm:(h + 1) * nm] if dmask is not None else None))
-            a = (G.linear_fwd_partials(ctx_[r], W.wo, ksplit=_FWD_KS)[0] if _LN_PARTIALS_WO
-                 else G.linear_fwd(ctx_[r], W.wo, ksplit=_FWD_KS))
+                     outs=(ctx_[r], lse[h * nl:(h + 1) * nl], dmask[h * nm:(h + 1) * nm] if dmask is not None else None),
+                     amax=sl(2))
+            wo_am = _am(am, sl(2), am and am.w[1])
+            a = (G.linear_fwd_partials(ctx_[r], W.wo, ksplit=_FWD_KS, amax=wo_am)[0] if _LN_PARTIALS_WO
+                 else G.linear_fwd(ctx_[r], W.wo, ksplit=_FWD_KS, amax=wo_am))
             ln_fwd(a, W.g1, W.b1, eps, bias=W.bo, resid=xh, p=p_h, mode=1, seed=s_1, off=o_1, row0=h * hr,
-                   outs=(h1[r], z1[r], m1[r], r1[r]))
-            G.linear_gelu_fwd(h1[r], W.w1, W.bi, out=(f1[r], f1pre[r]))
-            o = (G.linear_fwd_partials(f1[r], W.w2, ksplit=_FWD_KS)[0] if _LN_PARTIALS
-                 else G.linear_fwd(f1[r], W.w2, ksplit=_FWD_KS))
+                   outs=(h1[r], z1[r], m1[r], r1[r]), amax=sl(0))
+            G.linear_gelu_fwd(h1[r], W.w1, W.bi, out=(f1[r], f1pre[r]), amax=_am(am, sl(0), am and am.w[2]),
+                              amax_out=sl(4))
+            w2_am = _am(am, sl(4), am and am.w[3])
+            o = (G.linear_fwd_partials(f1[r], W.w2, ksplit=_FWD_KS, amax=w2_am)[0] if _LN_PARTIALS
+                 else G.linear_fwd(f1[r], W.w2, ksplit=_FWD_KS, amax=w2_am))
             ln_fwd(o, W.g2, W.bb2, eps, bias=W.b2, resid=h1[r], p=p_h, mode=1, seed=s_2, off=o_2, row0=h * hr,
-                   outs=(h2[r], z2[r], m2[r], r2[r]))
+                   outs=(h2[r], z2[r], m2[r], r2[r]), amax=sl(6))
     if save:
         return h2, (qkv, ctx_, lse, dmask, z1, m1, r1, h1, f1pre, f1, z2, m2, r2, x, ctx_)
     return h2, None
 
 
-def _layer_forward(x, mask, W, cfg, save):
+def _layer_forward(x, mask, W, cfg, save, am=None):
     """fp32 on the plane engine (``W.planes``): every GEMM operand is split-bf16 planes, written by
     the kernel that produces the tensor where it can -- the LN forwards (h1, h2: h2's planes wait
     in gemm.remember_planes for the next layer), the GELU epilogue (f1, planes only) -- and by a
     split pass for the attention output and the embedding output; saved planes feed the weight
     gradients of the backward."""
     if _fwd_split_ok(x, mask, W, cfg):
-        return _layer_forward_split(x, mask, W, cfg, save)
+        return _layer_forward_split(x, mask, W, cfg, save, am)
     B, S, NH, p_h, p_a, eps, seeds = cfg
     (s_a, o_a), (s_1, o_1), (s_2, o_2) = seeds
     pl = getattr(W, "planes", False)
     plb = pl and W.bwd is W  # the backward's GEMMs on planes too (else: fp32 operands saved)
+    if pl:
+        am = None  # (the plane engine needs no operand scales)
+    sl = (lambda off: am.a(off)) if am is not None else (lambda off: None)  # one chain: the first slot
     rows, H = x.shape
     xin = G.split_cached(x) if pl else x
-    qkv = G.linear_fwd(xin, W.wqkv)  # bias folded into the attention kernels' Q/K/V loads
-    ctx_, (lse, dmask) = attn_fwd(qkv, mask, B, S, NH, p_a, s_a, o_a, bias=W.bqkv)
+    qkv = G.linear_fwd(xin, W.wqkv, amax=_am(am, am and am.xw, am and am.w[0]))  # bias folded into the attention
+    ctx_, (lse, dmask) = attn_fwd(qkv, mask, B, S, NH, p_a, s_a, o_a, bias=W.bqkv, amax=sl(2))
     cin = G.split(ctx_) if pl else ctx_
-    a = G.linear_fwd(cin, W.wo) if (pl or not _LN_PARTIALS_WO) else G.linear_fwd_partials(cin, W.wo)[0]
+    wo_am = _am(am, sl(2), am and am.w[1])
+    a = G.linear_fwd(cin, W.wo, amax=wo_am) if (pl or not _LN_PARTIALS_WO) else G.linear_fwd_partials(
+        cin, W.wo, amax=wo_am)[0]
     h1p = _planes_buf(rows, H, x.device) if pl else None
-    h1, z1, m1, r1 = ln_fwd(a, W.g1, W.b1, eps, bias=W.bo, resid=x, p=p_h, mode=1, seed=s_1, off=o_1, planes=h1p)
+    h1, z1, m1, r1 = ln_fwd(a, W.g1, W.b1, eps, bias=W.bo, resid=x, p=p_h, mode=1, seed=s_1, off=o_1, planes=h1p,
+                            amax=sl(0))
     hin = _planes_of(h1p) if pl else h1
     if pl and not plb:  # forward-only planes: f1 in fp32 (saved) and as planes (the next product)
         f1, f1pre = G.linear_gelu_fwd(hin, W.w1, W.bi, emit_planes=True)
         fin = G.split_cached(f1)
     else:
-        f1, f1pre = G.linear_gelu_fwd(hin, W.w1, W.bi, planes_out=pl)  # f1pre: un-biased pre-activation
+        f1, f1pre = G.linear_gelu_fwd(hin, W.w1, W.bi, planes_out=pl, amax=_am(am, sl(0), am and am.w[2]),
+                                      amax_out=sl(4))  # f1pre: un-biased pre-activation
         fin = f1
     # FFN-out product: its split-K partials go straight into the LN (no reduce pass)
-    o = G.linear_fwd(fin, W.w2) if (pl or not _LN_PARTIALS) else G.linear_fwd_partials(fin, W.w2)[0]
+    w2_am = _am(am, sl(4), am and am.w[3])
+    o = G.linear_fwd(fin, W.w2, amax=w2_am) if (pl or not _LN_PARTIALS) else G.linear_fwd_partials(
+        fin, W.w2, amax=w2_am)[0]
     h2p = _planes_buf(rows, H, x.device) if pl else None
-    h2, z2, m2, r2 = ln_fwd(o, W.g2, W.bb2, eps, bias=W.b2, resid=h1, p=p_h, mode=1, seed=s_2, off=o_2, planes=h2p)
+    h2, z2, m2, r2 = ln_fwd(o, W.g2, W.bb2, eps, bias=W.b2, resid=h1, p=p_h, mode=1, seed=s_2, off=o_2, planes=h2p,
+                            amax=sl(6))
     if pl:
         G.remember_planes(h2, _planes_of(h2p))  # the next layer's QKV operand
     if save:
@@ -514,7 +559,7 @@ class FusedBertLayer(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, mask, meta, *params):
         W, cfg, recompute = meta["weights"](), meta["cfg"], meta["recompute"]
-        h2, saved = _layer_forward(x, mask, W, cfg, save=not recompute)
+        h2, saved = _layer_forward(x, mask, W, cfg, save=not recompute, am=meta.get("amax"))
         ctx.meta = meta
         ctx.cfg = cfg
         if recompute:
@@ -530,7 +575,7 @@ class FusedBertLayer(torch.autograd.Function):
         if meta["recompute"]:
             x, mask = ctx.saved_tensors
             with torch.no_grad():
-                _, saved = _layer_forward(x, mask, W, cfg, save=True)
+                _, saved = _layer_forward(x, mask, W, cfg, save=True, am=meta.get("amax"))
         else:
             x, mask = ctx.saved_tensors[:2]
             saved = ctx.saved_tensors[2:]
@@ -540,6 +585,9 @@ class FusedBertLayer(torch.autograd.Function):
         pl = getattr(W, "planes", False)
         if pl:  # GEMM operands saved as split planes
             h1, f1, xin, cin = (_planes_of(t) for t in (h1, f1, xin, cin))
+        am = None if pl else meta.get("amax")  # h3 engine: operand |max| slots (LayerAmax)
+        sl = (lambda off, n=1: am.a(off, n)) if am is not None else (lambda off, n=1: None)
+        wsl = (lambda i: am.w[i]) if am is not None else (lambda i: None)
         B, S, NH, p_h, p_a, eps, seeds = cfg
         (s_a, o_a), (s_1, o_1), (s_2, o_2) = seeds
         dh2 = dh2.contiguous()
@@ -560,46 +608,53 @@ class FusedBertLayer(torch.autograd.Function):
         store = meta.get("store")
         wacc = acc and not (side and _FRESH_WGRAD and store is not None and store.claim_fresh())
 
-        def wgrad(dy, xin_, out):
+        def wgrad(dy, xin_, out, amax=None):
             if not side:
-                return G.linear_wgrad(dy, xin_, out=out, accumulate=acc)
+                return G.linear_wgrad(dy, xin_, out=out, accumulate=acc, amax=amax)
             ks = streams.side_ksplit(dy.shape[1], xin_.shape[1])
             return streams.run(dy.device, lambda: G.linear_wgrad(dy, xin_, out=out, accumulate=wacc,
-                                                                 ksplit=ks), dy, xin_)
+                                                                 ksplit=ks, amax=amax), dy, xin_)
 
         # side-stream work forks at three points per layer; the launches at one point share one event
         with streams.coalesced():  # LN2 parameter gradients + the FFN-out weight gradient
             dz2, do_, dg2, dbb2, db2 = ln_bwd(dh2, z2, m2, r2, W.g2, p_h, 1, s_2, o_2, True, not pl,
-                                              acc=(Gv.g2, Gv.bb2, Gv.b2) if acc else None, side=side, da_planes=dop)
+                                              acc=(Gv.g2, Gv.bb2, Gv.b2) if acc else None, side=side, da_planes=dop,
+                                              amax=sl(8))
             do_p = _planes_of(dop) if pl else do_
-            dW2 = wgrad(do_p, f1, Gv.w2 if acc else None)
-        df1p, dbi = G.linear_dgrad_dgelu(do_p, W.w2, f1pre, W.bi, db_acc=Gv.bi if acc else None, planes_out=pl)
-        dW1 = wgrad(df1p, h1, Gv.w1 if acc else None)
-        dh1 = G.linear_dgrad(df1p, W.w1, out=dz2, accumulate=True, ksplit=dks)  # dz2 + df1pre @ W1
+            dW2 = wgrad(do_p, f1, Gv.w2 if acc else None, amax=_am(am, sl(8), sl(4, 2)))
+        df1p, dbi = G.linear_dgrad_dgelu(do_p, W.w2, f1pre, W.bi, db_acc=Gv.bi if acc else None, planes_out=pl,
+                                         amax=_am(am, sl(8), wsl(3)), amax_out=sl(9))
+        dW1 = wgrad(df1p, h1, Gv.w1 if acc else None, amax=_am(am, sl(9), sl(0, 2)))
+        dh1 = G.linear_dgrad(df1p, W.w1, out=dz2, accumulate=True, ksplit=dks,
+                             amax=_am(am, sl(9), wsl(2)))  # dz2 + df1pre @ W1
         dap = _planes_buf(rows, H, dh2.device) if pl else None
         with streams.coalesced():  # LN1 parameter gradients + the attention-output weight gradient
             dz1, da1, dg1, db1, dbo = ln_bwd(dh1, z1, m1, r1, W.g1, p_h, 1, s_1, o_1, True, not pl,
-                                             acc=(Gv.g1, Gv.b1, Gv.bo) if acc else None, side=side, da_planes=dap)
+                                             acc=(Gv.g1, Gv.b1, Gv.bo) if acc else None, side=side, da_planes=dap,
+                                             amax=sl(10))
             da1p = _planes_of(dap) if pl else da1
-            dWo = wgrad(da1p, cin, Gv.wo if acc else None)
-        dctx = G.linear_dgrad(da1p, W.wo, ksplit=dks)
-        dqkv = attn_bwd(qkv, mask, ctx_, dctx, (lse, dmask), B, S, NH, p_a, bias=W.bqkv)
+            dWo = wgrad(da1p, cin, Gv.wo if acc else None, amax=_am(am, sl(10), sl(2, 2)))
+        dctx = G.linear_dgrad(da1p, W.wo, ksplit=dks, amax=_am(am, sl(10), wsl(1)))
+        dqkv = attn_bwd(qkv, mask, ctx_, dctx, (lse, dmask), B, S, NH, p_a, bias=W.bqkv, amax=sl(11))
         dqkvp = G.split(dqkv) if pl else dqkv
+        qkv_w_am = _am(am, sl(11), am and am.xw)
         with streams.coalesced():  # QKV weight and bias gradients
             fused = False
             if side and not pl and _WGRAD_COLSUM:  # one launch: the bias gradient from the wgrad's staging
                 ks = streams.side_ksplit(dqkv.shape[1], xin.shape[1])
                 fused = streams.run(dqkv.device, lambda: G.linear_wgrad_colsum(dqkv, xin, Gv.wqkv, Gv.bqkv, ksplit=ks,
-                                                                               accumulate=wacc), dqkv, xin)
+                                                                               accumulate=wacc, amax=qkv_w_am),
+                                    dqkv, xin)
             if fused:
                 dWqkv, dbqkv = Gv.wqkv, Gv.bqkv
             else:
-                dWqkv = wgrad(dqkvp, xin, Gv.wqkv if acc else None)
+                dWqkv = wgrad(dqkvp, xin, Gv.wqkv if acc else None, amax=qkv_w_am)
                 if side:
                     dbqkv = streams.run(dqkv.device, lambda: colsum(dqkv, acc=Gv.bqkv), dqkv)
                 else:
                     dbqkv = colsum(dqkv, acc=Gv.bqkv if acc else None)
-        dx = G.linear_dgrad(dqkvp, W.wqkv, out=dz1, accumulate=True, ksplit=dks)  # dz1 + dqkv @ Wqkv
+        dx = G.linear_dgrad(dqkvp, W.wqkv, out=dz1, accumulate=True, ksplit=dks,
+                            amax=_am(am, sl(11), wsl(0)))  # dz1 + dqkv @ Wqkv
         if acc:
             return (dx, None, None) + (None,) * 16
         return (dx, None, None,
@@ -689,13 +744,14 @@ class FusedPreTrainingLoss(torch.autograd.Function):
         hsel = gather_rows(seq, idx)
         pl = isinstance(Wt, G.Planes)  # fp32 on the plane engine: transform GEMM operands split once
         hsel_in = G.split(hsel) if pl else hsel
-        t1pre = G.linear_fwd(hsel_in, Wt)
+        am = meta.get("amax")  # h3 engine: {seq, wt, wd, t2} |max| slots (hsel's bound: the whole sequence output)
+        t1pre = G.linear_fwd(hsel_in, Wt, amax=(am["seq"], am["wt"]) if am else None)
         t1 = bias_gelu_fwd(t1pre, bt)
-        t2, z, mean, rstd = ln_fwd(t1, g, b, eps)
+        t2, z, mean, rstd = ln_fwd(t1, g, b, eps, amax=am["t2"] if am else None)
         # tied decoder on the compacted rows; fp32: split-bf16 kernel on the vocabulary padded to
         # 512 (logits is a view of a zero-padded buffer the backward reuses), else library GEMM
         if t2.dtype == torch.float32:
-            logits, lbuf = G.decoder_logits(t2, Wd, bdec)
+            logits, lbuf = G.decoder_logits(t2, Wd, bdec, amax=(am["t2"], am["wd"]) if am else None)
         else:
             logits, lbuf = G.gemm(t2, Wd, tb=True, bias=bdec, epi=1, out_dtype=torch.float32), None
         out, lse = xent_fwd(logits, lab)
@@ -744,10 +800,13 @@ class FusedPreTrainingLoss(torch.autograd.Function):
         # gradient (the embedding backward adds its rows later): it stores, the 94 MB of zeros unread
         store = meta.get("store")
         dec_acc = not (side and _FRESH_WGRAD and store is not None and store.claim_fresh())
+        am = meta.get("amax")
+        am_dl = G.amax_of(lbuf) if (am and lbuf is not None) else None  # dlogits: both decoder gradients' operand
         if lbuf is not None:  # padded split-bf16 decoder products (pad columns of dlogits stay zero)
             def dwdec():
                 out_w = Gv[4] if acc else torch.zeros((V, t2.shape[1]), dtype=torch.float32, device=t2.device)
-                return G.decoder_wgrad(lbuf, t2, V, out_w, accumulate=dec_acc)
+                return G.decoder_wgrad(lbuf, t2, V, out_w, accumulate=dec_acc,
+                                       amax=(am_dl, am["t2"]) if am_dl is not None else None)
         else:
             def dwdec():
                 return G.linear_wgrad(dl_c, t2, out=Gv[4] if acc else None, accumulate=acc)
@@ -770,17 +829,20 @@ class FusedPreTrainingLoss(torch.autograd.Function):
             h = tied.lookup(Gv[4])
             if h is not None:
                 h.dense_ready(dl_c.device)
-        dt2 = G.decoder_dgrad(lbuf, Wd, V) if lbuf is not None else G.gemm(dl_c, Wd)
+        dt2 = G.decoder_dgrad(lbuf, Wd, V, amax=(am_dl, am["wd"]) if am_dl is not None else None) \
+            if lbuf is not None else G.gemm(dl_c, Wd)
         dt1, _, dg, db, _ = ln_bwd(dt2, z, mean, rstd, g, 0.0, 0, acc=(Gv[2], Gv[3]) if acc else None, side=side)
         dt1pre, dbt = gelu_bwd_colsum(dt1, t1pre, bt, db_acc=Gv[1] if acc else None)
         hsel_in = _planes_of(hsel) if ctx.planes else hsel
         dt1pre_in = G.split(dt1pre) if ctx.planes else dt1pre
+        am_d = G.amax_of(dt1pre) if am else None  # the transform's two gradient products share it
+        wt_am = (am_d, am["seq"]) if am else None
         if side:
-            dWt = streams.run(dt1pre.device, lambda: G.linear_wgrad(dt1pre_in, hsel_in, out=Gv[0], accumulate=True),
-                              dt1pre_in, hsel_in)
+            dWt = streams.run(dt1pre.device, lambda: G.linear_wgrad(dt1pre_in, hsel_in, out=Gv[0], accumulate=True,
+                                                                    amax=wt_am), dt1pre_in, hsel_in, am_d)
         else:
-            dWt = G.linear_wgrad(dt1pre_in, hsel_in, out=Gv[0] if acc else None, accumulate=acc)
-        dhsel = G.linear_dgrad(dt1pre_in, Wt)
+            dWt = G.linear_wgrad(dt1pre_in, hsel_in, out=Gv[0] if acc else None, accumulate=acc, amax=wt_am)
+        dhsel = G.linear_dgrad(dt1pre_in, Wt, amax=(am_d, am["wt"]) if am else None)
         H_ = seq.shape[1]
         dseq = torch.zeros((ctx.T, H_), dtype=seq.dtype, device=seq.device)
         hip().scatter_add_rows(dtype_code(dseq), dhsel.data_ptr(), idx.data_ptr(), dseq.data_ptr(), idx.numel(),

@@ -12,10 +12,12 @@ epilogue.  Two engines:
              per-shape solution comes from the measured TunableOp table, see
              runtime/gemm_tuning.py), followed by the separate HIP epilogue kernels.
 
-fp32 products on the HIP engine run on the bf16 matrix cores as six split-bf16
-products (``HETSEQ_FP32_GEMM=x6``, default: fp32-level error at ~2.7x the exact-fp32
-MFMA rate, see gemm.hip ``split8``) or on the exact-fp32 MFMA (``native``); ``x3``
-(two-term split, ~2^-16 relative error) exists for benchmarking only.
+fp32 products on the HIP engine run on the 16-bit matrix cores: as three split-fp16
+products with per-tensor power-of-two operand scales (``HETSEQ_FP32_GEMM=h3``: fp32-level
+error at half the MFMA work of x6, see gemm.hip ``split4h``; every operand needs its |max|,
+which the producing kernels emit -- :func:`amax_of` computes it for the rest), as six split-bf16
+products (``x6``: fp32-level error, no scale needed), or on the exact-fp32 MFMA (``native``);
+``x3`` (two-term bf16 split, ~2^-16 relative error) exists for benchmarking only.
 
 ``HETSEQ_GEMM=hip|blas|auto`` selects; ``auto`` (default) times both paths --
 including the epilogue work the fused kernel absorbs -- once per (shape,
@@ -37,10 +39,11 @@ from hetseq_amd.ops._C import hip, stream_handle
 
 GEMM_CHOICES: dict = {}
 _MODE = os.environ.get("HETSEQ_GEMM", "auto")
-_FP32_DT = {"native": 0, "x6": 2, "x3": 3}
+_FP32_DT = {"native": 0, "x6": 2, "x3": 3, "h3": 4}
 _FP32 = os.environ.get("HETSEQ_FP32_GEMM", "x6")
 FP32_DEFAULT = _FP32
-assert _FP32 in _FP32_DT, "HETSEQ_FP32_GEMM must be one of native|x6|x3"
+assert _FP32 in _FP32_DT, "HETSEQ_FP32_GEMM must be one of native|x6|x3|h3"
+SPLIT_ENGINES = ("x6", "h3")  # the fp32-level split engines (x3 is a benchmarking variant)
 _SLABS: dict = {}  # (device, stream) -> split-K partial-sum workspace
 
 EPI_NONE, EPI_BIAS, EPI_GELU, EPI_DGELU = 0, 1, 2, 3
@@ -81,8 +84,30 @@ def load_choices(path):
     return True
 
 
+def amax_of(x, out=None):
+    """|max| of fp32 ``x`` as a 1-element device tensor (``out`` if given): the operand scale source of
+    the h3 engine for tensors no fused producer reported.  NaN propagates (a NaN |max| leaves the
+    operand unscaled, so the NaN reaches the product)."""
+    if out is None:
+        out = torch.empty(1, dtype=torch.float32, device=x.device)
+    if (x.is_cuda and x.dtype == torch.float32 and x.is_contiguous() and x.numel() % 4 == 0
+            and x.data_ptr() % 16 == 0):
+        hip().amax(x.data_ptr(), x.numel(), out.data_ptr(), 1, stream_handle())
+    else:
+        out.copy_(x.detach().abs().amax().reshape(1).float())
+    return out
+
+
+def _amax_ptr(t, given):
+    """(pointer, count) of an operand's |max| partials for the h3 engine."""
+    am = given if given is not None else amax_of(t)
+    assert am.dtype == torch.float32 and am.is_contiguous() and 1 <= am.numel() <= 8
+    return am.data_ptr(), am.numel()
+
+
 def set_fp32_mode(mode):
-    """'x6' (split-bf16 products, fp32-level error), 'native' (exact-fp32 MFMA) or 'x3' (benchmark only)."""
+    """'h3' (split-fp16 products, per-tensor scales), 'x6' (split-bf16 products; both fp32-level
+    error), 'native' (exact-fp32 MFMA) or 'x3' (benchmark only)."""
     global _FP32
     assert mode in _FP32_DT
     _FP32 = mode
@@ -388,25 +413,32 @@ def _hip_ok(a, b, out, *extra):
 
 
 def _hip_gemm(a, b, ta, tb, out, bias=None, epi=EPI_NONE, beta=0.0, aux=None, part=None, colsum=None,
-              colsum_acc=False, tile=-1, fp32=None, ksplit=0, dims=None, valid=None):
+              colsum_acc=False, tile=-1, fp32=None, ksplit=0, dims=None, valid=None, amax=None, amax_out=None):
     """Launch the HIP kernel; returns False (nothing launched) if the shape is not served.
 
     ``fp32`` picks the product engine (default: the HETSEQ_FP32_GEMM policy); ``ksplit``
-    0 = automatic split-K for the split-bf16 engines, 1 = none, >1 forced.  ``dims`` /
-    ``valid``: (M, N, K) of a padded problem and its valid extents (split-bf16 engine only):
+    0 = automatic split-K for the split engines, 1 = none, >1 forced.  ``dims`` /
+    ``valid``: (M, N, K) of a padded problem and its valid extents (split engines only):
     operand rows past the valid extents read as zero, C rows past valid M are not written.
+    ``amax`` = (a's, b's) |max| partials (1-D fp32 device tensors of 1..8 values, or None: computed
+    here) for the h3 engine; ``amax_out``: a zeroed 1-element tensor the GELU / dGELU epilogues
+    max |C| into.
     """
     M, N, K = dims if dims is not None else _dims(a, b, ta, tb)
     mv, nv, kv = valid if valid is not None else (0, 0, 0)
     assert dims is not None or out.shape == (M, N)
     dt = _FP32_DT[fp32 or _FP32]
+    am = (0, 0, 0, 0)
+    if dt == 4:
+        am = _amax_ptr(a, amax[0] if amax is not None else None) + _amax_ptr(b, amax[1] if amax is not None else None)
     slab = _slab(M, N, ksplit, a.device) if (dt or ksplit > 1) and epi <= EPI_BIAS and ksplit != 1 else None
     rc = hip().gemm(dt, int(ta), int(tb), M, N, K, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0),
                     out.data_ptr(), out.stride(0), bias.data_ptr() if bias is not None else 0, epi, float(beta),
                     aux.data_ptr() if aux is not None else 0, aux.stride(0) if aux is not None else 0,
                     part.data_ptr() if part is not None else 0, colsum.data_ptr() if colsum is not None else 0,
                     int(colsum_acc), stream_handle(), tile, ksplit,
-                    slab.data_ptr() if slab is not None else 0, slab.numel() if slab is not None else 0, mv, nv, kv)
+                    slab.data_ptr() if slab is not None else 0, slab.numel() if slab is not None else 0, mv, nv, kv,
+                    am[0], am[1], am[2], am[3], amax_out.data_ptr() if amax_out is not None else 0)
     return rc == 0
 
 
@@ -460,8 +492,10 @@ def _choose(key, run_hip, run_blas):
     return c
 
 
-def gemm(a, b, ta=False, tb=False, out=None, bias=None, epi=EPI_NONE, beta=0.0, out_dtype=None, ksplit=None):
+def gemm(a, b, ta=False, tb=False, out=None, bias=None, epi=EPI_NONE, beta=0.0, out_dtype=None, ksplit=None,
+         amax=None):
     """out = beta*out + op(a) @ op(b) (+bias).  ``ksplit`` overrides the measured split-K of the HIP engine.
+    ``amax``: (a's, b's) |max| partials for the h3 engine (None entries are computed).
 
     Operands that are :class:`Planes` (fp32 split once) or bf16 matrices run on the bf16-plane
     engine (gemm_planes.hip); fp32 tensors on the in-kernel-split engine (gemm.hip) or the library."""
@@ -488,8 +522,11 @@ def gemm(a, b, ta=False, tb=False, out=None, bias=None, epi=EPI_NONE, beta=0.0, 
         scratch = None
         ks = [0]  # split-K of the HIP engine: 0 = kernel heuristic, else measured (auto mode)
 
+        if _FP32 == "h3" and amax is None:  # one |max| pass per operand, shared by the measuring runs
+            amax = (amax_of(a), amax_of(b))
+
         def run_hip():
-            return _hip_gemm(a, b, ta, tb, scratch, bias, epi, beta, ksplit=ks[0])
+            return _hip_gemm(a, b, ta, tb, scratch, bias, epi, beta, ksplit=ks[0], amax=amax)
 
         def run_blas():
             _blas_gemm(a, b, ta, tb, scratch, bias, epi, beta, out_dtype)
@@ -516,7 +553,8 @@ def gemm(a, b, ta=False, tb=False, out=None, bias=None, epi=EPI_NONE, beta=0.0, 
             ks[0] = c[3]
         if ksplit is not None:
             ks[0] = ksplit
-        if _choose(key, run_hip, run_blas) == "hip" and _hip_gemm(a, b, ta, tb, out, bias, epi, beta, ksplit=ks[0]):
+        if _choose(key, run_hip, run_blas) == "hip" and _hip_gemm(a, b, ta, tb, out, bias, epi, beta, ksplit=ks[0],
+                                                                  amax=amax):
             return out
     return _blas_gemm(a, b, ta, tb, out, bias, epi, beta, out_dtype)
 
@@ -533,7 +571,7 @@ def _padded_ok(*ts):
             and ts[0].shape[0] % 128 == 0)
 
 
-def decoder_logits(t2, w, bias):
+def decoder_logits(t2, w, bias, amax=None):
     """logits [R, V] = t2 [R, H] @ w[V, H]^T + bias, returned as a view of a [R, pad512(V)]
     buffer whose pad columns are zero -- the split-bf16 engine runs the padded problem with the
     missing weight rows / bias entries read as zero.  Library GEMM when faster or not served."""
@@ -545,8 +583,11 @@ def decoder_logits(t2, w, bias):
     buf = torch.empty((R, Vp), dtype=torch.float32, device=t2.device)
     key = (R, V, H, "decoder_fwd")
 
+    if _FP32 == "h3" and amax is None:
+        amax = (amax_of(t2), amax_of(w))
+
     def run_hip():
-        return _hip_gemm(t2, w, False, True, buf, bias, EPI_BIAS, 0.0, dims=(R, Vp, H), valid=(R, V, H))
+        return _hip_gemm(t2, w, False, True, buf, bias, EPI_BIAS, 0.0, dims=(R, Vp, H), valid=(R, V, H), amax=amax)
 
     def run_blas():
         buf[:, V:].zero_()
@@ -558,16 +599,19 @@ def decoder_logits(t2, w, bias):
     return buf[:, :V], buf
 
 
-def decoder_dgrad(dlogits_buf, w, V):
+def decoder_dgrad(dlogits_buf, w, V, amax=None):
     """dt2 [R, H] = dlogits [R, V] @ w [V, H] from the zero-padded [R, pad512(V)] buffer."""
     R, Vp = dlogits_buf.shape
     H = w.shape[1]
     out = torch.empty((R, H), dtype=torch.float32, device=w.device)
     key = (R, H, V, "decoder_dgrad")
     ks = [0]
+    if _FP32 == "h3" and amax is None:
+        amax = (amax_of(dlogits_buf), amax_of(w))
 
     def run_hip():
-        return _hip_gemm(dlogits_buf, w, False, False, out, dims=(R, H, Vp), valid=(R, H, V), ksplit=ks[0])
+        return _hip_gemm(dlogits_buf, w, False, False, out, dims=(R, H, Vp), valid=(R, H, V), ksplit=ks[0],
+                         amax=amax)
 
     def run_blas():
         torch.mm(dlogits_buf[:, :V], w, out=out)
@@ -594,15 +638,17 @@ def decoder_dgrad(dlogits_buf, w, V):
     return out
 
 
-def decoder_wgrad(dlogits_buf, t2, V, out, accumulate):
+def decoder_wgrad(dlogits_buf, t2, V, out, accumulate, amax=None):
     """dW [V, H] (+)= dlogits^T @ t2 from the zero-padded buffer (rows past V are not written)."""
     R, Vp = dlogits_buf.shape
     H = t2.shape[1]
     key = (V, H, R, "decoder_wgrad", bool(accumulate))
     beta = 1.0 if accumulate else 0.0
+    if _FP32 == "h3" and amax is None:
+        amax = (amax_of(dlogits_buf), amax_of(t2))
 
     def run_hip(dst):
-        return _hip_gemm(dlogits_buf, t2, True, False, dst, beta=beta, dims=(Vp, H, R), valid=(V, H, R))
+        return _hip_gemm(dlogits_buf, t2, True, False, dst, beta=beta, dims=(Vp, H, R), valid=(V, H, R), amax=amax)
 
     def run_blas(dst):
         if accumulate:
@@ -631,13 +677,13 @@ def _choose_padded(key, run_hip, run_blas):
     return _choose(key, run_hip, run_blas)
 
 
-def linear_fwd(x, w, bias=None, out=None, ksplit=None):
+def linear_fwd(x, w, bias=None, out=None, ksplit=None, amax=None):
     """x[T,K] @ w[N,K]^T (+bias)."""
     return gemm(x, w, ta=False, tb=True, out=out, bias=bias, epi=EPI_BIAS if bias is not None else EPI_NONE,
-                ksplit=ksplit)
+                ksplit=ksplit, amax=amax)
 
 
-def linear_fwd_partials(x, w, ksplit=None):
+def linear_fwd_partials(x, w, ksplit=None, amax=None):
     """x[T,K] @ w[N,K]^T for a consumer that sums split-K partials itself (the LN forward after the
     FFN-out product): ``(partials [ks, T, N], ks)`` with the split-bf16 engine's K slices left in the
     stream's slab -- no reduce pass, the LN reads the slices in the reduce kernel's order, so the
@@ -653,27 +699,31 @@ def linear_fwd_partials(x, w, ksplit=None):
             ks = ksplit if ksplit is not None else (c[3] if len(c) > 3 else 0)
             slab = _slab(M, N, ks, x.device)
             if slab is not None:
+                am = (0, 0, 0, 0)
+                if _FP32 == "h3":
+                    am = _amax_ptr(x, amax[0] if amax is not None else None) + _amax_ptr(
+                        w, amax[1] if amax is not None else None)
                 rc = hip().gemm(_FP32_DT[_FP32], 0, 1, M, N, K, x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0),
                                 0, N, 0, EPI_NONE, 0.0, 0, 0, 0, 0, 0, stream_handle(), -1, ks, slab.data_ptr(),
-                                slab.numel(), 0, 0, 0)
+                                slab.numel(), 0, 0, 0, am[0], am[1], am[2], am[3], 0)
                 if rc == 0:
                     n = hip().gemm_last_ksplit()
                     return slab[:n * M * N].view(n, M, N), n
-    return linear_fwd(x, w), 1
+    return linear_fwd(x, w, amax=amax), 1
 
 
-def linear_dgrad(dy, w, out=None, accumulate=False, ksplit=None):
+def linear_dgrad(dy, w, out=None, accumulate=False, ksplit=None, amax=None):
     """dy[T,N] @ w[N,K]; accumulate=True adds into ``out``."""
-    return gemm(dy, w, ta=False, tb=False, out=out, beta=1.0 if accumulate else 0.0, ksplit=ksplit)
+    return gemm(dy, w, ta=False, tb=False, out=out, beta=1.0 if accumulate else 0.0, ksplit=ksplit, amax=amax)
 
 
-def linear_wgrad(dy, x, out=None, accumulate=False, ksplit=None):
+def linear_wgrad(dy, x, out=None, accumulate=False, ksplit=None, amax=None):
     """dy[T,N]^T @ x[T,K] -> [N,K] in fp32; accumulate=True adds into ``out`` (flat grad view)."""
     return gemm(dy, x, ta=True, tb=False, out=out, out_dtype=torch.float32, beta=1.0 if accumulate else 0.0,
-                ksplit=ksplit)
+                ksplit=ksplit, amax=amax)
 
 
-def linear_wgrad_colsum(dy, x, out, colsum_out, ksplit=None, accumulate=True):
+def linear_wgrad_colsum(dy, x, out, colsum_out, ksplit=None, accumulate=True, amax=None):
     """``out (+)= dy^T @ x`` and ``colsum_out (+)= dy.sum(0)`` (a Linear's weight and bias gradients) in
     one split-bf16 launch: the weight-gradient blocks of the first column tile sum dy's columns from
     the registers they stage (gemm.hip, ``wcol``), and one small pass adds the K slices' partials
@@ -681,7 +731,7 @@ def linear_wgrad_colsum(dy, x, out, colsum_out, ksplit=None, accumulate=True):
     layouts): the caller then runs :func:`linear_wgrad` and a column sum."""
     T, M = dy.shape
     N = x.shape[1]
-    if not (_MODE != "blas" and _FP32 == "x6" and isinstance(dy, torch.Tensor) and isinstance(x, torch.Tensor)
+    if not (_MODE != "blas" and _FP32 in SPLIT_ENGINES and isinstance(dy, torch.Tensor) and isinstance(x, torch.Tensor)
             and dy.is_cuda and dy.dtype == torch.float32 and x.dtype == torch.float32 and out.is_contiguous()
             and colsum_out.is_contiguous() and colsum_out.numel() == M and _hip_ok(dy, x, out)):
         return False
@@ -694,7 +744,7 @@ def linear_wgrad_colsum(dy, x, out, colsum_out, ksplit=None, accumulate=True):
             if torch.cuda.is_current_stream_capturing():
                 return False
             gemm(dy, x, ta=True, tb=False, out=torch.empty_like(out), beta=1.0, out_dtype=torch.float32,
-                 ksplit=ksplit)  # first call: measures the engines (into scratch)
+                 ksplit=ksplit, amax=amax)  # first call: measures the engines (into scratch)
         c = GEMM_CHOICES.get(key)
         if c is None or c[0] != "hip":
             return False
@@ -702,10 +752,10 @@ def linear_wgrad_colsum(dy, x, out, colsum_out, ksplit=None, accumulate=True):
             ks = c[3]
     part = torch.empty((max(ks, 1) if ks > 0 else 8, M), dtype=torch.float32, device=dy.device)
     return _hip_gemm(dy, x, True, False, out, beta=1.0 if accumulate else 0.0, part=part, colsum=colsum_out,
-                     colsum_acc=accumulate, fp32="x6", ksplit=ks)
+                     colsum_acc=accumulate, ksplit=ks, amax=amax)
 
 
-def linear_gelu_fwd(x, w, b, planes_out=False, emit_planes=False, out=None):
+def linear_gelu_fwd(x, w, b, planes_out=False, emit_planes=False, out=None, amax=None, amax_out=None):
     """FFN-in forward: pre = x @ w^T (un-biased, kept for the backward), y = gelu(pre + b).
 
     Returns (y, pre).  One fused HIP GEMM (epilogue writes both) or library GEMM + bias_gelu kernel.
@@ -713,6 +763,8 @@ def linear_gelu_fwd(x, w, b, planes_out=False, emit_planes=False, out=None):
     epilogue (no fp32 copy).  ``emit_planes``: y fp32 AND its planes from the same epilogue, the
     planes left for :func:`split_cached` (forward-only plane mode: the backward reads fp32 y).
     ``out`` = (y, pre) buffers to write (fp32 operands; row slices of whole-batch tensors).
+    ``amax``: (x's, w's) |max| partials (h3 engine); ``amax_out``: a zeroed 1-element tensor that
+    receives |max| of y (the FFN-out product's operand scale) -- filled on every path.
     """
     from hetseq_amd.ops import bert_ops
 
@@ -743,9 +795,11 @@ def linear_gelu_fwd(x, w, b, planes_out=False, emit_planes=False, out=None):
         y = torch.empty_like(pre)
     if x.is_cuda and _MODE != "blas" and _hip_ok(x, w, y, b, pre):
         key = (T, N, x.shape[1], "gelu_fwd")
+        if _FP32 == "h3" and amax is None:
+            amax = (amax_of(x), amax_of(w))
 
-        def run_hip():
-            return _hip_gemm(x, w, False, True, y, b, EPI_GELU, 0.0, aux=pre)
+        def run_hip(amo=None):
+            return _hip_gemm(x, w, False, True, y, b, EPI_GELU, 0.0, aux=pre, amax=amax, amax_out=amo)
 
         def run_blas():
             torch.mm(x, w.t(), out=pre)
@@ -753,17 +807,21 @@ def linear_gelu_fwd(x, w, b, planes_out=False, emit_planes=False, out=None):
 
         if key not in GEMM_CHOICES and _MODE == "auto" and not run_hip():
             GEMM_CHOICES[key] = ("blas", None, None)
-        if _choose(key, run_hip, run_blas) == "hip" and run_hip():
+        if _choose(key, run_hip, run_blas) == "hip" and run_hip(amax_out):
             return y, pre
     torch.mm(x, w.t(), out=pre)
-    return bert_ops.bias_gelu_fwd(pre, b, out=y), pre
+    bert_ops.bias_gelu_fwd(pre, b, out=y)
+    if amax_out is not None:
+        amax_of(y, out=amax_out)
+    return y, pre
 
 
-def linear_dgrad_dgelu(dy, w, pre, b, db_acc=None, planes_out=False):
+def linear_dgrad_dgelu(dy, w, pre, b, db_acc=None, planes_out=False, amax=None, amax_out=None):
     """FFN backward through the GELU: dpre = (dy @ w) * gelu'(pre + b), db = colsum(dpre).
 
     ``db`` is accumulated into ``db_acc`` (flat-store view) when given.  Returns (dpre, db);
     ``planes_out`` (fp32 plane engine): dpre as split-bf16 :class:`Planes` (no fp32 copy).
+    ``amax`` / ``amax_out``: as in :func:`linear_gelu_fwd` (|max| of dpre into ``amax_out``).
     """
     from hetseq_amd.ops import bert_ops
 
@@ -786,10 +844,12 @@ def linear_dgrad_dgelu(dy, w, pre, b, db_acc=None, planes_out=False):
     if dy.is_cuda and _MODE != "blas" and _hip_ok(dy, w, dpre, pre, b):
         key = (T, N, dy.shape[1], "dgelu")
         part = torch.empty(((T + 63) // 64, N), dtype=torch.float32, device=dy.device)
+        if _FP32 == "h3" and amax is None:
+            amax = (amax_of(dy), amax_of(w))
 
-        def run_hip(out_db, acc):
+        def run_hip(out_db, acc, amo=None):
             return _hip_gemm(dy, w, False, False, dpre, b, EPI_DGELU, 0.0, aux=pre, part=part, colsum=out_db,
-                             colsum_acc=acc)
+                             colsum_acc=acc, amax=amax, amax_out=amo)
 
         if key not in GEMM_CHOICES and _MODE == "auto":
             scratch_db = torch.zeros_like(db)
@@ -801,7 +861,70 @@ def linear_dgrad_dgelu(dy, w, pre, b, db_acc=None, planes_out=False):
                 GEMM_CHOICES[key] = ("blas", None, None)
             else:
                 _choose(key, lambda: run_hip(scratch_db, True), run_blas)
-        if _choose(key, None, None) == "hip" and run_hip(db, db_acc is not None):
+        if _choose(key, None, None) == "hip" and run_hip(db, db_acc is not None, amax_out):
             return dpre, db
     df = torch.mm(dy, w)
-    return bert_ops.gelu_bwd_colsum(df, pre, b, db_acc=db_acc)
+    dpre, db = bert_ops.gelu_bwd_colsum(df, pre, b, db_acc=db_acc)
+    if amax_out is not None:
+        amax_of(dpre, out=amax_out)
+    return dpre, db
+
+
+# ------------------------------------------------------------------ h3 operand scales per forward
+_SEG_TABLES: dict = {}  # (device, ((ptr, numel), ...)) -> (base ptr, int64 [nblk, 3] table, nblk)
+_SEG_CHUNK4 = 16384  # float4s per amax_seg block (64 Ki floats)
+
+
+def _seg_table(ts):
+    """Block table of ``amax_seg`` over the fp32 tensors ``ts`` (each contiguous, 16-B aligned,
+    numel % 4 == 0): offsets are float4 indices from the lowest address, so separate allocations
+    (no flat store) work as well as views into one flat buffer."""
+    dev = ts[0].device
+    key = (dev, tuple((t.data_ptr(), t.numel()) for t in ts))
+    hit = _SEG_TABLES.get(key)
+    if hit is not None:
+        return hit
+    base = min(t.data_ptr() for t in ts)
+    rows = []
+    for i, t in enumerate(ts):
+        assert t.dtype == torch.float32 and t.is_contiguous() and t.numel() % 4 == 0 and t.data_ptr() % 16 == 0
+        lo = (t.data_ptr() - base) // 16
+        hi = lo + t.numel() // 4
+        for c in range(lo, hi, _SEG_CHUNK4):
+            rows.append((i, c, min(hi, c + _SEG_CHUNK4)))
+    tab = torch.tensor(rows, dtype=torch.int64, device=dev)
+    hit = (base, tab, len(rows))
+    if len(_SEG_TABLES) > 64:
+        _SEG_TABLES.clear()
+    _SEG_TABLES[key] = hit
+    return hit
+
+
+class AmaxPool(object):
+    """|max| slots of one forward + backward on the h3 engine (zeroed once, 1 launch):
+
+    * ``w(i)``: weight ``i`` of the list given at construction -- filled right away by ONE
+      ``amax_seg`` launch over all of them (weights change in place every update, so every forward
+      measures them again; ~50 us for BERT-base's 86 M GEMM weights);
+    * ``act(i, n)``: activation / gradient slots, atomically maxed by the kernels that produce
+      those tensors (LN forward / backward, GELU / dGELU epilogues, embedding) or by ``amax_of``.
+    Each slot has exactly one producer stream, and its consumers are ordered after that producer,
+    so the scales -- and the results -- are deterministic."""
+
+    def __init__(self, weights, n_act, device):
+        self.nw = len(weights)
+        self.buf = torch.zeros(self.nw + n_act, dtype=torch.float32, device=device)
+        if weights:
+            base, tab, nblk = _seg_table(weights)
+            hip().amax_seg(base, tab.data_ptr(), nblk, self.buf.data_ptr(), stream_handle())
+
+    def w(self, i):
+        return self.buf[i:i + 1]
+
+    def act(self, i, n=1):
+        return self.buf[self.nw + i:self.nw + i + n]
+
+
+def h3_active(dtype=torch.float32):
+    """True when fp32 GEMMs run on the h3 engine (operand |max| slots are worth tracking)."""
+    return _FP32 == "h3" and _MODE != "blas" and dtype == torch.float32

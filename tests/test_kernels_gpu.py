@@ -575,7 +575,8 @@ def test_cross_entropy(cuda):
         _close(x.grad, x2.grad, 1e-4, 1e-8, "xent bwd")
 
 
-@pytest.mark.parametrize("engine,ksplit", [("native", 1), ("x6", 1), ("x6", 2), ("x6", 0)])
+@pytest.mark.parametrize("engine,ksplit", [("native", 1), ("x6", 1), ("x6", 2), ("x6", 0), ("h3", 1), ("h3", 2),
+                                           ("h3", 0)])
 @pytest.mark.parametrize("ta,tb", [(0, 1), (0, 0), (1, 0)])
 @pytest.mark.parametrize("M,N,K", [(256, 384, 128), (4096, 768, 768), (4096, 3072, 768), (768, 3072, 4096),
                                    (300, 130, 72), (640, 30522, 64)])
@@ -627,7 +628,7 @@ def test_gemm_hip(cuda, engine, ksplit, ta, tb, M, N, K):
         _close(db, db0.double() + x.grad.sum(0), 1e-5, 1e-3, "gemm dgelu colsum")
 
 
-@pytest.mark.parametrize("engine", ["x6"])
+@pytest.mark.parametrize("engine", ["x6", "h3"])
 def test_gemm_splitk_deterministic(cuda, engine):
     """Split-K partial slabs are summed in slice order by one reduction pass: repeated runs are
     bitwise identical."""
@@ -644,6 +645,81 @@ def test_gemm_splitk_deterministic(cuda, engine):
         out = torch.empty_like(first)
         assert G._hip_gemm(a, b, 1, 0, out, fp32=engine, ksplit=4)
         assert torch.equal(out, first)
+
+
+def _wide_range(shape, cuda, gen, decades):
+    """Gradient-like data: N(0,1) values times 10^u, u uniform in [-decades, 0] per ROW (some rows
+    ~10^-decades of the tensor's max) and a few 100x outliers."""
+    x = torch.randn(shape, device=cuda, generator=gen)
+    x *= torch.pow(10.0, -decades * torch.rand((shape[0], 1), device=cuda, generator=gen))
+    idx = torch.randint(0, x.numel(), (8,), device=cuda, generator=gen)
+    x.view(-1)[idx] *= 100.0
+    return x
+
+
+@pytest.mark.parametrize("data", ["uniform", "wide"])
+@pytest.mark.parametrize("ta,tb,M,N,K", [(0, 1, 4096, 2304, 768), (0, 0, 4096, 768, 3072), (1, 0, 768, 3072, 4096),
+                                         (0, 1, 512, 512, 64)])
+def test_gemm_h3_error_matches_fp32(cuda, data, ta, tb, M, N, K):
+    """Split-fp16 products with per-tensor power-of-two scales carry fp32-level error: within 2x of
+    the exact-fp32 MFMA kernel and of the library SGEMM against fp64 (units of |A|@|B|), on uniform
+    data and on gradient-like data spanning 6 decades per tensor (rows scaled by 10^-6..1, outliers
+    100x) -- the case a per-tensor scale is weakest at -- and NaN / inf in an operand propagate."""
+    from hetseq_amd.ops import gemm as G
+
+    g = torch.Generator(device=cuda)
+    g.manual_seed(21)
+    if data == "uniform":
+        a = torch.rand((K, M) if ta else (M, K), device=cuda, generator=g) * 2 - 1
+        b = torch.rand((N, K) if tb else (K, N), device=cuda, generator=g) * 2 - 1
+    else:
+        a = _wide_range((K, M) if ta else (M, K), cuda, g, 6.0)
+        b = _wide_range((N, K) if tb else (K, N), cuda, g, 6.0) * 1e-7  # far from 1: the scale must adapt
+    At, Bt = (a.t() if ta else a), (b.t() if tb else b)
+    ref = At.double() @ Bt.double()
+    mag = At.double().abs() @ Bt.double().abs()
+    out = torch.empty(M, N, device=cuda)
+
+    def err():
+        return float(((out.double() - ref).abs() / mag).max())
+
+    errs = {}
+    torch.mm(At, Bt, out=out)
+    errs["blas"] = err()
+    for eng in ("native", "x6", "h3"):
+        assert G._hip_gemm(a, b, ta, tb, out, fp32=eng)
+        errs[eng] = err()
+    assert errs["h3"] <= 2.0 * max(errs["native"], errs["blas"]), errs
+    # NaN / inf in an operand reach the product (never scaled away)
+    a2 = a.clone()
+    a2.view(-1)[17] = float("nan")
+    assert G._hip_gemm(a2, b, ta, tb, out, fp32="h3")
+    assert torch.isnan(out).any()
+    a2.view(-1)[17] = float("inf")
+    assert G._hip_gemm(a2, b, ta, tb, out, fp32="h3")
+    assert (~torch.isfinite(out)).any()
+
+
+def test_amax_kernels(cuda):
+    """|max| kernels: standalone (with NaN above inf) and the per-segment flat-buffer form."""
+    from hetseq_amd.ops import gemm as G
+    from hetseq_amd.ops._C import hip, stream_handle
+
+    x = torch.randn(1000, 36, device=cuda)
+    x[3, 5] = -77.0
+    assert G.amax_of(x).item() == 77.0
+    x[7, 7] = float("inf")
+    assert G.amax_of(x).item() == float("inf")
+    x[9, 9] = float("nan")
+    assert torch.isnan(G.amax_of(x)).all()
+    flat = torch.randn(4096, device=cuda)
+    segs = [(0, 0, 100), (1, 100, 700), (0, 700, 1024)]  # (segment, first float4, end float4)
+    tab = torch.tensor(segs, dtype=torch.int64, device=cuda)
+    out = torch.zeros(2, device=cuda)
+    hip().amax_seg(flat.data_ptr(), tab.data_ptr(), len(segs), out.data_ptr(), stream_handle())
+    v = flat.view(-1, 4)
+    want0 = torch.cat([v[0:100], v[700:1024]]).abs().max()
+    assert out[0].item() == want0.item() and out[1].item() == v[100:700].abs().max().item()
 
 
 @pytest.mark.parametrize("ta,tb,M,N,K", [(0, 1, 4096, 2304, 768), (0, 0, 4096, 768, 3072), (1, 0, 768, 3072, 4096)])

@@ -84,6 +84,13 @@ def main():
             e = err()
             t = timeit(lambda: G._hip_gemm(A, B, ta, tb, C, fp32="x3"))
             res.append(("x3", t, e))
+        am = (G.amax_of(A), G.amax_of(B))  # producer-side |max| in the step: not timed here
+        for ks in [int(x) for x in a.ksplit.split(",")]:
+            if not G._hip_gemm(A, B, ta, tb, C, fp32="h3", ksplit=ks, amax=am):
+                continue
+            e = err()
+            t = timeit(lambda: G._hip_gemm(A, B, ta, tb, C, fp32="h3", ksplit=ks, amax=am))
+            res.append(("h3" + ("" if ks == 0 else "/k%d" % ks), t, e))
         line = "%-11s %5dx%5dx%5d " % (name, M, N, K) + "  ".join(
             "%s %6.1fus %6.1fTF err %.2e" % (n, t, fl / t / 1e6, e) for n, t, e in res)
         print(line, flush=True)
