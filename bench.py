@@ -75,6 +75,18 @@ def parse():
                         + ") in --ab-rounds rounds of --steps steps each, one process, and print each variant's "
                         "median ms per step (interleaving cancels drift in the box's clock / thermal state)")
     p.add_argument("--ab-rounds", type=int, default=6, help=argparse.SUPPRESS)
+    p.add_argument("--fp32-gemm", default=None, choices=[None, "h3", "x6", "native"],
+                   help="fp32 GEMM engine (default: HETSEQ_FP32_GEMM or the built-in default)")
+    p.add_argument("--emulate-world", type=int, default=None, metavar="W",
+                   help="1 GPU: predict the W-rank data-parallel step -- the DP engine on a 1-rank RCCL world whose "
+                        "bucket collectives are replaced by stand-in kernels with W-rank traffic, duration and "
+                        "channel footprint (parallel/comm.py set_emulation); the JSON carries comm_emulated: W")
+    p.add_argument("--emulate-busbw", type=float, default=400.0, metavar="GB/s",
+                   help="bus bandwidth of the emulated ring collectives (per-rank received bytes / time)")
+    p.add_argument("--emulate-latency-us", type=float, default=12.0, help="fixed cost per emulated collective")
+    p.add_argument("--comm-channels", type=int, default=None,
+                   help="RCCL channel cap (NCCL_MAX_NCHANNELS) of real runs; workgroups per emulated collective "
+                        "(default 32 when emulating)")
     p.add_argument("--gemm-choices", default=None,
                    help="JSON of measured GEMM engine choices: loaded if it exists (no measuring in warm-up), "
                         "else written after the run (profiling runs use it to keep tuning out of the trace)")
@@ -181,6 +193,14 @@ def run_rank(b):
         return 3 if b.dry_run == rank else 0
     if b.gemm:
         os.environ["HETSEQ_GEMM"] = b.gemm
+    if b.fp32_gemm:
+        os.environ["HETSEQ_FP32_GEMM"] = b.fp32_gemm
+    if b.emulate_world and b.emulate_world > 1:
+        if int(os.environ.get("WORLD_SIZE", "1")) != 1:
+            print("bench.py: --emulate-world runs on ONE rank", file=sys.stderr)
+            return 2
+        b.ddp_world1 = True  # the DP engine on a 1-rank world, native RCCL engine, emulated collectives
+        b.comm_engine = "native"
     import torch
     import torch.distributed as dist
 
@@ -211,6 +231,10 @@ def run_rank(b):
             "--update-freq", str(b.update_freq), "--comm-engine", b.comm_engine]
     if b.no_fused:
         argv.append("--no-fused")
+    if b.comm_channels:
+        argv += ["--comm-channels", str(b.comm_channels)]
+    if b.emulate_world and b.emulate_world > 1:
+        argv += ["--emulate-world", str(b.emulate_world)]
     if b.hip_graph:
         argv.append("--hip-graph")
     if world > 1:
@@ -231,6 +255,7 @@ def run_rank(b):
 
     streams.reserve(torch.device("cuda", args.device_id))  # hardware queues before RCCL's streams
     if args.force_ddp:
+        distributed_utils.apply_comm_channels(args)
         dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % _free_port(), world_size=1, rank=0,
                                 device_id=torch.device("cuda", args.device_id))
     if world > 1:
@@ -267,6 +292,17 @@ def run_rank(b):
     if b.gemm_choices and os.path.exists(b.gemm_choices):
         G.load_choices(b.gemm_choices)
     ctl.optimizer  # build optimizer/scheduler (and the DP engine) before timing
+    emul = None
+    if b.emulate_world and b.emulate_world > 1:
+        comm = getattr(ctl.model, "comm", None)
+        if comm is None:
+            print("bench.py: --emulate-world needs the native RCCL engine (%s)"
+                  % __import__("hetseq_amd.parallel.comm", fromlist=["LAST_STATUS"]).LAST_STATUS, file=sys.stderr)
+            return 2
+        emul = {"world": b.emulate_world, "channels": b.comm_channels or 32, "busbw_gbs": b.emulate_busbw,
+                "latency_us": b.emulate_latency_us}
+        comm.set_emulation(b.emulate_world, emul["channels"], b.emulate_busbw, b.emulate_latency_us)
+        _EMUL.update(emul, comm=comm)
     for _ in range(b.warmup):
         ctl.train_step(next(gen))
     torch.cuda.synchronize()
@@ -327,7 +363,8 @@ def run_rank(b):
         comm_kind = "none" if (world == 1 and not args.force_ddp) else (
             "rccl-native" if getattr(ctl.model, "comm", None) is not None else "c10d-" + b.dist_backend)
         par = "dp%d" % world + (" (hetero %s)" % "+".join(str(n) for n, _ in _groups(b)) if b.hetero else "") + (
-            " (DP engine on a 1-rank world)" if args.force_ddp else "")
+            " (DP engine on a 1-rank world)" if args.force_ddp else "") + (
+            " emulating dp%d" % emul["world"] if emul else "")
         out = {
             "metric": "avg sec/step, BERT-base seq%d bs=%d/GPU" % (b.seq_len, b.batch),
             "value": round(sec, 6),
@@ -355,7 +392,16 @@ def run_rank(b):
             "data_wait_ms_per_step": round(data_wait / b.steps * 1000, 3),
             "allocator_events": alloc_events,
             "gemm_choices": {str(k): v for k, v in list(G.GEMM_CHOICES.items())[:32]},
+            "fp32_gemm": G.fp32_mode(),
+            "comm_emulated": emul["world"] if emul else None,
+            "emulation": emul,
         }
+        ddp = ctl.model if hasattr(ctl.model, "comm_log") else None
+        if ddp is not None:  # the last step's collectives: count, payload and received bytes, exposed tail
+            out["dp_collectives"] = {"n": len(ddp.comm_log), "payload_mb": round(sum(x[1] for x in ddp.comm_log) / 2**20, 2),
+                                     "received_mb": round(sum(x[3] for x in ddp.comm_log) / 2**20, 2),
+                                     "tail_received_mb": round(ddp.tail_bytes() / 2**20, 2),
+                                     "buckets": len(ddp.buckets), "sparse_tables": ddp.tables is not None}
         sys.stdout.write(json.dumps(out) + "\n")  # one write: other ranks may share this pipe
         sys.stdout.flush()
     if world > 1 or args.force_ddp:
@@ -364,6 +410,19 @@ def run_rank(b):
             ctl.model.comm.close()
         dist.destroy_process_group()
     return 0
+
+
+_EMUL: dict = {}  # the emulation in force (bench.py --emulate-world), for the --ab channel variants
+
+
+def _set_emul_channels(n):
+    _EMUL["channels"] = n
+    _EMUL["comm"].set_emulation(_EMUL["world"], n, _EMUL["busbw_gbs"], _EMUL["latency_us"])
+
+
+def _set_emul_busbw(gbs):
+    _EMUL["busbw_gbs"] = gbs
+    _EMUL["comm"].set_emulation(_EMUL["world"], _EMUL["channels"], gbs, _EMUL["latency_us"])
 
 
 def _set_attn(code):
@@ -463,6 +522,15 @@ _AB = {
     "fo_ks4": lambda: _set_site_ks((2048, 768, 3072, False, True, 0, False), 4),
     "lnpo_on": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_LN_PARTIALS_WO", True),  # attention-output part
     "lnpo_off": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_LN_PARTIALS_WO", False),
+    # --emulate-world: workgroups per emulated collective (RCCL channels) and the emulated bus bandwidth
+    "emu_ch4": lambda: _set_emul_channels(4),
+    "emu_ch8": lambda: _set_emul_channels(8),
+    "emu_ch16": lambda: _set_emul_channels(16),
+    "emu_ch32": lambda: _set_emul_channels(32),
+    "emu_ch64": lambda: _set_emul_channels(64),
+    "emu_bw250": lambda: _set_emul_busbw(250.0),
+    "emu_bw400": lambda: _set_emul_busbw(400.0),
+    "emu_bw600": lambda: _set_emul_busbw(600.0),
 }
 
 

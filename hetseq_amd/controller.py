@@ -115,7 +115,8 @@ class Controller(object):
                                               find_unused_parameters=self.args.find_unused_parameters,
                                               comm_engine=getattr(self.args, "comm_engine", "auto"),
                                               timeout_s=getattr(self.args, "collective_timeout", 1800.0),
-                                              sparse_embedding=sparse, sparse_capacity=cap)
+                                              sparse_embedding=sparse, sparse_capacity=cap,
+                                              plan_world=getattr(self.args, "emulate_world", None))
             else:
                 self._wrapped_model = self._model
                 if self.args.distributed_world_size > 1 and dist.is_initialized() and self.args.use_bmuf:

@@ -72,6 +72,11 @@ ncclRedOp_t nccl_op(int code) {
 
 hipStream_t as_stream(uintptr_t h) { return reinterpret_cast<hipStream_t>(h); }
 
+// Emulated collectives (bench.py --emulate-world): the stand-in kernel of the HIP module
+// (csrc/kernels/comm_emul.hip, hetseq_comm_emulation), reached through its address.
+typedef void (*EmulFn)(const void* src, int64_t src_bytes, void* scratch, int64_t scratch_bytes, int64_t traffic_bytes,
+                       int channels, int64_t hold_ns, hipStream_t st);
+
 size_t elem_size(int code) {
   switch (code) {
     case 0: return 4;
@@ -160,6 +165,11 @@ class Comm {
       give_event(e);  // recorded + waited: reusable once the comm stream passes it (ordered)
     }
     void* p = reinterpret_cast<void*>(ptr);
+    if (emul_) {  // W-rank prediction: ring all-reduce, each rank receives 2(W-1)/W of the bucket
+      const int64_t bytes = count * (int64_t)elem_size(dtype);
+      emulate(p, bytes, 2 * (emul_world_ - 1) * bytes / emul_world_, stream_);
+      return;
+    }
     if (snap_dst_) {
       // test mode: copy the bucket as it stands when the collective would read it (the copy is
       // ordered exactly like the all-reduce: on the comm stream, behind the producer events)
@@ -197,6 +207,27 @@ class Comm {
                  "ncclAllGather");
     }
     track(stream_);
+    if (emul_) {  // after the real (1-rank) gather: the other W-1 ranks' rows over the links
+      const int64_t bytes = count * (int64_t)elem_size(dtype);
+      emulate(reinterpret_cast<void*>(send), bytes, (emul_world_ - 1) * bytes, stream_);
+    }
+  }
+
+  // Emulation mode (1-rank communicator only): every bucket all-reduce / all-gather on the comm
+  // stream becomes the stand-in kernel -- `channels` workgroups moving the bytes a rank of a
+  // `world`-rank ring receives and staying resident for latency + bytes / busbw.  world <= 1 ends it.
+  void set_emulation(uintptr_t fn, int world, int channels, double busbw_gbs, double latency_us, uintptr_t scratch,
+                     int64_t scratch_bytes) {
+    if (world > 1 && nranks_ != 1) throw std::invalid_argument("hetseq comm: emulation needs a 1-rank communicator");
+    if (world > 1 && (!fn || !scratch || scratch_bytes < 16 || channels < 1 || busbw_gbs <= 0))
+      throw std::invalid_argument("hetseq comm: bad emulation parameters");
+    emul_ = world > 1 ? reinterpret_cast<EmulFn>(fn) : nullptr;
+    emul_world_ = world;
+    emul_channels_ = channels;
+    emul_busbw_ = busbw_gbs;
+    emul_lat_us_ = latency_us;
+    emul_scratch_ = scratch;
+    emul_scratch_bytes_ = scratch_bytes;
   }
 
   // Test hook (single-GPU ordering check): while set, all_reduce_async copies each bucket of
@@ -220,6 +251,11 @@ class Comm {
   void all_reduce(uintptr_t ptr, int64_t count, int dtype, int op, uintptr_t stream) {
     check();
     void* p = reinterpret_cast<void*>(ptr);
+    if (emul_) {  // (the fast-stat vector: latency-bound at W ranks)
+      const int64_t bytes = count * (int64_t)elem_size(dtype);
+      emulate(p, bytes, 2 * (emul_world_ - 1) * bytes / emul_world_, as_stream(stream));
+      return;
+    }
     {
       std::lock_guard<std::mutex> g(op_mu_);
       check();
@@ -283,6 +319,19 @@ class Comm {
 
  private:
   uintptr_t snap_dst_ = 0, snap_src_ = 0, snap_bytes_ = 0;
+  EmulFn emul_ = nullptr;
+  int emul_world_ = 1, emul_channels_ = 1;
+  double emul_busbw_ = 1.0, emul_lat_us_ = 0.0;
+  uintptr_t emul_scratch_ = 0;
+  int64_t emul_scratch_bytes_ = 0;
+
+  void emulate(void* src, int64_t src_bytes, int64_t traffic, hipStream_t s) {
+    const double ns = emul_lat_us_ * 1e3 + (double)traffic / emul_busbw_;  // bytes / (GB/s) = ns
+    emul_(src, src_bytes, reinterpret_cast<void*>(emul_scratch_), emul_scratch_bytes_, traffic, emul_channels_,
+          (int64_t)ns, s);
+    hip_check(hipGetLastError(), "comm emulation kernel launch");
+    track(s);
+  }
 
   struct Pending {
     hipEvent_t ev;
@@ -426,6 +475,8 @@ PYBIND11_MODULE(_comm, m) {
       .def("close", &Comm::close, py::arg("graceful") = true)
       .def("inject_stall", &Comm::inject_stall)
       .def("set_snapshot", &Comm::set_snapshot, py::arg("dst"), py::arg("src"), py::arg("bytes"))
+      .def("set_emulation", &Comm::set_emulation, py::arg("fn"), py::arg("world"), py::arg("channels"),
+           py::arg("busbw_gbs"), py::arg("latency_us"), py::arg("scratch"), py::arg("scratch_bytes"))
       .def("outstanding", &Comm::outstanding)
       .def_property_readonly("stream", &Comm::stream)
       .def_property_readonly("rank", &Comm::rank)

@@ -113,6 +113,9 @@ void launch_mnist_fc2_wgrad(const float*, const float*, float*, float*, float*, 
 void launch_mnist_col2im(const float*, const float*, float*, int, hipStream_t);
 void launch_mnist_conv1_wgrad(const float*, const float*, float*, float*, float*, int, hipStream_t);
 
+// comm_emul.hip (called by the native comm engine through its address)
+extern "C" void hetseq_comm_emulation(const void*, int64_t, void*, int64_t, int64_t, int, int64_t, hipStream_t);
+
 // HIP-graph mode: device word holding the dropout seed (see common.h resolve_seed)
 namespace hs {
 const uint64_t* g_seed_dev = nullptr;
@@ -440,6 +443,15 @@ PYBIND11_MODULE(_hip, m) {
     check_launch("scatter_add_rows");
   });
 
+  m.def("comm_emulation_fn", []() { return reinterpret_cast<i64>(&hetseq_comm_emulation); },
+        "address of the collective stand-in launcher (bench.py --emulate-world; csrc/comm/comm.cpp set_emulation)");
+  m.def("comm_emulation", [](i64 src, i64 src_bytes, i64 scratch, i64 scratch_bytes, i64 traffic, int channels,
+                             i64 hold_ns, i64 st) {
+    pre_launch("comm_emulation");
+    hetseq_comm_emulation(P(const void*, src), src_bytes, P(void*, scratch), scratch_bytes, traffic, channels, hold_ns,
+                          ST(st));
+    check_launch("comm_emulation");
+  }, "the collective stand-in kernel launched directly (tests)");
   m.def("amax", [](i64 x, i64 n, i64 out, int zero_first, i64 st) {
     pre_launch("amax");
     check(launch_amax(P(const float*, x), n, P(float*, out), zero_first, ST(st)), "amax");

@@ -213,6 +213,10 @@ def add_mi355x_args(parser):
                        help="seed dropout with seed+num_updates+rank (reference uses the same seed on all ranks)")
     group.add_argument("--check-consistency", type=int, default=0, metavar="N",
                        help="every N updates all-reduce a parameter checksum and fail on divergence")
+    group.add_argument("--comm-channels", type=int, default=None, metavar="N",
+                       help="cap RCCL's channels (NCCL_MAX_NCHANNELS) for the gradient collectives: each channel "
+                            "holds a workgroup slot beside the backward's GEMMs (profiles/r4_dp_emulation.md)")
+    group.add_argument("--emulate-world", type=int, default=None, metavar="W", help=argparse.SUPPRESS)
     group.add_argument("--collective-timeout", type=float, default=1800.0, metavar="SEC",
                        help="timeout for process-group collectives; the native engine's watchdog aborts the "
                             "communicator when a collective outlives it")

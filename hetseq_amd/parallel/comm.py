@@ -98,6 +98,27 @@ class NativeComm(object):
             assert dst.numel() == src.numel() and dst.dtype == src.dtype
             self._c.set_snapshot(dst.data_ptr(), src.data_ptr(), src.numel() * src.element_size())
 
+    def set_emulation(self, world, channels=32, busbw_gbs=400.0, latency_us=12.0, scratch_mb=64):
+        """Predict a ``world``-rank step on this 1-rank communicator (bench.py --emulate-world):
+        every bucket all-reduce / row all-gather / stats all-reduce becomes the stand-in kernel of
+        csrc/kernels/comm_emul.hip -- ``channels`` workgroups (RCCL's one per channel) moving the
+        bytes one rank of a ``world``-rank ring receives (an all-reduce 2(W-1)/W of the payload, an
+        all-gather (W-1) payloads) through HBM and resident for ``latency_us`` + bytes / ``busbw_gbs``.
+        ``world`` <= 1 restores the real collectives."""
+        from hetseq_amd.ops._C import hip
+
+        if world > 1:
+            self._emul_scratch = torch.empty(int(scratch_mb) << 20, dtype=torch.uint8,
+                                             device=torch.device("cuda", self.device))
+            self._c.set_emulation(hip().comm_emulation_fn(), int(world), int(channels), float(busbw_gbs),
+                                  float(latency_us), self._emul_scratch.data_ptr(), self._emul_scratch.numel())
+        else:
+            self._c.set_emulation(0, 1, 1, 1.0, 0.0, 0, 0)
+            self._emul_scratch = None
+        self.emulated = (int(world), int(channels), float(busbw_gbs), float(latency_us)) if world > 1 else None
+
+    emulated = None
+
     def wait(self, stream=None):
         """``stream`` (default current) waits for every collective issued on the comm stream."""
         self._c.wait(_stream(stream))

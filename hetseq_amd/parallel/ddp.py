@@ -48,12 +48,16 @@ from hetseq_amd.runtime import profiling, streams
 
 class FlatDDP(torch.nn.Module):
     def __init__(self, module, store, process_group=None, bucket_cap_mb=25, find_unused_parameters=False,
-                 broadcast=True, comm_engine="auto", timeout_s=1800.0, sparse_embedding=None, sparse_capacity=None):
+                 broadcast=True, comm_engine="auto", timeout_s=1800.0, sparse_embedding=None, sparse_capacity=None,
+                 plan_world=None):
         super().__init__()
         self.module = module
         self.store = store
         self.process_group = process_group or dist.group.WORLD
         self.world_size = dist.get_world_size(self.process_group)
+        # world size the layout decisions (sparse tables) and the byte accounting are made for: the
+        # real one, or the W a 1-rank run emulates (bench.py --emulate-world)
+        self.plan_world = int(plan_world) if plan_world else self.world_size
         # native RCCL engine (None: torch.distributed); chosen identically on every rank
         # (a 1-rank group gets one only on an explicit "native" request: the single-GPU tests)
         self.comm = native_comm.create(comm_engine, store.grad.is_cuda, self.process_group, timeout_s) \
@@ -68,7 +72,7 @@ class FlatDDP(torch.nn.Module):
         self.tables = None
         own = set()
         if (sparse_embedding is not None and SparseTableSync.supported(store, list(sparse_embedding[0]))
-                and SparseTableSync.pays(self.world_size, sparse_capacity, list(sparse_embedding[0]))):
+                and SparseTableSync.pays(self.plan_world, sparse_capacity, list(sparse_embedding[0]))):
             tables, rest = sparse_embedding
             self.tables = SparseTableSync(self, list(tables), sparse_capacity)
             own = {id(p) for p in rest}
@@ -125,7 +129,7 @@ class FlatDDP(torch.nn.Module):
 
     def _log(self, what, t, kind="allreduce"):
         n = t.numel() * t.element_size()
-        W = self.world_size
+        W = getattr(self, "plan_world", self.world_size)
         # ring collectives: an all-reduce receives 2(W-1)/W of the payload, an all-gather the other
         # W-1 ranks' payloads
         recv = (W - 1) * n if kind == "allgather" else 2 * (W - 1) * n // max(W, 1)

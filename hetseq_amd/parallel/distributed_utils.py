@@ -53,6 +53,7 @@ def distributed_init(args):
 
             # the engine's streams take their hardware queues before RCCL creates its streams
             streams.reserve(torch.device("cuda", torch.cuda.current_device()))
+        apply_comm_channels(args)
         timeout = datetime.timedelta(seconds=float(getattr(args, "collective_timeout", 1800.0)))
         if backend == "nccl" and torch.cuda.is_available():
             kw["device_id"] = torch.device("cuda", torch.cuda.current_device())
@@ -64,6 +65,16 @@ def distributed_init(args):
     args.distributed_rank = dist.get_rank()
     print("| actual rank {}".format(args.distributed_rank))
     return args.distributed_rank
+
+
+def apply_comm_channels(args):
+    """``--comm-channels N``: cap RCCL's channels (one workgroup each, resident on a CU for a
+    collective's whole duration, beside the backward's GEMM blocks) before any communicator
+    exists.  The value comes from the one-GPU emulation sweep (profiles/r4_dp_emulation.md);
+    an NCCL_MAX_NCHANNELS already in the environment wins."""
+    n = getattr(args, "comm_channels", None)
+    if n and "NCCL_MAX_NCHANNELS" not in os.environ:
+        os.environ["NCCL_MAX_NCHANNELS"] = str(int(n))
 
 
 def shutdown(controller=None):

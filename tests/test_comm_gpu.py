@@ -360,3 +360,70 @@ def test_graph_captured_dp_step_matches_eager(group):
         streams.set_enabled(old)
     for g in outs:
         assert torch.equal(g, eager), (g - eager).abs().max().item()
+
+
+def test_emulated_collectives_timing_and_identity(group):
+    """bench.py --emulate-world: on the 1-rank engine every bucket all-reduce becomes the stand-in
+    kernel -- the bucket is left exactly as it was (a 1-rank all-reduce is the identity), the comm
+    stream is busy for at least latency + received bytes / bus bandwidth of a W-rank ring, and the
+    consumer join still orders after it; world 1 restores the real collective."""
+    from hetseq_amd.parallel.comm import NativeComm
+
+    c = NativeComm(group, timeout_s=60)
+    try:
+        n = 8 << 20  # 32 MB bucket
+        g = torch.randn(n, device="cuda")
+        ref = g.clone()
+        W, bw, lat = 8, 200.0, 20.0
+        c.set_emulation(W, channels=16, busbw_gbs=bw, latency_us=lat)
+        comm_stream = torch.cuda.ExternalStream(c.stream_handle)
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        s.record(comm_stream)
+        c.all_reduce_async(g)
+        e.record(comm_stream)
+        c.wait()
+        torch.cuda.synchronize()
+        want_ms = (lat * 1e3 + 2 * (W - 1) * n * 4 / W / bw) / 1e6  # bytes / (GB/s) = ns
+        got_ms = s.elapsed_time(e)
+        assert got_ms >= 0.95 * want_ms, (got_ms, want_ms)
+        assert got_ms < want_ms + 5.0, (got_ms, want_ms)
+        assert torch.equal(g, ref)
+        # the all-gather: the real 1-rank gather, then the other W-1 ranks' rows over the links
+        rows = torch.randn(4096, 768, device="cuda")
+        out = torch.empty_like(rows)
+        s.record(comm_stream)
+        c.all_gather_async(out, rows)
+        e.record(comm_stream)
+        c.wait()
+        torch.cuda.synchronize()
+        assert torch.equal(out, rows)
+        assert s.elapsed_time(e) >= 0.95 * (lat * 1e3 + (W - 1) * rows.numel() * 4 / bw) / 1e6
+        c.set_emulation(1)
+        x = torch.arange(64, dtype=torch.float32, device="cuda")
+        c.all_reduce_async(x)
+        c.wait()
+        torch.cuda.synchronize()
+        assert torch.equal(x, torch.arange(64, dtype=torch.float32, device="cuda"))
+        c.check()
+    finally:
+        c.close()
+
+
+def test_bench_emulate_world_reports(tmp_path):
+    """bench.py --emulate-world 8 runs the DP engine on one GPU with emulated collectives and says so."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "2", "--warmup", "1", "--layers", "2",
+                        "--emulate-world", "8", "--comm-channels", "8"], capture_output=True, text=True, timeout=600,
+                       cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["comm_emulated"] == 8 and out["n_gpus"] == 1
+    assert out["emulation"]["channels"] == 8
+    assert "emulating dp8" in out["config"]["parallelism"]
+    dc = out["dp_collectives"]
+    assert dc["n"] > 0 and dc["received_mb"] > dc["payload_mb"]  # 2(W-1)/W > 1 at W = 8
