@@ -248,8 +248,10 @@ def run_rank(b):
     args = options.parse_cli(argv)
     args.distributed_rank = rank
     args.force_ddp = bool(b.ddp_world1 and world == 1)
-    # local index -> device (group offset for heterogeneous launches); gloo rehearsal: all on GPU 0
-    args.device_id = 0 if b.dist_backend == "gloo" else distributed_utils.local_device_id(args, local_rank)
+    # local index -> device (group offset for heterogeneous launches); gloo rehearsal: all on GPU 0,
+    # but the map the nccl path would use is still computed here and reported (JSON device_map)
+    mapped_device = distributed_utils.local_device_id(args, local_rank)
+    args.device_id = 0 if b.dist_backend == "gloo" else mapped_device
     torch.cuda.set_device(args.device_id)
     from hetseq_amd.runtime import streams
 
@@ -355,6 +357,12 @@ def run_rank(b):
     bert_ops.check_device_errors()
     sec = elapsed / b.steps
     seqs = b.batch * b.update_freq * world
+    me = {"rank": rank, "local_rank": local_rank, "group": int(os.environ.get("HETSEQ_GROUP", "0")),
+          "device_id": mapped_device, "ran_on": args.device_id}
+    device_map = [me]
+    if world > 1:  # every rank's computed rank -> device map, in rank order (rank 0 reports it)
+        device_map = [None] * world
+        dist.all_gather_object(device_map, me)
     if rank == 0 and b.gemm_choices and not os.path.exists(b.gemm_choices):
         G.save_choices(b.gemm_choices)
     if rank == 0:
@@ -393,6 +401,7 @@ def run_rank(b):
             "allocator_events": alloc_events,
             "gemm_choices": {str(k): v for k, v in list(G.GEMM_CHOICES.items())[:32]},
             "fp32_gemm": G.fp32_mode(),
+            "device_map": device_map,
             "comm_emulated": emul["world"] if emul else None,
             "emulation": emul,
         }

@@ -57,8 +57,30 @@ HS_DEVICE uint32_t wave_umax(uint32_t v) {
   return v;
 }
 // |max| of a lane's values, kept as bits of |x| (integer max = float max, NaN above inf): amax_bits
-// folds one value in; the wave's result goes out with one atomic max (gemm.hip amax_commit)
+// folds one value in; a wave's result goes out with one atomic max (amax_commit).
 HS_DEVICE uint32_t amax_bits(uint32_t m, float x) { return max(m, __float_as_uint(x) & 0x7fffffffu); }
+// A |max| SLOT (the h3 GEMM engine's operand scale source, ops/gemm.py AmaxPool) is kAmaxShards
+// partial maxima one 64-B line apart: writers spread their atomics over the shards by wave index, so
+// a thousand blocks finishing together do not serialise on one address (one address took ~11 ns per
+// atomic: 82 us for a 4096-wave kernel's tail); readers max over the shards (amax_read).
+constexpr int kAmaxShards = 32;
+constexpr int kAmaxStride = 16;  // floats between shards
+HS_DEVICE void amax_put(float* slot, uint32_t m, int who) {
+  atomicMax(reinterpret_cast<unsigned int*>(slot + (who % kAmaxShards) * kAmaxStride), m);
+}
+// the wave's |max| into its shard (all 64 lanes call it; lane 0 issues the atomic)
+HS_DEVICE void amax_commit(float* slot, uint32_t m) {
+  m = wave_umax(m);
+  if ((threadIdx.x & 63) == 0) amax_put(slot, m, (int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
+}
+// |max| over `nslots` adjacent slots as |x| bits, read cooperatively by the whole wave (every lane
+// gets the result; all 64 lanes must call it)
+HS_DEVICE uint32_t amax_read(const float* slot, int nslots) {
+  uint32_t b = 0u;
+  for (int i = threadIdx.x & 63; i < nslots * kAmaxShards; i += 64)
+    b = max(b, __float_as_uint(slot[i * kAmaxStride]) & 0x7fffffffu);
+  return wave_umax(b);
+}
 HS_DEVICE double wave_sum_d(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

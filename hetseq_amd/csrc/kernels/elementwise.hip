@@ -458,38 +458,58 @@ HS_DEVICE uint32_t absbits4(uint4 v) {
   return max(max(v.x & 0x7fffffffu, v.y & 0x7fffffffu), max(v.z & 0x7fffffffu, v.w & 0x7fffffffu));
 }
 
+// 4 independent 16-B loads per lane per iteration; the wave maxima of a block are combined in LDS and
+// the block issues ONE atomic, into its shard of the slot
 __global__ void __launch_bounds__(256) amax_kernel(const float* __restrict__ x, int64_t n4, float* __restrict__ out) {
+  const uint4* v = reinterpret_cast<const uint4*>(x);
+  const int64_t stride = (int64_t)gridDim.x * 256;
   uint32_t m = 0u;
-  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256)
-    m = max(m, absbits4(reinterpret_cast<const uint4*>(x)[i]));
+  int64_t i = blockIdx.x * 256ll + threadIdx.x;
+  for (; i + 3 * stride < n4; i += 4 * stride)
+    m = max(max(m, max(absbits4(v[i]), absbits4(v[i + stride]))), max(absbits4(v[i + 2 * stride]),
+                                                                       absbits4(v[i + 3 * stride])));
+  for (; i < n4; i += stride) m = max(m, absbits4(v[i]));
   m = wave_umax(m);
-  if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned int*>(out), m);
+  __shared__ uint32_t red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) amax_put(out, max(max(red[0], red[1]), max(red[2], red[3])), blockIdx.x);
 }
 
-// block b reduces float4 range [tab[3b+1], tab[3b+2]) of the flat buffer into out[tab[3b]]
+// block b reduces float4 range [tab[3b+1], tab[3b+2]) of the flat buffer into slot tab[3b] of out
 __global__ void __launch_bounds__(256) amax_seg_kernel(const float* __restrict__ base, const int64_t* __restrict__ tab,
                                                        float* __restrict__ out) {
   const int64_t seg = tab[3 * blockIdx.x], lo = tab[3 * blockIdx.x + 1], hi = tab[3 * blockIdx.x + 2];
+  const uint4* v = reinterpret_cast<const uint4*>(base);
   uint32_t m = 0u;
-  for (int64_t i = lo + threadIdx.x; i < hi; i += 256) m = max(m, absbits4(reinterpret_cast<const uint4*>(base)[i]));
+  int64_t i = lo + threadIdx.x;
+  for (; i + 768 < hi; i += 1024)
+    m = max(max(m, max(absbits4(v[i]), absbits4(v[i + 256]))), max(absbits4(v[i + 512]), absbits4(v[i + 768])));
+  for (; i < hi; i += 256) m = max(m, absbits4(v[i]));
   m = wave_umax(m);
-  if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned int*>(out + seg), m);
+  __shared__ uint32_t red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    amax_put(out + seg * kAmaxShards * kAmaxStride, max(max(red[0], red[1]), max(red[2], red[3])), blockIdx.x);
 }
 
 }  // namespace hs
 
-// |max| of x[0, n) (n % 4 == 0, 16-B aligned) into *out; zero_first: out is cleared on the stream first
+// |max| of x[0, n) (n % 4 == 0, 16-B aligned) into the slot `out` (common.h: kAmaxShards shards);
+// zero_first: the slot is cleared on the stream first
 int launch_amax(const float* x, int64_t n, float* out, int zero_first, hipStream_t st) {
   if (n % 4 || (reinterpret_cast<uintptr_t>(x) & 15)) return -1;
-  if (zero_first && hipMemsetAsync(out, 0, sizeof(float), st) != hipSuccess) return -1;
+  if (zero_first && hipMemsetAsync(out, 0, sizeof(float) * kAmaxShards * kAmaxStride, st) != hipSuccess) return -1;
   if (n == 0) return 0;
   const int64_t n4 = n / 4;
-  const int grid = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
+  const int grid = (int)std::min<int64_t>((n4 + 1023) / 1024, 1024);
   hipLaunchKernelGGL(amax_kernel, dim3(grid), dim3(256), 0, st, x, n4, out);
   return 0;
 }
 
-// per-segment |max| over a flat buffer: tab = [nblk][3] int64 (segment, first float4, end float4)
+// per-segment |max| over a flat buffer into slots (segment i -> slot i of `out`): tab = [nblk][3] int64
+// (segment, first float4, end float4)
 void launch_amax_seg(const float* base, const int64_t* tab, int nblk, float* out, hipStream_t st) {
   if (nblk > 0) hipLaunchKernelGGL(amax_seg_kernel, dim3(nblk), dim3(256), 0, st, base, tab, out);
 }

@@ -81,8 +81,9 @@ struct GemmArgs {
   // rows past them read as zeros, C rows past Mv are not written, bias past Nv reads as zero
   int Mv, Nv, Kv;
   int slice_major;  // split-K block order: 1 = all tiles of slice 0, then slice 1, ... (else tile-major)
-  // fp16 two-term split (NT == 4): per-tensor |max| of op(A) / op(B), na / nb partial maxima each
-  // (e.g. one per half-batch producer); the kernel scales each operand by a power of two from them
+  // fp16 two-term split (NT == 4): per-tensor |max| of op(A) / op(B) as na / nb adjacent slots each
+  // (common.h kAmaxShards; e.g. one slot per half-batch producer); the kernel scales each operand by
+  // a power of two from them
   const float* amax_a;
   const float* amax_b;
   int namax_a, namax_b;
@@ -193,10 +194,8 @@ HS_DEVICE f32x16 mma_bf(bfx8 a, bfx8 b, f32x16 c) { return __builtin_amdgcn_mfma
 typedef _Float16 hx2 __attribute__((ext_vector_type(2)));
 typedef _Float16 hx8 __attribute__((ext_vector_type(8)));
 
-HS_DEVICE int h16_exp(const float* am, int n) {
-  uint32_t b = 0u;  // max over the partial maxima as |x| bits (a NaN partial wins)
-  for (int i = 0; i < n; ++i) b = max(b, __float_as_uint(am[i]) & 0x7fffffffu);
-  const float m = __uint_as_float(b);
+HS_DEVICE int h16_exp(const float* am, int nslots) {
+  const float m = __uint_as_float(amax_read(am, nslots));  // (a NaN partial wins)
   if (!(m > 0.f) || !(m <= 3.4028235e38f)) return 0;  // zero, NaN or inf: unscaled (NaN / inf propagate)
   return min(126, max(-126, 14 - ilogbf(m)));
 }
@@ -225,12 +224,8 @@ HS_DEVICE f32x16 mma_nt(bfx8 a, bfx8 b, f32x16 c) {
     return mma_bf(a, b, c);
 }
 
-// |max| of the values a lane wrote (amax_bits) -> one atomic max per wave (non-negative floats order as
+// (|max| of the values a lane wrote: amax_bits / amax_commit in common.h -- non-negative floats order as
 // their bit patterns; NaN's pattern sorts above inf, so a NaN output reaches the consumer's scale as NaN)
-HS_DEVICE void amax_commit(float* out, uint32_t m) {
-  m = wave_umax(m);
-  if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned int*>(out), m);
-}
 
 // Shared GEMM epilogue (both kernels): split-K slab, or C = acc (+bias) (+beta*C) / GELU /
 // dGELU + column partial sums.  acc[i][j] register r -> row m0+wm+MF*i+Mf::row(r,q), col n0+wn+MF*j+lr.
@@ -409,6 +404,11 @@ __global__ void __launch_bounds__(256, 2) gemm_f32_kernel(GemmArgs p) {
 // One LDS buffer (53 KB) + a register prefetch of the next K tile: two barriers
 // per K tile, two blocks per CU, so one block's staging overlaps the other's MFMAs.
 constexpr int XROW = 208;  // bytes per LDS image row
+// rows of the two-plane engines (NT 3, 4) drop the unused third plane: 144 B = 9 x 16 B, still an
+// odd number of 16-B slots, so the fragment reads stay conflict-free (tools/lds_banks.py) and a
+// block's two images take 36 KB instead of 53 KB
+template <int NT>
+constexpr int xrow() { return NT >= 6 ? XROW : 144; }
 
 template <bool SWZ>
 HS_DEVICE int xchunk(int r, int kc) { return SWZ ? kc ^ ((r ^ (r >> 3)) & 3) : kc; }
@@ -452,7 +452,7 @@ HS_DEVICE void x_store(char* __restrict__ S, const float4 (&v)[4], int t, float 
     const int r = 4 * g + i;
     uint2 h, m, l;
     split_nt<NT>(v[i], sc, h, m, l);
-    char* row = S + r * XROW + 16 * xchunk<!KCONTIG>(r, c >> 1) + 8 * (c & 1);
+    char* row = S + r * xrow<NT>() + 16 * xchunk<!KCONTIG>(r, c >> 1) + 8 * (c & 1);
     *reinterpret_cast<uint2*>(row) = h;
     *reinterpret_cast<uint2*>(row + 64) = m;
     if (NT >= 6) *reinterpret_cast<uint2*>(row + 128) = l;
@@ -460,10 +460,10 @@ HS_DEVICE void x_store(char* __restrict__ S, const float4 (&v)[4], int t, float 
 }
 
 // fragment of plane p (0 hi, 1 mid, 2 lo), k-slice ks, for the 32-row tile at `row`
-template <bool SWZ>
+template <bool SWZ, int NT = 6>
 HS_DEVICE bfx8 x_frag(const char* __restrict__ S, int row, int p, int ks, int lr, int h) {
   const int r = row + lr;
-  return *reinterpret_cast<const bfx8*>(S + r * XROW + 64 * p + 16 * xchunk<SWZ>(r, 2 * ks + h));
+  return *reinterpret_cast<const bfx8*>(S + r * xrow<NT>() + 64 * p + 16 * xchunk<SWZ>(r, 2 * ks + h));
 }
 
 // Transposed-read layout ("TR", mn-contiguous sources): instead of a register 4x4 transpose into
@@ -473,6 +473,8 @@ HS_DEVICE bfx8 x_frag(const char* __restrict__ S, int row, int p, int ks, int lr
 // row: conflict-free) and the transposed reads hit 4 different bank quarters per k-row quad.
 constexpr int TROW = 256;                // bytes per k row of one plane
 constexpr int TIMG = 3 * GBK * TROW;     // the three planes of one operand tile: 24 KB
+template <int NT>
+constexpr int timg() { return (NT >= 6 ? 3 : 2) * GBK * TROW; }  // two-plane engines: 16 KB
 typedef short sx4 __attribute__((ext_vector_type(4)));
 typedef short sx8 __attribute__((ext_vector_type(8)));
 
@@ -533,7 +535,7 @@ __global__ void __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(NB
   static_assert(!EDGE || (WV == 4 && EPI <= kEpiBias), "edge-masked launches: 4 waves, plain / bias epilogue");
   static_assert(PF == 1 || (WV == 4 && NBUF == 1 && !EDGE), "two-deep prefetch: 4-wave, single-buffer, unmasked");
   constexpr bool TRA = TRL && TA, TRB = TRL && !TB;  // operands staged in the transposed-read layout
-  constexpr int IA = TRA ? TIMG : 128 * XROW, IB = TRB ? TIMG : 128 * XROW;
+  constexpr int IA = TRA ? timg<NT>() : 128 * xrow<NT>(), IB = TRB ? timg<NT>() : 128 * xrow<NT>();
   __shared__ __attribute__((aligned(16))) char smem[NBUF * (IA + IB)];
   char* const As = smem;
   char* const Bs = smem + IA;
@@ -651,10 +653,10 @@ __global__ void __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(NB
       for (int pl = 0; pl < NPL; ++pl) {
 #pragma unroll
         for (int i = 0; i < TM; ++i)
-          af[ks][pl][i] = TRA ? x_frag_tr(Ab, wm + 32 * i, pl, ks, lane) : x_frag<TA>(Ab, wm + 32 * i, pl, ks, lr, q);
+          af[ks][pl][i] = TRA ? x_frag_tr(Ab, wm + 32 * i, pl, ks, lane) : x_frag<TA, NT>(Ab, wm + 32 * i, pl, ks, lr, q);
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          bf[ks][pl][j] = TRB ? x_frag_tr(Bb, wn + 32 * j, pl, ks, lane) : x_frag<!TB>(Bb, wn + 32 * j, pl, ks, lr, q);
+          bf[ks][pl][j] = TRB ? x_frag_tr(Bb, wn + 32 * j, pl, ks, lane) : x_frag<!TB, NT>(Bb, wn + 32 * j, pl, ks, lr, q);
       }
     between();
 #pragma unroll
@@ -990,6 +992,7 @@ int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, i
                 const float* amax_b, int namax_b, float* amax_c) {
   if ((dtype != 0 && dtype != 2 && dtype != 3 && dtype != 4) || M <= 0 || N <= 0 || K <= 0 || K % GBK != 0) return -1;
   if (dtype == 4 && (!amax_a || !amax_b || namax_a < 1 || namax_b < 1 || namax_a > 8 || namax_b > 8)) return -1;
+  // (namax_*: adjacent |max| slots of kAmaxShards shards each, common.h)
   auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
   if (!al16(A) || !al16(B) || lda % 4 || ldb % 4) return -1;
   if ((epi >= 1 && !bias) || (epi >= 2 && (!aux || beta != 0.f)) || (epi == 3 && (!part || !colsum_out)))

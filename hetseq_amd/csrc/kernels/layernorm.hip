@@ -111,10 +111,7 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const T* __restrict__ a, co
       rstd_out[row] = rstd;
     }
   }
-  if (amax_y) {
-    am = wave_umax(am);
-    if (lane == 0) atomicMax(reinterpret_cast<unsigned int*>(amax_y), am);
-  }
+  if (amax_y) amax_commit(amax_y, am);
 }
 
 // Column partials are written as part[blockIdx.x][H] (one row per block); the WV waves'
@@ -262,10 +259,7 @@ __global__ void __launch_bounds__(64 * kLnBwdWaves) ln_bwd_kernel(
     rstd = rn;
     row = nxt;
   }
-  if (amax_out) {
-    am = wave_umax(am);
-    if (lane == 0) atomicMax(reinterpret_cast<unsigned int*>(amax_out), am);
-  }
+  if (amax_out) amax_commit(amax_out, am);
   if constexpr (CHUNK) {
     static_assert(kLnBwdWaves == 4, "chunked partials: 4 waves");
     __shared__ __attribute__((aligned(16))) float win[768];
@@ -338,10 +332,7 @@ __global__ void __launch_bounds__(256) emb_fwd_kernel(const int64_t* __restrict_
       rstd_out[row] = rstd;
     }
   }
-  if (amax_y) {
-    am = wave_umax(am);
-    if (lane == 0) atomicMax(reinterpret_cast<unsigned int*>(amax_y), am);
-  }
+  if (amax_y) amax_commit(amax_y, am);
 }
 
 // Embedding LayerNorm backward: writes dx = d(word + pos + type) per row (fp32)

@@ -107,7 +107,7 @@ def ln_fwd(a, gamma, beta, eps=1e-12, bias=None, resid=None, p=0.0, mode=0, seed
                  z.data_ptr() if z is not None else 0, mean.data_ptr(), rstd.data_ptr(), rows, H, float(eps), float(p),
                  seed, off, mode, stream_handle(), planes.data_ptr() if planes is not None else 0,
                  rows * H if planes is not None else 0, nslab, stride if nslab > 1 else 0, int(row0),
-                 amax.data_ptr() if amax is not None else 0)
+                 G.slot_ptr(amax))
     return y, z, mean, rstd
 
 
@@ -128,7 +128,7 @@ def ln_bwd(dy, z, mean, rstd, gamma, p=0.0, mode=0, seed=0, off=0, want_dz=True,
                  dz.data_ptr() if dz is not None else 0, da.data_ptr() if da is not None else 0, part[0].data_ptr(),
                  part[1].data_ptr(), part[2].data_ptr(), rows, H, float(p), seed, off, mode, stream_handle(),
                  da_planes.data_ptr() if da_planes is not None else 0, rows * H if da_planes is not None else 0,
-                 amax.data_ptr() if amax is not None else 0)
+                 G.slot_ptr(amax))
     n = 3 if mode == 1 else 2
     if acc is not None:
         outs = list(acc[:n])
@@ -205,7 +205,7 @@ def attn_fwd(qkv, mask, B, S, NH, p, seed, off, bias=None, outs=None, b0=0, amax
                    ctx.data_ptr(), lse.data_ptr(), dmask.data_ptr() if dmask is not None else 0, B, S, NH, 64,
                    float(p), seed, off, stream_handle(), int(b0) * NH)
     if amax is not None:
-        hip().amax(ctx.data_ptr(), ctx.numel(), amax.data_ptr(), 0, stream_handle())
+        G.amax_into(ctx, amax)
     return ctx, (lse, dmask)
 
 
@@ -221,7 +221,7 @@ def attn_bwd(qkv, mask, ctx, dctx, lse, B, S, NH, p, seed=0, off=0, bias=None, a
                    ctx.data_ptr(), dctx.data_ptr(), lse.data_ptr(), dbuf.data_ptr(), dqkv.data_ptr(),
                    dmask.data_ptr() if dmask is not None else 0, B, S, NH, 64, float(p), stream_handle())
     if amax is not None:
-        hip().amax(dqkv.data_ptr(), dqkv.numel(), amax.data_ptr(), 0, stream_handle())
+        G.amax_into(dqkv, amax)
     return dqkv
 
 
@@ -345,7 +345,7 @@ class FusedEmbedding(torch.autograd.Function):
         hip().emb_fwd(dtype_code(y), ids.data_ptr(), tt.data_ptr() if tt is not None else 0, wword.data_ptr(),
                       wpos.data_ptr(), wtype.data_ptr(), gamma.data_ptr(), beta.data_ptr(), y.data_ptr(), z.data_ptr(),
                       mean.data_ptr(), rstd.data_ptr(), rows, S, H, V, TV, float(eps), float(p), seed, off,
-                      err.data_ptr(), stream_handle(), amax.data_ptr() if amax is not None else 0)
+                      err.data_ptr(), stream_handle(), G.slot_ptr(amax))
         ctx.save_for_backward(ids, tt if tt is not None else ids.new_zeros(0), z, mean, rstd, gamma)
         ctx.cfg = (B, S, V, H, TV, wpos.shape[0], p, seed, off, tt is not None)
         ctx.sink = sink

@@ -40,7 +40,7 @@ from hetseq_amd.ops._C import hip, stream_handle
 GEMM_CHOICES: dict = {}
 _MODE = os.environ.get("HETSEQ_GEMM", "auto")
 _FP32_DT = {"native": 0, "x6": 2, "x3": 3, "h3": 4}
-_FP32 = os.environ.get("HETSEQ_FP32_GEMM", "x6")
+_FP32 = os.environ.get("HETSEQ_FP32_GEMM", "h3")
 FP32_DEFAULT = _FP32
 assert _FP32 in _FP32_DT, "HETSEQ_FP32_GEMM must be one of native|x6|x3|h3"
 SPLIT_ENGINES = ("x6", "h3")  # the fp32-level split engines (x3 is a benchmarking variant)
@@ -84,25 +84,62 @@ def load_choices(path):
     return True
 
 
+# A |max| slot: AMAX_SHARDS partial maxima 64 B apart (csrc/kernels/common.h kAmaxShards): writers
+# spread their atomics over the shards, readers max over them
+AMAX_SHARDS, AMAX_STRIDE = 32, 16
+SLOT_FLOATS = AMAX_SHARDS * AMAX_STRIDE
+
+
+def amax_value(slot_tensor):
+    """The |max| a slot tensor (amax_of's result) holds (tests / diagnostics)."""
+    v = slot_tensor.view(-1, AMAX_STRIDE)[:, 0]
+    return v.view(-1, AMAX_SHARDS).max(dim=1).values
+
+
 def amax_of(x, out=None):
-    """|max| of fp32 ``x`` as a 1-element device tensor (``out`` if given): the operand scale source of
+    """|max| of fp32 ``x`` as a one-slot device tensor (``out`` if given): the operand scale source of
     the h3 engine for tensors no fused producer reported.  NaN propagates (a NaN |max| leaves the
     operand unscaled, so the NaN reaches the product)."""
     if out is None:
-        out = torch.empty(1, dtype=torch.float32, device=x.device)
+        out = torch.empty(SLOT_FLOATS, dtype=torch.float32, device=x.device)
     if (x.is_cuda and x.dtype == torch.float32 and x.is_contiguous() and x.numel() % 4 == 0
             and x.data_ptr() % 16 == 0):
         hip().amax(x.data_ptr(), x.numel(), out.data_ptr(), 1, stream_handle())
     else:
-        out.copy_(x.detach().abs().amax().reshape(1).float())
+        out.zero_()
+        amax_into(x, out)
     return out
 
 
-def _amax_ptr(t, given):
-    """(pointer, count) of an operand's |max| partials for the h3 engine."""
+def slot_ptr(a):
+    """Device address of a |max| slot: a (pointer, count) tuple (AmaxPool slots -- plain ints, no
+    tensor view per use), a 1-D fp32 tensor, or None (0)."""
+    if a is None:
+        return 0
+    return a[0] if isinstance(a, tuple) else a.data_ptr()
+
+
+def amax_into(x, slot):
+    """Atomically max |x| into an existing slot (tensor or (pointer, count)) on the current stream."""
+    if (x.is_cuda and x.dtype == torch.float32 and x.is_contiguous() and x.numel() % 4 == 0
+            and x.data_ptr() % 16 == 0):
+        hip().amax(x.data_ptr(), x.numel(), slot_ptr(slot), 0, stream_handle())
+    else:
+        tmp = torch.zeros(4, dtype=torch.float32, device=x.device)
+        tmp[0] = x.detach().abs().amax().float() if x.numel() else 0.0
+        hip().amax(tmp.data_ptr(), 4, slot_ptr(slot), 0, stream_handle())
+
+
+def _amax_ptr(t, given, keep):
+    """(pointer, count) of an operand's |max| partials for the h3 engine.  A |max| computed here is
+    appended to ``keep``: the caller holds it until the GEMM is launched -- freed earlier, the
+    caching allocator hands the same 4 bytes to the OTHER operand's |max| and both read one value."""
+    if isinstance(given, tuple):
+        return given
     am = given if given is not None else amax_of(t)
-    assert am.dtype == torch.float32 and am.is_contiguous() and 1 <= am.numel() <= 8
-    return am.data_ptr(), am.numel()
+    assert am.dtype == torch.float32 and am.is_contiguous() and am.numel() % SLOT_FLOATS == 0
+    keep.append(am)
+    return am.data_ptr(), am.numel() // SLOT_FLOATS
 
 
 def set_fp32_mode(mode):
@@ -428,9 +465,10 @@ def _hip_gemm(a, b, ta, tb, out, bias=None, epi=EPI_NONE, beta=0.0, aux=None, pa
     mv, nv, kv = valid if valid is not None else (0, 0, 0)
     assert dims is not None or out.shape == (M, N)
     dt = _FP32_DT[fp32 or _FP32]
-    am = (0, 0, 0, 0)
+    am, keep = (0, 0, 0, 0), []
     if dt == 4:
-        am = _amax_ptr(a, amax[0] if amax is not None else None) + _amax_ptr(b, amax[1] if amax is not None else None)
+        am = _amax_ptr(a, amax[0] if amax is not None else None, keep) + _amax_ptr(
+            b, amax[1] if amax is not None else None, keep)
     slab = _slab(M, N, ksplit, a.device) if (dt or ksplit > 1) and epi <= EPI_BIAS and ksplit != 1 else None
     rc = hip().gemm(dt, int(ta), int(tb), M, N, K, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0),
                     out.data_ptr(), out.stride(0), bias.data_ptr() if bias is not None else 0, epi, float(beta),
@@ -438,7 +476,7 @@ def _hip_gemm(a, b, ta, tb, out, bias=None, epi=EPI_NONE, beta=0.0, aux=None, pa
                     part.data_ptr() if part is not None else 0, colsum.data_ptr() if colsum is not None else 0,
                     int(colsum_acc), stream_handle(), tile, ksplit,
                     slab.data_ptr() if slab is not None else 0, slab.numel() if slab is not None else 0, mv, nv, kv,
-                    am[0], am[1], am[2], am[3], amax_out.data_ptr() if amax_out is not None else 0)
+                    am[0], am[1], am[2], am[3], slot_ptr(amax_out))
     return rc == 0
 
 
@@ -699,10 +737,10 @@ def linear_fwd_partials(x, w, ksplit=None, amax=None):
             ks = ksplit if ksplit is not None else (c[3] if len(c) > 3 else 0)
             slab = _slab(M, N, ks, x.device)
             if slab is not None:
-                am = (0, 0, 0, 0)
+                am, keep = (0, 0, 0, 0), []
                 if _FP32 == "h3":
-                    am = _amax_ptr(x, amax[0] if amax is not None else None) + _amax_ptr(
-                        w, amax[1] if amax is not None else None)
+                    am = _amax_ptr(x, amax[0] if amax is not None else None, keep) + _amax_ptr(
+                        w, amax[1] if amax is not None else None, keep)
                 rc = hip().gemm(_FP32_DT[_FP32], 0, 1, M, N, K, x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0),
                                 0, N, 0, EPI_NONE, 0.0, 0, 0, 0, 0, 0, stream_handle(), -1, ks, slab.data_ptr(),
                                 slab.numel(), 0, 0, 0, am[0], am[1], am[2], am[3], 0)
@@ -812,7 +850,7 @@ def linear_gelu_fwd(x, w, b, planes_out=False, emit_planes=False, out=None, amax
     torch.mm(x, w.t(), out=pre)
     bert_ops.bias_gelu_fwd(pre, b, out=y)
     if amax_out is not None:
-        amax_of(y, out=amax_out)
+        amax_into(y, amax_out)
     return y, pre
 
 
@@ -866,7 +904,7 @@ def linear_dgrad_dgelu(dy, w, pre, b, db_acc=None, planes_out=False, amax=None, 
     df = torch.mm(dy, w)
     dpre, db = bert_ops.gelu_bwd_colsum(df, pre, b, db_acc=db_acc)
     if amax_out is not None:
-        amax_of(dpre, out=amax_out)
+        amax_into(dpre, amax_out)
     return dpre, db
 
 
@@ -913,16 +951,23 @@ class AmaxPool(object):
 
     def __init__(self, weights, n_act, device):
         self.nw = len(weights)
-        self.buf = torch.zeros(self.nw + n_act, dtype=torch.float32, device=device)
+        self.buf = torch.zeros((self.nw + n_act) * SLOT_FLOATS, dtype=torch.float32, device=device)
+        self.ptr = self.buf.data_ptr()
         if weights:
             base, tab, nblk = _seg_table(weights)
-            hip().amax_seg(base, tab.data_ptr(), nblk, self.buf.data_ptr(), stream_handle())
+            hip().amax_seg(base, tab.data_ptr(), nblk, self.ptr, stream_handle())
 
+    # slots are (pointer, count) tuples: plain ints, so the ~150 uses per step cost no tensor views
     def w(self, i):
-        return self.buf[i:i + 1]
+        return (self.ptr + 4 * SLOT_FLOATS * i, 1)
 
     def act(self, i, n=1):
-        return self.buf[self.nw + i:self.nw + i + n]
+        return (self.ptr + 4 * SLOT_FLOATS * (self.nw + i), n)
+
+    def value(self, slot):
+        """|max| held by a slot (diagnostics; host sync)."""
+        i = (slot[0] - self.ptr) // (4 * SLOT_FLOATS)
+        return amax_value(self.buf[i * SLOT_FLOATS:(i + slot[1]) * SLOT_FLOATS]).max().item()
 
 
 def h3_active(dtype=torch.float32):

@@ -82,11 +82,15 @@ def load_engine_choices(dtype_tag="fp32"):
     file.  Entries measured under another fp32 engine policy are skipped."""
     if os.environ.get("HETSEQ_GEMM_CHOICES", "") == "measure" or not torch.cuda.is_available():
         return False
-    path = os.environ.get("HETSEQ_GEMM_CHOICES_FILE") or os.path.join(CHOICE_DIR, "gfx950_%s.json" % dtype_tag)
-    if not os.path.exists(path):
-        return False
     from hetseq_amd.ops import gemm as G
 
+    path = os.environ.get("HETSEQ_GEMM_CHOICES_FILE")
+    if not path:  # per fp32 engine policy (gfx950_fp32_h3.json, ...), else the dtype's file
+        path = os.path.join(CHOICE_DIR, "gfx950_%s_%s.json" % (dtype_tag, G.fp32_mode()))
+        if dtype_tag != "fp32" or not os.path.exists(path):
+            path = os.path.join(CHOICE_DIR, "gfx950_%s.json" % dtype_tag)
+    if not os.path.exists(path):
+        return False
     return G.load_choices(path)
 
 

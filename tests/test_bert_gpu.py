@@ -154,6 +154,8 @@ def test_fp32_plane_engine_matches_reference(cuda, monkeypatch):
     from hetseq_amd.ops import gemm as G
     from hetseq_amd.runtime.flat import FlatParamStore
 
+    G.set_fp32_mode("x6")  # (the plane engine is the six-term split's)
+
     monkeypatch.setattr(G, "_PLANES", "all")
     model, cfg = _tiny(cuda)
     model.eval()
@@ -195,10 +197,11 @@ def _grad_report(model, ref):
     return worst, where
 
 
-@pytest.mark.parametrize("planes", ["off", "fwd", "all"])
-def test_bert_base_shape_matches_reference_1e4(cuda, monkeypatch, planes):
+@pytest.mark.parametrize("planes,engine", [("off", "x6"), ("fwd", "x6"), ("all", "x6"), ("off", "h3")])
+def test_bert_base_shape_matches_reference_1e4(cuda, monkeypatch, planes, engine):
     """BERT-base (H 768, L 12, 12 heads, S 128, B 8), dropout off: the fused fp32 path -- in-kernel
-    split engine, split-bf16 planes on the ring kernel for the forward only or for every product --
+    split engine (six split-bf16 products, x6, or three split-fp16 products with per-tensor scales,
+    h3), split-bf16 planes on the ring kernel for the forward only or for every product --
     against the fp32 torch-op oracle (the
     reference module graph, bert_modeling.py:819-888).  Loss to 1e-5 relative; every parameter's
     gradient within 1e-4 of the oracle's largest gradient entry of that parameter."""
@@ -206,6 +209,7 @@ def test_bert_base_shape_matches_reference_1e4(cuda, monkeypatch, planes):
     from hetseq_amd.ops import gemm as G
     from hetseq_amd.runtime.flat import FlatParamStore
 
+    G.set_fp32_mode(engine)  # (conftest restores the default after the test)
     monkeypatch.setattr(G, "_PLANES", planes)
     torch.manual_seed(0)
     cfg = BertConfig(vocab_size_or_config_json_file=30522)
@@ -228,19 +232,23 @@ def test_bert_base_shape_matches_reference_1e4(cuda, monkeypatch, planes):
     l1.backward()
     assert abs(l1.item() - l2.item()) <= 1e-5 * abs(l2.item()), (l1.item(), l2.item())
     worst, where = _grad_report(model, ref)
-    print("bert-base fused vs oracle (planes=%s): loss %.8g vs %.8g, worst grad rel %.3g at %s"
-          % (planes, l1.item(), l2.item(), worst, where))
+    print("bert-base fused vs oracle (engine=%s planes=%s): loss %.8g vs %.8g, worst grad rel %.3g at %s"
+          % (engine, planes, l1.item(), l2.item(), worst, where))
     assert worst <= 1e-4, (worst, where)
 
 
-def test_trajectory_200_updates_tracks_reference(cuda, monkeypatch):
+@pytest.mark.parametrize("engine", ["x6", "h3"])
+def test_trajectory_200_updates_tracks_reference(cuda, monkeypatch, engine):
     """200 Adam updates of a tiny BERT, fused (flat store, fused Adam) vs the torch-op oracle with
     the reference Adam math (optim.py:162-231), identical seeds and batches, dropout off: the two
-    loss curves stay within 1e-4 relative of each other at every update."""
+    loss curves stay within 1e-4 relative of each other at every update (both fp32 GEMM engines)."""
     from argparse import Namespace
 
+    from hetseq_amd.ops import gemm as G
     from hetseq_amd.optim.optimizers import AdamReference, _Adam
     from hetseq_amd.runtime.flat import FlatParamStore
+
+    G.set_fp32_mode(engine)
 
     model, cfg = _tiny(cuda, H=256, L=2, NH=4, V=1000)
     model.eval()
@@ -274,7 +282,7 @@ def test_trajectory_200_updates_tracks_reference(cuda, monkeypatch):
         rel = abs(l1.item() - l2.item()) / abs(l2.item())
         worst = max(worst, rel)
         assert rel <= 1e-4, (step, l1.item(), l2.item())
-    print("200-update trajectory: worst loss rel diff %.3g" % worst)
+    print("200-update trajectory (%s): worst loss rel diff %.3g" % (engine, worst))
 
 
 def test_lamb_hip_step_matches_cpu_math(cuda):

@@ -113,6 +113,29 @@ def test_bench_self_launches_two_ranks(tmp_path):
     assert out["value"] > 0
 
 
+def test_bench_hetero_device_map_from_rank_processes(tmp_path):
+    """``bench.py --hetero 1,2 --dist-backend gloo``: two launch groups (1 + 2 ranks, tcp:// rendezvous)
+    of real rank processes.  gloo keeps all three on GPU 0 (``ran_on``), but each rank computes and
+    reports the device the nccl path would use -- group offset + local index (reference
+    train.py:189-193, Q24 fix): ranks 0 / 1 / 2 -> devices 0 / 1 / 2, local ranks 0 / 0 / 1."""
+    import json
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--hetero", "1,2", "--dist-backend", "gloo",
+                        "--steps", "1", "--warmup", "1", "--layers", "1"], env=env, capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    out = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")][-1]
+    assert out["n_gpus"] == 3 and "hetero 1+2" in out["config"]["parallelism"]
+    dm = out["device_map"]
+    assert [d["rank"] for d in dm] == [0, 1, 2]
+    assert [d["group"] for d in dm] == [0, 1, 1]
+    assert [d["local_rank"] for d in dm] == [0, 0, 1]
+    assert [d["device_id"] for d in dm] == [0, 1, 2]
+    assert all(d["ran_on"] == 0 for d in dm)
+
+
 def _tied_worker(rank, port, q, sparse):
     try:
         import torch
