@@ -535,6 +535,12 @@ _AB = {
     "fo_ks4": lambda: _set_site_ks((2048, 768, 3072, False, True, 0, False), 4),
     "lnpo_on": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_LN_PARTIALS_WO", True),  # attention-output part
     "lnpo_off": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_LN_PARTIALS_WO", False),
+    # h3 GEMMs at three blocks per CU: all plain products / forward / data gradients / weight gradients
+    "occ3_on": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_h3_occ3(7),
+    "occ3_off": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_h3_occ3(0),
+    "occ3_f": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_h3_occ3(1),
+    "occ3_d": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_h3_occ3(2),
+    "occ3_w": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_h3_occ3(4),
     # --emulate-world: workgroups per emulated collective (RCCL channels) and the emulated bus bandwidth
     "emu_ch4": lambda: _set_emul_channels(4),
     "emu_ch8": lambda: _set_emul_channels(8),

@@ -78,6 +78,7 @@ void launch_xent_bwd(int, void*, const int64_t*, const float*, int, int, int64_t
                      hipStream_t);
 // gemm.hip
 int gemm_last_ksplit();
+void set_h3_occ3(int on);
 int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, int64_t lda, const void* B,
                 int64_t ldb, void* C, int64_t ldc, const float* bias, int epi, float beta, float* aux, int64_t ldaux,
                 float* part, float* colsum_out, int colsum_acc, int tile_override, hipStream_t st, int ksplit,
@@ -529,6 +530,8 @@ PYBIND11_MODULE(_hip, m) {
       throw std::runtime_error("hipStreamCreateWithPriority failed");
     return reinterpret_cast<i64>(s);
   });
+  m.def("set_h3_occ3", &set_h3_occ3, "h3 GEMM engine, plain / bias epilogues at three blocks per CU (168 VGPRs): "
+        "bit mask 1 forward, 2 data gradient, 4 weight gradient");
   m.def("gemm_last_ksplit", &gemm_last_ksplit,
         "K slices of the last split-bf16 GEMM launch (with C = 0 its partials stay in the slab)");
   m.def("gemm", [](int dt, int ta, int tb, int M, int N, int K, i64 A, i64 lda, i64 B, i64 ldb, i64 C, i64 ldc, i64 bias,

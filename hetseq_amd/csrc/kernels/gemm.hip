@@ -527,9 +527,11 @@ HS_DEVICE bfx8 x_frag_tr(const char* __restrict__ S, int rc, int p, int ks, int 
 // MFMAs of this one; 2 = two register sets, each tile's loads issued two tiles ahead.
 // TRL: mn-contiguous operands in the transposed-read layout (above) instead of the register
 // transpose into k-contiguous images.
+// OCC > 0: waves per SIMD the register allocation targets (4-wave blocks: 3 = three blocks per CU,
+// <= 168 VGPRs) instead of the default two blocks per CU
 template <bool TA, bool TB, int EPI, int NT, int ABL = 0, int WV = 4, int NBUF = 1, bool EDGE = false, int PF = 1,
-          bool TRL = false>
-__global__ void __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(NBUF == 2 ? 2 : WV / 2, NBUF == 2 ? 2 : WV / 2))) gemm_x6s_kernel(GemmArgs p) {
+          bool TRL = false, int OCC = 0>
+__global__ void __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OCC ? OCC : NBUF == 2 ? 2 : WV / 2, OCC ? OCC : NBUF == 2 ? 2 : WV / 2))) gemm_x6s_kernel(GemmArgs p) {
   constexpr int BM = 128, BN = 128, WC = WV / 2, TM = 2, TN = BN / WC / 32;
   static_assert(NBUF == 1 || WV == 8, "double-buffered images: 8-wave variant only");
   static_assert(!EDGE || (WV == 4 && EPI <= kEpiBias), "edge-masked launches: 4 waves, plain / bias epilogue");
@@ -819,6 +821,13 @@ static const int g_x6_tr_env = [] {
   return e && e[0] == '0' ? 0 : 1;
 }();
 static int g_x6_tr = 0;
+// h3 engine (NT 4) at three 4-wave blocks per CU (registers for 168 VGPRs; two planes need less LDS):
+// HETSEQ_H3_OCC3=1, tile_override bit 10 forces it
+static int g_h3_occ3_env = [] {  // bit mask of the product kinds (launch_occ3); HETSEQ_H3_OCC3=7: all
+  const char* e = std::getenv("HETSEQ_H3_OCC3");
+  return e ? std::atoi(e) & 7 : 0;
+}();
+static int g_h3_occ3 = 0;
 // 8-wave variant with double-buffered LDS images (106 KB: one block per CU, one barrier per K
 // tile) -- HETSEQ_X6_DBUF=1; default single buffer (53 KB, blocks of other kernels co-reside).
 static const int g_x6_dbuf = [] {
@@ -858,6 +867,24 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
   }
 }
 
+// the h3 engine's three-blocks-per-CU variant (plain / bias epilogues only: the GELU epilogues spill
+// 70-90 registers at 168)
+template <bool TA, bool TB, int EPI, int NT>
+bool launch_occ3(const GemmArgs& a, int blocks, hipStream_t st) {
+  if constexpr (NT == 4 && EPI <= kEpiBias) {
+    // g_h3_occ3 bit mask: 1 forward (x W^T), 2 data gradient (dY W), 4 weight gradient (dY^T X)
+    if (!(g_h3_occ3 & (TA ? 4 : TB ? 1 : 2))) return false;
+    if (g_x6_tr && (TA || !TB))
+      hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 0, 4, 1, false, 1, true, 3>), dim3(blocks), dim3(256), 0, st,
+                         a);
+    else
+      hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 0, 4, 1, false, 1, false, 3>), dim3(blocks), dim3(256), 0, st,
+                         a);
+    return true;
+  }
+  return false;
+}
+
 template <int BM, int BN, int MF, bool TA, bool TB, int EPI, int NT>
 void launch_cfg(const GemmArgs& a, hipStream_t st) {
   const int blocks = (a.M / BM) * (a.N / BN) * a.ksplit;
@@ -879,6 +906,8 @@ void launch_cfg(const GemmArgs& a, hipStream_t st) {
         hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 3, 4>), dim3(blocks), dim3(256), 0, st, a);
       else if (g_x6_pf == 2)
         hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 0, 4, 1, false, 2>), dim3(blocks), dim3(256), 0, st, a);
+      else if (launch_occ3<TA, TB, EPI, NT>(a, blocks, st))
+        ;
       else if (g_x6_tr && (TA || !TB))
         hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 0, 4, 1, false, 1, true>), dim3(blocks), dim3(256), 0, st,
                            a);
@@ -984,6 +1013,7 @@ static int pick_tile_split(int M, int N, int K, int* ksplit) {
 // Returns -1 when the request is not served (caller falls back to the library).
 static thread_local int g_last_ks = 1;
 int gemm_last_ksplit() { return g_last_ks; }
+void set_h3_occ3(int mask) { g_h3_occ3_env = mask & 7; }
 
 int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, int64_t lda, const void* B,
                 int64_t ldb, void* C, int64_t ldc, const float* bias, int epi, float beta, float* aux, int64_t ldaux,
@@ -1014,6 +1044,7 @@ int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, i
   g_x6_pf = tile_override >= 0 && (tile_override & 128) ? 2 : g_x6_pf_env;
   g_x6_tr = tile_override >= 0 && (tile_override & 256) ? 1 : tile_override >= 0 && (tile_override & 512) ? 0
                                                               : g_x6_tr_env;
+  g_h3_occ3 = tile_override >= 0 && (tile_override & 1024) ? 7 : g_h3_occ3_env;
   tile_override = tile_override >= 0 ? (tile_override & 3) : -1;
   if (tile_override >= 0) {  // benchmarking hook: force a tile shape (must divide the problem)
     const int bm = tile_override == 2 ? 64 : 128, bn = tile_override == 0 ? 128 : 64;

@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--pf", type=int, default=1, help="with --only: 4-wave register prefetch depth (1/2)")
     ap.add_argument("--tr", type=int, default=-1, help="with --only: 1 transposed-read layout, 0 register transpose")
     ap.add_argument("--ks", type=int, default=1, help="with --only: split-K slices")
+    ap.add_argument("--occ3", type=int, default=0, help="with --only: h3 kernel at three blocks per CU")
     a = ap.parse_args()
     if a.only:
         M, N, K, ta, tb, eng = a.only.split(",")
@@ -39,10 +40,12 @@ def main():
         A = torch.rand((K, M) if ta else (M, K), device="cuda") * 2 - 1
         B = torch.rand((N, K) if tb else (K, N), device="cuda") * 2 - 1
         C = torch.empty(M, N, device="cuda")
+        am = (G.amax_of(A), G.amax_of(B)) if eng == "h3" else None
         f = (lambda: torch.mm(A.t() if ta else A, B.t() if tb else B, out=C)) if eng == "blas" else \
             (lambda: G._hip_gemm(A, B, ta, tb, C, fp32=eng, ksplit=a.ks,
                                  tile=(a.ablate << 3) | (32 if a.waves == 4 else 64) | (128 if a.pf == 2 else 0)
-                                 | (256 if a.tr == 1 else 512 if a.tr == 0 else 0)))
+                                 | (256 if a.tr == 1 else 512 if a.tr == 0 else 0) | (1024 if a.occ3 else 0),
+                                 amax=am))
         t = timeit(f, a.reps)
         f()
         At, Bt = (A.t() if ta else A).double(), (B.t() if tb else B).double()
