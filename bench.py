@@ -541,6 +541,7 @@ _AB = {
     "occ3_f": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_h3_occ3(1),
     "occ3_d": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_h3_occ3(2),
     "occ3_w": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_h3_occ3(4),
+    "occ3_fw": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_h3_occ3(5),
     # --emulate-world: workgroups per emulated collective (RCCL channels) and the emulated bus bandwidth
     "emu_ch4": lambda: _set_emul_channels(4),
     "emu_ch8": lambda: _set_emul_channels(8),

@@ -823,9 +823,13 @@ static const int g_x6_tr_env = [] {
 static int g_x6_tr = 0;
 // h3 engine (NT 4) at three 4-wave blocks per CU (registers for 168 VGPRs; two planes need less LDS):
 // HETSEQ_H3_OCC3=1, tile_override bit 10 forces it
-static int g_h3_occ3_env = [] {  // bit mask of the product kinds (launch_occ3); HETSEQ_H3_OCC3=7: all
+// Bit mask of the product kinds (launch_occ3) that run at three blocks per CU.  Default 5 (forward and
+// weight gradient): measured in the BERT-base fp32 step (interleaved A/B, 8 rounds) 12.13 ms against
+// 12.35 with none; data gradients at 3 blocks lose (+0.5 ms: they share the CUs with the weight-gradient
+// stream and the LN backward).  profiles/r4_h3_gemm.md.
+static int g_h3_occ3_env = [] {
   const char* e = std::getenv("HETSEQ_H3_OCC3");
-  return e ? std::atoi(e) & 7 : 0;
+  return e ? std::atoi(e) & 7 : 5;
 }();
 static int g_h3_occ3 = 0;
 // 8-wave variant with double-buffered LDS images (106 KB: one block per CU, one barrier per K
