@@ -631,14 +631,24 @@ int launch_attn_bwd_x6(const float* qkv, const int64_t* mask, const float* bqkv,
                        const float* lse, float* Dbuf, float* dqkv, const uint32_t* dmask, int B, int S, int NH,
                        int D, float p, bool fused, hipStream_t st);
 
-// fp32 attention products: "x6" (split-bf16 on the bf16 matrix cores, attention_x6.hip) or
-// "native" (exact-fp32 MFMA) -- HETSEQ_ATTN_FP32, default x6
+int launch_attn_fwd_h3(const float* qkv, const int64_t* mask, const float* bqkv, float* ctx, float* lse,
+                       uint32_t* dmask, int B, int S, int NH, int D, float p, uint64_t seed, uint64_t off,
+                       hipStream_t st, int bh0);
+
+int launch_attn_bwd_h3(const float* qkv, const int64_t* mask, const float* bqkv, const float* ctx, const float* dctx,
+                       const float* lse, float* Dbuf, float* dqkv, const uint32_t* dmask, int B, int S, int NH, int D,
+                       float p, hipStream_t st);
+
+// fp32 attention products: 2 "h3" (three split-fp16 products with in-kernel power-of-two scales,
+// attention_h3.hip; default), 1 "x6" (six split-bf16 products, attention_x6.hip) or 0 "native"
+// (exact-fp32 MFMA) -- HETSEQ_ATTN_FP32
 static int g_attn_fp32_x6 = [] {
   const char* e = std::getenv("HETSEQ_ATTN_FP32");
-  return e && std::string(e) == "native" ? 0 : 1;
+  if (e && std::string(e) == "native") return 0;
+  return e && std::string(e) == "x6" ? 1 : 2;
 }();
 
-void set_attn_fp32_mode(int x6) { g_attn_fp32_x6 = x6; }
+void set_attn_fp32_mode(int mode) { g_attn_fp32_x6 = mode; }
 int attn_fp32_mode() { return g_attn_fp32_x6; }
 
 // HETSEQ_ATTN_BF16_MFMA=0 keeps bf16 attention on the fp32-MFMA kernels (A/B and tests)
@@ -664,6 +674,9 @@ int launch_attn_fwd(int dtype, const void* qkv, const int64_t* mask, const float
   dim3 grid(B * NH, (S + 127) / 128);  // head-major: a head's blocks share one XCD's L2
   if (dtype != 0 && bf16_mfma_enabled())  // bf16 matrix cores (attention_bf16.hip)
     return launch_attn_fwd_bf16(qkv, mask, bqkv, ctx, lse, dmask, B, S, NH, D, p, seed, off, st, bh0);
+  if (dtype == 0 && g_attn_fp32_x6 == 2)  // fp32 as split-fp16 products (attention_h3.hip)
+    return launch_attn_fwd_h3((const float*)qkv, mask, bqkv, (float*)ctx, lse, dmask, B, S, NH, D, p, seed, off, st,
+                              bh0);
   if (dtype == 0 && g_attn_fp32_x6)  // fp32 as split-bf16 products (attention_x6.hip)
     return launch_attn_fwd_x6((const float*)qkv, mask, bqkv, (float*)ctx, lse, dmask, B, S, NH, D, p, seed, off, st,
                               bh0);
@@ -680,6 +693,9 @@ int launch_attn_bwd(int dtype, const void* qkv, const int64_t* mask, const float
                     const void* dctx, const float* lse, float* Dbuf, void* dqkv, const uint32_t* dmask, int B, int S,
                     int NH, int D, float p, hipStream_t st) {
   if (D != kD || S % 32 != 0 || S <= 0 || (p > 0.f && dmask == nullptr)) return -1;
+  if (dtype == 0 && g_attn_fp32_x6 == 2)
+    return launch_attn_bwd_h3((const float*)qkv, mask, bqkv, (const float*)ctx, (const float*)dctx, lse, Dbuf,
+                              (float*)dqkv, dmask, B, S, NH, D, p, st);
   if (dtype == 0 && g_attn_fp32_x6)  // fp32 as split-bf16 products (attention_x6.hip)
     return launch_attn_bwd_x6((const float*)qkv, mask, bqkv, (const float*)ctx, (const float*)dctx, lse, Dbuf,
                               (float*)dqkv, dmask, B, S, NH, D, p, fused_bwd_enabled(), st);

@@ -22,6 +22,8 @@
 
 namespace hs {
 
+int launch_attn_bwd_dsum(const float* ctx, const float* dctx, float* Dout, int B, int S, int NH, hipStream_t st);
+
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -1941,6 +1943,14 @@ int launch_attn_bwd_x6(const float* qkv, const int64_t* mask, const float* bqkv,
                      p, dmask);
   hipLaunchKernelGGL(attn_bwd_dkv_x6_kernel, grid, dim3(256), 0, st, qkv, mask, bqkv, dctx, lse, Dbuf, dqkv, S, NH, p,
                      dmask);
+  return 0;
+}
+
+// D = rowsum(dO o O) per (batch, head, query) for the S > 128 backward of either fp32 engine
+int hs::launch_attn_bwd_dsum(const float* ctx, const float* dctx, float* Dout, int B, int S, int NH, hipStream_t st) {
+  const int64_t units = (int64_t)B * S * NH;
+  hipLaunchKernelGGL(attn_bwd_dsum_kernel, dim3((unsigned)((units + 15) / 16)), dim3(256), 0, st, ctx, dctx, Dout, B, S,
+                     NH);
   return 0;
 }
 

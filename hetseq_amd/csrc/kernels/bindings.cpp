@@ -61,7 +61,7 @@ int launch_pool_nsp_bwd(int, const float*, const void*, void*, int, int, int, co
                         const int64_t*, const float*, const float*, const float*, const float*, float*, float*,
                         float*, float*, float*, float*, float*, int, hipStream_t);
 // attention.hip
-void set_attn_fp32_mode(int x6);
+void set_attn_fp32_mode(int mode);
 void set_attn_bwd_x6_planes(int on);
 void set_attn_timing(uint64_t* buf);
 void set_attn_bwd_fused_d(int on);
@@ -464,7 +464,7 @@ PYBIND11_MODULE(_hip, m) {
   }, "per-segment |max| over a flat fp32 buffer: tab = [nblk][3] int64 (segment, first float4, end float4); out "
      "must be zeroed");
 
-  m.def("set_attn_fp32_mode", &set_attn_fp32_mode, "fp32 attention products: 1 split-bf16 (x6), 0 exact-fp32 MFMA");
+  m.def("set_attn_fp32_mode", &set_attn_fp32_mode, "fp32 attention products: 2 split-fp16 (h3), 1 split-bf16 (x6), 0 exact-fp32 MFMA");
   m.def("set_attn_bwd_x6_planes", &set_attn_bwd_x6_planes,
         "fp32 split-bf16 attention backward: 2 key-block kernel (S <= 128) / plane-image pair, 1 plane-image dQ / dKV "
         "pair, 0 fused / gather kernels, -1 the HETSEQ_ATTN_BWD_X6 default");

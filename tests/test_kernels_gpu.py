@@ -351,6 +351,64 @@ def test_attention_bwd_x6_fp32_level(cuda, B, S, NH, p, family, monkeypatch):
     assert e6 <= 2 * e32 + 1e-7, (e6, e32)
 
 
+@pytest.mark.parametrize("B,S,NH,p", [(2, 128, 12, 0.0), (2, 96, 2, 0.1), (1, 512, 2, 0.0), (2, 192, 2, 0.1),
+                                       (3, 64, 4, 0.1), (2, 256, 12, 0.0), (8, 512, 12, 0.1)])
+@pytest.mark.parametrize("data", ["uniform", "wide"])
+def test_attention_h3_matches_fp64(cuda, B, S, NH, p, data):
+    """fp32 attention on three split-fp16 products with in-kernel power-of-two scales (attention_h3.hip,
+    the default fp32 engine): forward and backward against the exact-fp32 MFMA kernels on the same
+    forward (same keep bits), and against fp64 autograd at the exact-fp32 kernels' error level.
+    'wide': V and dO token magnitudes spread over three decades inside every head (and 100x outlier
+    V rows), Q / K over one decade (scores stay O(10), as from LayerNorm'd inputs: a saturated softmax
+    only measures the score rounding of either engine), so the chunk scales, the accumulator
+    rescaling between chunks and the running dS exponent are exercised."""
+    from hetseq_amd.ops import bert_ops
+    from hetseq_amd.ops._C import hip
+
+    torch.manual_seed(70 + S + B)
+    H = NH * 64
+    qkv = torch.randn(B * S, 3 * H, device=cuda)
+    if data == "wide":
+        qkv[:, :2 * H] *= torch.pow(10.0, torch.empty(B * S, 1, device=cuda).uniform_(-0.5, 0.5))
+        qkv[:, 2 * H:] *= torch.pow(10.0, torch.empty(B * S, 1, device=cuda).uniform_(-1.5, 1.5))
+        qkv[::37, 2 * H:] *= 100.0
+    bias = torch.randn(3 * H, device=cuda) * 0.1
+    mask = torch.ones(B, S, dtype=torch.int64, device=cuda)
+    mask[-1, S // 3:] = 0
+    old = hip().attn_fp32_mode()
+    try:
+        hip().set_attn_fp32_mode(0)
+        out32, saved32 = bert_ops.attn_fwd(qkv, mask, B, S, NH, p, 3, 11, bias=bias)
+        hip().set_attn_fp32_mode(2)
+        out3, saved3 = bert_ops.attn_fwd(qkv, mask, B, S, NH, p, 3, 11, bias=bias)
+        dout = torch.randn_like(out32)
+        if data == "wide":
+            dout *= torch.pow(10.0, torch.empty(B * S, 1, device=cuda).uniform_(-1.5, 1.5))
+        g3 = bert_ops.attn_bwd(qkv, mask, out32, dout, saved32, B, S, NH, p, bias=bias)
+        hip().set_attn_fp32_mode(0)
+        g32 = bert_ops.attn_bwd(qkv, mask, out32, dout, saved32, B, S, NH, p, bias=bias)
+    finally:
+        hip().set_attn_fp32_mode(old)
+    torch.cuda.synchronize()
+    if p > 0:
+        assert torch.equal(saved3[1], saved32[1])
+    keep = _keep_mask(saved32[1], B * NH, S) if p > 0 else None
+    x = (qkv.double() + bias.double()).requires_grad_()
+    ref = _ref_attention_drop(x, mask, B, S, NH, keep, p)
+    ref.backward(dout.double())
+    # 22-bit operands against fp32's 24: where a few terms dominate a short contraction (the wide data,
+    # 128 queries) the representation error shows, up to 4x the exact-fp32 kernels'; on uniform data the
+    # accumulation rounding of both dominates (within 2x)
+    f = 2.0 if data == "uniform" else 4.0
+    e3 = float((out3.double() - ref.detach()).abs().max())
+    e32 = float((out32.double() - ref.detach()).abs().max())
+    assert e3 <= f * e32 + 1e-7, ("forward", e3, e32)
+    g3e = float((g3.double() - x.grad).abs().max())
+    g32e = float((g32.double() - x.grad).abs().max())
+    assert g3e <= f * g32e + 1e-7, ("backward", g3e, g32e)
+    assert torch.isfinite(g3).all()
+
+
 @pytest.mark.parametrize("n,bound", [(4096, 30522), (1, 5), (777, 2), (16384, 30522), (5000, 100000)])
 def test_sort_keys_matches_stable_sort(cuda, n, bound):
     """The one-block LDS key sort returns torch.sort(stable=True)'s keys and indices exactly."""

@@ -6,7 +6,7 @@
 Counters of several single-pass runs of the same program are joined by kernel name (each pass is
 its own run: rocprofv3 does not split counters over passes).  Per kernel: dispatches, mean
 duration, the mean of every counter per dispatch, and derived columns when their inputs exist:
-bf16 MFMA TF/s (512 FLOP per MOPS unit), MFMA busy % of the dispatch's SQ busy cycles, LDS
+bf16 / fp16 MFMA TF/s (512 FLOP per MOPS unit), MFMA busy % of the dispatch's SQ busy cycles, LDS
 bank-conflict % of LDS-active cycles, L2 hit %, wait % of wave cycles.
 """
 import argparse
@@ -57,6 +57,8 @@ def main():
         row = {"kernel": short(k), "n": ndisp[k], "us": d / 1000.0}
         if "SQ_INSTS_VALU_MFMA_MOPS_BF16" in cs:
             row["bf16 TF/s"] = cs["SQ_INSTS_VALU_MFMA_MOPS_BF16"] * 512 / d / 1000.0
+        if "SQ_INSTS_VALU_MFMA_MOPS_F16" in cs:
+            row["f16 TF/s"] = cs["SQ_INSTS_VALU_MFMA_MOPS_F16"] * 512 / d / 1000.0
         if "SQ_VALU_MFMA_BUSY_CYCLES" in cs and "SQ_BUSY_CYCLES" in cs and cs["SQ_BUSY_CYCLES"]:
             row["mfma busy/SQ busy %"] = 100.0 * cs["SQ_VALU_MFMA_BUSY_CYCLES"] / (cs["SQ_BUSY_CYCLES"] * 4 * 4)
         if "SQ_LDS_BANK_CONFLICT" in cs and cs.get("SQ_LDS_IDX_ACTIVE"):
