@@ -423,6 +423,18 @@ class Controller(object):
         self.model.all_reduce_(stats)
         return g2.run([stats])
 
+    def _end_failed_capture(self):
+        """A failed capture can leave streams that joined it (the side stream, through an event wait)
+        still capturing, and an error pending that the next launch reports: end those captures so
+        the eager fallback runs."""
+        handles = set(streams.engine_streams(self.device).values())
+        handles.add(torch.cuda.current_stream(self.device).cuda_stream)
+        for h in handles:
+            was, err = hip().end_capture(h)
+            if was or err:
+                print("| ended the failed capture of stream {:#x} (pending HIP error {})".format(h, err), flush=True)
+        torch.cuda.synchronize(self.device)
+
     def _train_step_graphed(self, sample):
         from hetseq_amd.runtime.graphs import GraphedStep
 
@@ -455,6 +467,7 @@ class Controller(object):
             # capture failed (nothing ran): undo the host half of the update and fall back to eager
             print("| WARNING: HIP graph capture failed ({}); continuing eagerly".format(str(e).splitlines()[0]),
                   flush=True)
+            self._end_failed_capture()
             self.optimizer.step_count -= 1
             self._graph = False
             return None

@@ -513,6 +513,21 @@ PYBIND11_MODULE(_hip, m) {
   // returns 0 when launched, -1 when the shape/epilogue is not served (caller falls back)
   m.def("set_seed_ptr", [](i64 ptr) { hs::g_seed_dev = reinterpret_cast<const uint64_t*>(ptr); });
   m.def("stream_wait", [](i64 waiter, i64 signal) { stream_wait(ST(waiter), ST(signal)); });
+  // After a failed (invalidated) capture: end the capture a stream may still be in -- a stream that
+  // joined the capture through an event wait can be left capturing when the origin's capture fails --
+  // and take the error it left pending.  Returns (1 if the stream was capturing, that error code).
+  m.def("end_capture", [](i64 st) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(ST(st), &cs) != hipSuccess) cs = hipStreamCaptureStatusNone;
+    int was = cs != hipStreamCaptureStatusNone;
+    if (was) {
+      hipGraph_t g = nullptr;
+      (void)hipStreamEndCapture(ST(st), &g);
+      if (g) (void)hipGraphDestroy(g);
+    }
+    const int pending = static_cast<int>(hipGetLastError());
+    return std::make_pair(was, pending);
+  }, "end a (failed) capture the stream is still in; returns (was capturing, the pending error it took)");
   m.def("set_stream_wait_flags", [](int mode) {
     // 0: DisableTiming; 1: + DisableSystemFence; 2: + ReleaseToDevice; 3: + both
     g_wait_flags = hipEventDisableTiming | (mode & 1 ? hipEventDisableSystemFence : 0u) |
