@@ -61,6 +61,9 @@ def parse():
     p.add_argument("--profile-phases", action="store_true")
     p.add_argument("--hip-graph", action="store_true", help="replay the captured update as one HIP graph (1 GPU, or data-parallel on the native RCCL engine)")
     p.add_argument("--sync-debug", action="store_true", help="warn (with stack) on every host<->device sync in the timed loop")
+    p.add_argument("--prefill-us", type=float, default=0.0,
+                   help=argparse.SUPPRESS)  # diagnostic: a spin kernel of this length right before the timed loop
+    # (gives the host a head start: if the step's device gaps are host-caused, they disappear)
     p.add_argument("--host-profile", default=None, help="cProfile the timed loop into this file")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="process-group backend for N > 1 (nccl = RCCL; gloo only to rehearse several ranks on one GPU)")
@@ -327,6 +330,12 @@ def run_rank(b):
     if b.ab:
         return _ab_run(b, ctl, gen)
     ms0 = torch.cuda.memory_stats()
+    if b.prefill_us > 0:
+        from hetseq_amd.ops._C import hip as _hip, stream_handle as _sh
+
+        _pf = torch.zeros(1 << 16, device="cuda")
+        _hip().comm_emulation(_pf.data_ptr(), _pf.numel() * 4, _pf.data_ptr(), _pf.numel() * 4, 0, 8,
+                              int(b.prefill_us * 1000), _sh())
     t0 = time.perf_counter()
     host = 0.0  # host time spent inside train_step (enqueue cost; < ms_per_step means GPU-bound)
     data_wait = 0.0  # host time blocked on the input pipeline
@@ -542,6 +551,9 @@ _AB = {
     "occ3_d": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_h3_occ3(2),
     "occ3_w": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_h3_occ3(4),
     "occ3_fw": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_h3_occ3(5),
+    # fp32 attention engine: h3 (split-fp16, default) / x6 (split-bf16)
+    "attn_h3": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_fp32_mode(2),
+    "attn_x6": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_fp32_mode(1),
     # --emulate-world: workgroups per emulated collective (RCCL channels) and the emulated bus bandwidth
     "emu_ch4": lambda: _set_emul_channels(4),
     "emu_ch8": lambda: _set_emul_channels(8),

@@ -467,6 +467,10 @@ class Controller(object):
             # capture failed (nothing ran): undo the host half of the update and fall back to eager
             print("| WARNING: HIP graph capture failed ({}); continuing eagerly".format(str(e).splitlines()[0]),
                   flush=True)
+            if os.environ.get("HETSEQ_CAPTURE_DEBUG") == "1":
+                import traceback
+
+                traceback.print_exc()
             self._end_failed_capture()
             self.optimizer.step_count -= 1
             self._graph = False

@@ -516,6 +516,11 @@ PYBIND11_MODULE(_hip, m) {
   // After a failed (invalidated) capture: end the capture a stream may still be in -- a stream that
   // joined the capture through an event wait can be left capturing when the origin's capture fails --
   // and take the error it left pending.  Returns (1 if the stream was capturing, that error code).
+  m.def("capture_status", [](i64 st) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    const hipError_t e = hipStreamIsCapturing(ST(st), &cs);
+    return e == hipSuccess ? static_cast<int>(cs) : -static_cast<int>(e);
+  }, "capture status of a stream: 0 none, 1 active, 2 invalidated (negative: the query's HIP error)");
   m.def("end_capture", [](i64 st) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(ST(st), &cs) != hipSuccess) cs = hipStreamCaptureStatusNone;

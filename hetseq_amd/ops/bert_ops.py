@@ -451,8 +451,7 @@ _FWD_KS = None
 def _fwd_split_ok(x, mask, W, cfg):
     B, S = cfg[0], cfg[1]
     return (_FWD_SPLIT and x.is_cuda and x.dtype == torch.float32 and not getattr(W, "planes", False)
-            and B % 2 == 0 and B * S >= 1024 and streams.enabled() and x.is_contiguous()
-            and not torch.cuda.is_current_stream_capturing())  # (graphs: one chain; the same dropout masks)
+            and B % 2 == 0 and B * S >= 1024 and streams.enabled() and x.is_contiguous())
 
 
 def _layer_forward_split(x, mask, W, cfg, save, am=None):

@@ -522,7 +522,10 @@ def _choose(key, run_hip, run_blas):
     if c is not None:
         return c[0]
     if torch.cuda.is_current_stream_capturing():
-        return "blas"
+        # a shape the eager warm-up never ran (e.g. the one-chain forward of a capture after split
+        # warm-up steps): nothing can be timed here, and a first library call would create its
+        # handle inside the capture (hipblasCreate fails there) -- the HIP engine, which serves it
+        return "hip"
     t_hip = _bench(run_hip)
     t_blas = _bench(run_blas)
     c = "hip" if _hip_wins(t_hip, t_blas) else "blas"
@@ -710,8 +713,6 @@ def _choose_padded(key, run_hip, run_blas):
         return "hip"
     if key in GEMM_CHOICES:
         return GEMM_CHOICES[key][0]
-    if torch.cuda.is_current_stream_capturing():
-        return "blas"
     return _choose(key, run_hip, run_blas)
 
 

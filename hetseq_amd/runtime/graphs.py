@@ -75,9 +75,68 @@ class GraphedStep(object):
             torch.cuda.synchronize()
             self.graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph, capture_error_mode=self.mode):
-                self.static_out = self.fn(self.static_in)
+                with _CaptureProbe():
+                    self.static_out = self.fn(self.static_in)
         else:
             for dst, src in zip(self.static_in, inputs):
                 dst.copy_(src, non_blocking=True)
         self.graph.replay()
         return tuple(t.clone() for t in self.static_out)
+
+
+class _CaptureProbe(object):
+    """HETSEQ_CAPTURE_DEBUG=1: report the first kernel-library call after which the capture stream's
+    capture is no longer active (the call that invalidated it), with its Python stack."""
+
+    def __enter__(self):
+        import os
+
+        self.on = os.environ.get("HETSEQ_CAPTURE_DEBUG") == "1"
+        if not self.on:
+            return self
+        import traceback
+
+        from hetseq_amd.ops._C import hip
+
+        self.mod = hip()
+        self.origin = torch.cuda.current_stream().cuda_stream
+        self.saved = {}
+        state = {"reported": False, "last": None}
+        status = self.mod.capture_status
+        origin = self.origin
+
+        def report(what, name):
+            if not state["reported"]:
+                state["reported"] = True
+                print("| capture probe: %s %s (previous call %s)\n%s"
+                      % (what, name, state["last"], "".join(traceback.format_stack(limit=14))), flush=True)
+
+        def wrap(name, fn):
+            def probe(*a, **k):
+                st = status(origin)
+                if st != 1:
+                    report("capture status %d before" % st, name)
+                try:
+                    out = fn(*a, **k)
+                except Exception as e:
+                    report("exception %r in" % (str(e).splitlines()[0],), name)
+                    raise
+                st = status(origin)
+                if st != 1:
+                    report("capture status %d after" % st, name)
+                state["last"] = name
+                return out
+            return probe
+
+        for name in dir(self.mod):
+            fn = getattr(self.mod, name)
+            if callable(fn) and not name.startswith("_") and name not in ("capture_status", "end_capture"):
+                self.saved[name] = fn
+                setattr(self.mod, name, wrap(name, fn))
+        return self
+
+    def __exit__(self, *exc):
+        if self.on:
+            for name, fn in self.saved.items():
+                setattr(self.mod, name, fn)
+        return False
