@@ -61,6 +61,8 @@ def parse():
     p.add_argument("--profile-phases", action="store_true")
     p.add_argument("--hip-graph", action="store_true", help="replay the captured update as one HIP graph (1 GPU, or data-parallel on the native RCCL engine)")
     p.add_argument("--sync-debug", action="store_true", help="warn (with stack) on every host<->device sync in the timed loop")
+    p.add_argument("--host-phases", action="store_true",
+                   help="host time per step of each train_step phase (forward, backward, norm, step, ...)")
     p.add_argument("--prefill-us", type=float, default=0.0,
                    help=argparse.SUPPRESS)  # diagnostic: a spin kernel of this length right before the timed loop
     # (gives the host a head start: if the step's device gaps are host-caused, they disappear)
@@ -329,6 +331,7 @@ def run_rank(b):
         prof.enable()
     if b.ab:
         return _ab_run(b, ctl, gen)
+    phases = _host_phases(ctl) if b.host_phases else None
     ms0 = torch.cuda.memory_stats()
     if b.prefill_us > 0:
         from hetseq_amd.ops._C import hip as _hip, stream_handle as _sh
@@ -412,6 +415,8 @@ def run_rank(b):
             "host_ms_per_step": round(host / b.steps * 1000, 3),
             "data_wait_ms_per_step": round(data_wait / b.steps * 1000, 3),
             "allocator_events": alloc_events,
+            "host_phases_ms": ({k: [round(v[0] / b.steps * 1000, 3), round(v[1] * 1000, 3)] for k, v in phases.items()}
+                               if phases is not None else None),  # [mean per step, max]
             "gemm_choices": {str(k): v for k, v in list(G.GEMM_CHOICES.items())[:32]},
             "fp32_gemm": G.fp32_mode(),
             "device_map": device_map,
@@ -554,6 +559,8 @@ _AB = {
     # fp32 attention engine: h3 (split-fp16, default) / x6 (split-bf16)
     "attn_h3": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_fp32_mode(2),
     "attn_x6": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_fp32_mode(1),
+    "h3_dma_on": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_h3_dma(1),
+    "h3_dma_off": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_h3_dma(0),
     # --emulate-world: workgroups per emulated collective (RCCL channels) and the emulated bus bandwidth
     "emu_ch4": lambda: _set_emul_channels(4),
     "emu_ch8": lambda: _set_emul_channels(8),
@@ -564,6 +571,34 @@ _AB = {
     "emu_bw400": lambda: _set_emul_busbw(400.0),
     "emu_bw600": lambda: _set_emul_busbw(600.0),
 }
+
+
+def _host_phases(ctl):
+    """Wrap the phases of train_step with host timers (diagnostic, --host-phases): where the host
+    spends -- or waits out -- its time per step."""
+    acc = {}
+
+    def timed(obj, name, label):
+        fn = getattr(obj, name)
+
+        def wrapper(*a, **k):
+            t = time.perf_counter()
+            try:
+                return fn(*a, **k)
+            finally:
+                d = time.perf_counter() - t
+                s_, m_ = acc.get(label, (0.0, 0.0))
+                acc[label] = (s_ + d, max(m_, d))
+        setattr(obj, name, wrapper)
+
+    timed(ctl.model, "forward", "forward")
+    timed(ctl.optimizer, "backward", "backward")
+    timed(ctl.optimizer, "clip_grad_norm", "grad_norm")
+    timed(ctl.optimizer, "step", "optimizer_step")
+    timed(ctl, "zero_grad", "zero_grad")
+    timed(ctl, "_prepare_sample", "prepare_sample")
+    timed(ctl, "_set_seed", "set_seed")
+    return acc
 
 
 def _ab_run(b, ctl, gen):

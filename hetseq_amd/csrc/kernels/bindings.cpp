@@ -66,6 +66,7 @@ void set_attn_bwd_x6_planes(int on);
 void set_attn_timing(uint64_t* buf);
 void set_attn_bwd_fused_d(int on);
 void set_attn_fwd_x6_planes(int on);
+void set_attn_h3_dma(int on);
 void set_ln_bwd_lds(int chunked);
 int attn_fp32_mode();
 int launch_attn_fwd(int, const void*, const int64_t*, const float*, void*, float*, uint32_t*, int, int, int, int, float,
@@ -473,6 +474,7 @@ PYBIND11_MODULE(_hip, m) {
         "fp32 plane-pair attention backward: 1 = D = rowsum(dO o O) inside the kernel (S <= 128), 0 = separate pass");
   m.def("set_ln_bwd_lds", &set_ln_bwd_lds,
         "LN backward column partials: 1 = through a 3 KB LDS window (default), 0 = the [waves][H] LDS image");
+  m.def("set_attn_h3_dma", &set_attn_h3_dma, "h3 attention backward, S > 128: 1 next-chunk rows by LDS-DMA, 0 loads");
   m.def("set_attn_fwd_x6_planes", &set_attn_fwd_x6_planes,
         "fp32 attention forward: 1 = plane-image kernel (default), 0 = the first x6 forward");
   m.def("set_attn_timing", [](i64 buf) { set_attn_timing(P(uint64_t*, buf)); },

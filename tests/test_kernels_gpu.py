@@ -409,6 +409,36 @@ def test_attention_h3_matches_fp64(cuda, B, S, NH, p, data):
     assert torch.isfinite(g3).all()
 
 
+@pytest.mark.parametrize("S,p", [(256, 0.1), (512, 0.0), (384, 0.1)])
+def test_attention_h3_dma_matches_loads(cuda, S, p):
+    """S > 128 h3 backward: the next-chunk rows by LDS-DMA (default) give bitwise the gradients of the
+    plain per-chunk loads (same values staged, same order of every sum)."""
+    from hetseq_amd.ops import bert_ops
+    from hetseq_amd.ops._C import hip
+
+    torch.manual_seed(90 + S)
+    B, NH = 2, 12
+    H = NH * 64
+    qkv = torch.randn(B * S, 3 * H, device=cuda)
+    bias = torch.randn(3 * H, device=cuda) * 0.1
+    mask = torch.ones(B, S, dtype=torch.int64, device=cuda)
+    mask[-1, S // 3:] = 0
+    old = hip().attn_fp32_mode()
+    try:
+        hip().set_attn_fp32_mode(2)
+        out, saved = bert_ops.attn_fwd(qkv, mask, B, S, NH, p, 3, 11, bias=bias)
+        dout = torch.randn_like(out)
+        hip().set_attn_h3_dma(1)
+        g_dma = bert_ops.attn_bwd(qkv, mask, out, dout, saved, B, S, NH, p, bias=bias)
+        hip().set_attn_h3_dma(0)
+        g_ld = bert_ops.attn_bwd(qkv, mask, out, dout, saved, B, S, NH, p, bias=bias)
+    finally:
+        hip().set_attn_h3_dma(1)
+        hip().set_attn_fp32_mode(old)
+    torch.cuda.synchronize()
+    assert torch.equal(g_dma, g_ld)
+
+
 @pytest.mark.parametrize("n,bound", [(4096, 30522), (1, 5), (777, 2), (16384, 30522), (5000, 100000)])
 def test_sort_keys_matches_stable_sort(cuda, n, bound):
     """The one-block LDS key sort returns torch.sort(stable=True)'s keys and indices exactly."""

@@ -57,6 +57,15 @@ def main():
             tf = timeit(lambda: bert_ops.attn_fwd(qkv, mask, B, S, NH, 0.1, 1, 2, bias=bias), a.reps)
             tb = timeit(lambda: bert_ops.attn_bwd(qkv, mask, out, dout, saved, B, S, NH, 0.1, bias=bias), a.reps)
             row.append("%s fwd %.1f us bwd %.1f us" % (name, tf, tb))
+        if S > 128:  # h3 backward staging: LDS-DMA prefetch vs per-chunk loads
+            hip().set_attn_fp32_mode(2)
+            out, saved = bert_ops.attn_fwd(qkv, mask, B, S, NH, 0.1, 1, 2, bias=bias)
+            dout = torch.randn_like(out)
+            for name, on in (("dma", 1), ("loads", 0)):
+                hip().set_attn_h3_dma(on)
+                tb = timeit(lambda: bert_ops.attn_bwd(qkv, mask, out, dout, saved, B, S, NH, 0.1, bias=bias), a.reps)
+                row.append("h3 bwd[%s] %.1f us" % (name, tb))
+            hip().set_attn_h3_dma(1)
         hip().set_attn_fp32_mode(1)
         out, saved = bert_ops.attn_fwd(qkv, mask, B, S, NH, 0.1, 1, 2, bias=bias)
         dout = torch.randn_like(out)
