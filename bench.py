@@ -63,6 +63,8 @@ def parse():
     p.add_argument("--sync-debug", action="store_true", help="warn (with stack) on every host<->device sync in the timed loop")
     p.add_argument("--host-phases", action="store_true",
                    help="host time per step of each train_step phase (forward, backward, norm, step, ...)")
+    p.add_argument("--host-delay-us", type=float, default=0.0,
+                   help=argparse.SUPPRESS)  # diagnostic: host sleep before every timed step (the host's slack)
     p.add_argument("--prefill-us", type=float, default=0.0,
                    help=argparse.SUPPRESS)  # diagnostic: a spin kernel of this length right before the timed loop
     # (gives the host a head start: if the step's device gaps are host-caused, they disappear)
@@ -345,6 +347,8 @@ def run_rank(b):
     for _ in range(b.steps):
         d0 = time.perf_counter()
         batch = next(gen)
+        if b.host_delay_us > 0:
+            time.sleep(b.host_delay_us * 1e-6)
         h0 = time.perf_counter()
         data_wait += h0 - d0
         ctl.train_step(batch)

@@ -761,11 +761,14 @@ int launch_attn_fwd_h3(const float* qkv, const int64_t* mask, const float* bqkv,
   return 0;
 }
 
-// S > 128 backward: next-chunk rows by LDS-DMA (default) or loaded at each chunk's start
-// (HETSEQ_ATTN_H3_DMA=0; set_attn_h3_dma)
+// S > 128 backward: the chunk's rows loaded at its start (default) or prefetched by LDS-DMA under the
+// previous chunk (HETSEQ_ATTN_H3_DMA=1; set_attn_h3_dma).  The DMA variant measured no faster -- seq 512
+// backward 140.1 vs 134.7 us alone, phase-2 step 13.67 vs 13.63 ms (interleaved A/B): its extra barrier
+// per chunk costs what the hidden load latency saves (the kernel is bound by its exp / split VALU and
+// MFMA issue, not by the staging loads).
 static int g_bwd_dma = [] {
   const char* e = std::getenv("HETSEQ_ATTN_H3_DMA");
-  return e && e[0] == '0' ? 0 : 1;
+  return e && e[0] == '1' ? 1 : 0;
 }();
 void set_attn_h3_dma(int on) { g_bwd_dma = on; }
 

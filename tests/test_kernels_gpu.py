@@ -411,7 +411,7 @@ def test_attention_h3_matches_fp64(cuda, B, S, NH, p, data):
 
 @pytest.mark.parametrize("S,p", [(256, 0.1), (512, 0.0), (384, 0.1)])
 def test_attention_h3_dma_matches_loads(cuda, S, p):
-    """S > 128 h3 backward: the next-chunk rows by LDS-DMA (default) give bitwise the gradients of the
+    """S > 128 h3 backward: the next-chunk rows by LDS-DMA (opt-in) give bitwise the gradients of the
     plain per-chunk loads (same values staged, same order of every sum)."""
     from hetseq_amd.ops import bert_ops
     from hetseq_amd.ops._C import hip
@@ -433,7 +433,7 @@ def test_attention_h3_dma_matches_loads(cuda, S, p):
         hip().set_attn_h3_dma(0)
         g_ld = bert_ops.attn_bwd(qkv, mask, out, dout, saved, B, S, NH, p, bias=bias)
     finally:
-        hip().set_attn_h3_dma(1)
+        hip().set_attn_h3_dma(0)
         hip().set_attn_fp32_mode(old)
     torch.cuda.synchronize()
     assert torch.equal(g_dma, g_ld)
