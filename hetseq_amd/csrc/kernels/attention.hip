@@ -633,11 +633,11 @@ int launch_attn_bwd_x6(const float* qkv, const int64_t* mask, const float* bqkv,
 
 int launch_attn_fwd_h3(const float* qkv, const int64_t* mask, const float* bqkv, float* ctx, float* lse,
                        uint32_t* dmask, int B, int S, int NH, int D, float p, uint64_t seed, uint64_t off,
-                       hipStream_t st, int bh0);
+                       hipStream_t st, int bh0, float* amax);
 
 int launch_attn_bwd_h3(const float* qkv, const int64_t* mask, const float* bqkv, const float* ctx, const float* dctx,
                        const float* lse, float* Dbuf, float* dqkv, const uint32_t* dmask, int B, int S, int NH, int D,
-                       float p, hipStream_t st);
+                       float p, hipStream_t st, float* amax);
 
 // fp32 attention products: 2 "h3" (three split-fp16 products with in-kernel power-of-two scales,
 // attention_h3.hip; default), 1 "x6" (six split-bf16 products, attention_x6.hip) or 0 "native"
@@ -667,16 +667,22 @@ static bool fused_bwd_enabled() {
 // and read by both backward kernels (required when p > 0).
 // bh0: index of the launch's first (batch, head) in the whole batch -- the dropout keep bits of a
 // batch slice are the ones the whole-batch launch would draw for those heads.
+// amax (optional): |max| slot of the output; *amax_done = 1 when the kernel wrote it (the h3 engine),
+// else the caller runs a |max| pass
 int launch_attn_fwd(int dtype, const void* qkv, const int64_t* mask, const float* bqkv, void* ctx, float* lse,
                     uint32_t* dmask, int B, int S, int NH, int D, float p, uint64_t seed, uint64_t off,
-                    hipStream_t st, int bh0) {
+                    hipStream_t st, int bh0, float* amax, int* amax_done) {
+  if (amax_done) *amax_done = 0;
   if (D != kD || S % 32 != 0 || S <= 0 || bh0 < 0) return -1;
   dim3 grid(B * NH, (S + 127) / 128);  // head-major: a head's blocks share one XCD's L2
   if (dtype != 0 && bf16_mfma_enabled())  // bf16 matrix cores (attention_bf16.hip)
     return launch_attn_fwd_bf16(qkv, mask, bqkv, ctx, lse, dmask, B, S, NH, D, p, seed, off, st, bh0);
-  if (dtype == 0 && g_attn_fp32_x6 == 2)  // fp32 as split-fp16 products (attention_h3.hip)
-    return launch_attn_fwd_h3((const float*)qkv, mask, bqkv, (float*)ctx, lse, dmask, B, S, NH, D, p, seed, off, st,
-                              bh0);
+  if (dtype == 0 && g_attn_fp32_x6 == 2) {  // fp32 as split-fp16 products (attention_h3.hip)
+    const int rc = launch_attn_fwd_h3((const float*)qkv, mask, bqkv, (float*)ctx, lse, dmask, B, S, NH, D, p, seed, off,
+                                      st, bh0, amax);
+    if (rc == 0 && amax_done) *amax_done = amax != nullptr;
+    return rc;
+  }
   if (dtype == 0 && g_attn_fp32_x6)  // fp32 as split-bf16 products (attention_x6.hip)
     return launch_attn_fwd_x6((const float*)qkv, mask, bqkv, (float*)ctx, lse, dmask, B, S, NH, D, p, seed, off, st,
                               bh0);
@@ -691,11 +697,15 @@ int launch_attn_fwd(int dtype, const void* qkv, const int64_t* mask, const float
 
 int launch_attn_bwd(int dtype, const void* qkv, const int64_t* mask, const float* bqkv, const void* ctx,
                     const void* dctx, const float* lse, float* Dbuf, void* dqkv, const uint32_t* dmask, int B, int S,
-                    int NH, int D, float p, hipStream_t st) {
+                    int NH, int D, float p, hipStream_t st, float* amax, int* amax_done) {
+  if (amax_done) *amax_done = 0;
   if (D != kD || S % 32 != 0 || S <= 0 || (p > 0.f && dmask == nullptr)) return -1;
-  if (dtype == 0 && g_attn_fp32_x6 == 2)
-    return launch_attn_bwd_h3((const float*)qkv, mask, bqkv, (const float*)ctx, (const float*)dctx, lse, Dbuf,
-                              (float*)dqkv, dmask, B, S, NH, D, p, st);
+  if (dtype == 0 && g_attn_fp32_x6 == 2) {
+    const int rc = launch_attn_bwd_h3((const float*)qkv, mask, bqkv, (const float*)ctx, (const float*)dctx, lse, Dbuf,
+                                      (float*)dqkv, dmask, B, S, NH, D, p, st, amax);
+    if (rc == 0 && amax_done) *amax_done = amax != nullptr;
+    return rc;
+  }
   if (dtype == 0 && g_attn_fp32_x6)  // fp32 as split-bf16 products (attention_x6.hip)
     return launch_attn_bwd_x6((const float*)qkv, mask, bqkv, (const float*)ctx, (const float*)dctx, lse, Dbuf,
                               (float*)dqkv, dmask, B, S, NH, D, p, fused_bwd_enabled(), st);

@@ -149,15 +149,18 @@ HS_DEVICE void ptr2(const char* img, int q0, const TrBase& t, int dh, hx8 (&f)[2
   f[1] = ptr(img + kPl + q0 * kRowB, t, dh);
 }
 
-// 16 accumulator registers of two 32x32 C tiles (rows d, lane column) -> 64 fp32 of a token row
-HS_DEVICE void store_rows(float* out, const f32x16& c0, const f32x16& c1, int hf, float scale) {
+// 16 accumulator registers of two 32x32 C tiles (rows d, lane column) -> 64 fp32 of a token row; the
+// |max| of the written values folds into cm (the h3 GEMMs' operand scale, written by the producer)
+HS_DEVICE void store_rows(float* out, const f32x16& c0, const f32x16& c1, int hf, float scale, uint32_t& cm) {
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     const int d = 8 * g + 4 * hf;
-    *reinterpret_cast<float4*>(out + d) =
-        make_float4(c0[4 * g] * scale, c0[4 * g + 1] * scale, c0[4 * g + 2] * scale, c0[4 * g + 3] * scale);
-    *reinterpret_cast<float4*>(out + 32 + d) =
-        make_float4(c1[4 * g] * scale, c1[4 * g + 1] * scale, c1[4 * g + 2] * scale, c1[4 * g + 3] * scale);
+    const float4 a = make_float4(c0[4 * g] * scale, c0[4 * g + 1] * scale, c0[4 * g + 2] * scale, c0[4 * g + 3] * scale);
+    const float4 b = make_float4(c1[4 * g] * scale, c1[4 * g + 1] * scale, c1[4 * g + 2] * scale, c1[4 * g + 3] * scale);
+    cm = amax_bits(amax_bits(amax_bits(amax_bits(cm, a.x), a.y), a.z), a.w);
+    cm = amax_bits(amax_bits(amax_bits(amax_bits(cm, b.x), b.y), b.z), b.w);
+    *reinterpret_cast<float4*>(out + d) = a;
+    *reinterpret_cast<float4*>(out + 32 + d) = b;
   }
 }
 
@@ -322,7 +325,7 @@ HS_DEVICE void dkv_body(char* __restrict__ smem, int bx, int bh, const float* __
                         const int64_t* __restrict__ mask, const float* __restrict__ bqkv,
                         const float* __restrict__ dctx, const float* __restrict__ lse, const float* __restrict__ Dd,
                         float* __restrict__ dqkv, int S, int NH, float p, const uint32_t* __restrict__ dmask,
-                        const float* __restrict__ ctx) {
+                        const float* __restrict__ ctx, float* __restrict__ amax) {
   char* const Qp = smem;
   char* const Op = smem + kIm;
   float* const Ls = reinterpret_cast<float*>(smem + 2 * kIm);
@@ -480,8 +483,10 @@ HS_DEVICE void dkv_body(char* __restrict__ smem, int bx, int bh, const float* __
   }
   if (!active) return;
   float* out = dqkv + ((int64_t)b * S + key) * ld + h * kHD;
-  store_rows(out + H, dk0, dk1, hf, ldexpf(1.f, -(eq_run + es)));
-  store_rows(out + 2 * H, dv0, dv1, hf, ldexpf(1.f, -(eo_run + ep)));
+  uint32_t cm = 0u;
+  store_rows(out + H, dk0, dk1, hf, ldexpf(1.f, -(eq_run + es)), cm);
+  store_rows(out + 2 * H, dv0, dv1, hf, ldexpf(1.f, -(eo_run + ep)), cm);
+  if (amax) amax_commit(amax, cm);
 }
 
 // dQ for 32 queries per wave (lane = query) over 64-key chunks of K / V (biased); D from Dd or, with ctx
@@ -491,7 +496,7 @@ HS_DEVICE void dq_body(char* __restrict__ smem, int bx, int bh, const float* __r
                        const int64_t* __restrict__ mask, const float* __restrict__ bqkv,
                        const float* __restrict__ dctx, const float* __restrict__ lse, const float* __restrict__ Dd,
                        float* __restrict__ dqkv, int S, int NH, float p, const uint32_t* __restrict__ dmask,
-                       const float* __restrict__ ctx) {
+                       const float* __restrict__ ctx, float* __restrict__ amax) {
   char* const Kp = smem;
   char* const Vp = smem + kIm;
   float* const Ms = reinterpret_cast<float*>(smem + 2 * kIm);
@@ -598,7 +603,9 @@ HS_DEVICE void dq_body(char* __restrict__ smem, int bx, int bh, const float* __r
     }
   }
   if (!active) return;
-  store_rows(dqkv + tok * ld + h * kHD, dq0, dq1, hf, 0.125f * ldexpf(1.f, -(ek_run + es)));
+  uint32_t cm = 0u;
+  store_rows(dqkv + tok * ld + h * kHD, dq0, dq1, hf, 0.125f * ldexpf(1.f, -(ek_run + es)), cm);
+  if (amax) amax_commit(amax, cm);
 }
 
 }  // namespace
@@ -613,13 +620,13 @@ __global__ void __launch_bounds__(256, 2)
     attn_bwd_h3_kernel(const float* __restrict__ qkv, const int64_t* __restrict__ mask,
                        const float* __restrict__ bqkv, const float* __restrict__ dctx, const float* __restrict__ lse,
                        const float* __restrict__ Dd, float* __restrict__ dqkv, int S, int NH, float p,
-                       const uint32_t* __restrict__ dmask, const float* __restrict__ ctx) {
+                       const uint32_t* __restrict__ dmask, const float* __restrict__ ctx, float* __restrict__ amax) {
   __shared__ __attribute__((aligned(16))) char smem[DMA ? kBwdLdsDma : kBwdLds];
   const int nq = (S + 127) / 128, bh = blockIdx.x, y = blockIdx.y;
   if (y < nq)
-    dkv_body<DMA>(smem, y, bh, qkv, mask, bqkv, dctx, lse, Dd, dqkv, S, NH, p, dmask, DMA ? nullptr : ctx);
+    dkv_body<DMA>(smem, y, bh, qkv, mask, bqkv, dctx, lse, Dd, dqkv, S, NH, p, dmask, DMA ? nullptr : ctx, amax);
   else
-    dq_body<DMA>(smem, y - nq, bh, qkv, mask, bqkv, dctx, lse, Dd, dqkv, S, NH, p, dmask, DMA ? nullptr : ctx);
+    dq_body<DMA>(smem, y - nq, bh, qkv, mask, bqkv, dctx, lse, Dd, dqkv, S, NH, p, dmask, DMA ? nullptr : ctx, amax);
 }
 
 // Forward: a wave owns 32 queries (lane = query), S^T tiles with the key on the registers, online softmax;
@@ -628,7 +635,7 @@ __global__ void __launch_bounds__(256, 2)
     attn_fwd_h3_kernel(const float* __restrict__ qkv, const int64_t* __restrict__ mask,
                        const float* __restrict__ bqkv, float* __restrict__ ctx, float* __restrict__ lse,
                        uint32_t* __restrict__ dmask, int S, int NH, float p, uint64_t seed, uint64_t off,
-                       const uint64_t* __restrict__ seed_dev, int bh0) {
+                       const uint64_t* __restrict__ seed_dev, int bh0, float* __restrict__ amax) {
   seed = resolve_seed(seed, seed_dev);
   __shared__ __attribute__((aligned(16))) char smem[2 * kIm];
   __shared__ float Ms[64];
@@ -734,15 +741,9 @@ __global__ void __launch_bounds__(256, 2)
   }
   if (!active) return;
   const float inv = ldexpf(1.f, -(ev_run + ep)) / l;
-  float* out = ctx + ((int64_t)b * S + q0 + li) * H + h * kHD;
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const int d = 8 * g + 4 * hf;
-    *reinterpret_cast<float4*>(out + d) = make_float4(o0[4 * g] * inv, o0[4 * g + 1] * inv, o0[4 * g + 2] * inv,
-                                                      o0[4 * g + 3] * inv);
-    *reinterpret_cast<float4*>(out + 32 + d) = make_float4(o1[4 * g] * inv, o1[4 * g + 1] * inv,
-                                                           o1[4 * g + 2] * inv, o1[4 * g + 3] * inv);
-  }
+  uint32_t cm = 0u;
+  store_rows(ctx + ((int64_t)b * S + q0 + li) * H + h * kHD, o0, o1, hf, inv, cm);
+  if (amax) amax_commit(amax, cm);  // ctx's |max|: the output projection's operand scale
   if (hf == 0) lse[(int64_t)bh * S + q0 + li] = m + __logf(l);
 }
 
@@ -750,14 +751,15 @@ __global__ void __launch_bounds__(256, 2)
 
 using namespace hs;
 
+// amax (optional): a |max| slot (common.h) the kernels max |output| into (ctx forward, dqkv backward)
 int launch_attn_fwd_h3(const float* qkv, const int64_t* mask, const float* bqkv, float* ctx, float* lse,
                        uint32_t* dmask, int B, int S, int NH, int D, float p, uint64_t seed, uint64_t off,
-                       hipStream_t st, int bh0) {
+                       hipStream_t st, int bh0, float* amax) {
   if (D != kHD || S % 32 != 0 || S <= 0) return -1;
   // grid (B*NH, S/128): consecutive blocks are different heads, so every query block of a head lands on
   // the same XCD and its K / V come through one L2
   hipLaunchKernelGGL(attn_fwd_h3_kernel, dim3(B * NH, (S + 127) / 128), dim3(256), 0, st, qkv, mask, bqkv, ctx, lse,
-                     dmask, S, NH, p, seed, off, g_seed_dev, bh0);
+                     dmask, S, NH, p, seed, off, g_seed_dev, bh0, amax);
   return 0;
 }
 
@@ -774,7 +776,7 @@ void set_attn_h3_dma(int on) { g_bwd_dma = on; }
 
 int launch_attn_bwd_h3(const float* qkv, const int64_t* mask, const float* bqkv, const float* ctx, const float* dctx,
                        const float* lse, float* Dbuf, float* dqkv, const uint32_t* dmask, int B, int S, int NH, int D,
-                       float p, hipStream_t st) {
+                       float p, hipStream_t st, float* amax) {
   if (D != kHD || S % 32 != 0 || S <= 0 || (p > 0.f && dmask == nullptr)) return -1;
   const bool fused_d = S <= 128;  // each head's one dK / dV block stages every query once
   if (!fused_d) {
@@ -784,12 +786,12 @@ int launch_attn_bwd_h3(const float* qkv, const int64_t* mask, const float* bqkv,
   const dim3 grid(B * NH, 2 * ((S + 127) / 128));
   if (fused_d)
     hipLaunchKernelGGL(attn_bwd_h3_kernel<false>, grid, dim3(256), 0, st, qkv, mask, bqkv, dctx, lse, Dbuf, dqkv, S, NH,
-                       p, dmask, ctx);
+                       p, dmask, ctx, amax);
   else if (g_bwd_dma)
     hipLaunchKernelGGL(attn_bwd_h3_kernel<true>, grid, dim3(256), 0, st, qkv, mask, bqkv, dctx, lse, Dbuf, dqkv, S, NH,
-                       p, dmask, nullptr);
+                       p, dmask, nullptr, amax);
   else
     hipLaunchKernelGGL(attn_bwd_h3_kernel<false>, grid, dim3(256), 0, st, qkv, mask, bqkv, dctx, lse, Dbuf, dqkv, S, NH,
-                       p, dmask, nullptr);
+                       p, dmask, nullptr, amax);
   return 0;
 }

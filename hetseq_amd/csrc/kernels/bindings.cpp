@@ -70,9 +70,9 @@ void set_attn_h3_dma(int on);
 void set_ln_bwd_lds(int chunked);
 int attn_fp32_mode();
 int launch_attn_fwd(int, const void*, const int64_t*, const float*, void*, float*, uint32_t*, int, int, int, int, float,
-                    u64, u64, hipStream_t, int);
+                    u64, u64, hipStream_t, int, float*, int*);
 int launch_attn_bwd(int, const void*, const int64_t*, const float*, const void*, const void*, const float*, float*,
-                    void*, const uint32_t*, int, int, int, int, float, hipStream_t);
+                    void*, const uint32_t*, int, int, int, int, float, hipStream_t, float*, int*);
 // xent.hip
 void launch_xent_fwd(int, const void*, const int64_t*, int, int, int64_t, int, float*, float*, float*, hipStream_t);
 void launch_xent_bwd(int, void*, const int64_t*, const float*, int, int, int64_t, int, const float*, const float*,
@@ -479,23 +479,31 @@ PYBIND11_MODULE(_hip, m) {
         "fp32 attention forward: 1 = plane-image kernel (default), 0 = the first x6 forward");
   m.def("set_attn_timing", [](i64 buf) { set_attn_timing(P(uint64_t*, buf)); },
         "diagnostic: buffer of 16 uint64 per block for the key-block backward's phase clock stamps (0 = off)");
+  // amax: optional |max| slot of the output (ctx / dqkv); returns 1 when the kernel wrote it (h3 engine)
   m.def("attn_fwd", [](int dt, i64 qkv, i64 mask, i64 bqkv, i64 ctx, i64 lse, i64 dmask, int B, int S, int NH, int D,
-                       float p, u64 seed, u64 off, i64 st, int bh0) {
+                       float p, u64 seed, u64 off, i64 st, int bh0, i64 amax) {
     pre_launch("attn_fwd");
+    int done = 0;
     check(launch_attn_fwd(dt, P(const void*, qkv), P(const int64_t*, mask), P(const float*, bqkv), P(void*, ctx),
-                          P(float*, lse), P(uint32_t*, dmask), B, S, NH, D, p, seed, off, ST(st), bh0),
+                          P(float*, lse), P(uint32_t*, dmask), B, S, NH, D, p, seed, off, ST(st), bh0,
+                          P(float*, amax), &done),
           "attn_fwd");
+    return done;
   }, py::arg("dt"), py::arg("qkv"), py::arg("mask"), py::arg("bqkv"), py::arg("ctx"), py::arg("lse"), py::arg("dmask"),
      py::arg("B"), py::arg("S"), py::arg("NH"), py::arg("D"), py::arg("p"), py::arg("seed"), py::arg("off"),
-     py::arg("st"), py::arg("bh0") = 0);
+     py::arg("st"), py::arg("bh0") = 0, py::arg("amax") = 0);
   m.def("attn_bwd", [](int dt, i64 qkv, i64 mask, i64 bqkv, i64 ctx, i64 dctx, i64 lse, i64 dbuf, i64 dqkv, i64 dmask,
-                       int B, int S, int NH, int D, float p, i64 st) {
+                       int B, int S, int NH, int D, float p, i64 st, i64 amax) {
     pre_launch("attn_bwd");
+    int done = 0;
     check(launch_attn_bwd(dt, P(const void*, qkv), P(const int64_t*, mask), P(const float*, bqkv),
                           P(const void*, ctx), P(const void*, dctx), P(const float*, lse), P(float*, dbuf),
-                          P(void*, dqkv), P(const uint32_t*, dmask), B, S, NH, D, p, ST(st)),
+                          P(void*, dqkv), P(const uint32_t*, dmask), B, S, NH, D, p, ST(st), P(float*, amax), &done),
           "attn_bwd");
-  });
+    return done;
+  }, py::arg("dt"), py::arg("qkv"), py::arg("mask"), py::arg("bqkv"), py::arg("ctx"), py::arg("dctx"), py::arg("lse"),
+     py::arg("dbuf"), py::arg("dqkv"), py::arg("dmask"), py::arg("B"), py::arg("S"), py::arg("NH"), py::arg("D"),
+     py::arg("p"), py::arg("st"), py::arg("amax") = 0);
 
   m.def("xent_fwd", [](int dt, i64 logits, i64 labels, int rows, int V, i64 ldv, int ignore, i64 row_loss, i64 lse,
                        i64 out, i64 st) {

@@ -188,7 +188,7 @@ def attn_fwd(qkv, mask, B, S, NH, p, seed, off, bias=None, outs=None, b0=0, amax
     """qkv [B*S, 3H] (un-biased projection output if ``bias`` [3H] fp32 is given).  ``outs`` =
     (ctx, lse, dmask) buffers to write (slices of whole-batch tensors); ``b0``: the slice's first
     sequence in the whole batch (its dropout keep bits are the whole-batch launch's).  ``amax``:
-    slot receiving |max| of ctx (one pass right behind the kernel)."""
+    slot receiving |max| of ctx (written by the h3 kernel itself, else one pass behind it)."""
     T, H3 = qkv.shape
     H = H3 // 3
     assert T == B * S and H == NH * 64 and S % 32 == 0 and qkv.is_contiguous()
@@ -201,10 +201,11 @@ def attn_fwd(qkv, mask, B, S, NH, p, seed, off, bias=None, outs=None, b0=0, amax
         lse = torch.empty((B * NH * S,), dtype=torch.float32, device=qkv.device)
         # 1 keep-bit per attention probability, packed 32 keys per word, for the backward
         dmask = torch.empty((B * NH * S * (S // 32),), dtype=torch.int32, device=qkv.device) if p > 0 else None
-    hip().attn_fwd(dtype_code(qkv), qkv.data_ptr(), mask.data_ptr(), bias.data_ptr() if bias is not None else 0,
-                   ctx.data_ptr(), lse.data_ptr(), dmask.data_ptr() if dmask is not None else 0, B, S, NH, 64,
-                   float(p), seed, off, stream_handle(), int(b0) * NH)
-    if amax is not None:
+    done = hip().attn_fwd(dtype_code(qkv), qkv.data_ptr(), mask.data_ptr(), bias.data_ptr() if bias is not None else 0,
+                          ctx.data_ptr(), lse.data_ptr(), dmask.data_ptr() if dmask is not None else 0, B, S, NH, 64,
+                          float(p), seed, off, stream_handle(), int(b0) * NH,
+                          G.slot_ptr(amax) if amax is not None else 0)
+    if amax is not None and not done:  # (engines other than h3: one |max| pass behind the kernel)
         G.amax_into(ctx, amax)
     return ctx, (lse, dmask)
 
@@ -217,10 +218,11 @@ def attn_bwd(qkv, mask, ctx, dctx, lse, B, S, NH, p, seed=0, off=0, bias=None, a
     assert p == 0 or dmask is not None
     dqkv = torch.empty_like(qkv)
     dbuf = torch.empty_like(lse)
-    hip().attn_bwd(dtype_code(qkv), qkv.data_ptr(), mask.data_ptr(), bias.data_ptr() if bias is not None else 0,
-                   ctx.data_ptr(), dctx.data_ptr(), lse.data_ptr(), dbuf.data_ptr(), dqkv.data_ptr(),
-                   dmask.data_ptr() if dmask is not None else 0, B, S, NH, 64, float(p), stream_handle())
-    if amax is not None:
+    done = hip().attn_bwd(dtype_code(qkv), qkv.data_ptr(), mask.data_ptr(), bias.data_ptr() if bias is not None else 0,
+                          ctx.data_ptr(), dctx.data_ptr(), lse.data_ptr(), dbuf.data_ptr(), dqkv.data_ptr(),
+                          dmask.data_ptr() if dmask is not None else 0, B, S, NH, 64, float(p), stream_handle(),
+                          G.slot_ptr(amax) if amax is not None else 0)
+    if amax is not None and not done:
         G.amax_into(dqkv, amax)
     return dqkv
 

@@ -409,6 +409,36 @@ def test_attention_h3_matches_fp64(cuda, B, S, NH, p, data):
     assert torch.isfinite(g3).all()
 
 
+@pytest.mark.parametrize("S,engine", [(128, 2), (512, 2), (128, 1)])
+def test_attention_writes_output_amax(cuda, S, engine):
+    """The |max| slot the attention launch fills for the h3 GEMMs (ctx forward, dqkv backward): written by
+    the h3 kernels themselves, by a separate pass for the other engines -- exactly max |output| either way."""
+    from hetseq_amd.ops import bert_ops
+    from hetseq_amd.ops import gemm as G
+    from hetseq_amd.ops._C import hip
+
+    torch.manual_seed(5 + S)
+    B, NH = 4, 12
+    H = NH * 64
+    qkv = torch.randn(B * S, 3 * H, device=cuda)
+    bias = torch.randn(3 * H, device=cuda) * 0.1
+    mask = torch.ones(B, S, dtype=torch.int64, device=cuda)
+    mask[-1, S // 2:] = 0
+    sf = torch.zeros(G.SLOT_FLOATS, device=cuda)
+    sb = torch.zeros(G.SLOT_FLOATS, device=cuda)
+    old = hip().attn_fp32_mode()
+    try:
+        hip().set_attn_fp32_mode(engine)
+        ctx, saved = bert_ops.attn_fwd(qkv, mask, B, S, NH, 0.1, 3, 11, bias=bias, amax=sf)
+        dctx = torch.randn_like(ctx)
+        dqkv = bert_ops.attn_bwd(qkv, mask, ctx, dctx, saved, B, S, NH, 0.1, bias=bias, amax=sb)
+    finally:
+        hip().set_attn_fp32_mode(old)
+    torch.cuda.synchronize()
+    assert float(G.amax_value(sf)[0]) == float(ctx.abs().max())
+    assert float(G.amax_value(sb)[0]) == float(dqkv.abs().max())
+
+
 @pytest.mark.parametrize("S,p", [(256, 0.1), (512, 0.0), (384, 0.1)])
 def test_attention_h3_dma_matches_loads(cuda, S, p):
     """S > 128 h3 backward: the next-chunk rows by LDS-DMA (opt-in) give bitwise the gradients of the
