@@ -563,6 +563,8 @@ _AB = {
     # fp32 attention engine: h3 (split-fp16, default) / x6 (split-bf16)
     "attn_h3": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_fp32_mode(2),
     "attn_x6": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_fp32_mode(1),
+    "adam_8k": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_adam_config(8192, 2, 1),
+    "adam_64k": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_adam_config(65536, 2, 1),
     "h3_dma_on": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_h3_dma(1),
     "h3_dma_off": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_h3_dma(0),
     # --emulate-world: workgroups per emulated collective (RCCL channels) and the emulated bus bandwidth

@@ -24,6 +24,7 @@ void launch_stats_accum(double*, const float*, const float*, double, double, dou
 void launch_stats_finalize(double*, double, double, float*, hipStream_t);
 void launch_adam_flat(float*, const float*, float*, float*, void*, int64_t, const float*, float, float, float, float,
                       float, float, float, float, const float*, hipStream_t);
+void set_adam_config(int grid_cap, int unroll, int nt);
 void launch_adadelta_flat(float*, const float*, float*, float*, void*, int64_t, const float*, float, float, float,
                           float, float, hipStream_t);
 void launch_lamb_flat(float*, const float*, float*, float*, float*, void*, const int64_t*, int, float*, const float*,
@@ -200,6 +201,8 @@ PYBIND11_MODULE(_hip, m) {
      pybind11::arg("n"), pybind11::arg("gmul"), pybind11::arg("lr"), pybind11::arg("b1"), pybind11::arg("b2"),
      pybind11::arg("eps"), pybind11::arg("wd"), pybind11::arg("step_size"), pybind11::arg("st"),
      pybind11::arg("hyper") = 0);
+  m.def("set_adam_config", &set_adam_config, "fp32 Adam pass launch shape: grid cap, float4 groups per thread per "
+        "iteration (1 / 2 / 4), streaming accesses (benchmarking)");
   m.def("adadelta_flat", [](i64 p, i64 g, i64 sq, i64 acc, i64 shadow, i64 n, i64 gmul, float lr, double rho,
                             float eps, float wd, i64 st) {
     pre_launch("adadelta_flat");

@@ -24,14 +24,22 @@ __global__ void __launch_bounds__(kRedThreads) sumsq_partial_kernel(const float*
                                                                     double* __restrict__ partial) {
   const int64_t n4 = n >> 2;
   const float4* g4 = reinterpret_cast<const float4*>(g);
-  float acc = 0.f;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-    const float4 v = g4[i];
-    acc = fmaf(v.x, v.x, acc);
-    acc = fmaf(v.y, v.y, acc);
-    acc = fmaf(v.z, v.z, acc);
-    acc = fmaf(v.w, v.w, acc);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  // four float4 loads in flight per thread and iteration (one dependent chain each), fixed order
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n4; i += 4 * stride) {
+    const float4 v0 = g4[i], v1 = g4[i + stride], v2 = g4[i + 2 * stride], v3 = g4[i + 3 * stride];
+    a0 = fmaf(v0.x, v0.x, fmaf(v0.y, v0.y, fmaf(v0.z, v0.z, fmaf(v0.w, v0.w, a0))));
+    a1 = fmaf(v1.x, v1.x, fmaf(v1.y, v1.y, fmaf(v1.z, v1.z, fmaf(v1.w, v1.w, a1))));
+    a2 = fmaf(v2.x, v2.x, fmaf(v2.y, v2.y, fmaf(v2.z, v2.z, fmaf(v2.w, v2.w, a2))));
+    a3 = fmaf(v3.x, v3.x, fmaf(v3.y, v3.y, fmaf(v3.z, v3.z, fmaf(v3.w, v3.w, a3))));
   }
+  for (; i < n4; i += stride) {
+    const float4 v = g4[i];
+    a0 = fmaf(v.x, v.x, fmaf(v.y, v.y, fmaf(v.z, v.z, fmaf(v.w, v.w, a0))));
+  }
+  float acc = (a0 + a1) + (a2 + a3);
   if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
     const float v = g[(n4 << 2) + threadIdx.x];
     acc = fmaf(v, v, acc);
@@ -107,7 +115,17 @@ HS_DEVICE void adam4(float4& pp, const float4 gg, float4& mm, float4& vv, float 
   }
 }
 
-template <bool kShadow>
+HS_DEVICE float4 ld_mode(const float* p, bool nt) {
+  return nt ? ld_nt(p) : *reinterpret_cast<const float4*>(p);
+}
+HS_DEVICE void st_mode(float* p, float4 v, bool nt) {
+  if (nt) st_nt(p, v);
+  else *reinterpret_cast<float4*>(p) = v;
+}
+
+// U float4 groups per thread per iteration (4U independent 16-B loads in flight); NT: streaming
+// (non-temporal) accesses
+template <bool kShadow, int U = 2, bool NT = true>
 __global__ void __launch_bounds__(256) adam_flat_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                         float* __restrict__ m, float* __restrict__ v,
                                                         bf16_t* __restrict__ shadow, int64_t n,
@@ -123,30 +141,33 @@ __global__ void __launch_bounds__(256) adam_flat_kernel(float* __restrict__ p, c
   const int64_t n4 = n >> 2;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  // two float4 groups per thread per iteration: 8 independent 16-B loads in flight
-  for (; i + stride < n4; i += 2 * stride) {
-    float4 p0 = ld_nt(p + 4 * i), g0 = ld_nt(g + 4 * i), m0 = ld_nt(m + 4 * i), v0 = ld_nt(v + 4 * i);
-    const int64_t j = i + stride;
-    float4 p1 = ld_nt(p + 4 * j), g1 = ld_nt(g + 4 * j), m1 = ld_nt(m + 4 * j), v1 = ld_nt(v + 4 * j);
-    adam4<kShadow>(p0, g0, m0, v0, mul, b1, b2, omb1, omb2, eps, wd, decay, step_size);
-    adam4<kShadow>(p1, g1, m1, v1, mul, b1, b2, omb1, omb2, eps, wd, decay, step_size);
-    st_nt(p + 4 * i, p0);
-    st_nt(m + 4 * i, m0);
-    st_nt(v + 4 * i, v0);
-    st_nt(p + 4 * j, p1);
-    st_nt(m + 4 * j, m1);
-    st_nt(v + 4 * j, v1);
-    if (kShadow) {
-      store4(shadow + 4 * i, reinterpret_cast<const float*>(&p0));
-      store4(shadow + 4 * j, reinterpret_cast<const float*>(&p1));
+  for (; i + (U - 1) * stride < n4; i += U * stride) {
+    float4 pp[U], gg[U], mm[U], vv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t j = i + u * stride;
+      pp[u] = ld_mode(p + 4 * j, NT);
+      gg[u] = ld_mode(g + 4 * j, NT);
+      mm[u] = ld_mode(m + 4 * j, NT);
+      vv[u] = ld_mode(v + 4 * j, NT);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t j = i + u * stride;
+      adam4<kShadow>(pp[u], gg[u], mm[u], vv[u], mul, b1, b2, omb1, omb2, eps, wd, decay, step_size);
+      st_mode(p + 4 * j, pp[u], NT);
+      st_mode(m + 4 * j, mm[u], NT);
+      st_mode(v + 4 * j, vv[u], NT);
+      if (kShadow) store4(shadow + 4 * j, reinterpret_cast<const float*>(&pp[u]));
     }
   }
   for (; i < n4; i += stride) {
-    float4 p0 = ld_nt(p + 4 * i), g0 = ld_nt(g + 4 * i), m0 = ld_nt(m + 4 * i), v0 = ld_nt(v + 4 * i);
+    float4 p0 = ld_mode(p + 4 * i, NT), g0 = ld_mode(g + 4 * i, NT), m0 = ld_mode(m + 4 * i, NT),
+           v0 = ld_mode(v + 4 * i, NT);
     adam4<kShadow>(p0, g0, m0, v0, mul, b1, b2, omb1, omb2, eps, wd, decay, step_size);
-    st_nt(p + 4 * i, p0);
-    st_nt(m + 4 * i, m0);
-    st_nt(v + 4 * i, v0);
+    st_mode(p + 4 * i, p0, NT);
+    st_mode(m + 4 * i, m0, NT);
+    st_mode(v + 4 * i, v0, NT);
     if (kShadow) store4(shadow + 4 * i, reinterpret_cast<const float*>(&p0));
   }
   // scalar tail
@@ -296,16 +317,37 @@ void launch_grad_norm(const float* g, int64_t n, double* partial, const float* s
 // omb1 = 1 - b1, omb2 = 1 - b2 (and omr = 1 - rho below) come from the host, computed in double from
 // the Python hyper-parameters and rounded once: 1.0f - 0.999f is 0.00100004673, 4.7e-5 off the
 // reference's (1 - beta2) = 0.001 (optim.py:205-206 multiplies by the Python double).
+// launch shape of the fp32 Adam pass (set_adam_config, tools/bench_adam.py): grid cap, float4 groups per
+// thread per iteration (1 / 2 / 4), streaming accesses.  BERT-base's 110 M parameters, one MI355X: a grid
+// of up to 65536 blocks (each thread's two float4 groups in ONE iteration, 8 loads in flight) 552 us,
+// 5.6 TB/s over the seven streams, against 638 us with the grid-stride loop of 8192 blocks
+static int g_adam_grid = 65536, g_adam_unroll = 2, g_adam_nt = 1;
+void set_adam_config(int grid_cap, int unroll, int nt) {
+  g_adam_grid = grid_cap > 0 ? grid_cap : 65536;
+  g_adam_unroll = unroll == 4 ? 4 : unroll == 1 ? 1 : 2;
+  g_adam_nt = nt ? 1 : 0;
+}
+
 void launch_adam_flat(float* p, const float* g, float* m, float* v, void* shadow, int64_t n, const float* gmul,
                       float lr, float b1, float b2, float omb1, float omb2, float eps, float wd, float step_size,
                       const float* hyper, hipStream_t st) {
-  const int grid = grid_for(n / 4 + 1, 256, 8192);
-  if (shadow)
+  const int grid = grid_for(n / 4 + 1, 256, g_adam_grid);
+  if (shadow) {
     hipLaunchKernelGGL(adam_flat_kernel<true>, dim3(grid), dim3(256), 0, st, p, g, m, v,
                        reinterpret_cast<bf16_t*>(shadow), n, gmul, lr, b1, b2, omb1, omb2, eps, wd, step_size, hyper);
-  else
-    hipLaunchKernelGGL(adam_flat_kernel<false>, dim3(grid), dim3(256), 0, st, p, g, m, v, nullptr, n, gmul, lr, b1,
-                       b2, omb1, omb2, eps, wd, step_size, hyper);
+    return;
+  }
+#define HS_ADAM(U, NT)                                                                                          \
+  hipLaunchKernelGGL((adam_flat_kernel<false, U, NT>), dim3(grid), dim3(256), 0, st, p, g, m, v, nullptr, n, gmul, \
+                     lr, b1, b2, omb1, omb2, eps, wd, step_size, hyper)
+  if (g_adam_unroll == 4) {
+    if (g_adam_nt) HS_ADAM(4, true); else HS_ADAM(4, false);
+  } else if (g_adam_unroll == 1) {
+    if (g_adam_nt) HS_ADAM(1, true); else HS_ADAM(1, false);
+  } else {
+    if (g_adam_nt) HS_ADAM(2, true); else HS_ADAM(2, false);
+  }
+#undef HS_ADAM
 }
 
 void launch_adadelta_flat(float* p, const float* g, float* sq, float* acc, void* shadow, int64_t n,
