@@ -911,7 +911,7 @@ def linear_dgrad_dgelu(dy, w, pre, b, db_acc=None, planes_out=False, amax=None, 
 
 # ------------------------------------------------------------------ h3 operand scales per forward
 _SEG_TABLES: dict = {}  # (device, ((ptr, numel), ...)) -> (base ptr, int64 [nblk, 3] table, nblk)
-_SEG_CHUNK4 = 16384  # float4s per amax_seg block (64 Ki floats)
+_SEG_CHUNK4 = 2048  # float4s per amax_seg block (8 Ki floats; tools/bench_amax.py: 71 vs 77 us at 16384)
 
 
 def _seg_table(ts):
