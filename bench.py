@@ -565,6 +565,10 @@ _AB = {
     "attn_x6": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_fp32_mode(1),
     "adam_8k": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_adam_config(8192, 2, 1),
     "adam_64k": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_adam_config(65536, 2, 1),
+    # split-K of the side-stream weight gradients (runtime/streams.py): the default 2 (4 for <= 768 x 768)
+    "sideks_2": lambda: setattr(__import__("hetseq_amd.runtime.streams", fromlist=["x"]), "SIDE_KSPLIT", 2),
+    "sideks_1": lambda: setattr(__import__("hetseq_amd.runtime.streams", fromlist=["x"]), "SIDE_KSPLIT", 1),
+    "sideks_4": lambda: setattr(__import__("hetseq_amd.runtime.streams", fromlist=["x"]), "SIDE_KSPLIT", 4),
     "h3_dma_on": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_h3_dma(1),
     "h3_dma_off": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_h3_dma(0),
     # --emulate-world: workgroups per emulated collective (RCCL channels) and the emulated bus bandwidth
