@@ -569,6 +569,8 @@ _AB = {
     "sideks_2": lambda: setattr(__import__("hetseq_amd.runtime.streams", fromlist=["x"]), "SIDE_KSPLIT", 2),
     "sideks_1": lambda: setattr(__import__("hetseq_amd.runtime.streams", fromlist=["x"]), "SIDE_KSPLIT", 1),
     "sideks_4": lambda: setattr(__import__("hetseq_amd.runtime.streams", fromlist=["x"]), "SIDE_KSPLIT", 4),
+    "lazyzero_on": lambda: setattr(__import__("hetseq_amd.controller", fromlist=["x"]), "_LAZY_ZERO", True),
+    "lazyzero_off": lambda: setattr(__import__("hetseq_amd.controller", fromlist=["x"]), "_LAZY_ZERO", False),
     "h3_dma_on": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_h3_dma(1),
     "h3_dma_off": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_h3_dma(0),
     # --emulate-world: workgroups per emulated collective (RCCL channels) and the emulated bus bandwidth

@@ -41,6 +41,9 @@ from hetseq_amd.parallel.ddp import BMUF, FlatDDP
 from hetseq_amd.runtime import faults, profiling, rng, streams
 from hetseq_amd.runtime.flat import FlatParamStore
 
+# zero_grad clears only the gradient regions the next backward does not overwrite (HETSEQ_LAZY_ZERO=0: all)
+_LAZY_ZERO = os.environ.get("HETSEQ_LAZY_ZERO", "1") == "1"
+
 LN2 = math.log(2)
 
 
@@ -508,7 +511,8 @@ class Controller(object):
             raise RuntimeError("parameter checksum diverged across ranks: min {} max {}".format(float(lo), float(hi)))
 
     def zero_grad(self):
-        self.optimizer.zero_grad()
+        # lazy: the fused backward overwrites most of the gradient buffer (runtime/flat.py cover())
+        self.optimizer.zero_grad(lazy=_LAZY_ZERO and self.cuda)
 
     def clear_buffered_stats(self):
         self._all_reduce_list = [0.0] * 6

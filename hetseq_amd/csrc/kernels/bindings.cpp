@@ -55,6 +55,7 @@ void launch_gather_rows(int, const void*, const int32_t*, void*, int, int, hipSt
 void launch_scatter_add_rows(int, const void*, const int32_t*, void*, int, int, hipStream_t);
 int launch_amax(const float*, int64_t, float*, int, hipStream_t);
 void launch_amax_seg(const float*, const int64_t*, int, float*, hipStream_t);
+void launch_zero_segs(float*, const int64_t*, int, hipStream_t);
 // pool_nsp.hip
 int launch_pool_nsp_fwd(int, const void*, int, int, int, const float*, const float*, const float*, const float*,
                         const int64_t*, const float*, float*, float*, float*, float*, float*, hipStream_t);
@@ -461,6 +462,11 @@ PYBIND11_MODULE(_hip, m) {
     pre_launch("amax");
     check(launch_amax(P(const float*, x), n, P(float*, out), zero_first, ST(st)), "amax");
   }, "|max| of n fp32 values (n % 4 == 0, 16-B aligned) atomically maxed into *out (cleared first if zero_first)");
+  m.def("zero_segs", [](i64 base, i64 tab, int nblk, i64 st) {
+    pre_launch("zero_segs");
+    launch_zero_segs(P(float*, base), P(const int64_t*, tab), nblk, ST(st));
+    check_launch("zero_segs");
+  }, "zero the float4 ranges of a (lo, hi) block table from base (one launch)");
   m.def("amax_seg", [](i64 base, i64 tab, int nblk, i64 out, i64 st) {
     pre_launch("amax_seg");
     launch_amax_seg(P(const float*, base), P(const int64_t*, tab), nblk, P(float*, out), ST(st));

@@ -494,6 +494,14 @@ __global__ void __launch_bounds__(256) amax_seg_kernel(const float* __restrict__
     amax_put(out + seg * kAmaxShards * kAmaxStride, max(max(red[0], red[1]), max(red[2], red[3])), blockIdx.x);
 }
 
+// zero float4 ranges: block b clears [tab[2 b], tab[2 b + 1]) (float4 indices from base) -- the part of the
+// flat gradient buffer a lazy zero_grad clears (runtime/flat.py: the regions the backward overwrites stay)
+__global__ void __launch_bounds__(256) zero_segs_kernel(float* __restrict__ base, const int64_t* __restrict__ tab) {
+  const int64_t lo = tab[2 * blockIdx.x], hi = tab[2 * blockIdx.x + 1];
+  float4* v = reinterpret_cast<float4*>(base);
+  for (int64_t i = lo + threadIdx.x; i < hi; i += 256) v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
 }  // namespace hs
 
 // |max| of x[0, n) (n % 4 == 0, 16-B aligned) into the slot `out` (common.h: kAmaxShards shards);
@@ -512,4 +520,8 @@ int launch_amax(const float* x, int64_t n, float* out, int zero_first, hipStream
 // (segment, first float4, end float4)
 void launch_amax_seg(const float* base, const int64_t* tab, int nblk, float* out, hipStream_t st) {
   if (nblk > 0) hipLaunchKernelGGL(amax_seg_kernel, dim3(nblk), dim3(256), 0, st, base, tab, out);
+}
+
+void launch_zero_segs(float* base, const int64_t* tab, int nblk, hipStream_t st) {
+  if (nblk > 0) hipLaunchKernelGGL(zero_segs_kernel, dim3(nblk), dim3(256), 0, st, base, tab);
 }

@@ -449,6 +449,7 @@ class BertLayer(nn.Module):
         g.w1, g.bi = gv(self.intermediate.dense_act.weight), gv(self.intermediate.dense_act.bias)
         g.w2, g.b2 = gv(o.dense.weight), gv(o.dense.bias)
         g.g2, g.bb2 = gv(o.LayerNorm.weight), gv(o.LayerNorm.bias)
+        store.cover(g.wqkv, g.wo, g.w1, g.w2)  # the fused backward overwrites these (lazy zero_grad)
         return g
 
 
@@ -838,6 +839,7 @@ class BertForPreTraining(BertPreTrainedModel):
         if store is not None:
             meta["grad_sink"] = lambda: [store.grad_view(q) for q in params]
             meta["store"] = store
+            store.cover(store.grad_view(pred.decoder.weight))  # the tied decoder's gradient store (lazy zero_grad)
         return FusedPreTrainingLoss.apply(seq2d, labels.reshape(-1).contiguous(), nsp_label.reshape(-1).contiguous(),
                                           meta, *params)
 

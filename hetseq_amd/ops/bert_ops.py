@@ -609,12 +609,23 @@ class FusedBertLayer(torch.autograd.Function):
         store = meta.get("store")
         wacc = acc and not (side and _FRESH_WGRAD and store is not None and store.claim_fresh())
 
+        def claim(out, accumulate):  # lazy zero_grad bookkeeping (runtime/flat.py): on the writer's stream
+            if store is not None and out is not None:
+                if accumulate:
+                    store.ensure_zero(out)
+                else:
+                    store.mark_stored(out)
+
         def wgrad(dy, xin_, out, amax=None):
             if not side:
+                claim(out, acc)
                 return G.linear_wgrad(dy, xin_, out=out, accumulate=acc, amax=amax)
             ks = streams.side_ksplit(dy.shape[1], xin_.shape[1])
-            return streams.run(dy.device, lambda: G.linear_wgrad(dy, xin_, out=out, accumulate=wacc,
-                                                                 ksplit=ks, amax=amax), dy, xin_)
+
+            def run():
+                claim(out, wacc)
+                return G.linear_wgrad(dy, xin_, out=out, accumulate=wacc, ksplit=ks, amax=amax)
+            return streams.run(dy.device, run, dy, xin_)
 
         # side-stream work forks at three points per layer; the launches at one point share one event
         with streams.coalesced():  # LN2 parameter gradients + the FFN-out weight gradient
@@ -643,9 +654,12 @@ class FusedBertLayer(torch.autograd.Function):
             fused = False
             if side and not pl and _WGRAD_COLSUM:  # one launch: the bias gradient from the wgrad's staging
                 ks = streams.side_ksplit(dqkv.shape[1], xin.shape[1])
-                fused = streams.run(dqkv.device, lambda: G.linear_wgrad_colsum(dqkv, xin, Gv.wqkv, Gv.bqkv, ksplit=ks,
-                                                                               accumulate=wacc, amax=qkv_w_am),
-                                    dqkv, xin)
+
+                def run_colsum():
+                    claim(Gv.wqkv, wacc)
+                    return G.linear_wgrad_colsum(dqkv, xin, Gv.wqkv, Gv.bqkv, ksplit=ks, accumulate=wacc,
+                                                 amax=qkv_w_am)
+                fused = streams.run(dqkv.device, run_colsum, dqkv, xin)
             if fused:
                 dWqkv, dbqkv = Gv.wqkv, Gv.bqkv
             else:
@@ -805,11 +819,15 @@ class FusedPreTrainingLoss(torch.autograd.Function):
         am_dl = G.amax_of(lbuf) if (am and lbuf is not None) else None  # dlogits: both decoder gradients' operand
         if lbuf is not None:  # padded split-bf16 decoder products (pad columns of dlogits stay zero)
             def dwdec():
+                if acc and store is not None:  # lazy zero_grad bookkeeping, on the writer's stream
+                    (store.ensure_zero if dec_acc else store.mark_stored)(Gv[4])
                 out_w = Gv[4] if acc else torch.zeros((V, t2.shape[1]), dtype=torch.float32, device=t2.device)
                 return G.decoder_wgrad(lbuf, t2, V, out_w, accumulate=dec_acc,
                                        amax=(am_dl, am["t2"]) if am_dl is not None else None)
         else:
             def dwdec():
+                if acc and store is not None:
+                    store.ensure_zero(Gv[4])
                 return G.linear_wgrad(dl_c, t2, out=Gv[4] if acc else None, accumulate=acc)
 
         def dbias():

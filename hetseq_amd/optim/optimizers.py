@@ -101,6 +101,7 @@ class _Optimizer(object):
             if max_norm > 0:
                 return torch.nn.utils.clip_grad_norm_(params, max_norm)
             return torch.sqrt(sum(p.grad.data.float().norm() ** 2 for p in params))
+        self.store.flush_lazy()
         sc = self._scale_tensor()
         g = self.store.grad
         if g.is_cuda:
@@ -158,6 +159,7 @@ class _Optimizer(object):
         if self.store is None:
             self._step_unfused()
         else:
+            self.store.flush_lazy()
             gm = self._grad_multiplier()
             if self.store.param.is_cuda:
                 self._step_hip(gm)
@@ -168,9 +170,9 @@ class _Optimizer(object):
         self._norm_ready = False
         return loss
 
-    def zero_grad(self):
+    def zero_grad(self, lazy=False):
         if self.store is not None:
-            self.store.zero_grad()
+            self.store.zero_grad(lazy)
         else:
             for p in self.params:
                 p.grad = None

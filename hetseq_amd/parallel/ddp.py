@@ -189,6 +189,7 @@ class FlatDDP(torch.nn.Module):
 
     def _launch_range(self, lo, hi, name):
         profiling.range_push(name)
+        self.store.flush_range(lo, hi)  # (a lazily zeroed region no writer claimed: cleared before reducing)
         g = self.store.grad
         self._log(name, g[lo:hi])
         side = streams.active(g.device) if g.is_cuda else None

@@ -90,6 +90,66 @@ def test_direct_flat_grads_match_autograd_grads(cuda, side):
         streams.set_enabled(old)
 
 
+@pytest.mark.parametrize("side,micro", [(True, 1), (True, 2), (False, 1)])
+def test_lazy_zero_grad_matches_full_zero(cuda, side, micro):
+    """A lazy zero_grad (runtime/flat.py: only the regions the backward does not overwrite are cleared)
+    gives bitwise the gradients of a full zero_grad, from a buffer full of stale values: with the side
+    stream the first backward stores the covered regions, a second micro-batch accumulates onto them;
+    without it every covered writer accumulates after ensure_zero."""
+    from hetseq_amd.runtime import streams
+    from hetseq_amd.runtime.flat import FlatParamStore
+
+    old = streams.enabled()
+    streams.set_enabled(side)
+    try:
+        model, cfg = _tiny(cuda)
+        model.eval()
+        model.max_predictions_per_seq = 10
+        store = FlatParamStore(model)
+        model.attach_store(store, torch.float32)
+        batch = _batch(cuda, 4, 64, cfg.vocab_size)
+        store.zero_grad()
+        model(*batch).backward()  # registers the covered regions (fused layers, tied decoder)
+        assert store._cover, "no store-covered gradient regions registered"
+        grads = {}
+        for lazy in (False, True):
+            store.grad.fill_(123.0)
+            store.zero_grad(lazy=lazy)
+            for _ in range(micro):
+                model(*batch).backward()
+            store.flush_lazy()
+            torch.cuda.synchronize()
+            grads[lazy] = store.grad.clone()
+        assert torch.equal(grads[True], grads[False])
+    finally:
+        streams.set_enabled(old)
+
+
+def test_lazy_zero_grad_flushes_unclaimed_regions(cuda):
+    """Covered regions no writer claimed read as zero once the gradients are read (flush_lazy), and
+    ensure_zero clears a pending region exactly once."""
+    from hetseq_amd.runtime.flat import FlatParamStore
+
+    model, _ = _tiny(cuda)
+    store = FlatParamStore(model)
+    ps = [p for p in model.parameters() if p.dim() == 2 and p.numel() % 4 == 0][:3]
+    store.cover(*(store.grad_view(p) for p in ps))
+    store.grad.fill_(5.0)
+    store.zero_grad(lazy=True)
+    torch.cuda.synchronize()
+    covered = sum(p.numel() for p in ps)
+    assert int((store.grad != 0).sum()) == covered  # only the covered regions kept their stale values
+    store.ensure_zero(store.grad_view(ps[0]))
+    assert float(store.grad_view(ps[0]).abs().max()) == 0.0
+    store.grad_view(ps[0]).fill_(1.0)  # "accumulated" after ensure_zero: not cleared again
+    store.ensure_zero(store.grad_view(ps[0]))
+    assert float(store.grad_view(ps[0]).min()) == 1.0
+    store.mark_stored(store.grad_view(ps[1]))
+    store.flush_lazy()  # clears ps[2] only
+    assert float(store.grad_view(ps[2]).abs().max()) == 0.0
+    assert float(store.grad_view(ps[1]).min()) == 5.0
+
+
 def test_fused_train_step_with_store_and_dropout(cuda):
     from argparse import Namespace
 
