@@ -10,7 +10,8 @@ memory layout everything else is designed around:
 * the gradient-norm / clip is one reduction over one buffer;
 * data-parallel buckets are contiguous slices of ``store.grad`` -- all-reduce
   runs in place, zero-copy (hetseq_amd/parallel/ddp.py);
-* zero_grad is one memset;
+* zero_grad is one launch -- lazily, only over the regions the next backward does not
+  overwrite (see ``cover``);
 * an optional bf16 ``shadow`` buffer (same offsets) holds the compute copy
   of the weights for ``--dtype bf16``; the optimizer kernel refreshes it.
 
