@@ -569,6 +569,15 @@ _AB = {
     "sideks_2": lambda: setattr(__import__("hetseq_amd.runtime.streams", fromlist=["x"]), "SIDE_KSPLIT", 2),
     "sideks_1": lambda: setattr(__import__("hetseq_amd.runtime.streams", fromlist=["x"]), "SIDE_KSPLIT", 1),
     "sideks_4": lambda: setattr(__import__("hetseq_amd.runtime.streams", fromlist=["x"]), "SIDE_KSPLIT", 4),
+    # split-K finished by the last-arriving slice inside the GEMM launch (gemm.hip splitk_inlaunch)
+    "inl_on": lambda: setattr(__import__("hetseq_amd.ops.gemm", fromlist=["x"]), "_INLAUNCH", True),
+    "inl_wt": lambda: (setattr(__import__("hetseq_amd.ops.gemm", fromlist=["x"]), "_INLAUNCH", True),
+                       __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_splitk_wt(1)),
+    "inl_rel": lambda: (setattr(__import__("hetseq_amd.ops.gemm", fromlist=["x"]), "_INLAUNCH", True),
+                        __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_splitk_wt(0)),
+    "ffnbias_wgrad": lambda: setattr(__import__("hetseq_amd.ops.bert_ops", fromlist=["x"]), "_FFN_BIAS_WGRAD", True),
+    "ffnbias_dgelu": lambda: setattr(__import__("hetseq_amd.ops.bert_ops", fromlist=["x"]), "_FFN_BIAS_WGRAD", False),
+    "inl_off": lambda: setattr(__import__("hetseq_amd.ops.gemm", fromlist=["x"]), "_INLAUNCH", False),
     "lazyzero_on": lambda: setattr(__import__("hetseq_amd.controller", fromlist=["x"]), "_LAZY_ZERO", True),
     "lazyzero_off": lambda: setattr(__import__("hetseq_amd.controller", fromlist=["x"]), "_LAZY_ZERO", False),
     "h3_dma_on": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_h3_dma(1),
@@ -620,7 +629,8 @@ def _ab_run(b, ctl, gen):
     times = {n: [] for n in names}
     for r in range(b.ab_rounds):
         for n in (names if r % 2 == 0 else names[::-1]):  # alternate the order too
-            _AB[n]()
+            for part in n.split("+"):  # "a+b": both settings
+                _AB[part]()
             ctl.train_step(next(gen))  # one untimed step after a switch
             torch.cuda.synchronize()
             t0 = time.perf_counter()

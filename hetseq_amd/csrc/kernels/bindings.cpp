@@ -86,7 +86,9 @@ int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, i
                 int64_t ldb, void* C, int64_t ldc, const float* bias, int epi, float beta, float* aux, int64_t ldaux,
                 float* part, float* colsum_out, int colsum_acc, int tile_override, hipStream_t st, int ksplit,
                 float* slab, int64_t slab_floats, int mv, int nv, int kv, const float* amax_a, int namax_a,
-                const float* amax_b, int namax_b, float* amax_c);
+                const float* amax_b, int namax_b, float* amax_c, int* tickets);
+int splitk_tickets();
+void set_splitk_wt(int on);
 
 // gemm_planes.hip
 int launch_gemm_planes(int planes, int c_dtype, int ta, int tb, int M, int N, int K, const void* A, int64_t lda,
@@ -576,13 +578,13 @@ PYBIND11_MODULE(_hip, m) {
   m.def("gemm", [](int dt, int ta, int tb, int M, int N, int K, i64 A, i64 lda, i64 B, i64 ldb, i64 C, i64 ldc, i64 bias,
                    int epi, float beta, i64 aux, i64 ldaux, i64 part, i64 colsum, int colsum_acc, i64 st,
                    int tile, int ksplit, i64 slab, i64 slab_floats, int mv, int nv, int kv, i64 amax_a, int namax_a,
-                   i64 amax_b, int namax_b, i64 amax_c) {
+                   i64 amax_b, int namax_b, i64 amax_c, i64 tickets) {
     pre_launch("gemm");
     const int rc = launch_gemm(dt, ta, tb, M, N, K, P(const void*, A), lda, P(const void*, B), ldb, P(void*, C), ldc,
                                P(const float*, bias), epi, beta, P(float*, aux), ldaux, P(float*, part),
                                P(float*, colsum), colsum_acc, tile, ST(st), ksplit, P(float*, slab), slab_floats, mv, nv,
                                kv, P(const float*, amax_a), namax_a, P(const float*, amax_b), namax_b,
-                               P(float*, amax_c));
+                               P(float*, amax_c), P(int*, tickets));
     if (rc == 0) check_launch("gemm");
     return rc;
   }, pybind11::arg("dt"), pybind11::arg("ta"), pybind11::arg("tb"), pybind11::arg("M"), pybind11::arg("N"),
@@ -592,5 +594,8 @@ PYBIND11_MODULE(_hip, m) {
      pybind11::arg("colsum_acc"), pybind11::arg("st"), pybind11::arg("tile") = -1, pybind11::arg("ksplit") = 0,
      pybind11::arg("slab") = 0, pybind11::arg("slab_floats") = 0, pybind11::arg("mv") = 0, pybind11::arg("nv") = 0,
      pybind11::arg("kv") = 0, pybind11::arg("amax_a") = 0, pybind11::arg("namax_a") = 0, pybind11::arg("amax_b") = 0,
-     pybind11::arg("namax_b") = 0, pybind11::arg("amax_c") = 0);
+     pybind11::arg("namax_b") = 0, pybind11::arg("amax_c") = 0, pybind11::arg("tickets") = 0);
+  m.def("set_splitk_wt", &set_splitk_wt, "in-launch split-K slabs: 1 write-through stores, 0 plain + release fence");
+  m.def("splitk_tickets", &splitk_tickets,
+        "arrival counters a stream's in-launch split-K GEMMs need (an int32 buffer, zeroed once)");
 }

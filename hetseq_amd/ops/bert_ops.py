@@ -34,6 +34,10 @@ _LN_PARTIALS_WO = _LN_PARTIALS  # (the attention-output product's part of the sw
 # the QKV bias gradient summed by the QKV weight-gradient kernel (gemm.linear_wgrad_colsum) instead of
 # a column-sum pass over dqkv (HETSEQ_WGRAD_COLSUM=0: separate pass)
 _WGRAD_COLSUM = os.environ.get("HETSEQ_WGRAD_COLSUM", "1") == "1"
+# the FFN-in bias gradient the same way, from the FFN-in weight-gradient launch on the side stream,
+# instead of the dGELU data-gradient epilogue's column partials + a reduce pass on the compute stream
+# (HETSEQ_FFN_BIAS_WGRAD=0: in the dGELU epilogue)
+_FFN_BIAS_WGRAD = os.environ.get("HETSEQ_FFN_BIAS_WGRAD", "1") == "1"
 # weight gradients store (beta 0) in the first backward after zero_grad (HETSEQ_FRESH_WGRAD=0: always add)
 _FRESH_WGRAD = os.environ.get("HETSEQ_FRESH_WGRAD", "1") == "1"
 from hetseq_amd.ops._C import dtype_code, hip, stream_handle
@@ -627,6 +631,17 @@ class FusedBertLayer(torch.autograd.Function):
                 return G.linear_wgrad(dy, xin_, out=out, accumulate=wacc, ksplit=ks, amax=amax)
             return streams.run(dy.device, run, dy, xin_)
 
+        def wgrad_bias(dy, xin_, wout, bout, amax):  # side stream: weight + bias gradient, one launch if served
+            ks = streams.side_ksplit(dy.shape[1], xin_.shape[1])
+
+            def run_colsum():
+                claim(wout, wacc)
+                return G.linear_wgrad_colsum(dy, xin_, wout, bout, ksplit=ks, accumulate=wacc, amax=amax)
+            if streams.run(dy.device, run_colsum, dy, xin_):
+                return wout, bout
+            w_ = wgrad(dy, xin_, wout, amax=amax)
+            return w_, streams.run(dy.device, lambda: colsum(dy, acc=bout), dy)
+
         # side-stream work forks at three points per layer; the launches at one point share one event
         with streams.coalesced():  # LN2 parameter gradients + the FFN-out weight gradient
             dz2, do_, dg2, dbb2, db2 = ln_bwd(dh2, z2, m2, r2, W.g2, p_h, 1, s_2, o_2, True, not pl,
@@ -634,9 +649,13 @@ class FusedBertLayer(torch.autograd.Function):
                                               amax=sl(8))
             do_p = _planes_of(dop) if pl else do_
             dW2 = wgrad(do_p, f1, Gv.w2 if acc else None, amax=_am(am, sl(8), sl(4, 2)))
+        bi_in_wgrad = side and not pl and _WGRAD_COLSUM and _FFN_BIAS_WGRAD
         df1p, dbi = G.linear_dgrad_dgelu(do_p, W.w2, f1pre, W.bi, db_acc=Gv.bi if acc else None, planes_out=pl,
-                                         amax=_am(am, sl(8), wsl(3)), amax_out=sl(9))
-        dW1 = wgrad(df1p, h1, Gv.w1 if acc else None, amax=_am(am, sl(9), sl(0, 2)))
+                                         amax=_am(am, sl(8), wsl(3)), amax_out=sl(9), colsum=not bi_in_wgrad)
+        if dbi is None:  # the bias gradient comes with the FFN-in weight gradient (side stream)
+            dW1, dbi = wgrad_bias(df1p, h1, Gv.w1, Gv.bi, _am(am, sl(9), sl(0, 2)))
+        else:
+            dW1 = wgrad(df1p, h1, Gv.w1 if acc else None, amax=_am(am, sl(9), sl(0, 2)))
         dh1 = G.linear_dgrad(df1p, W.w1, out=dz2, accumulate=True, ksplit=dks,
                              amax=_am(am, sl(9), wsl(2)))  # dz2 + df1pre @ W1
         dap = _planes_buf(rows, H, dh2.device) if pl else None

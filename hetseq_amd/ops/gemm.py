@@ -172,6 +172,33 @@ def _slab(M, N, ksplit, device):
     return buf
 
 
+# In-launch split-K finish (gemm.hip splitk_inlaunch): the last K slice to arrive at a tile sums the
+# slices and writes C, instead of a separate splitk_reduce pass.  Opt-in (HETSEQ_SPLITK_INLAUNCH=1):
+# bitwise the same result, but in the BERT-base fp32 step it loses to the separate pass (interleaved
+# A/B, 8 rounds: 12.03 ms write-through slabs, 12.11 plain + release fence, against 11.88 with the
+# pass -- 64 KB per slice and tile is past the size where an in-launch combine pays, and the pass runs
+# on the weight-gradient stream beside the data-gradient chain anyway).
+_INLAUNCH = os.environ.get("HETSEQ_SPLITK_INLAUNCH", "0") == "1"
+_TICKETS = {}
+
+
+def _tickets(device):
+    """The arrival counters of the current stream role's split-K GEMMs (zero between launches: the
+    last arriver of each tile resets its counter), or None (off, or first use inside a capture)."""
+    if not _INLAUNCH:
+        return None
+    from hetseq_amd.runtime import streams
+
+    key = (device, streams.role(stream_handle()))
+    buf = _TICKETS.get(key)
+    if buf is None:
+        if torch.cuda.is_current_stream_capturing():
+            return None
+        buf = torch.zeros(hip().splitk_tickets(), dtype=torch.int32, device=device)
+        _TICKETS[key] = buf
+    return buf
+
+
 # ------------------------------------------------------------------ bf16-plane operands
 class Planes(object):
     """A [rows, cols] GEMM operand as P bf16 planes (csrc/kernels/gemm_planes.hip):
@@ -470,13 +497,14 @@ def _hip_gemm(a, b, ta, tb, out, bias=None, epi=EPI_NONE, beta=0.0, aux=None, pa
         am = _amax_ptr(a, amax[0] if amax is not None else None, keep) + _amax_ptr(
             b, amax[1] if amax is not None else None, keep)
     slab = _slab(M, N, ksplit, a.device) if (dt or ksplit > 1) and epi <= EPI_BIAS and ksplit != 1 else None
+    tk = _tickets(a.device) if slab is not None else None
     rc = hip().gemm(dt, int(ta), int(tb), M, N, K, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0),
                     out.data_ptr(), out.stride(0), bias.data_ptr() if bias is not None else 0, epi, float(beta),
                     aux.data_ptr() if aux is not None else 0, aux.stride(0) if aux is not None else 0,
                     part.data_ptr() if part is not None else 0, colsum.data_ptr() if colsum is not None else 0,
                     int(colsum_acc), stream_handle(), tile, ksplit,
                     slab.data_ptr() if slab is not None else 0, slab.numel() if slab is not None else 0, mv, nv, kv,
-                    am[0], am[1], am[2], am[3], slot_ptr(amax_out))
+                    am[0], am[1], am[2], am[3], slot_ptr(amax_out), tk.data_ptr() if tk is not None else 0)
     return rc == 0
 
 
@@ -855,10 +883,12 @@ def linear_gelu_fwd(x, w, b, planes_out=False, emit_planes=False, out=None, amax
     return y, pre
 
 
-def linear_dgrad_dgelu(dy, w, pre, b, db_acc=None, planes_out=False, amax=None, amax_out=None):
+def linear_dgrad_dgelu(dy, w, pre, b, db_acc=None, planes_out=False, amax=None, amax_out=None, colsum=True):
     """FFN backward through the GELU: dpre = (dy @ w) * gelu'(pre + b), db = colsum(dpre).
 
     ``db`` is accumulated into ``db_acc`` (flat-store view) when given.  Returns (dpre, db);
+    ``colsum=False`` (HIP engine only; else ignored): no db -- returns (dpre, None), the caller sums
+    the bias gradient elsewhere (bert_ops: inside the FFN-in weight-gradient launch);
     ``planes_out`` (fp32 plane engine): dpre as split-bf16 :class:`Planes` (no fp32 copy).
     ``amax`` / ``amax_out``: as in :func:`linear_gelu_fwd` (|max| of dpre into ``amax_out``).
     """
@@ -887,8 +917,9 @@ def linear_dgrad_dgelu(dy, w, pre, b, db_acc=None, planes_out=False, amax=None, 
             amax = (amax_of(dy), amax_of(w))
 
         def run_hip(out_db, acc, amo=None):
-            return _hip_gemm(dy, w, False, False, dpre, b, EPI_DGELU, 0.0, aux=pre, part=part, colsum=out_db,
-                             colsum_acc=acc, amax=amax, amax_out=amo)
+            return _hip_gemm(dy, w, False, False, dpre, b, EPI_DGELU, 0.0, aux=pre,
+                             part=part if out_db is not None else None, colsum=out_db, colsum_acc=acc, amax=amax,
+                             amax_out=amo)
 
         if key not in GEMM_CHOICES and _MODE == "auto":
             scratch_db = torch.zeros_like(db)
@@ -900,8 +931,8 @@ def linear_dgrad_dgelu(dy, w, pre, b, db_acc=None, planes_out=False, amax=None, 
                 GEMM_CHOICES[key] = ("blas", None, None)
             else:
                 _choose(key, lambda: run_hip(scratch_db, True), run_blas)
-        if _choose(key, None, None) == "hip" and run_hip(db, db_acc is not None, amax_out):
-            return dpre, db
+        if _choose(key, None, None) == "hip" and run_hip(db if colsum else None, db_acc is not None, amax_out):
+            return dpre, (db if colsum else None)
     df = torch.mm(dy, w)
     dpre, db = bert_ops.gelu_bwd_colsum(df, pre, b, db_acc=db_acc)
     if amax_out is not None:

@@ -765,6 +765,83 @@ def test_gemm_splitk_deterministic(cuda, engine):
         assert torch.equal(out, first)
 
 
+@pytest.mark.parametrize("engine", ["x6", "h3"])
+@pytest.mark.parametrize("ta,tb,M,N,K,ks", [(1, 0, 768, 3072, 4096, 2), (1, 0, 768, 768, 4096, 4),
+                                            (0, 1, 4096, 768, 3072, 2), (0, 0, 4096, 768, 768, 2),
+                                            (1, 0, 256, 384, 1024, 8)])
+def test_gemm_splitk_inlaunch_matches_reduce_pass(cuda, engine, ta, tb, M, N, K, ks):
+    """The split-K finish inside the launch (last-arriving slice sums the slices: gemm.hip
+    splitk_inlaunch) is bitwise the separate splitk_reduce / reduce_rows passes' result -- plain,
+    accumulating (beta 1), with a bias, with the weight gradient's fused column sums -- and leaves
+    the arrival counters at zero for the next launch."""
+    from hetseq_amd.ops import gemm as G
+
+    gen = torch.Generator(device=cuda).manual_seed(21)
+    a = torch.randn((K, M) if ta else (M, K), device=cuda, generator=gen)
+    b = torch.randn((N, K) if tb else (K, N), device=cuda, generator=gen)
+    bias = torch.randn(N, device=cuda, generator=gen)
+    c0 = torch.randn(M, N, device=cuda, generator=gen)
+    cs0 = torch.randn(M, device=cuda, generator=gen)
+    saved = G._INLAUNCH
+
+    def run(inl, beta, with_bias, wcol):
+        G._INLAUNCH = inl
+        out = c0.clone()
+        kw = dict(fp32=engine, ksplit=ks, beta=beta)
+        if with_bias:
+            kw.update(bias=bias, epi=G.EPI_BIAS)
+        cs = None
+        if wcol:
+            cs = cs0.clone()
+            kw.update(part=torch.empty((ks, M), device=cuda), colsum=cs, colsum_acc=beta != 0.0)
+        assert G._hip_gemm(a, b, ta, tb, out, **kw)
+        return out, cs
+
+    try:
+        cases = [(0.0, False, False), (1.0, False, False)]
+        if (ta, tb) == (0, 1):
+            cases.append((1.0, True, False))
+        if ta:
+            cases += [(1.0, False, True), (0.0, False, True)]
+        for wt in (1, 0):  # write-through slab stores / plain stores + release fence
+            G.hip().set_splitk_wt(wt)
+            for beta, with_bias, wcol in cases:
+                o1, c1 = run(True, beta, with_bias, wcol)
+                o0, c0_ = run(False, beta, with_bias, wcol)
+                assert torch.equal(o1, o0), (wt, beta, with_bias, wcol, (o1 - o0).abs().max().item())
+                if wcol:
+                    assert torch.equal(c1, c0_)
+        ref = (a.t() if ta else a).double() @ (b.t() if tb else b).double()
+        _close(run(True, 0.0, False, False)[0], ref, 1e-5, 1e-4, "splitk in-launch")
+        torch.cuda.synchronize()
+        for t in G._TICKETS.values():
+            assert int(t.abs().sum()) == 0
+    finally:
+        G._INLAUNCH = saved
+        G.hip().set_splitk_wt(1)
+
+
+@pytest.mark.parametrize("engine", ["x6", "h3"])
+def test_gemm_dgelu_without_colsum(cuda, engine):
+    """The dGELU data-gradient epilogue with no column partials (the FFN-in bias gradient then comes
+    from the weight-gradient launch) writes the same dpre, bitwise, as with them."""
+    from hetseq_amd.ops import gemm as G
+
+    gen = torch.Generator(device=cuda).manual_seed(3)
+    T, N, K = 4096, 3072, 768
+    dy = torch.randn(T, K, device=cuda, generator=gen)
+    w = torch.randn(K, N, device=cuda, generator=gen) * 0.05
+    pre = torch.randn(T, N, device=cuda, generator=gen)
+    b = torch.randn(N, device=cuda, generator=gen)
+    out1, out0 = torch.empty(T, N, device=cuda), torch.empty(T, N, device=cuda)
+    db = torch.zeros(N, device=cuda)
+    part = torch.empty((T // 64, N), device=cuda)
+    assert G._hip_gemm(dy, w, 0, 0, out1, b, G.EPI_DGELU, aux=pre, part=part, colsum=db, fp32=engine)
+    assert G._hip_gemm(dy, w, 0, 0, out0, b, G.EPI_DGELU, aux=pre, fp32=engine)
+    assert torch.equal(out0, out1)
+    _close(db, out1.double().sum(0), 1e-5, 1e-3, "dgelu colsum")
+
+
 def _wide_range(shape, cuda, gen, decades):
     """Gradient-like data: N(0,1) values times 10^u, u uniform in [-decades, 0] per ROW (some rows
     ~10^-decades of the tensor's max) and a few 100x outliers."""
