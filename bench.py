@@ -577,6 +577,8 @@ _AB = {
                         __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_splitk_wt(0)),
     "ffnbias_wgrad": lambda: setattr(__import__("hetseq_amd.ops.bert_ops", fromlist=["x"]), "_FFN_BIAS_WGRAD", True),
     "ffnbias_dgelu": lambda: setattr(__import__("hetseq_amd.ops.bert_ops", fromlist=["x"]), "_FFN_BIAS_WGRAD", False),
+    "wcolfold_on": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_wcol_fold(1),
+    "wcolfold_off": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_wcol_fold(0),
     "inl_off": lambda: setattr(__import__("hetseq_amd.ops.gemm", fromlist=["x"]), "_INLAUNCH", False),
     "lazyzero_on": lambda: setattr(__import__("hetseq_amd.controller", fromlist=["x"]), "_LAZY_ZERO", True),
     "lazyzero_off": lambda: setattr(__import__("hetseq_amd.controller", fromlist=["x"]), "_LAZY_ZERO", False),

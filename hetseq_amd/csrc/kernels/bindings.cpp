@@ -89,6 +89,7 @@ int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, i
                 const float* amax_b, int namax_b, float* amax_c, int* tickets);
 int splitk_tickets();
 void set_splitk_wt(int on);
+void set_wcol_fold(int on);
 
 // gemm_planes.hip
 int launch_gemm_planes(int planes, int c_dtype, int ta, int tb, int M, int N, int K, const void* A, int64_t lda,
@@ -595,6 +596,7 @@ PYBIND11_MODULE(_hip, m) {
      pybind11::arg("slab") = 0, pybind11::arg("slab_floats") = 0, pybind11::arg("mv") = 0, pybind11::arg("nv") = 0,
      pybind11::arg("kv") = 0, pybind11::arg("amax_a") = 0, pybind11::arg("namax_a") = 0, pybind11::arg("amax_b") = 0,
      pybind11::arg("namax_b") = 0, pybind11::arg("amax_c") = 0, pybind11::arg("tickets") = 0);
+  m.def("set_wcol_fold", &set_wcol_fold, "weight-gradient bias sums finished by the split-K pass (1) or reduce_rows (0)");
   m.def("set_splitk_wt", &set_splitk_wt, "in-launch split-K slabs: 1 write-through stores, 0 plain + release fence");
   m.def("splitk_tickets", &splitk_tickets,
         "arrival counters a stream's in-launch split-K GEMMs need (an int32 buffer, zeroed once)");

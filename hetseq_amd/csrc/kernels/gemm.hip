@@ -958,13 +958,26 @@ static const int g_x6_dbuf = [] {
   return e && e[0] == '1' ? 1 : 0;
 }();
 
-// split-K finish: C = sum_s slab[s] (+ bias) (+ beta * C), fixed slice order (deterministic)
+// split-K finish: C = sum_s slab[s] (+ bias) (+ beta * C), fixed slice order (deterministic).
+// Blocks past `gmain` (weight gradient with fused column sums, wcol) finish the bias gradient in the
+// same launch: colsum_out[m] (+)= sum_s part[s][m], slices in order -- no separate reduce_rows pass.
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ slab, int ksplit, int M, int N,
                                                             float* __restrict__ C, int64_t ldc,
-                                                            const float* __restrict__ bias, float beta, int Mv, int Nv) {
+                                                            const float* __restrict__ bias, float beta, int Mv, int Nv,
+                                                            int gmain, const float* __restrict__ part,
+                                                            float* __restrict__ colsum_out, int colsum_acc) {
+  if ((int)blockIdx.x >= gmain) {
+    const int m = ((int)blockIdx.x - gmain) * 256 + threadIdx.x;
+    if (m < M) {
+      float t = 0.f;
+      for (int s = 0; s < ksplit; ++s) t += part[(int64_t)s * M + m];
+      colsum_out[m] = colsum_acc ? colsum_out[m] + t : t;
+    }
+    return;
+  }
   const int n4 = N / 4;
   const int64_t total = (int64_t)Mv * n4, plane = (int64_t)M * N;  // rows past Mv are padding: not written
-  for (int64_t u = blockIdx.x * 256ll + threadIdx.x; u < total; u += (int64_t)gridDim.x * 256) {
+  for (int64_t u = blockIdx.x * 256ll + threadIdx.x; u < total; u += (int64_t)gmain * 256) {
     const int m = (int)(u / n4), n = (int)(u % n4) * 4;
     const float* s0 = slab + (int64_t)m * N + n;
     float4 a = *reinterpret_cast<const float4*>(s0);
@@ -1096,12 +1109,26 @@ int launch_split(int tile, int ta, int tb, int epi, const GemmArgs& a, hipStream
 
 using namespace hs;
 
-void launch_splitk_reduce(const float* slab, int ksplit, int M, int N, float* C, int64_t ldc, const float* bias,
-                          float beta, int Mv, int Nv, hipStream_t st) {
+static void launch_splitk_reduce_cols(const float* slab, int ksplit, int M, int N, float* C, int64_t ldc,
+                                      const float* bias, float beta, int Mv, int Nv, hipStream_t st, const float* part,
+                                      float* colsum_out, int colsum_acc) {
   const int64_t n4 = (int64_t)Mv * (N / 4);
   const int grid = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid), dim3(256), 0, st, slab, ksplit, M, N, C, ldc, bias, beta, Mv, Nv);
+  const int gcol = colsum_out ? (M + 255) / 256 : 0;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid + gcol), dim3(256), 0, st, slab, ksplit, M, N, C, ldc, bias, beta,
+                     Mv, Nv, grid, part, colsum_out, colsum_acc);
 }
+// (also called by gemm_planes.hip / gemm_ring.hip)
+void launch_splitk_reduce(const float* slab, int ksplit, int M, int N, float* C, int64_t ldc, const float* bias,
+                          float beta, int Mv, int Nv, hipStream_t st) {
+  launch_splitk_reduce_cols(slab, ksplit, M, N, C, ldc, bias, beta, Mv, Nv, st, nullptr, nullptr, 0);
+}
+// wcol's bias gradient folded into the split-K pass (HETSEQ_WCOL_IN_REDUCE=0: its own reduce_rows)
+static int g_wcol_fold = [] {
+  const char* e = std::getenv("HETSEQ_WCOL_IN_REDUCE");
+  return e && e[0] == '0' ? 0 : 1;
+}();
+void set_wcol_fold(int on) { g_wcol_fold = on ? 1 : 0; }
 
 // Tile choice: the largest tile that still gives >= 2 blocks per CU (256 CUs).
 static int pick_tile(int M, int N) {
@@ -1223,13 +1250,16 @@ int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, i
     rc = launch_split<0>(tile, ta, tb, epi, a, st);
   if (rc != 0) return rc;
   g_last_ks = ks;
-  if (ks > 1 && !keep_slab && !inl) launch_splitk_reduce(slab, ks, M, N, static_cast<float*>(C), ldc, epi >= 1 ? bias : nullptr, beta, a.Mv, a.Nv, st);
+  const bool fold = wcol && !inl && ks > 1 && !keep_slab && g_wcol_fold;  // bias gradient in the split-K pass
+  if (ks > 1 && !keep_slab && !inl)
+    launch_splitk_reduce_cols(slab, ks, M, N, static_cast<float*>(C), ldc, epi >= 1 ? bias : nullptr, beta, a.Mv,
+                              a.Nv, st, fold ? part : nullptr, fold ? colsum_out : nullptr, colsum_acc);
   if (epi == kEpiDGelu && part) {
     const int bm = tile == 2 ? 64 : 128;
     const float* parts[1] = {part};
     float* outs[1] = {colsum_out};
     launch_reduce_rows(parts, outs, 1, M / bm, N, colsum_acc, st);
-  } else if (wcol && !inl) {
+  } else if (wcol && !inl && !fold) {
     const float* parts[1] = {part};
     float* outs[1] = {colsum_out};
     launch_reduce_rows(parts, outs, 1, ks, M, colsum_acc, st);

@@ -811,6 +811,10 @@ def test_gemm_splitk_inlaunch_matches_reduce_pass(cuda, engine, ta, tb, M, N, K,
                 assert torch.equal(o1, o0), (wt, beta, with_bias, wcol, (o1 - o0).abs().max().item())
                 if wcol:
                     assert torch.equal(c1, c0_)
+                    G.hip().set_wcol_fold(0)  # the bias gradient by its own reduce_rows pass
+                    o2, c2 = run(False, beta, with_bias, wcol)
+                    G.hip().set_wcol_fold(1)
+                    assert torch.equal(o2, o0) and torch.equal(c2, c0_)
         ref = (a.t() if ta else a).double() @ (b.t() if tb else b).double()
         _close(run(True, 0.0, False, False)[0], ref, 1e-5, 1e-4, "splitk in-launch")
         torch.cuda.synchronize()
