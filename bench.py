@@ -579,6 +579,8 @@ _AB = {
     "ffnbias_dgelu": lambda: setattr(__import__("hetseq_amd.ops.bert_ops", fromlist=["x"]), "_FFN_BIAS_WGRAD", False),
     "wcolfold_on": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_wcol_fold(1),
     "wcolfold_off": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_wcol_fold(0),
+    "chain_on": lambda: setattr(__import__("hetseq_amd.runtime.streams", fromlist=["x"]), "FWD_CHAIN", True),
+    "chain_off": lambda: setattr(__import__("hetseq_amd.runtime.streams", fromlist=["x"]), "FWD_CHAIN", False),
     "inl_off": lambda: setattr(__import__("hetseq_amd.ops.gemm", fromlist=["x"]), "_INLAUNCH", False),
     "lazyzero_on": lambda: setattr(__import__("hetseq_amd.controller", fromlist=["x"]), "_LAZY_ZERO", True),
     "lazyzero_off": lambda: setattr(__import__("hetseq_amd.controller", fromlist=["x"]), "_LAZY_ZERO", False),

@@ -743,11 +743,16 @@ class BertModel(BertPreTrainedModel):
         x = self.embeddings.fused(input_ids, token_type_ids, self.compute_dtype,
                                   amax=pool.act(0) if pool is not None else None)
         range_pop()
-        for i, blk in enumerate(self.encoder.layer):
-            range_push("layer%d" % i)
-            x = blk.fused(x, mask, B, S, recompute=checkpoint_activations,
-                          amax=plan[i] if plan is not None else None)
-            range_pop()
+        from hetseq_amd.runtime import streams
+
+        # the two half-batch chains of the split forward meet only after the last layer (the
+        # tensors the second chain reads are kept alive until then: streams.chain_keep)
+        with streams.fwd_chain(x.device, on=x.is_cuda):
+            for i, blk in enumerate(self.encoder.layer):
+                range_push("layer%d" % i)
+                x = blk.fused(x, mask, B, S, recompute=checkpoint_activations,
+                              amax=plan[i] if plan is not None else None)
+                range_pop()
         return x
 
     def fused_forward(self, input_ids, token_type_ids, attention_mask, checkpoint_activations=False):

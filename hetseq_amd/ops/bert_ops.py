@@ -499,6 +499,8 @@ def _layer_forward_split(x, mask, W, cfg, save, am=None):
                  else G.linear_fwd(f1[r], W.w2, ksplit=_FWD_KS, amax=w2_am))
             ln_fwd(o, W.g2, W.bb2, eps, bias=W.b2, resid=h1[r], p=p_h, mode=1, seed=s_2, off=o_2, row0=h * hr,
                    outs=(h2[r], z2[r], m2[r], r2[r]), amax=sl(6))
+    # (inside a fwd_chain the second half may still read these after the return)
+    streams.chain_keep(x, mask, qkv, ctx_, lse, dmask, h1, z1, m1, r1, f1, f1pre, h2, z2, m2, r2)
     if save:
         return h2, (qkv, ctx_, lse, dmask, z1, m1, r1, h1, f1pre, f1, z2, m2, r2, x, ctx_)
     return h2, None
@@ -512,6 +514,7 @@ def _layer_forward(x, mask, W, cfg, save, am=None):
     gradients of the backward."""
     if _fwd_split_ok(x, mask, W, cfg):
         return _layer_forward_split(x, mask, W, cfg, save, am)
+    streams.chain_join(x.device)  # one chain from here: the half-batch chains meet first
     B, S, NH, p_h, p_a, eps, seeds = cfg
     (s_a, o_a), (s_1, o_1), (s_2, o_2) = seeds
     pl = getattr(W, "planes", False)

@@ -121,10 +121,61 @@ def role(stream_handle: int) -> str:
 # fills most of that bubble (profiles/r3_forks.md).
 
 
+# Half-batch chains that run through several layers without meeting (:class:`fwd_chain`): each
+# half only reads its own rows, so the two streams need to meet once before the first layer and
+# once after the last, not at every layer boundary (where the faster half idles until the slower
+# one's LayerNorm ends, and each meeting costs an event round trip).  HETSEQ_FWD_CHAIN=0: meet at
+# every layer.
+FWD_CHAIN = os.environ.get("HETSEQ_FWD_CHAIN", "1") == "1"
+_chain = {"depth": 0, "forked": None, "keep": []}
+
+
+class fwd_chain(object):
+    """``with fwd_chain(dev): <layers>`` -- the :class:`fwd_halves` blocks inside fork the second
+    half-batch chain once and do not join it; on exit (or at :func:`chain_join`) the current stream
+    waits for it.  Only for layers whose whole-batch tensors outlive the block (saved for the
+    backward): the second chain may still read them after a layer returns."""
+
+    def __init__(self, device, on=True):
+        self.device = device
+        self.on = on and FWD_CHAIN
+
+    def __enter__(self):
+        if self.on:
+            _chain["depth"] += 1
+        return self
+
+    def __exit__(self, *exc):
+        if self.on:
+            _chain["depth"] -= 1
+            if _chain["depth"] == 0:
+                chain_join(self.device)
+        return False
+
+
+def chain_join(device):
+    """The current stream waits for an open half-batch chain (no-op when none is forked); the tensors
+    the chain kept alive (:func:`chain_keep`) are released after the wait."""
+    st = _chain["forked"]
+    if st is not None:
+        from hetseq_amd.ops._C import hip, stream_handle
+
+        _chain["forked"] = None
+        hip().stream_wait(stream_handle(), st.cuda_stream)
+    _chain["keep"].clear()
+
+
+def chain_keep(*tensors):
+    """Keep tensors the second chain reads alive until it is joined (no-op outside a chain)."""
+    if _chain["forked"] is not None:
+        _chain["keep"].extend(t for t in tensors if t is not None)
+
+
 class fwd_halves(object):
     """``with fwd_halves(dev) as halves: for h in halves: ...`` -- iteration 0 on the current stream,
     iteration 1 on :func:`fwd2` (forked from the current stream with an event wait); on exit the
-    current stream waits for fwd2.  Tensors the second half allocates come from fwd2's pool."""
+    current stream waits for fwd2 -- unless inside a :class:`fwd_chain`, which forks once and joins
+    at its end.  Tensors the second half allocates come from fwd2's pool."""
 
     def __init__(self, device):
         self.device = device
@@ -134,7 +185,11 @@ class fwd_halves(object):
         from hetseq_amd.ops._C import hip, stream_handle
 
         self.st = fwd2(self.device)
-        hip().stream_wait(self.st.cuda_stream, stream_handle())
+        self.chained = _chain["depth"] > 0
+        if not (self.chained and _chain["forked"] is self.st):
+            hip().stream_wait(self.st.cuda_stream, stream_handle())
+            if self.chained:
+                _chain["forked"] = self.st
         self.gen = self._halves()
         return self.gen
 
@@ -152,7 +207,10 @@ class fwd_halves(object):
         from hetseq_amd.ops._C import hip, stream_handle
 
         self.gen.close()  # restores the current stream if the loop left early
-        hip().stream_wait(stream_handle(), self.st.cuda_stream)
+        if not self.chained or exc[0] is not None:
+            _chain["forked"] = None
+            hip().stream_wait(stream_handle(), self.st.cuda_stream)
+            _chain["keep"].clear()
         return False
 
 
