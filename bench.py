@@ -506,7 +506,26 @@ def _set_site_ks(key, ks):
 
 
 # runtime variants for --ab (switches that take effect on the next step without a rebuild)
+_HI_STREAM = []
+
+
+def _compute_stream(high):
+    """bench --ab cprio_hi / cprio_def: run the step on a high-priority stream (the data-gradient chain's
+    blocks dispatched ahead of the weight-gradient stream's) or on the default stream."""
+    import torch
+
+    torch.cuda.synchronize()
+    if high:
+        if not _HI_STREAM:
+            _HI_STREAM.append(torch.cuda.Stream(priority=-1))
+        torch.cuda.set_stream(_HI_STREAM[0])
+    else:
+        torch.cuda.set_stream(torch.cuda.default_stream())
+
+
 _AB = {
+    "cprio_hi": lambda: _compute_stream(True),
+    "cprio_def": lambda: _compute_stream(False),
     "dks1": lambda: _set_flag("hetseq_amd.runtime.streams", "DGRAD_KSPLIT", 1),  # data-gradient K split
     "dks2": lambda: _set_flag("hetseq_amd.runtime.streams", "DGRAD_KSPLIT", 2),
     "fks_auto": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FWD_KS", None),  # forward chains' K split
