@@ -600,6 +600,8 @@ _AB = {
     "wcolfold_off": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_wcol_fold(0),
     "chain_on": lambda: setattr(__import__("hetseq_amd.runtime.streams", fromlist=["x"]), "FWD_CHAIN", True),
     "chain_off": lambda: setattr(__import__("hetseq_amd.runtime.streams", fromlist=["x"]), "FWD_CHAIN", False),
+    "wamax_split": lambda: setattr(__import__("hetseq_amd.ops.gemm", fromlist=["x"]), "_SPLIT_WEIGHT_AMAX", True),
+    "wamax_inline": lambda: setattr(__import__("hetseq_amd.ops.gemm", fromlist=["x"]), "_SPLIT_WEIGHT_AMAX", False),
     "inl_off": lambda: setattr(__import__("hetseq_amd.ops.gemm", fromlist=["x"]), "_INLAUNCH", False),
     "lazyzero_on": lambda: setattr(__import__("hetseq_amd.controller", fromlist=["x"]), "_LAZY_ZERO", True),
     "lazyzero_off": lambda: setattr(__import__("hetseq_amd.controller", fromlist=["x"]), "_LAZY_ZERO", False),

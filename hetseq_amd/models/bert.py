@@ -717,7 +717,7 @@ class BertModel(BertPreTrainedModel):
             return None, None
         weights = [w for W in Ws for w in (W.wqkv, W.wo, W.w1, W.w2)] + list(extra_weights)
         L, NS = len(Ws), LayerAmax.NS
-        pool = G.AmaxPool(weights, 2 + L * NS + extra_slots, self.embeddings.word_embeddings.weight.device)
+        pool = G.AmaxPool(weights, 2 + L * NS + extra_slots, self.embeddings.word_embeddings.weight.device, split=4)
         plan = []
         for i in range(L):
             la = LayerAmax()
@@ -749,10 +749,14 @@ class BertModel(BertPreTrainedModel):
         # tensors the second chain reads are kept alive until then: streams.chain_keep)
         with streams.fwd_chain(x.device, on=x.is_cuda):
             for i, blk in enumerate(self.encoder.layer):
+                if i == 1 and pool is not None:
+                    pool.wait_rest()  # layers >= 1 read weight |max| measured on the side stream
                 range_push("layer%d" % i)
                 x = blk.fused(x, mask, B, S, recompute=checkpoint_activations,
                               amax=plan[i] if plan is not None else None)
                 range_pop()
+        if pool is not None:
+            pool.wait_rest()  # (one-layer models: the head's weights)
         return x
 
     def fused_forward(self, input_ids, token_type_ids, attention_mask, checkpoint_activations=False):

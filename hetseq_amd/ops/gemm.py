@@ -970,6 +970,19 @@ def _seg_table(ts):
     return hit
 
 
+# weight |max| of all but the first layer measured on the weight-gradient stream (idle at the start
+# of the forward) beside the first layer's work (HETSEQ_SPLIT_WEIGHT_AMAX=0: all at once, in line)
+_SPLIT_WEIGHT_AMAX = os.environ.get("HETSEQ_SPLIT_WEIGHT_AMAX", "1") == "1"
+_REST_EVENTS: dict = {}
+
+
+def _rest_event(device):
+    ev = _REST_EVENTS.get(device)
+    if ev is None:
+        ev = _REST_EVENTS[device] = torch.cuda.Event()
+    return ev
+
+
 class AmaxPool(object):
     """|max| slots of one forward + backward on the h3 engine (zeroed once, 1 launch):
 
@@ -981,13 +994,34 @@ class AmaxPool(object):
     Each slot has exactly one producer stream, and its consumers are ordered after that producer,
     so the scales -- and the results -- are deterministic."""
 
-    def __init__(self, weights, n_act, device):
+    def __init__(self, weights, n_act, device, split=0):
         self.nw = len(weights)
         self.buf = torch.zeros((self.nw + n_act) * SLOT_FLOATS, dtype=torch.float32, device=device)
         self.ptr = self.buf.data_ptr()
-        if weights:
+        self.rest = None
+        from hetseq_amd.runtime import streams
+
+        if 0 < split < len(weights) and _SPLIT_WEIGHT_AMAX and streams.enabled() and self.buf.is_cuda:
+            # weights [0, split) now; the rest on the side stream, beside the first layer's work
+            # (consumers on the current stream call wait_rest() first; the side stream's own later
+            # work is ordered after it)
+            base, tab, nblk = _seg_table(weights[:split])
+            hip().amax_seg(base, tab.data_ptr(), nblk, self.ptr, stream_handle())
+            base, tab, nblk = _seg_table(weights[split:])
+            st = streams.side(self.buf.device)
+            hip().stream_wait(st.cuda_stream, stream_handle())
+            hip().amax_seg(base, tab.data_ptr(), nblk, self.ptr + 4 * SLOT_FLOATS * split, st.cuda_stream)
+            self.rest = _rest_event(self.buf.device)
+            self.rest.record(st)
+        elif weights:
             base, tab, nblk = _seg_table(weights)
             hip().amax_seg(base, tab.data_ptr(), nblk, self.ptr, stream_handle())
+
+    def wait_rest(self):
+        """The current stream waits for the side-stream part of the weight |max| (no-op without one)."""
+        if self.rest is not None:
+            torch.cuda.current_stream(self.buf.device).wait_event(self.rest)
+            self.rest = None
 
     # slots are (pointer, count) tuples: plain ints, so the ~150 uses per step cost no tensor views
     def w(self, i):
