@@ -602,6 +602,9 @@ _AB = {
     "chain_off": lambda: setattr(__import__("hetseq_amd.runtime.streams", fromlist=["x"]), "FWD_CHAIN", False),
     "wamax_split": lambda: setattr(__import__("hetseq_amd.ops.gemm", fromlist=["x"]), "_SPLIT_WEIGHT_AMAX", True),
     "wamax_inline": lambda: setattr(__import__("hetseq_amd.ops.gemm", fromlist=["x"]), "_SPLIT_WEIGHT_AMAX", False),
+    "fwdks_auto": lambda: setattr(__import__("hetseq_amd.ops.bert_ops", fromlist=["x"]), "_FWD_KS", None),
+    "fwdks_1": lambda: setattr(__import__("hetseq_amd.ops.bert_ops", fromlist=["x"]), "_FWD_KS", 1),
+    "fwdks_2": lambda: setattr(__import__("hetseq_amd.ops.bert_ops", fromlist=["x"]), "_FWD_KS", 2),
     "inl_off": lambda: setattr(__import__("hetseq_amd.ops.gemm", fromlist=["x"]), "_INLAUNCH", False),
     "lazyzero_on": lambda: setattr(__import__("hetseq_amd.controller", fromlist=["x"]), "_LAZY_ZERO", True),
     "lazyzero_off": lambda: setattr(__import__("hetseq_amd.controller", fromlist=["x"]), "_LAZY_ZERO", False),
