@@ -676,6 +676,33 @@ def test_embedding_backward_bitwise_deterministic(cuda):
             assert torch.equal(a, c)
 
 
+@pytest.mark.parametrize("V,ld", [(30522, 30720), (4099, 4104), (1024, 1024), (1025, 1028)])
+def test_cross_entropy_aligned_rows(cuda, V, ld):
+    """fp32 logits whose rows start 16-B aligned (the MLM decoder's padded buffer) take the float4
+    kernels: loss, logsumexp and the in-place dlogits against PyTorch in fp64, a few rows shifted
+    by +-40 (online max), the pad columns untouched."""
+    from hetseq_amd.ops import bert_ops as B
+
+    gen = torch.Generator(device=cuda).manual_seed(4)
+    rows = 160
+    buf = torch.randn(rows, ld, device=cuda, generator=gen)
+    buf[::7] += 40.0
+    buf[3::11] -= 40.0
+    pad = buf[:, V:].clone()
+    x = buf[:, :V]
+    lab = torch.randint(0, V, (rows,), device=cuda, generator=gen)
+    lab[::5] = -1
+    xd = x.double().clone().requires_grad_()
+    ref = F.cross_entropy(xd, lab, ignore_index=-1)
+    ref.backward()
+    stats, lse = B.xent_fwd(x, lab)  # stats = (mean loss, valid rows)
+    _close(stats[0], ref, 1e-5, 1e-6, "xent fwd")
+    _close(lse, torch.logsumexp(x.double(), 1), 1e-6, 1e-5, "lse")
+    B.xent_bwd_(x, lab, lse, torch.ones(1, device=cuda), stats)
+    _close(x, xd.grad, 1e-4, 1e-9, "xent bwd")
+    assert torch.equal(buf[:, V:], pad)
+
+
 def test_cross_entropy(cuda):
     from hetseq_amd.ops.bert_ops import cross_entropy
 
