@@ -605,6 +605,8 @@ _AB = {
     "fwdks_auto": lambda: setattr(__import__("hetseq_amd.ops.bert_ops", fromlist=["x"]), "_FWD_KS", None),
     "fwdks_1": lambda: setattr(__import__("hetseq_amd.ops.bert_ops", fromlist=["x"]), "_FWD_KS", 1),
     "fwdks_2": lambda: setattr(__import__("hetseq_amd.ops.bert_ops", fromlist=["x"]), "_FWD_KS", 2),
+    "poolw_side": lambda: setattr(__import__("hetseq_amd.ops.bert_ops", fromlist=["x"]), "_POOL_WGRAD_SIDE", True),
+    "poolw_inline": lambda: setattr(__import__("hetseq_amd.ops.bert_ops", fromlist=["x"]), "_POOL_WGRAD_SIDE", False),
     "inl_off": lambda: setattr(__import__("hetseq_amd.ops.gemm", fromlist=["x"]), "_INLAUNCH", False),
     "lazyzero_on": lambda: setattr(__import__("hetseq_amd.controller", fromlist=["x"]), "_LAZY_ZERO", True),
     "lazyzero_off": lambda: setattr(__import__("hetseq_amd.controller", fromlist=["x"]), "_LAZY_ZERO", False),

@@ -61,7 +61,9 @@ int launch_pool_nsp_fwd(int, const void*, int, int, int, const float*, const flo
                         const int64_t*, const float*, float*, float*, float*, float*, float*, hipStream_t);
 int launch_pool_nsp_bwd(int, const float*, const void*, void*, int, int, int, const float*, const float*,
                         const int64_t*, const float*, const float*, const float*, const float*, float*, float*,
-                        float*, float*, float*, float*, float*, int, hipStream_t);
+                        float*, float*, float*, float*, float*, int, hipStream_t, int);
+void launch_pool_nsp_wgrad(int, const void*, const float*, const float*, const float*, int, int, int, float*, float*,
+                           float*, float*, int, hipStream_t);
 // attention.hip
 void set_attn_fp32_mode(int mode);
 void set_attn_bwd_x6_planes(int on);
@@ -418,15 +420,28 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("pool_nsp_bwd", [](int dt, i64 dloss, i64 seq, i64 dseq, int B, int S, int H, i64 Wp, i64 Wn, i64 label,
                            i64 pooled, i64 logits, i64 lse, i64 stats, i64 dlogits, i64 dpre, i64 part, i64 dWp,
-                           i64 dbp, i64 dWn, i64 dbn, int accumulate, i64 st) {
+                           i64 dbp, i64 dWn, i64 dbn, int accumulate, i64 st, int with_wgrad) {
     pre_launch("pool_nsp_bwd");
     check(launch_pool_nsp_bwd(dt, P(const float*, dloss), P(const void*, seq), P(void*, dseq), B, S, H,
                               P(const float*, Wp), P(const float*, Wn), P(const int64_t*, label),
                               P(const float*, pooled), P(const float*, logits), P(const float*, lse),
                               P(const float*, stats), P(float*, dlogits), P(float*, dpre), P(float*, part),
                               P(float*, dWp),
-                              P(float*, dbp), P(float*, dWn), P(float*, dbn), accumulate, ST(st)),
+                              P(float*, dbp), P(float*, dWn), P(float*, dbn), accumulate, ST(st), with_wgrad),
           "pool_nsp_bwd");
+  }, pybind11::arg("dt"), pybind11::arg("dloss"), pybind11::arg("seq"), pybind11::arg("dseq"), pybind11::arg("B"),
+     pybind11::arg("S"), pybind11::arg("H"), pybind11::arg("Wp"), pybind11::arg("Wn"), pybind11::arg("label"),
+     pybind11::arg("pooled"), pybind11::arg("logits"), pybind11::arg("lse"), pybind11::arg("stats"),
+     pybind11::arg("dlogits"), pybind11::arg("dpre"), pybind11::arg("part"), pybind11::arg("dWp"), pybind11::arg("dbp"),
+     pybind11::arg("dWn"), pybind11::arg("dbn"), pybind11::arg("accumulate"), pybind11::arg("st"),
+     pybind11::arg("with_wgrad") = 1);
+  m.def("pool_nsp_wgrad", [](int dt, i64 seq, i64 dpre, i64 dlogits, i64 pooled, int B, int S, int H, i64 dWp, i64 dbp,
+                             i64 dWn, i64 dbn, int accumulate, i64 st) {
+    pre_launch("pool_nsp_wgrad");
+    launch_pool_nsp_wgrad(dt, P(const void*, seq), P(const float*, dpre), P(const float*, dlogits),
+                          P(const float*, pooled), B, S, H, P(float*, dWp), P(float*, dbp), P(float*, dWn),
+                          P(float*, dbn), accumulate, ST(st));
+    check_launch("pool_nsp_wgrad");
   });
   m.def("colsum_row_chunks", &colsum_row_chunks);
   m.def("colsum", [](int dt, i64 dy, i64 x, i64 b, i64 dx, i64 part, i64 out, i64 rows, int N, int accumulate, i64 st) {

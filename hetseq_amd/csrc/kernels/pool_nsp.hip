@@ -315,25 +315,35 @@ int launch_pool_nsp_fwd(int dtype, const void* seq, int B, int S, int H, const f
   return 0;
 }
 
+// the pooler / NSP parameter gradients alone (after the backward's nsp_bwd wrote dpre / dlogits):
+// the fused BERT head runs them on the weight-gradient stream, off the data-gradient chain
+void launch_pool_nsp_wgrad(int dtype, const void* seq, const float* dpre, const float* dlogits, const float* pooled,
+                           int B, int S, int H, float* dWp, float* dbp, float* dWn, float* dbn, int accumulate,
+                           hipStream_t st) {
+  if (dtype == 0)
+    hipLaunchKernelGGL(pool_nsp_wgrad_kernel<float>, dim3(H / kWgRows + 2), dim3(kPoolThreads), 0, st,
+                       (const float*)seq, dpre, dlogits, pooled, B, S, H, dWp, dbp, dWn, dbn, accumulate);
+  else
+    hipLaunchKernelGGL(pool_nsp_wgrad_kernel<bf16_t>, dim3(H / kWgRows + 2), dim3(kPoolThreads), 0, st,
+                       (const bf16_t*)seq, dpre, dlogits, pooled, B, S, H, dWp, dbp, dWn, dbn, accumulate);
+}
+
 // scratch: dlogits [B, 2], dpre [B, H], part [B, 8, H] floats
 int launch_pool_nsp_bwd(int dtype, const float* dloss, const void* seq, void* dseq, int B, int S, int H,
                         const float* Wp, const float* Wn, const int64_t* label, const float* pooled,
                         const float* logits, const float* lse, const float* stats, float* dlogits, float* dpre,
                         float* part, float* dWp, float* dbp, float* dWn, float* dbn, int accumulate,
-                        hipStream_t st) {
+                        hipStream_t st, int with_wgrad) {
   if (B <= 0 || H <= 0 || H % 4 || H > 1024 || H % (kChunks * 4)) return -1;
   hipLaunchKernelGGL(nsp_bwd_kernel, dim3(B), dim3(kPoolThreads), 0, st, dloss, logits, lse, label, stats, pooled, Wn,
                      H, dlogits, dpre);
   hipLaunchKernelGGL(pool_dx_partial_kernel, dim3(kChunks, (B + kDxSeqs - 1) / kDxSeqs), dim3(kDxThreads),
                      (kDxThreads / 64) * (size_t)H * sizeof(float), st, dpre, Wp, B, H, part);
-  if (dtype == 0) {
+  if (dtype == 0)
     hipLaunchKernelGGL(pool_dx_finish_kernel<float>, dim3(B), dim3(kPoolThreads), 0, st, part, S, H, (float*)dseq);
-    hipLaunchKernelGGL(pool_nsp_wgrad_kernel<float>, dim3(H / kWgRows + 2), dim3(kPoolThreads), 0, st, (const float*)seq, dpre,
-                       dlogits, pooled, B, S, H, dWp, dbp, dWn, dbn, accumulate);
-  } else {
+  else
     hipLaunchKernelGGL(pool_dx_finish_kernel<bf16_t>, dim3(B), dim3(kPoolThreads), 0, st, part, S, H, (bf16_t*)dseq);
-    hipLaunchKernelGGL(pool_nsp_wgrad_kernel<bf16_t>, dim3(H / kWgRows + 2), dim3(kPoolThreads), 0, st, (const bf16_t*)seq,
-                       dpre, dlogits, pooled, B, S, H, dWp, dbp, dWn, dbn, accumulate);
-  }
+  if (with_wgrad)
+    launch_pool_nsp_wgrad(dtype, seq, dpre, dlogits, pooled, B, S, H, dWp, dbp, dWn, dbn, accumulate, st);
   return 0;
 }

@@ -38,6 +38,8 @@ _WGRAD_COLSUM = os.environ.get("HETSEQ_WGRAD_COLSUM", "1") == "1"
 # instead of the dGELU data-gradient epilogue's column partials + a reduce pass on the compute stream
 # (HETSEQ_FFN_BIAS_WGRAD=0: in the dGELU epilogue)
 _FFN_BIAS_WGRAD = os.environ.get("HETSEQ_FFN_BIAS_WGRAD", "1") == "1"
+# the pooler / NSP parameter gradients on the weight-gradient stream (HETSEQ_POOL_WGRAD_SIDE=0: in line)
+_POOL_WGRAD_SIDE = os.environ.get("HETSEQ_POOL_WGRAD_SIDE", "1") == "1"
 # weight gradients store (beta 0) in the first backward after zero_grad (HETSEQ_FRESH_WGRAD=0: always add)
 _FRESH_WGRAD = os.environ.get("HETSEQ_FRESH_WGRAD", "1") == "1"
 from hetseq_amd.ops._C import dtype_code, hip, stream_handle
@@ -905,7 +907,16 @@ class FusedPreTrainingLoss(torch.autograd.Function):
                            wp.data_ptr(), wn.data_ptr(), nsp_labels.data_ptr(), pooled.data_ptr(),
                            nsp_logits.data_ptr(), nsp_lse.data_ptr(), stats.data_ptr(), dnsp.data_ptr(),
                            dpre.data_ptr(), part.data_ptr(), dWp.data_ptr(), dbp.data_ptr(), dWn.data_ptr(),
-                           dbn.data_ptr(), int(acc), stream_handle())
+                           dbn.data_ptr(), int(acc), stream_handle(), with_wgrad=0)
+
+        def pool_wgrad():  # the pooler / NSP parameter gradients: off the data-gradient chain
+            hip().pool_nsp_wgrad(dtype_code(seq), seq.data_ptr(), dpre.data_ptr(), dnsp.data_ptr(), pooled.data_ptr(),
+                                 B, S, H, dWp.data_ptr(), dbp.data_ptr(), dWn.data_ptr(), dbn.data_ptr(), int(acc),
+                                 stream_handle())
+        if side and _POOL_WGRAD_SIDE:
+            streams.run(dev, pool_wgrad, seq, scratch, pooled, dWp, dbp, dWn, dbn)
+        else:
+            pool_wgrad()
         if acc:
             return (dseq,) + (None,) * 13
         return (dseq, None, None, None, dWt, dbt, dg, db, dWdec, dbdec, dWp, dbp, dWn, dbn)
