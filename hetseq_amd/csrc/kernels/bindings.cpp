@@ -80,7 +80,7 @@ int launch_attn_bwd(int, const void*, const int64_t*, const float*, const void*,
 // xent.hip
 void launch_xent_fwd(int, const void*, const int64_t*, int, int, int64_t, int, float*, float*, float*, hipStream_t);
 void launch_xent_bwd(int, void*, const int64_t*, const float*, int, int, int64_t, int, const float*, const float*,
-                     hipStream_t);
+                     hipStream_t, float*);
 // gemm.hip
 int gemm_last_ksplit();
 void set_h3_occ3(int on);
@@ -540,12 +540,14 @@ PYBIND11_MODULE(_hip, m) {
     check_launch("xent_fwd");
   });
   m.def("xent_bwd", [](int dt, i64 logits, i64 labels, i64 lse, int rows, int V, i64 ldv, int ignore, i64 dloss,
-                       i64 stats, i64 st) {
+                       i64 stats, i64 st, i64 amax) {
     pre_launch("xent_bwd");
     launch_xent_bwd(dt, P(void*, logits), P(const int64_t*, labels), P(const float*, lse), rows, V, ldv, ignore,
-                    P(const float*, dloss), P(const float*, stats), ST(st));
+                    P(const float*, dloss), P(const float*, stats), ST(st), P(float*, amax));
     check_launch("xent_bwd");
-  });
+  }, pybind11::arg("dt"), pybind11::arg("logits"), pybind11::arg("labels"), pybind11::arg("lse"), pybind11::arg("rows"),
+     pybind11::arg("V"), pybind11::arg("ldv"), pybind11::arg("ignore"), pybind11::arg("dloss"), pybind11::arg("stats"),
+     pybind11::arg("st"), pybind11::arg("amax") = 0);
 
   // returns 0 when launched, -1 when the shape/epilogue is not served (caller falls back)
   m.def("set_seed_ptr", [](i64 ptr) { hs::g_seed_dev = reinterpret_cast<const uint64_t*>(ptr); });

@@ -91,18 +91,22 @@ __global__ void xent_reduce_kernel(const float* __restrict__ row_loss, const int
 template <typename T>
 __global__ void __launch_bounds__(256) xent_bwd_kernel(T* __restrict__ logits, const int64_t* __restrict__ labels,
                                                        const float* __restrict__ lse, int V, int64_t ldv, int ignore,
-                                                       const float* __restrict__ dloss, const float* __restrict__ stats) {
+                                                       const float* __restrict__ dloss, const float* __restrict__ stats,
+                                                       float* __restrict__ amax) {
   const int row = blockIdx.x;
   const int64_t lab = labels[row];
   T* x = logits + (int64_t)row * ldv;
   const bool valid = !(lab == ignore || lab < 0 || lab >= V);
   const float g = valid ? dloss[0] / stats[1] : 0.f;
   const float L = lse[row];
+  uint32_t mb = 0u;
   for (int i = threadIdx.x; i < V; i += blockDim.x) {
     const float pr = __expf(to_f(x[i]) - L);
     const float d = valid ? g * (pr - (i == lab ? 1.f : 0.f)) : 0.f;
+    mb = amax_bits(mb, d);
     x[i] = from_f<T>(d);
   }
+  if (amax) amax_commit(amax, mb);  // (block-uniform: every lane of every wave reaches it)
 }
 
 // fp32 rows with 16-B aligned starts (ldv % 4 == 0): float4 loads, two independent (max, sum)
@@ -175,7 +179,7 @@ __global__ void __launch_bounds__(256) xent_bwd_vec_kernel(float* __restrict__ l
                                                            const int64_t* __restrict__ labels,
                                                            const float* __restrict__ lse, int V, int64_t ldv,
                                                            int ignore, const float* __restrict__ dloss,
-                                                           const float* __restrict__ stats) {
+                                                           const float* __restrict__ stats, float* __restrict__ amax) {
   const int row = blockIdx.x;
   const int64_t lab = labels[row];
   float* x = logits + (int64_t)row * ldv;
@@ -184,7 +188,12 @@ __global__ void __launch_bounds__(256) xent_bwd_vec_kernel(float* __restrict__ l
   const float g = valid ? dloss[0] / stats[1] : 0.f;
   const float L = lse[row];
   const int n4 = V >> 2, bd = blockDim.x;
-  auto grad = [&](float v, int idx) { return valid ? g * (__expf(v - L) - (idx == lab ? 1.f : 0.f)) : 0.f; };
+  uint32_t mb = 0u;  // |max| of the written gradient (the decoder products' operand scale)
+  auto grad = [&](float v, int idx) {
+    const float d = valid ? g * (__expf(v - L) - (idx == lab ? 1.f : 0.f)) : 0.f;
+    mb = amax_bits(mb, d);
+    return d;
+  };
   int i = threadIdx.x;
   for (; i + bd < n4; i += 2 * bd) {
     const float4 a = x4[i], b = x4[i + bd];
@@ -199,6 +208,7 @@ __global__ void __launch_bounds__(256) xent_bwd_vec_kernel(float* __restrict__ l
   }
   const int t = (n4 << 2) + threadIdx.x;
   if (t < V) x[t] = grad(x[t], t);
+  if (amax) amax_commit(amax, mb);
 }
 
 }  // namespace hs
@@ -225,17 +235,18 @@ void launch_xent_fwd(int dtype, const void* logits, const int64_t* labels, int r
   hipLaunchKernelGGL(xent_reduce_kernel, dim3(1), dim3(1024), 0, st, row_loss, labels, rows, V, ignore, out);
 }
 
+// amax (optional, a zeroed |max| slot): |max| of the written dlogits
 void launch_xent_bwd(int dtype, void* logits, const int64_t* labels, const float* lse, int rows, int V, int64_t ldv,
-                     int ignore, const float* dloss, const float* stats, hipStream_t st) {
+                     int ignore, const float* dloss, const float* stats, hipStream_t st, float* amax) {
   if (rows <= 0) return;
   const int threads = V >= 1024 ? 256 : 64;
   if (dtype == 0 && xent_vec_ok(logits, ldv, threads))
     hipLaunchKernelGGL(xent_bwd_vec_kernel, dim3(rows), dim3(threads), 0, st, (float*)logits, labels, lse, V, ldv,
-                       ignore, dloss, stats);
+                       ignore, dloss, stats, amax);
   else if (dtype == 0)
     hipLaunchKernelGGL(xent_bwd_kernel<float>, dim3(rows), dim3(threads), 0, st, (float*)logits, labels, lse, V, ldv,
-                       ignore, dloss, stats);
+                       ignore, dloss, stats, amax);
   else
     hipLaunchKernelGGL(xent_bwd_kernel<bf16_t>, dim3(rows), dim3(threads), 0, st, (bf16_t*)logits, labels, lse, V, ldv,
-                       ignore, dloss, stats);
+                       ignore, dloss, stats, amax);
 }

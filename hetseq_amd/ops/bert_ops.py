@@ -732,10 +732,12 @@ def xent_fwd(logits, labels, ignore_index=-1):
     return out, lse
 
 
-def xent_bwd_(logits, labels, lse, dloss, stats, ignore_index=-1):
+def xent_bwd_(logits, labels, lse, dloss, stats, ignore_index=-1, amax=None):
+    """dlogits in place; ``amax``: a zeroed |max| slot the kernel maxes the written values into."""
     rows, V = logits.shape
     hip().xent_bwd(dtype_code(logits), logits.data_ptr(), labels.data_ptr(), lse.data_ptr(), rows, V,
-                   logits.stride(0), ignore_index, dloss.data_ptr(), stats.data_ptr(), stream_handle())
+                   logits.stride(0), ignore_index, dloss.data_ptr(), stats.data_ptr(), stream_handle(),
+                   amax=G.slot_ptr(amax))
     return logits
 
 
@@ -826,7 +828,9 @@ class FusedPreTrainingLoss(torch.autograd.Function):
         Gv = sink() if sink is not None else None  # (wt, bt, g, b, wdec, bdec, wp, bp, wn, bn) flat-store views
         acc = Gv is not None
         dloss = dloss.reshape(1).float().contiguous()
-        dlogits = xent_bwd_(logits, lab, lse, dloss, out)  # in place, fp32
+        am = meta.get("amax")
+        # in place, fp32; with the h3 engine it also reports |dlogits| (both decoder gradients' operand)
+        dlogits = xent_bwd_(logits, lab, lse, dloss, out, amax=am["dl"] if (am and ctx.padded) else None)
         # tied decoder weight: accumulates into the word-embedding gradient
         # bf16 mode: both decoder GEMMs take bf16 operands (fp32 C for the weight gradient);
         # the fp32-operand weight GEMM cost 268 us vs 72 us (tools/bench_mlm_head.py)
@@ -839,8 +843,7 @@ class FusedPreTrainingLoss(torch.autograd.Function):
         # gradient (the embedding backward adds its rows later): it stores, the 94 MB of zeros unread
         store = meta.get("store")
         dec_acc = not (side and _FRESH_WGRAD and store is not None and store.claim_fresh())
-        am = meta.get("amax")
-        am_dl = G.amax_of(lbuf) if (am and lbuf is not None) else None  # dlogits: both decoder gradients' operand
+        am_dl = am["dl"] if (am and lbuf is not None) else None
         if lbuf is not None:  # padded split-bf16 decoder products (pad columns of dlogits stay zero)
             def dwdec():
                 if acc and store is not None:  # lazy zero_grad bookkeeping, on the writer's stream

@@ -698,9 +698,13 @@ def test_cross_entropy_aligned_rows(cuda, V, ld):
     stats, lse = B.xent_fwd(x, lab)  # stats = (mean loss, valid rows)
     _close(stats[0], ref, 1e-5, 1e-6, "xent fwd")
     _close(lse, torch.logsumexp(x.double(), 1), 1e-6, 1e-5, "lse")
-    B.xent_bwd_(x, lab, lse, torch.ones(1, device=cuda), stats)
+    from hetseq_amd.ops import gemm as G
+
+    slot = torch.zeros(G.SLOT_FLOATS, device=cuda)
+    B.xent_bwd_(x, lab, lse, torch.ones(1, device=cuda), stats, amax=slot)
     _close(x, xd.grad, 1e-4, 1e-9, "xent bwd")
     assert torch.equal(buf[:, V:], pad)
+    assert G.amax_value(slot).max().item() == x.abs().max().item()  # the written gradient's |max|
 
 
 def test_cross_entropy(cuda):
