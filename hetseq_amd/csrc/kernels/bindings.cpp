@@ -49,7 +49,8 @@ int launch_pos_grad(const float*, float*, int, int, int, hipStream_t);
 // elementwise.hip
 void launch_bias_gelu_fwd(int, const void*, const float*, void*, int64_t, int, hipStream_t);
 int colsum_row_chunks(int64_t);
-void launch_colsum(int, const void*, const void*, const float*, void*, float*, float*, int64_t, int, int, hipStream_t);
+void launch_colsum(int, const void*, const void*, const float*, void*, float*, float*, int64_t, int, int, hipStream_t,
+                   float*);
 void launch_mlm_compact(const int64_t*, int, int, int, int32_t*, int64_t*, int32_t*, int*, hipStream_t);
 void launch_gather_rows(int, const void*, const int32_t*, void*, int, int, hipStream_t);
 void launch_scatter_add_rows(int, const void*, const int32_t*, void*, int, int, hipStream_t);
@@ -444,12 +445,15 @@ PYBIND11_MODULE(_hip, m) {
     check_launch("pool_nsp_wgrad");
   });
   m.def("colsum_row_chunks", &colsum_row_chunks);
-  m.def("colsum", [](int dt, i64 dy, i64 x, i64 b, i64 dx, i64 part, i64 out, i64 rows, int N, int accumulate, i64 st) {
+  m.def("colsum", [](int dt, i64 dy, i64 x, i64 b, i64 dx, i64 part, i64 out, i64 rows, int N, int accumulate, i64 st,
+                     i64 amax) {
     pre_launch("colsum");
     launch_colsum(dt, P(const void*, dy), P(const void*, x), P(const float*, b), P(void*, dx), P(float*, part),
-                  P(float*, out), rows, N, accumulate, ST(st));
+                  P(float*, out), rows, N, accumulate, ST(st), P(float*, amax));
     check_launch("colsum");
-  });
+  }, pybind11::arg("dt"), pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("b"), pybind11::arg("dx"),
+     pybind11::arg("part"), pybind11::arg("out"), pybind11::arg("rows"), pybind11::arg("N"),
+     pybind11::arg("accumulate"), pybind11::arg("st"), pybind11::arg("amax") = 0);
   m.def("mlm_compact", [](i64 labels, int rows, int ignore, int cap, i64 idx, i64 lab_out, i64 count, i64 err, i64 st) {
     pre_launch("mlm_compact");
     launch_mlm_compact(P(const int64_t*, labels), rows, ignore, cap, P(int32_t*, idx), P(int64_t*, lab_out),

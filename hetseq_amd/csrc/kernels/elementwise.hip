@@ -42,9 +42,10 @@ template <typename T, bool kGelu>
 __global__ void __launch_bounds__(256) colsum_tile_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                           const float* __restrict__ b, T* __restrict__ dx,
                                                           float* __restrict__ part, int64_t rows, int N,
-                                                          int rows_per_chunk) {
+                                                          int rows_per_chunk, float* __restrict__ amax) {
   const int c = (blockIdx.x * 256 + threadIdx.x) * 4;
-  if (c >= N) return;
+  uint32_t mb = 0u;  // |max| of the written dx (kGelu with amax: the next product's h3 operand scale)
+  if (c < N) {
   const int64_t r0 = (int64_t)blockIdx.y * rows_per_chunk;
   int64_t r1 = r0 + rows_per_chunk;
   if (r1 > rows) r1 = rows;
@@ -64,7 +65,10 @@ __global__ void __launch_bounds__(256) colsum_tile_kernel(const T* __restrict__ 
     for (int u = 0; u < 4; ++u) {
       if (kGelu) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) d[u][j] *= gelu_grad_f(v[u][j] + bb[j]);
+        for (int j = 0; j < 4; ++j) {
+          d[u][j] *= gelu_grad_f(v[u][j] + bb[j]);
+          mb = amax_bits(mb, d[u][j]);
+        }
         store4(dx + (r + u) * N + c, d[u]);
       }
 #pragma unroll
@@ -79,13 +83,18 @@ __global__ void __launch_bounds__(256) colsum_tile_kernel(const T* __restrict__ 
       float v[4];
       load4(x + o, v);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) d[j] *= gelu_grad_f(v[j] + bb[j]);
+      for (int j = 0; j < 4; ++j) {
+        d[j] *= gelu_grad_f(v[j] + bb[j]);
+        mb = amax_bits(mb, d[j]);
+      }
       store4(dx + o, d);
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[j] += d[j];
   }
   store4(part + (int64_t)blockIdx.y * N + c, acc);
+  }
+  if (kGelu && amax) amax_commit(amax, mb);  // (every lane reaches it: no early return above)
 }
 
 // column partial sums for N not a multiple of 4 (e.g. the 30522-wide vocab)
@@ -389,7 +398,7 @@ int colsum_row_chunks(int64_t rows) {
 
 // gelu backward fused with bias-grad partials; if x == nullptr plain column sum of dy.
 void launch_colsum(int dtype, const void* dy, const void* x, const float* b, void* dx, float* part, float* out,
-                   int64_t rows, int N, int accumulate, hipStream_t st) {
+                   int64_t rows, int N, int accumulate, hipStream_t st, float* amax) {
   const int chunks = colsum_row_chunks(rows);
   const int rpc = (int)((rows + chunks - 1) / chunks);
   dim3 grid((N / 4 + 255) / 256, chunks);
@@ -402,17 +411,17 @@ void launch_colsum(int dtype, const void* dy, const void* x, const float* b, voi
   } else if (dtype == 0) {
     if (x)
       hipLaunchKernelGGL((colsum_tile_kernel<float, true>), grid, dim3(256), 0, st, (const float*)dy, (const float*)x,
-                         b, (float*)dx, part, rows, N, rpc);
+                         b, (float*)dx, part, rows, N, rpc, amax);
     else
       hipLaunchKernelGGL((colsum_tile_kernel<float, false>), grid, dim3(256), 0, st, (const float*)dy, nullptr, b,
-                         nullptr, part, rows, N, rpc);
+                         nullptr, part, rows, N, rpc, nullptr);
   } else {
     if (x)
       hipLaunchKernelGGL((colsum_tile_kernel<bf16_t, true>), grid, dim3(256), 0, st, (const bf16_t*)dy,
-                         (const bf16_t*)x, b, (bf16_t*)dx, part, rows, N, rpc);
+                         (const bf16_t*)x, b, (bf16_t*)dx, part, rows, N, rpc, amax);
     else
       hipLaunchKernelGGL((colsum_tile_kernel<bf16_t, false>), grid, dim3(256), 0, st, (const bf16_t*)dy, nullptr, b,
-                         nullptr, part, rows, N, rpc);
+                         nullptr, part, rows, N, rpc, nullptr);
   }
   const float* pp[1] = {part};
   float* oo[1] = {out};

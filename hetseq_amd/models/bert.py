@@ -828,7 +828,7 @@ class BertForPreTraining(BertPreTrainedModel):
         B, S = input_ids.shape
         wt_, wd_ = self._mlm_weights()
         head_w = (wt_, wd_) if isinstance(wt_, torch.Tensor) and wt_.dtype == torch.float32 else ()
-        pool, plan = self.bert._amax_plan(extra_weights=head_w, extra_slots=2)
+        pool, plan = self.bert._amax_plan(extra_weights=head_w, extra_slots=3)
         seq2d = self.bert.fused_encoder(input_ids, token_type_ids, attention_mask, checkpoint_activations,
                                         amax=(pool, plan))
         cap = B * S if self.max_predictions_per_seq is None else min(B * S, B * int(self.max_predictions_per_seq))
@@ -843,7 +843,8 @@ class BertForPreTraining(BertPreTrainedModel):
             # h3 slots of the head: the sequence output (last layer's h2 halves), the transform and
             # decoder weights, and the transform LN output t2 (the decoder's A operand)
             meta["amax"] = {"seq": last.a(6, 2), "wt": pool.w(4 * L), "wd": pool.w(4 * L + 1),
-                            "t2": pool.act(2 + L * last.NS), "dl": pool.act(2 + L * last.NS + 1)}
+                            "t2": pool.act(2 + L * last.NS), "dl": pool.act(2 + L * last.NS + 1),
+                            "dt": pool.act(2 + L * last.NS + 2)}
         store = getattr(self, "_hs_store", None)
         if store is not None:
             meta["grad_sink"] = lambda: [store.grad_view(q) for q in params]

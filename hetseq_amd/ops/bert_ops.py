@@ -165,8 +165,9 @@ def bias_gelu_fwd(x, b, out=None):
     return y
 
 
-def gelu_bwd_colsum(dy, x, b, db_acc=None):
-    """dx = dy * gelu'(x+b) and db = sum_rows(dx) (accumulated into ``db_acc`` if given)."""
+def gelu_bwd_colsum(dy, x, b, db_acc=None, amax=None):
+    """dx = dy * gelu'(x+b) and db = sum_rows(dx) (accumulated into ``db_acc`` if given); ``amax``: a
+    zeroed |max| slot the kernel maxes |dx| into."""
     rows, N = dy.shape
     assert N % 4 == 0 and dy.is_contiguous() and x.is_contiguous()
     chunks = hip().colsum_row_chunks(rows)
@@ -174,7 +175,7 @@ def gelu_bwd_colsum(dy, x, b, db_acc=None):
     db = db_acc if db_acc is not None else torch.empty(N, dtype=torch.float32, device=dy.device)
     dx = torch.empty_like(dy)
     hip().colsum(dtype_code(dy), dy.data_ptr(), x.data_ptr(), b.data_ptr(), dx.data_ptr(), part.data_ptr(),
-                 db.data_ptr(), rows, N, 1 if db_acc is not None else 0, stream_handle())
+                 db.data_ptr(), rows, N, 1 if db_acc is not None else 0, stream_handle(), amax=G.slot_ptr(amax))
     return dx, db
 
 
@@ -878,10 +879,10 @@ class FusedPreTrainingLoss(torch.autograd.Function):
         dt2 = G.decoder_dgrad(lbuf, Wd, V, amax=(am_dl, am["wd"]) if am_dl is not None else None) \
             if lbuf is not None else G.gemm(dl_c, Wd)
         dt1, _, dg, db, _ = ln_bwd(dt2, z, mean, rstd, g, 0.0, 0, acc=(Gv[2], Gv[3]) if acc else None, side=side)
-        dt1pre, dbt = gelu_bwd_colsum(dt1, t1pre, bt, db_acc=Gv[1] if acc else None)
+        am_d = am["dt"] if am else None  # |dt1pre|: the transform's two gradient products share it
+        dt1pre, dbt = gelu_bwd_colsum(dt1, t1pre, bt, db_acc=Gv[1] if acc else None, amax=am_d)
         hsel_in = _planes_of(hsel) if ctx.planes else hsel
         dt1pre_in = G.split(dt1pre) if ctx.planes else dt1pre
-        am_d = G.amax_of(dt1pre) if am else None  # the transform's two gradient products share it
         wt_am = (am_d, am["seq"]) if am else None
         if side:
             dWt = streams.run(dt1pre.device, lambda: G.linear_wgrad(dt1pre_in, hsel_in, out=Gv[0], accumulate=True,

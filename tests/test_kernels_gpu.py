@@ -676,6 +676,23 @@ def test_embedding_backward_bitwise_deterministic(cuda):
             assert torch.equal(a, c)
 
 
+@pytest.mark.parametrize("rows,N", [(640, 768), (257, 3072), (96, 1000)])
+def test_gelu_bwd_colsum_reports_amax(cuda, rows, N):
+    """The GELU backward + column-sum kernel maxes |dx| into a given slot (the MLM transform's h3
+    operand scale); dx and the column sums are unchanged by it."""
+    from hetseq_amd.ops import gemm as G
+    from hetseq_amd.ops.bert_ops import gelu_bwd_colsum
+
+    gen = torch.Generator(device=cuda).manual_seed(6)
+    dy, x = (torch.randn(rows, N, device=cuda, generator=gen) for _ in range(2))
+    b = torch.randn(N, device=cuda, generator=gen)
+    slot = torch.zeros(G.SLOT_FLOATS, device=cuda)
+    dx1, db1 = gelu_bwd_colsum(dy, x, b, amax=slot)
+    dx0, db0 = gelu_bwd_colsum(dy, x, b)
+    assert torch.equal(dx1, dx0) and torch.equal(db1, db0)
+    assert G.amax_value(slot).max().item() == dx0.abs().max().item()
+
+
 @pytest.mark.parametrize("V,ld", [(30522, 30720), (4099, 4104), (1024, 1024), (1025, 1028)])
 def test_cross_entropy_aligned_rows(cuda, V, ld):
     """fp32 logits whose rows start 16-B aligned (the MLM decoder's padded buffer) take the float4
