@@ -82,7 +82,7 @@ def parse():
                         + ") in --ab-rounds rounds of --steps steps each, one process, and print each variant's "
                         "median ms per step (interleaving cancels drift in the box's clock / thermal state)")
     p.add_argument("--ab-rounds", type=int, default=6, help=argparse.SUPPRESS)
-    p.add_argument("--fp32-gemm", default=None, choices=[None, "h3", "x6", "native"],
+    p.add_argument("--fp32-gemm", default=None, choices=[None, "h3p", "h3", "x6", "native"],
                    help="fp32 GEMM engine (default: HETSEQ_FP32_GEMM or the built-in default)")
     p.add_argument("--emulate-world", type=int, default=None, metavar="W",
                    help="1 GPU: predict the W-rank data-parallel step -- the DP engine on a 1-rank RCCL world whose "
@@ -612,6 +612,9 @@ _AB = {
     "lazyzero_off": lambda: setattr(__import__("hetseq_amd.controller", fromlist=["x"]), "_LAZY_ZERO", False),
     "h3_dma_on": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_h3_dma(1),
     "h3_dma_off": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_h3_dma(0),
+    # fp32 product engine of the encoder layers: h3p (pre-split block-scaled planes) / h3 (in-kernel split)
+    "eng_h3p": lambda: __import__("hetseq_amd.ops.gemm", fromlist=["x"]).set_fp32_mode("h3p"),
+    "eng_h3": lambda: __import__("hetseq_amd.ops.gemm", fromlist=["x"]).set_fp32_mode("h3"),
     # --emulate-world: workgroups per emulated collective (RCCL channels) and the emulated bus bandwidth
     "emu_ch4": lambda: _set_emul_channels(4),
     "emu_ch8": lambda: _set_emul_channels(8),

@@ -97,6 +97,25 @@ SOURCE_FLAGS = {
 }
 
 
+_INC_RE = re.compile(r'^\s*#\s*include\s*"([^"]+)"', re.M)
+
+
+def _included(src, headers):
+    """The module headers ``src`` includes, directly or through another of them (quoted includes):
+    an object is rebuilt when one of THOSE changes, not when any header of the directory does."""
+    by_name = {os.path.basename(h): h for h in headers}
+    seen, todo = [], [src]
+    while todo:
+        with open(todo.pop()) as fh:
+            text = fh.read()
+        for inc in _INC_RE.findall(text):
+            h = by_name.get(os.path.basename(inc))
+            if h is not None and h not in seen:
+                seen.append(h)
+                todo.append(h)
+    return seen
+
+
 def _compile_objs(compiler, flags, sources, headers, objdir, verbose, jobs):
     """Compile each source whose content hash (source + headers + flags) differs from the one
     recorded next to its object file."""
@@ -105,7 +124,7 @@ def _compile_objs(compiler, flags, sources, headers, objdir, verbose, jobs):
     for src in sources:
         obj = os.path.join(objdir, os.path.basename(src) + ".o")
         objs.append(obj)
-        want = _digest([src] + headers, [compiler] + flags + SOURCE_FLAGS.get(os.path.basename(src), []))
+        want = _digest([src] + _included(src, headers), [compiler] + flags + SOURCE_FLAGS.get(os.path.basename(src), []))
         try:
             with open(obj + ".hash") as fh:
                 have = fh.read().strip()

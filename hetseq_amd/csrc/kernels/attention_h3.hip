@@ -28,6 +28,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "h3p.h"
 
 namespace hs {
 
@@ -161,6 +162,40 @@ HS_DEVICE void store_rows(float* out, const f32x16& c0, const f32x16& c1, int hf
     cm = amax_bits(amax_bits(amax_bits(amax_bits(cm, b.x), b.y), b.z), b.w);
     *reinterpret_cast<float4*>(out + d) = a;
     *reinterpret_cast<float4*>(out + 32 + d) = b;
+  }
+}
+
+// Output also as h3p operand planes (h3p.h) of the next GEMM: `pl` plane 0 (plane 1 at + ps), `ex` the
+// exponents; null pl = off.  A wave's 32 x 64 output tile is two exponent blocks.
+struct AttnPl {
+  uint16_t* pl;
+  int64_t ps;
+  int8_t* ex;
+};
+
+// the wave's tile (rows: the lanes, 32-aligned; columns 0-31 in c0, 32-63 in c1, * scale) into the
+// planes at element e (the lane's row, the tile's first column) and its two exponents at ex
+HS_DEVICE void store_rows_h3p(const AttnPl& po, int64_t e, int8_t* ex, const f32x16& c0, const f32x16& c1, int hf,
+                              float scale) {
+  uint32_t m0 = 0u, m1 = 0u;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    m0 = amax_bits(m0, c0[r] * scale);
+    m1 = amax_bits(m1, c1[r] * scale);
+  }
+  const int e0 = h3p_exp_bits(wave_umax(m0)), e1 = h3p_exp_bits(wave_umax(m1));
+  const float s0 = h3p_scale(e0), s1 = h3p_scale(e1);
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int d = 8 * g + 4 * hf;
+    const float a[4] = {c0[4 * g] * scale, c0[4 * g + 1] * scale, c0[4 * g + 2] * scale, c0[4 * g + 3] * scale};
+    const float b[4] = {c1[4 * g] * scale, c1[4 * g + 1] * scale, c1[4 * g + 2] * scale, c1[4 * g + 3] * scale};
+    h3p_store4(po.pl, po.ps, e + d, a, s0);
+    h3p_store4(po.pl, po.ps, e + 32 + d, b, s1);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    ex[0] = static_cast<int8_t>(e0);
+    ex[1] = static_cast<int8_t>(e1);
   }
 }
 
@@ -325,7 +360,7 @@ HS_DEVICE void dkv_body(char* __restrict__ smem, int bx, int bh, const float* __
                         const int64_t* __restrict__ mask, const float* __restrict__ bqkv,
                         const float* __restrict__ dctx, const float* __restrict__ lse, const float* __restrict__ Dd,
                         float* __restrict__ dqkv, int S, int NH, float p, const uint32_t* __restrict__ dmask,
-                        const float* __restrict__ ctx, float* __restrict__ amax) {
+                        const float* __restrict__ ctx, float* __restrict__ amax, AttnPl po) {
   char* const Qp = smem;
   char* const Op = smem + kIm;
   float* const Ls = reinterpret_cast<float*>(smem + 2 * kIm);
@@ -487,6 +522,12 @@ HS_DEVICE void dkv_body(char* __restrict__ smem, int bx, int bh, const float* __
   store_rows(out + H, dk0, dk1, hf, ldexpf(1.f, -(eq_run + es)), cm);
   store_rows(out + 2 * H, dv0, dv1, hf, ldexpf(1.f, -(eo_run + ep)), cm);
   if (amax) amax_commit(amax, cm);
+  if (po.pl) {  // dK, dV as h3p planes of dqkv [B*S][3H] (exponent row stride 3H / 32)
+    const int64_t e = ((int64_t)b * S + key) * ld + h * kHD;
+    int8_t* ex = po.ex + ((int64_t)b * S + k0) / 32 * (ld / 32) + h * kHD / 32;
+    store_rows_h3p(po, e + H, ex + H / 32, dk0, dk1, hf, ldexpf(1.f, -(eq_run + es)));
+    store_rows_h3p(po, e + 2 * H, ex + 2 * H / 32, dv0, dv1, hf, ldexpf(1.f, -(eo_run + ep)));
+  }
 }
 
 // dQ for 32 queries per wave (lane = query) over 64-key chunks of K / V (biased); D from Dd or, with ctx
@@ -496,7 +537,7 @@ HS_DEVICE void dq_body(char* __restrict__ smem, int bx, int bh, const float* __r
                        const int64_t* __restrict__ mask, const float* __restrict__ bqkv,
                        const float* __restrict__ dctx, const float* __restrict__ lse, const float* __restrict__ Dd,
                        float* __restrict__ dqkv, int S, int NH, float p, const uint32_t* __restrict__ dmask,
-                       const float* __restrict__ ctx, float* __restrict__ amax) {
+                       const float* __restrict__ ctx, float* __restrict__ amax, AttnPl po) {
   char* const Kp = smem;
   char* const Vp = smem + kIm;
   float* const Ms = reinterpret_cast<float*>(smem + 2 * kIm);
@@ -606,6 +647,9 @@ HS_DEVICE void dq_body(char* __restrict__ smem, int bx, int bh, const float* __r
   uint32_t cm = 0u;
   store_rows(dqkv + tok * ld + h * kHD, dq0, dq1, hf, 0.125f * ldexpf(1.f, -(ek_run + es)), cm);
   if (amax) amax_commit(amax, cm);
+  if (po.pl)
+    store_rows_h3p(po, tok * ld + h * kHD, po.ex + ((int64_t)b * S + q0) / 32 * (ld / 32) + h * kHD / 32, dq0, dq1, hf,
+                   0.125f * ldexpf(1.f, -(ek_run + es)));
 }
 
 }  // namespace
@@ -620,13 +664,15 @@ __global__ void __launch_bounds__(256, 2)
     attn_bwd_h3_kernel(const float* __restrict__ qkv, const int64_t* __restrict__ mask,
                        const float* __restrict__ bqkv, const float* __restrict__ dctx, const float* __restrict__ lse,
                        const float* __restrict__ Dd, float* __restrict__ dqkv, int S, int NH, float p,
-                       const uint32_t* __restrict__ dmask, const float* __restrict__ ctx, float* __restrict__ amax) {
+                       const uint32_t* __restrict__ dmask, const float* __restrict__ ctx, float* __restrict__ amax,
+                       AttnPl po) {
   __shared__ __attribute__((aligned(16))) char smem[DMA ? kBwdLdsDma : kBwdLds];
   const int nq = (S + 127) / 128, bh = blockIdx.x, y = blockIdx.y;
   if (y < nq)
-    dkv_body<DMA>(smem, y, bh, qkv, mask, bqkv, dctx, lse, Dd, dqkv, S, NH, p, dmask, DMA ? nullptr : ctx, amax);
+    dkv_body<DMA>(smem, y, bh, qkv, mask, bqkv, dctx, lse, Dd, dqkv, S, NH, p, dmask, DMA ? nullptr : ctx, amax, po);
   else
-    dq_body<DMA>(smem, y - nq, bh, qkv, mask, bqkv, dctx, lse, Dd, dqkv, S, NH, p, dmask, DMA ? nullptr : ctx, amax);
+    dq_body<DMA>(smem, y - nq, bh, qkv, mask, bqkv, dctx, lse, Dd, dqkv, S, NH, p, dmask, DMA ? nullptr : ctx, amax,
+                 po);
 }
 
 // Forward: a wave owns 32 queries (lane = query), S^T tiles with the key on the registers, online softmax;
@@ -635,7 +681,7 @@ __global__ void __launch_bounds__(256, 2)
     attn_fwd_h3_kernel(const float* __restrict__ qkv, const int64_t* __restrict__ mask,
                        const float* __restrict__ bqkv, float* __restrict__ ctx, float* __restrict__ lse,
                        uint32_t* __restrict__ dmask, int S, int NH, float p, uint64_t seed, uint64_t off,
-                       const uint64_t* __restrict__ seed_dev, int bh0, float* __restrict__ amax) {
+                       const uint64_t* __restrict__ seed_dev, int bh0, float* __restrict__ amax, AttnPl po) {
   seed = resolve_seed(seed, seed_dev);
   __shared__ __attribute__((aligned(16))) char smem[2 * kIm];
   __shared__ float Ms[64];
@@ -744,6 +790,9 @@ __global__ void __launch_bounds__(256, 2)
   uint32_t cm = 0u;
   store_rows(ctx + ((int64_t)b * S + q0 + li) * H + h * kHD, o0, o1, hf, inv, cm);
   if (amax) amax_commit(amax, cm);  // ctx's |max|: the output projection's operand scale
+  if (po.pl)  // ctx as h3p planes of the output projection (exponent row stride H / 32)
+    store_rows_h3p(po, ((int64_t)b * S + q0 + li) * H + h * kHD, po.ex + ((int64_t)b * S + q0) / 32 * (H / 32) + 2 * h,
+                   o0, o1, hf, inv);
   if (hf == 0) lse[(int64_t)bh * S + q0 + li] = m + __logf(l);
 }
 
@@ -754,12 +803,13 @@ using namespace hs;
 // amax (optional): a |max| slot (common.h) the kernels max |output| into (ctx forward, dqkv backward)
 int launch_attn_fwd_h3(const float* qkv, const int64_t* mask, const float* bqkv, float* ctx, float* lse,
                        uint32_t* dmask, int B, int S, int NH, int D, float p, uint64_t seed, uint64_t off,
-                       hipStream_t st, int bh0, float* amax) {
+                       hipStream_t st, int bh0, float* amax, void* pl, int64_t ps, int8_t* ex) {
   if (D != kHD || S % 32 != 0 || S <= 0) return -1;
+  const AttnPl po{static_cast<uint16_t*>(pl), ps, ex};
   // grid (B*NH, S/128): consecutive blocks are different heads, so every query block of a head lands on
   // the same XCD and its K / V come through one L2
   hipLaunchKernelGGL(attn_fwd_h3_kernel, dim3(B * NH, (S + 127) / 128), dim3(256), 0, st, qkv, mask, bqkv, ctx, lse,
-                     dmask, S, NH, p, seed, off, g_seed_dev, bh0, amax);
+                     dmask, S, NH, p, seed, off, g_seed_dev, bh0, amax, po);
   return 0;
 }
 
@@ -776,8 +826,9 @@ void set_attn_h3_dma(int on) { g_bwd_dma = on; }
 
 int launch_attn_bwd_h3(const float* qkv, const int64_t* mask, const float* bqkv, const float* ctx, const float* dctx,
                        const float* lse, float* Dbuf, float* dqkv, const uint32_t* dmask, int B, int S, int NH, int D,
-                       float p, hipStream_t st, float* amax) {
+                       float p, hipStream_t st, float* amax, void* pl, int64_t ps, int8_t* ex) {
   if (D != kHD || S % 32 != 0 || S <= 0 || (p > 0.f && dmask == nullptr)) return -1;
+  const AttnPl po{static_cast<uint16_t*>(pl), ps, ex};
   const bool fused_d = S <= 128;  // each head's one dK / dV block stages every query once
   if (!fused_d) {
     if (Dbuf == nullptr) return -1;
@@ -786,12 +837,12 @@ int launch_attn_bwd_h3(const float* qkv, const int64_t* mask, const float* bqkv,
   const dim3 grid(B * NH, 2 * ((S + 127) / 128));
   if (fused_d)
     hipLaunchKernelGGL(attn_bwd_h3_kernel<false>, grid, dim3(256), 0, st, qkv, mask, bqkv, dctx, lse, Dbuf, dqkv, S, NH,
-                       p, dmask, ctx, amax);
+                       p, dmask, ctx, amax, po);
   else if (g_bwd_dma)
     hipLaunchKernelGGL(attn_bwd_h3_kernel<true>, grid, dim3(256), 0, st, qkv, mask, bqkv, dctx, lse, Dbuf, dqkv, S, NH,
-                       p, dmask, nullptr, amax);
+                       p, dmask, nullptr, amax, po);
   else
     hipLaunchKernelGGL(attn_bwd_h3_kernel<false>, grid, dim3(256), 0, st, qkv, mask, bqkv, dctx, lse, Dbuf, dqkv, S, NH,
-                       p, dmask, nullptr, amax);
+                       p, dmask, nullptr, amax, po);
   return 0;
 }

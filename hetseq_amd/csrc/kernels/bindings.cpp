@@ -42,6 +42,16 @@ int launch_emb_fwd(int, const int64_t*, const int64_t*, const float*, const floa
                    float*, hipStream_t);
 int launch_emb_bwd(int, const void*, const float*, const float*, const float*, const float*, float*, float*, float*,
                    const int64_t*, float*, int, int, float, u64, u64, hipStream_t);
+int launch_ln_fwd_h3p(const void*, const float*, const void*, const float*, const float*, void*, float*, float*, float*,
+                      int, int, float, float, u64, u64, int, int, int64_t, int, float*, void*, int64_t, int8_t*,
+                      hipStream_t);
+int launch_ln_bwd_h3p(const float*, const float*, const float*, const float*, const float*, float*, float*, float*,
+                      float*, int, int, float, u64, u64, void*, int64_t, int8_t*, hipStream_t);
+int launch_attn_fwd_h3(const float*, const int64_t*, const float*, float*, float*, uint32_t*, int, int, int, int, float,
+                       uint64_t, uint64_t, hipStream_t, int, float*, void*, int64_t, int8_t*);
+int launch_attn_bwd_h3(const float*, const int64_t*, const float*, const float*, const float*, const float*, float*,
+                       float*, const uint32_t*, int, int, int, int, float, hipStream_t, float*, void*, int64_t,
+                       int8_t*);
 void launch_colpart_finalize(const float* const*, float* const*, int, int, int, int, hipStream_t);
 int launch_segsum_rows(const float*, const int64_t*, const int64_t*, float*, float*, int, int, int, hipStream_t);
 int launch_sort_keys(const int64_t*, int, int64_t, int64_t*, int64_t*, int*, hipStream_t);
@@ -107,6 +117,17 @@ int launch_gemm_ring(int ta, int tb, int M, int N, int K, const void* A, int64_t
                      float* aux, int64_t ldaux, float* part, float* colsum_out, int colsum_acc, int ksplit,
                      float* slab, int64_t slab_floats, void* outp, int64_t o_ps, int bn, hipStream_t st);
 void set_planes_variant(int v);
+
+// gemm_h3p.hip
+int launch_gemm_h3p(int ta, int tb, int M, int N, int K, const void* A, int64_t lda, int64_t a_ps, const int8_t* ea,
+                    int64_t lde_a, const void* B, int64_t ldb, int64_t b_ps, const int8_t* eb, int64_t lde_b, float* C,
+                    int64_t ldc, const float* bias, int epi, float beta, float* aux, int64_t ldaux, float* part,
+                    float* colsum, int colsum_acc, void* cp, int64_t ldcp, int64_t cp_ps, int8_t* ec, int64_t lde_c,
+                    int ksplit, float* slab, int64_t slab_floats, hipStream_t st);
+int launch_h3p_split(const float* src, int64_t lds, int rows, int cols, void* dst, int64_t ldd, int64_t ps, int8_t* ex,
+                     int64_t lde, hipStream_t st);
+int h3p_split_seg_bytes();
+void launch_h3p_split_multi(const void* table, int nseg, int total, hipStream_t st);
 
 // mnist.hip
 void launch_mnist_conv1_fwd(const float*, const float*, const float*, float*, int, hipStream_t);
@@ -379,6 +400,65 @@ PYBIND11_MODULE(_hip, m) {
     pre_launch("bias_gelu_fwd");
     launch_bias_gelu_fwd(dt, P(const void*, x), P(const float*, b), P(void*, y), rows, N, ST(st));
     check_launch("bias_gelu_fwd");
+  });
+  m.def("gemm_h3p", [](int ta, int tb, int M, int N, int K, i64 A, i64 lda, i64 a_ps, i64 ea, i64 lde_a, i64 B,
+                       i64 ldb, i64 b_ps, i64 eb, i64 lde_b, i64 C, i64 ldc, i64 bias, int epi, float beta, i64 aux,
+                       i64 ldaux, i64 part, i64 colsum, int colsum_acc, i64 cp, i64 ldcp, i64 cp_ps, i64 ec, i64 lde_c,
+                       int ksplit, i64 slab, i64 slab_floats, i64 st) {
+    pre_launch("gemm_h3p");
+    const int rc = launch_gemm_h3p(ta, tb, M, N, K, P(const void*, A), lda, a_ps, P(const int8_t*, ea), lde_a,
+                                   P(const void*, B), ldb, b_ps, P(const int8_t*, eb), lde_b, P(float*, C), ldc,
+                                   P(const float*, bias), epi, beta, P(float*, aux), ldaux, P(float*, part),
+                                   P(float*, colsum), colsum_acc, P(void*, cp), ldcp, cp_ps, P(int8_t*, ec), lde_c,
+                                   ksplit, P(float*, slab), slab_floats, ST(st));
+    if (rc == 0) check_launch("gemm_h3p");
+    return rc;
+  }, "fp32 GEMM as three fp16 products over block-scaled h3p planes (gemm_h3p.hip); -1 = not served");
+  m.def("h3p_split", [](i64 src, i64 lds, int rows, int cols, i64 dst, i64 ldd, i64 ps, i64 ex, i64 lde, i64 st) {
+    pre_launch("h3p_split");
+    check(launch_h3p_split(P(const float*, src), lds, rows, cols, P(void*, dst), ldd, ps, P(int8_t*, ex), lde, ST(st)),
+          "h3p_split");
+  });
+  m.def("h3p_split_seg_bytes", &h3p_split_seg_bytes);
+  m.def("attn_fwd_h3p", [](i64 qkv, i64 mask, i64 bqkv, i64 ctx, i64 lse, i64 dmask, int B, int S, int NH, float p,
+                           u64 seed, u64 off, int bh0, i64 pl, i64 ps, i64 ex, i64 st) {
+    pre_launch("attn_fwd_h3p");
+    check(launch_attn_fwd_h3(P(const float*, qkv), P(const int64_t*, mask), P(const float*, bqkv), P(float*, ctx),
+                             P(float*, lse), P(uint32_t*, dmask), B, S, NH, 64, p, seed, off, ST(st), bh0, nullptr,
+                             P(void*, pl), ps, P(int8_t*, ex)),
+          "attn_fwd_h3p");
+  }, "h3 attention forward also writing ctx as h3p planes");
+  m.def("attn_bwd_h3p", [](i64 qkv, i64 mask, i64 bqkv, i64 ctx, i64 dctx, i64 lse, i64 dbuf, i64 dqkv, i64 dmask,
+                           int B, int S, int NH, float p, i64 pl, i64 ps, i64 ex, i64 st) {
+    pre_launch("attn_bwd_h3p");
+    check(launch_attn_bwd_h3(P(const float*, qkv), P(const int64_t*, mask), P(const float*, bqkv),
+                             P(const float*, ctx), P(const float*, dctx), P(const float*, lse), P(float*, dbuf),
+                             P(float*, dqkv), P(const uint32_t*, dmask), B, S, NH, 64, p, ST(st), nullptr,
+                             P(void*, pl), ps, P(int8_t*, ex)),
+          "attn_bwd_h3p");
+  }, "h3 attention backward also writing dqkv as h3p planes");
+  m.def("ln_fwd_h3p", [](i64 a, i64 bias, i64 resid, i64 gamma, i64 beta, i64 y, i64 z, i64 mean, i64 rstd, int rows,
+                         int H, float eps, float p, u64 seed, u64 off, int mode, int nslab, i64 slab_stride, int row0,
+                         i64 amax, i64 planes, i64 ps, i64 exps, i64 st) {
+    pre_launch("ln_fwd_h3p");
+    check(launch_ln_fwd_h3p(P(const void*, a), P(const float*, bias), P(const void*, resid), P(const float*, gamma),
+                            P(const float*, beta), P(void*, y), P(float*, z), P(float*, mean), P(float*, rstd), rows, H,
+                            eps, p, seed, off, mode, nslab, slab_stride, row0, P(float*, amax), P(void*, planes), ps,
+                            P(int8_t*, exps), ST(st)),
+          "ln_fwd_h3p");
+  });
+  m.def("ln_bwd_h3p", [](i64 dy, i64 z, i64 mean, i64 rstd, i64 gamma, i64 dz, i64 pg, i64 pb, i64 pbias, int rows,
+                         int H, float p, u64 seed, u64 off, i64 planes, i64 ps, i64 exps, i64 st) {
+    pre_launch("ln_bwd_h3p");
+    check(launch_ln_bwd_h3p(P(const float*, dy), P(const float*, z), P(const float*, mean), P(const float*, rstd),
+                            P(const float*, gamma), P(float*, dz), P(float*, pg), P(float*, pb), P(float*, pbias), rows,
+                            H, p, seed, off, P(void*, planes), ps, P(int8_t*, exps), ST(st)),
+          "ln_bwd_h3p");
+  });
+  m.def("h3p_split_multi", [](i64 table, int nseg, int total, i64 st) {
+    pre_launch("h3p_split_multi");
+    launch_h3p_split_multi(P(const void*, table), nseg, total, ST(st));
+    check_launch("h3p_split_multi");
   });
   m.def("gemm_planes", [](int planes, int c_dtype, int ta, int tb, int M, int N, int K, i64 A, i64 lda, i64 a_ps,
                           i64 B, i64 ldb, i64 b_ps, i64 C, i64 ldc, i64 bias, int epi, float beta, i64 aux,

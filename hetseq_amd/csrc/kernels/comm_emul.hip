@@ -43,7 +43,18 @@ __global__ void __launch_bounds__(256) comm_emul_kernel(const uint4* __restrict_
 // C signature the native comm engine (csrc/comm/comm.cpp) calls through a function pointer
 extern "C" void hetseq_comm_emulation(const void* src, int64_t src_bytes, void* scratch, int64_t scratch_bytes,
                                       int64_t traffic_bytes, int channels, int64_t hold_ns, hipStream_t st) {
-  const int64_t src16 = std::max<int64_t>(src_bytes / 16, 1), scr16 = std::max<int64_t>(scratch_bytes / 16, 1);
+  // whole 16-B lines inside the bucket only: a bucket slice of the flat gradient or the stats vector
+  // need not be 16-B aligned, and one shorter than a line is read from the (aligned) scratch instead
+  const uintptr_t s0 = reinterpret_cast<uintptr_t>(src), s1 = s0 + (uintptr_t)std::max<int64_t>(src_bytes, 0);
+  const uintptr_t a0 = (s0 + 15) & ~(uintptr_t)15;
+  int64_t src16 = a0 < s1 ? (int64_t)((s1 - a0) / 16) : 0;
+  const int64_t scr16 = std::max<int64_t>(scratch_bytes / 16, 1);
+  if (src16 < 1) {
+    src = scratch;
+    src16 = scr16;
+  } else {
+    src = reinterpret_cast<const void*>(a0);
+  }
   const int64_t traffic16 = std::max<int64_t>(traffic_bytes / 16, 0);
   int freq_khz = 100000;  // the wall clock's rate (hipDeviceAttributeWallClockRate, kHz)
   int dev = 0;

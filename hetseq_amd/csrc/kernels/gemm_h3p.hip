@@ -1,0 +1,457 @@
+// fp32 GEMM as three fp16 MFMA products over pre-split, block-scaled operand planes ("h3p"; the
+// operand format is described in h3p.h).  K01/K03/K04 GEMM parts of the BERT layer, reference
+// bert_modeling.py:352-354 (the attention projections), 166-172 (LinearActivation), 423-427
+// (BertOutput) and their autograd backward, which the reference runs as plain fp32 GEMMs.
+//
+//   C[M,N] = beta*C + op(A)[M,K] * op(B)[K,N]  (+ bias / GELU / dGELU epilogue)
+// op(A) = A (TA=0, A stored [M][K]) or A^T (TA=1, stored [K][M]); op(B) = B (TB=0, stored [K][N])
+// or B^T (TB=1, stored [N][K]).  The three Linear products: forward X W^T (0,1), data gradient
+// dY W (0,0), weight gradient dY^T X (1,0).
+//
+// Why this structure (gfx950):
+//  * the operand split (fp32 -> fp16 hi + lo) happens ONCE, in the kernel that produces the
+//    tensor, not in every GEMM block that stages it: the K loop is LDS-DMA + MFMA only.  The
+//    in-kernel-split engine (gemm.hip, gemm_x6s_kernel NT=4) spends as many issue cycles on the
+//    split VALU and the transposing ds_writes as on its MFMAs (profiles/r4_fp32_pmc.md);
+//  * 128 x 128 tile, 4 waves (2 x 2, 64 x 64 each = 2 x 2 v_mfma_f32_32x32x16_f16 tiles), BK = 32,
+//    two LDS stages of 32 KB (+ 4 KB of block factors): two workgroups per CU, so the other
+//    stream's GEMM blocks (the backward's weight-gradient stream) share the CUs;
+//  * staging is global_load_lds_dwordx4 (no VGPR round trip).  The LDS image is written
+//    lane-linearly, so the bank swizzle is in each lane's SOURCE address: k-contiguous operands
+//    as [128 rows][32 k] (64-B rows, 16-B chunks XOR (r>>2)&3, ds_read_b128 fragments),
+//    mn-contiguous ones (the data gradient's weight, both weight-gradient operands) as
+//    [32 k][128] (256-B rows, chunks XOR 4(r&3), fragments by ds_read_b64_tr_b16 -- the gfx950
+//    transposing read): no transpose pass anywhere;
+//  * block scales: each K tile's MFMAs accumulate into a fresh register tile (first MFMA with an
+//    inline-zero C), which is added to the fp32 accumulator with the tile's factor
+//    2^-(e_a + e_b) by one v_pk_fma per register pair.  The accumulator therefore holds TRUE fp32
+//    values (no running exponent, no overflow the fp32 result would not have), and each operand
+//    block keeps its own 2^18 window.  The factors of the block's K range are tabulated in LDS
+//    once (4 KB), read as two broadcast ds_read_b64 per tile;
+//  * XCD-contiguous, grouped block order (bijective for any grid): an XCD's resident blocks share
+//    operand panels in its private L2.
+// Epilogues: fp32 C (+ bias) (+ beta C); split-K fp32 slabs (summed by splitk_reduce_kernel, or by
+// the consumer); GELU (pre-activation kept in aux) and dGELU (column partials of the bias
+// gradient), each optionally writing its output as h3p planes for the next GEMM.
+#include <algorithm>
+
+#include "common.h"
+#include "h3p.h"
+#include "reduce.h"
+
+namespace hs {
+namespace {
+
+typedef _Float16 qh8 __attribute__((ext_vector_type(8)));
+typedef short qs4 __attribute__((ext_vector_type(4)));
+typedef short qs8 __attribute__((ext_vector_type(8)));
+typedef float qf16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) void q_lds_t;
+typedef __attribute__((address_space(1))) const void q_gbl_t;
+
+constexpr int QT = 128, QBK = 32;
+constexpr int QPLANE = QT * QBK * 2;  // one plane of one operand tile (8 KB)
+constexpr int QOPND = 2 * QPLANE;     // hi + lo (16 KB)
+constexpr int QSTAGE = 2 * QOPND;     // A and B (32 KB)
+constexpr int QMAXKT = 128;           // K tiles per block (K / ksplit <= 4096)
+constexpr int QSMEM = 2 * QSTAGE + 2 * QMAXKT * 4 * 4;
+
+enum { kQNone = 0, kQBias = 1, kQGelu = 2, kQDGelu = 3 };
+
+struct QArgs {
+  const uint16_t* A;
+  const int8_t* ea;
+  const uint16_t* B;
+  const int8_t* eb;
+  int64_t lda, a_ps, lde_a, ldb, b_ps, lde_b;
+  float* C;
+  int64_t ldc;
+  const float* bias;
+  float* aux;  // GELU: pre-activation out; dGELU: pre-activation in
+  int64_t ldaux;
+  float* part;  // dGELU: [M/128][N] column partials
+  uint16_t* cp;  // plane output of the epilogue's result (GELU / dGELU)
+  int8_t* ec;
+  int64_t ldcp, cp_ps, lde_c;
+  float* slab;  // split-K: [ksplit][M][N]
+  int M, N, K, ksplit;
+  float beta;
+};
+
+template <bool KC>
+struct QImg {
+  static constexpr int row_bytes = KC ? QBK * 2 : QT * 2;  // 64 ([mn][k]) or 256 ([k][mn])
+  HS_DEVICE static int swz(int r) { return KC ? ((r >> 2) & 3) : 4 * (r & 3); }
+};
+
+// per-lane source byte offsets (plane 0 of the operand, k = 0 of the block's range) of this wave's
+// four LDS-DMA instructions: instruction j fills bytes [1024 (4 j + w), +1024) of the operand image
+template <bool KC>
+HS_DEVICE void q_offsets(uint32_t (&off)[4], int64_t ld, int64_t ps, int mn0, int w, int lane) {
+  using I = QImg<KC>;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int byte = 1024 * (4 * j + w) + 16 * lane;
+    const int plane = byte / QPLANE, ib = byte % QPLANE;
+    const int row = ib / I::row_bytes, cl = (ib % I::row_bytes) / 16;
+    const int gc = cl ^ I::swz(row);  // the chunk this LDS position holds
+    const int64_t e = KC ? (int64_t)(mn0 + row) * ld + 8 * gc : (int64_t)row * ld + mn0 + 8 * gc;
+    off[j] = static_cast<uint32_t>(2 * (e + plane * ps));
+  }
+}
+
+HS_DEVICE void q_dma(const char* base, const uint32_t (&off)[4], char* img, int w) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    __builtin_amdgcn_global_load_lds((q_gbl_t*)(base + off[j]), (q_lds_t*)(img + 1024 * (4 * j + w)), 16, 0, 0);
+}
+
+// MFMA operand: 8 consecutive k (element j = k 16 ks + 8 (lane >> 5) + j) of row / column
+// rc + (lane & 31) from plane p of an operand image
+template <bool KC>
+HS_DEVICE qh8 q_frag(const char* img, int p, int rc, int ks, int lane) {
+  using I = QImg<KC>;
+  const char* pl = img + p * QPLANE;
+  if (KC) {
+    const int r = rc + (lane & 31), c = 2 * ks + (lane >> 5);
+    return *reinterpret_cast<const qh8*>(pl + r * I::row_bytes + 16 * (c ^ I::swz(r)));
+  } else {
+    // transposed read: lane 4q+p' of a 16-lane group addresses k row k0+q, columns c0+4p'..+3;
+    // lane i of the group receives column c0+i of the four rows
+    const int l16 = lane & 15, q = l16 >> 2, pp = l16 & 3, g = lane >> 4;
+    const int col = rc + 16 * (g & 1) + 4 * pp;
+    qs4 v[2];
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int row = 16 * ks + 8 * (g >> 1) + 4 * jj + q;
+      const char* a = pl + row * I::row_bytes + 16 * ((col >> 3) ^ I::swz(row)) + 2 * (col & 7);
+      v[jj] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) qs4*)(a));
+    }
+    const qs8 u = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w};
+    return __builtin_bit_cast(qh8, u);
+  }
+}
+
+HS_DEVICE qf16 q_mma(qh8 a, qh8 b, qf16 c) { return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0); }
+HS_DEVICE int q_row(int r, int q) { return (r & 3) + 8 * (r >> 2) + 4 * q; }
+
+template <bool TA, bool TB, int EPI>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) gemm_h3p_kernel(QArgs p) {
+  constexpr bool AK = !TA, BKc = TB;  // k-contiguous storage?
+  __shared__ __attribute__((aligned(16))) char smem[QSMEM];  // ALL LDS in one array (glds alias tracking)
+  float* const fA = reinterpret_cast<float*>(smem + 2 * QSTAGE);
+  float* const fB = fA + QMAXKT * 4;
+
+  const int tiles_m = p.M / QT, tiles_n = p.N / QT, ntile = tiles_m * tiles_n, nwg = ntile * p.ksplit;
+  const int orig = blockIdx.x;
+  const int xcd = orig % 8, qq = nwg / 8, rr = nwg % 8;
+  const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + orig / 8;
+  // slice-major split-K order: an XCD's contiguous range of blocks is one K slice over many tiles
+  const int slice = wg / ntile, tile = wg % ntile;
+  const int gsz = 8 * tiles_n, grp = tile / gsz, gm = min(8, tiles_m - 8 * grp);
+  const int tm = 8 * grp + (tile % gsz) % gm, tn = (tile % gsz) / gm;
+  const int m0 = tm * QT, n0 = tn * QT;
+  const int kofs = slice * (p.K / p.ksplit);
+  const int KT = p.K / p.ksplit / QBK;
+
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = w >> 1, wc = w & 1, wm = 64 * wr, wn = 64 * wc;
+
+  // block factors 2^-e of the block's K range: fA[t][g] for A's row group g, fB[t][g] for B's
+  // column group g (plain loads, all retired before the first LDS-DMA is issued)
+  for (int u = threadIdx.x; u < 4 * KT; u += 256) {
+    const int t = u >> 2, g = u & 3, kb = kofs / QBK + t;
+    const int64_t ia = AK ? (int64_t)(m0 / 32 + g) * p.lde_a + kb : (int64_t)kb * p.lde_a + m0 / 32 + g;
+    const int64_t ib = BKc ? (int64_t)(n0 / 32 + g) * p.lde_b + kb : (int64_t)kb * p.lde_b + n0 / 32 + g;
+    fA[u] = __builtin_ldexpf(1.f, -(int)p.ea[ia]);
+    fB[u] = __builtin_ldexpf(1.f, -(int)p.eb[ib]);
+  }
+
+  uint32_t offA[4], offB[4];
+  q_offsets<AK>(offA, p.lda, p.a_ps, m0, w, lane);
+  q_offsets<BKc>(offB, p.ldb, p.b_ps, n0, w, lane);
+  const int64_t stepA = AK ? 2 * QBK : 2 * (int64_t)QBK * p.lda, stepB = BKc ? 2 * QBK : 2 * (int64_t)QBK * p.ldb;
+  const char* ga = reinterpret_cast<const char*>(p.A) + (AK ? 2 * (int64_t)kofs : 2 * (int64_t)kofs * p.lda);
+  const char* gb = reinterpret_cast<const char*>(p.B) + (BKc ? 2 * (int64_t)kofs : 2 * (int64_t)kofs * p.ldb);
+
+  qf16 acc[2][2], tmp[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = qf16{};
+
+  struct Frags {
+    qh8 a[2][2], b[2][2];  // [plane][tile]
+  };
+  auto read = [&](Frags& f, const char* stage, int ks) {
+#pragma unroll
+    for (int pl = 0; pl < 2; ++pl)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        f.a[pl][i] = q_frag<AK>(stage, pl, wm + 32 * i, ks, lane);
+        f.b[pl][i] = q_frag<BKc>(stage + QOPND, pl, wn + 32 * i, ks, lane);
+      }
+  };
+  // the three products of one k slice, smallest first: lo_a hi_b, hi_a lo_b, hi_a hi_b
+  auto mma = [&](const Frags& f, bool first) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) tmp[i][j] = q_mma(f.a[1][i], f.b[0][j], first ? qf16{} : tmp[i][j]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) tmp[i][j] = q_mma(f.a[0][i], f.b[1][j], tmp[i][j]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) tmp[i][j] = q_mma(f.a[0][i], f.b[0][j], tmp[i][j]);
+  };
+
+  Frags f[2];
+  q_dma(ga, offA, smem, w);
+  q_dma(gb, offB, smem + QOPND, w);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // tile 0 and the factor tables visible to every wave
+  read(f[0], smem, 0);
+  for (int t = 0; t < KT; ++t) {
+    const char* cur = smem + (t & 1) * QSTAGE;
+    char* nxt = smem + ((t + 1) & 1) * QSTAGE;
+    if (t + 1 < KT) {  // the other stage was last read before the previous barrier
+      q_dma(ga + (t + 1) * stepA, offA, nxt, w);
+      q_dma(gb + (t + 1) * stepB, offB, nxt + QOPND, w);
+    }
+    read(f[1], cur, 1);
+    mma(f[0], true);
+    // keep slice 0's MFMAs ahead of the barrier (the scheduler would sink them past it and expose
+    // slice 1's LDS reads to the barrier's wait)
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // tile t+1 landed in every wave's share; nobody reads tile t any more
+    if (t + 1 < KT) read(f[0], nxt, 0);
+    mma(f[1], false);
+    const float2 fa = *reinterpret_cast<const float2*>(fA + 4 * t + 2 * wr);
+    const float2 fb = *reinterpret_cast<const float2*>(fB + 4 * t + 2 * wc);
+    const float fac[2][2] = {{fa.x * fb.x, fa.x * fb.y}, {fa.y * fb.x, fa.y * fb.y}};
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] += tmp[i][j] * fac[i][j];
+  }
+
+  // ---------------- epilogue: register r of acc[i][j] -> row m0+wm+32i+q_row(r,q), col n0+wn+32j+lr
+  const int lr = lane & 31, q = lane >> 5;
+  if (p.ksplit > 1) {  // fp32 partial slab; bias / beta / the sum in splitk_reduce_kernel (or the consumer)
+    float* sl = p.slab + (int64_t)slice * p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          sl[(int64_t)(m0 + wm + 32 * i + q_row(r, q)) * p.N + n0 + wn + 32 * j + lr] = acc[i][j][r];
+    return;
+  }
+  float csum[2] = {0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = n0 + wn + 32 * j + lr;
+    const float bv = EPI != kQNone ? p.bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int mb = m0 + wm + 32 * i;
+      if (EPI == kQGelu) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int64_t m = mb + q_row(r, q);
+          p.aux[m * p.ldaux + n] = acc[i][j][r];
+          acc[i][j][r] = gelu_f(acc[i][j][r] + bv);
+          if (p.C) p.C[m * p.ldc + n] = acc[i][j][r];
+        }
+      } else if (EPI == kQDGelu) {
+        float pre[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) pre[r] = p.aux[(int64_t)(mb + q_row(r, q)) * p.ldaux + n];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          acc[i][j][r] *= gelu_grad_f(pre[r] + bv);
+          csum[j] += acc[i][j][r];
+          if (p.C) p.C[(int64_t)(mb + q_row(r, q)) * p.ldc + n] = acc[i][j][r];
+        }
+      } else if (p.beta != 0.f) {
+        float old[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) old[r] = p.C[(int64_t)(mb + q_row(r, q)) * p.ldc + n];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) p.C[(int64_t)(mb + q_row(r, q)) * p.ldc + n] = acc[i][j][r] + bv + p.beta * old[r];
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) p.C[(int64_t)(mb + q_row(r, q)) * p.ldc + n] = acc[i][j][r] + bv;
+      }
+    }
+  }
+  if ((EPI == kQGelu || EPI == kQDGelu) && p.cp) {
+    // the result as h3p planes: one exponent per 32 x 32 accumulator tile (= one exponent block)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        uint32_t mb = 0u;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mb = amax_bits(mb, acc[i][j][r]);
+        const int e = h3p_exp_bits(wave_umax(mb));
+        const float s = h3p_scale(e);
+        const int rb = (m0 + wm) / 32 + i, cb = (n0 + wn) / 32 + j;
+        if (lane == 0) p.ec[(int64_t)rb * p.lde_c + cb] = static_cast<int8_t>(e);
+        const int n = n0 + wn + 32 * j + lr;
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          uint32_t hi, lo;
+          h3p_split2(acc[i][j][r], acc[i][j][r + 1], s, hi, lo);
+          const int64_t e0 = (int64_t)(m0 + wm + 32 * i + q_row(r, q)) * p.ldcp + n;
+          const int64_t e1 = (int64_t)(m0 + wm + 32 * i + q_row(r + 1, q)) * p.ldcp + n;
+          p.cp[e0] = static_cast<uint16_t>(hi);
+          p.cp[e1] = static_cast<uint16_t>(hi >> 16);
+          p.cp[p.cp_ps + e0] = static_cast<uint16_t>(lo);
+          p.cp[p.cp_ps + e1] = static_cast<uint16_t>(lo >> 16);
+        }
+      }
+  }
+  if (EPI == kQDGelu && p.part) {  // column sums over the block's 128 rows: lane halves, then wave rows
+    float* red = reinterpret_cast<float*>(smem);  // the K loop ended with a barrier
+#pragma unroll
+    for (int j = 0; j < 2; ++j) csum[j] += __shfl_xor(csum[j], 32, 64);
+    if (wr == 1 && q == 0)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) red[wn + 32 * j + lr] = csum[j];
+    __syncthreads();
+    if (wr == 0 && q == 0)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int c = wn + 32 * j + lr;
+        p.part[(int64_t)tm * p.N + n0 + c] = csum[j] + red[c];
+      }
+  }
+}
+
+// ---------------------------------------------------------------- fp32 -> h3p planes
+struct QSplitSeg {
+  const float* src;
+  uint16_t* dst;
+  int8_t* ex;
+  int64_t lds, ldd, ps, lde;
+  int rows, cols, blk0;  // blk0: index of the segment's first 32 x 32 block in the launch
+  int pad;
+};
+
+// one wave per 32 x 32 block: lane l loads row (l >> 3) + 8 q, columns 4 (l & 7) .. +3 (q = 0..3),
+// the block |max| by a wave reduction, then both planes and the exponent
+__global__ void __launch_bounds__(256) h3p_split_kernel(QSplitSeg one, const QSplitSeg* __restrict__ many, int nseg,
+                                                        int total) {
+  const int b = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+  if (b >= total) return;  // wave-uniform
+  QSplitSeg s = one;
+  if (many) {
+    int i = 0;
+    while (i + 1 < nseg && many[i + 1].blk0 <= b) ++i;
+    s = many[i];
+  }
+  const int lb = b - s.blk0, nbc = s.cols / 32;
+  const int br = lb / nbc, bc = lb % nbc;
+  const int lane = threadIdx.x & 63;
+  const int r0 = br * 32 + (lane >> 3), c = bc * 32 + 4 * (lane & 7);
+  float v[4][4];
+  uint32_t m = 0u;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    load4(s.src + (int64_t)(r0 + 8 * k) * s.lds + c, v[k]);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) m = amax_bits(m, v[k][e]);
+  }
+  const int e = h3p_exp_bits(wave_umax(m));
+  const float sc = h3p_scale(e);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) h3p_store4(s.dst, s.ps, (int64_t)(r0 + 8 * k) * s.ldd + c, v[k], sc);
+  if (lane == 0) s.ex[(int64_t)br * s.lde + bc] = static_cast<int8_t>(e);
+}
+
+template <bool TA, bool TB>
+int q_launch_epi(int epi, const QArgs& a, hipStream_t st) {
+  const dim3 grid((a.M / QT) * (a.N / QT) * a.ksplit), blk(256);
+  if (epi == kQNone) hipLaunchKernelGGL((gemm_h3p_kernel<TA, TB, kQNone>), grid, blk, 0, st, a);
+  else if (epi == kQBias) hipLaunchKernelGGL((gemm_h3p_kernel<TA, TB, kQBias>), grid, blk, 0, st, a);
+  else if (epi == kQGelu && !TA && TB) hipLaunchKernelGGL((gemm_h3p_kernel<false, true, kQGelu>), grid, blk, 0, st, a);
+  else if (epi == kQDGelu && !TA && !TB)
+    hipLaunchKernelGGL((gemm_h3p_kernel<false, false, kQDGelu>), grid, blk, 0, st, a);
+  else return -1;
+  return 0;
+}
+
+}  // namespace
+}  // namespace hs
+
+using namespace hs;
+
+// gemm.hip: C = sum of the ksplit fp32 slabs (fixed order) (+ bias) (+ beta * C)
+void launch_splitk_reduce(const float* slab, int ksplit, int M, int N, float* C, int64_t ldc, const float* bias,
+                          float beta, int Mv, int Nv, hipStream_t st);
+
+// Returns -1 (nothing launched) for a request the kernel does not serve.  Strides and plane strides
+// in elements; lde_*: row stride of the exponent arrays.  C == nullptr with ksplit > 1: the partial
+// slabs are left for the consumer (no reduce pass).  cp / ec (GELU, dGELU): the result's planes.
+int launch_gemm_h3p(int ta, int tb, int M, int N, int K, const void* A, int64_t lda, int64_t a_ps, const int8_t* ea,
+                    int64_t lde_a, const void* B, int64_t ldb, int64_t b_ps, const int8_t* eb, int64_t lde_b, float* C,
+                    int64_t ldc, const float* bias, int epi, float beta, float* aux, int64_t ldaux, float* part,
+                    float* colsum, int colsum_acc, void* cp, int64_t ldcp, int64_t cp_ps, int8_t* ec, int64_t lde_c,
+                    int ksplit, float* slab, int64_t slab_floats, hipStream_t st) {
+  ksplit = std::max(1, ksplit);
+  if (M <= 0 || N <= 0 || K <= 0 || M % QT || N % QT || K % (QBK * ksplit) || K / ksplit / QBK > QMAXKT) return -1;
+  if (ta && tb) return -1;
+  auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  if (!A || !B || !ea || !eb || !al16(A) || !al16(B) || lda % 8 || ldb % 8 || a_ps % 8 || b_ps % 8) return -1;
+  if (epi < 0 || epi > 3 || (epi >= 1 && !bias) || (epi >= 2 && (!aux || beta != 0.f || ksplit > 1))) return -1;
+  if (epi == 3 && !part != !colsum) return -1;
+  if (cp && (epi < 2 || !ec || ldcp % 2)) return -1;
+  if (epi < 2 && !C && ksplit == 1) return -1;
+  if (epi >= 2 && !C && !cp) return -1;
+  if (ksplit > 1 && (!slab || (int64_t)ksplit * M * N > slab_floats || (C && (N % 4 || ldc % 4 || !al16(C)))))
+    return -1;
+  // 32-bit per-lane DMA offsets: each operand's span (both planes) below 4 GiB
+  const int64_t spanA = 2 * (a_ps + (int64_t)(ta ? K : M) * lda), spanB = 2 * (b_ps + (int64_t)(tb ? N : K) * ldb);
+  if (spanA >= (1ll << 32) || spanB >= (1ll << 32)) return -1;
+  QArgs a{static_cast<const uint16_t*>(A), ea, static_cast<const uint16_t*>(B), eb, lda, a_ps, lde_a, ldb, b_ps,
+          lde_b, C, ldc, bias, aux, ldaux, part, static_cast<uint16_t*>(cp), ec, ldcp, cp_ps, lde_c, slab, M, N, K,
+          ksplit, beta};
+  const int rc = !ta && tb ? q_launch_epi<false, true>(ksplit > 1 ? 0 : epi, a, st)
+                 : !ta   ? q_launch_epi<false, false>(ksplit > 1 ? 0 : epi, a, st)
+                         : q_launch_epi<true, false>(ksplit > 1 ? 0 : epi, a, st);
+  if (rc) return rc;
+  if (ksplit > 1 && C) launch_splitk_reduce(slab, ksplit, M, N, C, ldc, epi == 1 ? bias : nullptr, beta, M, N, st);
+  if (epi == kQDGelu && part) {
+    const float* parts[1] = {part};
+    float* outs[1] = {colsum};
+    launch_reduce_rows(parts, outs, 1, M / QT, N, colsum_acc, st);
+  }
+  return 0;
+}
+
+// fp32 [rows][cols] (row stride lds) -> h3p planes (row stride ldd, plane stride ps) + exponents
+int launch_h3p_split(const float* src, int64_t lds, int rows, int cols, void* dst, int64_t ldd, int64_t ps, int8_t* ex,
+                     int64_t lde, hipStream_t st) {
+  if (rows <= 0 || cols <= 0 || rows % 32 || cols % 32 || lds % 4 || ldd % 4 || ps % 4) return -1;
+  if ((reinterpret_cast<uintptr_t>(src) & 15) || (reinterpret_cast<uintptr_t>(dst) & 7)) return -1;
+  QSplitSeg s{src, static_cast<uint16_t*>(dst), ex, lds, ldd, ps, lde, rows, cols, 0, 0};
+  const int total = (rows / 32) * (cols / 32);
+  hipLaunchKernelGGL(h3p_split_kernel, dim3((total + 3) / 4), dim3(256), 0, st, s, nullptr, 1, total);
+  return 0;
+}
+
+// several tensors in one launch: `table` = nseg QSplitSeg records in device memory (blk0 ascending,
+// built by the caller with h3p_split_seg_bytes / the Python packer), `total` = all their blocks
+int h3p_split_seg_bytes() { return static_cast<int>(sizeof(QSplitSeg)); }
+void launch_h3p_split_multi(const void* table, int nseg, int total, hipStream_t st) {
+  QSplitSeg none{};
+  hipLaunchKernelGGL(h3p_split_kernel, dim3((total + 3) / 4), dim3(256), 0, st, none,
+                     static_cast<const QSplitSeg*>(table), nseg, total);
+}

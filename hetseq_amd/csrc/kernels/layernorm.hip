@@ -18,6 +18,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "h3p.h"
 #include "reduce.h"
 
 namespace hs {
@@ -112,6 +113,113 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const T* __restrict__ a, co
     }
   }
   if (amax_y) amax_commit(amax_y, am);
+}
+
+// LayerNorm forward that also writes y as h3p operand planes (h3p.h): one block = 32 consecutive rows
+// (the exponent block's height), 8 waves x 4 rows; after the rows, each 32-column group's |max| over
+// the block's 32 rows (lanes, then waves through LDS) sets the block exponent, and every lane splits
+// the y values it still holds.  Same per-row arithmetic as ln_fwd_kernel (bitwise the same y).
+constexpr int kLnH3pWaves = 8;
+
+template <int NV, typename T>
+__global__ void __launch_bounds__(64 * kLnH3pWaves) ln_fwd_h3p_kernel(
+    const T* __restrict__ a, const float* __restrict__ bias, const T* __restrict__ resid,
+    const float* __restrict__ gamma, const float* __restrict__ beta, T* __restrict__ y, float* __restrict__ zsave,
+    float* __restrict__ mean_out, float* __restrict__ rstd_out, float eps, float p, uint64_t seed, uint64_t off, int mode,
+    const uint64_t* __restrict__ seed_dev, int nslab, int64_t slab_stride, int row0, float* __restrict__ amax_y,
+    uint16_t* __restrict__ planes, int64_t ps, int8_t* __restrict__ exps) {
+  constexpr int H = NV * 256, RPW = 32 / kLnH3pWaves;
+  __shared__ float red[kLnH3pWaves][NV * 8];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const float scale = p < 1.f ? 1.0f / (1.0f - p) : 0.f;
+  seed = resolve_seed(seed, seed_dev);
+  uint32_t am = 0u;
+  float o[RPW][NV][4];
+#pragma unroll
+  for (int j = 0; j < RPW; ++j) {
+    const int row = blockIdx.x * 32 + w * RPW + j;
+    const int64_t base = (int64_t)row * H;
+    float x[NV][4];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = (k * 64 + lane) * 4;
+      load4(a + base + c, x[k]);
+      for (int sl = 1; sl < nslab; ++sl) {
+        float t[4];
+        load4(a + sl * slab_stride + base + c, t);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[k][e] += t[e];
+      }
+      if (bias) {
+        float b[4];
+        load4(bias + c, b);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[k][e] += b[e];
+      }
+      if (mode == kBDR && p > 0.f) {
+        float m[4];
+        keep4(seed, off, (uint64_t)((int64_t)(row0 + row) * H + c) >> 2, p, scale, m);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[k][e] *= m[e];
+      }
+      if (resid) {
+        float r[4];
+        load4(resid + base + c, r);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[k][e] += r[e];
+      }
+      if (zsave) store4(zsave + base + c, x[k]);
+    }
+    float mean, rstd;
+    row_stats<NV>(x, H, mean, rstd, eps);
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = (k * 64 + lane) * 4;
+      float gw[4], gb[4];
+      load4(gamma + c, gw);
+      load4(beta + c, gb);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        o[j][k][e] = gw[e] * ((x[k][e] - mean) * rstd) + gb[e];
+        am = amax_bits(am, o[j][k][e]);
+      }
+      store4(y + base + c, o[j][k]);
+    }
+    if (lane == 0) {
+      mean_out[row] = mean;
+      rstd_out[row] = rstd;
+    }
+  }
+  if (amax_y) amax_commit(amax_y, am);
+  // 32-column group k * 8 + lane / 8: the lane's |max| over its rows, its 8 lanes, then the 8 waves
+  uint32_t gm[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    gm[k] = 0u;
+#pragma unroll
+    for (int j = 0; j < RPW; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) gm[k] = amax_bits(gm[k], o[j][k][e]);
+#pragma unroll
+    for (int sh = 1; sh < 8; sh <<= 1)
+      gm[k] = max(gm[k], static_cast<uint32_t>(__shfl_xor(static_cast<int>(gm[k]), sh, 64)));
+    if ((lane & 7) == 0) red[w][k * 8 + (lane >> 3)] = __uint_as_float(gm[k]);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    uint32_t m = 0u;
+#pragma unroll
+    for (int v = 0; v < kLnH3pWaves; ++v) m = max(m, __float_as_uint(red[v][k * 8 + (lane >> 3)]));
+    const int e = h3p_exp_bits(m);
+    const float sc = h3p_scale(e);
+#pragma unroll
+    for (int j = 0; j < RPW; ++j) {
+      const int row = blockIdx.x * 32 + w * RPW + j;
+      h3p_store4(planes, ps, (int64_t)row * H + (k * 64 + lane) * 4, o[j][k], sc);
+    }
+    if (w == 0 && (lane & 7) == 0) exps[(int64_t)blockIdx.x * (H / 32) + k * 8 + (lane >> 3)] = static_cast<int8_t>(e);
+  }
 }
 
 // Column partials are written as part[blockIdx.x][H] (one row per block); the WV waves'
@@ -273,6 +381,125 @@ __global__ void __launch_bounds__(64 * kLnBwdWaves) ln_bwd_kernel(
   }
 }
 
+// Column partials of an 8-wave block through a 7 KB LDS window: waves 1-7 hand wave 0 one 256-column
+// chunk at a time; wave 0 sums ((w0 + w1) + (w2 + w3)) + ((w4 + w5) + (w6 + w7)) (fixed order).
+template <int NV>
+HS_DEVICE void colpart8_store(float (&acc)[NV][4], float* __restrict__ part, float* lds) {
+  constexpr int H = NV * 256;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    if (w > 0) store4(lds + (w - 1) * 256 + lane * 4, acc[k]);
+    __syncthreads();
+    if (w == 0) {
+      float v[7][4], o[4];
+#pragma unroll
+      for (int u = 0; u < 7; ++u) load4(lds + u * 256 + lane * 4, v[u]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        o[e] = ((acc[k][e] + v[0][e]) + (v[1][e] + v[2][e])) + ((v[3][e] + v[4][e]) + (v[5][e] + v[6][e]));
+      store4(part + (int64_t)blockIdx.x * H + (k * 64 + lane) * 4, o);
+    }
+    __syncthreads();
+  }
+}
+
+// LayerNorm backward writing the residual-branch gradient da (mode kBDR) as h3p planes -- the next
+// data- and weight-gradient GEMMs' operand -- instead of fp32: one block = 32 rows (8 waves x 4 rows),
+// block exponents as in ln_fwd_h3p_kernel.  dz (fp32) and the per-block column partials of dgamma /
+// dbeta / dbias as ln_bwd_kernel (same per-row arithmetic; partials over 32-row blocks).
+template <int NV>
+__global__ void __launch_bounds__(64 * kLnH3pWaves) ln_bwd_h3p_kernel(
+    const float* __restrict__ dy, const float* __restrict__ zsave, const float* __restrict__ mean_in,
+    const float* __restrict__ rstd_in, const float* __restrict__ gamma, float* __restrict__ dz_out,
+    float* __restrict__ part_gamma, float* __restrict__ part_beta, float* __restrict__ part_bias, float p, uint64_t seed,
+    uint64_t off, const uint64_t* __restrict__ seed_dev, uint16_t* __restrict__ planes, int64_t ps,
+    int8_t* __restrict__ exps) {
+  constexpr int H = NV * 256, RPW = 32 / kLnH3pWaves;
+  __shared__ __attribute__((aligned(16))) float win[7 * 256];
+  __shared__ float red[kLnH3pWaves][NV * 8];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const float scale = p < 1.f ? 1.0f / (1.0f - p) : 0.f;
+  seed = resolve_seed(seed, seed_dev);
+  float ag[NV][4], ab[NV][4], abias[NV][4], gw[NV][4], da[RPW][NV][4];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    load4(gamma + (k * 64 + lane) * 4, gw[k]);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) ag[k][e] = ab[k][e] = abias[k][e] = 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < RPW; ++j) {
+    const int row = blockIdx.x * 32 + w * RPW + j;
+    const int64_t base = (int64_t)row * H;
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float d[NV][4], xh[NV][4], g[NV][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      float z[4];
+      load4(dy + base + (k * 64 + lane) * 4, d[k]);
+      load4(zsave + base + (k * 64 + lane) * 4, z);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        xh[k][e] = (z[e] - mean) * rstd;
+        g[k][e] = d[k][e] * gw[k][e];
+        ag[k][e] = fmaf(d[k][e], xh[k][e], ag[k][e]);
+        ab[k][e] += d[k][e];
+        s1 += g[k][e];
+        s2 = fmaf(g[k][e], xh[k][e], s2);
+      }
+    }
+    s1 = wave_sum(s1) / H;
+    s2 = wave_sum(s2) / H;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = (k * 64 + lane) * 4;
+      float dzv[4], m[4] = {1.f, 1.f, 1.f, 1.f};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dzv[e] = rstd * (g[k][e] - s1 - xh[k][e] * s2);
+      store4(dz_out + base + c, dzv);
+      if (p > 0.f) keep4(seed, off, (uint64_t)(base + c) >> 2, p, scale, m);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        da[j][k][e] = dzv[e] * m[e];
+        abias[k][e] += da[j][k][e];
+      }
+    }
+  }
+  uint32_t gm[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    gm[k] = 0u;
+#pragma unroll
+    for (int j = 0; j < RPW; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) gm[k] = amax_bits(gm[k], da[j][k][e]);
+#pragma unroll
+    for (int sh = 1; sh < 8; sh <<= 1)
+      gm[k] = max(gm[k], static_cast<uint32_t>(__shfl_xor(static_cast<int>(gm[k]), sh, 64)));
+    if ((lane & 7) == 0) red[w][k * 8 + (lane >> 3)] = __uint_as_float(gm[k]);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    uint32_t m = 0u;
+#pragma unroll
+    for (int v = 0; v < kLnH3pWaves; ++v) m = max(m, __float_as_uint(red[v][k * 8 + (lane >> 3)]));
+    const int e = h3p_exp_bits(m);
+    const float sc = h3p_scale(e);
+#pragma unroll
+    for (int j = 0; j < RPW; ++j) {
+      const int row = blockIdx.x * 32 + w * RPW + j;
+      h3p_store4(planes, ps, (int64_t)row * H + (k * 64 + lane) * 4, da[j][k], sc);
+    }
+    if (w == 0 && (lane & 7) == 0) exps[(int64_t)blockIdx.x * (H / 32) + k * 8 + (lane >> 3)] = static_cast<int8_t>(e);
+  }
+  colpart8_store<NV>(ag, part_gamma, win);
+  colpart8_store<NV>(ab, part_beta, win);
+  colpart8_store<NV>(abias, part_bias, win);
+}
+
 // ------------------------------------------------------------ embeddings
 template <int NV, typename T>
 __global__ void __launch_bounds__(256) emb_fwd_kernel(const int64_t* __restrict__ ids, const int64_t* __restrict__ tt,
@@ -428,6 +655,24 @@ void ln_fwd_launch(const void* a, const float* bias, const void* resid, const fl
 }
 
 template <int NV, typename T>
+void ln_fwd_h3p_launch(const void* a, const float* bias, const void* resid, const float* gamma, const float* beta,
+                       void* y, float* zsave, float* mean, float* rstd, int rows, float eps, float p, uint64_t seed,
+                       uint64_t off, int mode, int nslab, int64_t slab_stride, int row0, float* amax, uint16_t* planes,
+                       int64_t ps, int8_t* exps, hipStream_t st) {
+  hipLaunchKernelGGL((ln_fwd_h3p_kernel<NV, T>), dim3(rows / 32), dim3(64 * kLnH3pWaves), 0, st, (const T*)a, bias,
+                     (const T*)resid, gamma, beta, (T*)y, zsave, mean, rstd, eps, p, seed, off, mode, g_seed_dev, nslab,
+                     slab_stride, row0, amax, planes, ps, exps);
+}
+
+template <int NV>
+void ln_bwd_h3p_launch(const float* dy, const float* zsave, const float* mean, const float* rstd, const float* gamma,
+                       float* dz, float* pg, float* pb, float* pbias, int rows, float p, uint64_t seed, uint64_t off,
+                       uint16_t* planes, int64_t ps, int8_t* exps, hipStream_t st) {
+  hipLaunchKernelGGL((ln_bwd_h3p_kernel<NV>), dim3(rows / 32), dim3(64 * kLnH3pWaves), 0, st, dy, zsave, mean, rstd,
+                     gamma, dz, pg, pb, pbias, p, seed, off, g_seed_dev, planes, ps, exps);
+}
+
+template <int NV, typename T>
 void ln_bwd_launch(const void* dy, const float* zsave, const float* mean, const float* rstd, const float* gamma,
                    void* dz, void* da, float* pg, float* pb, float* pbias, int rows, float p, uint64_t seed,
                    uint64_t off, int mode, uint16_t* dap, int64_t daps, float* amax, hipStream_t st) {
@@ -496,6 +741,30 @@ int launch_ln_fwd(int dtype, const void* a, const float* bias, const void* resid
     HS_DISPATCH_H(H, (ln_fwd_launch<NV, bf16_t>(a, bias, resid, gamma, beta, y, zsave, mean, rstd, rows, eps, p, seed,
                                                 off, mode, nullptr, 0, 1, 0, row0, amax, st)));
   }
+  return 0;
+}
+
+// LayerNorm forward writing y also as h3p planes (fp32 only; rows a multiple of 32)
+int launch_ln_fwd_h3p(const void* a, const float* bias, const void* resid, const float* gamma, const float* beta,
+                      void* y, float* zsave, float* mean, float* rstd, int rows, int H, float eps, float p,
+                      uint64_t seed, uint64_t off, int mode, int nslab, int64_t slab_stride, int row0, float* amax,
+                      void* planes, int64_t ps, int8_t* exps, hipStream_t st) {
+  if (rows <= 0 || rows % 32 || !planes || !exps || ps % 4) return -1;
+  if (nslab < 1 || (nslab > 1 && (slab_stride < (int64_t)rows * H || slab_stride % 4))) return -1;
+  HS_DISPATCH_H(H, (ln_fwd_h3p_launch<NV, float>(a, bias, resid, gamma, beta, y, zsave, mean, rstd, rows, eps, p, seed,
+                                                 off, mode, nslab, slab_stride, row0, amax, (uint16_t*)planes, ps, exps,
+                                                 st)));
+  return 0;
+}
+
+// LayerNorm backward (bias-dropout-residual mode, fp32) writing da as h3p planes; partials are
+// [rows / 32][H] (ln_bwd_h3p_blocks)
+int launch_ln_bwd_h3p(const float* dy, const float* zsave, const float* mean, const float* rstd, const float* gamma,
+                      float* dz, float* pg, float* pb, float* pbias, int rows, int H, float p, uint64_t seed,
+                      uint64_t off, void* planes, int64_t ps, int8_t* exps, hipStream_t st) {
+  if (rows <= 0 || rows % 32 || !planes || !exps || !dz || ps % 4) return -1;
+  HS_DISPATCH_H(H, (ln_bwd_h3p_launch<NV>(dy, zsave, mean, rstd, gamma, dz, pg, pb, pbias, rows, p, seed, off,
+                                          (uint16_t*)planes, ps, exps, st)));
   return 0;
 }
 

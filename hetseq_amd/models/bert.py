@@ -343,14 +343,15 @@ class BertLayer(nn.Module):
 
     def _weights(self):
         """Kernel-side weight views.  With a flat store they are fixed views into its buffers
-        (parameters are updated in place), so they are built once and cached."""
+        (parameters are updated in place), so they are built once and cached.  ``W.h3p``: the GEMM
+        weights' h3p planes this forward's encoder refreshed (None: the layer runs another engine)."""
         cached = getattr(self, "_hs_wcache", None)
-        if cached is not None:
-            return cached
-        W = self._build_weights()
-        if getattr(self, "_hs_store", None) is not None:
-            self._hs_wcache = W
-        return W
+        if cached is None:
+            cached = self._build_weights()
+            if getattr(self, "_hs_store", None) is not None:
+                self._hs_wcache = cached
+        cached.h3p = self.__dict__.get("_hs_h3p_cur")
+        return cached
 
     def _build_weights(self):
         from hetseq_amd.ops.bert_ops import LayerWeights
@@ -694,6 +695,7 @@ class BertModel(BertPreTrainedModel):
             seq2d, pooled = self.fused_forward(input_ids, token_type_ids, attention_mask, checkpoint_activations)
             seq = seq2d.view(*input_ids.shape, -1)
             return ([seq] if output_all_encoded_layers else seq), pooled
+        _flush_lazy_grads(self)
         mask = self.additive_mask(attention_mask, self.embeddings.word_embeddings.weight.dtype)
         layers = self.encoder(self.embeddings(input_ids, token_type_ids), mask,
                               output_all_encoded_layers=output_all_encoded_layers,
@@ -715,7 +717,9 @@ class BertModel(BertPreTrainedModel):
         Ws = [blk._weights() for blk in self.encoder.layer]
         if any(getattr(W, "planes", False) for W in Ws):
             return None, None
-        weights = [w for W in Ws for w in (W.wqkv, W.wo, W.w1, W.w2)] + list(extra_weights)
+        # (h3p engine: the layers' products need no |max| -- their slots stay reserved, unmeasured)
+        weights = [None if G.h3p_active(self.compute_dtype) else w for W in Ws
+                   for w in (W.wqkv, W.wo, W.w1, W.w2)] + list(extra_weights)
         L, NS = len(Ws), LayerAmax.NS
         pool = G.AmaxPool(weights, 2 + L * NS + extra_slots, self.embeddings.word_embeddings.weight.device, split=4)
         plan = []
@@ -739,6 +743,7 @@ class BertModel(BertPreTrainedModel):
         B, S = input_ids.shape
         mask = attention_mask.to(torch.int64).contiguous()
         pool, plan = amax if amax is not None else self._amax_plan()
+        self._h3p_refresh(B * S)
         range_push("embeddings")
         x = self.embeddings.fused(input_ids, token_type_ids, self.compute_dtype,
                                   amax=pool.act(0) if pool is not None else None)
@@ -759,6 +764,42 @@ class BertModel(BertPreTrainedModel):
             pool.wait_rest()  # (one-layer models: the head's weights)
         return x
 
+    def _h3p_refresh(self, rows):
+        """h3p engine: split every layer's GEMM weights into block-scaled planes (one launch over all
+        of them -- the weights change in place at every update) and hand each layer its planes; the
+        layers of a forward the engine does not tile get None (they run the h3 engine)."""
+        from types import SimpleNamespace
+
+        from hetseq_amd.ops import gemm as G
+        from hetseq_amd.ops import h3p
+
+        blks = list(self.encoder.layer)
+        dev = self.embeddings.word_embeddings.weight.device
+        cfg = self.config
+        use = (G.h3p_active(self.compute_dtype) and dev.type == "cuda" and all(b.fused_ok(None, 32) for b in blks)
+               and h3p.ok_shape(rows, cfg.hidden_size, cfg.intermediate_size, 3 * cfg.hidden_size))
+        if not use:
+            for b in blks:
+                b.__dict__["_hs_h3p_cur"] = None
+            return
+
+        cached = self.__dict__.get("_hs_h3p")
+        store = getattr(self, "_hs_store", None)
+        if cached is None or cached[0] is not store or store is None:
+            pairs, per = [], []
+            for b in blks:
+                b.__dict__["_hs_h3p_cur"] = None
+                W = b._weights()
+                hp = SimpleNamespace(**{k: h3p.empty(getattr(W, k).shape[0], getattr(W, k).shape[1], dev)
+                                        for k in ("wqkv", "wo", "w1", "w2")})
+                pairs += [(getattr(W, k), getattr(hp, k)) for k in ("wqkv", "wo", "w1", "w2")]
+                per.append(hp)
+            cached = (store, h3p.SplitTable(pairs, dev), per)
+            self.__dict__["_hs_h3p"] = cached
+        cached[1].run()
+        for b, hp in zip(blks, cached[2]):
+            b.__dict__["_hs_h3p_cur"] = hp
+
     def fused_forward(self, input_ids, token_type_ids, attention_mask, checkpoint_activations=False):
         """Fused encoder + pooler: (sequence output [B*S, H], pooled [B, H])."""
         x = self.fused_encoder(input_ids, token_type_ids, attention_mask, checkpoint_activations)
@@ -769,6 +810,15 @@ class BertModel(BertPreTrainedModel):
 def _xent(logits, target, ignore_index=-100):
     """Cross-entropy in fp32 whatever the compute dtype."""
     return F.cross_entropy(logits.float(), target, ignore_index=ignore_index)
+
+
+def _flush_lazy_grads(module):
+    """Before a forward whose backward is not (entirely) the fused one: gradient regions a lazy
+    zero_grad left pending for the fused store-mode writers (runtime/flat.py ``cover``) are cleared
+    now, since autograd -- not those writers -- will accumulate into them."""
+    store = getattr(module, "_hs_store", None)
+    if store is not None:
+        store.flush_lazy()
 
 
 class BertForPreTraining(BertPreTrainedModel):
@@ -787,6 +837,7 @@ class BertForPreTraining(BertPreTrainedModel):
         if labelled and self.bert._can_fuse(input_ids):
             return self._fused_loss(input_ids, token_type_ids, attention_mask, masked_lm_labels, next_sentence_label,
                                     checkpoint_activations)
+        _flush_lazy_grads(self)
         seq, pooled = self.bert(input_ids, token_type_ids, attention_mask, output_all_encoded_layers=False,
                                 checkpoint_activations=checkpoint_activations)
         mlm_scores, nsp_scores = self.cls(seq, pooled)

@@ -117,6 +117,50 @@ def ln_fwd(a, gamma, beta, eps=1e-12, bias=None, resid=None, p=0.0, mode=0, seed
     return y, z, mean, rstd
 
 
+def ln_fwd_h3p(a, gamma, beta, eps, bias, resid, p, seed, off, outs, row0, hp, amax=None):
+    """ln_fwd (bias-dropout-residual mode, fp32) that also writes y as h3p planes into ``hp`` (an
+    ops.h3p.HP over the same rows): the next product's operand without a split pass."""
+    nslab, stride = 1, 0
+    if a.dim() == 3:
+        nslab, stride = a.shape[0], a.stride(0)
+        a = a[0]
+    rows, H = a.shape
+    y, z, mean, rstd = outs
+    hip().ln_fwd_h3p(a.data_ptr(), bias.data_ptr() if bias is not None else 0,
+                     resid.data_ptr() if resid is not None else 0, gamma.data_ptr(), beta.data_ptr(), y.data_ptr(),
+                     z.data_ptr(), mean.data_ptr(), rstd.data_ptr(), rows, H, float(eps), float(p), seed, off, 1,
+                     nslab, stride, int(row0), G.slot_ptr(amax), hp.data_ptr(), hp.ps, hp.exps_ptr(), stream_handle())
+    return y
+
+
+def ln_bwd_h3p(dy, z, mean, rstd, gamma, p, seed, off, hp, acc=None, side=False):
+    """LN backward of the bias-dropout-residual LN: dz (fp32, returned) and da written only as h3p
+    planes into ``hp``; parameter gradients (dgamma, dbeta, dbias) accumulated into ``acc`` (flat-store
+    views; finalised on the weight-gradient stream with ``side``) or returned fresh."""
+    rows, H = dy.shape
+    nb = rows // 32
+    part = _colpart_buf(nb, H, dy.device)
+    dz = torch.empty_like(dy)
+    hip().ln_bwd_h3p(dy.data_ptr(), z.data_ptr(), mean.data_ptr(), rstd.data_ptr(), gamma.data_ptr(), dz.data_ptr(),
+                     part[0].data_ptr(), part[1].data_ptr(), part[2].data_ptr(), rows, H, float(p), seed, off,
+                     hp.data_ptr(), hp.ps, hp.exps_ptr(), stream_handle())
+    if acc is not None:
+        outs = list(acc[:3])
+
+        def fin():
+            hip().colpart_finalize([part[i].data_ptr() for i in range(3)], [o.data_ptr() for o in outs], nb, H, 1,
+                                   stream_handle())
+        if side:
+            streams.run(dy.device, fin, part)
+        else:
+            fin()
+    else:
+        outs = torch.empty((3, H), dtype=torch.float32, device=dy.device)
+        hip().colpart_finalize([part[i].data_ptr() for i in range(3)], [outs[i].data_ptr() for i in range(3)], nb, H,
+                               0, stream_handle())
+    return dz, outs[0], outs[1], outs[2]
+
+
 def ln_bwd(dy, z, mean, rstd, gamma, p=0.0, mode=0, seed=0, off=0, want_dz=True, want_da=False, dz_out=None,
            acc=None, side=False, da_planes=None, amax=None):
     """LN backward.  ``acc`` = (dgamma, dbeta[, dbias]) fp32 tensors to ACCUMULATE into
@@ -231,6 +275,28 @@ def attn_bwd(qkv, mask, ctx, dctx, lse, B, S, NH, p, seed=0, off=0, bias=None, a
                           G.slot_ptr(amax) if amax is not None else 0)
     if amax is not None and not done:
         G.amax_into(dqkv, amax)
+    return dqkv
+
+
+def attn_fwd_h3p(qkv, mask, B, S, NH, p, seed, off, bias, outs, b0, hp):
+    """attn_fwd on the h3 attention kernel that also writes ctx as h3p planes into ``hp`` (an
+    ops.h3p.HP over the same rows): the output projection's operand without a split pass."""
+    ctx, lse, dmask = outs
+    hip().attn_fwd_h3p(qkv.data_ptr(), mask.data_ptr(), bias.data_ptr() if bias is not None else 0, ctx.data_ptr(),
+                       lse.data_ptr(), dmask.data_ptr() if dmask is not None else 0, B, S, NH, float(p), seed, off,
+                       int(b0) * NH, hp.data_ptr(), hp.ps, hp.exps_ptr(), stream_handle())
+    return ctx
+
+
+def attn_bwd_h3p(qkv, mask, ctx, dctx, lse, B, S, NH, p, bias, hp):
+    """attn_bwd on the h3 attention kernel that also writes dqkv as h3p planes into ``hp``."""
+    lse, dmask = lse
+    dqkv = torch.empty_like(qkv)
+    dbuf = torch.empty_like(lse)
+    hip().attn_bwd_h3p(qkv.data_ptr(), mask.data_ptr(), bias.data_ptr() if bias is not None else 0, ctx.data_ptr(),
+                       dctx.data_ptr(), lse.data_ptr(), dbuf.data_ptr(), dqkv.data_ptr(),
+                       dmask.data_ptr() if dmask is not None else 0, B, S, NH, float(p), hp.data_ptr(), hp.ps,
+                       hp.exps_ptr(), stream_handle())
     return dqkv
 
 
@@ -421,7 +487,7 @@ class LayerWeights(object):
     """Compute views of one encoder layer's weights: fp32 master, bf16 shadow, or (fp32 plane
     engine, ``planes`` True) the split-bf16 plane views (ops.gemm.Planes) of the GEMM weights."""
 
-    __slots__ = ("wqkv", "bqkv", "wo", "bo", "g1", "b1", "w1", "bi", "w2", "b2", "g2", "bb2", "planes", "bwd")
+    __slots__ = ("wqkv", "bqkv", "wo", "bo", "g1", "b1", "w1", "bi", "w2", "b2", "g2", "bb2", "planes", "bwd", "h3p")
 
 
 class LayerAmax(object):
@@ -515,6 +581,8 @@ def _layer_forward(x, mask, W, cfg, save, am=None):
     in gemm.remember_planes for the next layer), the GELU epilogue (f1, planes only) -- and by a
     split pass for the attention output and the embedding output; saved planes feed the weight
     gradients of the backward."""
+    if getattr(W, "h3p", None) is not None:
+        return _layer_forward_h3p(x, mask, W, cfg, save, am)
     if _fwd_split_ok(x, mask, W, cfg):
         return _layer_forward_split(x, mask, W, cfg, save, am)
     streams.chain_join(x.device)  # one chain from here: the half-batch chains meet first
@@ -562,6 +630,165 @@ def _layer_forward(x, mask, W, cfg, save, am=None):
     return h2, None
 
 
+# ----------------------------------------------------------------- encoder layer on the h3p engine
+# fp32 products as three fp16 MFMA products over block-scaled split planes written once per tensor
+# (ops/h3p.py, csrc/kernels/gemm_h3p.hip).  K slices of the forward's two N = 768 products, whose
+# tile grids (48-96 tiles per half-batch chain) would leave most of the chip idle; their slabs go
+# straight into the LayerNorm forward (no reduce pass).
+_H3P_KS_WO = int(os.environ.get("HETSEQ_H3P_KS_WO", "2"))
+_H3P_KS_W2 = int(os.environ.get("HETSEQ_H3P_KS_W2", "4"))
+
+
+class _OneChain(object):
+    """The single-chain stand-in for streams.fwd_halves (a batch too small to split)."""
+
+    def __enter__(self):
+        return iter((0,))
+
+    def __exit__(self, *exc):
+        return False
+
+
+def _layer_forward_h3p(x, mask, W, cfg, save, am=None):
+    """The layer forward on h3p operands (``W.h3p``: the GEMM weights' planes).  Like
+    _layer_forward_split, the batch runs as two half-batch chains on two streams when it splits
+    evenly into 128-row halves; each op writes its half of the whole-batch tensors.  Operand planes:
+    the layer input's from the previous layer (h3p.recall) or a split pass, the GELU output's from the
+    FFN-in GEMM's epilogue (no fp32 copy of it exists), the rest from split passes after their
+    producers."""
+    from hetseq_amd.ops import h3p
+
+    B, S, NH, p_h, p_a, eps, seeds = cfg
+    (s_a, o_a), (s_1, o_1), (s_2, o_2) = seeds
+    Wp = W.h3p
+    rows, H = x.shape
+    F = W.w1.shape[0]
+    dev, f32 = x.device, torch.float32
+    halves_ok = (B % 2 == 0 and (rows // 2) % 128 == 0 and rows >= 1024 and streams.enabled() and _FWD_SPLIT)
+    if not halves_ok:
+        streams.chain_join(dev)
+    xp = h3p.of(x)
+    qkv = torch.empty((rows, 3 * H), dtype=f32, device=dev)
+    ctx_ = torch.empty((rows, H), dtype=f32, device=dev)
+    lse = torch.empty((B * NH * S,), dtype=f32, device=dev)
+    dmask = torch.empty((B * NH * S * (S // 32),), dtype=torch.int32, device=dev) if p_a > 0 else None
+    h1, z1, h2, z2 = (torch.empty((rows, H), dtype=f32, device=dev) for _ in range(4))
+    m1, r1, m2, r2 = (torch.empty((rows,), dtype=f32, device=dev) for _ in range(4))
+    f1pre = torch.empty((rows, F), dtype=f32, device=dev)
+    ctxp, h1p, h2p = (h3p.empty(rows, H, dev) for _ in range(3))
+    f1p = h3p.empty(rows, F, dev)
+    nh = 2 if halves_ok else 1
+    hr, hb = rows // nh, B // nh
+    nl, nm = hb * NH * S, hb * NH * S * (S // 32)
+    with (streams.fwd_halves(dev) if halves_ok else _OneChain()) as halves:
+        for h in halves:
+            r = slice(h * hr, (h + 1) * hr)
+            r0, r1_ = h * hr, (h + 1) * hr
+            sl = (lambda off: am.a(off + h)) if am is not None else (lambda off: None)
+            h3p.gemm(xp.rows_slice(r0, r1_), Wp.wqkv, 0, 1, out=qkv[r])
+            attn_fwd_h3p(qkv[r], mask[h * hb:(h + 1) * hb], hb, S, NH, p_a, s_a, o_a, W.bqkv,
+                         (ctx_[r], lse[h * nl:(h + 1) * nl], dmask[h * nm:(h + 1) * nm] if dmask is not None else None),
+                         h * hb, ctxp.rows_slice(r0, r1_))
+            a = h3p.gemm(ctxp.rows_slice(r0, r1_), Wp.wo, 0, 1, ksplit=_H3P_KS_WO, slab_only=True)
+            ln_fwd_h3p(a, W.g1, W.b1, eps, W.bo, x[r], p_h, s_1, o_1, (h1[r], z1[r], m1[r], r1[r]), r0,
+                       h1p.rows_slice(r0, r1_))
+            h3p.gemm(h1p.rows_slice(r0, r1_), Wp.w1, 0, 1, bias=W.bi, epi=h3p.EPI_GELU, aux=f1pre[r],
+                     planes_out=f1p.rows_slice(r0, r1_))
+            o = h3p.gemm(f1p.rows_slice(r0, r1_), Wp.w2, 0, 1, ksplit=_H3P_KS_W2, slab_only=True)
+            ln_fwd_h3p(o, W.g2, W.bb2, eps, W.b2, h1[r], p_h, s_2, o_2, (h2[r], z2[r], m2[r], r2[r]), r0,
+                       h2p.rows_slice(r0, r1_), amax=sl(6))
+    h3p.remember(h2, h2p)  # the next layer's QKV operand
+    keep = (xp.planes, xp.exps, ctxp.planes, ctxp.exps, h1p.planes, h1p.exps, f1p.planes, f1p.exps, h2p.planes,
+            h2p.exps)
+    streams.chain_keep(x, mask, qkv, ctx_, lse, dmask, h1, z1, m1, r1, f1pre, h2, z2, m2, r2, *keep)
+    if save:
+        return h2, (qkv, ctx_, lse, dmask, z1, m1, r1, None, f1pre, None, z2, m2, r2, x, None,
+                    ("h3p", xp, ctxp, h1p, f1p))
+    return h2, None
+
+
+def _layer_backward_h3p(ctx, dh2, x, saved, W, meta, cfg):
+    """The layer backward on h3p operands: the data-gradient chain on the compute stream, the weight
+    gradients on the side stream (split-K slices summed by the reduce pass into the flat store)."""
+    from hetseq_amd.ops import h3p
+
+    qkv, ctx_, lse, dmask, z1, m1, r1, _, f1pre, _, z2, m2, r2, _, _, hps = saved
+    _, xp, ctxp, h1p, f1p = hps
+    Wp = W.h3p
+    B, S, NH, p_h, p_a, eps, seeds = cfg
+    (s_a, o_a), (s_1, o_1), (s_2, o_2) = seeds
+    dh2 = dh2.contiguous()
+    rows, H = dh2.shape
+    F = W.w1.shape[0]
+    dev = dh2.device
+    sink = meta.get("grad_sink")
+    Gv = sink() if sink is not None else None
+    acc = Gv is not None
+    side = acc and streams.enabled()
+    store = meta.get("store")
+    wacc = acc and not (side and _FRESH_WGRAD and store is not None and store.claim_fresh())
+    if not acc:
+        Gv = LayerWeights()
+        Gv.wqkv = torch.empty_like(W.wqkv)
+        Gv.bqkv = torch.zeros(3 * H, dtype=torch.float32, device=dev)
+        Gv.wo, Gv.w1, Gv.w2 = torch.empty_like(W.wo), torch.empty_like(W.w1), torch.empty_like(W.w2)
+        Gv.bi = torch.zeros(F, dtype=torch.float32, device=dev)
+
+    def wgrad(dyp, xpp, out):
+        """out (+)= dy^T x on the side stream (or in line without a flat store / side stream)."""
+        accumulate = wacc if side else acc
+        ks = streams.side_ksplit(out.shape[0], out.shape[1]) if side else 2
+        ks = max(ks or 1, -(-rows // 4096))  # a slice is at most 4096 tokens deep
+
+        def run():
+            if store is not None:
+                (store.ensure_zero if accumulate else store.mark_stored)(out)
+            h3p.gemm(dyp, xpp, 1, 0, out=out, beta=1.0 if accumulate else 0.0, ksplit=ks)
+        if side:
+            streams.run(dev, run, dyp.planes, dyp.exps, xpp.planes, xpp.exps)
+        else:
+            run()
+
+    with streams.coalesced():  # LN2 parameter gradients + the FFN-out weight gradient
+        da2p = h3p.empty(rows, H, dev)
+        dz2, dg2, dbb2, db2 = ln_bwd_h3p(dh2, z2, m2, r2, W.g2, p_h, s_2, o_2, da2p,
+                                         acc=(Gv.g2, Gv.bb2, Gv.b2) if acc else None, side=side)
+        wgrad(da2p, f1p, Gv.w2)
+    # FFN-in data gradient through the GELU: planes out only, the FFN-in bias gradient from the
+    # epilogue's column partials
+    df1p = h3p.empty(rows, F, dev)
+    part = torch.empty((rows // 128, F), dtype=torch.float32, device=dev)
+    h3p.gemm(da2p, Wp.w2, 0, 0, bias=W.bi, epi=h3p.EPI_DGELU, aux=f1pre, part=part, colsum=Gv.bi,
+             colsum_acc=acc, planes_out=df1p)
+    wgrad(df1p, h1p, Gv.w1)
+    h3p.gemm(df1p, Wp.w1, 0, 0, out=dz2, beta=1.0)  # dh1 = dz2 + df1pre @ W1
+    with streams.coalesced():  # LN1 parameter gradients + the attention-output weight gradient
+        da1p = h3p.empty(rows, H, dev)
+        dz1, dg1, db1, dbo = ln_bwd_h3p(dz2, z1, m1, r1, W.g1, p_h, s_1, o_1, da1p,
+                                        acc=(Gv.g1, Gv.b1, Gv.bo) if acc else None, side=side)
+        wgrad(da1p, ctxp, Gv.wo)
+    dctx = h3p.gemm(da1p, Wp.wo, 0, 0)
+    dqkvp = h3p.empty(rows, 3 * H, dev)
+    dqkv = attn_bwd_h3p(qkv, mask_of(ctx), ctx_, dctx, (lse, dmask), B, S, NH, p_a, W.bqkv, dqkvp)
+    with streams.coalesced():  # QKV weight and bias gradients
+        wgrad(dqkvp, xp, Gv.wqkv)
+        if side:
+            streams.run(dev, lambda: colsum(dqkv, acc=Gv.bqkv), dqkv)
+        else:
+            colsum(dqkv, acc=Gv.bqkv)
+    h3p.gemm(dqkvp, Wp.wqkv, 0, 0, out=dz1, beta=1.0)  # dx = dz1 + dqkv @ Wqkv
+    if acc:
+        return (dz1, None, None) + (None,) * 16
+    dWqkv, dbqkv = Gv.wqkv, Gv.bqkv
+    return (dz1, None, None,
+            dWqkv[:H], dbqkv[:H], dWqkv[H:2 * H], dbqkv[H:2 * H], dWqkv[2 * H:], dbqkv[2 * H:],
+            Gv.wo, dbo, dg1, db1, Gv.w1, Gv.bi, Gv.w2, db2, dg2, dbb2)
+
+
+def mask_of(ctx):
+    return ctx.saved_tensors[1]
+
+
 class FusedBertLayer(torch.autograd.Function):
     """One post-LN BERT encoder layer.  Inputs after ``x, mask, meta`` are the
     16 parameters in reference order (q.w, q.b, k.w, k.b, v.w, v.b, o.w, o.b,
@@ -573,9 +800,13 @@ class FusedBertLayer(torch.autograd.Function):
         h2, saved = _layer_forward(x, mask, W, cfg, save=not recompute, am=meta.get("amax"))
         ctx.meta = meta
         ctx.cfg = cfg
+        ctx.h3p = None
         if recompute:
             ctx.save_for_backward(x, mask)
         else:
+            if len(saved) > 15:  # h3p: the operand planes travel as a ctx attribute (not tensors)
+                ctx.h3p = saved[15]
+                saved = saved[:15]
             ctx.save_for_backward(x, mask, *saved)
         return h2
 
@@ -589,8 +820,10 @@ class FusedBertLayer(torch.autograd.Function):
                 _, saved = _layer_forward(x, mask, W, cfg, save=True, am=meta.get("amax"))
         else:
             x, mask = ctx.saved_tensors[:2]
-            saved = ctx.saved_tensors[2:]
-        qkv, ctx_, lse, dmask, z1, m1, r1, h1, f1pre, f1, z2, m2, r2, xin, cin = saved
+            saved = ctx.saved_tensors[2:] + (ctx.h3p,)
+        if isinstance(saved[-1], tuple) and saved[-1][0] == "h3p":
+            return _layer_backward_h3p(ctx, dh2, x, saved, W, meta, cfg)
+        qkv, ctx_, lse, dmask, z1, m1, r1, h1, f1pre, f1, z2, m2, r2, xin, cin = saved[:15]
         if getattr(W, "planes", False) and W.bwd is not W:
             W = W.bwd  # forward-only planes: the backward on the in-kernel-split engine (fp32 operands)
         pl = getattr(W, "planes", False)

@@ -39,11 +39,13 @@ from hetseq_amd.ops._C import hip, stream_handle
 
 GEMM_CHOICES: dict = {}
 _MODE = os.environ.get("HETSEQ_GEMM", "auto")
-_FP32_DT = {"native": 0, "x6": 2, "x3": 3, "h3": 4}
+# h3p: the encoder layers' products on pre-split block-scaled planes (ops/h3p.py, gemm_h3p.hip); every
+# other fp32 product (the pre-training heads, standalone calls) on the h3 engine (dtype code 4)
+_FP32_DT = {"native": 0, "x6": 2, "x3": 3, "h3": 4, "h3p": 4}
 _FP32 = os.environ.get("HETSEQ_FP32_GEMM", "h3")
 FP32_DEFAULT = _FP32
-assert _FP32 in _FP32_DT, "HETSEQ_FP32_GEMM must be one of native|x6|x3|h3"
-SPLIT_ENGINES = ("x6", "h3")  # the fp32-level split engines (x3 is a benchmarking variant)
+assert _FP32 in _FP32_DT, "HETSEQ_FP32_GEMM must be one of native|x6|x3|h3|h3p"
+SPLIT_ENGINES = ("x6", "h3", "h3p")  # the fp32-level split engines (x3 is a benchmarking variant)
 _SLABS: dict = {}  # (device, stream) -> split-K partial-sum workspace
 
 EPI_NONE, EPI_BIAS, EPI_GELU, EPI_DGELU = 0, 1, 2, 3
@@ -591,7 +593,7 @@ def gemm(a, b, ta=False, tb=False, out=None, bias=None, epi=EPI_NONE, beta=0.0, 
         scratch = None
         ks = [0]  # split-K of the HIP engine: 0 = kernel heuristic, else measured (auto mode)
 
-        if _FP32 == "h3" and amax is None:  # one |max| pass per operand, shared by the measuring runs
+        if _FP32 in ("h3", "h3p") and amax is None:  # one |max| pass per operand, shared by the measuring runs
             amax = (amax_of(a), amax_of(b))
 
         def run_hip():
@@ -652,7 +654,7 @@ def decoder_logits(t2, w, bias, amax=None):
     buf = torch.empty((R, Vp), dtype=torch.float32, device=t2.device)
     key = (R, V, H, "decoder_fwd")
 
-    if _FP32 == "h3" and amax is None:
+    if _FP32 in ("h3", "h3p") and amax is None:
         amax = (amax_of(t2), amax_of(w))
 
     def run_hip():
@@ -675,7 +677,7 @@ def decoder_dgrad(dlogits_buf, w, V, amax=None):
     out = torch.empty((R, H), dtype=torch.float32, device=w.device)
     key = (R, H, V, "decoder_dgrad")
     ks = [0]
-    if _FP32 == "h3" and amax is None:
+    if _FP32 in ("h3", "h3p") and amax is None:
         amax = (amax_of(dlogits_buf), amax_of(w))
 
     def run_hip():
@@ -713,7 +715,7 @@ def decoder_wgrad(dlogits_buf, t2, V, out, accumulate, amax=None):
     H = t2.shape[1]
     key = (V, H, R, "decoder_wgrad", bool(accumulate))
     beta = 1.0 if accumulate else 0.0
-    if _FP32 == "h3" and amax is None:
+    if _FP32 in ("h3", "h3p") and amax is None:
         amax = (amax_of(dlogits_buf), amax_of(t2))
 
     def run_hip(dst):
@@ -767,7 +769,7 @@ def linear_fwd_partials(x, w, ksplit=None, amax=None):
             slab = _slab(M, N, ks, x.device)
             if slab is not None:
                 am, keep = (0, 0, 0, 0), []
-                if _FP32 == "h3":
+                if _FP32 in ("h3", "h3p"):
                     am = _amax_ptr(x, amax[0] if amax is not None else None, keep) + _amax_ptr(
                         w, amax[1] if amax is not None else None, keep)
                 rc = hip().gemm(_FP32_DT[_FP32], 0, 1, M, N, K, x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0),
@@ -862,7 +864,7 @@ def linear_gelu_fwd(x, w, b, planes_out=False, emit_planes=False, out=None, amax
         y = torch.empty_like(pre)
     if x.is_cuda and _MODE != "blas" and _hip_ok(x, w, y, b, pre):
         key = (T, N, x.shape[1], "gelu_fwd")
-        if _FP32 == "h3" and amax is None:
+        if _FP32 in ("h3", "h3p") and amax is None:
             amax = (amax_of(x), amax_of(w))
 
         def run_hip(amo=None):
@@ -913,7 +915,7 @@ def linear_dgrad_dgelu(dy, w, pre, b, db_acc=None, planes_out=False, amax=None, 
     if dy.is_cuda and _MODE != "blas" and _hip_ok(dy, w, dpre, pre, b):
         key = (T, N, dy.shape[1], "dgelu")
         part = torch.empty(((T + 63) // 64, N), dtype=torch.float32, device=dy.device)
-        if _FP32 == "h3" and amax is None:
+        if _FP32 in ("h3", "h3p") and amax is None:
             amax = (amax_of(dy), amax_of(w))
 
         def run_hip(out_db, acc, amo=None):
@@ -988,7 +990,8 @@ class AmaxPool(object):
 
     * ``w(i)``: weight ``i`` of the list given at construction -- filled right away by ONE
       ``amax_seg`` launch over all of them (weights change in place every update, so every forward
-      measures them again; ~50 us for BERT-base's 86 M GEMM weights);
+      measures them again; ~50 us for BERT-base's 86 M GEMM weights); a None entry reserves its
+      slot unmeasured;
     * ``act(i, n)``: activation / gradient slots, atomically maxed by the kernels that produce
       those tensors (LN forward / backward, GELU / dGELU epilogues, embedding) or by ``amax_of``.
     Each slot has exactly one producer stream, and its consumers are ordered after that producer,
@@ -1001,6 +1004,13 @@ class AmaxPool(object):
         self.rest = None
         from hetseq_amd.runtime import streams
 
+        first = next((i for i, w in enumerate(weights) if w is not None), len(weights))
+        if first > 0:  # leading reserved slots (h3p engine layers): measure only the rest, in line
+            rest = [w for w in weights[first:]]
+            if rest and all(w is not None for w in rest):
+                base, tab, nblk = _seg_table(rest)
+                hip().amax_seg(base, tab.data_ptr(), nblk, self.ptr + 4 * SLOT_FLOATS * first, stream_handle())
+            return
         if 0 < split < len(weights) and _SPLIT_WEIGHT_AMAX and streams.enabled() and self.buf.is_cuda:
             # weights [0, split) now; the rest on the side stream, beside the first layer's work
             # (consumers on the current stream call wait_rest() first; the side stream's own later
@@ -1038,4 +1048,9 @@ class AmaxPool(object):
 
 def h3_active(dtype=torch.float32):
     """True when fp32 GEMMs run on the h3 engine (operand |max| slots are worth tracking)."""
-    return _FP32 == "h3" and _MODE != "blas" and dtype == torch.float32
+    return _FP32 in ("h3", "h3p") and _MODE != "blas" and dtype == torch.float32
+
+
+def h3p_active(dtype=torch.float32):
+    """True when the encoder layers' fp32 products run on the h3p plane engine (ops/h3p.py)."""
+    return _FP32 == "h3p" and _MODE != "blas" and dtype == torch.float32

@@ -200,7 +200,7 @@ def add_mi355x_args(parser):
     group = parser.add_argument_group("MI355X runtime (extensions)")
     group.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
                        help="compute dtype: fp32 (reference parity) or bf16 MFMA with fp32 master weights")
-    group.add_argument("--fp32-gemm", default=None, choices=["h3", "x6", "native"],
+    group.add_argument("--fp32-gemm", default=None, choices=["h3p", "h3", "x6", "native"],
                        help="fp32 GEMM engine: h3 = three split-fp16 products with per-tensor power-of-two "
                             "scales, x6 = six split-bf16 products (both on the 16-bit matrix cores with "
                             "fp32-level error), native = exact-fp32 MFMA (HETSEQ_FP32_GEMM)")

@@ -45,10 +45,12 @@ def _stream(s=None):
 class NativeComm(object):
     """One RCCL communicator over the ranks of ``group`` (all of them take part in construction)."""
 
-    def __init__(self, group=None, timeout_s=1800.0, device=None, rendezvous=True):
-        """``rendezvous=False``: only the local part (device, comm stream) and the unique-id
-        exchange through the c10d store; :meth:`rendezvous` then enters ncclCommInitRank (create()
-        agrees across ranks in between)."""
+    def __init__(self, group=None, timeout_s=1800.0, device=None, rendezvous=True, key=None):
+        """``rendezvous=False``: only the process-local part (device, comm stream) -- nothing that
+        waits for another rank; :meth:`rendezvous` then exchanges the unique id and enters
+        ncclCommInitRank (create() agrees across ranks in between).  ``key``: index of the store key
+        the unique id travels under (create() draws it on every rank before any check can fail, so
+        the ranks' keys stay aligned whatever happens on one of them)."""
         mod = module()
         if mod is None:
             raise RuntimeError("hetseq_amd._comm is not built (python -m hetseq_amd.csrc.build)")
@@ -56,11 +58,8 @@ class NativeComm(object):
         self.rank = dist.get_rank(self.group)
         self.size = dist.get_world_size(self.group)
         self.device = torch.cuda.current_device() if device is None else device
-        key = "hetseq_comm_uid_%d" % next(_ids)
-        store = dist.distributed_c10d._get_default_store()
-        if self.rank == 0:
-            store.set(key, mod.unique_id())
-        self._uid = store.get(key)  # blocks until rank 0 published it (the store's own timeout applies)
+        self._key = "hetseq_comm_uid_%d" % (next(_ids) if key is None else key)
+        self._mod = mod
         self._c = mod.Comm(self.size, self.rank, self.device, float(timeout_s))
         # at interpreter exit (no explicit close): abort -- frees the communicator without waiting
         # for peers, while the HIP runtime is still alive (never from static destructors)
@@ -70,8 +69,13 @@ class NativeComm(object):
             self.rendezvous()
 
     def rendezvous(self):
-        """The blocking RCCL rendezvous (every rank of the group must call it)."""
-        self._c.init(self._uid)
+        """The blocking RCCL rendezvous (every rank of the group must call it): rank 0 publishes the
+        unique id through the c10d store, every rank fetches it and enters ncclCommInitRank."""
+        store = dist.distributed_c10d._get_default_store()
+        if self.rank == 0:
+            store.set(self._key, self._mod.unique_id())
+        uid = store.get(self._key)  # blocks until rank 0 published it (the store's own timeout applies)
+        self._c.init(uid)
 
     # ------------------------------------------------------------------ bucket path
     def all_reduce_async(self, t, producers=(), op="sum"):
@@ -218,11 +222,12 @@ def create(engine, device_is_cuda, group=None, timeout_s=1800.0, factory=None):
     Construction is a cross-rank-agreed, two-round protocol, so a local failure on one rank never
     leaves the others inside the RCCL rendezvous or with a half-working engine:
 
-    1. every rank does everything that needs no rendezvous -- module built, backend, injected
-       ``init`` fault, and the engine's local construction (device, greatest-priority comm stream,
-       rank 0's unique id published through the c10d store and fetched by all); the ranks agree
-       (c10d all-reduce) before anyone calls ncclCommInitRank, which blocks until all ranks join;
-    2. every rank enters the rendezvous and runs one all-reduce through the communicator,
+    1. every rank does everything that needs no other rank -- module built, backend, injected
+       ``init`` fault, and the engine's local construction (device, greatest-priority comm stream);
+       the ranks agree (c10d all-reduce) before anyone waits on another rank (the unique-id store
+       exchange, ncclCommInitRank), so a failure on any rank -- rank 0 included -- strands nobody;
+    2. every rank fetches rank 0's unique id through the c10d store, enters the rendezvous and
+       runs one all-reduce through the communicator,
        checking the result on the host; the ranks agree again, and on any failure every rank
        aborts its communicator (never waits for peers) and falls back to c10d.
 
@@ -234,6 +239,7 @@ def create(engine, device_is_cuda, group=None, timeout_s=1800.0, factory=None):
     NativeComm constructor (tests drive the protocol over gloo with a stand-in engine).
     """
     global LAST_STATUS
+    key = next(_ids)  # drawn on every rank, whatever follows: the unique-id store keys stay aligned
     engine = os.environ.get("HETSEQ_COMM_ENGINE", engine or "auto")
     backend = dist.get_backend(group or dist.group.WORLD)
     if factory is None and (engine == "c10d" or not device_is_cuda or backend != "nccl"):
@@ -251,7 +257,7 @@ def create(engine, device_is_cuda, group=None, timeout_s=1800.0, factory=None):
         elif _fault("init", rank):
             reason = "injected init fault on rank %d" % rank
         else:
-            nc = (factory or NativeComm)(group, timeout_s=timeout_s, rendezvous=False)
+            nc = (factory or NativeComm)(group, timeout_s=timeout_s, rendezvous=False, key=key)
     except Exception as e:  # noqa: BLE001 - any local failure turns into the agreed fallback
         reason = "%s: %s" % (type(e).__name__, e)
     if not _agree(reason is None, group, dev):

@@ -100,7 +100,7 @@ def _fallback_worker(rank, world, path, fault, q):
         closed = None
         entered = False  # the (blocking) rendezvous was entered
 
-        def __init__(self, group, timeout_s=0.0, rendezvous=True):
+        def __init__(self, group, timeout_s=0.0, rendezvous=True, key=None):
             self.group = group
             if rendezvous:
                 self.rendezvous()
@@ -139,6 +139,20 @@ def _fallback(tmp_path, fault, world=2):
         p.join(60)
         assert p.exitcode == 0
     return out
+
+
+@pytest.mark.slow
+def test_init_fault_on_rank0_strands_nobody(tmp_path):
+    """Rank 0 failing its local checks (it would have published the unique id) must not leave the
+    other ranks waiting on the store: everyone agrees on the fallback within the call."""
+    import time
+
+    t0 = time.time()
+    out = _fallback(tmp_path, "init:0", world=3)
+    assert time.time() - t0 < 100
+    assert [o[1] for o in out] == [False, False, False]
+    assert "injected init fault on rank 0" in out[0][2]["reason"]
+    assert not any(o[4] for o in out)
 
 
 @pytest.mark.slow

@@ -125,6 +125,39 @@ def test_lazy_zero_grad_matches_full_zero(cuda, side, micro):
         streams.set_enabled(old)
 
 
+@pytest.mark.parametrize("kind", ["odd_seq", "unlabelled"])
+def test_lazy_zero_grad_then_unfused_backward(cuda, kind):
+    """A fused step registers the store-covered regions; a later lazy zero_grad followed by a batch
+    the fused path does not serve (S not a multiple of 32, or no labels: autograd accumulates into the
+    covered weight / tied-decoder gradients) must give the gradients of a full zero_grad -- the
+    non-fused forward clears the pending regions first (bert.py _flush_lazy_grads)."""
+    from hetseq_amd.runtime.flat import FlatParamStore
+
+    model, cfg = _tiny(cuda)
+    model.eval()
+    model.max_predictions_per_seq = 10
+    store = FlatParamStore(model)
+    model.attach_store(store, torch.float32)
+    store.zero_grad()
+    model(*_batch(cuda, 4, 64, cfg.vocab_size)).backward()  # fused: registers the covered regions
+    assert store._cover
+    if kind == "odd_seq":
+        batch = _batch(cuda, 4, 40, cfg.vocab_size)
+        run = lambda: model(*batch).backward()  # noqa: E731
+    else:
+        ids, tt, mask = _batch(cuda, 4, 64, cfg.vocab_size)[:3]
+        run = lambda: sum(t.float().square().sum() for t in model(ids, tt, mask)).backward()  # noqa: E731
+    grads = {}
+    for lazy in (False, True):
+        store.grad.fill_(123.0)
+        store.zero_grad(lazy=lazy)
+        run()
+        store.flush_lazy()
+        torch.cuda.synchronize()
+        grads[lazy] = store.grad.clone()
+    assert torch.equal(grads[True], grads[False])
+
+
 def test_lazy_zero_grad_flushes_unclaimed_regions(cuda):
     """Covered regions no writer claimed read as zero once the gradients are read (flush_lazy), and
     ensure_zero clears a pending region exactly once."""
@@ -257,7 +290,8 @@ def _grad_report(model, ref):
     return worst, where
 
 
-@pytest.mark.parametrize("planes,engine", [("off", "x6"), ("fwd", "x6"), ("all", "x6"), ("off", "h3")])
+@pytest.mark.parametrize("planes,engine", [("off", "x6"), ("fwd", "x6"), ("all", "x6"), ("off", "h3"),
+                                           ("off", "h3p")])
 def test_bert_base_shape_matches_reference_1e4(cuda, monkeypatch, planes, engine):
     """BERT-base (H 768, L 12, 12 heads, S 128, B 8), dropout off: the fused fp32 path -- in-kernel
     split engine (six split-bf16 products, x6, or three split-fp16 products with per-tensor scales,
@@ -297,7 +331,7 @@ def test_bert_base_shape_matches_reference_1e4(cuda, monkeypatch, planes, engine
     assert worst <= 1e-4, (worst, where)
 
 
-@pytest.mark.parametrize("engine", ["x6", "h3"])
+@pytest.mark.parametrize("engine", ["x6", "h3", "h3p"])
 def test_trajectory_200_updates_tracks_reference(cuda, monkeypatch, engine):
     """200 Adam updates of a tiny BERT, fused (flat store, fused Adam) vs the torch-op oracle with
     the reference Adam math (optim.py:162-231), identical seeds and batches, dropout off: the two

@@ -1,0 +1,265 @@
+"""h3p: block-scaled split-fp16 operands and the GEMM over them (csrc/kernels/gemm_h3p.hip).
+
+Numerics are measured against fp64 next to the exact-fp32 references (library SGEMM and the
+exact-fp32 MFMA kernel), in units of |A| @ |B| -- the scale of an fp32 GEMM's own rounding."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _wide(shape, dev, gen, decades):
+    """Gradient-like data: rows scaled over ``decades`` orders of magnitude, plus 100x outliers."""
+    x = torch.randn(shape, device=dev, generator=gen)
+    x *= torch.pow(10.0, -decades * torch.rand((shape[0], 1), device=dev, generator=gen))
+    idx = torch.randint(0, x.numel(), (8,), device=dev, generator=gen)
+    x.view(-1)[idx] *= 100.0
+    return x
+
+
+def _gelu_ref(x):  # the reference's erf-GELU constant (bert_modeling.py:104-111)
+    return x * 0.5 * (1.0 + torch.erf(x / 1.41421))
+
+
+def _gelu_grad_ref(x):
+    c = 1.41421
+    return 0.5 * (1.0 + torch.erf(x / c)) + x * (0.5641895835477563 / c) * torch.exp(-(x / c) ** 2)
+
+
+def test_split_roundtrip_and_exponents(cuda):
+    """Every element keeps 22 bits below its 32 x 32 block's |max| (block exponents, not one per
+    tensor): blocks 2^40 apart in one matrix both round-trip to 2^-21 of their own |max|; zero and
+    non-finite blocks are kept as such."""
+    from hetseq_amd.ops import h3p
+
+    g = torch.Generator(device=cuda)
+    g.manual_seed(1)
+    x = torch.randn((256, 384), device=cuda, generator=g)
+    x[:32, :32] *= 2.0 ** 40
+    x[32:64, 64:96] *= 2.0 ** -40
+    x[64:96, 96:128] = 0.0
+    hp = h3p.split(x)
+    y = hp.unsplit()
+    xb = x.view(8, 32, 12, 32).abs().amax(dim=(1, 3))  # block |max|
+    err = ((y - x).abs().view(8, 32, 12, 32).amax(dim=(1, 3)) / xb.clamp_min(1e-300))
+    assert float(err[xb > 0].max()) <= 2.0 ** -21
+    assert (y[64:96, 96:128] == 0).all()
+    e = hp.exps.to(torch.int32)
+    assert int(e[0, 0]) == 14 - int(torch.floor(torch.log2(xb[0, 0])).item())
+    x2 = x.clone()
+    x2[100, 200] = float("nan")
+    x2[200, 300] = float("inf")
+    y2 = h3p.split(x2).unsplit()
+    assert torch.isnan(y2[100, 200]) and torch.isinf(y2[200, 300])
+
+
+def _operands(ta, tb, M, N, K, data, dev, g):
+    if data == "uniform":
+        a = torch.rand((K, M) if ta else (M, K), device=dev, generator=g) * 2 - 1
+        b = torch.rand((N, K) if tb else (K, N), device=dev, generator=g) * 2 - 1
+    else:  # 6 decades of row scales (beyond the old per-tensor window), magnitudes far from 1
+        a = _wide((K, M) if ta else (M, K), dev, g, 6.0) * 1e-5
+        b = _wide((N, K) if tb else (K, N), dev, g, 6.0) * 1e3
+    return a, b
+
+
+@pytest.mark.parametrize("data", ["uniform", "wide"])
+@pytest.mark.parametrize("ta,tb,M,N,K,ks", [(0, 1, 4096, 2304, 768, 1), (0, 0, 2048, 768, 3072, 2),
+                                            (1, 0, 768, 3072, 4096, 4), (0, 1, 256, 384, 64, 1),
+                                            (1, 0, 768, 768, 1024, 1), (0, 0, 512, 256, 2048, 1)])
+def test_gemm_h3p_error_matches_fp32(cuda, data, ta, tb, M, N, K, ks):
+    """All three Linear layouts, with and without split-K: error within 2x of exact-fp32 GEMMs
+    against fp64 in units of |A|@|B|, including data with 6 decades of row scale (the per-block
+    exponents keep every row's bits; the per-tensor h3 engine loses them beyond 2^18)."""
+    from hetseq_amd.ops import gemm as G
+    from hetseq_amd.ops import h3p
+
+    g = torch.Generator(device=cuda)
+    g.manual_seed(7 + M + N + K)
+    a, b = _operands(ta, tb, M, N, K, data, cuda, g)
+    At, Bt = (a.t() if ta else a), (b.t() if tb else b)
+    ref = At.double() @ Bt.double()
+    mag = At.double().abs() @ Bt.double().abs()
+    out = torch.empty(M, N, device=cuda)
+
+    def err(o):
+        return float(((o.double() - ref).abs() / mag).max())
+
+    torch.mm(At, Bt, out=out)
+    e_blas = err(out)
+    assert G._hip_gemm(a, b, ta, tb, out, fp32="native")
+    e_nat = err(out)
+    o = h3p.gemm(h3p.split(a), h3p.split(b), ta, tb, ksplit=ks)
+    e = err(o)
+    assert e <= 2.0 * max(e_blas, e_nat), (e, e_blas, e_nat)
+
+
+def test_gemm_h3p_nonfinite_propagates(cuda):
+    from hetseq_amd.ops import h3p
+
+    g = torch.Generator(device=cuda)
+    g.manual_seed(3)
+    a = torch.randn(256, 256, device=cuda, generator=g)
+    b = torch.randn(256, 256, device=cuda, generator=g)
+    a[5, 17] = float("nan")
+    o = h3p.gemm(h3p.split(a), h3p.split(b), 0, 1)
+    assert torch.isnan(o[5]).all() and torch.isfinite(o[6]).all()
+    a[5, 17] = float("inf")
+    o = h3p.gemm(h3p.split(a), h3p.split(b), 0, 1)
+    assert (~torch.isfinite(o[5])).all()
+
+
+def test_gemm_h3p_epilogues(cuda):
+    """bias, beta accumulation, split-K with bias + beta, the consumer-summed slabs, GELU (pre-
+    activation out, planes out) and dGELU (planes out, bias-gradient column sums), against fp64."""
+    from hetseq_amd.ops import h3p
+
+    g = torch.Generator(device=cuda)
+    g.manual_seed(11)
+    M, N, K = 512, 384, 768
+    x = torch.randn(M, K, device=cuda, generator=g)
+    w = torch.randn(N, K, device=cuda, generator=g) * 0.05
+    bias = torch.randn(N, device=cuda, generator=g)
+    hx, hw = h3p.split(x), h3p.split(w)
+    ref = x.double() @ w.double().t()
+    mag = x.double().abs() @ w.double().abs().t()
+
+    def rel(o, r):
+        return float(((o.double() - r).abs() / (mag + r.abs())).max())
+
+    o = h3p.gemm(hx, hw, 0, 1, bias=bias, epi=h3p.EPI_BIAS)
+    assert rel(o, ref + bias.double()) < 1e-6
+    old = torch.randn(M, N, device=cuda, generator=g)
+    o2 = old.clone()
+    h3p.gemm(hx, hw, 0, 1, out=o2, beta=1.0)
+    assert rel(o2, ref + old.double()) < 1e-6
+    o3 = old.clone()
+    h3p.gemm(hx, hw, 0, 1, out=o3, bias=bias, epi=h3p.EPI_BIAS, beta=1.0, ksplit=3)
+    assert rel(o3, ref + old.double() + bias.double()) < 1e-6
+    sl = h3p.gemm(hx, hw, 0, 1, ksplit=2, slab_only=True)
+    assert sl.shape == (2, M, N) and rel(sl[0] + sl[1], ref) < 1e-6
+    # GELU: pre-activation (un-biased) in aux, gelu(pre + bias) in fp32 and as planes
+    pre = torch.empty(M, N, device=cuda)
+    y = torch.empty(M, N, device=cuda)
+    yp = h3p.empty(M, N, cuda)
+    h3p.gemm(hx, hw, 0, 1, out=y, bias=bias, epi=h3p.EPI_GELU, aux=pre, planes_out=yp)
+    assert rel(pre, ref) < 1e-6
+    yref = _gelu_ref(pre.double() + bias.double())
+    assert float((y.double() - yref).abs().max()) < 1e-6 * (1 + float(yref.abs().max()))
+    assert torch.equal(yp.unsplit(), h3p.split(y).unsplit())
+    # dGELU: dpre = (dy @ w) * gelu'(pre + bias); planes out only; db = column sums
+    dy = torch.randn(M, N, device=cuda, generator=g)
+    w2 = torch.randn(N, N, device=cuda, generator=g) * 0.05
+    db = torch.zeros(N, device=cuda)
+    part = torch.empty(M // 128, N, device=cuda)
+    dp = h3p.empty(M, N, cuda)
+    dpf = torch.empty(M, N, device=cuda)
+    h3p.gemm(h3p.split(dy), h3p.split(w2), 0, 0, out=dpf, bias=bias, epi=h3p.EPI_DGELU, aux=pre, part=part,
+             colsum=db, planes_out=dp)
+    dref = (dy.double() @ w2.double()) * _gelu_grad_ref(pre.double() + bias.double())
+    dmag = (dy.double().abs() @ w2.double().abs()) * _gelu_grad_ref(pre.double() + bias.double()).abs()
+    assert float(((dpf.double() - dref).abs() / (dmag + 1e-30)).max()) < 1e-5
+    assert torch.equal(dp.unsplit(), h3p.split(dpf).unsplit())
+    assert float((db.double() - dref.sum(0)).abs().max()) < 1e-4 * float(dmag.sum(0).max())
+
+
+def test_split_table_many_tensors(cuda):
+    """One launch splitting several matrices (the weights): bit-identical to per-tensor splits."""
+    from hetseq_amd.ops import h3p
+
+    g = torch.Generator(device=cuda)
+    g.manual_seed(5)
+    flat = torch.randn(768 * 2304 + 768 * 768 + 3072 * 768, device=cuda, generator=g)
+    mats = [flat[:768 * 2304].view(2304, 768), flat[768 * 2304:768 * 3072].view(768, 768),
+            flat[768 * 3072:].view(3072, 768)]
+    dst = [h3p.empty(m.shape[0], m.shape[1], cuda) for m in mats]
+    tab = h3p.SplitTable(list(zip(mats, dst)), cuda)
+    tab.run()
+    for m, d in zip(mats, dst):
+        ref = h3p.split(m)
+        assert torch.equal(d.planes, ref.planes) and torch.equal(d.exps, ref.exps)
+
+
+def test_rows_slice_view(cuda):
+    """A row window of an HP operand (the half-batch chains) computes the same rows as the whole."""
+    from hetseq_amd.ops import h3p
+
+    g = torch.Generator(device=cuda)
+    g.manual_seed(9)
+    x = torch.randn(512, 768, device=cuda, generator=g)
+    w = torch.randn(256, 768, device=cuda, generator=g)
+    hx, hw = h3p.split(x), h3p.split(w)
+    full = h3p.gemm(hx, hw, 0, 1)
+    half = h3p.gemm(hx.rows_slice(256, 512), hw, 0, 1)
+    assert torch.equal(full[256:], half)
+
+
+@pytest.mark.parametrize("H,p", [(768, 0.0), (768, 0.1), (1024, 0.1)])
+def test_layernorm_h3p_planes(cuda, H, p):
+    """The LN forward / backward that write h3p planes: y, z, statistics and dz bitwise those of the
+    plain kernels, the planes bitwise split(y) / split(da) (block exponents over 32-row blocks), the
+    parameter-gradient partials (32-row blocks) equal to the plain kernel's to fp32 rounding."""
+    from hetseq_amd.ops import bert_ops as O
+    from hetseq_amd.ops import h3p
+
+    g = torch.Generator(device=cuda)
+    g.manual_seed(H)
+    rows = 256
+    slabs = torch.randn(2, rows, H, device=cuda, generator=g)
+    bias = torch.randn(H, device=cuda, generator=g)
+    resid = torch.randn(rows, H, device=cuda, generator=g)
+    gamma = torch.rand(H, device=cuda, generator=g) + 0.5
+    beta = torch.randn(H, device=cuda, generator=g)
+    seed, off = 1234, 77
+    ref = O.ln_fwd(slabs, gamma, beta, 1e-12, bias=bias, resid=resid, p=p, mode=1, seed=seed, off=off, row0=64)
+    outs = tuple(torch.empty_like(t) for t in ref)
+    hp = h3p.empty(rows, H, cuda)
+    O.ln_fwd_h3p(slabs, gamma, beta, 1e-12, bias, resid, p, seed, off, outs, 64, hp)
+    for a, b in zip(ref, outs):
+        assert torch.equal(a, b)
+    sp = h3p.split(ref[0])
+    assert torch.equal(hp.planes, sp.planes) and torch.equal(hp.exps, sp.exps)
+    # backward
+    dy = torch.randn(rows, H, device=cuda, generator=g)
+    y, z, mean, rstd = ref
+    dz, da, dg, db, dbias = O.ln_bwd(dy, z, mean, rstd, gamma, p, 1, seed, off, True, True)
+    hp2 = h3p.empty(rows, H, cuda)
+    dz2, dg2, db2, dbias2 = O.ln_bwd_h3p(dy, z, mean, rstd, gamma, p, seed, off, hp2)
+    assert torch.equal(dz, dz2)
+    sp2 = h3p.split(da)
+    assert torch.equal(hp2.planes, sp2.planes) and torch.equal(hp2.exps, sp2.exps)
+    for a, b in ((dg, dg2), (db, db2), (dbias, dbias2)):
+        assert float((a - b).abs().max()) <= 1e-5 * (1 + float(a.abs().max()))
+
+
+@pytest.mark.parametrize("S,p", [(128, 0.0), (128, 0.1), (512, 0.1)])
+def test_attention_h3p_planes(cuda, S, p):
+    """The h3 attention kernels that also write their outputs as h3p planes: ctx / dqkv bitwise those
+    of the plain launch, the planes bitwise split(ctx) / split(dqkv)."""
+    from hetseq_amd.ops import bert_ops as O
+    from hetseq_amd.ops import h3p
+    from hetseq_amd.ops._C import hip
+
+    if hip().attn_fp32_mode() != 2:
+        pytest.skip("fp32 attention engine is not h3")
+    g = torch.Generator(device=cuda)
+    g.manual_seed(S)
+    B, NH, H = 4, 12, 768
+    qkv = torch.randn(B * S, 3 * H, device=cuda, generator=g)
+    bias = torch.randn(3 * H, device=cuda, generator=g) * 0.1
+    mask = torch.ones(B, S, dtype=torch.int64, device=cuda)
+    mask[1, S - 40:] = 0
+    ctx, (lse, dmask) = O.attn_fwd(qkv, mask, B, S, NH, p, 5, 9, bias=bias)
+    outs = (torch.empty_like(ctx), torch.empty_like(lse), torch.empty_like(dmask) if dmask is not None else None)
+    hp = h3p.empty(B * S, H, cuda)
+    O.attn_fwd_h3p(qkv, mask, B, S, NH, p, 5, 9, bias, outs, 0, hp)
+    assert torch.equal(outs[0], ctx) and torch.equal(outs[1], lse)
+    sp = h3p.split(ctx)
+    assert torch.equal(hp.planes, sp.planes) and torch.equal(hp.exps, sp.exps)
+    dctx = torch.randn(B * S, H, device=cuda, generator=g)
+    dq = O.attn_bwd(qkv, mask, ctx, dctx, (lse, dmask), B, S, NH, p, bias=bias)
+    hq = h3p.empty(B * S, 3 * H, cuda)
+    dq2 = O.attn_bwd_h3p(qkv, mask, ctx, dctx, (lse, dmask), B, S, NH, p, bias, hq)
+    assert torch.equal(dq, dq2)
+    sq = h3p.split(dq)
+    assert torch.equal(hq.planes, sq.planes) and torch.equal(hq.exps, sq.exps)
