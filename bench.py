@@ -598,6 +598,8 @@ _AB = {
     "ffnbias_dgelu": lambda: setattr(__import__("hetseq_amd.ops.bert_ops", fromlist=["x"]), "_FFN_BIAS_WGRAD", False),
     "wcolfold_on": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_wcol_fold(1),
     "wcolfold_off": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_wcol_fold(0),
+    "cfork_on": lambda: setattr(__import__("hetseq_amd.runtime.streams", fromlist=["x"]), "FWD_CHAIN_FORK", True),
+    "cfork_off": lambda: setattr(__import__("hetseq_amd.runtime.streams", fromlist=["x"]), "FWD_CHAIN_FORK", False),
     "chain_on": lambda: setattr(__import__("hetseq_amd.runtime.streams", fromlist=["x"]), "FWD_CHAIN", True),
     "chain_off": lambda: setattr(__import__("hetseq_amd.runtime.streams", fromlist=["x"]), "FWD_CHAIN", False),
     "wamax_split": lambda: setattr(__import__("hetseq_amd.ops.gemm", fromlist=["x"]), "_SPLIT_WEIGHT_AMAX", True),

@@ -127,6 +127,12 @@ def role(stream_handle: int) -> str:
 # one's LayerNorm ends, and each meeting costs an event round trip).  HETSEQ_FWD_CHAIN=0: meet at
 # every layer.
 FWD_CHAIN = os.environ.get("HETSEQ_FWD_CHAIN", "1") == "1"
+# Inside a chain, every later layer still orders fwd2 after the current stream's work so far (one
+# event, one way: the current stream never waits): that layer's whole-batch outputs come from the
+# current stream's allocator pool, which may hand out a block whose previous use -- a current-stream
+# kernel enqueued after the first fork -- is still pending; fwd2 must not write its half into it
+# before that kernel ran.  HETSEQ_FWD_CHAIN_FORK=0 drops the per-layer wait (unsafe; A/B only).
+FWD_CHAIN_FORK = os.environ.get("HETSEQ_FWD_CHAIN_FORK", "1") == "1"
 _chain = {"depth": 0, "forked": None, "keep": []}
 
 
@@ -186,7 +192,7 @@ class fwd_halves(object):
 
         self.st = fwd2(self.device)
         self.chained = _chain["depth"] > 0
-        if not (self.chained and _chain["forked"] is self.st):
+        if not (self.chained and _chain["forked"] is self.st) or FWD_CHAIN_FORK:
             hip().stream_wait(self.st.cuda_stream, stream_handle())
             if self.chained:
                 _chain["forked"] = self.st

@@ -449,6 +449,46 @@ def test_layer_forward_half_batch_streams_match(cuda, monkeypatch):
     assert torch.equal(sv_s[3], sv_1[3])  # attention keep bits
 
 
+def test_forward_chain_with_scratch_frees_matches_unchained(cuda, monkeypatch):
+    """Half-batch forward chains across layers, with large compute-stream scratch buffers freed
+    between layers (their blocks go back to the pool the next layer's whole-batch outputs come from):
+    the chained no-grad forward is bitwise the unchained one (streams.FWD_CHAIN_FORK orders the
+    second chain after each layer's allocations)."""
+    from hetseq_amd.models.bert import BertConfig, BertForPreTraining, BertLayer
+    from hetseq_amd.runtime import streams
+    from hetseq_amd.runtime.flat import FlatParamStore
+
+    if not streams.enabled():
+        pytest.skip("side stream disabled")
+    torch.manual_seed(0)
+    cfg = BertConfig(vocab_size_or_config_json_file=1024, hidden_size=768, num_hidden_layers=4,
+                     num_attention_heads=12, intermediate_size=3072)
+    model = BertForPreTraining(cfg).to(cuda)
+    model.eval()
+    store = FlatParamStore(model)
+    model.attach_store(store, torch.float32)
+    ids = torch.randint(0, 1024, (16, 128), device=cuda)
+    tt, mask = torch.zeros_like(ids), torch.ones_like(ids)
+    orig = BertLayer.fused
+
+    def noisy(self, *a, **k):
+        junk = torch.empty(16 * 128 * 3072 * 2, device=cuda)
+        junk.fill_(float("nan"))  # a compute-stream kernel on the block, then the block is freed
+        del junk
+        return orig(self, *a, **k)
+
+    monkeypatch.setattr(BertLayer, "fused", noisy)
+    outs = {}
+    for chain in (False, True):
+        monkeypatch.setattr(streams, "FWD_CHAIN", chain)
+        with torch.no_grad():
+            seq, _ = model.bert(ids, tt, mask, output_all_encoded_layers=False)
+        torch.cuda.synchronize()
+        outs[chain] = seq.clone()
+    assert torch.isfinite(outs[True]).all()
+    assert torch.equal(outs[True], outs[False])
+
+
 def test_checkpoint_activations_with_split_forward_matches(cuda):
     """--checkpoint-activations on the fused path: the backward recomputes each layer's forward (as
     two half-batch chains, the second on the side stream that already holds the later layers'

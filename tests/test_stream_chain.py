@@ -52,15 +52,27 @@ def test_every_block_forks_and_joins_outside_a_chain(fake):
     assert fake.calls == [(222, 111), (111, 222)] * 3
 
 
-def test_chain_forks_once_and_joins_at_its_end(fake):
+def test_chain_orders_each_layer_one_way_and_joins_at_its_end(fake):
+    """Inside a chain every layer orders the second stream after the current one (its half may
+    write into blocks the current stream's allocator re-issued) -- one-way waits only: the current
+    stream meets the second chain once, at the end."""
     t = torch.zeros(4)
     with streams.fwd_chain("cpu"):
         for _ in range(12):
             _layer("cpu", keep=t)
-        assert fake.calls == [(222, 111)]  # one fork, no join yet
+        assert fake.calls == [(222, 111)] * 12  # second stream waits; the current stream never does
         assert len(streams._chain["keep"]) == 12  # the layers' tensors stay referenced
-    assert fake.calls == [(222, 111), (111, 222)]
+    assert fake.calls == [(222, 111)] * 12 + [(111, 222)]
     assert streams._chain["forked"] is None and not streams._chain["keep"]
+
+
+def test_chain_forks_once_without_the_per_layer_wait(fake, monkeypatch):
+    monkeypatch.setattr(streams, "FWD_CHAIN_FORK", False)
+    with streams.fwd_chain("cpu"):
+        for _ in range(12):
+            _layer("cpu")
+        assert fake.calls == [(222, 111)]
+    assert fake.calls == [(222, 111), (111, 222)]
 
 
 def test_chain_join_before_an_unsplit_layer(fake):
