@@ -90,11 +90,7 @@ def _headers(dirpath):
 
 
 # per-translation-unit extra flags (kept in the object and module hashes)
-SOURCE_FLAGS = {
-    # MFMA accumulators in VGPRs: with AGPR accumulators hipcc rotates the ring kernel's 48-64
-    # accumulator registers through v_accvgpr moves on every loop iteration (72-96 per two K tiles)
-    "gemm_ring.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
-}
+SOURCE_FLAGS: dict = {}
 
 
 _INC_RE = re.compile(r'^\s*#\s*include\s*"([^"]+)"', re.M)

@@ -33,10 +33,9 @@ void launch_cast_f32_bf16(const float*, void*, int64_t, hipStream_t);
 // layernorm.hip
 int ln_bwd_num_blocks();
 int launch_ln_fwd(int, const void*, const float*, const void*, const float*, const float*, void*, float*, float*,
-                  float*, int, int, float, float, u64, u64, int, void*, int64_t, int, int64_t, int, float*,
-                  hipStream_t);
+                  float*, int, int, float, float, u64, u64, int, int, int64_t, int, float*, hipStream_t);
 int launch_ln_bwd(int, const void*, const float*, const float*, const float*, const float*, void*, void*, float*,
-                  float*, float*, int, int, float, u64, u64, int, void*, int64_t, float*, hipStream_t);
+                  float*, float*, int, int, float, u64, u64, int, float*, hipStream_t);
 int launch_emb_fwd(int, const int64_t*, const int64_t*, const float*, const float*, const float*, const float*,
                    const float*, void*, float*, float*, float*, int, int, int, int, int, float, float, u64, u64, int*,
                    float*, hipStream_t);
@@ -110,12 +109,6 @@ int launch_gemm_planes(int planes, int c_dtype, int ta, int tb, int M, int N, in
                        const float* bias, int epi, float beta, void* aux, int64_t ldaux, float* part,
                        float* colsum_out, int colsum_acc, int ksplit, float* slab, int64_t slab_floats,
                        int variant, hipStream_t st);
-void launch_split_planes(const float* x, void* out, int64_t n, int64_t ps, hipStream_t st);
-// gemm_ring.hip
-int launch_gemm_ring(int ta, int tb, int M, int N, int K, const void* A, int64_t lda, int64_t a_ps, const void* B,
-                     int64_t ldb, int64_t b_ps, float* C, int64_t ldc, const float* bias, int epi, float beta,
-                     float* aux, int64_t ldaux, float* part, float* colsum_out, int colsum_acc, int ksplit,
-                     float* slab, int64_t slab_floats, void* outp, int64_t o_ps, int bn, hipStream_t st);
 void set_planes_variant(int v);
 
 // gemm_h3p.hip
@@ -127,6 +120,8 @@ int launch_gemm_h3p(int ta, int tb, int M, int N, int K, const void* A, int64_t 
 int launch_h3p_split(const float* src, int64_t lds, int rows, int cols, void* dst, int64_t ldd, int64_t ps, int8_t* ex,
                      int64_t lde, hipStream_t st);
 int h3p_split_seg_bytes();
+void set_h3p_variant(int v);
+int h3p_variant();
 void launch_h3p_split_multi(const void* table, int nseg, int total, hipStream_t st);
 
 // mnist.hip
@@ -254,27 +249,27 @@ PYBIND11_MODULE(_hip, m) {
 
   m.def("ln_bwd_num_blocks", &ln_bwd_num_blocks);
   m.def("ln_fwd", [](int dt, i64 a, i64 bias, i64 resid, i64 gamma, i64 beta, i64 y, i64 zsave, i64 mean, i64 rstd,
-                     int rows, int H, float eps, float p, u64 seed, u64 off, int mode, i64 st, i64 yp, i64 yps,
+                     int rows, int H, float eps, float p, u64 seed, u64 off, int mode, i64 st,
                      int nslab, i64 slab_stride, int row0, i64 amax) {
     pre_launch("ln_fwd");
     check(launch_ln_fwd(dt, P(const void*, a), P(const float*, bias), P(const void*, resid), P(const float*, gamma),
                         P(const float*, beta), P(void*, y), P(float*, zsave), P(float*, mean), P(float*, rstd), rows, H,
-                        eps, p, seed, off, mode, P(void*, yp), yps, nslab, slab_stride, row0, P(float*, amax), ST(st)),
+                        eps, p, seed, off, mode, nslab, slab_stride, row0, P(float*, amax), ST(st)),
           "ln_fwd");
   }, py::arg("dt"), py::arg("a"), py::arg("bias"), py::arg("resid"), py::arg("gamma"), py::arg("beta"), py::arg("y"),
      py::arg("zsave"), py::arg("mean"), py::arg("rstd"), py::arg("rows"), py::arg("H"), py::arg("eps"), py::arg("p"),
-     py::arg("seed"), py::arg("off"), py::arg("mode"), py::arg("st"), py::arg("yp") = 0, py::arg("yps") = 0,
+     py::arg("seed"), py::arg("off"), py::arg("mode"), py::arg("st"),
      py::arg("nslab") = 1, py::arg("slab_stride") = 0, py::arg("row0") = 0, py::arg("amax") = 0);
   m.def("ln_bwd", [](int dt, i64 dy, i64 zsave, i64 mean, i64 rstd, i64 gamma, i64 dz, i64 da, i64 pg, i64 pb, i64 pbias,
-                     int rows, int H, float p, u64 seed, u64 off, int mode, i64 st, i64 dap, i64 daps, i64 amax) {
+                     int rows, int H, float p, u64 seed, u64 off, int mode, i64 st, i64 amax) {
     pre_launch("ln_bwd");
     check(launch_ln_bwd(dt, P(const void*, dy), P(const float*, zsave), P(const float*, mean), P(const float*, rstd),
                         P(const float*, gamma), P(void*, dz), P(void*, da), P(float*, pg), P(float*, pb),
-                        P(float*, pbias), rows, H, p, seed, off, mode, P(void*, dap), daps, P(float*, amax), ST(st)),
+                        P(float*, pbias), rows, H, p, seed, off, mode, P(float*, amax), ST(st)),
           "ln_bwd");
   }, py::arg("dt"), py::arg("dy"), py::arg("zsave"), py::arg("mean"), py::arg("rstd"), py::arg("gamma"), py::arg("dz"),
      py::arg("da"), py::arg("pg"), py::arg("pb"), py::arg("pbias"), py::arg("rows"), py::arg("H"), py::arg("p"),
-     py::arg("seed"), py::arg("off"), py::arg("mode"), py::arg("st"), py::arg("dap") = 0, py::arg("daps") = 0,
+     py::arg("seed"), py::arg("off"), py::arg("mode"), py::arg("st"),
      py::arg("amax") = 0);
   m.def("emb_fwd", [](int dt, i64 ids, i64 tt, i64 w, i64 pe, i64 te, i64 gamma, i64 beta, i64 y, i64 zsave, i64 mean,
                       i64 rstd, int rows, int S, int H, int V, int TV, float eps, float p, u64 seed, u64 off, i64 err,
@@ -420,6 +415,8 @@ PYBIND11_MODULE(_hip, m) {
           "h3p_split");
   });
   m.def("h3p_split_seg_bytes", &h3p_split_seg_bytes);
+  m.def("set_h3p_variant", &set_h3p_variant, "h3p GEMM kernel: 0 two 32-deep stages, 1 16-deep four-step ring");
+  m.def("h3p_variant", &h3p_variant);
   m.def("attn_fwd_h3p", [](i64 qkv, i64 mask, i64 bqkv, i64 ctx, i64 lse, i64 dmask, int B, int S, int NH, float p,
                            u64 seed, u64 off, int bh0, i64 pl, i64 ps, i64 ex, i64 st) {
     pre_launch("attn_fwd_h3p");
@@ -472,24 +469,7 @@ PYBIND11_MODULE(_hip, m) {
     if (rc == 0) check_launch("gemm_planes");
     return rc;
   });
-  m.def("gemm_ring", [](int ta, int tb, int M, int N, int K, i64 A, i64 lda, i64 a_ps, i64 B, i64 ldb, i64 b_ps, i64 C,
-                        i64 ldc, i64 bias, int epi, float beta, i64 aux, i64 ldaux, i64 part, i64 colsum,
-                        int colsum_acc, int ksplit, i64 slab, i64 slab_floats, i64 outp, i64 o_ps, int bn, i64 st) {
-    pre_launch("gemm_ring");
-    const int rc = launch_gemm_ring(ta, tb, M, N, K, P(const void*, A), lda, a_ps, P(const void*, B), ldb, b_ps,
-                                    P(float*, C), ldc, P(const float*, bias), epi, beta, P(float*, aux), ldaux,
-                                    P(float*, part), P(float*, colsum), colsum_acc, ksplit, P(float*, slab),
-                                    slab_floats, P(void*, outp), o_ps, bn, ST(st));
-    if (rc == 0) check_launch("gemm_ring");
-    return rc;
-  }, "fp32 GEMM on split-bf16 planes, 3-stage LDS-DMA ring (gemm_ring.hip); -1 = shape not served");
   m.def("set_planes_variant", &set_planes_variant, "plane GEMM variant: 0 default, 1 one LDS stage, 2 half K depth");
-  m.def("split_planes", [](i64 x, i64 out, i64 n, i64 ps, i64 st) {
-    pre_launch("split_planes");
-    if (n % 4 || ps % 4) throw std::invalid_argument("split_planes: n and the plane stride must be multiples of 4");
-    launch_split_planes(P(const float*, x), P(void*, out), n, ps, ST(st));
-    check_launch("split_planes");
-  });
   m.def("pool_nsp_fwd", [](int dt, i64 seq, int B, int S, int H, i64 Wp, i64 bp, i64 Wn, i64 bn, i64 label,
                            i64 mlm_loss, i64 pooled, i64 logits, i64 lse, i64 stats, i64 total, i64 st) {
     pre_launch("pool_nsp_fwd");

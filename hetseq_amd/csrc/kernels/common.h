@@ -167,25 +167,6 @@ HS_DEVICE void load4(const bf16_t* p, float v[4]) {
 HS_DEVICE void store4(float* p, const float v[4]) {
   *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
 }
-// x -> three bf16 planes hi / mid / lo (RNE at each step, x = hi + mid + lo to 2^-27 |x|): the
-// operand format of the fp32 GEMM engine (gemm_ring.hip); bit-identical to split_planes_kernel.
-// `pl` is plane 0 at element index i, plane k at i + k * ps.
-HS_DEVICE void store4_planes(uint16_t* pl, int64_t ps, int64_t i, const float v[4]) {
-#pragma clang fp contract(off)  // residuals of v exactly as stored, never of an fma'd product
-  typedef __bf16 b2 __attribute__((ext_vector_type(2)));
-  typedef float f2 __attribute__((ext_vector_type(2)));
-  const f2 x0 = {v[0], v[1]}, x1 = {v[2], v[3]};
-  const b2 h0 = __builtin_convertvector(x0, b2), h1 = __builtin_convertvector(x1, b2);
-  const f2 r0 = x0 - __builtin_convertvector(h0, f2), r1 = x1 - __builtin_convertvector(h1, f2);
-  const b2 m0 = __builtin_convertvector(r0, b2), m1 = __builtin_convertvector(r1, b2);
-  const b2 l0 = __builtin_convertvector(r0 - __builtin_convertvector(m0, f2), b2);
-  const b2 l1 = __builtin_convertvector(r1 - __builtin_convertvector(m1, f2), b2);
-  *reinterpret_cast<uint2*>(pl + i) = make_uint2(__builtin_bit_cast(uint32_t, h0), __builtin_bit_cast(uint32_t, h1));
-  *reinterpret_cast<uint2*>(pl + i + ps) =
-      make_uint2(__builtin_bit_cast(uint32_t, m0), __builtin_bit_cast(uint32_t, m1));
-  *reinterpret_cast<uint2*>(pl + i + 2 * ps) =
-      make_uint2(__builtin_bit_cast(uint32_t, l0), __builtin_bit_cast(uint32_t, l1));
-}
 HS_DEVICE void store4(bf16_t* p, const float v[4]) {
   const bf16_t a = from_f<bf16_t>(v[0]), b = from_f<bf16_t>(v[1]), c = from_f<bf16_t>(v[2]),
                d = from_f<bf16_t>(v[3]);

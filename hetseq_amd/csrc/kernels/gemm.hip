@@ -1118,7 +1118,7 @@ static void launch_splitk_reduce_cols(const float* slab, int ksplit, int M, int 
   hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid + gcol), dim3(256), 0, st, slab, ksplit, M, N, C, ldc, bias, beta,
                      Mv, Nv, grid, part, colsum_out, colsum_acc);
 }
-// (also called by gemm_planes.hip / gemm_ring.hip)
+// (also called by gemm_planes.hip / gemm_h3p.hip)
 void launch_splitk_reduce(const float* slab, int ksplit, int M, int N, float* C, int64_t ldc, const float* bias,
                           float beta, int Mv, int Nv, hipStream_t st) {
   launch_splitk_reduce_cols(slab, ksplit, M, N, C, ldc, bias, beta, Mv, Nv, st, nullptr, nullptr, 0);

@@ -34,6 +34,7 @@
 // the consumer); GELU (pre-activation kept in aux) and dGELU (column partials of the bias
 // gradient), each optionally writing its output as h3p planes for the next GEMM.
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 #include "h3p.h"
@@ -134,6 +135,105 @@ HS_DEVICE qh8 q_frag(const char* img, int p, int rc, int ks, int lane) {
 
 HS_DEVICE qf16 q_mma(qh8 a, qh8 b, qf16 c) { return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0); }
 HS_DEVICE int q_row(int r, int q) { return (r & 3) + 8 * (r >> 2) + 4 * q; }
+
+// Shared epilogue: register r of acc[i][j] -> row m0+wm+32i+q_row(r,q), col n0+wn+32j+lr.  `smem`: the
+// kernel's LDS (free: the K loop ended with a barrier), used for the dGELU column sums.
+template <int EPI>
+HS_DEVICE void q_epilogue(const QArgs& p, qf16 (&acc)[2][2], char* smem, int m0, int n0, int tm, int slice, int wm,
+                          int wn, int wr, int lane) {
+  const int lr = lane & 31, q = lane >> 5;
+  if (p.ksplit > 1) {  // fp32 partial slab; bias / beta / the sum in splitk_reduce_kernel (or the consumer)
+    float* sl = p.slab + (int64_t)slice * p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          sl[(int64_t)(m0 + wm + 32 * i + q_row(r, q)) * p.N + n0 + wn + 32 * j + lr] = acc[i][j][r];
+    return;
+  }
+  float csum[2] = {0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = n0 + wn + 32 * j + lr;
+    const float bv = EPI != kQNone ? p.bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int mb = m0 + wm + 32 * i;
+      if (EPI == kQGelu) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int64_t m = mb + q_row(r, q);
+          p.aux[m * p.ldaux + n] = acc[i][j][r];
+          acc[i][j][r] = gelu_f(acc[i][j][r] + bv);
+          if (p.C) p.C[m * p.ldc + n] = acc[i][j][r];
+        }
+      } else if (EPI == kQDGelu) {
+        float pre[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) pre[r] = p.aux[(int64_t)(mb + q_row(r, q)) * p.ldaux + n];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          acc[i][j][r] *= gelu_grad_f(pre[r] + bv);
+          csum[j] += acc[i][j][r];
+          if (p.C) p.C[(int64_t)(mb + q_row(r, q)) * p.ldc + n] = acc[i][j][r];
+        }
+      } else if (p.beta != 0.f) {
+        float old[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) old[r] = p.C[(int64_t)(mb + q_row(r, q)) * p.ldc + n];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) p.C[(int64_t)(mb + q_row(r, q)) * p.ldc + n] = acc[i][j][r] + bv + p.beta * old[r];
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) p.C[(int64_t)(mb + q_row(r, q)) * p.ldc + n] = acc[i][j][r] + bv;
+      }
+    }
+  }
+  if ((EPI == kQGelu || EPI == kQDGelu) && p.cp) {
+    // the result as h3p planes: one exponent per 32 x 32 accumulator tile (= one exponent block)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        uint32_t mb = 0u;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mb = amax_bits(mb, acc[i][j][r]);
+        const int e = h3p_exp_bits(wave_umax(mb));
+        const float s = h3p_scale(e);
+        const int rb = (m0 + wm) / 32 + i, cb = (n0 + wn) / 32 + j;
+        if (lane == 0) p.ec[(int64_t)rb * p.lde_c + cb] = static_cast<int8_t>(e);
+        const int n = n0 + wn + 32 * j + lr;
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          uint32_t hi, lo;
+          h3p_split2(acc[i][j][r], acc[i][j][r + 1], s, hi, lo);
+          const int64_t e0 = (int64_t)(m0 + wm + 32 * i + q_row(r, q)) * p.ldcp + n;
+          const int64_t e1 = (int64_t)(m0 + wm + 32 * i + q_row(r + 1, q)) * p.ldcp + n;
+          p.cp[e0] = static_cast<uint16_t>(hi);
+          p.cp[e1] = static_cast<uint16_t>(hi >> 16);
+          p.cp[p.cp_ps + e0] = static_cast<uint16_t>(lo);
+          p.cp[p.cp_ps + e1] = static_cast<uint16_t>(lo >> 16);
+        }
+      }
+  }
+  if (EPI == kQDGelu && p.part) {  // column sums over the block's 128 rows: lane halves, then wave rows
+    float* red = reinterpret_cast<float*>(smem);  // the K loop ended with a barrier
+#pragma unroll
+    for (int j = 0; j < 2; ++j) csum[j] += __shfl_xor(csum[j], 32, 64);
+    if (wr == 1 && q == 0)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) red[wn + 32 * j + lr] = csum[j];
+    __syncthreads();
+    if (wr == 0 && q == 0)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int c = wn + 32 * j + lr;
+        p.part[(int64_t)tm * p.N + n0 + c] = csum[j] + red[c];
+      }
+  }
+}
 
 template <bool TA, bool TB, int EPI>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) gemm_h3p_kernel(QArgs p) {
@@ -240,99 +340,207 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
       for (int j = 0; j < 2; ++j) acc[i][j] += tmp[i][j] * fac[i][j];
   }
 
-  // ---------------- epilogue: register r of acc[i][j] -> row m0+wm+32i+q_row(r,q), col n0+wn+32j+lr
-  const int lr = lane & 31, q = lane >> 5;
-  if (p.ksplit > 1) {  // fp32 partial slab; bias / beta / the sum in splitk_reduce_kernel (or the consumer)
-    float* sl = p.slab + (int64_t)slice * p.M * p.N;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          sl[(int64_t)(m0 + wm + 32 * i + q_row(r, q)) * p.N + n0 + wn + 32 * j + lr] = acc[i][j][r];
-    return;
-  }
-  float csum[2] = {0.f, 0.f};
+  q_epilogue<EPI>(p, acc, smem, m0, n0, tm, slice, wm, wn, wr, lane);
+}
+
+// ---------------------------------------------------------------- variant 1: BK = 16 steps, 4-deep ring
+// The two-stage loop above waits (vmcnt(0)) for the next K tile's LDS-DMA half way through the current
+// tile: one tile of MFMAs (~770 cycles per wave) is all the latency it can hide.  Here each step is
+// one 16-deep K slice (16 KB of planes), the LDS holds a ring of four steps (64 KB: still two blocks
+// per CU), and a step's DMA is issued three steps before it is read:
+//   step s: this wave's share of step s+1 landed (counted vmcnt: step s+2 stays in flight) ->
+//   barrier (step s+1 visible to every wave; every wave's reads of step s-1 done, its stage free) ->
+//   step s's 12 MFMAs (fragments in registers, read during step s-1), with the DMA of step s+3 into
+//   the freed stage and the fragment reads of step s+1 interleaved between them in pinned order.
+// The DMA pieces are asm statements: hipcc would otherwise drain vmcnt(0) before
+// every LDS read it cannot prove disjoint from a pending DMA.  Block factors apply per 32-deep K tile
+// (every second step), as in variant 0.
+constexpr int RBK = 16;
+constexpr int RPLANE = QT * RBK * 2;  // one plane of one operand step: 4 KB
+constexpr int ROPND = 2 * RPLANE;     // 8 KB
+constexpr int RSTAGE = 2 * ROPND;     // A and B: 16 KB
+constexpr int RNS = 4;
+constexpr int RSMEM = RNS * RSTAGE + 2 * QMAXKT * 4 * 4;
+
+template <bool KC>
+struct RImg {
+  static constexpr int row_bytes = KC ? RBK * 2 : QT * 2;  // 32 ([mn][k]) or 256 ([k][mn])
+  // k-contiguous: rows 8 apart share banks -> chunk ^ ((r >> 3) & 1) spreads a b128 lane group over
+  // both chunk columns (conflict-free); [k][mn]: the transposed read's four k rows in four quarters
+  HS_DEVICE static int swz(int r) { return KC ? ((r >> 3) & 1) : 4 * (r & 3); }
+};
+
+// byte offsets (plane 0, k = 0 of the block's range) of this wave's two pieces of one operand:
+// piece j (0, 1) fills bytes [1024 (4 j + w), +1024) of the operand's 8 KB step image
+template <bool KC>
+HS_DEVICE void r_offsets(uint32_t (&off)[2], int64_t ld, int64_t ps, int mn0, int w, int lane) {
+  using I = RImg<KC>;
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    const int n = n0 + wn + 32 * j + lr;
-    const float bv = EPI != kQNone ? p.bias[n] : 0.f;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int mb = m0 + wm + 32 * i;
-      if (EPI == kQGelu) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int64_t m = mb + q_row(r, q);
-          p.aux[m * p.ldaux + n] = acc[i][j][r];
-          acc[i][j][r] = gelu_f(acc[i][j][r] + bv);
-          if (p.C) p.C[m * p.ldc + n] = acc[i][j][r];
-        }
-      } else if (EPI == kQDGelu) {
-        float pre[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) pre[r] = p.aux[(int64_t)(mb + q_row(r, q)) * p.ldaux + n];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          acc[i][j][r] *= gelu_grad_f(pre[r] + bv);
-          csum[j] += acc[i][j][r];
-          if (p.C) p.C[(int64_t)(mb + q_row(r, q)) * p.ldc + n] = acc[i][j][r];
-        }
-      } else if (p.beta != 0.f) {
-        float old[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) old[r] = p.C[(int64_t)(mb + q_row(r, q)) * p.ldc + n];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) p.C[(int64_t)(mb + q_row(r, q)) * p.ldc + n] = acc[i][j][r] + bv + p.beta * old[r];
-      } else {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) p.C[(int64_t)(mb + q_row(r, q)) * p.ldc + n] = acc[i][j][r] + bv;
-      }
-    }
+    const int byte = 1024 * (4 * j + w) + 16 * lane;
+    const int plane = byte / RPLANE, ib = byte % RPLANE;
+    const int row = ib / I::row_bytes, cl = (ib % I::row_bytes) / 16;
+    const int gc = cl ^ I::swz(row);
+    const int64_t e = KC ? (int64_t)(mn0 + row) * ld + 8 * gc : (int64_t)row * ld + mn0 + 8 * gc;
+    off[j] = static_cast<uint32_t>(2 * (e + plane * ps));
   }
-  if ((EPI == kQGelu || EPI == kQDGelu) && p.cp) {
-    // the result as h3p planes: one exponent per 32 x 32 accumulator tile (= one exponent block)
+}
+
+// one LDS-DMA piece (1 KB per wave), hidden from hipcc's wait insertion (see above); M0 is written and
+// restored inside the statement
+HS_DEVICE void r_dma(const void* gsrc, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_dst));
+}
+
+// vmcnt(N) through the builtin (gfx9 encoding), lgkmcnt / expcnt untouched
+template <int N_>
+HS_DEVICE void r_wait_vm() {
+  static_assert(N_ >= 0 && N_ < 64, "vmcnt is 6 bits");
+  __builtin_amdgcn_s_waitcnt((N_ & 15) | ((N_ >> 4) << 14) | 0x70 | 0xF00);
+}
+
+HS_DEVICE void r_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's fragment reads are back
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <bool KC>
+HS_DEVICE qh8 r_frag(const char* img, int p, int rc, int lane) {
+  using I = RImg<KC>;
+  const char* pl = img + p * RPLANE;
+  if (KC) {
+    const int r = rc + (lane & 31), c = lane >> 5;
+    return *reinterpret_cast<const qh8*>(pl + r * I::row_bytes + 16 * (c ^ I::swz(r)));
+  } else {
+    const int l16 = lane & 15, q = l16 >> 2, pp = l16 & 3, g = lane >> 4;
+    const int col = rc + 16 * (g & 1) + 4 * pp;
+    qs4 v[2];
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int row = 8 * (g >> 1) + 4 * jj + q;
+      const char* a = pl + row * I::row_bytes + 16 * ((col >> 3) ^ I::swz(row)) + 2 * (col & 7);
+      v[jj] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) qs4*)(a));
+    }
+    const qs8 u = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w};
+    return __builtin_bit_cast(qh8, u);
+  }
+}
+
+template <bool TA, bool TB, int EPI>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) gemm_h3p_ring_kernel(QArgs p) {
+  constexpr bool AK = !TA, BKc = TB;
+  __shared__ __attribute__((aligned(1024))) char smem[RSMEM];
+  float* const fA = reinterpret_cast<float*>(smem + RNS * RSTAGE);
+  float* const fB = fA + QMAXKT * 4;
+
+  const int tiles_m = p.M / QT, tiles_n = p.N / QT, ntile = tiles_m * tiles_n, nwg = ntile * p.ksplit;
+  const int orig = blockIdx.x;
+  const int xcd = orig % 8, qq = nwg / 8, rr = nwg % 8;
+  const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + orig / 8;
+  const int slice = wg / ntile, tile = wg % ntile;
+  const int gsz = 8 * tiles_n, grp = tile / gsz, gm = min(8, tiles_m - 8 * grp);
+  const int tm = 8 * grp + (tile % gsz) % gm, tn = (tile % gsz) / gm;
+  const int m0 = tm * QT, n0 = tn * QT;
+  const int kofs = slice * (p.K / p.ksplit);
+  const int KT = p.K / p.ksplit / QBK;  // 32-deep K tiles (exponent blocks)
+  const int NSTEP = 2 * KT;
+
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = w >> 1, wc = w & 1, wm = 64 * wr, wn = 64 * wc;
+
+  for (int u = threadIdx.x; u < 4 * KT; u += 256) {
+    const int t = u >> 2, g = u & 3, kb = kofs / QBK + t;
+    const int64_t ia = AK ? (int64_t)(m0 / 32 + g) * p.lde_a + kb : (int64_t)kb * p.lde_a + m0 / 32 + g;
+    const int64_t ib = BKc ? (int64_t)(n0 / 32 + g) * p.lde_b + kb : (int64_t)kb * p.lde_b + n0 / 32 + g;
+    fA[u] = __builtin_ldexpf(1.f, -(int)p.ea[ia]);
+    fB[u] = __builtin_ldexpf(1.f, -(int)p.eb[ib]);
+  }
+
+  uint32_t offA[2], offB[2];
+  r_offsets<AK>(offA, p.lda, p.a_ps, m0, w, lane);
+  r_offsets<BKc>(offB, p.ldb, p.b_ps, n0, w, lane);
+  const int64_t stepA = AK ? 2 * RBK : 2 * (int64_t)RBK * p.lda, stepB = BKc ? 2 * RBK : 2 * (int64_t)RBK * p.ldb;
+  const char* ga = reinterpret_cast<const char*>(p.A) + (AK ? 2 * (int64_t)kofs : 2 * (int64_t)kofs * p.lda);
+  const char* gb = reinterpret_cast<const char*>(p.B) + (BKc ? 2 * (int64_t)kofs : 2 * (int64_t)kofs * p.ldb);
+  const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((q_lds_t*)smem));
+  // DMA piece j of step s (clamped: past the last step a stage nobody reads again gets the last step's
+  // bytes again, so every step issues the same four pieces and the counted waits stay exact)
+  auto dma = [&](int j, int s, int stage) __attribute__((always_inline)) {
+    const int64_t ss = min(s, NSTEP - 1);
+    const char* src = j < 2 ? ga + ss * stepA + offA[j] : gb + ss * stepB + offB[j - 2];
+    r_dma(src, __builtin_amdgcn_readfirstlane(lds0 + stage * RSTAGE + (j < 2 ? 0 : ROPND) + 1024 * (4 * (j & 1) + w)));
+  };
+
+  qf16 acc[2][2], tmp[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = qf16{};
+  struct Frags {
+    qh8 a[2][2], b[2][2];  // [plane][tile]
+  };
+  // fragment reads of one step as 8 pieces: A (plane, tile), then B (plane, tile)
+  auto read_piece = [&](Frags& f, int stage, int r) __attribute__((always_inline)) {
+    const char* img = smem + stage * RSTAGE;
+    if (r < 4) f.a[r >> 1][r & 1] = r_frag<AK>(img, r >> 1, wm + 32 * (r & 1), lane);
+    else f.b[(r - 4) >> 1][r & 1] = r_frag<BKc>(img + ROPND, (r - 4) >> 1, wn + 32 * (r & 1), lane);
+  };
+  // 12 MFMAs (terms smallest first: lo_a hi_b, hi_a lo_b, hi_a hi_b; 4 tiles each); between them, in
+  // source order pinned by sched_barrier: the four DMA pieces of step s+3, then the 8 fragment reads
+  // of step s+1
+  auto body = [&](const Frags& f, Frags& nf, int s, int st_free, int st_next, bool first, bool read_next)
+      __attribute__((always_inline)) {
+#pragma unroll
+    for (int c = 0; c < 12; ++c) {
+      const int term = c >> 2, i = (c >> 1) & 1, j = c & 1;
+      const qh8 a = term == 0 ? f.a[1][i] : f.a[0][i];
+      const qh8 b = term == 1 ? f.b[1][j] : f.b[0][j];
+      tmp[i][j] = q_mma(a, b, (first && term == 0) ? qf16{} : tmp[i][j]);
+      if (c < 4) dma(c, s + 3, st_free);
+      else if (read_next) read_piece(nf, st_next, c - 4);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  // prologue: three steps in flight, wait for the first
+#pragma unroll
+  for (int j = 0; j < 4; ++j) dma(j, 0, 0);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) dma(j, 1, 1);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) dma(j, 2, 2);
+  r_wait_vm<8>();
+  __syncthreads();  // step 0 and the factor tables visible to every wave
+  Frags F[2];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) read_piece(F[0], 0, r);
+  // K tile t = steps 2t (F[0], stage 2t % 4) and 2t+1 (F[1]); stage of step s is s % 4
+  for (int t = 0; t < KT; ++t) {
+    const int s0 = 2 * t, st0 = s0 & 3;
+    r_wait_vm<4>();  // step s0+1 landed (this wave's pieces); s0+2 in flight
+    r_barrier();
+    body(F[0], F[1], s0, (st0 + 3) & 3, (st0 + 1) & 3, true, true);
+    r_wait_vm<4>();
+    r_barrier();
+    const float2 fa = *reinterpret_cast<const float2*>(fA + 4 * t + 2 * wr);
+    const float2 fb = *reinterpret_cast<const float2*>(fB + 4 * t + 2 * wc);
+    // (the last tile's reads of "step s0+2" fetch a stage holding a duplicate DMA: harmless, unused)
+    body(F[1], F[0], s0 + 1, st0, (st0 + 2) & 3, false, true);
+    const float fac[2][2] = {{fa.x * fb.x, fa.x * fb.y}, {fa.y * fb.x, fa.y * fb.y}};
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        uint32_t mb = 0u;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) mb = amax_bits(mb, acc[i][j][r]);
-        const int e = h3p_exp_bits(wave_umax(mb));
-        const float s = h3p_scale(e);
-        const int rb = (m0 + wm) / 32 + i, cb = (n0 + wn) / 32 + j;
-        if (lane == 0) p.ec[(int64_t)rb * p.lde_c + cb] = static_cast<int8_t>(e);
-        const int n = n0 + wn + 32 * j + lr;
-#pragma unroll
-        for (int r = 0; r < 16; r += 2) {
-          uint32_t hi, lo;
-          h3p_split2(acc[i][j][r], acc[i][j][r + 1], s, hi, lo);
-          const int64_t e0 = (int64_t)(m0 + wm + 32 * i + q_row(r, q)) * p.ldcp + n;
-          const int64_t e1 = (int64_t)(m0 + wm + 32 * i + q_row(r + 1, q)) * p.ldcp + n;
-          p.cp[e0] = static_cast<uint16_t>(hi);
-          p.cp[e1] = static_cast<uint16_t>(hi >> 16);
-          p.cp[p.cp_ps + e0] = static_cast<uint16_t>(lo);
-          p.cp[p.cp_ps + e1] = static_cast<uint16_t>(lo >> 16);
-        }
-      }
+      for (int j = 0; j < 2; ++j) acc[i][j] += tmp[i][j] * fac[i][j];
   }
-  if (EPI == kQDGelu && p.part) {  // column sums over the block's 128 rows: lane halves, then wave rows
-    float* red = reinterpret_cast<float*>(smem);  // the K loop ended with a barrier
-#pragma unroll
-    for (int j = 0; j < 2; ++j) csum[j] += __shfl_xor(csum[j], 32, 64);
-    if (wr == 1 && q == 0)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) red[wn + 32 * j + lr] = csum[j];
-    __syncthreads();
-    if (wr == 0 && q == 0)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int c = wn + 32 * j + lr;
-        p.part[(int64_t)tm * p.N + n0 + c] = csum[j] + red[c];
-      }
-  }
+  r_wait_vm<0>();  // the trailing duplicate DMAs land before the LDS is reused
+  __syncthreads();
+  q_epilogue<EPI>(p, acc, smem, m0, n0, tm, slice, wm, wn, wr, lane);
 }
 
 // ---------------------------------------------------------------- fp32 -> h3p planes
@@ -376,14 +584,26 @@ __global__ void __launch_bounds__(256) h3p_split_kernel(QSplitSeg one, const QSp
   if (lane == 0) s.ex[(int64_t)br * s.lde + bc] = static_cast<int8_t>(e);
 }
 
+// kernel variant: 0 = two 32-deep stages (gemm_h3p_kernel), 1 = the 16-deep four-step ring
+// (gemm_h3p_ring_kernel).  HETSEQ_H3P_KERNEL=stage2|ring; set_h3p_variant for A/Bs.
+static int g_h3p_variant = [] {
+  const char* e = std::getenv("HETSEQ_H3P_KERNEL");
+  return e && e[0] == 's' ? 0 : e && e[0] == 'r' ? 1 : 0;
+}();
+
+template <bool TA, bool TB, int EPI>
+void q_launch(const QArgs& a, hipStream_t st) {
+  const dim3 grid((a.M / QT) * (a.N / QT) * a.ksplit), blk(256);
+  if (g_h3p_variant == 1) hipLaunchKernelGGL((gemm_h3p_ring_kernel<TA, TB, EPI>), grid, blk, 0, st, a);
+  else hipLaunchKernelGGL((gemm_h3p_kernel<TA, TB, EPI>), grid, blk, 0, st, a);
+}
+
 template <bool TA, bool TB>
 int q_launch_epi(int epi, const QArgs& a, hipStream_t st) {
-  const dim3 grid((a.M / QT) * (a.N / QT) * a.ksplit), blk(256);
-  if (epi == kQNone) hipLaunchKernelGGL((gemm_h3p_kernel<TA, TB, kQNone>), grid, blk, 0, st, a);
-  else if (epi == kQBias) hipLaunchKernelGGL((gemm_h3p_kernel<TA, TB, kQBias>), grid, blk, 0, st, a);
-  else if (epi == kQGelu && !TA && TB) hipLaunchKernelGGL((gemm_h3p_kernel<false, true, kQGelu>), grid, blk, 0, st, a);
-  else if (epi == kQDGelu && !TA && !TB)
-    hipLaunchKernelGGL((gemm_h3p_kernel<false, false, kQDGelu>), grid, blk, 0, st, a);
+  if (epi == kQNone) q_launch<TA, TB, kQNone>(a, st);
+  else if (epi == kQBias) q_launch<TA, TB, kQBias>(a, st);
+  else if (epi == kQGelu && !TA && TB) q_launch<false, true, kQGelu>(a, st);
+  else if (epi == kQDGelu && !TA && !TB) q_launch<false, false, kQDGelu>(a, st);
   else return -1;
   return 0;
 }
@@ -455,3 +675,6 @@ void launch_h3p_split_multi(const void* table, int nseg, int total, hipStream_t 
   hipLaunchKernelGGL(h3p_split_kernel, dim3((total + 3) / 4), dim3(256), 0, st, none,
                      static_cast<const QSplitSeg*>(table), nseg, total);
 }
+
+void set_h3p_variant(int v) { g_h3p_variant = v; }
+int h3p_variant() { return g_h3p_variant; }

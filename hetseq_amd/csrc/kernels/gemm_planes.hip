@@ -1,18 +1,12 @@
-// bf16-plane MFMA GEMM: the engine behind both precision modes (K01/K03/K04 GEMM parts).
+// bf16 MFMA GEMM on "plane" operands (the --dtype bf16 step's hand-written GEMMs).
 //
 //   C[M,N] = beta*C + op(A)[M,K] * op(B)[K,N]  (+ bias / GELU / dGELU epilogue)
 //
-// Operands arrive as P bf16 "planes" of the same shape (plane stride ps elements):
-//   P = 1  --dtype bf16: the bf16 activation / weight shadow itself, one product;
-//   P = 3  fp32 (the reference's precision) as split-bf16: x = hi + mid + lo + r,
-//          |r| <= 2^-27 |x| (RNE each time), and a*b summed from the six cross
-//          terms of order <= 2^-16 (lo*hi, hi*lo, mid*mid, mid*hi, hi*mid, hi*hi,
-//          smallest first).  Every bf16 x bf16 product is exact in the fp32
-//          accumulator, so the result carries fp32-level error.
-// The planes are produced ONCE per tensor (split_planes_kernel below, or the
-// optimizer for the weights), not once per GEMM block as in gemm_x6s_kernel
-// (gemm.hip), whose in-block splitting VALU work co-issued with -- and capped --
-// its MFMAs.  Here the K loop is pure data movement + MFMA:
+// Operands are bf16 matrices (P = 1: the bf16 activation / weight shadow itself).
+// The kernel template keeps a plane count P, but only P = 1 is instantiated: the
+// split-bf16 fp32 engine (P = 3, six cross products) was retired in round 5 for the
+// three-product fp16 block-scaled engine (gemm_h3p.hip), which reads half the bytes.
+// The K loop is pure data movement + MFMA:
 //
 //  * tiles of 128x128, 4 waves (2x2, 64x64 each = 2x2 v_mfma_f32_32x32x16_bf16
 //    accumulators), BK = 32 (P = 3) or 64 (P = 1);
@@ -473,26 +467,6 @@ __global__ void __launch_bounds__(256) splitk_reduce_bf16_kernel(const float* __
   }
 }
 
-// fp32 -> three bf16 planes (hi, mid, lo), RNE at each step: out[p * n + i].
-__global__ void __launch_bounds__(256) split_planes_kernel(const float* __restrict__ x, uint16_t* __restrict__ out,
-                                                           int64_t n4, int64_t ps) {
-  typedef __bf16 b2 __attribute__((ext_vector_type(2)));
-  typedef float f2 __attribute__((ext_vector_type(2)));
-  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
-    const float4 v = reinterpret_cast<const float4*>(x)[i];
-    const f2 x0 = {v.x, v.y}, x1 = {v.z, v.w};
-    const b2 h0 = __builtin_convertvector(x0, b2), h1 = __builtin_convertvector(x1, b2);
-    const f2 r0 = x0 - __builtin_convertvector(h0, f2), r1 = x1 - __builtin_convertvector(h1, f2);
-    const b2 m0 = __builtin_convertvector(r0, b2), m1 = __builtin_convertvector(r1, b2);
-    const b2 l0 = __builtin_convertvector(r0 - __builtin_convertvector(m0, f2), b2);
-    const b2 l1 = __builtin_convertvector(r1 - __builtin_convertvector(m1, f2), b2);
-    uint2* o = reinterpret_cast<uint2*>(out);
-    o[i] = make_uint2(__builtin_bit_cast(uint32_t, h0), __builtin_bit_cast(uint32_t, h1));
-    o[i + ps / 4] = make_uint2(__builtin_bit_cast(uint32_t, m0), __builtin_bit_cast(uint32_t, m1));
-    o[i + ps / 2] = make_uint2(__builtin_bit_cast(uint32_t, l0), __builtin_bit_cast(uint32_t, l1));
-  }
-}
-
 template <int P, int BK, int STAGES, int WV, typename TC>
 int launch_planes_cfg(int ta, int tb, int epi, const PlanesArgs& a, hipStream_t st) {
   const dim3 grid((a.M / kPB) * (a.N / kPB) * a.ksplit), blk(64 * WV);
@@ -525,7 +499,7 @@ void launch_splitk_reduce(const float* slab, int ksplit, int M, int N, float* C,
 
 using namespace hs;
 
-static int g_planes_variant = 0;  // microbenchmark / tuning hook (tools/bench_planes.py)
+static int g_planes_variant = 0;  // microbenchmark / tuning hook
 void set_planes_variant(int v) { g_planes_variant = v; }
 
 // planes: 1 (bf16) or 3 (split fp32); c_dtype: 0 fp32 C, 1 bf16 C.  Operand strides / plane
@@ -542,7 +516,7 @@ int launch_gemm_planes(int planes, int c_dtype, int ta, int tb, int M, int N, in
                        const float* bias, int epi, float beta, void* aux, int64_t ldaux, float* part,
                        float* colsum_out, int colsum_acc, int ksplit, float* slab, int64_t slab_floats,
                        int variant, hipStream_t st) {
-  if (planes != 1 && planes != 3) return -1;
+  if (planes != 1) return -1;  // (the split-fp32 P = 3 engine was retired for h3p, gemm_h3p.hip)
   // variant (tile K depth, LDS stages, waves): 0 = two stages, 4 waves; 1 = one stage; 2 = half
   // depth; 3 = 8 waves; 4 = 8 waves + one stage.  < 0: the process default (set_planes_variant)
   if (variant < 0) variant = g_planes_variant;
@@ -570,11 +544,7 @@ int launch_gemm_planes(int planes, int c_dtype, int ta, int tb, int M, int N, in
 #define HS_CFG(P_, BK_, S_, W_)                                                        \
   (c_dtype ? launch_planes_cfg<P_, BK_, S_, W_, bf16_t>(ta, tb, epi, a, st) \
            : launch_planes_cfg<P_, BK_, S_, W_, float>(ta, tb, epi, a, st))
-  if (planes == 3)
-    rc = variant == 1 ? HS_CFG(3, 32, 1, 4) : variant == 2 ? HS_CFG(3, 16, 2, 4) : variant == 3 ? HS_CFG(3, 32, 2, 8)
-       : variant == 4 ? HS_CFG(3, 32, 1, 8) : HS_CFG(3, 32, 2, 4);
-  else
-    rc = variant == 1 ? HS_CFG(1, 64, 1, 4) : variant == 2 ? HS_CFG(1, 32, 2, 4) : variant == 3 ? HS_CFG(1, 64, 2, 8)
+  rc = variant == 1 ? HS_CFG(1, 64, 1, 4) : variant == 2 ? HS_CFG(1, 32, 2, 4) : variant == 3 ? HS_CFG(1, 64, 2, 8)
        : variant == 4 ? HS_CFG(1, 64, 1, 8) : HS_CFG(1, 64, 2, 4);
 #undef HS_CFG
   if (rc) return rc;
@@ -591,10 +561,4 @@ int launch_gemm_planes(int planes, int c_dtype, int ta, int tb, int M, int N, in
     launch_reduce_rows(parts, outs, 1, M / kPB, N, colsum_acc, st);
   }
   return 0;
-}
-
-void launch_split_planes(const float* x, void* out, int64_t n, int64_t ps, hipStream_t st) {
-  const int64_t n4 = n / 4;
-  const int grid = (int)std::min<int64_t>((n4 + 255) / 256, 4096);
-  hipLaunchKernelGGL(split_planes_kernel, dim3(grid), dim3(256), 0, st, x, static_cast<uint16_t*>(out), n4, ps);
 }

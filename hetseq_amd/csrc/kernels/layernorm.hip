@@ -51,7 +51,7 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const T* __restrict__ a, co
                                                      float* __restrict__ rstd_out, int rows, float eps, float p,
                                                      uint64_t seed, uint64_t off, int mode,
                                                      const uint64_t* __restrict__ seed_dev,
-                                                     uint16_t* __restrict__ yp, int64_t yps, int nslab,
+                                                     int nslab,
                                                      int64_t slab_stride, int row0, float* __restrict__ amax_y) {
   constexpr int H = NV * 256;
   const int lane = threadIdx.x & 63;
@@ -105,7 +105,6 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const T* __restrict__ a, co
         am = amax_bits(am, o[j]);
       }
       store4(y + base + c, o);
-      if (yp) store4_planes(yp, yps, base + c, o);  // y again as the next GEMM's split-bf16 operand
     }
     if (lane == 0) {
       mean_out[row] = mean;
@@ -283,8 +282,8 @@ __global__ void __launch_bounds__(64 * kLnBwdWaves) ln_bwd_kernel(
     const T* __restrict__ dy, const float* __restrict__ zsave, const float* __restrict__ mean_in,
     const float* __restrict__ rstd_in, const float* __restrict__ gamma, T* __restrict__ dz_out, T* __restrict__ da_out,
     float* __restrict__ part_gamma, float* __restrict__ part_beta, float* __restrict__ part_bias, int rows, float p,
-    uint64_t seed, uint64_t off, int mode, const uint64_t* __restrict__ seed_dev, uint16_t* __restrict__ dap,
-    int64_t daps, float* __restrict__ amax_out) {
+    uint64_t seed, uint64_t off, int mode, const uint64_t* __restrict__ seed_dev,
+    float* __restrict__ amax_out) {
   constexpr int H = NV * 256;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int lane = threadIdx.x & 63;
@@ -353,7 +352,6 @@ __global__ void __launch_bounds__(64 * kLnBwdWaves) ln_bwd_kernel(
           am = amax_bits(am, dzv[j]);
         }
         if (da_out) store4(da_out + base + c, dzv);
-        if (dap) store4_planes(dap, daps, base + c, dzv);  // da as the dgrad / wgrad GEMMs' operand
       }
     }
 #pragma unroll
@@ -645,13 +643,12 @@ static const int kLnBwdBlocks = [] {
 template <int NV, typename T>
 void ln_fwd_launch(const void* a, const float* bias, const void* resid, const float* gamma, const float* beta, void* y,
                    float* zsave, float* mean, float* rstd, int rows, float eps, float p, uint64_t seed, uint64_t off,
-                   int mode, uint16_t* yp, int64_t yps, int nslab, int64_t slab_stride, int row0, float* amax,
-                   hipStream_t st) {
+                   int mode, int nslab, int64_t slab_stride, int row0, float* amax, hipStream_t st) {
   int grid = (rows + 3) / 4;
   if (grid > 4096) grid = 4096;
   hipLaunchKernelGGL((ln_fwd_kernel<NV, T>), dim3(grid), dim3(256), 0, st, (const T*)a, bias, (const T*)resid, gamma,
-                     beta, (T*)y, zsave, mean, rstd, rows, eps, p, seed, off, mode, g_seed_dev, yp, yps, nslab,
-                     slab_stride, row0, amax);
+                     beta, (T*)y, zsave, mean, rstd, rows, eps, p, seed, off, mode, g_seed_dev, nslab, slab_stride,
+                     row0, amax);
 }
 
 template <int NV, typename T>
@@ -675,19 +672,19 @@ void ln_bwd_h3p_launch(const float* dy, const float* zsave, const float* mean, c
 template <int NV, typename T>
 void ln_bwd_launch(const void* dy, const float* zsave, const float* mean, const float* rstd, const float* gamma,
                    void* dz, void* da, float* pg, float* pb, float* pbias, int rows, float p, uint64_t seed,
-                   uint64_t off, int mode, uint16_t* dap, int64_t daps, float* amax, hipStream_t st) {
+                   uint64_t off, int mode, float* amax, hipStream_t st) {
   constexpr int H = NV * 256;
   if constexpr (NV <= 3) {
     if (g_lnbwd_chunked) {
       hipLaunchKernelGGL((ln_bwd_kernel<NV, T, true>), dim3(kLnBwdBlocks), dim3(64 * kLnBwdWaves), 0, st,
                          (const T*)dy, zsave, mean, rstd, gamma, (T*)dz, (T*)da, pg, pb, pbias, rows, p, seed, off, mode,
-                         g_seed_dev, dap, daps, amax);
+                         g_seed_dev, amax);
       return;
     }
   }
   hipLaunchKernelGGL((ln_bwd_kernel<NV, T>), dim3(kLnBwdBlocks), dim3(64 * kLnBwdWaves), kLnBwdWaves * H * sizeof(float), st, (const T*)dy,
                      zsave, mean, rstd, gamma, (T*)dz, (T*)da, pg, pb, pbias, rows, p, seed, off, mode, g_seed_dev,
-                     dap, daps, amax);
+                     amax);
 }
 
 template <int NV, typename T>
@@ -730,16 +727,15 @@ void set_ln_bwd_lds(int chunked) { g_lnbwd_chunked = chunked; }
 
 int launch_ln_fwd(int dtype, const void* a, const float* bias, const void* resid, const float* gamma,
                   const float* beta, void* y, float* zsave, float* mean, float* rstd, int rows, int H, float eps,
-                  float p, uint64_t seed, uint64_t off, int mode, void* yp, int64_t yps, int nslab,
+                  float p, uint64_t seed, uint64_t off, int mode, int nslab,
                   int64_t slab_stride, int row0, float* amax, hipStream_t st) {
-  if (yp && dtype != 0) return -1;  // plane output: fp32 mode only
   if (nslab < 1 || (nslab > 1 && (dtype != 0 || slab_stride < (int64_t)rows * H || slab_stride % 4))) return -1;
   if (dtype == 0) {
     HS_DISPATCH_H(H, (ln_fwd_launch<NV, float>(a, bias, resid, gamma, beta, y, zsave, mean, rstd, rows, eps, p, seed,
-                                               off, mode, (uint16_t*)yp, yps, nslab, slab_stride, row0, amax, st)));
+                                               off, mode, nslab, slab_stride, row0, amax, st)));
   } else {
     HS_DISPATCH_H(H, (ln_fwd_launch<NV, bf16_t>(a, bias, resid, gamma, beta, y, zsave, mean, rstd, rows, eps, p, seed,
-                                                off, mode, nullptr, 0, 1, 0, row0, amax, st)));
+                                                off, mode, 1, 0, row0, amax, st)));
   }
   return 0;
 }
@@ -770,14 +766,13 @@ int launch_ln_bwd_h3p(const float* dy, const float* zsave, const float* mean, co
 
 int launch_ln_bwd(int dtype, const void* dy, const float* zsave, const float* mean, const float* rstd,
                   const float* gamma, void* dz, void* da, float* pg, float* pb, float* pbias, int rows, int H, float p,
-                  uint64_t seed, uint64_t off, int mode, void* dap, int64_t daps, float* amax, hipStream_t st) {
-  if (dap && (dtype != 0 || mode != kBDR)) return -1;  // plane output of da: fp32, bias-dropout-residual mode
+                  uint64_t seed, uint64_t off, int mode, float* amax, hipStream_t st) {
   if (dtype == 0) {
     HS_DISPATCH_H(H, (ln_bwd_launch<NV, float>(dy, zsave, mean, rstd, gamma, dz, da, pg, pb, pbias, rows, p, seed, off,
-                                               mode, (uint16_t*)dap, daps, amax, st)));
+                                               mode, amax, st)));
   } else {
     HS_DISPATCH_H(H, (ln_bwd_launch<NV, bf16_t>(dy, zsave, mean, rstd, gamma, dz, da, pg, pb, pbias, rows, p, seed,
-                                                off, mode, nullptr, 0, amax, st)));
+                                                off, mode, amax, st)));
   }
   return 0;
 }

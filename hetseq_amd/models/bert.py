@@ -383,25 +383,6 @@ class BertLayer(nn.Module):
         W.w1, W.bi = cw(self.intermediate.dense_act.weight), self.intermediate.dense_act.bias.detach()
         W.w2, W.b2 = cw(o.dense.weight), o.dense.bias.detach()
         W.g2, W.bb2 = o.LayerNorm.weight.detach(), o.LayerNorm.bias.detach()
-        W.planes = False
-        W.bwd = W
-        if not bf16 and store is not None and store.planes is not None:
-            from hetseq_amd.ops import gemm as G
-
-            if not G.planes_backward():  # forward-only planes: the backward keeps the fp32 views
-                Wb = LayerWeights()
-                for k in LayerWeights.__slots__:
-                    if k != "bwd":
-                        setattr(Wb, k, getattr(W, k))
-                Wb.bwd = Wb
-                W.bwd = Wb
-            # fp32 on the plane engine: GEMM weights as their split-bf16 planes (refreshed by the optimizer)
-            W.wqkv = store.planes_view(qkv, (3 * sa.all_head_size, H))
-            W.wo = store.planes_view([ao.dense.weight], tuple(ao.dense.weight.shape))
-            W.w1 = store.planes_view([self.intermediate.dense_act.weight],
-                                     tuple(self.intermediate.dense_act.weight.shape))
-            W.w2 = store.planes_view([o.dense.weight], tuple(o.dense.weight.shape))
-            W.planes = True
         return W
 
     def fused_ok(self, x, S):
@@ -609,11 +590,6 @@ class BertPreTrainedModel(nn.Module):
 
     # --- runtime plumbing (flat store / compute dtype / fused switch)
     def attach_store(self, store, compute_dtype=torch.float32):
-        if compute_dtype == torch.float32 and store.param.is_cuda:
-            from hetseq_amd.ops import gemm as G
-
-            if G.planes_enabled():
-                store.enable_planes()  # fp32 GEMM weights as split-bf16 planes (plane engine)
         for m in self.modules():
             m._hs_store = store
             m._hs_dtype = compute_dtype
@@ -715,8 +691,6 @@ class BertModel(BertPreTrainedModel):
         from hetseq_amd.ops.bert_ops import LayerAmax
 
         Ws = [blk._weights() for blk in self.encoder.layer]
-        if any(getattr(W, "planes", False) for W in Ws):
-            return None, None
         # (h3p engine: the layers' products need no |max| -- their slots stay reserved, unmeasured)
         weights = [None if G.h3p_active(self.compute_dtype) else w for W in Ws
                    for w in (W.wqkv, W.wo, W.w1, W.w2)] + list(extra_weights)
@@ -851,10 +825,6 @@ class BertForPreTraining(BertPreTrainedModel):
         wt, wd = t.dense_act.weight, self.cls.predictions.decoder.weight
         store = getattr(self, "_hs_store", None)
         if self.compute_dtype != torch.bfloat16:
-            from hetseq_amd.ops import gemm as G
-
-            if store is not None and store.planes is not None and G.planes_backward():  # transform on planes
-                return store.planes_view([wt], tuple(wt.shape)), wd.detach()
             return wt.detach(), wd.detach()
         if store is not None:
             return store.shadow_view(wt), store.shadow_view(wd)

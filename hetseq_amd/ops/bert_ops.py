@@ -80,14 +80,9 @@ def _colpart_buf(nparts, H, device, n=3):
 
 
 # --------------------------------------------------------------------- basic ops
-def _planes_buf(rows, cols, device):
-    return torch.empty((3, rows, cols), dtype=torch.bfloat16, device=device)
-
-
-def ln_fwd(a, gamma, beta, eps=1e-12, bias=None, resid=None, p=0.0, mode=0, seed=0, off=0, save_z=True, planes=None,
+def ln_fwd(a, gamma, beta, eps=1e-12, bias=None, resid=None, p=0.0, mode=0, seed=0, off=0, save_z=True,
            outs=None, row0=0, amax=None):
-    """LayerNorm forward (+ bias / dropout / residual in mode 1).  ``planes``: a [3, rows, H] bf16
-    buffer that also receives y as split-bf16 planes (the fp32 GEMM engine's operand format).
+    """LayerNorm forward (+ bias / dropout / residual in mode 1).
     ``a`` may be [ks, rows, H] split-K partials of the producing GEMM (gemm.linear_fwd_partials),
     summed in slice order as the GEMM's own reduce pass would.  ``outs`` = (y, z, mean, rstd) buffers to
     write (row slices of whole-batch tensors); ``row0``: the first row's index in the whole batch
@@ -111,8 +106,7 @@ def ln_fwd(a, gamma, beta, eps=1e-12, bias=None, resid=None, p=0.0, mode=0, seed
     hip().ln_fwd(dtype_code(a), a.data_ptr(), bias.data_ptr() if bias is not None else 0,
                  resid.data_ptr() if resid is not None else 0, gamma.data_ptr(), beta.data_ptr(), y.data_ptr(),
                  z.data_ptr() if z is not None else 0, mean.data_ptr(), rstd.data_ptr(), rows, H, float(eps), float(p),
-                 seed, off, mode, stream_handle(), planes.data_ptr() if planes is not None else 0,
-                 rows * H if planes is not None else 0, nslab, stride if nslab > 1 else 0, int(row0),
+                 seed, off, mode, stream_handle(), nslab, stride if nslab > 1 else 0, int(row0),
                  G.slot_ptr(amax))
     return y, z, mean, rstd
 
@@ -162,12 +156,11 @@ def ln_bwd_h3p(dy, z, mean, rstd, gamma, p, seed, off, hp, acc=None, side=False)
 
 
 def ln_bwd(dy, z, mean, rstd, gamma, p=0.0, mode=0, seed=0, off=0, want_dz=True, want_da=False, dz_out=None,
-           acc=None, side=False, da_planes=None, amax=None):
+           acc=None, side=False, amax=None):
     """LN backward.  ``acc`` = (dgamma, dbeta[, dbias]) fp32 tensors to ACCUMULATE into
     (flat-store gradient views); otherwise fresh tensors are returned.  ``side``: run the
     parameter-gradient finalisation on the weight-gradient stream (runtime/streams.py) --
-    only dz / da are on the critical path.  ``da_planes``: [3, rows, H] bf16 buffer receiving da
-    as split-bf16 planes (mode 1; with ``want_da`` False the fp32 da is not written at all).
+    only dz / da are on the critical path.
     ``amax``: slot receiving |max| of da (mode 1) or dz (mode 0) -- the next GEMMs' operand."""
     rows, H = dy.shape
     nb = hip().ln_bwd_num_blocks()
@@ -177,7 +170,6 @@ def ln_bwd(dy, z, mean, rstd, gamma, p=0.0, mode=0, seed=0, off=0, want_dz=True,
     hip().ln_bwd(dtype_code(dy), dy.data_ptr(), z.data_ptr(), mean.data_ptr(), rstd.data_ptr(), gamma.data_ptr(),
                  dz.data_ptr() if dz is not None else 0, da.data_ptr() if da is not None else 0, part[0].data_ptr(),
                  part[1].data_ptr(), part[2].data_ptr(), rows, H, float(p), seed, off, mode, stream_handle(),
-                 da_planes.data_ptr() if da_planes is not None else 0, rows * H if da_planes is not None else 0,
                  G.slot_ptr(amax))
     n = 3 if mode == 1 else 2
     if acc is not None:
@@ -484,10 +476,10 @@ class FusedEmbedding(torch.autograd.Function):
 
 # --------------------------------------------------------------------- encoder layer
 class LayerWeights(object):
-    """Compute views of one encoder layer's weights: fp32 master, bf16 shadow, or (fp32 plane
-    engine, ``planes`` True) the split-bf16 plane views (ops.gemm.Planes) of the GEMM weights."""
+    """Compute views of one encoder layer's weights: fp32 master or bf16 shadow; ``h3p``: the GEMM
+    weights' block-scaled planes (ops.h3p.HP) when the layer runs on the h3p engine."""
 
-    __slots__ = ("wqkv", "bqkv", "wo", "bo", "g1", "b1", "w1", "bi", "w2", "b2", "g2", "bb2", "planes", "bwd", "h3p")
+    __slots__ = ("wqkv", "bqkv", "wo", "bo", "g1", "b1", "w1", "bi", "w2", "b2", "g2", "bb2", "h3p")
 
 
 class LayerAmax(object):
@@ -509,11 +501,6 @@ def _am(am, *pairs):
     return None if am is None else pairs
 
 
-def _planes_of(buf):
-    """Planes over a [3, rows, cols] split buffer (what G.split returns / the layer saves)."""
-    return G.Planes(buf, buf.shape[1], buf.shape[2], buf.shape[2], buf.shape[1] * buf.shape[2], 3)
-
-
 # The fp32 encoder-layer forward runs the batch as two half-batch chains on two streams (the compute
 # stream and streams.fwd2, the idle weight-gradient stream): a single chain leaves the GEMMs' last partial round of tiles on a mostly
 # idle chip (QKV: 576 tiles of 128 x 128 for 512 block slots), and the other half's kernels fill it
@@ -525,7 +512,7 @@ _FWD_KS = None
 
 def _fwd_split_ok(x, mask, W, cfg):
     B, S = cfg[0], cfg[1]
-    return (_FWD_SPLIT and x.is_cuda and x.dtype == torch.float32 and not getattr(W, "planes", False)
+    return (_FWD_SPLIT and x.is_cuda and x.dtype == torch.float32
             and B % 2 == 0 and B * S >= 1024 and streams.enabled() and x.is_contiguous())
 
 
@@ -576,11 +563,8 @@ def _layer_forward_split(x, mask, W, cfg, save, am=None):
 
 
 def _layer_forward(x, mask, W, cfg, save, am=None):
-    """fp32 on the plane engine (``W.planes``): every GEMM operand is split-bf16 planes, written by
-    the kernel that produces the tensor where it can -- the LN forwards (h1, h2: h2's planes wait
-    in gemm.remember_planes for the next layer), the GELU epilogue (f1, planes only) -- and by a
-    split pass for the attention output and the embedding output; saved planes feed the weight
-    gradients of the backward."""
+    """One layer forward: the h3p engine's (``W.h3p``), the two half-batch chains (_fwd_split_ok), or
+    one chain on the fp32 in-kernel-split / bf16 engines (``am``: the h3 engine's |max| slots)."""
     if getattr(W, "h3p", None) is not None:
         return _layer_forward_h3p(x, mask, W, cfg, save, am)
     if _fwd_split_ok(x, mask, W, cfg):
@@ -588,44 +572,21 @@ def _layer_forward(x, mask, W, cfg, save, am=None):
     streams.chain_join(x.device)  # one chain from here: the half-batch chains meet first
     B, S, NH, p_h, p_a, eps, seeds = cfg
     (s_a, o_a), (s_1, o_1), (s_2, o_2) = seeds
-    pl = getattr(W, "planes", False)
-    plb = pl and W.bwd is W  # the backward's GEMMs on planes too (else: fp32 operands saved)
-    if pl:
-        am = None  # (the plane engine needs no operand scales)
     sl = (lambda off: am.a(off)) if am is not None else (lambda off: None)  # one chain: the first slot
-    rows, H = x.shape
-    xin = G.split_cached(x) if pl else x
-    qkv = G.linear_fwd(xin, W.wqkv, amax=_am(am, am and am.xw, am and am.w[0]))  # bias folded into the attention
+    qkv = G.linear_fwd(x, W.wqkv, amax=_am(am, am and am.xw, am and am.w[0]))  # bias folded into the attention
     ctx_, (lse, dmask) = attn_fwd(qkv, mask, B, S, NH, p_a, s_a, o_a, bias=W.bqkv, amax=sl(2))
-    cin = G.split(ctx_) if pl else ctx_
     wo_am = _am(am, sl(2), am and am.w[1])
-    a = G.linear_fwd(cin, W.wo, amax=wo_am) if (pl or not _LN_PARTIALS_WO) else G.linear_fwd_partials(
-        cin, W.wo, amax=wo_am)[0]
-    h1p = _planes_buf(rows, H, x.device) if pl else None
-    h1, z1, m1, r1 = ln_fwd(a, W.g1, W.b1, eps, bias=W.bo, resid=x, p=p_h, mode=1, seed=s_1, off=o_1, planes=h1p,
-                            amax=sl(0))
-    hin = _planes_of(h1p) if pl else h1
-    if pl and not plb:  # forward-only planes: f1 in fp32 (saved) and as planes (the next product)
-        f1, f1pre = G.linear_gelu_fwd(hin, W.w1, W.bi, emit_planes=True)
-        fin = G.split_cached(f1)
-    else:
-        f1, f1pre = G.linear_gelu_fwd(hin, W.w1, W.bi, planes_out=pl, amax=_am(am, sl(0), am and am.w[2]),
-                                      amax_out=sl(4))  # f1pre: un-biased pre-activation
-        fin = f1
+    a = G.linear_fwd(ctx_, W.wo, amax=wo_am) if not _LN_PARTIALS_WO else G.linear_fwd_partials(
+        ctx_, W.wo, amax=wo_am)[0]
+    h1, z1, m1, r1 = ln_fwd(a, W.g1, W.b1, eps, bias=W.bo, resid=x, p=p_h, mode=1, seed=s_1, off=o_1, amax=sl(0))
+    f1, f1pre = G.linear_gelu_fwd(h1, W.w1, W.bi, amax=_am(am, sl(0), am and am.w[2]),
+                                  amax_out=sl(4))  # f1pre: un-biased pre-activation
     # FFN-out product: its split-K partials go straight into the LN (no reduce pass)
     w2_am = _am(am, sl(4), am and am.w[3])
-    o = G.linear_fwd(fin, W.w2, amax=w2_am) if (pl or not _LN_PARTIALS) else G.linear_fwd_partials(
-        fin, W.w2, amax=w2_am)[0]
-    h2p = _planes_buf(rows, H, x.device) if pl else None
-    h2, z2, m2, r2 = ln_fwd(o, W.g2, W.bb2, eps, bias=W.b2, resid=h1, p=p_h, mode=1, seed=s_2, off=o_2, planes=h2p,
-                            amax=sl(6))
-    if pl:
-        G.remember_planes(h2, _planes_of(h2p))  # the next layer's QKV operand
+    o = G.linear_fwd(f1, W.w2, amax=w2_am) if not _LN_PARTIALS else G.linear_fwd_partials(f1, W.w2,
+                                                                                        amax=w2_am)[0]
+    h2, z2, m2, r2 = ln_fwd(o, W.g2, W.bb2, eps, bias=W.b2, resid=h1, p=p_h, mode=1, seed=s_2, off=o_2, amax=sl(6))
     if save:
-        if plb:
-            keep = lambda t: t.buf  # noqa: E731
-            return h2, (qkv, ctx_, lse, dmask, z1, m1, r1, keep(hin), f1pre, keep(fin), z2, m2, r2, keep(xin),
-                        keep(cin))
         return h2, (qkv, ctx_, lse, dmask, z1, m1, r1, h1, f1pre, f1, z2, m2, r2, x, ctx_)
     return h2, None
 
@@ -685,16 +646,16 @@ def _layer_forward_h3p(x, mask, W, cfg, save, am=None):
             r = slice(h * hr, (h + 1) * hr)
             r0, r1_ = h * hr, (h + 1) * hr
             sl = (lambda off: am.a(off + h)) if am is not None else (lambda off: None)
-            h3p.gemm(xp.rows_slice(r0, r1_), Wp.wqkv, 0, 1, out=qkv[r])
+            h3p.gemm(xp.rows_slice(r0, r1_), Wp.wqkv, 0, 1, out=qkv[r], site="qkv_fwd")
             attn_fwd_h3p(qkv[r], mask[h * hb:(h + 1) * hb], hb, S, NH, p_a, s_a, o_a, W.bqkv,
                          (ctx_[r], lse[h * nl:(h + 1) * nl], dmask[h * nm:(h + 1) * nm] if dmask is not None else None),
                          h * hb, ctxp.rows_slice(r0, r1_))
-            a = h3p.gemm(ctxp.rows_slice(r0, r1_), Wp.wo, 0, 1, ksplit=_H3P_KS_WO, slab_only=True)
+            a = h3p.gemm(ctxp.rows_slice(r0, r1_), Wp.wo, 0, 1, ksplit=_H3P_KS_WO, slab_only=True, site="wo_fwd")
             ln_fwd_h3p(a, W.g1, W.b1, eps, W.bo, x[r], p_h, s_1, o_1, (h1[r], z1[r], m1[r], r1[r]), r0,
                        h1p.rows_slice(r0, r1_))
             h3p.gemm(h1p.rows_slice(r0, r1_), Wp.w1, 0, 1, bias=W.bi, epi=h3p.EPI_GELU, aux=f1pre[r],
-                     planes_out=f1p.rows_slice(r0, r1_))
-            o = h3p.gemm(f1p.rows_slice(r0, r1_), Wp.w2, 0, 1, ksplit=_H3P_KS_W2, slab_only=True)
+                     planes_out=f1p.rows_slice(r0, r1_), site="ffn1_fwd")
+            o = h3p.gemm(f1p.rows_slice(r0, r1_), Wp.w2, 0, 1, ksplit=_H3P_KS_W2, slab_only=True, site="ffn2_fwd")
             ln_fwd_h3p(o, W.g2, W.bb2, eps, W.b2, h1[r], p_h, s_2, o_2, (h2[r], z2[r], m2[r], r2[r]), r0,
                        h2p.rows_slice(r0, r1_), amax=sl(6))
     h3p.remember(h2, h2p)  # the next layer's QKV operand
@@ -734,7 +695,7 @@ def _layer_backward_h3p(ctx, dh2, x, saved, W, meta, cfg):
         Gv.wo, Gv.w1, Gv.w2 = torch.empty_like(W.wo), torch.empty_like(W.w1), torch.empty_like(W.w2)
         Gv.bi = torch.zeros(F, dtype=torch.float32, device=dev)
 
-    def wgrad(dyp, xpp, out):
+    def wgrad(dyp, xpp, out, site):
         """out (+)= dy^T x on the side stream (or in line without a flat store / side stream)."""
         accumulate = wacc if side else acc
         ks = streams.side_ksplit(out.shape[0], out.shape[1]) if side else 2
@@ -743,7 +704,7 @@ def _layer_backward_h3p(ctx, dh2, x, saved, W, meta, cfg):
         def run():
             if store is not None:
                 (store.ensure_zero if accumulate else store.mark_stored)(out)
-            h3p.gemm(dyp, xpp, 1, 0, out=out, beta=1.0 if accumulate else 0.0, ksplit=ks)
+            h3p.gemm(dyp, xpp, 1, 0, out=out, beta=1.0 if accumulate else 0.0, ksplit=ks, site=site)
         if side:
             streams.run(dev, run, dyp.planes, dyp.exps, xpp.planes, xpp.exps)
         else:
@@ -753,30 +714,30 @@ def _layer_backward_h3p(ctx, dh2, x, saved, W, meta, cfg):
         da2p = h3p.empty(rows, H, dev)
         dz2, dg2, dbb2, db2 = ln_bwd_h3p(dh2, z2, m2, r2, W.g2, p_h, s_2, o_2, da2p,
                                          acc=(Gv.g2, Gv.bb2, Gv.b2) if acc else None, side=side)
-        wgrad(da2p, f1p, Gv.w2)
+        wgrad(da2p, f1p, Gv.w2, "ffn2_wgrad")
     # FFN-in data gradient through the GELU: planes out only, the FFN-in bias gradient from the
     # epilogue's column partials
     df1p = h3p.empty(rows, F, dev)
     part = torch.empty((rows // 128, F), dtype=torch.float32, device=dev)
     h3p.gemm(da2p, Wp.w2, 0, 0, bias=W.bi, epi=h3p.EPI_DGELU, aux=f1pre, part=part, colsum=Gv.bi,
-             colsum_acc=acc, planes_out=df1p)
-    wgrad(df1p, h1p, Gv.w1)
-    h3p.gemm(df1p, Wp.w1, 0, 0, out=dz2, beta=1.0)  # dh1 = dz2 + df1pre @ W1
+             colsum_acc=acc, planes_out=df1p, site="ffn2_dgrad")
+    wgrad(df1p, h1p, Gv.w1, "ffn1_wgrad")
+    h3p.gemm(df1p, Wp.w1, 0, 0, out=dz2, beta=1.0, site="ffn1_dgrad")  # dh1 = dz2 + df1pre @ W1
     with streams.coalesced():  # LN1 parameter gradients + the attention-output weight gradient
         da1p = h3p.empty(rows, H, dev)
         dz1, dg1, db1, dbo = ln_bwd_h3p(dz2, z1, m1, r1, W.g1, p_h, s_1, o_1, da1p,
                                         acc=(Gv.g1, Gv.b1, Gv.bo) if acc else None, side=side)
-        wgrad(da1p, ctxp, Gv.wo)
-    dctx = h3p.gemm(da1p, Wp.wo, 0, 0)
+        wgrad(da1p, ctxp, Gv.wo, "wo_wgrad")
+    dctx = h3p.gemm(da1p, Wp.wo, 0, 0, site="wo_dgrad")
     dqkvp = h3p.empty(rows, 3 * H, dev)
     dqkv = attn_bwd_h3p(qkv, mask_of(ctx), ctx_, dctx, (lse, dmask), B, S, NH, p_a, W.bqkv, dqkvp)
     with streams.coalesced():  # QKV weight and bias gradients
-        wgrad(dqkvp, xp, Gv.wqkv)
+        wgrad(dqkvp, xp, Gv.wqkv, "qkv_wgrad")
         if side:
             streams.run(dev, lambda: colsum(dqkv, acc=Gv.bqkv), dqkv)
         else:
             colsum(dqkv, acc=Gv.bqkv)
-    h3p.gemm(dqkvp, Wp.wqkv, 0, 0, out=dz1, beta=1.0)  # dx = dz1 + dqkv @ Wqkv
+    h3p.gemm(dqkvp, Wp.wqkv, 0, 0, out=dz1, beta=1.0, site="qkv_dgrad")  # dx = dz1 + dqkv @ Wqkv
     if acc:
         return (dz1, None, None) + (None,) * 16
     dWqkv, dbqkv = Gv.wqkv, Gv.bqkv
@@ -824,12 +785,7 @@ class FusedBertLayer(torch.autograd.Function):
         if isinstance(saved[-1], tuple) and saved[-1][0] == "h3p":
             return _layer_backward_h3p(ctx, dh2, x, saved, W, meta, cfg)
         qkv, ctx_, lse, dmask, z1, m1, r1, h1, f1pre, f1, z2, m2, r2, xin, cin = saved[:15]
-        if getattr(W, "planes", False) and W.bwd is not W:
-            W = W.bwd  # forward-only planes: the backward on the in-kernel-split engine (fp32 operands)
-        pl = getattr(W, "planes", False)
-        if pl:  # GEMM operands saved as split planes
-            h1, f1, xin, cin = (_planes_of(t) for t in (h1, f1, xin, cin))
-        am = None if pl else meta.get("amax")  # h3 engine: operand |max| slots (LayerAmax)
+        am = meta.get("amax")  # h3 engine: operand |max| slots (LayerAmax)
         sl = (lambda off, n=1: am.a(off, n)) if am is not None else (lambda off, n=1: None)
         wsl = (lambda i: am.w[i]) if am is not None else (lambda i: None)
         B, S, NH, p_h, p_a, eps, seeds = cfg
@@ -845,8 +801,6 @@ class FusedBertLayer(torch.autograd.Function):
         # stay in order
         side = acc and streams.enabled()
         dks = streams.DGRAD_KSPLIT if side else None  # K split of the dgrads beside the side stream
-        rows = dh2.shape[0]
-        dop = _planes_buf(rows, H, dh2.device) if pl else None  # the LN backwards write da as planes
         # first backward after zero_grad: the weight gradients are the only writers of their regions
         # and store instead of accumulating (the split-K reduce does not read the zeros back)
         store = meta.get("store")
@@ -883,13 +837,11 @@ class FusedBertLayer(torch.autograd.Function):
 
         # side-stream work forks at three points per layer; the launches at one point share one event
         with streams.coalesced():  # LN2 parameter gradients + the FFN-out weight gradient
-            dz2, do_, dg2, dbb2, db2 = ln_bwd(dh2, z2, m2, r2, W.g2, p_h, 1, s_2, o_2, True, not pl,
-                                              acc=(Gv.g2, Gv.bb2, Gv.b2) if acc else None, side=side, da_planes=dop,
-                                              amax=sl(8))
-            do_p = _planes_of(dop) if pl else do_
-            dW2 = wgrad(do_p, f1, Gv.w2 if acc else None, amax=_am(am, sl(8), sl(4, 2)))
-        bi_in_wgrad = side and not pl and _WGRAD_COLSUM and _FFN_BIAS_WGRAD
-        df1p, dbi = G.linear_dgrad_dgelu(do_p, W.w2, f1pre, W.bi, db_acc=Gv.bi if acc else None, planes_out=pl,
+            dz2, do_, dg2, dbb2, db2 = ln_bwd(dh2, z2, m2, r2, W.g2, p_h, 1, s_2, o_2, True, True,
+                                              acc=(Gv.g2, Gv.bb2, Gv.b2) if acc else None, side=side, amax=sl(8))
+            dW2 = wgrad(do_, f1, Gv.w2 if acc else None, amax=_am(am, sl(8), sl(4, 2)))
+        bi_in_wgrad = side and _WGRAD_COLSUM and _FFN_BIAS_WGRAD
+        df1p, dbi = G.linear_dgrad_dgelu(do_, W.w2, f1pre, W.bi, db_acc=Gv.bi if acc else None,
                                          amax=_am(am, sl(8), wsl(3)), amax_out=sl(9), colsum=not bi_in_wgrad)
         if dbi is None:  # the bias gradient comes with the FFN-in weight gradient (side stream)
             dW1, dbi = wgrad_bias(df1p, h1, Gv.w1, Gv.bi, _am(am, sl(9), sl(0, 2)))
@@ -897,20 +849,16 @@ class FusedBertLayer(torch.autograd.Function):
             dW1 = wgrad(df1p, h1, Gv.w1 if acc else None, amax=_am(am, sl(9), sl(0, 2)))
         dh1 = G.linear_dgrad(df1p, W.w1, out=dz2, accumulate=True, ksplit=dks,
                              amax=_am(am, sl(9), wsl(2)))  # dz2 + df1pre @ W1
-        dap = _planes_buf(rows, H, dh2.device) if pl else None
         with streams.coalesced():  # LN1 parameter gradients + the attention-output weight gradient
-            dz1, da1, dg1, db1, dbo = ln_bwd(dh1, z1, m1, r1, W.g1, p_h, 1, s_1, o_1, True, not pl,
-                                             acc=(Gv.g1, Gv.b1, Gv.bo) if acc else None, side=side, da_planes=dap,
-                                             amax=sl(10))
-            da1p = _planes_of(dap) if pl else da1
-            dWo = wgrad(da1p, cin, Gv.wo if acc else None, amax=_am(am, sl(10), sl(2, 2)))
-        dctx = G.linear_dgrad(da1p, W.wo, ksplit=dks, amax=_am(am, sl(10), wsl(1)))
+            dz1, da1, dg1, db1, dbo = ln_bwd(dh1, z1, m1, r1, W.g1, p_h, 1, s_1, o_1, True, True,
+                                             acc=(Gv.g1, Gv.b1, Gv.bo) if acc else None, side=side, amax=sl(10))
+            dWo = wgrad(da1, cin, Gv.wo if acc else None, amax=_am(am, sl(10), sl(2, 2)))
+        dctx = G.linear_dgrad(da1, W.wo, ksplit=dks, amax=_am(am, sl(10), wsl(1)))
         dqkv = attn_bwd(qkv, mask, ctx_, dctx, (lse, dmask), B, S, NH, p_a, bias=W.bqkv, amax=sl(11))
-        dqkvp = G.split(dqkv) if pl else dqkv
         qkv_w_am = _am(am, sl(11), am and am.xw)
         with streams.coalesced():  # QKV weight and bias gradients
             fused = False
-            if side and not pl and _WGRAD_COLSUM:  # one launch: the bias gradient from the wgrad's staging
+            if side and _WGRAD_COLSUM:  # one launch: the bias gradient from the wgrad's staging
                 ks = streams.side_ksplit(dqkv.shape[1], xin.shape[1])
 
                 def run_colsum():
@@ -921,12 +869,12 @@ class FusedBertLayer(torch.autograd.Function):
             if fused:
                 dWqkv, dbqkv = Gv.wqkv, Gv.bqkv
             else:
-                dWqkv = wgrad(dqkvp, xin, Gv.wqkv if acc else None, amax=qkv_w_am)
+                dWqkv = wgrad(dqkv, xin, Gv.wqkv if acc else None, amax=qkv_w_am)
                 if side:
                     dbqkv = streams.run(dqkv.device, lambda: colsum(dqkv, acc=Gv.bqkv), dqkv)
                 else:
                     dbqkv = colsum(dqkv, acc=Gv.bqkv if acc else None)
-        dx = G.linear_dgrad(dqkvp, W.wqkv, out=dz1, accumulate=True, ksplit=dks,
+        dx = G.linear_dgrad(dqkv, W.wqkv, out=dz1, accumulate=True, ksplit=dks,
                             amax=_am(am, sl(11), wsl(0)))  # dz1 + dqkv @ Wqkv
         if acc:
             return (dx, None, None) + (None,) * 16
@@ -1017,8 +965,7 @@ class FusedPreTrainingLoss(torch.autograd.Function):
         Wt, Wd = meta["weights"]()
         idx, lab, cnt = mlm_compact(labels.reshape(-1), cap)
         hsel = gather_rows(seq, idx)
-        pl = isinstance(Wt, G.Planes)  # fp32 on the plane engine: transform GEMM operands split once
-        hsel_in = G.split(hsel) if pl else hsel
+        hsel_in = hsel
         am = meta.get("amax")  # h3 engine: {seq, wt, wd, t2} |max| slots (hsel's bound: the whole sequence output)
         t1pre = G.linear_fwd(hsel_in, Wt, amax=(am["seq"], am["wt"]) if am else None)
         t1 = bias_gelu_fwd(t1pre, bt)
@@ -1041,10 +988,9 @@ class FusedPreTrainingLoss(torch.autograd.Function):
                            nsp_logits.data_ptr(), nsp_lse.data_ptr(), stats.data_ptr(), stats[2:].data_ptr(),
                            stream_handle())
         ctx.padded = lbuf is not None
-        ctx.save_for_backward(idx, lab, hsel_in.buf if pl else hsel, t1pre, t1, z, mean, rstd, t2,
+        ctx.save_for_backward(idx, lab, hsel, t1pre, t1, z, mean, rstd, t2,
                               lbuf if lbuf is not None else logits, lse, out, g, bt, seq, nsp_labels, pooled,
                               nsp_logits, nsp_lse, stats, wp, wn)
-        ctx.planes = pl
         ctx.meta = meta
         ctx.T = T
         return stats[2]
@@ -1114,8 +1060,7 @@ class FusedPreTrainingLoss(torch.autograd.Function):
         dt1, _, dg, db, _ = ln_bwd(dt2, z, mean, rstd, g, 0.0, 0, acc=(Gv[2], Gv[3]) if acc else None, side=side)
         am_d = am["dt"] if am else None  # |dt1pre|: the transform's two gradient products share it
         dt1pre, dbt = gelu_bwd_colsum(dt1, t1pre, bt, db_acc=Gv[1] if acc else None, amax=am_d)
-        hsel_in = _planes_of(hsel) if ctx.planes else hsel
-        dt1pre_in = G.split(dt1pre) if ctx.planes else dt1pre
+        hsel_in, dt1pre_in = hsel, dt1pre
         wt_am = (am_d, am["seq"]) if am else None
         if side:
             dWt = streams.run(dt1pre.device, lambda: G.linear_wgrad(dt1pre_in, hsel_in, out=Gv[0], accumulate=True,

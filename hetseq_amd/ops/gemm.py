@@ -144,6 +144,32 @@ def _amax_ptr(t, given, keep):
     return am.data_ptr(), am.numel() // SLOT_FLOATS
 
 
+def _h3_census(site, a, b):
+    """Precision census of the per-tensor-scaled h3 engine (ops/h3p.py CENSUS, same metric): nonzero
+    elements below their TENSOR's 2^18 window (|x * 2^e| < 2^-3, e from the tensor's |max|)."""
+    from hetseq_amd.ops import h3p
+
+    if not h3p._CENSUS_ON[0]:
+        return
+    for role, t in (("A", a), ("B", b)):
+        x = t.detach().double()
+        ax = x.abs()
+        m = float(ax.max()) if x.numel() else 0.0
+        if not m > 0.0:
+            continue
+        import math
+
+        e = 14 - math.floor(math.log2(m))
+        nz = x != 0
+        out = nz & (ax * 2.0 ** e < 0.125)
+        c = h3p.CENSUS.setdefault(("h3",) + tuple(site) + (role,), [0, 0, 0.0, 0.0, 0])
+        c[0] += int(nz.sum())
+        c[1] += int(out.sum())
+        c[2] += float(ax[out].sum())
+        c[3] += float(ax.sum())
+        c[4] += 1
+
+
 def set_fp32_mode(mode):
     """'h3' (split-fp16 products, per-tensor scales), 'x6' (split-bf16 products; both fp32-level
     error), 'native' (exact-fp32 MFMA) or 'x3' (benchmark only)."""
@@ -174,40 +200,11 @@ def _slab(M, N, ksplit, device):
     return buf
 
 
-# In-launch split-K finish (gemm.hip splitk_inlaunch): the last K slice to arrive at a tile sums the
-# slices and writes C, instead of a separate splitk_reduce pass.  Opt-in (HETSEQ_SPLITK_INLAUNCH=1):
-# bitwise the same result, but in the BERT-base fp32 step it loses to the separate pass (interleaved
-# A/B, 8 rounds: 12.03 ms write-through slabs, 12.11 plain + release fence, against 11.88 with the
-# pass -- 64 KB per slice and tile is past the size where an in-launch combine pays, and the pass runs
-# on the weight-gradient stream beside the data-gradient chain anyway).
-_INLAUNCH = os.environ.get("HETSEQ_SPLITK_INLAUNCH", "0") == "1"
-_TICKETS = {}
-
-
-def _tickets(device):
-    """The arrival counters of the current stream role's split-K GEMMs (zero between launches: the
-    last arriver of each tile resets its counter), or None (off, or first use inside a capture)."""
-    if not _INLAUNCH:
-        return None
-    from hetseq_amd.runtime import streams
-
-    key = (device, streams.role(stream_handle()))
-    buf = _TICKETS.get(key)
-    if buf is None:
-        if torch.cuda.is_current_stream_capturing():
-            return None
-        buf = torch.zeros(hip().splitk_tickets(), dtype=torch.int32, device=device)
-        _TICKETS[key] = buf
-    return buf
-
-
 # ------------------------------------------------------------------ bf16-plane operands
 class Planes(object):
-    """A [rows, cols] GEMM operand as P bf16 planes (csrc/kernels/gemm_planes.hip):
-    P = 3 -- an fp32 matrix split once into hi + mid + lo (the fp32 engine's operand);
-    P = 1 -- a bf16 matrix as it is (--dtype bf16).
-    ``buf`` owns the storage; element (r, c) of plane p sits at flat index
-    ``offset + p * ps + r * ld + c`` of it."""
+    """A [rows, cols] bf16 GEMM operand of the bf16-plane engine (csrc/kernels/gemm_planes.hip,
+    --dtype bf16; P = 1).  ``buf`` owns the storage; element (r, c) sits at flat index
+    ``offset + r * ld + c`` of it."""
 
     __slots__ = ("buf", "rows", "cols", "ld", "ps", "P", "offset")
 
@@ -236,75 +233,15 @@ class Planes(object):
         return Planes(x, x.shape[0], x.shape[1], x.stride(0), 0, 1)
 
     def unsplit(self):
-        """fp32 value of the planes (tests / debugging)."""
+        """fp32 value (tests / debugging)."""
         v = self.buf.reshape(-1)[self.offset:]
-        if self.P == 1:
-            return torch.as_strided(v, (self.rows, self.cols), (self.ld, 1)).float()
-        parts = [torch.as_strided(v[p * self.ps:], (self.rows, self.cols), (self.ld, 1)).float() for p in range(3)]
-        return parts[2] + parts[1] + parts[0]
-
-
-def planes_enabled():
-    """fp32 GEMMs on pre-split planes (HETSEQ_GEMM_PLANES=0 keeps the in-kernel-split x6 engine)."""
-    return _PLANES != "off" and _FP32 == "x6" and _MODE != "blas"
-
-
-def planes_backward():
-    """The backward's GEMMs on the plane engine too (HETSEQ_GEMM_PLANES=1), or only the forward's
-    (HETSEQ_GEMM_PLANES=fwd: the backward stays on the in-kernel-split engine, whose blocks share
-    CUs with the weight-gradient side stream's -- profiles/r3_gemm_ring.md)."""
-    return planes_enabled() and _PLANES == "all"
-
-
-def set_planes_mode(mode):
-    """'off' | 'fwd' | 'all' (tests / benchmarks; takes effect for weights built afterwards)."""
-    global _PLANES
-    assert mode in ("off", "fwd", "all")
-    _PLANES = mode
-
-
-# HETSEQ_GEMM_PLANES: 0 (in-kernel-split engine everywhere), fwd (forward products on the ring
-# plane kernel, fed by producers that emit planes), 1 (every product on planes)
-_PLANES = {"0": "off", "1": "all", "all": "all", "fwd": "fwd"}.get(os.environ.get("HETSEQ_GEMM_PLANES", "0"), "off")
-
-
-# Tensors whose split-bf16 planes a producer kernel already wrote (an LN forward emitting its
-# output in both formats): the consumer's split() is then free.  Keyed by the tensor object and
-# its version counter, so an in-place update invalidates the entry.
-_KNOWN_PLANES: dict = {}
-
-
-def remember_planes(t, planes):
-    import weakref
-
-    _KNOWN_PLANES[id(t)] = (weakref.ref(t), t._version, planes)
-
-
-def split_cached(x):
-    """:func:`split` unless a producer already emitted ``x``'s planes (entry consumed once)."""
-    e = _KNOWN_PLANES.pop(id(x), None)
-    if e is not None and e[0]() is x and e[1] == x._version:
-        return e[2]
-    if len(_KNOWN_PLANES) > 8:  # entries of tensors that were never consumed (the last layer's output)
-        for k in [k for k, v in _KNOWN_PLANES.items() if v[0]() is None]:
-            del _KNOWN_PLANES[k]
-    return split(x.contiguous())
-
-
-def split(x, out=None):
-    """fp32 [rows, cols] (contiguous) -> P = 3 Planes (one elementwise pass: read 4 B, write 6 B)."""
-    assert x.dtype == torch.float32 and x.dim() == 2 and x.is_contiguous() and x.numel() % 4 == 0
-    rows, cols = x.shape
-    if out is None:
-        out = torch.empty((3, rows, cols), dtype=torch.bfloat16, device=x.device)
-    hip().split_planes(x.data_ptr(), out.data_ptr(), x.numel(), rows * cols, stream_handle())
-    return Planes(out, rows, cols, cols, rows * cols, 3)
+        return torch.as_strided(v, (self.rows, self.cols), (self.ld, 1)).float()
 
 
 def _unplane(x):
-    """fp32 value of a P = 3 operand for the engines that take fp32 (shapes the plane engine does
-    not tile, e.g. a 40-row masked-LM head in a test); other operands unchanged."""
-    return x.unsplit() if isinstance(x, Planes) and x.P == 3 else (x.buf if isinstance(x, Planes) else x)
+    """The bf16 matrix behind a Planes operand (shapes the plane engine does not tile); other operands
+    unchanged."""
+    return x.buf if isinstance(x, Planes) else x
 
 
 def _as_planes(x):
@@ -315,85 +252,19 @@ def _as_planes(x):
     return None
 
 
-RING = 5  # gemm_planes variant id of the 3-stage LDS-DMA ring kernel (csrc/kernels/gemm_ring.hip)
-_RING_OFF = os.environ.get("HETSEQ_GEMM_RING", "1") == "0"
-
-
-def _ring_bn(M, N, ta):
-    """Tile width the ring launcher picks (mirror of gemm_ring.hip pick_bn)."""
-    ok96, ok128 = N % 96 == 0, N % 128 == 0
-    if not (ok96 or ok128):
-        return 0
-    if ta and ok96:
-        return 96
-    if not ok96:
-        return 128
-    if not ok128:
-        return 96
-    t96, t128 = (M // 128) * (N // 96), (M // 128) * (N // 128)
-    return 128 if -(-t128 // 256) * 128 <= -(-t96 // 256) * 96 else 96
-
-
-def ring_ksplit(M, N, K, ta):
-    """K slices for a ring launch: minimise (rounds of one-per-CU blocks) x (K per block) plus the
-    fp32 slab traffic of the split (written and read once): t ~ rounds * 128 * BN * K/s * 12 FLOP at
-    ~5 TF/s per CU  +  s * M * N * 8 B at ~5 TB/s."""
-    bn = _ring_bn(M, N, ta)
-    if bn == 0 or M % 128:
-        return 1
-    tiles = (M // 128) * (N // bn)
-    best = None
-    for s in (1, 2, 4, 8):
-        if K % (32 * s) or (s > 1 and K // s < 256):
-            continue
-        t = -(-tiles * s // 256) * 128 * bn * (K // s) * 12 / 5.1e12 + (s * M * N * 8 / 5e12 if s > 1 else 0.0)
-        if best is None or t < best[0]:
-            best = (t, s)
-    return best[1] if best else 1
-
-
 def gemm_planes(a, b, ta, tb, out, bias=None, epi=EPI_NONE, beta=0.0, aux=None, part=None, colsum=None,
-                colsum_acc=False, ksplit=1, variant=-1, outp=None, ring_bn=0):
+                colsum_acc=False, ksplit=1, variant=-1):
     """Launch the bf16-plane engine on Planes operands; False (nothing launched) if not served.
     ``variant``: kernel variant (gemm_planes.hip: 0 two LDS stages, 1 one stage, 2 half K depth,
-    3 eight waves, 4 eight waves + one stage; 5 = RING, gemm_ring.hip); -1 = the ring kernel for
-    split-fp32 planes when it serves the shape, else :func:`planes_variant`.  ``outp``: a [3, M, N]
-    bf16 buffer that receives the result again as split planes (ring kernel, GELU / dGELU
-    epilogues: the output is the next GEMM's operand)."""
+    3 eight waves, 4 eight waves + one stage); -1 = :func:`planes_variant`."""
     M, N, K = _dims(a, b, ta, tb)
-    if out is None:  # plane output only (ring kernel, fused-activation epilogues)
-        if outp is None or a.P != 3 or variant not in (-1, RING) or _RING_OFF:
-            return False
-    elif a.P != b.P or not out.is_cuda or out.stride(1) != 1 or out.dtype not in (torch.float32, torch.bfloat16) \
-            or out.shape != (M, N):
-        return False
-    if a.P == 3 and (out is None or out.dtype == torch.float32) and variant in (-1, RING) and not _RING_OFF:
-        ks = ksplit if ksplit and ksplit > 0 else 1
-        dev = a.device
-        slab = _slab(M, N, ks, dev) if ks > 1 else None
-        if ks > 1 and slab is None:
-            ks = 1
-        ldc = out.stride(0) if out is not None else N
-        if outp is None or (tuple(outp.shape) == (3, M, N) and ldc == N):
-            rc = hip().gemm_ring(int(ta), int(tb), M, N, K, a.data_ptr(), a.ld, a.ps, b.data_ptr(), b.ld, b.ps,
-                                 out.data_ptr() if out is not None else 0, ldc,
-                                 bias.data_ptr() if bias is not None else 0, epi,
-                                 float(beta), aux.data_ptr() if aux is not None else 0,
-                                 aux.stride(0) if aux is not None else 0, part.data_ptr() if part is not None else 0,
-                                 colsum.data_ptr() if colsum is not None else 0, int(colsum_acc), int(ks),
-                                 slab.data_ptr() if slab is not None else 0, slab.numel() if slab is not None else 0,
-                                 outp.data_ptr() if outp is not None else 0, M * N if outp is not None else 0,
-                                 int(ring_bn), stream_handle())
-            if rc == 0:
-                return True
-        if variant == RING:
-            return False
-    if outp is not None or out is None:
+    if out is None or a.P != b.P or not out.is_cuda or out.stride(1) != 1 or \
+            out.dtype not in (torch.float32, torch.bfloat16) or out.shape != (M, N):
         return False
     slab = _slab(M, N, ksplit, out.device) if ksplit > 1 else None
     if ksplit > 1 and slab is None:
         ksplit = 1
-    if variant < 0 or variant == RING:
+    if variant < 0:
         variant = planes_variant(M, N, K, a.P, ta)
     rc = hip().gemm_planes(a.P, 1 if out.dtype == torch.bfloat16 else 0, int(ta), int(tb), M, N, K, a.data_ptr(),
                            a.ld, a.ps, b.data_ptr(), b.ld, b.ps, out.data_ptr(), out.stride(0),
@@ -406,9 +277,8 @@ def gemm_planes(a, b, ta, tb, out, bias=None, epi=EPI_NONE, beta=0.0, aux=None, 
 
 
 def planes_variant(M, N, K, P, ta):
-    """Default kernel variant per shape, from tools/bench_planes.py on MI355X (profiles/
-    r2_gemm_engines.md): one LDS stage (3 workgroups per CU) for the split-fp32 planes, except
-    the small-grid 768 x 768-class products (8 waves); bf16 sites are measured (gemm())."""
+    """Default kernel variant per shape (profiles/r2_gemm_engines.md): one LDS stage (3 workgroups per
+    CU), except the small-grid 768 x 768-class products (8 waves); call sites are measured (gemm())."""
     tiles = (M // 128) * (N // 128)
     if tiles <= 256 and K <= 1024 and not ta:
         return 3
@@ -424,11 +294,8 @@ def _planes_ksplit(M, N, K, P):
     key = (M, N, K, P)
     if key in PLANES_KSPLIT:
         return PLANES_KSPLIT[key]
-    if P == 3 and not _RING_OFF and _ring_bn(M, N, True):
-        return ring_ksplit(M, N, K, True)
     tiles, s = (M // 128) * (N // 128), 1
-    bk = 32 if P == 3 else 64
-    while tiles * s < 384 and s < 8 and K % (2 * s * bk) == 0 and K // (2 * s) >= 512:
+    while tiles * s < 384 and s < 8 and K % (2 * s * 64) == 0 and K // (2 * s) >= 512:
         s *= 2
     return s
 
@@ -494,19 +361,20 @@ def _hip_gemm(a, b, ta, tb, out, bias=None, epi=EPI_NONE, beta=0.0, aux=None, pa
     mv, nv, kv = valid if valid is not None else (0, 0, 0)
     assert dims is not None or out.shape == (M, N)
     dt = _FP32_DT[fp32 or _FP32]
+    if dt == 4:
+        _h3_census((M, N, K, ta, tb, epi), a, b)
     am, keep = (0, 0, 0, 0), []
     if dt == 4:
         am = _amax_ptr(a, amax[0] if amax is not None else None, keep) + _amax_ptr(
             b, amax[1] if amax is not None else None, keep)
     slab = _slab(M, N, ksplit, a.device) if (dt or ksplit > 1) and epi <= EPI_BIAS and ksplit != 1 else None
-    tk = _tickets(a.device) if slab is not None else None
     rc = hip().gemm(dt, int(ta), int(tb), M, N, K, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0),
                     out.data_ptr(), out.stride(0), bias.data_ptr() if bias is not None else 0, epi, float(beta),
                     aux.data_ptr() if aux is not None else 0, aux.stride(0) if aux is not None else 0,
                     part.data_ptr() if part is not None else 0, colsum.data_ptr() if colsum is not None else 0,
                     int(colsum_acc), stream_handle(), tile, ksplit,
                     slab.data_ptr() if slab is not None else 0, slab.numel() if slab is not None else 0, mv, nv, kv,
-                    am[0], am[1], am[2], am[3], slot_ptr(amax_out), tk.data_ptr() if tk is not None else 0)
+                    am[0], am[1], am[2], am[3], slot_ptr(amax_out), 0)
     return rc == 0
 
 
@@ -568,21 +436,19 @@ def gemm(a, b, ta=False, tb=False, out=None, bias=None, epi=EPI_NONE, beta=0.0, 
     """out = beta*out + op(a) @ op(b) (+bias).  ``ksplit`` overrides the measured split-K of the HIP engine.
     ``amax``: (a's, b's) |max| partials for the h3 engine (None entries are computed).
 
-    Operands that are :class:`Planes` (fp32 split once) or bf16 matrices run on the bf16-plane
-    engine (gemm_planes.hip); fp32 tensors on the in-kernel-split engine (gemm.hip) or the library."""
+    bf16 operands (:class:`Planes` or bf16 matrices) run on the bf16-plane engine (gemm_planes.hip)
+    or the library, per measured call site; fp32 tensors on the in-kernel-split engine (gemm.hip) or
+    the library."""
     M, N, K = _dims(a, b, ta, tb)
     pa, pb = _as_planes(a), _as_planes(b)
     if pa is not None and pb is not None and _MODE != "blas":
-        odt = out_dtype or (torch.float32 if pa.P == 3 else torch.bfloat16)
+        odt = out_dtype or torch.bfloat16
         if out is None:
             out = torch.empty((M, N), dtype=odt, device=pa.device)
         ks = ksplit if ksplit is not None else (_planes_ksplit(M, N, K, pa.P) if ta and epi == EPI_NONE
                                                 and out.dtype == torch.float32 else 1)
-        if pa.P == 3:
-            if gemm_planes(pa, pb, ta, tb, out, bias, epi, beta, ksplit=ks):
-                return out
-        elif _bf16_choice((M, N, K, ta, tb, epi, beta != 0.0, "bf16"), pa, pb, ta, tb, out, bias, epi, beta, ks,
-                          out_dtype) is not None:
+        if _bf16_choice((M, N, K, ta, tb, epi, beta != 0.0, "bf16"), pa, pb, ta, tb, out, bias, epi, beta, ks,
+                        out_dtype) is not None:
             return out
         a, b = _unplane(a), _unplane(b)  # a shape the plane engine does not serve, or the library
     odt = out_dtype or a.dtype
@@ -769,6 +635,7 @@ def linear_fwd_partials(x, w, ksplit=None, amax=None):
             slab = _slab(M, N, ks, x.device)
             if slab is not None:
                 am, keep = (0, 0, 0, 0), []
+                _h3_census((M, N, K, 0, 1, 0), x, w)
                 if _FP32 in ("h3", "h3p"):
                     am = _amax_ptr(x, amax[0] if amax is not None else None, keep) + _amax_ptr(
                         w, amax[1] if amax is not None else None, keep)
@@ -824,13 +691,10 @@ def linear_wgrad_colsum(dy, x, out, colsum_out, ksplit=None, accumulate=True, am
                      colsum_acc=accumulate, ksplit=ks, amax=amax)
 
 
-def linear_gelu_fwd(x, w, b, planes_out=False, emit_planes=False, out=None, amax=None, amax_out=None):
+def linear_gelu_fwd(x, w, b, out=None, amax=None, amax_out=None):
     """FFN-in forward: pre = x @ w^T (un-biased, kept for the backward), y = gelu(pre + b).
 
     Returns (y, pre).  One fused HIP GEMM (epilogue writes both) or library GEMM + bias_gelu kernel.
-    ``planes_out`` (fp32 plane engine): y is returned as split-bf16 :class:`Planes` written by the
-    epilogue (no fp32 copy).  ``emit_planes``: y fp32 AND its planes from the same epilogue, the
-    planes left for :func:`split_cached` (forward-only plane mode: the backward reads fp32 y).
     ``out`` = (y, pre) buffers to write (fp32 operands; row slices of whole-batch tensors).
     ``amax``: (x's, w's) |max| partials (h3 engine); ``amax_out``: a zeroed 1-element tensor that
     receives |max| of y (the FFN-out product's operand scale) -- filled on every path.
@@ -839,23 +703,11 @@ def linear_gelu_fwd(x, w, b, planes_out=False, emit_planes=False, out=None, amax
 
     T, N = x.shape[0], w.shape[0]
     px, pw = _as_planes(x), _as_planes(w)
-    if px is not None and pw is not None and _MODE != "blas":
-        dt = torch.float32 if px.P == 3 else torch.bfloat16
-        pre = torch.empty((T, N), dtype=dt, device=px.device)
-        if px.P == 3 and planes_out:
-            # y only as split planes (its one use is the next GEMM's operand): Planes, pre
-            yp = torch.empty((3, T, N), dtype=torch.bfloat16, device=px.device)
-            if gemm_planes(px, pw, False, True, None, b, EPI_GELU, 0.0, aux=pre, outp=yp):
-                return Planes(yp, T, N, N, T * N, 3), pre
-        if px.P == 3 and emit_planes:
-            y = torch.empty_like(pre)
-            yp = torch.empty((3, T, N), dtype=torch.bfloat16, device=px.device)
-            if gemm_planes(px, pw, False, True, y, b, EPI_GELU, 0.0, aux=pre, outp=yp):
-                remember_planes(y, Planes(yp, T, N, N, T * N, 3))
-                return y, pre
+    if px is not None and pw is not None and _MODE != "blas":  # bf16 operands
+        pre = torch.empty((T, N), dtype=torch.bfloat16, device=px.device)
         y = torch.empty_like(pre)
         if gemm_planes(px, pw, False, True, y, b, EPI_GELU, 0.0, aux=pre):
-            return (split(y) if planes_out else y), pre
+            return y, pre
         x, w = _unplane(x), _unplane(w)
     if out is not None:
         y, pre = out
@@ -885,13 +737,12 @@ def linear_gelu_fwd(x, w, b, planes_out=False, emit_planes=False, out=None, amax
     return y, pre
 
 
-def linear_dgrad_dgelu(dy, w, pre, b, db_acc=None, planes_out=False, amax=None, amax_out=None, colsum=True):
+def linear_dgrad_dgelu(dy, w, pre, b, db_acc=None, amax=None, amax_out=None, colsum=True):
     """FFN backward through the GELU: dpre = (dy @ w) * gelu'(pre + b), db = colsum(dpre).
 
     ``db`` is accumulated into ``db_acc`` (flat-store view) when given.  Returns (dpre, db);
     ``colsum=False`` (HIP engine only; else ignored): no db -- returns (dpre, None), the caller sums
-    the bias gradient elsewhere (bert_ops: inside the FFN-in weight-gradient launch);
-    ``planes_out`` (fp32 plane engine): dpre as split-bf16 :class:`Planes` (no fp32 copy).
+    the bias gradient elsewhere (bert_ops: inside the FFN-in weight-gradient launch).
     ``amax`` / ``amax_out``: as in :func:`linear_gelu_fwd` (|max| of dpre into ``amax_out``).
     """
     from hetseq_amd.ops import bert_ops
@@ -899,17 +750,12 @@ def linear_dgrad_dgelu(dy, w, pre, b, db_acc=None, planes_out=False, amax=None, 
     T, N = dy.shape[0], w.shape[1]
     db = db_acc if db_acc is not None else torch.empty(N, dtype=torch.float32, device=dy.device)
     pd, pw = _as_planes(dy), _as_planes(w)
-    if pd is not None and pw is not None and _MODE != "blas":
+    if pd is not None and pw is not None and _MODE != "blas":  # bf16 operands
         part = torch.empty(((T + 127) // 128, N), dtype=torch.float32, device=pre.device)
-        if pd.P == 3 and planes_out:
-            dp = torch.empty((3, T, N), dtype=torch.bfloat16, device=pre.device)
-            if gemm_planes(pd, pw, False, False, None, b, EPI_DGELU, 0.0, aux=pre, part=part, colsum=db,
-                           colsum_acc=db_acc is not None, outp=dp):
-                return Planes(dp, T, N, N, T * N, 3), db
         dpre = torch.empty((T, N), dtype=pre.dtype, device=pre.device)
         if gemm_planes(pd, pw, False, False, dpre, b, EPI_DGELU, 0.0, aux=pre, part=part, colsum=db,
                        colsum_acc=db_acc is not None):
-            return (split(dpre) if planes_out else dpre), db
+            return dpre, db
         dy, w = _unplane(dy), _unplane(w)
     dpre = torch.empty((T, N), dtype=dy.dtype, device=dy.device)
     if dy.is_cuda and _MODE != "blas" and _hip_ok(dy, w, dpre, pre, b):

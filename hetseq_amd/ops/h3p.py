@@ -100,7 +100,7 @@ class SplitTable(object):
     """One launch that splits many fp32 matrices (the GEMM weights after every update): the
     segment records live in device memory, built once for fixed addresses."""
 
-    FMT = "QQQqqqqiiiii"
+    FMT = "QQQqqqqiiii"  # QSplitSeg (gemm_h3p.hip): src, dst, ex, lds, ldd, ps, lde, rows, cols, blk0, pad
 
     def __init__(self, pairs, device):
         """``pairs``: [(fp32 2-D tensor, HP destination)]."""
@@ -111,7 +111,7 @@ class SplitTable(object):
             assert x.dtype == torch.float32 and x.stride(1) == 1 and x.shape == (hp.rows, hp.cols)
             assert x.data_ptr() % 16 == 0 and x.stride(0) % 4 == 0
             recs.append(struct.pack("<" + self.FMT, x.data_ptr(), hp.data_ptr(), hp.exps_ptr(), x.stride(0), hp.ld,
-                                    hp.ps, hp.lde, hp.rows, hp.cols, blk, 0, 0))
+                                    hp.ps, hp.lde, hp.rows, hp.cols, blk, 0))
             blk += (hp.rows // BLK) * (hp.cols // BLK)
         raw = torch.frombuffer(bytearray(b"".join(recs)), dtype=torch.uint8)
         self.table = raw.to(device)
@@ -152,8 +152,46 @@ def ksplit_for(M, N, K):
     return s
 
 
+# ------------------------------------------------------------------ precision census
+# HETSEQ_H3P_CENSUS=1 (or census_start()): every gemm() records, per call site and operand, how many
+# nonzero elements lie below their block's 2^18 window (|x * 2^e| < 2^-3: fewer than 22 bits kept)
+# and their share of the operand's |x| mass.  Host-synchronising; a diagnostic (tools/h3p_census.py).
+CENSUS: dict = {}
+_CENSUS_ON = [__import__("os").environ.get("HETSEQ_H3P_CENSUS", "0") == "1"]
+
+
+def census_start():
+    CENSUS.clear()
+    _CENSUS_ON[0] = True
+
+
+def census_stop():
+    _CENSUS_ON[0] = False
+    return dict(CENSUS)
+
+
+def window_stats(hp):
+    """(nonzero elements, of them below the window, |x| mass below the window, total |x| mass)."""
+    flat = hp.planes.reshape(-1).view(torch.float16)
+    hi = torch.as_strided(flat, (hp.rows, hp.cols), (hp.ld, 1), hp.offset).float()
+    x = hp.unsplit().double()
+    nz = x != 0
+    out = nz & (hi.abs() < 0.125)
+    ax = x.abs()
+    return int(nz.sum()), int(out.sum()), float(ax[out].sum()), float(ax.sum())
+
+
+def _census(site, a, b):
+    for role, hp in (("A", a), ("B", b)):
+        st = window_stats(hp)
+        c = CENSUS.setdefault((site, role), [0, 0, 0.0, 0.0, 0])
+        for i in range(4):
+            c[i] += st[i]
+        c[4] += 1
+
+
 def gemm(a, b, ta=False, tb=False, out=None, bias=None, epi=EPI_NONE, beta=0.0, aux=None, part=None, colsum=None,
-         colsum_acc=False, ksplit=1, planes_out=None, slab_only=False):
+         colsum_acc=False, ksplit=1, planes_out=None, slab_only=False, site=None):
     """``out = beta*out + op(a) @ op(b)`` (+ epilogue) on h3p operands.
 
     ``epi``: EPI_BIAS (+bias), EPI_GELU (``aux`` <- pre-activation, result gelu(pre + bias)),
@@ -164,6 +202,8 @@ def gemm(a, b, ta=False, tb=False, out=None, bias=None, epi=EPI_NONE, beta=0.0, 
     the next split GEMM on this stream).  Raises on a request the kernel does not serve."""
     M, N, K = dims(a, b, ta, tb)
     assert (tb and b.cols == K) or (not tb and b.rows == K), "inner dimensions differ"
+    if _CENSUS_ON[0]:
+        _census(site or (M, N, K, ta, tb), a, b)
     dev = a.device
     slab = None
     if ksplit > 1:

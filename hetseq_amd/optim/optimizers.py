@@ -165,7 +165,6 @@ class _Optimizer(object):
                 self._step_hip(gm)
             else:
                 self._step_cpu(gm)
-            self.store.refresh_planes()  # split-bf16 weight planes of the fp32 GEMM engine
         self._mult = None
         self._norm_ready = False
         return loss

@@ -81,7 +81,6 @@ class FlatParamStore(object):
                     self.params.append(q)
                     self.names.append(name_of[id(q)])
         self.shadow = None
-        self.planes = None  # [3, total] bf16 hi/mid/lo split of ``param`` (enable_planes)
         if shadow_dtype is not None:
             self.shadow = torch.empty(total, dtype=shadow_dtype, device=dev)
             self.sync_shadow()
@@ -240,7 +239,6 @@ class FlatParamStore(object):
 
     def sync_shadow(self):
         if self.shadow is None:
-            self.refresh_planes()
             return
         with torch.no_grad():
             if self.param.is_cuda and self.shadow.dtype == torch.bfloat16:
@@ -249,36 +247,6 @@ class FlatParamStore(object):
                 hip().cast_f32_bf16(self.param.data_ptr(), self.shadow.data_ptr(), self.numel, stream_handle())
             else:
                 self.shadow.copy_(self.param)
-        self.refresh_planes()
-
-    def enable_planes(self):
-        """Keep a three-plane split-bf16 copy of the fp32 weights (x = hi + mid + lo, see
-        csrc/kernels/gemm_planes.hip) for the fp32 GEMM engine, refreshed after every
-        optimizer step.  Same offsets as ``param``; plane stride ``numel``."""
-        if self.planes is None and self.param.is_cuda:
-            self.planes = torch.empty((3, self.numel), dtype=torch.bfloat16, device=self.device)
-            self.refresh_planes()
-        return self.planes
-
-    def refresh_planes(self):
-        if self.planes is None:
-            return
-        from hetseq_amd.ops._C import hip, stream_handle
-
-        hip().split_planes(self.param.data_ptr(), self.planes.data_ptr(), self.numel, self.numel, stream_handle())
-
-    def planes_view(self, params, shape):
-        """Planes operand (ops.gemm.Planes) over adjacent ``params`` viewed as ``shape``."""
-        from hetseq_amd.ops.gemm import Planes
-
-        off = self.offsets[id(params[0])]
-        cur = off
-        for p in params:
-            assert self.offsets.get(id(p)) == cur, "parameters are not adjacent in the flat store"
-            cur += p.numel()
-        rows, cols = shape
-        assert rows * cols == cur - off
-        return Planes(self.planes, rows, cols, cols, self.numel, 3, off)
 
     def checksum(self):
         return self.param.double().sum()

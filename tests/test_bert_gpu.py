@@ -241,40 +241,6 @@ def test_base_model_param_count(cuda):
     assert len(m.state_dict()) == 207
 
 
-def test_fp32_plane_engine_matches_reference(cuda, monkeypatch):
-    """fp32 on the opt-in bf16-plane engine (HETSEQ_GEMM_PLANES=1: operands split once into
-    hi/mid/lo planes, weight planes refreshed by the optimizer) tracks the torch-op reference."""
-    from hetseq_amd.ops import gemm as G
-    from hetseq_amd.runtime.flat import FlatParamStore
-
-    G.set_fp32_mode("x6")  # (the plane engine is the six-term split's)
-
-    monkeypatch.setattr(G, "_PLANES", "all")
-    model, cfg = _tiny(cuda)
-    model.eval()
-    model.max_predictions_per_seq = 32  # 4 x 32 = 128 masked-LM rows: the transform GEMMs tile
-    ref = copy.deepcopy(model)
-    store = FlatParamStore(model)
-    model.attach_store(store, torch.float32)
-    assert store.planes is not None
-    batch = _batch(cuda, 4, 64, cfg.vocab_size, P=32)
-    l1 = model(*batch)
-    l2 = ref(*batch)
-    assert abs(l1.item() - l2.item()) < 1e-4 * abs(l2.item()) + 1e-5, (l1.item(), l2.item())
-    l1.backward()
-    l2.backward()
-    for (n, p1), (_, p2) in zip(model.named_parameters(), ref.named_parameters()):
-        d = (p1.grad - p2.grad).abs().max().item()
-        assert d <= 2e-3 * (p2.grad.abs().max().item() + 1e-6) + 1e-6, (n, d)
-    # the weight planes follow an in-place parameter update
-    with torch.no_grad():
-        store.param.mul_(0.5)
-    store.refresh_planes()
-    w = model.bert.encoder.layer[0].attention.output.dense.weight
-    pv = store.planes_view([w], tuple(w.shape)).unsplit()
-    assert torch.allclose(pv, w, rtol=2 ** -22, atol=0)
-
-
 def _grad_report(model, ref):
     """Worst per-parameter gradient difference relative to the oracle's largest entry of that
     parameter -- floored at 1e-3 of the model's largest gradient entry: the key biases' gradient
@@ -290,13 +256,31 @@ def _grad_report(model, ref):
     return worst, where
 
 
-@pytest.mark.parametrize("planes,engine", [("off", "x6"), ("fwd", "x6"), ("all", "x6"), ("off", "h3"),
-                                           ("off", "h3p")])
-def test_bert_base_shape_matches_reference_1e4(cuda, monkeypatch, planes, engine):
+def _row_grad_report(model, ref):
+    """Worst per-ROW gradient difference of the 2-D parameters: each row's largest |difference|
+    relative to the oracle's largest entry of that row (rows whose largest entry is below 1e-6 of the
+    parameter's are rounding noise in both paths and skipped) -- small rows are judged on their own
+    scale, not hidden under the parameter's largest entry."""
+    worst, where = 0.0, None
+    for (n, p1), (_, p2) in zip(model.named_parameters(), ref.named_parameters()):
+        if p1.dim() != 2:
+            continue
+        g1, g2 = p1.grad.double(), p2.grad.double()
+        rmax = g2.abs().amax(dim=1)
+        keep = rmax > 1e-6 * rmax.max()
+        if not keep.any():
+            continue
+        r = ((g1 - g2).abs().amax(dim=1)[keep] / rmax[keep]).max().item()
+        if r > worst:
+            worst, where = r, n
+    return worst, where
+
+
+@pytest.mark.parametrize("engine", ["x6", "h3", "h3p"])
+def test_bert_base_shape_matches_reference_1e4(cuda, engine):
     """BERT-base (H 768, L 12, 12 heads, S 128, B 8), dropout off: the fused fp32 path -- in-kernel
-    split engine (six split-bf16 products, x6, or three split-fp16 products with per-tensor scales,
-    h3), split-bf16 planes on the ring kernel for the forward only or for every product --
-    against the fp32 torch-op oracle (the
+    split engine (six split-bf16 products, x6; three split-fp16 products with per-tensor scales,
+    h3; three fp16-plane products with 32x32 block exponents, h3p) -- against the fp32 torch-op oracle (the
     reference module graph, bert_modeling.py:819-888).  Loss to 1e-5 relative; every parameter's
     gradient within 1e-4 of the oracle's largest gradient entry of that parameter."""
     from hetseq_amd.models.bert import BertConfig, BertForPreTraining
@@ -304,7 +288,6 @@ def test_bert_base_shape_matches_reference_1e4(cuda, monkeypatch, planes, engine
     from hetseq_amd.runtime.flat import FlatParamStore
 
     G.set_fp32_mode(engine)  # (conftest restores the default after the test)
-    monkeypatch.setattr(G, "_PLANES", planes)
     torch.manual_seed(0)
     cfg = BertConfig(vocab_size_or_config_json_file=30522)
     model = BertForPreTraining(cfg).to(cuda)
@@ -313,7 +296,6 @@ def test_bert_base_shape_matches_reference_1e4(cuda, monkeypatch, planes, engine
     ref = copy.deepcopy(model)
     store = FlatParamStore(model)
     model.attach_store(store, torch.float32)
-    assert (store.planes is not None) == (planes != "off")
     batch = _batch(cuda, 8, 128, cfg.vocab_size, P=20)
     assert model.bert._can_fuse(batch[0])
     l1 = model(*batch)
@@ -326,9 +308,12 @@ def test_bert_base_shape_matches_reference_1e4(cuda, monkeypatch, planes, engine
     l1.backward()
     assert abs(l1.item() - l2.item()) <= 1e-5 * abs(l2.item()), (l1.item(), l2.item())
     worst, where = _grad_report(model, ref)
-    print("bert-base fused vs oracle (engine=%s planes=%s): loss %.8g vs %.8g, worst grad rel %.3g at %s"
-          % (engine, planes, l1.item(), l2.item(), worst, where))
+    rworst, rwhere = _row_grad_report(model, ref)
+    print("bert-base fused vs oracle (engine=%s): loss %.8g vs %.8g, worst grad rel %.3g at %s, "
+          "worst per-row rel %.3g at %s" % (engine, l1.item(), l2.item(), worst, where, rworst, rwhere))
     assert worst <= 1e-4, (worst, where)
+    if engine == "h3p":
+        assert rworst <= 1e-3, (rworst, rwhere)
 
 
 @pytest.mark.parametrize("engine", ["x6", "h3", "h3p"])
@@ -377,6 +362,56 @@ def test_trajectory_200_updates_tracks_reference(cuda, monkeypatch, engine):
         worst = max(worst, rel)
         assert rel <= 1e-4, (step, l1.item(), l2.item())
     print("200-update trajectory (%s): worst loss rel diff %.3g" % (engine, worst))
+
+
+@pytest.mark.parametrize("engine", ["h3", "h3p"])
+def test_bert_base_trajectory_50_updates(cuda, engine):
+    """BERT-base (H 768, L 12, S 128, B 8) for 50 Adam updates, fused (flat store, fused Adam, the
+    given fp32 product engine) vs the fp32 torch-op oracle with the reference Adam math, identical
+    batches, dropout off: the loss curves stay within 1e-4 relative at every update."""
+    from argparse import Namespace
+
+    from hetseq_amd.models.bert import BertConfig, BertForPreTraining
+    from hetseq_amd.ops import gemm as G
+    from hetseq_amd.optim.optimizers import AdamReference, _Adam
+    from hetseq_amd.runtime.flat import FlatParamStore
+
+    G.set_fp32_mode(engine)
+    torch.manual_seed(0)
+    cfg = BertConfig(vocab_size_or_config_json_file=30522)
+    model = BertForPreTraining(cfg).to(cuda)
+    model.eval()
+    model.max_predictions_per_seq = 20
+    ref = copy.deepcopy(model)
+    store = FlatParamStore(model)
+    model.attach_store(store, torch.float32)
+    opt = _Adam(Namespace(lr=[1e-4], adam_betas="(0.9,0.999)", adam_eps=1e-8, weight_decay=0.01),
+                list(model.parameters()), store)
+    ropt = AdamReference(ref.parameters(), lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01)
+    batches = []
+    for i in range(4):
+        b = _batch(cuda, 8, 128, cfg.vocab_size, P=20)
+        torch.manual_seed(200 + i)
+        batches.append((torch.randint(0, cfg.vocab_size, b[0].shape, device=cuda),) + b[1:])
+    worst = 0.0
+    for step in range(50):
+        b = batches[step % 4]
+        opt.zero_grad()
+        l1 = model(*b)
+        l1.backward()
+        opt.step()
+        ropt.zero_grad()
+        os.environ["HETSEQ_DISABLE_FUSED"] = "1"
+        try:
+            l2 = ref(*b)
+            l2.backward()
+        finally:
+            del os.environ["HETSEQ_DISABLE_FUSED"]
+        ropt.step()
+        rel = abs(l1.item() - l2.item()) / abs(l2.item())
+        worst = max(worst, rel)
+        assert rel <= 1e-4, (step, l1.item(), l2.item())
+    print("BERT-base 50-update trajectory (%s): worst loss rel diff %.3g" % (engine, worst))
 
 
 def test_lamb_hip_step_matches_cpu_math(cuda):

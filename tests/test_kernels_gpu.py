@@ -1328,62 +1328,34 @@ def test_pretraining_heads_launch_no_torch_kernels(cuda):
     assert not bad, bad
 
 
-def test_split_planes_exact(cuda):
-    """fp32 -> hi/mid/lo bf16 planes: each plane is the RNE bf16 of the remaining residual, and
-    hi + mid + lo reproduces x to 2^-24 relative (gemm_planes.hip)."""
-    from hetseq_amd.ops import gemm as G
-
-    torch.manual_seed(60)
-    x = torch.randn(300, 512, device=cuda) * torch.logspace(-20, 20, 512, base=2.0, device=cuda)
-    pl = G.split(x)
-    hi = x.bfloat16()
-    mid = (x - hi.float()).bfloat16()
-    lo = (x - hi.float() - mid.float()).bfloat16()
-    assert torch.equal(pl.buf[0], hi) and torch.equal(pl.buf[1], mid) and torch.equal(pl.buf[2], lo)
-    back = pl.unsplit()
-    assert ((back - x).abs() <= x.abs() * 2.0 ** -24).all()
-
-
 def _planes_operand(x, P):
     from hetseq_amd.ops import gemm as G
 
-    return G.split(x.contiguous()) if P == 3 else G.Planes.of_bf16(x.bfloat16().contiguous())
+    assert P == 1  # (the split-bf16 P = 3 engine was retired for h3p)
+    return G.Planes.of_bf16(x.bfloat16().contiguous())
 
 
 @pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
-@pytest.mark.parametrize("P", [3, 1])
 @pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False)])
 @pytest.mark.parametrize("M,N,K,ks", [(256, 384, 512, 1), (640, 768, 768, 1), (384, 256, 1024, 4),
                                       (128, 128, 4096, 2)])
-def test_gemm_planes_vs_fp64(cuda, P, ta, tb, M, N, K, ks, variant):
-    """The bf16-plane engine in both layouts of each operand (k-contiguous b128 reads and
-    mn-contiguous transposed reads) and with split-K, against fp64.  P = 3 (fp32 as split bf16)
-    must carry fp32-level error: within 2x of torch's own fp32 GEMM error; P = 1 is exact bf16
+def test_gemm_planes_vs_fp64(cuda, ta, tb, M, N, K, ks, variant):
+    """The bf16 plane engine in both layouts of each operand (k-contiguous b128 reads and
+    mn-contiguous transposed reads) and with split-K, against fp64 of the bf16 operands: exact bf16
     products with fp32 accumulation."""
     from hetseq_amd.ops import gemm as G
 
     torch.manual_seed(61 + M + N + K)
     a = torch.randn((K, M) if ta else (M, K), device=cuda)
     b = torch.randn((N, K) if tb else (K, N), device=cuda)
-    pa, pb = _planes_operand(a, P), _planes_operand(b, P)
+    pa, pb = _planes_operand(a, 1), _planes_operand(b, 1)
     out = torch.empty(M, N, device=cuda)
-    from hetseq_amd.ops._C import hip
-
-    hip().set_planes_variant(variant)  # (0 two LDS stages, 1 one stage, 2 half K depth)
-    try:
-        assert G.gemm_planes(pa, pb, ta, tb, out, ksplit=ks)
-    finally:
-        hip().set_planes_variant(0)
-    ad, bd = (a.double(), b.double()) if P == 3 else (a.bfloat16().double(), b.bfloat16().double())
+    assert G.gemm_planes(pa, pb, ta, tb, out, ksplit=ks, variant=variant)
+    ad, bd = a.bfloat16().double(), b.bfloat16().double()
     ref = (ad.t() if ta else ad) @ (bd.t() if tb else bd)
     mag = (ad.abs().t() if ta else ad.abs()) @ (bd.abs().t() if tb else bd.abs())
-    err = float(((out.double() - ref).abs() / mag).max())  # in units of |A|@|B| (test_gemm_x6_error_...)
-    if P == 3:
-        f32 = (a.t() if ta else a) @ (b.t() if tb else b)
-        e32 = float(((f32.double() - ref).abs() / mag).max())
-        assert err <= 2.0 * e32 and err < 5e-7, (err, e32)
-    else:
-        assert err < 1e-5, err
+    err = float(((out.double() - ref).abs() / mag).max())  # in units of |A|@|B|
+    assert err < 1e-5, err
 
 
 @pytest.mark.parametrize("ks", [2, 4])
@@ -1406,7 +1378,7 @@ def test_gemm_planes_bf16_splitk(cuda, ks, epi_bias, beta):
     _close(y, ref, 1e-2, 1e-2, "bf16 split-K planes")
 
 
-@pytest.mark.parametrize("P", [3, 1])
+@pytest.mark.parametrize("P", [1])
 def test_gemm_planes_epilogues(cuda, P):
     """bias, beta-accumulate, GELU (pre-activation kept) and dGELU + bias-gradient column sums."""
     from hetseq_amd.models.bert import f_gelu
@@ -1443,94 +1415,6 @@ def test_gemm_planes_epilogues(cuda, P):
     f_gelu(pk + bk.double()).backward(dyd @ w2d)
     _close(dpre, pk.grad, tol, tol, "planes dgelu")
     _close(db, pk.grad.sum(0), tol, tol, "planes dgelu colsum")
-
-
-# ------------------------------------------------------------------ ring plane kernel (gemm_ring.hip)
-def _ring_err(a, b, ta, tb, out):
-    ad, bd = a.double(), b.double()
-    At, Bt = (ad.t() if ta else ad), (bd.t() if tb else bd)
-    ref = At @ Bt
-    mag = At.abs() @ Bt.abs()
-    f32 = (a.t() if ta else a) @ (b.t() if tb else b)
-    return float(((out.double() - ref).abs() / mag).max()), float(((f32.double() - ref).abs() / mag).max())
-
-
-@pytest.mark.parametrize("bn", [96, 128])
-@pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False)])
-@pytest.mark.parametrize("M,N,K,ks", [(256, 384, 512, 1), (128, 768, 96, 1), (384, 768, 1024, 4), (256, 384, 2048, 2),
-                                      (128, 384, 32, 1), (128, 384, 64, 1)])
-def test_gemm_ring_vs_fp64(cuda, bn, ta, tb, M, N, K, ks):
-    """Ring kernel, every operand layout (k-contiguous b128 images, mn-contiguous transposed
-    images), both tile widths, K of 1..64 tiles (prologue / odd tile counts) and split-K:
-    fp32-level error, within 2x of torch's own fp32 GEMM against fp64."""
-    from hetseq_amd.ops import gemm as G
-
-    torch.manual_seed(70 + M + N + K + bn)
-    a = torch.randn((K, M) if ta else (M, K), device=cuda)
-    b = torch.randn((N, K) if tb else (K, N), device=cuda)
-    out = torch.full((M, N), float("nan"), device=cuda)
-    assert G.gemm_planes(G.split(a.contiguous()), G.split(b.contiguous()), ta, tb, out, ksplit=ks,
-                         variant=G.RING, ring_bn=bn)
-    err, e32 = _ring_err(a, b, ta, tb, out)
-    assert err <= 2.0 * e32 and err < 5e-7, (err, e32)
-
-
-@pytest.mark.parametrize("ta,tb,M,N,K", [(0, 1, 4096, 2304, 768), (0, 1, 4096, 768, 768), (0, 1, 4096, 3072, 768),
-                                         (0, 0, 4096, 768, 3072), (0, 0, 4096, 768, 2304),
-                                         (1, 0, 768, 3072, 4096), (1, 0, 2304, 768, 4096)])
-def test_gemm_ring_bert_shapes(cuda, ta, tb, M, N, K):
-    """The BERT-base products on the ring kernel (the launcher's own tile and the K split of
-    the step): fp32-level error against fp64."""
-    from hetseq_amd.ops import gemm as G
-
-    torch.manual_seed(77)
-    a = torch.rand((K, M) if ta else (M, K), device=cuda) * 2 - 1
-    b = torch.rand((N, K) if tb else (K, N), device=cuda) * 2 - 1
-    out = torch.empty(M, N, device=cuda)
-    ks = G.ring_ksplit(M, N, K, bool(ta)) if ta else 1
-    assert G.gemm_planes(G.split(a), G.split(b), bool(ta), bool(tb), out, ksplit=ks, variant=G.RING)
-    err, e32 = _ring_err(a, b, ta, tb, out)
-    assert err <= 2.0 * e32 and err < 5e-7, (err, e32)
-
-
-def test_gemm_ring_epilogues_and_plane_output(cuda):
-    """bias, beta-accumulate, GELU (pre-activation kept, output planes) and dGELU + bias-gradient
-    column sums (output planes) on the ring kernel; the plane output equals split(C) bit for bit."""
-    from hetseq_amd.models.bert import f_gelu
-    from hetseq_amd.ops import gemm as G
-
-    torch.manual_seed(78)
-    T, K, N = 256, 512, 384
-    x, w, bias = torch.randn(T, K, device=cuda), torch.randn(N, K, device=cuda) * 0.05, torch.randn(N, device=cuda)
-    px, pw = G.split(x), G.split(w)
-    xd, wd = x.double(), w.double()
-    y = torch.empty(T, N, device=cuda)
-    assert G.gemm_planes(px, pw, False, True, y, bias, G.EPI_BIAS, variant=G.RING)
-    _close(y, xd @ wd.t() + bias.double(), 1e-5, 1e-5, "ring bias")
-    c0 = torch.randn(T, N, device=cuda)
-    c = c0.clone()
-    assert G.gemm_planes(px, pw, False, True, c, bias, G.EPI_BIAS, beta=1.0, variant=G.RING)
-    _close(c, xd @ wd.t() + bias.double() + c0.double(), 1e-5, 1e-5, "ring beta")
-    pre = torch.empty(T, N, device=cuda)
-    yp = torch.empty((3, T, N), dtype=torch.bfloat16, device=cuda)
-    assert G.gemm_planes(px, pw, False, True, y, bias, G.EPI_GELU, aux=pre, variant=G.RING, outp=yp)
-    _close(pre, xd @ wd.t(), 1e-5, 1e-5, "ring gelu pre")
-    _close(y, f_gelu(pre.double() + bias.double()), 1e-5, 1e-5, "ring gelu")
-    assert torch.equal(yp, G.split(y).buf.view(3, T, N))
-    dy = torch.randn(T, N, device=cuda)
-    w2 = torch.randn(N, K, device=cuda) * 0.05
-    prek, bk = torch.randn(T, K, device=cuda), torch.randn(K, device=cuda)
-    dpre = torch.empty(T, K, device=cuda)
-    dp = torch.empty((3, T, K), dtype=torch.bfloat16, device=cuda)
-    part = torch.empty((T // 128, K), device=cuda)
-    db = torch.empty(K, device=cuda)
-    assert G.gemm_planes(G.split(dy), G.split(w2), False, False, dpre, bk, G.EPI_DGELU, aux=prek, part=part,
-                         colsum=db, variant=G.RING, outp=dp)
-    pk = prek.double().requires_grad_()
-    f_gelu(pk + bk.double()).backward(dy.double() @ w2.double())
-    _close(dpre, pk.grad, 1e-5, 1e-5, "ring dgelu")
-    _close(db, pk.grad.sum(0), 1e-5, 1e-5, "ring dgelu colsum")
-    assert torch.equal(dp, G.split(dpre).buf.view(3, T, K))
 
 
 def test_fast_stat_kernels_match_torch_ops(cuda):

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-kernel summary of rocprofv3 counter databases (rocpd sqlite, ROCm 7.x).
 
-    python tools/pmc_summary.py gpurun_out/pmc_a/run_results.db [more.db ...] [--match gemm_ring] [--top 20]
+    python tools/pmc_summary.py gpurun_out/pmc_a/run_results.db [more.db ...] [--match gemm_h3p] [--top 20]
 
 Counters of several single-pass runs of the same program are joined by kernel name (each pass is
 its own run: rocprofv3 does not split counters over passes).  Per kernel: dispatches, mean
