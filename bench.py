@@ -456,12 +456,6 @@ def _set_emul_busbw(gbs):
     _EMUL["comm"].set_emulation(_EMUL["world"], _EMUL["channels"], gbs, _EMUL["latency_us"])
 
 
-def _set_attn(code):
-    from hetseq_amd.ops._C import hip
-
-    hip().set_attn_bwd_x6_planes(code)
-
-
 def _set_ln_partials(on):
     from hetseq_amd.ops import bert_ops
 
@@ -539,13 +533,6 @@ _AB = {
     "wks2s2": lambda: _set_side_ks(2, 2),
     "wks1": lambda: _set_side_ks(1, 1),  # no split-K (no reduce pass, fewer longer blocks)
     "wks1s4": lambda: _set_side_ks(1, 4),
-    "attn_k": lambda: _set_attn(2),    # key-block fp32 attention backward (S <= 128)
-    "attn_c": lambda: _set_attn(4),    # the key-block kernel in one 4-wave group (co-resides with a GEMM block)
-    "attn_p": lambda: _set_attn(1),    # plane-image dQ / dKV pair
-    "afwd_p": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_fwd_x6_planes(1),
-    "afwd_old": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_fwd_x6_planes(0),
-    "dsum_in": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_bwd_fused_d(1),
-    "dsum_sep": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_bwd_fused_d(0),
     "lnp_on": lambda: _set_ln_partials(True),    # FFN-out split-K partials summed in the LN forward
     "lnp_off": lambda: _set_ln_partials(False),  # ... or reduced by the GEMM's own pass
     "lnb_chunk": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_ln_bwd_lds(1),  # 3 KB LDS
@@ -588,12 +575,6 @@ _AB = {
     "sideks_2": lambda: setattr(__import__("hetseq_amd.runtime.streams", fromlist=["x"]), "SIDE_KSPLIT", 2),
     "sideks_1": lambda: setattr(__import__("hetseq_amd.runtime.streams", fromlist=["x"]), "SIDE_KSPLIT", 1),
     "sideks_4": lambda: setattr(__import__("hetseq_amd.runtime.streams", fromlist=["x"]), "SIDE_KSPLIT", 4),
-    # split-K finished by the last-arriving slice inside the GEMM launch (gemm.hip splitk_inlaunch)
-    "inl_on": lambda: setattr(__import__("hetseq_amd.ops.gemm", fromlist=["x"]), "_INLAUNCH", True),
-    "inl_wt": lambda: (setattr(__import__("hetseq_amd.ops.gemm", fromlist=["x"]), "_INLAUNCH", True),
-                       __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_splitk_wt(1)),
-    "inl_rel": lambda: (setattr(__import__("hetseq_amd.ops.gemm", fromlist=["x"]), "_INLAUNCH", True),
-                        __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_splitk_wt(0)),
     "ffnbias_wgrad": lambda: setattr(__import__("hetseq_amd.ops.bert_ops", fromlist=["x"]), "_FFN_BIAS_WGRAD", True),
     "ffnbias_dgelu": lambda: setattr(__import__("hetseq_amd.ops.bert_ops", fromlist=["x"]), "_FFN_BIAS_WGRAD", False),
     "wcolfold_on": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_wcol_fold(1),
@@ -609,11 +590,8 @@ _AB = {
     "fwdks_2": lambda: setattr(__import__("hetseq_amd.ops.bert_ops", fromlist=["x"]), "_FWD_KS", 2),
     "poolw_side": lambda: setattr(__import__("hetseq_amd.ops.bert_ops", fromlist=["x"]), "_POOL_WGRAD_SIDE", True),
     "poolw_inline": lambda: setattr(__import__("hetseq_amd.ops.bert_ops", fromlist=["x"]), "_POOL_WGRAD_SIDE", False),
-    "inl_off": lambda: setattr(__import__("hetseq_amd.ops.gemm", fromlist=["x"]), "_INLAUNCH", False),
     "lazyzero_on": lambda: setattr(__import__("hetseq_amd.controller", fromlist=["x"]), "_LAZY_ZERO", True),
     "lazyzero_off": lambda: setattr(__import__("hetseq_amd.controller", fromlist=["x"]), "_LAZY_ZERO", False),
-    "h3_dma_on": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_h3_dma(1),
-    "h3_dma_off": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_h3_dma(0),
     # fp32 product engine of the encoder layers: h3p (pre-split block-scaled planes) / h3 (in-kernel split)
     "eng_h3p": lambda: __import__("hetseq_amd.ops.gemm", fromlist=["x"]).set_fp32_mode("h3p"),
     "eng_h3": lambda: __import__("hetseq_amd.ops.gemm", fromlist=["x"]).set_fp32_mode("h3"),

@@ -629,7 +629,7 @@ int launch_attn_fwd_x6(const float* qkv, const int64_t* mask, const float* bqkv,
 
 int launch_attn_bwd_x6(const float* qkv, const int64_t* mask, const float* bqkv, const float* ctx, const float* dctx,
                        const float* lse, float* Dbuf, float* dqkv, const uint32_t* dmask, int B, int S, int NH,
-                       int D, float p, bool fused, hipStream_t st);
+                       int D, float p, hipStream_t st);
 
 int launch_attn_fwd_h3(const float* qkv, const int64_t* mask, const float* bqkv, float* ctx, float* lse,
                        uint32_t* dmask, int B, int S, int NH, int D, float p, uint64_t seed, uint64_t off,
@@ -709,7 +709,7 @@ int launch_attn_bwd(int dtype, const void* qkv, const int64_t* mask, const float
   }
   if (dtype == 0 && g_attn_fp32_x6)  // fp32 as split-bf16 products (attention_x6.hip)
     return launch_attn_bwd_x6((const float*)qkv, mask, bqkv, (const float*)ctx, (const float*)dctx, lse, Dbuf,
-                              (float*)dqkv, dmask, B, S, NH, D, p, fused_bwd_enabled(), st);
+                              (float*)dqkv, dmask, B, S, NH, D, p, st);
   if (S <= 128 && fused_bwd_enabled()) {  // one block per (batch, head): 5 products instead of 7
     if (dtype != 0 && bf16_mfma_enabled())
       return launch_attn_bwd_fused_bf16(qkv, mask, bqkv, ctx, dctx, lse, dqkv, dmask, B, S, NH, D, p, st);

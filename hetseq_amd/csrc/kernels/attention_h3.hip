@@ -275,60 +275,6 @@ HS_DEVICE void chunk_put(const Chunk& c, char* img0, char* img1, int n, int e0, 
   }
 }
 
-// ---- S > 128: the next chunk's rows arrive in LDS by DMA under the current chunk's MFMAs ----
-// A raw fp32 chunk image: two operands x 64 rows x 256 B (32 KB), written lane-linearly by
-// global_load_lds_dwordx4 (one 1-KB piece = 4 rows per wave instruction, 8 pieces per wave and chunk;
-// no VGPR round trip -- the register prefetch spilled the dK / dV role).  Read back once per chunk by
-// the staging units (row u >> 3, 8 d), which add the bias, scale, take the |max| and split.
-constexpr int kRawOp = 64 * 256;       // one operand's 64 rows
-constexpr int kRaw = 2 * kRawOp;       // 32 KB
-typedef __attribute__((address_space(3))) void lds_void_t;
-
-// one piece: M0 = the wave-uniform LDS destination, set and restored inside the statement (M0 is
-// compiler-reserved); the ordering against the readers is ours (dma_wait + the block barrier)
-HS_DEVICE void dma_piece(const void* gsrc, uint32_t lds_dst) {
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(gsrc), "s"(lds_dst)
-               : "memory");
-}
-HS_DEVICE void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
-// issue the DMA of rows [r0, r0 + 64) of two operands (row strides ld0 / ld1 floats; rows past S re-read
-// row S - 1: their image rows are never consumed) into `raw`
-HS_DEVICE void chunk_dma(char* raw, const float* base0, const float* base1, int64_t ld0, int64_t ld1, int r0, int S) {
-  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void_t*)raw));
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int piece = 8 * w + j, op = piece >> 4;  // pieces 0-15: operand 0, 16-31: operand 1
-    const int row = min(r0 + 4 * (piece & 15) + (lane >> 4), S - 1);
-    const float* src = (op ? base1 + (int64_t)row * ld1 : base0 + (int64_t)row * ld0) + 4 * (lane & 15);
-    dma_piece(src, __builtin_amdgcn_readfirstlane(lds0 + piece * 1024));
-  }
-}
-
-// the staging units' values from the raw image: (x + bias) * scale per operand, rows past n zero
-HS_DEVICE void chunk_from_raw(Chunk& c, const char* raw, int n, const float* bias0, const float* bias1, float scale0) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int u = threadIdx.x + 256 * i, r = u >> 3, c8 = 8 * (u & 7);
-#pragma unroll
-    for (int op = 0; op < 2; ++op) {
-      const float* src = reinterpret_cast<const float*>(raw + op * kRawOp + r * 256) + c8;
-      const float* bias = op ? bias1 : bias0;
-      const float sc = op ? 1.f : scale0;
-      if (r < n) {
-        ld8(src, bias ? bias + c8 : nullptr, sc, c.v[op][i]);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) c.v[op][i][j] = 0.f;
-      }
-    }
-  }
-}
-
 // fixed exponent of P (<= the dropout scale): its largest value below 2^14
 HS_DEVICE int p_exp(float pmax) { return 13 - (pmax >= 2.f ? ilogbf(pmax) : 0); }
 
@@ -352,10 +298,8 @@ HS_DEVICE float ds_scale(const float (&ds)[2][8], int& es, f32x16& a0, f32x16& a
 
 // ---------------------------------------------------------------------------------------------------
 // dK / dV for 32 keys per wave (lane = key) over 64-query chunks of Q (biased, * 1/8) and dO.
-constexpr int kBwdLds = 2 * kIm + 64 * 4 * 2 + 64 * 4 * 4 + 2 * 8 * 4;  // S <= 128 (registers staging)
-constexpr int kBwdLdsDma = kBwdLds + kRaw;                          // S > 128: + the raw DMA image
+constexpr int kBwdLds = 2 * kIm + 64 * 4 * 2 + 64 * 4 * 4 + 2 * 8 * 4;
 
-template <bool DMA>
 HS_DEVICE void dkv_body(char* __restrict__ smem, int bx, int bh, const float* __restrict__ qkv,
                         const int64_t* __restrict__ mask, const float* __restrict__ bqkv,
                         const float* __restrict__ dctx, const float* __restrict__ lse, const float* __restrict__ Dd,
@@ -407,17 +351,11 @@ HS_DEVICE void dkv_body(char* __restrict__ smem, int bx, int bh, const float* __
     }
   };
   const TrBase tb = tr_base(lane);
-  char* const raw = smem + kBwdLds;  // (DMA)
-  if (DMA) chunk_dma(raw, rows + h * kHD, drows + h * kHD, ld, H, 0, S);
   for (int c0 = 0, par = 0; c0 < S; c0 += 64, par ^= 1) {
     const int clen = min(64, S - c0);
-    if (DMA) {  // the chunk's rows landed in the raw image under the previous chunk's MFMAs
-      dma_wait();
-      __syncthreads();
-      chunk_from_raw(cur, raw, clen, bofs(bqkv, h * kHD), nullptr, 0.125f);
-    } else {
-      load(c0);  // (S <= 128: loaded here -- a register prefetch under the previous chunk would spill)
-    }
+    // loaded here: a register prefetch under the previous chunk spills, and an LDS-DMA prefetch
+    // (round 4) measured no faster -- its extra barrier per chunk cost what the hidden latency saved
+    load(c0);
     chunk_max(cur, red + 8 * par);
     __syncthreads();  // the previous chunk's images are free; the chunk's |max| partials visible
     const int eq = red_exp(red + 8 * par, 0), eo = red_exp(red + 8 * par, 1);
@@ -444,8 +382,7 @@ HS_DEVICE void dkv_body(char* __restrict__ smem, int bx, int bh, const float* __
         const int qi = i >> 2, kw = bx * 4 + (i & 3);
         Wd[qi][i & 3] = kw < (S >> 5) ? dmask[((uint64_t)bh * S + c0 + qi) * (uint64_t)(S >> 5) + kw] : 0u;
       }
-    __syncthreads();  // the images are ready and the raw image is consumed
-    if (DMA && c0 + 64 < S) chunk_dma(raw, rows + h * kHD, drows + h * kHD, ld, H, c0 + 64, S);
+    __syncthreads();  // the images are ready
     if (!active) continue;
     if (c0 > 0) {  // accumulators to this chunk's image scales (exact)
       const float fq = ldexpf(1.f, eq - eq_run), fo = ldexpf(1.f, eo - eo_run);
@@ -532,7 +469,6 @@ HS_DEVICE void dkv_body(char* __restrict__ smem, int bx, int bh, const float* __
 
 // dQ for 32 queries per wave (lane = query) over 64-key chunks of K / V (biased); D from Dd or, with ctx
 // (S <= 128), rowsum(dO o O) computed here.
-template <bool DMA>
 HS_DEVICE void dq_body(char* __restrict__ smem, int bx, int bh, const float* __restrict__ qkv,
                        const int64_t* __restrict__ mask, const float* __restrict__ bqkv,
                        const float* __restrict__ dctx, const float* __restrict__ lse, const float* __restrict__ Dd,
@@ -581,24 +517,15 @@ HS_DEVICE void dq_body(char* __restrict__ smem, int bx, int bh, const float* __r
                bofs(bqkv, 2 * H + h * kHD), 1.f);
   };
   const TrBase tb = tr_base(lane);
-  char* const raw = smem + kBwdLds;  // (DMA)
-  if (DMA) chunk_dma(raw, rows + H + h * kHD, rows + 2 * H + h * kHD, ld, ld, 0, S);
   for (int c0 = 0, par = 0; c0 < S; c0 += 64, par ^= 1) {
     const int clen = min(64, S - c0);
-    if (DMA) {
-      dma_wait();
-      __syncthreads();
-      chunk_from_raw(cur, raw, clen, bofs(bqkv, H + h * kHD), bofs(bqkv, 2 * H + h * kHD), 1.f);
-    } else {
-      load(c0);
-    }
+    load(c0);
     chunk_max(cur, red + 8 * par);
     __syncthreads();
     const int ek = red_exp(red + 8 * par, 0), ev = red_exp(red + 8 * par, 1);
     chunk_put(cur, Kp, Vp, clen, ek, ev);
     for (int i = tid; i < clen; i += 256) Ms[i] = (1.f - (float)mask[(int64_t)b * S + c0 + i]) * -10000.f;
     __syncthreads();
-    if (DMA && c0 + 64 < S) chunk_dma(raw, rows + H + h * kHD, rows + 2 * H + h * kHD, ld, ld, c0 + 64, S);
     if (!active) continue;
     if (c0 > 0) {
       const float fk = ldexpf(1.f, ek - ek_run);
@@ -657,22 +584,18 @@ HS_DEVICE void dq_body(char* __restrict__ smem, int bx, int bh, const float* __r
 // The backward's two roles in one launch (grid (B*NH, 2 * ceil(S/128)); dK / dV blocks first: the longer
 // role goes out first and the dQ blocks fill the tail of the last round).  ctx != nullptr: D computed by
 // the roles themselves (S <= 128).
-// DMA (S > 128, D precomputed: ctx == nullptr): the next chunk's rows arrive by LDS-DMA under the
-// current chunk's MFMAs (66 KB of LDS, two blocks per CU).
-template <bool DMA>
 __global__ void __launch_bounds__(256, 2)
     attn_bwd_h3_kernel(const float* __restrict__ qkv, const int64_t* __restrict__ mask,
                        const float* __restrict__ bqkv, const float* __restrict__ dctx, const float* __restrict__ lse,
                        const float* __restrict__ Dd, float* __restrict__ dqkv, int S, int NH, float p,
                        const uint32_t* __restrict__ dmask, const float* __restrict__ ctx, float* __restrict__ amax,
                        AttnPl po) {
-  __shared__ __attribute__((aligned(16))) char smem[DMA ? kBwdLdsDma : kBwdLds];
+  __shared__ __attribute__((aligned(16))) char smem[kBwdLds];
   const int nq = (S + 127) / 128, bh = blockIdx.x, y = blockIdx.y;
   if (y < nq)
-    dkv_body<DMA>(smem, y, bh, qkv, mask, bqkv, dctx, lse, Dd, dqkv, S, NH, p, dmask, DMA ? nullptr : ctx, amax, po);
+    dkv_body(smem, y, bh, qkv, mask, bqkv, dctx, lse, Dd, dqkv, S, NH, p, dmask, ctx, amax, po);
   else
-    dq_body<DMA>(smem, y - nq, bh, qkv, mask, bqkv, dctx, lse, Dd, dqkv, S, NH, p, dmask, DMA ? nullptr : ctx, amax,
-                 po);
+    dq_body(smem, y - nq, bh, qkv, mask, bqkv, dctx, lse, Dd, dqkv, S, NH, p, dmask, ctx, amax, po);
 }
 
 // Forward: a wave owns 32 queries (lane = query), S^T tiles with the key on the registers, online softmax;
@@ -813,17 +736,6 @@ int launch_attn_fwd_h3(const float* qkv, const int64_t* mask, const float* bqkv,
   return 0;
 }
 
-// S > 128 backward: the chunk's rows loaded at its start (default) or prefetched by LDS-DMA under the
-// previous chunk (HETSEQ_ATTN_H3_DMA=1; set_attn_h3_dma).  The DMA variant measured no faster -- seq 512
-// backward 140.1 vs 134.7 us alone, phase-2 step 13.67 vs 13.63 ms (interleaved A/B): its extra barrier
-// per chunk costs what the hidden load latency saves (the kernel is bound by its exp / split VALU and
-// MFMA issue, not by the staging loads).
-static int g_bwd_dma = [] {
-  const char* e = std::getenv("HETSEQ_ATTN_H3_DMA");
-  return e && e[0] == '1' ? 1 : 0;
-}();
-void set_attn_h3_dma(int on) { g_bwd_dma = on; }
-
 int launch_attn_bwd_h3(const float* qkv, const int64_t* mask, const float* bqkv, const float* ctx, const float* dctx,
                        const float* lse, float* Dbuf, float* dqkv, const uint32_t* dmask, int B, int S, int NH, int D,
                        float p, hipStream_t st, float* amax, void* pl, int64_t ps, int8_t* ex) {
@@ -835,14 +747,7 @@ int launch_attn_bwd_h3(const float* qkv, const int64_t* mask, const float* bqkv,
     launch_attn_bwd_dsum(ctx, dctx, Dbuf, B, S, NH, st);
   }
   const dim3 grid(B * NH, 2 * ((S + 127) / 128));
-  if (fused_d)
-    hipLaunchKernelGGL(attn_bwd_h3_kernel<false>, grid, dim3(256), 0, st, qkv, mask, bqkv, dctx, lse, Dbuf, dqkv, S, NH,
-                       p, dmask, ctx, amax, po);
-  else if (g_bwd_dma)
-    hipLaunchKernelGGL(attn_bwd_h3_kernel<true>, grid, dim3(256), 0, st, qkv, mask, bqkv, dctx, lse, Dbuf, dqkv, S, NH,
-                       p, dmask, nullptr, amax, po);
-  else
-    hipLaunchKernelGGL(attn_bwd_h3_kernel<false>, grid, dim3(256), 0, st, qkv, mask, bqkv, dctx, lse, Dbuf, dqkv, S, NH,
-                       p, dmask, nullptr, amax, po);
+  hipLaunchKernelGGL(attn_bwd_h3_kernel, grid, dim3(256), 0, st, qkv, mask, bqkv, dctx, lse, Dbuf, dqkv, S, NH, p,
+                     dmask, fused_d ? ctx : nullptr, amax, po);
   return 0;
 }

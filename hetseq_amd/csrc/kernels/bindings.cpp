@@ -76,11 +76,6 @@ void launch_pool_nsp_wgrad(int, const void*, const float*, const float*, const f
                            float*, float*, int, hipStream_t);
 // attention.hip
 void set_attn_fp32_mode(int mode);
-void set_attn_bwd_x6_planes(int on);
-void set_attn_timing(uint64_t* buf);
-void set_attn_bwd_fused_d(int on);
-void set_attn_fwd_x6_planes(int on);
-void set_attn_h3_dma(int on);
 void set_ln_bwd_lds(int chunked);
 int attn_fp32_mode();
 int launch_attn_fwd(int, const void*, const int64_t*, const float*, void*, float*, uint32_t*, int, int, int, int, float,
@@ -98,9 +93,7 @@ int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, i
                 int64_t ldb, void* C, int64_t ldc, const float* bias, int epi, float beta, float* aux, int64_t ldaux,
                 float* part, float* colsum_out, int colsum_acc, int tile_override, hipStream_t st, int ksplit,
                 float* slab, int64_t slab_floats, int mv, int nv, int kv, const float* amax_a, int namax_a,
-                const float* amax_b, int namax_b, float* amax_c, int* tickets);
-int splitk_tickets();
-void set_splitk_wt(int on);
+                const float* amax_b, int namax_b, float* amax_c);
 void set_wcol_fold(int on);
 
 // gemm_planes.hip
@@ -557,19 +550,9 @@ PYBIND11_MODULE(_hip, m) {
      "must be zeroed");
 
   m.def("set_attn_fp32_mode", &set_attn_fp32_mode, "fp32 attention products: 2 split-fp16 (h3), 1 split-bf16 (x6), 0 exact-fp32 MFMA");
-  m.def("set_attn_bwd_x6_planes", &set_attn_bwd_x6_planes,
-        "fp32 split-bf16 attention backward: 2 key-block kernel (S <= 128) / plane-image pair, 1 plane-image dQ / dKV "
-        "pair, 0 fused / gather kernels, -1 the HETSEQ_ATTN_BWD_X6 default");
   m.def("attn_fp32_mode", &attn_fp32_mode);
-  m.def("set_attn_bwd_fused_d", &set_attn_bwd_fused_d,
-        "fp32 plane-pair attention backward: 1 = D = rowsum(dO o O) inside the kernel (S <= 128), 0 = separate pass");
   m.def("set_ln_bwd_lds", &set_ln_bwd_lds,
         "LN backward column partials: 1 = through a 3 KB LDS window (default), 0 = the [waves][H] LDS image");
-  m.def("set_attn_h3_dma", &set_attn_h3_dma, "h3 attention backward, S > 128: 1 next-chunk rows by LDS-DMA, 0 loads");
-  m.def("set_attn_fwd_x6_planes", &set_attn_fwd_x6_planes,
-        "fp32 attention forward: 1 = plane-image kernel (default), 0 = the first x6 forward");
-  m.def("set_attn_timing", [](i64 buf) { set_attn_timing(P(uint64_t*, buf)); },
-        "diagnostic: buffer of 16 uint64 per block for the key-block backward's phase clock stamps (0 = off)");
   // amax: optional |max| slot of the output (ctx / dqkv); returns 1 when the kernel wrote it (h3 engine)
   m.def("attn_fwd", [](int dt, i64 qkv, i64 mask, i64 bqkv, i64 ctx, i64 lse, i64 dmask, int B, int S, int NH, int D,
                        float p, u64 seed, u64 off, i64 st, int bh0, i64 amax) {
@@ -660,13 +643,13 @@ PYBIND11_MODULE(_hip, m) {
   m.def("gemm", [](int dt, int ta, int tb, int M, int N, int K, i64 A, i64 lda, i64 B, i64 ldb, i64 C, i64 ldc, i64 bias,
                    int epi, float beta, i64 aux, i64 ldaux, i64 part, i64 colsum, int colsum_acc, i64 st,
                    int tile, int ksplit, i64 slab, i64 slab_floats, int mv, int nv, int kv, i64 amax_a, int namax_a,
-                   i64 amax_b, int namax_b, i64 amax_c, i64 tickets) {
+                   i64 amax_b, int namax_b, i64 amax_c) {
     pre_launch("gemm");
     const int rc = launch_gemm(dt, ta, tb, M, N, K, P(const void*, A), lda, P(const void*, B), ldb, P(void*, C), ldc,
                                P(const float*, bias), epi, beta, P(float*, aux), ldaux, P(float*, part),
                                P(float*, colsum), colsum_acc, tile, ST(st), ksplit, P(float*, slab), slab_floats, mv, nv,
                                kv, P(const float*, amax_a), namax_a, P(const float*, amax_b), namax_b,
-                               P(float*, amax_c), P(int*, tickets));
+                               P(float*, amax_c));
     if (rc == 0) check_launch("gemm");
     return rc;
   }, pybind11::arg("dt"), pybind11::arg("ta"), pybind11::arg("tb"), pybind11::arg("M"), pybind11::arg("N"),
@@ -676,9 +659,6 @@ PYBIND11_MODULE(_hip, m) {
      pybind11::arg("colsum_acc"), pybind11::arg("st"), pybind11::arg("tile") = -1, pybind11::arg("ksplit") = 0,
      pybind11::arg("slab") = 0, pybind11::arg("slab_floats") = 0, pybind11::arg("mv") = 0, pybind11::arg("nv") = 0,
      pybind11::arg("kv") = 0, pybind11::arg("amax_a") = 0, pybind11::arg("namax_a") = 0, pybind11::arg("amax_b") = 0,
-     pybind11::arg("namax_b") = 0, pybind11::arg("amax_c") = 0, pybind11::arg("tickets") = 0);
+     pybind11::arg("namax_b") = 0, pybind11::arg("amax_c") = 0);
   m.def("set_wcol_fold", &set_wcol_fold, "weight-gradient bias sums finished by the split-K pass (1) or reduce_rows (0)");
-  m.def("set_splitk_wt", &set_splitk_wt, "in-launch split-K slabs: 1 write-through stores, 0 plain + release fence");
-  m.def("splitk_tickets", &splitk_tickets,
-        "arrival counters a stream's in-launch split-K GEMMs need (an int32 buffer, zeroed once)");
 }

@@ -88,13 +88,6 @@ struct GemmArgs {
   const float* amax_b;
   int namax_a, namax_b;
   float* amax_c;  // GELU / dGELU epilogues: |max| of the written C (atomic max), the next product's operand
-  // in-launch split-K finish (splitk_inlaunch): one arrival counter per tile (zero between launches),
-  // the reduction's bias, and the weight-gradient column sums' destination (wcol)
-  int* tickets;
-  int inl_wt;  // 1: slab stores write through (sc1), no release fence; 0: plain stores + release
-  const float* red_bias;
-  float* colsum_out;
-  int colsum_acc;
 };
 
 // LDS image geometry of one operand (rows = BM or BN).  The [k][mn] image is
@@ -234,122 +227,13 @@ HS_DEVICE f32x16 mma_nt(bfx8 a, bfx8 b, f32x16 c) {
 // (|max| of the values a lane wrote: amax_bits / amax_commit in common.h -- non-negative floats order as
 // their bit patterns; NaN's pattern sorts above inf, so a NaN output reaches the consumer's scale as NaN)
 
-// Split-K finished inside the launch (p.tickets set): every K slice publishes its partial tile
-// in fragment order -- [wave][i][j][register group][lane] float4s, so each store instruction writes
-// 1 KB contiguously -- then takes a ticket on the tile's counter; the block that draws the last one
-// sums the slices in slice order (its own from registers: the same values, so the result is bitwise
-// the separate splitk_reduce pass's) and writes C (+bias) (+beta*C), and, for the weight gradient's
-// first column tile (wcol), the bias gradient from the slices' column partials.  Publication follows
-// the agent-scope release / acquire hand-off: stores drained, one release fence and the ticket from
-// lane 0, an acquire fence in the last arriver before any slab read -- correct for any placement of
-// a tile's slices over the XCDs.  The last arriver resets the counter for the next launch.
-template <int BM, int BN, int MF, bool EDGE>
-HS_DEVICE void splitk_inlaunch(const GemmArgs& p, typename Mf<MF>::acc_t (&acc)[BM / 2 / MF][BN / 2 / MF],
-                               float* smem, int m0, int n0, int slice, int tile, int ntile, int wm, int wn, int lr,
-                               int q) {
-  using M_ = Mf<MF>;
-  constexpr int TM = BM / 2 / MF, TN = BN / 2 / MF, NG = M_::nreg / 4, PER_WAVE = TM * TN * NG * 64;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t tile_floats = (int64_t)blockDim.x * TM * TN * M_::nreg;  // = the tile's elements
-  auto frag = [&](int s) {
-    return reinterpret_cast<float4*>(p.slab + ((int64_t)s * ntile + tile) * tile_floats) + w * PER_WAVE + lane;
-  };
-  if (p.inl_wt) {  // write-through stores: the bytes leave the XCD's L2 with the store, no release fence
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        p.slab + ((int64_t)slice * ntile + tile) * tile_floats, 0, (int)(tile_floats * 4), 0x00020000);
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int g = 0; g < NG; ++g) {
-          typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-          const u32x4 v = {__float_as_uint(acc[i][j][4 * g]), __float_as_uint(acc[i][j][4 * g + 1]),
-                           __float_as_uint(acc[i][j][4 * g + 2]), __float_as_uint(acc[i][j][4 * g + 3])};
-          __builtin_amdgcn_raw_buffer_store_b128(v, rs,
-                                                 (w * PER_WAVE + lane + ((i * TN + j) * NG + g) * 64) * 16, 0, 16);
-        }
-  } else {
-    float4* mine = frag(slice);
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int g = 0; g < NG; ++g)
-          mine[((i * TN + j) * NG + g) * 64] =
-              make_float4(acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slab (and column partial) stores done
-  __syncthreads();
-  int* flag = reinterpret_cast<int*>(smem);  // the K loop's LDS is free: every wave passed the barrier
-  if (threadIdx.x == 0) {
-    if (!p.inl_wt) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the write-back completes before the ticket
-    }
-    const int t = __hip_atomic_fetch_add(p.tickets + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = t == p.ksplit - 1;
-    if (last) {
-      __hip_atomic_store(p.tickets + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    flag[0] = last;
-  }
-  __syncthreads();
-  if (!flag[0]) return;
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wn + MF * j + lr;
-      const float bv = p.red_bias && (!EDGE || n < p.Nv) ? p.red_bias[n] : 0.f;
-#pragma unroll
-      for (int g = 0; g < NG; ++g) {
-        const int o = ((i * TN + j) * NG + g) * 64;
-        float4 a = slice == 0 ? make_float4(acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2],
-                                            acc[i][j][4 * g + 3])
-                              : frag(0)[o];
-        for (int s = 1; s < p.ksplit; ++s) {
-          const float4 b = s == slice ? make_float4(acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2],
-                                                    acc[i][j][4 * g + 3])
-                                      : frag(s)[o];
-          a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
-        }
-        const float v[4] = {a.x, a.y, a.z, a.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int m = m0 + wm + MF * i + M_::row(4 * g + e, q);
-          if (EDGE && m >= p.Mv) continue;
-          float* c = p.C + (int64_t)m * p.ldc + n;
-          float r = v[e];
-          if (p.red_bias) r += bv;
-          if (p.beta != 0.f) r += p.beta * *c;
-          *c = r;
-        }
-      }
-    }
-  if (p.colsum_out && n0 == 0 && threadIdx.x < BM) {  // wcol: the bias gradient, slices in order
-    float t = 0.f;
-    for (int s = 0; s < p.ksplit; ++s) t += p.part[(int64_t)s * p.M + m0 + threadIdx.x];
-    float* o = p.colsum_out + m0 + threadIdx.x;
-    *o = p.colsum_acc ? *o + t : t;
-  }
-}
-
 // Shared GEMM epilogue (both kernels): split-K slab, or C = acc (+bias) (+beta*C) / GELU /
 // dGELU + column partial sums.  acc[i][j] register r -> row m0+wm+MF*i+Mf::row(r,q), col n0+wn+MF*j+lr.
 template <int BM, int BN, int MF, int EPI, bool EDGE = false>
 HS_DEVICE void epilogue(const GemmArgs& p, typename Mf<MF>::acc_t (&acc)[BM / 2 / MF][BN / 2 / MF], float* smem, int m0,
-                        int n0, int tm, int slice, int wm, int wn, int wr, int lr, int q, int tile = 0,
-                        int ntile = 0) {
+                        int n0, int tm, int slice, int wm, int wn, int wr, int lr, int q) {
   using M_ = Mf<MF>;
   constexpr int TM = BM / 2 / MF, TN = BN / 2 / MF;
-  if (p.ksplit > 1 && p.tickets) {
-    splitk_inlaunch<BM, BN, MF, EDGE>(p, acc, smem, m0, n0, slice, tile, ntile, wm, wn, lr, q);
-    return;
-  }
   if (p.ksplit > 1) {  // split-K: plain partial slab, bias / beta / sum in splitk_reduce_kernel
     float* sl = p.slab + (int64_t)slice * p.M * p.N;
 #pragma unroll
@@ -501,7 +385,7 @@ __global__ void __launch_bounds__(256, 2) gemm_f32_kernel(GemmArgs p) {
     if (ABL < 2) __syncthreads();
   }
 
-  epilogue<BM, BN, MF, EPI>(p, acc, smem, m0, n0, tm, slice, wm, wn, wr, lr, q, tile, tiles_m * tiles_n);
+  epilogue<BM, BN, MF, EPI>(p, acc, smem, m0, n0, tm, slice, wm, wn, wr, lr, q);
 }
 
 // ---------------------------------------------------------------------------
@@ -887,10 +771,7 @@ __global__ void __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OC
         float v = 0.f;
 #pragma unroll
         for (int c = 0; c < 8; ++c) v += red[c * 128 + st];
-        if (p.tickets)  // handed to the in-launch reducer: stored write-through like its slab
-          __hip_atomic_store(p.part + (int64_t)slice * p.M + m0 + st, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else
-          p.part[(int64_t)slice * p.M + m0 + st] = v;
+        p.part[(int64_t)slice * p.M + m0 + st] = v;
       }
       __syncthreads();
     }
@@ -904,7 +785,7 @@ __global__ void __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OC
   }
   // the epilogue's tile geometry: TM x TN 32x32 accumulators per wave, two wave rows
   epilogue<BM, 2 * 32 * TN, 32, EPI, EDGE>(p, acc, reinterpret_cast<float*>(smem), m0, n0, tm, slice, wm, wn, wr, lr,
-                                           q, tile, ntile);
+                                           q);
 }
 
 static int g_ablation = 0;  // microbenchmark hook (tile_override bits 3-4)
@@ -1162,10 +1043,6 @@ static int pick_tile_split(int M, int N, int K, int* ksplit) {
 // [M][N] planes the consumer sums in slice order (gemm_last_ksplit() says how many), no reduce pass.
 // Returns -1 when the request is not served (caller falls back to the library).
 static thread_local int g_last_ks = 1;
-constexpr int kSplitkTickets = 4096;  // arrival counters per stream (ops/gemm.py _tickets)
-int splitk_tickets() { return kSplitkTickets; }
-static int g_inl_wt = 1;  // in-launch split-K slabs: write-through stores (1) or plain + release fence (0)
-void set_splitk_wt(int on) { g_inl_wt = on ? 1 : 0; }
 int gemm_last_ksplit() { return g_last_ks; }
 void set_h3_occ3(int mask) { g_h3_occ3_env = mask & 7; }
 
@@ -1173,7 +1050,7 @@ int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, i
                 int64_t ldb, void* C, int64_t ldc, const float* bias, int epi, float beta, float* aux, int64_t ldaux,
                 float* part, float* colsum_out, int colsum_acc, int tile_override, hipStream_t st, int ksplit,
                 float* slab, int64_t slab_floats, int mv, int nv, int kv, const float* amax_a, int namax_a,
-                const float* amax_b, int namax_b, float* amax_c, int* tickets) {
+                const float* amax_b, int namax_b, float* amax_c) {
   if ((dtype != 0 && dtype != 2 && dtype != 3 && dtype != 4) || M <= 0 || N <= 0 || K <= 0 || K % GBK != 0) return -1;
   if (dtype == 4 && (!amax_a || !amax_b || namax_a < 1 || namax_b < 1 || namax_a > 8 || namax_b > 8)) return -1;
   // (namax_*: adjacent |max| slots of kAmaxShards shards each, common.h)
@@ -1226,15 +1103,9 @@ int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, i
   const bool wcol = ta && epi == kEpiNone && part != nullptr;
   if (wcol && (!nt || !colsum_out || g_x6_waves != 4 || g_x6_pf != 1 || g_ablation || mv != M || nv != N || kv != K))
     return -1;
-  // split-K finished inside the launch (splitk_inlaunch) when the caller passes the stream's arrival
-  // counters (kSplitkTickets ints, zero between launches) -- else the separate reduction passes below
-  const int bm_t = nt ? 128 : tile == 2 ? 64 : 128, bn_t = nt ? 128 : tile == 0 ? 128 : 64;
-  const bool inl = ks > 1 && !keep_slab && tickets && (M / bm_t) * (N / bn_t) <= kSplitkTickets;
   GemmArgs a{static_cast<const float*>(A), static_cast<const float*>(B), static_cast<float*>(C), bias, aux, part,
              lda, ldb, ldc, ldaux, M, N, K, beta, ks, slab, mv, nv, kv, g_slice_major,
-             amax_a, amax_b, namax_a, namax_b, amax_c,
-             inl ? tickets : nullptr, g_inl_wt, inl && epi >= 1 ? bias : nullptr, inl && wcol ? colsum_out : nullptr,
-             colsum_acc};
+             amax_a, amax_b, namax_a, namax_b, amax_c};
   int rc;
   if (nt == 6)
     rc = launch_split<6>(tile, ta, tb, epi, a, st);
@@ -1250,8 +1121,8 @@ int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, i
     rc = launch_split<0>(tile, ta, tb, epi, a, st);
   if (rc != 0) return rc;
   g_last_ks = ks;
-  const bool fold = wcol && !inl && ks > 1 && !keep_slab && g_wcol_fold;  // bias gradient in the split-K pass
-  if (ks > 1 && !keep_slab && !inl)
+  const bool fold = wcol && ks > 1 && !keep_slab && g_wcol_fold;  // bias gradient in the split-K pass
+  if (ks > 1 && !keep_slab)
     launch_splitk_reduce_cols(slab, ks, M, N, static_cast<float*>(C), ldc, epi >= 1 ? bias : nullptr, beta, a.Mv,
                               a.Nv, st, fold ? part : nullptr, fold ? colsum_out : nullptr, colsum_acc);
   if (epi == kEpiDGelu && part) {
@@ -1259,7 +1130,7 @@ int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, i
     const float* parts[1] = {part};
     float* outs[1] = {colsum_out};
     launch_reduce_rows(parts, outs, 1, M / bm, N, colsum_acc, st);
-  } else if (wcol && !inl && !fold) {
+  } else if (wcol && !fold) {
     const float* parts[1] = {part};
     float* outs[1] = {colsum_out};
     launch_reduce_rows(parts, outs, 1, ks, M, colsum_acc, st);

@@ -374,7 +374,7 @@ def _hip_gemm(a, b, ta, tb, out, bias=None, epi=EPI_NONE, beta=0.0, aux=None, pa
                     part.data_ptr() if part is not None else 0, colsum.data_ptr() if colsum is not None else 0,
                     int(colsum_acc), stream_handle(), tile, ksplit,
                     slab.data_ptr() if slab is not None else 0, slab.numel() if slab is not None else 0, mv, nv, kv,
-                    am[0], am[1], am[2], am[3], slot_ptr(amax_out), 0)
+                    am[0], am[1], am[2], am[3], slot_ptr(amax_out))
     return rc == 0
 
 

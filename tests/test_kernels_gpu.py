@@ -273,15 +273,12 @@ def test_attention_long_seq_fwd_bwd_vs_fp64(cuda, S, B, NH, p):
 
 
 @pytest.mark.parametrize("B,S,NH,p", [(2, 128, 12, 0.0), (2, 96, 2, 0.1), (1, 512, 2, 0.0), (2, 192, 2, 0.1)])
-@pytest.mark.parametrize("family", ["planes", "old"])
-def test_attention_fwd_x6_fp32_level(cuda, B, S, NH, p, family):
-    """fp32 forward on split-bf16 products (the plane-image kernel, default, and the first x6
-    forward): the same keep bits as the exact-fp32 MFMA kernel, and an error against fp64 at the
+def test_attention_fwd_x6_fp32_level(cuda, B, S, NH, p):
+    """fp32 forward on split-bf16 products (the plane-image kernel): the same keep bits as the exact-fp32 MFMA kernel, and an error against fp64 at the
     exact-fp32 kernel's level (not bf16's)."""
     from hetseq_amd.ops import bert_ops
     from hetseq_amd.ops._C import hip
 
-    hip().set_attn_fwd_x6_planes(1 if family == "planes" else 0)
     torch.manual_seed(31)
     H = NH * 64
     qkv = torch.randn(B * S, 3 * H, device=cuda)
@@ -296,7 +293,6 @@ def test_attention_fwd_x6_fp32_level(cuda, B, S, NH, p, family):
         out32, (lse32, bits32) = bert_ops.attn_fwd(qkv, mask, B, S, NH, p, 3, 11, bias=bias)
     finally:
         hip().set_attn_fp32_mode(old)
-        hip().set_attn_fwd_x6_planes(1)
     if p > 0:
         assert torch.equal(bits6, bits32)
     _close(lse6, lse32, 1e-5, 1e-5, "x6 lse")
@@ -310,19 +306,13 @@ def test_attention_fwd_x6_fp32_level(cuda, B, S, NH, p, family):
 
 @pytest.mark.parametrize("B,S,NH,p", [(2, 128, 12, 0.0), (2, 96, 2, 0.1), (1, 512, 2, 0.0), (2, 192, 2, 0.1),
                                        (3, 64, 4, 0.1), (2, 256, 12, 0.0)])
-@pytest.mark.parametrize("family", ["keyblock", "keyblock4", "planes", "planes_dsum", "fused", "gather"])
-def test_attention_bwd_x6_fp32_level(cuda, B, S, NH, p, family, monkeypatch):
-    """fp32 backward on split-bf16 products -- the key-block kernel (default for S <= 128; the
-    plane-image pair above), the plane-image dQ / dKV pair, the fused S <= 128 kernel and the
-    gather dQ / dKV pair -- against the exact-fp32 MFMA backward on the same forward, and against
-    fp64 autograd: error at the exact-fp32 kernel's level."""
+def test_attention_bwd_x6_fp32_level(cuda, B, S, NH, p):
+    """fp32 backward on split-bf16 products (the plane-image dQ / dKV pair; D inside the roles for
+    S <= 128, a separate pass above) against the exact-fp32 MFMA backward on the same forward, and
+    against fp64 autograd: error at the exact-fp32 kernel's level."""
     from hetseq_amd.ops import bert_ops
     from hetseq_amd.ops._C import hip
 
-    if family == "gather":
-        monkeypatch.setenv("HETSEQ_ATTN_BWD", "split")
-    hip().set_attn_bwd_x6_planes({"keyblock": 2, "keyblock4": 4, "planes": 1, "planes_dsum": 1}.get(family, 0))
-    hip().set_attn_bwd_fused_d(0 if family == "planes_dsum" else 1)  # D inside the pair vs the separate pass
     torch.manual_seed(32 + S)
     H = NH * 64
     qkv = torch.randn(B * S, 3 * H, device=cuda)
@@ -339,8 +329,6 @@ def test_attention_bwd_x6_fp32_level(cuda, B, S, NH, p, family, monkeypatch):
         g6 = bert_ops.attn_bwd(qkv, mask, out, dout, saved, B, S, NH, p, bias=bias)
     finally:
         hip().set_attn_fp32_mode(old)
-        hip().set_attn_bwd_x6_planes(-1)
-        hip().set_attn_bwd_fused_d(1)
     torch.cuda.synchronize()
     _close(g6, g32, 1e-4, 1e-6, "x6 vs exact-fp32 attention backward")
     keep = _keep_mask(saved[1], B * NH, S) if p > 0 else None
@@ -437,36 +425,6 @@ def test_attention_writes_output_amax(cuda, S, engine):
     torch.cuda.synchronize()
     assert float(G.amax_value(sf)[0]) == float(ctx.abs().max())
     assert float(G.amax_value(sb)[0]) == float(dqkv.abs().max())
-
-
-@pytest.mark.parametrize("S,p", [(256, 0.1), (512, 0.0), (384, 0.1)])
-def test_attention_h3_dma_matches_loads(cuda, S, p):
-    """S > 128 h3 backward: the next-chunk rows by LDS-DMA (opt-in) give bitwise the gradients of the
-    plain per-chunk loads (same values staged, same order of every sum)."""
-    from hetseq_amd.ops import bert_ops
-    from hetseq_amd.ops._C import hip
-
-    torch.manual_seed(90 + S)
-    B, NH = 2, 12
-    H = NH * 64
-    qkv = torch.randn(B * S, 3 * H, device=cuda)
-    bias = torch.randn(3 * H, device=cuda) * 0.1
-    mask = torch.ones(B, S, dtype=torch.int64, device=cuda)
-    mask[-1, S // 3:] = 0
-    old = hip().attn_fp32_mode()
-    try:
-        hip().set_attn_fp32_mode(2)
-        out, saved = bert_ops.attn_fwd(qkv, mask, B, S, NH, p, 3, 11, bias=bias)
-        dout = torch.randn_like(out)
-        hip().set_attn_h3_dma(1)
-        g_dma = bert_ops.attn_bwd(qkv, mask, out, dout, saved, B, S, NH, p, bias=bias)
-        hip().set_attn_h3_dma(0)
-        g_ld = bert_ops.attn_bwd(qkv, mask, out, dout, saved, B, S, NH, p, bias=bias)
-    finally:
-        hip().set_attn_h3_dma(0)
-        hip().set_attn_fp32_mode(old)
-    torch.cuda.synchronize()
-    assert torch.equal(g_dma, g_ld)
 
 
 @pytest.mark.parametrize("n,bound", [(4096, 30522), (1, 5), (777, 2), (16384, 30522), (5000, 100000)])
@@ -817,11 +775,10 @@ def test_gemm_splitk_deterministic(cuda, engine):
 @pytest.mark.parametrize("ta,tb,M,N,K,ks", [(1, 0, 768, 3072, 4096, 2), (1, 0, 768, 768, 4096, 4),
                                             (0, 1, 4096, 768, 3072, 2), (0, 0, 4096, 768, 768, 2),
                                             (1, 0, 256, 384, 1024, 8)])
-def test_gemm_splitk_inlaunch_matches_reduce_pass(cuda, engine, ta, tb, M, N, K, ks):
-    """The split-K finish inside the launch (last-arriving slice sums the slices: gemm.hip
-    splitk_inlaunch) is bitwise the separate splitk_reduce / reduce_rows passes' result -- plain,
-    accumulating (beta 1), with a bias, with the weight gradient's fused column sums -- and leaves
-    the arrival counters at zero for the next launch."""
+def test_gemm_splitk_reduce_pass_and_colsum_fold(cuda, engine, ta, tb, M, N, K, ks):
+    """Split-K finished by the fixed-order reduce pass -- plain, accumulating (beta 1), with a bias,
+    with the weight gradient's column sums folded into that pass or summed by their own reduce_rows
+    launch (bitwise the same) -- against fp64."""
     from hetseq_amd.ops import gemm as G
 
     gen = torch.Generator(device=cuda).manual_seed(21)
@@ -830,10 +787,8 @@ def test_gemm_splitk_inlaunch_matches_reduce_pass(cuda, engine, ta, tb, M, N, K,
     bias = torch.randn(N, device=cuda, generator=gen)
     c0 = torch.randn(M, N, device=cuda, generator=gen)
     cs0 = torch.randn(M, device=cuda, generator=gen)
-    saved = G._INLAUNCH
 
-    def run(inl, beta, with_bias, wcol):
-        G._INLAUNCH = inl
+    def run(beta, with_bias, wcol):
         out = c0.clone()
         kw = dict(fp32=engine, ksplit=ks, beta=beta)
         if with_bias:
@@ -845,32 +800,26 @@ def test_gemm_splitk_inlaunch_matches_reduce_pass(cuda, engine, ta, tb, M, N, K,
         assert G._hip_gemm(a, b, ta, tb, out, **kw)
         return out, cs
 
+    ad, bd = (a.t() if ta else a).double(), (b.t() if tb else b).double()
+    ref = ad @ bd
+    cases = [(0.0, False, False), (1.0, False, False)]
+    if (ta, tb) == (0, 1):
+        cases.append((1.0, True, False))
+    if ta:
+        cases += [(1.0, False, True), (0.0, False, True)]
     try:
-        cases = [(0.0, False, False), (1.0, False, False)]
-        if (ta, tb) == (0, 1):
-            cases.append((1.0, True, False))
-        if ta:
-            cases += [(1.0, False, True), (0.0, False, True)]
-        for wt in (1, 0):  # write-through slab stores / plain stores + release fence
-            G.hip().set_splitk_wt(wt)
-            for beta, with_bias, wcol in cases:
-                o1, c1 = run(True, beta, with_bias, wcol)
-                o0, c0_ = run(False, beta, with_bias, wcol)
-                assert torch.equal(o1, o0), (wt, beta, with_bias, wcol, (o1 - o0).abs().max().item())
-                if wcol:
-                    assert torch.equal(c1, c0_)
-                    G.hip().set_wcol_fold(0)  # the bias gradient by its own reduce_rows pass
-                    o2, c2 = run(False, beta, with_bias, wcol)
-                    G.hip().set_wcol_fold(1)
-                    assert torch.equal(o2, o0) and torch.equal(c2, c0_)
-        ref = (a.t() if ta else a).double() @ (b.t() if tb else b).double()
-        _close(run(True, 0.0, False, False)[0], ref, 1e-5, 1e-4, "splitk in-launch")
-        torch.cuda.synchronize()
-        for t in G._TICKETS.values():
-            assert int(t.abs().sum()) == 0
+        for beta, with_bias, wcol in cases:
+            o0, c0_ = run(beta, with_bias, wcol)
+            want = ref + beta * c0.double() + (bias.double() if with_bias else 0.0)
+            _close(o0, want, 1e-5, 1e-4, "splitk beta=%g bias=%d" % (beta, with_bias))
+            if wcol:
+                _close(c0_, ad.sum(1) + (cs0.double() if beta else 0.0), 1e-5, 1e-4, "splitk colsum")
+                G.hip().set_wcol_fold(0)  # the bias gradient by its own reduce_rows pass
+                o2, c2 = run(beta, with_bias, wcol)
+                G.hip().set_wcol_fold(1)
+                assert torch.equal(o2, o0) and torch.equal(c2, c0_)
     finally:
-        G._INLAUNCH = saved
-        G.hip().set_splitk_wt(1)
+        G.hip().set_wcol_fold(1)
 
 
 @pytest.mark.parametrize("engine", ["x6", "h3"])
