@@ -174,9 +174,10 @@ struct AttnPl {
 };
 
 // the wave's tile (rows: the lanes, 32-aligned; columns 0-31 in c0, 32-63 in c1, * scale) into the
-// planes at element e (the lane's row, the tile's first column) and its two exponents at ex
-HS_DEVICE void store_rows_h3p(const AttnPl& po, int64_t e, int8_t* ex, const f32x16& c0, const f32x16& c1, int hf,
-                              float scale) {
+// blocked planes (h3p.h; row stride ld) at the lane's row `row`, the tile's first column col0 (a multiple
+// of 32), and its two exponents at ex
+HS_DEVICE void store_rows_h3p(const AttnPl& po, int64_t row, int64_t col0, int64_t ld, int8_t* ex, const f32x16& c0,
+                              const f32x16& c1, int hf, float scale) {
   uint32_t m0 = 0u, m1 = 0u;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -190,8 +191,8 @@ HS_DEVICE void store_rows_h3p(const AttnPl& po, int64_t e, int8_t* ex, const f32
     const int d = 8 * g + 4 * hf;
     const float a[4] = {c0[4 * g] * scale, c0[4 * g + 1] * scale, c0[4 * g + 2] * scale, c0[4 * g + 3] * scale};
     const float b[4] = {c1[4 * g] * scale, c1[4 * g + 1] * scale, c1[4 * g + 2] * scale, c1[4 * g + 3] * scale};
-    h3p_store4(po.pl, po.ps, e + d, a, s0);
-    h3p_store4(po.pl, po.ps, e + 32 + d, b, s1);
+    h3p_store4(po.pl, po.ps, h3p_index(row, col0 + d, ld, 1), a, s0);
+    h3p_store4(po.pl, po.ps, h3p_index(row, col0 + 32 + d, ld, 1), b, s1);
   }
   if ((threadIdx.x & 63) == 0) {
     ex[0] = static_cast<int8_t>(e0);
@@ -460,10 +461,10 @@ HS_DEVICE void dkv_body(char* __restrict__ smem, int bx, int bh, const float* __
   store_rows(out + 2 * H, dv0, dv1, hf, ldexpf(1.f, -(eo_run + ep)), cm);
   if (amax) amax_commit(amax, cm);
   if (po.pl) {  // dK, dV as h3p planes of dqkv [B*S][3H] (exponent row stride 3H / 32)
-    const int64_t e = ((int64_t)b * S + key) * ld + h * kHD;
+    const int64_t row = (int64_t)b * S + key;
     int8_t* ex = po.ex + ((int64_t)b * S + k0) / 32 * (ld / 32) + h * kHD / 32;
-    store_rows_h3p(po, e + H, ex + H / 32, dk0, dk1, hf, ldexpf(1.f, -(eq_run + es)));
-    store_rows_h3p(po, e + 2 * H, ex + 2 * H / 32, dv0, dv1, hf, ldexpf(1.f, -(eo_run + ep)));
+    store_rows_h3p(po, row, H + h * kHD, ld, ex + H / 32, dk0, dk1, hf, ldexpf(1.f, -(eq_run + es)));
+    store_rows_h3p(po, row, 2 * H + h * kHD, ld, ex + 2 * H / 32, dv0, dv1, hf, ldexpf(1.f, -(eo_run + ep)));
   }
 }
 
@@ -575,7 +576,7 @@ HS_DEVICE void dq_body(char* __restrict__ smem, int bx, int bh, const float* __r
   store_rows(dqkv + tok * ld + h * kHD, dq0, dq1, hf, 0.125f * ldexpf(1.f, -(ek_run + es)), cm);
   if (amax) amax_commit(amax, cm);
   if (po.pl)
-    store_rows_h3p(po, tok * ld + h * kHD, po.ex + ((int64_t)b * S + q0) / 32 * (ld / 32) + h * kHD / 32, dq0, dq1, hf,
+    store_rows_h3p(po, tok, h * kHD, ld, po.ex + ((int64_t)b * S + q0) / 32 * (ld / 32) + h * kHD / 32, dq0, dq1, hf,
                    0.125f * ldexpf(1.f, -(ek_run + es)));
 }
 
@@ -714,8 +715,8 @@ __global__ void __launch_bounds__(256, 2)
   store_rows(ctx + ((int64_t)b * S + q0 + li) * H + h * kHD, o0, o1, hf, inv, cm);
   if (amax) amax_commit(amax, cm);  // ctx's |max|: the output projection's operand scale
   if (po.pl)  // ctx as h3p planes of the output projection (exponent row stride H / 32)
-    store_rows_h3p(po, ((int64_t)b * S + q0 + li) * H + h * kHD, po.ex + ((int64_t)b * S + q0) / 32 * (H / 32) + 2 * h,
-                   o0, o1, hf, inv);
+    store_rows_h3p(po, (int64_t)b * S + q0 + li, h * kHD, H, po.ex + ((int64_t)b * S + q0) / 32 * (H / 32) + 2 * h, o0,
+                   o1, hf, inv);
   if (hf == 0) lse[(int64_t)bh * S + q0 + li] = m + __logf(l);
 }
 

@@ -109,12 +109,10 @@ int launch_gemm_h3p(int ta, int tb, int M, int N, int K, const void* A, int64_t 
                     int64_t lde_a, const void* B, int64_t ldb, int64_t b_ps, const int8_t* eb, int64_t lde_b, float* C,
                     int64_t ldc, const float* bias, int epi, float beta, float* aux, int64_t ldaux, float* part,
                     float* colsum, int colsum_acc, void* cp, int64_t ldcp, int64_t cp_ps, int8_t* ec, int64_t lde_c,
-                    int ksplit, float* slab, int64_t slab_floats, hipStream_t st);
+                    int ksplit, float* slab, int64_t slab_floats, int ablk, int bblk, hipStream_t st);
 int launch_h3p_split(const float* src, int64_t lds, int rows, int cols, void* dst, int64_t ldd, int64_t ps, int8_t* ex,
-                     int64_t lde, hipStream_t st);
+                     int64_t lde, int blocked, hipStream_t st);
 int h3p_split_seg_bytes();
-void set_h3p_variant(int v);
-int h3p_variant();
 void launch_h3p_split_multi(const void* table, int nseg, int total, hipStream_t st);
 
 // mnist.hip
@@ -392,24 +390,31 @@ PYBIND11_MODULE(_hip, m) {
   m.def("gemm_h3p", [](int ta, int tb, int M, int N, int K, i64 A, i64 lda, i64 a_ps, i64 ea, i64 lde_a, i64 B,
                        i64 ldb, i64 b_ps, i64 eb, i64 lde_b, i64 C, i64 ldc, i64 bias, int epi, float beta, i64 aux,
                        i64 ldaux, i64 part, i64 colsum, int colsum_acc, i64 cp, i64 ldcp, i64 cp_ps, i64 ec, i64 lde_c,
-                       int ksplit, i64 slab, i64 slab_floats, i64 st) {
+                       int ksplit, i64 slab, i64 slab_floats, i64 st, int ablk, int bblk) {
     pre_launch("gemm_h3p");
     const int rc = launch_gemm_h3p(ta, tb, M, N, K, P(const void*, A), lda, a_ps, P(const int8_t*, ea), lde_a,
                                    P(const void*, B), ldb, b_ps, P(const int8_t*, eb), lde_b, P(float*, C), ldc,
                                    P(const float*, bias), epi, beta, P(float*, aux), ldaux, P(float*, part),
                                    P(float*, colsum), colsum_acc, P(void*, cp), ldcp, cp_ps, P(int8_t*, ec), lde_c,
-                                   ksplit, P(float*, slab), slab_floats, ST(st));
+                                   ksplit, P(float*, slab), slab_floats, ablk, bblk, ST(st));
     if (rc == 0) check_launch("gemm_h3p");
     return rc;
-  }, "fp32 GEMM as three fp16 products over block-scaled h3p planes (gemm_h3p.hip); -1 = not served");
-  m.def("h3p_split", [](i64 src, i64 lds, int rows, int cols, i64 dst, i64 ldd, i64 ps, i64 ex, i64 lde, i64 st) {
+  }, "fp32 GEMM as three fp16 products over block-scaled h3p planes (gemm_h3p.hip); -1 = not served",
+     py::arg("ta"), py::arg("tb"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("A"), py::arg("lda"),
+     py::arg("a_ps"), py::arg("ea"), py::arg("lde_a"), py::arg("B"), py::arg("ldb"), py::arg("b_ps"), py::arg("eb"),
+     py::arg("lde_b"), py::arg("C"), py::arg("ldc"), py::arg("bias"), py::arg("epi"), py::arg("beta"), py::arg("aux"),
+     py::arg("ldaux"), py::arg("part"), py::arg("colsum"), py::arg("colsum_acc"), py::arg("cp"), py::arg("ldcp"),
+     py::arg("cp_ps"), py::arg("ec"), py::arg("lde_c"), py::arg("ksplit"), py::arg("slab"), py::arg("slab_floats"),
+     py::arg("st"), py::arg("ablk") = 0, py::arg("bblk") = 0);
+  m.def("h3p_split", [](i64 src, i64 lds, int rows, int cols, i64 dst, i64 ldd, i64 ps, i64 ex, i64 lde, i64 st,
+                        int blocked) {
     pre_launch("h3p_split");
-    check(launch_h3p_split(P(const float*, src), lds, rows, cols, P(void*, dst), ldd, ps, P(int8_t*, ex), lde, ST(st)),
+    check(launch_h3p_split(P(const float*, src), lds, rows, cols, P(void*, dst), ldd, ps, P(int8_t*, ex), lde, blocked,
+                           ST(st)),
           "h3p_split");
-  });
+  }, py::arg("src"), py::arg("lds"), py::arg("rows"), py::arg("cols"), py::arg("dst"), py::arg("ldd"), py::arg("ps"),
+     py::arg("ex"), py::arg("lde"), py::arg("st"), py::arg("blocked") = 0);
   m.def("h3p_split_seg_bytes", &h3p_split_seg_bytes);
-  m.def("set_h3p_variant", &set_h3p_variant, "h3p GEMM kernel: 0 two 32-deep stages, 1 16-deep four-step ring");
-  m.def("h3p_variant", &h3p_variant);
   m.def("attn_fwd_h3p", [](i64 qkv, i64 mask, i64 bqkv, i64 ctx, i64 lse, i64 dmask, int B, int S, int NH, float p,
                            u64 seed, u64 off, int bh0, i64 pl, i64 ps, i64 ex, i64 st) {
     pre_launch("attn_fwd_h3p");

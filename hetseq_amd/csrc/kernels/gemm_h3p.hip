@@ -13,26 +13,30 @@
 //    tensor, not in every GEMM block that stages it: the K loop is LDS-DMA + MFMA only.  The
 //    in-kernel-split engine (gemm.hip, gemm_x6s_kernel NT=4) spends as many issue cycles on the
 //    split VALU and the transposing ds_writes as on its MFMAs (profiles/r4_fp32_pmc.md);
-//  * 128 x 128 tile, 4 waves (2 x 2, 64 x 64 each = 2 x 2 v_mfma_f32_32x32x16_f16 tiles), BK = 32,
-//    two LDS stages of 32 KB (+ 4 KB of block factors): two workgroups per CU, so the other
-//    stream's GEMM blocks (the backward's weight-gradient stream) share the CUs;
-//  * staging is global_load_lds_dwordx4 (no VGPR round trip).  The LDS image is written
-//    lane-linearly, so the bank swizzle is in each lane's SOURCE address: k-contiguous operands
-//    as [128 rows][32 k] (64-B rows, 16-B chunks XOR (r>>2)&3, ds_read_b128 fragments),
-//    mn-contiguous ones (the data gradient's weight, both weight-gradient operands) as
-//    [32 k][128] (256-B rows, chunks XOR 4(r&3), fragments by ds_read_b64_tr_b16 -- the gfx950
-//    transposing read): no transpose pass anywhere;
-//  * block scales: each K tile's MFMAs accumulate into a fresh register tile (first MFMA with an
-//    inline-zero C), which is added to the fp32 accumulator with the tile's factor
-//    2^-(e_a + e_b) by one v_pk_fma per register pair.  The accumulator therefore holds TRUE fp32
-//    values (no running exponent, no overflow the fp32 result would not have), and each operand
-//    block keeps its own 2^18 window.  The factors of the block's K range are tabulated in LDS
-//    once (4 KB), read as two broadcast ds_read_b64 per tile;
+//  * the producers write the planes BLOCKED (h3p.h: 32 x 32 blocks of 2 KB): a 32-deep K tile of a
+//    128-wide operand is four whole blocks in either orientation, so every LDS-DMA wave-instruction
+//    reads full 128-B lines (row-major planes gave the k-contiguous operands 64- or 32-B pieces of
+//    each row: 2-4x the L2 requests and TA time, profiles/r5_fp32_pmc.md);
+//  * 128 x 128 tile, 4 waves (2 x 2, 64 x 64 each = 2 x 2 v_mfma_f32_32x32x16_f16 tiles), 16-deep K
+//    steps in a four-step LDS ring (64 KB + 4 KB of block factors: two workgroups per CU, so the
+//    backward's weight-gradient stream shares the CUs), each step's DMA issued three steps ahead;
+//  * the LDS image is written lane-linearly by the DMA, so the bank swizzle is in each lane's SOURCE
+//    address: k-contiguous operands as [128 rows][16 k] (32-B rows, 16-B chunks XOR (r>>3)&1,
+//    ds_read_b128 fragments), mn-contiguous ones (the data gradient's weight, both weight-gradient
+//    operands) as [16 k][128] (256-B rows, chunks XOR 4(r&3), fragments by ds_read_b64_tr_b16 -- the
+//    gfx950 transposing read): no transpose pass anywhere;
+//  * block scales: each 32-deep K tile's MFMAs accumulate into a fresh register tile (first MFMA with
+//    an inline-zero C), which is added to the fp32 accumulator with the tile's factor 2^-(e_a + e_b)
+//    by one v_pk_fma per register pair.  The accumulator therefore holds TRUE fp32 values (no running
+//    exponent, no overflow the fp32 result would not have), and each operand block keeps its own
+//    2^18 window.  The factors of the block's K range are tabulated in LDS once (4 KB);
 //  * XCD-contiguous, grouped block order (bijective for any grid): an XCD's resident blocks share
 //    operand panels in its private L2.
 // Epilogues: fp32 C (+ bias) (+ beta C); split-K fp32 slabs (summed by splitk_reduce_kernel, or by
 // the consumer); GELU (pre-activation kept in aux) and dGELU (column partials of the bias
-// gradient), each optionally writing its output as h3p planes for the next GEMM.
+// gradient), each optionally writing its output as blocked h3p planes for the next GEMM.
+// (Round 5 measured a two-stage 32-deep loop -- one vmcnt(0) + barrier per tile -- 14 % slower over
+// the BERT layer's twelve products and removed it: tools/bench_h3p.py, profiles/r5_fp32_pmc.md.)
 #include <algorithm>
 #include <cstdlib>
 
@@ -50,12 +54,8 @@ typedef float qf16 __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(3))) void q_lds_t;
 typedef __attribute__((address_space(1))) const void q_gbl_t;
 
-constexpr int QT = 128, QBK = 32;
-constexpr int QPLANE = QT * QBK * 2;  // one plane of one operand tile (8 KB)
-constexpr int QOPND = 2 * QPLANE;     // hi + lo (16 KB)
-constexpr int QSTAGE = 2 * QOPND;     // A and B (32 KB)
-constexpr int QMAXKT = 128;           // K tiles per block (K / ksplit <= 4096)
-constexpr int QSMEM = 2 * QSTAGE + 2 * QMAXKT * 4 * 4;
+constexpr int QT = 128, QBK = 32;  // tile edge; K tile (exponent block) depth
+constexpr int QMAXKT = 128;         // K tiles per block (K / ksplit <= 4096)
 
 enum { kQNone = 0, kQBias = 1, kQGelu = 2, kQDGelu = 3 };
 
@@ -77,61 +77,8 @@ struct QArgs {
   float* slab;  // split-K: [ksplit][M][N]
   int M, N, K, ksplit;
   float beta;
+  int ablk, bblk;  // operand plane layout: 0 row-major, 1 blocked (h3p.h: 32 x 32 blocks of 2 KB per plane)
 };
-
-template <bool KC>
-struct QImg {
-  static constexpr int row_bytes = KC ? QBK * 2 : QT * 2;  // 64 ([mn][k]) or 256 ([k][mn])
-  HS_DEVICE static int swz(int r) { return KC ? ((r >> 2) & 3) : 4 * (r & 3); }
-};
-
-// per-lane source byte offsets (plane 0 of the operand, k = 0 of the block's range) of this wave's
-// four LDS-DMA instructions: instruction j fills bytes [1024 (4 j + w), +1024) of the operand image
-template <bool KC>
-HS_DEVICE void q_offsets(uint32_t (&off)[4], int64_t ld, int64_t ps, int mn0, int w, int lane) {
-  using I = QImg<KC>;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int byte = 1024 * (4 * j + w) + 16 * lane;
-    const int plane = byte / QPLANE, ib = byte % QPLANE;
-    const int row = ib / I::row_bytes, cl = (ib % I::row_bytes) / 16;
-    const int gc = cl ^ I::swz(row);  // the chunk this LDS position holds
-    const int64_t e = KC ? (int64_t)(mn0 + row) * ld + 8 * gc : (int64_t)row * ld + mn0 + 8 * gc;
-    off[j] = static_cast<uint32_t>(2 * (e + plane * ps));
-  }
-}
-
-HS_DEVICE void q_dma(const char* base, const uint32_t (&off)[4], char* img, int w) {
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-    __builtin_amdgcn_global_load_lds((q_gbl_t*)(base + off[j]), (q_lds_t*)(img + 1024 * (4 * j + w)), 16, 0, 0);
-}
-
-// MFMA operand: 8 consecutive k (element j = k 16 ks + 8 (lane >> 5) + j) of row / column
-// rc + (lane & 31) from plane p of an operand image
-template <bool KC>
-HS_DEVICE qh8 q_frag(const char* img, int p, int rc, int ks, int lane) {
-  using I = QImg<KC>;
-  const char* pl = img + p * QPLANE;
-  if (KC) {
-    const int r = rc + (lane & 31), c = 2 * ks + (lane >> 5);
-    return *reinterpret_cast<const qh8*>(pl + r * I::row_bytes + 16 * (c ^ I::swz(r)));
-  } else {
-    // transposed read: lane 4q+p' of a 16-lane group addresses k row k0+q, columns c0+4p'..+3;
-    // lane i of the group receives column c0+i of the four rows
-    const int l16 = lane & 15, q = l16 >> 2, pp = l16 & 3, g = lane >> 4;
-    const int col = rc + 16 * (g & 1) + 4 * pp;
-    qs4 v[2];
-#pragma unroll
-    for (int jj = 0; jj < 2; ++jj) {
-      const int row = 16 * ks + 8 * (g >> 1) + 4 * jj + q;
-      const char* a = pl + row * I::row_bytes + 16 * ((col >> 3) ^ I::swz(row)) + 2 * (col & 7);
-      v[jj] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) qs4*)(a));
-    }
-    const qs8 u = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w};
-    return __builtin_bit_cast(qh8, u);
-  }
-}
 
 HS_DEVICE qf16 q_mma(qh8 a, qh8 b, qf16 c) { return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0); }
 HS_DEVICE int q_row(int r, int q) { return (r & 3) + 8 * (r >> 2) + 4 * q; }
@@ -209,8 +156,8 @@ HS_DEVICE void q_epilogue(const QArgs& p, qf16 (&acc)[2][2], char* smem, int m0,
         for (int r = 0; r < 16; r += 2) {
           uint32_t hi, lo;
           h3p_split2(acc[i][j][r], acc[i][j][r + 1], s, hi, lo);
-          const int64_t e0 = (int64_t)(m0 + wm + 32 * i + q_row(r, q)) * p.ldcp + n;
-          const int64_t e1 = (int64_t)(m0 + wm + 32 * i + q_row(r + 1, q)) * p.ldcp + n;
+          const int64_t e0 = h3p_index(m0 + wm + 32 * i + q_row(r, q), n, p.ldcp, 1);  // blocked planes
+          const int64_t e1 = h3p_index(m0 + wm + 32 * i + q_row(r + 1, q), n, p.ldcp, 1);
           p.cp[e0] = static_cast<uint16_t>(hi);
           p.cp[e1] = static_cast<uint16_t>(hi >> 16);
           p.cp[p.cp_ps + e0] = static_cast<uint16_t>(lo);
@@ -235,126 +182,14 @@ HS_DEVICE void q_epilogue(const QArgs& p, qf16 (&acc)[2][2], char* smem, int m0,
   }
 }
 
-template <bool TA, bool TB, int EPI>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) gemm_h3p_kernel(QArgs p) {
-  constexpr bool AK = !TA, BKc = TB;  // k-contiguous storage?
-  __shared__ __attribute__((aligned(16))) char smem[QSMEM];  // ALL LDS in one array (glds alias tracking)
-  float* const fA = reinterpret_cast<float*>(smem + 2 * QSTAGE);
-  float* const fB = fA + QMAXKT * 4;
-
-  const int tiles_m = p.M / QT, tiles_n = p.N / QT, ntile = tiles_m * tiles_n, nwg = ntile * p.ksplit;
-  const int orig = blockIdx.x;
-  const int xcd = orig % 8, qq = nwg / 8, rr = nwg % 8;
-  const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + orig / 8;
-  // slice-major split-K order: an XCD's contiguous range of blocks is one K slice over many tiles
-  const int slice = wg / ntile, tile = wg % ntile;
-  const int gsz = 8 * tiles_n, grp = tile / gsz, gm = min(8, tiles_m - 8 * grp);
-  const int tm = 8 * grp + (tile % gsz) % gm, tn = (tile % gsz) / gm;
-  const int m0 = tm * QT, n0 = tn * QT;
-  const int kofs = slice * (p.K / p.ksplit);
-  const int KT = p.K / p.ksplit / QBK;
-
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = w >> 1, wc = w & 1, wm = 64 * wr, wn = 64 * wc;
-
-  // block factors 2^-e of the block's K range: fA[t][g] for A's row group g, fB[t][g] for B's
-  // column group g (plain loads, all retired before the first LDS-DMA is issued)
-  for (int u = threadIdx.x; u < 4 * KT; u += 256) {
-    const int t = u >> 2, g = u & 3, kb = kofs / QBK + t;
-    const int64_t ia = AK ? (int64_t)(m0 / 32 + g) * p.lde_a + kb : (int64_t)kb * p.lde_a + m0 / 32 + g;
-    const int64_t ib = BKc ? (int64_t)(n0 / 32 + g) * p.lde_b + kb : (int64_t)kb * p.lde_b + n0 / 32 + g;
-    fA[u] = __builtin_ldexpf(1.f, -(int)p.ea[ia]);
-    fB[u] = __builtin_ldexpf(1.f, -(int)p.eb[ib]);
-  }
-
-  uint32_t offA[4], offB[4];
-  q_offsets<AK>(offA, p.lda, p.a_ps, m0, w, lane);
-  q_offsets<BKc>(offB, p.ldb, p.b_ps, n0, w, lane);
-  const int64_t stepA = AK ? 2 * QBK : 2 * (int64_t)QBK * p.lda, stepB = BKc ? 2 * QBK : 2 * (int64_t)QBK * p.ldb;
-  const char* ga = reinterpret_cast<const char*>(p.A) + (AK ? 2 * (int64_t)kofs : 2 * (int64_t)kofs * p.lda);
-  const char* gb = reinterpret_cast<const char*>(p.B) + (BKc ? 2 * (int64_t)kofs : 2 * (int64_t)kofs * p.ldb);
-
-  qf16 acc[2][2], tmp[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = qf16{};
-
-  struct Frags {
-    qh8 a[2][2], b[2][2];  // [plane][tile]
-  };
-  auto read = [&](Frags& f, const char* stage, int ks) {
-#pragma unroll
-    for (int pl = 0; pl < 2; ++pl)
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        f.a[pl][i] = q_frag<AK>(stage, pl, wm + 32 * i, ks, lane);
-        f.b[pl][i] = q_frag<BKc>(stage + QOPND, pl, wn + 32 * i, ks, lane);
-      }
-  };
-  // the three products of one k slice, smallest first: lo_a hi_b, hi_a lo_b, hi_a hi_b
-  auto mma = [&](const Frags& f, bool first) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) tmp[i][j] = q_mma(f.a[1][i], f.b[0][j], first ? qf16{} : tmp[i][j]);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) tmp[i][j] = q_mma(f.a[0][i], f.b[1][j], tmp[i][j]);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) tmp[i][j] = q_mma(f.a[0][i], f.b[0][j], tmp[i][j]);
-  };
-
-  Frags f[2];
-  q_dma(ga, offA, smem, w);
-  q_dma(gb, offB, smem + QOPND, w);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();  // tile 0 and the factor tables visible to every wave
-  read(f[0], smem, 0);
-  for (int t = 0; t < KT; ++t) {
-    const char* cur = smem + (t & 1) * QSTAGE;
-    char* nxt = smem + ((t + 1) & 1) * QSTAGE;
-    if (t + 1 < KT) {  // the other stage was last read before the previous barrier
-      q_dma(ga + (t + 1) * stepA, offA, nxt, w);
-      q_dma(gb + (t + 1) * stepB, offB, nxt + QOPND, w);
-    }
-    read(f[1], cur, 1);
-    mma(f[0], true);
-    // keep slice 0's MFMAs ahead of the barrier (the scheduler would sink them past it and expose
-    // slice 1's LDS reads to the barrier's wait)
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // tile t+1 landed in every wave's share; nobody reads tile t any more
-    if (t + 1 < KT) read(f[0], nxt, 0);
-    mma(f[1], false);
-    const float2 fa = *reinterpret_cast<const float2*>(fA + 4 * t + 2 * wr);
-    const float2 fb = *reinterpret_cast<const float2*>(fB + 4 * t + 2 * wc);
-    const float fac[2][2] = {{fa.x * fb.x, fa.x * fb.y}, {fa.y * fb.x, fa.y * fb.y}};
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] += tmp[i][j] * fac[i][j];
-  }
-
-  q_epilogue<EPI>(p, acc, smem, m0, n0, tm, slice, wm, wn, wr, lane);
-}
-
-// ---------------------------------------------------------------- variant 1: BK = 16 steps, 4-deep ring
-// The two-stage loop above waits (vmcnt(0)) for the next K tile's LDS-DMA half way through the current
-// tile: one tile of MFMAs (~770 cycles per wave) is all the latency it can hide.  Here each step is
-// one 16-deep K slice (16 KB of planes), the LDS holds a ring of four steps (64 KB: still two blocks
-// per CU), and a step's DMA is issued three steps before it is read:
+// ---------------------------------------------------------------- the K loop: 16-deep steps, 4-deep ring
 //   step s: this wave's share of step s+1 landed (counted vmcnt: step s+2 stays in flight) ->
 //   barrier (step s+1 visible to every wave; every wave's reads of step s-1 done, its stage free) ->
 //   step s's 12 MFMAs (fragments in registers, read during step s-1), with the DMA of step s+3 into
 //   the freed stage and the fragment reads of step s+1 interleaved between them in pinned order.
-// The DMA pieces are asm statements: hipcc would otherwise drain vmcnt(0) before
-// every LDS read it cannot prove disjoint from a pending DMA.  Block factors apply per 32-deep K tile
-// (every second step), as in variant 0.
+// The DMA pieces are asm statements: hipcc would otherwise drain vmcnt(0) before every LDS read it
+// cannot prove disjoint from a pending DMA.  Block factors apply per 32-deep K tile (every second
+// step).
 constexpr int RBK = 16;
 constexpr int RPLANE = QT * RBK * 2;  // one plane of one operand step: 4 KB
 constexpr int ROPND = 2 * RPLANE;     // 8 KB
@@ -373,7 +208,7 @@ struct RImg {
 // byte offsets (plane 0, k = 0 of the block's range) of this wave's two pieces of one operand:
 // piece j (0, 1) fills bytes [1024 (4 j + w), +1024) of the operand's 8 KB step image
 template <bool KC>
-HS_DEVICE void r_offsets(uint32_t (&off)[2], int64_t ld, int64_t ps, int mn0, int w, int lane) {
+HS_DEVICE void r_offsets(uint32_t (&off)[2], int64_t ld, int64_t ps, int mn0, int w, int lane, int blk) {
   using I = RImg<KC>;
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
@@ -381,7 +216,7 @@ HS_DEVICE void r_offsets(uint32_t (&off)[2], int64_t ld, int64_t ps, int mn0, in
     const int plane = byte / RPLANE, ib = byte % RPLANE;
     const int row = ib / I::row_bytes, cl = (ib % I::row_bytes) / 16;
     const int gc = cl ^ I::swz(row);
-    const int64_t e = KC ? (int64_t)(mn0 + row) * ld + 8 * gc : (int64_t)row * ld + mn0 + 8 * gc;
+    const int64_t e = KC ? h3p_index(mn0 + row, 8 * gc, ld, blk) : h3p_index(row, mn0 + 8 * gc, ld, blk);
     off[j] = static_cast<uint32_t>(2 * (e + plane * ps));
   }
 }
@@ -432,7 +267,7 @@ HS_DEVICE qh8 r_frag(const char* img, int p, int rc, int lane) {
 }
 
 template <bool TA, bool TB, int EPI>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) gemm_h3p_ring_kernel(QArgs p) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) gemm_h3p_kernel(QArgs p) {
   constexpr bool AK = !TA, BKc = TB;
   __shared__ __attribute__((aligned(1024))) char smem[RSMEM];
   float* const fA = reinterpret_cast<float*>(smem + RNS * RSTAGE);
@@ -463,17 +298,23 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   }
 
   uint32_t offA[2], offB[2];
-  r_offsets<AK>(offA, p.lda, p.a_ps, m0, w, lane);
-  r_offsets<BKc>(offB, p.ldb, p.b_ps, n0, w, lane);
-  const int64_t stepA = AK ? 2 * RBK : 2 * (int64_t)RBK * p.lda, stepB = BKc ? 2 * RBK : 2 * (int64_t)RBK * p.ldb;
-  const char* ga = reinterpret_cast<const char*>(p.A) + (AK ? 2 * (int64_t)kofs : 2 * (int64_t)kofs * p.lda);
-  const char* gb = reinterpret_cast<const char*>(p.B) + (BKc ? 2 * (int64_t)kofs : 2 * (int64_t)kofs * p.ldb);
+  r_offsets<AK>(offA, p.lda, p.a_ps, m0, w, lane, p.ablk);
+  r_offsets<BKc>(offB, p.ldb, p.b_ps, n0, w, lane, p.bblk);
+  // byte offset of 16-deep step s: k-contiguous = columns 16 s.., else rows 16 s.. (h3p_index is
+  // linear in whole blocks, so a step is its 32-deep tile plus the half-tile's offset)
+  const int64_t tileA = 2 * (AK ? h3p_index(0, QBK, p.lda, p.ablk) : h3p_index(QBK, 0, p.lda, p.ablk));
+  const int64_t tileB = 2 * (BKc ? h3p_index(0, QBK, p.ldb, p.bblk) : h3p_index(QBK, 0, p.ldb, p.bblk));
+  const int64_t halfA = 2 * (AK ? h3p_index(0, RBK, p.lda, p.ablk) : h3p_index(RBK, 0, p.lda, p.ablk));
+  const int64_t halfB = 2 * (BKc ? h3p_index(0, RBK, p.ldb, p.bblk) : h3p_index(RBK, 0, p.ldb, p.bblk));
+  const char* ga = reinterpret_cast<const char*>(p.A) + (kofs / QBK) * tileA;
+  const char* gb = reinterpret_cast<const char*>(p.B) + (kofs / QBK) * tileB;
   const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((q_lds_t*)smem));
   // DMA piece j of step s (clamped: past the last step a stage nobody reads again gets the last step's
   // bytes again, so every step issues the same four pieces and the counted waits stay exact)
   auto dma = [&](int j, int s, int stage) __attribute__((always_inline)) {
     const int64_t ss = min(s, NSTEP - 1);
-    const char* src = j < 2 ? ga + ss * stepA + offA[j] : gb + ss * stepB + offB[j - 2];
+    const char* src = j < 2 ? ga + (ss >> 1) * tileA + (ss & 1) * halfA + offA[j]
+                            : gb + (ss >> 1) * tileB + (ss & 1) * halfB + offB[j - 2];
     r_dma(src, __builtin_amdgcn_readfirstlane(lds0 + stage * RSTAGE + (j < 2 ? 0 : ROPND) + 1024 * (4 * (j & 1) + w)));
   };
 
@@ -550,7 +391,7 @@ struct QSplitSeg {
   int8_t* ex;
   int64_t lds, ldd, ps, lde;
   int rows, cols, blk0;  // blk0: index of the segment's first 32 x 32 block in the launch
-  int pad;
+  int blocked;           // destination layout (h3p_index)
 };
 
 // one wave per 32 x 32 block: lane l loads row (l >> 3) + 8 q, columns 4 (l & 7) .. +3 (q = 0..3),
@@ -580,22 +421,13 @@ __global__ void __launch_bounds__(256) h3p_split_kernel(QSplitSeg one, const QSp
   const int e = h3p_exp_bits(wave_umax(m));
   const float sc = h3p_scale(e);
 #pragma unroll
-  for (int k = 0; k < 4; ++k) h3p_store4(s.dst, s.ps, (int64_t)(r0 + 8 * k) * s.ldd + c, v[k], sc);
+  for (int k = 0; k < 4; ++k) h3p_store4(s.dst, s.ps, h3p_index(r0 + 8 * k, c, s.ldd, s.blocked), v[k], sc);
   if (lane == 0) s.ex[(int64_t)br * s.lde + bc] = static_cast<int8_t>(e);
 }
 
-// kernel variant: 0 = two 32-deep stages (gemm_h3p_kernel), 1 = the 16-deep four-step ring
-// (gemm_h3p_ring_kernel).  HETSEQ_H3P_KERNEL=stage2|ring; set_h3p_variant for A/Bs.
-static int g_h3p_variant = [] {
-  const char* e = std::getenv("HETSEQ_H3P_KERNEL");
-  return e && e[0] == 's' ? 0 : e && e[0] == 'r' ? 1 : 0;
-}();
-
 template <bool TA, bool TB, int EPI>
 void q_launch(const QArgs& a, hipStream_t st) {
-  const dim3 grid((a.M / QT) * (a.N / QT) * a.ksplit), blk(256);
-  if (g_h3p_variant == 1) hipLaunchKernelGGL((gemm_h3p_ring_kernel<TA, TB, EPI>), grid, blk, 0, st, a);
-  else hipLaunchKernelGGL((gemm_h3p_kernel<TA, TB, EPI>), grid, blk, 0, st, a);
+  hipLaunchKernelGGL((gemm_h3p_kernel<TA, TB, EPI>), dim3((a.M / QT) * (a.N / QT) * a.ksplit), dim3(256), 0, st, a);
 }
 
 template <bool TA, bool TB>
@@ -624,15 +456,16 @@ int launch_gemm_h3p(int ta, int tb, int M, int N, int K, const void* A, int64_t 
                     int64_t lde_a, const void* B, int64_t ldb, int64_t b_ps, const int8_t* eb, int64_t lde_b, float* C,
                     int64_t ldc, const float* bias, int epi, float beta, float* aux, int64_t ldaux, float* part,
                     float* colsum, int colsum_acc, void* cp, int64_t ldcp, int64_t cp_ps, int8_t* ec, int64_t lde_c,
-                    int ksplit, float* slab, int64_t slab_floats, hipStream_t st) {
+                    int ksplit, float* slab, int64_t slab_floats, int ablk, int bblk, hipStream_t st) {
   ksplit = std::max(1, ksplit);
+  if ((ablk && lda % 32) || (bblk && ldb % 32)) return -1;
   if (M <= 0 || N <= 0 || K <= 0 || M % QT || N % QT || K % (QBK * ksplit) || K / ksplit / QBK > QMAXKT) return -1;
   if (ta && tb) return -1;
   auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
   if (!A || !B || !ea || !eb || !al16(A) || !al16(B) || lda % 8 || ldb % 8 || a_ps % 8 || b_ps % 8) return -1;
   if (epi < 0 || epi > 3 || (epi >= 1 && !bias) || (epi >= 2 && (!aux || beta != 0.f || ksplit > 1))) return -1;
   if (epi == 3 && !part != !colsum) return -1;
-  if (cp && (epi < 2 || !ec || ldcp % 2)) return -1;
+  if (cp && (epi < 2 || !ec || ldcp % 32)) return -1;  // (the result's planes are written blocked)
   if (epi < 2 && !C && ksplit == 1) return -1;
   if (epi >= 2 && !C && !cp) return -1;
   if (ksplit > 1 && (!slab || (int64_t)ksplit * M * N > slab_floats || (C && (N % 4 || ldc % 4 || !al16(C)))))
@@ -642,7 +475,7 @@ int launch_gemm_h3p(int ta, int tb, int M, int N, int K, const void* A, int64_t 
   if (spanA >= (1ll << 32) || spanB >= (1ll << 32)) return -1;
   QArgs a{static_cast<const uint16_t*>(A), ea, static_cast<const uint16_t*>(B), eb, lda, a_ps, lde_a, ldb, b_ps,
           lde_b, C, ldc, bias, aux, ldaux, part, static_cast<uint16_t*>(cp), ec, ldcp, cp_ps, lde_c, slab, M, N, K,
-          ksplit, beta};
+          ksplit, beta, ablk, bblk};
   const int rc = !ta && tb ? q_launch_epi<false, true>(ksplit > 1 ? 0 : epi, a, st)
                  : !ta   ? q_launch_epi<false, false>(ksplit > 1 ? 0 : epi, a, st)
                          : q_launch_epi<true, false>(ksplit > 1 ? 0 : epi, a, st);
@@ -658,10 +491,11 @@ int launch_gemm_h3p(int ta, int tb, int M, int N, int K, const void* A, int64_t 
 
 // fp32 [rows][cols] (row stride lds) -> h3p planes (row stride ldd, plane stride ps) + exponents
 int launch_h3p_split(const float* src, int64_t lds, int rows, int cols, void* dst, int64_t ldd, int64_t ps, int8_t* ex,
-                     int64_t lde, hipStream_t st) {
+                     int64_t lde, int blocked, hipStream_t st) {
   if (rows <= 0 || cols <= 0 || rows % 32 || cols % 32 || lds % 4 || ldd % 4 || ps % 4) return -1;
+  if (blocked && ldd % 32) return -1;
   if ((reinterpret_cast<uintptr_t>(src) & 15) || (reinterpret_cast<uintptr_t>(dst) & 7)) return -1;
-  QSplitSeg s{src, static_cast<uint16_t*>(dst), ex, lds, ldd, ps, lde, rows, cols, 0, 0};
+  QSplitSeg s{src, static_cast<uint16_t*>(dst), ex, lds, ldd, ps, lde, rows, cols, 0, blocked};
   const int total = (rows / 32) * (cols / 32);
   hipLaunchKernelGGL(h3p_split_kernel, dim3((total + 3) / 4), dim3(256), 0, st, s, nullptr, 1, total);
   return 0;
@@ -675,6 +509,3 @@ void launch_h3p_split_multi(const void* table, int nseg, int total, hipStream_t 
   hipLaunchKernelGGL(h3p_split_kernel, dim3((total + 3) / 4), dim3(256), 0, st, none,
                      static_cast<const QSplitSeg*>(table), nseg, total);
 }
-
-void set_h3p_variant(int v) { g_h3p_variant = v; }
-int h3p_variant() { return g_h3p_variant; }

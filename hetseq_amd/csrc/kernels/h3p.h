@@ -9,6 +9,11 @@
 //     with e = 14 - floor(log2 |max of the block|), so the block's largest element lands in
 //     [2^14, 2^15) (fp16's largest finite value is 65504) and every element down to 2^-18 of the
 //     BLOCK's maximum keeps 22 significant bits (the window is per 32 x 32 block, not per tensor).
+// Plane layout (per tensor): row-major ([R][ld], element (r, c) at r ld + c) or BLOCKED: the same
+// 32-row panels, each stored as ld / 32 consecutive 32 x 32 blocks of 2 KB (row-major 64-B rows
+// inside), element (r, c) at (r / 32) 32 ld + (c / 32) 1024 + (r % 32) 32 + c % 32.  A blocked 32-deep
+// K tile of a 128-wide GEMM operand is four whole 2-KB blocks in EITHER orientation, so the GEMM's
+// LDS-DMA reads full 128-B lines for k-contiguous operands too (row-major: 64 B of each row).
 // A product a * b is then hi_a hi_b + hi_a lo_b + lo_a hi_b (the dropped lo_a lo_b is ~2^-22 |ab|),
 // each fp16 x fp16 product exact in the fp32 accumulator: three fp16 MFMAs per fp32 product, with
 // the block factor 2^-(e_a + e_b) applied once per 32-deep K tile (gemm_h3p.hip).
@@ -51,5 +56,10 @@ HS_DEVICE void h3p_store4(uint16_t* __restrict__ pl, int64_t ps, int64_t i, cons
 }
 
 HS_DEVICE float h3p_scale(int e) { return __builtin_ldexpf(1.f, e); }
+
+// element index of (r, c) in a plane (layout above; ld a multiple of 32 when blocked)
+HS_DEVICE int64_t h3p_index(int64_t r, int64_t c, int64_t ld, int blocked) {
+  return blocked ? (r >> 5) * 32 * ld + (c >> 5) * 1024 + (r & 31) * 32 + (c & 31) : r * ld + c;
+}
 
 }  // namespace hs

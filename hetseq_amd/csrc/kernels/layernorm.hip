@@ -215,7 +215,7 @@ __global__ void __launch_bounds__(64 * kLnH3pWaves) ln_fwd_h3p_kernel(
 #pragma unroll
     for (int j = 0; j < RPW; ++j) {
       const int row = blockIdx.x * 32 + w * RPW + j;
-      h3p_store4(planes, ps, (int64_t)row * H + (k * 64 + lane) * 4, o[j][k], sc);
+      h3p_store4(planes, ps, h3p_index(row, (k * 64 + lane) * 4, H, 1), o[j][k], sc);  // blocked planes
     }
     if (w == 0 && (lane & 7) == 0) exps[(int64_t)blockIdx.x * (H / 32) + k * 8 + (lane >> 3)] = static_cast<int8_t>(e);
   }
@@ -489,7 +489,7 @@ __global__ void __launch_bounds__(64 * kLnH3pWaves) ln_bwd_h3p_kernel(
 #pragma unroll
     for (int j = 0; j < RPW; ++j) {
       const int row = blockIdx.x * 32 + w * RPW + j;
-      h3p_store4(planes, ps, (int64_t)row * H + (k * 64 + lane) * 4, da[j][k], sc);
+      h3p_store4(planes, ps, h3p_index(row, (k * 64 + lane) * 4, H, 1), da[j][k], sc);  // blocked planes
     }
     if (w == 0 && (lane & 7) == 0) exps[(int64_t)blockIdx.x * (H / 32) + k * 8 + (lane >> 3)] = static_cast<int8_t>(e);
   }

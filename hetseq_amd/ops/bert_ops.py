@@ -114,6 +114,7 @@ def ln_fwd(a, gamma, beta, eps=1e-12, bias=None, resid=None, p=0.0, mode=0, seed
 def ln_fwd_h3p(a, gamma, beta, eps, bias, resid, p, seed, off, outs, row0, hp, amax=None):
     """ln_fwd (bias-dropout-residual mode, fp32) that also writes y as h3p planes into ``hp`` (an
     ops.h3p.HP over the same rows): the next product's operand without a split pass."""
+    assert hp.blk, "producers write blocked planes"
     nslab, stride = 1, 0
     if a.dim() == 3:
         nslab, stride = a.shape[0], a.stride(0)
@@ -131,6 +132,7 @@ def ln_bwd_h3p(dy, z, mean, rstd, gamma, p, seed, off, hp, acc=None, side=False)
     """LN backward of the bias-dropout-residual LN: dz (fp32, returned) and da written only as h3p
     planes into ``hp``; parameter gradients (dgamma, dbeta, dbias) accumulated into ``acc`` (flat-store
     views; finalised on the weight-gradient stream with ``side``) or returned fresh."""
+    assert hp.blk, "producers write blocked planes"
     rows, H = dy.shape
     nb = rows // 32
     part = _colpart_buf(nb, H, dy.device)
@@ -273,6 +275,7 @@ def attn_bwd(qkv, mask, ctx, dctx, lse, B, S, NH, p, seed=0, off=0, bias=None, a
 def attn_fwd_h3p(qkv, mask, B, S, NH, p, seed, off, bias, outs, b0, hp):
     """attn_fwd on the h3 attention kernel that also writes ctx as h3p planes into ``hp`` (an
     ops.h3p.HP over the same rows): the output projection's operand without a split pass."""
+    assert hp.blk, "producers write blocked planes"
     ctx, lse, dmask = outs
     hip().attn_fwd_h3p(qkv.data_ptr(), mask.data_ptr(), bias.data_ptr() if bias is not None else 0, ctx.data_ptr(),
                        lse.data_ptr(), dmask.data_ptr() if dmask is not None else 0, B, S, NH, float(p), seed, off,
@@ -282,6 +285,7 @@ def attn_fwd_h3p(qkv, mask, B, S, NH, p, seed, off, bias, outs, b0, hp):
 
 def attn_bwd_h3p(qkv, mask, ctx, dctx, lse, B, S, NH, p, bias, hp):
     """attn_bwd on the h3 attention kernel that also writes dqkv as h3p planes into ``hp``."""
+    assert hp.blk, "producers write blocked planes"
     lse, dmask = lse
     dqkv = torch.empty_like(qkv)
     dbuf = torch.empty_like(lse)

@@ -30,17 +30,20 @@ EPI_NONE, EPI_BIAS, EPI_GELU, EPI_DGELU = 0, 1, 2, 3
 class HP(object):
     """h3p planes of an fp32 ``[rows, cols]`` matrix: ``planes`` [2, rows, ld] fp16 (hi, lo) and
     ``exps`` [rows/32, cols/32] int8.  ``rows`` may be a row window of a larger allocation
-    (:meth:`rows_slice`: ``offset`` elements into ``planes``, ``eoff`` into ``exps``)."""
+    (:meth:`rows_slice`: ``offset`` elements into ``planes``, ``eoff`` into ``exps``).  ``blk``: the
+    planes' layout -- True blocked (32 x 32 blocks of 2 KB per plane: h3p.h; what every producer
+    kernel writes), False row-major (the split pass and the GEMM read both; tests)."""
 
-    __slots__ = ("planes", "exps", "rows", "cols", "ld", "ps", "offset", "eoff", "lde")
+    __slots__ = ("planes", "exps", "rows", "cols", "ld", "ps", "offset", "eoff", "lde", "blk")
 
-    def __init__(self, planes, exps, rows, cols, ld=None, ps=None, offset=0, eoff=0, lde=None):
+    def __init__(self, planes, exps, rows, cols, ld=None, ps=None, offset=0, eoff=0, lde=None, blk=True):
         self.planes, self.exps = planes, exps
         self.rows, self.cols = rows, cols
         self.ld = cols if ld is None else ld
         self.ps = planes[0].numel() if ps is None else ps
         self.offset, self.eoff = offset, eoff
         self.lde = cols // BLK if lde is None else lde
+        self.blk = bool(blk)
 
     @property
     def shape(self):
@@ -64,35 +67,43 @@ class HP(object):
         """The planes of rows [r0, r1) (multiples of 32): a view, no copy."""
         assert r0 % BLK == 0 and r1 % BLK == 0 and 0 <= r0 < r1 <= self.rows
         return HP(self.planes, self.exps, r1 - r0, self.cols, self.ld, self.ps, self.offset + r0 * self.ld,
-                  self.eoff + (r0 // BLK) * self.lde, self.lde)
+                  self.eoff + (r0 // BLK) * self.lde, self.lde, self.blk)
+
+    def plane(self, p):
+        """Plane ``p`` (0 hi, 1 lo) as an fp16 ``[rows, cols]`` tensor (a copy when blocked)."""
+        flat = self.planes.reshape(-1).view(torch.float16)
+        off = self.offset + p * self.ps
+        if not self.blk:
+            return torch.as_strided(flat, (self.rows, self.cols), (self.ld, 1), off)
+        v = torch.as_strided(flat, (self.rows // BLK, self.cols // BLK, BLK, BLK), (BLK * self.ld, BLK * BLK, BLK, 1),
+                             off)
+        return v.permute(0, 2, 1, 3).reshape(self.rows, self.cols)
 
     def unsplit(self):
         """fp32 value (hi + lo) * 2^-e (tests / diagnostics)."""
-        flat = self.planes.reshape(-1).view(torch.float16)
-        hi = torch.as_strided(flat, (self.rows, self.cols), (self.ld, 1), self.offset).float()
-        lo = torch.as_strided(flat, (self.rows, self.cols), (self.ld, 1), self.offset + self.ps).float()
+        hi, lo = self.plane(0).float(), self.plane(1).float()
         e = torch.as_strided(self.exps.reshape(-1), (self.rows // BLK, self.cols // BLK), (self.lde, 1),
                              self.eoff).to(torch.float32)
         scale = torch.exp2(-e).repeat_interleave(BLK, 0).repeat_interleave(BLK, 1)
         return (hi.double() + lo.double()).float() * scale
 
 
-def empty(rows, cols, device):
+def empty(rows, cols, device, blk=True):
     """Uninitialised HP storage for a producer kernel to fill."""
     assert rows % BLK == 0 and cols % BLK == 0
     planes = torch.empty((2, rows, cols), dtype=torch.int16, device=device)
     exps = torch.empty((rows // BLK, cols // BLK), dtype=torch.int8, device=device)
-    return HP(planes, exps, rows, cols)
+    return HP(planes, exps, rows, cols, blk=blk)
 
 
-def split(x, out=None):
+def split(x, out=None, blk=True):
     """fp32 ``[rows, cols]`` (row-major, rows and cols multiples of 32) -> :class:`HP` (one pass:
-    one wave per 32 x 32 block)."""
+    one wave per 32 x 32 block); ``blk``: blocked plane layout (ignored when ``out`` is given)."""
     assert x.dtype == torch.float32 and x.dim() == 2 and x.stride(1) == 1
     rows, cols = x.shape
-    hp = out if out is not None else empty(rows, cols, x.device)
+    hp = out if out is not None else empty(rows, cols, x.device, blk)
     hip().h3p_split(x.data_ptr(), x.stride(0), rows, cols, hp.data_ptr(), hp.ld, hp.ps, hp.exps_ptr(), hp.lde,
-                    stream_handle())
+                    stream_handle(), int(hp.blk))
     return hp
 
 
@@ -100,7 +111,7 @@ class SplitTable(object):
     """One launch that splits many fp32 matrices (the GEMM weights after every update): the
     segment records live in device memory, built once for fixed addresses."""
 
-    FMT = "QQQqqqqiiii"  # QSplitSeg (gemm_h3p.hip): src, dst, ex, lds, ldd, ps, lde, rows, cols, blk0, pad
+    FMT = "QQQqqqqiiii"  # QSplitSeg (gemm_h3p.hip): src, dst, ex, lds, ldd, ps, lde, rows, cols, blk0, blocked
 
     def __init__(self, pairs, device):
         """``pairs``: [(fp32 2-D tensor, HP destination)]."""
@@ -111,7 +122,7 @@ class SplitTable(object):
             assert x.dtype == torch.float32 and x.stride(1) == 1 and x.shape == (hp.rows, hp.cols)
             assert x.data_ptr() % 16 == 0 and x.stride(0) % 4 == 0
             recs.append(struct.pack("<" + self.FMT, x.data_ptr(), hp.data_ptr(), hp.exps_ptr(), x.stride(0), hp.ld,
-                                    hp.ps, hp.lde, hp.rows, hp.cols, blk, 0))
+                                    hp.ps, hp.lde, hp.rows, hp.cols, blk, int(hp.blk)))
             blk += (hp.rows // BLK) * (hp.cols // BLK)
         raw = torch.frombuffer(bytearray(b"".join(recs)), dtype=torch.uint8)
         self.table = raw.to(device)
@@ -172,8 +183,7 @@ def census_stop():
 
 def window_stats(hp):
     """(nonzero elements, of them below the window, |x| mass below the window, total |x| mass)."""
-    flat = hp.planes.reshape(-1).view(torch.float16)
-    hi = torch.as_strided(flat, (hp.rows, hp.cols), (hp.ld, 1), hp.offset).float()
+    hi = hp.plane(0).float()
     x = hp.unsplit().double()
     nz = x != 0
     out = nz & (hi.abs() < 0.125)
@@ -214,6 +224,7 @@ def gemm(a, b, ta=False, tb=False, out=None, bias=None, epi=EPI_NONE, beta=0.0, 
         out = torch.empty((M, N), dtype=torch.float32, device=dev)
     if out is not None:
         assert out.dtype == torch.float32 and out.shape == (M, N) and out.stride(1) == 1
+    assert planes_out is None or planes_out.blk, "the GEMM epilogue writes blocked planes"
     rc = hip().gemm_h3p(int(ta), int(tb), M, N, K, a.data_ptr(), a.ld, a.ps, a.exps_ptr(), a.lde,
                         b.data_ptr(), b.ld, b.ps, b.exps_ptr(), b.lde,
                         out.data_ptr() if out is not None else 0, out.stride(0) if out is not None else N,
@@ -226,7 +237,7 @@ def gemm(a, b, ta=False, tb=False, out=None, bias=None, epi=EPI_NONE, beta=0.0, 
                         planes_out.exps_ptr() if planes_out is not None else 0,
                         planes_out.lde if planes_out is not None else 0,
                         int(ksplit), slab.data_ptr() if slab is not None else 0,
-                        slab.numel() if slab is not None else 0, stream_handle())
+                        slab.numel() if slab is not None else 0, stream_handle(), int(a.blk), int(b.blk))
     if rc != 0:
         raise ValueError("gemm_h3p: request not served (M=%d N=%d K=%d ta=%d tb=%d epi=%d ksplit=%d)"
                          % (M, N, K, ta, tb, epi, ksplit))

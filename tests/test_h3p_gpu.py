@@ -54,6 +54,41 @@ def test_split_roundtrip_and_exponents(cuda):
     assert torch.isnan(y2[100, 200]) and not torch.isfinite(y2[200, 300])
 
 
+def test_blocked_layout_split_matches_row_major(cuda):
+    """The blocked plane layout (32 x 32 blocks of 2 KB) holds bitwise the row-major planes' values,
+    and a row window of it is a view of the same blocks."""
+    from hetseq_amd.ops import h3p
+
+    g = torch.Generator(device=cuda)
+    g.manual_seed(5)
+    x = torch.randn((256, 384), device=cuda, generator=g) * torch.logspace(-8, 8, 384, device=cuda)
+    a, b = h3p.split(x), h3p.split(x, blk=True)
+    assert b.blk and not a.blk
+    for p in (0, 1):
+        assert torch.equal(a.plane(p), b.plane(p))
+    assert torch.equal(a.exps, b.exps)
+    assert not torch.equal(a.planes, b.planes)  # (the storage order does differ)
+    assert torch.equal(b.rows_slice(64, 160).unsplit(), a.unsplit()[64:160])
+
+
+@pytest.mark.parametrize("ta,tb,M,N,K,ks", [(0, 1, 512, 384, 768, 1), (0, 0, 256, 768, 1024, 2),
+                                            (1, 0, 384, 256, 2048, 4)])
+def test_gemm_h3p_layouts_bitwise(cuda, ta, tb, M, N, K, ks):
+    """Row-major and blocked operands, in all four layout pairs, give bitwise the same product (same
+    values staged, same order of every sum)."""
+    from hetseq_amd.ops import h3p
+
+    g = torch.Generator(device=cuda)
+    g.manual_seed(6 + M + K)
+    a = torch.randn((K, M) if ta else (M, K), device=cuda, generator=g)
+    b = torch.randn((N, K) if tb else (K, N), device=cuda, generator=g)
+    ref = h3p.gemm(h3p.split(a), h3p.split(b), ta, tb, ksplit=ks)
+    for ab in (False, True):
+        for bb in (False, True):
+            out = h3p.gemm(h3p.split(a, blk=ab), h3p.split(b, blk=bb), ta, tb, ksplit=ks)
+            assert torch.equal(out, ref), (ab, bb, (out - ref).abs().max().item())
+
+
 def _operands(ta, tb, M, N, K, data, dev, g):
     if data == "uniform":
         a = torch.rand((K, M) if ta else (M, K), device=dev, generator=g) * 2 - 1

@@ -1,5 +1,6 @@
 """Isolated timing of the BERT-base fp32 products: the in-kernel-split h3 engine (gemm.hip, NT=4,
-per-tensor scales) against the h3p engine (gemm_h3p.hip, pre-split block-scaled planes).
+per-tensor scales) against the h3p engine (gemm_h3p.hip, pre-split block-scaled planes; blocked
+plane layout, and row-major planes for comparison).
 
     python tools/bench_h3p.py [--json out.jsonl]
 
@@ -38,6 +39,9 @@ def timeit(fn, iters=20):
     return s.elapsed_time(e) / iters * 1e3  # us
 
 
+VARIANTS = [("rowmajor", False), ("h3p", True)]  # operand plane layouts
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--json", default=None)
@@ -51,41 +55,32 @@ def main():
         b = torch.randn((N, K) if tb else (K, N), device=dev) * 0.05
         out = torch.empty(M, N, device=dev)
         am = (G.amax_of(a), G.amax_of(b))
-        ha, hb = h3p.split(a), h3p.split(b)
+        ops = {False: (h3p.split(a), h3p.split(b)), True: (h3p.split(a, blk=True), h3p.split(b, blk=True))}
         ks_opts = [s for s in (1, 2, 4, 8) if K % (32 * s) == 0 and K // s >= 256 and K // s <= 4096]
-        best_old, best_new, best_ring = {}, {}, {}
-        hip = __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip()
+        best = {}
         for _ in range(args.rounds):
-            hip.set_h3p_variant(1)
-            for ks in ks_opts:
-                t = timeit(lambda: h3p.gemm(ha, hb, ta, tb, out=out, ksplit=ks))
-                best_ring[ks] = min(best_ring.get(ks, 1e9), t)
-            hip.set_h3p_variant(0)
             for ks in (0, 1, 2, 4):
                 if not G._hip_gemm(a, b, ta, tb, out, fp32="h3", ksplit=ks, amax=am):
                     continue
                 t = timeit(lambda: G._hip_gemm(a, b, ta, tb, out, fp32="h3", ksplit=ks, amax=am))
-                best_old[ks] = min(best_old.get(ks, 1e9), t)
-            for ks in ks_opts:
-                t = timeit(lambda: h3p.gemm(ha, hb, ta, tb, out=out, ksplit=ks))
-                best_new[ks] = min(best_new.get(ks, 1e9), t)
-        to, ko = min((v, k) for k, v in best_old.items())
-        tn, kn = min((v, k) for k, v in best_new.items())
-        tr, kr = min((v, k) for k, v in best_ring.items())
+                best[("h3", ks)] = min(best.get(("h3", ks), 1e9), t)
+            for vn, blk in VARIANTS:
+                ha, hb = ops[blk]
+                for ks in ks_opts:
+                    t = timeit(lambda: h3p.gemm(ha, hb, ta, tb, out=out, ksplit=ks))
+                    best[(vn, ks)] = min(best.get((vn, ks), 1e9), t)
         tf = lambda t: 3 * 2.0 * M * N * K / (t * 1e-6) / 1e12  # noqa: E731
-        r = {"name": name, "M": M, "N": N, "K": K, "ta": ta, "tb": tb, "h3_us": round(to, 1), "h3_ks": ko,
-             "h3p_us": round(tn, 1), "h3p_ks": kn, "h3_tf16": round(tf(to)), "h3p_tf16": round(tf(tn)),
-             "speedup": round(to / tn, 3), "h3p_by_ks": {k: round(v, 1) for k, v in best_new.items()},
-             "ring_us": round(tr, 1), "ring_ks": kr, "ring_tf16": round(tf(tr)), "ring_speedup": round(to / tr, 3),
-             "ring_by_ks": {k: round(v, 1) for k, v in best_ring.items()}}
+        r = {"name": name, "M": M, "N": N, "K": K, "ta": ta, "tb": tb}
+        for vn in ["h3"] + [v[0] for v in VARIANTS]:
+            t, k = min((best[key], key[1]) for key in best if key[0] == vn)
+            r[vn] = round(t, 1)
+            r[vn + "_ks"] = k
+            r[vn + "_tf16"] = round(tf(t))
+            r[vn + "_by_ks"] = {key[1]: round(best[key], 1) for key in best if key[0] == vn}
         rows.append(r)
         print(json.dumps(r), flush=True)
-    tot_o = sum(r["h3_us"] for r in rows if "half" not in r["name"])
-    tot_n = sum(r["h3p_us"] for r in rows if "half" not in r["name"])
-    tot_r = sum(r["ring_us"] for r in rows if "half" not in r["name"])
-    print(json.dumps({"layer_12_products_h3_us": round(tot_o, 1), "h3p_us": round(tot_n, 1),
-                      "speedup": round(tot_o / tot_n, 3), "ring_us": round(tot_r, 1),
-                      "ring_speedup": round(tot_o / tot_r, 3)}))
+    tot = {vn: round(sum(r[vn] for r in rows if "half" not in r["name"]), 1) for vn in ["h3"] + [v[0] for v in VARIANTS]}
+    print(json.dumps({"layer_12_products_us": tot}))
     if args.json:
         with open(args.json, "w") as f:
             for r in rows:

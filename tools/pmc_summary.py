@@ -16,6 +16,7 @@ import sqlite3
 
 
 def short(name, n=70):
+    name = name.replace("(anonymous namespace)::", "")
     name = re.sub(r"\(.*", "", name)
     return name if len(name) <= n else name[:n - 3] + "..."
 
@@ -36,6 +37,7 @@ def main():
     ap.add_argument("dbs", nargs="+")
     ap.add_argument("--match", default=None)
     ap.add_argument("--top", type=int, default=25)
+    ap.add_argument("--raw", action="store_true", help="also print every counter's mean per dispatch")
     a = ap.parse_args()
     counters = collections.defaultdict(dict)  # kernel -> counter -> mean per dispatch
     ndisp, dur = {}, {}
@@ -71,6 +73,8 @@ def main():
                     row[w.replace("SQ_", "").lower() + " %"] = 100.0 * cs[w] / cs["SQ_WAVE_CYCLES"]
         if "GRBM_GUI_ACTIVE" in cs:
             row["clock GHz"] = cs["GRBM_GUI_ACTIVE"] / 8 / d
+        if a.raw:
+            row.update({c: float(v) for c, v in cs.items()})
         rows.append(row)
     rows.sort(key=lambda r: -r["us"] * r["n"])
     cols = ["kernel", "n", "us"] + sorted({c for r in rows for c in r} - {"kernel", "n", "us"})
