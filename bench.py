@@ -594,6 +594,18 @@ _AB = {
     "lazyzero_off": lambda: setattr(__import__("hetseq_amd.controller", fromlist=["x"]), "_LAZY_ZERO", False),
     # fp32 product engine of the encoder layers: h3p (pre-split block-scaled planes) / h3 (in-kernel split)
     "eng_h3p": lambda: __import__("hetseq_amd.ops.gemm", fromlist=["x"]).set_fp32_mode("h3p"),
+    # staged update: the optimizer chunks on their own stream, overlapped with the next forward
+    "staged_on": lambda: setattr(_CTL[0].optimizer, "staged", _CTL[0]._staged_ok()),
+    "staged_off": lambda: (_CTL[0].store.params_ready(), setattr(_CTL[0].optimizer, "staged", False)),
+    # K slices of the h3p forward's N = 768 products (ops/bert_ops.py _H3P_KS_WO / _H3P_KS_W2)
+    "wo_ks1": lambda: setattr(__import__("hetseq_amd.ops.bert_ops", fromlist=["x"]), "_H3P_KS_WO", 1),
+    "wo_ks2": lambda: setattr(__import__("hetseq_amd.ops.bert_ops", fromlist=["x"]), "_H3P_KS_WO", 2),
+    "w2_ks1": lambda: setattr(__import__("hetseq_amd.ops.bert_ops", fromlist=["x"]), "_H3P_KS_W2", 1),
+    "w2_ks2": lambda: setattr(__import__("hetseq_amd.ops.bert_ops", fromlist=["x"]), "_H3P_KS_W2", 2),
+    "w2_ks4": lambda: setattr(__import__("hetseq_amd.ops.bert_ops", fromlist=["x"]), "_H3P_KS_W2", 4),
+    # waves per 32-row block of the h3p LayerNorm forward
+    "lnw8": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_ln_h3p_waves(8),
+    "lnw16": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_ln_h3p_waves(16),
     "eng_h3": lambda: __import__("hetseq_amd.ops.gemm", fromlist=["x"]).set_fp32_mode("h3"),
     # --emulate-world: workgroups per emulated collective (RCCL channels) and the emulated bus bandwidth
     "emu_ch4": lambda: _set_emul_channels(4),
@@ -635,9 +647,13 @@ def _host_phases(ctl):
     return acc
 
 
+_CTL = [None]  # the controller of an --ab run (variants that switch its state)
+
+
 def _ab_run(b, ctl, gen):
     import torch
 
+    _CTL[0] = ctl
     names = b.ab.split(",")
     times = {n: [] for n in names}
     for r in range(b.ab_rounds):

@@ -43,6 +43,10 @@ from hetseq_amd.runtime.flat import FlatParamStore
 
 # zero_grad clears only the gradient regions the next backward does not overwrite (HETSEQ_LAZY_ZERO=0: all)
 _LAZY_ZERO = os.environ.get("HETSEQ_LAZY_ZERO", "1") == "1"
+# staged update: the optimizer step runs chunk by chunk on its own stream, overlapped with the next
+# forward (optim/optimizers.py; one GPU, eager steps, models that declare update chunks).
+# HETSEQ_STAGED_UPDATE=0: the whole update before the next step.
+STAGED_UPDATE = os.environ.get("HETSEQ_STAGED_UPDATE", "1") == "1"
 
 LN2 = math.log(2)
 
@@ -162,11 +166,20 @@ class Controller(object):
     def _build_optimizer(self):
         params = list(filter(lambda p: p.requires_grad, chain(self.model.parameters())))
         self._optimizer = build_optimizer(self.args, params, self.store)
+        self._optimizer.staged = self._staged_ok()
         self._lr_scheduler = build_lr_scheduler(self.args, self._optimizer)
         self._lr_scheduler.step_update(0)
 
+    def _staged_ok(self):
+        """Staged (overlapped) update: one GPU (a data-parallel step's collectives and the update
+        would share hardware queues), eager steps (a HIP graph replays the whole update), a model
+        whose forward waits per chunk (runtime/flat.py set_chunks)."""
+        return (STAGED_UPDATE and self.cuda and self.store.chunks is not None and not getattr(self.args, "hip_graph", False)
+                and not (self.args.distributed_world_size > 1 or getattr(self.args, "force_ddp", False)))
+
     # ------------------------------------------------------------------ checkpoints
     def save_checkpoint(self, filename, extra_state):
+        self.store.params_ready()
         if distributed_utils.is_master(self.args):
             extra_state["train_meters"] = self.meters
             checkpoint_utils.save_state(filename, self.args, self.get_model().state_dict(), None, self.optimizer,

@@ -41,6 +41,7 @@ int launch_emb_fwd(int, const int64_t*, const int64_t*, const float*, const floa
                    float*, hipStream_t);
 int launch_emb_bwd(int, const void*, const float*, const float*, const float*, const float*, float*, float*, float*,
                    const int64_t*, float*, int, int, float, u64, u64, hipStream_t);
+void set_ln_h3p_waves(int w);
 int launch_ln_fwd_h3p(const void*, const float*, const void*, const float*, const float*, void*, float*, float*, float*,
                       int, int, float, float, u64, u64, int, int, int64_t, int, float*, void*, int64_t, int8_t*,
                       hipStream_t);
@@ -432,6 +433,7 @@ PYBIND11_MODULE(_hip, m) {
                              P(void*, pl), ps, P(int8_t*, ex)),
           "attn_bwd_h3p");
   }, "h3 attention backward also writing dqkv as h3p planes");
+  m.def("set_ln_h3p_waves", &set_ln_h3p_waves, "h3p LayerNorm forward: waves per 32-row block (8 or 16)");
   m.def("ln_fwd_h3p", [](i64 a, i64 bias, i64 resid, i64 gamma, i64 beta, i64 y, i64 z, i64 mean, i64 rstd, int rows,
                          int H, float eps, float p, u64 seed, u64 off, int mode, int nslab, i64 slab_stride, int row0,
                          i64 amax, i64 planes, i64 ps, i64 exps, i64 st) {

@@ -120,15 +120,15 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const T* __restrict__ a, co
 // the y values it still holds.  Same per-row arithmetic as ln_fwd_kernel (bitwise the same y).
 constexpr int kLnH3pWaves = 8;
 
-template <int NV, typename T>
-__global__ void __launch_bounds__(64 * kLnH3pWaves) ln_fwd_h3p_kernel(
+template <int NV, typename T, int WV>
+__global__ void __launch_bounds__(64 * WV) ln_fwd_h3p_kernel(
     const T* __restrict__ a, const float* __restrict__ bias, const T* __restrict__ resid,
     const float* __restrict__ gamma, const float* __restrict__ beta, T* __restrict__ y, float* __restrict__ zsave,
     float* __restrict__ mean_out, float* __restrict__ rstd_out, float eps, float p, uint64_t seed, uint64_t off, int mode,
     const uint64_t* __restrict__ seed_dev, int nslab, int64_t slab_stride, int row0, float* __restrict__ amax_y,
     uint16_t* __restrict__ planes, int64_t ps, int8_t* __restrict__ exps) {
-  constexpr int H = NV * 256, RPW = 32 / kLnH3pWaves;
-  __shared__ float red[kLnH3pWaves][NV * 8];
+  constexpr int H = NV * 256, RPW = 32 / WV;
+  __shared__ float red[WV][NV * 8];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const float scale = p < 1.f ? 1.0f / (1.0f - p) : 0.f;
   seed = resolve_seed(seed, seed_dev);
@@ -209,7 +209,7 @@ __global__ void __launch_bounds__(64 * kLnH3pWaves) ln_fwd_h3p_kernel(
   for (int k = 0; k < NV; ++k) {
     uint32_t m = 0u;
 #pragma unroll
-    for (int v = 0; v < kLnH3pWaves; ++v) m = max(m, __float_as_uint(red[v][k * 8 + (lane >> 3)]));
+    for (int v = 0; v < WV; ++v) m = max(m, __float_as_uint(red[v][k * 8 + (lane >> 3)]));
     const int e = h3p_exp_bits(m);
     const float sc = h3p_scale(e);
 #pragma unroll
@@ -651,14 +651,21 @@ void ln_fwd_launch(const void* a, const float* bias, const void* resid, const fl
                      row0, amax);
 }
 
+static int g_ln_h3p_waves = 16;  // waves per 32-row block of the h3p LN forward (A/B hook)
+
 template <int NV, typename T>
 void ln_fwd_h3p_launch(const void* a, const float* bias, const void* resid, const float* gamma, const float* beta,
                        void* y, float* zsave, float* mean, float* rstd, int rows, float eps, float p, uint64_t seed,
                        uint64_t off, int mode, int nslab, int64_t slab_stride, int row0, float* amax, uint16_t* planes,
                        int64_t ps, int8_t* exps, hipStream_t st) {
-  hipLaunchKernelGGL((ln_fwd_h3p_kernel<NV, T>), dim3(rows / 32), dim3(64 * kLnH3pWaves), 0, st, (const T*)a, bias,
-                     (const T*)resid, gamma, beta, (T*)y, zsave, mean, rstd, eps, p, seed, off, mode, g_seed_dev, nslab,
-                     slab_stride, row0, amax, planes, ps, exps);
+  if (g_ln_h3p_waves == 16)
+    hipLaunchKernelGGL((ln_fwd_h3p_kernel<NV, T, 16>), dim3(rows / 32), dim3(64 * 16), 0, st, (const T*)a, bias,
+                       (const T*)resid, gamma, beta, (T*)y, zsave, mean, rstd, eps, p, seed, off, mode, g_seed_dev, nslab,
+                       slab_stride, row0, amax, planes, ps, exps);
+  else
+    hipLaunchKernelGGL((ln_fwd_h3p_kernel<NV, T, 8>), dim3(rows / 32), dim3(64 * 8), 0, st, (const T*)a, bias,
+                       (const T*)resid, gamma, beta, (T*)y, zsave, mean, rstd, eps, p, seed, off, mode, g_seed_dev, nslab,
+                       slab_stride, row0, amax, planes, ps, exps);
 }
 
 template <int NV>
@@ -739,6 +746,8 @@ int launch_ln_fwd(int dtype, const void* a, const float* bias, const void* resid
   }
   return 0;
 }
+
+void set_ln_h3p_waves(int w) { hs::g_ln_h3p_waves = w; }
 
 // LayerNorm forward writing y also as h3p planes (fp32 only; rows a multiple of 32)
 int launch_ln_fwd_h3p(const void* a, const float* bias, const void* resid, const float* gamma, const float* beta,

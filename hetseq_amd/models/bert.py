@@ -595,6 +595,14 @@ class BertPreTrainedModel(nn.Module):
             m._hs_dtype = compute_dtype
             m._hs_wcache = None
         self._compute_dtype = compute_dtype
+        groups = self.update_groups()
+        if groups is not None and store is not None:
+            store.set_chunks(groups)
+
+    def update_groups(self):
+        """Parameter groups in the order the fused forward first reads them (the staged update's
+        chunks, runtime/flat.py set_chunks); None: no chunk-aware forward."""
+        return None
 
     def set_compute_dtype(self, dtype):
         for m in self.modules():
@@ -690,6 +698,10 @@ class BertModel(BertPreTrainedModel):
             return None, None
         from hetseq_amd.ops.bert_ops import LayerAmax
 
+        if not G.h3p_active(self.compute_dtype):
+            store = getattr(self, "_hs_store", None)
+            if store is not None:
+                store.params_ready()  # (every weight's |max| is measured now, before the first layer)
         Ws = [blk._weights() for blk in self.encoder.layer]
         # (h3p engine: the layers' products need no |max| -- their slots stay reserved, unmeasured)
         weights = [None if G.h3p_active(self.compute_dtype) else w for W in Ws
@@ -709,6 +721,18 @@ class BertModel(BertPreTrainedModel):
             plan.append(la)
         return pool, plan
 
+    def update_groups(self):
+        e = self.embeddings
+        return ([list(e.parameters())] + [list(blk.parameters()) for blk in self.encoder.layer]
+                + [list(self.pooler.parameters())])
+
+    def _param_ready(self, chunk):
+        """Staged update (runtime/flat.py): wait for chunk ``chunk`` of the flat store -- 0 the
+        embeddings, 1 + i encoder layer i, then the rest."""
+        store = getattr(self, "_hs_store", None)
+        if store is not None and store.chunks is not None:
+            store.param_ready(chunk)
+
     def fused_encoder(self, input_ids, token_type_ids, attention_mask, checkpoint_activations=False, amax=None):
         """Fused embeddings + encoder: the sequence output [B*S, H] in the compute dtype.  ``amax``:
         (pool, per-layer slot maps) from :meth:`_amax_plan` (h3 engine); planned here when None."""
@@ -718,6 +742,7 @@ class BertModel(BertPreTrainedModel):
         mask = attention_mask.to(torch.int64).contiguous()
         pool, plan = amax if amax is not None else self._amax_plan()
         self._h3p_refresh(B * S)
+        self._param_ready(0)
         range_push("embeddings")
         x = self.embeddings.fused(input_ids, token_type_ids, self.compute_dtype,
                                   amax=pool.act(0) if pool is not None else None)
@@ -731,6 +756,7 @@ class BertModel(BertPreTrainedModel):
                 if i == 1 and pool is not None:
                     pool.wait_rest()  # layers >= 1 read weight |max| measured on the side stream
                 range_push("layer%d" % i)
+                self._param_ready(1 + i)  # (before the layer forks its second half-batch chain)
                 x = blk.fused(x, mask, B, S, recompute=checkpoint_activations,
                               amax=plan[i] if plan is not None else None)
                 range_pop()
@@ -759,20 +785,56 @@ class BertModel(BertPreTrainedModel):
 
         cached = self.__dict__.get("_hs_h3p")
         store = getattr(self, "_hs_store", None)
-        if cached is None or cached[0] is not store or store is None:
-            pairs, per = [], []
+        if cached is None or cached["store"] is not store or store is None:
+            pairs, per, tabs = [], [], []
             for b in blks:
                 b.__dict__["_hs_h3p_cur"] = None
                 W = b._weights()
                 hp = SimpleNamespace(**{k: h3p.empty(getattr(W, k).shape[0], getattr(W, k).shape[1], dev)
                                         for k in ("wqkv", "wo", "w1", "w2")})
-                pairs += [(getattr(W, k), getattr(hp, k)) for k in ("wqkv", "wo", "w1", "w2")]
+                lp = [(getattr(W, k), getattr(hp, k)) for k in ("wqkv", "wo", "w1", "w2")]
+                pairs += lp
                 per.append(hp)
-            cached = (store, h3p.SplitTable(pairs, dev), per)
+                tabs.append(h3p.SplitTable(lp, dev))
+            cached = {"store": store, "all": h3p.SplitTable(pairs, dev), "per": per, "tabs": tabs,
+                      "stamp": [None] * len(blks)}
             self.__dict__["_hs_h3p"] = cached
-        cached[1].run()
-        for b, hp in zip(blks, cached[2]):
+            if store is not None and store.chunks is not None:
+                # every update re-splits layer i's weights right after updating them (on the updating
+                # stream, before chunk 1 + i's fence: runtime/flat.py add_update_hook)
+                for i in range(len(blks)):
+                    store.add_update_hook(1 + i, self._h3p_hook(cached, i))
+        # planes made for the current parameters are kept; the others are split now (the first
+        # forward, parameters changed outside an update, no store)
+        now = store.stamp() if store is not None else None
+        stale = [i for i, st in enumerate(cached["stamp"]) if now is None or st != now]
+        if stale:
+            if store is not None:
+                store.params_ready()
+            if len(stale) == len(blks):
+                cached["all"].run()
+            else:
+                for i in stale:
+                    cached["tabs"][i].run()
+            for i in stale:
+                cached["stamp"][i] = now
+        for b, hp in zip(blks, cached["per"]):
             b.__dict__["_hs_h3p_cur"] = hp
+
+    def _h3p_hook(self, cached, i):
+        store = cached["store"]
+
+        def hook():
+            from hetseq_amd.ops import gemm as G
+
+            if self.__dict__.get("_hs_h3p") is not cached:
+                return
+            if G.h3p_active(self.compute_dtype):
+                cached["tabs"][i].run()
+                cached["stamp"][i] = store.stamp()
+            else:
+                cached["stamp"][i] = None  # (another engine: re-split when h3p is next used)
+        return hook
 
     def fused_forward(self, input_ids, token_type_ids, attention_mask, checkpoint_activations=False):
         """Fused encoder + pooler: (sequence output [B*S, H], pooled [B, H])."""
@@ -792,6 +854,7 @@ def _flush_lazy_grads(module):
     now, since autograd -- not those writers -- will accumulate into them."""
     store = getattr(module, "_hs_store", None)
     if store is not None:
+        store.params_ready()  # (this forward reads parameters outside the staged-update chunks)
         store.flush_lazy()
 
 
@@ -819,6 +882,18 @@ class BertForPreTraining(BertPreTrainedModel):
             return mlm_scores, nsp_scores
         return (_xent(mlm_scores.reshape(-1, self.config.vocab_size), masked_lm_labels.reshape(-1), -1)
                 + _xent(nsp_scores.reshape(-1, 2), next_sentence_label.reshape(-1), -1))
+
+    def update_groups(self):
+        """Embeddings, each encoder layer, then the pooler and heads (the tied decoder weight is the
+        word embedding: chunk 0)."""
+        b = self.bert
+        seen = set()
+        groups = []
+        for ps in b.update_groups()[:-1] + [list(b.pooler.parameters()) + list(self.cls.parameters())]:
+            g = [p for p in ps if id(p) not in seen]
+            seen.update(id(p) for p in g)
+            groups.append(g)
+        return groups
 
     def _mlm_weights(self):
         t = self.cls.predictions.transform
@@ -871,6 +946,10 @@ class BertForPreTraining(BertPreTrainedModel):
             meta["grad_sink"] = lambda: [store.grad_view(q) for q in params]
             meta["store"] = store
             store.cover(store.grad_view(pred.decoder.weight))  # the tied decoder's gradient store (lazy zero_grad)
+            if store.chunks is not None:
+                store.param_ready(len(store.chunks) - 1)  # the heads' chunk (and the deferred zero_grad)
+        if pool is not None:
+            pool.measure_deferred()  # (h3p engine: the head weights' |max|, now that they are current)
         return FusedPreTrainingLoss.apply(seq2d, labels.reshape(-1).contiguous(), nsp_label.reshape(-1).contiguous(),
                                           meta, *params)
 

@@ -850,12 +850,12 @@ class AmaxPool(object):
         self.rest = None
         from hetseq_amd.runtime import streams
 
+        self._deferred = None
         first = next((i for i, w in enumerate(weights) if w is not None), len(weights))
-        if first > 0:  # leading reserved slots (h3p engine layers): measure only the rest, in line
-            rest = [w for w in weights[first:]]
+        if first > 0:  # leading reserved slots (h3p engine layers): the rest is measured by
+            rest = [w for w in weights[first:]]  # measure_deferred(), just before its consumer
             if rest and all(w is not None for w in rest):
-                base, tab, nblk = _seg_table(rest)
-                hip().amax_seg(base, tab.data_ptr(), nblk, self.ptr + 4 * SLOT_FLOATS * first, stream_handle())
+                self._deferred = (_seg_table(rest), first)
             return
         if 0 < split < len(weights) and _SPLIT_WEIGHT_AMAX and streams.enabled() and self.buf.is_cuda:
             # weights [0, split) now; the rest on the side stream, beside the first layer's work
@@ -872,6 +872,14 @@ class AmaxPool(object):
         elif weights:
             base, tab, nblk = _seg_table(weights)
             hip().amax_seg(base, tab.data_ptr(), nblk, self.ptr, stream_handle())
+
+    def measure_deferred(self):
+        """Measure the weights after the leading reserved slots (the pre-training head's), on the
+        current stream -- called by their consumer once they are current (a staged update)."""
+        if self._deferred is not None:
+            (base, tab, nblk), first = self._deferred
+            self._deferred = None
+            hip().amax_seg(base, tab.data_ptr(), nblk, self.ptr + 4 * SLOT_FLOATS * first, stream_handle())
 
     def wait_rest(self):
         """The current stream waits for the side-stream part of the weight |max| (no-op without one)."""

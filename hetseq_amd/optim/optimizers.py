@@ -36,6 +36,23 @@ def _as_tuple(x):
     return ast.literal_eval(x) if isinstance(x, str) else tuple(x)
 
 
+_UPDATE_STREAMS: dict = {}
+
+
+def update_stream(device):
+    """The stream a staged update runs on (one per device, process lifetime).  A 1-GPU step uses
+    the compute, weight-gradient and copy streams, so this is the fourth and gets a hardware queue
+    of its own (GPU_MAX_HW_QUEUES = 4, runtime/streams.py reserve)."""
+    from hetseq_amd.runtime import streams
+
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    st = _UPDATE_STREAMS.get(idx)
+    if st is None:
+        st = streams._new_stream(idx)
+        _UPDATE_STREAMS[idx] = st
+    return st
+
+
 class _Optimizer(object):
     STATE_KEYS = ()
 
@@ -161,13 +178,42 @@ class _Optimizer(object):
         else:
             self.store.flush_lazy()
             gm = self._grad_multiplier()
-            if self.store.param.is_cuda:
+            self.store.bump()
+            if self._staged_now():
+                self._step_staged(gm)
+            elif self.store.param.is_cuda:
                 self._step_hip(gm)
+                self.store.run_hooks()
             else:
                 self._step_cpu(gm)
+                self.store.run_hooks()
         self._mult = None
         self._norm_ready = False
         return loss
+
+    # ------------------------------------------------------------ staged update
+    # staged = True (the controller's choice: one GPU, eager steps, a model that declared update
+    # chunks): step() runs the update chunk by chunk on update_stream(), recording a fence per chunk
+    # after the chunk's update hooks; the next forward waits for each chunk just before it reads it
+    # (runtime/flat.py param_ready), so the update overlaps that forward instead of preceding it.
+    staged = False
+    supports_staged = False
+
+    def _staged_now(self):
+        return (self.staged and self.supports_staged and self.store.chunks is not None and self.store.param.is_cuda
+                and self._hyper is None and not torch.cuda.is_current_stream_capturing())
+
+    def _step_staged(self, gmul):
+        s = self.store
+        st = update_stream(s.device)
+        st.wait_stream(torch.cuda.current_stream(s.device))  # the gradients, norm and multiplier
+        with torch.cuda.stream(st):
+            for i, (lo, hi) in enumerate(s.chunks):
+                self._step_hip(gmul, lo, hi)
+                s.run_hooks(i)
+                ev = torch.cuda.Event()
+                ev.record(st)
+                s._fences[i] = ev
 
     def zero_grad(self, lazy=False):
         if self.store is not None:
@@ -184,6 +230,8 @@ class _Optimizer(object):
             yield buf[off : off + p.numel()].view(p.shape)
 
     def state_dict(self):
+        if self.store is not None:
+            self.store.params_ready()  # (a staged update may still be writing the moments)
         groups = []
         for g in self.param_groups:
             d = {k: v for k, v in g.items() if k != "params"}
@@ -250,6 +298,7 @@ class _Adam(_Optimizer):
         return {k: v for k, v in self.defaults().items() if k != "amsgrad"}
 
     supports_device_hyper = True
+    supports_staged = True
 
     def _coeffs(self):
         g = self.param_groups[0]
@@ -262,13 +311,16 @@ class _Adam(_Optimizer):
         lr, _, _, _, _, step_size = self._coeffs()
         return [lr, step_size, 0.0, 0.0]
 
-    def _step_hip(self, gmul):
+    def _step_hip(self, gmul, lo=0, hi=None):
+        """The fused update of elements [lo, hi) of the flat buffers (default: all)."""
         lr, b1, b2, eps, wd, step_size = self._coeffs()
         s = self.store
-        shadow = s.shadow.data_ptr() if s.shadow is not None else 0
-        hip().adam_flat(s.param.data_ptr(), s.grad.data_ptr(), self._state["exp_avg"].data_ptr(),
-                        self._state["exp_avg_sq"].data_ptr(), shadow, s.numel, gmul.data_ptr(), lr, b1, b2, eps, wd,
-                        step_size, stream_handle(), self._hyper.dev.data_ptr() if self._hyper is not None else 0)
+        hi = s.numel if hi is None else hi
+        shadow = s.shadow.data_ptr() + lo * s.shadow.element_size() if s.shadow is not None else 0
+        hip().adam_flat(s.param.data_ptr() + 4 * lo, s.grad.data_ptr() + 4 * lo,
+                        self._state["exp_avg"].data_ptr() + 4 * lo, self._state["exp_avg_sq"].data_ptr() + 4 * lo,
+                        shadow, hi - lo, gmul.data_ptr(), lr, b1, b2, eps, wd, step_size, stream_handle(),
+                        self._hyper.dev.data_ptr() if self._hyper is not None else 0)
 
     def _step_cpu(self, gmul):
         lr, b1, b2, eps, wd, step_size = self._coeffs()

@@ -114,6 +114,7 @@ class FlatDDP(torch.nn.Module):
                     self.comm.broadcast(store.param, src=0)
                 else:
                     dist.broadcast(store.param, src=0, group=self.process_group)
+            store.bump()
             store.sync_shadow()
 
     def _reset_state(self):

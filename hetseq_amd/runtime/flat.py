@@ -33,6 +33,14 @@ def _align(n, a=ALIGN):
     return (n + a - 1) // a * a
 
 
+def bisect_chunk(chunks, off):
+    """Index of the (lo, hi) range of ``chunks`` holding element ``off`` (-1: none)."""
+    import bisect
+
+    i = bisect.bisect_right([lo for lo, _ in chunks], off) - 1
+    return i if i >= 0 and off < chunks[i][1] else -1
+
+
 class FlatParamStore(object):
     def __init__(self, module, device=None, shadow_dtype=None):
         named = OrderedDict()
@@ -176,6 +184,22 @@ class FlatParamStore(object):
         return self._zero_tab
 
     def zero_grad(self, lazy=False):
+        if self.staged_pending():
+            # the staged update still reads the gradients: clear them on its stream, after it, and
+            # make the LAST chunk's fence cover the clearing (the forward waits for that fence before
+            # the backward that writes them; params_ready waits for everything)
+            from hetseq_amd.optim.optimizers import update_stream
+
+            st = update_stream(self.device)
+            with torch.cuda.stream(st):
+                self._zero_now(lazy)
+                ev = torch.cuda.Event()
+                ev.record(st)
+            self._fences[-1] = ev
+            return
+        self._zero_now(lazy)
+
+    def _zero_now(self, lazy):
         if (lazy and self._cover and self.grad.is_cuda and self.numel % 4 == 0
                 and not torch.cuda.is_current_stream_capturing()):
             from hetseq_amd.ops._C import hip, stream_handle
@@ -236,6 +260,97 @@ class FlatParamStore(object):
             for off, n in list(self._pending.items()):
                 self.grad[off:off + n].zero_()
             self._pending = None
+
+    # ------------------------------------------------------------ staged update
+    # The optimizer can run an update chunk by chunk on a stream of its own (optim/optimizers.py,
+    # ``staged``), overlapped with the next forward: chunk i's parameters -- and what an update hook
+    # derives from them on that stream (the h3p weight planes) -- may be read once the forward has
+    # waited for chunk i's fence (param_ready).  Chunks are set by the model, in the order its
+    # forward first reads them (BertForPreTraining: embeddings, each encoder layer, the heads).
+    chunks = None   # [(lo, hi)] covering [0, numel), ascending
+    _fences = None  # per chunk: an event recorded after its update (None: nothing pending)
+    _hooks = None   # per chunk: [fn()] run on the updating stream after the chunk's update
+
+    def set_chunks(self, groups):
+        """Chunk boundaries from groups of parameters (each group contiguous in the buffer, groups
+        in buffer order).  Returns False (staging unavailable) if they do not tile the buffer."""
+        ranges = []
+        for ps in groups:
+            ps = [p for p in ps if id(p) in self.offsets]
+            if not ps:
+                continue
+            lo = min(self.offsets[id(p)] for p in ps)
+            hi = max(self.offsets[id(p)] + p.numel() for p in ps)
+            ranges.append((lo, hi))
+        if not ranges:
+            return False
+        ranges.sort()
+        # extend each range to the next one's start (alignment gaps), the first to 0, the last to numel
+        tiled = []
+        for i, (lo, hi) in enumerate(ranges):
+            nlo = 0 if i == 0 else tiled[-1][1]
+            nhi = ranges[i + 1][0] if i + 1 < len(ranges) else self.numel
+            if lo < nlo or hi > nhi or nlo % ALIGN or nhi % ALIGN:
+                return False
+            tiled.append((nlo, nhi))
+        covered = sum(hi - lo for lo, hi in tiled)
+        if covered != self.numel or sum(p.numel() for p in self.params) > covered:
+            return False
+        owners = [bisect_chunk(tiled, self.offsets[id(p)]) for p in self.params]
+        if any(o < 0 for o in owners):
+            return False
+        self.chunks = tiled
+        self._fences = [None] * len(tiled)
+        self._hooks = [[] for _ in tiled]
+        return True
+
+    def chunk_of(self, p):
+        return bisect_chunk(self.chunks, self.offsets[id(p)]) if self.chunks else -1
+
+    def add_update_hook(self, chunk, fn):
+        """Run ``fn()`` on the updating stream after every update of ``chunk`` (every chunk's
+        hooks also run, in chunk order, after an unstaged update)."""
+        self._hooks[chunk].append(fn)
+
+    def run_hooks(self, chunk=None):
+        if self._hooks is None:
+            return
+        for i in (range(len(self._hooks)) if chunk is None else (chunk,)):
+            for fn in self._hooks[i]:
+                fn()
+
+    # Bumped by every update that changes ``param`` through raw kernels (optimizer steps, the
+    # data-parallel broadcast): derived copies (h3p weight planes) are current iff made at this
+    # epoch and at the tensor's version (torch ops bump that).
+    epoch = 0
+
+    def bump(self):
+        self.epoch += 1
+
+    def stamp(self):
+        """The state a derived copy of the parameters is current for."""
+        return (self.epoch, self.param._version)
+
+    def staged_pending(self):
+        return self._fences is not None and any(e is not None for e in self._fences)
+
+    def param_ready(self, chunk):
+        """The current stream waits for ``chunk``'s staged update (no-op when none is pending)."""
+        if self._fences is not None and 0 <= chunk < len(self._fences) and self._fences[chunk] is not None:
+            torch.cuda.current_stream(self.device).wait_event(self._fences[chunk])
+            from hetseq_amd.runtime import streams
+
+            other = streams.chain_stream()  # (a half-batch chain forked once, without per-layer forks)
+            if other is not None:
+                other.wait_event(self._fences[chunk])
+            self._fences[chunk] = None
+
+    def params_ready(self):
+        """The current stream waits for every pending staged update (any reader that is not a
+        chunk-aware forward: checkpoints, evaluation, unfused paths, graph capture)."""
+        if self._fences is not None:
+            for i in range(len(self._fences)):
+                self.param_ready(i)
 
     def sync_shadow(self):
         if self.shadow is None:

@@ -171,6 +171,11 @@ def chain_join(device):
     _chain["keep"].clear()
 
 
+def chain_stream():
+    """The forked second half-batch chain's stream (None outside an open chain)."""
+    return _chain["forked"]
+
+
 def chain_keep(*tensors):
     """Keep tensors the second chain reads alive until it is joined (no-op outside a chain)."""
     if _chain["forked"] is not None:

@@ -414,6 +414,52 @@ def test_bert_base_trajectory_50_updates(cuda, engine):
     print("BERT-base 50-update trajectory (%s): worst loss rel diff %.3g" % (engine, worst))
 
 
+@pytest.mark.parametrize("engine", ["h3p", "h3"])
+def test_staged_update_matches_unstaged(cuda, engine):
+    """The staged update (optimizer chunks on their own stream overlapped with the next forward,
+    per-layer h3p weight planes re-split by update hooks, zero_grad queued behind the update) trains
+    bitwise like the unstaged one: same losses, parameters and moments after 6 steps, dropout on,
+    half-batch forward chains, gradient scale and clipping as the controller applies them."""
+    from argparse import Namespace
+
+    from hetseq_amd.ops import gemm as G
+    from hetseq_amd.optim.optimizers import _Adam
+    from hetseq_amd.runtime.flat import FlatParamStore
+
+    G.set_fp32_mode(engine)
+    runs = []
+    for staged in (False, True):
+        model, cfg = _tiny(cuda)
+        model.train()
+        model.max_predictions_per_seq = 10
+        store = FlatParamStore(model)
+        model.attach_store(store, torch.float32)
+        assert store.chunks is not None and len(store.chunks) == cfg.num_hidden_layers + 2
+        opt = _Adam(Namespace(lr=[1e-3], adam_betas="(0.9,0.999)", adam_eps=1e-8, weight_decay=0.01),
+                    list(model.parameters()), store)
+        opt.staged = staged
+        b = _batch(cuda, 16, 64, cfg.vocab_size)
+        assert model.bert._can_fuse(b[0])
+        losses = []
+        for step in range(6):
+            torch.manual_seed(100 + step)  # (the dropout seeds)
+            opt.zero_grad(lazy=True)
+            loss = model(*b)
+            loss.backward()
+            opt.multiply_grads(0.5)
+            opt.clip_grad_norm(1.0)
+            opt.step()
+            assert store.staged_pending() == staged
+            losses.append(loss.detach().clone())
+        sd = opt.state_dict()  # (waits for the staged update)
+        assert not store.staged_pending()
+        torch.cuda.synchronize()
+        runs.append((torch.stack(losses), store.param.clone(), opt._state["exp_avg"].clone(),
+                     opt._state["exp_avg_sq"].clone(), sd["state"][0]["exp_avg"].clone()))
+    for x, y in zip(runs[0], runs[1]):
+        assert torch.equal(x, y), (x - y).abs().max().item()
+
+
 def test_lamb_hip_step_matches_cpu_math(cuda):
     """The fused LAMB kernel (per-tensor trust ratios over the flat store) against the
     _step_cpu math on identical copies: parameters and both moments over several steps."""

@@ -87,3 +87,19 @@ def test_launch_wrappers_do_not_clear_pending_errors():
         assert "check(" in fn or "check_launch(" in fn, name
         checked += 1
     assert checked >= 30, checked
+
+
+def test_every_in_tree_module_links():
+    """Every built in-tree extension resolves all of its symbols at load time (RTLD_NOW): a binding
+    declared at one namespace and defined at another is an undefined symbol that only a GPU box's
+    import would otherwise find."""
+    import ctypes
+    import glob
+
+    from hetseq_amd.csrc import build
+
+    mods = glob.glob(os.path.join(os.path.dirname(build.HERE), "_*.so"))
+    if not mods:
+        pytest.skip("no built extension in the tree")
+    for so in mods:
+        ctypes.CDLL(so, mode=os.RTLD_NOW | os.RTLD_LOCAL)
