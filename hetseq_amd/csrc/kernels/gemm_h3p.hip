@@ -35,8 +35,11 @@
 // Epilogues: fp32 C (+ bias) (+ beta C); split-K fp32 slabs (summed by splitk_reduce_kernel, or by
 // the consumer); GELU (pre-activation kept in aux) and dGELU (column partials of the bias
 // gradient), each optionally writing its output as blocked h3p planes for the next GEMM.
-// (Round 5 measured a two-stage 32-deep loop -- one vmcnt(0) + barrier per tile -- 14 % slower over
-// the BERT layer's twelve products and removed it: tools/bench_h3p.py, profiles/r5_fp32_pmc.md.)
+// (Round 5 measured and removed two alternatives, tools/bench_h3p.py / profiles/r5_fp32_pmc.md: a
+// two-stage 32-deep loop -- one vmcnt(0) + barrier per tile -- 14 % slower over the BERT layer's
+// twelve products; three workgroups per CU -- a three-step ring, one fragment register set read at
+// each step's start, factors per step, 168 VGPRs -- 14 % slower: the exposed fragment reads and the
+// per-step FMAs cost more than the third resident tile saves on the 576- / 768-tile grids.)
 #include <algorithm>
 #include <cstdlib>
 

@@ -601,7 +601,7 @@ def _layer_forward(x, mask, W, cfg, save, am=None):
 # tile grids (48-96 tiles per half-batch chain) would leave most of the chip idle; their slabs go
 # straight into the LayerNorm forward (no reduce pass).
 _H3P_KS_WO = int(os.environ.get("HETSEQ_H3P_KS_WO", "2"))
-_H3P_KS_W2 = int(os.environ.get("HETSEQ_H3P_KS_W2", "4"))
+_H3P_KS_W2 = int(os.environ.get("HETSEQ_H3P_KS_W2", "2"))
 
 
 class _OneChain(object):

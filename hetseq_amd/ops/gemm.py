@@ -42,7 +42,7 @@ _MODE = os.environ.get("HETSEQ_GEMM", "auto")
 # h3p: the encoder layers' products on pre-split block-scaled planes (ops/h3p.py, gemm_h3p.hip); every
 # other fp32 product (the pre-training heads, standalone calls) on the h3 engine (dtype code 4)
 _FP32_DT = {"native": 0, "x6": 2, "x3": 3, "h3": 4, "h3p": 4}
-_FP32 = os.environ.get("HETSEQ_FP32_GEMM", "h3")
+_FP32 = os.environ.get("HETSEQ_FP32_GEMM", "h3p")
 FP32_DEFAULT = _FP32
 assert _FP32 in _FP32_DT, "HETSEQ_FP32_GEMM must be one of native|x6|x3|h3|h3p"
 SPLIT_ENGINES = ("x6", "h3", "h3p")  # the fp32-level split engines (x3 is a benchmarking variant)

@@ -39,7 +39,7 @@ def timeit(fn, iters=20):
     return s.elapsed_time(e) / iters * 1e3  # us
 
 
-VARIANTS = [("rowmajor", False), ("h3p", True)]  # operand plane layouts
+VARIANTS = [("h3p", None)]
 
 
 def main():
@@ -55,7 +55,7 @@ def main():
         b = torch.randn((N, K) if tb else (K, N), device=dev) * 0.05
         out = torch.empty(M, N, device=dev)
         am = (G.amax_of(a), G.amax_of(b))
-        ops = {False: (h3p.split(a), h3p.split(b)), True: (h3p.split(a, blk=True), h3p.split(b, blk=True))}
+        ha, hb = h3p.split(a), h3p.split(b)
         ks_opts = [s for s in (1, 2, 4, 8) if K % (32 * s) == 0 and K // s >= 256 and K // s <= 4096]
         best = {}
         for _ in range(args.rounds):
@@ -64,8 +64,7 @@ def main():
                     continue
                 t = timeit(lambda: G._hip_gemm(a, b, ta, tb, out, fp32="h3", ksplit=ks, amax=am))
                 best[("h3", ks)] = min(best.get(("h3", ks), 1e9), t)
-            for vn, blk in VARIANTS:
-                ha, hb = ops[blk]
+            for vn, _ in VARIANTS:
                 for ks in ks_opts:
                     t = timeit(lambda: h3p.gemm(ha, hb, ta, tb, out=out, ksplit=ks))
                     best[(vn, ks)] = min(best.get((vn, ks), 1e9), t)
