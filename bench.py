@@ -91,6 +91,8 @@ def parse():
     p.add_argument("--emulate-busbw", type=float, default=400.0, metavar="GB/s",
                    help="bus bandwidth of the emulated ring collectives (per-rank received bytes / time)")
     p.add_argument("--emulate-latency-us", type=float, default=12.0, help="fixed cost per emulated collective")
+    p.add_argument("--no-shard-optimizer", action="store_true",
+                   help="data parallel: every rank runs the whole Adam update (default: sharded, parallel/zero.py)")
     p.add_argument("--no-sparse-tables", action="store_true",
                    help="data parallel: all-reduce the embedding tables densely in the last bucket (no sparse row exchange)")
     p.add_argument("--comm-channels", type=int, default=None,
@@ -244,6 +246,8 @@ def run_rank(b):
         argv += ["--comm-channels", str(b.comm_channels)]
     if b.no_sparse_tables:
         argv.append("--no-sparse-embedding-exchange")
+    if b.no_shard_optimizer:
+        argv += ["--shard-optimizer", "off"]
     if b.emulate_world and b.emulate_world > 1:
         argv += ["--emulate-world", str(b.emulate_world)]
     if b.hip_graph:

@@ -60,7 +60,10 @@ def save_checkpoint(args, controller, epoch_itr, val_loss, end_of_epoch=None):
     prev_best = getattr(save_checkpoint, "best", val_loss)
     if val_loss is not None:
         save_checkpoint.best = max(val_loss, prev_best) if higher else min(val_loss, prev_best)
-    if args.no_save or not distributed_utils.is_master(args):
+    if args.no_save:
+        return
+    controller.consolidate_optimizer()  # (every rank: the sharded optimizer's collective gather)
+    if not distributed_utils.is_master(args):
         return
     clock = meters_mod.StopwatchMeter()
     clock.start()

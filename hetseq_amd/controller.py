@@ -123,7 +123,8 @@ class Controller(object):
                                               comm_engine=getattr(self.args, "comm_engine", "auto"),
                                               timeout_s=getattr(self.args, "collective_timeout", 1800.0),
                                               sparse_embedding=sparse, sparse_capacity=cap,
-                                              plan_world=getattr(self.args, "emulate_world", None))
+                                              plan_world=getattr(self.args, "emulate_world", None),
+                                              shard_optimizer=self._shard_ok())
             else:
                 self._wrapped_model = self._model
                 if self.args.distributed_world_size > 1 and dist.is_initialized() and self.args.use_bmuf:
@@ -170,14 +171,31 @@ class Controller(object):
         self._lr_scheduler = build_lr_scheduler(self.args, self._optimizer)
         self._lr_scheduler.step_update(0)
 
+    def _shard_ok(self):
+        """Sharded optimizer (parallel/zero.py): data-parallel Adam runs (the flat-store update with a
+        range form), eager steps, no BMUF; --shard-optimizer off disables it."""
+        return (getattr(self.args, "shard_optimizer", "auto") == "auto" and getattr(self.args, "optimizer", "adam") == "adam"
+                and not getattr(self.args, "hip_graph", False) and not self.args.use_bmuf)
+
     def _staged_ok(self):
-        """Staged (overlapped) update: one GPU (a data-parallel step's collectives and the update
-        would share hardware queues), eager steps (a HIP graph replays the whole update), a model
-        whose forward waits per chunk (runtime/flat.py set_chunks)."""
-        return (STAGED_UPDATE and self.cuda and self.store.chunks is not None and not getattr(self.args, "hip_graph", False)
-                and not (self.args.distributed_world_size > 1 or getattr(self.args, "force_ddp", False)))
+        """Staged (overlapped) update: eager steps (a HIP graph replays the whole update) of a model
+        whose forward waits per chunk (runtime/flat.py set_chunks), on one GPU (its own update stream)
+        or with the sharded data-parallel update on the native engine (the update and the chunks'
+        all-gathers on the comm stream); a data-parallel step's collectives and a fifth stream would
+        share hardware queues."""
+        if not (STAGED_UPDATE and self.cuda and self.store.chunks is not None and not getattr(self.args, "hip_graph", False)):
+            return False
+        if not (self.args.distributed_world_size > 1 or getattr(self.args, "force_ddp", False)):
+            return True
+        m = self.model
+        return getattr(m, "shard", None) is not None and getattr(m, "comm", None) is not None
 
     # ------------------------------------------------------------------ checkpoints
+    def consolidate_optimizer(self):
+        """Every rank, before the master's save: the sharded optimizer's state gathered whole."""
+        if self._optimizer is not None:
+            self._optimizer.consolidate()
+
     def save_checkpoint(self, filename, extra_state):
         self.store.params_ready()
         if distributed_utils.is_master(self.args):

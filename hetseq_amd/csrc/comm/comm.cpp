@@ -213,6 +213,53 @@ class Comm {
     }
   }
 
+  // Sharded update (parallel/zero.py): in-place reduce-scatter of [ptr, ptr + total) -- rank r keeps
+  // the sum of piece r, [ptr + r total / n, ...) -- on the comm stream after every producer stream's work
+  // so far; and the in-place all-gather of the updated pieces (each rank's piece r to every rank).
+  // `total` is a multiple of the rank count.  Emulated: the bytes one rank of the ring receives,
+  // (W-1)/W of the region either way.
+  void reduce_scatter_async(uintptr_t ptr, int64_t total, int dtype, int op, std::vector<uintptr_t> producers) {
+    check();
+    order_after(producers);
+    const int64_t bytes = total * (int64_t)elem_size(dtype);
+    if (emul_) {
+      emulate(reinterpret_cast<void*>(ptr), bytes, (emul_world_ - 1) * bytes / emul_world_, stream_);
+      return;
+    }
+    if (total % nranks_) throw std::invalid_argument("hetseq comm: reduce-scatter region not divisible by ranks");
+    const int64_t count = total / nranks_;
+    char* base = reinterpret_cast<char*>(ptr);
+    {
+      std::lock_guard<std::mutex> g(op_mu_);
+      check();
+      nccl_check(ncclReduceScatter(base, base + (int64_t)rank_ * count * (int64_t)elem_size(dtype), (size_t)count,
+                                   nccl_type(dtype), nccl_op(op), comm_, stream_),
+                 "ncclReduceScatter");
+    }
+    track(stream_);
+  }
+
+  void all_gather_inplace_async(uintptr_t ptr, int64_t total, int dtype, std::vector<uintptr_t> producers) {
+    check();
+    order_after(producers);
+    const int64_t bytes = total * (int64_t)elem_size(dtype);
+    if (emul_) {
+      emulate(reinterpret_cast<void*>(ptr), bytes, (emul_world_ - 1) * bytes / emul_world_, stream_);
+      return;
+    }
+    if (total % nranks_) throw std::invalid_argument("hetseq comm: all-gather region not divisible by ranks");
+    const int64_t count = total / nranks_;
+    char* base = reinterpret_cast<char*>(ptr);
+    {
+      std::lock_guard<std::mutex> g(op_mu_);
+      check();
+      nccl_check(ncclAllGather(base + (int64_t)rank_ * count * (int64_t)elem_size(dtype), base, (size_t)count,
+                               nccl_type(dtype), comm_, stream_),
+                 "ncclAllGather");
+    }
+    track(stream_);
+  }
+
   // Emulation mode (1-rank communicator only): every bucket all-reduce / all-gather on the comm
   // stream becomes the stand-in kernel -- `channels` workgroups moving the bytes a rank of a
   // `world`-rank ring receives and staying resident for latency + bytes / busbw.  world <= 1 ends it.
@@ -331,6 +378,15 @@ class Comm {
           (int64_t)ns, s);
     hip_check(hipGetLastError(), "comm emulation kernel launch");
     track(s);
+  }
+
+  void order_after(const std::vector<uintptr_t>& producers) {
+    for (uintptr_t s : producers) {
+      hipEvent_t e = take_event();
+      hip_check(hipEventRecord(e, as_stream(s)), "hipEventRecord(producer)");
+      hip_check(hipStreamWaitEvent(stream_, e, 0), "hipStreamWaitEvent(comm)");
+      give_event(e);
+    }
   }
 
   struct Pending {
@@ -462,6 +518,10 @@ PYBIND11_MODULE(_comm, m) {
       .def("all_reduce_async", &Comm::all_reduce_async, py::arg("ptr"), py::arg("count"), py::arg("dtype"),
            py::arg("op"), py::arg("producers"))
       .def("all_gather_async", &Comm::all_gather_async, py::arg("send"), py::arg("recv"), py::arg("count"),
+           py::arg("dtype"), py::arg("producers"))
+      .def("reduce_scatter_async", &Comm::reduce_scatter_async, py::arg("ptr"), py::arg("total"), py::arg("dtype"),
+           py::arg("op"), py::arg("producers"))
+      .def("all_gather_inplace_async", &Comm::all_gather_inplace_async, py::arg("ptr"), py::arg("total"),
            py::arg("dtype"), py::arg("producers"))
       .def("wait", &Comm::wait, py::arg("consumer"))
       .def("all_reduce", &Comm::all_reduce, py::arg("ptr"), py::arg("count"), py::arg("dtype"), py::arg("op"),

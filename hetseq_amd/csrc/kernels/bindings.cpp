@@ -20,6 +20,10 @@ using i64 = int64_t;
 
 // optim.hip
 void launch_grad_norm(const float*, int64_t, double*, const float*, float, float*, hipStream_t);
+int sumsq_blocks();
+void launch_sumsq_partial(const float*, int64_t, double*, int, hipStream_t);
+void launch_sum_partials(const double*, int, double*, hipStream_t);
+void launch_norm_finalize(const double*, int, const float*, float, float*, hipStream_t);
 void launch_stats_accum(double*, const float*, const float*, double, double, double, hipStream_t);
 void launch_stats_finalize(double*, double, double, float*, hipStream_t);
 void launch_adam_flat(float*, const float*, float*, float*, void*, int64_t, const float*, float, float, float, float,
@@ -189,6 +193,23 @@ PYBIND11_MODULE(_hip, m) {
   m.doc() = "hetseq_amd CDNA4 (gfx950) kernels";
   m.attr("arch") = "gfx950";
 
+  m.def("sumsq_blocks", &sumsq_blocks);
+  m.def("sumsq_partial", [](i64 g, i64 n, i64 partial, int blocks, i64 st) {
+    pre_launch("sumsq_partial");
+    if (blocks < 1 || blocks > sumsq_blocks()) throw std::invalid_argument("sumsq_partial: 1..sumsq_blocks() blocks");
+    launch_sumsq_partial(P(const float*, g), n, P(double*, partial), blocks, ST(st));
+    check_launch("sumsq_partial");
+  }, "sum of squares of g[0, n) into `blocks` fp64 partials (a range of a sharded gradient)");
+  m.def("sum_partials", [](i64 partial, int n, i64 out, i64 st) {
+    pre_launch("sum_partials");
+    launch_sum_partials(P(const double*, partial), n, P(double*, out), ST(st));
+    check_launch("sum_partials");
+  });
+  m.def("norm_finalize", [](i64 partial, int n, i64 scale, float max_norm, i64 out, i64 st) {
+    pre_launch("norm_finalize");
+    launch_norm_finalize(P(const double*, partial), n, P(const float*, scale), max_norm, P(float*, out), ST(st));
+    check_launch("norm_finalize");
+  }, "total norm / combined multiplier / clip coefficient from fp64 partial sums of squares");
   m.def("grad_norm", [](i64 g, i64 n, i64 partial, i64 scale, float max_norm, i64 out, i64 st) {
     pre_launch("grad_norm");
     launch_grad_norm(P(const float*, g), n, P(double*, partial), P(const float*, scale), max_norm, P(float*, out), ST(st));

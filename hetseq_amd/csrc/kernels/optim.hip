@@ -308,6 +308,39 @@ void launch_stats_finalize(double* st, double ln2, double w, float* scale, hipSt
   hipLaunchKernelGGL(stats_finalize_kernel, dim3(1), dim3(64), 0, stream, st, ln2, w, scale);
 }
 
+// Sharded update (parallel/zero.py): the sum of squares of several ranges of the gradient, one launch
+// per range into its own block of partials (pieces of one rank's shard), summed into one double by
+// sum_partials (then all-reduced across the ranks and finished by norm_finalize_kernel).
+__global__ void sum_partials_kernel(const double* __restrict__ partial, int n, double* __restrict__ out) {
+  double s = 0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) s += partial[i];
+  s = wave_sum_d(s);
+  __shared__ double red[16];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) red[w] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double tot = 0;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) tot += red[i];
+    out[0] = tot;
+  }
+}
+
+int sumsq_blocks() { return kRedBlocks; }
+
+void launch_sumsq_partial(const float* g, int64_t n, double* partial, int blocks, hipStream_t st) {
+  hipLaunchKernelGGL(sumsq_partial_kernel, dim3(blocks), dim3(kRedThreads), 0, st, g, n, partial);
+}
+
+void launch_sum_partials(const double* partial, int n, double* out, hipStream_t st) {
+  hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(1024), 0, st, partial, n, out);
+}
+
+void launch_norm_finalize(const double* partial, int n, const float* scale, float max_norm, float* out,
+                          hipStream_t st) {
+  hipLaunchKernelGGL(norm_finalize_kernel, dim3(1), dim3(1024), 0, st, partial, n, scale, max_norm, out);
+}
+
 void launch_grad_norm(const float* g, int64_t n, double* partial, const float* scale, float max_norm, float* out,
                       hipStream_t st) {
   hipLaunchKernelGGL(sumsq_partial_kernel, dim3(kRedBlocks), dim3(kRedThreads), 0, st, g, n, partial);

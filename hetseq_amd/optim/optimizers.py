@@ -121,7 +121,9 @@ class _Optimizer(object):
         self.store.flush_lazy()
         sc = self._scale_tensor()
         g = self.store.grad
-        if g.is_cuda:
+        if self.store.shard is not None:  # sharded update: squares over this rank's shard, one all-reduce
+            self.store.shard.grad_norm(sc, max_norm, self._dev_scalars[1:])
+        elif g.is_cuda:
             hip().grad_norm(g.data_ptr(), g.numel(), self._partials.data_ptr(), sc.data_ptr(), float(max_norm),
                             self._dev_scalars[1:].data_ptr(), stream_handle())
         else:
@@ -179,7 +181,11 @@ class _Optimizer(object):
             self.store.flush_lazy()
             gm = self._grad_multiplier()
             self.store.bump()
-            if self._staged_now():
+            if self.store.shard is not None:
+                if not self.supports_staged:
+                    raise NotImplementedError("%s has no sharded update" % type(self).__name__)
+                self.store.shard.step(self, gm, self.staged and not torch.cuda.is_current_stream_capturing())
+            elif self._staged_now():
                 self._step_staged(gm)
             elif self.store.param.is_cuda:
                 self._step_hip(gm)
@@ -202,6 +208,13 @@ class _Optimizer(object):
     def _staged_now(self):
         return (self.staged and self.supports_staged and self.store.chunks is not None and self.store.param.is_cuda
                 and self._hyper is None and not torch.cuda.is_current_stream_capturing())
+
+    def _step_range(self, gmul, lo, hi):
+        """The update of elements [lo, hi) on the current stream (sharded and staged updates)."""
+        if self.store.param.is_cuda:
+            self._step_hip(gmul, lo, hi)
+        else:
+            self._step_cpu(gmul, lo, hi)
 
     def _step_staged(self, gmul):
         s = self.store
@@ -228,6 +241,13 @@ class _Optimizer(object):
         for p in self.param_list:
             off = self.store.offset(p)
             yield buf[off : off + p.numel()].view(p.shape)
+
+    def consolidate(self):
+        """Sharded update: gather the whole optimizer state onto every rank (collective: every rank
+        calls it, before the master's state_dict())."""
+        if self.store is not None and self.store.shard is not None:
+            self.store.params_ready()
+            self.store.shard.consolidate(self)
 
     def state_dict(self):
         if self.store is not None:
@@ -322,12 +342,13 @@ class _Adam(_Optimizer):
                         shadow, hi - lo, gmul.data_ptr(), lr, b1, b2, eps, wd, step_size, stream_handle(),
                         self._hyper.dev.data_ptr() if self._hyper is not None else 0)
 
-    def _step_cpu(self, gmul):
+    def _step_cpu(self, gmul, lo=0, hi=None):
         lr, b1, b2, eps, wd, step_size = self._coeffs()
         s = self.store
+        hi = s.numel if hi is None else hi
         with torch.no_grad():
-            g = s.grad * gmul
-            m, v, p = self._state["exp_avg"], self._state["exp_avg_sq"], s.param
+            g = s.grad[lo:hi] * gmul
+            m, v, p = self._state["exp_avg"][lo:hi], self._state["exp_avg_sq"][lo:hi], s.param[lo:hi]
             m.mul_(b1).add_(g, alpha=1 - b1)
             v.mul_(b2).addcmul_(g, g, value=1 - b2)
             denom = v.sqrt().add_(eps)
@@ -335,7 +356,7 @@ class _Adam(_Optimizer):
                 p.add_(p, alpha=-wd * lr)
             p.addcdiv_(m, denom, value=-step_size)
             if s.shadow is not None:
-                s.shadow.copy_(p)
+                s.shadow[lo:hi].copy_(p)
 
 
 class _Adadelta(_Optimizer):

@@ -93,6 +93,28 @@ class NativeComm(object):
         self._c.all_gather_async(t.data_ptr(), out.data_ptr(), t.numel(), DTYPES[t.dtype], hs)
         return out
 
+    def reduce_scatter_async(self, t, producers=(), op="sum"):
+        """In-place reduce-scatter of contiguous ``t`` (numel a multiple of the rank count; emulated:
+        of the emulated world): rank r's piece r holds the sum, on the comm stream after ``producers``
+        (default: the current stream).  An empty ``producers`` tuple orders after the current stream;
+        pass ``producers=None`` to order only after earlier comm-stream work."""
+        hs = [] if producers is None else ([_stream(s) for s in producers] or [_stream()])
+        self._c.reduce_scatter_async(t.data_ptr(), t.numel(), DTYPES[t.dtype], OPS[op], hs)
+
+    def all_gather_inplace_async(self, t, producers=()):
+        """In-place all-gather of contiguous ``t``: every rank's piece r (of ``size`` equal pieces) to
+        all ranks, on the comm stream after ``producers`` (as :meth:`reduce_scatter_async`)."""
+        hs = [] if producers is None else ([_stream(s) for s in producers] or [_stream()])
+        self._c.all_gather_inplace_async(t.data_ptr(), t.numel(), DTYPES[t.dtype], hs)
+
+    def torch_stream(self):
+        """The comm stream as a torch stream (work enqueued on it is ordered with the collectives)."""
+        s = getattr(self, "_tstream", None)
+        if s is None:
+            s = torch.cuda.ExternalStream(self._c.stream, device=torch.device("cuda", self.device))
+            self._tstream = s
+        return s
+
     def set_snapshot(self, dst, src):
         """Test mode: every all_reduce_async of a slice of ``src`` copies it into the same offsets
         of ``dst`` on the comm stream instead (ordering check on one GPU); ``dst=None`` ends it."""

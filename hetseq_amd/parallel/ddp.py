@@ -49,7 +49,7 @@ from hetseq_amd.runtime import profiling, streams
 class FlatDDP(torch.nn.Module):
     def __init__(self, module, store, process_group=None, bucket_cap_mb=25, find_unused_parameters=False,
                  broadcast=True, comm_engine="auto", timeout_s=1800.0, sparse_embedding=None, sparse_capacity=None,
-                 plan_world=None):
+                 plan_world=None, shard_optimizer=False):
         super().__init__()
         self.module = module
         self.store = store
@@ -79,18 +79,28 @@ class FlatDDP(torch.nn.Module):
         skip = {id(p) for p in self.tables.tables} if self.tables is not None else set()
         order = sorted((p for p in params if id(p) not in skip), key=lambda p: store.offset(p), reverse=True)
         self.buckets = []  # (lo, hi, [params])
-        cur, size = [], 0
-        for p in order:
-            if id(p) in own and cur and not any(id(q) in own for q in cur):
+        if shard_optimizer and store.chunks is not None:
+            # sharded update: one bucket per update chunk (embeddings, each layer, the heads), so a
+            # chunk's all-gather after the update covers whole buckets
+            from hetseq_amd.runtime.flat import bisect_chunk
+
+            per = {}
+            for p in order:
+                per.setdefault(bisect_chunk(store.chunks, store.offset(p)), []).append(p)
+            self.buckets = [per[c] for c in sorted(per, reverse=True)]
+        else:
+            cur, size = [], 0
+            for p in order:
+                if id(p) in own and cur and not any(id(q) in own for q in cur):
+                    self.buckets.append(cur)
+                    cur, size = [], 0
+                cur.append(p)
+                size += p.numel()
+                if size >= cap:
+                    self.buckets.append(cur)
+                    cur, size = [], 0
+            if cur:
                 self.buckets.append(cur)
-                cur, size = [], 0
-            cur.append(p)
-            size += p.numel()
-            if size >= cap:
-                self.buckets.append(cur)
-                cur, size = [], 0
-        if cur:
-            self.buckets.append(cur)
         self.ranges = []
         self.bucket_of = {}
         for bi, ps in enumerate(self.buckets):
@@ -102,6 +112,22 @@ class FlatDDP(torch.nn.Module):
         # a bucket covers [first offset, last end) of its parameters, alignment gaps between them
         # included; gaps between buckets (<= 63 elements of 256-B padding, runtime/flat.py) are in no
         # range: their gradient entries stay zero on every rank and no parameter reads them
+        self.shard = None
+        if shard_optimizer:
+            from hetseq_amd.parallel.zero import ShardPlan
+
+            tables = []
+            if self.tables is not None:
+                offs = sorted((store.offset(p), store.offset(p) + p.numel()) for p in self.tables.tables)
+                for lo, hi in offs:  # contiguous tables (64-element alignment gaps included) as one region
+                    if tables and lo - tables[-1][1] < 64:
+                        tables[-1] = (tables[-1][0], hi)
+                    else:
+                        tables.append((lo, hi))
+            rank = dist.get_rank(self.process_group) if self.plan_world == self.world_size else 0
+            self.shard = ShardPlan(store, self.ranges, tables, self.plan_world, rank, comm=self.comm,
+                                   group=self.process_group)
+            store.shard = self.shard
         self._reset_state()
         # Readiness = post-accumulate-grad hooks.  They also fire when a fused
         # Function returned None for a parameter whose gradient it accumulated
@@ -133,7 +159,8 @@ class FlatDDP(torch.nn.Module):
         W = getattr(self, "plan_world", self.world_size)
         # ring collectives: an all-reduce receives 2(W-1)/W of the payload, an all-gather the other
         # W-1 ranks' payloads
-        recv = (W - 1) * n if kind == "allgather" else 2 * (W - 1) * n // max(W, 1)
+        recv = ((W - 1) * n if kind == "allgather" else (W - 1) * n // max(W, 1) if kind == "reducescatter"
+                else 2 * (W - 1) * n // max(W, 1))
         self.comm_log.append((what, n, self._in_tail, recv))
 
     def _tail_started(self):
@@ -192,12 +219,16 @@ class FlatDDP(torch.nn.Module):
         profiling.range_push(name)
         self.store.flush_range(lo, hi)  # (a lazily zeroed region no writer claimed: cleared before reducing)
         g = self.store.grad
-        self._log(name, g[lo:hi])
+        self._log(name, g[lo:hi], "reducescatter" if self.shard is not None and self.comm is not None else "allreduce")
         side = streams.active(g.device) if g.is_cuda else None
         if self.comm is not None:
             # the comm stream waits for both producers; neither producer stream is stalled
             cur = torch.cuda.current_stream(g.device)
-            self.comm.all_reduce_async(g[lo:hi], producers=(cur, side) if side is not None else (cur,))
+            prod = (cur, side) if side is not None else (cur,)
+            if self.shard is not None:  # sharded update: reduce-scatter (tail all-reduced)
+                self.shard.reduce_bucket(lo, hi, prod)
+            else:
+                self.comm.all_reduce_async(g[lo:hi], producers=prod)
             work = None
         elif side is not None:
             # the bucket's weight gradients come from the wgrad side stream, its biases / LN

@@ -190,7 +190,7 @@ class FlatParamStore(object):
             # the backward that writes them; params_ready waits for everything)
             from hetseq_amd.optim.optimizers import update_stream
 
-            st = update_stream(self.device)
+            st = self._update_stream or update_stream(self.device)
             with torch.cuda.stream(st):
                 self._zero_now(lazy)
                 ev = torch.cuda.Event()
@@ -268,6 +268,8 @@ class FlatParamStore(object):
     # waited for chunk i's fence (param_ready).  Chunks are set by the model, in the order its
     # forward first reads them (BertForPreTraining: embeddings, each encoder layer, the heads).
     chunks = None   # [(lo, hi)] covering [0, numel), ascending
+    _update_stream = None  # the stream the last staged update ran on (zero_grad queues behind it)
+    shard = None    # parallel/zero.py ShardPlan: the elements this rank updates (sharded optimizer)
     _fences = None  # per chunk: an event recorded after its update (None: nothing pending)
     _hooks = None   # per chunk: [fn()] run on the updating stream after the chunk's update
 
@@ -351,6 +353,19 @@ class FlatParamStore(object):
         if self._fences is not None:
             for i in range(len(self._fences)):
                 self.param_ready(i)
+
+    def cast_shadow(self, lo, hi):
+        """Refresh the bf16 shadow of elements [lo, hi) from the fp32 parameters (current stream)."""
+        if self.shadow is None or hi <= lo:
+            return
+        if self.param.is_cuda and self.shadow.dtype == torch.bfloat16 and lo % 4 == 0 and (hi - lo) % 4 == 0:
+            from hetseq_amd.ops._C import hip, stream_handle
+
+            hip().cast_f32_bf16(self.param.data_ptr() + 4 * lo, self.shadow.data_ptr() + 2 * lo, hi - lo,
+                                stream_handle())
+        else:
+            with torch.no_grad():
+                self.shadow[lo:hi].copy_(self.param[lo:hi])
 
     def sync_shadow(self):
         if self.shadow is None:
