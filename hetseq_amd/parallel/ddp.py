@@ -106,6 +106,12 @@ class FlatDDP(torch.nn.Module):
         for bi, ps in enumerate(self.buckets):
             lo = min(store.offset(p) for p in ps)
             hi = max(store.offset(p) + p.numel() for p in ps)
+            if shard_optimizer and store.chunks is not None:
+                # (to its chunk's aligned end: the padding is zero in every buffer, and the region then
+                # splits into W whole pieces -- runtime/flat.py CHUNK_ALIGN)
+                from hetseq_amd.runtime.flat import bisect_chunk
+
+                hi = store.chunks[bisect_chunk(store.chunks, lo)][1]
             self.ranges.append((lo, hi))
             for p in ps:
                 self.bucket_of[id(p)] = bi

@@ -163,6 +163,8 @@ class ShardPlan(object):
         chunk's pieces (and the bf16 shadow's re-cast), the chunk's update hooks, its fence."""
         s = self.store
         chunks = s.chunks if s.chunks is not None else [(0, s.numel)]
+        if getattr(self, "_per_chunk", None) is None or len(self._per_chunk) != len(chunks):
+            self._per_chunk = [(self.owned(lo, hi), self.regions_in(lo, hi)) for lo, hi in chunks]
         native = self.comm is not None and s.param.is_cuda
         if native:
             st = self.comm.torch_stream()
@@ -171,10 +173,9 @@ class ShardPlan(object):
         else:
             st, ctx = None, _nullctx()
         with ctx:
-            for i, (lo, hi) in enumerate(chunks):
-                for a, b in self.owned(lo, hi):
+            for i, (owned, regs) in enumerate(self._per_chunk):
+                for a, b in owned:
                     opt._step_range(gmul, a, b)
-                regs = self.regions_in(lo, hi)
                 self.gather(s.param, regs)
                 if s.shadow is not None:
                     for r in regs:

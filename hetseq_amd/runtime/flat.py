@@ -41,6 +41,9 @@ def bisect_chunk(chunks, off):
     return i if i >= 0 and off < chunks[i][1] else -1
 
 
+CHUNK_ALIGN = 4096  # update-chunk starts (elements): whole W-piece splits for W | 64 (parallel/zero.py)
+
+
 class FlatParamStore(object):
     def __init__(self, module, device=None, shadow_dtype=None):
         named = OrderedDict()
@@ -64,13 +67,22 @@ class FlatParamStore(object):
             order.append(members)
             placed.update(id(q) for q in members)
         dev = torch.device(device) if device is not None else next(iter(named.values())).device
+        # the model's update chunks (staged / sharded updates) start on CHUNK_ALIGN boundaries, so a
+        # chunk splits into W equal aligned pieces with no remainder
+        firsts = set()
+        ug = getattr(module, "update_groups", None)
+        pos = {id(q): i for i, m in enumerate(order) for q in m}
+        for g in (ug() or []) if callable(ug) else []:
+            ps = [p for p in g if id(p) in pos]
+            if ps:
+                firsts.add(id(min(ps, key=lambda p: pos[id(p)])))
         offsets, cur = OrderedDict(), 0
         for members in order:
-            cur = _align(cur)
+            cur = _align(cur, CHUNK_ALIGN) if any(id(q) in firsts for q in members) else _align(cur)
             for q in members:
                 offsets[id(q)] = cur
                 cur += q.numel()
-        total = _align(cur)
+        total = _align(cur, CHUNK_ALIGN) if firsts else _align(cur)
         self.numel = total
         self.device = dev
         self.param = torch.zeros(total, dtype=torch.float32, device=dev)
