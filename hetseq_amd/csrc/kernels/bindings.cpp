@@ -21,7 +21,7 @@ using i64 = int64_t;
 // optim.hip
 void launch_grad_norm(const float*, int64_t, double*, const float*, float, float*, hipStream_t);
 int sumsq_blocks();
-void launch_sumsq_partial(const float*, int64_t, double*, int, hipStream_t);
+void launch_sumsq_segs(const float*, const int64_t*, int, int, double*, hipStream_t);
 void launch_sum_partials(const double*, int, double*, hipStream_t);
 void launch_norm_finalize(const double*, int, const float*, float, float*, hipStream_t);
 void launch_stats_accum(double*, const float*, const float*, double, double, double, hipStream_t);
@@ -194,12 +194,13 @@ PYBIND11_MODULE(_hip, m) {
   m.attr("arch") = "gfx950";
 
   m.def("sumsq_blocks", &sumsq_blocks);
-  m.def("sumsq_partial", [](i64 g, i64 n, i64 partial, int blocks, i64 st) {
-    pre_launch("sumsq_partial");
-    if (blocks < 1 || blocks > sumsq_blocks()) throw std::invalid_argument("sumsq_partial: 1..sumsq_blocks() blocks");
-    launch_sumsq_partial(P(const float*, g), n, P(double*, partial), blocks, ST(st));
-    check_launch("sumsq_partial");
-  }, "sum of squares of g[0, n) into `blocks` fp64 partials (a range of a sharded gradient)");
+  m.def("sumsq_segs", [](i64 g, i64 segs, int nseg, int nblk, i64 partial, i64 st) {
+    pre_launch("sumsq_segs");
+    if (nseg < 1 || nblk < nseg) throw std::invalid_argument("sumsq_segs: >= 1 range, >= 1 block per range");
+    launch_sumsq_segs(P(const float*, g), P(const int64_t*, segs), nseg, nblk, P(double*, partial), ST(st));
+    check_launch("sumsq_segs");
+  }, "sums of squares of the ranges segs[3i:3i+2] of g into nblk fp64 partials (range i from block segs[3i+2]; "
+     "a sharded gradient's owned ranges, one launch)");
   m.def("sum_partials", [](i64 partial, int n, i64 out, i64 st) {
     pre_launch("sum_partials");
     launch_sum_partials(P(const double*, partial), n, P(double*, out), ST(st));

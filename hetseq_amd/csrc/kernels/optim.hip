@@ -308,9 +308,47 @@ void launch_stats_finalize(double* st, double ln2, double w, float* scale, hipSt
   hipLaunchKernelGGL(stats_finalize_kernel, dim3(1), dim3(64), 0, stream, st, ln2, w, scale);
 }
 
-// Sharded update (parallel/zero.py): the sum of squares of several ranges of the gradient, one launch
-// per range into its own block of partials (pieces of one rank's shard), summed into one double by
-// sum_partials (then all-reduced across the ranks and finished by norm_finalize_kernel).
+// Sharded update (parallel/zero.py): the sum of squares of the ranges of the gradient one rank owns, in
+// ONE launch.  segs = (lo, hi, first block) per range, the ranges' blocks consecutive: each block finds
+// its range (a short linear scan: tens of ranges), strides over it (float4 body, scalar ends by the
+// range's first block) and writes one fp64 partial; sum_partials adds them (then all-reduced across the
+// ranks and finished by norm_finalize_kernel).
+__global__ void __launch_bounds__(kRedThreads) sumsq_segs_kernel(const float* __restrict__ g,
+                                                                 const int64_t* __restrict__ segs, int nseg,
+                                                                 int nblk, double* __restrict__ partial) {
+  int s = 0;
+  while (s + 1 < nseg && segs[3 * (s + 1) + 2] <= (int64_t)blockIdx.x) ++s;
+  const int64_t lo = segs[3 * s], hi = segs[3 * s + 1], b0 = segs[3 * s + 2];
+  const int64_t b1 = s + 1 < nseg ? segs[3 * (s + 1) + 2] : nblk;
+  const int64_t nb = b1 - b0, bi = blockIdx.x - b0;
+  const int64_t a4 = (lo + 3) & ~(int64_t)3, e4 = a4 > (hi & ~(int64_t)3) ? a4 : (hi & ~(int64_t)3);
+  const float4* g4 = reinterpret_cast<const float4*>(g + a4);
+  const int64_t n4 = (e4 - a4) >> 2, stride = nb * blockDim.x;
+  float a0 = 0.f, a1 = 0.f;
+  int64_t i = bi * blockDim.x + threadIdx.x;
+  for (; i + stride < n4; i += 2 * stride) {
+    const float4 v0 = g4[i], v1 = g4[i + stride];
+    a0 = fmaf(v0.x, v0.x, fmaf(v0.y, v0.y, fmaf(v0.z, v0.z, fmaf(v0.w, v0.w, a0))));
+    a1 = fmaf(v1.x, v1.x, fmaf(v1.y, v1.y, fmaf(v1.z, v1.z, fmaf(v1.w, v1.w, a1))));
+  }
+  for (; i < n4; i += stride) {
+    const float4 v = g4[i];
+    a0 = fmaf(v.x, v.x, fmaf(v.y, v.y, fmaf(v.z, v.z, fmaf(v.w, v.w, a0))));
+  }
+  float acc = a0 + a1;
+  if (bi == 0) {  // the unaligned ends (< 4 elements each; the whole range when it is shorter)
+    const int64_t h = a4 < hi ? a4 : hi;
+    if (lo + threadIdx.x < h) acc = fmaf(g[lo + threadIdx.x], g[lo + threadIdx.x], acc);
+    if (e4 > h && e4 + threadIdx.x < hi) acc = fmaf(g[e4 + threadIdx.x], g[e4 + threadIdx.x], acc);
+  }
+  double d = wave_sum_d(static_cast<double>(acc));
+  __shared__ double red[kRedThreads / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) red[w] = d;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
 __global__ void sum_partials_kernel(const double* __restrict__ partial, int n, double* __restrict__ out) {
   double s = 0;
   for (int i = threadIdx.x; i < n; i += blockDim.x) s += partial[i];
@@ -328,8 +366,8 @@ __global__ void sum_partials_kernel(const double* __restrict__ partial, int n, d
 
 int sumsq_blocks() { return kRedBlocks; }
 
-void launch_sumsq_partial(const float* g, int64_t n, double* partial, int blocks, hipStream_t st) {
-  hipLaunchKernelGGL(sumsq_partial_kernel, dim3(blocks), dim3(kRedThreads), 0, st, g, n, partial);
+void launch_sumsq_segs(const float* g, const int64_t* segs, int nseg, int nblk, double* partial, hipStream_t st) {
+  hipLaunchKernelGGL(sumsq_segs_kernel, dim3(nblk), dim3(kRedThreads), 0, st, g, segs, nseg, nblk, partial);
 }
 
 void launch_sum_partials(const double* partial, int n, double* out, hipStream_t st) {

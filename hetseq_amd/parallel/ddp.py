@@ -225,7 +225,8 @@ class FlatDDP(torch.nn.Module):
         profiling.range_push(name)
         self.store.flush_range(lo, hi)  # (a lazily zeroed region no writer claimed: cleared before reducing)
         g = self.store.grad
-        self._log(name, g[lo:hi], "reducescatter" if self.shard is not None and self.comm is not None else "allreduce")
+        rs = self.shard is not None and self.comm is not None and self.shard.by_range[(lo, hi)].ps > 0
+        self._log(name, g[lo:hi], "reducescatter" if rs else "allreduce")
         side = streams.active(g.device) if g.is_cuda else None
         if self.comm is not None:
             # the comm stream waits for both producers; neither producer stream is stalled

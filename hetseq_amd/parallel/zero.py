@@ -15,8 +15,11 @@ rank).  Here, with ``--shard-optimizer`` (on by default for data-parallel Adam r
   ALL-GATHERED in place -- per update chunk (embeddings, each encoder layer, the heads) on the comm
   stream, each chunk fenced (runtime/flat.py ``param_ready``), so the gather of layer i overlaps the
   next forward of layers < i;
-* the sparsely exchanged embedding tables (parallel/tied.py) arrive whole on every rank: their region
-  is split the same way for the update and the gather, with no reduce-scatter.
+* the sparsely exchanged embedding tables (parallel/tied.py) stay REPLICATED: their dense part (the
+  tied decoder's gradient) is all-reduced, the gathered rows are added on every rank, and every rank
+  runs Adam over the whole region -- the tables are the first thing the next forward reads, and
+  re-gathering 94 MB there (BERT-base) would put a whole all-gather in front of it, where the update
+  of 23 M elements costs ~0.1 ms.
 
 Checkpoints stay in the unsharded ``torch.optim`` layout: ``consolidate()`` (every rank) all-gathers
 the Adam moments before the master writes them.  Under ``--emulate-world W`` (one real rank) the plan
@@ -36,7 +39,8 @@ class Region(object):
 
     def __init__(self, lo, hi, world, reduce):
         self.lo, self.hi, self.reduce = lo, hi, reduce
-        self.ps = ((hi - lo) // world) // ALIGN * ALIGN  # piece size (0: the whole region is tail)
+        # piece size (0: the whole region is tail -- replicated, as the sparse tables are)
+        self.ps = ((hi - lo) // world) // ALIGN * ALIGN if reduce else 0
         self.body = lo + world * self.ps
 
     def __repr__(self):
@@ -129,19 +133,20 @@ class ShardPlan(object):
         if g.is_cuda:
             from hetseq_amd.ops._C import hip, stream_handle
 
-            cap = hip().sumsq_blocks()
-            nbs = [max(1, min(cap, (b - a) // 16384)) for a, b in segs]
-            need = sum(nbs) + 1
-            if self._partials is None or self._partials.numel() < need:
-                self._partials = torch.zeros(max(need, 64), dtype=torch.float64, device=g.device)
+            if self._partials is None:  # (the plan is static: one segment table for the job)
+                cap = hip().sumsq_blocks()
+                rows, nb = [], 0
+                for a, b in segs:
+                    rows += [a, b, nb]
+                    nb += max(1, min(cap, (b - a) // 16384))
+                self._segs = torch.tensor(rows, dtype=torch.int64).to(g.device)
+                self._nblk = nb
+                self._partials = torch.zeros(nb + 1, dtype=torch.float64, device=g.device)
             p = self._partials
             st = stream_handle()
-            off = 0
-            for (a, b), nb in zip(segs, nbs):
-                hip().sumsq_partial(g.data_ptr() + 4 * a, b - a, p.data_ptr() + 8 * off, nb, st)
-                off += nb
-            tot = p[off:off + 1]
-            hip().sum_partials(p.data_ptr(), off, tot.data_ptr(), st)
+            hip().sumsq_segs(g.data_ptr(), self._segs.data_ptr(), len(segs), self._nblk, p.data_ptr(), st)
+            tot = p[self._nblk:self._nblk + 1]
+            hip().sum_partials(p.data_ptr(), self._nblk, tot.data_ptr(), st)
             self.all_reduce_scalar(tot)
             hip().norm_finalize(tot.data_ptr(), 1, scale.data_ptr(), float(max_norm), out.data_ptr(), st)
             return
@@ -160,15 +165,29 @@ class ShardPlan(object):
     # ------------------------------------------------------------------ update
     def step(self, opt, gmul, staged):
         """The sharded update: per chunk, Adam on the owned elements, the in-place all-gather of the
-        chunk's pieces (and the bf16 shadow's re-cast), the chunk's update hooks, its fence."""
+        chunk's pieces (and the bf16 shadow's re-cast), the chunk's update hooks, its fence.  The
+        replicated regions (the sparse tables) are updated on the current stream -- the next forward
+        reads them first, and the comm stream meanwhile starts the chunks' gathers."""
         s = self.store
         chunks = s.chunks if s.chunks is not None else [(0, s.numel)]
         if getattr(self, "_per_chunk", None) is None or len(self._per_chunk) != len(chunks):
-            self._per_chunk = [(self.owned(lo, hi), self.regions_in(lo, hi)) for lo, hi in chunks]
+            rep = [r for r in self.regions if r.ps == 0 and not r.reduce]
+            self._replicated = [(r.lo, r.hi) for r in rep]
+            self._per_chunk = [([(a, b) for a, b in self.owned(lo, hi) if (a, b) not in self._replicated],
+                                self.regions_in(lo, hi)) for lo, hi in chunks]
         native = self.comm is not None and s.param.is_cuda
         if native:
             st = self.comm.torch_stream()
-            st.wait_stream(torch.cuda.current_stream(s.device))  # the reduced gradients and the norm
+            cur = torch.cuda.current_stream(s.device)
+            ready = torch.cuda.Event()
+            ready.record(cur)  # the reduced gradients and the norm
+        for a, b in self._replicated:
+            opt._step_range(gmul, a, b)
+            s.cast_shadow(a, b)
+        if native:
+            rep_done = torch.cuda.Event()
+            rep_done.record(cur)
+            st.wait_event(ready)
             ctx = torch.cuda.stream(st)
         else:
             st, ctx = None, _nullctx()
@@ -179,12 +198,20 @@ class ShardPlan(object):
                 self.gather(s.param, regs)
                 if s.shadow is not None:
                     for r in regs:
-                        s.cast_shadow(r.lo, r.hi)
+                        if (r.lo, r.hi) not in self._replicated:
+                            s.cast_shadow(r.lo, r.hi)
+                if native and s.chunks is not None and s.has_hooks(i) and any(
+                        r.ps == 0 and not r.reduce for r in regs):
+                    st.wait_event(rep_done)  # (hooks reading a replicated region)
                 s.run_hooks(i) if s.chunks is not None else s.run_hooks()
                 if native and staged and s.chunks is not None:
                     ev = torch.cuda.Event()
                     ev.record(st)
                     s._fences[i] = ev
+            if native:
+                # later comm-stream work (the deferred zero_grad, the next step's exchanges) follows
+                # the replicated regions' update, which reads their gradients
+                st.wait_event(rep_done)
         if native:
             s._update_stream = st
             if not (staged and s.chunks is not None):

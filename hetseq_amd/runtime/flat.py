@@ -326,6 +326,9 @@ class FlatParamStore(object):
         hooks also run, in chunk order, after an unstaged update)."""
         self._hooks[chunk].append(fn)
 
+    def has_hooks(self, chunk):
+        return self._hooks is not None and bool(self._hooks[chunk])
+
     def run_hooks(self, chunk=None):
         if self._hooks is None:
             return

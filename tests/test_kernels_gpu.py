@@ -1396,3 +1396,23 @@ def test_fast_stat_kernels_match_torch_ops(cuda):
     hip().stats_finalize(z.data_ptr(), ln2, 1.0, scale.data_ptr(), stream_handle())
     torch.cuda.synchronize()
     assert scale.item() == 1.0
+
+
+def test_sumsq_segs_matches_fp64(cuda):
+    """Sharded gradient norm (parallel/zero.py): one launch over a table of ranges -- aligned pieces,
+    unaligned ends, ranges shorter than a float4 -- against the fp64 sums of squares."""
+    from hetseq_amd.ops._C import hip, stream_handle
+
+    torch.manual_seed(0)
+    g = torch.randn(3_000_003, device=cuda) * torch.logspace(-3, 3, 3_000_003, device=cuda)
+    segs = [(0, 65536), (70001, 70003), (100_000, 1_900_001), (1_900_005, 1_900_006), (2_000_001, 3_000_003)]
+    rows, nb = [], 0
+    for a, b in segs:
+        rows += [a, b, nb]
+        nb += max(1, min(hip().sumsq_blocks(), (b - a) // 16384))
+    tab = torch.tensor(rows, dtype=torch.int64, device=cuda)
+    p = torch.zeros(nb + 1, dtype=torch.float64, device=cuda)
+    hip().sumsq_segs(g.data_ptr(), tab.data_ptr(), len(segs), nb, p.data_ptr(), stream_handle())
+    hip().sum_partials(p.data_ptr(), nb, p[nb:].data_ptr(), stream_handle())
+    ref = sum(float(g[a:b].double().pow(2).sum()) for a, b in segs)
+    assert abs(float(p[nb]) - ref) <= 1e-6 * ref
