@@ -10,6 +10,8 @@
 #include <cstdint>
 #include <stdexcept>
 #include <string>
+#include <vector>
+#include <pybind11/stl.h>
 
 namespace py = pybind11;
 using u64 = uint64_t;
@@ -171,7 +173,7 @@ static void pre_launch(const char* what) {
 // g_wait_flags (hipEventDisableTiming by default; tools/probes/fork_gap.py measures the flag
 // choices, set_stream_wait_flags switches them).
 static unsigned g_wait_flags = hipEventDisableTiming;
-static void stream_wait(hipStream_t waiter, hipStream_t signal) {
+void hs_stream_wait(hipStream_t waiter, hipStream_t signal) {
   static hipEvent_t ring[64];
   static int n = 0;
   static unsigned made = ~0u;
@@ -189,10 +191,32 @@ static void stream_wait(hipStream_t waiter, hipStream_t signal) {
     throw std::runtime_error("stream_wait: hipEventRecord/hipStreamWaitEvent failed");
 }
 
+static void stream_wait(hipStream_t waiter, hipStream_t signal) { hs_stream_wait(waiter, signal); }
+
+// layer_prog.cpp
+std::vector<std::string> layer_plan_fields();
+void layer_fwd_h3p(int64_t, int64_t, int64_t, int64_t, int64_t, uint64_t, uint64_t, uint64_t, uint64_t, uint64_t,
+                   uint64_t, float, float, float, int64_t, int64_t, int64_t, int64_t);
+void layer_bwd_h3p(int64_t, int64_t, int64_t, int64_t, int64_t, uint64_t, uint64_t, uint64_t, uint64_t, float, float,
+                   int, int64_t, int64_t);
+
 PYBIND11_MODULE(_hip, m) {
   m.doc() = "hetseq_amd CDNA4 (gfx950) kernels";
   m.attr("arch") = "gfx950";
 
+  m.def("layer_plan_fields", &layer_plan_fields, "field names of a layer program's int64 plan (layer_prog.cpp)");
+  m.def("layer_fwd_h3p", [](i64 plan, i64 x, i64 xp, i64 xe, i64 mask, u64 sa, u64 oa, u64 s1, u64 o1, u64 s2, u64 o2,
+                            float eps, float p_h, float p_a, i64 st0, i64 st1, i64 amax0, i64 amax1) {
+    pre_launch("layer_fwd_h3p");
+    layer_fwd_h3p(plan, x, xp, xe, mask, sa, oa, s1, o1, s2, o2, eps, p_h, p_a, st0, st1, amax0, amax1);
+    check_launch("layer_fwd_h3p");
+  }, "one fused encoder-layer forward on the h3p engine from its plan (ops/layer_prog.py)");
+  m.def("layer_bwd_h3p", [](i64 plan, i64 dh2, i64 xp, i64 xe, i64 mask, u64 s1, u64 o1, u64 s2, u64 o2, float p_h,
+                            float p_a, int wacc, i64 st0, i64 st1) {
+    pre_launch("layer_bwd_h3p");
+    layer_bwd_h3p(plan, dh2, xp, xe, mask, s1, o1, s2, o2, p_h, p_a, wacc, st0, st1);
+    check_launch("layer_bwd_h3p");
+  }, "one fused encoder-layer backward on the h3p engine from its plan (ops/layer_prog.py)");
   m.def("sumsq_blocks", &sumsq_blocks);
   m.def("sumsq_segs", [](i64 g, i64 segs, int nseg, int nblk, i64 partial, i64 st) {
     pre_launch("sumsq_segs");

@@ -566,11 +566,11 @@ def _layer_forward_split(x, mask, W, cfg, save, am=None):
     return h2, None
 
 
-def _layer_forward(x, mask, W, cfg, save, am=None):
+def _layer_forward(x, mask, W, cfg, save, am=None, meta=None):
     """One layer forward: the h3p engine's (``W.h3p``), the two half-batch chains (_fwd_split_ok), or
     one chain on the fp32 in-kernel-split / bf16 engines (``am``: the h3 engine's |max| slots)."""
     if getattr(W, "h3p", None) is not None:
-        return _layer_forward_h3p(x, mask, W, cfg, save, am)
+        return _layer_forward_h3p(x, mask, W, cfg, save, am, meta)
     if _fwd_split_ok(x, mask, W, cfg):
         return _layer_forward_split(x, mask, W, cfg, save, am)
     streams.chain_join(x.device)  # one chain from here: the half-batch chains meet first
@@ -614,7 +614,83 @@ class _OneChain(object):
         return False
 
 
-def _layer_forward_h3p(x, mask, W, cfg, save, am=None):
+# the native launch path (ops/layer_prog.py): False runs the Python layer (A/B, bench --ab prog_off)
+LAYER_PROG = True
+_PROGS: dict = {}
+
+
+class _ProgSaved(object):
+    """What a program forward leaves for its backward: the program and the input's planes."""
+    __slots__ = ("prog", "xp")
+
+    def __init__(self, prog, xp):
+        self.prog, self.xp = prog, xp
+
+
+def _program(W, meta, B, S, NH, p_a, halves, dev):
+    """The layer's :class:`~hetseq_amd.ops.layer_prog.LayerProgram` for this shape, or None when the
+    forward is not eligible (no flat store / side stream, recompute; ``meta`` None: no backward)."""
+    if not (LAYER_PROG and not meta.get("recompute") and streams.enabled()
+            and meta.get("grad_sink") is not None and meta.get("store") is not None):
+        return None
+    Gv = meta["grad_sink"]()
+    key = (id(W.h3p), id(Gv), B, S, halves, p_a > 0)
+    prog = _PROGS.get(key)
+    if prog is None:
+        from hetseq_amd.ops.layer_prog import LayerProgram
+
+        rows = B * S
+        H, F = W.wo.shape[0], W.w1.shape[0]
+
+        def ksg(M, N):
+            return max(streams.side_ksplit(M, N) or 1, -(-rows // 4096))
+        prog = LayerProgram(W, Gv, B, S, NH, halves, _H3P_KS_WO, _H3P_KS_W2,
+                            {"qkv": ksg(3 * H, H), "wo": ksg(H, H), "w1": ksg(F, H), "w2": ksg(H, F)}, p_a > 0, dev)
+        _PROGS[key] = prog
+    return prog
+
+
+def _layer_forward_prog(prog, x, mask, W, cfg, am, halves_ok):
+    from hetseq_amd.ops import h3p
+
+    B, S, NH, p_h, p_a, eps, seeds = cfg
+    (s_a, o_a), (s_1, o_1), (s_2, o_2) = seeds
+    dev = x.device
+    xp = h3p.of(x)
+    prog.set_input_layout(xp)
+    if halves_ok:
+        st1 = streams.chain_fork(dev).cuda_stream
+    else:
+        streams.chain_join(dev)
+        st1 = 0
+    am0 = G.slot_ptr(am.a(6)) if am is not None else 0
+    am1 = G.slot_ptr(am.a(7)) if am is not None and halves_ok else 0
+    hip().layer_fwd_h3p(prog.addr, x.data_ptr(), xp.data_ptr(), xp.exps_ptr(), mask.data_ptr(), s_a, o_a, s_1, o_1,
+                        s_2, o_2, float(eps), float(p_h), float(p_a), stream_handle(), st1, am0, am1)
+    streams.chain_keep(x, mask, xp.planes, xp.exps)
+    h2 = prog.h2.view(prog.rows, prog.H)
+    h3p.remember(h2, prog.h2p)  # the next layer's QKV operand
+    return h2, _ProgSaved(prog, xp)
+
+
+def _layer_backward_prog(ctx, dh2, x, saved, W, meta, cfg):
+    B, S, NH, p_h, p_a, eps, seeds = cfg
+    (s_a, o_a), (s_1, o_1), (s_2, o_2) = seeds
+    prog, xp = saved.prog, saved.xp
+    dh2 = dh2.contiguous()
+    dev = dh2.device
+    store = meta["store"]
+    Gv = meta["grad_sink"]()
+    wacc = not (_FRESH_WGRAD and store.claim_fresh())
+    for out in (Gv.w2, Gv.w1, Gv.wo, Gv.wqkv):  # lazy zero_grad bookkeeping (runtime/flat.py)
+        (store.ensure_zero if wacc else store.mark_stored)(out)
+    side = streams.backward_forks(dev, xp.planes, xp.exps)
+    hip().layer_bwd_h3p(prog.addr, dh2.data_ptr(), xp.data_ptr(), xp.exps_ptr(), mask_of(ctx).data_ptr(), s_1, o_1,
+                        s_2, o_2, float(p_h), float(p_a), int(wacc), stream_handle(), side.cuda_stream)
+    return (prog.dz1.view(prog.rows, prog.H), None, None) + (None,) * 16
+
+
+def _layer_forward_h3p(x, mask, W, cfg, save, am=None, meta=None):
     """The layer forward on h3p operands (``W.h3p``: the GEMM weights' planes).  Like
     _layer_forward_split, the batch runs as two half-batch chains on two streams when it splits
     evenly into 128-row halves; each op writes its half of the whole-batch tensors.  Operand planes:
@@ -630,6 +706,9 @@ def _layer_forward_h3p(x, mask, W, cfg, save, am=None):
     F = W.w1.shape[0]
     dev, f32 = x.device, torch.float32
     halves_ok = (B % 2 == 0 and (rows // 2) % 128 == 0 and rows >= 1024 and streams.enabled() and _FWD_SPLIT)
+    prog = _program(W, meta, B, S, NH, p_a, 2 if halves_ok else 1, dev) if (save and meta is not None) else None
+    if prog is not None:
+        return _layer_forward_prog(prog, x, mask, W, cfg, am, halves_ok)
     if not halves_ok:
         streams.chain_join(dev)
     xp = h3p.of(x)
@@ -762,11 +841,17 @@ class FusedBertLayer(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, mask, meta, *params):
         W, cfg, recompute = meta["weights"](), meta["cfg"], meta["recompute"]
-        h2, saved = _layer_forward(x, mask, W, cfg, save=not recompute, am=meta.get("amax"))
+        # (the native program only for forwards whose backward will run: autograd is off in here)
+        h2, saved = _layer_forward(x, mask, W, cfg, save=not recompute, am=meta.get("amax"),
+                                   meta=meta if any(ctx.needs_input_grad) else None)
         ctx.meta = meta
         ctx.cfg = cfg
         ctx.h3p = None
-        if recompute:
+        ctx.prog = None
+        if isinstance(saved, _ProgSaved):
+            ctx.prog = saved
+            ctx.save_for_backward(x, mask)
+        elif recompute:
             ctx.save_for_backward(x, mask)
         else:
             if len(saved) > 15:  # h3p: the operand planes travel as a ctx attribute (not tensors)
@@ -779,6 +864,8 @@ class FusedBertLayer(torch.autograd.Function):
     def backward(ctx, dh2):
         meta, cfg = ctx.meta, ctx.cfg
         W = meta["weights"]()
+        if ctx.prog is not None:
+            return _layer_backward_prog(ctx, dh2, ctx.saved_tensors[0], ctx.prog, W, meta, cfg)
         if meta["recompute"]:
             x, mask = ctx.saved_tensors
             with torch.no_grad():

@@ -171,6 +171,19 @@ def chain_join(device):
     _chain["keep"].clear()
 
 
+def chain_fork(device):
+    """Open the second half-batch chain on fwd2 unless already open (the native layer program's
+    forward: its arena is the layer's own, so one fork per chain suffices -- no per-layer fork
+    against allocator reuse, FWD_CHAIN_FORK)."""
+    st = fwd2(device)
+    if _chain["forked"] is not st:
+        from hetseq_amd.ops._C import hip, stream_handle
+
+        hip().stream_wait(st.cuda_stream, stream_handle())
+        _chain["forked"] = st
+    return st
+
+
 def chain_stream():
     """The forked second half-batch chain's stream (None outside an open chain)."""
     return _chain["forked"]
@@ -297,6 +310,18 @@ def fork(device, *tensors) -> "torch.cuda.Stream":
         hip().stream_wait(s.cuda_stream, stream_handle())
         if c == 1:
             _state["coalesce"] = 2
+    _KEEP.extend(tensors)
+    if not _state["queued"]:
+        _state["queued"] = True
+        torch.autograd.Variable._execution_engine.queue_callback(join)
+    return s
+
+
+def backward_forks(device, *tensors):
+    """The bookkeeping of :func:`fork` for a caller that enqueues its own side-stream forks (the
+    native layer program): the end-of-backward join is queued and ``tensors`` (read on the side
+    stream) stay alive until it.  Returns the side stream."""
+    s = side(device)
     _KEEP.extend(tensors)
     if not _state["queued"]:
         _state["queued"] = True
