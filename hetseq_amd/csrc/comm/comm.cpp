@@ -213,6 +213,14 @@ class Comm {
     }
   }
 
+  // The comm stream waits for raw events the caller recorded (a fused backward's per-group
+  // readiness, ops/layer_prog.py): the next collective is ordered after exactly that work.
+  void wait_events(const std::vector<uintptr_t>& events) {
+    check();
+    for (uintptr_t e : events)
+      hip_check(hipStreamWaitEvent(stream_, reinterpret_cast<hipEvent_t>(e), 0), "hipStreamWaitEvent(events)");
+  }
+
   // Sharded update (parallel/zero.py): in-place reduce-scatter of [ptr, ptr + total) -- rank r keeps
   // the sum of piece r, [ptr + r total / n, ...) -- on the comm stream after every producer stream's work
   // so far; and the in-place all-gather of the updated pieces (each rank's piece r to every rank).
@@ -224,6 +232,15 @@ class Comm {
     const int64_t bytes = total * (int64_t)elem_size(dtype);
     if (emul_) {
       emulate(reinterpret_cast<void*>(ptr), bytes, (emul_world_ - 1) * bytes / emul_world_, stream_);
+      return;
+    }
+    if (snap_dst_) {  // test mode, as all_reduce_async: the region as the collective would read it
+      if (ptr < snap_src_ || ptr + (uintptr_t)bytes > snap_src_ + snap_bytes_)
+        throw std::invalid_argument("hetseq comm: snapshot range outside the registered buffer");
+      hip_check(hipMemcpyAsync(reinterpret_cast<void*>(snap_dst_ + (ptr - snap_src_)), reinterpret_cast<void*>(ptr),
+                               (size_t)bytes, hipMemcpyDeviceToDevice, stream_),
+                "hipMemcpyAsync(snapshot)");
+      track(stream_);
       return;
     }
     if (total % nranks_) throw std::invalid_argument("hetseq comm: reduce-scatter region not divisible by ranks");
@@ -519,6 +536,7 @@ PYBIND11_MODULE(_comm, m) {
            py::arg("op"), py::arg("producers"))
       .def("all_gather_async", &Comm::all_gather_async, py::arg("send"), py::arg("recv"), py::arg("count"),
            py::arg("dtype"), py::arg("producers"))
+      .def("wait_events", &Comm::wait_events, py::arg("events"))
       .def("reduce_scatter_async", &Comm::reduce_scatter_async, py::arg("ptr"), py::arg("total"), py::arg("dtype"),
            py::arg("op"), py::arg("producers"))
       .def("all_gather_inplace_async", &Comm::all_gather_inplace_async, py::arg("ptr"), py::arg("total"),

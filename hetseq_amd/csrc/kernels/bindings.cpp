@@ -198,7 +198,7 @@ std::vector<std::string> layer_plan_fields();
 void layer_fwd_h3p(int64_t, int64_t, int64_t, int64_t, int64_t, uint64_t, uint64_t, uint64_t, uint64_t, uint64_t,
                    uint64_t, float, float, float, int64_t, int64_t, int64_t, int64_t);
 void layer_bwd_h3p(int64_t, int64_t, int64_t, int64_t, int64_t, uint64_t, uint64_t, uint64_t, uint64_t, float, float,
-                   int, int64_t, int64_t);
+                   int, int64_t, int64_t, int64_t);
 
 PYBIND11_MODULE(_hip, m) {
   m.doc() = "hetseq_amd CDNA4 (gfx950) kernels";
@@ -212,11 +212,19 @@ PYBIND11_MODULE(_hip, m) {
     check_launch("layer_fwd_h3p");
   }, "one fused encoder-layer forward on the h3p engine from its plan (ops/layer_prog.py)");
   m.def("layer_bwd_h3p", [](i64 plan, i64 dh2, i64 xp, i64 xe, i64 mask, u64 s1, u64 o1, u64 s2, u64 o2, float p_h,
-                            float p_a, int wacc, i64 st0, i64 st1) {
+                            float p_a, int wacc, i64 st0, i64 st1, i64 events) {
     pre_launch("layer_bwd_h3p");
-    layer_bwd_h3p(plan, dh2, xp, xe, mask, s1, o1, s2, o2, p_h, p_a, wacc, st0, st1);
+    layer_bwd_h3p(plan, dh2, xp, xe, mask, s1, o1, s2, o2, p_h, p_a, wacc, st0, st1, events);
     check_launch("layer_bwd_h3p");
-  }, "one fused encoder-layer backward on the h3p engine from its plan (ops/layer_prog.py)");
+  }, "one fused encoder-layer backward on the h3p engine from its plan (ops/layer_prog.py); events: 0 or the "
+     "address of 4 hipEvent_t recorded as each parameter-gradient group completes", py::arg("plan"), py::arg("dh2"),
+     py::arg("xp"), py::arg("xe"), py::arg("mask"), py::arg("s1"), py::arg("o1"), py::arg("s2"), py::arg("o2"),
+     py::arg("p_h"), py::arg("p_a"), py::arg("wacc"), py::arg("st0"), py::arg("st1"), py::arg("events") = 0);
+  m.def("event_create", []() {
+    hipEvent_t e = nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) throw std::runtime_error("hipEventCreate");
+    return (i64) reinterpret_cast<uintptr_t>(e);
+  }, "a raw timing-free hipEvent_t (process lifetime; layer-program readiness events)");
   m.def("sumsq_blocks", &sumsq_blocks);
   m.def("sumsq_segs", [](i64 g, i64 segs, int nseg, int nblk, i64 partial, i64 st) {
     pre_launch("sumsq_segs");

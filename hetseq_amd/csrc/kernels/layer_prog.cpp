@@ -181,9 +181,19 @@ void layer_fwd_h3p(int64_t plan, int64_t x, int64_t xp, int64_t xe, int64_t mask
 // One layer backward (flat-store gradients, side stream).  dh2: the output gradient [rows, H];
 // xp / xe: the forward input's planes; wacc: the weight-gradient products accumulate (else store:
 // the first backward after zero_grad).  The input gradient is left in the plan's dz1.
+//
+// events: 0, or the address of four hipEvent_t handles recorded on the side stream as each group of the
+// layer's parameter gradients is complete -- FFN-out + LN2, FFN-in, attention output + LN1, QKV (the
+// data-parallel engine reduces each group behind its event: parallel/ddp.py early buckets).
 void layer_bwd_h3p(int64_t plan, int64_t dh2, int64_t xp, int64_t xe, int64_t mask, uint64_t s1, uint64_t o1,
-                   uint64_t s2, uint64_t o2, float p_h, float p_a, int wacc, int64_t st0_, int64_t st1_) {
+                   uint64_t s2, uint64_t o2, float p_h, float p_a, int wacc, int64_t st0_, int64_t st1_,
+                   int64_t events) {
   const int64_t* q = ptr<const int64_t>(plan);
+  const int64_t* evs = ptr<const int64_t>(events);
+  auto ready = [&](int g) {
+    if (evs && hipEventRecord(ptr<ihipEvent_t>(evs[g]), ptr<ihipStream_t>(st1_)) != hipSuccess)
+      throw std::runtime_error("layer program: hipEventRecord");
+  };
   hipStream_t st0 = ptr<ihipStream_t>(st0_), st1 = ptr<ihipStream_t>(st1_);
   const int B = (int)q[f_B], S = (int)q[f_S], NH = (int)q[f_NH], H = (int)q[f_H], F = (int)q[f_F];
   const int rows = (int)q[f_rows], nb = rows / 32;
@@ -216,12 +226,14 @@ void layer_bwd_h3p(int64_t plan, int64_t dh2, int64_t xp, int64_t xe, int64_t ma
   hs_stream_wait(st1, st0);
   finalize(q[f_part2_g], q[f_part2_b], q[f_part2_bias], q[f_gg2], q[f_gbb2], q[f_gb2]);
   wgrad(da2p, f1p, H, F, q[f_gw2], (int)q[f_ksg_w2], "FFN-out weight gradient");
+  ready(0);
   // FFN-in data gradient through the GELU (planes only; the FFN-in bias gradient from the column
   // partials), its weight gradient beside it, then dh1 = dz2 + df1 @ W1
   gemm(0, 0, rows, F, H, da2p, W2, nullptr, F, ptr<const float>(q[f_bi]), kEpiDgelu, 0.f, ptr<float>(q[f_f1pre]), F,
        ptr<float>(q[f_part_gelu]), ptr<float>(q[f_gbi]), 1, &df1p, 1, nullptr, 0, st0, "FFN-out data gradient");
   hs_stream_wait(st1, st0);
   wgrad(df1p, h1p, F, H, q[f_gw1], (int)q[f_ksg_w1], "FFN-in weight gradient");
+  ready(1);  // (the FFN-in bias gradient came from the compute stream before the fork)
   gemm(0, 0, rows, H, F, df1p, W1, dz2, H, nullptr, 0, 1.f, nullptr, 0, nullptr, nullptr, 0, nullptr, 1, nullptr, 0,
        st0, "FFN-in data gradient");
   // LN1 backward; its parameter gradients and the attention-output weight gradient on the side
@@ -233,6 +245,7 @@ void layer_bwd_h3p(int64_t plan, int64_t dh2, int64_t xp, int64_t xe, int64_t ma
   hs_stream_wait(st1, st0);
   finalize(q[f_part1_g], q[f_part1_b], q[f_part1_bias], q[f_gg1], q[f_gb1], q[f_gbo]);
   wgrad(da1p, ctxp, H, H, q[f_gwo], (int)q[f_ksg_wo], "attention-output weight gradient");
+  ready(2);
   float* dctx = ptr<float>(q[f_dctx]);
   gemm(0, 0, rows, H, H, da1p, Wo, dctx, H, nullptr, 0, 0.f, nullptr, 0, nullptr, nullptr, 0, nullptr, 1, nullptr, 0,
        st0, "attention-output data gradient");
@@ -247,6 +260,7 @@ void layer_bwd_h3p(int64_t plan, int64_t dh2, int64_t xp, int64_t xe, int64_t ma
   wgrad(dqkvp, X, 3 * H, H, q[f_gwqkv], (int)q[f_ksg_qkv], "QKV weight gradient");
   launch_colsum(0, dqkv, nullptr, nullptr, nullptr, ptr<float>(q[f_part_bq]), ptr<float>(q[f_gbqkv]), rows, 3 * H, 1,
                 st1, nullptr);
+  ready(3);
   gemm(0, 0, rows, H, 3 * H, dqkvp, Wqkv, dz1, H, nullptr, 0, 1.f, nullptr, 0, nullptr, nullptr, 0, nullptr, 1,
        nullptr, 0, st0, "QKV data gradient");
 }

@@ -385,6 +385,16 @@ class BertLayer(nn.Module):
         W.g2, W.bb2 = o.LayerNorm.weight.detach(), o.LayerNorm.bias.detach()
         return W
 
+    def grad_groups(self):
+        """This layer's parameters in the order the fused backward completes their gradients (FFN-out
+        + LN2, FFN-in, attention output + LN1, QKV): what the data-parallel engine may reduce one
+        group at a time (parallel/ddp.py early buckets)."""
+        sa, ao, o = self.attention.self, self.attention.output, self.output
+        return [[o.dense.weight, o.dense.bias, o.LayerNorm.weight, o.LayerNorm.bias],
+                [self.intermediate.dense_act.weight, self.intermediate.dense_act.bias],
+                [ao.dense.weight, ao.dense.bias, ao.LayerNorm.weight, ao.LayerNorm.bias],
+                [sa.query.weight, sa.key.weight, sa.value.weight, sa.query.bias, sa.key.bias, sa.value.bias]]
+
     def fused_ok(self, x, S):
         sa = self.attention.self
         H = sa.query.weight.shape[1]
@@ -404,6 +414,9 @@ class BertLayer(nn.Module):
         if getattr(self, "_hs_store", None) is not None:
             meta["grad_sink"] = self._grad_views
             meta["store"] = self._hs_store
+            early = self.__dict__.get("_hs_early")  # (parallel/ddp.py) per-group readiness of this layer
+            if early is not None:
+                meta["early"] = early
         return FusedBertLayer.apply(x2d, mask_i64, meta, *self.fused_params())
 
     def _grad_views(self):
@@ -726,6 +739,13 @@ class BertModel(BertPreTrainedModel):
         return ([list(e.parameters())] + [list(blk.parameters()) for blk in self.encoder.layer]
                 + [list(self.pooler.parameters())])
 
+    def grad_groups(self):
+        """The gradient groups of the encoder layer whose backward finishes last (layer 0)."""
+        return self.encoder.layer[0].grad_groups()
+
+    def early_layer(self):
+        return self.encoder.layer[0]
+
     def _param_ready(self, chunk):
         """Staged update (runtime/flat.py): wait for chunk ``chunk`` of the flat store -- 0 the
         embeddings, 1 + i encoder layer i, then the rest."""
@@ -882,6 +902,12 @@ class BertForPreTraining(BertPreTrainedModel):
             return mlm_scores, nsp_scores
         return (_xent(mlm_scores.reshape(-1, self.config.vocab_size), masked_lm_labels.reshape(-1), -1)
                 + _xent(nsp_scores.reshape(-1, 2), next_sentence_label.reshape(-1), -1))
+
+    def grad_groups(self):
+        return self.bert.grad_groups()
+
+    def early_layer(self):
+        return self.bert.early_layer()
 
     def update_groups(self):
         """Embeddings, each encoder layer, then the pooler and heads (the tied decoder weight is the

@@ -617,6 +617,7 @@ class _OneChain(object):
 # the native launch path (ops/layer_prog.py): False runs the Python layer (A/B, bench --ab prog_off)
 LAYER_PROG = True
 _PROGS: dict = {}
+_PROG_SIDE_DELAY = 0  # GPU cycles the side stream sleeps before a program backward (tests only)
 
 
 class _ProgSaved(object):
@@ -685,8 +686,15 @@ def _layer_backward_prog(ctx, dh2, x, saved, W, meta, cfg):
     for out in (Gv.w2, Gv.w1, Gv.wo, Gv.wqkv):  # lazy zero_grad bookkeeping (runtime/flat.py)
         (store.ensure_zero if wacc else store.mark_stored)(out)
     side = streams.backward_forks(dev, xp.planes, xp.exps)
+    if _PROG_SIDE_DELAY:  # (tests: a late side stream -- collectives must still wait for its groups)
+        with torch.cuda.stream(side):
+            torch.cuda._sleep(_PROG_SIDE_DELAY)
+    early = meta.get("early")  # (events address, launch callback): parallel/ddp.py early buckets
     hip().layer_bwd_h3p(prog.addr, dh2.data_ptr(), xp.data_ptr(), xp.exps_ptr(), mask_of(ctx).data_ptr(), s_1, o_1,
-                        s_2, o_2, float(p_h), float(p_a), int(wacc), stream_handle(), side.cuda_stream)
+                        s_2, o_2, float(p_h), float(p_a), int(wacc), stream_handle(), side.cuda_stream,
+                        early[0] if early is not None else 0)
+    if early is not None:
+        early[1]()
     return (prog.dz1.view(prog.rows, prog.H), None, None) + (None,) * 16
 
 

@@ -80,8 +80,9 @@ class NativeComm(object):
     # ------------------------------------------------------------------ bucket path
     def all_reduce_async(self, t, producers=(), op="sum"):
         """In-place all-reduce of contiguous ``t`` on the comm stream, ordered after the work
-        enqueued so far on every stream in ``producers`` (default: the current stream)."""
-        hs = [_stream(s) for s in producers] or [_stream()]
+        enqueued so far on every stream in ``producers`` (default: the current stream; None: only
+        after earlier comm-stream work)."""
+        hs = [] if producers is None else ([_stream(s) for s in producers] or [_stream()])
         self._c.all_reduce_async(t.data_ptr(), t.numel(), DTYPES[t.dtype], OPS[op], hs)
 
     def all_gather_async(self, out, t, producers=()):
@@ -100,6 +101,11 @@ class NativeComm(object):
         pass ``producers=None`` to order only after earlier comm-stream work."""
         hs = [] if producers is None else ([_stream(s) for s in producers] or [_stream()])
         self._c.reduce_scatter_async(t.data_ptr(), t.numel(), DTYPES[t.dtype], OPS[op], hs)
+
+    def wait_events(self, events):
+        """The comm stream waits for raw hipEvent_t handles the caller recorded (ordering the next
+        collective after exactly that work)."""
+        self._c.wait_events([int(e) for e in events])
 
     def all_gather_inplace_async(self, t, producers=()):
         """In-place all-gather of contiguous ``t``: every rank's piece r (of ``size`` equal pieces) to

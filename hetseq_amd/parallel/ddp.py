@@ -88,6 +88,22 @@ class FlatDDP(torch.nn.Module):
             for p in order:
                 per.setdefault(bisect_chunk(store.chunks, store.offset(p)), []).append(p)
             self.buckets = [per[c] for c in sorted(per, reverse=True)]
+            # the layer whose backward finishes last: one bucket per gradient group, each reduced
+            # behind its own readiness event from the fused backward (early buckets, below) -- only
+            # the last group's reduce-scatter is left for the end of the backward
+            eg = getattr(module, "grad_groups", None)
+            el = getattr(module, "early_layer", None)
+            groups = eg() if callable(eg) and callable(el) and self.comm is not None else None
+            if groups:
+                ids = [{id(p) for p in g} for g in groups]
+                c = bisect_chunk(store.chunks, store.offset(groups[0][0]))
+                if c in per and sum(len(x) for x in ids) == len(per[c]) and all(
+                        bisect_chunk(store.chunks, store.offset(p)) == c for g in groups for p in g):
+                    i = next(k for k, b in enumerate(self.buckets) if b is per[c])
+                    subs = [[p for p in per[c] if id(p) in x] for x in ids]
+                    self.buckets[i:i + 1] = subs
+                    self.early = list(range(i, i + len(subs)))
+                    self._early_layer = el()
         else:
             cur, size = [], 0
             for p in order:
@@ -103,15 +119,18 @@ class FlatDDP(torch.nn.Module):
                 self.buckets.append(cur)
         self.ranges = []
         self.bucket_of = {}
+        los = sorted(min(store.offset(p) for p in ps) for ps in self.buckets)
         for bi, ps in enumerate(self.buckets):
             lo = min(store.offset(p) for p in ps)
             hi = max(store.offset(p) + p.numel() for p in ps)
             if shard_optimizer and store.chunks is not None:
-                # (to its chunk's aligned end: the padding is zero in every buffer, and the region then
-                # splits into W whole pieces -- runtime/flat.py CHUNK_ALIGN)
+                # (to the next bucket's start inside its chunk, else the chunk's aligned end: the
+                # padding is zero in every buffer, and the region then splits into W whole pieces --
+                # runtime/flat.py CHUNK_ALIGN)
                 from hetseq_amd.runtime.flat import bisect_chunk
 
-                hi = store.chunks[bisect_chunk(store.chunks, lo)][1]
+                end = store.chunks[bisect_chunk(store.chunks, lo)][1]
+                hi = min([x for x in los if lo < x < end] + [end])
             self.ranges.append((lo, hi))
             for p in ps:
                 self.bucket_of[id(p)] = bi
@@ -134,6 +153,15 @@ class FlatDDP(torch.nn.Module):
             self.shard = ShardPlan(store, self.ranges, tables, self.plan_world, rank, comm=self.comm,
                                    group=self.process_group)
             store.shard = self.shard
+        if self.early and self.shard is not None and store.grad.is_cuda:
+            import array
+
+            from hetseq_amd.ops._C import hip
+
+            self._early_ev = array.array("q", [hip().event_create() for _ in self.early])
+            self._early_layer.__dict__["_hs_early"] = (self._early_ev.buffer_info()[0], self._early_launch)
+        else:
+            self.early = []
         self._reset_state()
         # Readiness = post-accumulate-grad hooks.  They also fire when a fused
         # Function returned None for a parameter whose gradient it accumulated
@@ -148,6 +176,21 @@ class FlatDDP(torch.nn.Module):
                     dist.broadcast(store.param, src=0, group=self.process_group)
             store.bump()
             store.sync_shadow()
+
+    early = []  # bucket indices reduced behind the fused backward's group events (backward order)
+
+    def _early_launch(self):
+        """Right after the early layer's fused backward was enqueued (ops/bert_ops.py): reduce its
+        gradient groups, each behind the event the backward recorded when the group was complete."""
+        if not self.require_sync:
+            return
+        for k, b in enumerate(self.early):
+            if self.next_launch != b:  # (an earlier bucket is not out yet: the hooks launch in order)
+                return
+            lo, hi = self.ranges[b]
+            self.comm.wait_events([self._early_ev[k]])
+            self._launch_range(lo, hi, "reducescatter_group%d" % b, producers=None)
+            self.next_launch += 1
 
     def _reset_state(self):
         self.pending = [len(ps) for ps in self.buckets]
@@ -221,7 +264,7 @@ class FlatDDP(torch.nn.Module):
             self._tail_started()  # the last bucket waited for the embedding backward (dense tables)
         self._launch_range(lo, hi, "allreduce_bucket%d" % b)
 
-    def _launch_range(self, lo, hi, name):
+    def _launch_range(self, lo, hi, name, producers=()):
         profiling.range_push(name)
         self.store.flush_range(lo, hi)  # (a lazily zeroed region no writer claimed: cleared before reducing)
         g = self.store.grad
@@ -231,7 +274,7 @@ class FlatDDP(torch.nn.Module):
         if self.comm is not None:
             # the comm stream waits for both producers; neither producer stream is stalled
             cur = torch.cuda.current_stream(g.device)
-            prod = (cur, side) if side is not None else (cur,)
+            prod = None if producers is None else ((cur, side) if side is not None else (cur,))
             if self.shard is not None:  # sharded update: reduce-scatter (tail all-reduced)
                 self.shard.reduce_bucket(lo, hi, prod)
             else:

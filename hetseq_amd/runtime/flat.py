@@ -71,8 +71,10 @@ class FlatParamStore(object):
         # chunk splits into W equal aligned pieces with no remainder
         firsts = set()
         ug = getattr(module, "update_groups", None)
+        gg = getattr(module, "grad_groups", None)  # finer groups the DP engine may reduce on their own
         pos = {id(q): i for i, m in enumerate(order) for q in m}
-        for g in (ug() or []) if callable(ug) else []:
+        groups_ = ((ug() or []) if callable(ug) else []) + ((gg() or []) if callable(gg) else [])
+        for g in groups_:
             ps = [p for p in g if id(p) in pos]
             if ps:
                 firsts.add(id(min(ps, key=lambda p: pos[id(p)])))

@@ -427,3 +427,58 @@ def test_bench_emulate_world_reports(tmp_path):
     assert "emulating dp8" in out["config"]["parallelism"]
     dc = out["dp_collectives"]
     assert dc["n"] > 0 and dc["received_mb"] > dc["payload_mb"]  # 2(W-1)/W > 1 at W = 8
+
+
+@pytest.mark.parametrize("delay", [0, 4_000_000])
+def test_sharded_early_buckets_snapshot_and_update(group, delay):
+    """Sharded update on the native engine (1 rank) with the layer program's per-group readiness
+    events: every reduce-scatter region -- the early layer's four groups included, with the side
+    stream held back -- reads the final gradient (snapshot mode), and an update step through the
+    shard plan equals the unsharded update."""
+    from argparse import Namespace
+
+    from hetseq_amd.ops import bert_ops
+    from hetseq_amd.ops import gemm as G
+    from hetseq_amd.optim.optimizers import _Adam
+    from hetseq_amd.parallel.ddp import FlatDDP
+    from hetseq_amd.runtime import rng
+    from hetseq_amd.runtime.flat import FlatParamStore
+    from tests.test_bert_gpu import _batch, _tiny
+
+    cuda = torch.device("cuda", 0)
+    G.set_fp32_mode("h3p")
+    out = {}
+    for shard in (False, True):
+        model, cfg = _tiny(cuda)
+        model.train()
+        model.max_predictions_per_seq = 10
+        store = FlatParamStore(model)
+        model.attach_store(store, torch.float32)
+        net = FlatDDP(model, store, comm_engine="native", timeout_s=60, shard_optimizer=shard)
+        opt = _Adam(Namespace(lr=[1e-3], adam_betas="(0.9,0.999)", adam_eps=1e-8, weight_decay=0.01),
+                    list(model.parameters()), store)
+        if shard:
+            assert store.shard is not None and len(net.early) == 4
+            snap = torch.full_like(store.grad, float("nan"))
+            net.comm.set_snapshot(snap, store.grad)
+        bert_ops._PROG_SIDE_DELAY = delay
+        try:
+            opt.zero_grad()
+            rng.set_seed(7)
+            net(*_batch(cuda, 16, 64, cfg.vocab_size)).backward()
+        finally:
+            bert_ops._PROG_SIDE_DELAY = 0
+        torch.cuda.synchronize()
+        if shard:
+            net.comm.set_snapshot(None, None)
+            for lo, hi in net.ranges:
+                assert torch.equal(snap[lo:hi], store.grad[lo:hi]), (lo, hi)
+            assert any(p.rows == 16 * 64 for p in bert_ops._PROGS.values())
+        opt.clip_grad_norm(1.0)
+        opt.step()
+        opt.state_dict()
+        torch.cuda.synchronize()
+        out[shard] = store.param.clone()
+        net.comm.check()
+        net.comm.close()
+    assert torch.allclose(out[True], out[False], rtol=1e-6, atol=1e-7), (out[True] - out[False]).abs().max().item()
