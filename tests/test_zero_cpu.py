@@ -38,9 +38,9 @@ def _batch(rank, step, cfg):
     return ids, tt, mask, labels, nsp
 
 
-def _worker(rank, port, shard, q):
+def _worker(rank, port, shard, q, world=2):
     try:
-        _work(rank, port, shard, q)
+        _work(rank, port, shard, q, world)
     except BaseException:
         import traceback
 
@@ -48,14 +48,14 @@ def _worker(rank, port, shard, q):
         raise
 
 
-def _work(rank, port, shard, q):
+def _work(rank, port, shard, q, world=2):
     from argparse import Namespace
 
     from hetseq_amd.optim.optimizers import _Adam
     from hetseq_amd.parallel.ddp import FlatDDP
     from hetseq_amd.runtime.flat import FlatParamStore
 
-    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, world_size=2, rank=rank)
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, world_size=world, rank=rank)
     torch.set_num_threads(2)
     model, cfg = _model()
     model.train(False)
@@ -86,17 +86,17 @@ def _work(rank, port, shard, q):
     dist.destroy_process_group()
 
 
-def _run(shard):
+def _run(shard, world=2):
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, port, shard, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, port, shard, q, world)) for r in range(world)]
     for p in procs:
         p.start()
-    out = [q.get(timeout=240) for _ in range(2)]
+    out = [q.get(timeout=240) for _ in range(world)]
     for o in out:
         assert o[0] != "error", o[2]
     for p in procs:
@@ -106,17 +106,19 @@ def _run(shard):
     return {r[1]: (r[0], r[1], conv(r[2]), r[3], {k: conv(v) for k, v in r[4].items()}, conv(r[5])) for r in out}
 
 
-def test_sharded_update_matches_unsharded_and_round_trips():
+@pytest.mark.parametrize("world", [2, pytest.param(8, marks=pytest.mark.skipif(
+    __import__("os").environ.get("HETSEQ_TEST_W8") != "1", reason="8 gloo ranks: HETSEQ_TEST_W8=1"))])
+def test_sharded_update_matches_unsharded_and_round_trips(world):
     from argparse import Namespace
 
     from hetseq_amd.optim.optimizers import _Adam
     from hetseq_amd.runtime.flat import FlatParamStore
 
-    full = _run(False)
-    sh = _run(True)
+    full = _run(False, world)
+    sh = _run(True, world)
     # every rank holds the same parameters after the all-gather
-    assert torch.equal(sh[0][2], sh[1][2])
-    for r in (0, 1):
+    assert all(torch.equal(sh[0][2], sh[r][2]) for r in range(1, world))
+    for r in range(world):
         p_full, p_sh = full[r][2], sh[r][2]
         assert torch.allclose(p_sh, p_full, rtol=1e-5, atol=1e-6), (p_sh - p_full).abs().max()
         for a, b in zip(full[r][3], sh[r][3]):
