@@ -793,51 +793,32 @@ static int g_ablation = 0;  // microbenchmark hook (tile_override bits 3-4)
 // transpose of its mn-contiguous staging, +8-12 % before the transposed-read layout; now it loses
 // in the step, see g_x6_wgrad_waves).  tile_override bit 5 forces 4, bit 6 forces 8.
 static int g_x6_waves = 4;
-// split-K block order of the split-bf16 kernel: slice-major (default; BERT-base fp32 step 15.04 vs
-// 15.13 ms tile-major, interleaved) or HETSEQ_X6_SLICE_MAJOR=0 tile-major
-static const int g_slice_major = [] {
-  const char* e = std::getenv("HETSEQ_X6_SLICE_MAJOR");
-  return e && e[0] == '0' ? 0 : 1;
-}();
-// waves per block of the weight-gradient (TA) launches: HETSEQ_X6_WGRAD_WAVES=4 / 8.  4 since the
-// transposed-read layout: beside the data-gradient chain (side stream, 2 K slices) the BERT-base fp32
-// step runs 15.20-15.28 ms vs 15.52-15.56 with 8 (interleaved, profiles/r2_gemm_experiments.md)
-static const int g_x6_wgrad_waves = [] {
-  const char* e = std::getenv("HETSEQ_X6_WGRAD_WAVES");
-  return e && e[0] == '8' ? 8 : 4;
-}();
-// 4-wave register prefetch depth (PF above): HETSEQ_X6_PF=1/2, tile_override bit 7 forces 2
-static const int g_x6_pf_env = [] {
-  const char* e = std::getenv("HETSEQ_X6_PF");
-  return e && e[0] == '2' ? 2 : 1;
-}();
+// split-K block order of the split-bf16 kernel: slice-major (BERT-base fp32 step 15.04 vs 15.13 ms
+// tile-major, interleaved)
+static const int g_slice_major = 1;
+// waves per block of the weight-gradient (TA) launches: 4 since the transposed-read layout: beside the
+// data-gradient chain (side stream, 2 K slices) the BERT-base fp32 step runs 15.20-15.28 ms vs
+// 15.52-15.56 with 8 (interleaved, profiles/r2_gemm_experiments.md)
+static const int g_x6_wgrad_waves = 4;
+// 4-wave register prefetch depth (PF above): 1; tile_override bit 7 forces 2 (tests)
+static const int g_x6_pf_env = 1;
 static int g_x6_pf = 1;
-// mn-contiguous operands in the transposed-read layout (default; HETSEQ_X6_TR=0 restores the
-// register transpose): weight gradients 7-12 % and NN data gradients 3-10 % faster on the BERT
-// shapes (profiles/r2_gemm_experiments.md).  tile_override bit 8 forces it, bit 9 forces the
-// register-transpose layout.
-static const int g_x6_tr_env = [] {
-  const char* e = std::getenv("HETSEQ_X6_TR");
-  return e && e[0] == '0' ? 0 : 1;
-}();
+// mn-contiguous operands in the transposed-read layout: weight gradients 7-12 % and NN data gradients
+// 3-10 % faster on the BERT shapes than the register transpose (profiles/r2_gemm_experiments.md).
+// tile_override bit 8 forces it, bit 9 forces the register-transpose layout (tests).
+static const int g_x6_tr_env = 1;
 static int g_x6_tr = 0;
 // h3 engine (NT 4) at three 4-wave blocks per CU (registers for 168 VGPRs; two planes need less LDS):
-// HETSEQ_H3_OCC3=1, tile_override bit 10 forces it
+// tile_override bit 10 forces it.
 // Bit mask of the product kinds (launch_occ3) that run at three blocks per CU.  Default 5 (forward and
 // weight gradient): measured in the BERT-base fp32 step (interleaved A/B, 8 rounds) 12.13 ms against
 // 12.35 with none; data gradients at 3 blocks lose (+0.5 ms: they share the CUs with the weight-gradient
 // stream and the LN backward).  profiles/r4_h3_gemm.md.
-static int g_h3_occ3_env = [] {
-  const char* e = std::getenv("HETSEQ_H3_OCC3");
-  return e ? std::atoi(e) & 7 : 5;
-}();
+static int g_h3_occ3_env = 5;
 static int g_h3_occ3 = 0;
-// 8-wave variant with double-buffered LDS images (106 KB: one block per CU, one barrier per K
-// tile) -- HETSEQ_X6_DBUF=1; default single buffer (53 KB, blocks of other kernels co-reside).
-static const int g_x6_dbuf = [] {
-  const char* e = std::getenv("HETSEQ_X6_DBUF");
-  return e && e[0] == '1' ? 1 : 0;
-}();
+// single-buffered LDS images (53 KB: blocks of other kernels co-reside; the double-buffered 106 KB
+// 8-wave variant measured slower in the step and is off)
+static const int g_x6_dbuf = 0;
 
 // split-K finish: C = sum_s slab[s] (+ bias) (+ beta * C), fixed slice order (deterministic).
 // Blocks past `gmain` (weight gradient with fused column sums, wcol) finish the bias gradient in the
@@ -1004,11 +985,8 @@ void launch_splitk_reduce(const float* slab, int ksplit, int M, int N, float* C,
                           float beta, int Mv, int Nv, hipStream_t st) {
   launch_splitk_reduce_cols(slab, ksplit, M, N, C, ldc, bias, beta, Mv, Nv, st, nullptr, nullptr, 0);
 }
-// wcol's bias gradient folded into the split-K pass (HETSEQ_WCOL_IN_REDUCE=0: its own reduce_rows)
-static int g_wcol_fold = [] {
-  const char* e = std::getenv("HETSEQ_WCOL_IN_REDUCE");
-  return e && e[0] == '0' ? 0 : 1;
-}();
+// wcol's bias gradient folded into the split-K pass (set_wcol_fold(0): its own reduce_rows; tests)
+static int g_wcol_fold = 1;
 void set_wcol_fold(int on) { g_wcol_fold = on ? 1 : 0; }
 
 // Tile choice: the largest tile that still gives >= 2 blocks per CU (256 CUs).

@@ -504,11 +504,8 @@ void set_planes_variant(int v) { g_planes_variant = v; }
 
 // planes: 1 (bf16) or 3 (split fp32); c_dtype: 0 fp32 C, 1 bf16 C.  Operand strides / plane
 // strides in elements.  Returns -1 (nothing launched) for shapes it does not serve: M, N
-// split-K block order (HETSEQ_PLANES_SLICE_MAJOR=1 slice-major, default tile-major)
-static const int g_planes_slice_major = [] {
-  const char* e = std::getenv("HETSEQ_PLANES_SLICE_MAJOR");
-  return e && e[0] == '1' ? 1 : 0;
-}();
+// split-K block order: tile-major
+static const int g_planes_slice_major = 0;
 
 // multiples of 128, K a multiple of BK * ksplit, 16-B aligned rows.
 int launch_gemm_planes(int planes, int c_dtype, int ta, int tb, int M, int N, int K, const void* A, int64_t lda,

@@ -265,10 +265,7 @@ HS_DEVICE void colpart_chunked_store(float (&acc)[NV][4], float* __restrict__ pa
 }
 
 // 0: [WV][H] LDS reduction (12 KB at H 768); 1: the 3 KB chunked one (default) -- set_ln_bwd_lds
-static int g_lnbwd_chunked = [] {
-  const char* e = std::getenv("HETSEQ_LNBWD_LDS");
-  return e && e[0] == 'f' ? 0 : 1;
-}();
+static int g_lnbwd_chunked = 1;
 
 // One row per wave at a time, with the NEXT row's dy / z / statistics loaded before this row's
 // reductions (two rows of loads in flight per wave); gamma is loaded once per wave.  Small
@@ -632,13 +629,9 @@ __global__ void __launch_bounds__(256) emb_bwd_kernel(const T* __restrict__ dy, 
   }
 }
 
-// column-partial blocks of the LN / embedding backward: HETSEQ_LNBWD_BLOCKS (default 256: 4 rows
-// per wave; 512 / 1024 blocks measured 25.0 / 27.0 us isolated vs 25.3, and slower in the step)
-static const int kLnBwdBlocks = [] {
-  const char* e = std::getenv("HETSEQ_LNBWD_BLOCKS");
-  const int v = e ? std::atoi(e) : 256;
-  return v >= 64 && v <= 4096 ? v : 256;
-}();
+// column-partial blocks of the LN / embedding backward: 256 (4 rows per wave; 512 / 1024 blocks
+// measured 25.0 / 27.0 us isolated vs 25.3, and slower in the step)
+static const int kLnBwdBlocks = 256;
 
 template <int NV, typename T>
 void ln_fwd_launch(const void* a, const float* bias, const void* resid, const float* gamma, const float* beta, void* y,

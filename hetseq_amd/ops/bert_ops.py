@@ -28,20 +28,20 @@ import torch
 from hetseq_amd.ops import gemm as G
 
 # the attention-output and FFN-out products' split-K partials summed by the LN forward instead of a
-# reduce pass (HETSEQ_LN_PARTIALS=0: reduce in the GEMM as before)
-_LN_PARTIALS = os.environ.get("HETSEQ_LN_PARTIALS", "1") == "1"
+# reduce pass 
+_LN_PARTIALS = True
 _LN_PARTIALS_WO = _LN_PARTIALS  # (the attention-output product's part of the switch, for bench --ab)
 # the QKV bias gradient summed by the QKV weight-gradient kernel (gemm.linear_wgrad_colsum) instead of
-# a column-sum pass over dqkv (HETSEQ_WGRAD_COLSUM=0: separate pass)
-_WGRAD_COLSUM = os.environ.get("HETSEQ_WGRAD_COLSUM", "1") == "1"
+# a column-sum pass over dqkv 
+_WGRAD_COLSUM = True
 # the FFN-in bias gradient the same way, from the FFN-in weight-gradient launch on the side stream,
 # instead of the dGELU data-gradient epilogue's column partials + a reduce pass on the compute stream
-# (HETSEQ_FFN_BIAS_WGRAD=0: in the dGELU epilogue)
-_FFN_BIAS_WGRAD = os.environ.get("HETSEQ_FFN_BIAS_WGRAD", "1") == "1"
-# the pooler / NSP parameter gradients on the weight-gradient stream (HETSEQ_POOL_WGRAD_SIDE=0: in line)
-_POOL_WGRAD_SIDE = os.environ.get("HETSEQ_POOL_WGRAD_SIDE", "1") == "1"
-# weight gradients store (beta 0) in the first backward after zero_grad (HETSEQ_FRESH_WGRAD=0: always add)
-_FRESH_WGRAD = os.environ.get("HETSEQ_FRESH_WGRAD", "1") == "1"
+# 
+_FFN_BIAS_WGRAD = True
+# the pooler / NSP parameter gradients on the weight-gradient stream
+_POOL_WGRAD_SIDE = True
+# weight gradients store (beta 0) in the first backward after zero_grad
+_FRESH_WGRAD = True
 from hetseq_amd.ops._C import dtype_code, hip, stream_handle
 from hetseq_amd.parallel import tied
 from hetseq_amd.runtime import rng, streams
@@ -508,8 +508,8 @@ def _am(am, *pairs):
 # The fp32 encoder-layer forward runs the batch as two half-batch chains on two streams (the compute
 # stream and streams.fwd2, the idle weight-gradient stream): a single chain leaves the GEMMs' last partial round of tiles on a mostly
 # idle chip (QKV: 576 tiles of 128 x 128 for 512 block slots), and the other half's kernels fill it
-# (12 BERT-base layers 4.96 -> 4.42 ms, tools/fwd_split_probe.py).  HETSEQ_FWD_SPLIT=0 turns it off.
-_FWD_SPLIT = os.environ.get("HETSEQ_FWD_SPLIT", "1") == "1"
+# (12 BERT-base layers 4.96 -> 4.42 ms, tools/fwd_split_probe.py).
+_FWD_SPLIT = True
 # K split of the half-batch chains' plain GEMMs (None: the per-shape isolated measurement)
 _FWD_KS = None
 
@@ -600,8 +600,8 @@ def _layer_forward(x, mask, W, cfg, save, am=None, meta=None):
 # (ops/h3p.py, csrc/kernels/gemm_h3p.hip).  K slices of the forward's two N = 768 products, whose
 # tile grids (48-96 tiles per half-batch chain) would leave most of the chip idle; their slabs go
 # straight into the LayerNorm forward (no reduce pass).
-_H3P_KS_WO = int(os.environ.get("HETSEQ_H3P_KS_WO", "2"))
-_H3P_KS_W2 = int(os.environ.get("HETSEQ_H3P_KS_W2", "2"))
+_H3P_KS_WO = 2
+_H3P_KS_W2 = 2
 
 
 class _OneChain(object):

@@ -22,7 +22,7 @@ products (``x6``: fp32-level error, no scale needed), or on the exact-fp32 MFMA 
 ``HETSEQ_GEMM=hip|blas|auto`` selects; ``auto`` (default) times both paths --
 including the epilogue work the fused kernel absorbs -- once per (shape,
 transpose, epilogue) on the GPU and keeps the hand-written engine unless the
-library is faster by more than ``HETSEQ_GEMM_HIP_MARGIN`` (default 1.10: a
+library is faster by more than ``HIP_MARGIN`` (1.10: a
 one-shot timing of two ~equal kernels is noise, and a 10 % edge measured alone
 did not survive inside the overlapped training step -- docs/kernels.md).  The choice is
 recorded in ``GEMM_CHOICES`` and logged by the benchmark.  In bf16 mode the
@@ -49,7 +49,7 @@ SPLIT_ENGINES = ("x6", "h3", "h3p")  # the fp32-level split engines (x3 is a ben
 _SLABS: dict = {}  # (device, stream) -> split-K partial-sum workspace
 
 EPI_NONE, EPI_BIAS, EPI_GELU, EPI_DGELU = 0, 1, 2, 3
-HIP_MARGIN = float(os.environ.get("HETSEQ_GEMM_HIP_MARGIN", "1.10"))
+HIP_MARGIN = 1.10
 
 
 def _hip_wins(t_hip, t_blas):
@@ -819,8 +819,8 @@ def _seg_table(ts):
 
 
 # weight |max| of all but the first layer measured on the weight-gradient stream (idle at the start
-# of the forward) beside the first layer's work (HETSEQ_SPLIT_WEIGHT_AMAX=0: all at once, in line)
-_SPLIT_WEIGHT_AMAX = os.environ.get("HETSEQ_SPLIT_WEIGHT_AMAX", "1") == "1"
+# of the forward) beside the first layer's work
+_SPLIT_WEIGHT_AMAX = True
 _REST_EVENTS: dict = {}
 
 

@@ -40,13 +40,12 @@ _ENABLED = os.environ.get("HETSEQ_WGRAD_STREAM", "1") == "1"
 # split-K of the side-stream wgrad GEMMs.  The per-call-site choice is measured with the GEMM
 # alone on the chip (4 slices for most weight gradients); running beside the dgrad chain, 2 slices
 # measured best (BERT-base fp32: 16.6 ms/step vs 17.6 with the isolated choice, 19.2 with 1).
-# "auto" = use the isolated measurement.
-_ks = os.environ.get("HETSEQ_SIDE_KSPLIT", "2")
-SIDE_KSPLIT = None if _ks == "auto" else int(_ks)
+# (None = the isolated measurement; re-measured in round 5: 1 or 2 slices everywhere were slower.)
+SIDE_KSPLIT = 2
 # ... except the small ones (output <= 768 x 768, the attention-output projection: 36 tiles, 72
 # blocks at 2 slices), which take 4: 15.431 / 15.442 / 15.451 ms/step vs 15.491 / 15.540 / 15.511
 # with 2 and 15.46-15.50 with 8 (interleaved, profiles/r2_gemm_experiments.md)
-SIDE_KSPLIT_SMALL = int(os.environ.get("HETSEQ_SIDE_KSPLIT_SMALL", "4"))
+SIDE_KSPLIT_SMALL = 4
 
 
 def side_ksplit(M, N):
@@ -59,12 +58,11 @@ def side_ksplit(M, N):
 # measurement picks (4 slices for the N = 768 products) only adds slab traffic and a reduction
 # pass.  1 measured best (BERT-base fp32, interleaved runs: 15.53 / 15.55 ms/step vs 15.72 with the
 # isolated choice, profiles/r2_gemm_experiments.md); "auto" = use the isolated measurement.
-_dks = os.environ.get("HETSEQ_DGRAD_KSPLIT", "1")
-DGRAD_KSPLIT = None if _dks == "auto" else int(_dks)
+DGRAD_KSPLIT = 1
 _STREAMS: dict = {}
 _state = {"queued": False, "coalesce": 0}
 # share one fork event between consecutive side-stream launches (bench --ab fork_co / fork_each)
-COALESCE = os.environ.get("HETSEQ_FORK_COALESCE", "1") == "1"
+COALESCE = True
 
 
 def set_enabled(flag: bool):
@@ -124,15 +122,14 @@ def role(stream_handle: int) -> str:
 # Half-batch chains that run through several layers without meeting (:class:`fwd_chain`): each
 # half only reads its own rows, so the two streams need to meet once before the first layer and
 # once after the last, not at every layer boundary (where the faster half idles until the slower
-# one's LayerNorm ends, and each meeting costs an event round trip).  HETSEQ_FWD_CHAIN=0: meet at
-# every layer.
-FWD_CHAIN = os.environ.get("HETSEQ_FWD_CHAIN", "1") == "1"
+# one's LayerNorm ends, and each meeting costs an event round trip).
+FWD_CHAIN = True
 # Inside a chain, every later layer still orders fwd2 after the current stream's work so far (one
 # event, one way: the current stream never waits): that layer's whole-batch outputs come from the
 # current stream's allocator pool, which may hand out a block whose previous use -- a current-stream
 # kernel enqueued after the first fork -- is still pending; fwd2 must not write its half into it
-# before that kernel ran.  HETSEQ_FWD_CHAIN_FORK=0 drops the per-layer wait (unsafe; A/B only).
-FWD_CHAIN_FORK = os.environ.get("HETSEQ_FWD_CHAIN_FORK", "1") == "1"
+# before that kernel ran.
+FWD_CHAIN_FORK = True
 _chain = {"depth": 0, "forked": None, "keep": []}
 
 
