@@ -411,12 +411,21 @@ class BertLayer(nn.Module):
         seeds = tuple(rng.fork() if p > 0 else (0, 0) for p in (p_a, p_h, p_h))
         cfg = (B, S, self.attention.self.num_attention_heads, p_h, p_a, self.output.LayerNorm.variance_epsilon, seeds)
         meta = {"weights": self._weights, "cfg": cfg, "recompute": recompute, "amax": amax}
-        if getattr(self, "_hs_store", None) is not None:
+        store = getattr(self, "_hs_store", None)
+        if store is not None:
             meta["grad_sink"] = self._grad_views
-            meta["store"] = self._hs_store
+            meta["store"] = store
             early = self.__dict__.get("_hs_early")  # (parallel/ddp.py) per-group readiness of this layer
             if early is not None:
                 meta["early"] = early
+            if x2d.requires_grad:
+                # gradients go straight into the store: no parameter inputs (no AccumulateGrad nodes,
+                # no per-parameter hooks); the backward reports the layer's parameters ready at its end
+                ready = getattr(store, "ready_cb", None)
+                if ready is not None:
+                    params = self.fused_params()
+                    meta["ready"] = lambda: ready(params)
+                return FusedBertLayer.apply(x2d, mask_i64, meta)
         return FusedBertLayer.apply(x2d, mask_i64, meta, *self.fused_params())
 
     def _grad_views(self):

@@ -844,10 +844,14 @@ def mask_of(ctx):
 class FusedBertLayer(torch.autograd.Function):
     """One post-LN BERT encoder layer.  Inputs after ``x, mask, meta`` are the
     16 parameters in reference order (q.w, q.b, k.w, k.b, v.w, v.b, o.w, o.b,
-    ln1.w, ln1.b, i.w, i.b, out.w, out.b, ln2.w, ln2.b)."""
+    ln1.w, ln1.b, i.w, i.b, out.w, out.b, ln2.w, ln2.b) -- or none, when the layer's
+    gradients go straight into a flat store (``meta["grad_sink"]``): autograd then keeps no
+    AccumulateGrad node per parameter, and the backward reports the parameters' readiness itself
+    (``meta["ready"]``: the data-parallel engine's bucket bookkeeping, parallel/ddp.py)."""
 
     @staticmethod
     def forward(ctx, x, mask, meta, *params):
+        ctx.nparams = len(params)
         W, cfg, recompute = meta["weights"](), meta["cfg"], meta["recompute"]
         # (the native program only for forwards whose backward will run: autograd is off in here)
         h2, saved = _layer_forward(x, mask, W, cfg, save=not recompute, am=meta.get("amax"),
@@ -870,6 +874,16 @@ class FusedBertLayer(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dh2):
+        grads = FusedBertLayer._backward(ctx, dh2)
+        if ctx.nparams == 0:
+            ready = ctx.meta.get("ready")
+            if ready is not None:
+                ready()
+            return grads[:3]
+        return grads
+
+    @staticmethod
+    def _backward(ctx, dh2):
         meta, cfg = ctx.meta, ctx.cfg
         W = meta["weights"]()
         if ctx.prog is not None:

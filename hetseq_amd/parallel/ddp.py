@@ -168,6 +168,9 @@ class FlatDDP(torch.nn.Module):
         # directly into the flat buffer (the AccumulateGrad node still runs, after
         # that Function's kernels were enqueued), so one signal covers both paths.
         self._hooks = [p.register_post_accumulate_grad_hook(self._grad_ready) for p in params]
+        # fused layers whose backward writes the store directly report their parameters here (one
+        # call per layer instead of one hook per parameter: models/bert.py BertLayer.fused)
+        store.ready_cb = self._params_ready
         if broadcast and (self.world_size > 1 or self.comm is not None):
             with torch.no_grad():
                 if self.comm is not None:
@@ -239,6 +242,10 @@ class FlatDDP(torch.nn.Module):
             self.require_sync = old
 
     # ------------------------------------------------------------- hooks
+    def _params_ready(self, params):
+        for p in params:
+            self._grad_ready(p)
+
     def _grad_ready(self, p):
         if not self.require_sync:
             return
