@@ -554,11 +554,7 @@ _AB = {
     "ddec8": lambda: _set_decoder_dgrad_ks(8),  # K split of the tied decoder's data gradient (K = vocab)
     "ddec16": lambda: _set_decoder_dgrad_ks(16),
     "ddec32": lambda: _set_decoder_dgrad_ks(32),
-    # K split of the half-batch attention-output product (its partials go to the LN forward)
-    "wo_ks1": lambda: _set_site_ks((2048, 768, 768, False, True, 0, False), 1),
-    "wo_ks2": lambda: _set_site_ks((2048, 768, 768, False, True, 0, False), 2),
-    "wo_ks4": lambda: _set_site_ks((2048, 768, 768, False, True, 0, False), 4),
-    # ... and of the half-batch FFN-out product
+    # K split of the half-batch FFN-out product (h3 engine; its partials go to the LN forward)
     "fo_ks2": lambda: _set_site_ks((2048, 768, 3072, False, True, 0, False), 2),
     "fo_ks4": lambda: _set_site_ks((2048, 768, 3072, False, True, 0, False), 4),
     "lnpo_on": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_LN_PARTIALS_WO", True),  # attention-output part
@@ -604,9 +600,11 @@ _AB = {
     # K slices of the h3p forward's N = 768 products (ops/bert_ops.py _H3P_KS_WO / _H3P_KS_W2)
     "wo_ks1": lambda: setattr(__import__("hetseq_amd.ops.bert_ops", fromlist=["x"]), "_H3P_KS_WO", 1),
     "wo_ks2": lambda: setattr(__import__("hetseq_amd.ops.bert_ops", fromlist=["x"]), "_H3P_KS_WO", 2),
+    "wo_ks4": lambda: setattr(__import__("hetseq_amd.ops.bert_ops", fromlist=["x"]), "_H3P_KS_WO", 4),
     "w2_ks1": lambda: setattr(__import__("hetseq_amd.ops.bert_ops", fromlist=["x"]), "_H3P_KS_W2", 1),
     "w2_ks2": lambda: setattr(__import__("hetseq_amd.ops.bert_ops", fromlist=["x"]), "_H3P_KS_W2", 2),
     "w2_ks4": lambda: setattr(__import__("hetseq_amd.ops.bert_ops", fromlist=["x"]), "_H3P_KS_W2", 4),
+    "w2_ks8": lambda: setattr(__import__("hetseq_amd.ops.bert_ops", fromlist=["x"]), "_H3P_KS_W2", 8),
     # waves per 32-row block of the h3p LayerNorm forward
     "lnw8": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_ln_h3p_waves(8),
     "lnw16": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_ln_h3p_waves(16),

@@ -601,7 +601,7 @@ def _layer_forward(x, mask, W, cfg, save, am=None, meta=None):
 # tile grids (48-96 tiles per half-batch chain) would leave most of the chip idle; their slabs go
 # straight into the LayerNorm forward (no reduce pass).
 _H3P_KS_WO = 2
-_H3P_KS_W2 = 2
+_H3P_KS_W2 = 4
 
 
 class _OneChain(object):
@@ -635,7 +635,7 @@ def _program(W, meta, B, S, NH, p_a, halves, dev):
             and meta.get("grad_sink") is not None and meta.get("store") is not None):
         return None
     Gv = meta["grad_sink"]()
-    key = (id(W.h3p), id(Gv), B, S, halves, p_a > 0)
+    key = (id(W.h3p), id(Gv), B, S, halves, p_a > 0, _H3P_KS_WO, _H3P_KS_W2)
     prog = _PROGS.get(key)
     if prog is None:
         from hetseq_amd.ops.layer_prog import LayerProgram
