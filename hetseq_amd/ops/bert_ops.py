@@ -635,7 +635,8 @@ def _program(W, meta, B, S, NH, p_a, halves, dev):
             and meta.get("grad_sink") is not None and meta.get("store") is not None):
         return None
     Gv = meta["grad_sink"]()
-    key = (id(W.h3p), id(Gv), B, S, halves, p_a > 0, _H3P_KS_WO, _H3P_KS_W2)
+    key = (id(W.h3p), id(Gv), B, S, halves, p_a > 0, _H3P_KS_WO, _H3P_KS_W2, streams.SIDE_KSPLIT,
+           streams.SIDE_KSPLIT_SMALL)
     prog = _PROGS.get(key)
     if prog is None:
         from hetseq_amd.ops.layer_prog import LayerProgram
