@@ -467,7 +467,7 @@ int launch_gemm_h3p(int ta, int tb, int M, int N, int K, const void* A, int64_t 
   auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
   if (!A || !B || !ea || !eb || !al16(A) || !al16(B) || lda % 8 || ldb % 8 || a_ps % 8 || b_ps % 8) return -1;
   if (epi < 0 || epi > 3 || (epi >= 1 && !bias) || (epi >= 2 && (!aux || beta != 0.f || ksplit > 1))) return -1;
-  if (epi == 3 && !part != !colsum) return -1;
+  if (epi == 3 && colsum && !part) return -1;  // (part without colsum: the caller reduces the partials)
   if (cp && (epi < 2 || !ec || ldcp % 32)) return -1;  // (the result's planes are written blocked)
   if (epi < 2 && !C && ksplit == 1) return -1;
   if (epi >= 2 && !C && !cp) return -1;
@@ -484,7 +484,7 @@ int launch_gemm_h3p(int ta, int tb, int M, int N, int K, const void* A, int64_t 
                          : q_launch_epi<true, false>(ksplit > 1 ? 0 : epi, a, st);
   if (rc) return rc;
   if (ksplit > 1 && C) launch_splitk_reduce(slab, ksplit, M, N, C, ldc, epi == 1 ? bias : nullptr, beta, M, N, st);
-  if (epi == kQDGelu && part) {
+  if (epi == kQDGelu && part && colsum) {
     const float* parts[1] = {part};
     float* outs[1] = {colsum};
     launch_reduce_rows(parts, outs, 1, M / QT, N, colsum_acc, st);

@@ -230,8 +230,13 @@ void layer_bwd_h3p(int64_t plan, int64_t dh2, int64_t xp, int64_t xe, int64_t ma
   // FFN-in data gradient through the GELU (planes only; the FFN-in bias gradient from the column
   // partials), its weight gradient beside it, then dh1 = dz2 + df1 @ W1
   gemm(0, 0, rows, F, H, da2p, W2, nullptr, F, ptr<const float>(q[f_bi]), kEpiDgelu, 0.f, ptr<float>(q[f_f1pre]), F,
-       ptr<float>(q[f_part_gelu]), ptr<float>(q[f_gbi]), 1, &df1p, 1, nullptr, 0, st0, "FFN-out data gradient");
+       ptr<float>(q[f_part_gelu]), nullptr, 1, &df1p, 1, nullptr, 0, st0, "FFN-out data gradient");
   hs_stream_wait(st1, st0);
+  {  // the FFN-in bias gradient from the dGELU epilogue's column partials, off the data-gradient chain
+    const float* parts[1] = {ptr<const float>(q[f_part_gelu])};
+    float* outs[1] = {ptr<float>(q[f_gbi])};
+    launch_colpart_finalize(parts, outs, 1, rows / 128, F, 1, st1);
+  }
   wgrad(df1p, h1p, F, H, q[f_gw1], (int)q[f_ksg_w1], "FFN-in weight gradient");
   ready(1);  // (the FFN-in bias gradient came from the compute stream before the fork)
   gemm(0, 0, rows, H, F, df1p, W1, dz2, H, nullptr, 0, 1.f, nullptr, 0, nullptr, nullptr, 0, nullptr, 1, nullptr, 0,
