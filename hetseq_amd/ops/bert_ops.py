@@ -616,7 +616,7 @@ class _OneChain(object):
 
 # the native launch path (ops/layer_prog.py): False runs the Python layer (A/B, bench --ab prog_off)
 LAYER_PROG = True
-_PROGS: dict = {}
+PROG_BUILDS = [0]  # programs built in this process (tests)
 _PROG_SIDE_DELAY = 0  # GPU cycles the side stream sleeps before a program backward (tests only)
 
 
@@ -635,9 +635,12 @@ def _program(W, meta, B, S, NH, p_a, halves, dev):
             and meta.get("grad_sink") is not None and meta.get("store") is not None):
         return None
     Gv = meta["grad_sink"]()
+    # (held by the layer module: a program -- its arena, the store addresses it bakes in -- lives as
+    # long as the model it was built for)
+    progs = meta["weights"].__self__.__dict__.setdefault("_hs_progs", {})
     key = (id(W.h3p), id(Gv), B, S, halves, p_a > 0, _H3P_KS_WO, _H3P_KS_W2, streams.SIDE_KSPLIT,
            streams.SIDE_KSPLIT_SMALL)
-    prog = _PROGS.get(key)
+    prog = progs.get(key)
     if prog is None:
         from hetseq_amd.ops.layer_prog import LayerProgram
 
@@ -648,7 +651,8 @@ def _program(W, meta, B, S, NH, p_a, halves, dev):
             return max(streams.side_ksplit(M, N) or 1, -(-rows // 4096))
         prog = LayerProgram(W, Gv, B, S, NH, halves, _H3P_KS_WO, _H3P_KS_W2,
                             {"qkv": ksg(3 * H, H), "wo": ksg(H, H), "w1": ksg(F, H), "w2": ksg(H, F)}, p_a > 0, dev)
-        _PROGS[key] = prog
+        progs[key] = prog
+        PROG_BUILDS[0] += 1
     return prog
 
 
