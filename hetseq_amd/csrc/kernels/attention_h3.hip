@@ -455,10 +455,12 @@ HS_DEVICE void dkv_body(char* __restrict__ smem, int bx, int bh, const float* __
     }
   }
   if (!active) return;
-  float* out = dqkv + ((int64_t)b * S + key) * ld + h * kHD;
   uint32_t cm = 0u;
-  store_rows(out + H, dk0, dk1, hf, ldexpf(1.f, -(eq_run + es)), cm);
-  store_rows(out + 2 * H, dv0, dv1, hf, ldexpf(1.f, -(eo_run + ep)), cm);
+  if (dqkv) {
+    float* out = dqkv + ((int64_t)b * S + key) * ld + h * kHD;
+    store_rows(out + H, dk0, dk1, hf, ldexpf(1.f, -(eq_run + es)), cm);
+    store_rows(out + 2 * H, dv0, dv1, hf, ldexpf(1.f, -(eo_run + ep)), cm);
+  }
   if (amax) amax_commit(amax, cm);
   if (po.pl) {  // dK, dV as h3p planes of dqkv [B*S][3H] (exponent row stride 3H / 32)
     const int64_t row = (int64_t)b * S + key;
@@ -573,7 +575,7 @@ HS_DEVICE void dq_body(char* __restrict__ smem, int bx, int bh, const float* __r
   }
   if (!active) return;
   uint32_t cm = 0u;
-  store_rows(dqkv + tok * ld + h * kHD, dq0, dq1, hf, 0.125f * ldexpf(1.f, -(ek_run + es)), cm);
+  if (dqkv) store_rows(dqkv + tok * ld + h * kHD, dq0, dq1, hf, 0.125f * ldexpf(1.f, -(ek_run + es)), cm);
   if (amax) amax_commit(amax, cm);
   if (po.pl)
     store_rows_h3p(po, tok, h * kHD, ld, po.ex + ((int64_t)b * S + q0) / 32 * (ld / 32) + h * kHD / 32, dq0, dq1, hf,
@@ -741,6 +743,7 @@ int launch_attn_bwd_h3(const float* qkv, const int64_t* mask, const float* bqkv,
                        const float* lse, float* Dbuf, float* dqkv, const uint32_t* dmask, int B, int S, int NH, int D,
                        float p, hipStream_t st, float* amax, void* pl, int64_t ps, int8_t* ex) {
   if (D != kHD || S % 32 != 0 || S <= 0 || (p > 0.f && dmask == nullptr)) return -1;
+  if (!dqkv && (!pl || amax)) return -1;  // dqkv may be written only as the planes
   const AttnPl po{static_cast<uint16_t*>(pl), ps, ex};
   const bool fused_d = S <= 128;  // each head's one dK / dV block stages every query once
   if (!fused_d) {

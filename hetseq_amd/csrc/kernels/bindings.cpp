@@ -120,6 +120,7 @@ int launch_gemm_h3p(int ta, int tb, int M, int N, int K, const void* A, int64_t 
 int launch_h3p_split(const float* src, int64_t lds, int rows, int cols, void* dst, int64_t ldd, int64_t ps, int8_t* ex,
                      int64_t lde, int blocked, hipStream_t st);
 int h3p_split_seg_bytes();
+int launch_h3p_colpart(const void*, int64_t, int64_t, const int8_t*, int64_t, int, int, float*, hipStream_t);
 void launch_h3p_split_multi(const void* table, int nseg, int total, hipStream_t st);
 
 // mnist.hip
@@ -461,6 +462,11 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("ldaux"), py::arg("part"), py::arg("colsum"), py::arg("colsum_acc"), py::arg("cp"), py::arg("ldcp"),
      py::arg("cp_ps"), py::arg("ec"), py::arg("lde_c"), py::arg("ksplit"), py::arg("slab"), py::arg("slab_floats"),
      py::arg("st"), py::arg("ablk") = 0, py::arg("bblk") = 0);
+  m.def("h3p_colpart", [](i64 pl, i64 ld, i64 ps, i64 ex, i64 lde, int rows, int cols, i64 part, i64 st) {
+    pre_launch("h3p_colpart");
+    check(launch_h3p_colpart(P(const void*, pl), ld, ps, P(const int8_t*, ex), lde, rows, cols, P(float*, part), ST(st)),
+          "h3p_colpart");
+  }, "column partials per 32-row panel of a blocked h3p operand: part[r / 32][c] (fp32 [rows / 32, cols])");
   m.def("h3p_split", [](i64 src, i64 lds, int rows, int cols, i64 dst, i64 ldd, i64 ps, i64 ex, i64 lde, i64 st,
                         int blocked) {
     pre_launch("h3p_split");
@@ -486,7 +492,7 @@ PYBIND11_MODULE(_hip, m) {
                              P(float*, dqkv), P(const uint32_t*, dmask), B, S, NH, 64, p, ST(st), nullptr,
                              P(void*, pl), ps, P(int8_t*, ex)),
           "attn_bwd_h3p");
-  }, "h3 attention backward also writing dqkv as h3p planes");
+  }, "h3 attention backward also writing dqkv as h3p planes (dqkv 0: only as the planes)");
   m.def("set_ln_h3p_waves", &set_ln_h3p_waves, "h3p LayerNorm forward: waves per 32-row block (8 or 16)");
   m.def("ln_fwd_h3p", [](i64 a, i64 bias, i64 resid, i64 gamma, i64 beta, i64 y, i64 z, i64 mean, i64 rstd, int rows,
                          int H, float eps, float p, u64 seed, u64 off, int mode, int nslab, i64 slab_stride, int row0,

@@ -388,6 +388,34 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 }
 
 // ---------------------------------------------------------------- fp32 -> h3p planes
+// Column partials of a blocked h3p operand: part[r / 32][c] = sum over the 32 rows of panel r / 32 of the
+// value the planes hold, (hi + lo) 2^-e (exact in fp32: 22 bits), rows in order (deterministic).  The
+// QKV bias gradient of the fused layer comes from dqkv's planes this way: the attention backward then
+// writes dqkv only as planes (no fp32 copy: 38 MB of writes and reads less per BERT-base layer).
+__global__ void __launch_bounds__(128) h3p_colpart_kernel(const uint16_t* __restrict__ pl, int64_t ld, int64_t ps,
+                                                         const int8_t* __restrict__ ex, int64_t lde, int cols,
+                                                         float* __restrict__ part) {
+  const int panel = blockIdx.y, c = (blockIdx.x * 128 + threadIdx.x) * 2;
+  if (c >= cols) return;
+  const int cb = c >> 5;
+  const uint16_t* base = pl + (int64_t)panel * 32 * ld + (int64_t)cb * 1024 + (c & 31);
+  uint32_t hv[32], lv[32];
+#pragma unroll
+  for (int r = 0; r < 32; ++r) {
+    hv[r] = *reinterpret_cast<const uint32_t*>(base + r * 32);
+    lv[r] = *reinterpret_cast<const uint32_t*>(base + ps + r * 32);
+  }
+  float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+  for (int r = 0; r < 32; ++r) {
+    const h3p_h2 h = __builtin_bit_cast(h3p_h2, hv[r]), l = __builtin_bit_cast(h3p_h2, lv[r]);
+    s0 += static_cast<float>(h[0]) + static_cast<float>(l[0]);
+    s1 += static_cast<float>(h[1]) + static_cast<float>(l[1]);
+  }
+  const float sc = h3p_scale(-ex[(int64_t)panel * lde + cb]);
+  *reinterpret_cast<float2*>(part + (int64_t)panel * cols + c) = make_float2(s0 * sc, s1 * sc);
+}
+
 struct QSplitSeg {
   const float* src;
   uint16_t* dst;
@@ -493,6 +521,14 @@ int launch_gemm_h3p(int ta, int tb, int M, int N, int K, const void* A, int64_t 
 }
 
 // fp32 [rows][cols] (row stride lds) -> h3p planes (row stride ldd, plane stride ps) + exponents
+int launch_h3p_colpart(const void* pl, int64_t ld, int64_t ps, const int8_t* ex, int64_t lde, int rows, int cols,
+                       float* part, hipStream_t st) {
+  if (rows <= 0 || rows % 32 || cols <= 0 || cols % 32 || ld % 32 || ps % 2) return -1;
+  hipLaunchKernelGGL(h3p_colpart_kernel, dim3((cols + 255) / 256, rows / 32), dim3(128), 0, st,
+                     static_cast<const uint16_t*>(pl), ld, ps, ex, lde, cols, part);
+  return 0;
+}
+
 int launch_h3p_split(const float* src, int64_t lds, int rows, int cols, void* dst, int64_t ldd, int64_t ps, int8_t* ex,
                      int64_t lde, int blocked, hipStream_t st) {
   if (rows <= 0 || cols <= 0 || rows % 32 || cols % 32 || lds % 4 || ldd % 4 || ps % 4) return -1;

@@ -41,9 +41,9 @@ int launch_attn_bwd_h3(const float*, const int64_t*, const float*, const float*,
                        float*, const uint32_t*, int, int, int, int, float, hipStream_t, float*, void*, int64_t,
                        int8_t*);
 void launch_colpart_finalize(const float* const*, float* const*, int, int, int, int, hipStream_t);
-void launch_colsum(int, const void*, const void*, const float*, void*, float*, float*, int64_t, int, int, hipStream_t,
-                   float*);
-void hs_stream_wait(hipStream_t waiter, hipStream_t signal);  // bindings.cpp (event ring)
+int launch_h3p_colpart(const void*, int64_t, int64_t, const int8_t*, int64_t, int, int, float*, hipStream_t);
+void hs_stream_wait(hipStream_t waiter, hipStream_t signal);
+  // bindings.cpp (event ring)
 
 // An h3p operand in the plan: planes address, leading dimension, plane stride, exponents address,
 // exponent leading dimension, blocked layout (ops/h3p.py HP).
@@ -57,7 +57,7 @@ void hs_stream_wait(hipStream_t waiter, hipStream_t signal);  // bindings.cpp (e
   X(xp_ld) X(xp_ps) X(xp_lde) X(xp_blk)                                                                       \
   X(slab0) X(slab1) X(slab_floats)                                                                            \
   X(gwqkv) X(gbqkv) X(gwo) X(gbo) X(gg1) X(gb1) X(gw1) X(gbi) X(gw2) X(gb2) X(gg2) X(gbb2)                     \
-  X(dz2) X(dz1) X(dctx) X(dqkv) X(dbuf)                                                                       \
+  X(dz2) X(dz1) X(dctx) X(dbuf)                                                                              \
   HPF(X, da2p) HPF(X, df1p) HPF(X, da1p) HPF(X, dqkvp)                                                        \
   X(part2_g) X(part2_b) X(part2_bias) X(part1_g) X(part1_b) X(part1_bias) X(part_gelu) X(part_bq)
 
@@ -254,17 +254,23 @@ void layer_bwd_h3p(int64_t plan, int64_t dh2, int64_t xp, int64_t xe, int64_t ma
   float* dctx = ptr<float>(q[f_dctx]);
   gemm(0, 0, rows, H, H, da1p, Wo, dctx, H, nullptr, 0, 0.f, nullptr, 0, nullptr, nullptr, 0, nullptr, 1, nullptr, 0,
        st0, "attention-output data gradient");
-  float* dqkv = ptr<float>(q[f_dqkv]);
+  // dqkv only as planes (the QKV bias gradient from their column partials below)
   req(launch_attn_bwd_h3(ptr<const float>(q[f_qkv]), ptr<const int64_t>(mask), ptr<const float>(q[f_bqkv]),
-                         ptr<const float>(q[f_ctx]), dctx, ptr<const float>(q[f_lse]), ptr<float>(q[f_dbuf]), dqkv,
+                         ptr<const float>(q[f_ctx]), dctx, ptr<const float>(q[f_lse]), ptr<float>(q[f_dbuf]), nullptr,
                          q[f_dmask] ? ptr<const uint32_t>(q[f_dmask]) : nullptr, B, S, NH, 64, p_a, st0, nullptr,
                          ptr<void>(dqkvp.p), dqkvp.ps, ptr<int8_t>(dqkvp.e)),
       "attention backward");
   // QKV weight and bias gradients on the side stream; dx = dz1 + dqkv @ Wqkv
   hs_stream_wait(st1, st0);
   wgrad(dqkvp, X, 3 * H, H, q[f_gwqkv], (int)q[f_ksg_qkv], "QKV weight gradient");
-  launch_colsum(0, dqkv, nullptr, nullptr, nullptr, ptr<float>(q[f_part_bq]), ptr<float>(q[f_gbqkv]), rows, 3 * H, 1,
-                st1, nullptr);
+  {
+    const float* parts[1] = {ptr<const float>(q[f_part_bq])};
+    float* outs[1] = {ptr<float>(q[f_gbqkv])};
+    req(launch_h3p_colpart(ptr<const void>(dqkvp.p), dqkvp.ld, dqkvp.ps, ptr<const int8_t>(dqkvp.e), dqkvp.lde, rows,
+                           3 * H, ptr<float>(q[f_part_bq]), st1),
+        "QKV bias-gradient partials");
+    launch_colpart_finalize(parts, outs, 1, nb, 3 * H, 1, st1);
+  }
   ready(3);
   gemm(0, 0, rows, H, 3 * H, dqkvp, Wqkv, dz1, H, nullptr, 0, 1.f, nullptr, 0, nullptr, nullptr, 0, nullptr, 1,
        nullptr, 0, st0, "QKV data gradient");

@@ -283,17 +283,26 @@ def attn_fwd_h3p(qkv, mask, B, S, NH, p, seed, off, bias, outs, b0, hp):
     return ctx
 
 
-def attn_bwd_h3p(qkv, mask, ctx, dctx, lse, B, S, NH, p, bias, hp):
-    """attn_bwd on the h3 attention kernel that also writes dqkv as h3p planes into ``hp``."""
+def attn_bwd_h3p(qkv, mask, ctx, dctx, lse, B, S, NH, p, bias, hp, fp32=True):
+    """attn_bwd on the h3 attention kernel that also writes dqkv as h3p planes into ``hp``; with
+    ``fp32=False`` ONLY as the planes (returns None)."""
     assert hp.blk, "producers write blocked planes"
     lse, dmask = lse
-    dqkv = torch.empty_like(qkv)
+    dqkv = torch.empty_like(qkv) if fp32 else None
     dbuf = torch.empty_like(lse)
     hip().attn_bwd_h3p(qkv.data_ptr(), mask.data_ptr(), bias.data_ptr() if bias is not None else 0, ctx.data_ptr(),
-                       dctx.data_ptr(), lse.data_ptr(), dbuf.data_ptr(), dqkv.data_ptr(),
+                       dctx.data_ptr(), lse.data_ptr(), dbuf.data_ptr(), dqkv.data_ptr() if fp32 else 0,
                        dmask.data_ptr() if dmask is not None else 0, B, S, NH, float(p), hp.data_ptr(), hp.ps,
                        hp.exps_ptr(), stream_handle())
     return dqkv
+
+
+def h3p_colpart(hp, part):
+    """part[r / 32, c] = column sums of a blocked h3p operand over each 32-row panel (fp32 [rows / 32, cols])."""
+    assert hp.blk and part.is_contiguous() and tuple(part.shape) == (hp.rows // 32, hp.cols)
+    hip().h3p_colpart(hp.data_ptr(), hp.ld, hp.ps, hp.exps_ptr(), hp.lde, hp.rows, hp.cols, part.data_ptr(),
+                      stream_handle())
+    return part
 
 
 # --------------------------------------------------------------------- standalone autograd ops
@@ -826,13 +835,19 @@ def _layer_backward_h3p(ctx, dh2, x, saved, W, meta, cfg):
         wgrad(da1p, ctxp, Gv.wo, "wo_wgrad")
     dctx = h3p.gemm(da1p, Wp.wo, 0, 0, site="wo_dgrad")
     dqkvp = h3p.empty(rows, 3 * H, dev)
-    dqkv = attn_bwd_h3p(qkv, mask_of(ctx), ctx_, dctx, (lse, dmask), B, S, NH, p_a, W.bqkv, dqkvp)
+    attn_bwd_h3p(qkv, mask_of(ctx), ctx_, dctx, (lse, dmask), B, S, NH, p_a, W.bqkv, dqkvp, fp32=False)
+    part_bq = torch.empty(rows // 32, 3 * H, dtype=torch.float32, device=dev)
+
+    def fin_bq():  # the QKV bias gradient: column sums of dqkv's planes (no fp32 dqkv exists)
+        h3p_colpart(dqkvp, part_bq)
+        hip().colpart_finalize([part_bq.data_ptr()], [Gv.bqkv.data_ptr()], rows // 32, 3 * H, 1, stream_handle())
+
     with streams.coalesced():  # QKV weight and bias gradients
         wgrad(dqkvp, xp, Gv.wqkv, "qkv_wgrad")
         if side:
-            streams.run(dev, lambda: colsum(dqkv, acc=Gv.bqkv), dqkv)
+            streams.run(dev, fin_bq, part_bq, dqkvp.planes, dqkvp.exps)
         else:
-            colsum(dqkv, acc=Gv.bqkv)
+            fin_bq()
     h3p.gemm(dqkvp, Wp.wqkv, 0, 0, out=dz1, beta=1.0, site="qkv_dgrad")  # dx = dz1 + dqkv @ Wqkv
     if acc:
         return (dz1, None, None) + (None,) * 16

@@ -74,13 +74,13 @@ class LayerProgram(object):
         self.ctxp, self.h1p, self.h2p = (h3p.empty(rows, H, device) for _ in range(3))
         self.f1p = h3p.empty(rows, Fd, device)
         self.dz2, self.dz1, self.dctx = z(rows, H), z(rows, H), z(rows, H)
-        self.dqkv, self.dbuf = z(rows, 3 * H), z(B * NH * S)
+        self.dbuf = z(B * NH * S)  # (dqkv itself exists only as the planes dqkvp)
         self.da2p, self.da1p = h3p.empty(rows, H, device), h3p.empty(rows, H, device)
         self.df1p, self.dqkvp = h3p.empty(rows, Fd, device), h3p.empty(rows, 3 * H, device)
         nb = rows // 32
         self.part2, self.part1 = bert_ops._colpart_buf(nb, H, device), bert_ops._colpart_buf(nb, H, device)
         self.part_gelu = z(rows // 128, Fd)
-        self.part_bq = z(hip().colsum_row_chunks(rows), 3 * H)
+        self.part_bq = z(rows // 32, 3 * H)  # the QKV bias gradient's column partials (from dqkvp)  # the attention backward's bias-gradient column partials
         hr = rows // halves
         need = max(ks_wo * hr * H, ks_w2 * hr * H, ksg["w2"] * H * Fd, ksg["w1"] * Fd * H, ksg["wo"] * H * H,
                    ksg["qkv"] * 3 * H * H)
@@ -107,7 +107,7 @@ class LayerProgram(object):
             assert t.is_contiguous() and t.dtype == torch.float32
             put(k, t.data_ptr())
         for k in ("qkv", "ctx", "lse", "h1", "z1", "m1", "r1", "f1pre", "h2", "z2", "m2", "r2", "dz2", "dz1", "dctx",
-                  "dqkv", "dbuf"):
+                  "dbuf"):
             put(k, getattr(self, k).data_ptr())
         put("dmask", self.dmask.data_ptr() if self.dmask is not None else 0)
         for k in ("ctxp", "h1p", "f1p", "h2p", "da2p", "df1p", "da1p", "dqkvp"):

@@ -338,3 +338,11 @@ def test_attention_h3p_planes(cuda, S, p):
     assert torch.equal(dq, dq2)
     sq = h3p.split(dq)
     assert torch.equal(hq.planes, sq.planes) and torch.equal(hq.exps, sq.exps)
+    # planes only; the bias gradient's column partials from the planes
+    hq3 = h3p.empty(B * S, 3 * H, cuda)
+    assert O.attn_bwd_h3p(qkv, mask, ctx, dctx, (lse, dmask), B, S, NH, p, bias, hq3, fp32=False) is None
+    assert torch.equal(hq3.planes, hq.planes) and torch.equal(hq3.exps, hq.exps)
+    part = O.h3p_colpart(hq3, torch.full((B * S // 32, 3 * H), float("nan"), device=cuda))
+    ref = dq.double().view(B * S // 32, 32, 3 * H).sum(1)
+    err = (part.double() - ref).abs().max().item()
+    assert err <= 1e-5 * (1.0 + ref.abs().max().item()), err
