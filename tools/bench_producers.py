@@ -104,7 +104,9 @@ def main():
                         a.reps)
             t2 = timeit(lambda: h3p.split(bert_ops.attn_bwd(qkv, mask, ctx, dctx, (outs[1], outs[2]), B, S, NH, 0.1,
                                                             bias=bq), out=hq), a.reps)
-            rec("attn_bwd B=%d" % B, fp32=t0, fused_h3p=t1, then_split=t2)
+            tp = timeit(lambda: bert_ops.attn_bwd_h3p(qkv, mask, ctx, dctx, (outs[1], outs[2]), B, S, NH, 0.1, bq, hq,
+                                                      fp32=False), a.reps)
+            rec("attn_bwd B=%d" % B, fp32=t0, fused_h3p=t1, then_split=t2, planes_only=tp)
     if a.json:
         with open(a.json, "w") as f:
             for r in res:
