@@ -24,9 +24,10 @@ case "$cmd" in
   pmc)
     tag=${2:-cur}
     for D in ${1:-fp32 bf16}; do
-      (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_INSTS_VALU_MFMA_MOPS_BF16 GRBM_GUI_ACTIVE SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE \
+      (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F16 SQ_INSTS_VALU_MFMA_MOPS_BF16 GRBM_GUI_ACTIVE SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE \
         --kernel-trace --output-format csv -d "$R/gpurun_out/pmc_${tag}_$D" -o run -- python3 "$R/bench.py" --steps 3 --warmup 2 --dtype "$D" > "$R/gpurun_out/pmc_${tag}_$D.log" 2>&1) || { tail -20 "$R/gpurun_out/pmc_${tag}_$D.log"; exit 1; }
-      python3 tools/pmc_summary.py "gpurun_out/pmc_${tag}_$D/run_counter_collection.csv" "BERT-base $D step: per-kernel MFMA / LDS counters ($tag)" 25 > "gpurun_out/pmc_${tag}_$D.md" || exit 1
+      { echo "# BERT-base $D step: per-kernel MFMA / LDS counters ($tag; counters serialise the kernels)"; echo;
+        python3 tools/pmc_summary.py "gpurun_out/pmc_${tag}_$D/run_counter_collection.csv" --top 25; } > "gpurun_out/pmc_${tag}_$D.md" || exit 1
       head -14 "gpurun_out/pmc_${tag}_$D.md" | tail -8
     done ;;
   bench)

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-kernel summary of rocprofv3 counter databases (rocpd sqlite, ROCm 7.x).
+"""Per-kernel summary of rocprofv3 counter databases (rocpd sqlite, ROCm 7.x) or counter CSVs.
 
     python tools/pmc_summary.py gpurun_out/pmc_a/run_results.db [more.db ...] [--match gemm_h3p] [--top 20]
 
@@ -22,6 +22,16 @@ def short(name, n=70):
 
 
 def load(db):
+    if db.endswith(".csv"):  # rocprofv3 --output-format csv: run_counter_collection.csv
+        import csv
+
+        per = collections.defaultdict(lambda: collections.defaultdict(list))
+        durs = collections.defaultdict(dict)
+        for r in csv.DictReader(open(db)):
+            name, disp = r["Kernel_Name"], int(r["Dispatch_Id"])
+            per[name][r["Counter_Name"]].append((disp, float(r["Counter_Value"])))
+            durs[name][disp] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        return per, durs
     c = sqlite3.connect(db)
     per = collections.defaultdict(lambda: collections.defaultdict(list))
     durs = collections.defaultdict(dict)
