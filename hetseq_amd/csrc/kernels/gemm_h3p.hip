@@ -520,7 +520,6 @@ int launch_gemm_h3p(int ta, int tb, int M, int N, int K, const void* A, int64_t 
   return 0;
 }
 
-// fp32 [rows][cols] (row stride lds) -> h3p planes (row stride ldd, plane stride ps) + exponents
 int launch_h3p_colpart(const void* pl, int64_t ld, int64_t ps, const int8_t* ex, int64_t lde, int rows, int cols,
                        float* part, hipStream_t st) {
   if (rows <= 0 || rows % 32 || cols <= 0 || cols % 32 || ld % 32 || ps % 2) return -1;
@@ -529,6 +528,7 @@ int launch_h3p_colpart(const void* pl, int64_t ld, int64_t ps, const int8_t* ex,
   return 0;
 }
 
+// fp32 [rows][cols] (row stride lds) -> h3p planes (row stride ldd, plane stride ps) + exponents
 int launch_h3p_split(const float* src, int64_t lds, int rows, int cols, void* dst, int64_t ldd, int64_t ps, int8_t* ex,
                      int64_t lde, int blocked, hipStream_t st) {
   if (rows <= 0 || cols <= 0 || rows % 32 || cols % 32 || lds % 4 || ldd % 4 || ps % 4) return -1;
