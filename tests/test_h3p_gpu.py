@@ -346,3 +346,20 @@ def test_attention_h3p_planes(cuda, S, p):
     ref = dq.double().view(B * S // 32, 32, 3 * H).sum(1)
     err = (part.double() - ref).abs().max().item()
     assert err <= 1e-5 * (1.0 + ref.abs().max().item()), err
+
+
+@pytest.mark.parametrize("rows,cols", [(64, 96), (256, 2304)])
+def test_h3p_colpart_matches_planes(cuda, rows, cols):
+    """h3p_colpart: per-32-row-panel column sums of what a blocked operand's planes hold ((hi + lo) 2^-e,
+    exact in fp32), including column counts that leave a partial 256-column block."""
+    from hetseq_amd.ops import bert_ops as O
+    from hetseq_amd.ops import h3p
+
+    g = torch.Generator(device=cuda)
+    g.manual_seed(rows + cols)
+    x = torch.randn(rows, cols, device=cuda, generator=g) * torch.logspace(-3, 3, cols, device=cuda)
+    hp = h3p.split(x)
+    part = O.h3p_colpart(hp, torch.full((rows // 32, cols), float("nan"), device=cuda))
+    ref = x.double().view(rows // 32, 32, cols).sum(1)
+    err = ((part.double() - ref).abs() / (1.0 + x.double().abs().view(rows // 32, 32, cols).sum(1))).max().item()
+    assert err <= 1e-6, err
