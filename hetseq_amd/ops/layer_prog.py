@@ -80,7 +80,7 @@ class LayerProgram(object):
         nb = rows // 32
         self.part2, self.part1 = bert_ops._colpart_buf(nb, H, device), bert_ops._colpart_buf(nb, H, device)
         self.part_gelu = z(rows // 128, Fd)
-        self.part_bq = z(rows // 32, 3 * H)  # the QKV bias gradient's column partials (from dqkvp)  # the attention backward's bias-gradient column partials
+        self.part_bq = z(rows // 32, 3 * H)  # the QKV bias gradient's column partials (from dqkvp)
         hr = rows // halves
         need = max(ks_wo * hr * H, ks_w2 * hr * H, ksg["w2"] * H * Fd, ksg["w1"] * Fd * H, ksg["wo"] * H * H,
                    ksg["qkv"] * 3 * H * H)
