@@ -57,7 +57,7 @@ def parse():
     p.add_argument("--layers", type=int, default=12)
     p.add_argument("--bucket-cap-mb", type=int, default=25)
     p.add_argument("--no-fused", action="store_true")
-    p.add_argument("--gemm", default=None, choices=[None, "hip", "blas", "auto"])
+    p.add_argument("--gemm", default=None, choices=[None, "hip", "blas"])
     p.add_argument("--profile-phases", action="store_true")
     p.add_argument("--hip-graph", action="store_true", help="replay the captured update as one HIP graph (1 GPU, or data-parallel on the native RCCL engine)")
     p.add_argument("--sync-debug", action="store_true", help="warn (with stack) on every host<->device sync in the timed loop")
@@ -309,6 +309,7 @@ def run_rank(b):
     if b.gemm_choices and os.path.exists(b.gemm_choices):
         G.load_choices(b.gemm_choices)
     ctl.optimizer  # build optimizer/scheduler (and the DP engine) before timing
+    comm_id = _comm_identity(ctl, world, rank)
     emul = None
     if b.emulate_world and b.emulate_world > 1:
         comm = getattr(ctl.model, "comm", None)
@@ -428,6 +429,8 @@ def run_rank(b):
             "gemm_choices": {str(k): v for k, v in list(G.GEMM_CHOICES.items())[:32]},
             "fp32_gemm": G.fp32_mode(),
             "device_map": device_map,
+            "rccl_ranks": comm_id[0].get("rccl_count", 1 if world == 1 else None),
+            "comm_identity": comm_id,
             "comm_emulated": emul["world"] if emul else None,
             "emulation": emul,
         }
@@ -608,6 +611,11 @@ _AB = {
     # waves per 32-row block of the h3p LayerNorm forward
     "lnw8": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_ln_h3p_waves(8),
     "lnw16": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_ln_h3p_waves(16),
+    "lnw0": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_ln_h3p_waves(0),
+    "lnw1": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_ln_h3p_waves(1),
+    "lnbc_on": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_ln_bwd_coop(1),
+    "lnbc_off": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_ln_bwd_coop(0),
+    "lnbc_4": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_ln_bwd_coop(2),
     "eng_h3": lambda: __import__("hetseq_amd.ops.gemm", fromlist=["x"]).set_fp32_mode("h3"),
     # --emulate-world: workgroups per emulated collective (RCCL channels) and the emulated bus bandwidth
     "emu_ch4": lambda: _set_emul_channels(4),
@@ -619,6 +627,37 @@ _AB = {
     "emu_bw400": lambda: _set_emul_busbw(400.0),
     "emu_bw600": lambda: _set_emul_busbw(600.0),
 }
+
+
+def _comm_identity(ctl, world, rank):
+    """Per rank, before timing: the PCI bus id of the device it runs on and -- on the native engine --
+    what RCCL itself reports for the communicator (ncclCommCount / ncclCommUserRank / its device) and
+    the bus bandwidth of a 64 MB all-reduce.  Rank 0 checks that the job is N ranks on N DISTINCT
+    devices and that RCCL saw N ranks 0..N-1 (a misconfigured launch fails here, not in the result)."""
+    import torch
+    import torch.distributed as dist
+
+    from hetseq_amd.ops._C import hip
+
+    dev = torch.cuda.current_device()
+    me = {"rank": rank, "hip_device": dev, "pci_bus_id": hip().pci_bus_id(dev)}
+    comm = getattr(ctl.model, "comm", None)
+    if comm is not None:
+        me.update(comm.identity())
+        me["allreduce_64mb_busbw_gbs"] = comm.busbw(64 << 20)
+    ids = [me]
+    if world > 1:
+        ids = [None] * world
+        dist.all_gather_object(ids, me)
+        buses = {i["pci_bus_id"] for i in ids}
+        # (gloo runs may share a device on purpose: the one-GPU multi-rank tests; RCCL never does)
+        if rank == 0 and len(buses) != world and dist.get_backend() == "nccl":
+            raise RuntimeError("bench.py: %d ranks on %d distinct devices: %s" % (world, len(buses), ids))
+        if rank == 0:
+            if comm is not None and (any(i.get("rccl_count") != world for i in ids)
+                                     or sorted(i.get("rccl_rank") for i in ids) != list(range(world))):
+                raise RuntimeError("bench.py: RCCL does not see %d ranks 0..%d: %s" % (world, world - 1, ids))
+    return ids
 
 
 def _host_phases(ctl):

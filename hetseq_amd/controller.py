@@ -173,9 +173,13 @@ class Controller(object):
 
     def _shard_ok(self):
         """Sharded optimizer (parallel/zero.py): data-parallel Adam runs (the flat-store update with a
-        range form), eager steps, no BMUF; --shard-optimizer off disables it."""
-        return (getattr(self.args, "shard_optimizer", "auto") == "auto" and getattr(self.args, "optimizer", "adam") == "adam"
-                and not getattr(self.args, "hip_graph", False) and not self.args.use_bmuf)
+        range form), eager steps, no BMUF.  "auto" (default): the data-parallel engine shards on the
+        native RCCL engine once its self-test passed (parallel/comm.py shard_self_test); "on" shards on
+        any engine; "off" never."""
+        mode = getattr(self.args, "shard_optimizer", "auto")
+        ok = (mode != "off" and getattr(self.args, "optimizer", "adam") == "adam"
+              and not getattr(self.args, "hip_graph", False) and not self.args.use_bmuf)
+        return ("auto" if mode == "auto" else True) if ok else False
 
     def _staged_ok(self):
         """Staged (overlapped) update: eager steps (a HIP graph replays the whole update) of a model

@@ -121,6 +121,25 @@ class Comm {
 
   ~Comm() { close(false); }
 
+  // What RCCL itself reports for this communicator (ncclCommCount / ncclCommUserRank /
+  // ncclCommCuDevice) and the PCI bus id of the HIP device it runs on: bench.py records these per
+  // rank, so a multi-GPU result carries proof of N ranks on N distinct devices.
+  py::dict identity() {
+    if (!comm_) throw std::logic_error("hetseq comm: identity before init");
+    int count = 0, user_rank = -1, dev = -1;
+    nccl_check(ncclCommCount(comm_, &count), "ncclCommCount");
+    nccl_check(ncclCommUserRank(comm_, &user_rank), "ncclCommUserRank");
+    nccl_check(ncclCommCuDevice(comm_, &dev), "ncclCommCuDevice");
+    char bus[64] = {0};
+    hip_check(hipDeviceGetPCIBusId(bus, sizeof(bus), dev), "hipDeviceGetPCIBusId");
+    py::dict d;
+    d["rccl_count"] = count;
+    d["rccl_rank"] = user_rank;
+    d["rccl_device"] = dev;
+    d["pci_bus_id"] = std::string(bus);
+    return d;
+  }
+
   // graceful: destroy the communicator when every operation has completed (all ranks close at
   // the same point); otherwise -- operations still outstanding (a peer died) or process exit --
   // abort it, which never waits for peers.
@@ -549,6 +568,7 @@ PYBIND11_MODULE(_comm, m) {
       .def("all_gather", &Comm::all_gather, py::arg("send"), py::arg("recv"), py::arg("count"), py::arg("dtype"),
            py::arg("stream"))
       .def("check", &Comm::check)
+      .def("identity", &Comm::identity, "RCCL's own count / rank / device and the device's PCI bus id")
       .def("watch_stream", &Comm::watch_stream, py::arg("stream"))
       .def("close", &Comm::close, py::arg("graceful") = true)
       .def("inject_stall", &Comm::inject_stall)

@@ -50,9 +50,11 @@ int launch_emb_bwd(int, const void*, const float*, const float*, const float*, c
 void set_ln_h3p_waves(int w);
 int launch_ln_fwd_h3p(const void*, const float*, const void*, const float*, const float*, void*, float*, float*, float*,
                       int, int, float, float, u64, u64, int, int, int64_t, int, float*, void*, int64_t, int8_t*,
-                      hipStream_t);
+                      uint32_t*, int, hipStream_t);
 int launch_ln_bwd_h3p(const float*, const float*, const float*, const float*, const float*, float*, float*, float*,
-                      float*, int, int, float, u64, u64, void*, int64_t, int8_t*, hipStream_t);
+                      float*, int, int, float, u64, u64, void*, int64_t, int8_t*, uint32_t*, hipStream_t);
+int ln_bwd_h3p_part_rows(int coop);
+void set_ln_bwd_coop(int on);
 int launch_attn_fwd_h3(const float*, const int64_t*, const float*, float*, float*, uint32_t*, int, int, int, int, float,
                        uint64_t, uint64_t, hipStream_t, int, float*, void*, int64_t, int8_t*);
 int launch_attn_bwd_h3(const float*, const int64_t*, const float*, const float*, const float*, const float*, float*,
@@ -112,13 +114,19 @@ int launch_gemm_planes(int planes, int c_dtype, int ta, int tb, int M, int N, in
 void set_planes_variant(int v);
 
 // gemm_h3p.hip
+int launch_gemm_h3p_v(int ta, int tb, int M, int N, int K, const void* A, int64_t lda, int64_t a_ps, const int8_t* ea,
+                      int64_t lde_a, const void* B, int64_t ldb, int64_t b_ps, const int8_t* eb, int64_t lde_b,
+                      float* C, int64_t ldc, const float* bias, int epi, float beta, float* aux, int64_t ldaux,
+                      float* part, float* colsum, int colsum_acc, void* cp, int64_t ldcp, int64_t cp_ps, int8_t* ec,
+                      int64_t lde_c, int ksplit, float* slab, int64_t slab_floats, int ablk, int bblk, int Mv, int Nv,
+                      hipStream_t st);
 int launch_gemm_h3p(int ta, int tb, int M, int N, int K, const void* A, int64_t lda, int64_t a_ps, const int8_t* ea,
                     int64_t lde_a, const void* B, int64_t ldb, int64_t b_ps, const int8_t* eb, int64_t lde_b, float* C,
                     int64_t ldc, const float* bias, int epi, float beta, float* aux, int64_t ldaux, float* part,
                     float* colsum, int colsum_acc, void* cp, int64_t ldcp, int64_t cp_ps, int8_t* ec, int64_t lde_c,
                     int ksplit, float* slab, int64_t slab_floats, int ablk, int bblk, hipStream_t st);
 int launch_h3p_split(const float* src, int64_t lds, int rows, int cols, void* dst, int64_t ldd, int64_t ps, int8_t* ex,
-                     int64_t lde, int blocked, hipStream_t st);
+                     int64_t lde, int blocked, int vrows, hipStream_t st);
 int h3p_split_seg_bytes();
 int launch_h3p_colpart(const void*, int64_t, int64_t, const int8_t*, int64_t, int, int, float*, hipStream_t);
 void launch_h3p_split_multi(const void* table, int nseg, int total, hipStream_t st);
@@ -204,6 +212,11 @@ void layer_bwd_h3p(int64_t, int64_t, int64_t, int64_t, int64_t, uint64_t, uint64
 PYBIND11_MODULE(_hip, m) {
   m.doc() = "hetseq_amd CDNA4 (gfx950) kernels";
   m.attr("arch") = "gfx950";
+  m.def("pci_bus_id", [](int dev) {
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof(bus), dev) != hipSuccess) throw std::runtime_error("hipDeviceGetPCIBusId");
+    return std::string(bus);
+  }, "PCI bus id of HIP device `dev` (bench.py: one rank per distinct device)");
 
   m.def("layer_plan_fields", &layer_plan_fields, "field names of a layer program's int64 plan (layer_prog.cpp)");
   m.def("layer_fwd_h3p", [](i64 plan, i64 x, i64 xp, i64 xe, i64 mask, u64 sa, u64 oa, u64 s1, u64 o1, u64 s2, u64 o2,
@@ -446,13 +459,13 @@ PYBIND11_MODULE(_hip, m) {
   m.def("gemm_h3p", [](int ta, int tb, int M, int N, int K, i64 A, i64 lda, i64 a_ps, i64 ea, i64 lde_a, i64 B,
                        i64 ldb, i64 b_ps, i64 eb, i64 lde_b, i64 C, i64 ldc, i64 bias, int epi, float beta, i64 aux,
                        i64 ldaux, i64 part, i64 colsum, int colsum_acc, i64 cp, i64 ldcp, i64 cp_ps, i64 ec, i64 lde_c,
-                       int ksplit, i64 slab, i64 slab_floats, i64 st, int ablk, int bblk) {
+                       int ksplit, i64 slab, i64 slab_floats, i64 st, int ablk, int bblk, int mv, int nv) {
     pre_launch("gemm_h3p");
-    const int rc = launch_gemm_h3p(ta, tb, M, N, K, P(const void*, A), lda, a_ps, P(const int8_t*, ea), lde_a,
-                                   P(const void*, B), ldb, b_ps, P(const int8_t*, eb), lde_b, P(float*, C), ldc,
-                                   P(const float*, bias), epi, beta, P(float*, aux), ldaux, P(float*, part),
-                                   P(float*, colsum), colsum_acc, P(void*, cp), ldcp, cp_ps, P(int8_t*, ec), lde_c,
-                                   ksplit, P(float*, slab), slab_floats, ablk, bblk, ST(st));
+    const int rc = launch_gemm_h3p_v(ta, tb, M, N, K, P(const void*, A), lda, a_ps, P(const int8_t*, ea), lde_a,
+                                     P(const void*, B), ldb, b_ps, P(const int8_t*, eb), lde_b, P(float*, C), ldc,
+                                     P(const float*, bias), epi, beta, P(float*, aux), ldaux, P(float*, part),
+                                     P(float*, colsum), colsum_acc, P(void*, cp), ldcp, cp_ps, P(int8_t*, ec), lde_c,
+                                     ksplit, P(float*, slab), slab_floats, ablk, bblk, mv, nv, ST(st));
     if (rc == 0) check_launch("gemm_h3p");
     return rc;
   }, "fp32 GEMM as three fp16 products over block-scaled h3p planes (gemm_h3p.hip); -1 = not served",
@@ -461,20 +474,20 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("lde_b"), py::arg("C"), py::arg("ldc"), py::arg("bias"), py::arg("epi"), py::arg("beta"), py::arg("aux"),
      py::arg("ldaux"), py::arg("part"), py::arg("colsum"), py::arg("colsum_acc"), py::arg("cp"), py::arg("ldcp"),
      py::arg("cp_ps"), py::arg("ec"), py::arg("lde_c"), py::arg("ksplit"), py::arg("slab"), py::arg("slab_floats"),
-     py::arg("st"), py::arg("ablk") = 0, py::arg("bblk") = 0);
+     py::arg("st"), py::arg("ablk") = 0, py::arg("bblk") = 0, py::arg("mv") = 0, py::arg("nv") = 0);
   m.def("h3p_colpart", [](i64 pl, i64 ld, i64 ps, i64 ex, i64 lde, int rows, int cols, i64 part, i64 st) {
     pre_launch("h3p_colpart");
     check(launch_h3p_colpart(P(const void*, pl), ld, ps, P(const int8_t*, ex), lde, rows, cols, P(float*, part), ST(st)),
           "h3p_colpart");
   }, "column partials per 32-row panel of a blocked h3p operand: part[r / 32][c] (fp32 [rows / 32, cols])");
   m.def("h3p_split", [](i64 src, i64 lds, int rows, int cols, i64 dst, i64 ldd, i64 ps, i64 ex, i64 lde, i64 st,
-                        int blocked) {
+                        int blocked, int vrows) {
     pre_launch("h3p_split");
     check(launch_h3p_split(P(const float*, src), lds, rows, cols, P(void*, dst), ldd, ps, P(int8_t*, ex), lde, blocked,
-                           ST(st)),
+                           vrows, ST(st)),
           "h3p_split");
   }, py::arg("src"), py::arg("lds"), py::arg("rows"), py::arg("cols"), py::arg("dst"), py::arg("ldd"), py::arg("ps"),
-     py::arg("ex"), py::arg("lde"), py::arg("st"), py::arg("blocked") = 0);
+     py::arg("ex"), py::arg("lde"), py::arg("st"), py::arg("blocked") = 0, py::arg("vrows") = 0);
   m.def("h3p_split_seg_bytes", &h3p_split_seg_bytes);
   m.def("attn_fwd_h3p", [](i64 qkv, i64 mask, i64 bqkv, i64 ctx, i64 lse, i64 dmask, int B, int S, int NH, float p,
                            u64 seed, u64 off, int bh0, i64 pl, i64 ps, i64 ex, i64 st) {
@@ -493,23 +506,27 @@ PYBIND11_MODULE(_hip, m) {
                              P(void*, pl), ps, P(int8_t*, ex)),
           "attn_bwd_h3p");
   }, "h3 attention backward also writing dqkv as h3p planes (dqkv 0: only as the planes)");
-  m.def("set_ln_h3p_waves", &set_ln_h3p_waves, "h3p LayerNorm forward: waves per 32-row block (8 or 16)");
+  m.def("set_ln_h3p_waves", &set_ln_h3p_waves,
+        "h3p LayerNorm forward kernel: 0 / 1 panel exchange at 8 / 4 rows per workgroup, 16 / 8 one 32-row block");
+  m.def("ln_bwd_h3p_part_rows", &ln_bwd_h3p_part_rows, "rows per column-partial row of ln_bwd_h3p (coop: psync given)");
+  m.def("set_ln_bwd_coop", &set_ln_bwd_coop, "h3p LayerNorm backward: 1 / 2 panel exchange (8 / 4 rows per workgroup), 0 32-row blocks");
+  m.def("panel_sync_words", []() { return 256; }, "uint32 words of one 32-row panel record (h3p.h kPanelSyncWords)");
   m.def("ln_fwd_h3p", [](i64 a, i64 bias, i64 resid, i64 gamma, i64 beta, i64 y, i64 z, i64 mean, i64 rstd, int rows,
                          int H, float eps, float p, u64 seed, u64 off, int mode, int nslab, i64 slab_stride, int row0,
-                         i64 amax, i64 planes, i64 ps, i64 exps, i64 st) {
+                         i64 amax, i64 planes, i64 ps, i64 exps, i64 psync, int panel0, i64 st) {
     pre_launch("ln_fwd_h3p");
     check(launch_ln_fwd_h3p(P(const void*, a), P(const float*, bias), P(const void*, resid), P(const float*, gamma),
                             P(const float*, beta), P(void*, y), P(float*, z), P(float*, mean), P(float*, rstd), rows, H,
                             eps, p, seed, off, mode, nslab, slab_stride, row0, P(float*, amax), P(void*, planes), ps,
-                            P(int8_t*, exps), ST(st)),
+                            P(int8_t*, exps), P(uint32_t*, psync), panel0, ST(st)),
           "ln_fwd_h3p");
   });
   m.def("ln_bwd_h3p", [](i64 dy, i64 z, i64 mean, i64 rstd, i64 gamma, i64 dz, i64 pg, i64 pb, i64 pbias, int rows,
-                         int H, float p, u64 seed, u64 off, i64 planes, i64 ps, i64 exps, i64 st) {
+                         int H, float p, u64 seed, u64 off, i64 planes, i64 ps, i64 exps, i64 psync, i64 st) {
     pre_launch("ln_bwd_h3p");
     check(launch_ln_bwd_h3p(P(const float*, dy), P(const float*, z), P(const float*, mean), P(const float*, rstd),
                             P(const float*, gamma), P(float*, dz), P(float*, pg), P(float*, pb), P(float*, pbias), rows,
-                            H, p, seed, off, P(void*, planes), ps, P(int8_t*, exps), ST(st)),
+                            H, p, seed, off, P(void*, planes), ps, P(int8_t*, exps), P(uint32_t*, psync), ST(st)),
           "ln_bwd_h3p");
   });
   m.def("h3p_split_multi", [](i64 table, int nseg, int total, i64 st) {

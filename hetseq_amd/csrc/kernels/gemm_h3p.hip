@@ -81,6 +81,10 @@ struct QArgs {
   int M, N, K, ksplit;
   float beta;
   int ablk, bblk;  // operand plane layout: 0 row-major, 1 blocked (h3p.h: 32 x 32 blocks of 2 KB per plane)
+  // valid extents of a padded problem (the tied decoder's vocabulary padded to 512): C rows from Mv on
+  // are not written (they are the NEXT tensor of the flat gradient store), bias entries from Nv on
+  // read as zero (the padded columns of C stay exactly the zero the padded operand rows give)
+  int Mv, Nv;
 };
 
 HS_DEVICE qf16 q_mma(qh8 a, qh8 b, qf16 c) { return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0); }
@@ -104,10 +108,26 @@ HS_DEVICE void q_epilogue(const QArgs& p, qf16 (&acc)[2][2], char* smem, int m0,
     return;
   }
   float csum[2] = {0.f, 0.f};
+  if (EPI <= kQBias && m0 + 128 > p.Mv) {  // a tile reaching past the valid rows (padded problems only)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + wn + 32 * j + lr;
+      const float bv = EPI != kQNone && n < p.Nv ? p.bias[n] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int64_t m = m0 + wm + 32 * i + q_row(r, q);
+          if (m < p.Mv)
+            p.C[m * p.ldc + n] = acc[i][j][r] + bv + (p.beta != 0.f ? p.beta * p.C[m * p.ldc + n] : 0.f);
+        }
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int n = n0 + wn + 32 * j + lr;
-    const float bv = EPI != kQNone ? p.bias[n] : 0.f;
+    const float bv = EPI != kQNone && n < p.Nv ? p.bias[n] : 0.f;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int mb = m0 + wm + 32 * i;
@@ -423,6 +443,8 @@ struct QSplitSeg {
   int64_t lds, ldd, ps, lde;
   int rows, cols, blk0;  // blk0: index of the segment's first 32 x 32 block in the launch
   int blocked;           // destination layout (h3p_index)
+  int vrows;             // source rows that exist (rows past them split as zeros: a padded vocabulary)
+  int pad_;
 };
 
 // one wave per 32 x 32 block: lane l loads row (l >> 3) + 8 q, columns 4 (l & 7) .. +3 (q = 0..3),
@@ -445,7 +467,12 @@ __global__ void __launch_bounds__(256) h3p_split_kernel(QSplitSeg one, const QSp
   uint32_t m = 0u;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    load4(s.src + (int64_t)(r0 + 8 * k) * s.lds + c, v[k]);
+    if (r0 + 8 * k < s.vrows) {
+      load4(s.src + (int64_t)(r0 + 8 * k) * s.lds + c, v[k]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[k][e] = 0.f;
+    }
 #pragma unroll
     for (int e = 0; e < 4; ++e) m = amax_bits(m, v[k][e]);
   }
@@ -483,12 +510,18 @@ void launch_splitk_reduce(const float* slab, int ksplit, int M, int N, float* C,
 // Returns -1 (nothing launched) for a request the kernel does not serve.  Strides and plane strides
 // in elements; lde_*: row stride of the exponent arrays.  C == nullptr with ksplit > 1: the partial
 // slabs are left for the consumer (no reduce pass).  cp / ec (GELU, dGELU): the result's planes.
-int launch_gemm_h3p(int ta, int tb, int M, int N, int K, const void* A, int64_t lda, int64_t a_ps, const int8_t* ea,
-                    int64_t lde_a, const void* B, int64_t ldb, int64_t b_ps, const int8_t* eb, int64_t lde_b, float* C,
-                    int64_t ldc, const float* bias, int epi, float beta, float* aux, int64_t ldaux, float* part,
-                    float* colsum, int colsum_acc, void* cp, int64_t ldcp, int64_t cp_ps, int8_t* ec, int64_t lde_c,
-                    int ksplit, float* slab, int64_t slab_floats, int ablk, int bblk, hipStream_t st) {
+// Mv / Nv (0: M / N): valid extents of a padded problem -- C rows from Mv on are left untouched,
+// bias entries from Nv on read as zero (plain and bias epilogues).
+int launch_gemm_h3p_v(int ta, int tb, int M, int N, int K, const void* A, int64_t lda, int64_t a_ps, const int8_t* ea,
+                      int64_t lde_a, const void* B, int64_t ldb, int64_t b_ps, const int8_t* eb, int64_t lde_b,
+                      float* C, int64_t ldc, const float* bias, int epi, float beta, float* aux, int64_t ldaux,
+                      float* part, float* colsum, int colsum_acc, void* cp, int64_t ldcp, int64_t cp_ps, int8_t* ec,
+                      int64_t lde_c, int ksplit, float* slab, int64_t slab_floats, int ablk, int bblk, int Mv, int Nv,
+                      hipStream_t st) {
   ksplit = std::max(1, ksplit);
+  Mv = Mv > 0 ? Mv : M;
+  Nv = Nv > 0 ? Nv : N;
+  if (Mv > M || Nv > N || (Mv < M && (epi > 1 || !C))) return -1;  // (valid rows: plain / bias products into C)
   if ((ablk && lda % 32) || (bblk && ldb % 32)) return -1;
   if (M <= 0 || N <= 0 || K <= 0 || M % QT || N % QT || K % (QBK * ksplit) || K / ksplit / QBK > QMAXKT) return -1;
   if (ta && tb) return -1;
@@ -506,18 +539,28 @@ int launch_gemm_h3p(int ta, int tb, int M, int N, int K, const void* A, int64_t 
   if (spanA >= (1ll << 32) || spanB >= (1ll << 32)) return -1;
   QArgs a{static_cast<const uint16_t*>(A), ea, static_cast<const uint16_t*>(B), eb, lda, a_ps, lde_a, ldb, b_ps,
           lde_b, C, ldc, bias, aux, ldaux, part, static_cast<uint16_t*>(cp), ec, ldcp, cp_ps, lde_c, slab, M, N, K,
-          ksplit, beta, ablk, bblk};
+          ksplit, beta, ablk, bblk, Mv, Nv};
   const int rc = !ta && tb ? q_launch_epi<false, true>(ksplit > 1 ? 0 : epi, a, st)
                  : !ta   ? q_launch_epi<false, false>(ksplit > 1 ? 0 : epi, a, st)
                          : q_launch_epi<true, false>(ksplit > 1 ? 0 : epi, a, st);
   if (rc) return rc;
-  if (ksplit > 1 && C) launch_splitk_reduce(slab, ksplit, M, N, C, ldc, epi == 1 ? bias : nullptr, beta, M, N, st);
+  if (ksplit > 1 && C) launch_splitk_reduce(slab, ksplit, M, N, C, ldc, epi == 1 ? bias : nullptr, beta, Mv, Nv, st);
   if (epi == kQDGelu && part && colsum) {
     const float* parts[1] = {part};
     float* outs[1] = {colsum};
     launch_reduce_rows(parts, outs, 1, M / QT, N, colsum_acc, st);
   }
   return 0;
+}
+
+int launch_gemm_h3p(int ta, int tb, int M, int N, int K, const void* A, int64_t lda, int64_t a_ps, const int8_t* ea,
+                    int64_t lde_a, const void* B, int64_t ldb, int64_t b_ps, const int8_t* eb, int64_t lde_b, float* C,
+                    int64_t ldc, const float* bias, int epi, float beta, float* aux, int64_t ldaux, float* part,
+                    float* colsum, int colsum_acc, void* cp, int64_t ldcp, int64_t cp_ps, int8_t* ec, int64_t lde_c,
+                    int ksplit, float* slab, int64_t slab_floats, int ablk, int bblk, hipStream_t st) {
+  return launch_gemm_h3p_v(ta, tb, M, N, K, A, lda, a_ps, ea, lde_a, B, ldb, b_ps, eb, lde_b, C, ldc, bias, epi, beta,
+                           aux, ldaux, part, colsum, colsum_acc, cp, ldcp, cp_ps, ec, lde_c, ksplit, slab, slab_floats,
+                           ablk, bblk, 0, 0, st);
 }
 
 int launch_h3p_colpart(const void* pl, int64_t ld, int64_t ps, const int8_t* ex, int64_t lde, int rows, int cols,
@@ -528,13 +571,15 @@ int launch_h3p_colpart(const void* pl, int64_t ld, int64_t ps, const int8_t* ex,
   return 0;
 }
 
-// fp32 [rows][cols] (row stride lds) -> h3p planes (row stride ldd, plane stride ps) + exponents
+// fp32 [rows][cols] (row stride lds) -> h3p planes (row stride ldd, plane stride ps) + exponents; source
+// rows from vrows on (0: rows) are not read and split as zeros
 int launch_h3p_split(const float* src, int64_t lds, int rows, int cols, void* dst, int64_t ldd, int64_t ps, int8_t* ex,
-                     int64_t lde, int blocked, hipStream_t st) {
-  if (rows <= 0 || cols <= 0 || rows % 32 || cols % 32 || lds % 4 || ldd % 4 || ps % 4) return -1;
+                     int64_t lde, int blocked, int vrows, hipStream_t st) {
+  vrows = vrows > 0 ? vrows : rows;
+  if (rows <= 0 || cols <= 0 || rows % 32 || cols % 32 || lds % 4 || ldd % 4 || ps % 4 || vrows > rows) return -1;
   if (blocked && ldd % 32) return -1;
   if ((reinterpret_cast<uintptr_t>(src) & 15) || (reinterpret_cast<uintptr_t>(dst) & 7)) return -1;
-  QSplitSeg s{src, static_cast<uint16_t*>(dst), ex, lds, ldd, ps, lde, rows, cols, 0, blocked};
+  QSplitSeg s{src, static_cast<uint16_t*>(dst), ex, lds, ldd, ps, lde, rows, cols, 0, blocked, vrows, 0};
   const int total = (rows / 32) * (cols / 32);
   hipLaunchKernelGGL(h3p_split_kernel, dim3((total + 3) / 4), dim3(256), 0, st, s, nullptr, 1, total);
   return 0;

@@ -62,4 +62,71 @@ HS_DEVICE int64_t h3p_index(int64_t r, int64_t c, int64_t ld, int blocked) {
   return blocked ? (r >> 5) * 32 * ld + (c >> 5) * 1024 + (r & 31) * 32 + (c & 31) : r * ld + c;
 }
 
+// ---------------------------------------------------------------- panel exchange
+// Block exponents from producers whose workgroups hold fewer than the 32 rows of an exponent block:
+// the np workgroups of one 32-row PANEL combine their per-32-column-group |max| through a record of
+// kPanelSyncWords uint32 in device memory (zero-initialised once by the owner, ops/bert_ops.py
+// panel_sync), and every workgroup then splits its own rows, still in registers, with the panel's
+// exponents.  A 32-row workgroup puts a 2048-row call on 64 of the 256 CUs (round-5 LayerNorm
+// forward: 40 us in the step for ~25 MB); 8-row workgroups spread it over all of them.
+//   word 0: generation (one increment per completed exchange), word 16: arrival count,
+//   words 64 + 64 (g & 1) ..: the |max| buffer of generation g (<= 64 groups: H <= 2048).
+// Every access is an agent-scope atomic, so no XCD's L2 or CU's L1 can hold a stale copy.  Protocol:
+// a workgroup reads g before it arrives (g cannot move before the last of the np arrivals), maxes its
+// values into buffer g & 1, waits for those atomics to return, then adds 1 to the count.  The last
+// arriver clears the count and the OTHER parity's buffer (the next call's; the previous call that
+// used it has ended: same stream), then increments the generation; the others poll the generation.
+// All then read buffer g & 1 (every max into it was performed before its writer's arrival).  Calls
+// that may run concurrently (the forward's two half-batch streams) use disjoint panels; the np
+// workgroups of a panel need not be co-resident at launch (a polling workgroup holds a slot only
+// until the rest of its panel, which nothing else waits on, is dispatched), and the poll is bounded
+// (word 32 records a timeout).
+constexpr int kPanelSyncWords = 256;
+
+HS_DEVICE uint32_t psync_gen(uint32_t* rec) {
+  return __hip_atomic_fetch_add(rec, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// psync_arrive: called by ALL 64 lanes of ONE wave of the workgroup; lane c < ng holds the
+// workgroup's |max| bits of column group c in `m`, g = psync_gen() read before this workgroup
+// arrived.  Returns true in the last arriver (which has already published the generation).
+// psync_wait: the same wave, later (work independent of the exponents may run in between);
+// returns the panel's |max| of group c in lane c.
+HS_DEVICE bool psync_arrive(uint32_t* rec, uint32_t g, uint32_t m, int ng, int np) {
+  const int lane = threadIdx.x & 63;
+  uint32_t* cur = rec + 64 + 64 * (g & 1u);
+  if (lane < ng) (void)__hip_atomic_fetch_max(cur + lane, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the maxima are performed before the arrival
+  uint32_t arrived = 0u;
+  if (lane == 0) arrived = __hip_atomic_fetch_add(rec + 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const bool last = __shfl(static_cast<int>(arrived), 0, 64) == np - 1;
+  if (last) {  // every arrival (and so every max) is in: reset for the next call, then publish
+    uint32_t* nxt = rec + 64 + 64 * ((g + 1u) & 1u);
+    if (lane == 0) (void)__hip_atomic_exchange(rec + 16, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane < ng) (void)__hip_atomic_exchange(nxt + lane, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) (void)__hip_atomic_fetch_add(rec, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  return last;
+}
+
+HS_DEVICE uint32_t psync_wait(uint32_t* rec, uint32_t g, bool last, int ng) {
+  const int lane = threadIdx.x & 63;
+  if (!last && lane == 0) {
+    int spins = 0;
+    while (psync_gen(rec) == g) {
+      if (++spins > (1 << 22)) {
+        (void)__hip_atomic_exchange(rec + 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  asm volatile("" ::: "memory");  // the reads below stay behind the poll
+  uint32_t r = 0u;
+  if (lane < ng)
+    r = __hip_atomic_fetch_or(rec + 64 + 64 * (g & 1u) + lane, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return r;
+}
+
 }  // namespace hs

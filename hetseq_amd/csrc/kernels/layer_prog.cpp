@@ -32,9 +32,10 @@ int launch_gemm_h3p(int ta, int tb, int M, int N, int K, const void* A, int64_t 
                     int ksplit, float* slab, int64_t slab_floats, int ablk, int bblk, hipStream_t st);
 int launch_ln_fwd_h3p(const void*, const float*, const void*, const float*, const float*, void*, float*, float*, float*,
                       int, int, float, float, uint64_t, uint64_t, int, int, int64_t, int, float*, void*, int64_t, int8_t*,
-                      hipStream_t);
+                      uint32_t*, int, hipStream_t);
 int launch_ln_bwd_h3p(const float*, const float*, const float*, const float*, const float*, float*, float*, float*,
-                      float*, int, int, float, uint64_t, uint64_t, void*, int64_t, int8_t*, hipStream_t);
+                      float*, int, int, float, uint64_t, uint64_t, void*, int64_t, int8_t*, uint32_t*, hipStream_t);
+int ln_bwd_h3p_part_rows(int coop);
 int launch_attn_fwd_h3(const float*, const int64_t*, const float*, float*, float*, uint32_t*, int, int, int, int, float,
                        uint64_t, uint64_t, hipStream_t, int, float*, void*, int64_t, int8_t*);
 int launch_attn_bwd_h3(const float*, const int64_t*, const float*, const float*, const float*, const float*, float*,
@@ -59,7 +60,8 @@ void hs_stream_wait(hipStream_t waiter, hipStream_t signal);
   X(gwqkv) X(gbqkv) X(gwo) X(gbo) X(gg1) X(gb1) X(gw1) X(gbi) X(gw2) X(gb2) X(gg2) X(gbb2)                     \
   X(dz2) X(dz1) X(dctx) X(dbuf)                                                                              \
   HPF(X, da2p) HPF(X, df1p) HPF(X, da1p) HPF(X, dqkvp)                                                        \
-  X(part2_g) X(part2_b) X(part2_bias) X(part1_g) X(part1_b) X(part1_bias) X(part_gelu) X(part_bq)
+  X(part2_g) X(part2_b) X(part2_bias) X(part1_g) X(part1_b) X(part1_bias) X(part_gelu) X(part_bq)            \
+  X(psync_f) X(psync_b)
 
 namespace {
 
@@ -163,7 +165,8 @@ void layer_fwd_h3p(int64_t plan, int64_t x, int64_t xp, int64_t xe, int64_t mask
     req(launch_ln_fwd_h3p(slab, ptr<const float>(q[f_bo]), ptr<const float>(x) + r0 * H, ptr<const float>(q[f_g1]),
                           ptr<const float>(q[f_b1]), h1, ptr<float>(q[f_z1]) + r0 * H, ptr<float>(q[f_m1]) + r0,
                           ptr<float>(q[f_r1]) + r0, hr, H, eps, p_h, s1, o1, 1, ks_wo, (int64_t)hr * H, (int)r0,
-                          nullptr, ptr<void>(p1.p), p1.ps, ptr<int8_t>(p1.e), st),
+                          nullptr, ptr<void>(p1.p), p1.ps, ptr<int8_t>(p1.e), ptr<uint32_t>(q[f_psync_f]),
+                          (int)(r0 / 32), st),
         "LayerNorm 1 forward");
     const HPv pf = f1p.rows_from(r0);
     gemm(0, 1, hr, F, H, p1, W1, nullptr, F, ptr<const float>(q[f_bi]), kEpiGelu, 0.f,
@@ -173,7 +176,8 @@ void layer_fwd_h3p(int64_t plan, int64_t x, int64_t xp, int64_t xe, int64_t mask
     req(launch_ln_fwd_h3p(slab, ptr<const float>(q[f_b2]), h1, ptr<const float>(q[f_g2]), ptr<const float>(q[f_bb2]),
                           ptr<float>(q[f_h2]) + r0 * H, ptr<float>(q[f_z2]) + r0 * H, ptr<float>(q[f_m2]) + r0,
                           ptr<float>(q[f_r2]) + r0, hr, H, eps, p_h, s2, o2, 1, ks_w2, (int64_t)hr * H, (int)r0,
-                          ptr<float>(h == 0 ? amax0 : amax1), ptr<void>(p2.p), p2.ps, ptr<int8_t>(p2.e), st),
+                          ptr<float>(h == 0 ? amax0 : amax1), ptr<void>(p2.p), p2.ps, ptr<int8_t>(p2.e),
+                          ptr<uint32_t>(q[f_psync_f]), (int)(r0 / 32), st),
         "LayerNorm 2 forward");
   }
 }
@@ -196,7 +200,8 @@ void layer_bwd_h3p(int64_t plan, int64_t dh2, int64_t xp, int64_t xe, int64_t ma
   };
   hipStream_t st0 = ptr<ihipStream_t>(st0_), st1 = ptr<ihipStream_t>(st1_);
   const int B = (int)q[f_B], S = (int)q[f_S], NH = (int)q[f_NH], H = (int)q[f_H], F = (int)q[f_F];
-  const int rows = (int)q[f_rows], nb = rows / 32;
+  const int rows = (int)q[f_rows], nb = rows / 32, npart = rows / ln_bwd_h3p_part_rows(q[f_psync_b] != 0);
+  uint32_t* psb = ptr<uint32_t>(q[f_psync_b]);
   const HPv Wqkv = hp_at(q, f_wqkv_p), Wo = hp_at(q, f_wo_p), W1 = hp_at(q, f_w1_p), W2 = hp_at(q, f_w2_p);
   const HPv X{xp, q[f_xp_ld], q[f_xp_ps], xe, q[f_xp_lde], q[f_xp_blk]};
   const HPv ctxp = hp_at(q, f_ctxp_p), h1p = hp_at(q, f_h1p_p), f1p = hp_at(q, f_f1p_p);
@@ -215,13 +220,13 @@ void layer_bwd_h3p(int64_t plan, int64_t dh2, int64_t xp, int64_t xe, int64_t ma
   auto finalize = [&](int64_t pg, int64_t pb, int64_t pbias, int64_t og, int64_t ob, int64_t obias) {
     const float* parts[3] = {ptr<const float>(pg), ptr<const float>(pb), ptr<const float>(pbias)};
     float* outs[3] = {ptr<float>(og), ptr<float>(ob), ptr<float>(obias)};
-    launch_colpart_finalize(parts, outs, 3, nb, H, 1, st1);
+    launch_colpart_finalize(parts, outs, 3, npart, H, 1, st1);
   };
   // LN2 backward; its parameter gradients and the FFN-out weight gradient on the side stream
   req(launch_ln_bwd_h3p(ptr<const float>(dh2), ptr<const float>(q[f_z2]), ptr<const float>(q[f_m2]),
                         ptr<const float>(q[f_r2]), ptr<const float>(q[f_g2]), dz2, ptr<float>(q[f_part2_g]),
                         ptr<float>(q[f_part2_b]), ptr<float>(q[f_part2_bias]), rows, H, p_h, s2, o2,
-                        ptr<void>(da2p.p), da2p.ps, ptr<int8_t>(da2p.e), st0),
+                        ptr<void>(da2p.p), da2p.ps, ptr<int8_t>(da2p.e), psb, st0),
       "LayerNorm 2 backward");
   hs_stream_wait(st1, st0);
   finalize(q[f_part2_g], q[f_part2_b], q[f_part2_bias], q[f_gg2], q[f_gbb2], q[f_gb2]);
@@ -245,7 +250,7 @@ void layer_bwd_h3p(int64_t plan, int64_t dh2, int64_t xp, int64_t xe, int64_t ma
   req(launch_ln_bwd_h3p(dz2, ptr<const float>(q[f_z1]), ptr<const float>(q[f_m1]), ptr<const float>(q[f_r1]),
                         ptr<const float>(q[f_g1]), dz1, ptr<float>(q[f_part1_g]), ptr<float>(q[f_part1_b]),
                         ptr<float>(q[f_part1_bias]), rows, H, p_h, s1, o1, ptr<void>(da1p.p), da1p.ps,
-                        ptr<int8_t>(da1p.e), st0),
+                        ptr<int8_t>(da1p.e), psb, st0),
       "LayerNorm 1 backward");
   hs_stream_wait(st1, st0);
   finalize(q[f_part1_g], q[f_part1_b], q[f_part1_bias], q[f_gg1], q[f_gb1], q[f_gbo]);

@@ -221,6 +221,120 @@ __global__ void __launch_bounds__(64 * WV) ln_fwd_h3p_kernel(
   }
 }
 
+// The same LayerNorm forward on 4-wave workgroups of 4 RPW rows (8 with RPW 2: a 2048-row call is 256
+// workgroups, one per CU, instead of 64 of 32 rows): the 32 / (4 RPW) workgroups of a 32-row panel
+// combine their column-group |max| through the panel record (h3p.h psync_exchange) and each splits
+// its own rows from registers.  Per-row arithmetic, y / z / planes / exponents bitwise those of
+// ln_fwd_h3p_kernel.  `psync`: the records of panels panel0 + (rows of this call) / 32.
+template <int NV, int RPW>
+__global__ void __launch_bounds__(256) ln_fwd_h3p_coop_kernel(
+    const float* __restrict__ a, const float* __restrict__ bias, const float* __restrict__ resid,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ y, float* __restrict__ zsave,
+    float* __restrict__ mean_out, float* __restrict__ rstd_out, float eps, float p, uint64_t seed, uint64_t off, int mode,
+    const uint64_t* __restrict__ seed_dev, int nslab, int64_t slab_stride, int row0, float* __restrict__ amax_y,
+    uint16_t* __restrict__ planes, int64_t ps, int8_t* __restrict__ exps, uint32_t* __restrict__ psync, int panel0) {
+  constexpr int H = NV * 256, NG = H / 32, RB = 4 * RPW, NP = 32 / RB;
+  __shared__ uint32_t red[4][NG];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int panel = blockIdx.x / NP;
+  uint32_t* rec = psync + (int64_t)(panel0 + panel) * kPanelSyncWords;
+  uint32_t gen = 0u;
+  if (threadIdx.x == 0) gen = psync_gen(rec);  // in flight behind the row loads
+  const float scale = p < 1.f ? 1.0f / (1.0f - p) : 0.f;
+  seed = resolve_seed(seed, seed_dev);
+  uint32_t am = 0u;
+  float o[RPW][NV][4];
+#pragma unroll
+  for (int j = 0; j < RPW; ++j) {
+    const int row = blockIdx.x * RB + w * RPW + j;
+    const int64_t base = (int64_t)row * H;
+    float x[NV][4];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = (k * 64 + lane) * 4;
+      load4(a + base + c, x[k]);
+      for (int sl = 1; sl < nslab; ++sl) {
+        float t[4];
+        load4(a + sl * slab_stride + base + c, t);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[k][e] += t[e];
+      }
+      if (bias) {
+        float b[4];
+        load4(bias + c, b);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[k][e] += b[e];
+      }
+      if (mode == kBDR && p > 0.f) {
+        float m[4];
+        keep4(seed, off, (uint64_t)((int64_t)(row0 + row) * H + c) >> 2, p, scale, m);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[k][e] *= m[e];
+      }
+      if (resid) {
+        float r[4];
+        load4(resid + base + c, r);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[k][e] += r[e];
+      }
+      if (zsave) store4(zsave + base + c, x[k]);
+    }
+    float mean, rstd;
+    row_stats<NV>(x, H, mean, rstd, eps);
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = (k * 64 + lane) * 4;
+      float gw[4], gb[4];
+      load4(gamma + c, gw);
+      load4(beta + c, gb);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        o[j][k][e] = gw[e] * ((x[k][e] - mean) * rstd) + gb[e];
+        am = amax_bits(am, o[j][k][e]);
+      }
+      store4(y + base + c, o[j][k]);
+    }
+    if (lane == 0) {
+      mean_out[row] = mean;
+      rstd_out[row] = rstd;
+    }
+  }
+  if (amax_y) amax_commit(amax_y, am);
+  // column group k * 8 + lane / 8: the lane's |max| over its rows, its 8 lanes, the 4 waves, the panel
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    uint32_t gm = 0u;
+#pragma unroll
+    for (int j = 0; j < RPW; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) gm = amax_bits(gm, o[j][k][e]);
+#pragma unroll
+    for (int sh = 1; sh < 8; sh <<= 1) gm = max(gm, static_cast<uint32_t>(__shfl_xor(static_cast<int>(gm), sh, 64)));
+    if ((lane & 7) == 0) red[w][k * 8 + (lane >> 3)] = gm;
+  }
+  __syncthreads();
+  if (w == 0) {
+    uint32_t m = 0u;
+    if (lane < NG) m = max(max(red[0][lane], red[1][lane]), max(red[2][lane], red[3][lane]));
+    const uint32_t g = static_cast<uint32_t>(__shfl(static_cast<int>(gen), 0, 64));
+    m = psync_wait(rec, g, psync_arrive(rec, g, m, NG, NP), NG);
+    if (lane < NG) red[0][lane] = m;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int e = h3p_exp_bits(red[0][k * 8 + (lane >> 3)]);
+    const float sc = h3p_scale(e);
+#pragma unroll
+    for (int j = 0; j < RPW; ++j) {
+      const int row = blockIdx.x * RB + w * RPW + j;
+      h3p_store4(planes, ps, h3p_index(row, (k * 64 + lane) * 4, H, 1), o[j][k], sc);  // blocked planes
+    }
+    if (w == 0 && (lane & 7) == 0 && (blockIdx.x % NP) == 0)
+      exps[(int64_t)panel * NG + k * 8 + (lane >> 3)] = static_cast<int8_t>(e);
+  }
+}
+
 // Column partials are written as part[blockIdx.x][H] (one row per block); the WV waves'
 // register partials are summed in a fixed pairwise order (deterministic).
 template <int NV, int WV = 4>
@@ -495,6 +609,114 @@ __global__ void __launch_bounds__(64 * kLnH3pWaves) ln_bwd_h3p_kernel(
   colpart8_store<NV>(abias, part_bias, win);
 }
 
+// The same backward on 4-wave workgroups of 4 RPW rows (the forward's panel exchange for the da
+// exponents): a 4096-row call is 512 workgroups instead of 128.  Column partials per WORKGROUP
+// (part[rows / (4 RPW)][H], ln_bwd_h3p_part_rows) through the 3 KB chunked window.
+template <int NV, int RPW>
+__global__ void __launch_bounds__(256) ln_bwd_h3p_coop_kernel(
+    const float* __restrict__ dy, const float* __restrict__ zsave, const float* __restrict__ mean_in,
+    const float* __restrict__ rstd_in, const float* __restrict__ gamma, float* __restrict__ dz_out,
+    float* __restrict__ part_gamma, float* __restrict__ part_beta, float* __restrict__ part_bias, float p, uint64_t seed,
+    uint64_t off, const uint64_t* __restrict__ seed_dev, uint16_t* __restrict__ planes, int64_t ps,
+    int8_t* __restrict__ exps, uint32_t* __restrict__ psync) {
+  constexpr int H = NV * 256, NG = H / 32, RB = 4 * RPW, NP = 32 / RB;
+  __shared__ __attribute__((aligned(16))) float win[3 * 256];
+  __shared__ uint32_t red[4][NG];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int panel = blockIdx.x / NP;
+  uint32_t* rec = psync + (int64_t)panel * kPanelSyncWords;
+  uint32_t gen = 0u;
+  if (threadIdx.x == 0) gen = psync_gen(rec);
+  const float scale = p < 1.f ? 1.0f / (1.0f - p) : 0.f;
+  seed = resolve_seed(seed, seed_dev);
+  float ag[NV][4], ab[NV][4], abias[NV][4], gw[NV][4], da[RPW][NV][4];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    load4(gamma + (k * 64 + lane) * 4, gw[k]);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) ag[k][e] = ab[k][e] = abias[k][e] = 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < RPW; ++j) {
+    const int row = blockIdx.x * RB + w * RPW + j;
+    const int64_t base = (int64_t)row * H;
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float d[NV][4], xh[NV][4], g[NV][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      float z[4];
+      load4(dy + base + (k * 64 + lane) * 4, d[k]);
+      load4(zsave + base + (k * 64 + lane) * 4, z);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        xh[k][e] = (z[e] - mean) * rstd;
+        g[k][e] = d[k][e] * gw[k][e];
+        ag[k][e] = fmaf(d[k][e], xh[k][e], ag[k][e]);
+        ab[k][e] += d[k][e];
+        s1 += g[k][e];
+        s2 = fmaf(g[k][e], xh[k][e], s2);
+      }
+    }
+    s1 = wave_sum(s1) / H;
+    s2 = wave_sum(s2) / H;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = (k * 64 + lane) * 4;
+      float dzv[4], m[4] = {1.f, 1.f, 1.f, 1.f};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dzv[e] = rstd * (g[k][e] - s1 - xh[k][e] * s2);
+      store4(dz_out + base + c, dzv);
+      if (p > 0.f) keep4(seed, off, (uint64_t)(base + c) >> 2, p, scale, m);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        da[j][k][e] = dzv[e] * m[e];
+        abias[k][e] += da[j][k][e];
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    uint32_t gm = 0u;
+#pragma unroll
+    for (int j = 0; j < RPW; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) gm = amax_bits(gm, da[j][k][e]);
+#pragma unroll
+    for (int sh = 1; sh < 8; sh <<= 1) gm = max(gm, static_cast<uint32_t>(__shfl_xor(static_cast<int>(gm), sh, 64)));
+    if ((lane & 7) == 0) red[w][k * 8 + (lane >> 3)] = gm;
+  }
+  __syncthreads();
+  bool last = false;
+  const uint32_t g = static_cast<uint32_t>(__shfl(static_cast<int>(gen), 0, 64));
+  if (w == 0) {
+    uint32_t m = 0u;
+    if (lane < NG) m = max(max(red[0][lane], red[1][lane]), max(red[2][lane], red[3][lane]));
+    last = psync_arrive(rec, g, m, NG, NP);
+  }
+  // the column partials do not need the exponents: they cover the rest of the panel's arrivals
+  colpart_chunked_store<NV>(ag, part_gamma, win);
+  colpart_chunked_store<NV>(ab, part_beta, win);
+  colpart_chunked_store<NV>(abias, part_bias, win);
+  if (w == 0) {
+    const uint32_t m = psync_wait(rec, g, last, NG);
+    if (lane < NG) red[0][lane] = m;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int e = h3p_exp_bits(red[0][k * 8 + (lane >> 3)]);
+    const float sc = h3p_scale(e);
+#pragma unroll
+    for (int j = 0; j < RPW; ++j) {
+      const int row = blockIdx.x * RB + w * RPW + j;
+      h3p_store4(planes, ps, h3p_index(row, (k * 64 + lane) * 4, H, 1), da[j][k], sc);  // blocked planes
+    }
+    if (w == 0 && (lane & 7) == 0 && (blockIdx.x % NP) == 0)
+      exps[(int64_t)panel * NG + k * 8 + (lane >> 3)] = static_cast<int8_t>(e);
+  }
+}
+
 // ------------------------------------------------------------ embeddings
 template <int NV, typename T>
 __global__ void __launch_bounds__(256) emb_fwd_kernel(const int64_t* __restrict__ ids, const int64_t* __restrict__ tt,
@@ -644,14 +866,33 @@ void ln_fwd_launch(const void* a, const float* bias, const void* resid, const fl
                      row0, amax);
 }
 
-static int g_ln_h3p_waves = 16;  // waves per 32-row block of the h3p LN forward (A/B hook)
+// h3p LN backward with the panel exchange (A/B hook, set_ln_bwd_coop): 1 = 8 rows per workgroup,
+// 2 = 4 rows per workgroup, 0 = the 32-row-block kernel
+static int g_ln_bwd_coop = 1;
+
+// h3p LN forward kernel (A/B hook, set_ln_h3p_waves): 1 = panel exchange, 4 rows per workgroup (default:
+// a 2048-row call is 512 workgroups); 0 = panel exchange, 8 rows per workgroup; 16 / 8 = one 32-row
+// workgroup of 16 / 8 waves (round 5).  Measured (round 6, tools/bench_producers.py, 2048 rows, 2 slabs):
+// 15.2 / 17.6 / 19.1 / 23.3 us alone; the BERT-base step 10.60 / 10.69 / 10.82 ms (bench.py --ab).
+static int g_ln_h3p_waves = 1;
 
 template <int NV, typename T>
 void ln_fwd_h3p_launch(const void* a, const float* bias, const void* resid, const float* gamma, const float* beta,
                        void* y, float* zsave, float* mean, float* rstd, int rows, float eps, float p, uint64_t seed,
                        uint64_t off, int mode, int nslab, int64_t slab_stride, int row0, float* amax, uint16_t* planes,
-                       int64_t ps, int8_t* exps, hipStream_t st) {
-  if (g_ln_h3p_waves == 16)
+                       int64_t ps, int8_t* exps, uint32_t* psync, int panel0, hipStream_t st) {
+  if (psync && (g_ln_h3p_waves == 0 || g_ln_h3p_waves == 1)) {
+    if (g_ln_h3p_waves == 0)
+      hipLaunchKernelGGL((ln_fwd_h3p_coop_kernel<NV, 2>), dim3(rows / 8), dim3(256), 0, st, (const float*)a, bias,
+                         (const float*)resid, gamma, beta, (float*)y, zsave, mean, rstd, eps, p, seed, off, mode,
+                         g_seed_dev, nslab, slab_stride, row0, amax, planes, ps, exps, psync, panel0);
+    else
+      hipLaunchKernelGGL((ln_fwd_h3p_coop_kernel<NV, 1>), dim3(rows / 4), dim3(256), 0, st, (const float*)a, bias,
+                         (const float*)resid, gamma, beta, (float*)y, zsave, mean, rstd, eps, p, seed, off, mode,
+                         g_seed_dev, nslab, slab_stride, row0, amax, planes, ps, exps, psync, panel0);
+    return;
+  }
+  if (g_ln_h3p_waves != 8)
     hipLaunchKernelGGL((ln_fwd_h3p_kernel<NV, T, 16>), dim3(rows / 32), dim3(64 * 16), 0, st, (const T*)a, bias,
                        (const T*)resid, gamma, beta, (T*)y, zsave, mean, rstd, eps, p, seed, off, mode, g_seed_dev, nslab,
                        slab_stride, row0, amax, planes, ps, exps);
@@ -664,7 +905,17 @@ void ln_fwd_h3p_launch(const void* a, const float* bias, const void* resid, cons
 template <int NV>
 void ln_bwd_h3p_launch(const float* dy, const float* zsave, const float* mean, const float* rstd, const float* gamma,
                        float* dz, float* pg, float* pb, float* pbias, int rows, float p, uint64_t seed, uint64_t off,
-                       uint16_t* planes, int64_t ps, int8_t* exps, hipStream_t st) {
+                       uint16_t* planes, int64_t ps, int8_t* exps, uint32_t* psync, hipStream_t st) {
+  if (psync && g_ln_bwd_coop == 1) {
+    hipLaunchKernelGGL((ln_bwd_h3p_coop_kernel<NV, 2>), dim3(rows / 8), dim3(256), 0, st, dy, zsave, mean, rstd, gamma,
+                       dz, pg, pb, pbias, p, seed, off, g_seed_dev, planes, ps, exps, psync);
+    return;
+  }
+  if (psync && g_ln_bwd_coop == 2) {
+    hipLaunchKernelGGL((ln_bwd_h3p_coop_kernel<NV, 1>), dim3(rows / 4), dim3(256), 0, st, dy, zsave, mean, rstd, gamma,
+                       dz, pg, pb, pbias, p, seed, off, g_seed_dev, planes, ps, exps, psync);
+    return;
+  }
   hipLaunchKernelGGL((ln_bwd_h3p_kernel<NV>), dim3(rows / 32), dim3(64 * kLnH3pWaves), 0, st, dy, zsave, mean, rstd,
                      gamma, dz, pg, pb, pbias, p, seed, off, g_seed_dev, planes, ps, exps);
 }
@@ -746,23 +997,27 @@ void set_ln_h3p_waves(int w) { hs::g_ln_h3p_waves = w; }
 int launch_ln_fwd_h3p(const void* a, const float* bias, const void* resid, const float* gamma, const float* beta,
                       void* y, float* zsave, float* mean, float* rstd, int rows, int H, float eps, float p,
                       uint64_t seed, uint64_t off, int mode, int nslab, int64_t slab_stride, int row0, float* amax,
-                      void* planes, int64_t ps, int8_t* exps, hipStream_t st) {
-  if (rows <= 0 || rows % 32 || !planes || !exps || ps % 4) return -1;
+                      void* planes, int64_t ps, int8_t* exps, uint32_t* psync, int panel0, hipStream_t st) {
+  if (rows <= 0 || rows % 32 || !planes || !exps || ps % 4 || panel0 < 0) return -1;
   if (nslab < 1 || (nslab > 1 && (slab_stride < (int64_t)rows * H || slab_stride % 4))) return -1;
   HS_DISPATCH_H(H, (ln_fwd_h3p_launch<NV, float>(a, bias, resid, gamma, beta, y, zsave, mean, rstd, rows, eps, p, seed,
                                                  off, mode, nslab, slab_stride, row0, amax, (uint16_t*)planes, ps, exps,
-                                                 st)));
+                                                 psync, panel0, st)));
   return 0;
 }
 
+// rows per column-partial row of launch_ln_bwd_h3p with a panel record (32 without)
+int ln_bwd_h3p_part_rows(int coop) { return !coop || !g_ln_bwd_coop ? 32 : g_ln_bwd_coop == 2 ? 4 : 8; }
+void set_ln_bwd_coop(int on) { g_ln_bwd_coop = on; }
+
 // LayerNorm backward (bias-dropout-residual mode, fp32) writing da as h3p planes; partials are
-// [rows / 32][H] (ln_bwd_h3p_blocks)
+// [rows / ln_bwd_h3p_part_rows(psync != 0)][H].  psync: panel records of the call's rows / 32 panels
 int launch_ln_bwd_h3p(const float* dy, const float* zsave, const float* mean, const float* rstd, const float* gamma,
                       float* dz, float* pg, float* pb, float* pbias, int rows, int H, float p, uint64_t seed,
-                      uint64_t off, void* planes, int64_t ps, int8_t* exps, hipStream_t st) {
+                      uint64_t off, void* planes, int64_t ps, int8_t* exps, uint32_t* psync, hipStream_t st) {
   if (rows <= 0 || rows % 32 || !planes || !exps || !dz || ps % 4) return -1;
   HS_DISPATCH_H(H, (ln_bwd_h3p_launch<NV>(dy, zsave, mean, rstd, gamma, dz, pg, pb, pbias, rows, p, seed, off,
-                                          (uint16_t*)planes, ps, exps, st)));
+                                          (uint16_t*)planes, ps, exps, psync, st)));
   return 0;
 }
 

@@ -940,6 +940,57 @@ class BertForPreTraining(BertPreTrainedModel):
             return store.shadow_view(wt), store.shadow_view(wd)
         return wt.detach().bfloat16(), wd.detach().bfloat16()
 
+    def _head_h3p(self):
+        """h3p engine: the masked-LM head's GEMM weights as block-scaled planes -- the transform's
+        [H, H] and the tied decoder's [V, H] padded to pad512(V) rows (the missing rows split as zeros)
+        -- or None (another engine, a CPU model, widths the engine does not tile).  Re-split right after
+        every update of their chunks (the word table is chunk 0, the transform the heads' last chunk:
+        runtime/flat.py add_update_hook, on the updating stream), else here when stale."""
+        from hetseq_amd.ops import gemm as G
+        from hetseq_amd.ops import h3p
+
+        wt = self.cls.predictions.transform.dense_act.weight
+        wd = self.cls.predictions.decoder.weight
+        H, V = wt.shape[0], wd.shape[0]
+        if not (G.h3p_active(self.compute_dtype) and wt.is_cuda and H % 128 == 0 and wt.dtype == torch.float32):
+            return None
+        store = getattr(self, "_hs_store", None)
+        cached = self.__dict__.get("_hs_head_h3p")
+        if cached is None or cached["store"] is not store:
+            Vp = (V + 511) // 512 * 512
+            tp, dp = h3p.empty(H, H, wt.device), h3p.empty(Vp, H, wt.device)
+            tabs = [h3p.SplitTable([(wd.detach(), dp)], wt.device), h3p.SplitTable([(wt.detach(), tp)], wt.device)]
+            cached = {"store": store, "planes": (tp, dp), "tabs": tabs, "stamp": [None, None]}
+            self.__dict__["_hs_head_h3p"] = cached
+            if store is not None and store.chunks is not None:
+                from hetseq_amd.runtime.flat import bisect_chunk
+
+                for k, w in enumerate((wd, wt)):
+                    store.add_update_hook(bisect_chunk(store.chunks, store.offset(w)), self._head_h3p_hook(cached, k))
+        now = store.stamp() if store is not None else None
+        for k in range(2):
+            if now is None or cached["stamp"][k] != now:
+                if store is not None:
+                    store.params_ready()
+                cached["tabs"][k].run()
+                cached["stamp"][k] = now
+        return cached["planes"]
+
+    def _head_h3p_hook(self, cached, k):
+        store = cached["store"]
+
+        def hook():
+            from hetseq_amd.ops import gemm as G
+
+            if self.__dict__.get("_hs_head_h3p") is not cached:
+                return
+            if G.h3p_active(self.compute_dtype):
+                cached["tabs"][k].run()
+                cached["stamp"][k] = store.stamp()
+            else:
+                cached["stamp"][k] = None
+        return hook
+
     def sparse_embedding(self):
         """(tables, rest) for the data-parallel engine's sparse table exchange (parallel/tied.py):
         the word / position / token-type tables, whose gradient rows the fused embedding backward
@@ -958,16 +1009,21 @@ class BertForPreTraining(BertPreTrainedModel):
             attention_mask = torch.ones_like(input_ids)
         B, S = input_ids.shape
         wt_, wd_ = self._mlm_weights()
-        head_w = (wt_, wd_) if isinstance(wt_, torch.Tensor) and wt_.dtype == torch.float32 else ()
+        head_hp = self._head_h3p()
+        head_w = (wt_, wd_) if isinstance(wt_, torch.Tensor) and wt_.dtype == torch.float32 and head_hp is None else ()
         pool, plan = self.bert._amax_plan(extra_weights=head_w, extra_slots=3)
         seq2d = self.bert.fused_encoder(input_ids, token_type_ids, attention_mask, checkpoint_activations,
                                         amax=(pool, plan))
         cap = B * S if self.max_predictions_per_seq is None else min(B * S, B * int(self.max_predictions_per_seq))
+        if head_hp is not None:  # (rows past the labelled ones are zero rows with label -1: no loss, no gradient)
+            cap = (cap + 127) // 128 * 128
         t, pred = self.cls.predictions.transform, self.cls.predictions
         pooler, nsp = self.bert.pooler.dense_act, self.cls.seq_relationship
         params = [t.dense_act.weight, t.dense_act.bias, t.LayerNorm.weight, t.LayerNorm.bias, pred.decoder.weight,
                   pred.bias, pooler.weight, pooler.bias, nsp.weight, nsp.bias]
         meta = {"cap": cap, "eps": t.LayerNorm.variance_epsilon, "weights": self._mlm_weights, "B": B, "S": S}
+        if head_hp is not None:
+            meta["h3p"] = head_hp
         if pool is not None and head_w:
             L = len(plan)
             last = plan[-1]

@@ -79,6 +79,32 @@ def _colpart_buf(nparts, H, device, n=3):
     return torch.empty((n, nparts, H), dtype=torch.float32, device=device)
 
 
+_PSYNC: dict = {}  # (device, region) -> zero-initialised panel records
+_OLD_PSYNC: list = []  # smaller record sets that plans built earlier still address
+
+
+def panel_sync(device, rows, region):
+    """Panel records (csrc/kernels/h3p.h psync_*) for ``rows`` rows of whole-batch row indices: the h3p
+    LayerNorm kernels' workgroups exchange their block |max| through them.  ``region`` 0 serves the
+    forward (its two half-batch streams address disjoint panels), 1 the backward, 2 the masked-LM
+    head's transform LayerNorm.  Zeroed once here;
+    the kernels leave every record ready for its next call."""
+    key = (device, region)
+    t = _PSYNC.get(key)
+    need = (rows + 31) // 32 * hip().panel_sync_words()
+    if t is None or t.numel() < need:
+        if t is not None:
+            _OLD_PSYNC.append(t)
+        t = torch.zeros(max(need, 128 * hip().panel_sync_words()), dtype=torch.int32, device=device)
+        _PSYNC[key] = t
+    return t
+
+
+def ln_bwd_h3p_parts(rows):
+    """Column-partial rows of ln_bwd_h3p (one per 8-row workgroup)."""
+    return rows // hip().ln_bwd_h3p_part_rows(1)
+
+
 # --------------------------------------------------------------------- basic ops
 def ln_fwd(a, gamma, beta, eps=1e-12, bias=None, resid=None, p=0.0, mode=0, seed=0, off=0, save_z=True,
            outs=None, row0=0, amax=None):
@@ -111,9 +137,10 @@ def ln_fwd(a, gamma, beta, eps=1e-12, bias=None, resid=None, p=0.0, mode=0, seed
     return y, z, mean, rstd
 
 
-def ln_fwd_h3p(a, gamma, beta, eps, bias, resid, p, seed, off, outs, row0, hp, amax=None):
+def ln_fwd_h3p(a, gamma, beta, eps, bias, resid, p, seed, off, outs, row0, hp, amax=None, region=0):
     """ln_fwd (bias-dropout-residual mode, fp32) that also writes y as h3p planes into ``hp`` (an
-    ops.h3p.HP over the same rows): the next product's operand without a split pass."""
+    ops.h3p.HP over the same rows): the next product's operand without a split pass.  ``region``: the
+    panel records (panel_sync) -- 0 the encoder's forward, 2 the masked-LM head's transform."""
     assert hp.blk, "producers write blocked planes"
     nslab, stride = 1, 0
     if a.dim() == 3:
@@ -121,10 +148,12 @@ def ln_fwd_h3p(a, gamma, beta, eps, bias, resid, p, seed, off, outs, row0, hp, a
         a = a[0]
     rows, H = a.shape
     y, z, mean, rstd = outs
+    psync = panel_sync(a.device, int(row0) + rows, region)
     hip().ln_fwd_h3p(a.data_ptr(), bias.data_ptr() if bias is not None else 0,
                      resid.data_ptr() if resid is not None else 0, gamma.data_ptr(), beta.data_ptr(), y.data_ptr(),
                      z.data_ptr(), mean.data_ptr(), rstd.data_ptr(), rows, H, float(eps), float(p), seed, off, 1,
-                     nslab, stride, int(row0), G.slot_ptr(amax), hp.data_ptr(), hp.ps, hp.exps_ptr(), stream_handle())
+                     nslab, stride, int(row0), G.slot_ptr(amax), hp.data_ptr(), hp.ps, hp.exps_ptr(),
+                     psync.data_ptr(), int(row0) // 32, stream_handle())
     return y
 
 
@@ -134,12 +163,13 @@ def ln_bwd_h3p(dy, z, mean, rstd, gamma, p, seed, off, hp, acc=None, side=False)
     views; finalised on the weight-gradient stream with ``side``) or returned fresh."""
     assert hp.blk, "producers write blocked planes"
     rows, H = dy.shape
-    nb = rows // 32
+    nb = ln_bwd_h3p_parts(rows)
     part = _colpart_buf(nb, H, dy.device)
     dz = torch.empty_like(dy)
+    psync = panel_sync(dy.device, rows, 1)
     hip().ln_bwd_h3p(dy.data_ptr(), z.data_ptr(), mean.data_ptr(), rstd.data_ptr(), gamma.data_ptr(), dz.data_ptr(),
                      part[0].data_ptr(), part[1].data_ptr(), part[2].data_ptr(), rows, H, float(p), seed, off,
-                     hp.data_ptr(), hp.ps, hp.exps_ptr(), stream_handle())
+                     hp.data_ptr(), hp.ps, hp.exps_ptr(), psync.data_ptr(), stream_handle())
     if acc is not None:
         outs = list(acc[:3])
 
@@ -1075,6 +1105,15 @@ class FusedCrossEntropy(torch.autograd.Function):
         return d, None, None
 
 
+def _dec_dgrad_ks(K):
+    """K slices of the tied decoder's data gradient on planes (K = the padded vocabulary, 30 output
+    tiles at BERT-base): slices of <= 2048 (16 at 30720), within the kernel's 4096 per slice."""
+    s = 1
+    while K // s > 2048 and K % (64 * s) == 0:
+        s *= 2
+    return s
+
+
 def cross_entropy(logits, labels, ignore_index=-1):
     return FusedCrossEntropy.apply(logits, labels, ignore_index)
 
@@ -1099,16 +1138,39 @@ class FusedPreTrainingLoss(torch.autograd.Function):
         idx, lab, cnt = mlm_compact(labels.reshape(-1), cap)
         hsel = gather_rows(seq, idx)
         hsel_in = hsel
+        hpw = meta.get("h3p")  # h3p engine: (transform planes, tied decoder planes padded to pad512(V) rows)
+        ctx.hp = None
+        if hpw is not None:
+            # every product on block-scaled planes: the gathered rows split once, the transform's GELU
+            # in its GEMM epilogue (pre-activation kept), the transform LN writing t2's planes, the
+            # decoder over the padded vocabulary (zero weight rows, bias past V read as zero)
+            from hetseq_amd.ops import h3p
+
+            Wtp, Wdp = hpw
+            R, V = hsel.shape[0], Wd.shape[0]
+            hselp = h3p.split(hsel)
+            t1pre = torch.empty((R, H), dtype=torch.float32, device=seq.device)
+            t1 = h3p.gemm(hselp, Wtp, tb=True, bias=bt, epi=h3p.EPI_GELU, aux=t1pre, site="mlm transform fwd")
+            outs = (torch.empty_like(t1), torch.empty_like(t1), torch.empty(R, dtype=torch.float32, device=seq.device),
+                    torch.empty(R, dtype=torch.float32, device=seq.device))
+            t2p = h3p.empty(R, H, seq.device)
+            ln_fwd_h3p(t1, g, b, eps, None, None, 0.0, 0, 0, outs, 0, t2p, region=2)
+            t2, z, mean, rstd = outs
+            lbuf = torch.empty((R, Wdp.rows), dtype=torch.float32, device=seq.device)
+            h3p.gemm(t2p, Wdp, tb=True, out=lbuf, bias=bdec, epi=h3p.EPI_BIAS, valid=(R, V), site="decoder fwd")
+            logits = lbuf[:, :V]
+            ctx.hp = (hselp, t2p, Wtp, Wdp)
         am = meta.get("amax")  # h3 engine: {seq, wt, wd, t2} |max| slots (hsel's bound: the whole sequence output)
-        t1pre = G.linear_fwd(hsel_in, Wt, amax=(am["seq"], am["wt"]) if am else None)
-        t1 = bias_gelu_fwd(t1pre, bt)
-        t2, z, mean, rstd = ln_fwd(t1, g, b, eps, amax=am["t2"] if am else None)
-        # tied decoder on the compacted rows; fp32: split-bf16 kernel on the vocabulary padded to
-        # 512 (logits is a view of a zero-padded buffer the backward reuses), else library GEMM
-        if t2.dtype == torch.float32:
-            logits, lbuf = G.decoder_logits(t2, Wd, bdec, amax=(am["t2"], am["wd"]) if am else None)
-        else:
-            logits, lbuf = G.gemm(t2, Wd, tb=True, bias=bdec, epi=1, out_dtype=torch.float32), None
+        if hpw is None:
+            t1pre = G.linear_fwd(hsel_in, Wt, amax=(am["seq"], am["wt"]) if am else None)
+            t1 = bias_gelu_fwd(t1pre, bt)
+            t2, z, mean, rstd = ln_fwd(t1, g, b, eps, amax=am["t2"] if am else None)
+            # tied decoder on the compacted rows; fp32: the padded split kernel (logits is a view of a
+            # zero-padded buffer the backward reuses); bf16: the plane engine
+            if t2.dtype == torch.float32:
+                logits, lbuf = G.decoder_logits(t2, Wd, bdec, amax=(am["t2"], am["wd"]) if am else None)
+            else:
+                logits, lbuf = G.gemm(t2, Wd, tb=True, bias=bdec, epi=1, out_dtype=torch.float32), None
         out, lse = xent_fwd(logits, lab)
         # pooler + NSP + CE; total = out[0] + nsp mean loss
         dev = seq.device
@@ -1157,7 +1219,20 @@ class FusedPreTrainingLoss(torch.autograd.Function):
         store = meta.get("store")
         dec_acc = not (side and _FRESH_WGRAD and store is not None and store.claim_fresh())
         am_dl = am["dl"] if (am and lbuf is not None) else None
-        if lbuf is not None:  # padded split-bf16 decoder products (pad columns of dlogits stay zero)
+        hpw = ctx.hp
+        if hpw is not None:  # h3p: dlogits split once (pad columns zero); both decoder gradients on planes
+            from hetseq_amd.ops import h3p
+
+            hselp, t2p, Wtp, Wdp = hpw
+            dlp = h3p.split(lbuf)
+
+            def dwdec():
+                if acc and store is not None:
+                    (store.ensure_zero if dec_acc else store.mark_stored)(Gv[4])
+                out_w = Gv[4] if acc else torch.zeros((V, t2.shape[1]), dtype=torch.float32, device=t2.device)
+                return h3p.gemm(dlp, t2p, ta=True, out=out_w, beta=1.0 if dec_acc else 0.0, valid=(V, t2.shape[1]),
+                                site="decoder wgrad")
+        elif lbuf is not None:  # padded split-bf16 decoder products (pad columns of dlogits stay zero)
             def dwdec():
                 if acc and store is not None:  # lazy zero_grad bookkeeping, on the writer's stream
                     (store.ensure_zero if dec_acc else store.mark_stored)(Gv[4])
@@ -1178,7 +1253,8 @@ class FusedPreTrainingLoss(torch.autograd.Function):
 
         if side:
             with streams.coalesced():  # (the mark records on the side stream: one fork serves both)
-                dWdec = streams.run(dl_c.device, dwdec, dl_c, t2, lbuf)
+                dWdec = streams.run(dl_c.device, dwdec, dl_c, t2, lbuf,
+                                    *((dlp.planes, dlp.exps, t2p.planes, t2p.exps) if hpw is not None else ()))
                 streams.mark(dl_c.device, "tied")  # the embedding backward waits for this GEMM only
                 dbdec = streams.run(dl_c.device, dbias, dlogits, lbuf)
         else:
@@ -1188,19 +1264,32 @@ class FusedPreTrainingLoss(torch.autograd.Function):
             h = tied.lookup(Gv[4])
             if h is not None:
                 h.dense_ready(dl_c.device)
-        dt2 = G.decoder_dgrad(lbuf, Wd, V, amax=(am_dl, am["wd"]) if am_dl is not None else None) \
-            if lbuf is not None else G.gemm(dl_c, Wd)
+        if hpw is not None:  # K = the padded vocabulary over 30 output tiles: 16 K slices
+            dt2 = h3p.gemm(dlp, Wdp, ksplit=_dec_dgrad_ks(dlp.cols), site="decoder dgrad")
+        elif lbuf is not None:
+            dt2 = G.decoder_dgrad(lbuf, Wd, V, amax=(am_dl, am["wd"]) if am_dl is not None else None)
+        else:
+            dt2 = G.gemm(dl_c, Wd)
         dt1, _, dg, db, _ = ln_bwd(dt2, z, mean, rstd, g, 0.0, 0, acc=(Gv[2], Gv[3]) if acc else None, side=side)
         am_d = am["dt"] if am else None  # |dt1pre|: the transform's two gradient products share it
         dt1pre, dbt = gelu_bwd_colsum(dt1, t1pre, bt, db_acc=Gv[1] if acc else None, amax=am_d)
         hsel_in, dt1pre_in = hsel, dt1pre
-        wt_am = (am_d, am["seq"]) if am else None
-        if side:
-            dWt = streams.run(dt1pre.device, lambda: G.linear_wgrad(dt1pre_in, hsel_in, out=Gv[0], accumulate=True,
-                                                                    amax=wt_am), dt1pre_in, hsel_in, am_d)
+        if hpw is not None:  # the transform's gradients on planes (dt1pre split once)
+            dtp = h3p.split(dt1pre)
+
+            def dwt():
+                out_t = Gv[0] if acc else torch.zeros_like(Wt)
+                return h3p.gemm(dtp, hselp, ta=True, out=out_t, beta=1.0, site="mlm transform wgrad")
+            dWt = streams.run(dt1pre.device, dwt, dtp.planes, dtp.exps, hselp.planes, hselp.exps) if side else dwt()
+            dhsel = h3p.gemm(dtp, Wtp, site="mlm transform dgrad")
         else:
-            dWt = G.linear_wgrad(dt1pre_in, hsel_in, out=Gv[0] if acc else None, accumulate=acc, amax=wt_am)
-        dhsel = G.linear_dgrad(dt1pre_in, Wt, amax=(am_d, am["wt"]) if am else None)
+            wt_am = (am_d, am["seq"]) if am else None
+            if side:
+                dWt = streams.run(dt1pre.device, lambda: G.linear_wgrad(dt1pre_in, hsel_in, out=Gv[0], accumulate=True,
+                                                                        amax=wt_am), dt1pre_in, hsel_in, am_d)
+            else:
+                dWt = G.linear_wgrad(dt1pre_in, hsel_in, out=Gv[0] if acc else None, accumulate=acc, amax=wt_am)
+            dhsel = G.linear_dgrad(dt1pre_in, Wt, amax=(am_d, am["wt"]) if am else None)
         H_ = seq.shape[1]
         dseq = torch.zeros((ctx.T, H_), dtype=seq.dtype, device=seq.device)
         hip().scatter_add_rows(dtype_code(dseq), dhsel.data_ptr(), idx.data_ptr(), dseq.data_ptr(), idx.numel(),

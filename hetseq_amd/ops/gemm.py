@@ -5,12 +5,12 @@ of a Linear layer; ``linear_gelu_fwd`` and ``linear_dgrad_dgelu`` are the FFN
 products with the GELU (and its backward + bias gradient) fused into the GEMM
 epilogue.  Two engines:
 
-* ``hip``  -- the hand-written gfx950 MFMA kernel (csrc/kernels/gemm.hip) with
-             fused epilogues (bias, bias+GELU, dGELU+bias-grad, beta-accumulate);
-             fp32 shapes that tile exactly.
-* ``blas`` -- hipBLASLt / rocBLAS through ``torch.mm`` (plain library GEMM; the
-             per-shape solution comes from the measured TunableOp table, see
-             runtime/gemm_tuning.py), followed by the separate HIP epilogue kernels.
+* ``hip``  -- the hand-written gfx950 MFMA kernels (csrc/kernels/gemm.hip, gemm_planes.hip,
+             gemm_h3p.hip) with fused epilogues (bias, bias+GELU, dGELU+bias-grad,
+             beta-accumulate).  The only engine of the training step.
+* ``blas`` -- hipBLASLt / rocBLAS through ``torch.mm``: a reference ORACLE for tests and
+             benchmarks (``HETSEQ_GEMM=blas`` / :func:`set_mode`), and the fallback for a shape
+             no hand-written kernel serves (odd test shapes; never a BERT-base site).
 
 fp32 products on the HIP engine run on the 16-bit matrix cores: as three split-fp16
 products with per-tensor power-of-two operand scales (``HETSEQ_FP32_GEMM=h3``: fp32-level
@@ -19,13 +19,10 @@ which the producing kernels emit -- :func:`amax_of` computes it for the rest), a
 products (``x6``: fp32-level error, no scale needed), or on the exact-fp32 MFMA (``native``);
 ``x3`` (two-term bf16 split, ~2^-16 relative error) exists for benchmarking only.
 
-``HETSEQ_GEMM=hip|blas|auto`` selects; ``auto`` (default) times both paths --
-including the epilogue work the fused kernel absorbs -- once per (shape,
-transpose, epilogue) on the GPU and keeps the hand-written engine unless the
-library is faster by more than ``HIP_MARGIN`` (1.10: a
-one-shot timing of two ~equal kernels is noise, and a 10 % edge measured alone
-did not survive inside the overlapped training step -- docs/kernels.md).  The choice is
-recorded in ``GEMM_CHOICES`` and logged by the benchmark.  In bf16 mode the
+``HETSEQ_GEMM=hip|blas`` selects (default ``hip``).  There is no run-time choice between the
+hand-written kernels and the library (round 6): per call site only the hand-written kernels'
+own variants are measured once (split-K, plane-engine variant), recorded in ``GEMM_CHOICES``
+and logged by the benchmark.  In bf16 mode the
 weight-gradient GEMM writes fp32 directly (``out_dtype``), so master gradients
 never round through bf16.
 """
@@ -38,7 +35,8 @@ import torch
 from hetseq_amd.ops._C import hip, stream_handle
 
 GEMM_CHOICES: dict = {}
-_MODE = os.environ.get("HETSEQ_GEMM", "auto")
+_MODE = os.environ.get("HETSEQ_GEMM", "hip")
+assert _MODE in ("hip", "blas"), "HETSEQ_GEMM must be hip or blas"
 # h3p: the encoder layers' products on pre-split block-scaled planes (ops/h3p.py, gemm_h3p.hip); every
 # other fp32 product (the pre-training heads, standalone calls) on the h3 engine (dtype code 4)
 _FP32_DT = {"native": 0, "x6": 2, "x3": 3, "h3": 4, "h3p": 4}
@@ -49,17 +47,11 @@ SPLIT_ENGINES = ("x6", "h3", "h3p")  # the fp32-level split engines (x3 is a ben
 _SLABS: dict = {}  # (device, stream) -> split-K partial-sum workspace
 
 EPI_NONE, EPI_BIAS, EPI_GELU, EPI_DGELU = 0, 1, 2, 3
-HIP_MARGIN = 1.10
-
-
-def _hip_wins(t_hip, t_blas):
-    """Per-call-site engine decision: the hand-written engine unless the library is clearly faster."""
-    return t_hip <= HIP_MARGIN * t_blas
 
 
 def set_mode(mode):
     global _MODE
-    assert mode in ("hip", "blas", "auto")
+    assert mode in ("hip", "blas")
     _MODE = mode
     GEMM_CHOICES.clear()
 
@@ -82,7 +74,8 @@ def load_choices(path):
     if d.get("fp32") != _FP32:
         return False
     for k, v in d["choices"].items():
-        GEMM_CHOICES[ast.literal_eval(k)] = tuple(v)
+        if v and v[0] == "hip":  # (older files also hold library choices: those sites are re-measured)
+            GEMM_CHOICES[ast.literal_eval(k)] = tuple(v)
     return True
 
 
@@ -301,11 +294,8 @@ def _planes_ksplit(M, N, K, P):
 
 
 def _bf16_choice(key, pa, pb, ta, tb, out, bias, epi, beta, ks, out_dtype):
-    """bf16 operands: the plane engine (best measured variant) or the library, chosen per call site
-    by timing both once (auto mode; results in GEMM_CHOICES); 'hip' mode always takes the engine.
-    Returns ``out`` when the engine ran, None when the caller should use the library."""
-    if _MODE == "hip":
-        return out if gemm_planes(pa, pb, ta, tb, out, bias, epi, beta, ksplit=ks) else None
+    """bf16 operands on the plane engine: its fastest variant and K split for the call site, measured
+    once (GEMM_CHOICES).  Returns ``out`` when the engine ran, None for a shape it does not serve."""
     c = GEMM_CHOICES.get(key)
     if c is None and not torch.cuda.is_current_stream_capturing():
         scratch = out.clone() if beta != 0.0 else torch.empty_like(out)
@@ -320,15 +310,12 @@ def _bf16_choice(key, pa, pb, ta, tb, out, bias, epi, beta, ks, out_dtype):
                 if gemm_planes(pa, pb, ta, tb, scratch, bias, epi, beta, ksplit=s, variant=v):
                     t = _bench(lambda: gemm_planes(pa, pb, ta, tb, scratch, bias, epi, beta, ksplit=s, variant=v))
                     best = (t, v, s) if best is None or t < best[0] else best
-        a, b = pa.buf if pa.P == 1 else None, pb.buf if pb.P == 1 else None
-        t_blas = _bench(lambda: _blas_gemm(a, b, ta, tb, scratch, bias, epi, beta, out_dtype))
         if best is None:
-            c = ("blas", None, round(t_blas, 4))
-        else:
-            c = ("hip" if _hip_wins(best[0], t_blas) else "blas", round(best[0], 4), round(t_blas, 4), best[2], best[1])
+            return None
+        c = ("hip", round(best[0], 4), None, best[2], best[1])
         GEMM_CHOICES[key] = c
-    if c is None or c[0] != "hip":
-        return None
+    if c is None:
+        return out if gemm_planes(pa, pb, ta, tb, out, bias, epi, beta, ksplit=ks) else None
     return out if gemm_planes(pa, pb, ta, tb, out, bias, epi, beta, ksplit=c[3], variant=c[4]) else None
 
 
@@ -413,22 +400,8 @@ def _bench(fn, iters=5):
 
 
 def _choose(key, run_hip, run_blas):
-    """'hip' or 'blas' for this call site; auto mode measures both once (side effects go to scratch)."""
-    if _MODE != "auto":
-        return _MODE
-    c = GEMM_CHOICES.get(key)
-    if c is not None:
-        return c[0]
-    if torch.cuda.is_current_stream_capturing():
-        # a shape the eager warm-up never ran (e.g. the one-chain forward of a capture after split
-        # warm-up steps): nothing can be timed here, and a first library call would create its
-        # handle inside the capture (hipblasCreate fails there) -- the HIP engine, which serves it
-        return "hip"
-    t_hip = _bench(run_hip)
-    t_blas = _bench(run_blas)
-    c = "hip" if _hip_wins(t_hip, t_blas) else "blas"
-    GEMM_CHOICES[key] = (c, round(t_hip, 4), round(t_blas, 4))
-    return c
+    """The engine of a call site: the hand-written kernels, or the library ORACLE in 'blas' mode."""
+    return "blas" if _MODE == "blas" else "hip"
 
 
 def gemm(a, b, ta=False, tb=False, out=None, bias=None, epi=EPI_NONE, beta=0.0, out_dtype=None, ksplit=None,
@@ -468,23 +441,20 @@ def gemm(a, b, ta=False, tb=False, out=None, bias=None, epi=EPI_NONE, beta=0.0, 
         def run_blas():
             _blas_gemm(a, b, ta, tb, scratch, bias, epi, beta, out_dtype)
 
-        if key not in GEMM_CHOICES and _MODE == "auto" and not torch.cuda.is_current_stream_capturing():
+        if (key not in GEMM_CHOICES and _MODE == "hip" and _FP32 != "native" and epi <= EPI_BIAS
+                and not torch.cuda.is_current_stream_capturing()):
+            # the split engines: measure the kernel's own K split once (wave quantisation vs slab traffic)
             scratch = out.clone() if beta != 0.0 else torch.empty_like(out)
-            if not run_hip():
-                GEMM_CHOICES[key] = ("blas", None, None)
-            elif _FP32 != "native" and epi <= EPI_BIAS:
-                # the split-bf16 engines: measure the K split too (wave quantisation vs slab traffic)
-                best = None
-                for cand in (0, 1, 2, 4):
-                    ks[0] = cand
-                    if run_hip():
-                        t = _bench(run_hip)
-                        if best is None or t < best[0]:
-                            best = (t, cand)
+            best = None
+            for cand in (0, 1, 2, 4):
+                ks[0] = cand
+                if run_hip():
+                    t = _bench(run_hip)
+                    if best is None or t < best[0]:
+                        best = (t, cand)
+            if best is not None:
                 ks[0] = best[1]
-                t_blas = _bench(run_blas)
-                c = "hip" if _hip_wins(best[0], t_blas) else "blas"
-                GEMM_CHOICES[key] = (c, round(best[0], 4), round(t_blas, 4), best[1])
+                GEMM_CHOICES[key] = ("hip", round(best[0], 4), None, best[1])
         c = GEMM_CHOICES.get(key)
         if c is not None and len(c) > 3:
             ks[0] = c[3]
@@ -553,19 +523,15 @@ def decoder_dgrad(dlogits_buf, w, V, amax=None):
     def run_blas():
         torch.mm(dlogits_buf[:, :V], w, out=out)
 
-    if key not in GEMM_CHOICES and _MODE == "auto" and not torch.cuda.is_current_stream_capturing():
+    if key not in GEMM_CHOICES and _MODE == "hip" and not torch.cuda.is_current_stream_capturing():
         best = None  # K = vocab over only (R/128) x (H/128) tiles: measure the split
         for cand in (4, 8, 16):
             ks[0] = cand
             if run_hip():
                 t = _bench(run_hip)
                 best = (t, cand) if best is None or t < best[0] else best
-        t_blas = _bench(run_blas)
-        if best is None:
-            GEMM_CHOICES[key] = ("blas", None, round(t_blas, 4))
-        else:
-            GEMM_CHOICES[key] = ("hip" if _hip_wins(best[0], t_blas) else "blas", round(best[0], 4), round(t_blas, 4),
-                                 best[1])
+        if best is not None:
+            GEMM_CHOICES[key] = ("hip", round(best[0], 4), None, best[1])
     c = GEMM_CHOICES.get(key)
     if c is not None and len(c) > 3:
         ks[0] = c[3]
@@ -593,9 +559,6 @@ def decoder_wgrad(dlogits_buf, t2, V, out, accumulate, amax=None):
         else:
             torch.mm(dlogits_buf[:, :V].t(), t2, out=dst)
 
-    if key not in GEMM_CHOICES and _MODE == "auto" and not torch.cuda.is_current_stream_capturing():
-        scratch = out.clone()  # measuring must not accumulate into the real gradient
-        _choose_padded(key, lambda: run_hip(scratch), lambda: run_blas(scratch))
     if _choose_padded(key, None, None) == "hip" and run_hip(out):
         return out
     run_blas(out)
@@ -603,12 +566,7 @@ def decoder_wgrad(dlogits_buf, t2, V, out, accumulate, amax=None):
 
 
 def _choose_padded(key, run_hip, run_blas):
-    """Engine choice for the padded decoder products: measured once per site in auto mode
-    (side effects only into buffers the caller overwrites afterwards), else the mode."""
-    if _MODE == "hip":
-        return "hip"
-    if key in GEMM_CHOICES:
-        return GEMM_CHOICES[key][0]
+    """Engine of the padded decoder products: the hand-written kernels (the library in 'blas' mode)."""
     return _choose(key, run_hip, run_blas)
 
 
@@ -675,17 +633,16 @@ def linear_wgrad_colsum(dy, x, out, colsum_out, ksplit=None, accumulate=True, am
     # on, whatever the choice table held: the bias gradient's summation order never switches)
     key = (M, N, T, True, False, EPI_NONE, True)
     ks = ksplit if ksplit is not None else 0
-    if _MODE == "auto":
-        if key not in GEMM_CHOICES:
-            if torch.cuda.is_current_stream_capturing():
-                return False
-            gemm(dy, x, ta=True, tb=False, out=torch.empty_like(out), beta=1.0, out_dtype=torch.float32,
-                 ksplit=ksplit, amax=amax)  # first call: measures the engines (into scratch)
-        c = GEMM_CHOICES.get(key)
-        if c is None or c[0] != "hip":
+    if key not in GEMM_CHOICES:
+        if torch.cuda.is_current_stream_capturing():
             return False
-        if ksplit is None and len(c) > 3:
-            ks = c[3]
+        gemm(dy, x, ta=True, tb=False, out=torch.empty_like(out), beta=1.0, out_dtype=torch.float32,
+             ksplit=ksplit, amax=amax)  # first call: measures the kernel's K split (into scratch)
+    c = GEMM_CHOICES.get(key)
+    if c is None or c[0] != "hip":
+        return False
+    if ksplit is None and len(c) > 3:
+        ks = c[3]
     part = torch.empty((max(ks, 1) if ks > 0 else 8, M), dtype=torch.float32, device=dy.device)
     return _hip_gemm(dy, x, True, False, out, beta=1.0 if accumulate else 0.0, part=part, colsum=colsum_out,
                      colsum_acc=accumulate, ksplit=ks, amax=amax)
@@ -726,8 +683,6 @@ def linear_gelu_fwd(x, w, b, out=None, amax=None, amax_out=None):
             torch.mm(x, w.t(), out=pre)
             bert_ops.bias_gelu_fwd(pre, b, out=y)
 
-        if key not in GEMM_CHOICES and _MODE == "auto" and not run_hip():
-            GEMM_CHOICES[key] = ("blas", None, None)
         if _choose(key, run_hip, run_blas) == "hip" and run_hip(amax_out):
             return y, pre
     torch.mm(x, w.t(), out=pre)
@@ -769,16 +724,6 @@ def linear_dgrad_dgelu(dy, w, pre, b, db_acc=None, amax=None, amax_out=None, col
                              part=part if out_db is not None else None, colsum=out_db, colsum_acc=acc, amax=amax,
                              amax_out=amo)
 
-        if key not in GEMM_CHOICES and _MODE == "auto":
-            scratch_db = torch.zeros_like(db)
-
-            def run_blas():
-                bert_ops.gelu_bwd_colsum(torch.mm(dy, w), pre, b, db_acc=scratch_db)
-
-            if not run_hip(scratch_db, True):
-                GEMM_CHOICES[key] = ("blas", None, None)
-            else:
-                _choose(key, lambda: run_hip(scratch_db, True), run_blas)
         if _choose(key, None, None) == "hip" and run_hip(db if colsum else None, db_acc is not None, amax_out):
             return dpre, (db if colsum else None)
     df = torch.mm(dy, w)

@@ -96,14 +96,16 @@ def empty(rows, cols, device, blk=True):
     return HP(planes, exps, rows, cols, blk=blk)
 
 
-def split(x, out=None, blk=True):
-    """fp32 ``[rows, cols]`` (row-major, rows and cols multiples of 32) -> :class:`HP` (one pass:
-    one wave per 32 x 32 block); ``blk``: blocked plane layout (ignored when ``out`` is given)."""
+def split(x, out=None, blk=True, rows=None):
+    """fp32 ``[rows, cols]`` (row-major, cols a multiple of 32) -> :class:`HP` (one pass: one wave per
+    32 x 32 block); ``blk``: blocked plane layout (ignored when ``out`` is given).  ``rows`` (a multiple
+    of 32, >= x's rows): the planes' row count -- x's missing rows split as zeros (a padded vocabulary)."""
     assert x.dtype == torch.float32 and x.dim() == 2 and x.stride(1) == 1
-    rows, cols = x.shape
+    vrows, cols = x.shape
+    rows = out.rows if out is not None else (vrows if rows is None else rows)
     hp = out if out is not None else empty(rows, cols, x.device, blk)
     hip().h3p_split(x.data_ptr(), x.stride(0), rows, cols, hp.data_ptr(), hp.ld, hp.ps, hp.exps_ptr(), hp.lde,
-                    stream_handle(), int(hp.blk))
+                    stream_handle(), int(hp.blk), vrows)
     return hp
 
 
@@ -111,18 +113,19 @@ class SplitTable(object):
     """One launch that splits many fp32 matrices (the GEMM weights after every update): the
     segment records live in device memory, built once for fixed addresses."""
 
-    FMT = "QQQqqqqiiii"  # QSplitSeg (gemm_h3p.hip): src, dst, ex, lds, ldd, ps, lde, rows, cols, blk0, blocked
+    FMT = "QQQqqqqiiiiii"  # QSplitSeg (gemm_h3p.hip): src, dst, ex, lds, ldd, ps, lde, rows, cols, blk0, blocked, vrows, pad
 
     def __init__(self, pairs, device):
-        """``pairs``: [(fp32 2-D tensor, HP destination)]."""
+        """``pairs``: [(fp32 2-D tensor, HP destination)]; a tensor with fewer rows than its destination
+        (a vocabulary padded to the GEMM tile) splits the missing rows as zeros."""
         nbytes = hip().h3p_split_seg_bytes()
         assert struct.calcsize("<" + self.FMT) == nbytes, "QSplitSeg layout changed"
         recs, blk = [], 0
         for x, hp in pairs:
-            assert x.dtype == torch.float32 and x.stride(1) == 1 and x.shape == (hp.rows, hp.cols)
+            assert x.dtype == torch.float32 and x.stride(1) == 1 and x.shape[1] == hp.cols and x.shape[0] <= hp.rows
             assert x.data_ptr() % 16 == 0 and x.stride(0) % 4 == 0
             recs.append(struct.pack("<" + self.FMT, x.data_ptr(), hp.data_ptr(), hp.exps_ptr(), x.stride(0), hp.ld,
-                                    hp.ps, hp.lde, hp.rows, hp.cols, blk, int(hp.blk)))
+                                    hp.ps, hp.lde, hp.rows, hp.cols, blk, int(hp.blk), x.shape[0], 0))
             blk += (hp.rows // BLK) * (hp.cols // BLK)
         raw = torch.frombuffer(bytearray(b"".join(recs)), dtype=torch.uint8)
         self.table = raw.to(device)
@@ -201,7 +204,7 @@ def _census(site, a, b):
 
 
 def gemm(a, b, ta=False, tb=False, out=None, bias=None, epi=EPI_NONE, beta=0.0, aux=None, part=None, colsum=None,
-         colsum_acc=False, ksplit=1, planes_out=None, slab_only=False, site=None):
+         colsum_acc=False, ksplit=1, planes_out=None, slab_only=False, site=None, valid=None):
     """``out = beta*out + op(a) @ op(b)`` (+ epilogue) on h3p operands.
 
     ``epi``: EPI_BIAS (+bias), EPI_GELU (``aux`` <- pre-activation, result gelu(pre + bias)),
@@ -209,7 +212,9 @@ def gemm(a, b, ta=False, tb=False, out=None, bias=None, epi=EPI_NONE, beta=0.0, 
     [M/128, N] scratch).  ``planes_out``: an :class:`HP` [M, N] that receives the GELU / dGELU result
     (``out`` may then be None).  ``ksplit`` > 1: fp32 slabs summed by a reduce pass into ``out``, or
     -- ``slab_only`` -- returned as a [ks, M, N] view for a consumer that sums them (valid until
-    the next split GEMM on this stream).  Raises on a request the kernel does not serve."""
+    the next split GEMM on this stream).  ``valid`` = (Mv, Nv): a padded problem's real extents --
+    ``out`` ([Mv, N] or [M, N]) gets rows < Mv only, bias entries past Nv read as zero.  Raises on a
+    request the kernel does not serve."""
     M, N, K = dims(a, b, ta, tb)
     assert (tb and b.cols == K) or (not tb and b.rows == K), "inner dimensions differ"
     if _CENSUS_ON[0]:
@@ -222,8 +227,9 @@ def gemm(a, b, ta=False, tb=False, out=None, bias=None, epi=EPI_NONE, beta=0.0, 
         out = _slab(M * N, dev)[:M * N].view(M, N)
     if out is None and not slab_only and planes_out is None:
         out = torch.empty((M, N), dtype=torch.float32, device=dev)
+    mv, nv = valid if valid is not None else (0, 0)
     if out is not None:
-        assert out.dtype == torch.float32 and out.shape == (M, N) and out.stride(1) == 1
+        assert out.dtype == torch.float32 and out.shape[1] == N and out.shape[0] in (M, mv) and out.stride(1) == 1
     assert planes_out is None or planes_out.blk, "the GEMM epilogue writes blocked planes"
     rc = hip().gemm_h3p(int(ta), int(tb), M, N, K, a.data_ptr(), a.ld, a.ps, a.exps_ptr(), a.lde,
                         b.data_ptr(), b.ld, b.ps, b.exps_ptr(), b.lde,
@@ -237,7 +243,7 @@ def gemm(a, b, ta=False, tb=False, out=None, bias=None, epi=EPI_NONE, beta=0.0, 
                         planes_out.exps_ptr() if planes_out is not None else 0,
                         planes_out.lde if planes_out is not None else 0,
                         int(ksplit), slab.data_ptr() if slab is not None else 0,
-                        slab.numel() if slab is not None else 0, stream_handle(), int(a.blk), int(b.blk))
+                        slab.numel() if slab is not None else 0, stream_handle(), int(a.blk), int(b.blk), int(mv), int(nv))
     if rc != 0:
         raise ValueError("gemm_h3p: request not served (M=%d N=%d K=%d ta=%d tb=%d epi=%d ksplit=%d)"
                          % (M, N, K, ta, tb, epi, ksplit))

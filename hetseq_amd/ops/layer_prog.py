@@ -77,8 +77,9 @@ class LayerProgram(object):
         self.dbuf = z(B * NH * S)  # (dqkv itself exists only as the planes dqkvp)
         self.da2p, self.da1p = h3p.empty(rows, H, device), h3p.empty(rows, H, device)
         self.df1p, self.dqkvp = h3p.empty(rows, Fd, device), h3p.empty(rows, 3 * H, device)
-        nb = rows // 32
+        nb = rows // 4  # (the most column-partial rows any ln_bwd_h3p kernel writes: 4-row workgroups)
         self.part2, self.part1 = bert_ops._colpart_buf(nb, H, device), bert_ops._colpart_buf(nb, H, device)
+        self.psync_f, self.psync_b = bert_ops.panel_sync(device, rows, 0), bert_ops.panel_sync(device, rows, 1)
         self.part_gelu = z(rows // 128, Fd)
         self.part_bq = z(rows // 32, 3 * H)  # the QKV bias gradient's column partials (from dqkvp)
         hr = rows // halves
@@ -124,6 +125,8 @@ class LayerProgram(object):
             put("part2_" + k, self.part2[i].data_ptr())
             put("part1_" + k, self.part1[i].data_ptr())
         put("part_gelu", self.part_gelu.data_ptr())
+        put("psync_f", self.psync_f.data_ptr())
+        put("psync_b", self.psync_b.data_ptr())
         put("part_bq", self.part_bq.data_ptr())
         self.q = q
         self.addr = q.buffer_info()[0]

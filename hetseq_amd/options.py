@@ -17,7 +17,7 @@ change a reference default):
   --check-consistency N     all-reduce a parameter checksum every N updates
   --collective-timeout S    timeout (seconds) for process-group collectives (and the RCCL watchdog)
   --comm-engine E           gradient collectives: native RCCL engine (auto on GPU+nccl) or c10d
-  --shard-optimizer {auto,off}  data-parallel Adam sharded over the ranks (reduce-scatter / all-gather)
+  --shard-optimizer {auto,on,off}  data-parallel Adam sharded over the ranks (reduce-scatter / all-gather)
   --no-sparse-embedding-exchange  all-reduce the embedding tables densely in the last bucket
                             (default: early dense bucket + sparse row exchange, parallel/tied.py)
   --checkpoint-activations  recompute encoder layers in backward
@@ -225,10 +225,12 @@ def add_mi355x_args(parser):
                        help="gradient / stats collectives: the native RCCL engine (greatest-priority comm "
                             "stream, event-gated buckets, watchdog; auto = on GPUs with the nccl backend) or "
                             "torch.distributed (c10d)")
-    group.add_argument("--shard-optimizer", default="auto", choices=["auto", "off"],
+    group.add_argument("--shard-optimizer", default="auto", choices=["auto", "on", "off"],
                        help="data-parallel Adam: reduce-scatter the gradient buckets, update 1/W of the parameters "
                             "per rank and all-gather them layer by layer beside the next forward "
-                            "(parallel/zero.py; auto = on for data-parallel Adam runs without BMUF / HIP graphs)")
+                            "(parallel/zero.py; auto = on for data-parallel Adam runs without BMUF / HIP graphs on "
+                            "the native RCCL engine, after its in-place collectives pass a self-test on the job's "
+                            "ranks; on = also with c10d)")
     group.add_argument("--no-sparse-embedding-exchange", dest="sparse_embedding_exchange", action="store_false",
                        help="all-reduce the embedding tables densely in the last bucket instead of the early "
                             "dense bucket (tied decoder part) + all-gather of the per-token rows")

@@ -197,6 +197,26 @@ class NativeComm(object):
     def outstanding(self):
         return self._c.outstanding()
 
+    def identity(self):
+        """RCCL's own view of this communicator: {rccl_count, rccl_rank, rccl_device, pci_bus_id}."""
+        return dict(self._c.identity())
+
+    def busbw(self, nbytes=64 << 20, iters=5):
+        """Bus bandwidth (GB/s) of an in-stream fp32 all-reduce of ``nbytes`` over this communicator:
+        2 (W - 1) / W x bytes / time (ring convention); the algorithm bandwidth when W = 1."""
+        x = torch.ones(nbytes // 4, dtype=torch.float32, device=torch.device("cuda", self.device))
+        for _ in range(2):
+            self.all_reduce(x)
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(iters):
+            self.all_reduce(x)
+        e.record()
+        e.synchronize()
+        t = s.elapsed_time(e) / iters * 1e-3
+        f = 2.0 * (self.size - 1) / self.size if self.size > 1 else 1.0
+        return round(f * nbytes / t / 1e9, 1)
+
     def close(self, graceful=True):
         """Destroy the communicator (every rank at the same point), or abort it when operations
         are still outstanding / ``graceful`` is False."""
@@ -218,6 +238,45 @@ def want_native(engine, device_is_cuda, group=None):
             raise RuntimeError("--comm-engine native: hetseq_amd._comm is not built")
         return False
     return True
+
+
+def shard_self_test(nc, group=None):
+    """Check the engine's in-place collectives that the sharded update relies on (parallel/zero.py),
+    on the ranks of ``group``, before the first step: a reduce-scatter whose piece r must hold the sum
+    on rank r, an all-reduce of a tail beside it, and an in-place all-gather whose every piece must
+    come back from its owner.  Host check once, then every rank agrees (c10d all-reduce of a failure
+    count).  Returns (ok, None) or (False, reason)."""
+    W, r = nc.size, nc.rank
+    dev = torch.device("cuda", nc.device)
+    ps, tail = 3 * 64, 17
+    why = None
+    try:
+        base = torch.arange(W * ps + tail, dtype=torch.float32, device=dev)
+        g = base * (r + 1)
+        nc.reduce_scatter_async(g[:W * ps])
+        nc.all_reduce_async(g[W * ps:])
+        p = torch.zeros(W * ps, dtype=torch.float32, device=dev)
+        p[r * ps:(r + 1) * ps] = base[r * ps:(r + 1) * ps] - 7.0 * r
+        nc.all_gather_inplace_async(p)
+        nc.wait()
+        tot = W * (W + 1) / 2.0
+        want_g = base[r * ps:(r + 1) * ps] * tot
+        want_t = base[W * ps:] * tot
+        want_p = base[:W * ps] - 7.0 * torch.arange(W, device=dev, dtype=torch.float32).repeat_interleave(ps)
+        nc.check()
+        if not torch.equal(g[r * ps:(r + 1) * ps], want_g):
+            why = "reduce-scatter: rank %d's piece does not hold the sum" % r
+        elif not torch.equal(g[W * ps:], want_t):
+            why = "tail all-reduce: wrong sum on rank %d" % r
+        elif not torch.equal(p, want_p):
+            why = "in-place all-gather: wrong pieces on rank %d" % r
+    except Exception as e:  # noqa: BLE001 - any failure: the replicated update
+        why = "%s: %s" % (type(e).__name__, e)
+    ok = _agree(why is None, group or dist.group.WORLD, dev)
+    if not ok:
+        why = why or "failed on another rank"
+        warnings.warn("sharded optimizer update not used: native engine self-test: %s" % why)
+    return ok, (None if ok else why)
 
 
 # What the last create() call decided, for logs and the benchmark record:

@@ -64,6 +64,17 @@ class FlatDDP(torch.nn.Module):
             if self.world_size > 1 or comm_engine == "native" else None
         self.find_unused_parameters = find_unused_parameters
         self.require_sync = True
+        # sharded update: "auto" shards only on the native engine (with c10d every bucket is all-reduced
+        # whole anyway, and the per-region all_gathers would only add collectives), and only once the
+        # engine's in-place reduce-scatter / all-gather passed a check on these very ranks
+        self.shard_status = None
+        if shard_optimizer == "auto":
+            shard_optimizer = self.comm is not None
+            if shard_optimizer and self.world_size > 1 and self.plan_world == self.world_size:
+                ok, why = native_comm.shard_self_test(self.comm, self.process_group)
+                self.shard_status = why
+                shard_optimizer = ok
+        shard_optimizer = bool(shard_optimizer)
         cap = max(1, int(bucket_cap_mb * 1024 * 1024 / 4))
         params = list(store.params)
         # embedding tables exchanged sparsely (parallel/tied.py): out of the buckets; the rest of

@@ -396,6 +396,9 @@ class FlatParamStore(object):
                 self.shadow.copy_(self.param)
 
     def checksum(self):
+        """fp64 sum of every parameter, behind any pending staged update (its in-place all-gathers
+        run on the comm stream; a checksum read beside them would see half-gathered parameters)."""
+        self.params_ready()
         return self.param.double().sum()
 
     def segments(self):

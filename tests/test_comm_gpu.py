@@ -67,6 +67,23 @@ def test_collectives_single_rank(group):
         c.close()
 
 
+def test_identity_reports_rccl_view(group):
+    """What bench.py records per rank: RCCL's own count / rank / device for the communicator and
+    the device's PCI bus id (here: 1 rank), and a positive 64 MB all-reduce bandwidth."""
+    from hetseq_amd.ops._C import hip
+    from hetseq_amd.parallel.comm import NativeComm
+
+    c = NativeComm(group, timeout_s=60)
+    try:
+        ident = c.identity()
+        assert ident["rccl_count"] == 1 and ident["rccl_rank"] == 0
+        assert ident["rccl_device"] == torch.cuda.current_device()
+        assert ident["pci_bus_id"] == hip().pci_bus_id(torch.cuda.current_device()) and ident["pci_bus_id"]
+        assert c.busbw(8 << 20, iters=2) > 0
+    finally:
+        c.close()
+
+
 def test_async_bucket_ordering(group):
     """The comm stream must wait for the producer stream (a long kernel writes the bucket) and
     the consumer must wait for the comm stream: the result equals the producer's output."""
@@ -475,10 +492,17 @@ def test_sharded_early_buckets_snapshot_and_update(group, delay):
                 assert torch.equal(snap[lo:hi], store.grad[lo:hi]), (lo, hi)
             assert any(p.rows == 16 * 64 for blk in model.bert.encoder.layer for p in blk.__dict__.get("_hs_progs", {}).values())
         opt.clip_grad_norm(1.0)
+        opt.staged = shard  # the sharded step staged: Adam and the chunk all-gathers on the comm stream
         opt.step()
+        cs = store.checksum()  # straight after the staged step: must wait for the pending gathers
         opt.state_dict()
         torch.cuda.synchronize()
         out[shard] = store.param.clone()
+        assert float(cs) == float(store.param.double().sum())
+        if shard:  # the engine's self-test of the in-place collectives the sharded update uses
+            from hetseq_amd.parallel import comm as native_comm
+
+            assert native_comm.shard_self_test(net.comm, group) == (True, None)
         net.comm.check()
         net.comm.close()
     assert torch.allclose(out[True], out[False], rtol=1e-6, atol=1e-7), (out[True] - out[False]).abs().max().item()

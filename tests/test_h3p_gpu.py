@@ -276,6 +276,7 @@ def test_layernorm_h3p_planes(cuda, H, p):
     parameter-gradient partials (32-row blocks) equal to the plain kernel's to fp32 rounding."""
     from hetseq_amd.ops import bert_ops as O
     from hetseq_amd.ops import h3p
+    from hetseq_amd.ops._C import hip
 
     g = torch.Generator(device=cuda)
     g.manual_seed(H)
@@ -287,24 +288,70 @@ def test_layernorm_h3p_planes(cuda, H, p):
     beta = torch.randn(H, device=cuda, generator=g)
     seed, off = 1234, 77
     ref = O.ln_fwd(slabs, gamma, beta, 1e-12, bias=bias, resid=resid, p=p, mode=1, seed=seed, off=off, row0=64)
-    outs = tuple(torch.empty_like(t) for t in ref)
-    hp = h3p.empty(rows, H, cuda)
-    O.ln_fwd_h3p(slabs, gamma, beta, 1e-12, bias, resid, p, seed, off, outs, 64, hp)
-    for a, b in zip(ref, outs):
-        assert torch.equal(a, b)
     sp = h3p.split(ref[0])
-    assert torch.equal(hp.planes, sp.planes) and torch.equal(hp.exps, sp.exps)
+    # every forward kernel (panel exchange at 8 / 4 rows per workgroup, one 32-row block of 16 / 8
+    # waves), each called three times: the panel records must come back ready for the next call
+    for mode in (0, 1, 16, 8, 1):
+        hip().set_ln_h3p_waves(mode)
+        try:
+            for _ in range(3):
+                outs = tuple(torch.full_like(t, float("nan")) for t in ref)
+                hp = h3p.empty(rows, H, cuda)
+                O.ln_fwd_h3p(slabs, gamma, beta, 1e-12, bias, resid, p, seed, off, outs, 64, hp)
+                for a, b in zip(ref, outs):
+                    assert torch.equal(a, b)
+                assert torch.equal(hp.planes, sp.planes) and torch.equal(hp.exps, sp.exps), mode
+        finally:
+            hip().set_ln_h3p_waves(1)
     # backward
     dy = torch.randn(rows, H, device=cuda, generator=g)
     y, z, mean, rstd = ref
     dz, da, dg, db, dbias = O.ln_bwd(dy, z, mean, rstd, gamma, p, 1, seed, off, True, True)
-    hp2 = h3p.empty(rows, H, cuda)
-    dz2, dg2, db2, dbias2 = O.ln_bwd_h3p(dy, z, mean, rstd, gamma, p, seed, off, hp2)
-    assert torch.equal(dz, dz2)
     sp2 = h3p.split(da)
-    assert torch.equal(hp2.planes, sp2.planes) and torch.equal(hp2.exps, sp2.exps)
-    for a, b in ((dg, dg2), (db, db2), (dbias, dbias2)):
-        assert float((a - b).abs().max()) <= 1e-5 * (1 + float(a.abs().max()))
+    for bmode in (1, 2, 0, 1):  # panel exchange at 8 / 4 rows per workgroup, the 32-row-block kernel
+        hip().set_ln_bwd_coop(bmode)
+        try:
+            for _ in range(3):
+                hp2 = h3p.empty(rows, H, cuda)
+                dz2, dg2, db2, dbias2 = O.ln_bwd_h3p(dy, z, mean, rstd, gamma, p, seed, off, hp2)
+                assert torch.equal(dz, dz2)
+                assert torch.equal(hp2.planes, sp2.planes) and torch.equal(hp2.exps, sp2.exps), bmode
+                for a, b in ((dg, dg2), (db, db2), (dbias, dbias2)):
+                    assert float((a - b).abs().max()) <= 1e-5 * (1 + float(a.abs().max()))
+        finally:
+            hip().set_ln_bwd_coop(1)
+    # no exchange timed out, and every record is back at rest (count 0; the other parity cleared)
+    torch.cuda.synchronize()
+    words = hip().panel_sync_words()
+    for region in (0, 1):
+        rec = O.panel_sync(cuda, rows + 64, region).view(-1, words)
+        assert int(rec[:, 32].abs().sum()) == 0, "panel exchange timed out"
+        assert int(rec[:, 16].abs().sum()) == 0
+
+
+def test_panel_exchange_with_extreme_blocks(cuda):
+    """Per-block exponents through the panel exchange when the 8-row workgroups of a panel disagree
+    by many decades: rows 8-31 of every panel are constant (their LN output is beta, ~1e-6), rows
+    0-7 are not (~1), and two column groups scale by 1e-20 / 1e20.  The exponent must be the
+    panel's, so the planes are bitwise split(y)."""
+    from hetseq_amd.ops import bert_ops as O
+    from hetseq_amd.ops import h3p
+
+    rows, H = 128, 768
+    g = torch.Generator(device=cuda)
+    g.manual_seed(3)
+    a = torch.randn(rows, H, device=cuda, generator=g) * 1e-3
+    a.view(-1, 32, H)[:, 8:] = 0.5
+    gamma = torch.ones(H, device=cuda)
+    beta = torch.randn(H, device=cuda, generator=g) * 1e-6
+    gamma[:32] = 1e-20  # column blocks with tiny values
+    gamma[32:64] = 1e20
+    ref = O.ln_fwd(a, gamma, beta, 1e-12, mode=1)
+    outs = tuple(torch.empty_like(t) for t in ref)
+    hp = h3p.empty(rows, H, cuda)
+    O.ln_fwd_h3p(a, gamma, beta, 1e-12, None, None, 0.0, 0, 0, outs, 0, hp)
+    sp = h3p.split(ref[0])
+    assert torch.equal(hp.planes, sp.planes) and torch.equal(hp.exps, sp.exps)
 
 
 @pytest.mark.parametrize("S,p", [(128, 0.0), (128, 0.1), (512, 0.1)])

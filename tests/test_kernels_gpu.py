@@ -980,7 +980,7 @@ def test_gemm_x6_error_matches_fp32(cuda, ta, tb, M, N, K):
     assert errs["x3"] > 2 * errs["x6"] and errs["bf16"] > 100 * errs["x6"], errs
 
 
-@pytest.mark.parametrize("mode", ["hip", "blas", "auto"])
+@pytest.mark.parametrize("mode", ["hip", "blas"])
 def test_fused_ffn_gemms_dispatch(cuda, mode):
     """linear_gelu_fwd / linear_dgrad_dgelu give the same result on every engine."""
     from hetseq_amd.ops import gemm as G

@@ -59,15 +59,19 @@ def main():
         hp = h3p.empty(rows, H, dev)
         a_in = slab if ks > 1 else slab[0]
         t0 = timeit(lambda: bert_ops.ln_fwd(a_in, g, bt, 1e-12, bias, resid, 0.1, 1, 1, 2, outs=outs), a.reps)
-        hip().set_ln_h3p_waves(8)
-        t8 = timeit(lambda: bert_ops.ln_fwd_h3p(a_in, g, bt, 1e-12, bias, resid, 0.1, 1, 2, outs, 0, hp), a.reps)
-        hip().set_ln_h3p_waves(16)
-        t1 = timeit(lambda: bert_ops.ln_fwd_h3p(a_in, g, bt, 1e-12, bias, resid, 0.1, 1, 2, outs, 0, hp), a.reps)
+        tv = {}
+        for _ in range(3):  # interleaved rounds (one process)
+            for mode in (0, 1, 16, 8):
+                hip().set_ln_h3p_waves(mode)
+                t = timeit(lambda: bert_ops.ln_fwd_h3p(a_in, g, bt, 1e-12, bias, resid, 0.1, 1, 2, outs, 0, hp),
+                           a.reps)
+                tv[mode] = min(tv.get(mode, 1e9), t)
+        hip().set_ln_h3p_waves(0)
         t2 = timeit(lambda: (bert_ops.ln_fwd(a_in, g, bt, 1e-12, bias, resid, 0.1, 1, 1, 2, outs=outs),
                              h3p.split(outs[0], out=hp)), a.reps)
         ts = timeit(lambda: h3p.split(outs[0], out=hp), a.reps)
-        rec("ln_fwd rows=%d nslab=%d" % (rows, ks), fp32=t0, fused_h3p=t1, fused_h3p_8waves=t8, then_split=t2,
-            split_alone=ts)
+        rec("ln_fwd rows=%d nslab=%d" % (rows, ks), fp32=t0, coop_8rows=tv[0], coop_4rows=tv[1],
+            block32_16waves=tv[16], block32_8waves=tv[8], then_split=t2, split_alone=ts)
 
     rows = 4096
     dy, z = torch.randn(rows, H, device=dev), torch.randn(rows, H, device=dev)
@@ -76,10 +80,18 @@ def main():
     hp = h3p.empty(rows, H, dev)
     t0 = timeit(lambda: bert_ops.ln_bwd(dy, z, mean, rstd, g, 0.1, 1, 1, 2, True, True, acc=acc), a.reps)
     t1 = timeit(lambda: bert_ops.ln_bwd_h3p(dy, z, mean, rstd, g, 0.1, 1, 2, hp, acc=acc), a.reps)
+    part32 = bert_ops._colpart_buf(rows // 32, H, dev)
+    dz = torch.empty_like(dy)
+
+    def old_bwd():  # the 32-row-block kernel (no panel record), partials only
+        hip().ln_bwd_h3p(dy.data_ptr(), z.data_ptr(), mean.data_ptr(), rstd.data_ptr(), g.data_ptr(), dz.data_ptr(),
+                         part32[0].data_ptr(), part32[1].data_ptr(), part32[2].data_ptr(), rows, H, 0.1, 1, 2,
+                         hp.data_ptr(), hp.ps, hp.exps_ptr(), 0, torch.cuda.current_stream().cuda_stream)
+    t1o = timeit(old_bwd, a.reps)
 
     t2 = timeit(lambda: h3p.split(bert_ops.ln_bwd(dy, z, mean, rstd, g, 0.1, 1, 1, 2, True, True, acc=acc)[1],
                                   out=hp), a.reps)
-    rec("ln_bwd rows=%d" % rows, fp32=t0, fused_h3p=t1, then_split=t2)
+    rec("ln_bwd rows=%d" % rows, fp32=t0, fused_h3p=t1, block32_kernel_only=t1o, then_split=t2)
 
     for B in (16, 32):
         T = B * S
