@@ -301,6 +301,7 @@ HS_DEVICE float ds_scale(const float (&ds)[2][8], int& es, f32x16& a0, f32x16& a
 // dK / dV for 32 keys per wave (lane = key) over 64-query chunks of Q (biased, * 1/8) and dO.
 constexpr int kBwdLds = 2 * kIm + 64 * 4 * 2 + 64 * 4 * 4 + 2 * 8 * 4;
 
+template <int OCC>
 HS_DEVICE void dkv_body(char* __restrict__ smem, int bx, int bh, const float* __restrict__ qkv,
                         const int64_t* __restrict__ mask, const float* __restrict__ bqkv,
                         const float* __restrict__ dctx, const float* __restrict__ lse, const float* __restrict__ Dd,
@@ -398,18 +399,28 @@ HS_DEVICE void dkv_body(char* __restrict__ smem, int bx, int bh, const float* __
 #pragma unroll 1
     for (int t = 0; t < clen; t += 32) {
       f32x16 sc = {}, dp = {};
+      if constexpr (OCC == 1) {  // (the register room of one workgroup per CU: the two chains interleave)
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const hx8 a[2] = {prow(Qp, 0, t + li, 2 * ks + hf), prow(Qp, 1, t + li, 2 * ks + hf)};
-        sc = mma3(a, kb[ks], sc);
-      }
-      __builtin_amdgcn_sched_barrier(0);  // bound the live fragments (no spills at 256 VGPRs)
+        for (int ks = 0; ks < 4; ++ks) {
+          const hx8 a[2] = {prow(Qp, 0, t + li, 2 * ks + hf), prow(Qp, 1, t + li, 2 * ks + hf)};
+          const hx8 o[2] = {prow(Op, 0, t + li, 2 * ks + hf), prow(Op, 1, t + li, 2 * ks + hf)};
+          sc = mma3(a, kb[ks], sc);
+          dp = mma3(o, vb[ks], dp);
+        }
+      } else {
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const hx8 a[2] = {prow(Op, 0, t + li, 2 * ks + hf), prow(Op, 1, t + li, 2 * ks + hf)};
-        dp = mma3(a, vb[ks], dp);
+        for (int ks = 0; ks < 4; ++ks) {
+          const hx8 a[2] = {prow(Qp, 0, t + li, 2 * ks + hf), prow(Qp, 1, t + li, 2 * ks + hf)};
+          sc = mma3(a, kb[ks], sc);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // bound the live fragments (no spills at 256 VGPRs)
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          const hx8 a[2] = {prow(Op, 0, t + li, 2 * ks + hf), prow(Op, 1, t + li, 2 * ks + hf)};
+          dp = mma3(a, vb[ks], dp);
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
-      __builtin_amdgcn_sched_barrier(0);
       // P in place of the scores; dV^T first, so the P-with-dropout copies die before dS exists
       // (the four accumulators and the lane's K / V fragments leave little register room)
 #pragma unroll
@@ -587,7 +598,8 @@ HS_DEVICE void dq_body(char* __restrict__ smem, int bx, int bh, const float* __r
 // The backward's two roles in one launch (grid (B*NH, 2 * ceil(S/128)); dK / dV blocks first: the longer
 // role goes out first and the dQ blocks fill the tail of the last round).  ctx != nullptr: D computed by
 // the roles themselves (S <= 128).
-__global__ void __launch_bounds__(256, 2)
+template <int OCC>
+__global__ void __launch_bounds__(256, OCC)
     attn_bwd_h3_kernel(const float* __restrict__ qkv, const int64_t* __restrict__ mask,
                        const float* __restrict__ bqkv, const float* __restrict__ dctx, const float* __restrict__ lse,
                        const float* __restrict__ Dd, float* __restrict__ dqkv, int S, int NH, float p,
@@ -596,14 +608,17 @@ __global__ void __launch_bounds__(256, 2)
   __shared__ __attribute__((aligned(16))) char smem[kBwdLds];
   const int nq = (S + 127) / 128, bh = blockIdx.x, y = blockIdx.y;
   if (y < nq)
-    dkv_body(smem, y, bh, qkv, mask, bqkv, dctx, lse, Dd, dqkv, S, NH, p, dmask, ctx, amax, po);
+    dkv_body<OCC>(smem, y, bh, qkv, mask, bqkv, dctx, lse, Dd, dqkv, S, NH, p, dmask, ctx, amax, po);
   else
     dq_body(smem, y - nq, bh, qkv, mask, bqkv, dctx, lse, Dd, dqkv, S, NH, p, dmask, ctx, amax, po);
 }
 
 // Forward: a wave owns 32 queries (lane = query), S^T tiles with the key on the registers, online softmax;
-// each 64-key chunk of K and V is split once into plane images with the chunk's exponents.
-__global__ void __launch_bounds__(256, 2)
+// each 64-key chunk of K and V is split once into plane images with the chunk's exponents.  PAIR: a whole
+// 64-key chunk's two score tiles at once (one workgroup per CU: its registers spill at two); else one
+// 32-key tile at a time at two workgroups per CU (round 5).
+template <bool PAIR>
+__global__ void __launch_bounds__(256, PAIR ? 1 : 2)
     attn_fwd_h3_kernel(const float* __restrict__ qkv, const int64_t* __restrict__ mask,
                        const float* __restrict__ bqkv, float* __restrict__ ctx, float* __restrict__ lse,
                        uint32_t* __restrict__ dmask, int S, int NH, float p, uint64_t seed, uint64_t off,
@@ -659,6 +674,68 @@ __global__ void __launch_bounds__(256, 2)
     }
     ev_run = ev;
     const float us = ldexpf(1.f, -(ek + eq));
+    if (PAIR && clen == 64) {
+      // the chunk's two 32-key tiles together: two independent score accumulators (the 12-MFMA chains
+      // interleave instead of running back to back), one softmax update and one rescale of the output
+      // accumulators per chunk.  Same keep-bit stream and words as the per-tile path below.
+      f32x16 s0 = {}, s1 = {};
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const hx8 ka[2] = {prow(Kimg, 0, li, 2 * ks + hf), prow(Kimg, 1, li, 2 * ks + hf)};
+        const hx8 kb[2] = {prow(Kimg, 0, 32 + li, 2 * ks + hf), prow(Kimg, 1, 32 + li, 2 * ks + hf)};
+        s0 = mma3(ka, qf[ks], s0);
+        s1 = mma3(kb, qf[ks], s1);
+      }
+      float mt = -1e30f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        s0[r] = s0[r] * us + Ms[xrow(r, hf)];
+        s1[r] = s1[r] * us + Ms[32 + xrow(r, hf)];
+        mt = fmaxf(mt, fmaxf(s0[r], s1[r]));
+      }
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      const float mn = fmaxf(m, mt);
+      const float alpha = __expf(m - mn);
+      m = mn;
+      float ps = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {  // the scores' registers become P
+        s0[r] = __expf(s0[r] - mn);
+        s1[r] = __expf(s1[r] - mn);
+        ps += s0[r] + s1[r];
+      }
+      ps += __shfl_xor(ps, 32, 64);
+      l = l * alpha + ps;
+      o0 *= alpha;
+      o1 *= alpha;
+      auto pv_tile = [&](f32x16& pr, const int tt) __attribute__((always_inline)) {
+        if (p > 0.f) {
+          const uint64_t e0 = (erow + c0 + 32 * tt) >> 3;
+          const uint32_t mine =
+              keep8_bits(seed, off, e0 + 2 * hf, thr) | (keep8_bits(seed, off, e0 + 2 * hf + 1, thr) << 8);
+          const uint32_t other = static_cast<uint32_t>(__shfl_xor(static_cast<int>(mine), 32, 64));
+          const uint32_t bits = hf == 0 ? (mine | (other << 16)) : (other | (mine << 16));
+#pragma unroll
+          for (int r = 0; r < 16; ++r) pr[r] = ((bits >> xrow(r, hf)) & 1u) ? pr[r] * dscale : 0.f;
+          if (dmask && hf == 0) dmask[((uint64_t)bh * S + q0 + li) * (uint64_t)(S >> 5) + ((c0 + 32 * tt) >> 5)] = bits;
+        }
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          float pv[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) pv[j] = pr[8 * ks + j];
+          hx8 pf[2], a[2];
+          split8h(pv, sp, pf[0], pf[1]);
+          ptr2(Vimg, 32 * tt + 16 * ks, tb, 0, a);
+          o0 = mma3(a, pf, o0);
+          ptr2(Vimg, 32 * tt + 16 * ks, tb, 1, a);
+          o1 = mma3(a, pf, o1);
+        }
+      };
+      pv_tile(s0, 0);
+      pv_tile(s1, 1);
+      continue;
+    }
 #pragma unroll 1
     for (int t = 0; t < clen; t += 32) {
       f32x16 s = {};
@@ -726,6 +803,14 @@ __global__ void __launch_bounds__(256, 2)
 
 using namespace hs;
 
+// A/B hooks (set_attn_h3_variant): the forward's paired-tile kernel (1) or the per-tile one (0); the
+// backward at one workgroup per CU (1: no spills) or two (2: 176 B of scratch)
+static int g_attn_fwd_pair = 1, g_attn_bwd_occ = 2;
+void set_attn_h3_variant(int fwd_pair, int bwd_occ) {
+  g_attn_fwd_pair = fwd_pair;
+  g_attn_bwd_occ = bwd_occ;
+}
+
 // amax (optional): a |max| slot (common.h) the kernels max |output| into (ctx forward, dqkv backward)
 int launch_attn_fwd_h3(const float* qkv, const int64_t* mask, const float* bqkv, float* ctx, float* lse,
                        uint32_t* dmask, int B, int S, int NH, int D, float p, uint64_t seed, uint64_t off,
@@ -734,8 +819,12 @@ int launch_attn_fwd_h3(const float* qkv, const int64_t* mask, const float* bqkv,
   const AttnPl po{static_cast<uint16_t*>(pl), ps, ex};
   // grid (B*NH, S/128): consecutive blocks are different heads, so every query block of a head lands on
   // the same XCD and its K / V come through one L2
-  hipLaunchKernelGGL(attn_fwd_h3_kernel, dim3(B * NH, (S + 127) / 128), dim3(256), 0, st, qkv, mask, bqkv, ctx, lse,
-                     dmask, S, NH, p, seed, off, g_seed_dev, bh0, amax, po);
+  if (g_attn_fwd_pair)
+    hipLaunchKernelGGL(attn_fwd_h3_kernel<true>, dim3(B * NH, (S + 127) / 128), dim3(256), 0, st, qkv, mask, bqkv, ctx,
+                       lse, dmask, S, NH, p, seed, off, g_seed_dev, bh0, amax, po);
+  else
+    hipLaunchKernelGGL(attn_fwd_h3_kernel<false>, dim3(B * NH, (S + 127) / 128), dim3(256), 0, st, qkv, mask, bqkv,
+                       ctx, lse, dmask, S, NH, p, seed, off, g_seed_dev, bh0, amax, po);
   return 0;
 }
 
@@ -751,7 +840,11 @@ int launch_attn_bwd_h3(const float* qkv, const int64_t* mask, const float* bqkv,
     launch_attn_bwd_dsum(ctx, dctx, Dbuf, B, S, NH, st);
   }
   const dim3 grid(B * NH, 2 * ((S + 127) / 128));
-  hipLaunchKernelGGL(attn_bwd_h3_kernel, grid, dim3(256), 0, st, qkv, mask, bqkv, dctx, lse, Dbuf, dqkv, S, NH, p,
-                     dmask, fused_d ? ctx : nullptr, amax, po);
+  if (g_attn_bwd_occ == 1)
+    hipLaunchKernelGGL(attn_bwd_h3_kernel<1>, grid, dim3(256), 0, st, qkv, mask, bqkv, dctx, lse, Dbuf, dqkv, S, NH, p,
+                       dmask, fused_d ? ctx : nullptr, amax, po);
+  else
+    hipLaunchKernelGGL(attn_bwd_h3_kernel<2>, grid, dim3(256), 0, st, qkv, mask, bqkv, dctx, lse, Dbuf, dqkv, S, NH, p,
+                       dmask, fused_d ? ctx : nullptr, amax, po);
   return 0;
 }

@@ -133,6 +133,12 @@ HS_DEVICE void keep4(uint64_t seed, uint64_t offset, uint64_t q, float p, float 
 // so launchers pass g_seed_dev -- a device word the host refreshes before every
 // replay -- and kernels read it instead.  Set through the `set_seed_ptr` binding.
 extern const uint64_t* g_seed_dev;
+
+// Diagnostic ablation (set_skip_launches; bench.py --ab skip_*): launches of the classes whose bit is
+// set return without launching -- kSkipSplitK the split-K finishing passes, kSkipReduceRows the
+// column-partial reductions.  Results are then meaningless; every buffer and address stays the same.
+enum : int { kSkipSplitK = 1, kSkipReduceRows = 2 };
+extern int g_hs_skip;
 HS_DEVICE uint64_t resolve_seed(uint64_t seed, const uint64_t* seed_dev) { return seed_dev ? *seed_dev : seed; }
 
 // 16-bit dropout decisions: one Philox call -> 8 keep bits (bit e: element e of the

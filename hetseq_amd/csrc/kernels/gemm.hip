@@ -974,6 +974,7 @@ using namespace hs;
 static void launch_splitk_reduce_cols(const float* slab, int ksplit, int M, int N, float* C, int64_t ldc,
                                       const float* bias, float beta, int Mv, int Nv, hipStream_t st, const float* part,
                                       float* colsum_out, int colsum_acc) {
+  if (g_hs_skip & kSkipSplitK) return;
   const int64_t n4 = (int64_t)Mv * (N / 4);
   const int grid = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
   const int gcol = colsum_out ? (M + 255) / 256 : 0;

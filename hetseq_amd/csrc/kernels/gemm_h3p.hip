@@ -289,7 +289,11 @@ HS_DEVICE qh8 r_frag(const char* img, int p, int rc, int lane) {
   }
 }
 
-template <bool TA, bool TB, int EPI>
+// LEAD: steps between a stage's DMA and its use.  3 (round 5): step s refills the stage of step s - 1;
+// 4: step s refills its OWN stage -- free once the barrier opening step s has passed (every wave read
+// step s's fragments into registers during step s - 1) -- so three steps stay in flight in the same
+// four stages.
+template <bool TA, bool TB, int EPI, int LEAD>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) gemm_h3p_kernel(QArgs p) {
   constexpr bool AK = !TA, BKc = TB;
   __shared__ __attribute__((aligned(1024))) char smem[RSMEM];
@@ -366,20 +370,26 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
       const qh8 a = term == 0 ? f.a[1][i] : f.a[0][i];
       const qh8 b = term == 1 ? f.b[1][j] : f.b[0][j];
       tmp[i][j] = q_mma(a, b, (first && term == 0) ? qf16{} : tmp[i][j]);
-      if (c < 4) dma(c, s + 3, st_free);
+      if (c < 4) dma(c, s + LEAD, st_free);
       else if (read_next) read_piece(nf, st_next, c - 4);
       __builtin_amdgcn_sched_barrier(0);
     }
   };
 
-  // prologue: three steps in flight, wait for the first
+  // prologue: LEAD steps in flight, wait for the first
 #pragma unroll
   for (int j = 0; j < 4; ++j) dma(j, 0, 0);
 #pragma unroll
   for (int j = 0; j < 4; ++j) dma(j, 1, 1);
 #pragma unroll
   for (int j = 0; j < 4; ++j) dma(j, 2, 2);
-  r_wait_vm<8>();
+  if constexpr (LEAD == 4) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dma(j, 3, 3);
+    r_wait_vm<12>();
+  } else {
+    r_wait_vm<8>();
+  }
   __syncthreads();  // step 0 and the factor tables visible to every wave
   Frags F[2];
 #pragma unroll
@@ -387,15 +397,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   // K tile t = steps 2t (F[0], stage 2t % 4) and 2t+1 (F[1]); stage of step s is s % 4
   for (int t = 0; t < KT; ++t) {
     const int s0 = 2 * t, st0 = s0 & 3;
-    r_wait_vm<4>();  // step s0+1 landed (this wave's pieces); s0+2 in flight
+    r_wait_vm<4 * (LEAD - 2)>();  // step s0+1 landed (this wave's pieces); the later ones in flight
     r_barrier();
-    body(F[0], F[1], s0, (st0 + 3) & 3, (st0 + 1) & 3, true, true);
-    r_wait_vm<4>();
+    body(F[0], F[1], s0, (st0 + LEAD) & 3, (st0 + 1) & 3, true, true);
+    r_wait_vm<4 * (LEAD - 2)>();
     r_barrier();
     const float2 fa = *reinterpret_cast<const float2*>(fA + 4 * t + 2 * wr);
     const float2 fb = *reinterpret_cast<const float2*>(fB + 4 * t + 2 * wc);
     // (the last tile's reads of "step s0+2" fetch a stage holding a duplicate DMA: harmless, unused)
-    body(F[1], F[0], s0 + 1, st0, (st0 + 2) & 3, false, true);
+    body(F[1], F[0], s0 + 1, (st0 + 1 + LEAD) & 3, (st0 + 2) & 3, false, true);
     const float fac[2][2] = {{fa.x * fb.x, fa.x * fb.y}, {fa.y * fb.x, fa.y * fb.y}};
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -483,9 +493,15 @@ __global__ void __launch_bounds__(256) h3p_split_kernel(QSplitSeg one, const QSp
   if (lane == 0) s.ex[(int64_t)br * s.lde + bc] = static_cast<int8_t>(e);
 }
 
+static int g_h3p_lead = 4;  // A/B hook (set_h3p_lead): 3 = round 5's ring
+
 template <bool TA, bool TB, int EPI>
 void q_launch(const QArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL((gemm_h3p_kernel<TA, TB, EPI>), dim3((a.M / QT) * (a.N / QT) * a.ksplit), dim3(256), 0, st, a);
+  const dim3 grid((a.M / QT) * (a.N / QT) * a.ksplit);
+  if (g_h3p_lead == 3)
+    hipLaunchKernelGGL((gemm_h3p_kernel<TA, TB, EPI, 3>), grid, dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((gemm_h3p_kernel<TA, TB, EPI, 4>), grid, dim3(256), 0, st, a);
 }
 
 template <bool TA, bool TB>
@@ -562,6 +578,8 @@ int launch_gemm_h3p(int ta, int tb, int M, int N, int K, const void* A, int64_t 
                            aux, ldaux, part, colsum, colsum_acc, cp, ldcp, cp_ps, ec, lde_c, ksplit, slab, slab_floats,
                            ablk, bblk, 0, 0, st);
 }
+
+void set_h3p_lead(int lead) { g_h3p_lead = lead == 3 ? 3 : 4; }
 
 int launch_h3p_colpart(const void* pl, int64_t ld, int64_t ps, const int8_t* ex, int64_t lde, int rows, int cols,
                        float* part, hipStream_t st) {

@@ -102,6 +102,7 @@ __global__ void __launch_bounds__(256) reduce_rows4_kernel(ReduceArgs args, int 
 
 inline void launch_reduce_rows(const float* const* parts, float* const* outs, int n, int nparts, int N,
                                int accumulate, hipStream_t st) {
+  if (g_hs_skip & kSkipReduceRows) return;
   ReduceArgs a{};
   for (int i = 0; i < n; ++i) {
     a.part[i] = parts[i];

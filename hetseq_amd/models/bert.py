@@ -872,6 +872,11 @@ class BertModel(BertPreTrainedModel):
         return x, self.pooler.dense_act(x.view(B, S, -1)[:, 0])
 
 
+# the masked-LM head's products on the h3p engine (BertForPreTraining._head_h3p); False: the per-tensor
+# h3 engine (A/B: bench.py --ab head_h3p,head_h3)
+HEAD_H3P = True
+
+
 def _xent(logits, target, ignore_index=-100):
     """Cross-entropy in fp32 whatever the compute dtype."""
     return F.cross_entropy(logits.float(), target, ignore_index=ignore_index)
@@ -952,7 +957,8 @@ class BertForPreTraining(BertPreTrainedModel):
         wt = self.cls.predictions.transform.dense_act.weight
         wd = self.cls.predictions.decoder.weight
         H, V = wt.shape[0], wd.shape[0]
-        if not (G.h3p_active(self.compute_dtype) and wt.is_cuda and H % 128 == 0 and wt.dtype == torch.float32):
+        if not (HEAD_H3P and G.h3p_active(self.compute_dtype) and wt.is_cuda and H % 128 == 0
+                and wt.dtype == torch.float32):
             return None
         store = getattr(self, "_hs_store", None)
         cached = self.__dict__.get("_hs_head_h3p")

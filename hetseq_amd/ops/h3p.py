@@ -194,13 +194,30 @@ def window_stats(hp):
     return int(nz.sum()), int(out.sum()), float(ax[out].sum()), float(ax.sum())
 
 
+def window_stats_tensor(hp):
+    """window_stats of the SAME values under ONE exponent for the whole tensor (the per-tensor scale of
+    the h3 engine): the per-block window can only keep more bits (each block's exponent is >= the
+    tensor's), so its counts must be <= these on every tensor -- the census checks it."""
+    import math
+
+    x = hp.unsplit().double()
+    ax = x.abs()
+    m = float(ax.max()) if x.numel() else 0.0
+    nz = x != 0
+    if not m > 0.0:
+        return int(nz.sum()), 0, 0.0, float(ax.sum())
+    e = 14 - math.floor(math.log2(m))
+    out = nz & (ax * 2.0 ** e < 0.125)
+    return int(nz.sum()), int(out.sum()), float(ax[out].sum()), float(ax.sum())
+
+
 def _census(site, a, b):
     for role, hp in (("A", a), ("B", b)):
-        st = window_stats(hp)
-        c = CENSUS.setdefault((site, role), [0, 0, 0.0, 0.0, 0])
-        for i in range(4):
-            c[i] += st[i]
-        c[4] += 1
+        for kind, st in (("", window_stats(hp)), ("/tensor", window_stats_tensor(hp))):
+            c = CENSUS.setdefault((site, role + kind), [0, 0, 0.0, 0.0, 0])
+            for i in range(4):
+                c[i] += st[i]
+            c[4] += 1
 
 
 def gemm(a, b, ta=False, tb=False, out=None, bias=None, epi=EPI_NONE, beta=0.0, aux=None, part=None, colsum=None,

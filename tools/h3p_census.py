@@ -28,8 +28,14 @@ def main():
     from argparse import Namespace
 
     from hetseq_amd.models.bert import BertConfig, BertForPreTraining
+    from hetseq_amd.ops import bert_ops
     from hetseq_amd.ops import gemm as G
     from hetseq_amd.ops import h3p
+
+    # the Python layer (the same kernels and arguments as the native layer program, which is bitwise
+    # equal to it: tests/test_layer_prog_gpu.py) -- its products pass through h3p.gemm, where the
+    # census records them
+    bert_ops.LAYER_PROG = False
     from hetseq_amd.optim.optimizers import _Adam
     from hetseq_amd.runtime import rng
     from hetseq_amd.runtime.flat import FlatParamStore
@@ -93,6 +99,16 @@ def main():
         nz, out, mo, mt, n = totals[key]
         lines.append("| %s | %s | %s | %d | %.3g | %.3g |" % (key[0], " ".join(str(x) for x in key[1:-1]), key[-1], n,
                                                                out / max(nz, 1), mo / max(mt, 1e-300)))
+    # the same h3p tensors under one exponent per tensor ("A/tensor", "B/tensor" rows): per site, the
+    # per-block count must not exceed the per-tensor one (a producer writing wrong exponents would)
+    viol = []
+    for key in totals:
+        if key[0] == "h3p" and not str(key[-1]).endswith("/tensor"):
+            tk = key[:-1] + (key[-1] + "/tensor",)
+            if tk in totals and totals[key][1] > totals[tk][1]:
+                viol.append(" ".join(str(x) for x in key[1:]))
+    lines += ["", "Same-tensor check (h3p operands, per-block vs per-tensor window on identical values): %s"
+              % ("per-block <= per-tensor at every site" if not viol else "VIOLATED at: " + "; ".join(viol))]
     text = "\n".join(lines) + "\n"
     print(text)
     if a.out:
