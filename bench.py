@@ -616,11 +616,9 @@ _AB = {
     "skip_splitk": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_skip_launches(1),
     "skip_reduce": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_skip_launches(2),
     "skip_both": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_skip_launches(3),
-    "lead3": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_h3p_lead(3),
-    "lead4": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_h3p_lead(4),
+    "attf_auto": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_h3_variant(-1, 2),
     "attf_pair": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_h3_variant(1, 2),
     "attf_tile": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_h3_variant(0, 2),
-    "attb_occ1": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_h3_variant(1, 1),
     "head_h3p": lambda: setattr(__import__("hetseq_amd.models.bert", fromlist=["x"]), "HEAD_H3P", True),
     "head_h3": lambda: setattr(__import__("hetseq_amd.models.bert", fromlist=["x"]), "HEAD_H3P", False),
     "lnw0": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_ln_h3p_waves(0),

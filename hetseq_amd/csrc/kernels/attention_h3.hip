@@ -301,7 +301,6 @@ HS_DEVICE float ds_scale(const float (&ds)[2][8], int& es, f32x16& a0, f32x16& a
 // dK / dV for 32 keys per wave (lane = key) over 64-query chunks of Q (biased, * 1/8) and dO.
 constexpr int kBwdLds = 2 * kIm + 64 * 4 * 2 + 64 * 4 * 4 + 2 * 8 * 4;
 
-template <int OCC>
 HS_DEVICE void dkv_body(char* __restrict__ smem, int bx, int bh, const float* __restrict__ qkv,
                         const int64_t* __restrict__ mask, const float* __restrict__ bqkv,
                         const float* __restrict__ dctx, const float* __restrict__ lse, const float* __restrict__ Dd,
@@ -399,28 +398,18 @@ HS_DEVICE void dkv_body(char* __restrict__ smem, int bx, int bh, const float* __
 #pragma unroll 1
     for (int t = 0; t < clen; t += 32) {
       f32x16 sc = {}, dp = {};
-      if constexpr (OCC == 1) {  // (the register room of one workgroup per CU: the two chains interleave)
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-          const hx8 a[2] = {prow(Qp, 0, t + li, 2 * ks + hf), prow(Qp, 1, t + li, 2 * ks + hf)};
-          const hx8 o[2] = {prow(Op, 0, t + li, 2 * ks + hf), prow(Op, 1, t + li, 2 * ks + hf)};
-          sc = mma3(a, kb[ks], sc);
-          dp = mma3(o, vb[ks], dp);
-        }
-      } else {
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-          const hx8 a[2] = {prow(Qp, 0, t + li, 2 * ks + hf), prow(Qp, 1, t + li, 2 * ks + hf)};
-          sc = mma3(a, kb[ks], sc);
-        }
-        __builtin_amdgcn_sched_barrier(0);  // bound the live fragments (no spills at 256 VGPRs)
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-          const hx8 a[2] = {prow(Op, 0, t + li, 2 * ks + hf), prow(Op, 1, t + li, 2 * ks + hf)};
-          dp = mma3(a, vb[ks], dp);
-        }
-        __builtin_amdgcn_sched_barrier(0);
+      for (int ks = 0; ks < 4; ++ks) {
+        const hx8 a[2] = {prow(Qp, 0, t + li, 2 * ks + hf), prow(Qp, 1, t + li, 2 * ks + hf)};
+        sc = mma3(a, kb[ks], sc);
       }
+      __builtin_amdgcn_sched_barrier(0);  // bound the live fragments (no spills at 256 VGPRs)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const hx8 a[2] = {prow(Op, 0, t + li, 2 * ks + hf), prow(Op, 1, t + li, 2 * ks + hf)};
+        dp = mma3(a, vb[ks], dp);
+      }
+      __builtin_amdgcn_sched_barrier(0);
       // P in place of the scores; dV^T first, so the P-with-dropout copies die before dS exists
       // (the four accumulators and the lane's K / V fragments leave little register room)
 #pragma unroll
@@ -598,8 +587,7 @@ HS_DEVICE void dq_body(char* __restrict__ smem, int bx, int bh, const float* __r
 // The backward's two roles in one launch (grid (B*NH, 2 * ceil(S/128)); dK / dV blocks first: the longer
 // role goes out first and the dQ blocks fill the tail of the last round).  ctx != nullptr: D computed by
 // the roles themselves (S <= 128).
-template <int OCC>
-__global__ void __launch_bounds__(256, OCC)
+__global__ void __launch_bounds__(256, 2)
     attn_bwd_h3_kernel(const float* __restrict__ qkv, const int64_t* __restrict__ mask,
                        const float* __restrict__ bqkv, const float* __restrict__ dctx, const float* __restrict__ lse,
                        const float* __restrict__ Dd, float* __restrict__ dqkv, int S, int NH, float p,
@@ -608,7 +596,7 @@ __global__ void __launch_bounds__(256, OCC)
   __shared__ __attribute__((aligned(16))) char smem[kBwdLds];
   const int nq = (S + 127) / 128, bh = blockIdx.x, y = blockIdx.y;
   if (y < nq)
-    dkv_body<OCC>(smem, y, bh, qkv, mask, bqkv, dctx, lse, Dd, dqkv, S, NH, p, dmask, ctx, amax, po);
+    dkv_body(smem, y, bh, qkv, mask, bqkv, dctx, lse, Dd, dqkv, S, NH, p, dmask, ctx, amax, po);
   else
     dq_body(smem, y - nq, bh, qkv, mask, bqkv, dctx, lse, Dd, dqkv, S, NH, p, dmask, ctx, amax, po);
 }
@@ -803,13 +791,14 @@ __global__ void __launch_bounds__(256, PAIR ? 1 : 2)
 
 using namespace hs;
 
-// A/B hooks (set_attn_h3_variant): the forward's paired-tile kernel (1) or the per-tile one (0); the
-// backward at one workgroup per CU (1: no spills) or two (2: 176 B of scratch)
-static int g_attn_fwd_pair = 1, g_attn_bwd_occ = 2;
-void set_attn_h3_variant(int fwd_pair, int bwd_occ) {
-  g_attn_fwd_pair = fwd_pair;
-  g_attn_bwd_occ = bwd_occ;
-}
+// The forward kernel per sequence length: the paired-tile one (one workgroup per CU) from S = 256 on,
+// the per-tile one (two per CU) below -- measured in the step (bench.py --ab, round 6): phase 2
+// (S 512) 11.98 vs 12.27 ms paired / per tile, phase 1 (S 128) 10.80 vs 10.68 ms.  The backward at
+// one workgroup per CU (no spills, the score and dP chains interleaved) measured slower than at two
+// (176 B of scratch) in both phases (10.98 vs 10.68 ms; 12.75 vs 12.27 ms) and was removed.
+// set_attn_h3_variant: -1 = that choice, 0 / 1 = always per tile / paired (tests, A/B).
+static int g_attn_fwd_pair = -1;
+void set_attn_h3_variant(int fwd_pair, int) { g_attn_fwd_pair = fwd_pair; }
 
 // amax (optional): a |max| slot (common.h) the kernels max |output| into (ctx forward, dqkv backward)
 int launch_attn_fwd_h3(const float* qkv, const int64_t* mask, const float* bqkv, float* ctx, float* lse,
@@ -819,7 +808,7 @@ int launch_attn_fwd_h3(const float* qkv, const int64_t* mask, const float* bqkv,
   const AttnPl po{static_cast<uint16_t*>(pl), ps, ex};
   // grid (B*NH, S/128): consecutive blocks are different heads, so every query block of a head lands on
   // the same XCD and its K / V come through one L2
-  if (g_attn_fwd_pair)
+  if (g_attn_fwd_pair > 0 || (g_attn_fwd_pair < 0 && S >= 256))
     hipLaunchKernelGGL(attn_fwd_h3_kernel<true>, dim3(B * NH, (S + 127) / 128), dim3(256), 0, st, qkv, mask, bqkv, ctx,
                        lse, dmask, S, NH, p, seed, off, g_seed_dev, bh0, amax, po);
   else
@@ -840,11 +829,7 @@ int launch_attn_bwd_h3(const float* qkv, const int64_t* mask, const float* bqkv,
     launch_attn_bwd_dsum(ctx, dctx, Dbuf, B, S, NH, st);
   }
   const dim3 grid(B * NH, 2 * ((S + 127) / 128));
-  if (g_attn_bwd_occ == 1)
-    hipLaunchKernelGGL(attn_bwd_h3_kernel<1>, grid, dim3(256), 0, st, qkv, mask, bqkv, dctx, lse, Dbuf, dqkv, S, NH, p,
-                       dmask, fused_d ? ctx : nullptr, amax, po);
-  else
-    hipLaunchKernelGGL(attn_bwd_h3_kernel<2>, grid, dim3(256), 0, st, qkv, mask, bqkv, dctx, lse, Dbuf, dqkv, S, NH, p,
-                       dmask, fused_d ? ctx : nullptr, amax, po);
+  hipLaunchKernelGGL(attn_bwd_h3_kernel, grid, dim3(256), 0, st, qkv, mask, bqkv, dctx, lse, Dbuf, dqkv, S, NH, p, dmask,
+                     fused_d ? ctx : nullptr, amax, po);
   return 0;
 }

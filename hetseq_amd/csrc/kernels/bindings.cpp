@@ -56,7 +56,6 @@ int launch_ln_bwd_h3p(const float*, const float*, const float*, const float*, co
 int ln_bwd_h3p_part_rows(int coop);
 void set_ln_bwd_coop(int on);
 void set_attn_h3_variant(int fwd_pair, int bwd_occ);
-void set_h3p_lead(int lead);
 int launch_attn_fwd_h3(const float*, const int64_t*, const float*, float*, float*, uint32_t*, int, int, int, int, float,
                        uint64_t, uint64_t, hipStream_t, int, float*, void*, int64_t, int8_t*);
 int launch_attn_bwd_h3(const float*, const int64_t*, const float*, const float*, const float*, const float*, float*,
@@ -514,8 +513,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("ln_bwd_h3p_part_rows", &ln_bwd_h3p_part_rows, "rows per column-partial row of ln_bwd_h3p (coop: psync given)");
   m.def("set_ln_bwd_coop", &set_ln_bwd_coop, "h3p LayerNorm backward: 1 / 2 panel exchange (8 / 4 rows per workgroup), 0 32-row blocks");
   m.def("set_attn_h3_variant", &set_attn_h3_variant,
-        "h3 attention kernels: forward paired 64-key tiles (1) or per tile (0); backward workgroups per CU (1 or 2)");
-  m.def("set_h3p_lead", &set_h3p_lead, "h3p GEMM: steps between a stage's LDS-DMA and its use (3 or 4)");
+        "h3 attention forward: -1 by sequence length (paired 64-key tiles from S = 256), 1 paired, 0 per tile");
   m.def("panel_sync_words", []() { return 256; }, "uint32 words of one 32-row panel record (h3p.h kPanelSyncWords)");
   m.def("ln_fwd_h3p", [](i64 a, i64 bias, i64 resid, i64 gamma, i64 beta, i64 y, i64 z, i64 mean, i64 rstd, int rows,
                          int H, float eps, float p, u64 seed, u64 off, int mode, int nslab, i64 slab_stride, int row0,

@@ -289,12 +289,18 @@ HS_DEVICE qh8 r_frag(const char* img, int p, int rc, int lane) {
   }
 }
 
-// LEAD: steps between a stage's DMA and its use.  3 (round 5): step s refills the stage of step s - 1;
-// 4: step s refills its OWN stage -- free once the barrier opening step s has passed (every wave read
-// step s's fragments into registers during step s - 1) -- so three steps stay in flight in the same
-// four stages.
-template <bool TA, bool TB, int EPI, int LEAD>
+// The DMA lead is four steps: step s refills its OWN stage -- free once the barrier opening step s has
+// passed (every wave read step s's fragments into registers during step s - 1) -- so three steps stay
+// in flight in the four stages (round 5 refilled the stage of step s - 1: two in flight; the step
+// measured the same: 10.79 vs 10.80 ms, bench.py --ab, round 6).
+// Issue order inside a step: the eight fragment reads of step s + 1 between the step's first eight
+// MFMAs, the four DMA pieces after the last four, so the reads complete under the step's last MFMAs
+// instead of in front of the closing lgkmcnt(0) + barrier (round 5 issued the DMA first: the layer's
+// twelve products 643.6 -> 634.1 us alone, the step 10.81 -> 10.73 ms, tools/bench_h3p.py and
+// bench.py --ab, round 6).
+template <bool TA, bool TB, int EPI>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) gemm_h3p_kernel(QArgs p) {
+  constexpr int LEAD = 4;
   constexpr bool AK = !TA, BKc = TB;
   __shared__ __attribute__((aligned(1024))) char smem[RSMEM];
   float* const fA = reinterpret_cast<float*>(smem + RNS * RSTAGE);
@@ -370,8 +376,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
       const qh8 a = term == 0 ? f.a[1][i] : f.a[0][i];
       const qh8 b = term == 1 ? f.b[1][j] : f.b[0][j];
       tmp[i][j] = q_mma(a, b, (first && term == 0) ? qf16{} : tmp[i][j]);
-      if (c < 4) dma(c, s + LEAD, st_free);
-      else if (read_next) read_piece(nf, st_next, c - 4);
+      if (c < 8) {
+        if (read_next) read_piece(nf, st_next, c);
+      } else {
+        dma(c - 8, s + LEAD, st_free);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -383,13 +392,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   for (int j = 0; j < 4; ++j) dma(j, 1, 1);
 #pragma unroll
   for (int j = 0; j < 4; ++j) dma(j, 2, 2);
-  if constexpr (LEAD == 4) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) dma(j, 3, 3);
-    r_wait_vm<12>();
-  } else {
-    r_wait_vm<8>();
-  }
+  for (int j = 0; j < 4; ++j) dma(j, 3, 3);
+  r_wait_vm<12>();
   __syncthreads();  // step 0 and the factor tables visible to every wave
   Frags F[2];
 #pragma unroll
@@ -493,15 +498,9 @@ __global__ void __launch_bounds__(256) h3p_split_kernel(QSplitSeg one, const QSp
   if (lane == 0) s.ex[(int64_t)br * s.lde + bc] = static_cast<int8_t>(e);
 }
 
-static int g_h3p_lead = 4;  // A/B hook (set_h3p_lead): 3 = round 5's ring
-
 template <bool TA, bool TB, int EPI>
 void q_launch(const QArgs& a, hipStream_t st) {
-  const dim3 grid((a.M / QT) * (a.N / QT) * a.ksplit);
-  if (g_h3p_lead == 3)
-    hipLaunchKernelGGL((gemm_h3p_kernel<TA, TB, EPI, 3>), grid, dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL((gemm_h3p_kernel<TA, TB, EPI, 4>), grid, dim3(256), 0, st, a);
+  hipLaunchKernelGGL((gemm_h3p_kernel<TA, TB, EPI>), dim3((a.M / QT) * (a.N / QT) * a.ksplit), dim3(256), 0, st, a);
 }
 
 template <bool TA, bool TB>
@@ -578,8 +577,6 @@ int launch_gemm_h3p(int ta, int tb, int M, int N, int K, const void* A, int64_t 
                            aux, ldaux, part, colsum, colsum_acc, cp, ldcp, cp_ps, ec, lde_c, ksplit, slab, slab_floats,
                            ablk, bblk, 0, 0, st);
 }
-
-void set_h3p_lead(int lead) { g_h3p_lead = lead == 3 ? 3 : 4; }
 
 int launch_h3p_colpart(const void* pl, int64_t ld, int64_t ps, const int8_t* ex, int64_t lde, int rows, int cols,
                        float* part, hipStream_t st) {

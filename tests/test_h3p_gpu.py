@@ -83,17 +83,10 @@ def test_gemm_h3p_layouts_bitwise(cuda, ta, tb, M, N, K, ks):
     a = torch.randn((K, M) if ta else (M, K), device=cuda, generator=g)
     b = torch.randn((N, K) if tb else (K, N), device=cuda, generator=g)
     ref = h3p.gemm(h3p.split(a), h3p.split(b), ta, tb, ksplit=ks)
-    from hetseq_amd.ops._C import hip
-
-    try:
-        for lead in (4, 3):  # the DMA ring's lead (gemm_h3p.hip LEAD): same values, same sums
-            hip().set_h3p_lead(lead)
-            for ab in (False, True):
-                for bb in (False, True):
-                    out = h3p.gemm(h3p.split(a, blk=ab), h3p.split(b, blk=bb), ta, tb, ksplit=ks)
-                    assert torch.equal(out, ref), (lead, ab, bb, (out - ref).abs().max().item())
-    finally:
-        hip().set_h3p_lead(4)
+    for ab in (False, True):
+        for bb in (False, True):
+            out = h3p.gemm(h3p.split(a, blk=ab), h3p.split(b, blk=bb), ta, tb, ksplit=ks)
+            assert torch.equal(out, ref), (ab, bb, (out - ref).abs().max().item())
 
 
 def _operands(ta, tb, M, N, K, data, dev, g):

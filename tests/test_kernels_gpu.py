@@ -340,7 +340,7 @@ def test_attention_bwd_x6_fp32_level(cuda, B, S, NH, p):
 
 
 @pytest.mark.parametrize("B,S,NH,p", [(2, 128, 12, 0.0), (2, 96, 2, 0.1), (1, 512, 2, 0.0), (2, 192, 2, 0.1),
-                                       (3, 64, 4, 0.1), (2, 256, 12, 0.0), (8, 512, 12, 0.1)])
+                                       (3, 64, 4, 0.1), (2, 256, 12, 0.0), (8, 512, 12, 0.1), (1, 288, 2, 0.1)])
 @pytest.mark.parametrize("data", ["uniform", "wide"])
 def test_attention_h3_matches_fp64(cuda, B, S, NH, p, data):
     """fp32 attention on three split-fp16 products with in-kernel power-of-two scales (attention_h3.hip,
