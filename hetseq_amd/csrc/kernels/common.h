@@ -136,8 +136,10 @@ extern const uint64_t* g_seed_dev;
 
 // Diagnostic ablation (set_skip_launches; bench.py --ab skip_*): launches of the classes whose bit is
 // set return without launching -- kSkipSplitK the split-K finishing passes, kSkipReduceRows the
-// column-partial reductions.  Results are then meaningless; every buffer and address stays the same.
-enum : int { kSkipSplitK = 1, kSkipReduceRows = 2 };
+// column-partial reductions; kSkipEpiAux / kSkipEpiPlanes / kSkipEpiMath: the h3p GEMM's GELU / dGELU
+// epilogue without its pre-activation store / load, its plane stores, its GELU math.  Results are then
+// meaningless; every buffer and address stays the same.
+enum : int { kSkipSplitK = 1, kSkipReduceRows = 2, kSkipEpiAux = 4, kSkipEpiPlanes = 8, kSkipEpiMath = 16 };
 extern int g_hs_skip;
 HS_DEVICE uint64_t resolve_seed(uint64_t seed, const uint64_t* seed_dev) { return seed_dev ? *seed_dev : seed; }
 

@@ -85,9 +85,14 @@ struct QArgs {
   // are not written (they are the NEXT tensor of the flat gradient store), bias entries from Nv on
   // read as zero (the padded columns of C stay exactly the zero the padded operand rows give)
   int Mv, Nv;
+  int skip;  // diagnostic ablation of the GELU / dGELU epilogue (common.h kSkipEpi*, shifted by 2)
 };
 
 HS_DEVICE qf16 q_mma(qh8 a, qh8 b, qf16 c) { return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0); }
+// x of lane l ^ 1 (one DPP quad permutation [1, 0, 3, 2])
+HS_DEVICE float q_swap1(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0xB1, 0xF, 0xF, false));
+}
 HS_DEVICE int q_row(int r, int q) { return (r & 3) + 8 * (r >> 2) + 4 * q; }
 
 // Shared epilogue: register r of acc[i][j] -> row m0+wm+32i+q_row(r,q), col n0+wn+32j+lr.  `smem`: the
@@ -124,45 +129,77 @@ HS_DEVICE void q_epilogue(const QArgs& p, qf16 (&acc)[2][2], char* smem, int m0,
     }
     return;
   }
+  if constexpr (EPI == kQGelu || EPI == kQDGelu) {
+    // Lanes l and l ^ 1 hold adjacent columns of the same rows: one DPP swap per register pair gives
+    // each lane two adjacent columns of ONE row (the even lane row R, the odd lane row R + 1 of the
+    // pair), so the pre-activation moves as 8-byte and each plane as 4-byte accesses at constant
+    // offsets from one base per tile (round 5: 4-byte / 2-byte accesses with a 64-bit index each,
+    // 13-20 us of the FFN GEMMs' epilogue per call).
+    const int odd = lane & 1, cp2 = lr & ~1;
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int n = n0 + wn + 32 * j + lr;
-    const float bv = EPI != kQNone && n < p.Nv ? p.bias[n] : 0.f;
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + wn + 32 * j + lr;
+      const float bv = n < p.Nv ? p.bias[n] : 0.f;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int mb = m0 + wm + 32 * i;
-      if (EPI == kQGelu) {
+      for (int i = 0; i < 2; ++i) {
+        const int mb = m0 + wm + 32 * i;
+        float* const auxb = p.aux + (int64_t)(mb + 4 * q + odd) * p.ldaux + (n0 + wn + 32 * j + cp2);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int64_t m = mb + q_row(r, q);
-          p.aux[m * p.ldaux + n] = acc[i][j][r];
-          acc[i][j][r] = gelu_f(acc[i][j][r] + bv);
-          if (p.C) p.C[m * p.ldc + n] = acc[i][j][r];
+        for (int r = 0; r < 16; r += 2) {
+          const int64_t ro = (int64_t)((r & 3) + 8 * (r >> 2)) * p.ldaux;  // row q_row(r, q) - 4 q
+          float pre0, pre1;
+          if (EPI == kQGelu) {
+            pre0 = acc[i][j][r];
+            pre1 = acc[i][j][r + 1];
+            const float recv = q_swap1(odd ? pre0 : pre1);
+            if (!(p.skip & 1))
+              *reinterpret_cast<float2*>(auxb + ro) = odd ? make_float2(recv, pre1) : make_float2(pre0, recv);
+            acc[i][j][r] = p.skip & 4 ? pre0 + bv : gelu_f(pre0 + bv);
+            acc[i][j][r + 1] = p.skip & 4 ? pre1 + bv : gelu_f(pre1 + bv);
+          } else {
+            const float2 ld = p.skip & 1 ? make_float2(acc[i][j][r], acc[i][j][r + 1])
+                                         : *reinterpret_cast<const float2*>(auxb + ro);
+            const float recv = q_swap1(odd ? ld.x : ld.y);
+            pre0 = odd ? recv : ld.x;
+            pre1 = odd ? ld.y : recv;
+            acc[i][j][r] *= p.skip & 4 ? pre0 + bv : gelu_grad_f(pre0 + bv);
+            acc[i][j][r + 1] *= p.skip & 4 ? pre1 + bv : gelu_grad_f(pre1 + bv);
+            csum[j] += acc[i][j][r];
+            csum[j] += acc[i][j][r + 1];
+          }
+          if (p.C) {
+            p.C[(int64_t)(mb + q_row(r, q)) * p.ldc + n] = acc[i][j][r];
+            p.C[(int64_t)(mb + q_row(r + 1, q)) * p.ldc + n] = acc[i][j][r + 1];
+          }
         }
-      } else if (EPI == kQDGelu) {
-        float pre[16];
+      }
+    }
+  } else {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) pre[r] = p.aux[(int64_t)(mb + q_row(r, q)) * p.ldaux + n];
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + wn + 32 * j + lr;
+      const float bv = EPI != kQNone && n < p.Nv ? p.bias[n] : 0.f;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          acc[i][j][r] *= gelu_grad_f(pre[r] + bv);
-          csum[j] += acc[i][j][r];
-          if (p.C) p.C[(int64_t)(mb + q_row(r, q)) * p.ldc + n] = acc[i][j][r];
+      for (int i = 0; i < 2; ++i) {
+        const int mb = m0 + wm + 32 * i;
+        if (p.beta != 0.f) {
+          float old[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) old[r] = p.C[(int64_t)(mb + q_row(r, q)) * p.ldc + n];
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            p.C[(int64_t)(mb + q_row(r, q)) * p.ldc + n] = acc[i][j][r] + bv + p.beta * old[r];
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) p.C[(int64_t)(mb + q_row(r, q)) * p.ldc + n] = acc[i][j][r] + bv;
         }
-      } else if (p.beta != 0.f) {
-        float old[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) old[r] = p.C[(int64_t)(mb + q_row(r, q)) * p.ldc + n];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) p.C[(int64_t)(mb + q_row(r, q)) * p.ldc + n] = acc[i][j][r] + bv + p.beta * old[r];
-      } else {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) p.C[(int64_t)(mb + q_row(r, q)) * p.ldc + n] = acc[i][j][r] + bv;
       }
     }
   }
-  if ((EPI == kQGelu || EPI == kQDGelu) && p.cp) {
-    // the result as h3p planes: one exponent per 32 x 32 accumulator tile (= one exponent block)
+  if ((EPI == kQGelu || EPI == kQDGelu) && p.cp && !(p.skip & 2)) {
+    // the result as h3p planes: one exponent per 32 x 32 accumulator tile (= one exponent block, 2 KB
+    // per plane, 64-B rows); the same pairing as above makes every plane access 4 bytes wide
+    const int odd = lane & 1, cp2 = lr & ~1;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -171,20 +208,19 @@ HS_DEVICE void q_epilogue(const QArgs& p, qf16 (&acc)[2][2], char* smem, int m0,
 #pragma unroll
         for (int r = 0; r < 16; ++r) mb = amax_bits(mb, acc[i][j][r]);
         const int e = h3p_exp_bits(wave_umax(mb));
-        const float s = h3p_scale(e);
+        const float sc = h3p_scale(e);
         const int rb = (m0 + wm) / 32 + i, cb = (n0 + wn) / 32 + j;
         if (lane == 0) p.ec[(int64_t)rb * p.lde_c + cb] = static_cast<int8_t>(e);
-        const int n = n0 + wn + 32 * j + lr;
+        uint16_t* const blk = p.cp + (int64_t)rb * 32 * p.ldcp + (int64_t)cb * 1024 + (4 * q + odd) * 32 + cp2;
 #pragma unroll
         for (int r = 0; r < 16; r += 2) {
-          uint32_t hi, lo;
-          h3p_split2(acc[i][j][r], acc[i][j][r + 1], s, hi, lo);
-          const int64_t e0 = h3p_index(m0 + wm + 32 * i + q_row(r, q), n, p.ldcp, 1);  // blocked planes
-          const int64_t e1 = h3p_index(m0 + wm + 32 * i + q_row(r + 1, q), n, p.ldcp, 1);
-          p.cp[e0] = static_cast<uint16_t>(hi);
-          p.cp[e1] = static_cast<uint16_t>(hi >> 16);
-          p.cp[p.cp_ps + e0] = static_cast<uint16_t>(lo);
-          p.cp[p.cp_ps + e1] = static_cast<uint16_t>(lo >> 16);
+          const uint32_t w0 = h3p_pack1(acc[i][j][r], sc), w1 = h3p_pack1(acc[i][j][r + 1], sc);  // hi | lo << 16
+          const uint32_t recv = __builtin_bit_cast(uint32_t, q_swap1(__builtin_bit_cast(float, odd ? w0 : w1)));
+          const uint32_t hi = odd ? ((recv & 0xffffu) | (w1 << 16)) : ((w0 & 0xffffu) | (recv << 16));
+          const uint32_t lo = odd ? ((recv >> 16) | (w1 & 0xffff0000u)) : ((w0 >> 16) | (recv & 0xffff0000u));
+          const int ro = ((r & 3) + 8 * (r >> 2)) * 32;
+          *reinterpret_cast<uint32_t*>(blk + ro) = hi;
+          *reinterpret_cast<uint32_t*>(blk + p.cp_ps + ro) = lo;
         }
       }
   }
@@ -554,7 +590,7 @@ int launch_gemm_h3p_v(int ta, int tb, int M, int N, int K, const void* A, int64_
   if (spanA >= (1ll << 32) || spanB >= (1ll << 32)) return -1;
   QArgs a{static_cast<const uint16_t*>(A), ea, static_cast<const uint16_t*>(B), eb, lda, a_ps, lde_a, ldb, b_ps,
           lde_b, C, ldc, bias, aux, ldaux, part, static_cast<uint16_t*>(cp), ec, ldcp, cp_ps, lde_c, slab, M, N, K,
-          ksplit, beta, ablk, bblk, Mv, Nv};
+          ksplit, beta, ablk, bblk, Mv, Nv, (g_hs_skip >> 2) & 7};
   const int rc = !ta && tb ? q_launch_epi<false, true>(ksplit > 1 ? 0 : epi, a, st)
                  : !ta   ? q_launch_epi<false, false>(ksplit > 1 ? 0 : epi, a, st)
                          : q_launch_epi<true, false>(ksplit > 1 ? 0 : epi, a, st);

@@ -73,6 +73,11 @@ def main():
             row["f16 TF/s"] = cs["SQ_INSTS_VALU_MFMA_MOPS_F16"] * 512 / d / 1000.0
         if "SQ_VALU_MFMA_BUSY_CYCLES" in cs and "SQ_BUSY_CYCLES" in cs and cs["SQ_BUSY_CYCLES"]:
             row["mfma busy/SQ busy %"] = 100.0 * cs["SQ_VALU_MFMA_BUSY_CYCLES"] / (cs["SQ_BUSY_CYCLES"] * 4 * 4)
+        if "SQ_INSTS_LDS" in cs and "GRBM_GUI_ACTIVE" in cs and cs["GRBM_GUI_ACTIVE"]:
+            # LDS instructions per CU per cycle (256 CUs; GRBM_GUI_ACTIVE sums the 8 XCDs' cycles)
+            row["lds inst/CU/kclk"] = 1000.0 * cs["SQ_INSTS_LDS"] / 256 / (cs["GRBM_GUI_ACTIVE"] / 8)
+        if "SQ_LDS_IDX_ACTIVE" in cs and cs.get("SQ_BUSY_CYCLES"):
+            row["lds active/SQ busy %"] = 100.0 * cs["SQ_LDS_IDX_ACTIVE"] / cs["SQ_BUSY_CYCLES"]
         if "SQ_LDS_BANK_CONFLICT" in cs and cs.get("SQ_LDS_IDX_ACTIVE"):
             row["lds conflict %"] = 100.0 * cs["SQ_LDS_BANK_CONFLICT"] / cs["SQ_LDS_IDX_ACTIVE"]
         if "TCC_HIT_sum" in cs and (cs["TCC_HIT_sum"] + cs.get("TCC_MISS_sum", 0)):
