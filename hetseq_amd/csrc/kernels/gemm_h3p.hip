@@ -97,9 +97,19 @@ HS_DEVICE int q_row(int r, int q) { return (r & 3) + 8 * (r >> 2) + 4 * q; }
 
 // Shared epilogue: register r of acc[i][j] -> row m0+wm+32i+q_row(r,q), col n0+wn+32j+lr.  `smem`: the
 // kernel's LDS (free: the K loop ended with a barrier), used for the dGELU column sums.
-template <int EPI>
+// dGELU: the pre-activation of a 32 x 32 tile as this lane's eight float2 (row 4 q + odd + row offset of
+// register pair r / 2, columns cp2, cp2 + 1; the pairing of the epilogue below)
+HS_DEVICE void q_aux_load(const QArgs& p, float2 (&v)[8], int mb, int nb, int lane) {
+  const int lr = lane & 31, q = lane >> 5, odd = lane & 1;
+  const float* auxb = p.aux + (int64_t)(mb + 4 * q + odd) * p.ldaux + (nb + (lr & ~1));
+#pragma unroll
+  for (int r = 0; r < 16; r += 2)
+    v[r / 2] = *reinterpret_cast<const float2*>(auxb + (int64_t)((r & 3) + 8 * (r >> 2)) * p.ldaux);
+}
+
+template <int EPI, int NPF>
 HS_DEVICE void q_epilogue(const QArgs& p, qf16 (&acc)[2][2], char* smem, int m0, int n0, int tm, int slice, int wm,
-                          int wn, int wr, int lane) {
+                          int wn, int wr, int lane, const float2 (&pf)[NPF][8]) {
   const int lr = lane & 31, q = lane >> 5;
   if (p.ksplit > 1) {  // fp32 partial slab; bias / beta / the sum in splitk_reduce_kernel (or the consumer)
     float* sl = p.slab + (int64_t)slice * p.M * p.N;
@@ -157,8 +167,9 @@ HS_DEVICE void q_epilogue(const QArgs& p, qf16 (&acc)[2][2], char* smem, int m0,
             acc[i][j][r] = p.skip & 4 ? pre0 + bv : gelu_f(pre0 + bv);
             acc[i][j][r + 1] = p.skip & 4 ? pre1 + bv : gelu_f(pre1 + bv);
           } else {
-            const float2 ld = p.skip & 1 ? make_float2(acc[i][j][r], acc[i][j][r + 1])
-                                         : *reinterpret_cast<const float2*>(auxb + ro);
+            const float2 ld = p.skip & 1         ? make_float2(acc[i][j][r], acc[i][j][r + 1])
+                              : 2 * i + j < (EPI == kQDGelu ? NPF : 0) ? pf[(2 * i + j) % NPF][r / 2]
+                                                : *reinterpret_cast<const float2*>(auxb + ro);
             const float recv = q_swap1(odd ? ld.x : ld.y);
             pre0 = odd ? recv : ld.x;
             pre1 = odd ? ld.y : recv;
@@ -334,6 +345,11 @@ HS_DEVICE qh8 r_frag(const char* img, int p, int rc, int lane) {
 // instead of in front of the closing lgkmcnt(0) + barrier (round 5 issued the DMA first: the layer's
 // twelve products 643.6 -> 634.1 us alone, the step 10.81 -> 10.73 ms, tools/bench_h3p.py and
 // bench.py --ab, round 6).
+#ifndef HS_QAUX_PREFETCH
+#define HS_QAUX_PREFETCH 2
+#endif
+constexpr int kQAuxPrefetch = HS_QAUX_PREFETCH;
+
 template <bool TA, bool TB, int EPI>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) gemm_h3p_kernel(QArgs p) {
   constexpr int LEAD = 4;
@@ -421,6 +437,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     }
   };
 
+  // dGELU: the pre-activation of the first kQAuxPrefetch tiles is loaded before the K loop (the
+  // epilogue's loads were 17 us of a 99-us FFN-out data gradient, issued when the MFMAs are done;
+  // the prologue's first counted wait covers them too)
+  constexpr int NPF = EPI == kQDGelu ? kQAuxPrefetch : 1;
+  float2 pf[NPF][8];
+  if constexpr (EPI == kQDGelu) {
+#pragma unroll
+    for (int t = 0; t < NPF; ++t) q_aux_load(p, pf[t], m0 + wm + 32 * (t >> 1), n0 + wn + 32 * (t & 1), lane);
+  }
   // prologue: LEAD steps in flight, wait for the first
 #pragma unroll
   for (int j = 0; j < 4; ++j) dma(j, 0, 0);
@@ -455,7 +480,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   }
   r_wait_vm<0>();  // the trailing duplicate DMAs land before the LDS is reused
   __syncthreads();
-  q_epilogue<EPI>(p, acc, smem, m0, n0, tm, slice, wm, wn, wr, lane);
+  q_epilogue<EPI, NPF>(p, acc, smem, m0, n0, tm, slice, wm, wn, wr, lane, pf);
 }
 
 // ---------------------------------------------------------------- fp32 -> h3p planes
