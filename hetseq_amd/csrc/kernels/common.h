@@ -136,10 +136,8 @@ extern const uint64_t* g_seed_dev;
 
 // Diagnostic ablation (set_skip_launches; bench.py --ab skip_*): launches of the classes whose bit is
 // set return without launching -- kSkipSplitK the split-K finishing passes, kSkipReduceRows the
-// column-partial reductions; kSkipEpiAux / kSkipEpiPlanes / kSkipEpiMath: the h3p GEMM's GELU / dGELU
-// epilogue without its pre-activation store / load, its plane stores, its GELU math.  Results are then
-// meaningless; every buffer and address stays the same.
-enum : int { kSkipSplitK = 1, kSkipReduceRows = 2, kSkipEpiAux = 4, kSkipEpiPlanes = 8, kSkipEpiMath = 16 };
+// column-partial reductions.  Results are then meaningless; every buffer and address stays the same.
+enum : int { kSkipSplitK = 1, kSkipReduceRows = 2 };
 extern int g_hs_skip;
 HS_DEVICE uint64_t resolve_seed(uint64_t seed, const uint64_t* seed_dev) { return seed_dev ? *seed_dev : seed; }
 
@@ -184,7 +182,6 @@ HS_DEVICE void store4(bf16_t* p, const float v[4]) {
   *reinterpret_cast<uint2*>(p) = t;
 }
 
-// erf-GELU with the reference's 1.41421 constant (reference: bert_modeling.py:104-111)
 // GELU with the reference's constant c = 1.41421 (bert_modeling.py:104-111): x/2 (1 + erf(x/c)).
 // 1 + erf(z) is evaluated as erfc(-z) from one branch-free rational form, erfc(a) = t exp(-a^2 + P(t)),
 // t = 1 / (1 + a/2), a = |z| (Numerical Recipes' erfcc, fractional error < 1.2e-7 on [0, inf)): about
@@ -193,28 +190,43 @@ HS_DEVICE void store4(bf16_t* p, const float v[4]) {
 // the GELU math alone took 18 us of a 92-us FFN-in product (tools/bench_h3p_epi.py, round 6).  The
 // form is also accurate in relative terms on the negative tail, where 1 + erff(z) cancels (measured in
 // fp32 against fp64 over [-10, 10]: max abs error 3.8e-7, as the erff form's 4.4e-7).
-HS_DEVICE float gelu_phi2(float z) {  // 1 + erf(z)
-  const float a = fabsf(z);
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.5f, a, 1.f));
-  float p = 0.17087277f;
-  p = fmaf(p, t, -0.82215223f);
-  p = fmaf(p, t, 1.48851587f);
-  p = fmaf(p, t, -1.13520398f);
-  p = fmaf(p, t, 0.27886807f);
-  p = fmaf(p, t, -0.18628806f);
-  p = fmaf(p, t, 0.09678418f);
-  p = fmaf(p, t, 0.37409196f);
-  p = fmaf(p, t, 1.00002368f);
-  p = fmaf(p, t, -1.26551223f);
-  const float e = t * __expf(fmaf(-a, a, p));  // erfc(a)
-  return z < 0.f ? e : 2.f - e;
+typedef float hs_f2 __attribute__((ext_vector_type(2)));
+HS_DEVICE hs_f2 hs_f2s(float v) { return hs_f2{v, v}; }
+HS_DEVICE hs_f2 hs_exp2v(hs_f2 x) { return hs_f2{__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)}; }
+// 1 + erf(z) on two values at once (packed fp32 FMAs: half the VALU issue of two scalar evaluations),
+// the exponential as exp2 of a log2(e)-scaled argument (the coefficients carry the factor: no range
+// fix-up around the exp)
+HS_DEVICE hs_f2 gelu_phi2v(hs_f2 z) {
+  constexpr float L = 1.4426950408889634f;  // log2(e)
+  const hs_f2 a = __builtin_elementwise_abs(z);
+  const hs_f2 d = __builtin_elementwise_fma(hs_f2s(0.5f), a, hs_f2s(1.f));
+  const hs_f2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  hs_f2 p = hs_f2s(0.17087277f * L);
+  p = __builtin_elementwise_fma(p, t, hs_f2s(-0.82215223f * L));
+  p = __builtin_elementwise_fma(p, t, hs_f2s(1.48851587f * L));
+  p = __builtin_elementwise_fma(p, t, hs_f2s(-1.13520398f * L));
+  p = __builtin_elementwise_fma(p, t, hs_f2s(0.27886807f * L));
+  p = __builtin_elementwise_fma(p, t, hs_f2s(-0.18628806f * L));
+  p = __builtin_elementwise_fma(p, t, hs_f2s(0.09678418f * L));
+  p = __builtin_elementwise_fma(p, t, hs_f2s(0.37409196f * L));
+  p = __builtin_elementwise_fma(p, t, hs_f2s(1.00002368f * L));
+  p = __builtin_elementwise_fma(p, t, hs_f2s(-1.26551223f * L));
+  const hs_f2 e = t * hs_exp2v(__builtin_elementwise_fma(-a, a * L, p));  // erfc(|z|)
+  return hs_f2{z.x < 0.f ? e.x : 2.f - e.x, z.y < 0.f ? e.y : 2.f - e.y};
 }
-HS_DEVICE float gelu_f(float x) { return x * 0.5f * gelu_phi2(x * (1.f / 1.41421f)); }
-HS_DEVICE float gelu_grad_f(float x) {
+// GELU and its derivative on two values (the GEMM epilogues: register pairs r, r + 1 are the two rows a
+// lane holds in one column)
+HS_DEVICE hs_f2 gelu_v(hs_f2 x) { return x * 0.5f * gelu_phi2v(x * (1.f / 1.41421f)); }
+HS_DEVICE hs_f2 gelu_grad_v(hs_f2 x) {
   // d/dx [x/2 (1+erf(x/c))] = 1/2 (1+erf(x/c)) + x/(c*sqrt(pi)) exp(-(x/c)^2)
-  const float z = x * (1.f / 1.41421f);
-  return 0.5f * gelu_phi2(z) + x * (0.5641895835477563f / 1.41421f) * __expf(-z * z);
+  constexpr float L = 1.4426950408889634f;
+  const hs_f2 z = x * (1.f / 1.41421f);
+  const hs_f2 g = hs_exp2v(-z * (z * L));  // exp(-z^2)
+  return __builtin_elementwise_fma(x * (0.5641895835477563f / 1.41421f), g, 0.5f * gelu_phi2v(z));
 }
+// one value: the same arithmetic in lane x of the pair
+HS_DEVICE float gelu_f(float x) { return gelu_v(hs_f2{x, 0.f}).x; }
+HS_DEVICE float gelu_grad_f(float x) { return gelu_grad_v(hs_f2{x, 0.f}).x; }
 
 inline int ceil_div(int64_t a, int64_t b) { return static_cast<int>((a + b - 1) / b); }
 

@@ -85,7 +85,6 @@ struct QArgs {
   // are not written (they are the NEXT tensor of the flat gradient store), bias entries from Nv on
   // read as zero (the padded columns of C stay exactly the zero the padded operand rows give)
   int Mv, Nv;
-  int skip;  // diagnostic ablation of the GELU / dGELU epilogue (common.h kSkipEpi*, shifted by 2)
 };
 
 HS_DEVICE qf16 q_mma(qh8 a, qh8 b, qf16 c) { return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0); }
@@ -142,9 +141,11 @@ HS_DEVICE void q_epilogue(const QArgs& p, qf16 (&acc)[2][2], char* smem, int m0,
   if constexpr (EPI == kQGelu || EPI == kQDGelu) {
     // Lanes l and l ^ 1 hold adjacent columns of the same rows: one DPP swap per register pair gives
     // each lane two adjacent columns of ONE row (the even lane row R, the odd lane row R + 1 of the
-    // pair), so the pre-activation moves as 8-byte and each plane as 4-byte accesses at constant
-    // offsets from one base per tile (round 5: 4-byte / 2-byte accesses with a 64-bit index each,
-    // 13-20 us of the FFN GEMMs' epilogue per call).
+    // pair), so the pre-activation moves as 8-byte accesses at constant offsets from one base per tile.
+    // The GELU math runs on the pair (acc[r], acc[r + 1]) -- one column, two rows -- as packed fp32.
+    // The epilogue runs when the tile's MFMAs are done and is VALU-bound (round 6, tools/bench_h3p_epi.py
+    // with each part skipped in turn: at M 4096 the erff-based GELU math cost 18 us of a 92-us FFN-in
+    // product, the plane stores 9, the pre-activation store 3; the dGELU's pre-activation loads 18).
     const int odd = lane & 1, cp2 = lr & ~1;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -154,35 +155,41 @@ HS_DEVICE void q_epilogue(const QArgs& p, qf16 (&acc)[2][2], char* smem, int m0,
       for (int i = 0; i < 2; ++i) {
         const int mb = m0 + wm + 32 * i;
         float* const auxb = p.aux + (int64_t)(mb + 4 * q + odd) * p.ldaux + (n0 + wn + 32 * j + cp2);
+        // the pre-activation moves first, then the math of the tile's eight pairs as one block (eight
+        // independent dependency chains for the scheduler to interleave)
+        hs_f2 pre[8];
 #pragma unroll
         for (int r = 0; r < 16; r += 2) {
           const int64_t ro = (int64_t)((r & 3) + 8 * (r >> 2)) * p.ldaux;  // row q_row(r, q) - 4 q
-          float pre0, pre1;
           if (EPI == kQGelu) {
-            pre0 = acc[i][j][r];
-            pre1 = acc[i][j][r + 1];
-            const float recv = q_swap1(odd ? pre0 : pre1);
-            if (!(p.skip & 1))
-              *reinterpret_cast<float2*>(auxb + ro) = odd ? make_float2(recv, pre1) : make_float2(pre0, recv);
-            acc[i][j][r] = p.skip & 4 ? pre0 + bv : gelu_f(pre0 + bv);
-            acc[i][j][r + 1] = p.skip & 4 ? pre1 + bv : gelu_f(pre1 + bv);
+            pre[r / 2] = hs_f2{acc[i][j][r], acc[i][j][r + 1]};
+            const float recv = q_swap1(odd ? acc[i][j][r] : acc[i][j][r + 1]);
+            *reinterpret_cast<float2*>(auxb + ro) =
+                odd ? make_float2(recv, acc[i][j][r + 1]) : make_float2(acc[i][j][r], recv);
           } else {
-            const float2 ld = p.skip & 1         ? make_float2(acc[i][j][r], acc[i][j][r + 1])
-                              : 2 * i + j < (EPI == kQDGelu ? NPF : 0) ? pf[(2 * i + j) % NPF][r / 2]
-                                                : *reinterpret_cast<const float2*>(auxb + ro);
+            const float2 ld = 2 * i + j < NPF ? pf[(2 * i + j) % NPF][r / 2]
+                                              : *reinterpret_cast<const float2*>(auxb + ro);
             const float recv = q_swap1(odd ? ld.x : ld.y);
-            pre0 = odd ? recv : ld.x;
-            pre1 = odd ? ld.y : recv;
-            acc[i][j][r] *= p.skip & 4 ? pre0 + bv : gelu_grad_f(pre0 + bv);
-            acc[i][j][r + 1] *= p.skip & 4 ? pre1 + bv : gelu_grad_f(pre1 + bv);
-            csum[j] += acc[i][j][r];
-            csum[j] += acc[i][j][r + 1];
-          }
-          if (p.C) {
-            p.C[(int64_t)(mb + q_row(r, q)) * p.ldc + n] = acc[i][j][r];
-            p.C[(int64_t)(mb + q_row(r + 1, q)) * p.ldc + n] = acc[i][j][r + 1];
+            pre[r / 2] = hs_f2{odd ? recv : ld.x, odd ? ld.y : recv};
           }
         }
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          hs_f2 res;
+          if (EPI == kQGelu) {
+            res = gelu_v(pre[r / 2] + bv);
+          } else {
+            res = hs_f2{acc[i][j][r], acc[i][j][r + 1]} * gelu_grad_v(pre[r / 2] + bv);
+          }
+          acc[i][j][r] = res.x;
+          acc[i][j][r + 1] = res.y;
+        }
+        if (EPI == kQDGelu)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) csum[j] += acc[i][j][r];
+        if (p.C)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) p.C[(int64_t)(mb + q_row(r, q)) * p.ldc + n] = acc[i][j][r];
       }
     }
   } else {
@@ -207,10 +214,12 @@ HS_DEVICE void q_epilogue(const QArgs& p, qf16 (&acc)[2][2], char* smem, int m0,
       }
     }
   }
-  if ((EPI == kQGelu || EPI == kQDGelu) && p.cp && !(p.skip & 2)) {
+  if ((EPI == kQGelu || EPI == kQDGelu) && p.cp) {
     // the result as h3p planes: one exponent per 32 x 32 accumulator tile (= one exponent block, 2 KB
     // per plane, 64-B rows); the same pairing as above makes every plane access 4 bytes wide
     const int odd = lane & 1, cp2 = lr & ~1;
+    const uint32_t sel_send = odd ? 0x05040100u : 0x07060302u;
+    const uint32_t sel_hi = odd ? 0x03020504u : 0x05040100u, sel_lo = odd ? 0x03020706u : 0x07060100u;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -225,10 +234,14 @@ HS_DEVICE void q_epilogue(const QArgs& p, qf16 (&acc)[2][2], char* smem, int m0,
         uint16_t* const blk = p.cp + (int64_t)rb * 32 * p.ldcp + (int64_t)cb * 1024 + (4 * q + odd) * 32 + cp2;
 #pragma unroll
         for (int r = 0; r < 16; r += 2) {
-          const uint32_t w0 = h3p_pack1(acc[i][j][r], sc), w1 = h3p_pack1(acc[i][j][r + 1], sc);  // hi | lo << 16
-          const uint32_t recv = __builtin_bit_cast(uint32_t, q_swap1(__builtin_bit_cast(float, odd ? w0 : w1)));
-          const uint32_t hi = odd ? ((recv & 0xffffu) | (w1 << 16)) : ((w0 & 0xffffu) | (recv << 16));
-          const uint32_t lo = odd ? ((recv >> 16) | (w1 & 0xffff0000u)) : ((w0 >> 16) | (recv & 0xffff0000u));
+          uint32_t h, l;  // rows r, r + 1 of this lane's column: (hi_r | hi_r+1 << 16), (lo_r | lo_r+1 << 16)
+          h3p_split2(acc[i][j][r], acc[i][j][r + 1], sc, h, l);
+          // the even lane keeps row r and sends row r + 1 (hi | lo << 16); the odd lane the reverse
+          // (byte selectors per lane parity: v_perm_b32 picks bytes 0-3 from its second operand)
+          const uint32_t send = __builtin_amdgcn_perm(l, h, sel_send);
+          const uint32_t recv = __builtin_bit_cast(uint32_t, q_swap1(__builtin_bit_cast(float, send)));
+          const uint32_t hi = __builtin_amdgcn_perm(recv, h, sel_hi);
+          const uint32_t lo = __builtin_amdgcn_perm(recv, l, sel_lo);
           const int ro = ((r & 3) + 8 * (r >> 2)) * 32;
           *reinterpret_cast<uint32_t*>(blk + ro) = hi;
           *reinterpret_cast<uint32_t*>(blk + p.cp_ps + ro) = lo;
@@ -615,7 +628,7 @@ int launch_gemm_h3p_v(int ta, int tb, int M, int N, int K, const void* A, int64_
   if (spanA >= (1ll << 32) || spanB >= (1ll << 32)) return -1;
   QArgs a{static_cast<const uint16_t*>(A), ea, static_cast<const uint16_t*>(B), eb, lda, a_ps, lde_a, ldb, b_ps,
           lde_b, C, ldc, bias, aux, ldaux, part, static_cast<uint16_t*>(cp), ec, ldcp, cp_ps, lde_c, slab, M, N, K,
-          ksplit, beta, ablk, bblk, Mv, Nv, (g_hs_skip >> 2) & 7};
+          ksplit, beta, ablk, bblk, Mv, Nv};
   const int rc = !ta && tb ? q_launch_epi<false, true>(ksplit > 1 ? 0 : epi, a, st)
                  : !ta   ? q_launch_epi<false, false>(ksplit > 1 ? 0 : epi, a, st)
                          : q_launch_epi<true, false>(ksplit > 1 ? 0 : epi, a, st);

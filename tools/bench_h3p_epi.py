@@ -55,12 +55,6 @@ def main():
             "dgrad dgelu+planes": lambda: h3p.gemm(dy, w2, 0, 0, out=None, bias=bi, epi=h3p.EPI_DGELU, aux=pre,
                                                    part=part, colsum=db, colsum_acc=True, planes_out=yp),
         }
-        # ablations of the epilogue (results meaningless): without the aux access / plane stores / math
-        hip = h3p.hip()
-        for tag, mask in (("-aux", 4), ("-planes", 8), ("-math", 16), ("-all", 28)):
-            for k in ("fwd gelu+planes", "dgrad dgelu+planes"):
-                runs[k + tag] = (lambda fn, m: lambda: (hip.set_skip_launches(m), fn(), hip.set_skip_launches(0)))(
-                    runs[k], mask)
         best = {}
         for _ in range(a.rounds):
             for k, fn in runs.items():
