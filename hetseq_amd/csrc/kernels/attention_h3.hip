@@ -47,6 +47,7 @@ constexpr int kHD = 64;             // head dim
 constexpr int kRowB = 128;          // bytes per image row (64 fp16)
 constexpr int kPl = 64 * kRowB;     // one plane of a 64-row chunk: 8 KB
 constexpr int kIm = 2 * kPl;        // hi + lo: 16 KB
+constexpr float kLog2e = 1.4426950408889634f, kLn2 = 0.6931471805599453f;
 
 HS_DEVICE f32x16 mma(hx8 a, hx8 b, f32x16 c) { return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0); }
 
@@ -329,7 +330,7 @@ HS_DEVICE void dkv_body(char* __restrict__ smem, int bx, int bh, const float* __
   hx8 kb[4][2], vb[4][2];
   const int ek = lane_row(rows + (int64_t)key * ld + H + h * kHD, bofs(bqkv, H + h * kHD), 1.f, active, hf, kb);
   const int ev = lane_row(rows + (int64_t)key * ld + 2 * H + h * kHD, bofs(bqkv, 2 * H + h * kHD), 1.f, active, hf, vb);
-  const float madd = active ? (1.f - (float)mask[(int64_t)b * S + key]) * -10000.f : 0.f;
+  const float madd = active ? (1.f - (float)mask[(int64_t)b * S + key]) * (-10000.f * kLog2e) : 0.f;  // base 2
 
   f32x16 dk0 = {}, dk1 = {}, dv0 = {}, dv1 = {};
   int eq_run = 0, eo_run = 0, es = 126;
@@ -371,10 +372,10 @@ HS_DEVICE void dkv_body(char* __restrict__ smem, int bx, int bh, const float* __
         const int r = (tid + 256 * i) >> 3;
         if (r < clen && (tid & 7) == 0) Ds[r] = s;
       }
-      for (int i = tid; i < clen; i += 256) Ls[i] = lse[(int64_t)bh * S + c0 + i];
+      for (int i = tid; i < clen; i += 256) Ls[i] = lse[(int64_t)bh * S + c0 + i] * kLog2e;
     } else {
       for (int i = tid; i < clen; i += 256) {
-        Ls[i] = lse[(int64_t)bh * S + c0 + i];
+        Ls[i] = lse[(int64_t)bh * S + c0 + i] * kLog2e;
         Ds[i] = Dd[(int64_t)bh * S + c0 + i];
       }
     }
@@ -394,7 +395,7 @@ HS_DEVICE void dkv_body(char* __restrict__ smem, int bx, int bh, const float* __
     }
     eq_run = eq;
     eo_run = eo;
-    const float us = ldexpf(1.f, -(eq + ek)), ud = ldexpf(1.f, -(eo + ev));
+    const float us = ldexpf(1.f, -(eq + ek)) * kLog2e, ud = ldexpf(1.f, -(eo + ev));
 #pragma unroll 1
     for (int t = 0; t < clen; t += 32) {
       f32x16 sc = {}, dp = {};
@@ -413,7 +414,7 @@ HS_DEVICE void dkv_body(char* __restrict__ smem, int bx, int bh, const float* __
       // P in place of the scores; dV^T first, so the P-with-dropout copies die before dS exists
       // (the four accumulators and the lane's K / V fragments leave little register room)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) sc[r] = __expf(sc[r] * us + madd - Ls[t + xrow(r, hf)]);
+      for (int r = 0; r < 16; ++r) sc[r] = __builtin_amdgcn_exp2f(sc[r] * us + madd - Ls[t + xrow(r, hf)]);
       uint32_t kbits = 0xffffu;  // keep bit of score register r (one register, not 16 live multipliers)
       if (p > 0.f) {
         kbits = 0u;
@@ -508,7 +509,7 @@ HS_DEVICE void dq_body(char* __restrict__ smem, int bx, int bh, const float* __r
     } else {
       dsum = Dd[(int64_t)bh * S + q0 + li];
     }
-    lq = lse[(int64_t)bh * S + q0 + li];
+    lq = lse[(int64_t)bh * S + q0 + li] * kLog2e;  // base 2 (the forward's softmax)
   }
   if (ctx) dsum += __shfl_xor(dsum, 32, 64);
 
@@ -527,7 +528,7 @@ HS_DEVICE void dq_body(char* __restrict__ smem, int bx, int bh, const float* __r
     __syncthreads();
     const int ek = red_exp(red + 8 * par, 0), ev = red_exp(red + 8 * par, 1);
     chunk_put(cur, Kp, Vp, clen, ek, ev);
-    for (int i = tid; i < clen; i += 256) Ms[i] = (1.f - (float)mask[(int64_t)b * S + c0 + i]) * -10000.f;
+    for (int i = tid; i < clen; i += 256) Ms[i] = (1.f - (float)mask[(int64_t)b * S + c0 + i]) * (-10000.f * kLog2e);
     __syncthreads();
     if (!active) continue;
     if (c0 > 0) {
@@ -536,7 +537,7 @@ HS_DEVICE void dq_body(char* __restrict__ smem, int bx, int bh, const float* __r
       dq1 *= fk;
     }
     ek_run = ek;
-    const float us = ldexpf(1.f, -(ek + eq)), ud = ldexpf(1.f, -(ev + eo));
+    const float us = ldexpf(1.f, -(ek + eq)) * kLog2e, ud = ldexpf(1.f, -(ev + eo));
 #pragma unroll 1
     for (int t = 0; t < clen; t += 32) {
       f32x16 sc = {}, dp = {};
@@ -558,7 +559,7 @@ HS_DEVICE void dq_body(char* __restrict__ smem, int bx, int bh, const float* __r
         for (int j = 0; j < 8; ++j) {
           const int r = 8 * ks + j, kj = xrow(r, hf);
           const float mk = p > 0.f ? (((word >> kj) & 1u) ? dscale : 0.f) : 1.f;
-          const float pv = __expf(sc[r] * us + Ms[t + kj] - lq);
+          const float pv = __builtin_amdgcn_exp2f(sc[r] * us + Ms[t + kj] - lq);
           ds[ks][j] = pv * (dp[r] * ud * mk - dsum);
         }
       const float ss = ds_scale(ds, es, dq0, dq1);
@@ -630,6 +631,8 @@ __global__ void __launch_bounds__(256, PAIR ? 1 : 2)
   const int ep = p_exp(p > 0.f ? dscale : 1.f);
   const float sp = ldexpf(1.f, ep);
 
+  // the softmax runs in base 2: scores, mask and running max carry log2(e), so every exponential is
+  // one v_exp_f32 (no range fix-up around __expf); lse is written in natural units
   // the lane's Q row, biased, * 1/sqrt(64) (exact), split with its row exponent
   hx8 qf[4][2];
   const int eq = lane_row(rows + (int64_t)(q0 + li) * ld + h * kHD, bofs(bqkv, h * kHD), 0.125f, active, hf, qf);
@@ -651,7 +654,7 @@ __global__ void __launch_bounds__(256, PAIR ? 1 : 2)
     __syncthreads();  // every wave done with the previous chunk's images; |max| partials visible
     const int ek = red_exp(red + 8 * par, 0), ev = red_exp(red + 8 * par, 1);
     chunk_put(cur, Kimg, Vimg, clen, ek, ev);
-    for (int i = tid; i < clen; i += 256) Ms[i] = (1.f - (float)mask[(int64_t)b * S + c0 + i]) * -10000.f;
+    for (int i = tid; i < clen; i += 256) Ms[i] = (1.f - (float)mask[(int64_t)b * S + c0 + i]) * (-10000.f * kLog2e);
     __syncthreads();
     if (c0 + 64 < S) load(c0 + 64);  // the next chunk's rows fly under this chunk's MFMAs
     if (!active) continue;
@@ -661,7 +664,7 @@ __global__ void __launch_bounds__(256, PAIR ? 1 : 2)
       o1 *= fv;
     }
     ev_run = ev;
-    const float us = ldexpf(1.f, -(ek + eq));
+    const float us = ldexpf(1.f, -(ek + eq)) * kLog2e;
     if (PAIR && clen == 64) {
       // the chunk's two 32-key tiles together: two independent score accumulators (the 12-MFMA chains
       // interleave instead of running back to back), one softmax update and one rescale of the output
@@ -683,13 +686,13 @@ __global__ void __launch_bounds__(256, PAIR ? 1 : 2)
       }
       mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
       const float mn = fmaxf(m, mt);
-      const float alpha = __expf(m - mn);
+      const float alpha = __builtin_amdgcn_exp2f(m - mn);
       m = mn;
       float ps = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {  // the scores' registers become P
-        s0[r] = __expf(s0[r] - mn);
-        s1[r] = __expf(s1[r] - mn);
+        s0[r] = __builtin_amdgcn_exp2f(s0[r] - mn);
+        s1[r] = __builtin_amdgcn_exp2f(s1[r] - mn);
         ps += s0[r] + s1[r];
       }
       ps += __shfl_xor(ps, 32, 64);
@@ -740,13 +743,13 @@ __global__ void __launch_bounds__(256, PAIR ? 1 : 2)
       }
       mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
       const float mn = fmaxf(m, mt);
-      const float alpha = __expf(m - mn);
+      const float alpha = __builtin_amdgcn_exp2f(m - mn);
       m = mn;
       float pr[16];
       float ps = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        pr[r] = __expf(s[r] - mn);
+        pr[r] = __builtin_amdgcn_exp2f(s[r] - mn);
         ps += pr[r];
       }
       ps += __shfl_xor(ps, 32, 64);
@@ -784,7 +787,7 @@ __global__ void __launch_bounds__(256, PAIR ? 1 : 2)
   if (po.pl)  // ctx as h3p planes of the output projection (exponent row stride H / 32)
     store_rows_h3p(po, (int64_t)b * S + q0 + li, h * kHD, H, po.ex + ((int64_t)b * S + q0) / 32 * (H / 32) + 2 * h, o0,
                    o1, hf, inv);
-  if (hf == 0) lse[(int64_t)bh * S + q0 + li] = m + __logf(l);
+  if (hf == 0) lse[(int64_t)bh * S + q0 + li] = m * kLn2 + __logf(l);
 }
 
 }  // namespace hs

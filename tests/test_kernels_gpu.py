@@ -547,7 +547,13 @@ def test_attention_fully_masked_row(cuda):
     qkv = torch.randn(B * S, 3 * NH * 64, device=cuda)
     mask = torch.zeros(B, S, dtype=torch.int64, device=cuda)
     out = attention(qkv, mask, B, S, NH, 0.0)
-    _close(out, _ref_attention(qkv, mask, B, S, NH), 1e-4, 1e-5, "masked fwd")
+    # every score sits near -10000, where fp32 resolves 2^-10: the fp32 reference itself is off the exact
+    # result by ~1e-4 there, so the kernel is held to the fp64 result within twice the fp32 reference's
+    # own error (the h3 softmax runs in base 2 and rounds differently from the natural-base reference)
+    ref64 = _ref_attention(qkv.double(), mask, B, S, NH)
+    e32 = (_ref_attention(qkv, mask, B, S, NH).double() - ref64).abs().max().item()
+    err = (out.double() - ref64).abs().max().item()
+    assert err <= 2 * e32 + 1e-5, "masked fwd: max err %.3e vs the fp32 reference's %.3e" % (err, e32)
     assert torch.isfinite(out).all()
 
 
