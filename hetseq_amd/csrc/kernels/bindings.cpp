@@ -111,7 +111,7 @@ int launch_gemm_planes(int planes, int c_dtype, int ta, int tb, int M, int N, in
                        int64_t a_ps, const void* B, int64_t ldb, int64_t b_ps, void* C, int64_t ldc,
                        const float* bias, int epi, float beta, void* aux, int64_t ldaux, float* part,
                        float* colsum_out, int colsum_acc, int ksplit, float* slab, int64_t slab_floats,
-                       int variant, hipStream_t st);
+                       int variant, hipStream_t st, int Mv);
 void set_planes_variant(int v);
 
 // gemm_h3p.hip
@@ -541,15 +541,19 @@ PYBIND11_MODULE(_hip, m) {
   m.def("gemm_planes", [](int planes, int c_dtype, int ta, int tb, int M, int N, int K, i64 A, i64 lda, i64 a_ps,
                           i64 B, i64 ldb, i64 b_ps, i64 C, i64 ldc, i64 bias, int epi, float beta, i64 aux,
                           i64 ldaux, i64 part, i64 colsum, int colsum_acc, int ksplit, i64 slab, i64 slab_floats,
-                          int variant, i64 st) {
+                          int variant, i64 st, int mv) {
     pre_launch("gemm_planes");
     const int rc = launch_gemm_planes(planes, c_dtype, ta, tb, M, N, K, P(const void*, A), lda, a_ps,
                                       P(const void*, B), ldb, b_ps, P(void*, C), ldc, P(const float*, bias), epi,
                                       beta, P(void*, aux), ldaux, P(float*, part), P(float*, colsum), colsum_acc,
-                                      ksplit, P(float*, slab), slab_floats, variant, ST(st));
+                                      ksplit, P(float*, slab), slab_floats, variant, ST(st), mv);
     if (rc == 0) check_launch("gemm_planes");
     return rc;
-  });
+  }, py::arg("planes"), py::arg("c_dtype"), py::arg("ta"), py::arg("tb"), py::arg("M"), py::arg("N"), py::arg("K"),
+     py::arg("A"), py::arg("lda"), py::arg("a_ps"), py::arg("B"), py::arg("ldb"), py::arg("b_ps"), py::arg("C"),
+     py::arg("ldc"), py::arg("bias"), py::arg("epi"), py::arg("beta"), py::arg("aux"), py::arg("ldaux"),
+     py::arg("part"), py::arg("colsum"), py::arg("colsum_acc"), py::arg("ksplit"), py::arg("slab"),
+     py::arg("slab_floats"), py::arg("variant"), py::arg("st"), py::arg("mv") = 0);
   m.def("set_planes_variant", &set_planes_variant, "plane GEMM variant: 0 default, 1 one LDS stage, 2 half K depth");
   m.def("pool_nsp_fwd", [](int dt, i64 seq, int B, int S, int H, i64 Wp, i64 bp, i64 Wn, i64 bn, i64 label,
                            i64 mlm_loss, i64 pooled, i64 logits, i64 lse, i64 stats, i64 total, i64 st) {

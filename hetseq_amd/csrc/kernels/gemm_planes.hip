@@ -59,6 +59,7 @@ struct PlanesArgs {
   int M, N, K, ksplit;
   float beta;
   int slice_major;  // split-K block order (see gemm.hip): 1 = slice-major
+  int Mv;           // valid rows of a padded problem (fp32 C, plain / bias epilogue): rows from Mv on are not written
 };
 
 // LDS image geometry of one operand plane (128 x BK bf16 elements either way).
@@ -381,6 +382,22 @@ __global__ void __launch_bounds__(64 * WV, (planes_waves_per_simd<P, BK, STAGES,
     }
     return;
   }
+  if (EPI <= kPEpiBias && m0 + kPB > p.Mv) {  // a tile reaching past the valid rows (padded problems only)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn + 32 * j + lr;
+      const float bv = EPI != kPEpiNone ? p.bias[n] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int64_t m = m0 + wm + 32 * i + acc_row(r, q);
+          if (m < p.Mv)
+            store_c(C + m * p.ldc + n, acc[i][j][r] + bv + (p.beta != 0.f ? p.beta * load_c(C + m * p.ldc + n) : 0.f));
+        }
+    }
+    return;
+  }
   float csum[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) csum[j] = 0.f;
@@ -512,8 +529,12 @@ int launch_gemm_planes(int planes, int c_dtype, int ta, int tb, int M, int N, in
                        int64_t a_ps, const void* B, int64_t ldb, int64_t b_ps, void* C, int64_t ldc,
                        const float* bias, int epi, float beta, void* aux, int64_t ldaux, float* part,
                        float* colsum_out, int colsum_acc, int ksplit, float* slab, int64_t slab_floats,
-                       int variant, hipStream_t st) {
-  if (planes != 1) return -1;  // (the split-fp32 P = 3 engine was retired for h3p, gemm_h3p.hip)
+                       int variant, hipStream_t st, int Mv) {
+  if (planes != 1) return -1;
+  // Mv (0: M): valid rows of a padded problem -- fp32 C, plain / bias epilogue; C rows from Mv on are
+  // neither read nor written (the tied decoder's weight gradient over the padded vocabulary)
+  Mv = Mv > 0 ? Mv : M;
+  if (Mv > M || (Mv < M && (c_dtype || epi > 1))) return -1;  // (the split-fp32 P = 3 engine was retired for h3p, gemm_h3p.hip)
   // variant (tile K depth, LDS stages, waves): 0 = two stages, 4 waves; 1 = one stage; 2 = half
   // depth; 3 = 8 waves; 4 = 8 waves + one stage.  < 0: the process default (set_planes_variant)
   if (variant < 0) variant = g_planes_variant;
@@ -536,7 +557,7 @@ int launch_gemm_planes(int planes, int c_dtype, int ta, int tb, int M, int N, in
   const int64_t spanB = 2 * ((planes - 1) * b_ps + (int64_t)(tb ? N : K) * ldb);
   if (spanA >= (1ll << 32) || spanB >= (1ll << 32)) return -1;
   PlanesArgs a{static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), C, bias, aux, part, slab,
-               lda, ldb, ldc, ldaux, a_ps, b_ps, M, N, K, ksplit, beta, g_planes_slice_major};
+               lda, ldb, ldc, ldaux, a_ps, b_ps, M, N, K, ksplit, beta, g_planes_slice_major, Mv};
   int rc;
 #define HS_CFG(P_, BK_, S_, W_)                                                        \
   (c_dtype ? launch_planes_cfg<P_, BK_, S_, W_, bf16_t>(ta, tb, epi, a, st) \
@@ -550,7 +571,7 @@ int launch_gemm_planes(int planes, int c_dtype, int ta, int tb, int M, int N, in
     hipLaunchKernelGGL(splitk_reduce_bf16_kernel, dim3((int)std::min<int64_t>((units + 255) / 256, 2048)), dim3(256),
                        0, st, slab, ksplit, M, N, static_cast<bf16_t*>(C), ldc, epi == 1 ? bias : nullptr, beta);
   } else if (ksplit > 1) {
-    launch_splitk_reduce(slab, ksplit, M, N, static_cast<float*>(C), ldc, epi == 1 ? bias : nullptr, beta, M, N, st);
+    launch_splitk_reduce(slab, ksplit, M, N, static_cast<float*>(C), ldc, epi == 1 ? bias : nullptr, beta, Mv, N, st);
   }
   if (epi == kPEpiDGelu) {
     const float* parts[1] = {part};

@@ -875,6 +875,9 @@ class BertModel(BertPreTrainedModel):
 # the masked-LM head's products on the h3p engine (BertForPreTraining._head_h3p); False: the per-tensor
 # h3 engine (A/B: bench.py --ab head_h3p,head_h3)
 HEAD_H3P = True
+# bf16: the tied decoder's products on the plane kernels over the padded vocabulary
+# (BertForPreTraining._head_bf16_pad); False: those three products on the library
+HEAD_BF16_PAD = True
 
 
 def _xent(logits, target, ignore_index=-100):
@@ -982,6 +985,49 @@ class BertForPreTraining(BertPreTrainedModel):
                 cached["stamp"][k] = now
         return cached["planes"]
 
+    def _head_bf16_pad(self):
+        """bf16 engine: the tied decoder's bf16 weight copied into a [pad512(V), H] buffer whose rows past
+        V are zero, plus an fp32 bias buffer of pad512(V) (zero past V): the hand-written plane kernels
+        tile only multiples of 128, so the vocabulary products run padded instead of on the library.
+        The copy is refreshed right after every update of the word table's chunk (its update hook, on
+        the updating stream), else here when stale.  None: another engine or a CPU model."""
+        from hetseq_amd.ops import gemm as G
+
+        wd = self.cls.predictions.decoder.weight
+        V, H = wd.shape
+        if not (HEAD_BF16_PAD and self.compute_dtype == torch.bfloat16 and wd.is_cuda and H % 128 == 0
+                and G.gemm_mode() != "blas"):
+            return None
+        store = getattr(self, "_hs_store", None)
+        cached = self.__dict__.get("_hs_head_bf16")
+        if cached is None or cached["store"] is not store:
+            Vp = (V + 511) // 512 * 512
+            cached = {"store": store, "w": torch.zeros((Vp, H), dtype=torch.bfloat16, device=wd.device),
+                      "b": torch.zeros(Vp, dtype=torch.float32, device=wd.device), "stamp": None}
+            self.__dict__["_hs_head_bf16"] = cached
+            if store is not None and store.chunks is not None:
+                from hetseq_amd.runtime.flat import bisect_chunk
+
+                store.add_update_hook(bisect_chunk(store.chunks, store.offset(wd)), self._head_bf16_hook(cached))
+        now = store.stamp() if store is not None else None
+        if now is None or cached["stamp"] != now:
+            if store is not None:
+                store.params_ready()
+            cached["w"][:V].copy_(self._mlm_weights()[1])
+            cached["stamp"] = now
+        return cached["w"], cached["b"]
+
+    def _head_bf16_hook(self, cached):
+        store = cached["store"]
+
+        def hook():
+            if self.__dict__.get("_hs_head_bf16") is not cached or self.compute_dtype != torch.bfloat16:
+                return
+            wd = self.cls.predictions.decoder.weight
+            cached["w"][:wd.shape[0]].copy_(store.shadow_view(wd))
+            cached["stamp"] = store.stamp()
+        return hook
+
     def _head_h3p_hook(self, cached, k):
         store = cached["store"]
 
@@ -1016,13 +1062,14 @@ class BertForPreTraining(BertPreTrainedModel):
         B, S = input_ids.shape
         wt_, wd_ = self._mlm_weights()
         head_hp = self._head_h3p()
+        head_bf = self._head_bf16_pad() if head_hp is None else None
         head_w = (wt_, wd_) if isinstance(wt_, torch.Tensor) and wt_.dtype == torch.float32 and head_hp is None else ()
         pool, plan = self.bert._amax_plan(extra_weights=head_w, extra_slots=3)
         seq2d = self.bert.fused_encoder(input_ids, token_type_ids, attention_mask, checkpoint_activations,
                                         amax=(pool, plan))
         cap = B * S if self.max_predictions_per_seq is None else min(B * S, B * int(self.max_predictions_per_seq))
-        if head_hp is not None:  # (rows past the labelled ones are zero rows with label -1: no loss, no gradient)
-            cap = (cap + 127) // 128 * 128
+        if head_hp is not None or head_bf is not None:
+            cap = (cap + 127) // 128 * 128  # (rows past the labelled ones: zero rows, label -1, no loss / gradient)
         t, pred = self.cls.predictions.transform, self.cls.predictions
         pooler, nsp = self.bert.pooler.dense_act, self.cls.seq_relationship
         params = [t.dense_act.weight, t.dense_act.bias, t.LayerNorm.weight, t.LayerNorm.bias, pred.decoder.weight,
@@ -1030,6 +1077,8 @@ class BertForPreTraining(BertPreTrainedModel):
         meta = {"cap": cap, "eps": t.LayerNorm.variance_epsilon, "weights": self._mlm_weights, "B": B, "S": S}
         if head_hp is not None:
             meta["h3p"] = head_hp
+        if head_bf is not None:
+            meta["bf16pad"] = head_bf
         if pool is not None and head_w:
             L = len(plan)
             last = plan[-1]

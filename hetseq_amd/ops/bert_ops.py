@@ -1167,8 +1167,18 @@ class FusedPreTrainingLoss(torch.autograd.Function):
             t2, z, mean, rstd = ln_fwd(t1, g, b, eps, amax=am["t2"] if am else None)
             # tied decoder on the compacted rows; fp32: the padded split kernel (logits is a view of a
             # zero-padded buffer the backward reuses); bf16: the plane engine
+            bfp = meta.get("bf16pad")  # bf16: (the tied decoder's weight padded to pad512(V) rows, bias buffer)
             if t2.dtype == torch.float32:
                 logits, lbuf = G.decoder_logits(t2, Wd, bdec, amax=(am["t2"], am["wd"]) if am else None)
+            elif bfp is not None:
+                # the plane kernels over the padded vocabulary (zero weight rows, zero bias past V): no
+                # library GEMM in the bf16 step; logits is a view of the zero-padded buffer
+                wdp, bpad = bfp  # (not `bp`: that name is the pooler bias below)
+                V = Wd.shape[0]
+                bpad[:V].copy_(bdec)
+                lbuf = torch.empty((t2.shape[0], wdp.shape[0]), dtype=torch.float32, device=seq.device)
+                G.gemm(t2, wdp, tb=True, out=lbuf, bias=bpad, epi=1)
+                logits = lbuf[:, :V]
             else:
                 logits, lbuf = G.gemm(t2, Wd, tb=True, bias=bdec, epi=1, out_dtype=torch.float32), None
         out, lse = xent_fwd(logits, lab)
@@ -1183,6 +1193,7 @@ class FusedPreTrainingLoss(torch.autograd.Function):
                            nsp_logits.data_ptr(), nsp_lse.data_ptr(), stats.data_ptr(), stats[2:].data_ptr(),
                            stream_handle())
         ctx.padded = lbuf is not None
+        ctx.bfp = meta.get("bf16pad") if (hpw is None and lbuf is not None and t2.dtype == torch.bfloat16) else None
         ctx.save_for_backward(idx, lab, hsel, t1pre, t1, z, mean, rstd, t2,
                               lbuf if lbuf is not None else logits, lse, out, g, bt, seq, nsp_labels, pooled,
                               nsp_logits, nsp_lse, stats, wp, wn)
@@ -1210,6 +1221,9 @@ class FusedPreTrainingLoss(torch.autograd.Function):
         # bf16 mode: both decoder GEMMs take bf16 operands (fp32 C for the weight gradient);
         # the fp32-operand weight GEMM cost 268 us vs 72 us (tools/bench_mlm_head.py)
         dl_c = dlogits.to(t2.dtype) if t2.dtype != torch.float32 else dlogits
+        bfp = ctx.bfp
+        if bfp is not None:  # bf16 padded decoder: the loss gradient over the padded vocabulary (pad columns zero)
+            dl_c = lbuf.to(torch.bfloat16)
         # parameter gradients on the weight-gradient stream when they go to the flat store (the
         # decoder one lands in the tied word-embedding gradient: FusedEmbedding.backward waits)
         side = acc and streams.enabled()
@@ -1232,6 +1246,12 @@ class FusedPreTrainingLoss(torch.autograd.Function):
                 out_w = Gv[4] if acc else torch.zeros((V, t2.shape[1]), dtype=torch.float32, device=t2.device)
                 return h3p.gemm(dlp, t2p, ta=True, out=out_w, beta=1.0 if dec_acc else 0.0, valid=(V, t2.shape[1]),
                                 site="decoder wgrad")
+        elif bfp is not None:  # bf16 plane kernels over the padded vocabulary (C rows past V untouched)
+            def dwdec():
+                if acc and store is not None:
+                    (store.ensure_zero if dec_acc else store.mark_stored)(Gv[4])
+                out_w = Gv[4] if acc else torch.zeros((V, t2.shape[1]), dtype=torch.float32, device=t2.device)
+                return G.decoder_wgrad_bf16(dl_c, t2, V, out_w, accumulate=dec_acc or not acc)
         elif lbuf is not None:  # padded split-bf16 decoder products (pad columns of dlogits stay zero)
             def dwdec():
                 if acc and store is not None:  # lazy zero_grad bookkeeping, on the writer's stream
@@ -1266,6 +1286,8 @@ class FusedPreTrainingLoss(torch.autograd.Function):
                 h.dense_ready(dl_c.device)
         if hpw is not None:  # K = the padded vocabulary over 30 output tiles: 16 K slices
             dt2 = h3p.gemm(dlp, Wdp, ksplit=_dec_dgrad_ks(dlp.cols), site="decoder dgrad")
+        elif bfp is not None:  # K = the padded vocabulary (zero rows / columns past V)
+            dt2 = G.gemm(dl_c, bfp[0])
         elif lbuf is not None:
             dt2 = G.decoder_dgrad(lbuf, Wd, V, amax=(am_dl, am["wd"]) if am_dl is not None else None)
         else:

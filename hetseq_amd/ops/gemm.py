@@ -49,6 +49,11 @@ _SLABS: dict = {}  # (device, stream) -> split-K partial-sum workspace
 EPI_NONE, EPI_BIAS, EPI_GELU, EPI_DGELU = 0, 1, 2, 3
 
 
+def gemm_mode():
+    """'hip' (the hand-written kernels) or 'blas' (the library oracle)."""
+    return _MODE
+
+
 def set_mode(mode):
     global _MODE
     assert mode in ("hip", "blas")
@@ -246,13 +251,14 @@ def _as_planes(x):
 
 
 def gemm_planes(a, b, ta, tb, out, bias=None, epi=EPI_NONE, beta=0.0, aux=None, part=None, colsum=None,
-                colsum_acc=False, ksplit=1, variant=-1):
+                colsum_acc=False, ksplit=1, variant=-1, mv=0):
     """Launch the bf16-plane engine on Planes operands; False (nothing launched) if not served.
     ``variant``: kernel variant (gemm_planes.hip: 0 two LDS stages, 1 one stage, 2 half K depth,
-    3 eight waves, 4 eight waves + one stage); -1 = :func:`planes_variant`."""
+    3 eight waves, 4 eight waves + one stage); -1 = :func:`planes_variant`.  ``mv`` > 0: the valid
+    rows of a padded problem (fp32 ``out`` of ``mv`` rows, plain / bias epilogue)."""
     M, N, K = _dims(a, b, ta, tb)
     if out is None or a.P != b.P or not out.is_cuda or out.stride(1) != 1 or \
-            out.dtype not in (torch.float32, torch.bfloat16) or out.shape != (M, N):
+            out.dtype not in (torch.float32, torch.bfloat16) or out.shape != ((mv or M), N):
         return False
     slab = _slab(M, N, ksplit, out.device) if ksplit > 1 else None
     if ksplit > 1 and slab is None:
@@ -265,7 +271,7 @@ def gemm_planes(a, b, ta, tb, out, bias=None, epi=EPI_NONE, beta=0.0, aux=None, 
                            aux.data_ptr() if aux is not None else 0, aux.stride(0) if aux is not None else 0,
                            part.data_ptr() if part is not None else 0, colsum.data_ptr() if colsum is not None else 0,
                            int(colsum_acc), int(ksplit), slab.data_ptr() if slab is not None else 0,
-                           slab.numel() if slab is not None else 0, int(variant), stream_handle())
+                           slab.numel() if slab is not None else 0, int(variant), stream_handle(), mv=int(mv))
     return rc == 0
 
 
@@ -302,8 +308,9 @@ def _bf16_choice(key, pa, pb, ta, tb, out, bias, epi, beta, ks, out_dtype):
         M, N, K = _dims(pa, pb, ta, tb)
         splits = [ks]
         if not ta and epi in (EPI_NONE, EPI_BIAS) and (M // 128) * (N // 128) < 384:
-            # a grid under 1.5 blocks per CU (the N = 768 products): also try K slices
-            splits = [s for s in (1, 2, 4) if K % (64 * s) == 0]
+            # a grid under 1.5 blocks per CU (the N = 768 products): also try K slices (up to 16 for a
+            # long K: the tied decoder's data gradient, K = the padded vocabulary over ~30 tiles)
+            splits = [s for s in ((1, 2, 4, 8, 16) if K >= 8192 else (1, 2, 4)) if K % (64 * s) == 0]
         best = None
         for s in splits:
             for v in (0, 1, 3, 4):
@@ -563,6 +570,21 @@ def decoder_wgrad(dlogits_buf, t2, V, out, accumulate, amax=None):
         return out
     run_blas(out)
     return out
+
+
+def decoder_wgrad_bf16(dl_p, t2, V, out, accumulate):
+    """bf16 engine: dW [V, H] (+)= dlogits^T @ t2 with dlogits the zero-padded [R, pad512(V)] bf16 copy
+    of the loss gradient -- the plane kernels over the padded rows, C rows past V neither read nor
+    written (fp32 ``out``).  The library (``torch.mm``) in 'blas' mode or for a shape not served."""
+    beta = 1.0 if accumulate else 0.0
+    if _MODE != "blas":
+        pa, pb = _as_planes(dl_p), _as_planes(t2)
+        if pa is not None and pb is not None:
+            Vp, H, R = dl_p.shape[1], t2.shape[1], t2.shape[0]
+            if gemm_planes(pa, pb, True, False, out, beta=beta, ksplit=_planes_ksplit(Vp, H, R, 1), mv=V):
+                return out
+    prod = torch.mm(dl_p[:, :V].t(), t2).float()
+    return out.add_(prod) if accumulate else out.copy_(prod)
 
 
 def _choose_padded(key, run_hip, run_blas):

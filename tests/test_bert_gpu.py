@@ -232,6 +232,57 @@ def test_bf16_mode_runs_and_tracks_fp32(cuda):
     assert torch.isfinite(store.grad).all()
 
 
+def test_bf16_padded_decoder_matches_library(cuda):
+    """bf16: the tied decoder's three products on the plane kernels over the padded vocabulary
+    (BertForPreTraining._head_bf16_pad) give the loss and gradients of the library products on the
+    unpadded shapes, to bf16 rounding -- and the padded weight copy follows the updates."""
+    import hetseq_amd.models.bert as MB
+    from hetseq_amd.runtime.flat import FlatParamStore
+
+    model, cfg = _tiny(cuda)
+    model.eval()
+    # cap = 4 x 32 = 128 rows in both runs (no row padding of its own): the MLM transform's products run
+    # on the same kernels either way, so only the three decoder products differ between the runs
+    model.max_predictions_per_seq = 32
+    ref = copy.deepcopy(model)
+    stores = []
+    for m in (model, ref):
+        st = FlatParamStore(m, shadow_dtype=torch.bfloat16)
+        m.attach_store(st, torch.bfloat16)
+        stores.append(st)
+    batch = _batch(cuda, 4, 128, cfg.vocab_size)
+    old = MB.HEAD_BF16_PAD
+    try:
+        MB.HEAD_BF16_PAD = True
+        l1 = model(*batch)
+        l1.backward()
+        assert model.__dict__.get("_hs_head_bf16") is not None
+        MB.HEAD_BF16_PAD = False
+        l2 = ref(*batch)
+        l2.backward()
+    finally:
+        MB.HEAD_BF16_PAD = old
+    assert abs(l1.item() - l2.item()) <= 2e-3 * abs(l2.item()), (l1.item(), l2.item())
+    g1, g2 = stores[0].grad.double(), stores[1].grad.double()
+    assert torch.isfinite(g1).all()
+    # per parameter, relative to its largest entry floored at 1 % of the model's largest gradient entry:
+    # the two runs round differently in bf16 (fp32 accumulation order of the decoder products, then the
+    # bf16 data gradient), and parameters whose gradient is that small hold mostly such noise
+    gmax = g2.abs().max().item()
+    worst, where = 0.0, None
+    for (n, p1), (_, p2) in zip(model.named_parameters(), ref.named_parameters()):
+        o1, o2 = stores[0].offset(p1), stores[1].offset(p2)
+        a, b = g1[o1:o1 + p1.numel()], g2[o2:o2 + p2.numel()]
+        r = (a - b).abs().max().item() / max(b.abs().max().item(), 1e-2 * gmax)
+        worst, where = (r, n) if r > worst else (worst, where)
+    assert worst <= 2e-2, (worst, where)
+    wd = model.cls.predictions.decoder.weight
+    off = stores[0].offset(wd)
+    n = wd.numel()
+    dg1, dg2 = g1[off:off + n], g2[off:off + n]
+    assert (dg1 - dg2).abs().max().item() <= 2e-2 * dg2.abs().max().item()  # the decoder's own gradient
+
+
 def test_base_model_param_count(cuda):
     from hetseq_amd.models.bert import BertConfig, BertForPreTraining
 

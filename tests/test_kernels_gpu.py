@@ -1313,6 +1313,33 @@ def test_gemm_planes_vs_fp64(cuda, ta, tb, M, N, K, ks, variant):
     assert err < 1e-5, err
 
 
+@pytest.mark.parametrize("ks", [1, 2])
+@pytest.mark.parametrize("beta", [0.0, 1.0])
+def test_gemm_planes_valid_rows(cuda, ks, beta):
+    """A padded weight-gradient product (the tied decoder over the padded vocabulary): M = 640 rows of
+    which the first 555 are valid -- C has only those rows, nothing past them is read or written."""
+    from hetseq_amd.ops import gemm as G
+
+    torch.manual_seed(67 + ks)
+    R, Mp, Mv, N = 256, 640, 555, 256
+    a = torch.randn(R, Mp, device=cuda)
+    a[:, Mv:] = 0.0  # (the loss gradient's pad columns are zero)
+    b = torch.randn(R, N, device=cuda)
+    guard = torch.full((Mv + 8, N), 7.0, device=cuda)  # rows past Mv: a canary
+    c0 = torch.randn(Mv, N, device=cuda)
+    out = guard[:Mv]
+    out.copy_(c0)
+    assert G.gemm_planes(_planes_operand(a, 1), _planes_operand(b, 1), True, False, out, beta=beta, ksplit=ks,
+                         mv=Mv)
+    ad, bd = a.bfloat16().double(), b.bfloat16().double()
+    ref = (ad.t() @ bd)[:Mv] + beta * c0.double()
+    _close(out, ref, 1e-5, 1e-4, "planes valid rows")
+    assert torch.equal(guard[Mv:], torch.full((8, N), 7.0, device=cuda))
+    # not served: a bf16 C or a GELU epilogue with fewer valid rows
+    assert not G.gemm_planes(_planes_operand(a, 1), _planes_operand(b, 1), True, False,
+                             torch.empty(Mv, N, device=cuda, dtype=torch.bfloat16), mv=Mv)
+
+
 @pytest.mark.parametrize("ks", [2, 4])
 @pytest.mark.parametrize("epi_bias,beta", [(False, 0.0), (True, 0.0), (True, 1.0)])
 def test_gemm_planes_bf16_splitk(cuda, ks, epi_bias, beta):
