@@ -553,9 +553,14 @@ _FWD_SPLIT = True
 _FWD_KS = None
 
 
+# bf16 compute: the same two half-batch chains (bench.py --ab fsplit_bf16_on / fsplit_bf16_off)
+_FWD_SPLIT_BF16 = True
+
+
 def _fwd_split_ok(x, mask, W, cfg):
     B, S = cfg[0], cfg[1]
-    return (_FWD_SPLIT and x.is_cuda and x.dtype == torch.float32
+    dt_ok = x.dtype == torch.float32 or (x.dtype == torch.bfloat16 and _FWD_SPLIT_BF16)
+    return (_FWD_SPLIT and x.is_cuda and dt_ok
             and B % 2 == 0 and B * S >= 1024 and streams.enabled() and x.is_contiguous())
 
 
@@ -567,14 +572,15 @@ def _layer_forward_split(x, mask, W, cfg, save, am=None):
     (s_a, o_a), (s_1, o_1), (s_2, o_2) = seeds
     rows, H = x.shape
     F = W.w1.shape[0]
-    dev, f32 = x.device, torch.float32
-    qkv = torch.empty((rows, 3 * H), dtype=f32, device=dev)
-    ctx_ = torch.empty((rows, H), dtype=f32, device=dev)
+    dev, f32, dt = x.device, torch.float32, x.dtype  # activations in the compute dtype, statistics fp32
+    qkv = torch.empty((rows, 3 * H), dtype=dt, device=dev)
+    ctx_ = torch.empty((rows, H), dtype=dt, device=dev)
     lse = torch.empty((B * NH * S,), dtype=f32, device=dev)
     dmask = torch.empty((B * NH * S * (S // 32),), dtype=torch.int32, device=dev) if p_a > 0 else None
-    h1, z1, h2, z2 = (torch.empty((rows, H), dtype=f32, device=dev) for _ in range(4))
+    h1, h2 = (torch.empty((rows, H), dtype=dt, device=dev) for _ in range(2))
+    z1, z2 = (torch.empty((rows, H), dtype=f32, device=dev) for _ in range(2))
     m1, r1, m2, r2 = (torch.empty((rows,), dtype=f32, device=dev) for _ in range(4))
-    f1, f1pre = torch.empty((rows, F), dtype=f32, device=dev), torch.empty((rows, F), dtype=f32, device=dev)
+    f1, f1pre = torch.empty((rows, F), dtype=dt, device=dev), torch.empty((rows, F), dtype=dt, device=dev)
     hr, hb = rows // 2, B // 2
     nl, nm = hb * NH * S, hb * NH * S * (S // 32)
     with streams.fwd_halves(dev) as halves:

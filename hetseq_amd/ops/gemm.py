@@ -683,8 +683,11 @@ def linear_gelu_fwd(x, w, b, out=None, amax=None, amax_out=None):
     T, N = x.shape[0], w.shape[0]
     px, pw = _as_planes(x), _as_planes(w)
     if px is not None and pw is not None and _MODE != "blas":  # bf16 operands
-        pre = torch.empty((T, N), dtype=torch.bfloat16, device=px.device)
-        y = torch.empty_like(pre)
+        if out is not None and all(t.dtype == torch.bfloat16 for t in out):
+            y, pre = out  # (row slices of whole-batch tensors: the half-batch forward chains)
+        else:
+            pre = torch.empty((T, N), dtype=torch.bfloat16, device=px.device)
+            y = torch.empty_like(pre)
         if gemm_planes(px, pw, False, True, y, b, EPI_GELU, 0.0, aux=pre):
             return y, pre
         x, w = _unplane(x), _unplane(w)
