@@ -535,6 +535,8 @@ _AB = {
     "fks4": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FWD_KS", 4),
     "fsplit_on": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FWD_SPLIT", True),  # half-batch forward chains
     "fsplit_off": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FWD_SPLIT", False),
+    "defer_on": lambda: setattr(__import__("hetseq_amd.parallel.ddp", fromlist=["x"]).FlatDDP, "DEFER_LAST_EARLY", True),
+    "defer_off": lambda: setattr(__import__("hetseq_amd.parallel.ddp", fromlist=["x"]).FlatDDP, "DEFER_LAST_EARLY", False),
     "fsplit_bf16_on": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FWD_SPLIT_BF16", True),  # bf16 half-batch chains
     "fsplit_bf16_off": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FWD_SPLIT_BF16", False),
     "wks2": lambda: _set_side_ks(2, 4),  # side-stream weight-gradient K split (default), small products 4

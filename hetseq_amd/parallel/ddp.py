@@ -193,18 +193,42 @@ class FlatDDP(torch.nn.Module):
 
     early = []  # bucket indices reduced behind the fused backward's group events (backward order)
 
+    # The early layer's last group (QKV) is complete only after the weight-gradient stream's last
+    # products, ~40 us after the embedding backward's rows are ready; the comm stream runs in issue
+    # order, so its reduce-scatter issued first held the rows' all-gather (the step's largest tail
+    # collective) behind it.  With the sparse table exchange armed that group is deferred until the
+    # rows' all-gather is enqueued (parallel/tied.py rows_ready -> launch_deferred_early).
+    DEFER_LAST_EARLY = True
+
     def _early_launch(self):
         """Right after the early layer's fused backward was enqueued (ops/bert_ops.py): reduce its
         gradient groups, each behind the event the backward recorded when the group was complete."""
         if not self.require_sync:
             return
+        defer = self.DEFER_LAST_EARLY and self.tables is not None and self.tables.armed
         for k, b in enumerate(self.early):
             if self.next_launch != b:  # (an earlier bucket is not out yet: the hooks launch in order)
                 return
-            lo, hi = self.ranges[b]
-            self.comm.wait_events([self._early_ev[k]])
-            self._launch_range(lo, hi, "reducescatter_group%d" % b, producers=None)
-            self.next_launch += 1
+            if defer and k == len(self.early) - 1:
+                self._deferred_early = k
+                return
+            self._launch_early(k)
+
+    def _launch_early(self, k):
+        b = self.early[k]
+        lo, hi = self.ranges[b]
+        self.comm.wait_events([self._early_ev[k]])
+        self._launch_range(lo, hi, "reducescatter_group%d" % b, producers=None)
+        self.next_launch += 1
+
+    def launch_deferred_early(self):
+        """The deferred early group (see DEFER_LAST_EARLY), then any bucket that became ready behind it."""
+        k = self._deferred_early
+        if k is None:
+            return
+        self._deferred_early = None
+        self._launch_early(k)
+        self._launch_ready()
 
     def _reset_state(self):
         self.pending = [len(ps) for ps in self.buckets]
@@ -216,6 +240,7 @@ class FlatDDP(torch.nn.Module):
         # kernel, bytes each rank RECEIVES over the links)
         self.comm_log = []
         self._in_tail = False
+        self._deferred_early = None
 
     def _log(self, what, t, kind="allreduce"):
         n = t.numel() * t.element_size()
@@ -273,6 +298,8 @@ class FlatDDP(torch.nn.Module):
 
     def _launch_ready(self):
         while self.next_launch < len(self.buckets) and self.ready[self.next_launch]:
+            if self._deferred_early is not None and self.next_launch == self.early[self._deferred_early]:
+                return  # (held back behind the rows' all-gather: launch_deferred_early)
             self._launch(self.next_launch)
             self.next_launch += 1
 
@@ -312,6 +339,7 @@ class FlatDDP(torch.nn.Module):
             self.works.append(work)
 
     def _finalize(self):
+        self.launch_deferred_early()
         if self.next_launch < len(self.buckets):
             missing = [i for i in range(len(self.buckets)) if not self.ready[i]]
             if missing and not self.find_unused_parameters:

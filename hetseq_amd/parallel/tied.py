@@ -260,6 +260,7 @@ class SparseTableSync(object):
                                                           async_op=True))
         profiling.range_pop()
         self.rows_launched = True
+        self.ddp.launch_deferred_early()  # (the early layer's last group, held back behind these rows)
 
     def launch_pending(self):
         """End of backward, before the engine's waits: the dense fallback when no rows came."""
