@@ -535,6 +535,10 @@ _AB = {
     "fks4": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FWD_KS", 4),
     "fsplit_on": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FWD_SPLIT", True),  # half-batch forward chains
     "fsplit_off": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FWD_SPLIT", False),
+    "stag0": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FWD_STAGGER", 0),  # forward chains in phase
+    "stag1": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FWD_STAGGER", 1),  # ... second after the QKV product
+    "stag2": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FWD_STAGGER", 2),  # ... after the attention
+    "stag3": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FWD_STAGGER", 3),  # ... after the first LayerNorm
     "defer_on": lambda: setattr(__import__("hetseq_amd.parallel.ddp", fromlist=["x"]).FlatDDP, "DEFER_LAST_EARLY", True),
     "defer_off": lambda: setattr(__import__("hetseq_amd.parallel.ddp", fromlist=["x"]).FlatDDP, "DEFER_LAST_EARLY", False),
     "fsplit_bf16_on": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FWD_SPLIT_BF16", True),  # bf16 half-batch chains

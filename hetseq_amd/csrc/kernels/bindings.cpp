@@ -207,7 +207,7 @@ static void stream_wait(hipStream_t waiter, hipStream_t signal) { hs_stream_wait
 // layer_prog.cpp
 std::vector<std::string> layer_plan_fields();
 void layer_fwd_h3p(int64_t, int64_t, int64_t, int64_t, int64_t, uint64_t, uint64_t, uint64_t, uint64_t, uint64_t,
-                   uint64_t, float, float, float, int64_t, int64_t, int64_t, int64_t);
+                   uint64_t, float, float, float, int64_t, int64_t, int64_t, int64_t, int);
 void layer_bwd_h3p(int64_t, int64_t, int64_t, int64_t, int64_t, uint64_t, uint64_t, uint64_t, uint64_t, float, float,
                    int, int64_t, int64_t, int64_t);
 
@@ -222,11 +222,15 @@ PYBIND11_MODULE(_hip, m) {
 
   m.def("layer_plan_fields", &layer_plan_fields, "field names of a layer program's int64 plan (layer_prog.cpp)");
   m.def("layer_fwd_h3p", [](i64 plan, i64 x, i64 xp, i64 xe, i64 mask, u64 sa, u64 oa, u64 s1, u64 o1, u64 s2, u64 o2,
-                            float eps, float p_h, float p_a, i64 st0, i64 st1, i64 amax0, i64 amax1) {
+                            float eps, float p_h, float p_a, i64 st0, i64 st1, i64 amax0, i64 amax1, int stagger) {
     pre_launch("layer_fwd_h3p");
-    layer_fwd_h3p(plan, x, xp, xe, mask, sa, oa, s1, o1, s2, o2, eps, p_h, p_a, st0, st1, amax0, amax1);
+    layer_fwd_h3p(plan, x, xp, xe, mask, sa, oa, s1, o1, s2, o2, eps, p_h, p_a, st0, st1, amax0, amax1, stagger);
     check_launch("layer_fwd_h3p");
-  }, "one fused encoder-layer forward on the h3p engine from its plan (ops/layer_prog.py)");
+  }, "one fused encoder-layer forward on the h3p engine from its plan (ops/layer_prog.py); stagger: the second "
+     "chain starts after the first chain's QKV product (1), attention (2) or first LayerNorm (3)",
+     py::arg("plan"), py::arg("x"), py::arg("xp"), py::arg("xe"), py::arg("mask"), py::arg("sa"), py::arg("oa"),
+     py::arg("s1"), py::arg("o1"), py::arg("s2"), py::arg("o2"), py::arg("eps"), py::arg("p_h"), py::arg("p_a"),
+     py::arg("st0"), py::arg("st1"), py::arg("amax0"), py::arg("amax1"), py::arg("stagger") = 0);
   m.def("layer_bwd_h3p", [](i64 plan, i64 dh2, i64 xp, i64 xe, i64 mask, u64 s1, u64 o1, u64 s2, u64 o2, float p_h,
                             float p_a, int wacc, i64 st0, i64 st1, i64 events) {
     pre_launch("layer_bwd_h3p");

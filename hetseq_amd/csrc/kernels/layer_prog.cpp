@@ -132,10 +132,13 @@ std::vector<std::string> layer_plan_fields() {
 
 // One layer forward.  x: the layer input [rows, H] fp32; xp / xe: its h3p planes / exponents (the
 // plan holds their layout); mask [B, S] int64; seeds (a: attention, 1 / 2: the two LayerNorms);
-// amax0 / amax1: |max| slots of each half's output (0: none).
+// amax0 / amax1: |max| slots of each half's output (0: none).  stagger (the chains' first layer): the
+// second chain waits for the first chain's QKV product (1), attention (2) or first LayerNorm (3), so
+// the two chains run out of phase -- one chain's latency-bound attention / LayerNorm beside the other
+// chain's GEMMs instead of both chains' attention at once.
 void layer_fwd_h3p(int64_t plan, int64_t x, int64_t xp, int64_t xe, int64_t mask, uint64_t sa, uint64_t oa,
                    uint64_t s1, uint64_t o1, uint64_t s2, uint64_t o2, float eps, float p_h, float p_a, int64_t st0,
-                   int64_t st1, int64_t amax0, int64_t amax1) {
+                   int64_t st1, int64_t amax0, int64_t amax1, int stagger) {
   const int64_t* q = ptr<const int64_t>(plan);
   const int B = (int)q[f_B], S = (int)q[f_S], NH = (int)q[f_NH], H = (int)q[f_H], F = (int)q[f_F];
   const int rows = (int)q[f_rows], nh = (int)q[f_halves];
@@ -152,12 +155,15 @@ void layer_fwd_h3p(int64_t plan, int64_t x, int64_t xp, int64_t xe, int64_t mask
     float* qkv = ptr<float>(q[f_qkv]) + r0 * 3 * H;
     gemm(0, 1, hr, 3 * H, H, X.rows_from(r0), Wqkv, qkv, 3 * H, nullptr, 0, 0.f, nullptr, 0, nullptr, nullptr, 0,
          nullptr, 1, nullptr, 0, st, "qkv forward");
+    const bool stag = h == 0 && nh > 1 && st1 != 0;
+    if (stag && stagger == 1) hs_stream_wait(ptr<ihipStream_t>(st1), st);
     const HPv cp = ctxp.rows_from(r0);
     req(launch_attn_fwd_h3(qkv, ptr<const int64_t>(mask) + (int64_t)h * hb * S, ptr<const float>(q[f_bqkv]),
                            ptr<float>(q[f_ctx]) + r0 * H, ptr<float>(q[f_lse]) + h * nl,
                            q[f_dmask] ? ptr<uint32_t>(q[f_dmask]) + h * nm : nullptr, hb, S, NH, 64, p_a, sa, oa, st,
                            h * hb * NH, nullptr, ptr<void>(cp.p), cp.ps, ptr<int8_t>(cp.e)),
         "attention forward");
+    if (stag && stagger == 2) hs_stream_wait(ptr<ihipStream_t>(st1), st);
     const int ks_wo = (int)q[f_ks_wo], ks_w2 = (int)q[f_ks_w2];
     gemm_slabs(hr, H, H, cp, Wo, ks_wo, slab, slab_floats, st, "attention-output forward");
     const HPv p1 = h1p.rows_from(r0);
@@ -168,6 +174,7 @@ void layer_fwd_h3p(int64_t plan, int64_t x, int64_t xp, int64_t xe, int64_t mask
                           nullptr, ptr<void>(p1.p), p1.ps, ptr<int8_t>(p1.e), ptr<uint32_t>(q[f_psync_f]),
                           (int)(r0 / 32), st),
         "LayerNorm 1 forward");
+    if (stag && stagger == 3) hs_stream_wait(ptr<ihipStream_t>(st1), st);
     const HPv pf = f1p.rows_from(r0);
     gemm(0, 1, hr, F, H, p1, W1, nullptr, F, ptr<const float>(q[f_bi]), kEpiGelu, 0.f,
          ptr<float>(q[f_f1pre]) + r0 * F, F, nullptr, nullptr, 0, &pf, 1, nullptr, 0, st, "FFN-in forward");

@@ -661,6 +661,9 @@ class _OneChain(object):
 
 # the native launch path (ops/layer_prog.py): False runs the Python layer (A/B, bench --ab prog_off)
 LAYER_PROG = True
+# the second half-batch chain's start in the first layer (layer_prog.cpp layer_fwd_h3p stagger):
+# 0 with the first chain, 1 / 2 / 3 after its QKV product / attention / first LayerNorm
+_FWD_STAGGER = 0
 PROG_BUILDS = [0]  # programs built in this process (tests)
 _PROG_SIDE_DELAY = 0  # GPU cycles the side stream sleeps before a program backward (tests only)
 
@@ -709,15 +712,18 @@ def _layer_forward_prog(prog, x, mask, W, cfg, am, halves_ok):
     dev = x.device
     xp = h3p.of(x)
     prog.set_input_layout(xp)
+    stagger = 0
     if halves_ok:
+        fresh = streams.chain_stream() is None  # (the chains' first layer: the fork happens here)
         st1 = streams.chain_fork(dev).cuda_stream
+        stagger = _FWD_STAGGER if fresh else 0
     else:
         streams.chain_join(dev)
         st1 = 0
     am0 = G.slot_ptr(am.a(6)) if am is not None else 0
     am1 = G.slot_ptr(am.a(7)) if am is not None and halves_ok else 0
     hip().layer_fwd_h3p(prog.addr, x.data_ptr(), xp.data_ptr(), xp.exps_ptr(), mask.data_ptr(), s_a, o_a, s_1, o_1,
-                        s_2, o_2, float(eps), float(p_h), float(p_a), stream_handle(), st1, am0, am1)
+                        s_2, o_2, float(eps), float(p_h), float(p_a), stream_handle(), st1, am0, am1, stagger=stagger)
     streams.chain_keep(x, mask, xp.planes, xp.exps)
     h2 = prog.h2.view(prog.rows, prog.H)
     h3p.remember(h2, prog.h2p)  # the next layer's QKV operand

@@ -1,7 +1,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
-J=j22
-timeout -k 10 600 python3 -u -m pytest -x -q --timeout 180 --timeout-method thread tests/test_comm_gpu.py -m gpu > gpurun_out/${J}_tests.log 2>&1 || { tail -60 gpurun_out/${J}_tests.log; exit 1; }
+J=j23
+timeout -k 10 600 python3 -u -m pytest -x -q --timeout 180 --timeout-method thread tests/test_layer_prog_gpu.py -m gpu > gpurun_out/${J}_tests.log 2>&1 || { tail -60 gpurun_out/${J}_tests.log; exit 1; }
 tail -2 gpurun_out/${J}_tests.log
-timeout -k 10 600 python3 -u bench.py --steps 10 --warmup 5 --emulate-world 8 --ab defer_on,defer_off --ab-rounds 6 > gpurun_out/${J}_ab.log 2>&1 || { tail -20 gpurun_out/${J}_ab.log; exit 1; }
+timeout -k 10 600 python3 -u bench.py --steps 10 --warmup 5 --ab stag0,stag1,stag2,stag3 --ab-rounds 6 > gpurun_out/${J}_ab.log 2>&1 || { tail -20 gpurun_out/${J}_ab.log; exit 1; }
 tail -1 gpurun_out/${J}_ab.log
