@@ -539,6 +539,8 @@ _AB = {
     "stag1": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FWD_STAGGER", 1),  # ... second after the QKV product
     "stag2": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FWD_STAGGER", 2),  # ... after the attention
     "stag3": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FWD_STAGGER", 3),  # ... after the first LayerNorm
+    "attds_on": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_ATTN_DS", True),  # dQ from the stored dS
+    "attds_off": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_ATTN_DS", False),  # ... or the fused dQ role
     "defer_on": lambda: setattr(__import__("hetseq_amd.parallel.ddp", fromlist=["x"]).FlatDDP, "DEFER_LAST_EARLY", True),
     "defer_off": lambda: setattr(__import__("hetseq_amd.parallel.ddp", fromlist=["x"]).FlatDDP, "DEFER_LAST_EARLY", False),
     "fsplit_bf16_on": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FWD_SPLIT_BF16", True),  # bf16 half-batch chains

@@ -638,7 +638,7 @@ int launch_attn_fwd_h3(const float* qkv, const int64_t* mask, const float* bqkv,
 int launch_attn_bwd_h3(const float* qkv, const int64_t* mask, const float* bqkv, const float* ctx, const float* dctx,
                        const float* lse, float* Dbuf, float* dqkv, const uint32_t* dmask, int B, int S, int NH, int D,
                        float p, hipStream_t st, float* amax, void* pl = nullptr, int64_t ps = 0,
-                       int8_t* ex = nullptr);
+                       int8_t* ex = nullptr, float* dsbuf = nullptr);
 
 // fp32 attention products: 2 "h3" (three split-fp16 products with in-kernel power-of-two scales,
 // attention_h3.hip; default), 1 "x6" (six split-bf16 products, attention_x6.hip) or 0 "native"

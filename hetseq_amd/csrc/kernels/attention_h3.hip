@@ -302,11 +302,13 @@ HS_DEVICE float ds_scale(const float (&ds)[2][8], int& es, f32x16& a0, f32x16& a
 // dK / dV for 32 keys per wave (lane = key) over 64-query chunks of Q (biased, * 1/8) and dO.
 constexpr int kBwdLds = 2 * kIm + 64 * 4 * 2 + 64 * 4 * 4 + 2 * 8 * 4;
 
+template <bool DS>
 HS_DEVICE void dkv_body(char* __restrict__ smem, int bx, int bh, const float* __restrict__ qkv,
                         const int64_t* __restrict__ mask, const float* __restrict__ bqkv,
                         const float* __restrict__ dctx, const float* __restrict__ lse, const float* __restrict__ Dd,
                         float* __restrict__ dqkv, int S, int NH, float p, const uint32_t* __restrict__ dmask,
-                        const float* __restrict__ ctx, float* __restrict__ amax, AttnPl po) {
+                        const float* __restrict__ ctx, float* __restrict__ amax, AttnPl po,
+                        float* __restrict__ dsw) {
   char* const Qp = smem;
   char* const Op = smem + kIm;
   float* const Ls = reinterpret_cast<float*>(smem + 2 * kIm);
@@ -446,6 +448,11 @@ HS_DEVICE void dkv_body(char* __restrict__ smem, int bx, int bh, const float* __
       const float ss = ds_scale(ds, es, dk0, dk1);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
+        if (DS) {  // dS [query][key] for the dQ kernel (attn_dq_ds_kernel): a row's 32 keys per store
+          float* const tb_ = dsw + ((int64_t)bh * S + c0 + t + 16 * ks) * S;  // (uniform)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) tb_[(4 * hf + (j & 3) + 8 * (j >> 2)) * S + key] = ds[ks][j];
+        }
         hx8 sb[2], a[2];
         split8h(ds[ks], ss, sb[0], sb[1]);
         ptr2(Qp, t + 16 * ks, tb, 0, a);
@@ -593,13 +600,123 @@ __global__ void __launch_bounds__(256, 2)
                        const float* __restrict__ bqkv, const float* __restrict__ dctx, const float* __restrict__ lse,
                        const float* __restrict__ Dd, float* __restrict__ dqkv, int S, int NH, float p,
                        const uint32_t* __restrict__ dmask, const float* __restrict__ ctx, float* __restrict__ amax,
-                       AttnPl po) {
+                       AttnPl po, float* __restrict__ dsw) {
   __shared__ __attribute__((aligned(16))) char smem[kBwdLds];
   const int nq = (S + 127) / 128, bh = blockIdx.x, y = blockIdx.y;
   if (y < nq)
-    dkv_body(smem, y, bh, qkv, mask, bqkv, dctx, lse, Dd, dqkv, S, NH, p, dmask, ctx, amax, po);
+    dkv_body<false>(smem, y, bh, qkv, mask, bqkv, dctx, lse, Dd, dqkv, S, NH, p, dmask, ctx, amax, po, dsw);
   else
     dq_body(smem, y - nq, bh, qkv, mask, bqkv, dctx, lse, Dd, dqkv, S, NH, p, dmask, ctx, amax, po);
+}
+
+// the dK / dV blocks alone, writing dS for attn_dq_ds_kernel
+__global__ void __launch_bounds__(256, 2)
+    attn_bwd_h3_dkv_ds_kernel(const float* __restrict__ qkv, const int64_t* __restrict__ mask,
+                              const float* __restrict__ bqkv, const float* __restrict__ dctx,
+                              const float* __restrict__ lse, const float* __restrict__ Dd, float* __restrict__ dqkv,
+                              int S, int NH, float p, const uint32_t* __restrict__ dmask, const float* __restrict__ ctx,
+                              float* __restrict__ amax, AttnPl po, float* __restrict__ dsw) {
+  __shared__ __attribute__((aligned(16))) char smem[kBwdLds];
+  dkv_body<true>(smem, blockIdx.y, blockIdx.x, qkv, mask, bqkv, dctx, lse, Dd, dqkv, S, NH, p, dmask, ctx, amax, po, dsw);
+}
+
+// diagnostic (set_attn_h3_variant bwd_roles 2): the dQ role's blocks alone
+__global__ void __launch_bounds__(256, 2)
+    attn_bwd_h3_dq_only_kernel(const float* __restrict__ qkv, const int64_t* __restrict__ mask,
+                               const float* __restrict__ bqkv, const float* __restrict__ dctx,
+                               const float* __restrict__ lse, const float* __restrict__ Dd, float* __restrict__ dqkv,
+                               int S, int NH, float p, const uint32_t* __restrict__ dmask, const float* __restrict__ ctx,
+                               float* __restrict__ amax, AttnPl po) {
+  __shared__ __attribute__((aligned(16))) char smem[kBwdLds];
+  dq_body(smem, blockIdx.y, blockIdx.x, qkv, mask, bqkv, dctx, lse, Dd, dqkv, S, NH, p, dmask, ctx, amax, po);
+}
+
+// dQ from the dS the dK / dV blocks wrote ([query][key] fp32, attn_bwd_h3_kernel dsw): dQ = dS K / 8 per
+// head, 32 queries per wave (lane = query) over 64-key chunks of K (biased), K split per chunk into plane
+// images, dS split with the running per-lane exponent (ds_scale) -- the dQ role of the fused backward
+// without recomputing the scores, P, dP and dS (round 6: that role was ~23 of the 58-us backward at
+// B 32, S 128, tools/bench_attn.py).
+__global__ void __launch_bounds__(256, 2)
+    attn_dq_ds_kernel(const float* __restrict__ qkv, const float* __restrict__ bqkv, const float* __restrict__ dsw,
+                      float* __restrict__ dqkv, int S, int NH, float* __restrict__ amax, AttnPl po) {
+  __shared__ __attribute__((aligned(16))) char smem[kIm + 16 * 4];
+  char* const Kp = smem;
+  float* const red = reinterpret_cast<float*>(smem + kIm);  // [parity][wave]
+  const int H = NH * kHD;
+  const int64_t ld = 3 * (int64_t)H;
+  const int bh = blockIdx.x, b = bh / NH, h = bh % NH;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hf = lane >> 5, li = lane & 31;
+  const int q0 = blockIdx.y * 128 + w * 32;
+  const bool active = q0 < S;
+  const int64_t tok = (int64_t)b * S + q0 + li;
+  const float* krows = qkv + (int64_t)b * S * ld + H + h * kHD;
+  const float* kbias = bofs(bqkv, H + h * kHD);
+  const float* dsrow = dsw + ((int64_t)bh * S + (active ? q0 + li : 0)) * S;  // this lane's query row of dS
+  f32x16 dq0 = {}, dq1 = {};
+  int ek_run = 0, es = 126;
+  const TrBase tb = tr_base(lane);
+  for (int c0 = 0, par = 0; c0 < S; c0 += 64, par ^= 1) {
+    const int clen = min(64, S - c0);
+    float kv[2][8];
+    float m = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {  // thread unit u = tid + 256 i: key row u >> 3, dims 8 (u & 7) .. + 7
+      const int u = tid + 256 * i, r = u >> 3, c8 = 8 * (u & 7);
+      if (r < clen) {
+        ld8(krows + (int64_t)(c0 + r) * ld + c8, kbias ? kbias + c8 : nullptr, 1.f, kv[i]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) kv[i][j] = 0.f;
+      }
+      m = amax8(kv[i], m);
+    }
+    m = wave_max(m);
+    if (lane == 0) red[8 * par + w] = m;
+    __syncthreads();  // the previous chunk's image is free; the chunk's |max| partials visible
+    const int ek = h16e(fmaxf(fmaxf(red[8 * par], red[8 * par + 1]), fmaxf(red[8 * par + 2], red[8 * par + 3])));
+    const float sk = ldexpf(1.f, ek);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int u = tid + 256 * i, r = u >> 3;
+      if (r < clen) put2(Kp, r, u & 7, kv[i], sk);
+    }
+    __syncthreads();  // the image is ready
+    if (!active) continue;
+    if (c0 > 0) {
+      const float fk = ldexpf(1.f, ek - ek_run);
+      dq0 *= fk;
+      dq1 *= fk;
+    }
+    ek_run = ek;
+#pragma unroll 1
+    for (int t = 0; t < clen; t += 32) {
+      float ds[2][8];  // ds[ks][j]: key t + xrow(8 ks + j, hf), the dQ role's register order
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const float4 x = *reinterpret_cast<const float4*>(dsrow + c0 + t + 16 * ks + 4 * hf);
+        const float4 y = *reinterpret_cast<const float4*>(dsrow + c0 + t + 16 * ks + 8 + 4 * hf);
+        ds[ks][0] = x.x; ds[ks][1] = x.y; ds[ks][2] = x.z; ds[ks][3] = x.w;
+        ds[ks][4] = y.x; ds[ks][5] = y.y; ds[ks][6] = y.z; ds[ks][7] = y.w;
+      }
+      const float ss = ds_scale(ds, es, dq0, dq1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        hx8 sb[2], a[2];
+        split8h(ds[ks], ss, sb[0], sb[1]);
+        ptr2(Kp, t + 16 * ks, tb, 0, a);
+        dq0 = mma3(a, sb, dq0);
+        ptr2(Kp, t + 16 * ks, tb, 1, a);
+        dq1 = mma3(a, sb, dq1);
+      }
+    }
+  }
+  if (!active) return;
+  uint32_t cm = 0u;
+  if (dqkv) store_rows(dqkv + tok * ld + h * kHD, dq0, dq1, hf, 0.125f * ldexpf(1.f, -(ek_run + es)), cm);
+  if (amax) amax_commit(amax, cm);
+  if (po.pl)
+    store_rows_h3p(po, tok, h * kHD, ld, po.ex + ((int64_t)b * S + q0) / 32 * (ld / 32) + h * kHD / 32, dq0, dq1, hf,
+                   0.125f * ldexpf(1.f, -(ek_run + es)));
 }
 
 // Forward: a wave owns 32 queries (lane = query), S^T tiles with the key on the registers, online softmax;
@@ -801,7 +918,11 @@ using namespace hs;
 // (176 B of scratch) in both phases (10.98 vs 10.68 ms; 12.75 vs 12.27 ms) and was removed.
 // set_attn_h3_variant: -1 = that choice, 0 / 1 = always per tile / paired (tests, A/B).
 static int g_attn_fwd_pair = -1;
-void set_attn_h3_variant(int fwd_pair, int) { g_attn_fwd_pair = fwd_pair; }
+static int g_attn_bwd_roles = 3;  // diagnostic: 1 = only the dK / dV blocks, 2 = only the dQ blocks
+void set_attn_h3_variant(int fwd_pair, int bwd_roles) {
+  g_attn_fwd_pair = fwd_pair;
+  g_attn_bwd_roles = bwd_roles > 0 ? bwd_roles : 3;
+}
 
 // amax (optional): a |max| slot (common.h) the kernels max |output| into (ctx forward, dqkv backward)
 int launch_attn_fwd_h3(const float* qkv, const int64_t* mask, const float* bqkv, float* ctx, float* lse,
@@ -820,9 +941,11 @@ int launch_attn_fwd_h3(const float* qkv, const int64_t* mask, const float* bqkv,
   return 0;
 }
 
+// dsbuf (B * NH * S * S floats, or null): dQ from the dS the dK / dV blocks write there (attn_dq_ds_kernel)
+// instead of the fused dQ role that recomputes it
 int launch_attn_bwd_h3(const float* qkv, const int64_t* mask, const float* bqkv, const float* ctx, const float* dctx,
                        const float* lse, float* Dbuf, float* dqkv, const uint32_t* dmask, int B, int S, int NH, int D,
-                       float p, hipStream_t st, float* amax, void* pl, int64_t ps, int8_t* ex) {
+                       float p, hipStream_t st, float* amax, void* pl, int64_t ps, int8_t* ex, float* dsbuf) {
   if (D != kHD || S % 32 != 0 || S <= 0 || (p > 0.f && dmask == nullptr)) return -1;
   if (!dqkv && (!pl || amax)) return -1;  // dqkv may be written only as the planes
   const AttnPl po{static_cast<uint16_t*>(pl), ps, ex};
@@ -831,8 +954,21 @@ int launch_attn_bwd_h3(const float* qkv, const int64_t* mask, const float* bqkv,
     if (Dbuf == nullptr) return -1;
     launch_attn_bwd_dsum(ctx, dctx, Dbuf, B, S, NH, st);
   }
-  const dim3 grid(B * NH, 2 * ((S + 127) / 128));
-  hipLaunchKernelGGL(attn_bwd_h3_kernel, grid, dim3(256), 0, st, qkv, mask, bqkv, dctx, lse, Dbuf, dqkv, S, NH, p, dmask,
-                     fused_d ? ctx : nullptr, amax, po);
+  const int nq = (S + 127) / 128;
+  if (dsbuf) {  // the dK / dV blocks (writing dS), then dQ from dS
+    hipLaunchKernelGGL(attn_bwd_h3_dkv_ds_kernel, dim3(B * NH, nq), dim3(256), 0, st, qkv, mask, bqkv, dctx, lse, Dbuf,
+                       dqkv, S, NH, p, dmask, fused_d ? ctx : nullptr, amax, po, dsbuf);
+    hipLaunchKernelGGL(attn_dq_ds_kernel, dim3(B * NH, nq), dim3(256), 0, st, qkv, bqkv, (const float*)dsbuf, dqkv, S,
+                       NH, amax, po);
+    return 0;
+  }
+  const dim3 grid(B * NH, g_attn_bwd_roles == 3 ? 2 * nq : nq);
+  if (g_attn_bwd_roles == 2) {  // (diagnostic: the dQ role alone -- its blocks' y index starts at nq)
+    hipLaunchKernelGGL(attn_bwd_h3_dq_only_kernel, grid, dim3(256), 0, st, qkv, mask, bqkv, dctx, lse, Dbuf, dqkv, S, NH,
+                       p, dmask, fused_d ? ctx : nullptr, amax, po);
+    return 0;
+  }
+  hipLaunchKernelGGL(attn_bwd_h3_kernel, grid, dim3(256), 0, st, qkv, mask, bqkv, dctx, lse, Dbuf, dqkv, S, NH, p,
+                     dmask, fused_d ? ctx : nullptr, amax, po, nullptr);
   return 0;
 }

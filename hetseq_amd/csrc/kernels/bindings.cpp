@@ -60,7 +60,7 @@ int launch_attn_fwd_h3(const float*, const int64_t*, const float*, float*, float
                        uint64_t, uint64_t, hipStream_t, int, float*, void*, int64_t, int8_t*);
 int launch_attn_bwd_h3(const float*, const int64_t*, const float*, const float*, const float*, const float*, float*,
                        float*, const uint32_t*, int, int, int, int, float, hipStream_t, float*, void*, int64_t,
-                       int8_t*);
+                       int8_t*, float*);
 void launch_colpart_finalize(const float* const*, float* const*, int, int, int, int, hipStream_t);
 int launch_segsum_rows(const float*, const int64_t*, const int64_t*, float*, float*, int, int, int, hipStream_t);
 int launch_sort_keys(const int64_t*, int, int64_t, int64_t*, int64_t*, int*, hipStream_t);
@@ -504,14 +504,17 @@ PYBIND11_MODULE(_hip, m) {
           "attn_fwd_h3p");
   }, "h3 attention forward also writing ctx as h3p planes");
   m.def("attn_bwd_h3p", [](i64 qkv, i64 mask, i64 bqkv, i64 ctx, i64 dctx, i64 lse, i64 dbuf, i64 dqkv, i64 dmask,
-                           int B, int S, int NH, float p, i64 pl, i64 ps, i64 ex, i64 st) {
+                           int B, int S, int NH, float p, i64 pl, i64 ps, i64 ex, i64 st, i64 dsbuf) {
     pre_launch("attn_bwd_h3p");
     check(launch_attn_bwd_h3(P(const float*, qkv), P(const int64_t*, mask), P(const float*, bqkv),
                              P(const float*, ctx), P(const float*, dctx), P(const float*, lse), P(float*, dbuf),
                              P(float*, dqkv), P(const uint32_t*, dmask), B, S, NH, 64, p, ST(st), nullptr,
-                             P(void*, pl), ps, P(int8_t*, ex)),
+                             P(void*, pl), ps, P(int8_t*, ex), P(float*, dsbuf)),
           "attn_bwd_h3p");
-  }, "h3 attention backward also writing dqkv as h3p planes (dqkv 0: only as the planes)");
+  }, "h3 attention backward also writing dqkv as h3p planes (dqkv 0: only as the planes; dsbuf: B*NH*S*S floats, "
+     "dQ from the stored dS)", py::arg("qkv"), py::arg("mask"), py::arg("bqkv"), py::arg("ctx"), py::arg("dctx"),
+     py::arg("lse"), py::arg("dbuf"), py::arg("dqkv"), py::arg("dmask"), py::arg("B"), py::arg("S"), py::arg("NH"),
+     py::arg("p"), py::arg("pl"), py::arg("ps"), py::arg("ex"), py::arg("st"), py::arg("dsbuf") = 0);
   m.def("set_ln_h3p_waves", &set_ln_h3p_waves,
         "h3p LayerNorm forward kernel: 0 / 1 panel exchange at 8 / 4 rows per workgroup, 16 / 8 one 32-row block");
   m.def("ln_bwd_h3p_part_rows", &ln_bwd_h3p_part_rows, "rows per column-partial row of ln_bwd_h3p (coop: psync given)");

@@ -40,7 +40,7 @@ int launch_attn_fwd_h3(const float*, const int64_t*, const float*, float*, float
                        uint64_t, uint64_t, hipStream_t, int, float*, void*, int64_t, int8_t*);
 int launch_attn_bwd_h3(const float*, const int64_t*, const float*, const float*, const float*, const float*, float*,
                        float*, const uint32_t*, int, int, int, int, float, hipStream_t, float*, void*, int64_t,
-                       int8_t*);
+                       int8_t*, float*);
 void launch_colpart_finalize(const float* const*, float* const*, int, int, int, int, hipStream_t);
 int launch_h3p_colpart(const void*, int64_t, int64_t, const int8_t*, int64_t, int, int, float*, hipStream_t);
 void hs_stream_wait(hipStream_t waiter, hipStream_t signal);
@@ -61,7 +61,7 @@ void hs_stream_wait(hipStream_t waiter, hipStream_t signal);
   X(dz2) X(dz1) X(dctx) X(dbuf)                                                                              \
   HPF(X, da2p) HPF(X, df1p) HPF(X, da1p) HPF(X, dqkvp)                                                        \
   X(part2_g) X(part2_b) X(part2_bias) X(part1_g) X(part1_b) X(part1_bias) X(part_gelu) X(part_bq)            \
-  X(psync_f) X(psync_b)
+  X(psync_f) X(psync_b) X(dsbuf)
 
 namespace {
 
@@ -270,7 +270,7 @@ void layer_bwd_h3p(int64_t plan, int64_t dh2, int64_t xp, int64_t xe, int64_t ma
   req(launch_attn_bwd_h3(ptr<const float>(q[f_qkv]), ptr<const int64_t>(mask), ptr<const float>(q[f_bqkv]),
                          ptr<const float>(q[f_ctx]), dctx, ptr<const float>(q[f_lse]), ptr<float>(q[f_dbuf]), nullptr,
                          q[f_dmask] ? ptr<const uint32_t>(q[f_dmask]) : nullptr, B, S, NH, 64, p_a, st0, nullptr,
-                         ptr<void>(dqkvp.p), dqkvp.ps, ptr<int8_t>(dqkvp.e)),
+                         ptr<void>(dqkvp.p), dqkvp.ps, ptr<int8_t>(dqkvp.e), ptr<float>(q[f_dsbuf])),
       "attention backward");
   // QKV weight and bias gradients on the side stream; dx = dz1 + dqkv @ Wqkv
   hs_stream_wait(st1, st0);

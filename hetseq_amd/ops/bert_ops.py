@@ -313,17 +313,19 @@ def attn_fwd_h3p(qkv, mask, B, S, NH, p, seed, off, bias, outs, b0, hp):
     return ctx
 
 
-def attn_bwd_h3p(qkv, mask, ctx, dctx, lse, B, S, NH, p, bias, hp, fp32=True):
+def attn_bwd_h3p(qkv, mask, ctx, dctx, lse, B, S, NH, p, bias, hp, fp32=True, ds=False):
     """attn_bwd on the h3 attention kernel that also writes dqkv as h3p planes into ``hp``; with
-    ``fp32=False`` ONLY as the planes (returns None)."""
+    ``fp32=False`` ONLY as the planes (returns None).  ``ds``: dQ from the stored dS (a B*NH*S*S
+    buffer) instead of the fused dQ role."""
     assert hp.blk, "producers write blocked planes"
     lse, dmask = lse
     dqkv = torch.empty_like(qkv) if fp32 else None
     dbuf = torch.empty_like(lse)
+    dsb = torch.empty(B * NH * S * S, dtype=torch.float32, device=qkv.device) if ds else None
     hip().attn_bwd_h3p(qkv.data_ptr(), mask.data_ptr(), bias.data_ptr() if bias is not None else 0, ctx.data_ptr(),
                        dctx.data_ptr(), lse.data_ptr(), dbuf.data_ptr(), dqkv.data_ptr() if fp32 else 0,
                        dmask.data_ptr() if dmask is not None else 0, B, S, NH, float(p), hp.data_ptr(), hp.ps,
-                       hp.exps_ptr(), stream_handle())
+                       hp.exps_ptr(), stream_handle(), dsbuf=dsb.data_ptr() if dsb is not None else 0)
     return dqkv
 
 
@@ -664,6 +666,16 @@ LAYER_PROG = True
 # the second half-batch chain's start in the first layer (layer_prog.cpp layer_fwd_h3p stagger):
 # 0 with the first chain, 1 / 2 / 3 after its QKV product / attention / first LayerNorm
 _FWD_STAGGER = 0
+# the layer program's attention backward: dQ from the dS its dK / dV blocks store (attention_h3.hip
+# attn_dq_ds_kernel) instead of the fused dQ role recomputing it, up to _ATTN_DS_MAX_S (bench.py --ab
+# attds_on / attds_off: S 128 10.302 -> 10.200 ms; S 512 11.687 -> 11.880, the 100 MB dS round trip
+# costs more than the recomputation saves there)
+_ATTN_DS = True
+_ATTN_DS_MAX_S = 128
+
+
+def _attn_ds(S):
+    return _ATTN_DS and S <= _ATTN_DS_MAX_S
 PROG_BUILDS = [0]  # programs built in this process (tests)
 _PROG_SIDE_DELAY = 0  # GPU cycles the side stream sleeps before a program backward (tests only)
 
@@ -687,7 +699,7 @@ def _program(W, meta, B, S, NH, p_a, halves, dev):
     # long as the model it was built for)
     progs = meta["weights"].__self__.__dict__.setdefault("_hs_progs", {})
     key = (id(W.h3p), id(Gv), B, S, halves, p_a > 0, _H3P_KS_WO, _H3P_KS_W2, streams.SIDE_KSPLIT,
-           streams.SIDE_KSPLIT_SMALL)
+           streams.SIDE_KSPLIT_SMALL, _attn_ds(S))
     prog = progs.get(key)
     if prog is None:
         from hetseq_amd.ops.layer_prog import LayerProgram
@@ -877,7 +889,7 @@ def _layer_backward_h3p(ctx, dh2, x, saved, W, meta, cfg):
         wgrad(da1p, ctxp, Gv.wo, "wo_wgrad")
     dctx = h3p.gemm(da1p, Wp.wo, 0, 0, site="wo_dgrad")
     dqkvp = h3p.empty(rows, 3 * H, dev)
-    attn_bwd_h3p(qkv, mask_of(ctx), ctx_, dctx, (lse, dmask), B, S, NH, p_a, W.bqkv, dqkvp, fp32=False)
+    attn_bwd_h3p(qkv, mask_of(ctx), ctx_, dctx, (lse, dmask), B, S, NH, p_a, W.bqkv, dqkvp, fp32=False, ds=_attn_ds(S))
     part_bq = torch.empty(rows // 32, 3 * H, dtype=torch.float32, device=dev)
 
     def fin_bq():  # the QKV bias gradient: column sums of dqkv's planes (no fp32 dqkv exists)

@@ -82,6 +82,9 @@ class LayerProgram(object):
         self.psync_f, self.psync_b = bert_ops.panel_sync(device, rows, 0), bert_ops.panel_sync(device, rows, 1)
         self.part_gelu = z(rows // 128, Fd)
         self.part_bq = z(rows // 32, 3 * H)  # the QKV bias gradient's column partials (from dqkvp)
+        # dS of the attention backward, [B * NH][S queries][S keys] fp32: the dQ product reads it instead of
+        # recomputing it (bert_ops._ATTN_DS; None: the fused dQ role)
+        self.dsbuf = z(B * NH * S * S) if bert_ops._attn_ds(S) else None
         hr = rows // halves
         need = max(ks_wo * hr * H, ks_w2 * hr * H, ksg["w2"] * H * Fd, ksg["w1"] * Fd * H, ksg["wo"] * H * H,
                    ksg["qkv"] * 3 * H * H)
@@ -128,6 +131,7 @@ class LayerProgram(object):
         put("psync_f", self.psync_f.data_ptr())
         put("psync_b", self.psync_b.data_ptr())
         put("part_bq", self.part_bq.data_ptr())
+        put("dsbuf", self.dsbuf.data_ptr() if self.dsbuf is not None else 0)
         self.q = q
         self.addr = q.buffer_info()[0]
         self._xp = None

@@ -373,6 +373,10 @@ def test_attention_h3_matches_fp64(cuda, B, S, NH, p, data):
         if data == "wide":
             dout *= torch.pow(10.0, torch.empty(B * S, 1, device=cuda).uniform_(-1.5, 1.5))
         g3 = bert_ops.attn_bwd(qkv, mask, out32, dout, saved32, B, S, NH, p, bias=bias)
+        # the same backward with dQ from the stored dS (the layer program's path)
+        from hetseq_amd.ops import h3p
+        g3ds = bert_ops.attn_bwd_h3p(qkv, mask, out32, dout, saved32, B, S, NH, p, bias,
+                                     h3p.empty(B * S, 3 * H, cuda), fp32=True, ds=True)
         hip().set_attn_fp32_mode(0)
         g32 = bert_ops.attn_bwd(qkv, mask, out32, dout, saved32, B, S, NH, p, bias=bias)
     finally:
@@ -395,6 +399,10 @@ def test_attention_h3_matches_fp64(cuda, B, S, NH, p, data):
     g32e = float((g32.double() - x.grad).abs().max())
     assert g3e <= f * g32e + 1e-7, ("backward", g3e, g32e)
     assert torch.isfinite(g3).all()
+    gdse = float((g3ds.double() - x.grad).abs().max())
+    assert gdse <= f * g32e + 1e-7, ("backward, dQ from the stored dS", gdse, g32e)
+    H3 = 3 * H  # the K / V gradients are the same kernel's either way
+    assert torch.equal(g3ds.view(-1, H3)[:, H:], g3.view(-1, H3)[:, H:])
 
 
 @pytest.mark.parametrize("S,engine", [(128, 2), (512, 2), (128, 1)])

@@ -61,6 +61,28 @@ def main():
                                                                                  (outs[1], outs[2]), B, S, NH, p,
                                                                                  bq, hq, fp32=False))(
                         qkv, mask, outs, dctx, B, p, bq, hq)
+        from hetseq_amd.ops._C import hip
+        bwd = [k for k in runs if k.startswith("bwd")]
+        for role, tag in ((1, "dkv only"), (2, "dq only")):  # (diagnostic: one backward role's blocks)
+            for k in bwd:
+                runs["%s %s" % (k, tag)] = (lambda fn, r: lambda: (hip().set_attn_h3_variant(-1, r), fn(),
+                                                                    hip().set_attn_h3_variant(-1, 3)))(runs[k], role)
+        if "ds" in __import__("inspect").signature(bert_ops.attn_bwd_h3p).parameters:
+            for p_ in (0.1, 0.0):  # dQ from the stored dS (the layer program's path)
+                B = Bw
+                T = B * S
+                qkv = torch.randn(T, 3 * H, device=dev)
+                bq = torch.randn(3 * H, device=dev) * 0.1
+                mask = torch.ones(B, S, dtype=torch.int64, device=dev)
+                outs = (torch.empty(T, H, device=dev), torch.empty(B * NH * S, device=dev),
+                        torch.empty(B * NH * S * (S // 32), dtype=torch.int32, device=dev))
+                bert_ops.attn_fwd_h3p(qkv, mask, B, S, NH, p_, 1, 2, bq, outs, 0, h3p.empty(T, H, dev))
+                dctx, hq = torch.randn(T, H, device=dev), h3p.empty(T, 3 * H, dev)
+                runs["bwd B%d p%g ds" % (B, p_)] = (lambda qkv, mask, outs, dctx, B, p_, bq, hq:
+                                                    lambda: bert_ops.attn_bwd_h3p(qkv, mask, outs[0], dctx,
+                                                                                  (outs[1], outs[2]), B, S, NH, p_,
+                                                                                  bq, hq, fp32=False, ds=True))(
+                    qkv, mask, outs, dctx, B, p_, bq, hq)
         best = {}
         for _ in range(a.rounds):
             for k, fn in runs.items():
