@@ -579,9 +579,9 @@ _AB = {
     "occ3_d": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_h3_occ3(2),
     "occ3_w": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_h3_occ3(4),
     "occ3_fw": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_h3_occ3(5),
-    # fp32 attention engine: h3 (split-fp16, default) / x6 (split-bf16)
+    # fp32 attention engine: h3 (split-fp16, default) / native (exact fp32)
+    "attn_native": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_fp32_mode(0),
     "attn_h3": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_fp32_mode(2),
-    "attn_x6": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_attn_fp32_mode(1),
     "adam_8k": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_adam_config(8192, 2, 1),
     "adam_64k": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_adam_config(65536, 2, 1),
     # split-K of the side-stream weight gradients (runtime/streams.py): the default 2 (4 for <= 768 x 768)

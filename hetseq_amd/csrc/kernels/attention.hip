@@ -623,14 +623,6 @@ int launch_attn_bwd_fused_bf16(const void* qkv, const int64_t* mask, const float
                                const void* dctx, const float* lse, void* dqkv, const uint32_t* dmask, int B, int S,
                                int NH, int D, float p, hipStream_t st);
 
-int launch_attn_fwd_x6(const float* qkv, const int64_t* mask, const float* bqkv, float* ctx, float* lse,
-                       uint32_t* dmask, int B, int S, int NH, int D, float p, uint64_t seed, uint64_t off,
-                       hipStream_t st, int bh0);
-
-int launch_attn_bwd_x6(const float* qkv, const int64_t* mask, const float* bqkv, const float* ctx, const float* dctx,
-                       const float* lse, float* Dbuf, float* dqkv, const uint32_t* dmask, int B, int S, int NH,
-                       int D, float p, hipStream_t st);
-
 int launch_attn_fwd_h3(const float* qkv, const int64_t* mask, const float* bqkv, float* ctx, float* lse,
                        uint32_t* dmask, int B, int S, int NH, int D, float p, uint64_t seed, uint64_t off,
                        hipStream_t st, int bh0, float* amax, void* pl = nullptr, int64_t ps = 0, int8_t* ex = nullptr);
@@ -641,16 +633,16 @@ int launch_attn_bwd_h3(const float* qkv, const int64_t* mask, const float* bqkv,
                        int8_t* ex = nullptr, float* dsbuf = nullptr);
 
 // fp32 attention products: 2 "h3" (three split-fp16 products with in-kernel power-of-two scales,
-// attention_h3.hip; default), 1 "x6" (six split-bf16 products, attention_x6.hip) or 0 "native"
-// (exact-fp32 MFMA) -- HETSEQ_ATTN_FP32
-static int g_attn_fp32_x6 = [] {
+// attention_h3.hip; default) or 0 "native" (exact-fp32 MFMA, the oracle) -- HETSEQ_ATTN_FP32.  (The
+// six-term split-bf16 kernels were retired in round 6: the h3 kernels' per-row / per-chunk scales
+// cover their range role, the exact kernels their accuracy role.)
+static int g_attn_fp32 = [] {
   const char* e = std::getenv("HETSEQ_ATTN_FP32");
-  if (e && std::string(e) == "native") return 0;
-  return e && std::string(e) == "x6" ? 1 : 2;
+  return e && std::string(e) == "native" ? 0 : 2;
 }();
 
-void set_attn_fp32_mode(int mode) { g_attn_fp32_x6 = mode; }
-int attn_fp32_mode() { return g_attn_fp32_x6; }
+void set_attn_fp32_mode(int mode) { g_attn_fp32 = mode == 0 ? 0 : 2; }
+int attn_fp32_mode() { return g_attn_fp32; }
 
 // HETSEQ_ATTN_BF16_MFMA=0 keeps bf16 attention on the fp32-MFMA kernels (A/B and tests)
 static bool bf16_mfma_enabled() {
@@ -678,15 +670,12 @@ int launch_attn_fwd(int dtype, const void* qkv, const int64_t* mask, const float
   dim3 grid(B * NH, (S + 127) / 128);  // head-major: a head's blocks share one XCD's L2
   if (dtype != 0 && bf16_mfma_enabled())  // bf16 matrix cores (attention_bf16.hip)
     return launch_attn_fwd_bf16(qkv, mask, bqkv, ctx, lse, dmask, B, S, NH, D, p, seed, off, st, bh0);
-  if (dtype == 0 && g_attn_fp32_x6 == 2) {  // fp32 as split-fp16 products (attention_h3.hip)
+  if (dtype == 0 && g_attn_fp32 == 2) {  // fp32 as split-fp16 products (attention_h3.hip)
     const int rc = launch_attn_fwd_h3((const float*)qkv, mask, bqkv, (float*)ctx, lse, dmask, B, S, NH, D, p, seed, off,
                                       st, bh0, amax);
     if (rc == 0 && amax_done) *amax_done = amax != nullptr;
     return rc;
   }
-  if (dtype == 0 && g_attn_fp32_x6)  // fp32 as split-bf16 products (attention_x6.hip)
-    return launch_attn_fwd_x6((const float*)qkv, mask, bqkv, (float*)ctx, lse, dmask, B, S, NH, D, p, seed, off, st,
-                              bh0);
   if (dtype == 0)
     hipLaunchKernelGGL(attn_fwd_kernel<float>, grid, dim3(256), 0, st, (const float*)qkv, mask, bqkv, (float*)ctx,
                        lse, dmask, S, NH, p, seed, off, g_seed_dev, bh0);
@@ -701,15 +690,12 @@ int launch_attn_bwd(int dtype, const void* qkv, const int64_t* mask, const float
                     int NH, int D, float p, hipStream_t st, float* amax, int* amax_done) {
   if (amax_done) *amax_done = 0;
   if (D != kD || S % 32 != 0 || S <= 0 || (p > 0.f && dmask == nullptr)) return -1;
-  if (dtype == 0 && g_attn_fp32_x6 == 2) {
+  if (dtype == 0 && g_attn_fp32 == 2) {
     const int rc = launch_attn_bwd_h3((const float*)qkv, mask, bqkv, (const float*)ctx, (const float*)dctx, lse, Dbuf,
                                       (float*)dqkv, dmask, B, S, NH, D, p, st, amax);
     if (rc == 0 && amax_done) *amax_done = amax != nullptr;
     return rc;
   }
-  if (dtype == 0 && g_attn_fp32_x6)  // fp32 as split-bf16 products (attention_x6.hip)
-    return launch_attn_bwd_x6((const float*)qkv, mask, bqkv, (const float*)ctx, (const float*)dctx, lse, Dbuf,
-                              (float*)dqkv, dmask, B, S, NH, D, p, st);
   if (S <= 128 && fused_bwd_enabled()) {  // one block per (batch, head): 5 products instead of 7
     if (dtype != 0 && bf16_mfma_enabled())
       return launch_attn_bwd_fused_bf16(qkv, mask, bqkv, ctx, dctx, lse, dqkv, dmask, B, S, NH, D, p, st);

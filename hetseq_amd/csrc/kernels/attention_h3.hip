@@ -1,7 +1,7 @@
 // fp32 attention as THREE split-fp16 products per fp32 product ("h3"; default fp32 attention engine).
 //
-// Same contract and algorithm as the plane-image x6 kernels (attention_x6.hip: attn_fwd_x6p_kernel,
-// attn_bwd_x6p_kernel; reference bert_modeling.py:351-377): Q/K/V read from the fused QKV projection
+// Same contract as the exact-fp32 kernels (attention.hip; reference bert_modeling.py:351-377), on the
+// plane-image algorithm of the round-3 split-bf16 kernels (retired in round 6): Q/K/V read from the fused QKV projection
 // output [B*S, 3H] with the projection bias folded into the loads, additive -10000 mask, Philox
 // dropout with the 1-bit keep mask (identical bit stream and word layout), flash forward with the
 // per-row log-sum-exp, and a backward of two roles in one launch (dK / dV blocks with the key on the
@@ -9,7 +9,7 @@
 //
 // Products: the GEMM engine's h3 scheme (gemm.hip split4h): an operand scaled by a power of two s is
 // split into fp16 hi + lo (22 significant bits) and a*b is accumulated from hi*hi + hi*lo + lo*hi on
-// v_mfma_f32_32x32x16_f16 -- 3 MFMAs per product instead of the x6 kernels' 6, and 2 LDS planes per
+// v_mfma_f32_32x32x16_f16 -- 3 MFMAs per product instead of a six-term bf16 split's 6, and 2 LDS planes per
 // image instead of 3 (16 KB per 64-row chunk).  The scales are chosen IN the kernel, uniform along
 // every product's contraction dimension, so no producer has to supply a |max|:
 //   * the lane's own Q / K / V / dO row (contraction over d): its row |max| (the two lanes holding
@@ -103,7 +103,7 @@ HS_DEVICE void ld8(const float* src, const float* bias, float scale, float (&v)[
 HS_DEVICE const float* bofs(const float* b, int off) { return b ? b + off : nullptr; }
 
 // Plane images of 64-row chunks: [row][64 d] fp16, 128-B rows, the 16-B chunk swizzle pswz (conflict-free
-// b128 row reads and ds_read_b64_tr_b16 transposed reads, as in attention_x6.hip).
+// b128 row reads and ds_read_b64_tr_b16 transposed reads; found by exhaustive search).
 HS_DEVICE int pswz(int r) { return ((r >> 2) & 1) | (((r >> 3) & 1) << 1) | (((r >> 1) & 1) << 2); }
 
 // 8 fp32 * s -> hi / lo planes at 16-B chunk c of row `row`
@@ -590,7 +590,38 @@ HS_DEVICE void dq_body(char* __restrict__ smem, int bx, int bh, const float* __r
                    0.125f * ldexpf(1.f, -(ek_run + es)));
 }
 
+// D[bh][q] = rowsum(dO o O) over the head's 64 dims (the S > 128 backward reads it): 16 lanes per
+// (token, head), float4 each.
+__global__ void __launch_bounds__(256) attn_bwd_dsum_kernel(const float* __restrict__ ctx,
+                                                            const float* __restrict__ dctx, float* __restrict__ Dout,
+                                                            int B, int S, int NH) {
+  const int64_t u = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);  // (token, head) unit
+  const int l = threadIdx.x & 15;
+  const int64_t units = (int64_t)B * S * NH;
+  const int64_t tok = u / NH;
+  const int h = (int)(u % NH);
+  float v = 0.f;
+  if (u < units) {
+    const int64_t o = tok * NH * kHD + h * kHD + 4 * l;
+    const float4 a = *reinterpret_cast<const float4*>(dctx + o), c = *reinterpret_cast<const float4*>(ctx + o);
+    v = a.x * c.x + a.y * c.y + a.z * c.z + a.w * c.w;
+  }
+#pragma unroll
+  for (int m = 8; m >= 1; m >>= 1) v += __shfl_xor(v, m, 16);
+  if (u < units && l == 0) {
+    const int64_t b = tok / S, q = tok % S;
+    Dout[(b * NH + h) * S + q] = v;
+  }
+}
+
 }  // namespace
+
+int launch_attn_bwd_dsum(const float* ctx, const float* dctx, float* Dout, int B, int S, int NH, hipStream_t st) {
+  const int64_t units = (int64_t)B * S * NH;
+  hipLaunchKernelGGL(attn_bwd_dsum_kernel, dim3((unsigned)((units + 15) / 16)), dim3(256), 0, st, ctx, dctx, Dout, B, S,
+                     NH);
+  return 0;
+}
 
 // The backward's two roles in one launch (grid (B*NH, 2 * ceil(S/128)); dK / dV blocks first: the longer
 // role goes out first and the dQ blocks fill the tail of the last round).  ctx != nullptr: D computed by

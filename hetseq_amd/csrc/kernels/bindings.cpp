@@ -648,7 +648,7 @@ PYBIND11_MODULE(_hip, m) {
   }, "per-segment |max| over a flat fp32 buffer: tab = [nblk][3] int64 (segment, first float4, end float4); out "
      "must be zeroed");
 
-  m.def("set_attn_fp32_mode", &set_attn_fp32_mode, "fp32 attention products: 2 split-fp16 (h3), 1 split-bf16 (x6), 0 exact-fp32 MFMA");
+  m.def("set_attn_fp32_mode", &set_attn_fp32_mode, "fp32 attention products: 2 split-fp16 (h3), 0 exact-fp32 MFMA");
   m.def("attn_fp32_mode", &attn_fp32_mode);
   m.def("set_ln_bwd_lds", &set_ln_bwd_lds,
         "LN backward column partials: 1 = through a 3 KB LDS window (default), 0 = the [waves][H] LDS image");

@@ -155,14 +155,12 @@ HS_DEVICE float comp(const float4& v, int s) { return s == 0 ? v.x : s == 1 ? v.
 // <= 2^-24 |a b|, the size of one fp32 rounding).  Every bf16 x bf16 product is
 // exact in the fp32 accumulator, so the result carries fp32-level error
 // (tests/test_kernels_gpu.py::test_gemm_x6_error_matches_fp32 measures it against fp64 next to the exact-fp32
-// MFMA kernel) at 6/16 of the f32 MFMA's cycles.  NT = 3 keeps only
-// hi*hi + hi*mid + mid*hi (two-term split, ~2^-16 relative: NOT fp32 accuracy,
-// a benchmarking variant only).
+// MFMA kernel) at 6/16 of the f32 MFMA's cycles.  (A two-term NT = 3 benchmarking variant, ~2^-16
+// relative, was retired in round 6.)
 typedef __bf16 bfx8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bfx2 __attribute__((ext_vector_type(2)));
 typedef float fx2 __attribute__((ext_vector_type(2)));
 
-template <int NT>
 HS_DEVICE void split4(float4 x, uint2& hi, uint2& mi, uint2& lo) {
   const fx2 x0 = {x.x, x.y}, x1 = {x.z, x.w};
   const bfx2 h0 = __builtin_convertvector(x0, bfx2), h1 = __builtin_convertvector(x1, bfx2);
@@ -170,11 +168,9 @@ HS_DEVICE void split4(float4 x, uint2& hi, uint2& mi, uint2& lo) {
   const bfx2 m0 = __builtin_convertvector(r0, bfx2), m1 = __builtin_convertvector(r1, bfx2);
   hi = make_uint2(__builtin_bit_cast(uint32_t, h0), __builtin_bit_cast(uint32_t, h1));
   mi = make_uint2(__builtin_bit_cast(uint32_t, m0), __builtin_bit_cast(uint32_t, m1));
-  if (NT >= 6) {
-    const bfx2 l0 = __builtin_convertvector(r0 - __builtin_convertvector(m0, fx2), bfx2);
-    const bfx2 l1 = __builtin_convertvector(r1 - __builtin_convertvector(m1, fx2), bfx2);
-    lo = make_uint2(__builtin_bit_cast(uint32_t, l0), __builtin_bit_cast(uint32_t, l1));
-  }
+  const bfx2 l0 = __builtin_convertvector(r0 - __builtin_convertvector(m0, fx2), bfx2);
+  const bfx2 l1 = __builtin_convertvector(r1 - __builtin_convertvector(m1, fx2), bfx2);
+  lo = make_uint2(__builtin_bit_cast(uint32_t, l0), __builtin_bit_cast(uint32_t, l1));
 }
 
 HS_DEVICE f32x16 mma_bf(bfx8 a, bfx8 b, f32x16 c) { return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0); }
@@ -209,11 +205,11 @@ HS_DEVICE void split4h(float4 x, float s, uint2& hi, uint2& lo) {
   lo = make_uint2(__builtin_bit_cast(uint32_t, l0), __builtin_bit_cast(uint32_t, l1));
 }
 
-// the split of one float4 for engine NT: bf16 hi / mid / lo (NT 3, 6) or fp16 hi / lo (NT 4, planes 0, 1)
+// the split of one float4 for engine NT: bf16 hi / mid / lo (NT 6) or fp16 hi / lo (NT 4, planes 0, 1)
 template <int NT>
 HS_DEVICE void split_nt(float4 x, float s, uint2& p0, uint2& p1, uint2& p2) {
   if constexpr (NT == 4) split4h(x, s, p0, p1);
-  else split4<NT>(x, p0, p1, p2);
+  else split4(x, p0, p1, p2);
 }
 
 template <int NT>
@@ -314,7 +310,7 @@ HS_DEVICE void epilogue(const GemmArgs& p, typename Mf<MF>::acc_t (&acc)[BM / 2 
   }
 }
 
-template <int BM, int BN, int MF, bool TA, bool TB, int EPI, int ABL = 0>
+template <int BM, int BN, int MF, bool TA, bool TB, int EPI>
 __global__ void __launch_bounds__(256, 2) gemm_f32_kernel(GemmArgs p) {
   using IA = Img<BM, !TA, MF>;
   using IB = Img<BN, TB, MF>;
@@ -357,10 +353,8 @@ __global__ void __launch_bounds__(256, 2) gemm_f32_kernel(GemmArgs p) {
     // prefetch the next K tile (the last iteration re-reads the final tile into the idle
     // buffer: keeps the staging registers unconditional, so they stay in VGPRs)
     const int kn = kofs + (kt + 1 < KT ? kt + 1 : kt) * GBK;
-    if (ABL == 0) {  // ABL: ablation builds for the microbenchmark (1: no global loads, 2: + no LDS writes/barrier)
-      g_load<BM, !TA>(p.A, p.lda, m0, kn, ra);
-      g_load<BN, TB>(p.B, p.ldb, n0, kn, rb);
-    }
+    g_load<BM, !TA>(p.A, p.lda, m0, kn, ra);
+    g_load<BN, TB>(p.B, p.ldb, n0, kn, rb);
     const float* as = As0 + cur * IA::size;
     const float* bs = Bs0 + cur * IB::size;
 #pragma unroll
@@ -378,11 +372,9 @@ __global__ void __launch_bounds__(256, 2) gemm_f32_kernel(GemmArgs p) {
           for (int j = 0; j < TN; ++j) acc[i][j] = M_::mma(comp(av[i], s), comp(bv[j], s), acc[i][j]);
     }
     // the other buffer was last read before the previous barrier
-    if (ABL < 2) {
-      s_store<BM, !TA, MF>(As0 + (cur ^ 1) * IA::size, ra);
-      s_store<BN, TB, MF>(Bs0 + (cur ^ 1) * IB::size, rb);
-    }
-    if (ABL < 2) __syncthreads();
+    s_store<BM, !TA, MF>(As0 + (cur ^ 1) * IA::size, ra);
+    s_store<BN, TB, MF>(Bs0 + (cur ^ 1) * IB::size, rb);
+    __syncthreads();
   }
 
   epilogue<BM, BN, MF, EPI>(p, acc, smem, m0, n0, tm, slice, wm, wn, wr, lr, q);
@@ -520,25 +512,21 @@ HS_DEVICE bfx8 x_frag_tr(const char* __restrict__ S, int rc, int p, int ks, int 
   return __builtin_bit_cast(bfx8, u);
 }
 
-// WV = 4: 2x2 waves of 64x64, every thread stages 4x4 of A and of B.
-// WV = 8: 2x4 waves of 64x32 (twice the waves per CU to hide each other's staging), threads
-//         0-255 stage A and 256-511 stage B with the same 4x4 micro-blocks.
-// PF (4 waves, single buffer): register prefetch depth -- 1 = the next K tile, loaded under the
-// MFMAs of this one; 2 = two register sets, each tile's loads issued two tiles ahead.
+// 2x2 waves of 64x64; every thread stages 4x4 of A and of B into one set of LDS images while the next
+// K tile is prefetched into registers under this tile's MFMAs.  (8-wave, double-buffered and
+// two-deep-prefetch variants were measured slower in the step -- profiles/r2_gemm_experiments.md --
+// and retired in round 6, as were the ablation builds.)
 // TRL: mn-contiguous operands in the transposed-read layout (above) instead of the register
 // transpose into k-contiguous images.
-// OCC > 0: waves per SIMD the register allocation targets (4-wave blocks: 3 = three blocks per CU,
-// <= 168 VGPRs) instead of the default two blocks per CU
-template <bool TA, bool TB, int EPI, int NT, int ABL = 0, int WV = 4, int NBUF = 1, bool EDGE = false, int PF = 1,
-          bool TRL = false, int OCC = 0>
-__global__ void __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OCC ? OCC : NBUF == 2 ? 2 : WV / 2, OCC ? OCC : NBUF == 2 ? 2 : WV / 2))) gemm_x6s_kernel(GemmArgs p) {
-  constexpr int BM = 128, BN = 128, WC = WV / 2, TM = 2, TN = BN / WC / 32;
-  static_assert(NBUF == 1 || WV == 8, "double-buffered images: 8-wave variant only");
-  static_assert(!EDGE || (WV == 4 && EPI <= kEpiBias), "edge-masked launches: 4 waves, plain / bias epilogue");
-  static_assert(PF == 1 || (WV == 4 && NBUF == 1 && !EDGE), "two-deep prefetch: 4-wave, single-buffer, unmasked");
+// OCC > 0: waves per SIMD the register allocation targets (3 = three blocks per CU, <= 168 VGPRs)
+// instead of the default two blocks per CU
+template <bool TA, bool TB, int EPI, int NT, bool EDGE = false, bool TRL = false, int OCC = 0>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC ? OCC : 2, OCC ? OCC : 2))) gemm_x6s_kernel(GemmArgs p) {
+  constexpr int BM = 128, BN = 128, TM = 2, TN = 2;
+  static_assert(!EDGE || EPI <= kEpiBias, "edge-masked launches: plain / bias epilogue");
   constexpr bool TRA = TRL && TA, TRB = TRL && !TB;  // operands staged in the transposed-read layout
   constexpr int IA = TRA ? timg<NT>() : 128 * xrow<NT>(), IB = TRB ? timg<NT>() : 128 * xrow<NT>();
-  __shared__ __attribute__((aligned(16))) char smem[NBUF * (IA + IB)];
+  __shared__ __attribute__((aligned(16))) char smem[IA + IB];
   char* const As = smem;
   char* const Bs = smem + IA;
 
@@ -558,8 +546,8 @@ __global__ void __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OC
   const int kofs = slice * (p.K / p.ksplit);
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int wr = w / WC, wc = w % WC;
-  const int wm = wr * (BM / 2), wn = wc * (BN / WC);
+  const int wr = w >> 1, wc = w & 1;
+  const int wm = wr * (BM / 2), wn = wc * (BN / 2);
   const int lr = lane & 31, q = lane >> 5;
 
   f32x16 acc[TM][TN];
@@ -569,8 +557,7 @@ __global__ void __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OC
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
 
   // staging: 32-bit per-thread offsets + a uniform K-tile base pointer (advanced per tile)
-  const int st = threadIdx.x & 255;
-  const bool stA = WV == 4 || threadIdx.x < 256, stB = WV == 4 || threadIdx.x >= 256;
+  const int st = threadIdx.x;
   uint32_t oa[4], ob[4];
   x_offsets<!TA>(p.lda, m0, oa, st);
   x_offsets<TB>(p.ldb, n0, ob, st);
@@ -608,31 +595,19 @@ __global__ void __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OC
     if (EDGE) {
       ldA(ab, va, TA ? p.Kv - kld : p.Mv - m0);
       ldB(bb, vb, TB ? p.Nv - n0 : p.Kv - kld);
-    } else if (WV == 4) {
+    } else {
       ldA(ab, va);
       ldB(bb, vb);
-    } else if (stA) {  // wave-uniform branch: one operand per half of the block
-      ldA(ab, va);
-    } else {
-      ldB(bb, va);
     }
   };
   auto store = [&]() {
-    if (WV == 4) {
-      stoA(As, va);
-      stoB(Bs, vb);
-    } else if (stA) {
-      stoA(As, va);
-    } else {
-      stoB(Bs, va);
-    }
+    stoA(As, va);
+    stoB(Bs, vb);
   };
-  (void)stB;
-  // weight gradient with p.part (TA only; the launcher admits it for the 4-wave single-buffer PF-1
-  // loop): the blocks of the first column tile also sum A over this slice's K -- the bias gradient
+  // weight gradient with p.part (TA only, unmasked launches): the blocks of the first column tile also sum A over this slice's K -- the bias gradient
   // of the same product (QKV: db = sum over tokens of dqkv) -- from the registers they stage anyway.
   // Thread st holds columns m0 + 4 (st & 31) + e of k rows 4 (st >> 5) + 0..3 in both A layouts.
-  const bool csum = TA && WV == 4 && NBUF == 1 && PF == 1 && !EDGE && p.part != nullptr && tn == 0;
+  const bool csum = TA && !EDGE && p.part != nullptr && tn == 0;
   float cs[4] = {0.f, 0.f, 0.f, 0.f};
   auto acc_cols = [&]() {
 #pragma unroll
@@ -670,79 +645,7 @@ __global__ void __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OC
 #pragma unroll
           for (int j = 0; j < TN; ++j) acc[i][j] = mma_nt<NT>(af[ks][PA[tt]][i], bf[ks][PB[tt]][j], acc[i][j]);
   };
-  // (ABL: ablation builds for tools/bench_gemm_x6.py --ablate, timing only, wrong results:
-  //  1 no global loads in the loop, 2 + no staging, 3 + no barriers)
-  if constexpr (NBUF == 2) {
-    // 8 waves: a thread stages ONE operand, so two register sets fit -- tile kt+1 waits in
-    // registers while tile kt+2 is in flight -- and the LDS images are double-buffered: staging
-    // tile kt+1 into the other buffer needs no barrier before it and overlaps this tile's MFMAs
-    // (the weight gradient runs at ~1 block per CU, with no second block to hide a staging
-    // phase).  Unrolled by two so the register sets and buffers keep fixed roles.
-    char* const As1 = smem + IA + IB;
-    char* const Bs1 = As1 + IA;
-    const char* gp = stA ? ab : bb;
-    const int64_t gs = stA ? sa : sb;
-    auto ld = [&](float4(&v)[4], int t) {
-      const char* base = gp + (int64_t)min(t, KT - 1) * gs;  // clamped: unconditional loads
-      if (stA) ldA(base, v);
-      else ldB(base, v);
-    };
-    auto sto = [&](char* A_, char* B_, const float4(&v)[4]) {
-      if (stA) stoA(A_, v);
-      else stoB(B_, v);
-    };
-    float4 r1[4];
-    ld(va, 0);
-    sto(As, Bs, va);
-    __syncthreads();
-    ld(va, 1);
-    ld(r1, 2);
-    int kt = 0;
-    for (; kt + 1 < KT; kt += 2) {  // buffer 0 = tile kt, va = kt+1, r1 = kt+2
-      compute([] {}, As, Bs);
-      if (ABL < 2) sto(As1, Bs1, va);  // buffer 1 was last read before the previous barrier
-      if (ABL < 1) ld(va, kt + 3);
-      if (ABL < 3) __syncthreads();
-      compute([] {}, As1, Bs1);
-      if (ABL < 2) sto(As, Bs, r1);
-      if (ABL < 1) ld(r1, kt + 4);
-      if (ABL < 3) __syncthreads();
-    }
-    if (kt < KT) compute([] {}, As, Bs);  // odd tile count: the last tile is already in buffer 0
-  } else if constexpr (PF == 2) {
-    // LDS = tile kt, (va, vb) = kt+1, (wa, wb) = kt+2: a tile's loads are issued right after the
-    // set that will hold it is staged, so their latency spans two compute phases.  Unrolled by two
-    // so the register sets keep fixed roles; loads past the end re-read the last tile (clamped).
-    float4 wa[4], wb[4];
-    auto ldt = [&](float4(&xa)[4], float4(&xb)[4], int t) {
-      const int64_t tt = min(t, KT - 1);
-      ldA(ab + tt * sa, xa);
-      ldB(bb + tt * sb, xb);
-    };
-    auto stt = [&](const float4(&xa)[4], const float4(&xb)[4]) {
-      stoA(As, xa);
-      stoB(Bs, xb);
-    };
-    ldt(va, vb, 0);
-    stt(va, vb);
-    __syncthreads();
-    ldt(va, vb, 1);
-    ldt(wa, wb, 2);
-    int kt = 0;
-    for (; kt + 1 < KT; kt += 2) {
-      compute([] {}, As, Bs);
-      __syncthreads();
-      stt(va, vb);
-      ldt(va, vb, kt + 3);
-      __syncthreads();
-      compute([] {}, As, Bs);
-      __syncthreads();
-      stt(wa, wb);
-      ldt(wa, wb, kt + 4);
-      __syncthreads();
-    }
-    if (kt < KT) compute([] {}, As, Bs);  // odd tile count: the last tile is staged already
-  } else {
+  {
     load();
     if (csum) acc_cols();
     store();
@@ -755,12 +658,12 @@ __global__ void __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OC
           bb += sb;
           kld += GBK;
         }
-        if (ABL < 1) load();
+        load();
       }, As, Bs);
-      if (ABL < 3) __syncthreads();  // every wave is done reading this K tile
+      __syncthreads();  // every wave is done reading this K tile
       if (csum && kt + 1 < KT) acc_cols();  // (not the re-read last tile)
-      if (ABL < 2) store();
-      if (ABL < 3) __syncthreads();
+      store();
+      __syncthreads();
     }
     if (csum) {  // block-uniform: the 8 k-row groups' sums in a fixed order -> part[slice][m]
       float* red = reinterpret_cast<float*>(smem);
@@ -788,21 +691,9 @@ __global__ void __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(OC
                                            q);
 }
 
-static int g_ablation = 0;  // microbenchmark hook (tile_override bits 3-4)
-// split-bf16 kernel waves per block: 4 (the weight gradient's 8-wave variant hid the register
-// transpose of its mn-contiguous staging, +8-12 % before the transposed-read layout; now it loses
-// in the step, see g_x6_wgrad_waves).  tile_override bit 5 forces 4, bit 6 forces 8.
-static int g_x6_waves = 4;
-// split-K block order of the split-bf16 kernel: slice-major (BERT-base fp32 step 15.04 vs 15.13 ms
+// split-K block order of the split kernels: slice-major (BERT-base fp32 step 15.04 vs 15.13 ms
 // tile-major, interleaved)
 static const int g_slice_major = 1;
-// waves per block of the weight-gradient (TA) launches: 4 since the transposed-read layout: beside the
-// data-gradient chain (side stream, 2 K slices) the BERT-base fp32 step runs 15.20-15.28 ms vs
-// 15.52-15.56 with 8 (interleaved, profiles/r2_gemm_experiments.md)
-static const int g_x6_wgrad_waves = 4;
-// 4-wave register prefetch depth (PF above): 1; tile_override bit 7 forces 2 (tests)
-static const int g_x6_pf_env = 1;
-static int g_x6_pf = 1;
 // mn-contiguous operands in the transposed-read layout: weight gradients 7-12 % and NN data gradients
 // 3-10 % faster on the BERT shapes than the register transpose (profiles/r2_gemm_experiments.md).
 // tile_override bit 8 forces it, bit 9 forces the register-transpose layout (tests).
@@ -816,9 +707,6 @@ static int g_x6_tr = 0;
 // stream and the LN backward).  profiles/r4_h3_gemm.md.
 static int g_h3_occ3_env = 5;
 static int g_h3_occ3 = 0;
-// single-buffered LDS images (53 KB: blocks of other kernels co-reside; the double-buffered 106 KB
-// 8-wave variant measured slower in the step and is off)
-static const int g_x6_dbuf = 0;
 
 // split-K finish: C = sum_s slab[s] (+ bias) (+ beta * C), fixed slice order (deterministic).
 // Blocks past `gmain` (weight gradient with fused column sums, wcol) finish the bias gradient in the
@@ -873,11 +761,9 @@ bool launch_occ3(const GemmArgs& a, int blocks, hipStream_t st) {
     // g_h3_occ3 bit mask: 1 forward (x W^T), 2 data gradient (dY W), 4 weight gradient (dY^T X)
     if (!(g_h3_occ3 & (TA ? 4 : TB ? 1 : 2))) return false;
     if (g_x6_tr && (TA || !TB))
-      hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 0, 4, 1, false, 1, true, 3>), dim3(blocks), dim3(256), 0, st,
-                         a);
+      hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, false, true, 3>), dim3(blocks), dim3(256), 0, st, a);
     else
-      hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 0, 4, 1, false, 1, false, 3>), dim3(blocks), dim3(256), 0, st,
-                         a);
+      hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, false, false, 3>), dim3(blocks), dim3(256), 0, st, a);
     return true;
   }
   return false;
@@ -886,56 +772,22 @@ bool launch_occ3(const GemmArgs& a, int blocks, hipStream_t st) {
 template <int BM, int BN, int MF, bool TA, bool TB, int EPI, int NT>
 void launch_cfg(const GemmArgs& a, hipStream_t st) {
   const int blocks = (a.M / BM) * (a.N / BN) * a.ksplit;
+  const bool tr = g_x6_tr && (TA || !TB);
   if constexpr (NT > 0) {
     if (a.Mv != a.M || a.Nv != a.N || a.Kv != a.K) {  // padded problem (launch_gemm checked epi)
       if constexpr (EPI <= kEpiBias) {
-        if (g_x6_tr && (TA || !TB))
-          hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 0, 4, 1, true, 1, true>), dim3(blocks), dim3(256), 0, st,
-                             a);
-        else
-          hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 0, 4, 1, true>), dim3(blocks), dim3(256), 0, st, a);
+        if (tr) hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, true, true>), dim3(blocks), dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, true>), dim3(blocks), dim3(256), 0, st, a);
       }
-    } else if (g_x6_waves == 4) {
-      if (EPI == kEpiNone && g_ablation == 1)
-        hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 1, 4>), dim3(blocks), dim3(256), 0, st, a);
-      else if (EPI == kEpiNone && g_ablation == 2)
-        hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 2, 4>), dim3(blocks), dim3(256), 0, st, a);
-      else if (EPI == kEpiNone && g_ablation == 3)
-        hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 3, 4>), dim3(blocks), dim3(256), 0, st, a);
-      else if (g_x6_pf == 2)
-        hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 0, 4, 1, false, 2>), dim3(blocks), dim3(256), 0, st, a);
-      else if (launch_occ3<TA, TB, EPI, NT>(a, blocks, st))
-        ;
-      else if (g_x6_tr && (TA || !TB))
-        hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 0, 4, 1, false, 1, true>), dim3(blocks), dim3(256), 0, st,
-                           a);
-      else
-        hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 0, 4>), dim3(blocks), dim3(256), 0, st, a);
-    } else if (g_x6_dbuf) {
-      if (EPI == kEpiNone && g_ablation == 1)
-        hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 1, 8, 2>), dim3(blocks), dim3(512), 0, st, a);
-      else if (EPI == kEpiNone && g_ablation == 2)
-        hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 2, 8, 2>), dim3(blocks), dim3(512), 0, st, a);
-      else if (EPI == kEpiNone && g_ablation == 3)
-        hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 3, 8, 2>), dim3(blocks), dim3(512), 0, st, a);
-      else
-        hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 0, 8, 2>), dim3(blocks), dim3(512), 0, st, a);
+    } else if (launch_occ3<TA, TB, EPI, NT>(a, blocks, st)) {
+    } else if (tr) {
+      hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, false, true>), dim3(blocks), dim3(256), 0, st, a);
     } else {
-      if (EPI == kEpiNone && g_ablation == 1)
-        hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 1, 8>), dim3(blocks), dim3(512), 0, st, a);
-      else if (g_x6_tr && (TA || !TB))
-        hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 0, 8, 1, false, 1, true>), dim3(blocks), dim3(512), 0, st,
-                           a);
-      else
-        hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT, 0, 8>), dim3(blocks), dim3(512), 0, st, a);
+      hipLaunchKernelGGL((gemm_x6s_kernel<TA, TB, EPI, NT>), dim3(blocks), dim3(256), 0, st, a);
     }
+  } else {
+    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, MF, TA, TB, EPI>), dim3(blocks), dim3(256), 0, st, a);
   }
-  else if (EPI == kEpiNone && g_ablation == 1)
-    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, MF, TA, TB, EPI, 1>), dim3(blocks), dim3(256), 0, st, a);
-  else if (EPI == kEpiNone && g_ablation == 2)
-    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, MF, TA, TB, EPI, 2>), dim3(blocks), dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, MF, TA, TB, EPI, 0>), dim3(blocks), dim3(256), 0, st, a);
 }
 
 template <int BM, int BN, int MF, int NT>
@@ -1010,7 +862,7 @@ static int pick_tile_split(int M, int N, int K, int* ksplit) {
 }
 
 // dtype: 0 fp32 on the exact-fp32 MFMA; 2 fp32 as 6 bf16 split products (fp32-level
-// error, see split8); 3 two-term split (3 products, ~2^-16: benchmarking only); 4 fp32 as 3 fp16
+// error at any range, see split4); 4 fp32 as 3 fp16
 // split products with per-tensor power-of-two scales (split4h; amax_a / amax_b required: na / nb
 // partial |max| values each, up to 8).  amax_c: GELU / dGELU epilogues atomically max |C| into it.
 // epi: 0 none, 1 +bias, 2 gelu(+bias) writing the pre-activation to aux,
@@ -1030,14 +882,14 @@ int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, i
                 float* part, float* colsum_out, int colsum_acc, int tile_override, hipStream_t st, int ksplit,
                 float* slab, int64_t slab_floats, int mv, int nv, int kv, const float* amax_a, int namax_a,
                 const float* amax_b, int namax_b, float* amax_c) {
-  if ((dtype != 0 && dtype != 2 && dtype != 3 && dtype != 4) || M <= 0 || N <= 0 || K <= 0 || K % GBK != 0) return -1;
+  if ((dtype != 0 && dtype != 2 && dtype != 4) || M <= 0 || N <= 0 || K <= 0 || K % GBK != 0) return -1;
   if (dtype == 4 && (!amax_a || !amax_b || namax_a < 1 || namax_b < 1 || namax_a > 8 || namax_b > 8)) return -1;
   // (namax_*: adjacent |max| slots of kAmaxShards shards each, common.h)
   auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
   if (!al16(A) || !al16(B) || lda % 4 || ldb % 4) return -1;
   if ((epi >= 1 && !bias) || (epi >= 2 && (!aux || beta != 0.f)) || (epi == 3 && (!part != !colsum_out)))
     return -1;
-  const int nt = dtype == 2 ? 6 : dtype == 3 ? 3 : dtype == 4 ? 4 : 0;
+  const int nt = dtype == 2 ? 6 : dtype == 4 ? 4 : 0;
   int tile, ks = 1;
   if (nt) {
     tile = pick_tile_split(M, N, K, &ks);
@@ -1047,11 +899,6 @@ int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, i
     tile = pick_tile(M, N);
     if (ksplit > 1 && epi <= kEpiBias && slab) ks = ksplit;  // exact-fp32 engine: forced split only
   }
-  const bool mfma16 = !nt && tile_override >= 0 && (tile_override & 4);  // benchmarking hook: 16x16x4 MFMA
-  g_ablation = tile_override >= 0 ? (tile_override >> 3) & 3 : 0;
-  g_x6_waves = tile_override >= 0 && (tile_override & 32) ? 4 : tile_override >= 0 && (tile_override & 64) ? 8
-                                                              : ta ? g_x6_wgrad_waves : 4;
-  g_x6_pf = tile_override >= 0 && (tile_override & 128) ? 2 : g_x6_pf_env;
   g_x6_tr = tile_override >= 0 && (tile_override & 256) ? 1 : tile_override >= 0 && (tile_override & 512) ? 0
                                                               : g_x6_tr_env;
   g_h3_occ3 = tile_override >= 0 && (tile_override & 1024) ? 7 : g_h3_occ3_env;
@@ -1076,11 +923,11 @@ int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, i
   nv = nv > 0 ? nv : N;
   kv = kv > 0 ? kv : K;
   if ((mv != M || nv != N || kv != K) && (!nt || epi > kEpiBias || mv > M || nv > N || kv > K)) return -1;
-  // weight gradient + the column sums of A (its bias gradient) in the same launch: split-bf16
-  // engine, 4-wave single-buffer PF-1 kernel, unpadded; part = [ks][M] partials, summed into
+  // weight gradient + the column sums of A (its bias gradient) in the same launch: split
+  // engines, unpadded; part = [ks][M] partials, summed into
   // colsum_out (added if colsum_acc) below
   const bool wcol = ta && epi == kEpiNone && part != nullptr;
-  if (wcol && (!nt || !colsum_out || g_x6_waves != 4 || g_x6_pf != 1 || g_ablation || mv != M || nv != N || kv != K))
+  if (wcol && (!nt || !colsum_out || mv != M || nv != N || kv != K))
     return -1;
   GemmArgs a{static_cast<const float*>(A), static_cast<const float*>(B), static_cast<float*>(C), bias, aux, part,
              lda, ldb, ldc, ldaux, M, N, K, beta, ks, slab, mv, nv, kv, g_slice_major,
@@ -1090,12 +937,6 @@ int launch_gemm(int dtype, int ta, int tb, int M, int N, int K, const void* A, i
     rc = launch_split<6>(tile, ta, tb, epi, a, st);
   else if (nt == 4)
     rc = launch_split<4>(tile, ta, tb, epi, a, st);
-  else if (nt == 3)
-    rc = launch_split<3>(tile, ta, tb, epi, a, st);
-  else if (mfma16)
-    rc = tile == 0 ? launch_tile<128, 128, 16, 0>(ta, tb, epi, a, st)
-         : tile == 1 ? launch_tile<128, 64, 16, 0>(ta, tb, epi, a, st)
-                     : launch_tile<64, 64, 16, 0>(ta, tb, epi, a, st);
   else
     rc = launch_split<0>(tile, ta, tb, epi, a, st);
   if (rc != 0) return rc;

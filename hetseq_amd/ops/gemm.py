@@ -16,8 +16,8 @@ fp32 products on the HIP engine run on the 16-bit matrix cores: as three split-f
 products with per-tensor power-of-two operand scales (``HETSEQ_FP32_GEMM=h3``: fp32-level
 error at half the MFMA work of x6, see gemm.hip ``split4h``; every operand needs its |max|,
 which the producing kernels emit -- :func:`amax_of` computes it for the rest), as six split-bf16
-products (``x6``: fp32-level error, no scale needed), or on the exact-fp32 MFMA (``native``);
-``x3`` (two-term bf16 split, ~2^-16 relative error) exists for benchmarking only.
+products (``x6``: fp32-level error at any dynamic range, no scale needed), or on the exact-fp32 MFMA
+(``native``: the accuracy oracle).
 
 ``HETSEQ_GEMM=hip|blas`` selects (default ``hip``).  There is no run-time choice between the
 hand-written kernels and the library (round 6): per call site only the hand-written kernels'
@@ -39,11 +39,11 @@ _MODE = os.environ.get("HETSEQ_GEMM", "hip")
 assert _MODE in ("hip", "blas"), "HETSEQ_GEMM must be hip or blas"
 # h3p: the encoder layers' products on pre-split block-scaled planes (ops/h3p.py, gemm_h3p.hip); every
 # other fp32 product (the pre-training heads, standalone calls) on the h3 engine (dtype code 4)
-_FP32_DT = {"native": 0, "x6": 2, "x3": 3, "h3": 4, "h3p": 4}
+_FP32_DT = {"native": 0, "x6": 2, "h3": 4, "h3p": 4}
 _FP32 = os.environ.get("HETSEQ_FP32_GEMM", "h3p")
 FP32_DEFAULT = _FP32
-assert _FP32 in _FP32_DT, "HETSEQ_FP32_GEMM must be one of native|x6|x3|h3|h3p"
-SPLIT_ENGINES = ("x6", "h3", "h3p")  # the fp32-level split engines (x3 is a benchmarking variant)
+assert _FP32 in _FP32_DT, "HETSEQ_FP32_GEMM must be one of native|x6|h3|h3p"
+SPLIT_ENGINES = ("x6", "h3", "h3p")  # the fp32-level split engines
 _SLABS: dict = {}  # (device, stream) -> split-K partial-sum workspace
 
 EPI_NONE, EPI_BIAS, EPI_GELU, EPI_DGELU = 0, 1, 2, 3
@@ -169,8 +169,9 @@ def _h3_census(site, a, b):
 
 
 def set_fp32_mode(mode):
-    """'h3' (split-fp16 products, per-tensor scales), 'x6' (split-bf16 products; both fp32-level
-    error), 'native' (exact-fp32 MFMA) or 'x3' (benchmark only)."""
+    """'h3p' (encoder layers on block-scaled planes, h3 elsewhere), 'h3' (split-fp16 products,
+    per-tensor scales), 'x6' (split-bf16 products, no scale: wide-range data; both fp32-level error)
+    or 'native' (exact-fp32 MFMA)."""
     global _FP32
     assert mode in _FP32_DT
     _FP32 = mode

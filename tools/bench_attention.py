@@ -3,8 +3,7 @@
 
     python tools/bench_attention.py [--reps 20]
 
-Phase 1: B=32, S=128, NH=12; phase 2: B=8, S=512, NH=12.  Engines: h3 (split-fp16 products, default), x6 (split-bf16 products on the
-bf16 matrix cores) and native
+Phase 1: B=32, S=128, NH=12; phase 2: B=8, S=512, NH=12.  Engines: h3 (split-fp16 products, default) and native
 (exact-fp32 v_mfma_f32_32x32x2_f32); dropout 0.1 as in training.  Prints median us per call.
 """
 import argparse
@@ -45,7 +44,7 @@ def main():
         mask = torch.ones(B, S, dtype=torch.int64, device="cuda")
         mask[:, S - S // 8:] = 0
         row = []
-        for name, mode in (("h3", 2), ("x6", 1), ("native", 0)):
+        for name, mode in (("h3", 2), ("native", 0)):
             hip().set_attn_fp32_mode(mode)
             out, saved = bert_ops.attn_fwd(qkv, mask, B, S, NH, 0.1, 1, 2, bias=bias)
             dout = torch.randn_like(out)

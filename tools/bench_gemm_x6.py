@@ -2,8 +2,8 @@
 """fp32 GEMM engines on BERT-base shapes: speed and error against an fp64 oracle.
 
 Engines: the library (hipBLASLt/rocBLAS via torch.mm, TunableOp table), the
-hand-written exact-fp32 MFMA kernel, and the split-bf16 kernels (x6: six bf16
-products per fp32 product, fp32-level error; x3: three, ~2^-16 relative).
+hand-written exact-fp32 MFMA kernel, the split-bf16 kernel (x6: six bf16 products
+per fp32 product, fp32-level error) and the per-tensor split-fp16 kernel (h3).
 Error metric per engine: max over elements of |C - C64| / (|A| @ |B|), i.e. the
 error in units of the magnitude sum the product accumulates (fp32 rounding of a
 K-long dot product gives ~1e-7 on this scale).
@@ -27,9 +27,6 @@ def main():
     ap.add_argument("--ksplit", default="0", help="comma list of split-K settings for x6 (0 = automatic)")
     ap.add_argument("--only", default=None, help="profile mode: 'M,N,K,ta,tb,engine' run --reps times, nothing else")
     ap.add_argument("--reps", type=int, default=50)
-    ap.add_argument("--waves", type=int, default=8, help="with --only: waves per block of the split kernel (4/8)")
-    ap.add_argument("--ablate", type=int, default=0, help="with --only: 1 no global loads, 2 + no staging, 3 + no barriers")
-    ap.add_argument("--pf", type=int, default=1, help="with --only: 4-wave register prefetch depth (1/2)")
     ap.add_argument("--tr", type=int, default=-1, help="with --only: 1 transposed-read layout, 0 register transpose")
     ap.add_argument("--ks", type=int, default=1, help="with --only: split-K slices")
     ap.add_argument("--occ3", type=int, default=0, help="with --only: h3 kernel at three blocks per CU")
@@ -43,15 +40,14 @@ def main():
         am = (G.amax_of(A), G.amax_of(B)) if eng == "h3" else None
         f = (lambda: torch.mm(A.t() if ta else A, B.t() if tb else B, out=C)) if eng == "blas" else \
             (lambda: G._hip_gemm(A, B, ta, tb, C, fp32=eng, ksplit=a.ks,
-                                 tile=(a.ablate << 3) | (32 if a.waves == 4 else 64) | (128 if a.pf == 2 else 0)
-                                 | (256 if a.tr == 1 else 512 if a.tr == 0 else 0) | (1024 if a.occ3 else 0),
+                                 tile=(256 if a.tr == 1 else 512 if a.tr == 0 else 0) | (1024 if a.occ3 else 0),
                                  amax=am))
         t = timeit(f, a.reps)
         f()
         At, Bt = (A.t() if ta else A).double(), (B.t() if tb else B).double()
         err = float(((C.double() - At @ Bt).abs() / (At.abs() @ Bt.abs())).max())
-        print("%s tr%d ks%d w%d pf%d%s %dx%dx%d %.1fus %.1fTF err %.2e" % (eng, a.tr, a.ks, a.waves, a.pf, " ablate=%d" % a.ablate if a.ablate
-                                                                else "", M, N, K, t, 2.0 * M * N * K / t / 1e6, err))
+        print("%s tr%d ks%d %dx%dx%d %.1fus %.1fTF err %.2e" % (eng, a.tr, a.ks, M, N, K, t,
+                                                              2.0 * M * N * K / t / 1e6, err))
         return
     from hetseq_amd.runtime import gemm_tuning
     gemm_tuning.enable("fp32", tune_missing=False)
@@ -83,10 +79,6 @@ def main():
             e = err()
             t = timeit(lambda: G._hip_gemm(A, B, ta, tb, C, fp32="x6", ksplit=ks))
             res.append(("x6" + ("" if ks == 0 else "/k%d" % ks), t, e))
-        if G._hip_gemm(A, B, ta, tb, C, fp32="x3"):
-            e = err()
-            t = timeit(lambda: G._hip_gemm(A, B, ta, tb, C, fp32="x3"))
-            res.append(("x3", t, e))
         am = (G.amax_of(A), G.amax_of(B))  # producer-side |max| in the step: not timed here
         for ks in [int(x) for x in a.ksplit.split(",")]:
             if not G._hip_gemm(A, B, ta, tb, C, fp32="h3", ksplit=ks, amax=am):

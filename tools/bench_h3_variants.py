@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """h3 GEMM kernel variants on the BERT-base shapes, interleaved in one process (medians of rounds):
-default (4 waves, two blocks per CU), 8 waves (64 x 32 per wave), 4 waves at three blocks per CU
-(168 VGPRs), against the six-term x6 kernel.  usage: python tools/bench_h3_variants.py [--rounds R]"""
+default (4 waves, two blocks per CU), 4 waves at three blocks per CU (168 VGPRs), against the
+six-term x6 kernel.  usage: python tools/bench_h3_variants.py [--rounds R]"""
 import argparse
 import os
 import sys
@@ -12,7 +12,7 @@ import torch  # noqa: E402
 from hetseq_amd.ops import gemm as G  # noqa: E402
 from tools.bench_gemm import SHAPES  # noqa: E402
 
-VARIANTS = {"x6": ("x6", -1), "h3": ("h3", -1), "h3_w8": ("h3", 64), "h3_occ3": ("h3", 1024)}
+VARIANTS = {"x6": ("x6", -1), "h3": ("h3", -1), "h3_occ3": ("h3", 1024)}
 
 
 def main():
