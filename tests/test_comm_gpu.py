@@ -506,3 +506,49 @@ def test_sharded_early_buckets_snapshot_and_update(group, delay):
         net.comm.check()
         net.comm.close()
     assert torch.allclose(out[True], out[False], rtol=1e-6, atol=1e-7), (out[True] - out[False]).abs().max().item()
+
+
+@pytest.mark.parametrize("defer", [True, False])
+def test_sharded_tables_deferred_early_group(group, defer):
+    """Sharded update + sparse table exchange on the native engine (1 rank, snapshot mode): with
+    DEFER_LAST_EARLY the early layer's last gradient group is reduce-scattered after the embedding
+    rows' all-gather (parallel/ddp.py launch_deferred_early), otherwise before it; either way every
+    reduce-scatter region reads its final gradient and the gradient equals the other order's."""
+    from hetseq_amd.ops import gemm as G
+    from hetseq_amd.parallel.ddp import FlatDDP
+    from hetseq_amd.runtime import rng
+    from hetseq_amd.runtime.flat import FlatParamStore
+    from tests.test_bert_gpu import _batch, _tiny
+
+    cuda = torch.device("cuda", 0)
+    G.set_fp32_mode("h3p")
+    model, cfg = _tiny(cuda)
+    model.train()
+    model.max_predictions_per_seq = 10
+    store = FlatParamStore(model)
+    model.attach_store(store, torch.float32)
+    net = FlatDDP(model, store, comm_engine="native", timeout_s=60, shard_optimizer=True,
+                  sparse_embedding=model.sparse_embedding())
+    old = FlatDDP.DEFER_LAST_EARLY
+    FlatDDP.DEFER_LAST_EARLY = defer
+    try:
+        assert net.tables is not None and store.shard is not None and len(net.early) == 4
+        snap = torch.full_like(store.grad, float("nan"))
+        net.comm.set_snapshot(snap, store.grad)
+        store.zero_grad()
+        rng.set_seed(7)
+        net(*_batch(cuda, 16, 64, cfg.vocab_size)).backward()
+        torch.cuda.synchronize()
+        net.comm.set_snapshot(None, None)
+        names = [w for w, *_ in net.comm_log]
+        last = "reducescatter_group%d" % net.early[-1]
+        assert last in names and "rows" in names, names
+        assert (names.index(last) > names.index("rows")) == defer, names
+        for lo, hi in net.ranges:
+            if hi <= net.tables.lo or lo >= net.tables.hi:  # (the tables: reduced before the rows are added)
+                assert torch.equal(snap[lo:hi], store.grad[lo:hi]), (lo, hi)
+        assert torch.isfinite(store.grad).all()
+    finally:
+        FlatDDP.DEFER_LAST_EARLY = old
+        net.comm.check()
+        net.comm.close()
