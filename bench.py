@@ -539,6 +539,9 @@ _AB = {
     "stag1": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FWD_STAGGER", 1),  # ... second after the QKV product
     "stag2": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FWD_STAGGER", 2),  # ... after the attention
     "stag3": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_FWD_STAGGER", 3),  # ... after the first LayerNorm
+    # h3p LN forward: split-K slab count at compile time (every load of a row in flight) / runtime loop
+    "lnns_on": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_ln_fwd_ns(1),
+    "lnns_off": lambda: __import__("hetseq_amd.ops._C", fromlist=["hip"]).hip().set_ln_fwd_ns(0),
     "attds_on": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_ATTN_DS", True),  # dQ from the stored dS
     "attds_off": lambda: _set_flag("hetseq_amd.ops.bert_ops", "_ATTN_DS", False),  # ... or the fused dQ role
     "defer_on": lambda: setattr(__import__("hetseq_amd.parallel.ddp", fromlist=["x"]).FlatDDP, "DEFER_LAST_EARLY", True),

@@ -48,6 +48,7 @@ int launch_emb_fwd(int, const int64_t*, const int64_t*, const float*, const floa
 int launch_emb_bwd(int, const void*, const float*, const float*, const float*, const float*, float*, float*, float*,
                    const int64_t*, float*, int, int, float, u64, u64, hipStream_t);
 void set_ln_h3p_waves(int w);
+void set_ln_fwd_ns(int on);
 int launch_ln_fwd_h3p(const void*, const float*, const void*, const float*, const float*, void*, float*, float*, float*,
                       int, int, float, float, u64, u64, int, int, int64_t, int, float*, void*, int64_t, int8_t*,
                       uint32_t*, int, hipStream_t);
@@ -515,6 +516,7 @@ PYBIND11_MODULE(_hip, m) {
      "dQ from the stored dS)", py::arg("qkv"), py::arg("mask"), py::arg("bqkv"), py::arg("ctx"), py::arg("dctx"),
      py::arg("lse"), py::arg("dbuf"), py::arg("dqkv"), py::arg("dmask"), py::arg("B"), py::arg("S"), py::arg("NH"),
      py::arg("p"), py::arg("pl"), py::arg("ps"), py::arg("ex"), py::arg("st"), py::arg("dsbuf") = 0);
+  m.def("set_ln_fwd_ns", &set_ln_fwd_ns, "h3p LN forward: slab count at compile time (1) / runtime loop (0)");
   m.def("set_ln_h3p_waves", &set_ln_h3p_waves,
         "h3p LayerNorm forward kernel: 0 / 1 panel exchange at 8 / 4 rows per workgroup, 16 / 8 one 32-row block");
   m.def("ln_bwd_h3p_part_rows", &ln_bwd_h3p_part_rows, "rows per column-partial row of ln_bwd_h3p (coop: psync given)");

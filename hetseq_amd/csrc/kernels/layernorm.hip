@@ -226,7 +226,11 @@ __global__ void __launch_bounds__(64 * WV) ln_fwd_h3p_kernel(
 // combine their column-group |max| through the panel record (h3p.h psync_exchange) and each splits
 // its own rows from registers.  Per-row arithmetic, y / z / planes / exponents bitwise those of
 // ln_fwd_h3p_kernel.  `psync`: the records of panels panel0 + (rows of this call) / 32.
-template <int NV, int RPW>
+// NS > 0: the call's split-K slab count, fixed at compile time, so every load of a row -- the NS slabs,
+// the bias and the residual -- is issued before the first is consumed (a runtime slab loop waited out
+// each load in turn: 18 serialised round trips per row at two waves per SIMD); the sums keep the slice
+// order, so the result is bitwise that of NS = 0 (runtime nslab, loads in turn).
+template <int NV, int RPW, int NS = 0>
 __global__ void __launch_bounds__(256) ln_fwd_h3p_coop_kernel(
     const float* __restrict__ a, const float* __restrict__ bias, const float* __restrict__ resid,
     const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ y, float* __restrict__ zsave,
@@ -243,53 +247,93 @@ __global__ void __launch_bounds__(256) ln_fwd_h3p_coop_kernel(
   const float scale = p < 1.f ? 1.0f / (1.0f - p) : 0.f;
   seed = resolve_seed(seed, seed_dev);
   uint32_t am = 0u;
-  float o[RPW][NV][4];
+  float o[RPW][NV][4], gw[NV][4], gb[NV][4];  // (gamma / beta in flight with the first row's loads)
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    load4(gamma + (k * 64 + lane) * 4, gw[k]);
+    load4(beta + (k * 64 + lane) * 4, gb[k]);
+  }
 #pragma unroll
   for (int j = 0; j < RPW; ++j) {
     const int row = blockIdx.x * RB + w * RPW + j;
     const int64_t base = (int64_t)row * H;
     float x[NV][4];
+    if constexpr (NS > 0) {
+      // every load first (absent bias / residual read stand-in rows -- gamma, the input -- and are
+      // selected away), then the combination in the order of the NS = 0 path
+      float t[NS > 1 ? NS - 1 : 1][NV][4], bv[NV][4], rv[NV][4];
+      const float* const bsrc = bias ? bias : gamma;
+      const float* const rsrc = resid ? resid : a;
 #pragma unroll
-    for (int k = 0; k < NV; ++k) {
-      const int c = (k * 64 + lane) * 4;
-      load4(a + base + c, x[k]);
-      for (int sl = 1; sl < nslab; ++sl) {
-        float t[4];
-        load4(a + sl * slab_stride + base + c, t);
+      for (int k = 0; k < NV; ++k) load4(a + base + (k * 64 + lane) * 4, x[k]);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) x[k][e] += t[e];
+      for (int sl = 1; sl < NS; ++sl)
+#pragma unroll
+        for (int k = 0; k < NV; ++k) load4(a + sl * slab_stride + base + (k * 64 + lane) * 4, t[sl - 1][k]);
+#pragma unroll
+      for (int k = 0; k < NV; ++k) load4(bsrc + (k * 64 + lane) * 4, bv[k]);
+#pragma unroll
+      for (int k = 0; k < NV; ++k) load4(rsrc + base + (k * 64 + lane) * 4, rv[k]);
+      const bool hb = bias != nullptr, hr = resid != nullptr;
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const int c = (k * 64 + lane) * 4;
+#pragma unroll
+        for (int sl = 1; sl < NS; ++sl)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) x[k][e] += t[sl - 1][k][e];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[k][e] = hb ? x[k][e] + bv[k][e] : x[k][e];
+        if (mode == kBDR && p > 0.f) {
+          float m[4];
+          keep4(seed, off, (uint64_t)((int64_t)(row0 + row) * H + c) >> 2, p, scale, m);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) x[k][e] *= m[e];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[k][e] = hr ? x[k][e] + rv[k][e] : x[k][e];
+        if (zsave) store4(zsave + base + c, x[k]);
       }
-      if (bias) {
-        float b[4];
-        load4(bias + c, b);
+    } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) x[k][e] += b[e];
-      }
-      if (mode == kBDR && p > 0.f) {
-        float m[4];
-        keep4(seed, off, (uint64_t)((int64_t)(row0 + row) * H + c) >> 2, p, scale, m);
+      for (int k = 0; k < NV; ++k) {
+        const int c = (k * 64 + lane) * 4;
+        load4(a + base + c, x[k]);
+        for (int sl = 1; sl < nslab; ++sl) {
+          float t[4];
+          load4(a + sl * slab_stride + base + c, t);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) x[k][e] *= m[e];
-      }
-      if (resid) {
-        float r[4];
-        load4(resid + base + c, r);
+          for (int e = 0; e < 4; ++e) x[k][e] += t[e];
+        }
+        if (bias) {
+          float b[4];
+          load4(bias + c, b);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) x[k][e] += r[e];
+          for (int e = 0; e < 4; ++e) x[k][e] += b[e];
+        }
+        if (mode == kBDR && p > 0.f) {
+          float m[4];
+          keep4(seed, off, (uint64_t)((int64_t)(row0 + row) * H + c) >> 2, p, scale, m);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) x[k][e] *= m[e];
+        }
+        if (resid) {
+          float r[4];
+          load4(resid + base + c, r);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) x[k][e] += r[e];
+        }
+        if (zsave) store4(zsave + base + c, x[k]);
       }
-      if (zsave) store4(zsave + base + c, x[k]);
     }
     float mean, rstd;
     row_stats<NV>(x, H, mean, rstd, eps);
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
       const int c = (k * 64 + lane) * 4;
-      float gw[4], gb[4];
-      load4(gamma + c, gw);
-      load4(beta + c, gb);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        o[j][k][e] = gw[e] * ((x[k][e] - mean) * rstd) + gb[e];
+        o[j][k][e] = gw[k][e] * ((x[k][e] - mean) * rstd) + gb[k][e];
         am = amax_bits(am, o[j][k][e]);
       }
       store4(y + base + c, o[j][k]);
@@ -875,6 +919,9 @@ static int g_ln_bwd_coop = 1;
 // workgroup of 16 / 8 waves (round 5).  Measured (round 6, tools/bench_producers.py, 2048 rows, 2 slabs):
 // 15.2 / 17.6 / 19.1 / 23.3 us alone; the BERT-base step 10.60 / 10.69 / 10.82 ms (bench.py --ab).
 static int g_ln_h3p_waves = 1;
+// the coop forward with the slab count fixed at compile time (1, 2, 4: every load of a row in flight
+// at once) -- A/B hook set_ln_fwd_ns (0 = the runtime slab loop)
+static int g_ln_fwd_ns = 1;
 
 template <int NV, typename T>
 void ln_fwd_h3p_launch(const void* a, const float* bias, const void* resid, const float* gamma, const float* beta,
@@ -884,6 +931,18 @@ void ln_fwd_h3p_launch(const void* a, const float* bias, const void* resid, cons
   if (psync && (g_ln_h3p_waves == 0 || g_ln_h3p_waves == 1)) {
     if (g_ln_h3p_waves == 0)
       hipLaunchKernelGGL((ln_fwd_h3p_coop_kernel<NV, 2>), dim3(rows / 8), dim3(256), 0, st, (const float*)a, bias,
+                         (const float*)resid, gamma, beta, (float*)y, zsave, mean, rstd, eps, p, seed, off, mode,
+                         g_seed_dev, nslab, slab_stride, row0, amax, planes, ps, exps, psync, panel0);
+    else if (g_ln_fwd_ns && nslab == 1)
+      hipLaunchKernelGGL((ln_fwd_h3p_coop_kernel<NV, 1, 1>), dim3(rows / 4), dim3(256), 0, st, (const float*)a, bias,
+                         (const float*)resid, gamma, beta, (float*)y, zsave, mean, rstd, eps, p, seed, off, mode,
+                         g_seed_dev, nslab, slab_stride, row0, amax, planes, ps, exps, psync, panel0);
+    else if (g_ln_fwd_ns && nslab == 2)
+      hipLaunchKernelGGL((ln_fwd_h3p_coop_kernel<NV, 1, 2>), dim3(rows / 4), dim3(256), 0, st, (const float*)a, bias,
+                         (const float*)resid, gamma, beta, (float*)y, zsave, mean, rstd, eps, p, seed, off, mode,
+                         g_seed_dev, nslab, slab_stride, row0, amax, planes, ps, exps, psync, panel0);
+    else if (g_ln_fwd_ns && nslab == 4)
+      hipLaunchKernelGGL((ln_fwd_h3p_coop_kernel<NV, 1, 4>), dim3(rows / 4), dim3(256), 0, st, (const float*)a, bias,
                          (const float*)resid, gamma, beta, (float*)y, zsave, mean, rstd, eps, p, seed, off, mode,
                          g_seed_dev, nslab, slab_stride, row0, amax, planes, ps, exps, psync, panel0);
     else
@@ -992,6 +1051,7 @@ int launch_ln_fwd(int dtype, const void* a, const float* bias, const void* resid
 }
 
 void set_ln_h3p_waves(int w) { hs::g_ln_h3p_waves = w; }
+void set_ln_fwd_ns(int on) { hs::g_ln_fwd_ns = on ? 1 : 0; }
 
 // LayerNorm forward writing y also as h3p planes (fp32 only; rows a multiple of 32)
 int launch_ln_fwd_h3p(const void* a, const float* bias, const void* resid, const float* gamma, const float* beta,

@@ -269,11 +269,14 @@ def test_rows_slice_view(cuda):
     assert torch.equal(full[256:], half)
 
 
-@pytest.mark.parametrize("H,p", [(768, 0.0), (768, 0.1), (1024, 0.1)])
-def test_layernorm_h3p_planes(cuda, H, p):
+@pytest.mark.parametrize("H,p,ns", [(768, 0.0, 2), (768, 0.1, 2), (1024, 0.1, 2), (768, 0.1, 4), (768, 0.1, 1),
+                                     (768, 0.0, 3)])
+def test_layernorm_h3p_planes(cuda, H, p, ns):
     """The LN forward / backward that write h3p planes: y, z, statistics and dz bitwise those of the
     plain kernels, the planes bitwise split(y) / split(da) (block exponents over 32-row blocks), the
-    parameter-gradient partials (32-row blocks) equal to the plain kernel's to fp32 rounding."""
+    parameter-gradient partials (32-row blocks) equal to the plain kernel's to fp32 rounding.  ns: split-K
+    slabs summed by the forward (1 / 2 / 4: the compile-time slab-count kernels, 3: the runtime loop);
+    the 4-rows-per-workgroup forward runs with both slab paths (set_ln_fwd_ns)."""
     from hetseq_amd.ops import bert_ops as O
     from hetseq_amd.ops import h3p
     from hetseq_amd.ops._C import hip
@@ -281,7 +284,7 @@ def test_layernorm_h3p_planes(cuda, H, p):
     g = torch.Generator(device=cuda)
     g.manual_seed(H)
     rows = 256
-    slabs = torch.randn(2, rows, H, device=cuda, generator=g)
+    slabs = torch.randn(ns, rows, H, device=cuda, generator=g)
     bias = torch.randn(H, device=cuda, generator=g)
     resid = torch.randn(rows, H, device=cuda, generator=g)
     gamma = torch.rand(H, device=cuda, generator=g) + 0.5
@@ -291,8 +294,9 @@ def test_layernorm_h3p_planes(cuda, H, p):
     sp = h3p.split(ref[0])
     # every forward kernel (panel exchange at 8 / 4 rows per workgroup, one 32-row block of 16 / 8
     # waves), each called three times: the panel records must come back ready for the next call
-    for mode in (0, 1, 16, 8, 1):
+    for mode, fns in ((0, 1), (1, 0), (16, 1), (8, 1), (1, 1)):
         hip().set_ln_h3p_waves(mode)
+        hip().set_ln_fwd_ns(fns)
         try:
             for _ in range(3):
                 outs = tuple(torch.full_like(t, float("nan")) for t in ref)
@@ -303,6 +307,19 @@ def test_layernorm_h3p_planes(cuda, H, p):
                 assert torch.equal(hp.planes, sp.planes) and torch.equal(hp.exps, sp.exps), mode
         finally:
             hip().set_ln_h3p_waves(1)
+            hip().set_ln_fwd_ns(1)
+    # no bias / no residual (the MLM head's LayerNorm): the stand-in loads are selected away
+    ref0 = O.ln_fwd(slabs, gamma, beta, 1e-12, p=p, mode=1, seed=seed, off=off, row0=64)
+    for fns in (1, 0):
+        hip().set_ln_fwd_ns(fns)
+        try:
+            outs = tuple(torch.full_like(t, float("nan")) for t in ref0)
+            hp = h3p.empty(rows, H, cuda)
+            O.ln_fwd_h3p(slabs, gamma, beta, 1e-12, None, None, p, seed, off, outs, 64, hp)
+            for a, b in zip(ref0, outs):
+                assert torch.equal(a, b), fns
+        finally:
+            hip().set_ln_fwd_ns(1)
     # backward
     dy = torch.randn(rows, H, device=cuda, generator=g)
     y, z, mean, rstd = ref

@@ -61,17 +61,20 @@ def main():
         t0 = timeit(lambda: bert_ops.ln_fwd(a_in, g, bt, 1e-12, bias, resid, 0.1, 1, 1, 2, outs=outs), a.reps)
         tv = {}
         for _ in range(3):  # interleaved rounds (one process)
-            for mode in (0, 1, 16, 8):
+            for mode, fns in ((0, 1), (1, 1), (1, 0), (16, 1), (8, 1)):
                 hip().set_ln_h3p_waves(mode)
+                hip().set_ln_fwd_ns(fns)
                 t = timeit(lambda: bert_ops.ln_fwd_h3p(a_in, g, bt, 1e-12, bias, resid, 0.1, 1, 2, outs, 0, hp),
                            a.reps)
-                tv[mode] = min(tv.get(mode, 1e9), t)
-        hip().set_ln_h3p_waves(0)
+                tv[mode, fns] = min(tv.get((mode, fns), 1e9), t)
+        hip().set_ln_h3p_waves(1)
+        hip().set_ln_fwd_ns(1)
         t2 = timeit(lambda: (bert_ops.ln_fwd(a_in, g, bt, 1e-12, bias, resid, 0.1, 1, 1, 2, outs=outs),
                              h3p.split(outs[0], out=hp)), a.reps)
         ts = timeit(lambda: h3p.split(outs[0], out=hp), a.reps)
-        rec("ln_fwd rows=%d nslab=%d" % (rows, ks), fp32=t0, coop_8rows=tv[0], coop_4rows=tv[1],
-            block32_16waves=tv[16], block32_8waves=tv[8], then_split=t2, split_alone=ts)
+        rec("ln_fwd rows=%d nslab=%d" % (rows, ks), fp32=t0, coop_8rows=tv[0, 1], coop_4rows=tv[1, 1],
+            coop_4rows_runtime_slabs=tv[1, 0], block32_16waves=tv[16, 1], block32_8waves=tv[8, 1], then_split=t2,
+            split_alone=ts)
 
     rows = 4096
     dy, z = torch.randn(rows, H, device=dev), torch.randn(rows, H, device=dev)
