@@ -701,6 +701,20 @@ __global__ void __launch_bounds__(256, 2)
       }
       m = amax8(kv[i], m);
     }
+    // this chunk's dS rows, both 32-key tiles, in flight with the K rows (a 32-key tail chunk's second
+    // tile re-reads the first: unconditional loads)
+    float dsc[2][2][8];  // [tile][ks][j]: key c0 + 32 tile + xrow(8 ks + j, hf)
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      const int t = min(32 * tt, clen - 32);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const float4 x = *reinterpret_cast<const float4*>(dsrow + c0 + t + 16 * ks + 4 * hf);
+        const float4 y = *reinterpret_cast<const float4*>(dsrow + c0 + t + 16 * ks + 8 + 4 * hf);
+        dsc[tt][ks][0] = x.x; dsc[tt][ks][1] = x.y; dsc[tt][ks][2] = x.z; dsc[tt][ks][3] = x.w;
+        dsc[tt][ks][4] = y.x; dsc[tt][ks][5] = y.y; dsc[tt][ks][6] = y.z; dsc[tt][ks][7] = y.w;
+      }
+    }
     m = wave_max(m);
     if (lane == 0) red[8 * par + w] = m;
     __syncthreads();  // the previous chunk's image is free; the chunk's |max| partials visible
@@ -719,16 +733,11 @@ __global__ void __launch_bounds__(256, 2)
       dq1 *= fk;
     }
     ek_run = ek;
-#pragma unroll 1
-    for (int t = 0; t < clen; t += 32) {
-      float ds[2][8];  // ds[ks][j]: key t + xrow(8 ks + j, hf), the dQ role's register order
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const float4 x = *reinterpret_cast<const float4*>(dsrow + c0 + t + 16 * ks + 4 * hf);
-        const float4 y = *reinterpret_cast<const float4*>(dsrow + c0 + t + 16 * ks + 8 + 4 * hf);
-        ds[ks][0] = x.x; ds[ks][1] = x.y; ds[ks][2] = x.z; ds[ks][3] = x.w;
-        ds[ks][4] = y.x; ds[ks][5] = y.y; ds[ks][6] = y.z; ds[ks][7] = y.w;
-      }
+    for (int tt = 0; tt < 2; ++tt) {
+      const int t = 32 * tt;
+      if (t >= clen) break;
+      float (&ds)[2][8] = dsc[tt];  // ds[ks][j]: key t + xrow(8 ks + j, hf), the dQ role's register order
       const float ss = ds_scale(ds, es, dq0, dq1);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
