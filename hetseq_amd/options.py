@@ -202,9 +202,11 @@ def add_mi355x_args(parser):
     group.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
                        help="compute dtype: fp32 (reference parity) or bf16 MFMA with fp32 master weights")
     group.add_argument("--fp32-gemm", default=None, choices=["h3p", "h3", "x6", "native"],
-                       help="fp32 GEMM engine: h3 = three split-fp16 products with per-tensor power-of-two "
-                            "scales, x6 = six split-bf16 products (both on the 16-bit matrix cores with "
-                            "fp32-level error), native = exact-fp32 MFMA (HETSEQ_FP32_GEMM)")
+                       help="fp32 GEMM engine (default h3p; HETSEQ_FP32_GEMM): h3p = the encoder and head on "
+                            "pre-split fp16 planes with a power-of-two exponent per 32 x 32 block, h3 elsewhere; "
+                            "h3 = three split-fp16 products with per-tensor power-of-two scales; x6 = six "
+                            "split-bf16 products, no scale (fp32-level error at any range); native = exact-fp32 "
+                            "MFMA")
     group.add_argument("--fused", dest="fused", action="store_true", default=True,
                        help="use the gfx950 HIP kernel path on GPU (default)")
     group.add_argument("--no-fused", dest="fused", action="store_false", help="use the torch-op reference path")
