@@ -43,7 +43,9 @@ HS_DEVICE void row_stats(const float (&x)[NV][4], int H, float& mean, float& rst
   rstd = 1.0f / sqrtf(v + eps);
 }
 
-template <int NV, typename T>
+// NS > 0: the slab count at compile time -- every load of a row in flight at once, combined in the
+// NS = 0 order (ln_fwd_h3p_coop_kernel); the bf16 step's calls are NS = 1.
+template <int NV, typename T, int NS = 0>
 __global__ void __launch_bounds__(256) ln_fwd_kernel(const T* __restrict__ a, const float* __restrict__ bias,
                                                      const T* __restrict__ resid, const float* __restrict__ gamma,
                                                      const float* __restrict__ beta, T* __restrict__ y,
@@ -61,35 +63,71 @@ __global__ void __launch_bounds__(256) ln_fwd_kernel(const T* __restrict__ a, co
   for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += gridDim.x * 4) {
     const int64_t base = (int64_t)row * H;
     float x[NV][4];
+    if constexpr (NS > 0) {
+      float t[NS > 1 ? NS - 1 : 1][NV][4], bv[NV][4], rv[NV][4];
+      const float* const bsrc = bias ? bias : gamma;
+      const T* const rsrc = resid ? resid : a;
 #pragma unroll
-    for (int k = 0; k < NV; ++k) {
-      const int c = (k * 64 + lane) * 4;
-      load4(a + base + c, x[k]);
-      for (int sl = 1; sl < nslab; ++sl) {  // split-K partials of the producing GEMM, summed in slice order
-        float t[4];
-        load4(a + sl * slab_stride + base + c, t);
+      for (int k = 0; k < NV; ++k) load4(a + base + (k * 64 + lane) * 4, x[k]);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) x[k][j] += t[j];
+      for (int sl = 1; sl < NS; ++sl)
+#pragma unroll
+        for (int k = 0; k < NV; ++k) load4(a + sl * slab_stride + base + (k * 64 + lane) * 4, t[sl - 1][k]);
+#pragma unroll
+      for (int k = 0; k < NV; ++k) load4(bsrc + (k * 64 + lane) * 4, bv[k]);
+#pragma unroll
+      for (int k = 0; k < NV; ++k) load4(rsrc + base + (k * 64 + lane) * 4, rv[k]);
+      const bool hb = bias != nullptr, hr = resid != nullptr;
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const int c = (k * 64 + lane) * 4;
+#pragma unroll
+        for (int sl = 1; sl < NS; ++sl)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) x[k][j] += t[sl - 1][k][j];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) x[k][j] = hb ? x[k][j] + bv[k][j] : x[k][j];
+        if (mode == kBDR && p > 0.f) {
+          float m[4];
+          keep4(seed, off, (uint64_t)((int64_t)(row0 + row) * H + c) >> 2, p, scale, m);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) x[k][j] *= m[j];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) x[k][j] = hr ? x[k][j] + rv[k][j] : x[k][j];
+        if (zsave) store4(zsave + base + c, x[k]);
       }
-      if (bias) {
-        float b[4];
-        load4(bias + c, b);
+    } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) x[k][j] += b[j];
-      }
-      if (mode == kBDR && p > 0.f) {  // counter of the element's row in the whole batch (row0: a row slice)
-        float m[4];
-        keep4(seed, off, (uint64_t)((int64_t)(row0 + row) * H + c) >> 2, p, scale, m);
+      for (int k = 0; k < NV; ++k) {
+        const int c = (k * 64 + lane) * 4;
+        load4(a + base + c, x[k]);
+        for (int sl = 1; sl < nslab; ++sl) {  // split-K partials of the producing GEMM, summed in slice order
+          float t[4];
+          load4(a + sl * slab_stride + base + c, t);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) x[k][j] *= m[j];
-      }
-      if (resid) {
-        float r[4];
-        load4(resid + base + c, r);
+          for (int j = 0; j < 4; ++j) x[k][j] += t[j];
+        }
+        if (bias) {
+          float b[4];
+          load4(bias + c, b);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) x[k][j] += r[j];
+          for (int j = 0; j < 4; ++j) x[k][j] += b[j];
+        }
+        if (mode == kBDR && p > 0.f) {  // counter of the element's row in the whole batch (row0: a row slice)
+          float m[4];
+          keep4(seed, off, (uint64_t)((int64_t)(row0 + row) * H + c) >> 2, p, scale, m);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) x[k][j] *= m[j];
+        }
+        if (resid) {
+          float r[4];
+          load4(resid + base + c, r);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) x[k][j] += r[j];
+        }
+        if (zsave) store4(zsave + base + c, x[k]);
       }
-      if (zsave) store4(zsave + base + c, x[k]);
     }
     float mean, rstd;
     row_stats<NV>(x, H, mean, rstd, eps);
@@ -899,15 +937,25 @@ __global__ void __launch_bounds__(256) emb_bwd_kernel(const T* __restrict__ dy, 
 // measured 25.0 / 27.0 us isolated vs 25.3, and slower in the step)
 static const int kLnBwdBlocks = 256;
 
+// the LN forwards with the slab count fixed at compile time (1, 2, 4: every load of a row in flight
+// at once) -- A/B hook set_ln_fwd_ns (0 = the runtime slab loop)
+static int g_ln_fwd_ns = 1;
+
 template <int NV, typename T>
 void ln_fwd_launch(const void* a, const float* bias, const void* resid, const float* gamma, const float* beta, void* y,
                    float* zsave, float* mean, float* rstd, int rows, float eps, float p, uint64_t seed, uint64_t off,
                    int mode, int nslab, int64_t slab_stride, int row0, float* amax, hipStream_t st) {
   int grid = (rows + 3) / 4;
   if (grid > 4096) grid = 4096;
-  hipLaunchKernelGGL((ln_fwd_kernel<NV, T>), dim3(grid), dim3(256), 0, st, (const T*)a, bias, (const T*)resid, gamma,
-                     beta, (T*)y, zsave, mean, rstd, rows, eps, p, seed, off, mode, g_seed_dev, nslab, slab_stride,
-                     row0, amax);
+#define HS_LN_FWD(NS_)                                                                                           \
+  hipLaunchKernelGGL((ln_fwd_kernel<NV, T, NS_>), dim3(grid), dim3(256), 0, st, (const T*)a, bias, (const T*)resid, \
+                     gamma, beta, (T*)y, zsave, mean, rstd, rows, eps, p, seed, off, mode, g_seed_dev, nslab,         \
+                     slab_stride, row0, amax)
+  if (g_ln_fwd_ns && nslab == 1) HS_LN_FWD(1);
+  else if (g_ln_fwd_ns && nslab == 2) HS_LN_FWD(2);
+  else if (g_ln_fwd_ns && nslab == 4) HS_LN_FWD(4);
+  else HS_LN_FWD(0);
+#undef HS_LN_FWD
 }
 
 // h3p LN backward with the panel exchange (A/B hook, set_ln_bwd_coop): 1 = 8 rows per workgroup,
@@ -919,9 +967,6 @@ static int g_ln_bwd_coop = 1;
 // workgroup of 16 / 8 waves (round 5).  Measured (round 6, tools/bench_producers.py, 2048 rows, 2 slabs):
 // 15.2 / 17.6 / 19.1 / 23.3 us alone; the BERT-base step 10.60 / 10.69 / 10.82 ms (bench.py --ab).
 static int g_ln_h3p_waves = 1;
-// the coop forward with the slab count fixed at compile time (1, 2, 4: every load of a row in flight
-// at once) -- A/B hook set_ln_fwd_ns (0 = the runtime slab loop)
-static int g_ln_fwd_ns = 1;
 
 template <int NV, typename T>
 void ln_fwd_h3p_launch(const void* a, const float* bias, const void* resid, const float* gamma, const float* beta,
