@@ -46,16 +46,6 @@ HS_DEVICE void h3p_split2(float x0, float x1, float s, uint32_t& hi, uint32_t& l
   lo = __builtin_bit_cast(uint32_t, l);
 }
 
-// one value scaled by s: hi | lo << 16 (the same rounding as h3p_split2)
-HS_DEVICE uint32_t h3p_pack1(float x, float s) {
-#pragma clang fp contract(off)
-  const float v = x * s;
-  const _Float16 h = static_cast<_Float16>(v);
-  const _Float16 l = static_cast<_Float16>(v - static_cast<float>(h));
-  return static_cast<uint32_t>(__builtin_bit_cast(uint16_t, h)) |
-         (static_cast<uint32_t>(__builtin_bit_cast(uint16_t, l)) << 16);
-}
-
 // four consecutive values of a row -> 8 B of each plane at element index i (plane 1 at + ps)
 HS_DEVICE void h3p_store4(uint16_t* __restrict__ pl, int64_t ps, int64_t i, const float v[4], float s) {
   uint32_t h0, l0, h1, l1;
